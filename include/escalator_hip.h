@@ -1,0 +1,374 @@
+/*
+ * escalator_hip.h — C ABI of the MI355X-native Escalator scale-decision hot path.
+ *
+ * The Go host (github.com/atlassian/escalator) keeps its pkg/k8s and pkg/controller
+ * signatures and calls this library through a thin cgo shim.  Every
+ * entry point below names the reference function it replaces (file:line, relative to
+ * the reference repository root).
+ *
+ * Conventions
+ *   - extern "C", plain pointers and sizes; no C++ or torch types cross this boundary.
+ *   - Return value int32: ESC_OK (0) or a negative ESC_E_* code.  esc_strerror() gives
+ *     the message.  Per-group outcomes that the reference reports as Go `error` values
+ *     are carried as ESC_ST_* codes whose esc_status_string() is the reference's text
+ *     verbatim.
+ *   - Caller-owned input arrays are read during the call only and never retained (the
+ *     cgo pointer-passing rule).  Outputs go to caller-allocated buffers.
+ *   - One esc_ctx per process / device, driven from one thread (the reference's RunOnce
+ *     is a single goroutine, pkg/controller/controller.go:416).
+ *
+ * Hot path: group membership (a1-a7), per-pod effective requests (a8),
+ * per-group int64 sums (a9, a10), node classification (a11), first-node capacity (a12),
+ * gates + usage percentages + scale delta (a13-a17), and creation-time ordering (a18,
+ * a19).  The HIP kernels run on gfx950; the decision arithmetic is bit-exact with the
+ * Go code (int64 two's complement, IEEE float64 without contraction).
+ */
+#ifndef ESCALATOR_HIP_H
+#define ESCALATOR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ESC_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- return codes */
+#define ESC_OK          0
+#define ESC_E_INVAL    -1   /* bad argument / shape                                  */
+#define ESC_E_HIP      -2   /* HIP runtime error (no device, launch failure, fault)   */
+#define ESC_E_NOMEM    -3   /* device or host allocation failed                      */
+#define ESC_E_LIMIT    -4   /* input exceeds a documented encoding limit              */
+#define ESC_E_STATE    -5   /* call order violated (e.g. decide before load)          */
+#define ESC_E_NODEV    -6   /* library loaded without a usable gfx950 device          */
+
+/* ------------------------------------------------------- per-group status codes
+ * esc_status_string(code) returns the reference's error text verbatim.            */
+#define ESC_ST_OK             0
+#define ESC_ST_ERR_MIN_NODES  1  /* pkg/controller/controller.go:239 "node count less than the minimum"  */
+#define ESC_ST_ERR_MAX_NODES  2  /* pkg/controller/controller.go:248 "node count larger than the maximum" */
+#define ESC_ST_ERR_DIV_ZERO   3  /* pkg/controller/util.go:75 "cannot divide by zero in percent calculation" */
+#define ESC_ST_ERR_NEG_DELTA  4  /* pkg/controller/util.go:43 "negative scale up delta"                   */
+#define ESC_ST_ERR_OVERFLOW   5  /* a sum left int64: the reference switches Quantity to inf.Dec
+                                    (apimachinery v0.22.5, not vendored) — reported, not emulated     */
+#define ESC_ST_ERR_TAINT_MIN  6  /* pkg/controller/scale_down.go:150-154 (formatted; see esc_taint_error) */
+
+/* ------------------------------------------------------------- decision branch
+ * Which arm of scaleNodeGroup (pkg/controller/controller.go:192-397) produced delta. */
+#define ESC_BR_EMPTY      0  /* no pods and no nodes -> 0, nil               controller.go:233 */
+#define ESC_BR_GATE       1  /* min/max node-count gate error                controller.go:238-255 */
+#define ESC_BR_BELOW_MIN  2  /* untainted < MinNodes -> ScaleUp(min-untainted) controller.go:281 */
+#define ESC_BR_PCT_ERR    3  /* calcPercentUsage error                       controller.go:299 */
+#define ESC_BR_LOCKED     4  /* scale-up lock held -> requestedNodes         controller.go:317 */
+#define ESC_BR_FAST_DOWN  5  /* max% < TaintLower -> -FastNodeRemovalRate    controller.go:335 */
+#define ESC_BR_SLOW_DOWN  6  /* max% < TaintUpper -> -SlowNodeRemovalRate    controller.go:338 */
+#define ESC_BR_SCALE_UP   7  /* max% > ScaleUp   -> calcScaleUpDelta         controller.go:342 */
+#define ESC_BR_NONE       8  /* no change                                    controller.go:377 */
+
+/* ------------------------------------------------------------------ group spec
+ * NodeGroupOptions fields the hot path reads (pkg/controller/node_group.go:20-52).
+ * A group named "default" selects NewPodDefaultFilterFunc for pods
+ * (pkg/controller/client.go:58-64, node_group.go:16); every group uses
+ * NewNodeLabelFilterFunc(label_key, label_value) for nodes (node_group.go:278, :301). */
+typedef struct esc_group_spec {
+    const char* name;
+    const char* label_key;
+    const char* label_value;
+    int32_t min_nodes;
+    int32_t max_nodes;
+    int32_t taint_upper_pct;     /* TaintUpperCapacityThresholdPercent */
+    int32_t taint_lower_pct;     /* TaintLowerCapacityThresholdPercent */
+    int32_t scale_up_pct;        /* ScaleUpThresholdPercent            */
+    int32_t slow_removal_rate;   /* SlowNodeRemovalRate                */
+    int32_t fast_removal_rate;   /* FastNodeRemovalRate                */
+    int32_t dry_mode;            /* c.Opts.DryMode || group.DryMode (controller.go:115-117) */
+} esc_group_spec;
+
+/* Per-run host state of a group (NodeGroupState, pkg/controller/controller.go:28-44). */
+typedef struct esc_group_state {
+    int32_t locked;              /* nodeGroup.scaleUpLock.locked()              controller.go:317 */
+    int32_t requested_nodes;     /* nodeGroup.scaleUpLock.requestedNodes        controller.go:322 */
+    int64_t cached_cpu_m;        /* nodeGroup.cpuCapacity.MilliValue()          controller.go:209 */
+    int64_t cached_mem_b;        /* nodeGroup.memCapacity.Value()               controller.go:210 */
+} esc_group_state;
+
+/* Per-group totals: the lister + filterNodes + Calculate*Total results. */
+typedef struct esc_group_totals {
+    int64_t pod_cpu_m;           /* CalculatePodsRequestsTotal cpu  pkg/k8s/util.go:27 */
+    int64_t pod_mem_b;           /* CalculatePodsRequestsTotal mem                      */
+    int64_t n_pods;              /* len(pods)                       controller.go:194  */
+    int64_t node_cpu_m;          /* CalculateNodesCapacityTotal(untainted) cpu util.go:41, controller.go:268 */
+    int64_t node_mem_b;
+    int64_t n_nodes;             /* len(allNodes)                   controller.go:201  */
+    int64_t n_untainted;         /* filterNodes                     controller.go:120  */
+    int64_t n_tainted;
+    int64_t n_cordoned;
+    int64_t first_node;          /* snapshot index of allNodes[0], -1 if none  controller.go:208 */
+    int64_t first_cpu_m;         /* allNodes[0].Status.Allocatable.Cpu().MilliValue() */
+    int64_t first_mem_b;         /* allNodes[0].Status.Allocatable.Memory().Value()   */
+    int64_t flags;               /* ESC_TF_* */
+} esc_group_totals;
+
+#define ESC_TF_POD_OVERFLOW   1  /* a pod sum left int64 (Quantity would switch to inf.Dec) */
+#define ESC_TF_NODE_OVERFLOW  2  /* a node capacity sum left int64                          */
+
+/* Per-group scale decision. */
+typedef struct esc_group_decision {
+    double  cpu_pct;             /* calcPercentUsage  pkg/controller/util.go:58  */
+    double  mem_pct;
+    int64_t delta;               /* scaleNodeGroup's returned nodesDelta; BELOW_MIN: MinNodes-untainted;
+                                    LOCKED: requestedNodes                                      */
+    int64_t n_to_taint;          /* scaleDownTaint clamp (scale_down.go:138-158) when delta < 0 */
+    int64_t cached_cpu_m;        /* updated cached capacity (controller.go:208-211)            */
+    int64_t cached_mem_b;
+    int32_t status;              /* ESC_ST_* of scaleNodeGroup                                  */
+    int32_t branch;              /* ESC_BR_*                                                    */
+    int32_t taint_status;        /* ESC_ST_OK or ESC_ST_ERR_TAINT_MIN                           */
+    int32_t reserved;
+} esc_group_decision;
+
+/* ---------------------------------------------------------- object-level input
+ * What the cgo shim copies out of *v1.Pod / *v1.Node (no Go pointers retained).
+ * Resource quantities arrive as Quantity.MilliValue() (cpu) and Quantity.Value()
+ * (memory) with a presence flag — absent keys contribute nothing
+ * (pkg/k8s/scheduler/types.go:14-43).                                              */
+typedef struct esc_kv { const char* key; const char* value; } esc_kv;
+
+typedef struct esc_request {
+    int64_t cpu_m;
+    int64_t mem_b;
+    int32_t has_cpu;
+    int32_t has_mem;
+} esc_request;
+
+typedef struct esc_selector_expr {       /* v1.NodeSelectorRequirement */
+    const char*        key;
+    const char*        op;               /* "In", "NotIn", "Exists", ...  only "In" matches */
+    const char* const* values;
+    int32_t            n_values;
+    int32_t            term;             /* index of the NodeSelectorTerm it belongs to    */
+} esc_selector_expr;
+
+typedef struct esc_pod_obj {
+    const char* const* owner_kinds;      /* ObjectMeta.OwnerReferences[*].Kind   util.go:11 */
+    int32_t            n_owner_kinds;
+    int32_t            has_config_source;/* Annotations["kubernetes.io/config.source"] present util.go:22 */
+    const char*        config_source;
+    const esc_kv*      node_selector;    /* Spec.NodeSelector                    node_group.go:226 */
+    int32_t            n_node_selector;
+    int32_t            has_affinity;     /* Spec.Affinity != nil                  node_group.go:271 */
+    int32_t            has_node_affinity;
+    int32_t            has_pod_affinity;
+    int32_t            has_pod_anti_affinity;
+    int32_t            has_required;     /* NodeAffinity.RequiredDuringScheduling... != nil node_group.go:211 */
+    const esc_selector_expr* exprs;      /* flattened NodeSelectorTerms[*].MatchExpressions */
+    int32_t            n_exprs;
+    const esc_request* containers;       /* Spec.Containers[*].Resources.Requests  types.go:74 */
+    int32_t            n_containers;
+    const esc_request* init_containers;  /* Spec.InitContainers                    types.go:79 */
+    int32_t            n_init_containers;
+    int32_t            has_overhead;     /* Spec.Overhead != nil                   types.go:84 */
+    esc_request        overhead;
+} esc_pod_obj;
+
+typedef struct esc_node_obj {
+    const char*   name;
+    const esc_kv* labels;                /* ObjectMeta.Labels                   node_group.go:280 */
+    int32_t       n_labels;
+    int32_t       unschedulable;         /* Spec.Unschedulable                   controller.go:141 */
+    const char* const* taint_keys;       /* Spec.Taints[*].Key                   taint.go:80       */
+    int32_t       n_taints;
+    esc_request   allocatable;           /* Status.Allocatable cpu/memory        util.go:46        */
+    int64_t       created_unix_ns;       /* CreationTimestamp (sec*1e9+nsec)     sort.go:19        */
+} esc_node_obj;
+
+/* ------------------------------------------------------------- packed snapshot
+ * Struct-of-arrays layout streamed by the kernels.  Pods:
+ *   flags  u32  ESC_PF_* bits + counts of extra records
+ *   cpu0   u32  cpu (millicores) of the inline regular container
+ *   mem0   i64  memory (bytes)   of the inline regular container
+ *   pair0  u32  head group of the pod's first matching (key,value) pair, ESC_NONE if none
+ *   xc_cpu/xc_mem i64  extra containers per pod: [regular extras][init][overhead]
+ *   xp_group u32       extra matching pairs (head groups)
+ * Nodes:
+ *   nflags u32, label0 u32, ncpu i64, nmem i64, created i64, xl_group u32.        */
+#define ESC_NONE 0xFFFFFFFFu
+
+#define ESC_PF_DAEMONSET   (1u << 0)   /* PodIsDaemonSet  util.go:11   (also marks padding) */
+#define ESC_PF_STATIC      (1u << 1)   /* PodIsStatic     util.go:21   */
+#define ESC_PF_HAS_SEL     (1u << 2)   /* len(NodeSelector) > 0        node_group.go:271 */
+#define ESC_PF_AFF_BLOCK   (1u << 3)   /* Affinity != nil && any sub-affinity != nil node_group.go:271-273 */
+#define ESC_PF_HAS_OVH     (1u << 4)   /* overhead record present (Spec.Overhead != nil) */
+#define ESC_PF_XREG_SHIFT  8           /* bits  8..15: regular containers beyond the inline one */
+#define ESC_PF_XINIT_SHIFT 16          /* bits 16..23: init containers                         */
+#define ESC_PF_XPAIR_SHIFT 24          /* bits 24..29: extra matching pairs                    */
+#define ESC_PF_CNT_MASK    0xFFu
+#define ESC_PF_PAIR_MASK   0x3Fu
+
+#define ESC_NF_UNSCHED     (1u << 0)   /* Spec.Unschedulable           controller.go:141 */
+#define ESC_NF_TAINTED     (1u << 1)   /* has atlassian.com/escalator  taint.go:31,80    */
+#define ESC_NF_TRACKED     (1u << 2)   /* in some group's dry-mode taintTracker controller.go:128 */
+#define ESC_NF_XLBL_SHIFT  8           /* bits 8..15: extra matching labels */
+
+typedef struct esc_pod_soa {
+    int64_t         n_pods;
+    const uint32_t* flags;
+    const uint32_t* cpu0;
+    const int64_t*  mem0;
+    const uint32_t* pair0;
+    const int64_t*  xc_cpu;
+    const int64_t*  xc_mem;
+    int64_t         n_xc;
+    const uint32_t* xp_group;
+    int64_t         n_xp;
+} esc_pod_soa;
+
+typedef struct esc_node_soa {
+    int64_t         n_nodes;
+    const uint32_t* flags;
+    const uint32_t* label0;
+    const int64_t*  cpu;
+    const int64_t*  mem;
+    const int64_t*  created_ns;
+    const uint32_t* xl_group;
+    int64_t         n_xl;
+    const int32_t*  trk_node;    /* dry-mode taintTracker entries resolved to (node, group), */
+    const int32_t*  trk_group;   /* sorted by (node, group); may be NULL when n_trk == 0     */
+    int64_t         n_trk;
+} esc_node_soa;
+
+/* ------------------------------------------------------------------- library */
+int32_t     esc_abi_version(void);
+const char* esc_strerror(int32_t code);
+const char* esc_status_string(int32_t status);
+/* scale_down.go:150-154: "the number of nodes(%v) is less than specified minimum of %v. Taking no action" */
+int32_t     esc_taint_error(int64_t n_untainted, int32_t min_nodes, char* buf, int32_t buf_len);
+
+/* ------------------------------------------------------------------- context
+ * Groups are fixed for the context's lifetime (the reference builds its listers once,
+ * pkg/controller/client.go:55-64).  rank/world describe the sharding when one process
+ * drives each GPU; the per-group int64 exchange itself is done by the caller's
+ * collective (RCCL via torch.distributed, or ncclAllReduce in a cgo host) on the
+ * buffers returned by esc_exchange_buffers.                                         */
+typedef struct esc_ctx esc_ctx;
+
+int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t device,
+                       int32_t rank, int32_t world, esc_ctx** out);
+int32_t esc_ctx_destroy(esc_ctx* ctx);
+int32_t esc_ctx_set_stream(esc_ctx* ctx, void* hip_stream);   /* NULL = ctx-owned stream */
+int32_t esc_ctx_num_groups(const esc_ctx* ctx);
+/* Head group of (key,value) for pods (side 0, default group excluded) or nodes (side 1). */
+uint32_t esc_ctx_pair_head(const esc_ctx* ctx, const char* key, const char* value, int32_t side);
+
+/* ------------------------------------------------------------- K0 host packer
+ * Replaces the per-group List()+filter object walk (pkg/k8s/pod_listers.go:33,
+ * node_listers.go:33, pkg/controller/node_group.go:208-287): interns (key,value) pairs
+ * against the context's groups and packs the SoA above.                             */
+typedef struct esc_packer esc_packer;
+int32_t esc_packer_create(const esc_ctx* ctx, esc_packer** out);
+int32_t esc_packer_destroy(esc_packer* pk);
+int32_t esc_packer_add_pods(esc_packer* pk, const esc_pod_obj* pods, int64_t n);
+int32_t esc_packer_add_nodes(esc_packer* pk, const esc_node_obj* nodes, int64_t n);
+/* nodeGroup.taintTracker (controller.go:35) of `group`: node names, resolved at finish. */
+int32_t esc_packer_set_tracker(esc_packer* pk, int32_t group, const char* const* names, int64_t n);
+/* List mode, for the per-function drop-ins: every pod / node is a member of group 0,
+ * no filter applied (CalculatePodsRequestsTotal / CalculateNodesCapacityTotal take an
+ * already-filtered slice).                                                          */
+int32_t esc_packer_set_list_mode(esc_packer* pk, int32_t list_mode);
+int32_t esc_packer_view(esc_packer* pk, esc_pod_soa* pods, esc_node_soa* nodes);
+
+/* -------------------------------------------------------------- device snapshot
+ * esc_load_pods: copies this rank's pod shard (global pod indices [offset, offset+n)).
+ * esc_load_nodes: copies the full node table; this rank streams nodes [lo, hi).     */
+int32_t esc_load_pods(esc_ctx* ctx, const esc_pod_soa* pods, int64_t global_offset);
+int32_t esc_load_nodes(esc_ctx* ctx, const esc_node_soa* nodes, int64_t lo, int64_t hi);
+/* Number of device-resident copies of the pod shard to rotate through on successive
+ * decisions (benchmarks use >1 so that timings are HBM-, not Infinity-Cache-, served). */
+int32_t esc_set_replicas(esc_ctx* ctx, int32_t n_replicas);
+
+/* ------------------------------------------------------------ scale decision
+ * esc_reduce     : async. Per-shard group totals (K1 pods + K2 nodes + combine).
+ * esc_exchange_buffers: device buffers to all-reduce between esc_reduce and esc_decide:
+ *                  sum_buf  int64[sum_count]  with op SUM,
+ *                  min_buf  int64[min_count]  with op MIN.
+ * esc_decide     : async. K4 decide on the (exchanged) totals; results land in the
+ *                  context's host buffers after esc_sync.
+ * esc_run        : esc_reduce + esc_decide for world == 1, optionally graph-captured.
+ * esc_sync       : waits; validates; falls back to the exact wide path if any record
+ *                  exceeded the fast path's packing range.           */
+int32_t esc_set_state(esc_ctx* ctx, const esc_group_state* state);   /* NULL = zero state */
+int32_t esc_reduce(esc_ctx* ctx);
+int32_t esc_exchange_buffers(esc_ctx* ctx, void** sum_buf, int64_t* sum_count,
+                             void** min_buf, int64_t* min_count);
+int32_t esc_decide(esc_ctx* ctx);
+int32_t esc_run(esc_ctx* ctx);
+int32_t esc_sync(esc_ctx* ctx);
+int32_t esc_results(esc_ctx* ctx, esc_group_totals* totals, esc_group_decision* decisions);
+int32_t esc_use_graph(esc_ctx* ctx, int32_t enable);
+int32_t esc_force_wide(esc_ctx* ctx, int32_t enable);   /* testing: always take the wide path */
+/* Last kernel's device time in ms per stage (timing mode), see DESIGN.md §6. */
+int32_t esc_set_timing(esc_ctx* ctx, int32_t enable);
+int32_t esc_stage_times(esc_ctx* ctx, double* ms_out, int32_t n);
+
+/* ----------------------------------------------------------------- ordering
+ * K5: per-group creation-time order of the context's node shard (a18/a19):
+ *   which 0: untainted members oldest-first (taintOldestN,   scale_down.go:171)
+ *   which 1: tainted members newest-first   (untaintNewestN, scale_up.go:118)
+ * Writes up to `cap` snapshot node indices; *n_out = number of members in that list.
+ * Ties (equal timestamps) are broken by snapshot index (Go's sort.Sort is unstable,
+ * so its tie order is not reproducible).                             */
+int32_t esc_sort_nodes(esc_ctx* ctx);          /* async: full segmented sort          */
+int32_t esc_group_order(esc_ctx* ctx, int32_t group, int32_t which,
+                        int64_t* idx_out, int64_t cap, int64_t* n_out);
+
+/* ----------------------------------------------- per-function drop-ins (GPU)
+ * Same argument meaning as the Go functions; these pack the given slice in list mode
+ * and run the batched kernels on it.                                                */
+/* pkg/k8s/util.go:27 — returns (mem, cpu) like the Go function. */
+int32_t esc_pods_requests_total(esc_ctx* ctx, const esc_pod_obj* pods, int64_t n,
+                                int64_t* mem_b, int64_t* cpu_m);
+/* pkg/k8s/util.go:41 */
+int32_t esc_nodes_capacity_total(esc_ctx* ctx, const esc_node_obj* nodes, int64_t n,
+                                 int64_t* mem_b, int64_t* cpu_m);
+/* pkg/controller/scale_down.go:171 / scale_up.go:118 — indices into the given slice;
+ * oldest != 0: oldest first, else newest first; returns min(n_take, n) indices.      */
+int32_t esc_order_by_creation(esc_ctx* ctx, const int64_t* created_ns, int64_t n,
+                              int32_t oldest, int64_t n_take, int64_t* idx_out);
+
+/* --------------------------------------------- scalar decision math (host)
+ * Bit-exact restatements used by the shim for single calls; the batched path runs
+ * the same __host__ __device__ code inside the K4 kernel.                            */
+/* pkg/controller/util.go:58 — returns ESC_ST_OK or ESC_ST_ERR_DIV_ZERO. */
+int32_t esc_calc_percent_usage(int64_t cpu_req_m, int64_t mem_req_b, int64_t cpu_cap_m,
+                               int64_t mem_cap_b, int64_t n_untainted,
+                               double* cpu_pct, double* mem_pct);
+/* pkg/controller/util.go:13 — returns ESC_ST_OK or ESC_ST_ERR_NEG_DELTA. */
+int32_t esc_calc_scale_up_delta(int64_t n_untainted, double cpu_pct, double mem_pct,
+                                int64_t cpu_req_m, int64_t mem_req_b,
+                                int64_t cached_cpu_m, int64_t cached_mem_b,
+                                int32_t scale_up_pct, int64_t* delta);
+
+/* ------------------------------------------------- synthetic snapshots (bench)
+ * Deterministic counter-hash generator of BASELINE.md's configs; fills the SoA of
+ * pods [p_lo, p_hi) and nodes, plus the group specs.  Host memory is owned by the
+ * returned handle.                                                                  */
+typedef struct esc_synth esc_synth;
+typedef struct esc_synth_params {
+    int64_t  n_pods;
+    int64_t  n_nodes;
+    int32_t  n_groups;
+    int32_t  config;             /* 1..5: BASELINE.md §3 row, selects distributions  */
+    uint64_t seed;
+    int32_t  with_default;       /* group 0 named "default"                          */
+    int32_t  n_threads;          /* host threads for generation (0 = 1)              */
+} esc_synth_params;
+int32_t esc_synth_create(const esc_synth_params* p, int64_t p_lo, int64_t p_hi, esc_synth** out);
+int32_t esc_synth_destroy(esc_synth* s);
+int32_t esc_synth_groups(const esc_synth* s, const esc_group_spec** groups, int32_t* n);
+int32_t esc_synth_view(const esc_synth* s, esc_pod_soa* pods, esc_node_soa* nodes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ESCALATOR_HIP_H */
