@@ -1,0 +1,258 @@
+"""Python host of the batched scale decision (over the C ABI).
+
+``Context`` is the MI355X-resident equivalent of the reference's per-scan loop
+(``(*Controller).RunOnce`` pkg/controller/controller.go:400 -> ``scaleNodeGroup`` :192 per
+group): it holds one device snapshot and computes every group's totals and decision in
+one pass.  ``Synth`` wraps the deterministic snapshot generator used by tests and the
+benchmark.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from .objects import groups_from_c, groups_to_c, nodes_to_c, pods_to_c, states_to_c
+
+TOTALS_DTYPE = np.dtype([(n, np.int64) for n, _ in L.GroupTotals._fields_])
+DECISION_DTYPE = np.dtype({"names": [n for n, _ in L.GroupDecision._fields_],
+                           "formats": [np.float64, np.float64, np.int64, np.int64, np.int64, np.int64,
+                                       np.int32, np.int32, np.int32, np.int32]})
+assert TOTALS_DTYPE.itemsize == C.sizeof(L.GroupTotals)
+assert DECISION_DTYPE.itemsize == C.sizeof(L.GroupDecision)
+
+_POD_FIELDS = [("flags", np.uint32, "n_pods"), ("cpu0", np.uint32, "n_pods"), ("mem0", np.int64, "n_pods"),
+               ("pair0", np.uint32, "n_pods"), ("xc_cpu", np.int64, "n_xc"), ("xc_mem", np.int64, "n_xc"),
+               ("xp_group", np.uint32, "n_xp")]
+_NODE_FIELDS = [("flags", np.uint32, "n_nodes"), ("label0", np.uint32, "n_nodes"), ("cpu", np.int64, "n_nodes"),
+                ("mem", np.int64, "n_nodes"), ("created_ns", np.int64, "n_nodes"), ("xl_group", np.uint32, "n_xl"),
+                ("trk_node", np.int32, "n_trk"), ("trk_group", np.int32, "n_trk")]
+
+
+def _view(struct, fields) -> dict:
+    out = {}
+    for name, dt, count in fields:
+        n = int(getattr(struct, count))
+        ptr = getattr(struct, name)
+        out[name] = np.ctypeslib.as_array(ptr, shape=(n,)).view(dt) if n and ptr else np.zeros(0, dt)
+    return out
+
+
+def _soa_from(arrays: dict, fields, struct_t, count_names):
+    """Build a SoA struct pointing at numpy arrays (kept alive by the caller)."""
+    s = struct_t()
+    keep = []
+    for name, dt, count in fields:
+        a = np.ascontiguousarray(arrays[name], dtype=dt)
+        keep.append(a)
+        setattr(s, name, a.ctypes.data_as(dict(s._fields_)[name]))
+    for cname, val in count_names.items():
+        setattr(s, cname, int(val))
+    return s, keep
+
+
+def pod_soa(arrays: dict):
+    return _soa_from(arrays, _POD_FIELDS, L.PodSoA, {"n_pods": len(arrays["flags"]), "n_xc": len(arrays["xc_cpu"]),
+                                                      "n_xp": len(arrays["xp_group"])})
+
+
+def node_soa(arrays: dict):
+    return _soa_from(arrays, _NODE_FIELDS, L.NodeSoA, {"n_nodes": len(arrays["flags"]), "n_xl": len(arrays["xl_group"]),
+                                                        "n_trk": len(arrays["trk_node"])})
+
+
+class Synth:
+    """Deterministic synthetic snapshot."""
+
+    def __init__(self, n_pods: int, n_nodes: int, n_groups: int, config: int = 2, seed: int = 0xE5CA1A7E00000002,
+                 with_default: bool = True, p_lo: int = 0, p_hi: int | None = None, threads: int = 8):
+        self.lib = L.load()
+        p = L.SynthParams(n_pods, n_nodes, n_groups, config, seed & ((1 << 64) - 1), int(with_default), threads)
+        self.handle = C.c_void_p()
+        L.check(self.lib.esc_synth_create(C.byref(p), p_lo, n_pods if p_hi is None else p_hi, C.byref(self.handle)),
+                "esc_synth_create")
+        specs = C.POINTER(L.GroupSpec)()
+        n = C.c_int32()
+        L.check(self.lib.esc_synth_groups(self.handle, C.byref(specs), C.byref(n)))
+        self.specs, self.n_groups = specs, n.value
+        self.groups = groups_from_c(specs, n.value)
+        st = C.POINTER(L.GroupState)()
+        L.check(self.lib.esc_synth_states(self.handle, C.byref(st)))
+        self.state_ptr = st
+        self.states = [{"locked": st[i].locked, "requested_nodes": st[i].requested_nodes,
+                        "cached_cpu_m": st[i].cached_cpu_m, "cached_mem_b": st[i].cached_mem_b}
+                       for i in range(n.value)]
+        self.pod_c = L.PodSoA()
+        self.node_c = L.NodeSoA()
+        L.check(self.lib.esc_synth_view(self.handle, C.byref(self.pod_c), C.byref(self.node_c)))
+
+    def pods(self) -> dict:
+        return _view(self.pod_c, _POD_FIELDS)
+
+    def nodes(self) -> dict:
+        return _view(self.node_c, _NODE_FIELDS)
+
+    def close(self):
+        if self.handle:
+            self.lib.esc_synth_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Context:
+    """One device snapshot + the batched decision over every group."""
+
+    def __init__(self, groups, device: int = 0, rank: int = 0, world: int = 1):
+        self.lib = L.load()
+        if isinstance(groups, Synth):
+            spec_ptr, self._gkeep, self.G = groups.specs, None, groups.n_groups
+            self.groups = groups.groups
+        else:
+            spec_arr, self._gkeep = groups_to_c(groups)
+            spec_ptr, self.G = spec_arr, len(groups)
+            self.groups = list(groups)
+        self.handle = C.c_void_p()
+        L.check(self.lib.esc_ctx_create(spec_ptr, self.G, device, rank, world, C.byref(self.handle)),
+                "esc_ctx_create")
+        self.world = world
+        self._keep = []
+
+    # ------------------------------------------------------------- loading
+    def pack(self, pods: list[dict], nodes: list[dict], trackers: dict | None = None, list_mode: bool = False):
+        """K0 packer: objects -> packed SoA (numpy copies)."""
+        pk = C.c_void_p()
+        L.check(self.lib.esc_packer_create(self.handle, C.byref(pk)), "esc_packer_create")
+        try:
+            if list_mode:
+                L.check(self.lib.esc_packer_set_list_mode(pk, 1))
+            pc, npods, k1 = pods_to_c(pods)
+            nc, nnodes, k2 = nodes_to_c(nodes)
+            L.check(self.lib.esc_packer_add_pods(pk, pc, npods), "esc_packer_add_pods")
+            L.check(self.lib.esc_packer_add_nodes(pk, nc, nnodes), "esc_packer_add_nodes")
+            for g, names in (trackers or {}).items():
+                arr = (C.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+                L.check(self.lib.esc_packer_set_tracker(pk, g, arr, len(names)), "esc_packer_set_tracker")
+            ps, ns = L.PodSoA(), L.NodeSoA()
+            L.check(self.lib.esc_packer_view(pk, C.byref(ps), C.byref(ns)), "esc_packer_view")
+            pods_np = {k: v.copy() for k, v in _view(ps, _POD_FIELDS).items()}
+            nodes_np = {k: v.copy() for k, v in _view(ns, _NODE_FIELDS).items()}
+        finally:
+            self.lib.esc_packer_destroy(pk)
+        return pods_np, nodes_np
+
+    def load(self, pods: dict, nodes: dict, pod_offset: int = 0, node_lo: int = 0, node_hi: int | None = None,
+             replicas: int = 1):
+        L.check(self.lib.esc_set_replicas(self.handle, replicas), "esc_set_replicas")
+        ps, k1 = pod_soa(pods)
+        ns, k2 = node_soa(nodes)
+        L.check(self.lib.esc_load_pods(self.handle, C.byref(ps), pod_offset), "esc_load_pods")
+        hi = len(nodes["flags"]) if node_hi is None else node_hi
+        L.check(self.lib.esc_load_nodes(self.handle, C.byref(ns), node_lo, hi), "esc_load_nodes")
+
+    def load_synth(self, s: Synth, pod_offset: int = 0, node_lo: int = 0, node_hi: int | None = None,
+                   replicas: int = 1):
+        L.check(self.lib.esc_set_replicas(self.handle, replicas), "esc_set_replicas")
+        L.check(self.lib.esc_load_pods(self.handle, C.byref(s.pod_c), pod_offset), "esc_load_pods")
+        hi = s.node_c.n_nodes if node_hi is None else node_hi
+        L.check(self.lib.esc_load_nodes(self.handle, C.byref(s.node_c), node_lo, hi), "esc_load_nodes")
+
+    def set_state(self, states: list[dict] | None):
+        self._state = states_to_c(states, self.G)
+        L.check(self.lib.esc_set_state(self.handle, self._state), "esc_set_state")
+
+    # ------------------------------------------------------------- decision
+    def set_stream(self, stream_handle: int | None):
+        L.check(self.lib.esc_ctx_set_stream(self.handle, C.c_void_p(stream_handle or 0)), "esc_ctx_set_stream")
+
+    def use_graph(self, on: bool = True):
+        L.check(self.lib.esc_use_graph(self.handle, int(on)))
+
+    def force_wide(self, on: bool = True):
+        L.check(self.lib.esc_force_wide(self.handle, int(on)))
+
+    def set_timing(self, on: bool = True):
+        L.check(self.lib.esc_set_timing(self.handle, int(on)))
+
+    def stage_times(self) -> list[float]:
+        a = (C.c_double * 8)()
+        L.check(self.lib.esc_stage_times(self.handle, a, 8))
+        return list(a)
+
+    def run(self):
+        L.check(self.lib.esc_run(self.handle), "esc_run")
+
+    def reduce(self):
+        L.check(self.lib.esc_reduce(self.handle), "esc_reduce")
+
+    def decide(self):
+        L.check(self.lib.esc_decide(self.handle), "esc_decide")
+
+    def sync(self):
+        L.check(self.lib.esc_sync(self.handle), "esc_sync")
+
+    def exchange_buffers(self):
+        sb, mb = C.c_void_p(), C.c_void_p()
+        sc, mc = C.c_int64(), C.c_int64()
+        L.check(self.lib.esc_exchange_buffers(self.handle, C.byref(sb), C.byref(sc), C.byref(mb), C.byref(mc)))
+        return (sb.value, sc.value), (mb.value, mc.value)
+
+    def bind_exchange(self, sum_ptr: int | None, min_ptr: int | None):
+        L.check(self.lib.esc_bind_exchange_buffers(self.handle, C.c_void_p(sum_ptr or 0), C.c_void_p(min_ptr or 0)),
+                "esc_bind_exchange_buffers")
+
+    def exchange_download(self):
+        (_, sc), (_, mc) = self.exchange_buffers()
+        s = np.zeros(sc, np.int64)
+        m = np.zeros(mc, np.int64)
+        L.check(self.lib.esc_exchange_download(self.handle, s.ctypes.data_as(C.POINTER(C.c_int64)),
+                                               m.ctypes.data_as(C.POINTER(C.c_int64))), "esc_exchange_download")
+        return s, m
+
+    def exchange_upload(self, s: np.ndarray, m: np.ndarray):
+        s = np.ascontiguousarray(s, np.int64)
+        m = np.ascontiguousarray(m, np.int64)
+        L.check(self.lib.esc_exchange_upload(self.handle, s.ctypes.data_as(C.POINTER(C.c_int64)),
+                                             m.ctypes.data_as(C.POINTER(C.c_int64))), "esc_exchange_upload")
+
+    def results(self):
+        t = np.zeros(self.G, TOTALS_DTYPE)
+        d = np.zeros(self.G, DECISION_DTYPE)
+        L.check(self.lib.esc_results(self.handle, t.ctypes.data_as(C.POINTER(L.GroupTotals)),
+                                     d.ctypes.data_as(C.POINTER(L.GroupDecision))), "esc_results")
+        return t, d
+
+    def decide_all(self, states: list[dict] | None = None):
+        """One full decision (world == 1): totals and decisions for every group."""
+        self.set_state(states)
+        self.run()
+        return self.results()
+
+    # ------------------------------------------------------------- ordering
+    def sort_nodes(self):
+        L.check(self.lib.esc_sort_nodes(self.handle), "esc_sort_nodes")
+
+    def group_order(self, group: int, which: int, cap: int | None = None) -> np.ndarray:
+        n = C.c_int64()
+        L.check(self.lib.esc_group_order(self.handle, group, which, None, 0, C.byref(n)), "esc_group_order")
+        m = n.value if cap is None else min(cap, n.value)
+        out = np.zeros(max(m, 1), np.int64)
+        L.check(self.lib.esc_group_order(self.handle, group, which, out.ctypes.data_as(C.POINTER(C.c_int64)), m,
+                                         C.byref(n)), "esc_group_order")
+        return out[:m]
+
+    def close(self):
+        if self.handle:
+            self.lib.esc_ctx_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,108 @@
+"""Mirror of the reference's ``pkg/controller`` decision path over the GPU path.
+
+* ``calc_percent_usage`` / ``calc_scale_up_delta`` — pkg/controller/util.go:58 / :13
+  (the library's bit-exact scalar build of the K4 kernel's arithmetic).
+* ``taint_oldest_n`` / ``untaint_newest_n`` — scale_down.go:171 / scale_up.go:118 orderings
+  (GPU radix sort; every taint/untaint succeeds, i.e. the dry-mode walk).
+* ``Controller`` — (*Controller).RunOnce (controller.go:400) over every group in ONE
+  batched decision: listers -> K0 packer -> HIP reduce -> K4 decide.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+ERRORS = {L.ESC_ST_OK: None, L.ESC_ST_ERR_MIN_NODES: "node count less than the minimum",
+          L.ESC_ST_ERR_MAX_NODES: "node count larger than the maximum",
+          L.ESC_ST_ERR_DIV_ZERO: "cannot divide by zero in percent calculation",
+          L.ESC_ST_ERR_NEG_DELTA: "negative scale up delta",
+          L.ESC_ST_ERR_OVERFLOW: "int64 overflow (Quantity inf.Dec regime, not emulated)"}
+
+
+def calc_percent_usage(cpu_request: int, mem_request: int, cpu_capacity: int, mem_capacity: int,
+                       number_of_untainted_nodes: int):
+    """calcPercentUsage — pkg/controller/util.go:58.  Returns (cpu%, mem%, error-or-None)."""
+    a, b = C.c_double(), C.c_double()
+    st = L.load().esc_calc_percent_usage(cpu_request, mem_request, cpu_capacity, mem_capacity,
+                                         number_of_untainted_nodes, C.byref(a), C.byref(b))
+    return a.value, b.value, ERRORS.get(st, "status %d" % st)
+
+
+def calc_scale_up_delta(n_untainted: int, cpu_percent: float, mem_percent: float, cpu_request: int,
+                        mem_request: int, cached_cpu_m: int, cached_mem_b: int, scale_up_threshold_percent: int):
+    """calcScaleUpDelta — pkg/controller/util.go:13.  Returns (delta, error-or-None)."""
+    d = C.c_int64()
+    st = L.load().esc_calc_scale_up_delta(n_untainted, cpu_percent, mem_percent, cpu_request, mem_request,
+                                          cached_cpu_m, cached_mem_b, scale_up_threshold_percent, C.byref(d))
+    return d.value, ERRORS.get(st, "status %d" % st)
+
+
+def _order(created_ns, n: int, oldest: bool, device: int) -> list[int]:
+    from .k8s import _device_ctx
+    ctx = _device_ctx(device)
+    ts = np.ascontiguousarray(created_ns, np.int64)
+    k = max(0, min(int(n), len(ts)))
+    out = np.zeros(max(k, 1), np.int64)
+    L.check(ctx.lib.esc_order_by_creation(ctx.handle, ts.ctypes.data_as(C.POINTER(C.c_int64)), len(ts),
+                                          int(oldest), k, out.ctypes.data_as(C.POINTER(C.c_int64))),
+            "esc_order_by_creation")
+    return [int(x) for x in out[:k]]
+
+
+def taint_oldest_n(created_ns, n: int, device: int = 0) -> list[int]:
+    """taintOldestN — scale_down.go:171: indices (into the given list) of the n oldest."""
+    return _order(created_ns, n, True, device)
+
+
+def untaint_newest_n(created_ns, n: int, device: int = 0) -> list[int]:
+    """untaintNewestN — scale_up.go:118: indices of the n newest (over the tainted list)."""
+    return _order(created_ns, n, False, device)
+
+
+class Controller:
+    """RunOnce over every node group as one GPU decision.
+
+    ``list_pods`` / ``list_nodes`` play the informer-backed listers
+    (pkg/k8s/pod_listers.go:33, node_listers.go:33): callables returning the full
+    cluster lists (plain-dict records, escalator_amd/objects.py) or raising."""
+
+    def __init__(self, groups: list[dict], device: int = 0, dry_mode: bool = False):
+        from .context import Context
+        self.groups = [dict(g, dry_mode=bool(g.get("dry_mode")) or dry_mode) for g in groups]
+        self.ctx = Context(self.groups, device=device)
+        self.state = [{"locked": False, "requested_nodes": 0, "cached_cpu_m": 0, "cached_mem_b": 0}
+                      for _ in groups]
+        self.taint_tracker = {g: [] for g in range(len(groups))}
+
+    def run_once(self, list_pods, list_nodes) -> list[dict]:
+        try:
+            pods = list_pods()
+        except Exception as e:                   # controller.go:195-198
+            return [{"delta": 0, "err": str(e)} for _ in self.groups]
+        try:
+            nodes = list_nodes()
+        except Exception as e:                   # controller.go:202-205
+            return [{"delta": 0, "err": str(e)} for _ in self.groups]
+        trackers = {g: t for g, t in self.taint_tracker.items() if t}
+        P, N = self.ctx.pack(pods, nodes, trackers)
+        self.ctx.load(P, N)
+        tot, dec = self.ctx.decide_all(self.state)
+        out = []
+        for g in range(len(self.groups)):
+            d = dec[g]
+            self.state[g]["cached_cpu_m"] = int(d["cached_cpu_m"])        # controller.go:208-211
+            self.state[g]["cached_mem_b"] = int(d["cached_mem_b"])
+            out.append({"delta": int(d["delta"]), "err": ERRORS.get(int(d["status"])),
+                        "branch": L.BRANCHES[int(d["branch"])], "cpu_pct": float(d["cpu_pct"]),
+                        "mem_pct": float(d["mem_pct"]), "n_to_taint": int(d["n_to_taint"]),
+                        "totals": {k: int(tot[g][k]) for k in tot.dtype.names}})
+        return out
+
+    def scale_node_group(self, name: str, list_pods, list_nodes) -> tuple[int, str | None]:
+        """(*Controller).scaleNodeGroup — controller.go:192, for one named group."""
+        g = next(i for i, s in enumerate(self.groups) if s["name"] == name)
+        r = self.run_once(list_pods, list_nodes)[g]
+        return r["delta"], r["err"]

@@ -1,0 +1,700 @@
+// esc_kernels.hip — gfx950 kernels of the scale-decision hot path.
+//
+//  K1 k_pod_reduce   : FilteredPodsLister.List (pod_listers.go:33) for EVERY group at once
+//                      + ComputePodResourceRequest (scheduler/types.go:72) +
+//                      CalculatePodsRequestsTotal (util.go:27).  One pass over the pod SoA,
+//                      16-B-per-lane coalesced loads (4 pods per lane, 256 per wave), int64
+//                      per-group partials privatised in LDS (ds_add_u64), flushed once per
+//                      workgroup.  HBM-bound; no MFMA (nothing is a contraction).
+//  K2 k_node_reduce  : FilteredNodesLister.List + filterNodes (controller.go:120) +
+//                      CalculateNodesCapacityTotal(untainted) (util.go:41) + allNodes[0]
+//                      (controller.go:208).  Group-tiled LDS privatisation.
+//  K3 k_combine      : sums the per-workgroup partials into the exchanged int64 words;
+//                      for one rank it also runs K4.
+//  K4 k_decide       : calcPercentUsage / switch / calcScaleUpDelta / scaleDownTaint clamp
+//                      (util.go:13-81, controller.go:233-351, scale_down.go:138-158).
+//  K5 sort kernels   : segmented LSD radix sort for taintOldestN / untaintNewestN
+//                      (scale_down.go:171, scale_up.go:118, sort.go:18,33).
+// Wide variants      : exact any-range fallback with global atomics.
+#include <hip/hip_runtime.h>
+
+#include "esc_kernels.h"
+
+namespace esc {
+
+namespace {
+
+constexpr int BLOCK = 1024;          // 16 waves per workgroup
+constexpr int WAVES = BLOCK / 64;
+
+__device__ __forceinline__ uint4 ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ ulonglong2 ld2(const int64_t* p) {
+    return *reinterpret_cast<const ulonglong2*>(p);
+}
+
+__device__ __forceinline__ void lds_add(uint64_t* a, uint64_t v) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v);
+}
+__device__ __forceinline__ void g_add(int64_t* a, int64_t v) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v);
+}
+
+// Effective request of one pod — ComputePodResourceRequest, scheduler/types.go:72-89:
+// regular containers summed (Resource.Add, plain int64 += wraps), then max with every
+// init container (SetMaxResource; an absent key is INT64_MIN so max() ignores it),
+// then the overhead record added.  `o` walks the pod's extra records.
+__device__ __forceinline__ void pod_request(uint32_t f, uint32_t cpu0, int64_t mem0,
+                                            const int64_t* __restrict__ xc_cpu,
+                                            const int64_t* __restrict__ xc_mem, uint32_t& o,
+                                            int64_t& cpu, int64_t& mem) {
+    uint64_t c = cpu0, m = (uint64_t)mem0;
+    const uint32_t nreg = pf_xreg(f), ninit = pf_xinit(f);
+    for (uint32_t r = 0; r < nreg; ++r, ++o) { c += (uint64_t)xc_cpu[o]; m += (uint64_t)xc_mem[o]; }
+    for (uint32_t r = 0; r < ninit; ++r, ++o) {
+        const int64_t ic = xc_cpu[o], im = xc_mem[o];
+        c = ((int64_t)c >= ic) ? c : (uint64_t)ic;
+        m = ((int64_t)m >= im) ? m : (uint64_t)im;
+    }
+    if (f & ESC_PF_HAS_OVH) { c += (uint64_t)xc_cpu[o]; m += (uint64_t)xc_mem[o]; ++o; }
+    cpu = (int64_t)c;
+    mem = (int64_t)m;
+}
+
+// Wave-inclusive scan of a 64-bit value (two packed u32 counters).
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v0, int lane) {
+    unsigned long long v = v0;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        unsigned long long y = __shfl_up(v, (unsigned)d, 64);
+        if (lane >= d) v += y;
+    }
+    return (uint64_t)v;
+}
+
+__device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
+
+// ------------------------------------------------------------- accumulators
+struct PodLds {          // fast path: LDS partials of a group window
+    uint64_t* cc;        // cpu | count << 40
+    uint64_t* mem;
+    int32_t g0;
+    uint32_t gw;
+    __device__ __forceinline__ void add(uint32_t g, uint64_t vcc, uint64_t vmem) const {
+        const uint32_t i = g - (uint32_t)g0;
+        if (i < gw) { lds_add(cc + i, vcc); lds_add(mem + i, vmem); }
+    }
+};
+
+struct PodWide {         // exact path: global int64 words, values split lo32/hi
+    int64_t* w;
+    __device__ __forceinline__ void add(uint32_t g, int64_t cpu, int64_t mem) const {
+        int64_t* r = w + (int64_t)g * WP_K;
+        g_add(r + WP_CPU_LO, (int64_t)((uint64_t)cpu & 0xFFFFFFFFull));
+        g_add(r + WP_CPU_HI, cpu >> 32);
+        g_add(r + WP_MEM_LO, (int64_t)((uint64_t)mem & 0xFFFFFFFFull));
+        g_add(r + WP_MEM_HI, mem >> 32);
+        g_add(r + WP_CNT, 1);
+    }
+};
+
+// Per-group membership of one pod — NewPodAffinityFilterFunc (node_group.go:218) for
+// every labelled group via the pair chains, NewPodDefaultFilterFunc (:256) for the
+// default group.  Daemonset pods never reach here.
+template <class F>
+__device__ __forceinline__ void pod_groups(uint32_t f, uint32_t g, const uint32_t* __restrict__ xp,
+                                           uint32_t& q, const GroupDev& G, F&& emit) {
+    if (pf_default_ok(f) && G.default_group != NONE) emit(G.default_group);
+    const uint32_t nx = pf_xpair(f);
+    for (uint32_t k = 0;; ++k) {
+        if (g != NONE) {
+            emit(g);
+            if (G.pod_chains)
+                for (uint32_t h = G.pod_next[g]; h != NONE; h = G.pod_next[h]) emit(h);
+        }
+        if (k >= nx) break;
+        g = xp[q++];
+    }
+}
+
+}  // namespace
+
+// =====================================================================  K1 (fast)
+__global__ __launch_bounds__(BLOCK) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
+                                                      uint64_t* __restrict__ part,
+                                                      int64_t* __restrict__ wide) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    PodLds acc{lds, lds + gw, g0, gw};
+    for (uint32_t i = threadIdx.x; i < 2 * gw; i += BLOCK) lds[i] = 0;
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int64_t per = (P.n_tiles + gridDim.x - 1) / gridDim.x;
+    const int64_t t_lo = (int64_t)blockIdx.x * per;
+    const int64_t t_hi = t_lo + per < P.n_tiles ? t_lo + per : P.n_tiles;
+
+    for (int64_t t = t_lo + wid; t < t_hi; t += WAVES) {
+        const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
+        const uint4 f4 = ld4(P.flags + p0);
+        const uint4 c4 = ld4(P.cpu0 + p0);
+        const ulonglong2 m01 = ld2(P.mem0 + p0);
+        const ulonglong2 m23 = ld2(P.mem0 + p0 + 2);
+        const uint4 g4 = ld4(P.pair0 + p0);
+        const uint32_t fs[4] = {f4.x, f4.y, f4.z, f4.w};
+        const uint32_t cs[4] = {c4.x, c4.y, c4.z, c4.w};
+        const int64_t ms[4] = {(int64_t)m01.x, (int64_t)m01.y, (int64_t)m23.x, (int64_t)m23.y};
+        const uint32_t gs[4] = {g4.x, g4.y, g4.z, g4.w};
+
+        uint32_t nxc = 0, nxp = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { nxc += pf_xctr(fs[j]); nxp += pf_xpair(fs[j]); }
+        uint32_t oc = 0, op = 0;
+        if (__ballot((nxc | nxp) != 0)) {            // wave-uniform: locate the extras
+            const uint64_t v = (uint64_t)nxc | ((uint64_t)nxp << 32);
+            const uint64_t s = wave_incl_scan(v, lane) - v;
+            oc = P.xc_base[t] + (uint32_t)s;
+            op = P.xp_base[t] + (uint32_t)(s >> 32);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t f = fs[j];
+            if (f & ESC_PF_DAEMONSET) {              // PodIsDaemonSet -> no group (node_group.go:221,259)
+                oc += pf_xctr(f);
+                op += pf_xpair(f);
+                continue;
+            }
+            int64_t cpu, mem;
+            pod_request(f, cs[j], ms[j], P.xc_cpu, P.xc_mem, oc, cpu, mem);
+            if ((uint64_t)cpu >= (uint64_t)POD_CPU_LIMIT || (uint64_t)mem >= (uint64_t)POD_MEM_LIMIT) {
+                // Outside the packed range: exact spill to the wide accumulators.
+                const PodWide spill{wide};
+                pod_groups(f, gs[j], P.xp, op, G, [&](uint32_t g) {
+                    if (g - (uint32_t)g0 < gw) spill.add(g, cpu, mem);
+                });
+                continue;
+            }
+            const uint64_t vcc = (uint64_t)cpu | (1ull << CNT_SHIFT);
+            pod_groups(f, gs[j], P.xp, op, G, [&](uint32_t g) { acc.add(g, vcc, (uint64_t)mem); });
+        }
+    }
+    __syncthreads();
+    uint64_t* out = part + (int64_t)blockIdx.x * 2 * G.G + g0;
+    for (uint32_t i = threadIdx.x; i < gw; i += BLOCK) {
+        out[i] = acc.cc[i];
+        out[G.G + i] = acc.mem[i];
+    }
+}
+
+// =====================================================================  K1 (wide)
+__global__ __launch_bounds__(256) void k_pod_wide(PodDev P, GroupDev G, int64_t* __restrict__ wide) {
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    PodWide acc{wide};
+    for (int64_t t = wave; t < P.n_tiles; t += nwaves) {
+        const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
+        uint32_t nxc = 0, nxp = 0;
+        for (int j = 0; j < 4; ++j) { nxc += pf_xctr(P.flags[p0 + j]); nxp += pf_xpair(P.flags[p0 + j]); }
+        const uint64_t v = (uint64_t)nxc | ((uint64_t)nxp << 32);
+        const uint64_t s = wave_incl_scan(v, lane) - v;
+        uint32_t oc = P.xc_base[t] + (uint32_t)s, op = P.xp_base[t] + (uint32_t)(s >> 32);
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t f = P.flags[p0 + j];
+            if (f & ESC_PF_DAEMONSET) { oc += pf_xctr(f); op += pf_xpair(f); continue; }
+            int64_t cpu, mem;
+            pod_request(f, P.cpu0[p0 + j], P.mem0[p0 + j], P.xc_cpu, P.xc_mem, oc, cpu, mem);
+            pod_groups(f, P.pair0[p0 + j], P.xp, op, G, [&](uint32_t g) { acc.add(g, cpu, mem); });
+        }
+    }
+}
+
+// =====================================================================  K2 nodes
+namespace {
+
+// Is (node, group) in the group's dry-mode taintTracker (controller.go:128-133)?
+__device__ __forceinline__ bool tracked(const NodeDev& N, int32_t node, int32_t g) {
+    int64_t lo = 0, hi = N.n_trk;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int32_t a = N.trk_node[mid], b = N.trk_group[mid];
+        if (a < node || (a == node && b < g)) lo = mid + 1; else hi = mid;
+    }
+    return lo < N.n_trk && N.trk_node[lo] == node && N.trk_group[lo] == g;
+}
+
+// filterNodes classification (controller.go:125-150): 0 untainted, 1 tainted, 2 cordoned.
+// Dry mode separates only tracker members; cordoned nodes are not split out there.
+__device__ __forceinline__ int node_class(const NodeDev& N, const GroupDev& G, uint32_t f, int64_t i,
+                                          uint32_t g) {
+    if (G.dry[g]) return ((f & ESC_NF_TRACKED) && tracked(N, (int32_t)i, (int32_t)g)) ? 1 : 0;
+    if (f & ESC_NF_UNSCHED) return 2;
+    return (f & ESC_NF_TAINTED) ? 1 : 0;
+}
+
+template <class F>
+__device__ __forceinline__ void node_groups(const NodeDev& N, const GroupDev& G, uint32_t f, int64_t i,
+                                            F&& emit) {
+    uint32_t g = N.label0[i];
+    const uint32_t nx = nf_xlbl(f);
+    uint32_t q = nx ? N.xl_off[i] : 0;
+    for (uint32_t k = 0;; ++k) {
+        if (g != NONE) {
+            emit(g);
+            if (G.node_chains)
+                for (uint32_t h = G.node_next[g]; h != NONE; h = G.node_next[h]) emit(h);
+        }
+        if (k >= nx) break;
+        g = N.xl[q++];
+    }
+}
+
+}  // namespace
+
+// Exact (any-range) node contribution; WN_FIRST keeps ~index under atomicMax so the
+// all-zero row means "no member" and the accumulators can self-clean to zero.
+__device__ __forceinline__ void node_wide_add(const NodeDev& N, const GroupDev& G, int64_t* __restrict__ wide,
+                                              uint32_t f, int64_t i, uint32_t g, int64_t cpu, int64_t m) {
+    int64_t* r = wide + (int64_t)g * WN_K;
+    atomicMax(reinterpret_cast<unsigned long long*>(r + WN_FIRST), ~(unsigned long long)i);
+    const int c = node_class(N, G, f, i, g);
+    if (c == 0) {
+        g_add(r + WN_CPU_LO, (int64_t)((uint64_t)cpu & 0xFFFFFFFFull));
+        g_add(r + WN_CPU_HI, cpu >> 32);
+        g_add(r + WN_MEM_LO, (int64_t)((uint64_t)m & 0xFFFFFFFFull));
+        g_add(r + WN_MEM_HI, m >> 32);
+        g_add(r + WN_UNT, 1);
+    } else {
+        g_add(r + (c == 1 ? WN_TAINT : WN_CORD), 1);
+    }
+}
+
+// grid (n_chunk, n_gtile); LDS tile of gt groups: cc, mem, tc (u64), first (u32).
+__global__ __launch_bounds__(BLOCK) void k_node_reduce(NodeDev N, GroupDev G, int32_t gt,
+                                                       uint64_t* __restrict__ part,
+                                                       int64_t* __restrict__ wide) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    uint64_t* cc = lds;
+    uint64_t* mem = lds + gt;
+    uint64_t* tc = lds + 2 * gt;
+    uint32_t* first = reinterpret_cast<uint32_t*>(lds + 3 * gt);
+    for (int32_t i = threadIdx.x; i < gt; i += BLOCK) { cc[i] = 0; mem[i] = 0; tc[i] = 0; first[i] = NONE; }
+    __syncthreads();
+    const uint32_t g_lo = blockIdx.y * (uint32_t)gt;
+    const uint32_t g_n = (uint32_t)min(gt, G.G - (int32_t)g_lo);
+    const int64_t n = N.hi - N.lo;
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = N.lo + (int64_t)blockIdx.x * per;
+    const int64_t hi = imin64(N.hi, lo + per);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += BLOCK) {
+        const uint32_t f = N.flags[i];
+        const int64_t cpu = N.cpu[i], m = N.mem[i];
+        if ((uint64_t)cpu >= (uint64_t)NODE_CPU_LIMIT || (uint64_t)m >= (uint64_t)NODE_MEM_LIMIT) {
+            node_groups(N, G, f, i, [&](uint32_t g) {
+                if (g - g_lo < g_n) node_wide_add(N, G, wide, f, i, g, cpu, m);
+            });
+            continue;
+        }
+        node_groups(N, G, f, i, [&](uint32_t g) {
+            const uint32_t k = g - g_lo;
+            if (k >= g_n) return;
+            atomicMin(first + k, (uint32_t)i);
+            const int c = node_class(N, G, f, i, g);
+            if (c == 0) { lds_add(cc + k, (uint64_t)cpu | (1ull << CNT_SHIFT)); lds_add(mem + k, (uint64_t)m); }
+            else lds_add(tc + k, c == 1 ? 1ull : (1ull << 32));
+        });
+    }
+    __syncthreads();
+    uint64_t* out = part + (int64_t)blockIdx.x * 4 * G.G + g_lo;
+    for (uint32_t k = threadIdx.x; k < g_n; k += BLOCK) {
+        out[k] = cc[k];
+        out[G.G + k] = mem[k];
+        out[2 * G.G + k] = tc[k];
+        out[3 * G.G + k] = first[k];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_node_wide(NodeDev N, GroupDev G, int64_t* __restrict__ wide) {
+    for (int64_t i = N.lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N.hi;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t f = N.flags[i];
+        const int64_t cpu = N.cpu[i], m = N.mem[i];
+        node_groups(N, G, f, i, [&](uint32_t g) { node_wide_add(N, G, wide, f, i, g, cpu, m); });
+    }
+}
+
+// ===================================================================== K3 / K4
+namespace {
+
+constexpr int CB_WAVES = 8;
+
+__device__ __forceinline__ void u128_add(uint64_t& lo, uint64_t& hi, uint64_t v) { lo += v; hi += (lo < v) ? 1 : 0; }
+
+__device__ __forceinline__ void split_store(int64_t* w, int k, __int128 t) {
+    w[k] = (int64_t)((unsigned __int128)t & 0xFFFFFFFFull);
+    w[k + 1] = (int64_t)(t >> 32);
+}
+
+// Exact total from split words; false when it is outside int64 (Quantity -> inf.Dec).
+__device__ __forceinline__ bool join_split(int64_t lo_sum, int64_t hi_sum, int64_t& out) {
+    const __int128 t = ((__int128)hi_sum << 32) + (__int128)lo_sum;
+    out = (int64_t)t;
+    return t >= (__int128)INT64_MIN && t <= (__int128)INT64_MAX;
+}
+
+__device__ __forceinline__ void finalize(const GroupDev& G, const NodeDev& N, int32_t g,
+                                         const int64_t* __restrict__ w, int64_t first,
+                                         esc_group_decision* __restrict__ dec) {
+    Totals t;
+    int64_t flags = 0;
+    if (!join_split(w[TW_POD_CPU_LO], w[TW_POD_CPU_HI], t.pod_cpu)) flags |= ESC_TF_POD_OVERFLOW;
+    if (!join_split(w[TW_POD_MEM_LO], w[TW_POD_MEM_HI], t.pod_mem)) flags |= ESC_TF_POD_OVERFLOW;
+    t.n_pods = w[TW_N_PODS];
+    if (!join_split(w[TW_NODE_CPU_LO], w[TW_NODE_CPU_HI], t.node_cpu)) flags |= ESC_TF_NODE_OVERFLOW;
+    if (!join_split(w[TW_NODE_MEM_LO], w[TW_NODE_MEM_HI], t.node_mem)) flags |= ESC_TF_NODE_OVERFLOW;
+    t.n_unt = w[TW_N_UNT];
+    t.n_taint = w[TW_N_TAINT];
+    t.n_cord = w[TW_N_CORD];
+    t.n_nodes = t.n_unt + t.n_taint + t.n_cord;
+    t.first = first;
+    t.first_cpu = first != INT64_MAX ? N.cpu[first] : 0;
+    t.first_mem = first != INT64_MAX ? N.mem[first] : 0;
+    t.flags = flags;
+    decide_one(G.params[g], t, dec[g]);
+}
+
+}  // namespace
+
+// Row-parallel reduction of the per-workgroup partials: a workgroup owns 64 groups (one
+// per lane, coalesced 512-B row reads) and its 8 waves split the partial rows; the wide
+// accumulators are merged and reset to zero (self-cleaning for the next decision).
+__global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N,
+                                                           const uint64_t* __restrict__ pod_part, int nblk,
+                                                           const uint64_t* __restrict__ node_part, int n_chunk,
+                                                           int64_t* __restrict__ wide_pod,
+                                                           int64_t* __restrict__ wide_node,
+                                                           int64_t* __restrict__ words,
+                                                           int64_t* __restrict__ firsts, int decide,
+                                                           esc_group_decision* __restrict__ dec) {
+    constexpr int NW = 12;
+    __shared__ uint64_t red[CB_WAVES][NW][64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int32_t g = blockIdx.x * 64 + lane;
+    const bool ok = g < G.G;
+    uint64_t a[NW] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // a: 0 pcpu 1 pcnt 2 pmem_lo 3 pmem_hi 4 ncpu 5 nunt 6 nmem_lo 7 nmem_hi 8 taint 9 cord 10 first
+    a[10] = ~0ull;
+    if (ok) {
+        for (int b = wid; b < nblk; b += CB_WAVES) {
+            const uint64_t c = pod_part[(int64_t)b * 2 * G.G + g];
+            a[0] += c & CPU_MASK;
+            a[1] += c >> CNT_SHIFT;
+            u128_add(a[2], a[3], pod_part[((int64_t)b * 2 + 1) * G.G + g]);
+        }
+        for (int c = wid; c < n_chunk; c += CB_WAVES) {
+            const uint64_t* r = node_part + (int64_t)c * 4 * G.G + g;
+            const uint64_t x = r[0];
+            a[4] += x & CPU_MASK;
+            a[5] += x >> CNT_SHIFT;
+            u128_add(a[6], a[7], r[G.G]);
+            const uint64_t tc = r[2 * G.G];
+            a[8] += tc & 0xFFFFFFFFull;
+            a[9] += tc >> 32;
+            const uint64_t fv = r[3 * G.G];
+            a[10] = fv < a[10] ? fv : a[10];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NW; ++k) red[wid][k][lane] = a[k];
+    __syncthreads();
+    if (wid != 0 || !ok) return;
+    for (int w = 1; w < CB_WAVES; ++w) {
+        a[0] += red[w][0][lane];
+        a[1] += red[w][1][lane];
+        u128_add(a[2], a[3], red[w][2][lane]); a[3] += red[w][3][lane];
+        a[4] += red[w][4][lane];
+        a[5] += red[w][5][lane];
+        u128_add(a[6], a[7], red[w][6][lane]); a[7] += red[w][7][lane];
+        a[8] += red[w][8][lane];
+        a[9] += red[w][9][lane];
+        a[10] = red[w][10][lane] < a[10] ? red[w][10][lane] : a[10];
+    }
+    int64_t* wp = wide_pod + (int64_t)g * WP_K;
+    int64_t* wn = wide_node + (int64_t)g * WN_K;
+    int64_t p[WP_K], q[WN_K];
+#pragma unroll
+    for (int k = 0; k < WP_K; ++k) { p[k] = wp[k]; wp[k] = 0; }
+#pragma unroll
+    for (int k = 0; k < WN_K; ++k) { q[k] = wn[k]; wn[k] = 0; }
+    int64_t* w = words + (int64_t)g * TW_K;
+    const __int128 pcpu = (__int128)a[0] + ((__int128)p[WP_CPU_HI] << 32) + (__int128)p[WP_CPU_LO];
+    const __int128 pmem = (__int128)(((unsigned __int128)a[3] << 64) | a[2]) + ((__int128)p[WP_MEM_HI] << 32) +
+                          (__int128)p[WP_MEM_LO];
+    const __int128 ncpu = (__int128)a[4] + ((__int128)q[WN_CPU_HI] << 32) + (__int128)q[WN_CPU_LO];
+    const __int128 nmem = (__int128)(((unsigned __int128)a[7] << 64) | a[6]) + ((__int128)q[WN_MEM_HI] << 32) +
+                          (__int128)q[WN_MEM_LO];
+    split_store(w, TW_POD_CPU_LO, pcpu);
+    split_store(w, TW_POD_MEM_LO, pmem);
+    w[TW_N_PODS] = (int64_t)a[1] + p[WP_CNT];
+    split_store(w, TW_NODE_CPU_LO, ncpu);
+    split_store(w, TW_NODE_MEM_LO, nmem);
+    w[TW_N_UNT] = (int64_t)a[5] + q[WN_UNT];
+    w[TW_N_TAINT] = (int64_t)a[8] + q[WN_TAINT];
+    w[TW_N_CORD] = (int64_t)a[9] + q[WN_CORD];
+    int64_t fst = a[10] >= (uint64_t)NONE ? INT64_MAX : (int64_t)a[10];
+    if (q[WN_FIRST] != 0) {
+        const int64_t fw = (int64_t)~(uint64_t)q[WN_FIRST];
+        fst = fw < fst ? fw : fst;
+    }
+    firsts[g] = fst;
+    if (decide) finalize(G, N, g, w, fst, dec);
+}
+
+__global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ words,
+                                                const int64_t* __restrict__ firsts,
+                                                esc_group_decision* __restrict__ dec) {
+    const int32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= G.G) return;
+    finalize(G, N, g, words + (int64_t)g * TW_K, firsts[g], dec);
+}
+
+// ===================================================================== K5 sort
+// Key: [group | class(2) | creation offset (R bits)], value: node index.  Class 1
+// (tainted) stores the complemented offset so ascending order is newest-first.
+namespace {
+constexpr int SORT_BLOCK = 1024;
+constexpr int SORT_WAVES = SORT_BLOCK / 64;
+}
+
+// Membership count per node chunk (pass 1 of the deterministic expansion).
+__global__ __launch_bounds__(SORT_BLOCK) void k_sort_count(NodeDev N, GroupDev G, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t tot;
+    if (threadIdx.x == 0) tot = 0;
+    __syncthreads();
+    const int64_t n = N.hi - N.lo;
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = N.lo + (int64_t)blockIdx.x * per, hi = imin64(N.hi, lo + per);
+    uint32_t c = 0;
+    for (int64_t i = lo + threadIdx.x; i < hi; i += SORT_BLOCK)
+        node_groups(N, G, N.flags[i], i, [&](uint32_t) { ++c; });
+    atomicAdd(&tot, c);
+    __syncthreads();
+    if (threadIdx.x == 0) hist[blockIdx.x] = tot;
+}
+
+// Exclusive scan of n u32 in place by one workgroup; total to *total.
+__global__ __launch_bounds__(SORT_BLOCK) void k_scan_small(uint32_t* __restrict__ a, int n, uint32_t* __restrict__ total) {
+    __shared__ uint32_t carry;
+    __shared__ uint32_t wsum[SORT_WAVES];
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int base = 0; base < n; base += SORT_BLOCK) {
+        const int i = base + threadIdx.x;
+        const uint32_t v = i < n ? a[i] : 0;
+        uint32_t s = v;
+        for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(s, d, 64); if (lane >= d) s += y; }
+        if (lane == 63) wsum[wid] = s;
+        __syncthreads();
+        uint32_t wpre = 0;
+        for (int k = 0; k < wid; ++k) wpre += wsum[k];
+        uint32_t blk = 0;
+        for (int k = 0; k < SORT_WAVES; ++k) blk += wsum[k];
+        if (i < n) a[i] = carry + wpre + s - v;
+        __syncthreads();
+        if (threadIdx.x == 0) carry += blk;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && total) *total = carry;
+}
+
+// Pass 2: write memberships in node order (stable => ties resolve by node index).
+__global__ __launch_bounds__(SORT_BLOCK) void k_sort_expand(NodeDev N, GroupDev G, const uint32_t* __restrict__ base,
+                                                            int64_t ts_min, uint64_t ts_div,
+                                                            int R, uint64_t* __restrict__ keys,
+                                                            uint32_t* __restrict__ vals) {
+    __shared__ uint32_t wsum[SORT_WAVES];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = base[blockIdx.x];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int64_t n = N.hi - N.lo;
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = N.lo + (int64_t)blockIdx.x * per, hi = imin64(N.hi, lo + per);
+    const uint64_t rmask = R >= 64 ? ~0ull : ((1ull << R) - 1);
+    for (int64_t b = lo; b < hi; b += SORT_BLOCK) {
+        const int64_t i = b + threadIdx.x;
+        uint32_t c = 0;
+        uint32_t f = 0;
+        if (i < hi) { f = N.flags[i]; node_groups(N, G, f, i, [&](uint32_t) { ++c; }); }
+        uint32_t s = c;
+        for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(s, d, 64); if (lane >= d) s += y; }
+        if (lane == 63) wsum[wid] = s;
+        __syncthreads();
+        uint32_t pos = carry + s - c;
+        for (int k = 0; k < wid; ++k) pos += wsum[k];
+        if (i < hi && c) {
+            uint64_t off = (uint64_t)(N.created[i] - ts_min);
+            off = ts_div > 1 ? off / ts_div : off;
+            node_groups(N, G, f, i, [&](uint32_t g) {
+                const int cls = node_class(N, G, f, i, g);
+                const uint64_t ts = cls == 1 ? (~off & rmask) : off;
+                keys[pos] = ((uint64_t)g << (R + 2)) | ((uint64_t)cls << R) | ts;
+                vals[pos] = (uint32_t)i;
+                ++pos;
+            });
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) { uint32_t t = 0; for (int k = 0; k < SORT_WAVES; ++k) t += wsum[k]; carry += t; }
+        __syncthreads();
+    }
+}
+
+// One LSD pass, 8-bit digit at `shift`: per-block digit histogram.
+__global__ __launch_bounds__(SORT_BLOCK) void k_radix_hist(const uint64_t* __restrict__ keys, int64_t n, int shift,
+                                                           uint32_t* __restrict__ hist) {
+    __shared__ uint32_t h[256];
+    for (int i = threadIdx.x; i < 256; i += SORT_BLOCK) h[i] = 0;
+    __syncthreads();
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += SORT_BLOCK) atomicAdd(&h[(keys[i] >> shift) & 255], 1u);
+    __syncthreads();
+    for (int d = threadIdx.x; d < 256; d += SORT_BLOCK) hist[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
+}
+
+// Stable scatter: rank = digit offset of the block + rank inside the block in input order.
+__global__ __launch_bounds__(SORT_BLOCK) void k_radix_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                              uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                              int64_t n, int shift, const uint32_t* __restrict__ hist) {
+    __shared__ uint32_t run[256];
+    __shared__ uint32_t wh[SORT_WAVES][256];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int d = threadIdx.x; d < 256; d += SORT_BLOCK) run[d] = hist[(int64_t)d * gridDim.x + blockIdx.x];
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int64_t b = lo; b < hi; b += SORT_BLOCK) {
+        for (int k = threadIdx.x; k < SORT_WAVES * 256; k += SORT_BLOCK) (&wh[0][0])[k] = 0;
+        __syncthreads();
+        const int64_t i = b + threadIdx.x;
+        const bool ok = i < hi;
+        uint64_t key = ok ? kin[i] : 0;
+        uint32_t val = ok ? vin[i] : 0;
+        const uint32_t d = (uint32_t)(key >> shift) & 255;
+        unsigned long long m = __ballot(ok);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            const unsigned long long bb = __ballot((d >> bit) & 1);
+            m &= ((d >> bit) & 1) ? bb : ~bb;
+        }
+        const uint32_t r_in_wave = __popcll(m & lt);
+        if (ok && r_in_wave == 0) wh[wid][d] = __popcll(m);
+        __syncthreads();
+        uint32_t pre = 0;
+        for (int k = 0; k < wid; ++k) pre += wh[k][d];
+        if (ok) {
+            const uint32_t dst = run[d] + pre + r_in_wave;
+            kout[dst] = key;
+            vout[dst] = val;
+        }
+        __syncthreads();
+        for (int dd = threadIdx.x; dd < 256; dd += SORT_BLOCK) {
+            uint32_t t = 0;
+            for (int k = 0; k < SORT_WAVES; ++k) t += wh[k][dd];
+            run[dd] += t;
+        }
+        __syncthreads();
+    }
+}
+
+// Lower bound of each (group, class) prefix in the sorted keys: seg[g*3+cls].
+__global__ __launch_bounds__(256) void k_group_bounds(const uint64_t* __restrict__ keys, int64_t n, int key_shift,
+                                                      int32_t nseg, int64_t* __restrict__ seg) {
+    const int32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s > nseg) return;
+    const uint64_t target = (uint64_t)s;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((keys[mid] >> key_shift) < target) lo = mid + 1; else hi = mid;
+    }
+    seg[s] = lo;
+}
+
+// ===================================================================== launchers
+hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk,
+                             uint64_t* part, int64_t* wide, hipStream_t st) {
+    const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
+    hipLaunchKernelGGL(k_pod_reduce, dim3(nblk), dim3(BLOCK), lds, st, p, g, g0, (uint32_t)gw, part, wide);
+    return hipGetLastError();
+}
+
+hipError_t launch_node_reduce(const NodeDev& n, const GroupDev& g, int n_chunk, int gt,
+                              uint64_t* part, int64_t* wide, hipStream_t st) {
+    const int n_tiles = (g.G + gt - 1) / gt;
+    const size_t lds = (size_t)gt * (3 * sizeof(uint64_t) + sizeof(uint32_t));
+    hipLaunchKernelGGL(k_node_reduce, dim3(n_chunk, n_tiles), dim3(BLOCK), lds, st, n, g, gt, part, wide);
+    return hipGetLastError();
+}
+
+hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* pod_part, int nblk,
+                          const uint64_t* node_part, int n_chunk, int64_t* wide_pod, int64_t* wide_node,
+                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st) {
+    hipLaunchKernelGGL(k_combine, dim3((g.G + 63) / 64), dim3(CB_WAVES * 64), 0, st, g, n, pod_part, nblk,
+                       node_part, n_chunk, wide_pod, wide_node, words, first, decide ? 1 : 0, dec);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st) {
+    hipLaunchKernelGGL(k_pod_wide, dim3(1024), dim3(256), 0, st, p, g, wide);
+    return hipGetLastError();
+}
+
+hipError_t launch_wide_nodes(const NodeDev& n, const GroupDev& g, int64_t* wide, hipStream_t st) {
+    hipLaunchKernelGGL(k_node_wide, dim3(1024), dim3(256), 0, st, n, g, wide);
+    return hipGetLastError();
+}
+
+hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* words,
+                         const int64_t* first, esc_group_decision* dec, hipStream_t st) {
+    hipLaunchKernelGGL(k_decide, dim3((g.G + 255) / 256), dim3(256), 0, st, g, n, words, first, dec);
+    return hipGetLastError();
+}
+
+hipError_t launch_sort_count(const NodeDev& n, const GroupDev& g, int nblk, uint32_t* hist, hipStream_t st) {
+    hipLaunchKernelGGL(k_sort_count, dim3(nblk), dim3(SORT_BLOCK), 0, st, n, g, hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_scan_small(uint32_t* a, int n, uint32_t* total, hipStream_t st) {
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SORT_BLOCK), 0, st, a, n, total);
+    return hipGetLastError();
+}
+
+hipError_t launch_sort_expand2(const NodeDev& n, const GroupDev& g, int nblk, const uint32_t* base,
+                               int64_t ts_min, uint64_t ts_div, int R, uint64_t* keys, uint32_t* vals,
+                               hipStream_t st) {
+    hipLaunchKernelGGL(k_sort_expand, dim3(nblk), dim3(SORT_BLOCK), 0, st, n, g, base, ts_min, ts_div, R,
+                       keys, vals);
+    return hipGetLastError();
+}
+
+hipError_t launch_radix_pass(const uint64_t* kin, const uint32_t* vin, uint64_t* kout, uint32_t* vout,
+                             int64_t n, int shift, int nblk, uint32_t* hist, hipStream_t st) {
+    hipLaunchKernelGGL(k_radix_hist, dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, n, shift, hist);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SORT_BLOCK), 0, st, hist, nblk * 256, (uint32_t*)nullptr);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_radix_scatter, dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, vin, kout, vout, n, shift, hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_group_bounds(const uint64_t* keys, int64_t n, int key_shift, int32_t nseg, int64_t* seg,
+                               hipStream_t st) {
+    hipLaunchKernelGGL(k_group_bounds, dim3((nseg + 1 + 255) / 256), dim3(256), 0, st, keys, n, key_shift, nseg, seg);
+    return hipGetLastError();
+}
+
+}  // namespace esc

@@ -1,0 +1,276 @@
+// esc_pack.cpp — K0 host packer / interner.
+//
+// Replaces the object walk each group's lister performs on every scan
+// (FilteredPodsLister.List pkg/k8s/pod_listers.go:33, FilteredNodesLister.List
+// pkg/k8s/node_listers.go:33) by ONE pass that turns *v1.Pod / *v1.Node field copies
+// into the struct-of-arrays the kernels stream:
+//   - (key,value) strings are interned against the groups' label pairs
+//     (node_group.go:226-247, :280), keeping only pairs some group selects;
+//   - the group-independent predicates PodIsDaemonSet (util.go:11), PodIsStatic
+//     (util.go:21) and the default filter's selector/affinity tests
+//     (node_group.go:271-273) become flag bits;
+//   - container requests become the (inline + extra records) encoding that
+//     ComputePodResourceRequest (scheduler/types.go:72-89) is evaluated on by K1.
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <set>
+
+#include "esc_internal.h"
+
+using namespace esc;
+
+void GroupIndex::build(const esc_group_spec* specs, int32_t n) {
+    G = n;
+    groups.resize(n);
+    default_group = -1;
+    for (int32_t g = 0; g < n; ++g) {
+        GroupSpecCopy& c = groups[g];
+        c.name = specs[g].name ? specs[g].name : "";
+        c.key = specs[g].label_key ? specs[g].label_key : "";
+        c.value = specs[g].label_value ? specs[g].label_value : "";
+        c.spec = specs[g];
+        c.spec.name = c.name.c_str();
+        c.spec.label_key = c.key.c_str();
+        c.spec.label_value = c.value.c_str();
+        // pkg/controller/client.go:59 — the lister choice is by name; names are map keys
+        // in the reference (controller.go:93), so at most one "default" exists.
+        if (c.name == "default" && default_group < 0) default_group = g;
+    }
+    // Re-point after the vector is final (no reallocation below).
+    for (auto& c : groups) { c.spec.name = c.name.c_str(); c.spec.label_key = c.key.c_str(); c.spec.label_value = c.value.c_str(); }
+    pod_next.assign(n, NONE);
+    node_next.assign(n, NONE);
+    pod_head.clear();
+    node_head.clear();
+    std::unordered_map<std::string, uint32_t> pod_tail, node_tail;
+    pod_chains = node_chains = false;
+    for (int32_t g = 0; g < n; ++g) {
+        std::string k = pair_key(groups[g].key.c_str(), groups[g].value.c_str());
+        auto it = node_tail.find(k);
+        if (it == node_tail.end()) { node_head[k] = g; node_tail[k] = g; }
+        else { node_next[it->second] = g; it->second = g; node_chains = true; }
+        if (g == default_group) continue;
+        auto jt = pod_tail.find(k);
+        if (jt == pod_tail.end()) { pod_head[k] = g; pod_tail[k] = g; }
+        else { pod_next[jt->second] = g; jt->second = g; pod_chains = true; }
+    }
+}
+
+void HostSnapshot::view(esc_pod_soa* p, esc_node_soa* n) const {
+    if (p) {
+        p->n_pods = (int64_t)flags.size();
+        p->flags = flags.data(); p->cpu0 = cpu0.data(); p->mem0 = mem0.data(); p->pair0 = pair0.data();
+        p->xc_cpu = xc_cpu.data(); p->xc_mem = xc_mem.data(); p->n_xc = (int64_t)xc_cpu.size();
+        p->xp_group = xp.data(); p->n_xp = (int64_t)xp.size();
+    }
+    if (n) {
+        n->n_nodes = (int64_t)nflags.size();
+        n->flags = nflags.data(); n->label0 = label0.data(); n->cpu = ncpu.data(); n->mem = nmem.data();
+        n->created_ns = created.data(); n->xl_group = xl.data(); n->n_xl = (int64_t)xl.size();
+        n->trk_node = trk_node.data(); n->trk_group = trk_group.data(); n->n_trk = (int64_t)trk_node.size();
+    }
+}
+
+struct esc_packer {
+    const GroupIndex* gi = nullptr;
+    bool list_mode = false;
+    bool finished = false;
+    HostSnapshot s;
+    std::vector<std::string> node_names;
+    std::vector<std::vector<std::string>> trackers;
+};
+
+namespace {
+
+inline int64_t req_or(int32_t has, int64_t v, int64_t absent) { return has ? v : absent; }
+
+int32_t pack_pod(esc_packer* pk, const esc_pod_obj& o) {
+    HostSnapshot& s = pk->s;
+    uint32_t f = 0;
+    std::vector<uint32_t> heads;
+    if (!pk->list_mode) {
+        for (int32_t i = 0; i < o.n_owner_kinds; ++i)                        // util.go:12-16
+            if (o.owner_kinds[i] && std::strcmp(o.owner_kinds[i], "DaemonSet") == 0) { f |= ESC_PF_DAEMONSET; break; }
+        if (o.has_config_source && o.config_source && std::strcmp(o.config_source, "file") == 0)
+            f |= ESC_PF_STATIC;                                              // util.go:22-23
+        if (o.n_node_selector > 0) f |= ESC_PF_HAS_SEL;                      // node_group.go:271
+        if (o.has_affinity && (o.has_node_affinity || o.has_pod_affinity || o.has_pod_anti_affinity))
+            f |= ESC_PF_AFF_BLOCK;                                           // node_group.go:271-273
+        // NewPodAffinityFilterFunc's two match routes (node_group.go:226-249) as a set of
+        // head groups; a group counts a pod once however many routes match.
+        for (int32_t i = 0; i < o.n_node_selector; ++i) {
+            uint32_t h = pk->gi->head(o.node_selector[i].key, o.node_selector[i].value, 0);
+            if (h != NONE) heads.push_back(h);
+        }
+        if (o.has_affinity && o.has_node_affinity && o.has_required) {     // unwrapNodeSelectorTerms :208
+            for (int32_t e = 0; e < o.n_exprs; ++e) {
+                const esc_selector_expr& x = o.exprs[e];
+                if (!x.op || std::strcmp(x.op, "In") != 0) continue;         // only In (:241)
+                for (int32_t v = 0; v < x.n_values; ++v) {
+                    uint32_t h = pk->gi->head(x.key, x.values[v], 0);
+                    if (h != NONE) heads.push_back(h);
+                }
+            }
+        }
+        std::sort(heads.begin(), heads.end());
+        heads.erase(std::unique(heads.begin(), heads.end()), heads.end());
+    } else {
+        heads.push_back(0);
+    }
+    if (heads.size() > 1 + ESC_PF_PAIR_MASK) return ESC_E_LIMIT;
+    const uint32_t pair0 = heads.empty() ? NONE : heads[0];
+    for (size_t i = 1; i < heads.size(); ++i) s.xp.push_back(heads[i]);
+    f |= (uint32_t)(heads.empty() ? 0 : heads.size() - 1) << ESC_PF_XPAIR_SHIFT;
+
+    // Containers: the first regular container is inline when its cpu fits u32.
+    uint32_t cpu0 = 0;
+    int64_t mem0 = 0;
+    int32_t first_extra = 0;
+    if (o.n_containers > 0) {
+        const esc_request& c = o.containers[0];
+        int64_t cpu = req_or(c.has_cpu, c.cpu_m, 0);
+        if (cpu >= 0 && cpu <= 0xFFFFFFFFll) {
+            cpu0 = (uint32_t)cpu;
+            mem0 = req_or(c.has_mem, c.mem_b, 0);
+            first_extra = 1;
+        }
+    }
+    const int32_t n_xreg = o.n_containers - first_extra;
+    if (n_xreg > (int32_t)ESC_PF_CNT_MASK || o.n_init_containers > (int32_t)ESC_PF_CNT_MASK) return ESC_E_LIMIT;
+    for (int32_t i = first_extra; i < o.n_containers; ++i) {             // Resource.Add types.go:14
+        s.xc_cpu.push_back(req_or(o.containers[i].has_cpu, o.containers[i].cpu_m, 0));
+        s.xc_mem.push_back(req_or(o.containers[i].has_mem, o.containers[i].mem_b, 0));
+    }
+    for (int32_t i = 0; i < o.n_init_containers; ++i) {                  // SetMaxResource types.go:30
+        s.xc_cpu.push_back(req_or(o.init_containers[i].has_cpu, o.init_containers[i].cpu_m, INT64_MIN));
+        s.xc_mem.push_back(req_or(o.init_containers[i].has_mem, o.init_containers[i].mem_b, INT64_MIN));
+    }
+    if (o.has_overhead && (o.overhead.has_cpu || o.overhead.has_mem)) {  // types.go:84-86
+        s.xc_cpu.push_back(req_or(o.overhead.has_cpu, o.overhead.cpu_m, 0));
+        s.xc_mem.push_back(req_or(o.overhead.has_mem, o.overhead.mem_b, 0));
+        f |= ESC_PF_HAS_OVH;
+    }
+    f |= (uint32_t)n_xreg << ESC_PF_XREG_SHIFT;
+    f |= (uint32_t)o.n_init_containers << ESC_PF_XINIT_SHIFT;
+    s.flags.push_back(f);
+    s.cpu0.push_back(cpu0);
+    s.mem0.push_back(mem0);
+    s.pair0.push_back(pair0);
+    return ESC_OK;
+}
+
+int32_t pack_node(esc_packer* pk, const esc_node_obj& o) {
+    HostSnapshot& s = pk->s;
+    uint32_t f = 0;
+    std::vector<uint32_t> heads;
+    if (!pk->list_mode) {
+        if (o.unschedulable) f |= ESC_NF_UNSCHED;                            // controller.go:141
+        for (int32_t i = 0; i < o.n_taints; ++i)                             // taint.go:81-85
+            if (o.taint_keys[i] && std::strcmp(o.taint_keys[i], "atlassian.com/escalator") == 0) { f |= ESC_NF_TAINTED; break; }
+        for (int32_t i = 0; i < o.n_labels; ++i) {                           // node_group.go:280
+            uint32_t h = pk->gi->head(o.labels[i].key, o.labels[i].value, 1);
+            if (h != NONE) heads.push_back(h);
+        }
+        std::sort(heads.begin(), heads.end());
+        heads.erase(std::unique(heads.begin(), heads.end()), heads.end());
+    } else {
+        heads.push_back(0);
+    }
+    if (heads.size() > 1 + ESC_PF_CNT_MASK) return ESC_E_LIMIT;
+    s.label0.push_back(heads.empty() ? NONE : heads[0]);
+    for (size_t i = 1; i < heads.size(); ++i) s.xl.push_back(heads[i]);
+    f |= (uint32_t)(heads.empty() ? 0 : heads.size() - 1) << ESC_NF_XLBL_SHIFT;
+    s.nflags.push_back(f);
+    s.ncpu.push_back(req_or(o.allocatable.has_cpu, o.allocatable.cpu_m, 0));   // util.go:47 absent -> 0
+    s.nmem.push_back(req_or(o.allocatable.has_mem, o.allocatable.mem_b, 0));
+    s.created.push_back(o.created_unix_ns);
+    pk->node_names.emplace_back(o.name ? o.name : "");
+    return ESC_OK;
+}
+
+}  // namespace
+
+// Implemented in esc_api.hip (needs the ctx layout).
+namespace esc { const GroupIndex* ctx_group_index(const esc_ctx* ctx); }
+
+extern "C" {
+
+int32_t esc_packer_create(const esc_ctx* ctx, esc_packer** out) {
+    if (!ctx || !out) return ESC_E_INVAL;
+    esc_packer* pk = new (std::nothrow) esc_packer();
+    if (!pk) return ESC_E_NOMEM;
+    pk->gi = esc::ctx_group_index(ctx);
+    pk->trackers.resize(pk->gi->G);
+    *out = pk;
+    return ESC_OK;
+}
+
+int32_t esc_packer_destroy(esc_packer* pk) { delete pk; return ESC_OK; }
+
+int32_t esc_packer_set_list_mode(esc_packer* pk, int32_t list_mode) {
+    if (!pk || !pk->s.flags.empty() || !pk->s.nflags.empty()) return ESC_E_STATE;
+    pk->list_mode = list_mode != 0;
+    return ESC_OK;
+}
+
+int32_t esc_packer_add_pods(esc_packer* pk, const esc_pod_obj* pods, int64_t n) {
+    if (!pk || (n > 0 && !pods) || n < 0) return ESC_E_INVAL;
+    if (pk->finished) return ESC_E_STATE;
+    for (int64_t i = 0; i < n; ++i) {
+        int32_t rc = pack_pod(pk, pods[i]);
+        if (rc != ESC_OK) return rc;
+    }
+    return ESC_OK;
+}
+
+int32_t esc_packer_add_nodes(esc_packer* pk, const esc_node_obj* nodes, int64_t n) {
+    if (!pk || (n > 0 && !nodes) || n < 0) return ESC_E_INVAL;
+    if (pk->finished) return ESC_E_STATE;
+    for (int64_t i = 0; i < n; ++i) {
+        int32_t rc = pack_node(pk, nodes[i]);
+        if (rc != ESC_OK) return rc;
+    }
+    return ESC_OK;
+}
+
+int32_t esc_packer_set_tracker(esc_packer* pk, int32_t group, const char* const* names, int64_t n) {
+    if (!pk || group < 0 || group >= pk->gi->G || n < 0 || (n > 0 && !names)) return ESC_E_INVAL;
+    if (pk->finished) return ESC_E_STATE;
+    auto& t = pk->trackers[group];
+    t.clear();
+    for (int64_t i = 0; i < n; ++i) t.emplace_back(names[i] ? names[i] : "");
+    return ESC_OK;
+}
+
+int32_t esc_packer_view(esc_packer* pk, esc_pod_soa* pods, esc_node_soa* nodes) {
+    if (!pk) return ESC_E_INVAL;
+    if (!pk->finished) {
+        // Resolve taintTracker names (controller.go:128-133) to (node, group) entries.
+        std::unordered_map<std::string, std::vector<int64_t>> by_name;
+        bool any = false;
+        for (auto& t : pk->trackers) any |= !t.empty();
+        if (any) {
+            for (size_t i = 0; i < pk->node_names.size(); ++i) by_name[pk->node_names[i]].push_back((int64_t)i);
+            std::vector<std::pair<int32_t, int32_t>> ent;
+            for (int32_t g = 0; g < (int32_t)pk->trackers.size(); ++g)
+                for (auto& nm : pk->trackers[g]) {
+                    auto it = by_name.find(nm);
+                    if (it == by_name.end()) continue;
+                    for (int64_t idx : it->second) ent.emplace_back((int32_t)idx, g);
+                }
+            std::sort(ent.begin(), ent.end());
+            ent.erase(std::unique(ent.begin(), ent.end()), ent.end());
+            for (auto& e : ent) {
+                pk->s.trk_node.push_back(e.first);
+                pk->s.trk_group.push_back(e.second);
+                pk->s.nflags[e.first] |= ESC_NF_TRACKED;
+            }
+        }
+        pk->finished = true;
+    }
+    pk->s.view(pods, nodes);
+    return ESC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,958 @@
+// esc_runtime.hip — host runtime behind the C ABI (include/escalator_hip.h).
+//
+// One esc_ctx per process and GPU.  The context owns the device-resident snapshot
+// (pod shard replicas + full node table), the per-workgroup partial buffers, the
+// exchanged per-group words and the decision buffers, one HIP stream (or the caller's)
+// and an optional hipGraph of the whole decision step.  The only host<->device
+// traffic per decision is the launch (a graph replay for one rank) and the copy of the
+// per-group decisions back to pinned host memory.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "esc_internal.h"
+#include "esc_kernels.h"
+
+using namespace esc;
+
+namespace {
+
+constexpr int LDS_BYTES = 160 * 1024;
+constexpr int POD_WINDOW_MAX = LDS_BYTES / 16;      // groups whose pod partials fit in LDS
+constexpr int NODE_TILE = 2048;                     // groups per node-reduce LDS tile (56 KiB)
+constexpr int MAX_STAGES = 8;
+
+#define HIP_TRY(x)                                              \
+    do {                                                        \
+        hipError_t e_ = (x);                                    \
+        if (e_ != hipSuccess) return fail_hip(e_, #x);          \
+    } while (0)
+
+thread_local char g_last_error[256];
+
+int32_t fail_hip(hipError_t e, const char* what) {
+    std::snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? ESC_E_NOMEM : ESC_E_HIP;
+}
+
+template <class T>
+hipError_t dalloc(T** p, size_t n) {
+    *p = nullptr;
+    if (n == 0) n = 1;
+    return hipMalloc(reinterpret_cast<void**>(p), n * sizeof(T));
+}
+
+template <class T>
+void dfree(T*& p) {
+    if (p) hipFree(p);
+    p = nullptr;
+}
+
+struct PodBuf {
+    uint32_t *flags = nullptr, *cpu0 = nullptr, *pair0 = nullptr, *xp = nullptr, *xc_base = nullptr,
+             *xp_base = nullptr;
+    int64_t *mem0 = nullptr, *xc_cpu = nullptr, *xc_mem = nullptr;
+    void release() {
+        dfree(flags); dfree(cpu0); dfree(pair0); dfree(xp); dfree(xc_base); dfree(xp_base);
+        dfree(mem0); dfree(xc_cpu); dfree(xc_mem);
+    }
+};
+
+struct NodeBuf {
+    uint32_t *flags = nullptr, *label0 = nullptr, *xl = nullptr, *xl_off = nullptr;
+    int64_t *cpu = nullptr, *mem = nullptr, *created = nullptr;
+    int32_t *trk_node = nullptr, *trk_group = nullptr;
+    void release() {
+        dfree(flags); dfree(label0); dfree(xl); dfree(xl_off); dfree(cpu); dfree(mem); dfree(created);
+        dfree(trk_node); dfree(trk_group);
+    }
+};
+
+int bit_width(uint64_t v) {
+    int b = 0;
+    while (v) { ++b; v >>= 1; }
+    return b;
+}
+
+}  // namespace
+
+struct esc_ctx {
+    int device = -1, rank = 0, world = 1;
+    bool has_device = false;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int cu_count = 0;
+    GroupIndex gi;
+    std::vector<GroupParams> params;
+    // device group tables
+    uint32_t *d_pod_next = nullptr, *d_node_next = nullptr;
+    uint8_t* d_dry = nullptr;
+    GroupParams* d_params = nullptr;
+    // snapshot
+    std::vector<PodBuf> pods;
+    int n_replicas = 1, cur = 0;
+    int64_t n_pods = 0, n_tiles = 0, n_xc = 0, n_xp = 0, pod_offset = 0;
+    bool pods_loaded = false;
+    NodeBuf nodes;
+    int64_t n_nodes = 0, n_xl = 0, n_trk = 0, node_lo = 0, node_hi = 0;
+    int64_t ts_min = 0, ts_max = 0;
+    bool nodes_loaded = false;
+    // work
+    int nblk = 0, n_chunk = 0, gt = 0;
+    uint64_t *d_pod_part = nullptr, *d_node_part = nullptr;
+    int64_t *d_wide_pod = nullptr, *d_wide_node = nullptr;
+    int64_t *d_words = nullptr, *d_first = nullptr;          // active exchange buffers
+    int64_t *own_words = nullptr, *own_first = nullptr;      // context-owned ones
+    esc_group_decision* d_dec = nullptr;
+    esc_group_decision* h_dec = nullptr;
+    int64_t *bound_words = nullptr, *bound_first = nullptr;  // caller-bound (RCCL) buffers
+    bool work_ready = false;
+    bool force_wide = false;
+    // graph
+    bool use_graph = false;
+    std::vector<hipGraphExec_t> graphs;
+    // timing
+    bool timing = false;
+    hipEvent_t ev[MAX_STAGES] = {};
+    double stage_ms[MAX_STAGES] = {};
+    int n_stage_ev = 0;
+    bool pending = false;
+    // sort
+    uint64_t* d_keys[2] = {nullptr, nullptr};
+    uint32_t* d_vals[2] = {nullptr, nullptr};
+    uint32_t* d_hist = nullptr;
+    uint32_t* d_total = nullptr;
+    int64_t* d_seg = nullptr;
+    int64_t sort_cap = 0, sort_n = 0;
+    int sort_src = 0;
+    int sort_R = 0;
+    bool sorted = false;
+    // per-function drop-ins run on a one-group list context
+    esc_ctx* list_ctx = nullptr;
+};
+
+namespace esc {
+const GroupIndex* ctx_group_index(const esc_ctx* ctx) { return &ctx->gi; }
+}
+
+namespace {
+
+GroupDev group_dev(const esc_ctx* c) {
+    GroupDev g;
+    g.pod_next = c->d_pod_next;
+    g.node_next = c->d_node_next;
+    g.dry = c->d_dry;
+    g.params = c->d_params;
+    g.G = c->gi.G;
+    g.default_group = c->gi.default_group < 0 ? NONE : (uint32_t)c->gi.default_group;
+    g.pod_chains = c->gi.pod_chains ? 1 : 0;
+    g.node_chains = c->gi.node_chains ? 1 : 0;
+    return g;
+}
+
+PodDev pod_dev(const esc_ctx* c, int replica) {
+    const PodBuf& b = c->pods[replica];
+    PodDev p;
+    p.flags = b.flags; p.cpu0 = b.cpu0; p.mem0 = b.mem0; p.pair0 = b.pair0;
+    p.xc_cpu = b.xc_cpu; p.xc_mem = b.xc_mem; p.xp = b.xp;
+    p.xc_base = b.xc_base; p.xp_base = b.xp_base;
+    p.n_tiles = c->n_tiles;
+    return p;
+}
+
+NodeDev node_dev(const esc_ctx* c) {
+    NodeDev n;
+    n.flags = c->nodes.flags; n.label0 = c->nodes.label0; n.cpu = c->nodes.cpu; n.mem = c->nodes.mem;
+    n.created = c->nodes.created; n.xl = c->nodes.xl; n.xl_off = c->nodes.xl_off;
+    n.trk_node = c->nodes.trk_node; n.trk_group = c->nodes.trk_group; n.n_trk = c->n_trk;
+    n.lo = c->node_lo; n.hi = c->node_hi;
+    return n;
+}
+
+void params_from(GroupParams& p, const esc_group_spec& s, const esc_group_state* st) {
+    p.min_nodes = s.min_nodes; p.max_nodes = s.max_nodes;
+    p.taint_upper = s.taint_upper_pct; p.taint_lower = s.taint_lower_pct; p.scale_up = s.scale_up_pct;
+    p.slow_rate = s.slow_removal_rate; p.fast_rate = s.fast_removal_rate;
+    p.dry = s.dry_mode ? 1 : 0;
+    p.locked = st ? st->locked : 0;
+    p.requested = st ? st->requested_nodes : 0;
+    p.cached_cpu = st ? st->cached_cpu_m : 0;
+    p.cached_mem = st ? st->cached_mem_b : 0;
+}
+
+void drop_graphs(esc_ctx* c) {
+    for (auto& g : c->graphs)
+        if (g) hipGraphExecDestroy(g);
+    c->graphs.clear();
+}
+
+void release_work(esc_ctx* c) {
+    dfree(c->d_pod_part); dfree(c->d_node_part); dfree(c->d_wide_pod); dfree(c->d_wide_node);
+    dfree(c->own_words); dfree(c->own_first); dfree(c->d_dec);
+    c->d_words = nullptr;
+    c->d_first = nullptr;
+    if (c->h_dec) hipHostFree(c->h_dec);
+    c->h_dec = nullptr;
+    c->work_ready = false;
+    drop_graphs(c);
+}
+
+void release_sort(esc_ctx* c) {
+    for (int i = 0; i < 2; ++i) { dfree(c->d_keys[i]); dfree(c->d_vals[i]); }
+    dfree(c->d_hist); dfree(c->d_total); dfree(c->d_seg);
+    c->sort_cap = 0;
+    c->sorted = false;
+}
+
+// Grid geometry for the current snapshot.
+int32_t ensure_work(esc_ctx* c) {
+    if (c->work_ready) return ESC_OK;
+    const int32_t G = c->gi.G;
+    const int gw = std::min(G, POD_WINDOW_MAX);
+    const int lds = gw * 16;
+    const int per_cu = std::max(1, std::min(2, LDS_BYTES / std::max(lds, 1)));
+    int nblk = c->cu_count * per_cu;
+    const int64_t pods_per_block = (c->n_tiles * TILE + nblk - 1) / std::max(nblk, 1);
+    if (pods_per_block > PODS_PER_BLOCK_MAX) nblk = (int)((c->n_tiles * TILE + PODS_PER_BLOCK_MAX - 1) / PODS_PER_BLOCK_MAX);
+    if (c->n_tiles == 0) nblk = 0;
+    nblk = (int)std::min<int64_t>(nblk, std::max<int64_t>(c->n_tiles, 0));
+    c->nblk = nblk;
+    // nodes: group tiles x node chunks; keep the partial flush below ~half the node bytes
+    const int64_t n_local = c->node_hi - c->node_lo;
+    c->gt = std::min(G, NODE_TILE);
+    const int n_gtile = (G + c->gt - 1) / c->gt;
+    int64_t n_chunk = std::max<int64_t>(1, (2 * c->cu_count) / n_gtile);
+    const int64_t flush_cap = std::max<int64_t>(1, n_local * 24 / (2 * (int64_t)G * 32));
+    n_chunk = std::min(n_chunk, flush_cap);
+    n_chunk = std::max<int64_t>(n_chunk, (n_local + NODES_PER_CHUNK_MAX - 1) / NODES_PER_CHUNK_MAX);
+    if (n_local == 0) n_chunk = 0;
+    c->n_chunk = (int)n_chunk;
+    HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max(nblk, 1) * 2 * G));
+    HIP_TRY(dalloc(&c->d_node_part, (size_t)std::max<int64_t>(n_chunk, 1) * 4 * G));
+    HIP_TRY(dalloc(&c->d_wide_pod, (size_t)G * WP_K));
+    HIP_TRY(dalloc(&c->d_wide_node, (size_t)G * WN_K));
+    HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)G * WP_K * sizeof(int64_t)));
+    HIP_TRY(hipMemset(c->d_wide_node, 0, (size_t)G * WN_K * sizeof(int64_t)));
+    HIP_TRY(dalloc(&c->own_words, (size_t)G * TW_K));
+    HIP_TRY(dalloc(&c->own_first, (size_t)G));
+    c->d_words = c->bound_words ? c->bound_words : c->own_words;
+    c->d_first = c->bound_first ? c->bound_first : c->own_first;
+    HIP_TRY(dalloc(&c->d_dec, (size_t)G));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_dec), (size_t)G * sizeof(esc_group_decision)));
+    c->work_ready = true;
+    return ESC_OK;
+}
+
+// Enqueue K1 + K2 + K3 (and K4 + the decision copy when decide) for replica r.
+int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
+    const GroupDev g = group_dev(c);
+    const NodeDev n = node_dev(c);
+    hipStream_t st = c->stream;
+    int e = 0;
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    int nblk = 0, n_chunk = 0;
+    if (c->force_wide) {
+        if (c->n_tiles) HIP_TRY(launch_wide_pods(pod_dev(c, r), g, c->d_wide_pod, st));
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+        if (n.hi > n.lo) HIP_TRY(launch_wide_nodes(n, g, c->d_wide_node, st));
+    } else {
+        if (c->nblk) {
+            const PodDev p = pod_dev(c, r);
+            for (int32_t g0 = 0; g0 < g.G; g0 += POD_WINDOW_MAX) {
+                const int32_t gw = std::min(POD_WINDOW_MAX, g.G - g0);
+                HIP_TRY(launch_pod_reduce(p, g, g0, gw, c->nblk, c->d_pod_part, c->d_wide_pod, st));
+            }
+        }
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+        if (c->n_chunk) HIP_TRY(launch_node_reduce(n, g, c->n_chunk, c->gt, c->d_node_part, c->d_wide_node, st));
+        nblk = c->nblk;
+        n_chunk = c->n_chunk;
+    }
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    HIP_TRY(launch_combine(g, n, c->d_pod_part, nblk, c->d_node_part, n_chunk, c->d_wide_pod, c->d_wide_node,
+                           c->d_words, c->d_first, decide, c->d_dec, st));
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    if (copy_out) {
+        HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)g.G * sizeof(esc_group_decision),
+                               hipMemcpyDeviceToHost, st));
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    }
+    c->n_stage_ev = e;
+    return ESC_OK;
+}
+
+int32_t check_ready(esc_ctx* c) {
+    if (!c) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
+    return ensure_work(c);
+}
+
+}  // namespace
+
+// ======================================================================= C ABI
+extern "C" {
+
+int32_t esc_abi_version(void) { return ESC_ABI_VERSION; }
+
+const char* esc_strerror(int32_t code) {
+    switch (code) {
+        case ESC_OK: return "ok";
+        case ESC_E_INVAL: return "invalid argument";
+        case ESC_E_HIP: return g_last_error[0] ? g_last_error : "HIP runtime error";
+        case ESC_E_NOMEM: return "out of memory";
+        case ESC_E_LIMIT: return "input exceeds an encoding limit";
+        case ESC_E_STATE: return "call order violated";
+        case ESC_E_NODEV: return "no gfx950 device available";
+        default: return "unknown error";
+    }
+}
+
+const char* esc_status_string(int32_t status) {
+    switch (status) {
+        case ESC_ST_OK: return "";
+        case ESC_ST_ERR_MIN_NODES: return "node count less than the minimum";
+        case ESC_ST_ERR_MAX_NODES: return "node count larger than the maximum";
+        case ESC_ST_ERR_DIV_ZERO: return "cannot divide by zero in percent calculation";
+        case ESC_ST_ERR_NEG_DELTA: return "negative scale up delta";
+        case ESC_ST_ERR_OVERFLOW: return "int64 overflow (Quantity inf.Dec regime, not emulated)";
+        case ESC_ST_ERR_TAINT_MIN: return "the number of nodes is less than specified minimum. Taking no action";
+        default: return "unknown status";
+    }
+}
+
+int32_t esc_taint_error(int64_t n_untainted, int32_t min_nodes, char* buf, int32_t buf_len) {
+    if (!buf || buf_len <= 0) return ESC_E_INVAL;
+    std::snprintf(buf, (size_t)buf_len, "the number of nodes(%lld) is less than specified minimum of %d. Taking no action",
+                  (long long)n_untainted, (int)min_nodes);
+    return ESC_OK;
+}
+
+int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t device, int32_t rank,
+                       int32_t world, esc_ctx** out) {
+    if (!out || !groups || n_groups <= 0 || world < 1 || rank < 0 || rank >= world) return ESC_E_INVAL;
+    if ((uint32_t)n_groups >= NONE) return ESC_E_LIMIT;
+    esc_ctx* c = new (std::nothrow) esc_ctx();
+    if (!c) return ESC_E_NOMEM;
+    c->rank = rank;
+    c->world = world;
+    c->gi.build(groups, n_groups);
+    c->params.resize(n_groups);
+    for (int32_t g = 0; g < n_groups; ++g) params_from(c->params[g], groups[g], nullptr);
+    c->pods.resize(1);
+    *out = c;
+    if (device < 0) return ESC_OK;                         // host-only: packer + scalar math
+    int n_dev = 0;
+    if (hipGetDeviceCount(&n_dev) != hipSuccess || device >= n_dev) { *out = nullptr; delete c; return ESC_E_NODEV; }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        *out = nullptr;
+        delete c;
+        return ESC_E_NODEV;
+    }
+    c->device = device;
+    c->has_device = true;
+    c->cu_count = prop.multiProcessorCount;
+    int32_t rc = ESC_OK;
+    auto fail = [&](int32_t r) { esc_ctx_destroy(c); *out = nullptr; return r; };
+    if (hipSetDevice(device) != hipSuccess) return fail(ESC_E_HIP);
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return fail(ESC_E_HIP);
+    c->own_stream = true;
+    for (int i = 0; i < MAX_STAGES; ++i)
+        if (hipEventCreate(&c->ev[i]) != hipSuccess) return fail(ESC_E_HIP);
+    const size_t G = (size_t)n_groups;
+    if (dalloc(&c->d_pod_next, G) || dalloc(&c->d_node_next, G) || dalloc(&c->d_dry, G) || dalloc(&c->d_params, G))
+        return fail(ESC_E_NOMEM);
+    std::vector<uint8_t> dry(G);
+    for (size_t g = 0; g < G; ++g) dry[g] = (uint8_t)c->params[g].dry;
+    if (hipMemcpy(c->d_pod_next, c->gi.pod_next.data(), G * 4, hipMemcpyHostToDevice) ||
+        hipMemcpy(c->d_node_next, c->gi.node_next.data(), G * 4, hipMemcpyHostToDevice) ||
+        hipMemcpy(c->d_dry, dry.data(), G, hipMemcpyHostToDevice) ||
+        hipMemcpy(c->d_params, c->params.data(), G * sizeof(GroupParams), hipMemcpyHostToDevice))
+        return fail(ESC_E_HIP);
+    (void)rc;
+    return ESC_OK;
+}
+
+int32_t esc_ctx_destroy(esc_ctx* c) {
+    if (!c) return ESC_OK;
+    if (c->list_ctx) esc_ctx_destroy(c->list_ctx);
+    if (c->has_device) {
+        hipSetDevice(c->device);
+        if (c->stream) hipStreamSynchronize(c->stream);
+        release_work(c);
+        release_sort(c);
+        for (auto& b : c->pods) b.release();
+        c->nodes.release();
+        dfree(c->d_pod_next); dfree(c->d_node_next); dfree(c->d_dry); dfree(c->d_params);
+        for (int i = 0; i < MAX_STAGES; ++i)
+            if (c->ev[i]) hipEventDestroy(c->ev[i]);
+        if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    }
+    delete c;
+    return ESC_OK;
+}
+
+int32_t esc_ctx_set_stream(esc_ctx* c, void* hip_stream) {
+    if (!c) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    drop_graphs(c);
+    if (hip_stream) {
+        c->stream = reinterpret_cast<hipStream_t>(hip_stream);
+        c->own_stream = false;
+    } else {
+        if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return ESC_E_HIP;
+        c->own_stream = true;
+    }
+    return ESC_OK;
+}
+
+int32_t esc_ctx_num_groups(const esc_ctx* c) { return c ? c->gi.G : 0; }
+
+uint32_t esc_ctx_pair_head(const esc_ctx* c, const char* key, const char* value, int32_t side) {
+    if (!c) return NONE;
+    return c->gi.head(key, value, side ? 1 : 0);
+}
+
+int32_t esc_set_replicas(esc_ctx* c, int32_t n) {
+    if (!c || n < 1 || n > 64) return ESC_E_INVAL;
+    if (c->pods_loaded) return ESC_E_STATE;
+    c->n_replicas = n;
+    return ESC_OK;
+}
+
+int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
+    if (!c || !p || p->n_pods < 0) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    const int64_t n = p->n_pods;
+    if (n > 0 && (!p->flags || !p->cpu0 || !p->mem0 || !p->pair0)) return ESC_E_INVAL;
+    if ((p->n_xc > 0 && (!p->xc_cpu || !p->xc_mem)) || (p->n_xp > 0 && !p->xp_group)) return ESC_E_INVAL;
+    if (p->n_xc >= (int64_t)0xFFFFFFFF || p->n_xp >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
+    const uint32_t G = (uint32_t)c->gi.G;
+    // Validate every group id (a bad id would index outside the LDS / group tables) and
+    // build the per-tile offsets of the extra records.
+    const int64_t n_tiles = (n + TILE - 1) / TILE;
+    std::vector<uint32_t> xc_base(std::max<int64_t>(n_tiles, 1)), xp_base(std::max<int64_t>(n_tiles, 1));
+    uint64_t sc = 0, sp = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if ((i & (TILE - 1)) == 0) { xc_base[i / TILE] = (uint32_t)sc; xp_base[i / TILE] = (uint32_t)sp; }
+        const uint32_t f = p->flags[i];
+        if (p->pair0[i] != NONE && p->pair0[i] >= G) return ESC_E_INVAL;
+        sc += pf_xctr(f);
+        sp += pf_xpair(f);
+    }
+    if ((int64_t)sc != p->n_xc || (int64_t)sp != p->n_xp) return ESC_E_INVAL;
+    for (int64_t i = 0; i < p->n_xp; ++i)
+        if (p->xp_group[i] >= G) return ESC_E_INVAL;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    drop_graphs(c);
+    release_work(c);
+    release_sort(c);
+    for (auto& b : c->pods) b.release();
+    c->pods.assign(c->n_replicas, PodBuf());
+    const int64_t npad = n_tiles * TILE;
+    for (int r = 0; r < c->n_replicas; ++r) {
+        PodBuf& b = c->pods[r];
+        HIP_TRY(dalloc(&b.flags, npad)); HIP_TRY(dalloc(&b.cpu0, npad)); HIP_TRY(dalloc(&b.mem0, npad));
+        HIP_TRY(dalloc(&b.pair0, npad)); HIP_TRY(dalloc(&b.xc_cpu, p->n_xc)); HIP_TRY(dalloc(&b.xc_mem, p->n_xc));
+        HIP_TRY(dalloc(&b.xp, p->n_xp)); HIP_TRY(dalloc(&b.xc_base, n_tiles)); HIP_TRY(dalloc(&b.xp_base, n_tiles));
+        if (r == 0) {
+            if (n) {
+                HIP_TRY(hipMemcpy(b.flags, p->flags, n * 4, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(b.cpu0, p->cpu0, n * 4, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(b.mem0, p->mem0, n * 8, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(b.pair0, p->pair0, n * 4, hipMemcpyHostToDevice));
+            }
+            if (npad > n) {
+                std::vector<uint32_t> pad_f(npad - n, ESC_PF_DAEMONSET), pad_g(npad - n, NONE);
+                HIP_TRY(hipMemcpy(b.flags + n, pad_f.data(), (npad - n) * 4, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(b.pair0 + n, pad_g.data(), (npad - n) * 4, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemset(b.cpu0 + n, 0, (npad - n) * 4));
+                HIP_TRY(hipMemset(b.mem0 + n, 0, (npad - n) * 8));
+            }
+            if (p->n_xc) {
+                HIP_TRY(hipMemcpy(b.xc_cpu, p->xc_cpu, p->n_xc * 8, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(b.xc_mem, p->xc_mem, p->n_xc * 8, hipMemcpyHostToDevice));
+            }
+            if (p->n_xp) HIP_TRY(hipMemcpy(b.xp, p->xp_group, p->n_xp * 4, hipMemcpyHostToDevice));
+            if (n_tiles) {
+                HIP_TRY(hipMemcpy(b.xc_base, xc_base.data(), n_tiles * 4, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(b.xp_base, xp_base.data(), n_tiles * 4, hipMemcpyHostToDevice));
+            }
+        } else {
+            const PodBuf& a = c->pods[0];
+            HIP_TRY(hipMemcpy(b.flags, a.flags, npad * 4, hipMemcpyDeviceToDevice));
+            HIP_TRY(hipMemcpy(b.cpu0, a.cpu0, npad * 4, hipMemcpyDeviceToDevice));
+            HIP_TRY(hipMemcpy(b.mem0, a.mem0, npad * 8, hipMemcpyDeviceToDevice));
+            HIP_TRY(hipMemcpy(b.pair0, a.pair0, npad * 4, hipMemcpyDeviceToDevice));
+            if (p->n_xc) {
+                HIP_TRY(hipMemcpy(b.xc_cpu, a.xc_cpu, p->n_xc * 8, hipMemcpyDeviceToDevice));
+                HIP_TRY(hipMemcpy(b.xc_mem, a.xc_mem, p->n_xc * 8, hipMemcpyDeviceToDevice));
+            }
+            if (p->n_xp) HIP_TRY(hipMemcpy(b.xp, a.xp, p->n_xp * 4, hipMemcpyDeviceToDevice));
+            if (n_tiles) {
+                HIP_TRY(hipMemcpy(b.xc_base, a.xc_base, n_tiles * 4, hipMemcpyDeviceToDevice));
+                HIP_TRY(hipMemcpy(b.xp_base, a.xp_base, n_tiles * 4, hipMemcpyDeviceToDevice));
+            }
+        }
+    }
+    c->n_pods = n;
+    c->n_tiles = n_tiles;
+    c->n_xc = p->n_xc;
+    c->n_xp = p->n_xp;
+    c->pod_offset = global_offset;
+    c->cur = 0;
+    c->pods_loaded = true;
+    return ESC_OK;
+}
+
+int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi) {
+    if (!c || !s || s->n_nodes < 0 || lo < 0 || hi < lo || hi > s->n_nodes) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    const int64_t n = s->n_nodes;
+    if (n >= (int64_t)0x7FFFFFFF) return ESC_E_LIMIT;
+    if (n > 0 && (!s->flags || !s->label0 || !s->cpu || !s->mem || !s->created_ns)) return ESC_E_INVAL;
+    if ((s->n_xl > 0 && !s->xl_group) || (s->n_trk > 0 && (!s->trk_node || !s->trk_group))) return ESC_E_INVAL;
+    const uint32_t G = (uint32_t)c->gi.G;
+    std::vector<uint32_t> xl_off(std::max<int64_t>(n, 1));
+    uint64_t sx = 0;
+    int64_t tmin = 0, tmax = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        xl_off[i] = (uint32_t)sx;
+        sx += nf_xlbl(s->flags[i]);
+        if (s->label0[i] != NONE && s->label0[i] >= G) return ESC_E_INVAL;
+        if (i >= lo && i < hi) {
+            if (i == lo || s->created_ns[i] < tmin) tmin = s->created_ns[i];
+            if (i == lo || s->created_ns[i] > tmax) tmax = s->created_ns[i];
+        }
+    }
+    if ((int64_t)sx != s->n_xl) return ESC_E_INVAL;
+    for (int64_t i = 0; i < s->n_xl; ++i)
+        if (s->xl_group[i] >= G) return ESC_E_INVAL;
+    for (int64_t i = 0; i < s->n_trk; ++i) {
+        if (s->trk_node[i] < 0 || s->trk_node[i] >= n || s->trk_group[i] < 0 || (uint32_t)s->trk_group[i] >= G)
+            return ESC_E_INVAL;
+        if (i && (s->trk_node[i] < s->trk_node[i - 1] ||
+                  (s->trk_node[i] == s->trk_node[i - 1] && s->trk_group[i] <= s->trk_group[i - 1])))
+            return ESC_E_INVAL;                      // must be sorted by (node, group), unique
+    }
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    drop_graphs(c);
+    release_work(c);
+    release_sort(c);
+    c->nodes.release();
+    NodeBuf& b = c->nodes;
+    HIP_TRY(dalloc(&b.flags, n)); HIP_TRY(dalloc(&b.label0, n)); HIP_TRY(dalloc(&b.cpu, n));
+    HIP_TRY(dalloc(&b.mem, n)); HIP_TRY(dalloc(&b.created, n)); HIP_TRY(dalloc(&b.xl, s->n_xl));
+    HIP_TRY(dalloc(&b.xl_off, n)); HIP_TRY(dalloc(&b.trk_node, s->n_trk)); HIP_TRY(dalloc(&b.trk_group, s->n_trk));
+    if (n) {
+        HIP_TRY(hipMemcpy(b.flags, s->flags, n * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(b.label0, s->label0, n * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(b.cpu, s->cpu, n * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(b.mem, s->mem, n * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(b.created, s->created_ns, n * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(b.xl_off, xl_off.data(), n * 4, hipMemcpyHostToDevice));
+    }
+    if (s->n_xl) HIP_TRY(hipMemcpy(b.xl, s->xl_group, s->n_xl * 4, hipMemcpyHostToDevice));
+    if (s->n_trk) {
+        HIP_TRY(hipMemcpy(b.trk_node, s->trk_node, s->n_trk * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(b.trk_group, s->trk_group, s->n_trk * 4, hipMemcpyHostToDevice));
+    }
+    c->n_nodes = n;
+    c->n_xl = s->n_xl;
+    c->n_trk = s->n_trk;
+    c->node_lo = lo;
+    c->node_hi = hi;
+    c->ts_min = tmin;
+    c->ts_max = tmax;
+    c->nodes_loaded = true;
+    return ESC_OK;
+}
+
+int32_t esc_set_state(esc_ctx* c, const esc_group_state* st) {
+    if (!c) return ESC_E_INVAL;
+    for (int32_t g = 0; g < c->gi.G; ++g) params_from(c->params[g], c->gi.groups[g].spec, st ? st + g : nullptr);
+    if (!c->has_device) return ESC_OK;
+    hipSetDevice(c->device);
+    HIP_TRY(hipMemcpyAsync(c->d_params, c->params.data(), c->params.size() * sizeof(GroupParams),
+                           hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ESC_OK;
+}
+
+int32_t esc_use_graph(esc_ctx* c, int32_t enable) {
+    if (!c) return ESC_E_INVAL;
+    c->use_graph = enable != 0;
+    if (!c->use_graph) drop_graphs(c);
+    return ESC_OK;
+}
+
+int32_t esc_force_wide(esc_ctx* c, int32_t enable) {
+    if (!c) return ESC_E_INVAL;
+    c->force_wide = enable != 0;
+    drop_graphs(c);
+    return ESC_OK;
+}
+
+int32_t esc_set_timing(esc_ctx* c, int32_t enable) {
+    if (!c) return ESC_E_INVAL;
+    c->timing = enable != 0;
+    drop_graphs(c);
+    return ESC_OK;
+}
+
+int32_t esc_stage_times(esc_ctx* c, double* ms, int32_t n) {
+    if (!c || !ms || n <= 0) return ESC_E_INVAL;
+    for (int i = 0; i < n && i < MAX_STAGES; ++i) ms[i] = c->stage_ms[i];
+    return ESC_OK;
+}
+
+int32_t esc_reduce(esc_ctx* c) {
+    int32_t rc = check_ready(c);
+    if (rc) return rc;
+    hipSetDevice(c->device);
+    rc = enqueue_step(c, c->cur, false, false);
+    c->cur = (c->cur + 1) % c->n_replicas;
+    c->pending = true;
+    return rc;
+}
+
+int32_t esc_exchange_buffers(esc_ctx* c, void** sum_buf, int64_t* sum_count, void** min_buf, int64_t* min_count) {
+    int32_t rc = check_ready(c);
+    if (rc) return rc;
+    if (sum_buf) *sum_buf = c->d_words;
+    if (sum_count) *sum_count = (int64_t)c->gi.G * TW_K;
+    if (min_buf) *min_buf = c->d_first;
+    if (min_count) *min_count = c->gi.G;
+    return ESC_OK;
+}
+
+int32_t esc_bind_exchange_buffers(esc_ctx* c, void* sum_buf, void* min_buf) {
+    if (!c || (!sum_buf) != (!min_buf)) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    c->bound_words = reinterpret_cast<int64_t*>(sum_buf);
+    c->bound_first = reinterpret_cast<int64_t*>(min_buf);
+    if (c->work_ready) {
+        c->d_words = c->bound_words ? c->bound_words : c->own_words;
+        c->d_first = c->bound_first ? c->bound_first : c->own_first;
+    }
+    drop_graphs(c);
+    return ESC_OK;
+}
+
+int32_t esc_exchange_download(esc_ctx* c, int64_t* sum_out, int64_t* min_out) {
+    int32_t rc = check_ready(c);
+    if (rc) return rc;
+    if (!sum_out || !min_out) return ESC_E_INVAL;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(sum_out, c->d_words, (size_t)c->gi.G * TW_K * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(min_out, c->d_first, (size_t)c->gi.G * 8, hipMemcpyDeviceToHost));
+    return ESC_OK;
+}
+
+int32_t esc_exchange_upload(esc_ctx* c, const int64_t* sum_in, const int64_t* min_in) {
+    int32_t rc = check_ready(c);
+    if (rc) return rc;
+    if (!sum_in || !min_in) return ESC_E_INVAL;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(c->d_words, sum_in, (size_t)c->gi.G * TW_K * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_first, min_in, (size_t)c->gi.G * 8, hipMemcpyHostToDevice));
+    return ESC_OK;
+}
+
+int32_t esc_decide(esc_ctx* c) {
+    int32_t rc = check_ready(c);
+    if (rc) return rc;
+    hipSetDevice(c->device);
+    HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_words, c->d_first, c->d_dec, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)c->gi.G * sizeof(esc_group_decision),
+                           hipMemcpyDeviceToHost, c->stream));
+    c->pending = true;
+    return ESC_OK;
+}
+
+int32_t esc_run(esc_ctx* c) {
+    int32_t rc = check_ready(c);
+    if (rc) return rc;
+    if (c->world != 1) return ESC_E_STATE;            // multi-rank: reduce, exchange, decide
+    hipSetDevice(c->device);
+    const int r = c->cur;
+    c->cur = (c->cur + 1) % c->n_replicas;
+    c->pending = true;
+    if (!c->use_graph || c->timing) return enqueue_step(c, r, true, true);
+    if ((int)c->graphs.size() != c->n_replicas) { drop_graphs(c); c->graphs.assign(c->n_replicas, nullptr); }
+    if (!c->graphs[r]) {
+        hipGraph_t graph = nullptr;
+        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        rc = enqueue_step(c, r, true, true);
+        hipError_t e = hipStreamEndCapture(c->stream, &graph);
+        if (rc) { if (graph) hipGraphDestroy(graph); return rc; }
+        if (e != hipSuccess) return fail_hip(e, "hipStreamEndCapture");
+        e = hipGraphInstantiate(&c->graphs[r], graph, nullptr, nullptr, 0);
+        hipGraphDestroy(graph);
+        if (e != hipSuccess) return fail_hip(e, "hipGraphInstantiate");
+    }
+    HIP_TRY(hipGraphLaunch(c->graphs[r], c->stream));
+    return ESC_OK;
+}
+
+int32_t esc_sync(esc_ctx* c) {
+    if (!c) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->timing && c->pending && c->n_stage_ev > 1) {
+        float ms = 0;
+        for (int i = 0; i + 1 < c->n_stage_ev; ++i) {
+            HIP_TRY(hipEventElapsedTime(&ms, c->ev[i], c->ev[i + 1]));
+            c->stage_ms[i] = ms;
+        }
+        HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[c->n_stage_ev - 1]));
+        c->stage_ms[MAX_STAGES - 1] = ms;
+    }
+    c->pending = false;
+    return ESC_OK;
+}
+
+int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* decisions) {
+    if (!c) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->work_ready) return ESC_E_STATE;
+    int32_t rc = esc_sync(c);
+    if (rc) return rc;
+    const int32_t G = c->gi.G;
+    if (decisions) std::memcpy(decisions, c->h_dec, (size_t)G * sizeof(esc_group_decision));
+    if (totals) {
+        std::vector<int64_t> w((size_t)G * TW_K), f((size_t)G);
+        HIP_TRY(hipMemcpy(w.data(), c->d_words, w.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(f.data(), c->d_first, f.size() * 8, hipMemcpyDeviceToHost));
+        std::vector<int64_t> ncpu, nmem;
+        for (int32_t g = 0; g < G; ++g) {
+            const int64_t* x = &w[(size_t)g * TW_K];
+            esc_group_totals& t = totals[g];
+            auto join = [&](int k, int64_t& out) {
+                const __int128 v = ((__int128)x[k + 1] << 32) + (__int128)x[k];
+                out = (int64_t)v;
+                return v >= (__int128)INT64_MIN && v <= (__int128)INT64_MAX;
+            };
+            t.flags = 0;
+            if (!join(TW_POD_CPU_LO, t.pod_cpu_m)) t.flags |= ESC_TF_POD_OVERFLOW;
+            if (!join(TW_POD_MEM_LO, t.pod_mem_b)) t.flags |= ESC_TF_POD_OVERFLOW;
+            t.n_pods = x[TW_N_PODS];
+            if (!join(TW_NODE_CPU_LO, t.node_cpu_m)) t.flags |= ESC_TF_NODE_OVERFLOW;
+            if (!join(TW_NODE_MEM_LO, t.node_mem_b)) t.flags |= ESC_TF_NODE_OVERFLOW;
+            t.n_untainted = x[TW_N_UNT];
+            t.n_tainted = x[TW_N_TAINT];
+            t.n_cordoned = x[TW_N_CORD];
+            t.n_nodes = t.n_untainted + t.n_tainted + t.n_cordoned;
+            t.first_node = f[g] == INT64_MAX ? -1 : f[g];
+            t.first_cpu_m = 0;
+            t.first_mem_b = 0;
+            if (t.first_node >= 0) {
+                HIP_TRY(hipMemcpy(&t.first_cpu_m, c->nodes.cpu + t.first_node, 8, hipMemcpyDeviceToHost));
+                HIP_TRY(hipMemcpy(&t.first_mem_b, c->nodes.mem + t.first_node, 8, hipMemcpyDeviceToHost));
+            }
+        }
+    }
+    return ESC_OK;
+}
+
+// ----------------------------------------------------------------- ordering
+int32_t esc_sort_nodes(esc_ctx* c) {
+    if (!c) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->nodes_loaded) return ESC_E_STATE;
+    hipSetDevice(c->device);
+    const GroupDev g = group_dev(c);
+    const NodeDev n = node_dev(c);
+    hipStream_t st = c->stream;
+    const int64_t n_local = c->node_hi - c->node_lo;
+    // creation offsets: divide by the largest of 1e9/1e6/1e3 that divides them all
+    // (metav1.Time is whole seconds on the wire), an exact order-preserving transform
+    uint64_t div = 1;
+    if (n_local > 0) {
+        std::vector<int64_t> ts(n_local);
+        HIP_TRY(hipMemcpy(ts.data(), c->nodes.created + c->node_lo, n_local * 8, hipMemcpyDeviceToHost));
+        for (uint64_t d : {1000000000ull, 1000000ull, 1000ull}) {
+            bool ok = true;
+            for (int64_t i = 0; i < n_local && ok; ++i) ok = ((uint64_t)(ts[i] - c->ts_min)) % d == 0;
+            if (ok) { div = d; break; }
+        }
+    }
+    const int R = std::max(1, bit_width((uint64_t)(c->ts_max - c->ts_min) / div));
+    const int gbits = std::max(1, bit_width((uint64_t)(g.G - 1)));
+    if (R + 2 + gbits > 64) return ESC_E_LIMIT;
+    const int total_bits = R + 2 + gbits;
+    const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(2 * c->cu_count, (n_local + 4095) / 4096));
+    if (!c->d_hist) {
+        HIP_TRY(dalloc(&c->d_hist, (size_t)512 * 256 + 1));
+        HIP_TRY(dalloc(&c->d_total, 1));
+        HIP_TRY(dalloc(&c->d_seg, (size_t)4 * g.G + 1));
+    }
+    HIP_TRY(launch_sort_count(n, g, nblk, c->d_hist, st));
+    HIP_TRY(launch_scan_small(c->d_hist, nblk, c->d_total, st));
+    uint32_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, c->d_total, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if ((int64_t)total > c->sort_cap) {
+        for (int i = 0; i < 2; ++i) { dfree(c->d_keys[i]); dfree(c->d_vals[i]); }
+        for (int i = 0; i < 2; ++i) { HIP_TRY(dalloc(&c->d_keys[i], total)); HIP_TRY(dalloc(&c->d_vals[i], total)); }
+        c->sort_cap = total;
+    }
+    HIP_TRY(launch_sort_expand2(n, g, nblk, c->d_hist, c->ts_min, div, R, c->d_keys[0], c->d_vals[0], st));
+    const int sblk = (int)std::max<int64_t>(1, std::min<int64_t>(512, ((int64_t)total + 8191) / 8192));
+    int src = 0;
+    for (int shift = 0; shift < total_bits; shift += 8) {
+        HIP_TRY(launch_radix_pass(c->d_keys[src], c->d_vals[src], c->d_keys[src ^ 1], c->d_vals[src ^ 1], total, shift,
+                                  sblk, c->d_hist, st));
+        src ^= 1;
+    }
+    HIP_TRY(launch_group_bounds(c->d_keys[src], total, R, 4 * g.G, c->d_seg, st));
+    c->sort_n = total;
+    c->sort_src = src;
+    c->sort_R = R;
+    c->sorted = true;
+    return ESC_OK;
+}
+
+int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_out, int64_t cap, int64_t* n_out) {
+    if (!c || group < 0 || group >= c->gi.G || (which != 0 && which != 1) || cap < 0 || (cap > 0 && !idx_out))
+        return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->sorted) return ESC_E_STATE;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    int64_t seg[2];
+    HIP_TRY(hipMemcpy(seg, c->d_seg + 4 * (int64_t)group + which, 16, hipMemcpyDeviceToHost));
+    const int64_t cnt = seg[1] - seg[0];
+    if (n_out) *n_out = cnt;
+    const int64_t m = std::min(cnt, cap);
+    if (m > 0) {
+        std::vector<uint32_t> v(m);
+        HIP_TRY(hipMemcpy(v.data(), c->d_vals[c->sort_src] + seg[0], m * 4, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < m; ++i) idx_out[i] = v[i];
+    }
+    return ESC_OK;
+}
+
+// ---------------------------------------------------------------- drop-ins
+namespace {
+
+int32_t list_context(esc_ctx* c, esc_ctx** out) {
+    if (!c->list_ctx) {
+        esc_group_spec s;
+        std::memset(&s, 0, sizeof s);
+        s.name = "\x01list";
+        s.label_key = "\x01list";
+        s.label_value = "\x01list";
+        int32_t rc = esc_ctx_create(&s, 1, c->device, 0, 1, &c->list_ctx);
+        if (rc) return rc;
+    }
+    *out = c->list_ctx;
+    return ESC_OK;
+}
+
+int32_t run_list(esc_ctx* L, const esc_pod_obj* pods, int64_t np, const esc_node_obj* nodes, int64_t nn,
+                 esc_group_totals* t) {
+    esc_packer* pk = nullptr;
+    int32_t rc = esc_packer_create(L, &pk);
+    if (rc) return rc;
+    esc_packer_set_list_mode(pk, 1);
+    rc = esc_packer_add_pods(pk, pods, np);
+    if (!rc) rc = esc_packer_add_nodes(pk, nodes, nn);
+    esc_pod_soa ps;
+    esc_node_soa ns;
+    if (!rc) rc = esc_packer_view(pk, &ps, &ns);
+    if (!rc) rc = esc_load_pods(L, &ps, 0);
+    if (!rc) rc = esc_load_nodes(L, &ns, 0, ns.n_nodes);
+    esc_packer_destroy(pk);
+    if (!rc) rc = esc_run(L);
+    if (!rc) rc = esc_results(L, t, nullptr);
+    return rc;
+}
+
+}  // namespace
+
+int32_t esc_pods_requests_total(esc_ctx* c, const esc_pod_obj* pods, int64_t n, int64_t* mem_b, int64_t* cpu_m) {
+    if (!c || n < 0 || (n > 0 && !pods) || !mem_b || !cpu_m) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    esc_ctx* L = nullptr;
+    int32_t rc = list_context(c, &L);
+    if (rc) return rc;
+    esc_group_totals t;
+    rc = run_list(L, pods, n, nullptr, 0, &t);
+    if (rc) return rc;
+    if (t.flags & ESC_TF_POD_OVERFLOW) return ESC_E_LIMIT;
+    *mem_b = t.pod_mem_b;
+    *cpu_m = t.pod_cpu_m;
+    return ESC_OK;
+}
+
+int32_t esc_nodes_capacity_total(esc_ctx* c, const esc_node_obj* nodes, int64_t n, int64_t* mem_b, int64_t* cpu_m) {
+    if (!c || n < 0 || (n > 0 && !nodes) || !mem_b || !cpu_m) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    esc_ctx* L = nullptr;
+    int32_t rc = list_context(c, &L);
+    if (rc) return rc;
+    esc_group_totals t;
+    rc = run_list(L, nullptr, 0, nodes, n, &t);
+    if (rc) return rc;
+    if (t.flags & ESC_TF_NODE_OVERFLOW) return ESC_E_LIMIT;
+    *mem_b = t.node_mem_b;
+    *cpu_m = t.node_cpu_m;
+    return ESC_OK;
+}
+
+int32_t esc_order_by_creation(esc_ctx* c, const int64_t* created_ns, int64_t n, int32_t oldest, int64_t n_take,
+                              int64_t* idx_out) {
+    if (!c || n < 0 || (n > 0 && !created_ns) || (n_take > 0 && !idx_out)) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    esc_ctx* L = nullptr;
+    int32_t rc = list_context(c, &L);
+    if (rc) return rc;
+    // all nodes in group 0; class 0 sorts oldest-first, class 1 (tainted) newest-first
+    HostSnapshot s;
+    s.nflags.assign(n, oldest ? 0u : ESC_NF_TAINTED);
+    s.label0.assign(n, 0u);
+    s.ncpu.assign(n, 0);
+    s.nmem.assign(n, 0);
+    s.created.assign(created_ns, created_ns + n);
+    esc_pod_soa ps;
+    esc_node_soa ns;
+    s.view(&ps, &ns);
+    rc = esc_load_pods(L, &ps, 0);
+    if (!rc) rc = esc_load_nodes(L, &ns, 0, n);
+    if (!rc) rc = esc_sort_nodes(L);
+    int64_t cnt = 0;
+    if (!rc) rc = esc_group_order(L, 0, oldest ? 0 : 1, idx_out, std::max<int64_t>(0, std::min(n_take, n)), &cnt);
+    return rc;
+}
+
+// ------------------------------------------------------- scalar decision math
+int32_t esc_calc_percent_usage(int64_t cpu_req_m, int64_t mem_req_b, int64_t cpu_cap_m, int64_t mem_cap_b,
+                               int64_t n_untainted, double* cpu_pct, double* mem_pct) {
+    if (!cpu_pct || !mem_pct) return ESC_E_INVAL;
+    return percent_usage(cpu_req_m, mem_req_b, cpu_cap_m, mem_cap_b, n_untainted, cpu_pct, mem_pct);
+}
+
+int32_t esc_calc_scale_up_delta(int64_t n_untainted, double cpu_pct, double mem_pct, int64_t cpu_req_m,
+                                int64_t mem_req_b, int64_t cached_cpu_m, int64_t cached_mem_b, int32_t scale_up_pct,
+                                int64_t* delta) {
+    if (!delta) return ESC_E_INVAL;
+    return scale_up_delta(n_untainted, cpu_pct, mem_pct, cpu_req_m, mem_req_b, cached_cpu_m, cached_mem_b,
+                          scale_up_pct, delta);
+}
+
+}  // extern "C"

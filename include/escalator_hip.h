@@ -301,6 +301,13 @@ int32_t esc_set_state(esc_ctx* ctx, const esc_group_state* state);   /* NULL = z
 int32_t esc_reduce(esc_ctx* ctx);
 int32_t esc_exchange_buffers(esc_ctx* ctx, void** sum_buf, int64_t* sum_count,
                              void** min_buf, int64_t* min_count);
+/* Use caller-allocated device buffers (e.g. torch tensors handed to RCCL) as the
+ * exchange buffers; sizes as reported by esc_exchange_buffers.  NULL restores the
+ * context's own buffers. */
+int32_t esc_bind_exchange_buffers(esc_ctx* ctx, void* sum_buf, void* min_buf);
+/* Host-staged exchange for hosts without a device collective (synchronous). */
+int32_t esc_exchange_download(esc_ctx* ctx, int64_t* sum_out, int64_t* min_out);
+int32_t esc_exchange_upload(esc_ctx* ctx, const int64_t* sum_in, const int64_t* min_in);
 int32_t esc_decide(esc_ctx* ctx);
 int32_t esc_run(esc_ctx* ctx);
 int32_t esc_sync(esc_ctx* ctx);
@@ -366,6 +373,7 @@ typedef struct esc_synth_params {
 int32_t esc_synth_create(const esc_synth_params* p, int64_t p_lo, int64_t p_hi, esc_synth** out);
 int32_t esc_synth_destroy(esc_synth* s);
 int32_t esc_synth_groups(const esc_synth* s, const esc_group_spec** groups, int32_t* n);
+int32_t esc_synth_states(const esc_synth* s, const esc_group_state** states);
 int32_t esc_synth_view(const esc_synth* s, esc_pod_soa* pods, esc_node_soa* nodes);
 
 #ifdef __cplusplus

@@ -1,0 +1,154 @@
+"""ctypes front-end of the C oracle (oracle/esc_oracle.c) over packed snapshots.
+
+TEST INFRASTRUCTURE ONLY (tests/, __graft_entry__.smoke(), bench.py cpu_baseline).
+
+``group_tables`` restates the group/label matching of the reference independently of
+the product's interner: a pod matches a labelled group iff one of its (key, value)
+pairs equals the group's (label_key, label_value) (NewPodAffinityFilterFunc,
+pkg/controller/node_group.go:218-253); the group named "default" takes pods through
+NewPodDefaultFilterFunc instead (node_group.go:256, controller/client.go:58-64); nodes
+match any group by label (NewNodeLabelFilterFunc node_group.go:278, :301).  Groups that
+share one (key, value) pair form a chain head -> next (lowest index first).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+NONE = 0xFFFFFFFF
+BRANCH_NAMES = ["empty", "gate", "below_min", "pct_err", "locked", "fast_down", "slow_down", "scale_up", "none"]
+STATUS_ERR = {0: None, 1: "node count less than the minimum", 2: "node count larger than the maximum",
+              3: "cannot divide by zero in percent calculation", 4: "negative scale up delta",
+              5: "int64 overflow (Quantity inf.Dec regime, not emulated)"}
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = C.CDLL(LIB)
+        _lib.orc_totals.restype = C.c_int
+        _lib.orc_ref_scan.restype = C.c_int
+        _lib.orc_order.restype = C.c_int64
+        _lib.orc_percent.restype = C.c_int
+        _lib.orc_scale_up.restype = C.c_int
+        _lib.orc_percent.argtypes = [C.c_int64] * 5 + [C.POINTER(C.c_double)] * 2
+        _lib.orc_scale_up.argtypes = [C.c_int64, C.c_double, C.c_double, C.c_int64, C.c_int64, C.c_int64,
+                                      C.c_int64, C.c_int32, C.POINTER(C.c_int64)]
+    return _lib
+
+
+def group_tables(groups: list[dict]) -> dict:
+    G = len(groups)
+    default = next((i for i, g in enumerate(groups) if g["name"] == "default"), -1)
+    pod_next = np.full(G, NONE, np.uint32)
+    node_next = np.full(G, NONE, np.uint32)
+    pod_head, node_head, pod_tail, node_tail = {}, {}, {}, {}
+    for g, spec in enumerate(groups):
+        k = (spec.get("label_key", ""), spec.get("label_value", ""))
+        if k in node_tail:
+            node_next[node_tail[k]] = g
+        else:
+            node_head[k] = g
+        node_tail[k] = g
+        if g == default:
+            continue
+        if k in pod_tail:
+            pod_next[pod_tail[k]] = g
+        else:
+            pod_head[k] = g
+        pod_tail[k] = g
+    dry = np.array([1 if s.get("dry_mode") else 0 for s in groups], np.uint8)
+    return {"G": G, "default": default, "pod_next": pod_next, "node_next": node_next, "pod_head": pod_head,
+            "node_head": node_head, "dry": dry}
+
+
+def _p(a, t):
+    return np.ascontiguousarray(a).ctypes.data_as(C.POINTER(t))
+
+
+def _node_args(nodes):
+    return [C.c_int64(len(nodes["flags"])), _p(nodes["flags"], C.c_uint32), _p(nodes["label0"], C.c_uint32),
+            _p(nodes["cpu"], C.c_int64), _p(nodes["mem"], C.c_int64)]
+
+
+TOT_FIELDS = ["pod_cpu_m", "pod_mem_b", "n_pods", "node_cpu_m", "node_mem_b", "n_nodes", "n_untainted",
+              "n_tainted", "n_cordoned", "first_node", "first_cpu_m", "first_mem_b", "flags"]
+
+
+def totals(pods: dict, nodes: dict, groups: list[dict], node_lo: int = 0, node_hi: int | None = None,
+           reference_shaped: bool = False, g_range: tuple[int, int] | None = None) -> np.ndarray:
+    """int64 [G, 13] in esc_group_totals order."""
+    t = group_tables(groups)
+    G = t["G"]
+    out = np.zeros((G, 13), np.int64)
+    hi = len(nodes["flags"]) if node_hi is None else node_hi
+    keep = [pods, nodes, t]
+    pa = [C.c_int64(len(pods["flags"])), _p(pods["flags"], C.c_uint32), _p(pods["cpu0"], C.c_uint32),
+          _p(pods["mem0"], C.c_int64), _p(pods["pair0"], C.c_uint32), _p(pods["xc_cpu"], C.c_int64),
+          _p(pods["xc_mem"], C.c_int64), _p(pods["xp_group"], C.c_uint32)]
+    na = _node_args(nodes) + [_p(nodes["xl_group"], C.c_uint32), _p(nodes["trk_node"], C.c_int32),
+                              _p(nodes["trk_group"], C.c_int32), C.c_int64(len(nodes["trk_node"]))]
+    if reference_shaped:
+        lo, hi_g = g_range or (0, G)
+        rc = lib().orc_ref_scan(*pa, *na, C.c_int32(G), C.c_int32(t["default"]), _p(t["pod_next"], C.c_uint32),
+                                _p(t["node_next"], C.c_uint32), _p(t["dry"], C.c_uint8), C.c_int32(lo),
+                                C.c_int32(hi_g), _p(out, C.c_int64))
+    else:
+        rc = lib().orc_totals(*pa, *na, C.c_int64(node_lo), C.c_int64(hi), C.c_int32(G), C.c_int32(t["default"]),
+                              _p(t["pod_next"], C.c_uint32), _p(t["node_next"], C.c_uint32),
+                              _p(t["dry"], C.c_uint8), _p(out, C.c_int64))
+    del keep
+    assert rc == 0
+    return out
+
+
+def params(groups: list[dict], states: list[dict] | None) -> np.ndarray:
+    out = np.zeros((len(groups), 12), np.int64)
+    for g, s in enumerate(groups):
+        st = (states[g] if states else None) or {}
+        out[g] = [s.get("min_nodes", 0), s.get("max_nodes", 0), s.get("taint_upper_pct", 0),
+                  s.get("taint_lower_pct", 0), s.get("scale_up_pct", 0), s.get("slow_removal_rate", 0),
+                  s.get("fast_removal_rate", 0), int(bool(s.get("dry_mode"))), int(bool(st.get("locked", 0))),
+                  st.get("requested_nodes", 0), st.get("cached_cpu_m", 0), st.get("cached_mem_b", 0)]
+    return out
+
+
+def decide(groups: list[dict], states: list[dict] | None, tot: np.ndarray):
+    """Returns (float64 [G,2] cpu/mem pct, int64 [G,7] delta,n_to_taint,cached_cpu,cached_mem,status,branch,taint)."""
+    G = len(groups)
+    pr = params(groups, states)
+    df = np.zeros((G, 2), np.float64)
+    di = np.zeros((G, 7), np.int64)
+    tot = np.ascontiguousarray(tot, np.int64)
+    lib().orc_decide(C.c_int32(G), _p(pr, C.c_int64), _p(tot, C.c_int64), _p(df, C.c_double), _p(di, C.c_int64))
+    return df, di
+
+
+def order(nodes: dict, groups: list[dict], group: int, which: int, node_lo: int = 0,
+          node_hi: int | None = None, cap: int | None = None) -> np.ndarray:
+    t = group_tables(groups)
+    n = len(nodes["flags"])
+    hi = n if node_hi is None else node_hi
+    out = np.zeros(max(hi - node_lo, 1), np.int64)
+    m = lib().orc_order(C.c_int64(n), _p(nodes["flags"], C.c_uint32), _p(nodes["label0"], C.c_uint32),
+                        _p(nodes["created_ns"], C.c_int64), _p(nodes["xl_group"], C.c_uint32),
+                        _p(nodes["trk_node"], C.c_int32), _p(nodes["trk_group"], C.c_int32),
+                        C.c_int64(len(nodes["trk_node"])), C.c_int64(node_lo), C.c_int64(hi),
+                        _p(t["node_next"], C.c_uint32), _p(t["dry"], C.c_uint8), C.c_int32(group),
+                        C.c_int32(which), _p(out, C.c_int64), C.c_int64(len(out)))
+    m = int(m)
+    out = out[:m]
+    return out if cap is None else out[:cap]

@@ -1,0 +1,262 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracles.
+
+Bit-exact everywhere: int64 sums and counts, float64 percentages compared as bits,
+deltas, statuses and node orderings."""
+import random
+import struct
+
+import numpy as np
+import pytest
+
+from builders import build_test_node, build_test_nodes, build_test_pod, build_test_pods, unix_ns
+from oracle import oracle as O
+from oracle import soa
+from randobj import make_groups, make_nodes, make_pods, make_states, make_trackers
+
+pytestmark = pytest.mark.gpu
+soa.build()
+
+
+def _bits(x):
+    return struct.pack("<d", float(x))
+
+
+@pytest.fixture(scope="module")
+def esc():
+    import escalator_amd
+    return escalator_amd
+
+
+def check_against_c_oracle(tot, dec, otot, odf, odi):
+    names = list(tot.dtype.names)
+    for k, name in enumerate(soa.TOT_FIELDS):
+        if name == "flags":
+            assert np.array_equal(tot[name] != 0, otot[:, k] != 0), name
+            continue
+        assert np.array_equal(tot[name], otot[:, k]), (name, np.nonzero(tot[name] != otot[:, k])[0][:10])
+    assert names
+    assert np.array_equal(dec["cpu_pct"].view(np.uint64), odf[:, 0].view(np.uint64))
+    assert np.array_equal(dec["mem_pct"].view(np.uint64), odf[:, 1].view(np.uint64))
+    for k, name in enumerate(["delta", "n_to_taint", "cached_cpu_m", "cached_mem_b", "status", "branch",
+                              "taint_status"]):
+        assert np.array_equal(dec[name].astype(np.int64), odi[:, k]), (name, np.nonzero(dec[name] != odi[:, k])[0][:10])
+
+
+# ------------------------------------------------------------------ fixtures
+def test_fixture_pods_requests_total(esc, golden):
+    from escalator_amd import k8s
+    fx = golden["k8s_util"]
+    for c in fx["calculate_pods_requests_total"]:
+        pods = [build_test_pod(fx["pods"][n]) for n in c["pods"]]
+        assert k8s.calculate_pods_requests_total(pods) == (c["mem"], c["cpu"]), c["name"]
+
+
+def test_fixture_nodes_capacity_total(esc, golden):
+    from escalator_amd import k8s
+    fx = golden["k8s_util"]
+    for c in fx["calculate_nodes_capacity_total"]:
+        nodes = [build_test_node(fx["nodes"][n]) for n in c["nodes"]]
+        assert k8s.calculate_nodes_capacity_total(nodes) == (c["mem"], c["cpu"]), c["name"]
+
+
+def test_fixture_orderings(esc, golden):
+    from escalator_amd import controller
+    fx = golden["controller"]
+    dates = [unix_ns(*d) for d in fx["six_nodes"]["dates"]]
+    for c in fx["taint_oldest_n"]:
+        assert controller.taint_oldest_n(dates[:c["slice"]], c["n"]) == c["want"], c["name"]
+    for c in fx["untaint_newest_n"]:
+        assert controller.untaint_newest_n(dates[:c["slice"]], c["n"]) == c["want"], c["name"]
+    old = [unix_ns(*d) for d in fx["sort_dates"]["oldest_ordered"]]
+    rng = random.Random(3)
+    for _ in range(10):
+        perm = list(range(6))
+        rng.shuffle(perm)
+        got = controller.taint_oldest_n([old[i] for i in perm], 6)
+        assert [perm[i] for i in got] == list(range(6))
+
+
+def _default_group(opts):
+    g = {"name": "default", "label_key": "", "label_value": ""}
+    g.update(opts)
+    g.setdefault("max_nodes", 0)
+    return g
+
+
+def test_fixture_scale_node_group(esc, golden):
+    from escalator_amd.controller import Controller
+    for c in golden["controller"]["scale_node_group"]["cases"]:
+        n_n, n_cpu, n_mem = c["nodes"]
+        n_p, p_cpu, p_mem = c["pods"]
+        nodes = build_test_nodes(n_n, {"CPU": n_cpu, "Mem": n_mem})
+        pods = build_test_pods(n_p, {"CPU": [p_cpu], "Mem": [p_mem]})
+        ctl = Controller([_default_group(c["opts"])])
+
+        def lp():
+            if c.get("lister_error") == "pods":
+                raise RuntimeError("unable to list pods")
+            return pods
+
+        def ln():
+            if c.get("lister_error") == "nodes":
+                raise RuntimeError("unable to list nodes")
+            return nodes
+
+        delta, err = ctl.scale_node_group("default", lp, ln)
+        assert (delta, err) == (c["delta"], c["err"]), c["name"]
+        if delta > 0:                       # re-run after the cloud brought the nodes up -> 0
+            more = nodes + build_test_nodes(delta, {"CPU": n_cpu, "Mem": n_mem}, "m")
+            assert ctl.scale_node_group("default", lambda: pods, lambda: more)[0] == 0, c["name"]
+
+
+def test_fixture_multiple_runs_first_delta(esc, golden):
+    from escalator_amd.controller import Controller
+    for c in golden["controller"]["scale_node_group_multiple_runs"]["cases"]:
+        n_n, n_cpu, n_mem = c["nodes"]
+        n_p, p_cpu, p_mem = c["pods"]
+        nodes = build_test_nodes(n_n, {"CPU": n_cpu, "Mem": n_mem})
+        pods = build_test_pods(n_p, {"CPU": [p_cpu], "Mem": [p_mem]})
+        ctl = Controller([_default_group(c["opts"])])
+        if c["cached"]:
+            ctl.state[0]["cached_cpu_m"], ctl.state[0]["cached_mem_b"] = c["cached"]
+        assert ctl.scale_node_group("default", lambda: pods, lambda: nodes) == (c["delta"], None), c["name"]
+
+
+def test_fixture_filter_nodes_dry_and_wet(esc, golden):
+    fx = golden["controller"]["filter_nodes"]
+    nodes = [build_test_node(o) for o in fx["nodes"]]
+    for c in fx["cases"]:
+        g = {"name": "g", "label_key": "", "label_value": "", "max_nodes": 100, "dry_mode": c["dry"]}
+        ctx = esc.Context([g])
+        P, N = ctx.pack([], nodes, {0: c["tracker"]} if c["tracker"] else None)
+        ctx.load(P, N)
+        tot, _ = ctx.decide_all()
+        assert (tot["n_untainted"][0], tot["n_tainted"][0], tot["n_cordoned"][0]) == \
+            (len(c["untainted"]), len(c["tainted"]), len(c["cordoned"]))
+        ctx.sort_nodes()
+        assert list(ctx.group_order(0, 0)) == c["untainted"]
+        assert sorted(ctx.group_order(0, 1)) == c["tainted"]
+
+
+# ------------------------------------------------------ random object clusters
+@pytest.mark.parametrize("seed", range(10))
+def test_random_objects_vs_literal(esc, seed):
+    rng = random.Random(2000 + seed)
+    G = rng.choice([1, 3, 8, 20])
+    groups = make_groups(rng, G, with_default=rng.random() < 0.6)
+    pods = make_pods(rng, rng.choice([0, 60, 500]) if seed else 0, groups, big_frac=0.03)
+    nodes = make_nodes(rng, rng.choice([10, 40, 150]) if seed else 0, groups, big_frac=0.03)
+    trackers = make_trackers(rng, groups, nodes)
+    states = make_states(rng, G)
+    ctx = esc.Context(groups)
+    P, N = ctx.pack(pods, nodes, trackers)
+    ctx.load(P, N)
+    for wide in (False, True):
+        ctx.force_wide(wide)
+        tot, dec = ctx.decide_all(states)
+        for g in range(G):
+            L = O.scale_node_group(groups[g], states[g], pods, nodes, tracker=trackers.get(g, []))
+            t, d = tot[g], dec[g]
+            assert (t["n_pods"], t["n_nodes"], t["n_untainted"], t["n_tainted"], t["n_cordoned"], t["first_node"]) == \
+                (L["n_pods"], L["n_nodes"], L["n_untainted"], L["n_tainted"], L["n_cordoned"], L["first_node"]), g
+            if L["pod_cpu_m"] is not None:
+                assert (t["pod_cpu_m"], t["pod_mem_b"], t["node_cpu_m"], t["node_mem_b"]) == \
+                    (L["pod_cpu_m"], L["pod_mem_b"], L["node_cpu_m"], L["node_mem_b"]), g
+            assert esc._lib.BRANCHES[d["branch"]] == L["branch"], (g, L)
+            assert int(d["delta"]) == L["delta"] and int(d["n_to_taint"]) == L["n_to_taint"], (g, L)
+            assert _bits(d["cpu_pct"]) == _bits(L["cpu_pct"]) and _bits(d["mem_pct"]) == _bits(L["mem_pct"])
+            assert (int(d["cached_cpu_m"]), int(d["cached_mem_b"])) == (L["cached_cpu_m"], L["cached_mem_b"])
+    ctx.force_wide(False)
+    ctx.sort_nodes()
+    for g in range(G):
+        L = O.scale_node_group(groups[g], states[g], pods, nodes, tracker=trackers.get(g, []))
+        unt = L["untainted"]
+        assert list(ctx.group_order(g, 0)) == [unt[i] for i in O.oldest_first([nodes[i]["created_ns"] for i in unt])]
+        tn = L["tainted"]
+        assert list(ctx.group_order(g, 1)) == [tn[i] for i in O.newest_first([nodes[i]["created_ns"] for i in tn])]
+
+
+def test_overflow_flagged(esc):
+    groups = [{"name": "a", "label_key": "k", "label_value": "v", "max_nodes": 10}]
+    pods = [{"containers": [{"cpu": 1, "mem": (1 << 62) + 5}], "node_selector": {"k": "v"}} for _ in range(3)]
+    nodes = [{"name": "n", "labels": {"k": "v"}, "cpu": 1000, "mem": 1000, "created_ns": 1}]
+    ctx = esc.Context(groups)
+    ctx.load(*ctx.pack(pods, nodes))
+    tot, dec = ctx.decide_all()
+    assert tot["flags"][0] & 1 and dec["status"][0] == esc._lib.ESC_ST_ERR_OVERFLOW
+
+
+# ---------------------------------------------------------- synthetic configs
+@pytest.mark.parametrize("cfg,P,N,G", [(1, 1000, 50, 1), (2, 1_000_000, 10_000, 100), (3, 2_000_000, 20_000, 100),
+                                       (4, 2_000_000, 20_000, 10_000), (5, 200_000, 300_000, 100)])
+def test_synthetic_vs_c_oracle(esc, cfg, P, N, G):
+    s = esc.Synth(P, N, G, config=cfg, seed=0xE5CA1A7E00000000 + cfg)
+    pods, nodes = s.pods(), s.nodes()
+    otot = soa.totals(pods, nodes, s.groups)
+    odf, odi = soa.decide(s.groups, s.states, otot)
+    ctx = esc.Context(s)
+    ctx.load_synth(s, replicas=2)
+    ctx.use_graph(True)
+    ctx.set_state(s.states)
+    for _ in range(3):                        # graph replays over both replicas
+        ctx.run()
+        tot, dec = ctx.results()
+        check_against_c_oracle(tot, dec, otot, odf, odi)
+    assert len(set(dec["branch"].tolist())) >= (1 if G == 1 else 4)
+    ctx.force_wide(True)
+    ctx.run()
+    tot, dec = ctx.results()
+    check_against_c_oracle(tot, dec, otot, odf, odi)
+
+
+def test_synthetic_sort_vs_c_oracle(esc):
+    s = esc.Synth(10_000, 400_000, 100, config=5, seed=0xE5CA1A7E00000005)
+    nodes = s.nodes()
+    ctx = esc.Context(s)
+    ctx.load_synth(s)
+    ctx.sort_nodes()
+    for g in list(range(0, 100, 7)) + [99]:
+        for which in (0, 1):
+            assert np.array_equal(ctx.group_order(g, which), soa.order(nodes, s.groups, g, which)), (g, which)
+
+
+def test_sharded_two_contexts_host_exchange(esc):
+    """Two ranks' shards on one device, exchanged through the host: == whole snapshot."""
+    from escalator_amd.dist import shard_range
+    P, N, G = 300_000, 30_000, 1000
+    full = esc.Synth(P, N, G, config=4, seed=11)
+    otot = soa.totals(full.pods(), full.nodes(), full.groups)
+    odf, odi = soa.decide(full.groups, full.states, otot)
+    ctxs, words, firsts = [], [], []
+    for r in range(3):
+        lo, hi = shard_range(P, r, 3)
+        s = esc.Synth(P, N, G, config=4, seed=11, p_lo=lo, p_hi=hi)
+        nlo, nhi = shard_range(N, r, 3)
+        c = esc.Context(s, rank=r, world=3)
+        c.load_synth(s, pod_offset=lo, node_lo=nlo, node_hi=nhi)
+        c.set_state(full.states)
+        c.reduce()
+        w, f = c.exchange_download()
+        words.append(w)
+        firsts.append(f)
+        ctxs.append((c, s))
+    W = np.sum(words, axis=0)
+    F = np.min(firsts, axis=0)
+    for c, _ in ctxs:
+        c.exchange_upload(W, F)
+        c.decide()
+        tot, dec = c.results()
+        check_against_c_oracle(tot, dec, otot, odf, odi)
+
+
+def test_determinism_repeat(esc):
+    s = esc.Synth(500_000, 5_000, 500, config=4, seed=99)
+    ctx = esc.Context(s)
+    ctx.load_synth(s)
+    ctx.set_state(s.states)
+    ctx.run()
+    t0, d0 = ctx.results()
+    for _ in range(5):
+        ctx.run()
+        t1, d1 = ctx.results()
+        assert t0.tobytes() == t1.tobytes() and d0.tobytes() == d1.tobytes()

@@ -1,0 +1,145 @@
+"""CPU: K0 packer (product, host C++) -> packed SoA -> C oracle, against the literal
+Python oracle on the original objects.  Pins the C oracle (used at full sizes) to the
+fixture-pinned literal oracle, and checks the packer's encoding without a GPU."""
+import random
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from oracle import soa
+from randobj import make_groups, make_nodes, make_pods, make_states, make_trackers
+
+soa.build()
+
+
+def _ctx(groups):
+    from escalator_amd.context import Context
+    return Context(groups, device=-1)
+
+
+def literal_all(groups, states, pods, nodes, trackers):
+    out = []
+    for g, spec in enumerate(groups):
+        out.append(O.scale_node_group(spec, states[g], pods, nodes, tracker=trackers.get(g, [])))
+    return out
+
+
+def _bits(x):
+    return struct.pack("<d", x)
+
+
+def compare(groups, states, pods, nodes, trackers, tot, df, di):
+    lit = literal_all(groups, states, pods, nodes, trackers)
+    for g, L in enumerate(lit):
+        t = tot[g]
+        assert t[2] == L["n_pods"], (g, "n_pods")
+        assert (t[5], t[6], t[7], t[8]) == (L["n_nodes"], L["n_untainted"], L["n_tainted"], L["n_cordoned"]), g
+        assert t[9] == L["first_node"], g
+        if L["pod_cpu_m"] is not None:
+            assert (t[0], t[1], t[3], t[4]) == (L["pod_cpu_m"], L["pod_mem_b"], L["node_cpu_m"], L["node_mem_b"]), g
+            assert t[12] == 0
+        else:
+            assert t[12] != 0
+        assert soa.BRANCH_NAMES[di[g, 5]] == L["branch"], (g, L)
+        assert soa.STATUS_ERR[di[g, 4]] == L["err"], (g, L)
+        assert di[g, 0] == L["delta"], (g, L)
+        assert _bits(df[g, 0]) == _bits(L["cpu_pct"]) and _bits(df[g, 1]) == _bits(L["mem_pct"]), (g, L)
+        assert (di[g, 2], di[g, 3]) == (L["cached_cpu_m"], L["cached_mem_b"]), g
+        assert di[g, 1] == L["n_to_taint"] and (di[g, 6] != 0) == (L["taint_err"] is not None), (g, L)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_packer_c_oracle_vs_literal(seed):
+    rng = random.Random(1000 + seed)
+    G = rng.choice([1, 3, 8, 20])
+    groups = make_groups(rng, G, with_default=rng.random() < 0.6)
+    pods = make_pods(rng, rng.choice([0, 60, 400]) if seed else 0, groups)
+    nodes = make_nodes(rng, rng.choice([10, 40, 120]) if seed else 0, groups)
+    trackers = make_trackers(rng, groups, nodes)
+    states = make_states(rng, G)
+    ctx = _ctx(groups)
+    P, N = ctx.pack(pods, nodes, trackers)
+    tot = soa.totals(P, N, groups)
+    df, di = soa.decide(groups, states, tot)
+    compare(groups, states, pods, nodes, trackers, tot, df, di)
+    # reference-shaped scan gives identical totals
+    assert np.array_equal(soa.totals(P, N, groups, reference_shaped=True), tot)
+    # orderings
+    for g in range(G):
+        L = O.scale_node_group(groups[g], states[g], pods, nodes, tracker=trackers.get(g, []))
+        unt = L["untainted"]
+        want = [unt[i] for i in O.oldest_first([nodes[i]["created_ns"] for i in unt])]
+        assert list(soa.order(N, groups, g, 0)) == want
+        tn = L["tainted"]
+        want = [tn[i] for i in O.newest_first([nodes[i]["created_ns"] for i in tn])]
+        assert list(soa.order(N, groups, g, 1)) == want
+
+
+def test_packer_list_mode_fixtures(golden):
+    from builders import build_test_node, build_test_pod
+    fx = golden["k8s_util"]
+    ctx = _ctx([{"name": "x", "label_key": "k", "label_value": "v"}])
+    for c in fx["calculate_pods_requests_total"]:
+        pods = [build_test_pod(fx["pods"][n]) for n in c["pods"]]
+        P, N = ctx.pack(pods, [], list_mode=True)
+        tot = soa.totals(P, N, [{"name": "x"}])
+        assert (tot[0, 1], tot[0, 0]) == (c["mem"], c["cpu"]), c["name"]
+    for c in fx["calculate_nodes_capacity_total"]:
+        nodes = [build_test_node(fx["nodes"][n]) for n in c["nodes"]]
+        P, N = ctx.pack([], nodes, list_mode=True)
+        tot = soa.totals(P, N, [{"name": "x"}])
+        assert (tot[0, 4], tot[0, 3]) == (c["mem"], c["cpu"]), c["name"]
+
+
+def test_packer_encoding_details():
+    groups = [{"name": "default", "label_key": "customer", "label_value": "default"},
+              {"name": "a", "label_key": "customer", "label_value": "a"},
+              {"name": "b", "label_key": "customer", "label_value": "a"},
+              {"name": "c", "label_key": "pool", "label_value": "p"}]
+    ctx = _ctx(groups)
+    pods = [
+        {"containers": [{"cpu": 5, "mem": 6}], "node_selector": {"customer": "a", "pool": "p"},
+         "affinity": {"node_affinity": {"required": [[{"key": "customer", "op": "In", "values": ["a", "zz"]}]]}}},
+        {"containers": [{"cpu": 1 << 33, "mem": 1}, {"cpu": 2, "mem": 3}], "init_containers": [{"cpu": None, "mem": 9}],
+         "overhead": {"cpu": None, "mem": None}},
+        {"owner_kinds": ["DaemonSet"], "containers": []},
+    ]
+    P, N = ctx.pack(pods, [])
+    # pod 0: pairs {a-head(1), c(3)} deduped across selector+affinity; pod-side head of (customer,a) is 1
+    assert P["pair0"][0] == 1 and list(P["xp_group"]) == [3]
+    assert (P["flags"][0] >> 24) & 63 == 1 and P["flags"][0] & 0b1100 == 0b1100
+    # pod 1: first container cpu does not fit u32 -> all regulars are extras; absent init cpu = INT64_MIN;
+    # an overhead map with no keys adds nothing and is dropped
+    assert P["cpu0"][1] == 0 and (P["flags"][1] >> 8) & 255 == 2 and (P["flags"][1] >> 16) & 255 == 1
+    assert not P["flags"][1] & 16
+    assert list(P["xc_cpu"]) == [1 << 33, 2, -(1 << 63)] and list(P["xc_mem"]) == [1, 3, 9]
+    assert P["pair0"][1] == 0xFFFFFFFF
+    assert P["flags"][2] & 1
+
+
+def test_scalar_math_matches_literal():
+    """The library's host build of the decision math (same code as the K4 kernel)."""
+    import ctypes as C
+    from escalator_amd import _lib as L
+    lib = L.load()
+    rng = random.Random(5)
+    cases = [(50, 50, 100, 100, 1), (50, 50, 0, 0, 10), (0, 0, 0, 0, 1), (0, 0, 66, 66, 1), (0, 0, 0, 0, 0),
+             (50000, 60000, 15000, 50000, 10)]
+    for _ in range(3000):
+        cases.append((rng.randrange(-10, 1 << 62), rng.randrange(0, 1 << 62), rng.choice([0, rng.randrange(1, 1 << 62)]),
+                      rng.choice([0, rng.randrange(1, 1 << 60)]), rng.randrange(0, 3)))
+    a, b = C.c_double(), C.c_double()
+    for c in cases:
+        st = lib.esc_calc_percent_usage(*c, C.byref(a), C.byref(b))
+        cpu, mem, err = O.calc_percent_usage(*c)
+        assert _bits(a.value) == _bits(cpu) and _bits(b.value) == _bits(mem), c
+        assert (st == 3) == (err is not None)
+        d = C.c_int64()
+        for thr in (0, 1, 3, 70, 110):
+            for cached in ((0, 0), (4000, 8 << 30)):
+                st = lib.esc_calc_scale_up_delta(c[4], a.value, b.value, c[0], c[1], cached[0], cached[1], thr,
+                                                 C.byref(d))
+                want, err = O.calc_scale_up_delta(c[4], a.value, b.value, c[0], c[1], cached[0], cached[1], thr)
+                assert d.value == want and (st == 4) == (err is not None), (c, thr, cached)
