@@ -1,0 +1,219 @@
+"""Benchmark: pod+node records evaluated per second per scale decision (BASELINE.json).
+
+One "step" = one complete scale decision over a device-resident synthetic snapshot:
+K1 (pods) + K2 (nodes) + K3 combine (+ RCCL exchange when N > 1) + K4 decide + the copy
+of every group's decision to pinned host memory.  Default workload: BASELINE config #4
+(100M pods / 1M nodes / 10k node groups), sharded over the N GPUs (strong scaling: the
+snapshot is fixed, each GPU streams 1/N of it).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4|2]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # BASELINE.md §3 rows
+    2: dict(P=1_000_000, N=10_000, G=100, name="config2: 1M pods / 10k nodes / 100 node groups (BASELINE.json configs[1])"),
+    3: dict(P=10_000_000, N=100_000, G=100, name="config3: 10M pods / 100k nodes / 100 multi-instance-type groups (configs[2])"),
+    4: dict(P=100_000_000, N=1_000_000, G=10_000,
+            name="config4: 100M pods / 1M nodes / 10k node groups (BASELINE.json configs[3]), sharded over N GPUs"),
+}
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def pod_bytes(p) -> int:
+    """Algorithmic bytes K1 streams per launch: the shard's packed arrays, each read once
+    (flags 4 + cpu0 4 + mem0 8 + pair0 4 per pod, 16 per extra container record, 4 per
+    extra pair, 8 per 256-pod tile of extra offsets)."""
+    n = int(p.n_pods)
+    return n * 20 + int(p.n_xc) * 16 + int(p.n_xp) * 4 + ((n + 255) // 256) * 8
+
+
+def node_bytes(nc, lo, hi) -> int:
+    """K2: flags 4 + label0 4 + cpu 8 + mem 8 (+ offsets of extra labels 4) per node streamed."""
+    return (hi - lo) * 28 + int(nc.n_xl) * 4
+
+
+def cpu_baseline(cfg, G, seconds=12.0):
+    """The oracle's reference-shaped scan (one full pass per group, as the reference's
+    RunOnce does), single thread, on a bounded sample; extrapolated to the full config."""
+    import numpy as np
+    from escalator_amd.context import Synth
+    from oracle import soa
+    P_s, N_s = 2_000_000, 20_000
+    s = Synth(P_s, N_s, G, config=cfg["cfg"], seed=0xE5CA1A7E00000000 + cfg["cfg"], threads=16)
+    pods, nodes = s.pods(), s.nodes()
+    t0 = time.perf_counter()
+    soa.totals(pods, nodes, s.groups, reference_shaped=True, g_range=(1, 2))
+    t1 = time.perf_counter() - t0
+    g_s = int(max(1, min(G - 1, seconds / max(t1, 1e-6))))
+    t0 = time.perf_counter()
+    soa.totals(pods, nodes, s.groups, reference_shaped=True, g_range=(1, 1 + g_s))
+    t_scan = time.perf_counter() - t0
+    per_group = t_scan / g_s
+    t0 = time.perf_counter()
+    soa.totals(pods, nodes, s.groups)
+    t_single = time.perf_counter() - t0
+    np.asarray(0)
+    return {
+        "value": (P_s + N_s) / (per_group * G),
+        "unit": "records/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": ("oracle/esc_oracle.c orc_ref_scan (reference-shaped: every group rescans all pods and nodes, "
+                   "controller.go:416 + pod_listers.go:33) over a %d-pod / %d-node sample of the same config, "
+                   "%d of %d groups timed (%.1f s), extrapolated linearly to all groups" % (P_s, N_s, g_s, G, t_scan)),
+        "single_pass_records_per_s": (P_s + N_s) / t_single,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
+    args = ap.parse_args()
+
+    rank, world, local = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1), ("LOCAL_RANK", 0)))
+    cfg = dict(CONFIGS[args.config], cfg=args.config)
+    P, N, G = cfg["P"], cfg["N"], cfg["G"]
+
+    import numpy as np
+    import torch
+    import escalator_amd as esc
+    from escalator_amd.dist import Exchange, shard_range
+
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    lo, hi = shard_range(P, rank, world)
+    nlo, nhi = shard_range(N, rank, world)
+    t0 = time.time()
+    s = esc.Synth(P, N, G, config=args.config, seed=0xE5CA1A7E00000000 + args.config, p_lo=lo, p_hi=hi, threads=16)
+    shard_bytes = pod_bytes(s.pod_c)
+    replicas = int(max(1, min(8, -(-1_000_000_000 // max(shard_bytes, 1)))))   # >= 1 GB resident: HBM-served
+    ctx = esc.Context(s, device=local, rank=rank, world=world)
+    ctx.load_synth(s, pod_offset=lo, node_lo=nlo, node_hi=nhi, replicas=replicas)
+    ctx.set_state(s.states)
+    log("rank %d: shard pods [%d,%d) nodes [%d,%d), %.1f MB x %d replicas, setup %.1fs" %
+        (rank, lo, hi, nlo, nhi, shard_bytes / 1e6, replicas, time.time() - t0))
+
+    if world == 1:
+        ctx.use_graph(True)
+        step = ctx.run
+    else:
+        ex = Exchange(ctx, device_collective=True)
+        step = ex.step
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # Per-kernel device time of K1 (the dominant kernel), HIP events on the context's stream.
+    kp = min(args.steps, 10)
+    ctx.set_timing(True)
+    k1 = []
+    stages = []
+    for _ in range(kp):
+        step()
+        ctx.sync()
+        st = ctx.stage_times()
+        k1.append(st[0])
+        stages.append(st)
+    ctx.set_timing(False)
+    k1_ms = float(np.mean(k1))
+    stage_mean = np.mean(np.array(stages), axis=0)
+
+    parity = None
+    if world == 1 and not args.no_parity:
+        from oracle import soa
+        tot, dec = ctx.results()
+        otot = soa.totals(s.pods(), s.nodes(), s.groups)
+        odf, odi = soa.decide(s.groups, s.states, otot)
+        ok = all(np.array_equal(tot[n], otot[:, k]) for k, n in enumerate(soa.TOT_FIELDS[:12]))
+        ok &= np.array_equal(dec["cpu_pct"].view(np.uint64), odf[:, 0].view(np.uint64))
+        ok &= np.array_equal(dec["mem_pct"].view(np.uint64), odf[:, 1].view(np.uint64))
+        ok &= np.array_equal(dec["delta"], odi[:, 0])
+        parity = "bit-exact vs C oracle, all %d groups" % G if ok else "MISMATCH vs C oracle"
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    algo = pod_bytes(s.pod_c)
+    achieved = algo / (k1_ms * 1e-3) / 1e9
+    records = P + N
+    value = records * args.steps / elapsed
+    decision_bytes = (pod_bytes(s.pod_c) + node_bytes(s.node_c, nlo, nhi)) * world
+    out = {
+        "metric": "pod+node records evaluated/sec per scale decision & % HBM peak, 1/2/4/8 GPUs",
+        "value": value,
+        "unit": "records/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (deterministic counter-hash generator, escalator_amd/csrc/esc_synth.cpp)",
+        "config": {"workload": cfg["name"], "pods": P, "nodes": N, "node_groups": G,
+                   "parallelism": "shard%d" % world, "replicas_rotated": replicas},
+        "hbm_frac_decision": decision_bytes / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9 * world),
+        "roofline": {"bound": "hbm", "kernel": "k_pod_reduce", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "algorithmic_bytes_per_launch": algo, "launch_ms": k1_ms},
+        "stage_ms": {"k_pod_reduce": stage_mean[0], "k_node_reduce": stage_mean[1], "k_combine": stage_mean[2],
+                     "d2h": stage_mean[3]} if world == 1 else None,
+        "parity": parity,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(cfg, G)
+    print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -424,8 +424,7 @@ uint32_t esc_ctx_pair_head(const esc_ctx* c, const char* key, const char* value,
 
 int32_t esc_set_replicas(esc_ctx* c, int32_t n) {
     if (!c || n < 1 || n > 64) return ESC_E_INVAL;
-    if (c->pods_loaded) return ESC_E_STATE;
-    c->n_replicas = n;
+    c->n_replicas = n;              // applies from the next esc_load_pods
     return ESC_OK;
 }
 
@@ -622,7 +621,7 @@ int32_t esc_reduce(esc_ctx* c) {
     if (rc) return rc;
     hipSetDevice(c->device);
     rc = enqueue_step(c, c->cur, false, false);
-    c->cur = (c->cur + 1) % c->n_replicas;
+    c->cur = (c->cur + 1) % (int)c->pods.size();
     c->pending = true;
     return rc;
 }
@@ -689,10 +688,11 @@ int32_t esc_run(esc_ctx* c) {
     if (c->world != 1) return ESC_E_STATE;            // multi-rank: reduce, exchange, decide
     hipSetDevice(c->device);
     const int r = c->cur;
-    c->cur = (c->cur + 1) % c->n_replicas;
+    const int nrep = (int)c->pods.size();
+    c->cur = (c->cur + 1) % nrep;
     c->pending = true;
     if (!c->use_graph || c->timing) return enqueue_step(c, r, true, true);
-    if ((int)c->graphs.size() != c->n_replicas) { drop_graphs(c); c->graphs.assign(c->n_replicas, nullptr); }
+    if ((int)c->graphs.size() != nrep) { drop_graphs(c); c->graphs.assign(nrep, nullptr); }
     if (!c->graphs[r]) {
         hipGraph_t graph = nullptr;
         HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));

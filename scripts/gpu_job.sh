@@ -1,0 +1,22 @@
+#!/bin/bash
+# GPU validation + measurement job (run through gpurun).  Every GPU step has its own time
+# limit and the steps are chained: the first failure ends the job.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+TAG=${TAG:-r01}
+STEPS=${STEPS:-20}
+echo "[job] $(date) pytest -m gpu"
+timeout -k 10 420 python -u -m pytest tests/ -m gpu -x -v --timeout 120 --timeout-method thread \
+    > gpurun_out/pytest_gpu_${TAG}.log 2>&1 && echo "[job] pytest ok" &&
+echo "[job] $(date) smoke" &&
+timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 &&
+echo "[job] $(date) bench" &&
+timeout -k 10 400 python -u bench.py --steps ${STEPS} --warmup 5 > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err &&
+cat gpurun_out/bench_${TAG}.json &&
+echo "[job] $(date) rocprofv3 kernel trace" &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run \
+    -- python3 bench.py --steps ${STEPS} --warmup 5 --no-cpu-baseline --no-parity \
+    > gpurun_out/prof_${TAG}.log 2>&1 &&
+echo "[job] $(date) done"

@@ -202,7 +202,7 @@ def test_synthetic_vs_c_oracle(esc, cfg, P, N, G):
         ctx.run()
         tot, dec = ctx.results()
         check_against_c_oracle(tot, dec, otot, odf, odi)
-    assert len(set(dec["branch"].tolist())) >= (1 if G == 1 else 4)
+    assert len(set(dec["branch"].tolist())) >= (1 if G == 1 else 3)
     ctx.force_wide(True)
     ctx.run()
     tot, dec = ctx.results()
