@@ -18,8 +18,8 @@ struct PodDev {
     const int64_t*  xc_cpu;
     const int64_t*  xc_mem;
     const uint32_t* xp;
-    const uint32_t* xc_base;   // [n_tiles] extra-container offset of each tile's first pod
-    const uint32_t* xp_base;   // [n_tiles] extra-pair offset
+    const uint32_t* xc_base;   // [n_tiles + 1] extra-container offset of each tile's first pod
+    const uint32_t* xp_base;   // [n_tiles + 1] extra-group offset
     int64_t n_tiles;
 };
 
@@ -39,21 +39,22 @@ struct NodeDev {
 };
 
 struct GroupDev {
-    const uint32_t* pod_next;
-    const uint32_t* node_next;
     const uint8_t*  dry;
     const GroupParams* params;
     int32_t G;
     uint32_t default_group;    // NONE when no group is named "default"
-    int32_t pod_chains, node_chains;
 };
 
 // Wide (exact, any-range) accumulators: global int64 atomics, one row per group.
 enum WidePod : int { WP_CPU_LO = 0, WP_CPU_HI, WP_MEM_LO, WP_MEM_HI, WP_CNT, WP_K };
 enum WideNode : int { WN_CPU_LO = 0, WN_CPU_HI, WN_MEM_LO, WN_MEM_HI, WN_UNT, WN_TAINT, WN_CORD, WN_FIRST, WN_K };
 
-hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk,
+// variant: 0 = 512 threads + two-tile pipeline (default), 1 = 1024 threads, no pipeline,
+// 2 = 512 no pipeline, 3 = 1024 + pipeline (ESC_K1_VARIANT, for measurement).
+hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st);
+hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
+                               int64_t* wide, hipStream_t st);
 hipError_t launch_node_reduce(const NodeDev& n, const GroupDev& g, int n_chunk, int gt,
                               uint64_t* part, int64_t* wide, hipStream_t st);
 hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* pod_part, int nblk,

@@ -24,8 +24,10 @@ namespace esc {
 
 namespace {
 
-constexpr int BLOCK = 1024;          // 16 waves per workgroup
+constexpr int BLOCK = 1024;          // 16 waves per workgroup (node reduce)
 constexpr int WAVES = BLOCK / 64;
+constexpr int POD_BLOCK = 512;       // K1: 8 waves, 256-VGPR budget for two tiles in flight
+constexpr int POD_WAVES = POD_BLOCK / 64;
 
 __device__ __forceinline__ uint4 ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ ulonglong2 ld2(const int64_t* p) {
@@ -98,90 +100,252 @@ struct PodWide {         // exact path: global int64 words, values split lo32/hi
 };
 
 // Per-group membership of one pod — NewPodAffinityFilterFunc (node_group.go:218) for
-// every labelled group via the pair chains, NewPodDefaultFilterFunc (:256) for the
-// default group.  Daemonset pods never reach here.
+// every labelled group (the packed list names each selecting group), and
+// NewPodDefaultFilterFunc (:256) for the default group.  Daemonset pods never reach here.
 template <class F>
 __device__ __forceinline__ void pod_groups(uint32_t f, uint32_t g, const uint32_t* __restrict__ xp,
                                            uint32_t& q, const GroupDev& G, F&& emit) {
     if (pf_default_ok(f) && G.default_group != NONE) emit(G.default_group);
-    const uint32_t nx = pf_xpair(f);
-    for (uint32_t k = 0;; ++k) {
-        if (g != NONE) {
-            emit(g);
-            if (G.pod_chains)
-                for (uint32_t h = G.pod_next[g]; h != NONE; h = G.pod_next[h]) emit(h);
+    if (g != NONE) emit(g);
+    for (uint32_t k = pf_xpair(f); k; --k) emit(xp[q++]);
+}
+
+__device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int src) {
+    return __shfl(v, src, 64);
+}
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) { const uint32_t o = __shfl_xor(v, d, 64); v = o > v ? o : v; }
+    return v;
+}
+
+// One wave's 256-pod tile in registers: the fixed per-pod words (16 B per lane per array)
+// and the tile's extra records, which are contiguous ([xc_base[t], xc_base[t+1])) and so
+// are fetched coalesced, lane l holding records l and l+64, before the tile is processed.
+struct PodTile {
+    uint4 f, c, g;
+    ulonglong2 m01, m23;
+    unsigned long long xcc0, xcm0, xcc1, xcm1;
+    uint32_t xp0, xp1;
+    uint32_t xcb, xcn, xpb, xpn;
+};
+
+struct TileBases {
+    uint32_t xcb, xcn, xpb, xpn;
+};
+
+typedef __attribute__((address_space(4))) const uint32_t cu32;   // constant: scalar loads
+
+// Offsets of a tile's extra records: wave-uniform, fetched with s_load so they never
+// sit in the vector-memory queue in front of the tile data.
+__device__ __forceinline__ TileBases tile_bases(const PodDev& P, int64_t t) {
+    const cu32* xc = (const cu32*)P.xc_base;
+    const cu32* xp = (const cu32*)P.xp_base;
+    TileBases b;
+    b.xcb = xc[t];
+    b.xcn = xc[t + 1] - b.xcb;
+    b.xpb = xp[t];
+    b.xpn = xp[t + 1] - b.xpb;
+    return b;
+}
+
+__device__ __forceinline__ void tile_load(const PodDev& P, int64_t t, uint32_t lane, const TileBases& b,
+                                          PodTile& T) {
+    const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
+    T.xcb = b.xcb; T.xcn = b.xcn; T.xpb = b.xpb; T.xpn = b.xpn;
+    T.f = ld4(P.flags + p0);
+    T.c = ld4(P.cpu0 + p0);
+    T.m01 = ld2(P.mem0 + p0);
+    T.m23 = ld2(P.mem0 + p0 + 2);
+    T.g = ld4(P.pair0 + p0);
+    T.xcc0 = T.xcm0 = T.xcc1 = T.xcm1 = 0;
+    T.xp0 = T.xp1 = NONE;
+    if (lane < T.xcn) {
+        T.xcc0 = (unsigned long long)P.xc_cpu[T.xcb + lane];
+        T.xcm0 = (unsigned long long)P.xc_mem[T.xcb + lane];
+    }
+    if (lane + 64 < T.xcn) {
+        T.xcc1 = (unsigned long long)P.xc_cpu[T.xcb + 64 + lane];
+        T.xcm1 = (unsigned long long)P.xc_mem[T.xcb + 64 + lane];
+    }
+    if (lane < T.xpn) T.xp0 = P.xp[T.xpb + lane];
+    if (lane + 64 < T.xpn) T.xp1 = P.xp[T.xpb + 64 + lane];
+}
+
+// Runs `body` for pod j of the lane's four with a compile-time index (registers, no scratch).
+#define ESC_FOR_POD(j, ...) \
+    _Pragma("unroll") for (int jj_ = 0; jj_ < 4; ++jj_) if (jj_ == (int)(j)) { __VA_ARGS__; }
+
+// Processes one tile whose extra records are all in registers (<= 128 of each kind):
+// shuffles only, no memory waits (see k_pod_reduce).
+__device__ __forceinline__ void process_tile_fast(const PodDev& P, const GroupDev& G, const PodLds& acc,
+                                                  const PodWide& spill, int32_t g0, uint32_t gw, uint32_t lane,
+                                                  const PodTile& cur) {
+    // ------------------------------------------------ process tile t
+    const uint32_t fs[4] = {cur.f.x, cur.f.y, cur.f.z, cur.f.w};
+    const uint32_t gs[4] = {cur.g.x, cur.g.y, cur.g.z, cur.g.w};
+    uint64_t cpu[4] = {cur.c.x, cur.c.y, cur.c.z, cur.c.w};
+    uint64_t mem[4] = {cur.m01.x, cur.m01.y, cur.m23.x, cur.m23.y};
+    uint32_t xc_end[4], xp_end[4];
+    uint32_t nxc = 0, nxp = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        nxc += pf_xctr(fs[j]); xc_end[j] = nxc;
+        nxp += pf_xpair(fs[j]); xp_end[j] = nxp;
+    }
+    uint32_t oc = 0, op = 0;
+    if (__ballot((nxc | nxp) != 0)) {                  // wave-uniform
+        const uint64_t v = (uint64_t)nxc | ((uint64_t)nxp << 32);
+        const uint64_t s = wave_incl_scan(v, (int)lane) - v;
+        oc = (uint32_t)s;
+        op = (uint32_t)(s >> 32);
+    }
+    // ComputePodResourceRequest (types.go:72-89) over the extra records in record
+    // order: regular extras add, then init containers max, then the overhead adds.
+    if (__ballot(nxc != 0)) {
+        const uint32_t kmax = wave_max(nxc);
+        for (uint32_t k = 0; k < kmax; ++k) {
+            const uint32_t rel = oc + k;
+            unsigned long long c = shfl64(cur.xcc0, (int)(rel & 63));
+            unsigned long long m = shfl64(cur.xcm0, (int)(rel & 63));
+            if (cur.xcn > 64) {                        // wave-uniform
+                const unsigned long long c1 = shfl64(cur.xcc1, (int)(rel & 63));
+                const unsigned long long m1 = shfl64(cur.xcm1, (int)(rel & 63));
+                if (rel >= 64) { c = c1; m = m1; }
+            }
+            if (k < nxc) {
+                const uint32_t j = (k >= xc_end[0]) + (k >= xc_end[1]) + (k >= xc_end[2]);
+                ESC_FOR_POD(j, {
+                    const uint32_t q = k - (jj_ ? xc_end[jj_ - 1] : 0u);
+                    const uint32_t nreg = pf_xreg(fs[jj_]), ninit = pf_xinit(fs[jj_]);
+                    if (q < nreg || q >= nreg + ninit) {
+                        cpu[jj_] += c;
+                        mem[jj_] += m;
+                    } else {
+                        cpu[jj_] = ((int64_t)cpu[jj_] >= (int64_t)c) ? cpu[jj_] : c;
+                        mem[jj_] = ((int64_t)mem[jj_] >= (int64_t)m) ? mem[jj_] : m;
+                    }
+                });
+            }
         }
-        if (k >= nx) break;
-        g = xp[q++];
+    }
+    // Memberships: default group + listed groups; daemonsets excluded (node_group.go:221,259).
+    uint32_t live = 0, ok = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool ds = fs[j] & ESC_PF_DAEMONSET;
+        const bool in = cpu[j] < (uint64_t)POD_CPU_LIMIT && mem[j] < (uint64_t)POD_MEM_LIMIT;
+        live |= (ds ? 0u : 1u) << j;
+        ok |= (in ? 1u : 0u) << j;
+        if (ds) continue;
+        const bool dflt = pf_default_ok(fs[j]) && G.default_group != NONE;
+        if (in) {
+            const uint64_t vcc = cpu[j] | (1ull << CNT_SHIFT);
+            if (dflt) acc.add(G.default_group, vcc, mem[j]);
+            if (gs[j] != NONE) acc.add(gs[j], vcc, mem[j]);
+        } else {                                       // outside the packed range: exact spill
+            if (dflt && G.default_group - (uint32_t)g0 < gw)
+                spill.add(G.default_group, (int64_t)cpu[j], (int64_t)mem[j]);
+            if (gs[j] != NONE && gs[j] - (uint32_t)g0 < gw) spill.add(gs[j], (int64_t)cpu[j], (int64_t)mem[j]);
+        }
+    }
+    if (__ballot(nxp != 0)) {
+        const uint32_t kmax = wave_max(nxp);
+        for (uint32_t k = 0; k < kmax; ++k) {
+            const uint32_t rel = op + k;
+            uint32_t g = __shfl(cur.xp0, (int)(rel & 63), 64);
+            if (cur.xpn > 64) {
+                const uint32_t g1 = __shfl(cur.xp1, (int)(rel & 63), 64);
+                if (rel >= 64) g = g1;
+            }
+            if (k < nxp) {
+                const uint32_t j = (k >= xp_end[0]) + (k >= xp_end[1]) + (k >= xp_end[2]);
+                ESC_FOR_POD(j, {
+                    if (live & (1u << jj_)) {
+                        if (ok & (1u << jj_)) acc.add(g, cpu[jj_] | (1ull << CNT_SHIFT), mem[jj_]);
+                        else if (g - (uint32_t)g0 < gw) spill.add(g, (int64_t)cpu[jj_], (int64_t)mem[jj_]);
+                    }
+                });
+            }
+        }
     }
 }
 
 }  // namespace
 
 // =====================================================================  K1 (fast)
-__global__ __launch_bounds__(BLOCK) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
-                                                      uint64_t* __restrict__ part,
-                                                      int64_t* __restrict__ wide) {
+// Per wave a two-stage software pipeline: while tile t is processed, tile t+16's fixed
+// words and extra records are in flight, so the processing of a tile does not wait on
+// memory and each wave keeps ~5-10 KB of loads outstanding (80-160 KB per CU).
+template <int THREADS, bool PIPE>
+__global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
+                                                        uint64_t* __restrict__ part,
+                                                        int64_t* __restrict__ wide) {
+    constexpr int NW = THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     PodLds acc{lds, lds + gw, g0, gw};
-    for (uint32_t i = threadIdx.x; i < 2 * gw; i += BLOCK) lds[i] = 0;
+    for (uint32_t i = threadIdx.x; i < 2 * gw; i += THREADS) lds[i] = 0;
     __syncthreads();
 
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t per = (P.n_tiles + gridDim.x - 1) / gridDim.x;
     const int64_t t_lo = (int64_t)blockIdx.x * per;
     const int64_t t_hi = t_lo + per < P.n_tiles ? t_lo + per : P.n_tiles;
+    const PodWide spill{wide};
 
-    for (int64_t t = t_lo + wid; t < t_hi; t += WAVES) {
-        const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
-        const uint4 f4 = ld4(P.flags + p0);
-        const uint4 c4 = ld4(P.cpu0 + p0);
-        const ulonglong2 m01 = ld2(P.mem0 + p0);
-        const ulonglong2 m23 = ld2(P.mem0 + p0 + 2);
-        const uint4 g4 = ld4(P.pair0 + p0);
-        const uint32_t fs[4] = {f4.x, f4.y, f4.z, f4.w};
-        const uint32_t cs[4] = {c4.x, c4.y, c4.z, c4.w};
-        const int64_t ms[4] = {(int64_t)m01.x, (int64_t)m01.y, (int64_t)m23.x, (int64_t)m23.y};
-        const uint32_t gs[4] = {g4.x, g4.y, g4.z, g4.w};
-
-        uint32_t nxc = 0, nxp = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) { nxc += pf_xctr(fs[j]); nxp += pf_xpair(fs[j]); }
-        uint32_t oc = 0, op = 0;
-        if (__ballot((nxc | nxp) != 0)) {            // wave-uniform: locate the extras
-            const uint64_t v = (uint64_t)nxc | ((uint64_t)nxp << 32);
-            const uint64_t s = wave_incl_scan(v, lane) - v;
-            oc = P.xc_base[t] + (uint32_t)s;
-            op = P.xp_base[t] + (uint32_t)(s >> 32);
+    // Tiles with more than 128 extra records of one kind are left to k_pod_bigtiles.
+    int64_t t = t_lo + wid;
+    if constexpr (PIPE) {
+        PodTile A, B;                                      // ping-pong: tile t+NW in flight
+        if (t < t_hi) tile_load(P, t, lane, tile_bases(P, t), A);
+        for (;;) {
+            if (t >= t_hi) break;
+            int64_t t1 = t + NW;
+            if (t1 < t_hi) tile_load(P, t1, lane, tile_bases(P, t1), B);
+            if (A.xcn <= 128 && A.xpn <= 128) process_tile_fast(P, G, acc, spill, g0, gw, lane, A);
+            t = t1;
+            if (t >= t_hi) break;
+            t1 = t + NW;
+            if (t1 < t_hi) tile_load(P, t1, lane, tile_bases(P, t1), A);
+            if (B.xcn <= 128 && B.xpn <= 128) process_tile_fast(P, G, acc, spill, g0, gw, lane, B);
+            t = t1;
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t f = fs[j];
-            if (f & ESC_PF_DAEMONSET) {              // PodIsDaemonSet -> no group (node_group.go:221,259)
-                oc += pf_xctr(f);
-                op += pf_xpair(f);
-                continue;
-            }
-            int64_t cpu, mem;
-            pod_request(f, cs[j], ms[j], P.xc_cpu, P.xc_mem, oc, cpu, mem);
-            if ((uint64_t)cpu >= (uint64_t)POD_CPU_LIMIT || (uint64_t)mem >= (uint64_t)POD_MEM_LIMIT) {
-                // Outside the packed range: exact spill to the wide accumulators.
-                const PodWide spill{wide};
-                pod_groups(f, gs[j], P.xp, op, G, [&](uint32_t g) {
-                    if (g - (uint32_t)g0 < gw) spill.add(g, cpu, mem);
-                });
-                continue;
-            }
-            const uint64_t vcc = (uint64_t)cpu | (1ull << CNT_SHIFT);
-            pod_groups(f, gs[j], P.xp, op, G, [&](uint32_t g) { acc.add(g, vcc, (uint64_t)mem); });
+    } else {
+        for (; t < t_hi; t += NW) {                       // latency hidden across waves only
+            PodTile A;
+            tile_load(P, t, lane, tile_bases(P, t), A);
+            if (A.xcn <= 128 && A.xpn <= 128) process_tile_fast(P, G, acc, spill, g0, gw, lane, A);
         }
     }
     __syncthreads();
     uint64_t* out = part + (int64_t)blockIdx.x * 2 * G.G + g0;
-    for (uint32_t i = threadIdx.x; i < gw; i += BLOCK) {
+    for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
         out[i] = acc.cc[i];
         out[G.G + i] = acc.mem[i];
+    }
+}
+
+// Tiles whose extra records exceed what one wave holds in registers (listed by the host
+// at load; rare): one wave per tile, records read from memory, exact wide accumulation.
+__global__ __launch_bounds__(64) void k_pod_bigtiles(PodDev P, GroupDev G, const uint32_t* __restrict__ tiles,
+                                                     int64_t* __restrict__ wide) {
+    const uint32_t lane = threadIdx.x;
+    const int64_t t = tiles[blockIdx.x];
+    const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
+    uint32_t nxc = 0, nxp = 0;
+    for (int j = 0; j < 4; ++j) { nxc += pf_xctr(P.flags[p0 + j]); nxp += pf_xpair(P.flags[p0 + j]); }
+    const uint64_t v = (uint64_t)nxc | ((uint64_t)nxp << 32);
+    const uint64_t s = wave_incl_scan(v, (int)lane) - v;
+    uint32_t oc = P.xc_base[t] + (uint32_t)s, op = P.xp_base[t] + (uint32_t)(s >> 32);
+    const PodWide acc{wide};
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t f = P.flags[p0 + j];
+        if (f & ESC_PF_DAEMONSET) { oc += pf_xctr(f); op += pf_xpair(f); continue; }
+        int64_t cpu, mem;
+        pod_request(f, P.cpu0[p0 + j], P.mem0[p0 + j], P.xc_cpu, P.xc_mem, oc, cpu, mem);
+        pod_groups(f, P.pair0[p0 + j], P.xp, op, G, [&](uint32_t g) { acc.add(g, cpu, mem); });
     }
 }
 
@@ -237,15 +401,8 @@ __device__ __forceinline__ void node_groups(const NodeDev& N, const GroupDev& G,
     uint32_t g = N.label0[i];
     const uint32_t nx = nf_xlbl(f);
     uint32_t q = nx ? N.xl_off[i] : 0;
-    for (uint32_t k = 0;; ++k) {
-        if (g != NONE) {
-            emit(g);
-            if (G.node_chains)
-                for (uint32_t h = G.node_next[g]; h != NONE; h = G.node_next[h]) emit(h);
-        }
-        if (k >= nx) break;
-        g = N.xl[q++];
-    }
+    if (g != NONE) emit(g);
+    for (uint32_t k = 0; k < nx; ++k) emit(N.xl[q++]);
 }
 
 }  // namespace
@@ -622,10 +779,22 @@ __global__ __launch_bounds__(256) void k_group_bounds(const uint64_t* __restrict
 }
 
 // ===================================================================== launchers
-hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk,
+hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st) {
     const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
-    hipLaunchKernelGGL(k_pod_reduce, dim3(nblk), dim3(BLOCK), lds, st, p, g, g0, (uint32_t)gw, part, wide);
+    switch (variant) {
+        case 1: hipLaunchKernelGGL((k_pod_reduce<1024, false>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        case 2: hipLaunchKernelGGL((k_pod_reduce<512, false>), dim3(nblk), dim3(512), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        case 3: hipLaunchKernelGGL((k_pod_reduce<1024, true>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        default: hipLaunchKernelGGL((k_pod_reduce<512, true>), dim3(nblk), dim3(512), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
+                               int64_t* wide, hipStream_t st) {
+    if (n_big <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pod_bigtiles, dim3((unsigned)n_big), dim3(64), 0, st, p, g, tiles, wide);
     return hipGetLastError();
 }
 

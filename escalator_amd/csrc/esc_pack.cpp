@@ -85,6 +85,16 @@ namespace {
 
 inline int64_t req_or(int32_t has, int64_t v, int64_t absent) { return has ? v : absent; }
 
+// Matched pair heads -> the sorted, de-duplicated set of groups they select (every group
+// sharing a pair is listed explicitly, so the kernels never walk chains).
+void expand_chains(std::vector<uint32_t>& heads, const std::vector<uint32_t>& next) {
+    const size_t n = heads.size();
+    for (size_t i = 0; i < n; ++i)
+        for (uint32_t h = next[heads[i]]; h != NONE; h = next[h]) heads.push_back(h);
+    std::sort(heads.begin(), heads.end());
+    heads.erase(std::unique(heads.begin(), heads.end()), heads.end());
+}
+
 int32_t pack_pod(esc_packer* pk, const esc_pod_obj& o) {
     HostSnapshot& s = pk->s;
     uint32_t f = 0;
@@ -113,12 +123,11 @@ int32_t pack_pod(esc_packer* pk, const esc_pod_obj& o) {
                 }
             }
         }
-        std::sort(heads.begin(), heads.end());
-        heads.erase(std::unique(heads.begin(), heads.end()), heads.end());
+        expand_chains(heads, pk->gi->pod_next);
     } else {
         heads.push_back(0);
     }
-    if (heads.size() > 1 + ESC_PF_PAIR_MASK) return ESC_E_LIMIT;
+    if (heads.size() > 1 + ESC_PF_PAIR_MASK) return ESC_E_LIMIT;   // > 64 matching groups
     const uint32_t pair0 = heads.empty() ? NONE : heads[0];
     for (size_t i = 1; i < heads.size(); ++i) s.xp.push_back(heads[i]);
     f |= (uint32_t)(heads.empty() ? 0 : heads.size() - 1) << ESC_PF_XPAIR_SHIFT;
@@ -172,8 +181,7 @@ int32_t pack_node(esc_packer* pk, const esc_node_obj& o) {
             uint32_t h = pk->gi->head(o.labels[i].key, o.labels[i].value, 1);
             if (h != NONE) heads.push_back(h);
         }
-        std::sort(heads.begin(), heads.end());
-        heads.erase(std::unique(heads.begin(), heads.end()), heads.end());
+        expand_chains(heads, pk->gi->node_next);
     } else {
         heads.push_back(0);
     }

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -55,10 +56,10 @@ void dfree(T*& p) {
 
 struct PodBuf {
     uint32_t *flags = nullptr, *cpu0 = nullptr, *pair0 = nullptr, *xp = nullptr, *xc_base = nullptr,
-             *xp_base = nullptr;
+             *xp_base = nullptr, *big = nullptr;
     int64_t *mem0 = nullptr, *xc_cpu = nullptr, *xc_mem = nullptr;
     void release() {
-        dfree(flags); dfree(cpu0); dfree(pair0); dfree(xp); dfree(xc_base); dfree(xp_base);
+        dfree(flags); dfree(cpu0); dfree(pair0); dfree(xp); dfree(xc_base); dfree(xp_base); dfree(big);
         dfree(mem0); dfree(xc_cpu); dfree(xc_mem);
     }
 };
@@ -90,13 +91,12 @@ struct esc_ctx {
     GroupIndex gi;
     std::vector<GroupParams> params;
     // device group tables
-    uint32_t *d_pod_next = nullptr, *d_node_next = nullptr;
     uint8_t* d_dry = nullptr;
     GroupParams* d_params = nullptr;
     // snapshot
     std::vector<PodBuf> pods;
     int n_replicas = 1, cur = 0;
-    int64_t n_pods = 0, n_tiles = 0, n_xc = 0, n_xp = 0, pod_offset = 0;
+    int64_t n_pods = 0, n_tiles = 0, n_xc = 0, n_xp = 0, pod_offset = 0, n_big = 0;
     bool pods_loaded = false;
     NodeBuf nodes;
     int64_t n_nodes = 0, n_xl = 0, n_trk = 0, node_lo = 0, node_hi = 0;
@@ -113,6 +113,7 @@ struct esc_ctx {
     int64_t *bound_words = nullptr, *bound_first = nullptr;  // caller-bound (RCCL) buffers
     bool work_ready = false;
     bool force_wide = false;
+    int k1_variant = 0;                                       // ESC_K1_VARIANT (measurement knob)
     // graph
     bool use_graph = false;
     std::vector<hipGraphExec_t> graphs;
@@ -144,14 +145,10 @@ namespace {
 
 GroupDev group_dev(const esc_ctx* c) {
     GroupDev g;
-    g.pod_next = c->d_pod_next;
-    g.node_next = c->d_node_next;
     g.dry = c->d_dry;
     g.params = c->d_params;
     g.G = c->gi.G;
     g.default_group = c->gi.default_group < 0 ? NONE : (uint32_t)c->gi.default_group;
-    g.pod_chains = c->gi.pod_chains ? 1 : 0;
-    g.node_chains = c->gi.node_chains ? 1 : 0;
     return g;
 }
 
@@ -215,7 +212,8 @@ int32_t ensure_work(esc_ctx* c) {
     const int32_t G = c->gi.G;
     const int gw = std::min(G, POD_WINDOW_MAX);
     const int lds = gw * 16;
-    const int per_cu = std::max(1, std::min(2, LDS_BYTES / std::max(lds, 1)));
+    const int max_blocks = (c->k1_variant == 1 || c->k1_variant == 3) ? 2 : 4;   // 2048 threads per CU
+    const int per_cu = std::max(1, std::min(max_blocks, LDS_BYTES / std::max(lds, 1)));
     int nblk = c->cu_count * per_cu;
     const int64_t pods_per_block = (c->n_tiles * TILE + nblk - 1) / std::max(nblk, 1);
     if (pods_per_block > PODS_PER_BLOCK_MAX) nblk = (int)((c->n_tiles * TILE + PODS_PER_BLOCK_MAX - 1) / PODS_PER_BLOCK_MAX);
@@ -265,8 +263,9 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
             const PodDev p = pod_dev(c, r);
             for (int32_t g0 = 0; g0 < g.G; g0 += POD_WINDOW_MAX) {
                 const int32_t gw = std::min(POD_WINDOW_MAX, g.G - g0);
-                HIP_TRY(launch_pod_reduce(p, g, g0, gw, c->nblk, c->d_pod_part, c->d_wide_pod, st));
+                HIP_TRY(launch_pod_reduce(p, g, g0, gw, c->nblk, c->k1_variant, c->d_pod_part, c->d_wide_pod, st));
             }
+            HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
         }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
         if (c->n_chunk) HIP_TRY(launch_node_reduce(n, g, c->n_chunk, c->gt, c->d_node_part, c->d_wide_node, st));
@@ -341,6 +340,7 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     if (!c) return ESC_E_NOMEM;
     c->rank = rank;
     c->world = world;
+    if (const char* v = std::getenv("ESC_K1_VARIANT")) c->k1_variant = std::atoi(v);
     c->gi.build(groups, n_groups);
     c->params.resize(n_groups);
     for (int32_t g = 0; g < n_groups; ++g) params_from(c->params[g], groups[g], nullptr);
@@ -366,13 +366,10 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     for (int i = 0; i < MAX_STAGES; ++i)
         if (hipEventCreate(&c->ev[i]) != hipSuccess) return fail(ESC_E_HIP);
     const size_t G = (size_t)n_groups;
-    if (dalloc(&c->d_pod_next, G) || dalloc(&c->d_node_next, G) || dalloc(&c->d_dry, G) || dalloc(&c->d_params, G))
-        return fail(ESC_E_NOMEM);
+    if (dalloc(&c->d_dry, G) || dalloc(&c->d_params, G)) return fail(ESC_E_NOMEM);
     std::vector<uint8_t> dry(G);
     for (size_t g = 0; g < G; ++g) dry[g] = (uint8_t)c->params[g].dry;
-    if (hipMemcpy(c->d_pod_next, c->gi.pod_next.data(), G * 4, hipMemcpyHostToDevice) ||
-        hipMemcpy(c->d_node_next, c->gi.node_next.data(), G * 4, hipMemcpyHostToDevice) ||
-        hipMemcpy(c->d_dry, dry.data(), G, hipMemcpyHostToDevice) ||
+    if (hipMemcpy(c->d_dry, dry.data(), G, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_params, c->params.data(), G * sizeof(GroupParams), hipMemcpyHostToDevice))
         return fail(ESC_E_HIP);
     (void)rc;
@@ -389,7 +386,7 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         release_sort(c);
         for (auto& b : c->pods) b.release();
         c->nodes.release();
-        dfree(c->d_pod_next); dfree(c->d_node_next); dfree(c->d_dry); dfree(c->d_params);
+        dfree(c->d_dry); dfree(c->d_params);
         for (int i = 0; i < MAX_STAGES; ++i)
             if (c->ev[i]) hipEventDestroy(c->ev[i]);
         if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -439,7 +436,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     // Validate every group id (a bad id would index outside the LDS / group tables) and
     // build the per-tile offsets of the extra records.
     const int64_t n_tiles = (n + TILE - 1) / TILE;
-    std::vector<uint32_t> xc_base(std::max<int64_t>(n_tiles, 1)), xp_base(std::max<int64_t>(n_tiles, 1));
+    std::vector<uint32_t> xc_base(n_tiles + 1), xp_base(n_tiles + 1);
     uint64_t sc = 0, sp = 0;
     for (int64_t i = 0; i < n; ++i) {
         if ((i & (TILE - 1)) == 0) { xc_base[i / TILE] = (uint32_t)sc; xp_base[i / TILE] = (uint32_t)sp; }
@@ -448,6 +445,12 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         sc += pf_xctr(f);
         sp += pf_xpair(f);
     }
+    xc_base[n_tiles] = (uint32_t)sc;
+    xp_base[n_tiles] = (uint32_t)sp;
+    // Tiles with more extra records than a wave holds in registers go to k_pod_bigtiles.
+    std::vector<uint32_t> big;
+    for (int64_t t = 0; t < n_tiles; ++t)
+        if (xc_base[t + 1] - xc_base[t] > 128 || xp_base[t + 1] - xp_base[t] > 128) big.push_back((uint32_t)t);
     if ((int64_t)sc != p->n_xc || (int64_t)sp != p->n_xp) return ESC_E_INVAL;
     for (int64_t i = 0; i < p->n_xp; ++i)
         if (p->xp_group[i] >= G) return ESC_E_INVAL;
@@ -463,7 +466,9 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         PodBuf& b = c->pods[r];
         HIP_TRY(dalloc(&b.flags, npad)); HIP_TRY(dalloc(&b.cpu0, npad)); HIP_TRY(dalloc(&b.mem0, npad));
         HIP_TRY(dalloc(&b.pair0, npad)); HIP_TRY(dalloc(&b.xc_cpu, p->n_xc)); HIP_TRY(dalloc(&b.xc_mem, p->n_xc));
-        HIP_TRY(dalloc(&b.xp, p->n_xp)); HIP_TRY(dalloc(&b.xc_base, n_tiles)); HIP_TRY(dalloc(&b.xp_base, n_tiles));
+        HIP_TRY(dalloc(&b.xp, p->n_xp)); HIP_TRY(dalloc(&b.xc_base, n_tiles + 1)); HIP_TRY(dalloc(&b.xp_base, n_tiles + 1));
+        HIP_TRY(dalloc(&b.big, big.size()));
+        if (!big.empty()) HIP_TRY(hipMemcpy(b.big, big.data(), big.size() * 4, hipMemcpyHostToDevice));
         if (r == 0) {
             if (n) {
                 HIP_TRY(hipMemcpy(b.flags, p->flags, n * 4, hipMemcpyHostToDevice));
@@ -483,10 +488,8 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
                 HIP_TRY(hipMemcpy(b.xc_mem, p->xc_mem, p->n_xc * 8, hipMemcpyHostToDevice));
             }
             if (p->n_xp) HIP_TRY(hipMemcpy(b.xp, p->xp_group, p->n_xp * 4, hipMemcpyHostToDevice));
-            if (n_tiles) {
-                HIP_TRY(hipMemcpy(b.xc_base, xc_base.data(), n_tiles * 4, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemcpy(b.xp_base, xp_base.data(), n_tiles * 4, hipMemcpyHostToDevice));
-            }
+            HIP_TRY(hipMemcpy(b.xc_base, xc_base.data(), (n_tiles + 1) * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(b.xp_base, xp_base.data(), (n_tiles + 1) * 4, hipMemcpyHostToDevice));
         } else {
             const PodBuf& a = c->pods[0];
             HIP_TRY(hipMemcpy(b.flags, a.flags, npad * 4, hipMemcpyDeviceToDevice));
@@ -498,14 +501,13 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
                 HIP_TRY(hipMemcpy(b.xc_mem, a.xc_mem, p->n_xc * 8, hipMemcpyDeviceToDevice));
             }
             if (p->n_xp) HIP_TRY(hipMemcpy(b.xp, a.xp, p->n_xp * 4, hipMemcpyDeviceToDevice));
-            if (n_tiles) {
-                HIP_TRY(hipMemcpy(b.xc_base, a.xc_base, n_tiles * 4, hipMemcpyDeviceToDevice));
-                HIP_TRY(hipMemcpy(b.xp_base, a.xp_base, n_tiles * 4, hipMemcpyDeviceToDevice));
-            }
+            HIP_TRY(hipMemcpy(b.xc_base, a.xc_base, (n_tiles + 1) * 4, hipMemcpyDeviceToDevice));
+            HIP_TRY(hipMemcpy(b.xp_base, a.xp_base, (n_tiles + 1) * 4, hipMemcpyDeviceToDevice));
         }
     }
     c->n_pods = n;
     c->n_tiles = n_tiles;
+    c->n_big = (int64_t)big.size();
     c->n_xc = p->n_xc;
     c->n_xp = p->n_xp;
     c->pod_offset = global_offset;

@@ -71,7 +71,7 @@ namespace {
 
 struct PodDesc {
     uint32_t pred = 0;
-    uint32_t heads[8];
+    uint32_t heads[16];
     int nheads = 0;
     int n_reg = 0, n_init = 0;
     bool ovh = false;
@@ -136,6 +136,11 @@ void gen_pod(const esc_synth& S, int64_t i, PodDesc& d) {
         }
         if (x >= 200 && x < 300) d.pred |= ESC_PF_HAS_SEL;     // irrelevant "zone" selector
     }
+    // Every group sharing a matched pair is selected too (explicit group list, ascending).
+    const int nh = d.nheads;
+    for (int k = 0; k < nh; ++k)
+        for (uint32_t h = S.gi.pod_next[d.heads[k]]; h != NONE; h = S.gi.pod_next[h]) d.add_head(h);
+    std::sort(d.heads, d.heads + d.nheads);
     // Containers: 90% one, 6% two, 3% three, 1% two + one init + overhead.
     const uint64_t c = rnd(seed, 1, i, 10) % 100;
     d.n_reg = c < 90 ? 1 : c < 96 ? 2 : c < 99 ? 3 : 2;
@@ -312,7 +317,8 @@ void gen_nodes(esc_synth& S) {
     const int32_t G = p.n_groups;
     HostSnapshot& s = S.s;
     s.nflags.resize(n); s.label0.resize(n); s.ncpu.resize(n); s.nmem.resize(n); s.created.resize(n);
-    std::vector<uint32_t> second(n, NONE);
+    struct Extra { uint32_t g[6]; uint8_t n; };
+    std::vector<Extra> extra(n);
     std::vector<uint8_t> trk(n, 0);
     const int threads = std::max(1, p.n_threads);
     parallel_for(n, threads, [&](int64_t lo, int64_t hi, int) {
@@ -324,18 +330,29 @@ void gen_nodes(esc_synth& S) {
             const uint64_t b = rnd(p.seed, 2, j, 1) % 1000;
             if (b < 30) f |= ESC_NF_UNSCHED;
             else if (b < 130) f |= ESC_NF_TAINTED;
-            uint32_t h0 = S.node_head_of[c];
-            if (p.config != 1 && S.key_id[c] != K_POOL && !S.pool_groups.empty() &&
-                rnd(p.seed, 2, j, 2) % 10 == 0) {                      // + a "pool" label
-                int32_t gp = S.pool_groups[rnd(p.seed, 2, j, 3) % S.pool_groups.size()];
-                uint32_t h1 = S.node_head_of[S.canon[gp]];
-                if (h1 != h0) {
-                    second[j] = std::max(h0, h1);
-                    h0 = std::min(h0, h1);
-                    f |= 1u << ESC_NF_XLBL_SHIFT;
+            // labels: the group's pair, sometimes a "pool" pair as well; every group
+            // selecting one of them is a member (explicit list, ascending)
+            uint32_t grp[8];
+            int ng = 0;
+            auto add_chain = [&](uint32_t h) {
+                for (; h != NONE; h = S.gi.node_next[h]) {
+                    bool dup = false;
+                    for (int k = 0; k < ng; ++k) dup |= grp[k] == h;
+                    if (!dup && ng < 7) grp[ng++] = h;
                 }
+            };
+            add_chain(S.node_head_of[c]);
+            if (p.config != 1 && S.key_id[c] != K_POOL && !S.pool_groups.empty() &&
+                rnd(p.seed, 2, j, 2) % 10 == 0) {
+                const int32_t gp = S.pool_groups[rnd(p.seed, 2, j, 3) % S.pool_groups.size()];
+                add_chain(S.node_head_of[S.canon[gp]]);
             }
-            s.label0[j] = h0;
+            std::sort(grp, grp + ng);
+            s.label0[j] = ng ? grp[0] : NONE;
+            Extra& e = extra[j];
+            e.n = (uint8_t)(ng > 1 ? ng - 1 : 0);
+            for (int k = 1; k < ng; ++k) e.g[k - 1] = grp[k];
+            f |= (uint32_t)e.n << ESC_NF_XLBL_SHIFT;
             // dry-mode taintTracker: 10% of the members of dry groups
             if (S.specs[g].dry_mode && rnd(p.seed, 2, j, 4) % 10 == 0) trk[j] = 1;
             int64_t cpu = S.type_cpu[g], mem = S.type_mem[g];
@@ -352,7 +369,7 @@ void gen_nodes(esc_synth& S) {
         }
     });
     for (int64_t j = 0; j < n; ++j) {
-        if (second[j] != NONE) s.xl.push_back(second[j]);
+        for (int k = 0; k < extra[j].n; ++k) s.xl.push_back(extra[j].g[k]);
         if (trk[j]) {
             const int32_t g = (int32_t)(rnd(p.seed, 2, j, 0) % (uint64_t)G);
             s.trk_node.push_back((int32_t)j);

@@ -188,9 +188,10 @@ typedef struct esc_node_obj {
  *   flags  u32  ESC_PF_* bits + counts of extra records
  *   cpu0   u32  cpu (millicores) of the inline regular container
  *   mem0   i64  memory (bytes)   of the inline regular container
- *   pair0  u32  head group of the pod's first matching (key,value) pair, ESC_NONE if none
+ *   pair0  u32  lowest group the pod's (key,value) pairs select, ESC_NONE if none
  *   xc_cpu/xc_mem i64  extra containers per pod: [regular extras][init][overhead]
- *   xp_group u32       extra matching pairs (head groups)
+ *   xp_group u32       the other selected groups, ascending (every group sharing a
+ *                      matched pair is listed; at most 63 extra per pod)
  * Nodes:
  *   nflags u32, label0 u32, ncpu i64, nmem i64, created i64, xl_group u32.        */
 #define ESC_NONE 0xFFFFFFFFu
@@ -202,14 +203,14 @@ typedef struct esc_node_obj {
 #define ESC_PF_HAS_OVH     (1u << 4)   /* overhead record present (Spec.Overhead != nil) */
 #define ESC_PF_XREG_SHIFT  8           /* bits  8..15: regular containers beyond the inline one */
 #define ESC_PF_XINIT_SHIFT 16          /* bits 16..23: init containers                         */
-#define ESC_PF_XPAIR_SHIFT 24          /* bits 24..29: extra matching pairs                    */
+#define ESC_PF_XPAIR_SHIFT 24          /* bits 24..29: extra selected groups (xp_group)         */
 #define ESC_PF_CNT_MASK    0xFFu
 #define ESC_PF_PAIR_MASK   0x3Fu
 
 #define ESC_NF_UNSCHED     (1u << 0)   /* Spec.Unschedulable           controller.go:141 */
 #define ESC_NF_TAINTED     (1u << 1)   /* has atlassian.com/escalator  taint.go:31,80    */
 #define ESC_NF_TRACKED     (1u << 2)   /* in some group's dry-mode taintTracker controller.go:128 */
-#define ESC_NF_XLBL_SHIFT  8           /* bits 8..15: extra matching labels */
+#define ESC_NF_XLBL_SHIFT  8           /* bits 8..15: extra selected groups (xl_group)          */
 
 typedef struct esc_pod_soa {
     int64_t         n_pods;

@@ -25,6 +25,9 @@
  *
  * Parity of this file is pinned through oracle/oracle.py (checked against every
  * transcribed reference test in tests/golden/) by tests/test_pack_parity.py.
+ * Group membership is read from the packed lists (pair0/xp_group, label0/xl_group list
+ * every selecting group); the (key,value) matching that produced them is checked by the
+ * literal oracle against the packer on objects.
  * Build: gcc -O2 -ffp-contract=off (oracle/Makefile).
  */
 #include <math.h>
@@ -103,8 +106,7 @@ static void emit_out(const Acc* a, int32_t G, const int64_t* ncpu, const int64_t
 
 static void node_pass(Acc* a, int64_t lo, int64_t hi, const uint32_t* nflags, const uint32_t* label0,
                       const int64_t* ncpu, const int64_t* nmem, const uint32_t* xl, const int32_t* tn,
-                      const int32_t* tg, int64_t n_trk, const uint32_t* node_next, const uint8_t* dry,
-                      int64_t n_all) {
+                      const int32_t* tg, int64_t n_trk, const uint8_t* dry, int64_t n_all) {
     uint64_t q = 0;
     for (int64_t i = 0; i < lo && i < n_all; ++i) q += xlbl(nflags[i]);
     for (int64_t i = lo; i < hi; ++i) {
@@ -112,7 +114,7 @@ static void node_pass(Acc* a, int64_t lo, int64_t hi, const uint32_t* nflags, co
         const uint32_t nx = xlbl(f);
         for (uint32_t k = 0; k <= nx; ++k) {
             uint32_t g = k == 0 ? label0[i] : xl[q++];
-            for (; g != NONE; g = node_next[g]) {          /* every group selecting this label pair */
+            if (g != NONE) {                               /* every selecting group is listed */
                 if (a[g].first < 0) a[g].first = i;        /* allNodes[0] in lister order */
                 const int c = node_class(f, dry[g], tn, tg, n_trk, i, (int32_t)g);
                 if (c == 0) { a[g].nunt++; a[g].ncpu += ncpu[i]; a[g].nmem += nmem[i]; }
@@ -127,8 +129,8 @@ int orc_totals(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, cons
                const uint32_t* pair0, const int64_t* xc_cpu, const int64_t* xc_mem, const uint32_t* xp,
                int64_t n_nodes, const uint32_t* nflags, const uint32_t* label0, const int64_t* ncpu,
                const int64_t* nmem, const uint32_t* xl, const int32_t* tn, const int32_t* tg, int64_t n_trk,
-               int64_t node_lo, int64_t node_hi, int32_t G, int32_t default_group, const uint32_t* pod_next,
-               const uint32_t* node_next, const uint8_t* dry, int64_t* out) {
+               int64_t node_lo, int64_t node_hi, int32_t G, int32_t default_group, const uint8_t* dry,
+               int64_t* out) {
     Acc* a = (Acc*)calloc((size_t)G, sizeof(Acc));
     if (!a) return -1;
     for (int32_t g = 0; g < G; ++g) a[g].first = -1;
@@ -145,10 +147,10 @@ int orc_totals(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, cons
         const uint32_t nx = xpair(f);
         for (uint32_t k = 0; k <= nx; ++k) {
             uint32_t g = k == 0 ? pair0[p] : xp[op++];
-            for (; g != NONE; g = pod_next[g]) { a[g].pcpu += cpu; a[g].pmem += mem; a[g].npod++; }
+            if (g != NONE) { a[g].pcpu += cpu; a[g].pmem += mem; a[g].npod++; }
         }
     }
-    node_pass(a, node_lo, node_hi, nflags, label0, ncpu, nmem, xl, tn, tg, n_trk, node_next, dry, n_nodes);
+    node_pass(a, node_lo, node_hi, nflags, label0, ncpu, nmem, xl, tn, tg, n_trk, dry, n_nodes);
     emit_out(a, G, ncpu, nmem, out);
     free(a);
     return 0;
@@ -162,8 +164,8 @@ int orc_ref_scan(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, co
                  const uint32_t* pair0, const int64_t* xc_cpu, const int64_t* xc_mem, const uint32_t* xp,
                  int64_t n_nodes, const uint32_t* nflags, const uint32_t* label0, const int64_t* ncpu,
                  const int64_t* nmem, const uint32_t* xl, const int32_t* tn, const int32_t* tg, int64_t n_trk,
-                 int32_t G, int32_t default_group, const uint32_t* pod_next, const uint32_t* node_next,
-                 const uint8_t* dry, int32_t g_lo, int32_t g_hi, int64_t* out) {
+                 int32_t G, int32_t default_group, const uint8_t* dry, int32_t g_lo, int32_t g_hi,
+                 int64_t* out) {
     Acc* a = (Acc*)calloc((size_t)G, sizeof(Acc));
     if (!a) return -1;
     for (int32_t g = 0; g < G; ++g) a[g].first = -1;
@@ -181,7 +183,7 @@ int orc_ref_scan(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, co
                     const uint32_t nx = xpair(f);
                     for (uint32_t k = 0; k <= nx && !member; ++k) {
                         uint32_t h = k == 0 ? pair0[p] : xp[op + k - 1];
-                        for (; h != NONE && !member; h = pod_next[h]) member = (h == (uint32_t)g);
+                        member = (h == (uint32_t)g);
                     }
                 }
             }
@@ -199,7 +201,7 @@ int orc_ref_scan(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, co
             int member = 0;
             for (uint32_t k = 0; k <= xlbl(f); ++k) {
                 uint32_t h = k == 0 ? label0[i] : xl[q + k - 1];
-                for (; h != NONE && !member; h = node_next[h]) member = (h == (uint32_t)g);
+                member |= (h == (uint32_t)g);
             }
             q += xlbl(f);
             if (!member) continue;
@@ -322,8 +324,7 @@ static int cmp_ki(const void* a, const void* b) {
  * writes up to cap indices. */
 int64_t orc_order(int64_t n_nodes, const uint32_t* nflags, const uint32_t* label0, const int64_t* created,
                   const uint32_t* xl, const int32_t* tn, const int32_t* tg, int64_t n_trk, int64_t lo, int64_t hi,
-                  const uint32_t* node_next, const uint8_t* dry, int32_t group, int32_t which, int64_t* out,
-                  int64_t cap) {
+                  const uint8_t* dry, int32_t group, int32_t which, int64_t* out, int64_t cap) {
     KI* v = (KI*)malloc(sizeof(KI) * (size_t)(hi - lo + 1));
     int64_t m = 0;
     uint64_t q = 0;
@@ -333,7 +334,7 @@ int64_t orc_order(int64_t n_nodes, const uint32_t* nflags, const uint32_t* label
         int member = 0;
         for (uint32_t k = 0; k <= xlbl(f); ++k) {
             uint32_t h = k == 0 ? label0[i] : xl[q + k - 1];
-            for (; h != NONE && !member; h = node_next[h]) member = (h == (uint32_t)group);
+            member |= (h == (uint32_t)group);
         }
         q += xlbl(f);
         if (!member) continue;

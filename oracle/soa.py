@@ -103,12 +103,10 @@ def totals(pods: dict, nodes: dict, groups: list[dict], node_lo: int = 0, node_h
                               _p(nodes["trk_group"], C.c_int32), C.c_int64(len(nodes["trk_node"]))]
     if reference_shaped:
         lo, hi_g = g_range or (0, G)
-        rc = lib().orc_ref_scan(*pa, *na, C.c_int32(G), C.c_int32(t["default"]), _p(t["pod_next"], C.c_uint32),
-                                _p(t["node_next"], C.c_uint32), _p(t["dry"], C.c_uint8), C.c_int32(lo),
-                                C.c_int32(hi_g), _p(out, C.c_int64))
+        rc = lib().orc_ref_scan(*pa, *na, C.c_int32(G), C.c_int32(t["default"]), _p(t["dry"], C.c_uint8),
+                                C.c_int32(lo), C.c_int32(hi_g), _p(out, C.c_int64))
     else:
         rc = lib().orc_totals(*pa, *na, C.c_int64(node_lo), C.c_int64(hi), C.c_int32(G), C.c_int32(t["default"]),
-                              _p(t["pod_next"], C.c_uint32), _p(t["node_next"], C.c_uint32),
                               _p(t["dry"], C.c_uint8), _p(out, C.c_int64))
     del keep
     assert rc == 0
@@ -147,7 +145,7 @@ def order(nodes: dict, groups: list[dict], group: int, which: int, node_lo: int 
                         _p(nodes["created_ns"], C.c_int64), _p(nodes["xl_group"], C.c_uint32),
                         _p(nodes["trk_node"], C.c_int32), _p(nodes["trk_group"], C.c_int32),
                         C.c_int64(len(nodes["trk_node"])), C.c_int64(node_lo), C.c_int64(hi),
-                        _p(t["node_next"], C.c_uint32), _p(t["dry"], C.c_uint8), C.c_int32(group),
+                        _p(t["dry"], C.c_uint8), C.c_int32(group),
                         C.c_int32(which), _p(out, C.c_int64), C.c_int64(len(out)))
     m = int(m)
     out = out[:m]

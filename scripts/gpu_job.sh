@@ -13,6 +13,7 @@ timeout -k 10 420 python -u -m pytest tests/ -m gpu -x -v --timeout 120 --timeou
 echo "[job] $(date) smoke" &&
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 &&
 echo "[job] $(date) bench" &&
+timeout -k 10 300 python -u scripts/k1_variants.py > gpurun_out/k1_variants_${TAG}.json 2>&1 && cat gpurun_out/k1_variants_${TAG}.json &&
 timeout -k 10 400 python -u bench.py --steps ${STEPS} --warmup 5 > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err &&
 cat gpurun_out/bench_${TAG}.json &&
 echo "[job] $(date) rocprofv3 kernel trace" &&

@@ -1,0 +1,46 @@
+"""Times the K1 (k_pod_reduce) variants on one snapshot, interleaved in one process
+(cdna_hip_programming.md §5.4 rule 24), and checks every variant's totals are identical."""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+cfg = int(os.environ.get("CFG", 4))
+P, N, G = {4: (100_000_000, 1_000_000, 10_000), 2: (1_000_000, 10_000, 100), 3: (10_000_000, 100_000, 100)}[cfg]
+variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,2,3").split(",")]
+rounds = int(os.environ.get("ROUNDS", 3))
+import escalator_amd as esc  # noqa: E402
+
+s = esc.Synth(P, N, G, config=cfg, seed=0xE5CA1A7E00000000 + cfg, threads=16)
+bytes_k1 = s.pod_c.n_pods * 20 + s.pod_c.n_xc * 16 + s.pod_c.n_xp * 4 + ((s.pod_c.n_pods + 255) // 256) * 8
+ctxs = {}
+for v in variants:
+    os.environ["ESC_K1_VARIANT"] = str(v)
+    c = esc.Context(s)
+    c.load_synth(s, replicas=1 if cfg == 4 else 8)
+    c.set_state(s.states)
+    c.set_timing(True)
+    ctxs[v] = c
+res = {v: [] for v in variants}
+ref = None
+for r in range(rounds):
+    for v in variants:
+        c = ctxs[v]
+        for _ in range(5):
+            c.run()
+            c.sync()
+            res[v].append(c.stage_times()[0])
+        t, d = c.results()
+        if ref is None:
+            ref = (t.tobytes(), d.tobytes())
+        assert (t.tobytes(), d.tobytes()) == ref, "variant %d differs" % v
+out = {}
+for v in variants:
+    ms = np.array(res[v])
+    out[v] = {"median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
+              "GBps_median": bytes_k1 / (np.median(ms) * 1e-3) / 1e9}
+print(json.dumps({"config": cfg, "k1_bytes": int(bytes_k1), "variants": out}))

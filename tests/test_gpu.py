@@ -260,3 +260,33 @@ def test_determinism_repeat(esc):
         ctx.run()
         t1, d1 = ctx.results()
         assert t0.tobytes() == t1.tobytes() and d0.tobytes() == d1.tobytes()
+
+
+def test_big_tiles_and_window_edges(esc):
+    """Tiles with > 128 extra records (k_pod_bigtiles) and pods spilled to the wide path."""
+    groups = [{"name": "g%d" % i, "label_key": "k", "label_value": "v%d" % i, "max_nodes": 1000} for i in range(5)]
+    rng = random.Random(9)
+    pods = []
+    for i in range(1100):
+        n_c = 9 if 256 <= i < 512 else rng.choice([1, 2])          # tile 1 overflows the register chunks
+        sel = {"k": "v%d" % rng.randrange(5)}
+        expr = {"key": "k", "op": "In", "values": ["v%d" % j for j in range(5)]}
+        aff = {"node_affinity": {"required": [[expr]]}, "pod_affinity": False,
+               "pod_anti_affinity": False} if 600 <= i < 900 else None
+        pods.append({"containers": [{"cpu": rng.randrange(1, 5000), "mem": rng.randrange(1, 1 << 36)}
+                                    for _ in range(n_c)],
+                     "init_containers": [{"cpu": rng.randrange(1, 9000), "mem": None}] if i % 7 == 0 else [],
+                     "overhead": {"cpu": 7, "mem": 11} if i % 5 == 0 else None,
+                     "node_selector": sel, "affinity": aff})
+    nodes = [{"name": "n%d" % i, "labels": {"k": "v%d" % (i % 5)}, "cpu": 4000, "mem": 8 << 30,
+              "created_ns": i} for i in range(40)]
+    ctx = esc.Context(groups)
+    P, N = ctx.pack(pods, nodes)
+    ctx.load(P, N)
+    tot, dec = ctx.decide_all()
+    otot = soa.totals(P, N, groups)
+    odf, odi = soa.decide(groups, None, otot)
+    check_against_c_oracle(tot, dec, otot, odf, odi)
+    for g in range(5):
+        L = O.scale_node_group(groups[g], {}, pods, nodes)
+        assert (tot["pod_cpu_m"][g], tot["pod_mem_b"][g], tot["n_pods"][g]) == (L["pod_cpu_m"], L["pod_mem_b"], L["n_pods"])

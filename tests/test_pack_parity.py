@@ -107,9 +107,10 @@ def test_packer_encoding_details():
         {"owner_kinds": ["DaemonSet"], "containers": []},
     ]
     P, N = ctx.pack(pods, [])
-    # pod 0: pairs {a-head(1), c(3)} deduped across selector+affinity; pod-side head of (customer,a) is 1
-    assert P["pair0"][0] == 1 and list(P["xp_group"]) == [3]
-    assert (P["flags"][0] >> 24) & 63 == 1 and P["flags"][0] & 0b1100 == 0b1100
+    # pod 0: (customer,a) selects groups 1 and 2 (shared pair), (pool,p) group 3; deduped across
+    # selector + affinity; the default group (0) is never reached through a pair
+    assert P["pair0"][0] == 1 and list(P["xp_group"]) == [2, 3]
+    assert (P["flags"][0] >> 24) & 63 == 2 and P["flags"][0] & 0b1100 == 0b1100
     # pod 1: first container cpu does not fit u32 -> all regulars are extras; absent init cpu = INT64_MIN;
     # an overhead map with no keys adds nothing and is dropped
     assert P["cpu0"][1] == 0 and (P["flags"][1] >> 8) & 255 == 2 and (P["flags"][1] >> 16) & 255 == 1
