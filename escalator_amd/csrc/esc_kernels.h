@@ -49,8 +49,9 @@ struct GroupDev {
 enum WidePod : int { WP_CPU_LO = 0, WP_CPU_HI, WP_MEM_LO, WP_MEM_HI, WP_CNT, WP_K };
 enum WideNode : int { WN_CPU_LO = 0, WN_CPU_HI, WN_MEM_LO, WN_MEM_HI, WN_UNT, WN_TAINT, WN_CORD, WN_FIRST, WN_K };
 
-// variant: 0 = 512 threads + two-tile pipeline (default), 1 = 1024 threads, no pipeline,
-// 2 = 512 no pipeline, 3 = 1024 + pipeline (ESC_K1_VARIANT, for measurement).
+// variant (ESC_K1_VARIANT, measurement knob): 0 = 1024 threads, offsets prefetched (default),
+// 2 = 512 threads, 3 = 1024 + two-tile register pipeline, 4 = 512 + pipeline,
+// 9 = timing-only ablation of the LDS atomics (wrong results).
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st);
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,

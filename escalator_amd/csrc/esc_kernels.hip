@@ -179,9 +179,19 @@ __device__ __forceinline__ void tile_load(const PodDev& P, int64_t t, uint32_t l
 
 // Processes one tile whose extra records are all in registers (<= 128 of each kind):
 // shuffles only, no memory waits (see k_pod_reduce).
-__device__ __forceinline__ void process_tile_fast(const PodDev& P, const GroupDev& G, const PodLds& acc,
+template <int ABLATE = 0>
+__device__ __forceinline__ void process_tile_fast(const PodDev& P, const GroupDev& G, const PodLds& acc0,
                                                   const PodWide& spill, int32_t g0, uint32_t gw, uint32_t lane,
                                                   const PodTile& cur) {
+    // ABLATE (timing-only builds, wrong results): bit 0 replaces the LDS atomics by a
+    // register sink, bit 1 skips the container-record fold, bit 2 the extra-group adds.
+    struct Sink {
+        const PodLds& a;
+        __device__ __forceinline__ void add(uint32_t g, uint64_t vcc, uint64_t vmem) const {
+            if constexpr (ABLATE & 1) asm volatile("" :: "v"(g), "v"(vcc), "v"(vmem));
+            else a.add(g, vcc, vmem);
+        }
+    } acc{acc0};
     // ------------------------------------------------ process tile t
     const uint32_t fs[4] = {cur.f.x, cur.f.y, cur.f.z, cur.f.w};
     const uint32_t gs[4] = {cur.g.x, cur.g.y, cur.g.z, cur.g.w};
@@ -195,7 +205,7 @@ __device__ __forceinline__ void process_tile_fast(const PodDev& P, const GroupDe
         nxp += pf_xpair(fs[j]); xp_end[j] = nxp;
     }
     uint32_t oc = 0, op = 0;
-    if (__ballot((nxc | nxp) != 0)) {                  // wave-uniform
+    if ((ABLATE & 6) != 6 && __ballot((nxc | nxp) != 0)) {   // wave-uniform
         const uint64_t v = (uint64_t)nxc | ((uint64_t)nxp << 32);
         const uint64_t s = wave_incl_scan(v, (int)lane) - v;
         oc = (uint32_t)s;
@@ -203,7 +213,7 @@ __device__ __forceinline__ void process_tile_fast(const PodDev& P, const GroupDe
     }
     // ComputePodResourceRequest (types.go:72-89) over the extra records in record
     // order: regular extras add, then init containers max, then the overhead adds.
-    if (__ballot(nxc != 0)) {
+    if (!(ABLATE & 2) && __ballot(nxc != 0)) {
         const uint32_t kmax = wave_max(nxc);
         for (uint32_t k = 0; k < kmax; ++k) {
             const uint32_t rel = oc + k;
@@ -250,7 +260,7 @@ __device__ __forceinline__ void process_tile_fast(const PodDev& P, const GroupDe
             if (gs[j] != NONE && gs[j] - (uint32_t)g0 < gw) spill.add(gs[j], (int64_t)cpu[j], (int64_t)mem[j]);
         }
     }
-    if (__ballot(nxp != 0)) {
+    if (!(ABLATE & 4) && __ballot(nxp != 0)) {
         const uint32_t kmax = wave_max(nxp);
         for (uint32_t k = 0; k < kmax; ++k) {
             const uint32_t rel = op + k;
@@ -278,7 +288,7 @@ __device__ __forceinline__ void process_tile_fast(const PodDev& P, const GroupDe
 // Per wave a two-stage software pipeline: while tile t is processed, tile t+16's fixed
 // words and extra records are in flight, so the processing of a tile does not wait on
 // memory and each wave keeps ~5-10 KB of loads outstanding (80-160 KB per CU).
-template <int THREADS, bool PIPE>
+template <int THREADS, bool PIPE, int ABLATE = 0>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
                                                         int64_t* __restrict__ wide) {
@@ -304,19 +314,25 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
             if (t >= t_hi) break;
             int64_t t1 = t + NW;
             if (t1 < t_hi) tile_load(P, t1, lane, tile_bases(P, t1), B);
-            if (A.xcn <= 128 && A.xpn <= 128) process_tile_fast(P, G, acc, spill, g0, gw, lane, A);
+            if (A.xcn <= 128 && A.xpn <= 128) process_tile_fast<ABLATE>(P, G, acc, spill, g0, gw, lane, A);
             t = t1;
             if (t >= t_hi) break;
             t1 = t + NW;
             if (t1 < t_hi) tile_load(P, t1, lane, tile_bases(P, t1), A);
-            if (B.xcn <= 128 && B.xpn <= 128) process_tile_fast(P, G, acc, spill, g0, gw, lane, B);
+            if (B.xcn <= 128 && B.xpn <= 128) process_tile_fast<ABLATE>(P, G, acc, spill, g0, gw, lane, B);
             t = t1;
         }
     } else {
-        for (; t < t_hi; t += NW) {                       // latency hidden across waves only
+        // Latency hidden across the 16 waves; the next tile's record offsets (scalar
+        // registers, s_load) are fetched one tile ahead so the tile's words and its extra
+        // records are issued together.
+        TileBases nb{0, 0, 0, 0};
+        if (t < t_hi) nb = tile_bases(P, t);
+        for (; t < t_hi; t += NW) {
             PodTile A;
-            tile_load(P, t, lane, tile_bases(P, t), A);
-            if (A.xcn <= 128 && A.xpn <= 128) process_tile_fast(P, G, acc, spill, g0, gw, lane, A);
+            tile_load(P, t, lane, nb, A);
+            if (t + NW < t_hi) nb = tile_bases(P, t + NW);
+            if (A.xcn <= 128 && A.xpn <= 128) process_tile_fast<ABLATE>(P, G, acc, spill, g0, gw, lane, A);
         }
     }
     __syncthreads();
@@ -783,10 +799,16 @@ hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int
                              uint64_t* part, int64_t* wide, hipStream_t st) {
     const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
     switch (variant) {
-        case 1: hipLaunchKernelGGL((k_pod_reduce<1024, false>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
         case 2: hipLaunchKernelGGL((k_pod_reduce<512, false>), dim3(nblk), dim3(512), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
         case 3: hipLaunchKernelGGL((k_pod_reduce<1024, true>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
-        default: hipLaunchKernelGGL((k_pod_reduce<512, true>), dim3(nblk), dim3(512), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        case 4: hipLaunchKernelGGL((k_pod_reduce<512, true>), dim3(nblk), dim3(512), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        // Timing-only ablations (wrong results; scripts/k1_variants.py): see process_tile_fast.
+        case 9: hipLaunchKernelGGL((k_pod_reduce<1024, false, 1>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        case 10: hipLaunchKernelGGL((k_pod_reduce<1024, false, 2>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        case 11: hipLaunchKernelGGL((k_pod_reduce<1024, false, 4>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        case 12: hipLaunchKernelGGL((k_pod_reduce<1024, false, 6>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        case 13: hipLaunchKernelGGL((k_pod_reduce<1024, false, 7>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        default: hipLaunchKernelGGL((k_pod_reduce<1024, false>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
     }
     return hipGetLastError();
 }

@@ -212,7 +212,7 @@ int32_t ensure_work(esc_ctx* c) {
     const int32_t G = c->gi.G;
     const int gw = std::min(G, POD_WINDOW_MAX);
     const int lds = gw * 16;
-    const int max_blocks = (c->k1_variant == 1 || c->k1_variant == 3) ? 2 : 4;   // 2048 threads per CU
+    const int max_blocks = (c->k1_variant == 2 || c->k1_variant == 4) ? 4 : 2;   // 2048 threads per CU
     const int per_cu = std::max(1, std::min(max_blocks, LDS_BYTES / std::max(lds, 1)));
     int nblk = c->cu_count * per_cu;
     const int64_t pods_per_block = (c->n_tiles * TILE + nblk - 1) / std::max(nblk, 1);
