@@ -34,17 +34,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pod_bytes(p) -> int:
-    """Algorithmic bytes K1 streams per launch: the shard's packed arrays, each read once
-    (flags 4 + cpu0 4 + mem0 8 + pair0 4 per pod, 16 per extra container record, 4 per
-    extra pair, 8 per 256-pod tile of extra offsets)."""
-    n = int(p.n_pods)
-    return n * 20 + int(p.n_xc) * 16 + int(p.n_xp) * 4 + ((n + 255) // 256) * 8
+def pod_bytes(s) -> int:
+    """Algorithmic bytes K1 streams per launch (escalator_amd/layout.py)."""
+    from escalator_amd import layout
+    return layout.pod_bytes(s.pods()["flags"], s.pod_c.n_xc, s.pod_c.n_xp)
 
 
 def node_bytes(nc, lo, hi) -> int:
-    """K2: flags 4 + label0 4 + cpu 8 + mem 8 (+ offsets of extra labels 4) per node streamed."""
-    return (hi - lo) * 28 + int(nc.n_xl) * 4
+    """K2: flags 4 + label0 4 + cpu 8 + mem 8 per node streamed (+ extra label pairs)."""
+    from escalator_amd import layout
+    return layout.node_bytes(hi - lo, nc.n_xl)
 
 
 def cpu_baseline(cfg, G, seconds=12.0):
@@ -109,7 +108,7 @@ def main():
     nlo, nhi = shard_range(N, rank, world)
     t0 = time.time()
     s = esc.Synth(P, N, G, config=args.config, seed=0xE5CA1A7E00000000 + args.config, p_lo=lo, p_hi=hi, threads=16)
-    shard_bytes = pod_bytes(s.pod_c)
+    shard_bytes = pod_bytes(s)
     replicas = int(max(1, min(8, -(-1_000_000_000 // max(shard_bytes, 1)))))   # >= 1 GB resident: HBM-served
     ctx = esc.Context(s, device=local, rank=rank, world=world)
     ctx.load_synth(s, pod_offset=lo, node_lo=nlo, node_hi=nhi, replicas=replicas)
@@ -180,11 +179,11 @@ def main():
             dist.destroy_process_group()
         return
 
-    algo = pod_bytes(s.pod_c)
+    algo = pod_bytes(s)
     achieved = algo / (k1_ms * 1e-3) / 1e9
     records = P + N
     value = records * args.steps / elapsed
-    decision_bytes = (pod_bytes(s.pod_c) + node_bytes(s.node_c, nlo, nhi)) * world
+    decision_bytes = (pod_bytes(s) + node_bytes(s.node_c, nlo, nhi)) * world
     out = {
         "metric": "pod+node records evaluated/sec per scale decision & % HBM peak, 1/2/4/8 GPUs",
         "value": value,

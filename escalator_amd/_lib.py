@@ -85,12 +85,12 @@ class NodeObj(C.Structure):
 class PodSoA(C.Structure):
     _fields_ = [("n_pods", i64), ("flags", P(u32)), ("cpu0", P(u32)), ("mem0", P(i64)),
                 ("pair0", P(u32)), ("xc_cpu", P(i64)), ("xc_mem", P(i64)), ("n_xc", i64),
-                ("xp_group", P(u32)), ("n_xp", i64)]
+                ("xp_pair", P(u32)), ("n_xp", i64)]
 
 
 class NodeSoA(C.Structure):
     _fields_ = [("n_nodes", i64), ("flags", P(u32)), ("label0", P(u32)), ("cpu", P(i64)),
-                ("mem", P(i64)), ("created_ns", P(i64)), ("xl_group", P(u32)), ("n_xl", i64),
+                ("mem", P(i64)), ("created_ns", P(i64)), ("xl_pair", P(u32)), ("n_xl", i64),
                 ("trk_node", P(i32)), ("trk_group", P(i32)), ("n_trk", i64)]
 
 
@@ -109,7 +109,8 @@ _SIGS = {
     "esc_ctx_destroy": (i32, [VP]),
     "esc_ctx_set_stream": (i32, [VP, VP]),
     "esc_ctx_num_groups": (i32, [VP]),
-    "esc_ctx_pair_head": (u32, [VP, cstr, cstr, i32]),
+    "esc_ctx_pair_id": (u32, [VP, cstr, cstr]),
+    "esc_ctx_num_group_pairs": (i32, [VP]),
     "esc_packer_create": (i32, [VP, P(VP)]),
     "esc_packer_destroy": (i32, [VP]),
     "esc_packer_add_pods": (i32, [VP, P(PodObj), i64]),
@@ -165,6 +166,13 @@ def load():
         if not os.path.exists(LIB_PATH):
             raise ImportError("escalator_amd: %s is missing — run __graft_entry__.build() "
                               "(make -C escalator_amd/csrc); there is no CPU fallback" % LIB_PATH)
+        # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64, so when torch
+        # is installed it is loaded first and the library binds to that runtime (loading
+        # /opt/rocm's first and torch's second leaves two runtimes that disagree on devices).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(lib, name)

@@ -24,9 +24,9 @@ assert DECISION_DTYPE.itemsize == C.sizeof(L.GroupDecision)
 
 _POD_FIELDS = [("flags", np.uint32, "n_pods"), ("cpu0", np.uint32, "n_pods"), ("mem0", np.int64, "n_pods"),
                ("pair0", np.uint32, "n_pods"), ("xc_cpu", np.int64, "n_xc"), ("xc_mem", np.int64, "n_xc"),
-               ("xp_group", np.uint32, "n_xp")]
+               ("xp_pair", np.uint32, "n_xp")]
 _NODE_FIELDS = [("flags", np.uint32, "n_nodes"), ("label0", np.uint32, "n_nodes"), ("cpu", np.int64, "n_nodes"),
-                ("mem", np.int64, "n_nodes"), ("created_ns", np.int64, "n_nodes"), ("xl_group", np.uint32, "n_xl"),
+                ("mem", np.int64, "n_nodes"), ("created_ns", np.int64, "n_nodes"), ("xl_pair", np.uint32, "n_xl"),
                 ("trk_node", np.int32, "n_trk"), ("trk_group", np.int32, "n_trk")]
 
 
@@ -54,11 +54,11 @@ def _soa_from(arrays: dict, fields, struct_t, count_names):
 
 def pod_soa(arrays: dict):
     return _soa_from(arrays, _POD_FIELDS, L.PodSoA, {"n_pods": len(arrays["flags"]), "n_xc": len(arrays["xc_cpu"]),
-                                                      "n_xp": len(arrays["xp_group"])})
+                                                      "n_xp": len(arrays["xp_pair"])})
 
 
 def node_soa(arrays: dict):
-    return _soa_from(arrays, _NODE_FIELDS, L.NodeSoA, {"n_nodes": len(arrays["flags"]), "n_xl": len(arrays["xl_group"]),
+    return _soa_from(arrays, _NODE_FIELDS, L.NodeSoA, {"n_nodes": len(arrays["flags"]), "n_xl": len(arrays["xl_pair"]),
                                                         "n_trk": len(arrays["trk_node"])})
 
 

@@ -17,8 +17,10 @@
 namespace esc {
 
 constexpr uint32_t NONE = ESC_NONE;
-constexpr int TILE = 256;                 // pods per wave iteration: 64 lanes x 4 pods
+constexpr int TILE = 256;                 // S tile: 64 lanes x 4 pods
 constexpr int PODS_PER_LANE = 4;
+constexpr int CTILE = 64;                 // C tile: 64 lanes x 1 pod
+constexpr uint32_t CODE_MULTI = 0x80000000u;   // pair code: offset of a [count, g...] list
 
 // Fast-path packing ranges.  A record outside them is spilled by the
 // same kernel to the exact "wide" global accumulators, so every input stays exact.

@@ -17,19 +17,23 @@ struct GroupSpecCopy {
     esc_group_spec spec;   // string pointers re-pointed at the members above
 };
 
-// (key,value) interning against the configured groups.  Each group selects exactly one
-// (label_key, label_value) pair (node_group.go:290-303), so a pair maps to the set of
-// groups sharing it.  The set is stored as a chain: head = lowest-index group with the
-// pair, next[g] = next higher-index group with the same pair.  Pods use the chain that
-// excludes the "default" group (its pods come from NewPodDefaultFilterFunc instead,
-// client.go:58-64); nodes use the chain over all groups (node_group.go:301).
+// The groups' selector pairs and the pair -> groups tables the kernels resolve.
+// Each group selects exactly one (label_key, label_value) pair (node_group.go:290-303);
+// pair ids 0 .. n_gp-1 are the distinct group pairs in order of first appearance
+// (the numbering rule of include/escalator_hip.h).  A pair may be shared by several
+// groups, so each node-table entry is a "code": a single group id, NONE, or
+// CODE_MULTI | offset of a [count, g...] list in `code_list` (node_group.go:301).
+// Pods are accumulated per pair and joined to groups through `gpair` (the "default"
+// group takes its pods from NewPodDefaultFilterFunc instead, client.go:58-64).
 struct GroupIndex {
     int32_t G = 0;
     int32_t default_group = -1;
     std::vector<GroupSpecCopy> groups;
-    std::unordered_map<std::string, uint32_t> pod_head, node_head;
-    std::vector<uint32_t> pod_next, node_next;
-    bool pod_chains = false, node_chains = false;
+    std::unordered_map<std::string, uint32_t> pair_ids;   // group pair -> id
+    std::unordered_map<std::string, int> keys;            // label keys some group uses
+    uint32_t n_gp = 0;
+    std::vector<uint32_t> gpair;                          // group -> pair id
+    std::vector<uint32_t> node_code, code_list;
 
     static std::string pair_key(const char* k, const char* v) {
         std::string s(k ? k : "");
@@ -38,11 +42,11 @@ struct GroupIndex {
         return s;
     }
     void build(const esc_group_spec* specs, int32_t n);
-    uint32_t head(const char* k, const char* v, int side) const {
-        const auto& m = side == 0 ? pod_head : node_head;
-        auto it = m.find(pair_key(k, v));
-        return it == m.end() ? NONE : it->second;
+    uint32_t pair_id(const char* k, const char* v) const {
+        auto it = pair_ids.find(pair_key(k, v));
+        return it == pair_ids.end() ? NONE : it->second;
     }
+    bool is_key(const char* k) const { return keys.count(std::string(k ? k : "")) != 0; }
 };
 
 // Host-side packed snapshot (owned vectors) produced by the packer or the generator.

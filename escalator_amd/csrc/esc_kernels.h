@@ -8,8 +8,11 @@
 
 namespace esc {
 
-// Device view of a pod shard (arrays padded to a whole number of 256-pod tiles; the
-// padding pods carry ESC_PF_DAEMONSET so every filter rejects them).
+// Device view of a pod shard.  Two sections of the same arrays: pods without extra
+// records ("simple": one container, at most one selector pair) in 256-pod S tiles
+// (4 per lane), then the others in 64-pod C tiles (1 per lane) whose extra records are
+// contiguous per tile.  The split is a stable partition made at load (esc_load_pods);
+// sums are order-independent.  Padding pods carry ESC_PF_DAEMONSET.
 struct PodDev {
     const uint32_t* flags;
     const uint32_t* cpu0;
@@ -18,9 +21,10 @@ struct PodDev {
     const int64_t*  xc_cpu;
     const int64_t*  xc_mem;
     const uint32_t* xp;
-    const uint32_t* xc_base;   // [n_tiles + 1] extra-container offset of each tile's first pod
-    const uint32_t* xp_base;   // [n_tiles + 1] extra-group offset
-    int64_t n_tiles;
+    const uint32_t* xc_base;   // [c_tiles + 1] extra-container offset of each C tile
+    const uint32_t* xp_base;   // [c_tiles + 1] extra-pair offset
+    int64_t s_tiles;           // S section: pods [0, s_tiles * 256)
+    int64_t c_tiles;           // C section: pods [s_tiles * 256, + c_tiles * 64)
 };
 
 // Device view of the node table; this rank streams nodes [lo, hi).
@@ -41,6 +45,10 @@ struct NodeDev {
 struct GroupDev {
     const uint8_t*  dry;
     const GroupParams* params;
+    const uint32_t* gpair;     // [G] group -> its pair id (K3 joins pod slots to groups)
+    const uint32_t* node_code; // [n_gp] pair id -> group code for nodes
+    const uint32_t* code_list; // CODE_MULTI lists: [count, g...]
+    uint32_t n_gp;             // pod slots: pair ids [0, n_gp) + the default filter's slot n_gp
     int32_t G;
     uint32_t default_group;    // NONE when no group is named "default"
 };
@@ -49,11 +57,11 @@ struct GroupDev {
 enum WidePod : int { WP_CPU_LO = 0, WP_CPU_HI, WP_MEM_LO, WP_MEM_HI, WP_CNT, WP_K };
 enum WideNode : int { WN_CPU_LO = 0, WN_CPU_HI, WN_MEM_LO, WN_MEM_HI, WN_UNT, WN_TAINT, WN_CORD, WN_FIRST, WN_K };
 
-// variant (ESC_K1_VARIANT, measurement knob): 0 = 1024 threads, offsets prefetched (default),
-// 2 = 512 threads, 3 = 1024 + two-tile register pipeline, 4 = 512 + pipeline,
-// 9 = timing-only ablation of the LDS atomics (wrong results).
+// variant (ESC_K1_VARIANT, measurement knob): 0 = 1024 threads (default), 2 = 512 threads,
+// 9.. = timing-only ablations (wrong results, scripts/k1_variants.py).
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st);
+hipError_t launch_zero(int64_t* p, int64_t n, hipStream_t st);
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
                                int64_t* wide, hipStream_t st);
 hipError_t launch_node_reduce(const NodeDev& n, const GroupDev& g, int n_chunk, int gt,

@@ -18,16 +18,15 @@
 // Wide variants      : exact any-range fallback with global atomics.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "esc_kernels.h"
 
 namespace esc {
 
 namespace {
 
-constexpr int BLOCK = 1024;          // 16 waves per workgroup (node reduce)
-constexpr int WAVES = BLOCK / 64;
-constexpr int POD_BLOCK = 512;       // K1: 8 waves, 256-VGPR budget for two tiles in flight
-constexpr int POD_WAVES = POD_BLOCK / 64;
+constexpr int BLOCK = 1024;          // 16 waves per workgroup
 
 __device__ __forceinline__ uint4 ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ ulonglong2 ld2(const int64_t* p) {
@@ -62,18 +61,55 @@ __device__ __forceinline__ void pod_request(uint32_t f, uint32_t cpu0, int64_t m
     mem = (int64_t)m;
 }
 
-// Wave-inclusive scan of a 64-bit value (two packed u32 counters).
-__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v0, int lane) {
-    unsigned long long v = v0;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        unsigned long long y = __shfl_up(v, (unsigned)d, 64);
-        if (lane >= d) v += y;
-    }
-    return (uint64_t)v;
+// ------------------------------------------------------------- wave primitives
+// DPP lane movement (no LDS traffic).  Out-of-row sources and masked rows read 0.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+
+// Inclusive prefix sum over the wave's 64 lanes: row_shr 1/2/4/8 inside each 16-lane
+// row, then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry row totals.
+__device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
+    v += dpp<0x111, 0xF>(v);
+    v += dpp<0x112, 0xF>(v);
+    v += dpp<0x114, 0xF>(v);
+    v += dpp<0x118, 0xF>(v);
+    v += dpp<0x142, 0xA>(v);
+    v += dpp<0x143, 0xC>(v);
+    return v;
+}
+
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
+
+__device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int src) {
+    return __shfl(v, src, 64);
 }
 
 __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
+
+// ------------------------------------------------------- selector-pair matching
+// NewPodAffinityFilterFunc / NewNodeLabelFilterFunc (node_group.go:218, :278) for all
+// groups at once: a pair id selects the groups whose (label_key, label_value) it is;
+// ids >= n_gp are values no group selects.
+//  - pods: K1 accumulates per pair (LDS slot = pair id, plus one slot for the default
+//    filter) and K3 joins each group to its pair's slot — the per-pod test
+//    "(K_g, V_g) in pod pairs" evaluated for every group without a per-pod lookup;
+//  - nodes: K2 resolves each label pair through the node code table (a group id, NONE,
+//    or a list of the groups sharing the pair), since node classes depend on the group.
+__device__ __forceinline__ uint32_t node_code(const GroupDev& G, uint32_t pair) {
+    return pair < G.n_gp ? G.node_code[pair] : NONE;
+}
+template <class F>
+__device__ __forceinline__ void for_code(const GroupDev& G, uint32_t code, F&& emit) {
+    if (code < CODE_MULTI) {
+        emit(code);
+    } else if (code != NONE) {                       // groups sharing one pair (rare)
+        const uint32_t* l = G.code_list + (code & ~CODE_MULTI);
+        const uint32_t n = l[0];
+        for (uint32_t k = 1; k <= n; ++k) emit(l[k]);
+    }
+}
 
 // ------------------------------------------------------------- accumulators
 struct PodLds {          // fast path: LDS partials of a group window
@@ -99,46 +135,71 @@ struct PodWide {         // exact path: global int64 words, values split lo32/hi
     }
 };
 
-// Per-group membership of one pod — NewPodAffinityFilterFunc (node_group.go:218) for
-// every labelled group (the packed list names each selecting group), and
-// NewPodDefaultFilterFunc (:256) for the default group.  Daemonset pods never reach here.
-template <class F>
-__device__ __forceinline__ void pod_groups(uint32_t f, uint32_t g, const uint32_t* __restrict__ xp,
-                                           uint32_t& q, const GroupDev& G, F&& emit) {
-    if (pf_default_ok(f) && G.default_group != NONE) emit(G.default_group);
-    if (g != NONE) emit(g);
-    for (uint32_t k = pf_xpair(f); k; --k) emit(xp[q++]);
-}
-
-__device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int src) {
-    return __shfl(v, src, 64);
-}
-
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) { const uint32_t o = __shfl_xor(v, d, 64); v = o > v ? o : v; }
-    return v;
-}
-
-// One wave's 256-pod tile in registers: the fixed per-pod words (16 B per lane per array)
-// and the tile's extra records, which are contiguous ([xc_base[t], xc_base[t+1])) and so
-// are fetched coalesced, lane l holding records l and l+64, before the tile is processed.
-struct PodTile {
-    uint4 f, c, g;
-    ulonglong2 m01, m23;
-    unsigned long long xcc0, xcm0, xcc1, xcm1;
-    uint32_t xp0, xp1;
-    uint32_t xcb, xcn, xpb, xpn;
+// One pod's contribution to pod slot `g` (a pair id, or n_gp for the default filter):
+// LDS when the effective request is inside the packed range, else the exact wide words
+// (only for slots of this launch's window).
+// ABLATE bit 0 (timing-only builds, wrong results) replaces the LDS atomics by a sink.
+template <int ABLATE>
+struct PodSink {
+    PodLds acc;
+    PodWide spill;
+    __device__ __forceinline__ void add(uint32_t g, uint64_t cpu, uint64_t mem, bool in) const {
+        if (in) {
+            if constexpr (ABLATE & 1) asm volatile("" :: "v"(g), "v"(cpu), "v"(mem));
+            else acc.add(g, cpu | (1ull << CNT_SHIFT), mem);
+        } else if (g - (uint32_t)acc.g0 < acc.gw) {
+            spill.add(g, (int64_t)cpu, (int64_t)mem);
+        }
+    }
 };
 
+__device__ __forceinline__ bool in_range(uint64_t cpu, uint64_t mem) {
+    return cpu < (uint64_t)POD_CPU_LIMIT && mem < (uint64_t)POD_MEM_LIMIT;
+}
+
+// ------------------------------------------------------------------ S tiles
+// 256 simple pods per wave, 4 per lane, 16-B loads per lane per array (20 B/pod).
+struct STile {
+    uint4 f, c, p;
+    ulonglong2 m01, m23;
+};
+// (S tiles are pods with one container and at most one selector pair.)
+
+__device__ __forceinline__ void s_load(const PodDev& P, int64_t t, uint32_t lane, STile& T) {
+    const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
+    T.f = ld4(P.flags + p0);
+    T.c = ld4(P.cpu0 + p0);
+    T.m01 = ld2(P.mem0 + p0);
+    T.m23 = ld2(P.mem0 + p0 + 2);
+    T.p = ld4(P.pair0 + p0);
+}
+
+template <int ABLATE>
+__device__ __forceinline__ void s_process(const GroupDev& G, const PodSink<ABLATE>& K, const STile& T) {
+    const uint32_t fs[4] = {T.f.x, T.f.y, T.f.z, T.f.w};
+    const uint32_t ps[4] = {T.p.x, T.p.y, T.p.z, T.p.w};
+    const uint64_t cpu[4] = {T.c.x, T.c.y, T.c.z, T.c.w};
+    const uint64_t mem[4] = {T.m01.x, T.m01.y, T.m23.x, T.m23.y};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        if (fs[j] & ESC_PF_DAEMONSET) continue;                      // node_group.go:221, :259
+        const bool in = in_range(cpu[j], mem[j]);
+        if (pf_default_ok(fs[j]) && G.default_group != NONE) K.add(G.n_gp, cpu[j], mem[j], in);
+        if (ps[j] < G.n_gp) K.add(ps[j], cpu[j], mem[j], in);
+    }
+}
+
+// ------------------------------------------------------------------ C tiles
+// 64 pods with extra records per wave, one per lane.  The tile's records are contiguous
+// ([xc_base[t], xc_base[t+1])), fetched coalesced (lane l holds records l and l+64) and
+// handed to their pods with ds_bpermute; tiles with more than 128 records of a kind are
+// listed at load and left to k_pod_bigtiles.
 struct TileBases {
     uint32_t xcb, xcn, xpb, xpn;
 };
 
 typedef __attribute__((address_space(4))) const uint32_t cu32;   // constant: scalar loads
 
-// Offsets of a tile's extra records: wave-uniform, fetched with s_load so they never
-// sit in the vector-memory queue in front of the tile data.
 __device__ __forceinline__ TileBases tile_bases(const PodDev& P, int64_t t) {
     const cu32* xc = (const cu32*)P.xc_base;
     const cu32* xp = (const cu32*)P.xp_base;
@@ -150,242 +211,178 @@ __device__ __forceinline__ TileBases tile_bases(const PodDev& P, int64_t t) {
     return b;
 }
 
-__device__ __forceinline__ void tile_load(const PodDev& P, int64_t t, uint32_t lane, const TileBases& b,
-                                          PodTile& T) {
-    const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
-    T.xcb = b.xcb; T.xcn = b.xcn; T.xpb = b.xpb; T.xpn = b.xpn;
-    T.f = ld4(P.flags + p0);
-    T.c = ld4(P.cpu0 + p0);
-    T.m01 = ld2(P.mem0 + p0);
-    T.m23 = ld2(P.mem0 + p0 + 2);
-    T.g = ld4(P.pair0 + p0);
+struct CTile {
+    uint32_t f, c, p;
+    uint64_t m;
+    unsigned long long xcc0, xcm0, xcc1, xcm1;
+    uint32_t xp0, xp1;
+    TileBases b;
+};
+
+__device__ __forceinline__ void c_load(const PodDev& P, int64_t t, uint32_t lane, const TileBases& b, CTile& T) {
+    const int64_t i = P.s_tiles * TILE + t * CTILE + lane;
+    T.b = b;
+    T.f = P.flags[i];
+    T.c = P.cpu0[i];
+    T.m = (uint64_t)P.mem0[i];
+    T.p = P.pair0[i];
     T.xcc0 = T.xcm0 = T.xcc1 = T.xcm1 = 0;
     T.xp0 = T.xp1 = NONE;
-    if (lane < T.xcn) {
-        T.xcc0 = (unsigned long long)P.xc_cpu[T.xcb + lane];
-        T.xcm0 = (unsigned long long)P.xc_mem[T.xcb + lane];
+    if (lane < b.xcn) {
+        T.xcc0 = (unsigned long long)P.xc_cpu[b.xcb + lane];
+        T.xcm0 = (unsigned long long)P.xc_mem[b.xcb + lane];
     }
-    if (lane + 64 < T.xcn) {
-        T.xcc1 = (unsigned long long)P.xc_cpu[T.xcb + 64 + lane];
-        T.xcm1 = (unsigned long long)P.xc_mem[T.xcb + 64 + lane];
+    if (lane + 64 < b.xcn) {
+        T.xcc1 = (unsigned long long)P.xc_cpu[b.xcb + 64 + lane];
+        T.xcm1 = (unsigned long long)P.xc_mem[b.xcb + 64 + lane];
     }
-    if (lane < T.xpn) T.xp0 = P.xp[T.xpb + lane];
-    if (lane + 64 < T.xpn) T.xp1 = P.xp[T.xpb + 64 + lane];
+    if (lane < b.xpn) T.xp0 = P.xp[b.xpb + lane];
+    if (lane + 64 < b.xpn) T.xp1 = P.xp[b.xpb + 64 + lane];
 }
 
-// Runs `body` for pod j of the lane's four with a compile-time index (registers, no scratch).
-#define ESC_FOR_POD(j, ...) \
-    _Pragma("unroll") for (int jj_ = 0; jj_ < 4; ++jj_) if (jj_ == (int)(j)) { __VA_ARGS__; }
+template <int ABLATE>
+__device__ __forceinline__ void c_process(const GroupDev& G, const PodSink<ABLATE>& K, const CTile& T) {
+    const uint32_t f = T.f;
+    const uint32_t nxc = pf_xctr(f), nxp = pf_xpair(f);
+    const uint32_t v = nxc | (nxp << 16);                 // tile totals <= 128 each
+    const uint32_t ex = wave_incl_scan32(v) - v;
+    const uint32_t oc = ex & 0xFFFF, op = ex >> 16;
+    // ComputePodResourceRequest (types.go:72-89) over the pod's records in order:
+    // regular extras add, init containers max, the overhead adds.
+    uint64_t cpu = T.c, mem = T.m;
+    const uint32_t nreg = pf_xreg(f), add_from = nreg + pf_xinit(f);
+    for (uint32_t k = 0; wave_any(k < nxc); ++k) {
+        const uint32_t rel = oc + k;
+        unsigned long long c = shfl64(T.xcc0, (int)(rel & 63));
+        unsigned long long m = shfl64(T.xcm0, (int)(rel & 63));
+        if (T.b.xcn > 64) {                               // wave-uniform
+            const unsigned long long c1 = shfl64(T.xcc1, (int)(rel & 63));
+            const unsigned long long m1 = shfl64(T.xcm1, (int)(rel & 63));
+            if (rel >= 64) { c = c1; m = m1; }
+        }
+        if (k < nxc) {
+            if (k < nreg || k >= add_from) {
+                cpu += c;
+                mem += m;
+            } else {
+                cpu = ((int64_t)cpu >= (int64_t)c) ? cpu : c;
+                mem = ((int64_t)mem >= (int64_t)m) ? mem : m;
+            }
+        }
+    }
+    const bool live = !(f & ESC_PF_DAEMONSET);            // node_group.go:221, :259
+    const bool in = in_range(cpu, mem);
+    if (live) {
+        if (pf_default_ok(f) && G.default_group != NONE) K.add(G.n_gp, cpu, mem, in);
+        if (T.p < G.n_gp) K.add(T.p, cpu, mem, in);
+    }
+    for (uint32_t k = 0; wave_any(k < nxp); ++k) {
+        const uint32_t rel = op + k;
+        uint32_t q = __shfl(T.xp0, (int)(rel & 63), 64);
+        if (T.b.xpn > 64) {
+            const uint32_t q1 = __shfl(T.xp1, (int)(rel & 63), 64);
+            if (rel >= 64) q = q1;
+        }
+        if (live && k < nxp && q < G.n_gp) K.add(q, cpu, mem, in);
+    }
+}
 
-// Processes one tile whose extra records are all in registers (<= 128 of each kind):
-// shuffles only, no memory waits (see k_pod_reduce).
-template <int ABLATE = 0>
-__device__ __forceinline__ void process_tile_fast(const PodDev& P, const GroupDev& G, const PodLds& acc0,
-                                                  const PodWide& spill, int32_t g0, uint32_t gw, uint32_t lane,
-                                                  const PodTile& cur) {
-    // ABLATE (timing-only builds, wrong results): bit 0 replaces the LDS atomics by a
-    // register sink, bit 1 skips the container-record fold, bit 2 the extra-group adds.
-    struct Sink {
-        const PodLds& a;
-        __device__ __forceinline__ void add(uint32_t g, uint64_t vcc, uint64_t vmem) const {
-            if constexpr (ABLATE & 1) asm volatile("" :: "v"(g), "v"(vcc), "v"(vmem));
-            else a.add(g, vcc, vmem);
-        }
-    } acc{acc0};
-    // ------------------------------------------------ process tile t
-    const uint32_t fs[4] = {cur.f.x, cur.f.y, cur.f.z, cur.f.w};
-    const uint32_t gs[4] = {cur.g.x, cur.g.y, cur.g.z, cur.g.w};
-    uint64_t cpu[4] = {cur.c.x, cur.c.y, cur.c.z, cur.c.w};
-    uint64_t mem[4] = {cur.m01.x, cur.m01.y, cur.m23.x, cur.m23.y};
-    uint32_t xc_end[4], xp_end[4];
-    uint32_t nxc = 0, nxp = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        nxc += pf_xctr(fs[j]); xc_end[j] = nxc;
-        nxp += pf_xpair(fs[j]); xp_end[j] = nxp;
-    }
-    uint32_t oc = 0, op = 0;
-    if ((ABLATE & 6) != 6 && __ballot((nxc | nxp) != 0)) {   // wave-uniform
-        const uint64_t v = (uint64_t)nxc | ((uint64_t)nxp << 32);
-        const uint64_t s = wave_incl_scan(v, (int)lane) - v;
-        oc = (uint32_t)s;
-        op = (uint32_t)(s >> 32);
-    }
-    // ComputePodResourceRequest (types.go:72-89) over the extra records in record
-    // order: regular extras add, then init containers max, then the overhead adds.
-    if (!(ABLATE & 2) && __ballot(nxc != 0)) {
-        const uint32_t kmax = wave_max(nxc);
-        for (uint32_t k = 0; k < kmax; ++k) {
-            const uint32_t rel = oc + k;
-            unsigned long long c = shfl64(cur.xcc0, (int)(rel & 63));
-            unsigned long long m = shfl64(cur.xcm0, (int)(rel & 63));
-            if (cur.xcn > 64) {                        // wave-uniform
-                const unsigned long long c1 = shfl64(cur.xcc1, (int)(rel & 63));
-                const unsigned long long m1 = shfl64(cur.xcm1, (int)(rel & 63));
-                if (rel >= 64) { c = c1; m = m1; }
-            }
-            if (k < nxc) {
-                const uint32_t j = (k >= xc_end[0]) + (k >= xc_end[1]) + (k >= xc_end[2]);
-                ESC_FOR_POD(j, {
-                    const uint32_t q = k - (jj_ ? xc_end[jj_ - 1] : 0u);
-                    const uint32_t nreg = pf_xreg(fs[jj_]), ninit = pf_xinit(fs[jj_]);
-                    if (q < nreg || q >= nreg + ninit) {
-                        cpu[jj_] += c;
-                        mem[jj_] += m;
-                    } else {
-                        cpu[jj_] = ((int64_t)cpu[jj_] >= (int64_t)c) ? cpu[jj_] : c;
-                        mem[jj_] = ((int64_t)mem[jj_] >= (int64_t)m) ? mem[jj_] : m;
-                    }
-                });
-            }
-        }
-    }
-    // Memberships: default group + listed groups; daemonsets excluded (node_group.go:221,259).
-    uint32_t live = 0, ok = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const bool ds = fs[j] & ESC_PF_DAEMONSET;
-        const bool in = cpu[j] < (uint64_t)POD_CPU_LIMIT && mem[j] < (uint64_t)POD_MEM_LIMIT;
-        live |= (ds ? 0u : 1u) << j;
-        ok |= (in ? 1u : 0u) << j;
-        if (ds) continue;
-        const bool dflt = pf_default_ok(fs[j]) && G.default_group != NONE;
-        if (in) {
-            const uint64_t vcc = cpu[j] | (1ull << CNT_SHIFT);
-            if (dflt) acc.add(G.default_group, vcc, mem[j]);
-            if (gs[j] != NONE) acc.add(gs[j], vcc, mem[j]);
-        } else {                                       // outside the packed range: exact spill
-            if (dflt && G.default_group - (uint32_t)g0 < gw)
-                spill.add(G.default_group, (int64_t)cpu[j], (int64_t)mem[j]);
-            if (gs[j] != NONE && gs[j] - (uint32_t)g0 < gw) spill.add(gs[j], (int64_t)cpu[j], (int64_t)mem[j]);
-        }
-    }
-    if (!(ABLATE & 4) && __ballot(nxp != 0)) {
-        const uint32_t kmax = wave_max(nxp);
-        for (uint32_t k = 0; k < kmax; ++k) {
-            const uint32_t rel = op + k;
-            uint32_t g = __shfl(cur.xp0, (int)(rel & 63), 64);
-            if (cur.xpn > 64) {
-                const uint32_t g1 = __shfl(cur.xp1, (int)(rel & 63), 64);
-                if (rel >= 64) g = g1;
-            }
-            if (k < nxp) {
-                const uint32_t j = (k >= xp_end[0]) + (k >= xp_end[1]) + (k >= xp_end[2]);
-                ESC_FOR_POD(j, {
-                    if (live & (1u << jj_)) {
-                        if (ok & (1u << jj_)) acc.add(g, cpu[jj_] | (1ull << CNT_SHIFT), mem[jj_]);
-                        else if (g - (uint32_t)g0 < gw) spill.add(g, (int64_t)cpu[jj_], (int64_t)mem[jj_]);
-                    }
-                });
-            }
-        }
-    }
+// Exact (any-range) evaluation of one C tile from memory, one pod per lane.
+__device__ __forceinline__ void c_tile_exact(const PodDev& P, const GroupDev& G, int64_t t, uint32_t lane,
+                                             int64_t* __restrict__ wide) {
+    const int64_t i = P.s_tiles * TILE + t * CTILE + lane;
+    const uint32_t f = P.flags[i];
+    const uint32_t nxc = pf_xctr(f), nxp = pf_xpair(f);
+    uint32_t oc = P.xc_base[t] + wave_incl_scan32(nxc) - nxc;
+    const uint32_t op = P.xp_base[t] + wave_incl_scan32(nxp) - nxp;
+    if (f & ESC_PF_DAEMONSET) return;
+    int64_t cpu, mem;
+    pod_request(f, P.cpu0[i], P.mem0[i], P.xc_cpu, P.xc_mem, oc, cpu, mem);
+    const PodWide acc{wide};
+    if (pf_default_ok(f) && G.default_group != NONE) acc.add(G.n_gp, cpu, mem);
+    if (P.pair0[i] < G.n_gp) acc.add(P.pair0[i], cpu, mem);
+    for (uint32_t k = 0; k < nxp; ++k)
+        if (P.xp[op + k] < G.n_gp) acc.add(P.xp[op + k], cpu, mem);
 }
 
 }  // namespace
 
 // =====================================================================  K1 (fast)
-// Per wave a two-stage software pipeline: while tile t is processed, tile t+16's fixed
-// words and extra records are in flight, so the processing of a tile does not wait on
-// memory and each wave keeps ~5-10 KB of loads outstanding (80-160 KB per CU).
-template <int THREADS, bool PIPE, int ABLATE = 0>
+// Each workgroup takes an equal share of the S tiles and of the C tiles; its waves
+// interleave tiles (t = lo + wave, + waves).  16 waves per CU keep ~80 KB of tile loads
+// in flight per CU; the per-group partials stay in LDS and are flushed once.
+// ABLATE (timing-only builds): bit 0 LDS sink, bit 1 skip S tiles, bit 2 skip C tiles.
+template <int THREADS, int ABLATE = 0>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
                                                         int64_t* __restrict__ wide) {
     constexpr int NW = THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    PodLds acc{lds, lds + gw, g0, gw};
     for (uint32_t i = threadIdx.x; i < 2 * gw; i += THREADS) lds[i] = 0;
     __syncthreads();
-
+    const PodSink<ABLATE> K{PodLds{lds, lds + gw, g0, gw}, PodWide{wide}};
     const uint32_t lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t per = (P.n_tiles + gridDim.x - 1) / gridDim.x;
-    const int64_t t_lo = (int64_t)blockIdx.x * per;
-    const int64_t t_hi = t_lo + per < P.n_tiles ? t_lo + per : P.n_tiles;
-    const PodWide spill{wide};
-
-    // Tiles with more than 128 extra records of one kind are left to k_pod_bigtiles.
-    int64_t t = t_lo + wid;
-    if constexpr (PIPE) {
-        PodTile A, B;                                      // ping-pong: tile t+NW in flight
-        if (t < t_hi) tile_load(P, t, lane, tile_bases(P, t), A);
-        for (;;) {
-            if (t >= t_hi) break;
-            int64_t t1 = t + NW;
-            if (t1 < t_hi) tile_load(P, t1, lane, tile_bases(P, t1), B);
-            if (A.xcn <= 128 && A.xpn <= 128) process_tile_fast<ABLATE>(P, G, acc, spill, g0, gw, lane, A);
-            t = t1;
-            if (t >= t_hi) break;
-            t1 = t + NW;
-            if (t1 < t_hi) tile_load(P, t1, lane, tile_bases(P, t1), A);
-            if (B.xcn <= 128 && B.xpn <= 128) process_tile_fast<ABLATE>(P, G, acc, spill, g0, gw, lane, B);
-            t = t1;
+    if (!(ABLATE & 2)) {
+        const int64_t per = (P.s_tiles + gridDim.x - 1) / gridDim.x;
+        const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(lo + per, P.s_tiles);
+        for (int64_t t = lo + wid; t < hi; t += NW) {
+            STile A;
+            s_load(P, t, lane, A);
+            s_process<ABLATE>(G, K, A);
         }
-    } else {
-        // Latency hidden across the 16 waves; the next tile's record offsets (scalar
-        // registers, s_load) are fetched one tile ahead so the tile's words and its extra
-        // records are issued together.
+    }
+    if (!(ABLATE & 4)) {
+        const int64_t per = (P.c_tiles + gridDim.x - 1) / gridDim.x;
+        const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(lo + per, P.c_tiles);
+        int64_t t = lo + wid;
         TileBases nb{0, 0, 0, 0};
-        if (t < t_hi) nb = tile_bases(P, t);
-        for (; t < t_hi; t += NW) {
-            PodTile A;
-            tile_load(P, t, lane, nb, A);
-            if (t + NW < t_hi) nb = tile_bases(P, t + NW);
-            if (A.xcn <= 128 && A.xpn <= 128) process_tile_fast<ABLATE>(P, G, acc, spill, g0, gw, lane, A);
+        if (t < hi) nb = tile_bases(P, t);                // next tile's offsets: scalar, one ahead
+        for (; t < hi; t += NW) {
+            CTile A;
+            c_load(P, t, lane, nb, A);
+            if (t + NW < hi) nb = tile_bases(P, t + NW);
+            if (A.b.xcn <= 128 && A.b.xpn <= 128) c_process<ABLATE>(G, K, A);
         }
     }
     __syncthreads();
-    uint64_t* out = part + (int64_t)blockIdx.x * 2 * G.G + g0;
+    const int64_t S = G.n_gp + 1;
+    uint64_t* out = part + (int64_t)blockIdx.x * 2 * S + g0;
     for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
-        out[i] = acc.cc[i];
-        out[G.G + i] = acc.mem[i];
+        out[i] = lds[i];
+        out[S + i] = lds[gw + i];
     }
 }
 
-// Tiles whose extra records exceed what one wave holds in registers (listed by the host
-// at load; rare): one wave per tile, records read from memory, exact wide accumulation.
+// C tiles with more than 128 extra records of a kind (listed by the host at load):
+// one wave per tile, records read from memory, exact wide accumulation.
 __global__ __launch_bounds__(64) void k_pod_bigtiles(PodDev P, GroupDev G, const uint32_t* __restrict__ tiles,
                                                      int64_t* __restrict__ wide) {
-    const uint32_t lane = threadIdx.x;
-    const int64_t t = tiles[blockIdx.x];
-    const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
-    uint32_t nxc = 0, nxp = 0;
-    for (int j = 0; j < 4; ++j) { nxc += pf_xctr(P.flags[p0 + j]); nxp += pf_xpair(P.flags[p0 + j]); }
-    const uint64_t v = (uint64_t)nxc | ((uint64_t)nxp << 32);
-    const uint64_t s = wave_incl_scan(v, (int)lane) - v;
-    uint32_t oc = P.xc_base[t] + (uint32_t)s, op = P.xp_base[t] + (uint32_t)(s >> 32);
-    const PodWide acc{wide};
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t f = P.flags[p0 + j];
-        if (f & ESC_PF_DAEMONSET) { oc += pf_xctr(f); op += pf_xpair(f); continue; }
-        int64_t cpu, mem;
-        pod_request(f, P.cpu0[p0 + j], P.mem0[p0 + j], P.xc_cpu, P.xc_mem, oc, cpu, mem);
-        pod_groups(f, P.pair0[p0 + j], P.xp, op, G, [&](uint32_t g) { acc.add(g, cpu, mem); });
-    }
+    c_tile_exact(P, G, tiles[blockIdx.x], threadIdx.x, wide);
+}
+
+__global__ __launch_bounds__(256) void k_zero(int64_t* __restrict__ p, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
 }
 
 // =====================================================================  K1 (wide)
+// The whole shard through the exact accumulators (esc_force_wide; fallback testing).
 __global__ __launch_bounds__(256) void k_pod_wide(PodDev P, GroupDev G, int64_t* __restrict__ wide) {
-    const int lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    PodWide acc{wide};
-    for (int64_t t = wave; t < P.n_tiles; t += nwaves) {
-        const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
-        uint32_t nxc = 0, nxp = 0;
-        for (int j = 0; j < 4; ++j) { nxc += pf_xctr(P.flags[p0 + j]); nxp += pf_xpair(P.flags[p0 + j]); }
-        const uint64_t v = (uint64_t)nxc | ((uint64_t)nxp << 32);
-        const uint64_t s = wave_incl_scan(v, lane) - v;
-        uint32_t oc = P.xc_base[t] + (uint32_t)s, op = P.xp_base[t] + (uint32_t)(s >> 32);
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t f = P.flags[p0 + j];
-            if (f & ESC_PF_DAEMONSET) { oc += pf_xctr(f); op += pf_xpair(f); continue; }
-            int64_t cpu, mem;
-            pod_request(f, P.cpu0[p0 + j], P.mem0[p0 + j], P.xc_cpu, P.xc_mem, oc, cpu, mem);
-            pod_groups(f, P.pair0[p0 + j], P.xp, op, G, [&](uint32_t g) { acc.add(g, cpu, mem); });
+    const PodWide acc{wide};
+    for (int64_t t = wave; t < P.s_tiles; t += nwaves) {
+        for (int j = 0; j < PODS_PER_LANE; ++j) {
+            const int64_t i = t * TILE + lane * PODS_PER_LANE + j;
+            const uint32_t f = P.flags[i];
+            if (f & ESC_PF_DAEMONSET) continue;
+            const int64_t cpu = (int64_t)P.cpu0[i], mem = P.mem0[i];
+            if (pf_default_ok(f) && G.default_group != NONE) acc.add(G.n_gp, cpu, mem);
+            if (P.pair0[i] < G.n_gp) acc.add(P.pair0[i], cpu, mem);
         }
     }
+    for (int64_t t = wave; t < P.c_tiles; t += nwaves) c_tile_exact(P, G, t, lane, wide);
 }
 
 // =====================================================================  K2 nodes
@@ -411,14 +408,17 @@ __device__ __forceinline__ int node_class(const NodeDev& N, const GroupDev& G, u
     return (f & ESC_NF_TAINTED) ? 1 : 0;
 }
 
+// Groups a node belongs to: NewNodeLabelFilterFunc (node_group.go:278) over its label
+// pairs, resolved through the node pair table.
 template <class F>
 __device__ __forceinline__ void node_groups(const NodeDev& N, const GroupDev& G, uint32_t f, int64_t i,
                                             F&& emit) {
-    uint32_t g = N.label0[i];
+    for_code(G, node_code(G, N.label0[i]), emit);
     const uint32_t nx = nf_xlbl(f);
-    uint32_t q = nx ? N.xl_off[i] : 0;
-    if (g != NONE) emit(g);
-    for (uint32_t k = 0; k < nx; ++k) emit(N.xl[q++]);
+    if (nx) {
+        const uint32_t q = N.xl_off[i];
+        for (uint32_t k = 0; k < nx; ++k) for_code(G, node_code(G, N.xl[q + k]), emit);
+    }
 }
 
 }  // namespace
@@ -556,12 +556,15 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
     uint64_t a[NW] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     // a: 0 pcpu 1 pcnt 2 pmem_lo 3 pmem_hi 4 ncpu 5 nunt 6 nmem_lo 7 nmem_hi 8 taint 9 cord 10 first
     a[10] = ~0ull;
+    // The group's pod slot: its pair (NewPodAffinityFilterFunc) or the default filter's.
+    const int64_t S = G.n_gp + 1;
+    const int64_t slot = !ok ? 0 : ((uint32_t)g == G.default_group ? (int64_t)G.n_gp : (int64_t)G.gpair[g]);
     if (ok) {
         for (int b = wid; b < nblk; b += CB_WAVES) {
-            const uint64_t c = pod_part[(int64_t)b * 2 * G.G + g];
+            const uint64_t c = pod_part[(int64_t)b * 2 * S + slot];
             a[0] += c & CPU_MASK;
             a[1] += c >> CNT_SHIFT;
-            u128_add(a[2], a[3], pod_part[((int64_t)b * 2 + 1) * G.G + g]);
+            u128_add(a[2], a[3], pod_part[((int64_t)b * 2 + 1) * S + slot]);
         }
         for (int c = wid; c < n_chunk; c += CB_WAVES) {
             const uint64_t* r = node_part + (int64_t)c * 4 * G.G + g;
@@ -591,11 +594,11 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
         a[9] += red[w][9][lane];
         a[10] = red[w][10][lane] < a[10] ? red[w][10][lane] : a[10];
     }
-    int64_t* wp = wide_pod + (int64_t)g * WP_K;
+    const int64_t* wp = wide_pod + slot * WP_K;    // slots may be shared: zeroed per step by the host
     int64_t* wn = wide_node + (int64_t)g * WN_K;
     int64_t p[WP_K], q[WN_K];
 #pragma unroll
-    for (int k = 0; k < WP_K; ++k) { p[k] = wp[k]; wp[k] = 0; }
+    for (int k = 0; k < WP_K; ++k) p[k] = wp[k];
 #pragma unroll
     for (int k = 0; k < WN_K; ++k) { q[k] = wn[k]; wn[k] = 0; }
     int64_t* w = words + (int64_t)g * TW_K;
@@ -798,18 +801,24 @@ __global__ __launch_bounds__(256) void k_group_bounds(const uint64_t* __restrict
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st) {
     const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
+#define ESC_K1(T, A) hipLaunchKernelGGL((k_pod_reduce<T, A>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, wide)
     switch (variant) {
-        case 2: hipLaunchKernelGGL((k_pod_reduce<512, false>), dim3(nblk), dim3(512), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
-        case 3: hipLaunchKernelGGL((k_pod_reduce<1024, true>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
-        case 4: hipLaunchKernelGGL((k_pod_reduce<512, true>), dim3(nblk), dim3(512), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
-        // Timing-only ablations (wrong results; scripts/k1_variants.py): see process_tile_fast.
-        case 9: hipLaunchKernelGGL((k_pod_reduce<1024, false, 1>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
-        case 10: hipLaunchKernelGGL((k_pod_reduce<1024, false, 2>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
-        case 11: hipLaunchKernelGGL((k_pod_reduce<1024, false, 4>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
-        case 12: hipLaunchKernelGGL((k_pod_reduce<1024, false, 6>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
-        case 13: hipLaunchKernelGGL((k_pod_reduce<1024, false, 7>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
-        default: hipLaunchKernelGGL((k_pod_reduce<1024, false>), dim3(nblk), dim3(1024), lds, st, p, g, g0, (uint32_t)gw, part, wide); break;
+        case 2: ESC_K1(512, 0); break;
+        // Timing-only ablations (wrong results; scripts/k1_variants.py), see k_pod_reduce.
+        case 9: ESC_K1(1024, 1); break;
+        case 10: ESC_K1(1024, 2); break;
+        case 11: ESC_K1(1024, 4); break;
+        case 12: ESC_K1(1024, 3); break;
+        case 13: ESC_K1(1024, 5); break;
+        default: ESC_K1(1024, 0); break;
     }
+#undef ESC_K1
+    return hipGetLastError();
+}
+
+hipError_t launch_zero(int64_t* p, int64_t n, hipStream_t st) {
+    const int64_t nb = std::min<int64_t>((n + 255) / 256, 1024);
+    if (nb > 0) hipLaunchKernelGGL(k_zero, dim3((unsigned)nb), dim3(256), 0, st, p, n);
     return hipGetLastError();
 }
 

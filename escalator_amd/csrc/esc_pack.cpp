@@ -4,8 +4,9 @@
 // (FilteredPodsLister.List pkg/k8s/pod_listers.go:33, FilteredNodesLister.List
 // pkg/k8s/node_listers.go:33) by ONE pass that turns *v1.Pod / *v1.Node field copies
 // into the struct-of-arrays the kernels stream:
-//   - (key,value) strings are interned against the groups' label pairs
-//     (node_group.go:226-247, :280), keeping only pairs some group selects;
+//   - (key,value) strings whose key some group filters on are interned to pair ids
+//     (node_group.go:226-247, :280); which groups a pair selects is resolved on the
+//     device (K1/K2) through the context's pair tables;
 //   - the group-independent predicates PodIsDaemonSet (util.go:11), PodIsStatic
 //     (util.go:21) and the default filter's selector/affinity tests
 //     (node_group.go:271-273) become flag bits;
@@ -30,31 +31,43 @@ void GroupIndex::build(const esc_group_spec* specs, int32_t n) {
         c.key = specs[g].label_key ? specs[g].label_key : "";
         c.value = specs[g].label_value ? specs[g].label_value : "";
         c.spec = specs[g];
-        c.spec.name = c.name.c_str();
-        c.spec.label_key = c.key.c_str();
-        c.spec.label_value = c.value.c_str();
         // pkg/controller/client.go:59 — the lister choice is by name; names are map keys
         // in the reference (controller.go:93), so at most one "default" exists.
         if (c.name == "default" && default_group < 0) default_group = g;
     }
     // Re-point after the vector is final (no reallocation below).
     for (auto& c : groups) { c.spec.name = c.name.c_str(); c.spec.label_key = c.key.c_str(); c.spec.label_value = c.value.c_str(); }
-    pod_next.assign(n, NONE);
-    node_next.assign(n, NONE);
-    pod_head.clear();
-    node_head.clear();
-    std::unordered_map<std::string, uint32_t> pod_tail, node_tail;
-    pod_chains = node_chains = false;
+    pair_ids.clear();
+    keys.clear();
+    gpair.assign(n, NONE);
+    std::vector<std::vector<uint32_t>> node_groups;   // per pair id, ascending
     for (int32_t g = 0; g < n; ++g) {
-        std::string k = pair_key(groups[g].key.c_str(), groups[g].value.c_str());
-        auto it = node_tail.find(k);
-        if (it == node_tail.end()) { node_head[k] = g; node_tail[k] = g; }
-        else { node_next[it->second] = g; it->second = g; node_chains = true; }
-        if (g == default_group) continue;
-        auto jt = pod_tail.find(k);
-        if (jt == pod_tail.end()) { pod_head[k] = g; pod_tail[k] = g; }
-        else { pod_next[jt->second] = g; jt->second = g; pod_chains = true; }
+        keys[groups[g].key] = 1;
+        const std::string k = pair_key(groups[g].key.c_str(), groups[g].value.c_str());
+        auto it = pair_ids.find(k);
+        uint32_t id;
+        if (it == pair_ids.end()) {
+            id = (uint32_t)pair_ids.size();
+            pair_ids.emplace(k, id);
+            node_groups.emplace_back();
+        } else {
+            id = it->second;
+        }
+        gpair[g] = id;
+        node_groups[id].push_back((uint32_t)g);
     }
+    n_gp = (uint32_t)pair_ids.size();
+    code_list.clear();
+    auto encode = [&](const std::vector<uint32_t>& gs) -> uint32_t {
+        if (gs.empty()) return NONE;
+        if (gs.size() == 1) return gs[0];
+        const uint32_t off = (uint32_t)code_list.size();
+        code_list.push_back((uint32_t)gs.size());
+        code_list.insert(code_list.end(), gs.begin(), gs.end());
+        return CODE_MULTI | off;
+    };
+    node_code.resize(n_gp);
+    for (uint32_t i = 0; i < n_gp; ++i) node_code[i] = encode(node_groups[i]);
 }
 
 void HostSnapshot::view(esc_pod_soa* p, esc_node_soa* n) const {
@@ -62,12 +75,12 @@ void HostSnapshot::view(esc_pod_soa* p, esc_node_soa* n) const {
         p->n_pods = (int64_t)flags.size();
         p->flags = flags.data(); p->cpu0 = cpu0.data(); p->mem0 = mem0.data(); p->pair0 = pair0.data();
         p->xc_cpu = xc_cpu.data(); p->xc_mem = xc_mem.data(); p->n_xc = (int64_t)xc_cpu.size();
-        p->xp_group = xp.data(); p->n_xp = (int64_t)xp.size();
+        p->xp_pair = xp.data(); p->n_xp = (int64_t)xp.size();
     }
     if (n) {
         n->n_nodes = (int64_t)nflags.size();
         n->flags = nflags.data(); n->label0 = label0.data(); n->cpu = ncpu.data(); n->mem = nmem.data();
-        n->created_ns = created.data(); n->xl_group = xl.data(); n->n_xl = (int64_t)xl.size();
+        n->created_ns = created.data(); n->xl_pair = xl.data(); n->n_xl = (int64_t)xl.size();
         n->trk_node = trk_node.data(); n->trk_group = trk_group.data(); n->n_trk = (int64_t)trk_node.size();
     }
 }
@@ -79,26 +92,38 @@ struct esc_packer {
     HostSnapshot s;
     std::vector<std::string> node_names;
     std::vector<std::vector<std::string>> trackers;
+    std::unordered_map<std::string, uint32_t> other_pairs;   // group-key values no group selects
 };
 
 namespace {
 
 inline int64_t req_or(int32_t has, int64_t v, int64_t absent) { return has ? v : absent; }
 
-// Matched pair heads -> the sorted, de-duplicated set of groups they select (every group
-// sharing a pair is listed explicitly, so the kernels never walk chains).
-void expand_chains(std::vector<uint32_t>& heads, const std::vector<uint32_t>& next) {
-    const size_t n = heads.size();
-    for (size_t i = 0; i < n; ++i)
-        for (uint32_t h = next[heads[i]]; h != NONE; h = next[h]) heads.push_back(h);
-    std::sort(heads.begin(), heads.end());
-    heads.erase(std::unique(heads.begin(), heads.end()), heads.end());
+// Pair id of (key, value) for a key some group uses: the group pair's id, or a
+// packer-local id >= n_gp for a value no group selects (the numbering rule of
+// include/escalator_hip.h).  Returns false when the id space is exhausted.
+bool intern(esc_packer* pk, const char* k, const char* v, uint32_t& id) {
+    id = pk->gi->pair_id(k, v);
+    if (id != NONE) return true;
+    const std::string key = GroupIndex::pair_key(k, v);
+    auto it = pk->other_pairs.find(key);
+    if (it != pk->other_pairs.end()) { id = it->second; return true; }
+    const uint64_t nid = (uint64_t)pk->gi->n_gp + pk->other_pairs.size();
+    if (nid >= ESC_PAIR_LIMIT) return false;
+    id = (uint32_t)nid;
+    pk->other_pairs.emplace(key, id);
+    return true;
+}
+
+void sort_unique(std::vector<uint32_t>& v) {
+    std::sort(v.begin(), v.end());
+    v.erase(std::unique(v.begin(), v.end()), v.end());
 }
 
 int32_t pack_pod(esc_packer* pk, const esc_pod_obj& o) {
     HostSnapshot& s = pk->s;
     uint32_t f = 0;
-    std::vector<uint32_t> heads;
+    std::vector<uint32_t> pairs;
     if (!pk->list_mode) {
         for (int32_t i = 0; i < o.n_owner_kinds; ++i)                        // util.go:12-16
             if (o.owner_kinds[i] && std::strcmp(o.owner_kinds[i], "DaemonSet") == 0) { f |= ESC_PF_DAEMONSET; break; }
@@ -107,30 +132,37 @@ int32_t pack_pod(esc_packer* pk, const esc_pod_obj& o) {
         if (o.n_node_selector > 0) f |= ESC_PF_HAS_SEL;                      // node_group.go:271
         if (o.has_affinity && (o.has_node_affinity || o.has_pod_affinity || o.has_pod_anti_affinity))
             f |= ESC_PF_AFF_BLOCK;                                           // node_group.go:271-273
-        // NewPodAffinityFilterFunc's two match routes (node_group.go:226-249) as a set of
-        // head groups; a group counts a pod once however many routes match.
+        // The (key, value) pairs NewPodAffinityFilterFunc can match on (node_group.go:226-249):
+        // Spec.NodeSelector entries and the values of "In" expressions of the required
+        // node-affinity terms, for keys some group filters on.  As a set: a group counts
+        // a pod once however many routes match.  K1 resolves pair -> groups.
         for (int32_t i = 0; i < o.n_node_selector; ++i) {
-            uint32_t h = pk->gi->head(o.node_selector[i].key, o.node_selector[i].value, 0);
-            if (h != NONE) heads.push_back(h);
+            const esc_kv& kv = o.node_selector[i];
+            if (!pk->gi->is_key(kv.key)) continue;
+            uint32_t id;
+            if (!intern(pk, kv.key, kv.value, id)) return ESC_E_LIMIT;
+            pairs.push_back(id);
         }
         if (o.has_affinity && o.has_node_affinity && o.has_required) {     // unwrapNodeSelectorTerms :208
             for (int32_t e = 0; e < o.n_exprs; ++e) {
                 const esc_selector_expr& x = o.exprs[e];
                 if (!x.op || std::strcmp(x.op, "In") != 0) continue;         // only In (:241)
+                if (!pk->gi->is_key(x.key)) continue;
                 for (int32_t v = 0; v < x.n_values; ++v) {
-                    uint32_t h = pk->gi->head(x.key, x.values[v], 0);
-                    if (h != NONE) heads.push_back(h);
+                    uint32_t id;
+                    if (!intern(pk, x.key, x.values[v], id)) return ESC_E_LIMIT;
+                    pairs.push_back(id);
                 }
             }
         }
-        expand_chains(heads, pk->gi->pod_next);
+        sort_unique(pairs);
     } else {
-        heads.push_back(0);
+        pairs.push_back(0);                                                  // the list group's pair
     }
-    if (heads.size() > 1 + ESC_PF_PAIR_MASK) return ESC_E_LIMIT;   // > 64 matching groups
-    const uint32_t pair0 = heads.empty() ? NONE : heads[0];
-    for (size_t i = 1; i < heads.size(); ++i) s.xp.push_back(heads[i]);
-    f |= (uint32_t)(heads.empty() ? 0 : heads.size() - 1) << ESC_PF_XPAIR_SHIFT;
+    if (pairs.size() > 1 + ESC_PF_PAIR_MASK) return ESC_E_LIMIT;   // > 64 distinct pairs
+    const uint32_t pair0 = pairs.empty() ? NONE : pairs[0];
+    for (size_t i = 1; i < pairs.size(); ++i) s.xp.push_back(pairs[i]);
+    f |= (uint32_t)(pairs.empty() ? 0 : pairs.size() - 1) << ESC_PF_XPAIR_SHIFT;
 
     // Containers: the first regular container is inline when its cpu fits u32.
     uint32_t cpu0 = 0;
@@ -172,23 +204,25 @@ int32_t pack_pod(esc_packer* pk, const esc_pod_obj& o) {
 int32_t pack_node(esc_packer* pk, const esc_node_obj& o) {
     HostSnapshot& s = pk->s;
     uint32_t f = 0;
-    std::vector<uint32_t> heads;
+    std::vector<uint32_t> pairs;
     if (!pk->list_mode) {
         if (o.unschedulable) f |= ESC_NF_UNSCHED;                            // controller.go:141
         for (int32_t i = 0; i < o.n_taints; ++i)                             // taint.go:81-85
             if (o.taint_keys[i] && std::strcmp(o.taint_keys[i], "atlassian.com/escalator") == 0) { f |= ESC_NF_TAINTED; break; }
         for (int32_t i = 0; i < o.n_labels; ++i) {                           // node_group.go:280
-            uint32_t h = pk->gi->head(o.labels[i].key, o.labels[i].value, 1);
-            if (h != NONE) heads.push_back(h);
+            if (!pk->gi->is_key(o.labels[i].key)) continue;                  // Labels[K] for group keys
+            uint32_t id;
+            if (!intern(pk, o.labels[i].key, o.labels[i].value, id)) return ESC_E_LIMIT;
+            pairs.push_back(id);
         }
-        expand_chains(heads, pk->gi->node_next);
+        sort_unique(pairs);
     } else {
-        heads.push_back(0);
+        pairs.push_back(0);
     }
-    if (heads.size() > 1 + ESC_PF_CNT_MASK) return ESC_E_LIMIT;
-    s.label0.push_back(heads.empty() ? NONE : heads[0]);
-    for (size_t i = 1; i < heads.size(); ++i) s.xl.push_back(heads[i]);
-    f |= (uint32_t)(heads.empty() ? 0 : heads.size() - 1) << ESC_NF_XLBL_SHIFT;
+    if (pairs.size() > 1 + ESC_PF_CNT_MASK) return ESC_E_LIMIT;
+    s.label0.push_back(pairs.empty() ? NONE : pairs[0]);
+    for (size_t i = 1; i < pairs.size(); ++i) s.xl.push_back(pairs[i]);
+    f |= (uint32_t)(pairs.empty() ? 0 : pairs.size() - 1) << ESC_NF_XLBL_SHIFT;
     s.nflags.push_back(f);
     s.ncpu.push_back(req_or(o.allocatable.has_cpu, o.allocatable.cpu_m, 0));   // util.go:47 absent -> 0
     s.nmem.push_back(req_or(o.allocatable.has_mem, o.allocatable.mem_b, 0));

@@ -93,10 +93,11 @@ struct esc_ctx {
     // device group tables
     uint8_t* d_dry = nullptr;
     GroupParams* d_params = nullptr;
+    uint32_t *d_gpair = nullptr, *d_node_code = nullptr, *d_code_list = nullptr;
     // snapshot
     std::vector<PodBuf> pods;
     int n_replicas = 1, cur = 0;
-    int64_t n_pods = 0, n_tiles = 0, n_xc = 0, n_xp = 0, pod_offset = 0, n_big = 0;
+    int64_t n_pods = 0, s_tiles = 0, c_tiles = 0, n_xc = 0, n_xp = 0, pod_offset = 0, n_big = 0;
     bool pods_loaded = false;
     NodeBuf nodes;
     int64_t n_nodes = 0, n_xl = 0, n_trk = 0, node_lo = 0, node_hi = 0;
@@ -147,6 +148,10 @@ GroupDev group_dev(const esc_ctx* c) {
     GroupDev g;
     g.dry = c->d_dry;
     g.params = c->d_params;
+    g.gpair = c->d_gpair;
+    g.node_code = c->d_node_code;
+    g.code_list = c->d_code_list;
+    g.n_gp = c->gi.n_gp;
     g.G = c->gi.G;
     g.default_group = c->gi.default_group < 0 ? NONE : (uint32_t)c->gi.default_group;
     return g;
@@ -158,7 +163,8 @@ PodDev pod_dev(const esc_ctx* c, int replica) {
     p.flags = b.flags; p.cpu0 = b.cpu0; p.mem0 = b.mem0; p.pair0 = b.pair0;
     p.xc_cpu = b.xc_cpu; p.xc_mem = b.xc_mem; p.xp = b.xp;
     p.xc_base = b.xc_base; p.xp_base = b.xp_base;
-    p.n_tiles = c->n_tiles;
+    p.s_tiles = c->s_tiles;
+    p.c_tiles = c->c_tiles;
     return p;
 }
 
@@ -206,20 +212,27 @@ void release_sort(esc_ctx* c) {
     c->sorted = false;
 }
 
+// Pod accumulator slots: one per group pair + one for the default filter.
+int64_t pod_slots(const esc_ctx* c) { return (int64_t)c->gi.n_gp + 1; }
+
 // Grid geometry for the current snapshot.
 int32_t ensure_work(esc_ctx* c) {
     if (c->work_ready) return ESC_OK;
     const int32_t G = c->gi.G;
-    const int gw = std::min(G, POD_WINDOW_MAX);
+    const int64_t S = pod_slots(c);
+    const int gw = (int)std::min<int64_t>(S, POD_WINDOW_MAX);
     const int lds = gw * 16;
     const int max_blocks = (c->k1_variant == 2 || c->k1_variant == 4) ? 4 : 2;   // 2048 threads per CU
     const int per_cu = std::max(1, std::min(max_blocks, LDS_BYTES / std::max(lds, 1)));
-    int nblk = c->cu_count * per_cu;
-    const int64_t pods_per_block = (c->n_tiles * TILE + nblk - 1) / std::max(nblk, 1);
-    if (pods_per_block > PODS_PER_BLOCK_MAX) nblk = (int)((c->n_tiles * TILE + PODS_PER_BLOCK_MAX - 1) / PODS_PER_BLOCK_MAX);
-    if (c->n_tiles == 0) nblk = 0;
-    nblk = (int)std::min<int64_t>(nblk, std::max<int64_t>(c->n_tiles, 0));
-    c->nblk = nblk;
+    int64_t nblk = c->cu_count * per_cu;
+    // every workgroup takes ceil(s_tiles/nblk) S tiles + ceil(c_tiles/nblk) C tiles;
+    // keep that within PODS_PER_BLOCK_MAX (exactness of the packed LDS partials)
+    auto block_pods = [&](int64_t b) {
+        return ((c->s_tiles + b - 1) / b) * TILE + ((c->c_tiles + b - 1) / b) * CTILE;
+    };
+    while (block_pods(nblk) > PODS_PER_BLOCK_MAX) nblk *= 2;
+    nblk = std::min<int64_t>(nblk, std::max(c->s_tiles, c->c_tiles));
+    c->nblk = (int)nblk;
     // nodes: group tiles x node chunks; keep the partial flush below ~half the node bytes
     const int64_t n_local = c->node_hi - c->node_lo;
     c->gt = std::min(G, NODE_TILE);
@@ -230,11 +243,11 @@ int32_t ensure_work(esc_ctx* c) {
     n_chunk = std::max<int64_t>(n_chunk, (n_local + NODES_PER_CHUNK_MAX - 1) / NODES_PER_CHUNK_MAX);
     if (n_local == 0) n_chunk = 0;
     c->n_chunk = (int)n_chunk;
-    HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max(nblk, 1) * 2 * G));
+    HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * S));
     HIP_TRY(dalloc(&c->d_node_part, (size_t)std::max<int64_t>(n_chunk, 1) * 4 * G));
-    HIP_TRY(dalloc(&c->d_wide_pod, (size_t)G * WP_K));
+    HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
     HIP_TRY(dalloc(&c->d_wide_node, (size_t)G * WN_K));
-    HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)G * WP_K * sizeof(int64_t)));
+    HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)S * WP_K * sizeof(int64_t)));
     HIP_TRY(hipMemset(c->d_wide_node, 0, (size_t)G * WN_K * sizeof(int64_t)));
     HIP_TRY(dalloc(&c->own_words, (size_t)G * TW_K));
     HIP_TRY(dalloc(&c->own_first, (size_t)G));
@@ -255,14 +268,15 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     int nblk = 0, n_chunk = 0;
     if (c->force_wide) {
-        if (c->n_tiles) HIP_TRY(launch_wide_pods(pod_dev(c, r), g, c->d_wide_pod, st));
+        if (c->s_tiles + c->c_tiles) HIP_TRY(launch_wide_pods(pod_dev(c, r), g, c->d_wide_pod, st));
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
         if (n.hi > n.lo) HIP_TRY(launch_wide_nodes(n, g, c->d_wide_node, st));
     } else {
         if (c->nblk) {
             const PodDev p = pod_dev(c, r);
-            for (int32_t g0 = 0; g0 < g.G; g0 += POD_WINDOW_MAX) {
-                const int32_t gw = std::min(POD_WINDOW_MAX, g.G - g0);
+            const int32_t S = (int32_t)pod_slots(c);
+            for (int32_t g0 = 0; g0 < S; g0 += POD_WINDOW_MAX) {       // LDS windows of pod slots
+                const int32_t gw = std::min(POD_WINDOW_MAX, S - g0);
                 HIP_TRY(launch_pod_reduce(p, g, g0, gw, c->nblk, c->k1_variant, c->d_pod_part, c->d_wide_pod, st));
             }
             HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
@@ -275,6 +289,8 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     HIP_TRY(launch_combine(g, n, c->d_pod_part, nblk, c->d_node_part, n_chunk, c->d_wide_pod, c->d_wide_node,
                            c->d_words, c->d_first, decide, c->d_dec, st));
+    // pod wide rows are per slot and may be read by several groups in K3: cleared after it
+    HIP_TRY(launch_zero(c->d_wide_pod, pod_slots(c) * WP_K, st));
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     if (copy_out) {
         HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)g.G * sizeof(esc_group_decision),
@@ -367,6 +383,15 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
         if (hipEventCreate(&c->ev[i]) != hipSuccess) return fail(ESC_E_HIP);
     const size_t G = (size_t)n_groups;
     if (dalloc(&c->d_dry, G) || dalloc(&c->d_params, G)) return fail(ESC_E_NOMEM);
+    const GroupIndex& gi = c->gi;
+    if (dalloc(&c->d_gpair, G) || dalloc(&c->d_node_code, gi.n_gp) ||
+        dalloc(&c->d_code_list, gi.code_list.size()))
+        return fail(ESC_E_NOMEM);
+    if (hipMemcpy(c->d_gpair, gi.gpair.data(), G * 4, hipMemcpyHostToDevice) ||
+        hipMemcpy(c->d_node_code, gi.node_code.data(), gi.n_gp * 4, hipMemcpyHostToDevice) ||
+        (!gi.code_list.empty() &&
+         hipMemcpy(c->d_code_list, gi.code_list.data(), gi.code_list.size() * 4, hipMemcpyHostToDevice)))
+        return fail(ESC_E_HIP);
     std::vector<uint8_t> dry(G);
     for (size_t g = 0; g < G; ++g) dry[g] = (uint8_t)c->params[g].dry;
     if (hipMemcpy(c->d_dry, dry.data(), G, hipMemcpyHostToDevice) ||
@@ -387,6 +412,7 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         for (auto& b : c->pods) b.release();
         c->nodes.release();
         dfree(c->d_dry); dfree(c->d_params);
+        dfree(c->d_gpair); dfree(c->d_node_code); dfree(c->d_code_list);
         for (int i = 0; i < MAX_STAGES; ++i)
             if (c->ev[i]) hipEventDestroy(c->ev[i]);
         if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -414,10 +440,12 @@ int32_t esc_ctx_set_stream(esc_ctx* c, void* hip_stream) {
 
 int32_t esc_ctx_num_groups(const esc_ctx* c) { return c ? c->gi.G : 0; }
 
-uint32_t esc_ctx_pair_head(const esc_ctx* c, const char* key, const char* value, int32_t side) {
+uint32_t esc_ctx_pair_id(const esc_ctx* c, const char* key, const char* value) {
     if (!c) return NONE;
-    return c->gi.head(key, value, side ? 1 : 0);
+    return c->gi.pair_id(key, value);
 }
+
+int32_t esc_ctx_num_group_pairs(const esc_ctx* c) { return c ? (int32_t)c->gi.n_gp : 0; }
 
 int32_t esc_set_replicas(esc_ctx* c, int32_t n) {
     if (!c || n < 1 || n > 64) return ESC_E_INVAL;
@@ -430,30 +458,60 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     if (!c->has_device) return ESC_E_NODEV;
     const int64_t n = p->n_pods;
     if (n > 0 && (!p->flags || !p->cpu0 || !p->mem0 || !p->pair0)) return ESC_E_INVAL;
-    if ((p->n_xc > 0 && (!p->xc_cpu || !p->xc_mem)) || (p->n_xp > 0 && !p->xp_group)) return ESC_E_INVAL;
+    if ((p->n_xc > 0 && (!p->xc_cpu || !p->xc_mem)) || (p->n_xp > 0 && !p->xp_pair)) return ESC_E_INVAL;
     if (p->n_xc >= (int64_t)0xFFFFFFFF || p->n_xp >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
-    const uint32_t G = (uint32_t)c->gi.G;
-    // Validate every group id (a bad id would index outside the LDS / group tables) and
-    // build the per-tile offsets of the extra records.
-    const int64_t n_tiles = (n + TILE - 1) / TILE;
-    std::vector<uint32_t> xc_base(n_tiles + 1), xp_base(n_tiles + 1);
+    // Validate the pair lists (ascending, unique, < ESC_PAIR_LIMIT: a pod matches each
+    // group at most once) and the record counts; count the pods with extra records.
     uint64_t sc = 0, sp = 0;
+    int64_t n_c = 0;
     for (int64_t i = 0; i < n; ++i) {
-        if ((i & (TILE - 1)) == 0) { xc_base[i / TILE] = (uint32_t)sc; xp_base[i / TILE] = (uint32_t)sp; }
         const uint32_t f = p->flags[i];
-        if (p->pair0[i] != NONE && p->pair0[i] >= G) return ESC_E_INVAL;
-        sc += pf_xctr(f);
-        sp += pf_xpair(f);
+        const uint32_t nx = pf_xpair(f), nc = pf_xctr(f);
+        uint32_t last = p->pair0[i];
+        if (last == NONE ? nx != 0 : last >= ESC_PAIR_LIMIT) return ESC_E_INVAL;
+        if (sp + nx > (uint64_t)p->n_xp) return ESC_E_INVAL;
+        for (uint32_t k = 0; k < nx; ++k) {
+            const uint32_t q = p->xp_pair[sp + k];
+            if (q >= ESC_PAIR_LIMIT || q <= last) return ESC_E_INVAL;
+            last = q;
+        }
+        sc += nc;
+        sp += nx;
+        n_c += (nc | nx) ? 1 : 0;
     }
-    xc_base[n_tiles] = (uint32_t)sc;
-    xp_base[n_tiles] = (uint32_t)sp;
-    // Tiles with more extra records than a wave holds in registers go to k_pod_bigtiles.
-    std::vector<uint32_t> big;
-    for (int64_t t = 0; t < n_tiles; ++t)
-        if (xc_base[t + 1] - xc_base[t] > 128 || xp_base[t + 1] - xp_base[t] > 128) big.push_back((uint32_t)t);
     if ((int64_t)sc != p->n_xc || (int64_t)sp != p->n_xp) return ESC_E_INVAL;
-    for (int64_t i = 0; i < p->n_xp; ++i)
-        if (p->xp_group[i] >= G) return ESC_E_INVAL;
+    // Stable partition: simple pods (no extra records) -> S section, padded to whole
+    // 256-pod tiles; the others -> C section of 64-pod tiles.  Records keep their order
+    // (simple pods own none), so only the per-pod arrays move.
+    const int64_t s_tiles = (n - n_c + TILE - 1) / TILE, c_tiles = (n_c + CTILE - 1) / CTILE;
+    const int64_t c0 = s_tiles * TILE, npad = c0 + c_tiles * CTILE;
+    std::vector<uint32_t> hf(npad, ESC_PF_DAEMONSET), hc(npad, 0), hp(npad, NONE);
+    std::vector<int64_t> hm(npad, 0);
+    std::vector<uint32_t> xc_base(c_tiles + 1, 0), xp_base(c_tiles + 1, 0);
+    {
+        int64_t is = 0, ic = 0;
+        uint32_t oc = 0, op = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            const uint32_t f = p->flags[i];
+            const uint32_t nx = pf_xpair(f), nc = pf_xctr(f);
+            int64_t d;
+            if ((nc | nx) == 0) {
+                d = is++;
+            } else {
+                if (ic % CTILE == 0) { xc_base[ic / CTILE] = oc; xp_base[ic / CTILE] = op; }
+                d = c0 + ic++;
+                oc += nc;
+                op += nx;
+            }
+            hf[d] = f; hc[d] = p->cpu0[i]; hm[d] = p->mem0[i]; hp[d] = p->pair0[i];
+        }
+        xc_base[c_tiles] = oc;
+        xp_base[c_tiles] = op;
+    }
+    // C tiles with more extra records than a wave holds in registers go to k_pod_bigtiles.
+    std::vector<uint32_t> big;
+    for (int64_t t = 0; t < c_tiles; ++t)
+        if (xc_base[t + 1] - xc_base[t] > 128 || xp_base[t + 1] - xp_base[t] > 128) big.push_back((uint32_t)t);
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     drop_graphs(c);
@@ -461,52 +519,47 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     release_sort(c);
     for (auto& b : c->pods) b.release();
     c->pods.assign(c->n_replicas, PodBuf());
-    const int64_t npad = n_tiles * TILE;
     for (int r = 0; r < c->n_replicas; ++r) {
         PodBuf& b = c->pods[r];
         HIP_TRY(dalloc(&b.flags, npad)); HIP_TRY(dalloc(&b.cpu0, npad)); HIP_TRY(dalloc(&b.mem0, npad));
         HIP_TRY(dalloc(&b.pair0, npad)); HIP_TRY(dalloc(&b.xc_cpu, p->n_xc)); HIP_TRY(dalloc(&b.xc_mem, p->n_xc));
-        HIP_TRY(dalloc(&b.xp, p->n_xp)); HIP_TRY(dalloc(&b.xc_base, n_tiles + 1)); HIP_TRY(dalloc(&b.xp_base, n_tiles + 1));
+        HIP_TRY(dalloc(&b.xp, p->n_xp)); HIP_TRY(dalloc(&b.xc_base, c_tiles + 1)); HIP_TRY(dalloc(&b.xp_base, c_tiles + 1));
         HIP_TRY(dalloc(&b.big, big.size()));
         if (!big.empty()) HIP_TRY(hipMemcpy(b.big, big.data(), big.size() * 4, hipMemcpyHostToDevice));
         if (r == 0) {
-            if (n) {
-                HIP_TRY(hipMemcpy(b.flags, p->flags, n * 4, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemcpy(b.cpu0, p->cpu0, n * 4, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemcpy(b.mem0, p->mem0, n * 8, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemcpy(b.pair0, p->pair0, n * 4, hipMemcpyHostToDevice));
-            }
-            if (npad > n) {
-                std::vector<uint32_t> pad_f(npad - n, ESC_PF_DAEMONSET), pad_g(npad - n, NONE);
-                HIP_TRY(hipMemcpy(b.flags + n, pad_f.data(), (npad - n) * 4, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemcpy(b.pair0 + n, pad_g.data(), (npad - n) * 4, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemset(b.cpu0 + n, 0, (npad - n) * 4));
-                HIP_TRY(hipMemset(b.mem0 + n, 0, (npad - n) * 8));
+            if (npad) {
+                HIP_TRY(hipMemcpy(b.flags, hf.data(), npad * 4, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(b.cpu0, hc.data(), npad * 4, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(b.mem0, hm.data(), npad * 8, hipMemcpyHostToDevice));
+                HIP_TRY(hipMemcpy(b.pair0, hp.data(), npad * 4, hipMemcpyHostToDevice));
             }
             if (p->n_xc) {
                 HIP_TRY(hipMemcpy(b.xc_cpu, p->xc_cpu, p->n_xc * 8, hipMemcpyHostToDevice));
                 HIP_TRY(hipMemcpy(b.xc_mem, p->xc_mem, p->n_xc * 8, hipMemcpyHostToDevice));
             }
-            if (p->n_xp) HIP_TRY(hipMemcpy(b.xp, p->xp_group, p->n_xp * 4, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(b.xc_base, xc_base.data(), (n_tiles + 1) * 4, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(b.xp_base, xp_base.data(), (n_tiles + 1) * 4, hipMemcpyHostToDevice));
+            if (p->n_xp) HIP_TRY(hipMemcpy(b.xp, p->xp_pair, p->n_xp * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(b.xc_base, xc_base.data(), (c_tiles + 1) * 4, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(b.xp_base, xp_base.data(), (c_tiles + 1) * 4, hipMemcpyHostToDevice));
         } else {
             const PodBuf& a = c->pods[0];
-            HIP_TRY(hipMemcpy(b.flags, a.flags, npad * 4, hipMemcpyDeviceToDevice));
-            HIP_TRY(hipMemcpy(b.cpu0, a.cpu0, npad * 4, hipMemcpyDeviceToDevice));
-            HIP_TRY(hipMemcpy(b.mem0, a.mem0, npad * 8, hipMemcpyDeviceToDevice));
-            HIP_TRY(hipMemcpy(b.pair0, a.pair0, npad * 4, hipMemcpyDeviceToDevice));
+            if (npad) {
+                HIP_TRY(hipMemcpy(b.flags, a.flags, npad * 4, hipMemcpyDeviceToDevice));
+                HIP_TRY(hipMemcpy(b.cpu0, a.cpu0, npad * 4, hipMemcpyDeviceToDevice));
+                HIP_TRY(hipMemcpy(b.mem0, a.mem0, npad * 8, hipMemcpyDeviceToDevice));
+                HIP_TRY(hipMemcpy(b.pair0, a.pair0, npad * 4, hipMemcpyDeviceToDevice));
+            }
             if (p->n_xc) {
                 HIP_TRY(hipMemcpy(b.xc_cpu, a.xc_cpu, p->n_xc * 8, hipMemcpyDeviceToDevice));
                 HIP_TRY(hipMemcpy(b.xc_mem, a.xc_mem, p->n_xc * 8, hipMemcpyDeviceToDevice));
             }
             if (p->n_xp) HIP_TRY(hipMemcpy(b.xp, a.xp, p->n_xp * 4, hipMemcpyDeviceToDevice));
-            HIP_TRY(hipMemcpy(b.xc_base, a.xc_base, (n_tiles + 1) * 4, hipMemcpyDeviceToDevice));
-            HIP_TRY(hipMemcpy(b.xp_base, a.xp_base, (n_tiles + 1) * 4, hipMemcpyDeviceToDevice));
+            HIP_TRY(hipMemcpy(b.xc_base, a.xc_base, (c_tiles + 1) * 4, hipMemcpyDeviceToDevice));
+            HIP_TRY(hipMemcpy(b.xp_base, a.xp_base, (c_tiles + 1) * 4, hipMemcpyDeviceToDevice));
         }
     }
     c->n_pods = n;
-    c->n_tiles = n_tiles;
+    c->s_tiles = s_tiles;
+    c->c_tiles = c_tiles;
     c->n_big = (int64_t)big.size();
     c->n_xc = p->n_xc;
     c->n_xp = p->n_xp;
@@ -522,23 +575,29 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     const int64_t n = s->n_nodes;
     if (n >= (int64_t)0x7FFFFFFF) return ESC_E_LIMIT;
     if (n > 0 && (!s->flags || !s->label0 || !s->cpu || !s->mem || !s->created_ns)) return ESC_E_INVAL;
-    if ((s->n_xl > 0 && !s->xl_group) || (s->n_trk > 0 && (!s->trk_node || !s->trk_group))) return ESC_E_INVAL;
+    if ((s->n_xl > 0 && !s->xl_pair) || (s->n_trk > 0 && (!s->trk_node || !s->trk_group))) return ESC_E_INVAL;
     const uint32_t G = (uint32_t)c->gi.G;
     std::vector<uint32_t> xl_off(std::max<int64_t>(n, 1));
     uint64_t sx = 0;
     int64_t tmin = 0, tmax = 0;
     for (int64_t i = 0; i < n; ++i) {
         xl_off[i] = (uint32_t)sx;
-        sx += nf_xlbl(s->flags[i]);
-        if (s->label0[i] != NONE && s->label0[i] >= G) return ESC_E_INVAL;
+        const uint32_t nx = nf_xlbl(s->flags[i]);
+        uint32_t last = s->label0[i];                // label pairs ascending, unique
+        if (last == NONE ? nx != 0 : last >= ESC_PAIR_LIMIT) return ESC_E_INVAL;
+        if (sx + nx > (uint64_t)s->n_xl) return ESC_E_INVAL;
+        for (uint32_t k = 0; k < nx; ++k) {
+            const uint32_t q = s->xl_pair[sx + k];
+            if (q >= ESC_PAIR_LIMIT || q <= last) return ESC_E_INVAL;
+            last = q;
+        }
+        sx += nx;
         if (i >= lo && i < hi) {
             if (i == lo || s->created_ns[i] < tmin) tmin = s->created_ns[i];
             if (i == lo || s->created_ns[i] > tmax) tmax = s->created_ns[i];
         }
     }
     if ((int64_t)sx != s->n_xl) return ESC_E_INVAL;
-    for (int64_t i = 0; i < s->n_xl; ++i)
-        if (s->xl_group[i] >= G) return ESC_E_INVAL;
     for (int64_t i = 0; i < s->n_trk; ++i) {
         if (s->trk_node[i] < 0 || s->trk_node[i] >= n || s->trk_group[i] < 0 || (uint32_t)s->trk_group[i] >= G)
             return ESC_E_INVAL;
@@ -564,7 +623,7 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
         HIP_TRY(hipMemcpy(b.created, s->created_ns, n * 8, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(b.xl_off, xl_off.data(), n * 4, hipMemcpyHostToDevice));
     }
-    if (s->n_xl) HIP_TRY(hipMemcpy(b.xl, s->xl_group, s->n_xl * 4, hipMemcpyHostToDevice));
+    if (s->n_xl) HIP_TRY(hipMemcpy(b.xl, s->xl_pair, s->n_xl * 4, hipMemcpyHostToDevice));
     if (s->n_trk) {
         HIP_TRY(hipMemcpy(b.trk_node, s->trk_node, s->n_trk * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(b.trk_group, s->trk_group, s->n_trk * 4, hipMemcpyHostToDevice));

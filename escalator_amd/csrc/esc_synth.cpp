@@ -59,7 +59,7 @@ struct esc_synth {
     GroupIndex gi;
     // per-group derived tables
     std::vector<int32_t> canon, key_id;
-    std::vector<uint32_t> pod_head_of, node_head_of;   // head of the group's own pair
+    std::vector<uint32_t> pair_of;                      // pair id of the group's own pair
     std::vector<int32_t> nondefault, pool_groups;
     std::vector<int64_t> type_cpu, type_mem;
     uint64_t default_bp = 0;        // basis points of pods that carry no selector at all
@@ -71,7 +71,7 @@ namespace {
 
 struct PodDesc {
     uint32_t pred = 0;
-    uint32_t heads[16];
+    uint32_t heads[16];                                 // selected pair ids
     int nheads = 0;
     int n_reg = 0, n_init = 0;
     bool ovh = false;
@@ -82,6 +82,13 @@ struct PodDesc {
         heads[nheads++] = h;
     }
 };
+
+// Pair id of a (group key, value) that no group selects: the generator's own interning
+// of "other" values, above the group pairs (numbering rule, include/escalator_hip.h).
+// `v` < n_groups stands for the value "g<v>", larger ones for values no group uses.
+uint32_t other_pair(const esc_synth& S, int key, uint32_t v) {
+    return S.gi.n_gp + (uint32_t)key * ((uint32_t)S.p.n_groups + 2000u) + v;
+}
 
 // The object-level pod that index i stands for.  Its fields map 1:1 onto esc_pod_obj:
 // owner kind DaemonSet, config.source=file, a nodeSelector, a required node affinity
@@ -95,10 +102,10 @@ void gen_pod(const esc_synth& S, int64_t i, PodDesc& d) {
     if (S.p.config == 1) {                              // 1 group, every non-DS pod selects it
         if (r < 500) d.pred |= ESC_PF_DAEMONSET;
         d.pred |= ESC_PF_HAS_SEL;
-        d.add_head(S.pod_head_of[0]);
+        d.add_head(S.pair_of[0]);
     } else if (r < 500) {                               // daemonset with a selector
         d.pred |= ESC_PF_DAEMONSET | ESC_PF_HAS_SEL;
-        if (nnd) d.add_head(S.pod_head_of[pick(1)]);
+        if (nnd) d.add_head(S.pair_of[pick(1)]);
     } else if (r < 550) {                               // static pod, no selector
         d.pred |= ESC_PF_STATIC;
     } else if (r < 550 + S.default_bp) {                // default-group pod (~one group's share)
@@ -110,11 +117,11 @@ void gen_pod(const esc_synth& S, int64_t i, PodDesc& d) {
         const int32_t k1 = S.key_id[g1];
         auto aff_head = [&](int32_t gk) {               // (key(g1), value(gk)) is a group pair
             const int32_t c = S.canon[gk];              // iff key(gk) == key(g1)
-            return S.key_id[c] == k1 ? S.pod_head_of[c] : NONE;
+            return S.key_id[c] == k1 ? S.pair_of[c] : other_pair(S, k1, (uint32_t)c);
         };
         if (sub < 70) {                                 // nodeSelector only
             d.pred |= ESC_PF_HAS_SEL;
-            d.add_head(S.pod_head_of[g1]);
+            d.add_head(S.pair_of[g1]);
         } else if (sub < 90) {                          // affinity In with 1-3 values
             d.pred |= ESC_PF_AFF_BLOCK;
             const int nv = 1 + (int)(rnd(seed, 1, i, 4) % 3);
@@ -123,7 +130,7 @@ void gen_pod(const esc_synth& S, int64_t i, PodDesc& d) {
             if (nv > 2) d.add_head(aff_head(pick(6)));
         } else {                                        // both (duplicate pair -> counted once)
             d.pred |= ESC_PF_HAS_SEL | ESC_PF_AFF_BLOCK;
-            d.add_head(S.pod_head_of[g1]);
+            d.add_head(S.pair_of[g1]);
             d.add_head(aff_head(g1));
             d.add_head(aff_head(pick(7)));
         }
@@ -132,14 +139,12 @@ void gen_pod(const esc_synth& S, int64_t i, PodDesc& d) {
         if (x >= 100 && x < 150 && !S.pool_groups.empty()) {   // extra "pool" selector
             d.pred |= ESC_PF_HAS_SEL;
             int32_t gp = S.pool_groups[rnd(seed, 1, i, 9) % S.pool_groups.size()];
-            d.add_head(S.pod_head_of[S.canon[gp]]);
+            d.add_head(S.pair_of[S.canon[gp]]);
         }
-        if (x >= 200 && x < 300) d.pred |= ESC_PF_HAS_SEL;     // irrelevant "zone" selector
+        if (x >= 200 && x < 300) d.pred |= ESC_PF_HAS_SEL;     // "zone" selector: no group key, not carried
+        if (x >= 300 && x < 330)                                // a customer value no group has
+            d.add_head(other_pair(S, K_CUSTOMER, (uint32_t)S.p.n_groups + (uint32_t)(rnd(seed, 1, i, 11) % 1000)));
     }
-    // Every group sharing a matched pair is selected too (explicit group list, ascending).
-    const int nh = d.nheads;
-    for (int k = 0; k < nh; ++k)
-        for (uint32_t h = S.gi.pod_next[d.heads[k]]; h != NONE; h = S.gi.pod_next[h]) d.add_head(h);
     std::sort(d.heads, d.heads + d.nheads);
     // Containers: 90% one, 6% two, 3% three, 1% two + one init + overhead.
     const uint64_t c = rnd(seed, 1, i, 10) % 100;
@@ -260,11 +265,9 @@ void build_groups(esc_synth& S) {
     S.default_bp = dflt ? std::max<uint64_t>(1, std::min<uint64_t>(1000, 10000 / (uint64_t)G)) : 1000;
     S.mem_mib_max = p.config == 3 ? 8192 : 16384;
     S.gi.build(S.specs.data(), G);
-    S.pod_head_of.assign(G, NONE);
-    S.node_head_of.assign(G, NONE);
+    S.pair_of.assign(G, NONE);
     for (int32_t g = 0; g < G; ++g) {
-        S.pod_head_of[g] = S.gi.head(S.keys[g].c_str(), S.values[g].c_str(), 0);
-        S.node_head_of[g] = S.gi.head(S.keys[g].c_str(), S.values[g].c_str(), 1);
+        S.pair_of[g] = S.gi.gpair[g];
         if (g != S.gi.default_group) S.nondefault.push_back(g);
         if (S.key_id[g] == K_POOL && S.canon[g] == g) S.pool_groups.push_back(g);
     }
@@ -330,22 +333,17 @@ void gen_nodes(esc_synth& S) {
             const uint64_t b = rnd(p.seed, 2, j, 1) % 1000;
             if (b < 30) f |= ESC_NF_UNSCHED;
             else if (b < 130) f |= ESC_NF_TAINTED;
-            // labels: the group's pair, sometimes a "pool" pair as well; every group
-            // selecting one of them is a member (explicit list, ascending)
+            // label pairs (group keys only): the group's own pair, sometimes a "pool" pair
+            // as well; 1% of nodes carry a customer value no group has instead.
             uint32_t grp[8];
             int ng = 0;
-            auto add_chain = [&](uint32_t h) {
-                for (; h != NONE; h = S.gi.node_next[h]) {
-                    bool dup = false;
-                    for (int k = 0; k < ng; ++k) dup |= grp[k] == h;
-                    if (!dup && ng < 7) grp[ng++] = h;
-                }
-            };
-            add_chain(S.node_head_of[c]);
+            const bool orphan = p.config != 1 && rnd(p.seed, 2, j, 8) % 100 == 0;
+            grp[ng++] = orphan ? other_pair(S, K_CUSTOMER, (uint32_t)G + 1000 + (uint32_t)(j % 97))
+                               : S.pair_of[c];
             if (p.config != 1 && S.key_id[c] != K_POOL && !S.pool_groups.empty() &&
                 rnd(p.seed, 2, j, 2) % 10 == 0) {
                 const int32_t gp = S.pool_groups[rnd(p.seed, 2, j, 3) % S.pool_groups.size()];
-                add_chain(S.node_head_of[S.canon[gp]]);
+                grp[ng++] = S.pair_of[S.canon[gp]];
             }
             std::sort(grp, grp + ng);
             s.label0[j] = ng ? grp[0] : NONE;

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define ESC_ABI_VERSION 1
+#define ESC_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- return codes */
 #define ESC_OK          0
@@ -184,17 +184,31 @@ typedef struct esc_node_obj {
 } esc_node_obj;
 
 /* ------------------------------------------------------------- packed snapshot
- * Struct-of-arrays layout streamed by the kernels.  Pods:
+ * Struct-of-arrays layout streamed by the kernels.
+ *
+ * Selector pairs.  Every group filter is a (label_key, label_value) test
+ * (NewPodAffinityFilterFunc node_group.go:218, NewNodeLabelFilterFunc :278), so pods and
+ * nodes carry the (key, value) pairs they could be matched on, interned to u32 "pair
+ * ids", and the kernels resolve pair -> groups on the device.  Numbering rule (shared by
+ * every packer and checked by the oracle): ids 0 .. n_group_pairs-1 are the distinct
+ * (label_key, label_value) of the context's groups in order of first appearance
+ * (esc_ctx_pair_id); any other (key, value) whose key is some group's label_key gets an
+ * id in [n_group_pairs, ESC_PAIR_LIMIT) that matches no group.  Keys no group uses are
+ * never looked up by any filter and are not carried.
+ *
+ * Pods:
  *   flags  u32  ESC_PF_* bits + counts of extra records
  *   cpu0   u32  cpu (millicores) of the inline regular container
  *   mem0   i64  memory (bytes)   of the inline regular container
- *   pair0  u32  lowest group the pod's (key,value) pairs select, ESC_NONE if none
+ *   pair0  u32  lowest pair id the pod selects through Spec.NodeSelector or an "In"
+ *               expression of a required node-affinity term, ESC_NONE if none
  *   xc_cpu/xc_mem i64  extra containers per pod: [regular extras][init][overhead]
- *   xp_group u32       the other selected groups, ascending (every group sharing a
- *                      matched pair is listed; at most 63 extra per pod)
+ *   xp_pair u32        the pod's other pair ids, ascending, de-duplicated (<= 63)
  * Nodes:
- *   nflags u32, label0 u32, ncpu i64, nmem i64, created i64, xl_group u32.        */
+ *   nflags u32, label0 u32 (lowest label pair id), ncpu i64, nmem i64, created i64,
+ *   xl_pair u32 (other label pair ids, ascending).                                  */
 #define ESC_NONE 0xFFFFFFFFu
+#define ESC_PAIR_LIMIT 0x7FFFFFFFu   /* pair ids are < this */
 
 #define ESC_PF_DAEMONSET   (1u << 0)   /* PodIsDaemonSet  util.go:11   (also marks padding) */
 #define ESC_PF_STATIC      (1u << 1)   /* PodIsStatic     util.go:21   */
@@ -203,14 +217,14 @@ typedef struct esc_node_obj {
 #define ESC_PF_HAS_OVH     (1u << 4)   /* overhead record present (Spec.Overhead != nil) */
 #define ESC_PF_XREG_SHIFT  8           /* bits  8..15: regular containers beyond the inline one */
 #define ESC_PF_XINIT_SHIFT 16          /* bits 16..23: init containers                         */
-#define ESC_PF_XPAIR_SHIFT 24          /* bits 24..29: extra selected groups (xp_group)         */
+#define ESC_PF_XPAIR_SHIFT 24          /* bits 24..29: extra selector pairs (xp_pair)            */
 #define ESC_PF_CNT_MASK    0xFFu
 #define ESC_PF_PAIR_MASK   0x3Fu
 
 #define ESC_NF_UNSCHED     (1u << 0)   /* Spec.Unschedulable           controller.go:141 */
 #define ESC_NF_TAINTED     (1u << 1)   /* has atlassian.com/escalator  taint.go:31,80    */
 #define ESC_NF_TRACKED     (1u << 2)   /* in some group's dry-mode taintTracker controller.go:128 */
-#define ESC_NF_XLBL_SHIFT  8           /* bits 8..15: extra selected groups (xl_group)          */
+#define ESC_NF_XLBL_SHIFT  8           /* bits 8..15: extra label pairs (xl_pair)                */
 
 typedef struct esc_pod_soa {
     int64_t         n_pods;
@@ -221,7 +235,7 @@ typedef struct esc_pod_soa {
     const int64_t*  xc_cpu;
     const int64_t*  xc_mem;
     int64_t         n_xc;
-    const uint32_t* xp_group;
+    const uint32_t* xp_pair;
     int64_t         n_xp;
 } esc_pod_soa;
 
@@ -232,7 +246,7 @@ typedef struct esc_node_soa {
     const int64_t*  cpu;
     const int64_t*  mem;
     const int64_t*  created_ns;
-    const uint32_t* xl_group;
+    const uint32_t* xl_pair;
     int64_t         n_xl;
     const int32_t*  trk_node;    /* dry-mode taintTracker entries resolved to (node, group), */
     const int32_t*  trk_group;   /* sorted by (node, group); may be NULL when n_trk == 0     */
@@ -259,13 +273,16 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
 int32_t esc_ctx_destroy(esc_ctx* ctx);
 int32_t esc_ctx_set_stream(esc_ctx* ctx, void* hip_stream);   /* NULL = ctx-owned stream */
 int32_t esc_ctx_num_groups(const esc_ctx* ctx);
-/* Head group of (key,value) for pods (side 0, default group excluded) or nodes (side 1). */
-uint32_t esc_ctx_pair_head(const esc_ctx* ctx, const char* key, const char* value, int32_t side);
+/* Pair id of (key,value) if some group selects it (the numbering rule above), else ESC_NONE. */
+uint32_t esc_ctx_pair_id(const esc_ctx* ctx, const char* key, const char* value);
+/* Number of distinct group pairs (ids 0 .. n-1). */
+int32_t  esc_ctx_num_group_pairs(const esc_ctx* ctx);
 
 /* ------------------------------------------------------------- K0 host packer
- * Replaces the per-group List()+filter object walk (pkg/k8s/pod_listers.go:33,
- * node_listers.go:33, pkg/controller/node_group.go:208-287): interns (key,value) pairs
- * against the context's groups and packs the SoA above.                             */
+ * One pass over *v1.Pod / *v1.Node field copies: evaluates the object predicates
+ * (util.go:11-24, node_group.go:208-215, :271-273, taint.go:80), interns the (key,value)
+ * pairs whose key is a group label key, and packs the SoA above.  Which group a pair
+ * selects is decided on the device (K1/K2), not here.                               */
 typedef struct esc_packer esc_packer;
 int32_t esc_packer_create(const esc_ctx* ctx, esc_packer** out);
 int32_t esc_packer_destroy(esc_packer* pk);

@@ -25,9 +25,12 @@
  *
  * Parity of this file is pinned through oracle/oracle.py (checked against every
  * transcribed reference test in tests/golden/) by tests/test_pack_parity.py.
- * Group membership is read from the packed lists (pair0/xp_group, label0/xl_group list
- * every selecting group); the (key,value) matching that produced them is checked by the
- * literal oracle against the packer on objects.
+ * Group membership: a pod / node carries interned (key, value) pair ids (pair0 + xp,
+ * label0 + xl); group g selects pair gpair[g] (the numbering rule of
+ * include/escalator_hip.h, restated in oracle/soa.py from the group specs).  A pod is
+ * in a non-default group g iff gpair[g] is among its pairs (NewPodAffinityFilterFunc,
+ * node_group.go:218-253); a node iff gpair[g] is among its label pairs
+ * (NewNodeLabelFilterFunc, node_group.go:278-287).
  * Build: gcc -O2 -ffp-contract=off (oracle/Makefile).
  */
 #include <math.h>
@@ -88,6 +91,29 @@ static int node_class(uint32_t f, int dry, const int32_t* tn, const int32_t* tg,
     return (f & NF_TAINTED) ? 1 : 0;
 }
 
+/* pair id -> groups selecting it, ascending (a chain head[q] -> nxt[g]); pods skip the
+ * default group (client.go:58-64 gives it NewPodDefaultFilterFunc instead). */
+typedef struct { int32_t* head; int32_t* nxt; uint32_t n_gp; } PairIdx;
+
+static int pair_idx(PairIdx* x, const uint32_t* gpair, uint32_t n_gp, int32_t G, int32_t skip) {
+    x->head = (int32_t*)malloc(sizeof(int32_t) * (n_gp + 1));
+    x->nxt = (int32_t*)malloc(sizeof(int32_t) * ((size_t)G + 1));
+    x->n_gp = n_gp;
+    if (!x->head || !x->nxt) return -1;
+    for (uint32_t q = 0; q < n_gp; ++q) x->head[q] = -1;
+    for (int32_t g = G - 1; g >= 0; --g) {
+        x->nxt[g] = -1;
+        if (g == skip || gpair[g] >= n_gp) continue;
+        x->nxt[g] = x->head[gpair[g]];
+        x->head[gpair[g]] = g;
+    }
+    return 0;
+}
+
+static void pair_idx_free(PairIdx* x) { free(x->head); free(x->nxt); }
+
+static int32_t first_group(const PairIdx* x, uint32_t q) { return q < x->n_gp ? x->head[q] : -1; }
+
 static void emit_out(const Acc* a, int32_t G, const int64_t* ncpu, const int64_t* nmem, int64_t* out) {
     for (int32_t g = 0; g < G; ++g) {
         int64_t* o = out + (int64_t)g * 13;
@@ -106,17 +132,17 @@ static void emit_out(const Acc* a, int32_t G, const int64_t* ncpu, const int64_t
 
 static void node_pass(Acc* a, int64_t lo, int64_t hi, const uint32_t* nflags, const uint32_t* label0,
                       const int64_t* ncpu, const int64_t* nmem, const uint32_t* xl, const int32_t* tn,
-                      const int32_t* tg, int64_t n_trk, const uint8_t* dry, int64_t n_all) {
+                      const int32_t* tg, int64_t n_trk, const uint8_t* dry, int64_t n_all, const PairIdx* px) {
     uint64_t q = 0;
     for (int64_t i = 0; i < lo && i < n_all; ++i) q += xlbl(nflags[i]);
     for (int64_t i = lo; i < hi; ++i) {
         const uint32_t f = nflags[i];
         const uint32_t nx = xlbl(f);
         for (uint32_t k = 0; k <= nx; ++k) {
-            uint32_t g = k == 0 ? label0[i] : xl[q++];
-            if (g != NONE) {                               /* every selecting group is listed */
+            const uint32_t pr = k == 0 ? label0[i] : xl[q++];
+            for (int32_t g = first_group(px, pr); g >= 0; g = px->nxt[g]) {
                 if (a[g].first < 0) a[g].first = i;        /* allNodes[0] in lister order */
-                const int c = node_class(f, dry[g], tn, tg, n_trk, i, (int32_t)g);
+                const int c = node_class(f, dry[g], tn, tg, n_trk, i, g);
                 if (c == 0) { a[g].nunt++; a[g].ncpu += ncpu[i]; a[g].nmem += nmem[i]; }
                 else if (c == 1) a[g].ntaint++;
                 else a[g].ncord++;
@@ -129,10 +155,11 @@ int orc_totals(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, cons
                const uint32_t* pair0, const int64_t* xc_cpu, const int64_t* xc_mem, const uint32_t* xp,
                int64_t n_nodes, const uint32_t* nflags, const uint32_t* label0, const int64_t* ncpu,
                const int64_t* nmem, const uint32_t* xl, const int32_t* tn, const int32_t* tg, int64_t n_trk,
-               int64_t node_lo, int64_t node_hi, int32_t G, int32_t default_group, const uint8_t* dry,
-               int64_t* out) {
+               int64_t node_lo, int64_t node_hi, int32_t G, int32_t default_group, const uint32_t* gpair,
+               uint32_t n_gp, const uint8_t* dry, int64_t* out) {
     Acc* a = (Acc*)calloc((size_t)G, sizeof(Acc));
-    if (!a) return -1;
+    PairIdx pp, np;
+    if (!a || pair_idx(&pp, gpair, n_gp, G, default_group) || pair_idx(&np, gpair, n_gp, G, -1)) return -1;
     for (int32_t g = 0; g < G; ++g) a[g].first = -1;
     uint64_t oc = 0, op = 0;
     for (int64_t p = 0; p < n_pods; ++p) {
@@ -146,12 +173,16 @@ int orc_totals(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, cons
         }
         const uint32_t nx = xpair(f);
         for (uint32_t k = 0; k <= nx; ++k) {
-            uint32_t g = k == 0 ? pair0[p] : xp[op++];
-            if (g != NONE) { a[g].pcpu += cpu; a[g].pmem += mem; a[g].npod++; }
+            const uint32_t pr = k == 0 ? pair0[p] : xp[op++];
+            for (int32_t g = first_group(&pp, pr); g >= 0; g = pp.nxt[g]) {
+                a[g].pcpu += cpu; a[g].pmem += mem; a[g].npod++;
+            }
         }
     }
-    node_pass(a, node_lo, node_hi, nflags, label0, ncpu, nmem, xl, tn, tg, n_trk, dry, n_nodes);
+    node_pass(a, node_lo, node_hi, nflags, label0, ncpu, nmem, xl, tn, tg, n_trk, dry, n_nodes, &np);
     emit_out(a, G, ncpu, nmem, out);
+    pair_idx_free(&pp);
+    pair_idx_free(&np);
     free(a);
     return 0;
 }
@@ -164,8 +195,8 @@ int orc_ref_scan(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, co
                  const uint32_t* pair0, const int64_t* xc_cpu, const int64_t* xc_mem, const uint32_t* xp,
                  int64_t n_nodes, const uint32_t* nflags, const uint32_t* label0, const int64_t* ncpu,
                  const int64_t* nmem, const uint32_t* xl, const int32_t* tn, const int32_t* tg, int64_t n_trk,
-                 int32_t G, int32_t default_group, const uint8_t* dry, int32_t g_lo, int32_t g_hi,
-                 int64_t* out) {
+                 int32_t G, int32_t default_group, const uint32_t* gpair, const uint8_t* dry, int32_t g_lo,
+                 int32_t g_hi, int64_t* out) {
     Acc* a = (Acc*)calloc((size_t)G, sizeof(Acc));
     if (!a) return -1;
     for (int32_t g = 0; g < G; ++g) a[g].first = -1;
@@ -180,10 +211,10 @@ int orc_ref_scan(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, co
                 if (g == default_group) {
                     member = !(f & (PF_STATIC | PF_SEL | PF_AFF));
                 } else {
-                    const uint32_t nx = xpair(f);
+                    const uint32_t nx = xpair(f);          /* NodeSelector[K]==V || In(K,V) */
                     for (uint32_t k = 0; k <= nx && !member; ++k) {
                         uint32_t h = k == 0 ? pair0[p] : xp[op + k - 1];
-                        member = (h == (uint32_t)g);
+                        member = (h == gpair[g]);
                     }
                 }
             }
@@ -199,9 +230,9 @@ int orc_ref_scan(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, co
         for (int64_t i = 0; i < n_nodes; ++i) {
             const uint32_t f = nflags[i];
             int member = 0;
-            for (uint32_t k = 0; k <= xlbl(f); ++k) {
+            for (uint32_t k = 0; k <= xlbl(f); ++k) {              /* Labels[K] == V */
                 uint32_t h = k == 0 ? label0[i] : xl[q + k - 1];
-                member |= (h == (uint32_t)g);
+                member |= (h == gpair[g]);
             }
             q += xlbl(f);
             if (!member) continue;
@@ -324,7 +355,8 @@ static int cmp_ki(const void* a, const void* b) {
  * writes up to cap indices. */
 int64_t orc_order(int64_t n_nodes, const uint32_t* nflags, const uint32_t* label0, const int64_t* created,
                   const uint32_t* xl, const int32_t* tn, const int32_t* tg, int64_t n_trk, int64_t lo, int64_t hi,
-                  const uint8_t* dry, int32_t group, int32_t which, int64_t* out, int64_t cap) {
+                  const uint8_t* dry, const uint32_t* gpair, int32_t group, int32_t which, int64_t* out,
+                  int64_t cap) {
     KI* v = (KI*)malloc(sizeof(KI) * (size_t)(hi - lo + 1));
     int64_t m = 0;
     uint64_t q = 0;
@@ -334,7 +366,7 @@ int64_t orc_order(int64_t n_nodes, const uint32_t* nflags, const uint32_t* label
         int member = 0;
         for (uint32_t k = 0; k <= xlbl(f); ++k) {
             uint32_t h = k == 0 ? label0[i] : xl[q + k - 1];
-            member |= (h == (uint32_t)group);
+            member |= (h == gpair[group]);
         }
         q += xlbl(f);
         if (!member) continue;

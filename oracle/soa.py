@@ -2,13 +2,13 @@
 
 TEST INFRASTRUCTURE ONLY (tests/, __graft_entry__.smoke(), bench.py cpu_baseline).
 
-``group_tables`` restates the group/label matching of the reference independently of
-the product's interner: a pod matches a labelled group iff one of its (key, value)
-pairs equals the group's (label_key, label_value) (NewPodAffinityFilterFunc,
+``group_tables`` restates the pair numbering of include/escalator_hip.h from the group
+specs (pair ids 0..n_gp-1 = distinct (label_key, label_value) in order of first
+appearance), independently of the product's interner.  The C oracle then matches: a pod
+is in a labelled group iff one of its pair ids is the group's (NewPodAffinityFilterFunc,
 pkg/controller/node_group.go:218-253); the group named "default" takes pods through
 NewPodDefaultFilterFunc instead (node_group.go:256, controller/client.go:58-64); nodes
-match any group by label (NewNodeLabelFilterFunc node_group.go:278, :301).  Groups that
-share one (key, value) pair form a chain head -> next (lowest index first).
+match any group by label pair (NewNodeLabelFilterFunc node_group.go:278, :301).
 """
 from __future__ import annotations
 
@@ -53,26 +53,13 @@ def lib():
 def group_tables(groups: list[dict]) -> dict:
     G = len(groups)
     default = next((i for i, g in enumerate(groups) if g["name"] == "default"), -1)
-    pod_next = np.full(G, NONE, np.uint32)
-    node_next = np.full(G, NONE, np.uint32)
-    pod_head, node_head, pod_tail, node_tail = {}, {}, {}, {}
+    ids: dict = {}
+    gpair = np.zeros(G, np.uint32)
     for g, spec in enumerate(groups):
         k = (spec.get("label_key", ""), spec.get("label_value", ""))
-        if k in node_tail:
-            node_next[node_tail[k]] = g
-        else:
-            node_head[k] = g
-        node_tail[k] = g
-        if g == default:
-            continue
-        if k in pod_tail:
-            pod_next[pod_tail[k]] = g
-        else:
-            pod_head[k] = g
-        pod_tail[k] = g
+        gpair[g] = ids.setdefault(k, len(ids))
     dry = np.array([1 if s.get("dry_mode") else 0 for s in groups], np.uint8)
-    return {"G": G, "default": default, "pod_next": pod_next, "node_next": node_next, "pod_head": pod_head,
-            "node_head": node_head, "dry": dry}
+    return {"G": G, "default": default, "gpair": gpair, "n_gp": len(ids), "pair_ids": ids, "dry": dry}
 
 
 def _p(a, t):
@@ -98,16 +85,17 @@ def totals(pods: dict, nodes: dict, groups: list[dict], node_lo: int = 0, node_h
     keep = [pods, nodes, t]
     pa = [C.c_int64(len(pods["flags"])), _p(pods["flags"], C.c_uint32), _p(pods["cpu0"], C.c_uint32),
           _p(pods["mem0"], C.c_int64), _p(pods["pair0"], C.c_uint32), _p(pods["xc_cpu"], C.c_int64),
-          _p(pods["xc_mem"], C.c_int64), _p(pods["xp_group"], C.c_uint32)]
-    na = _node_args(nodes) + [_p(nodes["xl_group"], C.c_uint32), _p(nodes["trk_node"], C.c_int32),
+          _p(pods["xc_mem"], C.c_int64), _p(pods["xp_pair"], C.c_uint32)]
+    na = _node_args(nodes) + [_p(nodes["xl_pair"], C.c_uint32), _p(nodes["trk_node"], C.c_int32),
                               _p(nodes["trk_group"], C.c_int32), C.c_int64(len(nodes["trk_node"]))]
     if reference_shaped:
         lo, hi_g = g_range or (0, G)
-        rc = lib().orc_ref_scan(*pa, *na, C.c_int32(G), C.c_int32(t["default"]), _p(t["dry"], C.c_uint8),
-                                C.c_int32(lo), C.c_int32(hi_g), _p(out, C.c_int64))
+        rc = lib().orc_ref_scan(*pa, *na, C.c_int32(G), C.c_int32(t["default"]), _p(t["gpair"], C.c_uint32),
+                                _p(t["dry"], C.c_uint8), C.c_int32(lo), C.c_int32(hi_g), _p(out, C.c_int64))
     else:
         rc = lib().orc_totals(*pa, *na, C.c_int64(node_lo), C.c_int64(hi), C.c_int32(G), C.c_int32(t["default"]),
-                              _p(t["dry"], C.c_uint8), _p(out, C.c_int64))
+                              _p(t["gpair"], C.c_uint32), C.c_uint32(t["n_gp"]), _p(t["dry"], C.c_uint8),
+                              _p(out, C.c_int64))
     del keep
     assert rc == 0
     return out
@@ -142,10 +130,10 @@ def order(nodes: dict, groups: list[dict], group: int, which: int, node_lo: int 
     hi = n if node_hi is None else node_hi
     out = np.zeros(max(hi - node_lo, 1), np.int64)
     m = lib().orc_order(C.c_int64(n), _p(nodes["flags"], C.c_uint32), _p(nodes["label0"], C.c_uint32),
-                        _p(nodes["created_ns"], C.c_int64), _p(nodes["xl_group"], C.c_uint32),
+                        _p(nodes["created_ns"], C.c_int64), _p(nodes["xl_pair"], C.c_uint32),
                         _p(nodes["trk_node"], C.c_int32), _p(nodes["trk_group"], C.c_int32),
                         C.c_int64(len(nodes["trk_node"])), C.c_int64(node_lo), C.c_int64(hi),
-                        _p(t["dry"], C.c_uint8), C.c_int32(group),
+                        _p(t["dry"], C.c_uint8), _p(t["gpair"], C.c_uint32), C.c_int32(group),
                         C.c_int32(which), _p(out, C.c_int64), C.c_int64(len(out)))
     m = int(m)
     out = out[:m]

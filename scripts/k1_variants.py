@@ -11,12 +11,13 @@ import numpy as np  # noqa: E402
 
 cfg = int(os.environ.get("CFG", 4))
 P, N, G = {4: (100_000_000, 1_000_000, 10_000), 2: (1_000_000, 10_000, 100), 3: (10_000_000, 100_000, 100)}[cfg]
-variants = [int(v) for v in os.environ.get("VARIANTS", "0,2,3,9").split(",")]
+variants = [int(v) for v in os.environ.get("VARIANTS", "0,2,9,10,11").split(",")]
 rounds = int(os.environ.get("ROUNDS", 3))
 import escalator_amd as esc  # noqa: E402
 
 s = esc.Synth(P, N, G, config=cfg, seed=0xE5CA1A7E00000000 + cfg, threads=16)
-bytes_k1 = s.pod_c.n_pods * 20 + s.pod_c.n_xc * 16 + s.pod_c.n_xp * 4 + ((s.pod_c.n_pods + 255) // 256) * 8
+from escalator_amd import layout  # noqa: E402
+bytes_k1 = layout.pod_bytes(s.pods()["flags"], s.pod_c.n_xc, s.pod_c.n_xp)
 ctxs = {}
 for v in variants:
     os.environ["ESC_K1_VARIANT"] = str(v)

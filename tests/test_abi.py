@@ -14,7 +14,7 @@ def test_library_exports_every_header_symbol():
     assert len(fns) >= 40
     assert [f for f in fns if not hasattr(lib, f)] == []
     assert sorted(set(fns) - set(L._SIGS)) == []
-    assert lib.esc_abi_version() == 1
+    assert lib.esc_abi_version() == 2
 
 
 def test_status_strings_verbatim():
@@ -45,11 +45,11 @@ def test_group_interning_matches_oracle_tables():
               {"name": "z", "label_key": "pool", "label_value": "a"}]
     ctx = Context(groups, device=-1)
     t = soa.group_tables(groups)
-    for (k, v), h in t["pod_head"].items():
-        assert ctx.lib.esc_ctx_pair_head(ctx.handle, k.encode(), v.encode(), 0) == h
-    for (k, v), h in t["node_head"].items():
-        assert ctx.lib.esc_ctx_pair_head(ctx.handle, k.encode(), v.encode(), 1) == h
-    assert ctx.lib.esc_ctx_pair_head(ctx.handle, b"customer", b"zz", 0) == 0xFFFFFFFF
+    assert t["n_gp"] == 2 and list(t["gpair"]) == [0, 0, 0, 1]
+    assert ctx.lib.esc_ctx_num_group_pairs(ctx.handle) == t["n_gp"]
+    for (k, v), i in t["pair_ids"].items():
+        assert ctx.lib.esc_ctx_pair_id(ctx.handle, k.encode(), v.encode()) == i
+    assert ctx.lib.esc_ctx_pair_id(ctx.handle, b"customer", b"zz") == 0xFFFFFFFF
 
 
 def test_synth_shards_are_slices_and_single_pass_equals_reference_shaped():

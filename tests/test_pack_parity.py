@@ -107,9 +107,10 @@ def test_packer_encoding_details():
         {"owner_kinds": ["DaemonSet"], "containers": []},
     ]
     P, N = ctx.pack(pods, [])
-    # pod 0: (customer,a) selects groups 1 and 2 (shared pair), (pool,p) group 3; deduped across
-    # selector + affinity; the default group (0) is never reached through a pair
-    assert P["pair0"][0] == 1 and list(P["xp_group"]) == [2, 3]
+    # pair ids (numbering rule): (customer,default)=0, (customer,a)=1 shared by groups a and b,
+    # (pool,p)=2; (customer,zz) is a group-key value no group has -> first packer id, 3.
+    # pod 0 carries {1, 2, 3}, deduped across selector + affinity; group resolution is K1's
+    assert P["pair0"][0] == 1 and list(P["xp_pair"]) == [2, 3]
     assert (P["flags"][0] >> 24) & 63 == 2 and P["flags"][0] & 0b1100 == 0b1100
     # pod 1: first container cpu does not fit u32 -> all regulars are extras; absent init cpu = INT64_MIN;
     # an overhead map with no keys adds nothing and is dropped
