@@ -68,7 +68,10 @@ hipError_t launch_node_reduce(const NodeDev& n, const GroupDev& g, int n_chunk, 
                               uint64_t* part, int64_t* wide, hipStream_t st);
 hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* pod_part, int nblk,
                           const uint64_t* node_part, int n_chunk, int64_t* wide_pod, int64_t* wide_node,
-                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st);
+                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, bool node_reset,
+                          hipStream_t st);
+hipError_t launch_node_atomic(const NodeDev& n, const GroupDev& g, uint64_t* rows, int64_t* wide, hipStream_t st);
+hipError_t launch_fill(uint64_t* p, int64_t n, uint64_t v, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
 hipError_t launch_wide_nodes(const NodeDev& n, const GroupDev& g, int64_t* wide, hipStream_t st);
 hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* words,

@@ -100,6 +100,11 @@ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ?
 __device__ __forceinline__ uint32_t node_code(const GroupDev& G, uint32_t pair) {
     return pair < G.n_gp ? G.node_code[pair] : NONE;
 }
+// Membership entries carry the group's dry-mode bit (ESC_NODE_DRY_BIT) next to its id, so
+// classifying a node needs no per-group load.
+__device__ __forceinline__ uint32_t mg(uint32_t m) { return m & NODE_GROUP_MASK; }
+__device__ __forceinline__ bool mdry(uint32_t m) { return (m & NODE_DRY_BIT) != 0; }
+
 template <class F>
 __device__ __forceinline__ void for_code(const GroupDev& G, uint32_t code, F&& emit) {
     if (code < CODE_MULTI) {
@@ -214,11 +219,14 @@ __device__ __forceinline__ TileBases tile_bases(const PodDev& P, int64_t t) {
 struct CTile {
     uint32_t f, c, p;
     uint64_t m;
-    unsigned long long xcc0, xcm0, xcc1, xcm1;
-    uint32_t xp0, xp1;
+    unsigned long long xcc0, xcm0, xcc1, xcm1;   // records l and l+64 (clamped: only the
+    uint32_t xp0, xp1;                           // first xcn / xpn are meaningful)
     TileBases b;
 };
 
+// Every load is issued unconditionally (indices clamped into the tile's records; the
+// record arrays carry one element of padding), so the compiler's vmcnt accounting can
+// leave a second tile's loads in flight while the first is processed.
 __device__ __forceinline__ void c_load(const PodDev& P, int64_t t, uint32_t lane, const TileBases& b, CTile& T) {
     const int64_t i = P.s_tiles * TILE + t * CTILE + lane;
     T.b = b;
@@ -226,18 +234,15 @@ __device__ __forceinline__ void c_load(const PodDev& P, int64_t t, uint32_t lane
     T.c = P.cpu0[i];
     T.m = (uint64_t)P.mem0[i];
     T.p = P.pair0[i];
-    T.xcc0 = T.xcm0 = T.xcc1 = T.xcm1 = 0;
-    T.xp0 = T.xp1 = NONE;
-    if (lane < b.xcn) {
-        T.xcc0 = (unsigned long long)P.xc_cpu[b.xcb + lane];
-        T.xcm0 = (unsigned long long)P.xc_mem[b.xcb + lane];
-    }
-    if (lane + 64 < b.xcn) {
-        T.xcc1 = (unsigned long long)P.xc_cpu[b.xcb + 64 + lane];
-        T.xcm1 = (unsigned long long)P.xc_mem[b.xcb + 64 + lane];
-    }
-    if (lane < b.xpn) T.xp0 = P.xp[b.xpb + lane];
-    if (lane + 64 < b.xpn) T.xp1 = P.xp[b.xpb + 64 + lane];
+    const uint32_t lc = (b.xcn ? b.xcn : 1u) - 1u, lp = (b.xpn ? b.xpn : 1u) - 1u;
+    const uint32_t c0 = b.xcb + min(lane, lc), c1 = b.xcb + min(lane + 64, lc);
+    const uint32_t p0 = b.xpb + min(lane, lp), p1 = b.xpb + min(lane + 64, lp);
+    T.xcc0 = (unsigned long long)P.xc_cpu[c0];
+    T.xcm0 = (unsigned long long)P.xc_mem[c0];
+    T.xcc1 = (unsigned long long)P.xc_cpu[c1];
+    T.xcm1 = (unsigned long long)P.xc_mem[c1];
+    T.xp0 = P.xp[p0];
+    T.xp1 = P.xp[p1];
 }
 
 template <int ABLATE>
@@ -326,23 +331,35 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     if (!(ABLATE & 2)) {
         const int64_t per = (P.s_tiles + gridDim.x - 1) / gridDim.x;
         const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(lo + per, P.s_tiles);
-        for (int64_t t = lo + wid; t < hi; t += NW) {
-            STile A;
+        // Two tiles per wave iteration (10 KB in flight per wave); B's loads are issued
+        // unconditionally (a repeat of A at the end) so they stay in flight during A.
+        for (int64_t t = lo + wid; t < hi; t += 2 * NW) {
+            const bool has_b = t + NW < hi;
+            STile A, B;
             s_load(P, t, lane, A);
+            s_load(P, has_b ? t + NW : t, lane, B);
             s_process<ABLATE>(G, K, A);
+            if (has_b) s_process<ABLATE>(G, K, B);
         }
     }
     if (!(ABLATE & 4)) {
         const int64_t per = (P.c_tiles + gridDim.x - 1) / gridDim.x;
         const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(lo + per, P.c_tiles);
+        // Two tiles per wave iteration: B's loads stay in flight while A is processed.
+        // Offsets are scalar loads fetched one iteration ahead.
         int64_t t = lo + wid;
-        TileBases nb{0, 0, 0, 0};
-        if (t < hi) nb = tile_bases(P, t);                // next tile's offsets: scalar, one ahead
-        for (; t < hi; t += NW) {
-            CTile A;
-            c_load(P, t, lane, nb, A);
-            if (t + NW < hi) nb = tile_bases(P, t + NW);
+        TileBases na{0, 0, 0, 0}, nb{0, 0, 0, 0};
+        if (t < hi) na = tile_bases(P, t);
+        nb = (t + NW < hi) ? tile_bases(P, t + NW) : na;
+        for (; t < hi; t += 2 * NW) {
+            const bool has_b = t + NW < hi;               // wave-uniform
+            CTile A, B;
+            c_load(P, t, lane, na, A);
+            c_load(P, has_b ? t + NW : t, lane, nb, B);   // a repeat of A when there is no B
+            if (t + 2 * NW < hi) na = tile_bases(P, t + 2 * NW);
+            nb = (t + 3 * NW < hi) ? tile_bases(P, t + 3 * NW) : na;
             if (A.b.xcn <= 128 && A.b.xpn <= 128) c_process<ABLATE>(G, K, A);
+            if (has_b && B.b.xcn <= 128 && B.b.xpn <= 128) c_process<ABLATE>(G, K, B);
         }
     }
     __syncthreads();
@@ -363,6 +380,10 @@ __global__ __launch_bounds__(64) void k_pod_bigtiles(PodDev P, GroupDev G, const
 
 __global__ __launch_bounds__(256) void k_zero(int64_t* __restrict__ p, int64_t n) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
+}
+
+__global__ __launch_bounds__(256) void k_fill(uint64_t* __restrict__ p, int64_t n, uint64_t v) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
 // =====================================================================  K1 (wide)
@@ -401,9 +422,8 @@ __device__ __forceinline__ bool tracked(const NodeDev& N, int32_t node, int32_t 
 
 // filterNodes classification (controller.go:125-150): 0 untainted, 1 tainted, 2 cordoned.
 // Dry mode separates only tracker members; cordoned nodes are not split out there.
-__device__ __forceinline__ int node_class(const NodeDev& N, const GroupDev& G, uint32_t f, int64_t i,
-                                          uint32_t g) {
-    if (G.dry[g]) return ((f & ESC_NF_TRACKED) && tracked(N, (int32_t)i, (int32_t)g)) ? 1 : 0;
+__device__ __forceinline__ int node_class(const NodeDev& N, uint32_t f, int64_t i, uint32_t m) {
+    if (mdry(m)) return ((f & ESC_NF_TRACKED) && tracked(N, (int32_t)i, (int32_t)mg(m))) ? 1 : 0;
     if (f & ESC_NF_UNSCHED) return 2;
     return (f & ESC_NF_TAINTED) ? 1 : 0;
 }
@@ -425,11 +445,11 @@ __device__ __forceinline__ void node_groups(const NodeDev& N, const GroupDev& G,
 
 // Exact (any-range) node contribution; WN_FIRST keeps ~index under atomicMax so the
 // all-zero row means "no member" and the accumulators can self-clean to zero.
-__device__ __forceinline__ void node_wide_add(const NodeDev& N, const GroupDev& G, int64_t* __restrict__ wide,
-                                              uint32_t f, int64_t i, uint32_t g, int64_t cpu, int64_t m) {
-    int64_t* r = wide + (int64_t)g * WN_K;
+__device__ __forceinline__ void node_wide_add(const NodeDev& N, int64_t* __restrict__ wide,
+                                              uint32_t f, int64_t i, uint32_t mb, int64_t cpu, int64_t m) {
+    int64_t* r = wide + (int64_t)mg(mb) * WN_K;
     atomicMax(reinterpret_cast<unsigned long long*>(r + WN_FIRST), ~(unsigned long long)i);
-    const int c = node_class(N, G, f, i, g);
+    const int c = node_class(N, f, i, mb);
     if (c == 0) {
         g_add(r + WN_CPU_LO, (int64_t)((uint64_t)cpu & 0xFFFFFFFFull));
         g_add(r + WN_CPU_HI, cpu >> 32);
@@ -441,7 +461,12 @@ __device__ __forceinline__ void node_wide_add(const NodeDev& N, const GroupDev& 
     }
 }
 
-// grid (n_chunk, n_gtile); LDS tile of gt groups: cc, mem, tc (u64), first (u32).
+// grid (n_gtile, n_chunk): the group tiles of one node chunk are adjacent in dispatch
+// order, so the chunk's repeat reads are served on-die.  LDS tile of gt groups: cc, mem,
+// tc (u64), first (u32).  Each thread carries NODE_ILP nodes per iteration so their
+// loads and pair-table gathers are in flight together.
+constexpr int NODE_ILP = 4;
+
 __global__ __launch_bounds__(BLOCK) void k_node_reduce(NodeDev N, GroupDev G, int32_t gt,
                                                        uint64_t* __restrict__ part,
                                                        int64_t* __restrict__ wide) {
@@ -452,32 +477,60 @@ __global__ __launch_bounds__(BLOCK) void k_node_reduce(NodeDev N, GroupDev G, in
     uint32_t* first = reinterpret_cast<uint32_t*>(lds + 3 * gt);
     for (int32_t i = threadIdx.x; i < gt; i += BLOCK) { cc[i] = 0; mem[i] = 0; tc[i] = 0; first[i] = NONE; }
     __syncthreads();
-    const uint32_t g_lo = blockIdx.y * (uint32_t)gt;
+    const uint32_t g_lo = blockIdx.x * (uint32_t)gt;
     const uint32_t g_n = (uint32_t)min(gt, G.G - (int32_t)g_lo);
     const int64_t n = N.hi - N.lo;
-    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t lo = N.lo + (int64_t)blockIdx.x * per;
+    const int64_t per = (n + gridDim.y - 1) / gridDim.y;
+    const int64_t lo = N.lo + (int64_t)blockIdx.y * per;
     const int64_t hi = imin64(N.hi, lo + per);
-    for (int64_t i = lo + threadIdx.x; i < hi; i += BLOCK) {
-        const uint32_t f = N.flags[i];
-        const int64_t cpu = N.cpu[i], m = N.mem[i];
-        if ((uint64_t)cpu >= (uint64_t)NODE_CPU_LIMIT || (uint64_t)m >= (uint64_t)NODE_MEM_LIMIT) {
-            node_groups(N, G, f, i, [&](uint32_t g) {
-                if (g - g_lo < g_n) node_wide_add(N, G, wide, f, i, g, cpu, m);
-            });
-            continue;
+    for (int64_t b = lo; b < hi; b += (int64_t)BLOCK * NODE_ILP) {
+        // three dependent rounds for NODE_ILP nodes at once: node words (+ offset of the
+        // extra label pairs), then pair codes and the first extra pair, then its code
+        uint32_t f[NODE_ILP], l0[NODE_ILP], xo[NODE_ILP], x1[NODE_ILP], code[NODE_ILP], xcode[NODE_ILP];
+        int64_t cpu[NODE_ILP], m[NODE_ILP];
+#pragma unroll
+        for (int k = 0; k < NODE_ILP; ++k) {
+            const int64_t i = b + threadIdx.x + (int64_t)k * BLOCK;
+            f[k] = 0; l0[k] = NONE; cpu[k] = 0; m[k] = 0; xo[k] = 0;
+            if (i < hi) {
+                f[k] = N.flags[i]; l0[k] = N.label0[i]; cpu[k] = N.cpu[i]; m[k] = N.mem[i]; xo[k] = N.xl_off[i];
+            }
         }
-        node_groups(N, G, f, i, [&](uint32_t g) {
-            const uint32_t k = g - g_lo;
-            if (k >= g_n) return;
-            atomicMin(first + k, (uint32_t)i);
-            const int c = node_class(N, G, f, i, g);
-            if (c == 0) { lds_add(cc + k, (uint64_t)cpu | (1ull << CNT_SHIFT)); lds_add(mem + k, (uint64_t)m); }
-            else lds_add(tc + k, c == 1 ? 1ull : (1ull << 32));
-        });
+#pragma unroll
+        for (int k = 0; k < NODE_ILP; ++k) {
+            code[k] = node_code(G, l0[k]);
+            x1[k] = nf_xlbl(f[k]) ? N.xl[xo[k]] : NONE;
+        }
+#pragma unroll
+        for (int k = 0; k < NODE_ILP; ++k) xcode[k] = node_code(G, x1[k]);
+#pragma unroll
+        for (int k = 0; k < NODE_ILP; ++k) {
+            const int64_t i = b + threadIdx.x + (int64_t)k * BLOCK;
+            if (i >= hi) continue;
+            const uint32_t fk = f[k];
+            const int64_t ck = cpu[k], mk = m[k];
+            if ((uint64_t)ck >= (uint64_t)NODE_CPU_LIMIT || (uint64_t)mk >= (uint64_t)NODE_MEM_LIMIT) {
+                node_groups(N, G, fk, i, [&](uint32_t mb) {
+                    if (mg(mb) - g_lo < g_n) node_wide_add(N, wide, fk, i, mb, ck, mk);
+                });
+                continue;
+            }
+            auto visit = [&](uint32_t mb) {
+                const uint32_t t = mg(mb) - g_lo;
+                if (t >= g_n) return;
+                atomicMin(first + t, (uint32_t)i);
+                const int c = node_class(N, fk, i, mb);
+                if (c == 0) { lds_add(cc + t, (uint64_t)ck | (1ull << CNT_SHIFT)); lds_add(mem + t, (uint64_t)mk); }
+                else lds_add(tc + t, c == 1 ? 1ull : (1ull << 32));
+            };
+            for_code(G, code[k], visit);
+            for_code(G, xcode[k], visit);
+            const uint32_t nx = nf_xlbl(fk);
+            for (uint32_t e = 1; e < nx; ++e) for_code(G, node_code(G, N.xl[xo[k] + e]), visit);
+        }
     }
     __syncthreads();
-    uint64_t* out = part + (int64_t)blockIdx.x * 4 * G.G + g_lo;
+    uint64_t* out = part + (int64_t)blockIdx.y * 4 * G.G + g_lo;
     for (uint32_t k = threadIdx.x; k < g_n; k += BLOCK) {
         out[k] = cc[k];
         out[G.G + k] = mem[k];
@@ -486,12 +539,42 @@ __global__ __launch_bounds__(BLOCK) void k_node_reduce(NodeDev N, GroupDev G, in
     }
 }
 
+// Node pass without group tiles (ESC_K2 variant 1, for many groups): every node is
+// read once and its memberships go straight to per-group global rows laid out like one
+// k_node_reduce chunk (cc, mem, tc, first), which K3 reads and resets.  Exact while a
+// node's cpu < 2^20 m and mem < 2^43 B and the rank streams <= 2^20 nodes (checked by the
+// host): the packed row words cannot carry.  Other nodes take the wide words.
+__global__ __launch_bounds__(256) void k_node_atomic(NodeDev N, GroupDev G, uint64_t* __restrict__ rows,
+                                                     int64_t* __restrict__ wide) {
+    const int64_t GG = G.G;
+    for (int64_t i = N.lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N.hi;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t f = N.flags[i];
+        const int64_t cpu = N.cpu[i], m = N.mem[i];
+        if ((uint64_t)cpu >= (uint64_t)NODE_CPU_LIMIT || (uint64_t)m >= (uint64_t)NODE_MEM_LIMIT_ATOMIC) {
+            node_groups(N, G, f, i, [&](uint32_t mb) { node_wide_add(N, wide, f, i, mb, cpu, m); });
+            continue;
+        }
+        node_groups(N, G, f, i, [&](uint32_t mb) {
+            const uint32_t g = mg(mb);
+            atomicMin(reinterpret_cast<unsigned long long*>(rows + 3 * GG + g), (unsigned long long)i);
+            const int c = node_class(N, f, i, mb);
+            if (c == 0) {
+                atomicAdd(reinterpret_cast<unsigned long long*>(rows + g), (unsigned long long)cpu | (1ull << CNT_SHIFT));
+                atomicAdd(reinterpret_cast<unsigned long long*>(rows + GG + g), (unsigned long long)m);
+            } else {
+                atomicAdd(reinterpret_cast<unsigned long long*>(rows + 2 * GG + g), c == 1 ? 1ull : (1ull << 32));
+            }
+        });
+    }
+}
+
 __global__ __launch_bounds__(256) void k_node_wide(NodeDev N, GroupDev G, int64_t* __restrict__ wide) {
     for (int64_t i = N.lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N.hi;
          i += (int64_t)gridDim.x * blockDim.x) {
         const uint32_t f = N.flags[i];
         const int64_t cpu = N.cpu[i], m = N.mem[i];
-        node_groups(N, G, f, i, [&](uint32_t g) { node_wide_add(N, G, wide, f, i, g, cpu, m); });
+        node_groups(N, G, f, i, [&](uint32_t mb) { node_wide_add(N, wide, f, i, mb, cpu, m); });
     }
 }
 
@@ -547,7 +630,7 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
                                                            int64_t* __restrict__ wide_node,
                                                            int64_t* __restrict__ words,
                                                            int64_t* __restrict__ firsts, int decide,
-                                                           esc_group_decision* __restrict__ dec) {
+                                                           esc_group_decision* __restrict__ dec, int node_reset) {
     constexpr int NW = 12;
     __shared__ uint64_t red[CB_WAVES][NW][64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -577,6 +660,10 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
             a[9] += tc >> 32;
             const uint64_t fv = r[3 * G.G];
             a[10] = fv < a[10] ? fv : a[10];
+            if (node_reset) {                             // k_node_atomic rows: ready for the next step
+                uint64_t* w = const_cast<uint64_t*>(r);
+                w[0] = 0; w[G.G] = 0; w[2 * G.G] = 0; w[3 * G.G] = NONE;
+            }
         }
     }
 #pragma unroll
@@ -711,8 +798,9 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_expand(NodeDev N, GroupDev 
         if (i < hi && c) {
             uint64_t off = (uint64_t)(N.created[i] - ts_min);
             off = ts_div > 1 ? off / ts_div : off;
-            node_groups(N, G, f, i, [&](uint32_t g) {
-                const int cls = node_class(N, G, f, i, g);
+            node_groups(N, G, f, i, [&](uint32_t mb) {
+                const uint32_t g = mg(mb);
+                const int cls = node_class(N, f, i, mb);
                 const uint64_t ts = cls == 1 ? (~off & rmask) : off;
                 keys[pos] = ((uint64_t)g << (R + 2)) | ((uint64_t)cls << R) | ts;
                 vals[pos] = (uint32_t)i;
@@ -816,6 +904,19 @@ hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int
     return hipGetLastError();
 }
 
+hipError_t launch_node_atomic(const NodeDev& n, const GroupDev& g, uint64_t* rows, int64_t* wide, hipStream_t st) {
+    const int64_t cnt = n.hi - n.lo;
+    const int64_t nb = std::min<int64_t>((cnt + 255) / 256, 8192);
+    if (nb > 0) hipLaunchKernelGGL(k_node_atomic, dim3((unsigned)nb), dim3(256), 0, st, n, g, rows, wide);
+    return hipGetLastError();
+}
+
+hipError_t launch_fill(uint64_t* p, int64_t n, uint64_t v, hipStream_t st) {
+    const int64_t nb = std::min<int64_t>((n + 255) / 256, 1024);
+    if (nb > 0) hipLaunchKernelGGL(k_fill, dim3((unsigned)nb), dim3(256), 0, st, p, n, v);
+    return hipGetLastError();
+}
+
 hipError_t launch_zero(int64_t* p, int64_t n, hipStream_t st) {
     const int64_t nb = std::min<int64_t>((n + 255) / 256, 1024);
     if (nb > 0) hipLaunchKernelGGL(k_zero, dim3((unsigned)nb), dim3(256), 0, st, p, n);
@@ -833,15 +934,17 @@ hipError_t launch_node_reduce(const NodeDev& n, const GroupDev& g, int n_chunk, 
                               uint64_t* part, int64_t* wide, hipStream_t st) {
     const int n_tiles = (g.G + gt - 1) / gt;
     const size_t lds = (size_t)gt * (3 * sizeof(uint64_t) + sizeof(uint32_t));
-    hipLaunchKernelGGL(k_node_reduce, dim3(n_chunk, n_tiles), dim3(BLOCK), lds, st, n, g, gt, part, wide);
+    hipLaunchKernelGGL(k_node_reduce, dim3(n_tiles, n_chunk), dim3(BLOCK), lds, st, n, g, gt, part, wide);
     return hipGetLastError();
 }
 
 hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* pod_part, int nblk,
                           const uint64_t* node_part, int n_chunk, int64_t* wide_pod, int64_t* wide_node,
-                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st) {
+                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, bool node_reset,
+                          hipStream_t st) {
     hipLaunchKernelGGL(k_combine, dim3((g.G + 63) / 64), dim3(CB_WAVES * 64), 0, st, g, n, pod_part, nblk,
-                       node_part, n_chunk, wide_pod, wide_node, words, first, decide ? 1 : 0, dec);
+                       node_part, n_chunk, wide_pod, wide_node, words, first, decide ? 1 : 0, dec,
+                       node_reset ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -54,7 +54,8 @@ void GroupIndex::build(const esc_group_spec* specs, int32_t n) {
             id = it->second;
         }
         gpair[g] = id;
-        node_groups[id].push_back((uint32_t)g);
+        // node entries carry the dry-mode bit (node classes depend on it, controller.go:115-117)
+        node_groups[id].push_back((uint32_t)g | (groups[g].spec.dry_mode ? NODE_DRY_BIT : 0u));
     }
     n_gp = (uint32_t)pair_ids.size();
     code_list.clear();

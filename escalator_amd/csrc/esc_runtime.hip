@@ -115,6 +115,8 @@ struct esc_ctx {
     bool work_ready = false;
     bool force_wide = false;
     int k1_variant = 0;                                       // ESC_K1_VARIANT (measurement knob)
+    int k2_variant = 0;                                       // ESC_K2_VARIANT: 0 group tiles, 1 atomic rows
+    bool node_atomic = false;                                 // this snapshot uses k_node_atomic
     // graph
     bool use_graph = false;
     std::vector<hipGraphExec_t> graphs;
@@ -237,14 +239,22 @@ int32_t ensure_work(esc_ctx* c) {
     const int64_t n_local = c->node_hi - c->node_lo;
     c->gt = std::min(G, NODE_TILE);
     const int n_gtile = (G + c->gt - 1) / c->gt;
-    int64_t n_chunk = std::max<int64_t>(1, (2 * c->cu_count) / n_gtile);
-    const int64_t flush_cap = std::max<int64_t>(1, n_local * 24 / (2 * (int64_t)G * 32));
-    n_chunk = std::min(n_chunk, flush_cap);
+    // ~2 workgroups per CU, but no chunk below 4096 nodes (the partial flush of a chunk
+    // is 32 B per group of its tile, re-read by K3)
+    int64_t n_chunk = std::max<int64_t>(1, (2 * c->cu_count + n_gtile - 1) / n_gtile);
+    n_chunk = std::min<int64_t>(n_chunk, std::max<int64_t>(1, (n_local + 4095) / 4096));
     n_chunk = std::max<int64_t>(n_chunk, (n_local + NODES_PER_CHUNK_MAX - 1) / NODES_PER_CHUNK_MAX);
     if (n_local == 0) n_chunk = 0;
+    c->node_atomic = c->k2_variant == 1 && n_local > 0 && n_local <= NODES_ATOMIC_MAX;
+    if (c->node_atomic) n_chunk = 1;                 // one set of per-group rows, reset by K3
     c->n_chunk = (int)n_chunk;
     HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * S));
     HIP_TRY(dalloc(&c->d_node_part, (size_t)std::max<int64_t>(n_chunk, 1) * 4 * G));
+    if (c->node_atomic) {
+        HIP_TRY(hipMemset(c->d_node_part, 0, (size_t)3 * G * sizeof(uint64_t)));
+        HIP_TRY(launch_fill(c->d_node_part + 3 * (int64_t)G, G, NONE, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
     HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
     HIP_TRY(dalloc(&c->d_wide_node, (size_t)G * WN_K));
     HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)S * WP_K * sizeof(int64_t)));
@@ -282,13 +292,14 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
             HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
         }
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-        if (c->n_chunk) HIP_TRY(launch_node_reduce(n, g, c->n_chunk, c->gt, c->d_node_part, c->d_wide_node, st));
+        if (c->node_atomic) HIP_TRY(launch_node_atomic(n, g, c->d_node_part, c->d_wide_node, st));
+        else if (c->n_chunk) HIP_TRY(launch_node_reduce(n, g, c->n_chunk, c->gt, c->d_node_part, c->d_wide_node, st));
         nblk = c->nblk;
         n_chunk = c->n_chunk;
     }
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     HIP_TRY(launch_combine(g, n, c->d_pod_part, nblk, c->d_node_part, n_chunk, c->d_wide_pod, c->d_wide_node,
-                           c->d_words, c->d_first, decide, c->d_dec, st));
+                           c->d_words, c->d_first, decide, c->d_dec, c->node_atomic && n_chunk > 0, st));
     // pod wide rows are per slot and may be read by several groups in K3: cleared after it
     HIP_TRY(launch_zero(c->d_wide_pod, pod_slots(c) * WP_K, st));
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
@@ -351,12 +362,13 @@ int32_t esc_taint_error(int64_t n_untainted, int32_t min_nodes, char* buf, int32
 int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t device, int32_t rank,
                        int32_t world, esc_ctx** out) {
     if (!out || !groups || n_groups <= 0 || world < 1 || rank < 0 || rank >= world) return ESC_E_INVAL;
-    if ((uint32_t)n_groups >= NONE) return ESC_E_LIMIT;
+    if ((uint32_t)n_groups > NODE_GROUP_MASK) return ESC_E_LIMIT;   // ids share a word with flag bits
     esc_ctx* c = new (std::nothrow) esc_ctx();
     if (!c) return ESC_E_NOMEM;
     c->rank = rank;
     c->world = world;
     if (const char* v = std::getenv("ESC_K1_VARIANT")) c->k1_variant = std::atoi(v);
+    if (const char* v = std::getenv("ESC_K2_VARIANT")) c->k2_variant = std::atoi(v);
     c->gi.build(groups, n_groups);
     c->params.resize(n_groups);
     for (int32_t g = 0; g < n_groups; ++g) params_from(c->params[g], groups[g], nullptr);
@@ -522,8 +534,9 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     for (int r = 0; r < c->n_replicas; ++r) {
         PodBuf& b = c->pods[r];
         HIP_TRY(dalloc(&b.flags, npad)); HIP_TRY(dalloc(&b.cpu0, npad)); HIP_TRY(dalloc(&b.mem0, npad));
-        HIP_TRY(dalloc(&b.pair0, npad)); HIP_TRY(dalloc(&b.xc_cpu, p->n_xc)); HIP_TRY(dalloc(&b.xc_mem, p->n_xc));
-        HIP_TRY(dalloc(&b.xp, p->n_xp)); HIP_TRY(dalloc(&b.xc_base, c_tiles + 1)); HIP_TRY(dalloc(&b.xp_base, c_tiles + 1));
+        // record arrays: one element of padding (K1 clamps its unconditional record loads)
+        HIP_TRY(dalloc(&b.pair0, npad)); HIP_TRY(dalloc(&b.xc_cpu, p->n_xc + 1)); HIP_TRY(dalloc(&b.xc_mem, p->n_xc + 1));
+        HIP_TRY(dalloc(&b.xp, p->n_xp + 1)); HIP_TRY(dalloc(&b.xc_base, c_tiles + 1)); HIP_TRY(dalloc(&b.xp_base, c_tiles + 1));
         HIP_TRY(dalloc(&b.big, big.size()));
         if (!big.empty()) HIP_TRY(hipMemcpy(b.big, big.data(), big.size() * 4, hipMemcpyHostToDevice));
         if (r == 0) {

@@ -18,4 +18,5 @@ run fetch FETCH_SIZE &&
 run write WRITE_SIZE &&
 run sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD &&
 run lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS &&
+run occ SQ_WAVES SQ_BUSY_CU_CYCLES SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_ANY SQ_INSTS_LDS_ATOMIC SQ_LEVEL_WAVES SQ_INST_LEVEL_VMEM GRBM_GUI_ACTIVE GRBM_COUNT &&
 echo "[pmc] $(date) done"

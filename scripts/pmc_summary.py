@@ -30,7 +30,7 @@ def load(path):
 def main():
     pre, out = sys.argv[1], sys.argv[2]
     merged = collections.defaultdict(dict)
-    for tag in ("fetch", "write", "sq", "lds"):
+    for tag in ("fetch", "write", "sq", "lds", "occ"):
         for k, cs in load(f"{pre}_{tag}/run_counter_collection.csv").items():
             for c, v in cs.items():
                 merged[k][c] = sum(v) / len(v)
