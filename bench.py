@@ -28,22 +28,37 @@ CONFIGS = {
             name="config4: 100M pods / 1M nodes / 10k node groups (BASELINE.json configs[3]), sharded over N GPUs"),
 }
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# PMC passes (scripts/pmc_job.sh) of the kernels as built at this tag: HBM bytes per launch
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v4", "pmc_summary.json")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pod_bytes(s) -> int:
-    """Algorithmic bytes K1 streams per launch (escalator_amd/layout.py)."""
+def stream_bytes(ctx, s, rank, world) -> tuple[int, int]:
+    """Algorithmic bytes K1 / K2 stream per decision on this rank (esc_stream_bytes),
+    cross-checked against the independent restatement in escalator_amd/layout.py."""
     from escalator_amd import layout
-    return layout.pod_bytes(s.pods()["flags"], s.pod_c.n_xc, s.pod_c.n_xp)
+    from oracle import soa
+    pb, nb = ctx.stream_bytes()
+    assert pb == layout.pod_bytes(s.pods()["flags"], s.pod_c.n_xc, s.pod_c.n_xp), "K1 bytes"
+    n_gp = len(soa.group_tables(s.groups)["pair_ids"])
+    assert nb == layout.node_bytes(s.nodes(), n_gp, rank, world), "K2 bytes"
+    return pb, nb
 
 
-def node_bytes(nc, lo, hi) -> int:
-    """K2: flags 4 + label0 4 + cpu 8 + mem 8 per node streamed (+ extra label pairs)."""
-    from escalator_amd import layout
-    return layout.node_bytes(hi - lo, nc.n_xl)
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary (or None)."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    for name, v in d.items():
+        if kernel in name:
+            return v.get("hbm_bytes")
+    return None
 
 
 def cpu_baseline(cfg, G, seconds=12.0):
@@ -108,11 +123,13 @@ def main():
     nlo, nhi = shard_range(N, rank, world)
     t0 = time.time()
     s = esc.Synth(P, N, G, config=args.config, seed=0xE5CA1A7E00000000 + args.config, p_lo=lo, p_hi=hi, threads=16)
-    shard_bytes = pod_bytes(s)
+    from escalator_amd import layout
+    shard_bytes = layout.pod_bytes(s.pods()["flags"], s.pod_c.n_xc, s.pod_c.n_xp)
     replicas = int(max(1, min(8, -(-1_000_000_000 // max(shard_bytes, 1)))))   # >= 1 GB resident: HBM-served
     ctx = esc.Context(s, device=local, rank=rank, world=world)
     ctx.load_synth(s, pod_offset=lo, node_lo=nlo, node_hi=nhi, replicas=replicas)
     ctx.set_state(s.states)
+    pod_b, node_b = stream_bytes(ctx, s, rank, world)
     log("rank %d: shard pods [%d,%d) nodes [%d,%d), %.1f MB x %d replicas, setup %.1fs" %
         (rank, lo, hi, nlo, nhi, shard_bytes / 1e6, replicas, time.time() - t0))
 
@@ -179,11 +196,12 @@ def main():
             dist.destroy_process_group()
         return
 
-    algo = pod_bytes(s)
+    algo = pod_b
     achieved = algo / (k1_ms * 1e-3) / 1e9
     records = P + N
     value = records * args.steps / elapsed
-    decision_bytes = (pod_bytes(s) + node_bytes(s.node_c, nlo, nhi)) * world
+    decision_bytes = (pod_b + node_b) * world         # shards are near-equal; rank 0's x N
+    traffic = pmc_traffic("k_pod_reduce")
     out = {
         "metric": "pod+node records evaluated/sec per scale decision & % HBM peak, 1/2/4/8 GPUs",
         "value": value,
@@ -201,9 +219,11 @@ def main():
                    "parallelism": "shard%d" % world, "replicas_rotated": replicas},
         "hbm_frac_decision": decision_bytes / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9 * world),
         "roofline": {"bound": "hbm", "kernel": "k_pod_reduce", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) if traffic else None,
                      "algorithmic_bytes_per_launch": algo, "launch_ms": k1_ms},
-        "stage_ms": {"k_pod_reduce": stage_mean[0], "k_node_reduce": stage_mean[1], "k_combine": stage_mean[2],
+        "node_bytes_per_decision": node_b,
+        "stage_ms": {"k_pod_reduce": stage_mean[0], "k_node_pieces": stage_mean[1], "k_combine": stage_mean[2],
                      "d2h": stage_mean[3]} if world == 1 else None,
         "parity": parity,
     }

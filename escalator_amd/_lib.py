@@ -121,6 +121,7 @@ _SIGS = {
     "esc_load_pods": (i32, [VP, P(PodSoA), i64]),
     "esc_load_nodes": (i32, [VP, P(NodeSoA), i64, i64]),
     "esc_set_replicas": (i32, [VP, i32]),
+    "esc_stream_bytes": (i32, [VP, P(i64), P(i64)]),
     "esc_set_state": (i32, [VP, P(GroupState)]),
     "esc_reduce": (i32, [VP]),
     "esc_exchange_buffers": (i32, [VP, P(VP), P(i64), P(VP), P(i64)]),

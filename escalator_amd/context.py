@@ -162,6 +162,12 @@ class Context:
         hi = s.node_c.n_nodes if node_hi is None else node_hi
         L.check(self.lib.esc_load_nodes(self.handle, C.byref(s.node_c), node_lo, hi), "esc_load_nodes")
 
+    def stream_bytes(self) -> tuple[int, int]:
+        """Algorithmic HBM bytes one decision streams on this rank: (K1 pods, K2 nodes)."""
+        a, b = C.c_int64(), C.c_int64()
+        L.check(self.lib.esc_stream_bytes(self.handle, C.byref(a), C.byref(b)), "esc_stream_bytes")
+        return a.value, b.value
+
     def set_state(self, states: list[dict] | None):
         self._state = states_to_c(states, self.G)
         L.check(self.lib.esc_set_state(self.handle, self._state), "esc_set_state")
@@ -207,18 +213,21 @@ class Context:
                 "esc_bind_exchange_buffers")
 
     def exchange_download(self):
+        """Host copies of the words to SUM-exchange and (if min_count > 0) to MIN-exchange."""
         (_, sc), (_, mc) = self.exchange_buffers()
         s = np.zeros(sc, np.int64)
         m = np.zeros(mc, np.int64)
-        L.check(self.lib.esc_exchange_download(self.handle, s.ctypes.data_as(C.POINTER(C.c_int64)),
-                                               m.ctypes.data_as(C.POINTER(C.c_int64))), "esc_exchange_download")
+        mp = m.ctypes.data_as(C.POINTER(C.c_int64)) if mc else None
+        L.check(self.lib.esc_exchange_download(self.handle, s.ctypes.data_as(C.POINTER(C.c_int64)), mp),
+                "esc_exchange_download")
         return s, m
 
     def exchange_upload(self, s: np.ndarray, m: np.ndarray):
         s = np.ascontiguousarray(s, np.int64)
         m = np.ascontiguousarray(m, np.int64)
-        L.check(self.lib.esc_exchange_upload(self.handle, s.ctypes.data_as(C.POINTER(C.c_int64)),
-                                             m.ctypes.data_as(C.POINTER(C.c_int64))), "esc_exchange_upload")
+        mp = m.ctypes.data_as(C.POINTER(C.c_int64)) if m.size else None
+        L.check(self.lib.esc_exchange_upload(self.handle, s.ctypes.data_as(C.POINTER(C.c_int64)), mp),
+                "esc_exchange_upload")
 
     def results(self):
         t = np.zeros(self.G, TOTALS_DTYPE)

@@ -24,16 +24,12 @@ constexpr uint32_t CODE_MULTI = 0x80000000u;   // pair code: offset of a [count,
 constexpr uint32_t NODE_DRY_BIT = 0x40000000u; // node membership entry: the group is in dry mode
 constexpr uint32_t NODE_GROUP_MASK = 0x3FFFFFFFu;
 
-// Fast-path packing ranges.  A record outside them is spilled by the
-// same kernel to the exact "wide" global accumulators, so every input stays exact.
+// Fast-path packing ranges of K1's LDS partials.  A pod outside them is
+// spilled by the same kernel to the exact "wide" global accumulators, so every input
+// stays exact.  (Node sums are exact for any int64 input: K2 keeps them split lo32/hi.)
 constexpr int64_t POD_CPU_LIMIT  = int64_t(1) << 20;   // per-pod effective millicores
 constexpr int64_t POD_MEM_LIMIT  = int64_t(1) << 44;   // per-pod effective bytes
-constexpr int64_t NODE_CPU_LIMIT = int64_t(1) << 20;
-constexpr int64_t NODE_MEM_LIMIT = int64_t(1) << 46;
-constexpr int64_t NODE_MEM_LIMIT_ATOMIC = int64_t(1) << 43;   // k_node_atomic: <= 2^20 nodes per rank
-constexpr int64_t NODES_ATOMIC_MAX = int64_t(1) << 20;
 constexpr int64_t PODS_PER_BLOCK_MAX  = int64_t(1) << 20;  // keeps cpu|count<<40 exact
-constexpr int64_t NODES_PER_CHUNK_MAX = int64_t(1) << 18;  // keeps node mem partial < 2^64
 constexpr int CNT_SHIFT = 40;
 constexpr uint64_t CPU_MASK = (uint64_t(1) << CNT_SHIFT) - 1;
 

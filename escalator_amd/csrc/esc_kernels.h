@@ -27,7 +27,17 @@ struct PodDev {
     int64_t c_tiles;           // C section: pods [s_tiles * 256, + c_tiles * 64)
 };
 
-// Device view of the node table; this rank streams nodes [lo, hi).
+// Device view of the node snapshot.
+//
+// Two layouts of the same records, both resident on every rank:
+//  - the node table in snapshot order: flags, label pairs, allocatable, creation time.
+//    K5 (ordering) streams nodes [lo, hi) of it; K3 reads allNodes[0]'s capacity.
+//  - the pair-major entries: one entry per (label pair, node), sorted by (pair, node)
+//    at load (e_flags / e_cpu / e_mem / e_node).  NewNodeLabelFilterFunc
+//    (node_group.go:278) is "(K_g, V_g) in the node's label pairs", so a group's members
+//    are exactly the entries of its pair, in snapshot order.  K2 reduces the entries per
+//    piece (a run of <= NODE_PIECE entries of one pair); this rank reduces pieces
+//    [pc_lo, pc_hi).  K3 joins each group to its pair's pieces.
 struct NodeDev {
     const uint32_t* flags;
     const uint32_t* label0;
@@ -36,44 +46,64 @@ struct NodeDev {
     const int64_t*  created;
     const uint32_t* xl;
     const uint32_t* xl_off;    // [n_nodes] offset of each node's extra labels
-    const int32_t*  trk_node;
+    const int32_t*  trk_node;  // dry-mode tracker, sorted by (node, group)
     const int32_t*  trk_group;
+    const uint32_t* trk_start; // [n_nodes] first tracker entry of a tracked node
     int64_t n_trk;
-    int64_t lo, hi;
+    int64_t lo, hi;            // K5's node range
+    // pair-major entries
+    const uint32_t* e_flags;
+    const int64_t*  e_cpu;
+    const int64_t*  e_mem;
+    const uint32_t* e_node;    // snapshot index of the entry's node
+    const uint32_t* piece_off; // [n_pieces + 1] entry offsets
+    const uint32_t* piece_pair;// [n_pieces]
+    const uint32_t* pp_off;    // [n_gp + 1]: pieces of group pair q are [pp_off[q], pp_off[q+1])
+    int64_t n_pieces, pc_lo, pc_hi;
 };
+
+// K2 output row per piece (int64 words, stored word-major: rows[word * n_pieces + piece]).
+// Sums travel split lo32 / hi (arithmetic) so they add without wrapping; counts are
+// packed 21 bits each (a piece has <= NODE_PIECE entries).
+enum NodeRow : int {
+    NR_UCPU_LO = 0, NR_UCPU_HI, NR_UMEM_LO, NR_UMEM_HI,    // untainted members (wet classes)
+    NR_ACPU_LO, NR_ACPU_HI, NR_AMEM_LO, NR_AMEM_HI,        // every member (dry mode)
+    NR_COUNTS,                                             // unt | taint << 21 | cord << 42
+    NR_K
+};
+constexpr int NODE_PIECE = 1024;
+constexpr int NR_CNT_BITS = 21;
+constexpr uint64_t NR_CNT_MASK = (uint64_t(1) << NR_CNT_BITS) - 1;
 
 struct GroupDev {
     const uint8_t*  dry;
     const GroupParams* params;
-    const uint32_t* gpair;     // [G] group -> its pair id (K3 joins pod slots to groups)
-    const uint32_t* node_code; // [n_gp] pair id -> group code for nodes
+    const uint32_t* gpair;     // [G] group -> its pair id (K3 joins pod slots / node pieces to groups)
+    const uint32_t* node_code; // [n_gp] pair id -> group code (K5)
     const uint32_t* code_list; // CODE_MULTI lists: [count, g...]
+    const uint32_t* slot_readers; // [n_gp + 1] groups reading each pod slot in K3
     uint32_t n_gp;             // pod slots: pair ids [0, n_gp) + the default filter's slot n_gp
     int32_t G;
     uint32_t default_group;    // NONE when no group is named "default"
 };
 
-// Wide (exact, any-range) accumulators: global int64 atomics, one row per group.
+// Wide (exact, any-range) pod accumulators: global int64 atomics, one row per pod slot.
+// K3 reads them and the last reader of a non-zero row resets it (wp_cnt).
 enum WidePod : int { WP_CPU_LO = 0, WP_CPU_HI, WP_MEM_LO, WP_MEM_HI, WP_CNT, WP_K };
-enum WideNode : int { WN_CPU_LO = 0, WN_CPU_HI, WN_MEM_LO, WN_MEM_HI, WN_UNT, WN_TAINT, WN_CORD, WN_FIRST, WN_K };
+// Per dry-mode group: the tracked members' count and split sums (K2 adds, K3 resets).
+enum TrkAcc : int { TA_CNT = 0, TA_CPU_LO, TA_CPU_HI, TA_MEM_LO, TA_MEM_HI, TA_K };
 
 // variant (ESC_K1_VARIANT, measurement knob): 0 = 1024 threads (default), 2 = 512 threads,
 // 9.. = timing-only ablations (wrong results, scripts/k1_variants.py).
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st);
-hipError_t launch_zero(int64_t* p, int64_t n, hipStream_t st);
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
                                int64_t* wide, hipStream_t st);
-hipError_t launch_node_reduce(const NodeDev& n, const GroupDev& g, int n_chunk, int gt,
-                              uint64_t* part, int64_t* wide, hipStream_t st);
+hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows, int64_t* trk_acc, hipStream_t st);
 hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* pod_part, int nblk,
-                          const uint64_t* node_part, int n_chunk, int64_t* wide_pod, int64_t* wide_node,
-                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, bool node_reset,
-                          hipStream_t st);
-hipError_t launch_node_atomic(const NodeDev& n, const GroupDev& g, uint64_t* rows, int64_t* wide, hipStream_t st);
-hipError_t launch_fill(uint64_t* p, int64_t n, uint64_t v, hipStream_t st);
+                          const int64_t* node_rows, int64_t* wide_pod, uint32_t* wp_cnt, int64_t* trk_acc,
+                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
-hipError_t launch_wide_nodes(const NodeDev& n, const GroupDev& g, int64_t* wide, hipStream_t st);
 hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* words,
                          const int64_t* first, esc_group_decision* dec, hipStream_t st);
 

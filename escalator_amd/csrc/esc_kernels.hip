@@ -6,16 +6,19 @@
 //                      16-B-per-lane coalesced loads (4 pods per lane, 256 per wave), int64
 //                      per-group partials privatised in LDS (ds_add_u64), flushed once per
 //                      workgroup.  HBM-bound; no MFMA (nothing is a contraction).
-//  K2 k_node_reduce  : FilteredNodesLister.List + filterNodes (controller.go:120) +
-//                      CalculateNodesCapacityTotal(untainted) (util.go:41) + allNodes[0]
-//                      (controller.go:208).  Group-tiled LDS privatisation.
-//  K3 k_combine      : sums the per-workgroup partials into the exchanged int64 words;
-//                      for one rank it also runs K4.
+//  K2 k_node_pieces  : FilteredNodesLister.List + filterNodes (controller.go:120) +
+//                      CalculateNodesCapacityTotal(untainted) (util.go:41) over the
+//                      pair-major node entries: one wave per piece, register sums, one
+//                      row per piece.  No LDS, no atomics, exact for any int64 input.
+//  K3 k_combine      : joins every group to its pod slot and its pair's node pieces, sums
+//                      the partials into the exchanged int64 words (+ allNodes[0],
+//                      controller.go:208, and the dry-mode tracker); for one rank it also
+//                      runs K4.
 //  K4 k_decide       : calcPercentUsage / switch / calcScaleUpDelta / scaleDownTaint clamp
 //                      (util.go:13-81, controller.go:233-351, scale_down.go:138-158).
 //  K5 sort kernels   : segmented LSD radix sort for taintOldestN / untaintNewestN
 //                      (scale_down.go:171, scale_up.go:118, sort.go:18,33).
-// Wide variants      : exact any-range fallback with global atomics.
+// Wide variants      : exact any-range pod fallback with global atomics.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,8 +28,6 @@
 namespace esc {
 
 namespace {
-
-constexpr int BLOCK = 1024;          // 16 waves per workgroup
 
 __device__ __forceinline__ uint4 ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
 __device__ __forceinline__ ulonglong2 ld2(const int64_t* p) {
@@ -86,7 +87,15 @@ __device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int s
     return __shfl(v, src, 64);
 }
 
+// Sum over the wave's 64 lanes, result in every lane (butterfly).
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
 __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ? a : b; }
+__device__ __forceinline__ int64_t imax64(int64_t a, int64_t b) { return a > b ? a : b; }
 
 // ------------------------------------------------------- selector-pair matching
 // NewPodAffinityFilterFunc / NewNodeLabelFilterFunc (node_group.go:218, :278) for all
@@ -95,8 +104,9 @@ __device__ __forceinline__ int64_t imin64(int64_t a, int64_t b) { return a < b ?
 //  - pods: K1 accumulates per pair (LDS slot = pair id, plus one slot for the default
 //    filter) and K3 joins each group to its pair's slot — the per-pod test
 //    "(K_g, V_g) in pod pairs" evaluated for every group without a per-pod lookup;
-//  - nodes: K2 resolves each label pair through the node code table (a group id, NONE,
-//    or a list of the groups sharing the pair), since node classes depend on the group.
+//  - nodes: K2 accumulates the pair-major entries per piece and K3 joins each group to
+//    its pair's pieces; K5 resolves each label pair through the node code table (a group
+//    id, NONE, or a list of the groups sharing the pair).
 __device__ __forceinline__ uint32_t node_code(const GroupDev& G, uint32_t pair) {
     return pair < G.n_gp ? G.node_code[pair] : NONE;
 }
@@ -314,10 +324,14 @@ __device__ __forceinline__ void c_tile_exact(const PodDev& P, const GroupDev& G,
 
 // =====================================================================  K1 (fast)
 // Each workgroup takes an equal share of the S tiles and of the C tiles; its waves
-// interleave tiles (t = lo + wave, + waves).  16 waves per CU keep ~80 KB of tile loads
-// in flight per CU; the per-group partials stay in LDS and are flushed once.
+// interleave tiles (t = lo + wave, + waves).  Each wave runs a rolling pipeline of DS (S)
+// or DC (C) tile slots: slot d is processed, then refilled with the tile DS (DC) rounds
+// ahead, so DS-1 tiles stay in flight while one is processed.  Refill loads past the
+// end repeat the tile just processed (an L2 hit, no HBM bytes) so that every load is
+// unconditional and the compiler's vmcnt accounting never waits early.  The per-group
+// partials stay in LDS and are flushed once.
 // ABLATE (timing-only builds): bit 0 LDS sink, bit 1 skip S tiles, bit 2 skip C tiles.
-template <int THREADS, int ABLATE = 0>
+template <int THREADS, int ABLATE = 0, int DS = 2, int DC = 2>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
                                                         int64_t* __restrict__ wide) {
@@ -331,35 +345,57 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     if (!(ABLATE & 2)) {
         const int64_t per = (P.s_tiles + gridDim.x - 1) / gridDim.x;
         const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(lo + per, P.s_tiles);
-        // Two tiles per wave iteration (10 KB in flight per wave); B's loads are issued
-        // unconditionally (a repeat of A at the end) so they stay in flight during A.
-        for (int64_t t = lo + wid; t < hi; t += 2 * NW) {
-            const bool has_b = t + NW < hi;
-            STile A, B;
-            s_load(P, t, lane, A);
-            s_load(P, has_b ? t + NW : t, lane, B);
-            s_process<ABLATE>(G, K, A);
-            if (has_b) s_process<ABLATE>(G, K, B);
+        const int64_t t0 = lo + wid;
+        if (t0 < hi) {
+            STile T[DS];
+#pragma unroll
+            for (int d = 0; d < DS; ++d) {
+                const int64_t u = t0 + (int64_t)d * NW;
+                s_load(P, u < hi ? u : t0, lane, T[d]);
+            }
+            for (int64_t t = t0; t < hi; t += (int64_t)DS * NW) {
+#pragma unroll
+                for (int d = 0; d < DS; ++d) {
+                    const int64_t u = t + (int64_t)d * NW;
+                    if (u < hi) s_process<ABLATE>(G, K, T[d]);           // wave-uniform
+                    const int64_t nu = u + (int64_t)DS * NW;
+                    s_load(P, nu < hi ? nu : (u < hi ? u : t0), lane, T[d]);
+                }
+            }
         }
     }
     if (!(ABLATE & 4)) {
         const int64_t per = (P.c_tiles + gridDim.x - 1) / gridDim.x;
         const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(lo + per, P.c_tiles);
-        // Two tiles per wave iteration: B's loads stay in flight while A is processed.
-        // Offsets are scalar loads fetched one iteration ahead.
-        int64_t t = lo + wid;
-        TileBases na{0, 0, 0, 0}, nb{0, 0, 0, 0};
-        if (t < hi) na = tile_bases(P, t);
-        nb = (t + NW < hi) ? tile_bases(P, t + NW) : na;
-        for (; t < hi; t += 2 * NW) {
-            const bool has_b = t + NW < hi;               // wave-uniform
-            CTile A, B;
-            c_load(P, t, lane, na, A);
-            c_load(P, has_b ? t + NW : t, lane, nb, B);   // a repeat of A when there is no B
-            if (t + 2 * NW < hi) na = tile_bases(P, t + 2 * NW);
-            nb = (t + 3 * NW < hi) ? tile_bases(P, t + 3 * NW) : na;
-            if (A.b.xcn <= 128 && A.b.xpn <= 128) c_process<ABLATE>(G, K, A);
-            if (has_b && B.b.xcn <= 128 && B.b.xpn <= 128) c_process<ABLATE>(G, K, B);
+        const int64_t t0 = lo + wid;
+        if (t0 < hi) {
+            // Record offsets of the tile a slot loads next are scalar loads, fetched one
+            // round ahead (nb[d]).
+            CTile T[DC];
+            TileBases nb[DC];
+            const TileBases b0 = tile_bases(P, t0);
+#pragma unroll
+            for (int d = 0; d < DC; ++d) {
+                const int64_t u = t0 + (int64_t)d * NW;
+                c_load(P, u < hi ? u : t0, lane, u < hi ? tile_bases(P, u) : b0, T[d]);
+            }
+#pragma unroll
+            for (int d = 0; d < DC; ++d) {
+                const int64_t nu = t0 + (int64_t)(d + DC) * NW;
+                nb[d] = nu < hi ? tile_bases(P, nu) : T[d].b;
+            }
+            for (int64_t t = t0; t < hi; t += (int64_t)DC * NW) {
+#pragma unroll
+                for (int d = 0; d < DC; ++d) {
+                    const int64_t u = t + (int64_t)d * NW;
+                    if (u < hi && T[d].b.xcn <= 128 && T[d].b.xpn <= 128) c_process<ABLATE>(G, K, T[d]);
+                    const int64_t nu = u + (int64_t)DC * NW;
+                    const int64_t ru = nu < hi ? nu : (u < hi ? u : t0);
+                    c_load(P, ru, lane, nb[d], T[d]);
+                    const int64_t nnu = nu + (int64_t)DC * NW;
+                    nb[d] = nnu < hi ? tile_bases(P, nnu) : T[d].b;
+                }
+            }
         }
     }
     __syncthreads();
@@ -376,14 +412,6 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
 __global__ __launch_bounds__(64) void k_pod_bigtiles(PodDev P, GroupDev G, const uint32_t* __restrict__ tiles,
                                                      int64_t* __restrict__ wide) {
     c_tile_exact(P, G, tiles[blockIdx.x], threadIdx.x, wide);
-}
-
-__global__ __launch_bounds__(256) void k_zero(int64_t* __restrict__ p, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = 0;
-}
-
-__global__ __launch_bounds__(256) void k_fill(uint64_t* __restrict__ p, int64_t n, uint64_t v) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
 // =====================================================================  K1 (wide)
@@ -410,14 +438,11 @@ __global__ __launch_bounds__(256) void k_pod_wide(PodDev P, GroupDev G, int64_t*
 namespace {
 
 // Is (node, group) in the group's dry-mode taintTracker (controller.go:128-133)?
+// Only called for nodes flagged ESC_NF_TRACKED; trk_start points at their first entry.
 __device__ __forceinline__ bool tracked(const NodeDev& N, int32_t node, int32_t g) {
-    int64_t lo = 0, hi = N.n_trk;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        const int32_t a = N.trk_node[mid], b = N.trk_group[mid];
-        if (a < node || (a == node && b < g)) lo = mid + 1; else hi = mid;
-    }
-    return lo < N.n_trk && N.trk_node[lo] == node && N.trk_group[lo] == g;
+    for (int64_t k = N.trk_start[node]; k < N.n_trk && N.trk_node[k] == node; ++k)
+        if (N.trk_group[k] == g) return true;
+    return false;
 }
 
 // filterNodes classification (controller.go:125-150): 0 untainted, 1 tainted, 2 cordoned.
@@ -429,7 +454,7 @@ __device__ __forceinline__ int node_class(const NodeDev& N, uint32_t f, int64_t 
 }
 
 // Groups a node belongs to: NewNodeLabelFilterFunc (node_group.go:278) over its label
-// pairs, resolved through the node pair table.
+// pairs, resolved through the node pair table (K5).
 template <class F>
 __device__ __forceinline__ void node_groups(const NodeDev& N, const GroupDev& G, uint32_t f, int64_t i,
                                             F&& emit) {
@@ -441,147 +466,96 @@ __device__ __forceinline__ void node_groups(const NodeDev& N, const GroupDev& G,
     }
 }
 
+// Does node i carry label pair q (label0 or one of its ascending extra pairs)?
+__device__ __forceinline__ bool node_has_pair(const NodeDev& N, int64_t i, uint32_t q) {
+    const uint32_t l0 = N.label0[i];
+    if (l0 == q) return true;
+    if (l0 == NONE || l0 > q) return false;
+    const uint32_t nx = nf_xlbl(N.flags[i]), o = N.xl_off[i];
+    for (uint32_t k = 0; k < nx; ++k) {
+        const uint32_t x = N.xl[o + k];
+        if (x >= q) return x == q;
+    }
+    return false;
+}
+
+constexpr int K2_WAVES = 4;
+
+// Adds one entry to the piece accumulators: its wet class (filterNodes,
+// controller.go:141-150: Spec.Unschedulable first, then the escalator taint) and the
+// every-member sums used by dry-mode groups.
+struct PieceAcc {
+    unsigned long long ucl = 0, uch = 0, uml = 0, umh = 0, acl = 0, ach = 0, aml = 0, amh = 0, cnt = 0;
+    __device__ __forceinline__ void add(uint32_t f, int64_t c, int64_t m) {
+        const unsigned long long cl = (uint64_t)c & 0xFFFFFFFFull, ml = (uint64_t)m & 0xFFFFFFFFull;
+        const unsigned long long chh = (unsigned long long)(c >> 32), mhh = (unsigned long long)(m >> 32);
+        acl += cl; ach += chh; aml += ml; amh += mhh;
+        const int cls = (f & ESC_NF_UNSCHED) ? 2 : ((f & ESC_NF_TAINTED) ? 1 : 0);
+        if (cls == 0) { ucl += cl; uch += chh; uml += ml; umh += mhh; }
+        cnt += 1ull << (NR_CNT_BITS * cls);
+    }
+};
+
 }  // namespace
 
-// Exact (any-range) node contribution; WN_FIRST keeps ~index under atomicMax so the
-// all-zero row means "no member" and the accumulators can self-clean to zero.
-__device__ __forceinline__ void node_wide_add(const NodeDev& N, int64_t* __restrict__ wide,
-                                              uint32_t f, int64_t i, uint32_t mb, int64_t cpu, int64_t m) {
-    int64_t* r = wide + (int64_t)mg(mb) * WN_K;
-    atomicMax(reinterpret_cast<unsigned long long*>(r + WN_FIRST), ~(unsigned long long)i);
-    const int c = node_class(N, f, i, mb);
-    if (c == 0) {
-        g_add(r + WN_CPU_LO, (int64_t)((uint64_t)cpu & 0xFFFFFFFFull));
-        g_add(r + WN_CPU_HI, cpu >> 32);
-        g_add(r + WN_MEM_LO, (int64_t)((uint64_t)m & 0xFFFFFFFFull));
-        g_add(r + WN_MEM_HI, m >> 32);
-        g_add(r + WN_UNT, 1);
-    } else {
-        g_add(r + (c == 1 ? WN_TAINT : WN_CORD), 1);
+// One wave per piece of this rank's range [pc_lo, pc_hi): <= NODE_PIECE entries of one
+// label pair, 24 B per entry streamed coalesced, two 64-entry rounds in flight per
+// iteration, wave sums by butterfly, one NR_K-word row per piece stored word-major
+// (rows[k * n_pieces + p], so K3's lanes read consecutive pieces coalesced).  Pieces of
+// pairs no group selects (ids >= n_gp) are skipped.
+// Blocks past the pieces take the dry-mode tracker entries (controller.go:128-133): a
+// (node, dry group) entry whose node is a member of the group and lies in this rank's
+// share of the group's pieces adds the node to the group's tracked sums (trk_acc, global
+// atomics: a few thousand entries), which K3 reads and resets.
+__global__ __launch_bounds__(K2_WAVES * 64) void k_node_pieces(NodeDev N, GroupDev G, int64_t nb_pieces,
+                                                               int64_t* __restrict__ rows,
+                                                               int64_t* __restrict__ trk_acc) {
+    const int lane = threadIdx.x & 63;
+    if ((int64_t)blockIdx.x >= nb_pieces) {
+        const int64_t k = ((int64_t)blockIdx.x - nb_pieces) * (K2_WAVES * 64) + threadIdx.x;
+        if (k >= N.n_trk) return;
+        const int32_t j = N.trk_node[k], g = N.trk_group[k];
+        if (!G.dry[g]) return;                       // wet groups ignore the tracker
+        const uint32_t q = G.gpair[g];
+        const int64_t plo = imax64((int64_t)N.pp_off[q], N.pc_lo), phi = imin64((int64_t)N.pp_off[q + 1], N.pc_hi);
+        if (phi <= plo) return;
+        const uint32_t lo_node = N.e_node[N.piece_off[plo]], hi_node = N.e_node[N.piece_off[phi] - 1];
+        if ((uint32_t)j < lo_node || (uint32_t)j > hi_node || !node_has_pair(N, j, q)) return;
+        const int64_t c = N.cpu[j], m = N.mem[j];
+        int64_t* r = trk_acc + (int64_t)g * TA_K;
+        g_add(r + TA_CNT, 1);
+        g_add(r + TA_CPU_LO, (int64_t)((uint64_t)c & 0xFFFFFFFFull));
+        g_add(r + TA_CPU_HI, c >> 32);
+        g_add(r + TA_MEM_LO, (int64_t)((uint64_t)m & 0xFFFFFFFFull));
+        g_add(r + TA_MEM_HI, m >> 32);
+        return;
     }
-}
-
-// grid (n_gtile, n_chunk): the group tiles of one node chunk are adjacent in dispatch
-// order, so the chunk's repeat reads are served on-die.  LDS tile of gt groups: cc, mem,
-// tc (u64), first (u32).  Each thread carries NODE_ILP nodes per iteration so their
-// loads and pair-table gathers are in flight together.
-constexpr int NODE_ILP = 4;
-
-__global__ __launch_bounds__(BLOCK) void k_node_reduce(NodeDev N, GroupDev G, int32_t gt,
-                                                       uint64_t* __restrict__ part,
-                                                       int64_t* __restrict__ wide) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
-    uint64_t* cc = lds;
-    uint64_t* mem = lds + gt;
-    uint64_t* tc = lds + 2 * gt;
-    uint32_t* first = reinterpret_cast<uint32_t*>(lds + 3 * gt);
-    for (int32_t i = threadIdx.x; i < gt; i += BLOCK) { cc[i] = 0; mem[i] = 0; tc[i] = 0; first[i] = NONE; }
-    __syncthreads();
-    const uint32_t g_lo = blockIdx.x * (uint32_t)gt;
-    const uint32_t g_n = (uint32_t)min(gt, G.G - (int32_t)g_lo);
-    const int64_t n = N.hi - N.lo;
-    const int64_t per = (n + gridDim.y - 1) / gridDim.y;
-    const int64_t lo = N.lo + (int64_t)blockIdx.y * per;
-    const int64_t hi = imin64(N.hi, lo + per);
-    for (int64_t b = lo; b < hi; b += (int64_t)BLOCK * NODE_ILP) {
-        // three dependent rounds for NODE_ILP nodes at once: node words (+ offset of the
-        // extra label pairs), then pair codes and the first extra pair, then its code
-        uint32_t f[NODE_ILP], l0[NODE_ILP], xo[NODE_ILP], x1[NODE_ILP], code[NODE_ILP], xcode[NODE_ILP];
-        int64_t cpu[NODE_ILP], m[NODE_ILP];
+    const int64_t p = N.pc_lo + (int64_t)blockIdx.x * K2_WAVES + (threadIdx.x >> 6);
+    if (p >= N.pc_hi) return;
+    if (N.piece_pair[p] >= G.n_gp) return;
+    const uint32_t a = N.piece_off[p], b = N.piece_off[p + 1];
+    PieceAcc acc;
+    for (uint32_t i = a + lane; i < b; i += 128) {
+        const uint32_t j = i + 64;
+        const bool has_j = j < b;
+        const uint32_t jj = has_j ? j : i;
+        const uint32_t f0 = N.e_flags[i], f1 = N.e_flags[jj];
+        const int64_t c0 = N.e_cpu[i], c1 = N.e_cpu[jj];
+        const int64_t m0 = N.e_mem[i], m1 = N.e_mem[jj];
+        acc.add(f0, c0, m0);
+        if (has_j) acc.add(f1, c1, m1);
+    }
+    const unsigned long long v[NR_K] = {wave_sum64(acc.ucl), wave_sum64(acc.uch), wave_sum64(acc.uml),
+                                        wave_sum64(acc.umh), wave_sum64(acc.acl), wave_sum64(acc.ach),
+                                        wave_sum64(acc.aml), wave_sum64(acc.amh), wave_sum64(acc.cnt)};
+    unsigned long long w = 0;
 #pragma unroll
-        for (int k = 0; k < NODE_ILP; ++k) {
-            const int64_t i = b + threadIdx.x + (int64_t)k * BLOCK;
-            f[k] = 0; l0[k] = NONE; cpu[k] = 0; m[k] = 0; xo[k] = 0;
-            if (i < hi) {
-                f[k] = N.flags[i]; l0[k] = N.label0[i]; cpu[k] = N.cpu[i]; m[k] = N.mem[i]; xo[k] = N.xl_off[i];
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < NODE_ILP; ++k) {
-            code[k] = node_code(G, l0[k]);
-            x1[k] = nf_xlbl(f[k]) ? N.xl[xo[k]] : NONE;
-        }
-#pragma unroll
-        for (int k = 0; k < NODE_ILP; ++k) xcode[k] = node_code(G, x1[k]);
-#pragma unroll
-        for (int k = 0; k < NODE_ILP; ++k) {
-            const int64_t i = b + threadIdx.x + (int64_t)k * BLOCK;
-            if (i >= hi) continue;
-            const uint32_t fk = f[k];
-            const int64_t ck = cpu[k], mk = m[k];
-            if ((uint64_t)ck >= (uint64_t)NODE_CPU_LIMIT || (uint64_t)mk >= (uint64_t)NODE_MEM_LIMIT) {
-                node_groups(N, G, fk, i, [&](uint32_t mb) {
-                    if (mg(mb) - g_lo < g_n) node_wide_add(N, wide, fk, i, mb, ck, mk);
-                });
-                continue;
-            }
-            auto visit = [&](uint32_t mb) {
-                const uint32_t t = mg(mb) - g_lo;
-                if (t >= g_n) return;
-                atomicMin(first + t, (uint32_t)i);
-                const int c = node_class(N, fk, i, mb);
-                if (c == 0) { lds_add(cc + t, (uint64_t)ck | (1ull << CNT_SHIFT)); lds_add(mem + t, (uint64_t)mk); }
-                else lds_add(tc + t, c == 1 ? 1ull : (1ull << 32));
-            };
-            for_code(G, code[k], visit);
-            for_code(G, xcode[k], visit);
-            const uint32_t nx = nf_xlbl(fk);
-            for (uint32_t e = 1; e < nx; ++e) for_code(G, node_code(G, N.xl[xo[k] + e]), visit);
-        }
-    }
-    __syncthreads();
-    uint64_t* out = part + (int64_t)blockIdx.y * 4 * G.G + g_lo;
-    for (uint32_t k = threadIdx.x; k < g_n; k += BLOCK) {
-        out[k] = cc[k];
-        out[G.G + k] = mem[k];
-        out[2 * G.G + k] = tc[k];
-        out[3 * G.G + k] = first[k];
-    }
-}
-
-// Node pass without group tiles (ESC_K2 variant 1, for many groups): every node is
-// read once and its memberships go straight to per-group global rows laid out like one
-// k_node_reduce chunk (cc, mem, tc, first), which K3 reads and resets.  Exact while a
-// node's cpu < 2^20 m and mem < 2^43 B and the rank streams <= 2^20 nodes (checked by the
-// host): the packed row words cannot carry.  Other nodes take the wide words.
-__global__ __launch_bounds__(256) void k_node_atomic(NodeDev N, GroupDev G, uint64_t* __restrict__ rows,
-                                                     int64_t* __restrict__ wide) {
-    const int64_t GG = G.G;
-    for (int64_t i = N.lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N.hi;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t f = N.flags[i];
-        const int64_t cpu = N.cpu[i], m = N.mem[i];
-        if ((uint64_t)cpu >= (uint64_t)NODE_CPU_LIMIT || (uint64_t)m >= (uint64_t)NODE_MEM_LIMIT_ATOMIC) {
-            node_groups(N, G, f, i, [&](uint32_t mb) { node_wide_add(N, wide, f, i, mb, cpu, m); });
-            continue;
-        }
-        node_groups(N, G, f, i, [&](uint32_t mb) {
-            const uint32_t g = mg(mb);
-            atomicMin(reinterpret_cast<unsigned long long*>(rows + 3 * GG + g), (unsigned long long)i);
-            const int c = node_class(N, f, i, mb);
-            if (c == 0) {
-                atomicAdd(reinterpret_cast<unsigned long long*>(rows + g), (unsigned long long)cpu | (1ull << CNT_SHIFT));
-                atomicAdd(reinterpret_cast<unsigned long long*>(rows + GG + g), (unsigned long long)m);
-            } else {
-                atomicAdd(reinterpret_cast<unsigned long long*>(rows + 2 * GG + g), c == 1 ? 1ull : (1ull << 32));
-            }
-        });
-    }
-}
-
-__global__ __launch_bounds__(256) void k_node_wide(NodeDev N, GroupDev G, int64_t* __restrict__ wide) {
-    for (int64_t i = N.lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N.hi;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t f = N.flags[i];
-        const int64_t cpu = N.cpu[i], m = N.mem[i];
-        node_groups(N, G, f, i, [&](uint32_t mb) { node_wide_add(N, wide, f, i, mb, cpu, m); });
-    }
+    for (int k = 0; k < NR_K; ++k) w = lane == k ? v[k] : w;
+    if (lane < NR_K) rows[(int64_t)lane * N.n_pieces + p] = (int64_t)w;
 }
 
 // ===================================================================== K3 / K4
 namespace {
-
-constexpr int CB_WAVES = 8;
 
 __device__ __forceinline__ void u128_add(uint64_t& lo, uint64_t& hi, uint64_t v) { lo += v; hi += (lo < v) ? 1 : 0; }
 
@@ -595,6 +569,11 @@ __device__ __forceinline__ bool join_split(int64_t lo_sum, int64_t hi_sum, int64
     const __int128 t = ((__int128)hi_sum << 32) + (__int128)lo_sum;
     out = (int64_t)t;
     return t >= (__int128)INT64_MIN && t <= (__int128)INT64_MAX;
+}
+
+// (unsigned 128-bit sum of lo32 parts, int64 sum of hi parts) -> the exact total
+__device__ __forceinline__ __int128 join_parts(uint64_t lo, uint64_t lo_carry, int64_t hi) {
+    return (__int128)(((unsigned __int128)lo_carry << 64) | lo) + ((__int128)hi << 32);
 }
 
 __device__ __forceinline__ void finalize(const GroupDev& G, const NodeDev& N, int32_t g,
@@ -618,96 +597,155 @@ __device__ __forceinline__ void finalize(const GroupDev& G, const NodeDev& N, in
     decide_one(G.params[g], t, dec[g]);
 }
 
+__device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
-// Row-parallel reduction of the per-workgroup partials: a workgroup owns 64 groups (one
-// per lane, coalesced 512-B row reads) and its 8 waves split the partial rows; the wide
-// accumulators are merged and reset to zero (self-cleaning for the next decision).
+// One lane per group (64 groups per workgroup); the 16 waves split the group's pod
+// partial rows (K1 workgroups, coalesced reads of consecutive slots) and its pair's node
+// piece rows, three LDS rounds merge the waves, and wave 0 adds the wide and tracker
+// accumulators and writes the exchanged words.
+//  - pods: the group's slot is its pair (NewPodAffinityFilterFunc, node_group.go:218) or,
+//    for the group named "default", the default filter's slot (client.go:58-64);
+//  - nodes: the pieces of the group's pair (NewNodeLabelFilterFunc, node_group.go:278);
+//    wet groups take the filterNodes classes, dry groups (controller.go:126-138) take
+//    every member as untainted (cordoned ones included) except the tracked members;
+//  - allNodes[0] (controller.go:208): the first entry of the pair = lowest node index
+//    (every rank holds every piece's offsets, so this needs no exchange).
+// The wide pod row of a slot is read by every group of the slot; the last reader of a
+// non-zero row resets it for the next decision (wp_cnt, slot_readers).  A group's tracker
+// row has one reader and is reset by it.
+constexpr int CB_WAVES = 16;
+
 __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N,
                                                            const uint64_t* __restrict__ pod_part, int nblk,
-                                                           const uint64_t* __restrict__ node_part, int n_chunk,
+                                                           const int64_t* __restrict__ node_rows,
                                                            int64_t* __restrict__ wide_pod,
-                                                           int64_t* __restrict__ wide_node,
+                                                           uint32_t* __restrict__ wp_cnt,
+                                                           int64_t* __restrict__ trk_acc,
                                                            int64_t* __restrict__ words,
                                                            int64_t* __restrict__ firsts, int decide,
-                                                           esc_group_decision* __restrict__ dec, int node_reset) {
-    constexpr int NW = 12;
-    __shared__ uint64_t red[CB_WAVES][NW][64];
+                                                           esc_group_decision* __restrict__ dec) {
+    // a: 0 pod cpu, 1 pod count, 2-3 pod mem (lo, carry), 4-6 untainted / tainted /
+    //    cordoned counts, then node sums as (lo, carry, hi) triples: 7-9 untainted cpu,
+    //    10-12 untainted mem, 13-15 every-member cpu, 16-18 every-member mem
+    constexpr int NA = 19, NPH = 7;
+    __shared__ uint64_t red[CB_WAVES][NPH][64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int32_t g = blockIdx.x * 64 + lane;
     const bool ok = g < G.G;
-    uint64_t a[NW] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    // a: 0 pcpu 1 pcnt 2 pmem_lo 3 pmem_hi 4 ncpu 5 nunt 6 nmem_lo 7 nmem_hi 8 taint 9 cord 10 first
-    a[10] = ~0ull;
-    // The group's pod slot: its pair (NewPodAffinityFilterFunc) or the default filter's.
+    uint64_t a[NA];
+#pragma unroll
+    for (int k = 0; k < NA; ++k) a[k] = 0;
     const int64_t S = G.n_gp + 1;
     const int64_t slot = !ok ? 0 : ((uint32_t)g == G.default_group ? (int64_t)G.n_gp : (int64_t)G.gpair[g]);
+    const uint32_t q = ok ? G.gpair[g] : 0;
+    const uint32_t p0 = ok ? N.pp_off[q] : 0, p1 = ok ? N.pp_off[q + 1] : 0;
+    const int64_t plo = imax64((int64_t)p0, N.pc_lo), phi = imin64((int64_t)p1, N.pc_hi);   // this rank's share
     if (ok) {
+#pragma unroll 4
         for (int b = wid; b < nblk; b += CB_WAVES) {
             const uint64_t c = pod_part[(int64_t)b * 2 * S + slot];
+            const uint64_t m = pod_part[((int64_t)b * 2 + 1) * S + slot];
             a[0] += c & CPU_MASK;
             a[1] += c >> CNT_SHIFT;
-            u128_add(a[2], a[3], pod_part[((int64_t)b * 2 + 1) * S + slot]);
+            u128_add(a[2], a[3], m);
         }
-        for (int c = wid; c < n_chunk; c += CB_WAVES) {
-            const uint64_t* r = node_part + (int64_t)c * 4 * G.G + g;
-            const uint64_t x = r[0];
-            a[4] += x & CPU_MASK;
-            a[5] += x >> CNT_SHIFT;
-            u128_add(a[6], a[7], r[G.G]);
-            const uint64_t tc = r[2 * G.G];
-            a[8] += tc & 0xFFFFFFFFull;
-            a[9] += tc >> 32;
-            const uint64_t fv = r[3 * G.G];
-            a[10] = fv < a[10] ? fv : a[10];
-            if (node_reset) {                             // k_node_atomic rows: ready for the next step
-                uint64_t* w = const_cast<uint64_t*>(r);
-                w[0] = 0; w[G.G] = 0; w[2 * G.G] = 0; w[3 * G.G] = NONE;
+        const int64_t np = N.n_pieces;
+        for (int64_t p = plo + wid; p < phi; p += CB_WAVES) {
+            const int64_t* r = node_rows + p;
+            u128_add(a[7], a[8], (uint64_t)r[NR_UCPU_LO * np]); a[9] += (uint64_t)r[NR_UCPU_HI * np];
+            u128_add(a[10], a[11], (uint64_t)r[NR_UMEM_LO * np]); a[12] += (uint64_t)r[NR_UMEM_HI * np];
+            u128_add(a[13], a[14], (uint64_t)r[NR_ACPU_LO * np]); a[15] += (uint64_t)r[NR_ACPU_HI * np];
+            u128_add(a[16], a[17], (uint64_t)r[NR_AMEM_LO * np]); a[18] += (uint64_t)r[NR_AMEM_HI * np];
+            const uint64_t cn = (uint64_t)r[NR_COUNTS * np];
+            a[4] += cn & NR_CNT_MASK;
+            a[5] += (cn >> NR_CNT_BITS) & NR_CNT_MASK;
+            a[6] += cn >> (2 * NR_CNT_BITS);
+        }
+    }
+    // round 1: words 0-6 (plain sums except the pod mem pair)
+#pragma unroll
+    for (int k = 0; k < NPH; ++k) red[wid][k][lane] = a[k];
+    __syncthreads();
+    if (wid == 0) {
+        for (int w = 1; w < CB_WAVES; ++w) {
+            a[0] += red[w][0][lane];
+            a[1] += red[w][1][lane];
+            u128_add(a[2], a[3], red[w][2][lane]); a[3] += red[w][3][lane];
+            a[4] += red[w][4][lane];
+            a[5] += red[w][5][lane];
+            a[6] += red[w][6][lane];
+        }
+    }
+    // rounds 2, 3: the (lo, carry, hi) triples 7-12 and 13-18
+#pragma unroll
+    for (int r0 = 7; r0 < NA; r0 += 6) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 6; ++k) red[wid][k][lane] = a[r0 + k];
+        __syncthreads();
+        if (wid == 0) {
+            for (int w = 1; w < CB_WAVES; ++w) {
+#pragma unroll
+                for (int k = 0; k < 6; k += 3) {
+                    u128_add(a[r0 + k], a[r0 + k + 1], red[w][k][lane]);
+                    a[r0 + k + 1] += red[w][k + 1][lane];
+                    a[r0 + k + 2] += red[w][k + 2][lane];
+                }
             }
         }
     }
-#pragma unroll
-    for (int k = 0; k < NW; ++k) red[wid][k][lane] = a[k];
-    __syncthreads();
     if (wid != 0 || !ok) return;
-    for (int w = 1; w < CB_WAVES; ++w) {
-        a[0] += red[w][0][lane];
-        a[1] += red[w][1][lane];
-        u128_add(a[2], a[3], red[w][2][lane]); a[3] += red[w][3][lane];
-        a[4] += red[w][4][lane];
-        a[5] += red[w][5][lane];
-        u128_add(a[6], a[7], red[w][6][lane]); a[7] += red[w][7][lane];
-        a[8] += red[w][8][lane];
-        a[9] += red[w][9][lane];
-        a[10] = red[w][10][lane] < a[10] ? red[w][10][lane] : a[10];
+    // wide pod row of the slot (agent-scope loads: written by K1's device-scope atomics)
+    int64_t* wp = wide_pod + slot * WP_K;
+    int64_t p[WP_K];
+#pragma unroll
+    for (int k = 0; k < WP_K; ++k) p[k] = ld_agent(wp + k);
+    if ((p[0] | p[1] | p[2] | p[3] | p[4]) != 0) {
+        __threadfence();
+        const uint32_t seen = atomicAdd(wp_cnt + slot, 1u) + 1u;
+        if (seen == G.slot_readers[slot]) {             // every reader has its copy: reset
+#pragma unroll
+            for (int k = 0; k < WP_K; ++k)
+                __hip_atomic_store(wp + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(wp_cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    const int64_t* wp = wide_pod + slot * WP_K;    // slots may be shared: zeroed per step by the host
-    int64_t* wn = wide_node + (int64_t)g * WN_K;
-    int64_t p[WP_K], q[WN_K];
-#pragma unroll
-    for (int k = 0; k < WP_K; ++k) p[k] = wp[k];
-#pragma unroll
-    for (int k = 0; k < WN_K; ++k) { q[k] = wn[k]; wn[k] = 0; }
     int64_t* w = words + (int64_t)g * TW_K;
     const __int128 pcpu = (__int128)a[0] + ((__int128)p[WP_CPU_HI] << 32) + (__int128)p[WP_CPU_LO];
     const __int128 pmem = (__int128)(((unsigned __int128)a[3] << 64) | a[2]) + ((__int128)p[WP_MEM_HI] << 32) +
                           (__int128)p[WP_MEM_LO];
-    const __int128 ncpu = (__int128)a[4] + ((__int128)q[WN_CPU_HI] << 32) + (__int128)q[WN_CPU_LO];
-    const __int128 nmem = (__int128)(((unsigned __int128)a[7] << 64) | a[6]) + ((__int128)q[WN_MEM_HI] << 32) +
-                          (__int128)q[WN_MEM_LO];
     split_store(w, TW_POD_CPU_LO, pcpu);
     split_store(w, TW_POD_MEM_LO, pmem);
     w[TW_N_PODS] = (int64_t)a[1] + p[WP_CNT];
+    __int128 ncpu, nmem;
+    uint64_t n_unt = a[4], n_taint = a[5], n_cord = a[6];
+    if (!G.dry[g]) {
+        ncpu = join_parts(a[7], a[8], (int64_t)a[9]);
+        nmem = join_parts(a[10], a[11], (int64_t)a[12]);
+    } else {
+        // dry mode (controller.go:126-138): untainted = every member but the tracked ones
+        int64_t* t = trk_acc + (int64_t)g * TA_K;
+        int64_t tr[TA_K];
+#pragma unroll
+        for (int k = 0; k < TA_K; ++k)
+            tr[k] = __hip_atomic_exchange(t + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ncpu = join_parts(a[13], a[14], (int64_t)a[15]) - (((__int128)tr[TA_CPU_HI] << 32) + (__int128)tr[TA_CPU_LO]);
+        nmem = join_parts(a[16], a[17], (int64_t)a[18]) - (((__int128)tr[TA_MEM_HI] << 32) + (__int128)tr[TA_MEM_LO]);
+        const uint64_t n_all = n_unt + n_taint + n_cord;
+        n_unt = n_all - (uint64_t)tr[TA_CNT];
+        n_taint = (uint64_t)tr[TA_CNT];
+        n_cord = 0;
+    }
     split_store(w, TW_NODE_CPU_LO, ncpu);
     split_store(w, TW_NODE_MEM_LO, nmem);
-    w[TW_N_UNT] = (int64_t)a[5] + q[WN_UNT];
-    w[TW_N_TAINT] = (int64_t)a[8] + q[WN_TAINT];
-    w[TW_N_CORD] = (int64_t)a[9] + q[WN_CORD];
-    int64_t fst = a[10] >= (uint64_t)NONE ? INT64_MAX : (int64_t)a[10];
-    if (q[WN_FIRST] != 0) {
-        const int64_t fw = (int64_t)~(uint64_t)q[WN_FIRST];
-        fst = fw < fst ? fw : fst;
-    }
+    w[TW_N_UNT] = (int64_t)n_unt;
+    w[TW_N_TAINT] = (int64_t)n_taint;
+    w[TW_N_CORD] = (int64_t)n_cord;
+    const int64_t fst = p1 > p0 ? (int64_t)N.e_node[N.piece_off[p0]] : INT64_MAX;
     firsts[g] = fst;
     if (decide) finalize(G, N, g, w, fst, dec);
 }
@@ -889,37 +927,27 @@ __global__ __launch_bounds__(256) void k_group_bounds(const uint64_t* __restrict
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st) {
     const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
-#define ESC_K1(T, A) hipLaunchKernelGGL((k_pod_reduce<T, A>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, wide)
+#define ESC_K1(T, A, DS, DC)                                                                              \
+    hipLaunchKernelGGL((k_pod_reduce<T, A, DS, DC>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, \
+                       wide)
     switch (variant) {
-        case 2: ESC_K1(512, 0); break;
+        case 1: ESC_K1(1024, 0, 2, 2); break;
+        case 2: ESC_K1(512, 0, 2, 2); break;
+        case 3: ESC_K1(1024, 0, 3, 3); break;
+        case 4: ESC_K1(1024, 0, 4, 4); break;
+        case 5: ESC_K1(1024, 0, 4, 2); break;
+        case 6: ESC_K1(1024, 0, 2, 4); break;
+        case 7: ESC_K1(1024, 0, 4, 3); break;
+        case 8: ESC_K1(1024, 0, 3, 4); break;
         // Timing-only ablations (wrong results; scripts/k1_variants.py), see k_pod_reduce.
-        case 9: ESC_K1(1024, 1); break;
-        case 10: ESC_K1(1024, 2); break;
-        case 11: ESC_K1(1024, 4); break;
-        case 12: ESC_K1(1024, 3); break;
-        case 13: ESC_K1(1024, 5); break;
-        default: ESC_K1(1024, 0); break;
+        case 9: ESC_K1(1024, 1, 3, 3); break;
+        case 10: ESC_K1(1024, 2, 3, 3); break;
+        case 11: ESC_K1(1024, 4, 3, 3); break;
+        case 12: ESC_K1(1024, 3, 3, 3); break;
+        case 13: ESC_K1(1024, 5, 3, 3); break;
+        default: ESC_K1(1024, 0, 3, 3); break;
     }
 #undef ESC_K1
-    return hipGetLastError();
-}
-
-hipError_t launch_node_atomic(const NodeDev& n, const GroupDev& g, uint64_t* rows, int64_t* wide, hipStream_t st) {
-    const int64_t cnt = n.hi - n.lo;
-    const int64_t nb = std::min<int64_t>((cnt + 255) / 256, 8192);
-    if (nb > 0) hipLaunchKernelGGL(k_node_atomic, dim3((unsigned)nb), dim3(256), 0, st, n, g, rows, wide);
-    return hipGetLastError();
-}
-
-hipError_t launch_fill(uint64_t* p, int64_t n, uint64_t v, hipStream_t st) {
-    const int64_t nb = std::min<int64_t>((n + 255) / 256, 1024);
-    if (nb > 0) hipLaunchKernelGGL(k_fill, dim3((unsigned)nb), dim3(256), 0, st, p, n, v);
-    return hipGetLastError();
-}
-
-hipError_t launch_zero(int64_t* p, int64_t n, hipStream_t st) {
-    const int64_t nb = std::min<int64_t>((n + 255) / 256, 1024);
-    if (nb > 0) hipLaunchKernelGGL(k_zero, dim3((unsigned)nb), dim3(256), 0, st, p, n);
     return hipGetLastError();
 }
 
@@ -930,31 +958,25 @@ hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_
     return hipGetLastError();
 }
 
-hipError_t launch_node_reduce(const NodeDev& n, const GroupDev& g, int n_chunk, int gt,
-                              uint64_t* part, int64_t* wide, hipStream_t st) {
-    const int n_tiles = (g.G + gt - 1) / gt;
-    const size_t lds = (size_t)gt * (3 * sizeof(uint64_t) + sizeof(uint32_t));
-    hipLaunchKernelGGL(k_node_reduce, dim3(n_tiles, n_chunk), dim3(BLOCK), lds, st, n, g, gt, part, wide);
+hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows, int64_t* trk_acc, hipStream_t st) {
+    const int64_t np = n.pc_hi - n.pc_lo;
+    const int64_t nb = (np + K2_WAVES - 1) / K2_WAVES;
+    const int64_t nt = (n.n_trk + K2_WAVES * 64 - 1) / (K2_WAVES * 64);
+    if (nb + nt <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_node_pieces, dim3((unsigned)(nb + nt)), dim3(K2_WAVES * 64), 0, st, n, g, nb, rows, trk_acc);
     return hipGetLastError();
 }
 
 hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* pod_part, int nblk,
-                          const uint64_t* node_part, int n_chunk, int64_t* wide_pod, int64_t* wide_node,
-                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, bool node_reset,
-                          hipStream_t st) {
+                          const int64_t* node_rows, int64_t* wide_pod, uint32_t* wp_cnt, int64_t* trk_acc,
+                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st) {
     hipLaunchKernelGGL(k_combine, dim3((g.G + 63) / 64), dim3(CB_WAVES * 64), 0, st, g, n, pod_part, nblk,
-                       node_part, n_chunk, wide_pod, wide_node, words, first, decide ? 1 : 0, dec,
-                       node_reset ? 1 : 0);
+                       node_rows, wide_pod, wp_cnt, trk_acc, words, first, decide ? 1 : 0, dec);
     return hipGetLastError();
 }
 
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st) {
     hipLaunchKernelGGL(k_pod_wide, dim3(1024), dim3(256), 0, st, p, g, wide);
-    return hipGetLastError();
-}
-
-hipError_t launch_wide_nodes(const NodeDev& n, const GroupDev& g, int64_t* wide, hipStream_t st) {
-    hipLaunchKernelGGL(k_node_wide, dim3(1024), dim3(256), 0, st, n, g, wide);
     return hipGetLastError();
 }
 

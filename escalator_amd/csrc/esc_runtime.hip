@@ -25,7 +25,6 @@ namespace {
 
 constexpr int LDS_BYTES = 160 * 1024;
 constexpr int POD_WINDOW_MAX = LDS_BYTES / 16;      // groups whose pod partials fit in LDS
-constexpr int NODE_TILE = 2048;                     // groups per node-reduce LDS tile (56 KiB)
 constexpr int MAX_STAGES = 8;
 
 #define HIP_TRY(x)                                              \
@@ -65,12 +64,18 @@ struct PodBuf {
 };
 
 struct NodeBuf {
-    uint32_t *flags = nullptr, *label0 = nullptr, *xl = nullptr, *xl_off = nullptr;
+    // node table (snapshot order)
+    uint32_t *flags = nullptr, *label0 = nullptr, *xl = nullptr, *xl_off = nullptr, *trk_start = nullptr;
     int64_t *cpu = nullptr, *mem = nullptr, *created = nullptr;
     int32_t *trk_node = nullptr, *trk_group = nullptr;
+    // pair-major entries, pieces, tracker by group, K2 rows
+    uint32_t *e_flags = nullptr, *e_node = nullptr, *piece_off = nullptr, *piece_pair = nullptr, *pp_off = nullptr;
+    int64_t *e_cpu = nullptr, *e_mem = nullptr, *rows = nullptr;
     void release() {
-        dfree(flags); dfree(label0); dfree(xl); dfree(xl_off); dfree(cpu); dfree(mem); dfree(created);
-        dfree(trk_node); dfree(trk_group);
+        dfree(flags); dfree(label0); dfree(xl); dfree(xl_off); dfree(trk_start); dfree(cpu); dfree(mem);
+        dfree(created); dfree(trk_node); dfree(trk_group);
+        dfree(e_flags); dfree(e_node); dfree(piece_off); dfree(piece_pair); dfree(pp_off);
+        dfree(e_cpu); dfree(e_mem); dfree(rows);
     }
 };
 
@@ -93,7 +98,7 @@ struct esc_ctx {
     // device group tables
     uint8_t* d_dry = nullptr;
     GroupParams* d_params = nullptr;
-    uint32_t *d_gpair = nullptr, *d_node_code = nullptr, *d_code_list = nullptr;
+    uint32_t *d_gpair = nullptr, *d_node_code = nullptr, *d_code_list = nullptr, *d_slot_readers = nullptr;
     // snapshot
     std::vector<PodBuf> pods;
     int n_replicas = 1, cur = 0;
@@ -101,12 +106,15 @@ struct esc_ctx {
     bool pods_loaded = false;
     NodeBuf nodes;
     int64_t n_nodes = 0, n_xl = 0, n_trk = 0, node_lo = 0, node_hi = 0;
+    int64_t n_entries = 0, n_pieces = 0, pc_lo = 0, pc_hi = 0, node_bytes = 0;
     int64_t ts_min = 0, ts_max = 0;
     bool nodes_loaded = false;
     // work
-    int nblk = 0, n_chunk = 0, gt = 0;
-    uint64_t *d_pod_part = nullptr, *d_node_part = nullptr;
-    int64_t *d_wide_pod = nullptr, *d_wide_node = nullptr;
+    int nblk = 0;
+    uint64_t* d_pod_part = nullptr;
+    int64_t* d_wide_pod = nullptr;
+    uint32_t* d_wp_cnt = nullptr;
+    int64_t* d_trk_acc = nullptr;                             // [G][TA_K] dry-mode tracked sums
     int64_t *d_words = nullptr, *d_first = nullptr;          // active exchange buffers
     int64_t *own_words = nullptr, *own_first = nullptr;      // context-owned ones
     esc_group_decision* d_dec = nullptr;
@@ -115,8 +123,6 @@ struct esc_ctx {
     bool work_ready = false;
     bool force_wide = false;
     int k1_variant = 0;                                       // ESC_K1_VARIANT (measurement knob)
-    int k2_variant = 0;                                       // ESC_K2_VARIANT: 0 group tiles, 1 atomic rows
-    bool node_atomic = false;                                 // this snapshot uses k_node_atomic
     // graph
     bool use_graph = false;
     std::vector<hipGraphExec_t> graphs;
@@ -153,6 +159,7 @@ GroupDev group_dev(const esc_ctx* c) {
     g.gpair = c->d_gpair;
     g.node_code = c->d_node_code;
     g.code_list = c->d_code_list;
+    g.slot_readers = c->d_slot_readers;
     g.n_gp = c->gi.n_gp;
     g.G = c->gi.G;
     g.default_group = c->gi.default_group < 0 ? NONE : (uint32_t)c->gi.default_group;
@@ -174,8 +181,12 @@ NodeDev node_dev(const esc_ctx* c) {
     NodeDev n;
     n.flags = c->nodes.flags; n.label0 = c->nodes.label0; n.cpu = c->nodes.cpu; n.mem = c->nodes.mem;
     n.created = c->nodes.created; n.xl = c->nodes.xl; n.xl_off = c->nodes.xl_off;
-    n.trk_node = c->nodes.trk_node; n.trk_group = c->nodes.trk_group; n.n_trk = c->n_trk;
+    n.trk_node = c->nodes.trk_node; n.trk_group = c->nodes.trk_group; n.trk_start = c->nodes.trk_start;
+    n.n_trk = c->n_trk;
     n.lo = c->node_lo; n.hi = c->node_hi;
+    n.e_flags = c->nodes.e_flags; n.e_cpu = c->nodes.e_cpu; n.e_mem = c->nodes.e_mem; n.e_node = c->nodes.e_node;
+    n.piece_off = c->nodes.piece_off; n.piece_pair = c->nodes.piece_pair; n.pp_off = c->nodes.pp_off;
+    n.n_pieces = c->n_pieces; n.pc_lo = c->pc_lo; n.pc_hi = c->pc_hi;
     return n;
 }
 
@@ -197,7 +208,7 @@ void drop_graphs(esc_ctx* c) {
 }
 
 void release_work(esc_ctx* c) {
-    dfree(c->d_pod_part); dfree(c->d_node_part); dfree(c->d_wide_pod); dfree(c->d_wide_node);
+    dfree(c->d_pod_part); dfree(c->d_wide_pod); dfree(c->d_wp_cnt); dfree(c->d_trk_acc);
     dfree(c->own_words); dfree(c->own_first); dfree(c->d_dec);
     c->d_words = nullptr;
     c->d_first = nullptr;
@@ -224,7 +235,7 @@ int32_t ensure_work(esc_ctx* c) {
     const int64_t S = pod_slots(c);
     const int gw = (int)std::min<int64_t>(S, POD_WINDOW_MAX);
     const int lds = gw * 16;
-    const int max_blocks = (c->k1_variant == 2 || c->k1_variant == 4) ? 4 : 2;   // 2048 threads per CU
+    const int max_blocks = c->k1_variant == 2 ? 4 : 2;   // 2048 threads per CU
     const int per_cu = std::max(1, std::min(max_blocks, LDS_BYTES / std::max(lds, 1)));
     int64_t nblk = c->cu_count * per_cu;
     // every workgroup takes ceil(s_tiles/nblk) S tiles + ceil(c_tiles/nblk) C tiles;
@@ -235,30 +246,13 @@ int32_t ensure_work(esc_ctx* c) {
     while (block_pods(nblk) > PODS_PER_BLOCK_MAX) nblk *= 2;
     nblk = std::min<int64_t>(nblk, std::max(c->s_tiles, c->c_tiles));
     c->nblk = (int)nblk;
-    // nodes: group tiles x node chunks; keep the partial flush below ~half the node bytes
-    const int64_t n_local = c->node_hi - c->node_lo;
-    c->gt = std::min(G, NODE_TILE);
-    const int n_gtile = (G + c->gt - 1) / c->gt;
-    // ~2 workgroups per CU, but no chunk below 4096 nodes (the partial flush of a chunk
-    // is 32 B per group of its tile, re-read by K3)
-    int64_t n_chunk = std::max<int64_t>(1, (2 * c->cu_count + n_gtile - 1) / n_gtile);
-    n_chunk = std::min<int64_t>(n_chunk, std::max<int64_t>(1, (n_local + 4095) / 4096));
-    n_chunk = std::max<int64_t>(n_chunk, (n_local + NODES_PER_CHUNK_MAX - 1) / NODES_PER_CHUNK_MAX);
-    if (n_local == 0) n_chunk = 0;
-    c->node_atomic = c->k2_variant == 1 && n_local > 0 && n_local <= NODES_ATOMIC_MAX;
-    if (c->node_atomic) n_chunk = 1;                 // one set of per-group rows, reset by K3
-    c->n_chunk = (int)n_chunk;
     HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * S));
-    HIP_TRY(dalloc(&c->d_node_part, (size_t)std::max<int64_t>(n_chunk, 1) * 4 * G));
-    if (c->node_atomic) {
-        HIP_TRY(hipMemset(c->d_node_part, 0, (size_t)3 * G * sizeof(uint64_t)));
-        HIP_TRY(launch_fill(c->d_node_part + 3 * (int64_t)G, G, NONE, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-    }
     HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
-    HIP_TRY(dalloc(&c->d_wide_node, (size_t)G * WN_K));
+    HIP_TRY(dalloc(&c->d_wp_cnt, (size_t)S));
     HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)S * WP_K * sizeof(int64_t)));
-    HIP_TRY(hipMemset(c->d_wide_node, 0, (size_t)G * WN_K * sizeof(int64_t)));
+    HIP_TRY(hipMemset(c->d_wp_cnt, 0, (size_t)S * sizeof(uint32_t)));
+    HIP_TRY(dalloc(&c->d_trk_acc, (size_t)G * TA_K));
+    HIP_TRY(hipMemset(c->d_trk_acc, 0, (size_t)G * TA_K * sizeof(int64_t)));
     HIP_TRY(dalloc(&c->own_words, (size_t)G * TW_K));
     HIP_TRY(dalloc(&c->own_first, (size_t)G));
     c->d_words = c->bound_words ? c->bound_words : c->own_words;
@@ -276,32 +270,24 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     hipStream_t st = c->stream;
     int e = 0;
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-    int nblk = 0, n_chunk = 0;
+    int nblk = 0;
     if (c->force_wide) {
         if (c->s_tiles + c->c_tiles) HIP_TRY(launch_wide_pods(pod_dev(c, r), g, c->d_wide_pod, st));
-        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-        if (n.hi > n.lo) HIP_TRY(launch_wide_nodes(n, g, c->d_wide_node, st));
-    } else {
-        if (c->nblk) {
-            const PodDev p = pod_dev(c, r);
-            const int32_t S = (int32_t)pod_slots(c);
-            for (int32_t g0 = 0; g0 < S; g0 += POD_WINDOW_MAX) {       // LDS windows of pod slots
-                const int32_t gw = std::min(POD_WINDOW_MAX, S - g0);
-                HIP_TRY(launch_pod_reduce(p, g, g0, gw, c->nblk, c->k1_variant, c->d_pod_part, c->d_wide_pod, st));
-            }
-            HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
+    } else if (c->nblk) {
+        const PodDev p = pod_dev(c, r);
+        const int32_t S = (int32_t)pod_slots(c);
+        for (int32_t g0 = 0; g0 < S; g0 += POD_WINDOW_MAX) {           // LDS windows of pod slots
+            const int32_t gw = std::min(POD_WINDOW_MAX, S - g0);
+            HIP_TRY(launch_pod_reduce(p, g, g0, gw, c->nblk, c->k1_variant, c->d_pod_part, c->d_wide_pod, st));
         }
-        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-        if (c->node_atomic) HIP_TRY(launch_node_atomic(n, g, c->d_node_part, c->d_wide_node, st));
-        else if (c->n_chunk) HIP_TRY(launch_node_reduce(n, g, c->n_chunk, c->gt, c->d_node_part, c->d_wide_node, st));
+        HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
         nblk = c->nblk;
-        n_chunk = c->n_chunk;
     }
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-    HIP_TRY(launch_combine(g, n, c->d_pod_part, nblk, c->d_node_part, n_chunk, c->d_wide_pod, c->d_wide_node,
-                           c->d_words, c->d_first, decide, c->d_dec, c->node_atomic && n_chunk > 0, st));
-    // pod wide rows are per slot and may be read by several groups in K3: cleared after it
-    HIP_TRY(launch_zero(c->d_wide_pod, pod_slots(c) * WP_K, st));
+    HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, st));
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    HIP_TRY(launch_combine(g, n, c->d_pod_part, nblk, c->nodes.rows, c->d_wide_pod, c->d_wp_cnt, c->d_trk_acc,
+                           c->d_words, c->d_first, decide, c->d_dec, st));
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     if (copy_out) {
         HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)g.G * sizeof(esc_group_decision),
@@ -368,7 +354,6 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     c->rank = rank;
     c->world = world;
     if (const char* v = std::getenv("ESC_K1_VARIANT")) c->k1_variant = std::atoi(v);
-    if (const char* v = std::getenv("ESC_K2_VARIANT")) c->k2_variant = std::atoi(v);
     c->gi.build(groups, n_groups);
     c->params.resize(n_groups);
     for (int32_t g = 0; g < n_groups; ++g) params_from(c->params[g], groups[g], nullptr);
@@ -397,8 +382,14 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     if (dalloc(&c->d_dry, G) || dalloc(&c->d_params, G)) return fail(ESC_E_NOMEM);
     const GroupIndex& gi = c->gi;
     if (dalloc(&c->d_gpair, G) || dalloc(&c->d_node_code, gi.n_gp) ||
-        dalloc(&c->d_code_list, gi.code_list.size()))
+        dalloc(&c->d_code_list, gi.code_list.size()) || dalloc(&c->d_slot_readers, (size_t)gi.n_gp + 1))
         return fail(ESC_E_NOMEM);
+    // groups reading each pod slot in K3: the default group reads the default filter's
+    // slot n_gp, every other group its pair's slot
+    std::vector<uint32_t> readers((size_t)gi.n_gp + 1, 0);
+    for (int32_t g = 0; g < n_groups; ++g) ++readers[g == gi.default_group ? gi.n_gp : gi.gpair[g]];
+    if (hipMemcpy(c->d_slot_readers, readers.data(), readers.size() * 4, hipMemcpyHostToDevice))
+        return fail(ESC_E_HIP);
     if (hipMemcpy(c->d_gpair, gi.gpair.data(), G * 4, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_node_code, gi.node_code.data(), gi.n_gp * 4, hipMemcpyHostToDevice) ||
         (!gi.code_list.empty() &&
@@ -424,7 +415,7 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         for (auto& b : c->pods) b.release();
         c->nodes.release();
         dfree(c->d_dry); dfree(c->d_params);
-        dfree(c->d_gpair); dfree(c->d_node_code); dfree(c->d_code_list);
+        dfree(c->d_gpair); dfree(c->d_node_code); dfree(c->d_code_list); dfree(c->d_slot_readers);
         for (int i = 0; i < MAX_STAGES; ++i)
             if (c->ev[i]) hipEventDestroy(c->ev[i]);
         if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -618,6 +609,54 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
                   (s->trk_node[i] == s->trk_node[i - 1] && s->trk_group[i] <= s->trk_group[i - 1])))
             return ESC_E_INVAL;                      // must be sorted by (node, group), unique
     }
+    // Pair-major entries: one per (label pair, node) of the whole table, sorted by
+    // (pair, node) — the group-independent index K2 streams.  Pieces are
+    // runs of <= NODE_PIECE entries of one pair; this rank reduces the pieces that start
+    // in its 1/world share of the entries.
+    std::vector<uint64_t> ent;
+    ent.reserve((size_t)n + (size_t)s->n_xl);
+    for (int64_t i = 0; i < n; ++i) {
+        if (s->label0[i] == NONE) continue;
+        ent.push_back(((uint64_t)s->label0[i] << 32) | (uint64_t)i);
+        const uint32_t nx = nf_xlbl(s->flags[i]);
+        for (uint32_t k = 0; k < nx; ++k) ent.push_back(((uint64_t)s->xl_pair[xl_off[i] + k] << 32) | (uint64_t)i);
+    }
+    std::sort(ent.begin(), ent.end());
+    const int64_t E = (int64_t)ent.size();
+    if (E >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
+    std::vector<uint32_t> e_flags(std::max<int64_t>(E, 1)), e_node(std::max<int64_t>(E, 1));
+    std::vector<int64_t> e_cpu(std::max<int64_t>(E, 1)), e_mem(std::max<int64_t>(E, 1));
+    std::vector<uint32_t> piece_off, piece_pair;
+    for (int64_t k = 0; k < E; ++k) {
+        const uint32_t q = (uint32_t)(ent[k] >> 32), i = (uint32_t)ent[k];
+        if (k == 0 || q != piece_pair.back() || k - (int64_t)piece_off.back() == NODE_PIECE) {
+            piece_off.push_back((uint32_t)k);
+            piece_pair.push_back(q);
+        }
+        e_flags[k] = s->flags[i];
+        e_node[k] = i;
+        e_cpu[k] = s->cpu[i];
+        e_mem[k] = s->mem[i];
+    }
+    const int64_t n_pieces = (int64_t)piece_pair.size();
+    piece_off.push_back((uint32_t)E);
+    const uint32_t n_gp = c->gi.n_gp;
+    std::vector<uint32_t> pp_off((size_t)n_gp + 1);
+    for (uint32_t q = 0; q <= n_gp; ++q)
+        pp_off[q] = (uint32_t)(std::lower_bound(piece_pair.begin(), piece_pair.end(), q) - piece_pair.begin());
+    auto piece_at = [&](int64_t r) {                 // first piece starting at or after E*r/world
+        const uint64_t e0 = (uint64_t)((__int128)E * r / c->world);
+        return (int64_t)(std::lower_bound(piece_off.begin(), piece_off.end() - 1, (uint32_t)e0) - piece_off.begin());
+    };
+    const int64_t pc_lo = piece_at(c->rank), pc_hi = c->rank + 1 == c->world ? n_pieces : piece_at(c->rank + 1);
+    int64_t node_bytes = 0;                          // algorithmic bytes K2 streams per decision
+    for (int64_t p = pc_lo; p < pc_hi; ++p) {
+        node_bytes += 8;                             // piece_pair + piece_off
+        if (piece_pair[p] < n_gp) node_bytes += 24 * (int64_t)(piece_off[p + 1] - piece_off[p]);
+    }
+    // dry-mode tracker: each tracked node's first entry (the (node, group) list is node-sorted)
+    std::vector<uint32_t> trk_start(std::max<int64_t>(n, 1), NONE);
+    for (int64_t k = s->n_trk - 1; k >= 0; --k) trk_start[s->trk_node[k]] = (uint32_t)k;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     drop_graphs(c);
@@ -641,6 +680,25 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
         HIP_TRY(hipMemcpy(b.trk_node, s->trk_node, s->n_trk * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(b.trk_group, s->trk_group, s->n_trk * 4, hipMemcpyHostToDevice));
     }
+    HIP_TRY(dalloc(&b.trk_start, trk_start.size()));
+    HIP_TRY(hipMemcpy(b.trk_start, trk_start.data(), trk_start.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(dalloc(&b.e_flags, e_flags.size())); HIP_TRY(dalloc(&b.e_node, e_node.size()));
+    HIP_TRY(dalloc(&b.e_cpu, e_cpu.size())); HIP_TRY(dalloc(&b.e_mem, e_mem.size()));
+    HIP_TRY(hipMemcpy(b.e_flags, e_flags.data(), e_flags.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b.e_node, e_node.data(), e_node.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b.e_cpu, e_cpu.data(), e_cpu.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b.e_mem, e_mem.data(), e_mem.size() * 8, hipMemcpyHostToDevice));
+    HIP_TRY(dalloc(&b.piece_off, piece_off.size())); HIP_TRY(dalloc(&b.piece_pair, std::max<size_t>(piece_pair.size(), 1)));
+    HIP_TRY(dalloc(&b.pp_off, pp_off.size()));
+    HIP_TRY(hipMemcpy(b.piece_off, piece_off.data(), piece_off.size() * 4, hipMemcpyHostToDevice));
+    if (n_pieces) HIP_TRY(hipMemcpy(b.piece_pair, piece_pair.data(), piece_pair.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(b.pp_off, pp_off.data(), pp_off.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(dalloc(&b.rows, (size_t)std::max<int64_t>(n_pieces, 1) * NR_K));
+    c->n_entries = E;
+    c->n_pieces = n_pieces;
+    c->pc_lo = pc_lo;
+    c->pc_hi = pc_hi;
+    c->node_bytes = node_bytes;
     c->n_nodes = n;
     c->n_xl = s->n_xl;
     c->n_trk = s->n_trk;
@@ -649,6 +707,16 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     c->ts_min = tmin;
     c->ts_max = tmax;
     c->nodes_loaded = true;
+    return ESC_OK;
+}
+
+int32_t esc_stream_bytes(const esc_ctx* c, int64_t* pod_bytes, int64_t* node_bytes) {
+    if (!c || !pod_bytes || !node_bytes) return ESC_E_INVAL;
+    if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
+    // K1: flags 4 + cpu0 4 + mem0 8 + pair0 4 per pod, 16 per extra container record,
+    // 4 per extra pair, 8 per C tile (record offsets); K2: see esc_load_nodes
+    *pod_bytes = c->n_pods * 20 + c->n_xc * 16 + c->n_xp * 4 + c->c_tiles * 8;
+    *node_bytes = c->node_bytes;
     return ESC_OK;
 }
 
@@ -705,13 +773,15 @@ int32_t esc_exchange_buffers(esc_ctx* c, void** sum_buf, int64_t* sum_count, voi
     if (rc) return rc;
     if (sum_buf) *sum_buf = c->d_words;
     if (sum_count) *sum_count = (int64_t)c->gi.G * TW_K;
-    if (min_buf) *min_buf = c->d_first;
-    if (min_count) *min_count = c->gi.G;
+    // allNodes[0] is resolved from the pair-major index every rank holds in full, so the
+    // first-member words need no MIN exchange in this build
+    if (min_buf) *min_buf = nullptr;
+    if (min_count) *min_count = 0;
     return ESC_OK;
 }
 
 int32_t esc_bind_exchange_buffers(esc_ctx* c, void* sum_buf, void* min_buf) {
-    if (!c || (!sum_buf) != (!min_buf)) return ESC_E_INVAL;
+    if (!c || (!sum_buf && min_buf)) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     c->bound_words = reinterpret_cast<int64_t*>(sum_buf);
     c->bound_first = reinterpret_cast<int64_t*>(min_buf);
@@ -726,22 +796,22 @@ int32_t esc_bind_exchange_buffers(esc_ctx* c, void* sum_buf, void* min_buf) {
 int32_t esc_exchange_download(esc_ctx* c, int64_t* sum_out, int64_t* min_out) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
-    if (!sum_out || !min_out) return ESC_E_INVAL;
+    if (!sum_out) return ESC_E_INVAL;
+    (void)min_out;                                   // min_count is 0: nothing to MIN-exchange
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipMemcpy(sum_out, c->d_words, (size_t)c->gi.G * TW_K * 8, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(min_out, c->d_first, (size_t)c->gi.G * 8, hipMemcpyDeviceToHost));
     return ESC_OK;
 }
 
 int32_t esc_exchange_upload(esc_ctx* c, const int64_t* sum_in, const int64_t* min_in) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
-    if (!sum_in || !min_in) return ESC_E_INVAL;
+    if (!sum_in) return ESC_E_INVAL;
+    (void)min_in;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipMemcpy(c->d_words, sum_in, (size_t)c->gi.G * TW_K * 8, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemcpy(c->d_first, min_in, (size_t)c->gi.G * 8, hipMemcpyHostToDevice));
     return ESC_OK;
 }
 

@@ -1,12 +1,13 @@
 """One process per GPU: sharded snapshot + one exchange of the per-group int64 words.
 
 The reference has no parallelism (groups run sequentially,
-controller.go:416).  Here every rank holds a contiguous shard of the pod SoA and streams a
-contiguous range of the node table; the per-group words are all-reduced (SUM) and the
-first-member indices all-reduced (MIN) — over RCCL/xGMI with the ``nccl`` backend (the
-words live in torch tensors bound as the context's exchange buffers, stream-ordered), or
-host-staged over ``gloo``.  int64 addition is associative, so any reduction order gives
-bit-identical totals; every rank then runs K4 on the same words.
+controller.go:416).  Here every rank holds a contiguous shard of the pod SoA and reduces
+its 1/world share of the node index; the per-group words are all-reduced with SUM — over
+RCCL/xGMI with the ``nccl`` backend (the words live in a torch tensor bound as the
+context's exchange buffer, stream-ordered), or host-staged over ``gloo``.  int64 addition
+is associative, so any reduction order gives bit-identical totals; every rank then runs
+K4 on the same words.  The first-member words (allNodes[0]) need no exchange in this
+build (the context reports min_count 0); a MIN all-reduce runs only if one is asked for.
 """
 from __future__ import annotations
 
@@ -35,11 +36,12 @@ class Exchange:
         self.ctx, self.dist, self.torch = ctx, dist, torch
         self.device_collective = device_collective
         (_, sc), (_, mc) = ctx.exchange_buffers()
+        self.min_count = mc
         if device_collective:
             dev = torch.device("cuda", torch.cuda.current_device())
             self.words = torch.zeros(sc, dtype=torch.int64, device=dev)
-            self.first = torch.zeros(mc, dtype=torch.int64, device=dev)
-            ctx.bind_exchange(self.words.data_ptr(), self.first.data_ptr())
+            self.first = torch.zeros(mc, dtype=torch.int64, device=dev) if mc else None
+            ctx.bind_exchange(self.words.data_ptr(), self.first.data_ptr() if mc else None)
             ctx.set_stream(torch.cuda.current_stream().cuda_stream)
 
     def step(self):
@@ -47,12 +49,14 @@ class Exchange:
         self.ctx.reduce()
         if self.device_collective:
             self.dist.all_reduce(self.words, op=self.dist.ReduceOp.SUM)
-            self.dist.all_reduce(self.first, op=self.dist.ReduceOp.MIN)
+            if self.min_count:
+                self.dist.all_reduce(self.first, op=self.dist.ReduceOp.MIN)
         else:
             s, m = self.ctx.exchange_download()
             ts, tm = self.torch.from_numpy(s), self.torch.from_numpy(m)
             self.dist.all_reduce(ts, op=self.dist.ReduceOp.SUM)
-            self.dist.all_reduce(tm, op=self.dist.ReduceOp.MIN)
+            if self.min_count:
+                self.dist.all_reduce(tm, op=self.dist.ReduceOp.MIN)
             self.ctx.exchange_upload(ts.numpy(), tm.numpy())
         self.ctx.decide()
 

@@ -1,14 +1,18 @@
-"""Algorithmic HBM bytes of the streamed snapshot.
+"""Algorithmic HBM bytes of the streamed snapshot — an independent
+restatement of what ``esc_stream_bytes`` reports, used to cross-check it.
 
 K1 reads the pod shard once per decision: per pod flags 4 + cpu0 4 + mem0 8 + pair0 4 B,
 16 B per extra container record, 4 B per extra selector pair, and 8 B of record offsets
 per 64-pod C tile (the pods that own extra records, placed in their own section at load).
-K2 streams per node flags 4 + label0 4 + cpu 8 + mem 8 B, plus 4 B per extra label pair
-and 4 B of offset for each node that has extra label pairs.
+K2 reads the node index once per decision: 24 B per (label pair, node) entry of a pair
+some group selects (flags 4 + cpu 8 + mem 8 + node 4) and 8 B per piece (offset + pair);
+a rank reads the pieces that start in its 1/world share of the entries.
 """
 import numpy as np
 
 XTRA_MASK = 0x3FFFFF10      # ESC_PF_HAS_OVH | extra container counts | extra pair count
+NODE_PIECE = 1024
+NONE = 0xFFFFFFFF
 
 
 def complex_pods(flags: np.ndarray) -> int:
@@ -21,5 +25,26 @@ def pod_bytes(flags: np.ndarray, n_xc: int, n_xp: int) -> int:
     return n * 20 + int(n_xc) * 16 + int(n_xp) * 4 + c_tiles * 8
 
 
-def node_bytes(n_streamed: int, n_xl: int) -> int:
-    return n_streamed * 28 + int(n_xl) * 4
+def node_entries(nodes: dict) -> np.ndarray:
+    """Label pair of every (pair, node) entry, in entry (pair-sorted) order."""
+    label0 = np.asarray(nodes["label0"], np.uint32)
+    pairs = np.concatenate([label0[label0 != NONE], np.asarray(nodes["xl_pair"], np.uint32)])
+    return np.sort(pairs, kind="stable")
+
+
+def node_bytes(nodes: dict, n_gp: int, rank: int = 0, world: int = 1) -> int:
+    q = node_entries(nodes)
+    E = len(q)
+    if E == 0:
+        return 0
+    # pieces: runs of <= NODE_PIECE entries of one pair
+    starts = np.flatnonzero(np.r_[True, q[1:] != q[:-1]])
+    counts = np.diff(np.r_[starts, E])
+    n_pc = (counts + NODE_PIECE - 1) // NODE_PIECE
+    p_start = np.repeat(starts, n_pc) + NODE_PIECE * (np.arange(n_pc.sum()) - np.repeat(np.cumsum(n_pc) - n_pc, n_pc))
+    p_len = np.diff(np.r_[p_start, E])
+    p_pair = q[p_start]
+    lo = E * rank // world
+    hi = E * (rank + 1) // world if rank + 1 < world else E + 1
+    mine = (p_start >= lo) & (p_start < hi)
+    return int(8 * mine.sum() + 24 * p_len[mine & (p_pair < n_gp)].sum())

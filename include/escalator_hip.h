@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define ESC_ABI_VERSION 2
+#define ESC_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- return codes */
 #define ESC_OK          0
@@ -298,32 +298,41 @@ int32_t esc_packer_view(esc_packer* pk, esc_pod_soa* pods, esc_node_soa* nodes);
 
 /* -------------------------------------------------------------- device snapshot
  * esc_load_pods: copies this rank's pod shard (global pod indices [offset, offset+n)).
- * esc_load_nodes: copies the full node table; this rank streams nodes [lo, hi).     */
+ * esc_load_nodes: copies the full node table and builds its pair-major index (one
+ *   entry per (label pair, node), sorted by pair then node — DESIGN.md §3); the
+ *   decision reduces this rank's 1/world share of the index; the ordering (K5)
+ *   streams nodes [lo, hi).                                                         */
 int32_t esc_load_pods(esc_ctx* ctx, const esc_pod_soa* pods, int64_t global_offset);
 int32_t esc_load_nodes(esc_ctx* ctx, const esc_node_soa* nodes, int64_t lo, int64_t hi);
 /* Number of device-resident copies of the pod shard to rotate through on successive
  * decisions (benchmarks use >1 so that timings are HBM-, not Infinity-Cache-, served). */
 int32_t esc_set_replicas(esc_ctx* ctx, int32_t n_replicas);
+/* Algorithmic HBM bytes one decision streams on this rank: K1 (pod shard) and K2
+ * (this rank's node index share).  DESIGN.md §6; cross-checked by escalator_amd/layout.py. */
+int32_t esc_stream_bytes(const esc_ctx* ctx, int64_t* pod_bytes, int64_t* node_bytes);
 
 /* ------------------------------------------------------------ scale decision
  * esc_reduce     : async. Per-shard group totals (K1 pods + K2 nodes + combine).
  * esc_exchange_buffers: device buffers to all-reduce between esc_reduce and esc_decide:
  *                  sum_buf  int64[sum_count]  with op SUM,
- *                  min_buf  int64[min_count]  with op MIN.
+ *                  min_buf  int64[min_count]  with op MIN (min_count 0 = nothing to
+ *                  exchange: this build resolves allNodes[0] from the node index
+ *                  every rank holds, so min_buf is NULL).
  * esc_decide     : async. K4 decide on the (exchanged) totals; results land in the
  *                  context's host buffers after esc_sync.
  * esc_run        : esc_reduce + esc_decide for world == 1, optionally graph-captured.
- * esc_sync       : waits; validates; falls back to the exact wide path if any record
- *                  exceeded the fast path's packing range.           */
+ * esc_sync       : waits for the queued work (records outside the fast path's packing
+ *                  range are summed exactly in-kernel).               */
 int32_t esc_set_state(esc_ctx* ctx, const esc_group_state* state);   /* NULL = zero state */
 int32_t esc_reduce(esc_ctx* ctx);
 int32_t esc_exchange_buffers(esc_ctx* ctx, void** sum_buf, int64_t* sum_count,
                              void** min_buf, int64_t* min_count);
 /* Use caller-allocated device buffers (e.g. torch tensors handed to RCCL) as the
  * exchange buffers; sizes as reported by esc_exchange_buffers.  NULL restores the
- * context's own buffers. */
+ * context's own buffers (min_buf may be NULL when min_count is 0). */
 int32_t esc_bind_exchange_buffers(esc_ctx* ctx, void* sum_buf, void* min_buf);
-/* Host-staged exchange for hosts without a device collective (synchronous). */
+/* Host-staged exchange for hosts without a device collective (synchronous); the min
+ * arrays are ignored (may be NULL) when min_count is 0. */
 int32_t esc_exchange_download(esc_ctx* ctx, int64_t* sum_out, int64_t* min_out);
 int32_t esc_exchange_upload(esc_ctx* ctx, const int64_t* sum_in, const int64_t* min_in);
 int32_t esc_decide(esc_ctx* ctx);

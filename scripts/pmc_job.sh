@@ -11,7 +11,7 @@ rocprofv3 -L > gpurun_out/counters_${TAG}.txt 2>&1 || true
 run() {   # name, counters...
     local name=$1; shift
     echo "[pmc] $(date) $name: $*"
-    timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "k_pod_reduce|k_node_reduce|k_combine" \
+    timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "k_pod_reduce|k_node_pieces|k_combine" \
         --output-format csv -d gpurun_out/pmc_${TAG}_${name} -o run -- $CMD > gpurun_out/pmc_${TAG}_${name}.log 2>&1
 }
 run fetch FETCH_SIZE &&

@@ -290,3 +290,40 @@ def test_big_tiles_and_window_edges(esc):
     for g in range(5):
         L = O.scale_node_group(groups[g], {}, pods, nodes)
         assert (tot["pod_cpu_m"][g], tot["pod_mem_b"][g], tot["n_pods"][g]) == (L["pod_cpu_m"], L["pod_mem_b"], L["n_pods"])
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+def test_node_index_split_within_pairs(esc, world):
+    """Pairs with many pieces (10k members each), a dry group with tracked members, the
+    node index split across `world` ranks inside pairs; SUM of the ranks' words == the
+    whole snapshot, and every rank resolves allNodes[0] on its own."""
+    from escalator_amd import layout
+    from oracle import soa as S
+    P, N, G = 50_000, 200_000, 20
+    full = esc.Synth(P, N, G, config=5, seed=0xE5CA1A7E00000005)
+    assert any(g.get("dry_mode") for g in full.groups) and len(full.nodes()["trk_node"]) > 0
+    otot = S.totals(full.pods(), full.nodes(), full.groups)
+    odf, odi = S.decide(full.groups, full.states, otot)
+    ctxs, words = [], []
+    n_gp = len(S.group_tables(full.groups)["pair_ids"])
+    for r in range(world):
+        from escalator_amd.dist import shard_range
+        lo, hi = shard_range(P, r, world)
+        s = esc.Synth(P, N, G, config=5, seed=0xE5CA1A7E00000005, p_lo=lo, p_hi=hi)
+        c = esc.Context(s, rank=r, world=world)
+        c.load_synth(s, pod_offset=lo)
+        pb, nb = c.stream_bytes()
+        assert pb == layout.pod_bytes(s.pods()["flags"], s.pod_c.n_xc, s.pod_c.n_xp)
+        assert nb == layout.node_bytes(s.nodes(), n_gp, r, world)
+        c.set_state(full.states)
+        c.reduce()
+        w, m = c.exchange_download()
+        assert m.size == 0
+        words.append(w)
+        ctxs.append((c, s))
+    W = np.sum(words, axis=0)
+    for c, _ in ctxs:
+        c.exchange_upload(W, np.zeros(0, np.int64))
+        c.decide()
+        tot, dec = c.results()
+        check_against_c_oracle(tot, dec, otot, odf, odi)
