@@ -8,11 +8,28 @@
 
 namespace esc {
 
-// Device view of a pod shard.  Two sections of the same arrays: pods without extra
-// records ("simple": one container, at most one selector pair) in 256-pod S tiles
-// (4 per lane), then the others in 64-pod C tiles (1 per lane) whose extra records are
-// contiguous per tile.  The split is a stable partition made at load (esc_load_pods);
-// sums are order-independent.  Padding pods carry ESC_PF_DAEMONSET.
+// A class of homogeneous pod tiles: every pod of the class has the same record
+// signature (extra regular containers, init containers, overhead, extra pairs), so record
+// k of a tile's 256 pods is one contiguous 256-entry row.
+struct PodClass {
+    int64_t t0, t1;            // tiles [t0, t1) of the K section
+    int64_t xc0, xp0;          // first record-row entry of tile t0 (xc_cpu / xc_mem, xp)
+    int64_t w0;                // K1 work weight of the tiles before t0
+    uint32_t xreg, xinit, ovh, nxp;
+    uint32_t kind;             // (xreg + xinit + ovh) * 4 + nxp: selects K1's pipeline
+    uint32_t wt;               // work weight of one tile: its 16-B loads per lane
+};
+// weight (16-B loads per lane) of a K tile with R records and NXP extra pairs per pod
+constexpr uint32_t k_tile_weight(uint32_t R, uint32_t NXP) { return 5 + 4 * R + NXP; }
+constexpr int POD_CLASS_IDS = 128;   // signatures with <= 3 extra records and <= 3 extra pairs
+
+// Device view of a pod shard.  Two sections of the same arrays, made at load
+// (esc_load_pods; sums are order-independent):
+//  - K: pods with at most 3 extra container records and at most 3 extra pairs, grouped by
+//    record signature into 256-pod tiles (4 pods per lane, every array a 16-B load);
+//  - C: the others, in 64-pod tiles (1 per lane) whose extra records are contiguous per
+//    tile (xc_base / xp_base).
+// Padding pods carry ESC_PF_DAEMONSET.
 struct PodDev {
     const uint32_t* flags;
     const uint32_t* cpu0;
@@ -21,10 +38,13 @@ struct PodDev {
     const int64_t*  xc_cpu;
     const int64_t*  xc_mem;
     const uint32_t* xp;
+    const PodClass* cls;       // [n_cls] K classes, in tile order
     const uint32_t* xc_base;   // [c_tiles + 1] extra-container offset of each C tile
     const uint32_t* xp_base;   // [c_tiles + 1] extra-pair offset
-    int64_t s_tiles;           // S section: pods [0, s_tiles * 256)
-    int64_t c_tiles;           // C section: pods [s_tiles * 256, + c_tiles * 64)
+    int32_t n_cls;
+    int64_t k_tiles;           // K section: pods [0, k_tiles * 256)
+    int64_t k_weight;          // total work weight of the K tiles (K1 splits it evenly)
+    int64_t c_tiles;           // C section: pods [k_tiles * 256, + c_tiles * 64)
 };
 
 // Device view of the node snapshot.
@@ -93,8 +113,9 @@ enum WidePod : int { WP_CPU_LO = 0, WP_CPU_HI, WP_MEM_LO, WP_MEM_HI, WP_CNT, WP_
 // Per dry-mode group: the tracked members' count and split sums (K2 adds, K3 resets).
 enum TrkAcc : int { TA_CNT = 0, TA_CPU_LO, TA_CPU_HI, TA_MEM_LO, TA_MEM_HI, TA_K };
 
-// variant (ESC_K1_VARIANT, measurement knob): 0 = 1024 threads (default), 2 = 512 threads,
-// 9.. = timing-only ablations (wrong results, scripts/k1_variants.py).
+// variant (ESC_K1_VARIANT, measurement knob): 0 = 1024 threads (default), 1 = two C tiles
+// in flight, 2 = 512 threads, 9.. = timing-only ablations (wrong results,
+// scripts/k1_variants.py).
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st);
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,

@@ -29,10 +29,24 @@ namespace esc {
 
 namespace {
 
-__device__ __forceinline__ uint4 ld4(const uint32_t* p) { return *reinterpret_cast<const uint4*>(p); }
-__device__ __forceinline__ ulonglong2 ld2(const int64_t* p) {
-    return *reinterpret_cast<const ulonglong2*>(p);
+// Streamed (read-once) snapshot loads are nontemporal: on this MI355X a 2.4 GB 16-B-per-
+// lane sweep reads at 6.95 TB/s with nt loads vs 6.37 TB/s without (scripts/stream_probe.hip,
+// profiles/r01_v4/stream_probe.json).
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+typedef uint64_t v2u64 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ld4(const uint32_t* p) {
+    const v4u32 t = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(p));
+    return make_uint4(t.x, t.y, t.z, t.w);
 }
+__device__ __forceinline__ ulonglong2 ld2(const int64_t* p) {
+    const v2u64 t = __builtin_nontemporal_load(reinterpret_cast<const v2u64*>(p));
+    ulonglong2 r;
+    r.x = t.x;
+    r.y = t.y;
+    return r;
+}
+template <class T>
+__device__ __forceinline__ T ldnt(const T* p) { return __builtin_nontemporal_load(p); }
 
 __device__ __forceinline__ void lds_add(uint64_t* a, uint64_t v) {
     atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v);
@@ -172,35 +186,140 @@ __device__ __forceinline__ bool in_range(uint64_t cpu, uint64_t mem) {
     return cpu < (uint64_t)POD_CPU_LIMIT && mem < (uint64_t)POD_MEM_LIMIT;
 }
 
-// ------------------------------------------------------------------ S tiles
-// 256 simple pods per wave, 4 per lane, 16-B loads per lane per array (20 B/pod).
-struct STile {
+// ------------------------------------------------------------------ K tiles
+// Homogeneous 256-pod tiles: every pod of a class has the same record signature, so
+// record k of a tile's pods is one 256-entry row and every array — the pods' own fields
+// and each record / pair row — is one 16-B load per lane (4 pods per lane).  No per-pod
+// offsets, no cross-lane moves, wave-uniform record semantics.
+template <int R, int NXP>
+struct KTile {
     uint4 f, c, p;
-    ulonglong2 m01, m23;
+    ulonglong2 m[2];
+    ulonglong2 rc[R > 0 ? R : 1][2], rm[R > 0 ? R : 1][2];
+    uint4 rq[NXP > 0 ? NXP : 1];
 };
-// (S tiles are pods with one container and at most one selector pair.)
 
-__device__ __forceinline__ void s_load(const PodDev& P, int64_t t, uint32_t lane, STile& T) {
+__device__ __forceinline__ uint32_t lane4(const uint4& v, int j) {
+    return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
+}
+__device__ __forceinline__ uint64_t lane4(const ulonglong2 (&v)[2], int j) {
+    return (j & 1) ? v[j >> 1].y : v[j >> 1].x;
+}
+
+typedef __attribute__((address_space(4))) const PodClass cPodClass;   // scalar loads
+__device__ __forceinline__ PodClass load_class(const PodClass* cls, int i) {
+    const cPodClass* q = (const cPodClass*)cls + i;
+    PodClass k;
+    k.t0 = q->t0; k.t1 = q->t1; k.xc0 = q->xc0; k.xp0 = q->xp0;
+    k.w0 = q->w0;
+    k.xreg = q->xreg; k.xinit = q->xinit; k.ovh = q->ovh; k.nxp = q->nxp; k.kind = q->kind; k.wt = q->wt;
+    return k;
+}
+
+template <int R, int NXP>
+__device__ __forceinline__ void k_load(const PodDev& P, const PodClass& C, int64_t t, uint32_t lane,
+                                       KTile<R, NXP>& T) {
     const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
     T.f = ld4(P.flags + p0);
     T.c = ld4(P.cpu0 + p0);
-    T.m01 = ld2(P.mem0 + p0);
-    T.m23 = ld2(P.mem0 + p0 + 2);
+    T.m[0] = ld2(P.mem0 + p0);
+    T.m[1] = ld2(P.mem0 + p0 + 2);
     T.p = ld4(P.pair0 + p0);
+    const int64_t rt = t - C.t0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const int64_t o = C.xc0 + (rt * R + k) * TILE + lane * PODS_PER_LANE;
+        T.rc[k][0] = ld2(P.xc_cpu + o);
+        T.rc[k][1] = ld2(P.xc_cpu + o + 2);
+        T.rm[k][0] = ld2(P.xc_mem + o);
+        T.rm[k][1] = ld2(P.xc_mem + o + 2);
+    }
+#pragma unroll
+    for (int k = 0; k < NXP; ++k) T.rq[k] = ld4(P.xp + C.xp0 + (rt * NXP + k) * TILE + lane * PODS_PER_LANE);
 }
 
-template <int ABLATE>
-__device__ __forceinline__ void s_process(const GroupDev& G, const PodSink<ABLATE>& K, const STile& T) {
-    const uint32_t fs[4] = {T.f.x, T.f.y, T.f.z, T.f.w};
-    const uint32_t ps[4] = {T.p.x, T.p.y, T.p.z, T.p.w};
-    const uint64_t cpu[4] = {T.c.x, T.c.y, T.c.z, T.c.w};
-    const uint64_t mem[4] = {T.m01.x, T.m01.y, T.m23.x, T.m23.y};
+// ComputePodResourceRequest (scheduler/types.go:72-89) for each of the lane's 4 pods:
+// records [0, xreg) are regular containers (add), [xreg, xreg + xinit) init containers
+// (max; an absent key is INT64_MIN), the last the overhead (add), with Go's wrapping
+// int64 +=; then the pod's memberships (node_group.go:218-275).
+template <int R, int NXP, int ABLATE>
+__device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLATE>& K, const PodClass& C,
+                                          const KTile<R, NXP>& T) {
+    const uint32_t init_end = C.xreg + C.xinit;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        if (fs[j] & ESC_PF_DAEMONSET) continue;                      // node_group.go:221, :259
-        const bool in = in_range(cpu[j], mem[j]);
-        if (pf_default_ok(fs[j]) && G.default_group != NONE) K.add(G.n_gp, cpu[j], mem[j], in);
-        if (ps[j] < G.n_gp) K.add(ps[j], cpu[j], mem[j], in);
+    for (int j = 0; j < PODS_PER_LANE; ++j) {
+        const uint32_t f = lane4(T.f, j);
+        if (f & ESC_PF_DAEMONSET) continue;                          // node_group.go:221, :259
+        uint64_t cpu = lane4(T.c, j), mem = lane4(T.m, j);
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const uint64_t c = lane4(T.rc[k], j), m = lane4(T.rm[k], j);
+            if ((uint32_t)k < C.xreg || (uint32_t)k >= init_end) {
+                cpu += c;
+                mem += m;
+            } else {
+                cpu = ((int64_t)cpu >= (int64_t)c) ? cpu : c;
+                mem = ((int64_t)mem >= (int64_t)m) ? mem : m;
+            }
+        }
+        const bool in = in_range(cpu, mem);
+        if (pf_default_ok(f) && G.default_group != NONE) K.add(G.n_gp, cpu, mem, in);
+        const uint32_t q0 = lane4(T.p, j);
+        if (q0 < G.n_gp) K.add(q0, cpu, mem, in);
+#pragma unroll
+        for (int k = 0; k < NXP; ++k) {
+            const uint32_t q = lane4(T.rq[k], j);
+            if (q < G.n_gp) K.add(q, cpu, mem, in);
+        }
+    }
+}
+
+template <int R, int NXP>
+__device__ __forceinline__ void k_sink(const KTile<R, NXP>& T) {   // loads-only ablation
+    uint32_t x = T.f.x ^ T.f.y ^ T.f.z ^ T.f.w ^ T.c.x ^ T.c.y ^ T.c.z ^ T.c.w ^ T.p.x ^ T.p.y ^ T.p.z ^ T.p.w;
+    uint64_t y = T.m[0].x ^ T.m[0].y ^ T.m[1].x ^ T.m[1].y;
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) y ^= T.rc[k][h].x ^ T.rc[k][h].y ^ T.rm[k][h].x ^ T.rm[k][h].y;
+#pragma unroll
+    for (int k = 0; k < NXP; ++k) x ^= T.rq[k].x ^ T.rq[k].y ^ T.rq[k].z ^ T.rq[k].w;
+    asm volatile("" :: "v"(x), "v"(y));
+}
+
+// Tiles a, a + NW, ... (< b) of one class for this wave: a rolling pipeline of DS tile
+// slots (slot d is processed, then refilled with the tile DS rounds ahead).  DS follows
+// the tile's register footprint.  Refills past the end re-read the tile the slot just
+// held (an L2 hit; never one address shared by every wave — that serialises on one
+// channel: 0.9 ms instead of 0.4 ms for config 4), so that every load is unconditional
+// and the compiler's vmcnt accounting never waits early.
+template <int R, int NXP, int NW, int ABLATE>
+__device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const PodSink<ABLATE>& K,
+                                      const PodClass& C, int64_t a, int64_t b, uint32_t lane) {
+    constexpr int L = 5 + 4 * R + NXP;                   // 16-B loads per lane per tile
+    constexpr int DS = L <= 7 ? 3 : (L <= 10 ? 2 : 1);
+    KTile<R, NXP> T[DS];
+#pragma unroll
+    for (int d = 0; d < DS; ++d) {
+        const int64_t u = a + (int64_t)d * NW;
+        k_load(P, C, u < b ? u : a, lane, T[d]);
+        __builtin_amdgcn_sched_barrier(0);            // slots issue in order (see below)
+    }
+    for (int64_t t = a; t < b; t += (int64_t)DS * NW) {
+#pragma unroll
+        for (int d = 0; d < DS; ++d) {
+            const int64_t u = t + (int64_t)d * NW;
+            if (u < b) {                                       // wave-uniform
+                if constexpr (ABLATE & 32) k_sink(T[d]);
+                else k_process<R, NXP, ABLATE>(G, K, C, T[d]);
+            }
+            // keep slot d's refill after its use: hoisting it would make the next slots'
+            // waits count it (vmcnt is in order) and drain the pipeline
+            __builtin_amdgcn_sched_barrier(0);
+            const int64_t nu = u + (int64_t)DS * NW;
+            k_load(P, C, nu < b ? nu : (u < b ? u : a), lane, T[d]);
+            __builtin_amdgcn_sched_barrier(0);
+        }
     }
 }
 
@@ -238,23 +357,60 @@ struct CTile {
 // record arrays carry one element of padding), so the compiler's vmcnt accounting can
 // leave a second tile's loads in flight while the first is processed.
 __device__ __forceinline__ void c_load(const PodDev& P, int64_t t, uint32_t lane, const TileBases& b, CTile& T) {
-    const int64_t i = P.s_tiles * TILE + t * CTILE + lane;
+    const int64_t i = P.k_tiles * TILE + t * CTILE + lane;
     T.b = b;
-    T.f = P.flags[i];
-    T.c = P.cpu0[i];
-    T.m = (uint64_t)P.mem0[i];
-    T.p = P.pair0[i];
+    T.f = ldnt(P.flags + i);
+    T.c = ldnt(P.cpu0 + i);
+    T.m = (uint64_t)ldnt(P.mem0 + i);
+    T.p = ldnt(P.pair0 + i);
     const uint32_t lc = (b.xcn ? b.xcn : 1u) - 1u, lp = (b.xpn ? b.xpn : 1u) - 1u;
     const uint32_t c0 = b.xcb + min(lane, lc), c1 = b.xcb + min(lane + 64, lc);
     const uint32_t p0 = b.xpb + min(lane, lp), p1 = b.xpb + min(lane + 64, lp);
-    T.xcc0 = (unsigned long long)P.xc_cpu[c0];
-    T.xcm0 = (unsigned long long)P.xc_mem[c0];
-    T.xcc1 = (unsigned long long)P.xc_cpu[c1];
-    T.xcm1 = (unsigned long long)P.xc_mem[c1];
-    T.xp0 = P.xp[p0];
-    T.xp1 = P.xp[p1];
+    T.xcc0 = (unsigned long long)ldnt(P.xc_cpu + c0);
+    T.xcm0 = (unsigned long long)ldnt(P.xc_mem + c0);
+    T.xcc1 = (unsigned long long)ldnt(P.xc_cpu + c1);
+    T.xcm1 = (unsigned long long)ldnt(P.xc_mem + c1);
+    T.xp0 = ldnt(P.xp + p0);
+    T.xp1 = ldnt(P.xp + p1);
 }
 
+// Record k of every lane's run [o, o + n) of the tile's records (lane l holds records l
+// and l + 64), fetched with ds_bpermute; `hi` = the tile has more than 64 records.
+__device__ __forceinline__ void rec64(const unsigned long long (&r)[2], uint32_t rel, bool hi, unsigned long long& v) {
+    v = shfl64(r[0], (int)(rel & 63));
+    if (hi) {
+        const unsigned long long v1 = shfl64(r[1], (int)(rel & 63));
+        if (rel >= 64) v = v1;
+    }
+}
+__device__ __forceinline__ uint32_t rec32(uint32_t r0, uint32_t r1, uint32_t rel, bool hi) {
+    uint32_t v = __shfl(r0, (int)(rel & 63), 64);
+    if (hi) {
+        const uint32_t v1 = __shfl(r1, (int)(rel & 63), 64);
+        if (rel >= 64) v = v1;
+    }
+    return v;
+}
+
+// ComputePodResourceRequest step for record k of a pod (types.go:72-89): regular extras
+// add, init containers max, the overhead adds (Go's wrapping int64 +=).
+__device__ __forceinline__ void apply_rec(uint32_t k, uint32_t nxc, uint32_t nreg, uint32_t add_from,
+                                          unsigned long long c, unsigned long long m, uint64_t& cpu, uint64_t& mem) {
+    if (k < nxc) {
+        if (k < nreg || k >= add_from) {
+            cpu += c;
+            mem += m;
+        } else {
+            cpu = ((int64_t)cpu >= (int64_t)c) ? cpu : c;
+            mem = ((int64_t)mem >= (int64_t)m) ? mem : m;
+        }
+    }
+}
+
+// One C tile: the per-pod record offsets come from a DPP wave prefix sum of the packed
+// counts; each pod pulls its k-th record / pair with ds_bpermute in a wave-uniform loop.
+// (Issuing the first rounds' bpermutes back to back measured slower: the C path is
+// LDS-issue-bound, not latency-bound.)
 template <int ABLATE>
 __device__ __forceinline__ void c_process(const GroupDev& G, const PodSink<ABLATE>& K, const CTile& T) {
     const uint32_t f = T.f;
@@ -262,28 +418,15 @@ __device__ __forceinline__ void c_process(const GroupDev& G, const PodSink<ABLAT
     const uint32_t v = nxc | (nxp << 16);                 // tile totals <= 128 each
     const uint32_t ex = wave_incl_scan32(v) - v;
     const uint32_t oc = ex & 0xFFFF, op = ex >> 16;
-    // ComputePodResourceRequest (types.go:72-89) over the pod's records in order:
-    // regular extras add, init containers max, the overhead adds.
+    const bool chi = T.b.xcn > 64, phi = T.b.xpn > 64;   // wave-uniform
+    const unsigned long long xc[2] = {T.xcc0, T.xcc1}, xm[2] = {T.xcm0, T.xcm1};
     uint64_t cpu = T.c, mem = T.m;
     const uint32_t nreg = pf_xreg(f), add_from = nreg + pf_xinit(f);
     for (uint32_t k = 0; wave_any(k < nxc); ++k) {
-        const uint32_t rel = oc + k;
-        unsigned long long c = shfl64(T.xcc0, (int)(rel & 63));
-        unsigned long long m = shfl64(T.xcm0, (int)(rel & 63));
-        if (T.b.xcn > 64) {                               // wave-uniform
-            const unsigned long long c1 = shfl64(T.xcc1, (int)(rel & 63));
-            const unsigned long long m1 = shfl64(T.xcm1, (int)(rel & 63));
-            if (rel >= 64) { c = c1; m = m1; }
-        }
-        if (k < nxc) {
-            if (k < nreg || k >= add_from) {
-                cpu += c;
-                mem += m;
-            } else {
-                cpu = ((int64_t)cpu >= (int64_t)c) ? cpu : c;
-                mem = ((int64_t)mem >= (int64_t)m) ? mem : m;
-            }
-        }
+        unsigned long long c, m;
+        rec64(xc, oc + k, chi, c);
+        rec64(xm, oc + k, chi, m);
+        apply_rec(k, nxc, nreg, add_from, c, m, cpu, mem);
     }
     const bool live = !(f & ESC_PF_DAEMONSET);            // node_group.go:221, :259
     const bool in = in_range(cpu, mem);
@@ -292,12 +435,7 @@ __device__ __forceinline__ void c_process(const GroupDev& G, const PodSink<ABLAT
         if (T.p < G.n_gp) K.add(T.p, cpu, mem, in);
     }
     for (uint32_t k = 0; wave_any(k < nxp); ++k) {
-        const uint32_t rel = op + k;
-        uint32_t q = __shfl(T.xp0, (int)(rel & 63), 64);
-        if (T.b.xpn > 64) {
-            const uint32_t q1 = __shfl(T.xp1, (int)(rel & 63), 64);
-            if (rel >= 64) q = q1;
-        }
+        const uint32_t q = rec32(T.xp0, T.xp1, op + k, phi);
         if (live && k < nxp && q < G.n_gp) K.add(q, cpu, mem, in);
     }
 }
@@ -305,7 +443,7 @@ __device__ __forceinline__ void c_process(const GroupDev& G, const PodSink<ABLAT
 // Exact (any-range) evaluation of one C tile from memory, one pod per lane.
 __device__ __forceinline__ void c_tile_exact(const PodDev& P, const GroupDev& G, int64_t t, uint32_t lane,
                                              int64_t* __restrict__ wide) {
-    const int64_t i = P.s_tiles * TILE + t * CTILE + lane;
+    const int64_t i = P.k_tiles * TILE + t * CTILE + lane;
     const uint32_t f = P.flags[i];
     const uint32_t nxc = pf_xctr(f), nxp = pf_xpair(f);
     uint32_t oc = P.xc_base[t] + wave_incl_scan32(nxc) - nxc;
@@ -323,15 +461,14 @@ __device__ __forceinline__ void c_tile_exact(const PodDev& P, const GroupDev& G,
 }  // namespace
 
 // =====================================================================  K1 (fast)
-// Each workgroup takes an equal share of the S tiles and of the C tiles; its waves
-// interleave tiles (t = lo + wave, + waves).  Each wave runs a rolling pipeline of DS (S)
-// or DC (C) tile slots: slot d is processed, then refilled with the tile DS (DC) rounds
-// ahead, so DS-1 tiles stay in flight while one is processed.  Refill loads past the
-// end repeat the tile just processed (an L2 hit, no HBM bytes) so that every load is
-// unconditional and the compiler's vmcnt accounting never waits early.  The per-group
-// partials stay in LDS and are flushed once.
-// ABLATE (timing-only builds): bit 0 LDS sink, bit 1 skip S tiles, bit 2 skip C tiles.
-template <int THREADS, int ABLATE = 0, int DS = 2, int DC = 2>
+// Each workgroup takes an equal contiguous share of the K tiles' work weight (16-B loads)
+// and of the C tiles.  K tiles: the share is walked class by class (the class table is sorted by tile), each
+// class run by the pipeline instantiated for its record shape; waves interleave tiles
+// (t = first + wave, + waves).  C tiles: a rolling pipeline of DC slots, as k_run.  The
+// per-group partials stay in LDS and are flushed once.
+// ABLATE (timing-only builds): bit 0 LDS sink, bit 1 skip K tiles, bit 2 skip C tiles,
+// bit 5 loads only.
+template <int THREADS, int ABLATE = 0, int DC = 3>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
                                                         int64_t* __restrict__ wide) {
@@ -343,24 +480,27 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     const uint32_t lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (!(ABLATE & 2)) {
-        const int64_t per = (P.s_tiles + gridDim.x - 1) / gridDim.x;
-        const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(lo + per, P.s_tiles);
-        const int64_t t0 = lo + wid;
-        if (t0 < hi) {
-            STile T[DS];
-#pragma unroll
-            for (int d = 0; d < DS; ++d) {
-                const int64_t u = t0 + (int64_t)d * NW;
-                s_load(P, u < hi ? u : t0, lane, T[d]);
-            }
-            for (int64_t t = t0; t < hi; t += (int64_t)DS * NW) {
-#pragma unroll
-                for (int d = 0; d < DS; ++d) {
-                    const int64_t u = t + (int64_t)d * NW;
-                    if (u < hi) s_process<ABLATE>(G, K, T[d]);           // wave-uniform
-                    const int64_t nu = u + (int64_t)DS * NW;
-                    s_load(P, nu < hi ? nu : (u < hi ? u : t0), lane, T[d]);
-                }
+        // equal shares of work weight (bytes), not of tiles: a tile of a class with three
+        // container records streams ~3.4x the bytes of a simple one
+        const int64_t wl = P.k_weight * blockIdx.x / gridDim.x, wh = P.k_weight * (blockIdx.x + 1) / gridDim.x;
+        for (int ci = 0; ci < P.n_cls; ++ci) {
+            const PodClass C = load_class(P.cls, ci);
+            if (C.w0 >= wh) break;
+            // tiles of the class whose start weight lies in [wl, wh)
+            const int64_t n = C.t1 - C.t0;
+            const int64_t i0 = imin64(n, imax64(0, (wl - C.w0 + C.wt - 1) / C.wt));
+            const int64_t i1 = imin64(n, imax64(0, (wh - C.w0 + C.wt - 1) / C.wt));
+            const int64_t a = C.t0 + i0 + wid, b = C.t0 + i1;
+            if (a >= b) continue;
+            switch (C.kind) {
+#define ESC_KRUN(RR, XX) \
+    case RR * 4 + XX: k_run<RR, XX, NW, ABLATE>(P, G, K, C, a, b, lane); break;
+                ESC_KRUN(0, 0) ESC_KRUN(0, 1) ESC_KRUN(0, 2) ESC_KRUN(0, 3)
+                ESC_KRUN(1, 0) ESC_KRUN(1, 1) ESC_KRUN(1, 2) ESC_KRUN(1, 3)
+                ESC_KRUN(2, 0) ESC_KRUN(2, 1) ESC_KRUN(2, 2) ESC_KRUN(2, 3)
+                ESC_KRUN(3, 0) ESC_KRUN(3, 1) ESC_KRUN(3, 2) ESC_KRUN(3, 3)
+#undef ESC_KRUN
+                default: break;
             }
         }
     }
@@ -388,7 +528,10 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
 #pragma unroll
                 for (int d = 0; d < DC; ++d) {
                     const int64_t u = t + (int64_t)d * NW;
-                    if (u < hi && T[d].b.xcn <= 128 && T[d].b.xpn <= 128) c_process<ABLATE>(G, K, T[d]);
+                    if constexpr (ABLATE & 32) {
+                        if (u < hi) asm volatile("" :: "v"(T[d].f ^ T[d].c ^ T[d].p ^ T[d].xp0 ^ T[d].xp1),
+                                                 "v"(T[d].m ^ T[d].xcc0 ^ T[d].xcm0 ^ T[d].xcc1 ^ T[d].xcm1));
+                    } else if (u < hi && T[d].b.xcn <= 128 && T[d].b.xpn <= 128) c_process<ABLATE>(G, K, T[d]);
                     const int64_t nu = u + (int64_t)DC * NW;
                     const int64_t ru = nu < hi ? nu : (u < hi ? u : t0);
                     c_load(P, ru, lane, nb[d], T[d]);
@@ -415,21 +558,42 @@ __global__ __launch_bounds__(64) void k_pod_bigtiles(PodDev P, GroupDev G, const
 }
 
 // =====================================================================  K1 (wide)
+namespace {
+// Exact (any-range) evaluation of one K tile from memory, 4 pods per lane.
+__device__ __forceinline__ void k_tile_exact(const PodDev& P, const GroupDev& G, const PodClass& C, int64_t t,
+                                             uint32_t lane, int64_t* __restrict__ wide) {
+    const PodWide acc{wide};
+    const uint32_t R = C.xreg + C.xinit + C.ovh;
+    const int64_t rt = t - C.t0;
+    for (int j = 0; j < PODS_PER_LANE; ++j) {
+        const int64_t s = lane * PODS_PER_LANE + j, i = t * TILE + s;
+        const uint32_t f = P.flags[i];
+        if (f & ESC_PF_DAEMONSET) continue;
+        uint64_t cpu = P.cpu0[i], mem = (uint64_t)P.mem0[i];
+        for (uint32_t k = 0; k < R; ++k) {
+            const int64_t o = C.xc0 + (rt * R + k) * TILE + s;
+            apply_rec(k, R, C.xreg, C.xreg + C.xinit, (unsigned long long)P.xc_cpu[o],
+                      (unsigned long long)P.xc_mem[o], cpu, mem);
+        }
+        if (pf_default_ok(f) && G.default_group != NONE) acc.add(G.n_gp, (int64_t)cpu, (int64_t)mem);
+        if (P.pair0[i] < G.n_gp) acc.add(P.pair0[i], (int64_t)cpu, (int64_t)mem);
+        for (uint32_t k = 0; k < C.nxp; ++k) {
+            const uint32_t q = P.xp[C.xp0 + (rt * C.nxp + k) * TILE + s];
+            if (q < G.n_gp) acc.add(q, (int64_t)cpu, (int64_t)mem);
+        }
+    }
+}
+}  // namespace
+
 // The whole shard through the exact accumulators (esc_force_wide; fallback testing).
 __global__ __launch_bounds__(256) void k_pod_wide(PodDev P, GroupDev G, int64_t* __restrict__ wide) {
     const uint32_t lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-    const PodWide acc{wide};
-    for (int64_t t = wave; t < P.s_tiles; t += nwaves) {
-        for (int j = 0; j < PODS_PER_LANE; ++j) {
-            const int64_t i = t * TILE + lane * PODS_PER_LANE + j;
-            const uint32_t f = P.flags[i];
-            if (f & ESC_PF_DAEMONSET) continue;
-            const int64_t cpu = (int64_t)P.cpu0[i], mem = P.mem0[i];
-            if (pf_default_ok(f) && G.default_group != NONE) acc.add(G.n_gp, cpu, mem);
-            if (P.pair0[i] < G.n_gp) acc.add(P.pair0[i], cpu, mem);
-        }
+    for (int64_t t = wave; t < P.k_tiles; t += nwaves) {
+        int ci = 0;
+        while (ci + 1 < P.n_cls && t >= P.cls[ci].t1) ++ci;
+        k_tile_exact(P, G, P.cls[ci], t, lane, wide);
     }
     for (int64_t t = wave; t < P.c_tiles; t += nwaves) c_tile_exact(P, G, t, lane, wide);
 }
@@ -927,25 +1091,18 @@ __global__ __launch_bounds__(256) void k_group_bounds(const uint64_t* __restrict
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st) {
     const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
-#define ESC_K1(T, A, DS, DC)                                                                              \
-    hipLaunchKernelGGL((k_pod_reduce<T, A, DS, DC>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, \
-                       wide)
+#define ESC_K1(T, A, DC)                                                                              \
+    hipLaunchKernelGGL((k_pod_reduce<T, A, DC>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, wide)
     switch (variant) {
-        case 1: ESC_K1(1024, 0, 2, 2); break;
-        case 2: ESC_K1(512, 0, 2, 2); break;
-        case 3: ESC_K1(1024, 0, 3, 3); break;
-        case 4: ESC_K1(1024, 0, 4, 4); break;
-        case 5: ESC_K1(1024, 0, 4, 2); break;
-        case 6: ESC_K1(1024, 0, 2, 4); break;
-        case 7: ESC_K1(1024, 0, 4, 3); break;
-        case 8: ESC_K1(1024, 0, 3, 4); break;
+        case 1: ESC_K1(1024, 0, 2); break;
+        case 2: ESC_K1(512, 0, 3); break;
         // Timing-only ablations (wrong results; scripts/k1_variants.py), see k_pod_reduce.
-        case 9: ESC_K1(1024, 1, 3, 3); break;
-        case 10: ESC_K1(1024, 2, 3, 3); break;
-        case 11: ESC_K1(1024, 4, 3, 3); break;
-        case 12: ESC_K1(1024, 3, 3, 3); break;
-        case 13: ESC_K1(1024, 5, 3, 3); break;
-        default: ESC_K1(1024, 0, 3, 3); break;
+        case 9: ESC_K1(1024, 1, 3); break;        // LDS atomics replaced by a sink
+        case 10: ESC_K1(1024, 2, 3); break;       // C tiles only
+        case 11: ESC_K1(1024, 4, 3); break;       // K tiles only
+        case 12: ESC_K1(1024, 4 | 32, 3); break;  // K tiles, loads only
+        case 13: ESC_K1(1024, 2 | 32, 3); break;  // C tiles, loads only
+        default: ESC_K1(1024, 0, 3); break;
     }
 #undef ESC_K1
     return hipGetLastError();

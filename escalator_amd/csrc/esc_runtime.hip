@@ -57,9 +57,10 @@ struct PodBuf {
     uint32_t *flags = nullptr, *cpu0 = nullptr, *pair0 = nullptr, *xp = nullptr, *xc_base = nullptr,
              *xp_base = nullptr, *big = nullptr;
     int64_t *mem0 = nullptr, *xc_cpu = nullptr, *xc_mem = nullptr;
+    PodClass* cls = nullptr;
     void release() {
         dfree(flags); dfree(cpu0); dfree(pair0); dfree(xp); dfree(xc_base); dfree(xp_base); dfree(big);
-        dfree(mem0); dfree(xc_cpu); dfree(xc_mem);
+        dfree(mem0); dfree(xc_cpu); dfree(xc_mem); dfree(cls);
     }
 };
 
@@ -102,7 +103,9 @@ struct esc_ctx {
     // snapshot
     std::vector<PodBuf> pods;
     int n_replicas = 1, cur = 0;
-    int64_t n_pods = 0, s_tiles = 0, c_tiles = 0, n_xc = 0, n_xp = 0, pod_offset = 0, n_big = 0;
+    int64_t k_weight = 0;
+    int64_t n_pods = 0, k_tiles = 0, c_tiles = 0, n_xc = 0, n_xp = 0, pod_offset = 0, n_big = 0;
+    int32_t n_cls = 0;
     bool pods_loaded = false;
     NodeBuf nodes;
     int64_t n_nodes = 0, n_xl = 0, n_trk = 0, node_lo = 0, node_hi = 0;
@@ -172,7 +175,10 @@ PodDev pod_dev(const esc_ctx* c, int replica) {
     p.flags = b.flags; p.cpu0 = b.cpu0; p.mem0 = b.mem0; p.pair0 = b.pair0;
     p.xc_cpu = b.xc_cpu; p.xc_mem = b.xc_mem; p.xp = b.xp;
     p.xc_base = b.xc_base; p.xp_base = b.xp_base;
-    p.s_tiles = c->s_tiles;
+    p.cls = b.cls;
+    p.n_cls = c->n_cls;
+    p.k_tiles = c->k_tiles;
+    p.k_weight = c->k_weight;
     p.c_tiles = c->c_tiles;
     return p;
 }
@@ -238,13 +244,16 @@ int32_t ensure_work(esc_ctx* c) {
     const int max_blocks = c->k1_variant == 2 ? 4 : 2;   // 2048 threads per CU
     const int per_cu = std::max(1, std::min(max_blocks, LDS_BYTES / std::max(lds, 1)));
     int64_t nblk = c->cu_count * per_cu;
-    // every workgroup takes ceil(s_tiles/nblk) S tiles + ceil(c_tiles/nblk) C tiles;
+    // every workgroup takes 1/nblk of the K tiles' weight + ceil(c_tiles/nblk) C tiles;
     // keep that within PODS_PER_BLOCK_MAX (exactness of the packed LDS partials)
     auto block_pods = [&](int64_t b) {
-        return ((c->s_tiles + b - 1) / b) * TILE + ((c->c_tiles + b - 1) / b) * CTILE;
+        // a weight share holds at most share / (lightest tile weight) + one partial tile
+        // per class
+        return ((c->k_weight + b - 1) / b / k_tile_weight(0, 0) + c->n_cls + 1) * TILE +
+               ((c->c_tiles + b - 1) / b) * CTILE;
     };
     while (block_pods(nblk) > PODS_PER_BLOCK_MAX) nblk *= 2;
-    nblk = std::min<int64_t>(nblk, std::max(c->s_tiles, c->c_tiles));
+    nblk = std::min<int64_t>(nblk, std::max(c->k_tiles, c->c_tiles));
     c->nblk = (int)nblk;
     HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * S));
     HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
@@ -272,7 +281,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     int nblk = 0;
     if (c->force_wide) {
-        if (c->s_tiles + c->c_tiles) HIP_TRY(launch_wide_pods(pod_dev(c, r), g, c->d_wide_pod, st));
+        if (c->k_tiles + c->c_tiles) HIP_TRY(launch_wide_pods(pod_dev(c, r), g, c->d_wide_pod, st));
     } else if (c->nblk) {
         const PodDev p = pod_dev(c, r);
         const int32_t S = (int32_t)pod_slots(c);
@@ -466,7 +475,6 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     // Validate the pair lists (ascending, unique, < ESC_PAIR_LIMIT: a pod matches each
     // group at most once) and the record counts; count the pods with extra records.
     uint64_t sc = 0, sp = 0;
-    int64_t n_c = 0;
     for (int64_t i = 0; i < n; ++i) {
         const uint32_t f = p->flags[i];
         const uint32_t nx = pf_xpair(f), nc = pf_xctr(f);
@@ -480,41 +488,109 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         }
         sc += nc;
         sp += nx;
-        n_c += (nc | nx) ? 1 : 0;
     }
     if ((int64_t)sc != p->n_xc || (int64_t)sp != p->n_xp) return ESC_E_INVAL;
-    // Stable partition: simple pods (no extra records) -> S section, padded to whole
-    // 256-pod tiles; the others -> C section of 64-pod tiles.  Records keep their order
-    // (simple pods own none), so only the per-pod arrays move.
-    const int64_t s_tiles = (n - n_c + TILE - 1) / TILE, c_tiles = (n_c + CTILE - 1) / CTILE;
-    const int64_t c0 = s_tiles * TILE, npad = c0 + c_tiles * CTILE;
+    // Layout.  Pods with at most 3 extra container records and at most 3
+    // extra pairs go to homogeneous K classes, one per record signature (extra regular /
+    // init containers, overhead, extra pairs), in 256-pod tiles whose records sit in
+    // per-tile rows; the rest go to 64-pod C tiles with per-tile record offsets.  Sums are
+    // order-independent, so the placement changes no result.  Padding pods carry
+    // ESC_PF_DAEMONSET, padding records are 0 and padding pairs NONE.
+    auto class_id = [](uint32_t f) -> int {
+        const uint32_t xr = pf_xreg(f), xi = pf_xinit(f), ov = (f & ESC_PF_HAS_OVH) ? 1u : 0u, np = pf_xpair(f);
+        if (xr + xi + ov > 3 || np > 3) return -1;
+        return (int)(((xr * 4 + xi) * 2 + ov) * 4 + np);
+    };
+    std::vector<int64_t> cnt(POD_CLASS_IDS, 0);
+    uint64_t sc_c = 0, sp_c = 0;
+    int64_t n_c = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint32_t f = p->flags[i];
+        const int id = class_id(f);
+        if (id >= 0) {
+            ++cnt[id];
+        } else {
+            ++n_c;
+            sc_c += pf_xctr(f);
+            sp_c += pf_xpair(f);
+        }
+    }
+    std::vector<PodClass> cls;
+    std::vector<int> cls_of(POD_CLASS_IDS, -1);
+    int64_t kt = 0, xk = 0, pk = 0, kw = 0;
+    for (int id = 0; id < POD_CLASS_IDS; ++id) {
+        if (!cnt[id]) continue;
+        PodClass k;
+        std::memset(&k, 0, sizeof k);
+        k.nxp = (uint32_t)(id % 4);
+        k.ovh = (uint32_t)((id / 4) % 2);
+        k.xinit = (uint32_t)((id / 8) % 4);
+        k.xreg = (uint32_t)(id / 32);
+        const int64_t R = k.xreg + k.xinit + k.ovh, tiles = (cnt[id] + TILE - 1) / TILE;
+        k.t0 = kt;
+        k.t1 = kt + tiles;
+        k.xc0 = xk;
+        k.xp0 = pk;
+        k.kind = (uint32_t)(R * 4 + k.nxp);
+        k.wt = k_tile_weight((uint32_t)R, k.nxp);
+        k.w0 = kw;
+        kw += tiles * k.wt;
+        kt += tiles;
+        xk += tiles * R * TILE;
+        pk += tiles * (int64_t)k.nxp * TILE;
+        cls_of[id] = (int)cls.size();
+        cls.push_back(k);
+    }
+    const int64_t k_tiles = kt, c_tiles = (n_c + CTILE - 1) / CTILE;
+    const int64_t c0 = k_tiles * TILE, npad = c0 + c_tiles * CTILE;
+    // record arrays: K rows, then the C records; one element of padding (K1 clamps its
+    // unconditional C record loads)
+    const int64_t nxc_dev = xk + (int64_t)sc_c + 1, nxp_dev = pk + (int64_t)sp_c + 1;
+    if (nxc_dev >= (int64_t)0xFFFFFFFF || nxp_dev >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
     std::vector<uint32_t> hf(npad, ESC_PF_DAEMONSET), hc(npad, 0), hp(npad, NONE);
-    std::vector<int64_t> hm(npad, 0);
+    std::vector<int64_t> hm(npad, 0), hxc(nxc_dev, 0), hxm(nxc_dev, 0);
+    std::vector<uint32_t> hxp(nxp_dev, NONE);
     std::vector<uint32_t> xc_base(c_tiles + 1, 0), xp_base(c_tiles + 1, 0);
     {
-        int64_t is = 0, ic = 0;
-        uint32_t oc = 0, op = 0;
+        std::vector<int64_t> pos(POD_CLASS_IDS, 0);
+        int64_t ic = 0;
+        uint64_t rc = 0, rp = 0;                          // the pod's records in the input
+        uint64_t oc = (uint64_t)xk, op = (uint64_t)pk;    // C record cursors
         for (int64_t i = 0; i < n; ++i) {
             const uint32_t f = p->flags[i];
             const uint32_t nx = pf_xpair(f), nc = pf_xctr(f);
+            const int id = class_id(f);
             int64_t d;
-            if ((nc | nx) == 0) {
-                d = is++;
+            if (id >= 0) {
+                const PodClass& k = cls[cls_of[id]];
+                const int64_t q = pos[id]++, rt = q / TILE, sl = q % TILE;
+                d = (k.t0 + rt) * TILE + sl;
+                for (uint32_t j = 0; j < nc; ++j) {
+                    const int64_t o = k.xc0 + (rt * nc + j) * TILE + sl;
+                    hxc[o] = p->xc_cpu[rc + j];
+                    hxm[o] = p->xc_mem[rc + j];
+                }
+                for (uint32_t j = 0; j < nx; ++j) hxp[k.xp0 + (rt * nx + j) * TILE + sl] = p->xp_pair[rp + j];
             } else {
-                if (ic % CTILE == 0) { xc_base[ic / CTILE] = oc; xp_base[ic / CTILE] = op; }
+                if (ic % CTILE == 0) { xc_base[ic / CTILE] = (uint32_t)oc; xp_base[ic / CTILE] = (uint32_t)op; }
                 d = c0 + ic++;
+                for (uint32_t j = 0; j < nc; ++j) { hxc[oc + j] = p->xc_cpu[rc + j]; hxm[oc + j] = p->xc_mem[rc + j]; }
+                for (uint32_t j = 0; j < nx; ++j) hxp[op + j] = p->xp_pair[rp + j];
                 oc += nc;
                 op += nx;
             }
+            rc += nc;
+            rp += nx;
             hf[d] = f; hc[d] = p->cpu0[i]; hm[d] = p->mem0[i]; hp[d] = p->pair0[i];
         }
-        xc_base[c_tiles] = oc;
-        xp_base[c_tiles] = op;
+        xc_base[c_tiles] = (uint32_t)oc;
+        xp_base[c_tiles] = (uint32_t)op;
     }
     // C tiles with more extra records than a wave holds in registers go to k_pod_bigtiles.
     std::vector<uint32_t> big;
     for (int64_t t = 0; t < c_tiles; ++t)
         if (xc_base[t + 1] - xc_base[t] > 128 || xp_base[t + 1] - xp_base[t] > 128) big.push_back((uint32_t)t);
+    const int64_t n_cls = (int64_t)cls.size();
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     drop_graphs(c);
@@ -525,44 +601,30 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     for (int r = 0; r < c->n_replicas; ++r) {
         PodBuf& b = c->pods[r];
         HIP_TRY(dalloc(&b.flags, npad)); HIP_TRY(dalloc(&b.cpu0, npad)); HIP_TRY(dalloc(&b.mem0, npad));
-        // record arrays: one element of padding (K1 clamps its unconditional record loads)
-        HIP_TRY(dalloc(&b.pair0, npad)); HIP_TRY(dalloc(&b.xc_cpu, p->n_xc + 1)); HIP_TRY(dalloc(&b.xc_mem, p->n_xc + 1));
-        HIP_TRY(dalloc(&b.xp, p->n_xp + 1)); HIP_TRY(dalloc(&b.xc_base, c_tiles + 1)); HIP_TRY(dalloc(&b.xp_base, c_tiles + 1));
-        HIP_TRY(dalloc(&b.big, big.size()));
-        if (!big.empty()) HIP_TRY(hipMemcpy(b.big, big.data(), big.size() * 4, hipMemcpyHostToDevice));
-        if (r == 0) {
-            if (npad) {
-                HIP_TRY(hipMemcpy(b.flags, hf.data(), npad * 4, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemcpy(b.cpu0, hc.data(), npad * 4, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemcpy(b.mem0, hm.data(), npad * 8, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemcpy(b.pair0, hp.data(), npad * 4, hipMemcpyHostToDevice));
-            }
-            if (p->n_xc) {
-                HIP_TRY(hipMemcpy(b.xc_cpu, p->xc_cpu, p->n_xc * 8, hipMemcpyHostToDevice));
-                HIP_TRY(hipMemcpy(b.xc_mem, p->xc_mem, p->n_xc * 8, hipMemcpyHostToDevice));
-            }
-            if (p->n_xp) HIP_TRY(hipMemcpy(b.xp, p->xp_pair, p->n_xp * 4, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(b.xc_base, xc_base.data(), (c_tiles + 1) * 4, hipMemcpyHostToDevice));
-            HIP_TRY(hipMemcpy(b.xp_base, xp_base.data(), (c_tiles + 1) * 4, hipMemcpyHostToDevice));
-        } else {
-            const PodBuf& a = c->pods[0];
-            if (npad) {
-                HIP_TRY(hipMemcpy(b.flags, a.flags, npad * 4, hipMemcpyDeviceToDevice));
-                HIP_TRY(hipMemcpy(b.cpu0, a.cpu0, npad * 4, hipMemcpyDeviceToDevice));
-                HIP_TRY(hipMemcpy(b.mem0, a.mem0, npad * 8, hipMemcpyDeviceToDevice));
-                HIP_TRY(hipMemcpy(b.pair0, a.pair0, npad * 4, hipMemcpyDeviceToDevice));
-            }
-            if (p->n_xc) {
-                HIP_TRY(hipMemcpy(b.xc_cpu, a.xc_cpu, p->n_xc * 8, hipMemcpyDeviceToDevice));
-                HIP_TRY(hipMemcpy(b.xc_mem, a.xc_mem, p->n_xc * 8, hipMemcpyDeviceToDevice));
-            }
-            if (p->n_xp) HIP_TRY(hipMemcpy(b.xp, a.xp, p->n_xp * 4, hipMemcpyDeviceToDevice));
-            HIP_TRY(hipMemcpy(b.xc_base, a.xc_base, (c_tiles + 1) * 4, hipMemcpyDeviceToDevice));
-            HIP_TRY(hipMemcpy(b.xp_base, a.xp_base, (c_tiles + 1) * 4, hipMemcpyDeviceToDevice));
+        HIP_TRY(dalloc(&b.pair0, npad)); HIP_TRY(dalloc(&b.xc_cpu, nxc_dev)); HIP_TRY(dalloc(&b.xc_mem, nxc_dev));
+        HIP_TRY(dalloc(&b.xp, nxp_dev)); HIP_TRY(dalloc(&b.xc_base, c_tiles + 1)); HIP_TRY(dalloc(&b.xp_base, c_tiles + 1));
+        HIP_TRY(dalloc(&b.big, big.size())); HIP_TRY(dalloc(&b.cls, n_cls));
+        const hipMemcpyKind kind = r == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+        const PodBuf& a = c->pods[0];
+        auto src = [&](const void* host, const void* dev) { return r == 0 ? host : dev; };
+        if (npad) {
+            HIP_TRY(hipMemcpy(b.flags, src(hf.data(), a.flags), npad * 4, kind));
+            HIP_TRY(hipMemcpy(b.cpu0, src(hc.data(), a.cpu0), npad * 4, kind));
+            HIP_TRY(hipMemcpy(b.mem0, src(hm.data(), a.mem0), npad * 8, kind));
+            HIP_TRY(hipMemcpy(b.pair0, src(hp.data(), a.pair0), npad * 4, kind));
         }
+        HIP_TRY(hipMemcpy(b.xc_cpu, src(hxc.data(), a.xc_cpu), nxc_dev * 8, kind));
+        HIP_TRY(hipMemcpy(b.xc_mem, src(hxm.data(), a.xc_mem), nxc_dev * 8, kind));
+        HIP_TRY(hipMemcpy(b.xp, src(hxp.data(), a.xp), nxp_dev * 4, kind));
+        HIP_TRY(hipMemcpy(b.xc_base, src(xc_base.data(), a.xc_base), (c_tiles + 1) * 4, kind));
+        HIP_TRY(hipMemcpy(b.xp_base, src(xp_base.data(), a.xp_base), (c_tiles + 1) * 4, kind));
+        if (!big.empty()) HIP_TRY(hipMemcpy(b.big, src(big.data(), a.big), big.size() * 4, kind));
+        if (n_cls) HIP_TRY(hipMemcpy(b.cls, src(cls.data(), a.cls), n_cls * sizeof(PodClass), kind));
     }
     c->n_pods = n;
-    c->s_tiles = s_tiles;
+    c->k_tiles = k_tiles;
+    c->k_weight = kw;
+    c->n_cls = (int32_t)n_cls;
     c->c_tiles = c_tiles;
     c->n_big = (int64_t)big.size();
     c->n_xc = p->n_xc;

@@ -3,20 +3,24 @@ restatement of what ``esc_stream_bytes`` reports, used to cross-check it.
 
 K1 reads the pod shard once per decision: per pod flags 4 + cpu0 4 + mem0 8 + pair0 4 B,
 16 B per extra container record, 4 B per extra selector pair, and 8 B of record offsets
-per 64-pod C tile (the pods that own extra records, placed in their own section at load).
+per 64-pod C tile (pods with more than 3 extra container records or more than 3 extra
+pairs; all other pods sit in homogeneous 256-pod K tiles that need no offsets).
 K2 reads the node index once per decision: 24 B per (label pair, node) entry of a pair
 some group selects (flags 4 + cpu 8 + mem 8 + node 4) and 8 B per piece (offset + pair);
 a rank reads the pieces that start in its 1/world share of the entries.
 """
 import numpy as np
 
-XTRA_MASK = 0x3FFFFF10      # ESC_PF_HAS_OVH | extra container counts | extra pair count
 NODE_PIECE = 1024
 NONE = 0xFFFFFFFF
 
 
 def complex_pods(flags: np.ndarray) -> int:
-    return int(np.count_nonzero(np.asarray(flags) & XTRA_MASK))
+    """Pods outside the homogeneous K classes (more than 3 extra container records or
+    more than 3 extra pairs): they go to the 64-pod C tiles."""
+    f = np.asarray(flags, np.uint64)
+    recs = ((f >> 8) & 0xFF) + ((f >> 16) & 0xFF) + ((f >> 4) & 1)
+    return int(np.count_nonzero((recs > 3) | (((f >> 24) & 0x3F) > 3)))
 
 
 def pod_bytes(flags: np.ndarray, n_xc: int, n_xp: int) -> int:

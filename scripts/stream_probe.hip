@@ -1,0 +1,127 @@
+// stream_probe.hip — practical HBM read ceiling on this MI355X for the access shapes K1 uses.
+// Standalone measurement tool (not part of the product): reads a 2.4 GB buffer with
+// 16-B-per-lane loads in several launch shapes and prints GB/s per shape as JSON.
+//   hipcc --offload-arch=gfx950 -O3 -o stream_probe scripts/stream_probe.hip
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                      \
+    do {                                                                           \
+        hipError_t e_ = (x);                                                       \
+        if (e_ != hipSuccess) {                                                    \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                               \
+        }                                                                          \
+    } while (0)
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+// Contiguous share per workgroup; waves interleave 1-KB wave tiles; U loads per lane in flight.
+template <int THREADS, int U, bool NT>
+__global__ __launch_bounds__(THREADS) void k_chunk(const uint4* __restrict__ p, int64_t n16, uint32_t* out) {
+    const int64_t per = (n16 + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * per;
+    const int64_t hi = lo + per < n16 ? lo + per : n16;
+    uint32_t acc = 0;
+    for (int64_t b = lo + threadIdx.x; b < hi; b += (int64_t)THREADS * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = b + (int64_t)u * THREADS;
+            const int64_t j = i < hi ? i : lo;
+            if constexpr (NT) {
+                const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p + j));
+                v[u] = make_uint4(t.x, t.y, t.z, t.w);
+            } else {
+                v[u] = p[j];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// Grid-stride (every wave walks the whole buffer at a stride of the grid).
+template <int THREADS, int U>
+__global__ __launch_bounds__(THREADS) void k_stride(const uint4* __restrict__ p, int64_t n16, uint32_t* out) {
+    const int64_t stride = (int64_t)gridDim.x * THREADS;
+    uint32_t acc = 0;
+    for (int64_t b = (int64_t)blockIdx.x * THREADS + threadIdx.x; b < n16; b += stride * U) {
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = b + (int64_t)u * stride;
+            v[u] = p[i < n16 ? i : b];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <class F>
+static float time_ms(F&& launch, int reps) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    launch();
+    CK(hipDeviceSynchronize());
+    std::vector<float> ts;
+    for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(a));
+        launch();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        ts.push_back(ms);
+    }
+    std::sort(ts.begin(), ts.end());
+    return ts[ts.size() / 2];
+}
+
+int main() {
+    const int64_t bytes = 2400ll << 20;
+    const int64_t n16 = bytes / 16;
+    uint4* p;
+    uint32_t* out;
+    CK(hipMalloc(&p, bytes));
+    CK(hipMalloc(&out, 4));
+    CK(hipMemset(p, 1, bytes));
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    printf("{\"bytes\": %lld, \"cus\": %d, \"GBps\": {", (long long)bytes, cus);
+    bool first = true;
+    auto rep = [&](const char* name, float ms) {
+        printf("%s\"%s\": %.0f", first ? "" : ", ", name, bytes / (ms * 1e-3) / 1e9);
+        first = false;
+        fflush(stdout);
+    };
+#define RUN_CHUNK(T, U, NT, WPC)                                                                         \
+    rep("chunk_t" #T "_u" #U "_nt" #NT "_wgpercu" #WPC,                                                   \
+        time_ms([&] { hipLaunchKernelGGL((k_chunk<T, U, NT>), dim3(cus * WPC), dim3(T), 0, 0, p, n16, out); }, 10))
+    RUN_CHUNK(1024, 2, false, 1);
+    RUN_CHUNK(1024, 4, false, 1);
+    RUN_CHUNK(1024, 8, false, 1);
+    RUN_CHUNK(1024, 4, true, 1);
+    RUN_CHUNK(1024, 4, false, 2);
+    RUN_CHUNK(512, 4, false, 2);
+    RUN_CHUNK(512, 4, false, 4);
+    RUN_CHUNK(256, 4, false, 8);
+    RUN_CHUNK(256, 8, false, 8);
+    RUN_CHUNK(256, 4, false, 16);
+    RUN_CHUNK(256, 4, false, 64);
+#define RUN_STRIDE(T, U, WPC)                                                                             \
+    rep("stride_t" #T "_u" #U "_wgpercu" #WPC,                                                           \
+        time_ms([&] { hipLaunchKernelGGL((k_stride<T, U>), dim3(cus * WPC), dim3(T), 0, 0, p, n16, out); }, 10))
+    RUN_STRIDE(1024, 4, 1);
+    RUN_STRIDE(256, 4, 8);
+    RUN_STRIDE(256, 8, 8);
+    printf("}}\n");
+    return 0;
+}
