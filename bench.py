@@ -223,8 +223,10 @@ def main():
                      "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) if traffic else None,
                      "algorithmic_bytes_per_launch": algo, "launch_ms": k1_ms},
         "node_bytes_per_decision": node_b,
-        "stage_ms": {"k_pod_reduce": stage_mean[0], "k_node_pieces": stage_mean[1], "k_combine": stage_mean[2],
-                     "d2h": stage_mean[3]} if world == 1 else None,
+        # stages timed in order on one stream (timing mode); "d2h" only when the decisions
+        # are copied rather than written to pinned host memory by K3 (zero-copy)
+        "stage_ms": {k: float(v) for k, v in zip(["k_pod_reduce", "k_node_pieces", "k_combine", "d2h"], stage_mean)
+                     if v > 0} if world == 1 else None,
         "parity": parity,
     }
     if world == 1 and not args.no_cpu_baseline:

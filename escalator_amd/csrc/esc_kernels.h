@@ -113,9 +113,10 @@ enum WidePod : int { WP_CPU_LO = 0, WP_CPU_HI, WP_MEM_LO, WP_MEM_HI, WP_CNT, WP_
 // Per dry-mode group: the tracked members' count and split sums (K2 adds, K3 resets).
 enum TrkAcc : int { TA_CNT = 0, TA_CPU_LO, TA_CPU_HI, TA_MEM_LO, TA_MEM_HI, TA_K };
 
-// variant (ESC_K1_VARIANT, measurement knob): 0 = 1024 threads (default), 1 = two C tiles
-// in flight, 2 = 512 threads, 9.. = timing-only ablations (wrong results,
-// scripts/k1_variants.py).
+// variant (ESC_K1_VARIANT, measurement knob): 0 = 512 threads (default: 8 waves per CU with
+// up to 256 VGPRs, 3-4 K tiles in flight per wave), 1 = two C tiles in flight, 2 = 1024
+// threads (16 waves, 128 VGPRs, 1-3 tiles in flight), 9.. = timing-only ablations (wrong
+// results, scripts/k1_variants.py).
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st);
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,

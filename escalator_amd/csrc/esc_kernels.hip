@@ -216,23 +216,29 @@ __device__ __forceinline__ PodClass load_class(const PodClass* cls, int i) {
     return k;
 }
 
+// In-tile positions: pod j of lane l is element 4l + j of the 4-byte arrays and element
+// (j / 2) * 128 + 2l + j % 2 of the 8-byte ones (pos64), so that every wave-load of either
+// width reads one contiguous 1 KB (an 8-byte array read as lanes x 4 consecutive pods would
+// stride 32 B and double the requests per byte).
+__device__ __forceinline__ int64_t pos64(uint32_t s) { return ((s & 3) >> 1) * 128 + 2 * (s >> 2) + (s & 1); }
+
 template <int R, int NXP>
 __device__ __forceinline__ void k_load(const PodDev& P, const PodClass& C, int64_t t, uint32_t lane,
                                        KTile<R, NXP>& T) {
-    const int64_t p0 = t * TILE + lane * PODS_PER_LANE;
+    const int64_t p0 = t * TILE + lane * PODS_PER_LANE, q0 = t * TILE + lane * 2;
     T.f = ld4(P.flags + p0);
     T.c = ld4(P.cpu0 + p0);
-    T.m[0] = ld2(P.mem0 + p0);
-    T.m[1] = ld2(P.mem0 + p0 + 2);
+    T.m[0] = ld2(P.mem0 + q0);
+    T.m[1] = ld2(P.mem0 + q0 + 128);
     T.p = ld4(P.pair0 + p0);
     const int64_t rt = t - C.t0;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        const int64_t o = C.xc0 + (rt * R + k) * TILE + lane * PODS_PER_LANE;
+        const int64_t o = C.xc0 + (rt * R + k) * TILE + lane * 2;
         T.rc[k][0] = ld2(P.xc_cpu + o);
-        T.rc[k][1] = ld2(P.xc_cpu + o + 2);
+        T.rc[k][1] = ld2(P.xc_cpu + o + 128);
         T.rm[k][0] = ld2(P.xc_mem + o);
-        T.rm[k][1] = ld2(P.xc_mem + o + 2);
+        T.rm[k][1] = ld2(P.xc_mem + o + 128);
     }
 #pragma unroll
     for (int k = 0; k < NXP; ++k) T.rq[k] = ld4(P.xp + C.xp0 + (rt * NXP + k) * TILE + lane * PODS_PER_LANE);
@@ -297,7 +303,9 @@ template <int R, int NXP, int NW, int ABLATE>
 __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const PodSink<ABLATE>& K,
                                       const PodClass& C, int64_t a, int64_t b, uint32_t lane) {
     constexpr int L = 5 + 4 * R + NXP;                   // 16-B loads per lane per tile
-    constexpr int DS = L <= 7 ? 3 : (L <= 10 ? 2 : 1);
+    // slots that fit the VGPR budget: 16 waves per CU leave 128 VGPRs a wave, 8 leave 256
+    constexpr int DS = NW >= 16 ? (L <= 7 ? 3 : (L <= 10 ? 2 : 1))
+                                : (4 * L * 4 <= 176 ? 4 : (4 * L * 3 <= 176 ? 3 : (4 * L * 2 <= 176 ? 2 : 1)));
     KTile<R, NXP> T[DS];
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
@@ -566,12 +574,13 @@ __device__ __forceinline__ void k_tile_exact(const PodDev& P, const GroupDev& G,
     const uint32_t R = C.xreg + C.xinit + C.ovh;
     const int64_t rt = t - C.t0;
     for (int j = 0; j < PODS_PER_LANE; ++j) {
-        const int64_t s = lane * PODS_PER_LANE + j, i = t * TILE + s;
+        const uint32_t s = lane * PODS_PER_LANE + j;
+        const int64_t i = t * TILE + s, i64 = t * TILE + pos64(s);
         const uint32_t f = P.flags[i];
         if (f & ESC_PF_DAEMONSET) continue;
-        uint64_t cpu = P.cpu0[i], mem = (uint64_t)P.mem0[i];
+        uint64_t cpu = P.cpu0[i], mem = (uint64_t)P.mem0[i64];
         for (uint32_t k = 0; k < R; ++k) {
-            const int64_t o = C.xc0 + (rt * R + k) * TILE + s;
+            const int64_t o = C.xc0 + (rt * R + k) * TILE + pos64(s);
             apply_rec(k, R, C.xreg, C.xreg + C.xinit, (unsigned long long)P.xc_cpu[o],
                       (unsigned long long)P.xc_mem[o], cpu, mem);
         }
@@ -1094,15 +1103,15 @@ hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int
 #define ESC_K1(T, A, DC)                                                                              \
     hipLaunchKernelGGL((k_pod_reduce<T, A, DC>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, wide)
     switch (variant) {
-        case 1: ESC_K1(1024, 0, 2); break;
-        case 2: ESC_K1(512, 0, 3); break;
+        case 1: ESC_K1(512, 0, 2); break;
+        case 2: ESC_K1(1024, 0, 3); break;
         // Timing-only ablations (wrong results; scripts/k1_variants.py), see k_pod_reduce.
-        case 9: ESC_K1(1024, 1, 3); break;        // LDS atomics replaced by a sink
-        case 10: ESC_K1(1024, 2, 3); break;       // C tiles only
-        case 11: ESC_K1(1024, 4, 3); break;       // K tiles only
-        case 12: ESC_K1(1024, 4 | 32, 3); break;  // K tiles, loads only
-        case 13: ESC_K1(1024, 2 | 32, 3); break;  // C tiles, loads only
-        default: ESC_K1(1024, 0, 3); break;
+        case 9: ESC_K1(512, 1, 3); break;        // LDS atomics replaced by a sink
+        case 10: ESC_K1(512, 2, 3); break;       // C tiles only
+        case 11: ESC_K1(512, 4, 3); break;       // K tiles only
+        case 12: ESC_K1(512, 4 | 32, 3); break;  // K tiles, loads only
+        case 13: ESC_K1(512, 2 | 32, 3); break;  // C tiles, loads only
+        default: ESC_K1(512, 0, 3); break;
     }
 #undef ESC_K1
     return hipGetLastError();

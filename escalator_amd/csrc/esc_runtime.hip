@@ -122,6 +122,11 @@ struct esc_ctx {
     int64_t *own_words = nullptr, *own_first = nullptr;      // context-owned ones
     esc_group_decision* d_dec = nullptr;
     esc_group_decision* h_dec = nullptr;
+    esc_group_decision* h_dec_dev = nullptr;                 // device view of h_dec (zero-copy)
+    bool zero_copy = true;                                    // K3/K4 write decisions to h_dec
+    bool fork_nodes = true;                                   // K2 on the side stream, beside K1
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int64_t *bound_words = nullptr, *bound_first = nullptr;  // caller-bound (RCCL) buffers
     bool work_ready = false;
     bool force_wide = false;
@@ -220,6 +225,7 @@ void release_work(esc_ctx* c) {
     c->d_first = nullptr;
     if (c->h_dec) hipHostFree(c->h_dec);
     c->h_dec = nullptr;
+    c->h_dec_dev = nullptr;
     c->work_ready = false;
     drop_graphs(c);
 }
@@ -241,7 +247,7 @@ int32_t ensure_work(esc_ctx* c) {
     const int64_t S = pod_slots(c);
     const int gw = (int)std::min<int64_t>(S, POD_WINDOW_MAX);
     const int lds = gw * 16;
-    const int max_blocks = c->k1_variant == 2 ? 4 : 2;   // 2048 threads per CU
+    const int max_blocks = c->k1_variant == 2 ? 2 : 4;   // 2048 threads per CU
     const int per_cu = std::max(1, std::min(max_blocks, LDS_BYTES / std::max(lds, 1)));
     int64_t nblk = c->cu_count * per_cu;
     // every workgroup takes 1/nblk of the K tiles' weight + ceil(c_tiles/nblk) C tiles;
@@ -268,17 +274,27 @@ int32_t ensure_work(esc_ctx* c) {
     c->d_first = c->bound_first ? c->bound_first : c->own_first;
     HIP_TRY(dalloc(&c->d_dec, (size_t)G));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_dec), (size_t)G * sizeof(esc_group_decision)));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_dec_dev), c->h_dec, 0));
     c->work_ready = true;
     return ESC_OK;
 }
 
-// Enqueue K1 + K2 + K3 (and K4 + the decision copy when decide) for replica r.
+// Enqueue K1 + K2 + K3 (and K4 + the decisions when decide) for replica r.  K2 (nodes)
+// runs on the side stream beside K1 (it needs no LDS, so its waves fit next to K1's
+// workgroups) and K3 joins both; with timing on, the stages run in order on one stream so
+// that each has its own events.  Decisions go straight to pinned host memory (zero-copy)
+// unless disabled, in which case a copy follows K3.
 int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     const GroupDev g = group_dev(c);
     const NodeDev n = node_dev(c);
     hipStream_t st = c->stream;
+    const bool fork = c->fork_nodes && !c->timing && c->side;
     int e = 0;
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    if (fork) {
+        HIP_TRY(hipEventRecord(c->ev_fork, st));
+        HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+    }
     int nblk = 0;
     if (c->force_wide) {
         if (c->k_tiles + c->c_tiles) HIP_TRY(launch_wide_pods(pod_dev(c, r), g, c->d_wide_pod, st));
@@ -292,13 +308,20 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
         HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
         nblk = c->nblk;
     }
+    if (fork) {
+        HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, c->side));
+        HIP_TRY(hipEventRecord(c->ev_join, c->side));
+        HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
+    } else {
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+        HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, st));
+    }
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-    HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, st));
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    esc_group_decision* dec = c->zero_copy ? c->h_dec_dev : c->d_dec;
     HIP_TRY(launch_combine(g, n, c->d_pod_part, nblk, c->nodes.rows, c->d_wide_pod, c->d_wp_cnt, c->d_trk_acc,
-                           c->d_words, c->d_first, decide, c->d_dec, st));
+                           c->d_words, c->d_first, decide, dec, st));
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-    if (copy_out) {
+    if (copy_out && !c->zero_copy) {
         HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)g.G * sizeof(esc_group_decision),
                                hipMemcpyDeviceToHost, st));
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
@@ -387,6 +410,12 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     c->own_stream = true;
     for (int i = 0; i < MAX_STAGES; ++i)
         if (hipEventCreate(&c->ev[i]) != hipSuccess) return fail(ESC_E_HIP);
+    if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
+        return fail(ESC_E_HIP);
+    if (const char* v = std::getenv("ESC_NO_FORK")) c->fork_nodes = std::atoi(v) == 0;
+    if (const char* v = std::getenv("ESC_NO_ZEROCOPY")) c->zero_copy = std::atoi(v) == 0;
     const size_t G = (size_t)n_groups;
     if (dalloc(&c->d_dry, G) || dalloc(&c->d_params, G)) return fail(ESC_E_NOMEM);
     const GroupIndex& gi = c->gi;
@@ -427,6 +456,10 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         dfree(c->d_gpair); dfree(c->d_node_code); dfree(c->d_code_list); dfree(c->d_slot_readers);
         for (int i = 0; i < MAX_STAGES; ++i)
             if (c->ev[i]) hipEventDestroy(c->ev[i]);
+        if (c->side) hipStreamSynchronize(c->side);
+        if (c->ev_fork) hipEventDestroy(c->ev_fork);
+        if (c->ev_join) hipEventDestroy(c->ev_join);
+        if (c->side) hipStreamDestroy(c->side);
         if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     }
     delete c;
@@ -560,20 +593,22 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
             const uint32_t f = p->flags[i];
             const uint32_t nx = pf_xpair(f), nc = pf_xctr(f);
             const int id = class_id(f);
-            int64_t d;
+            int64_t d, d64;                               // slot in the 4- / 8-byte arrays
             if (id >= 0) {
                 const PodClass& k = cls[cls_of[id]];
                 const int64_t q = pos[id]++, rt = q / TILE, sl = q % TILE;
+                const int64_t s64 = ((sl & 3) >> 1) * 128 + 2 * (sl >> 2) + (sl & 1);   // K1's pos64
                 d = (k.t0 + rt) * TILE + sl;
+                d64 = (k.t0 + rt) * TILE + s64;
                 for (uint32_t j = 0; j < nc; ++j) {
-                    const int64_t o = k.xc0 + (rt * nc + j) * TILE + sl;
+                    const int64_t o = k.xc0 + (rt * nc + j) * TILE + s64;
                     hxc[o] = p->xc_cpu[rc + j];
                     hxm[o] = p->xc_mem[rc + j];
                 }
                 for (uint32_t j = 0; j < nx; ++j) hxp[k.xp0 + (rt * nx + j) * TILE + sl] = p->xp_pair[rp + j];
             } else {
                 if (ic % CTILE == 0) { xc_base[ic / CTILE] = (uint32_t)oc; xp_base[ic / CTILE] = (uint32_t)op; }
-                d = c0 + ic++;
+                d = d64 = c0 + ic++;
                 for (uint32_t j = 0; j < nc; ++j) { hxc[oc + j] = p->xc_cpu[rc + j]; hxm[oc + j] = p->xc_mem[rc + j]; }
                 for (uint32_t j = 0; j < nx; ++j) hxp[op + j] = p->xp_pair[rp + j];
                 oc += nc;
@@ -581,7 +616,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
             }
             rc += nc;
             rp += nx;
-            hf[d] = f; hc[d] = p->cpu0[i]; hm[d] = p->mem0[i]; hp[d] = p->pair0[i];
+            hf[d] = f; hc[d] = p->cpu0[i]; hm[d64] = p->mem0[i]; hp[d] = p->pair0[i];
         }
         xc_base[c_tiles] = (uint32_t)oc;
         xp_base[c_tiles] = (uint32_t)op;
@@ -881,9 +916,11 @@ int32_t esc_decide(esc_ctx* c) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
     hipSetDevice(c->device);
-    HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_words, c->d_first, c->d_dec, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)c->gi.G * sizeof(esc_group_decision),
-                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_words, c->d_first,
+                          c->zero_copy ? c->h_dec_dev : c->d_dec, c->stream));
+    if (!c->zero_copy)
+        HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)c->gi.G * sizeof(esc_group_decision),
+                               hipMemcpyDeviceToHost, c->stream));
     c->pending = true;
     return ESC_OK;
 }
