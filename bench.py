@@ -94,16 +94,80 @@ def cpu_baseline(cfg, G, seconds=12.0):
     }
 
 
+def bench_order(args):
+    """BASELINE config #5: the scale-down / scale-up orderings over 10M nodes (taintOldestN
+    scale_down.go:171, untaintNewestN scale_up.go:118).  Times (a) the per-decision ordering
+    (esc_sort_nodes: classify every membership, stable partition by (group, class)) and
+    (b) the age-index build it relies on (esc_build_age_index: LSD radix sort of the 10M
+    creation times + the memberships in age order, once per snapshot)."""
+    import numpy as np
+    import escalator_amd as esc
+    from oracle import soa
+    N, G = 10_000_000, 100
+    s = esc.Synth(100_000, N, G, config=5, seed=0xE5CA1A7E00000005, threads=16)
+    ctx = esc.Context(s)
+    ctx.load_synth(s)
+
+    def timed(fn, k):
+        for _ in range(args.warmup):
+            fn()
+        ctx.sync()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        ctx.sync()
+        return (time.perf_counter() - t0) / k * 1e3
+
+    order_ms = timed(ctx.sort_nodes, args.steps)
+    index_ms = timed(ctx.build_age_index, max(3, args.steps // 4))
+    ctx.sort_nodes()
+    counts = [len(ctx.group_order(g, w)) for g in range(G) for w in (0, 1)]
+    nodes = s.nodes()
+    parity = all(np.array_equal(ctx.group_order(g, w), soa.order(nodes, s.groups, g, w)) for g in (0, 37, 99)
+                 for w in (0, 1))
+    n_memb, R = ctx.order_info()
+    # bytes the ordering moves per membership: classify 12 read + 8 written; each 8-bit LSD
+    # pass over the (group << 2 | class) keys: 4 (histogram) + 8 read + 8 written
+    passes = -(-max(1, int(np.ceil(np.log2(4 * G)))) // 8)
+    order_bytes = n_memb * (20 + passes * 20)
+    idx_passes = -(-R // 8)
+    index_bytes = N * (16 + idx_passes * 32)       # keys 8 + vals 4 per pass (hist 8 + r/w 24), + entries
+    out = {
+        "metric": "config5 node orderings: memberships ordered/sec per decision (taint/untaint selection)",
+        "value": n_memb / (order_ms * 1e-3),
+        "unit": "memberships/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": order_ms,
+        "higher_is_better": True,
+        "dtype": "int64 keys",
+        "data": "synthetic (esc_synth.cpp config 5: 10M nodes, 100 groups, unique ns creation times)",
+        "config": {"workload": "config5: 10M nodes oldest-first / newest-first orderings, 100 node groups",
+                   "nodes": N, "node_groups": G, "memberships": n_memb},
+        "roofline": {"bound": "hbm", "kernel": "per-decision ordering (classify + %d partition pass(es))" % passes,
+                     "achieved": order_bytes / (order_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": order_bytes / (order_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_decision": order_bytes},
+        "age_index_build": {"ms": index_ms, "nodes_per_s": N / (index_ms * 1e-3), "key_bits": R,
+                            "lsd_passes": idx_passes, "GBps_moved": index_bytes / (index_ms * 1e-3) / 1e9},
+        "segments_nonempty": int(sum(1 for c in counts if c)),
+        "parity": "bit-exact vs C oracle on groups 0, 37, 99 (both orders)" if parity else "MISMATCH",
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS))
+    ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS) + [5])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     args = ap.parse_args()
 
+    if args.config == 5:
+        return bench_order(args)
     rank, world, local = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1), ("LOCAL_RANK", 0)))
     cfg = dict(CONFIGS[args.config], cfg=args.config)
     P, N, G = cfg["P"], cfg["N"], cfg["G"]

@@ -246,6 +246,16 @@ class Context:
     def sort_nodes(self):
         L.check(self.lib.esc_sort_nodes(self.handle), "esc_sort_nodes")
 
+    def order_info(self) -> tuple[int, int]:
+        """(memberships of the node range, creation-key bits of the age index)."""
+        n, b = C.c_int64(), C.c_int32()
+        L.check(self.lib.esc_order_info(self.handle, C.byref(n), C.byref(b)), "esc_order_info")
+        return n.value, b.value
+
+    def build_age_index(self):
+        """Re-run the snapshot's age index build (normally done by load)."""
+        L.check(self.lib.esc_build_age_index(self.handle), "esc_build_age_index")
+
     def group_order(self, group: int, which: int, cap: int | None = None) -> np.ndarray:
         n = C.c_int64()
         L.check(self.lib.esc_group_order(self.handle, group, which, None, 0, C.byref(n)), "esc_group_order")

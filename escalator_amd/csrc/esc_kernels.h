@@ -129,15 +129,17 @@ hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, h
 hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* words,
                          const int64_t* first, esc_group_decision* dec, hipStream_t st);
 
-// Ordering (K5): segmented LSD radix sort of (group, class, creation) keys.
-hipError_t launch_sort_count(const NodeDev& n, const GroupDev& g, int nblk, uint32_t* hist, hipStream_t st);
-hipError_t launch_scan_small(uint32_t* a, int n, uint32_t* total, hipStream_t st);
-hipError_t launch_sort_expand2(const NodeDev& n, const GroupDev& g, int nblk, const uint32_t* base,
-                               int64_t ts_min, uint64_t ts_div, int R, uint64_t* keys, uint32_t* vals,
-                               hipStream_t st);
-hipError_t launch_radix_pass(const uint64_t* kin, const uint32_t* vin, uint64_t* kout, uint32_t* vout,
-                             int64_t n, int shift, int nblk, uint32_t* hist, hipStream_t st);
-hipError_t launch_group_bounds(const uint64_t* keys, int64_t n, int key_shift, int32_t nseg, int64_t* seg,
-                               hipStream_t st);
+// Ordering (K5), see esc_kernels.hip: the age index (once per snapshot) and the per-decision
+// (group, class) partition.
+size_t sort_hist_words(int64_t n);   // digit-histogram words one LSD pass over n keys needs
+hipError_t launch_age_index(const NodeDev& n, int64_t ts_min, uint64_t div, int R, uint64_t* keys64[2],
+                            uint32_t* vals[2], uint32_t* hist, uint32_t* tot, uint32_t** age_out, hipStream_t st);
+hipError_t launch_memb_count(const NodeDev& n, const GroupDev& g, const uint32_t* age, int nblk, uint32_t* cnt,
+                             uint32_t* total, hipStream_t st);
+hipError_t launch_memb_expand(const NodeDev& n, const GroupDev& g, const uint32_t* age, int nblk, const uint32_t* base,
+                              uint32_t* e_node, uint32_t* e_grp, uint32_t* e_flags, hipStream_t st);
+hipError_t launch_order(const NodeDev& n, const uint32_t* e_node, const uint32_t* e_grp, const uint32_t* e_flags,
+                        int64_t n_e, int seg_bits, uint32_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t* tot,
+                        int32_t nseg, int64_t* seg, int* src, hipStream_t st);
 
 }  // namespace esc

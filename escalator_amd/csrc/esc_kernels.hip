@@ -16,8 +16,10 @@
 //                      runs K4.
 //  K4 k_decide       : calcPercentUsage / switch / calcScaleUpDelta / scaleDownTaint clamp
 //                      (util.go:13-81, controller.go:233-351, scale_down.go:138-158).
-//  K5 sort kernels   : segmented LSD radix sort for taintOldestN / untaintNewestN
-//                      (scale_down.go:171, scale_up.go:118, sort.go:18,33).
+//  K5 ordering       : taintOldestN / untaintNewestN (scale_down.go:171, scale_up.go:118,
+//                      sort.go:18,33): an age index (LSD radix sort of creation times,
+//                      once per snapshot) + a per-decision stable partition by
+//                      (group, class).
 // Wide variants      : exact any-range pod fallback with global atomics.
 #include <hip/hip_runtime.h>
 
@@ -931,28 +933,163 @@ __global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int
     finalize(G, N, g, words + (int64_t)g * TW_K, firsts[g], dec);
 }
 
-// ===================================================================== K5 sort
-// Key: [group | class(2) | creation offset (R bits)], value: node index.  Class 1
-// (tainted) stores the complemented offset so ascending order is newest-first.
+// ===================================================================== K5 ordering
+// taintOldestN / untaintNewestN (scale_down.go:171, scale_up.go:118) order a group's
+// untainted (tainted) nodes by CreationTimestamp (sort.go:6-39).  Creation times and
+// label memberships are immutable, so the snapshot carries an AGE INDEX built once per
+// load (esc_load_nodes): this rank's nodes sorted by creation time (a full LSD radix sort
+// of the creation offsets, ties by snapshot index), and their group memberships listed in
+// that order with a copy of the node flags (like K2's pair-major entries).  Per decision
+// only the class can change (taint / cordon / dry-mode tracker), so ordering = classify
+// every membership and stable-partition by (group, class): LSD radix passes over the
+// segment id alone.  A segment then lists its nodes oldest first; newest first is the
+// segment read backwards (esc_group_order restores index order inside equal timestamps).
 namespace {
 constexpr int SORT_BLOCK = 1024;
 constexpr int SORT_WAVES = SORT_BLOCK / 64;
 }
 
-// Membership count per node chunk (pass 1 of the deterministic expansion).
-__global__ __launch_bounds__(SORT_BLOCK) void k_sort_count(NodeDev N, GroupDev G, uint32_t* __restrict__ hist) {
+// Creation offsets of nodes [lo, lo + n) (divided by div when exact) and their indices.
+__global__ __launch_bounds__(256) void k_age_keys(NodeDev N, int64_t lo, int64_t n, int64_t ts_min, uint64_t div,
+                                                  uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t off = (uint64_t)(N.created[lo + i] - ts_min);
+    keys[i] = div > 1 ? off / div : off;
+    vals[i] = (uint32_t)(lo + i);
+}
+
+// ---- LSD radix sort building blocks (stable), BITS-bit digits, KT = uint64_t or uint32_t.
+// hist is digit-major: hist[d * nblk + b] = keys of block b with digit d.
+template <class KT, int BITS>
+__global__ __launch_bounds__(SORT_BLOCK) void k_rs_hist(const KT* __restrict__ keys, int64_t n, int shift,
+                                                        uint32_t* __restrict__ hist) {
+    constexpr int NB = 1 << BITS;
+    __shared__ uint32_t h[NB];
+    for (int i = threadIdx.x; i < NB; i += SORT_BLOCK) h[i] = 0;
+    __syncthreads();
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
+    for (int64_t i = lo + threadIdx.x; i < hi; i += SORT_BLOCK) atomicAdd(&h[(uint32_t)(keys[i] >> shift) & (NB - 1)], 1u);
+    __syncthreads();
+    for (int d = threadIdx.x; d < NB; d += SORT_BLOCK) hist[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
+}
+
+// Exclusive scan of each digit's row hist[d][0..nblk) in place (one wave per digit) and the
+// digit totals into tot[d].
+__global__ __launch_bounds__(256) void k_rs_scan_rows(uint32_t* __restrict__ hist, int nblk, int nb,
+                                                      uint32_t* __restrict__ tot) {
+    const int d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (d >= nb) return;
+    uint32_t* row = hist + (int64_t)d * nblk;
+    uint32_t carry = 0;
+    for (int b0 = 0; b0 < nblk; b0 += 64) {
+        const int b = b0 + lane;
+        const uint32_t v = b < nblk ? row[b] : 0;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (b < nblk) row[b] = carry + x - v;
+        carry += __shfl(x, 63, 64);
+    }
+    if (lane == 0) tot[d] = carry;
+}
+
+// Exclusive scan of the digit totals in place (one workgroup, nb <= 4096).
+__global__ __launch_bounds__(SORT_BLOCK) void k_rs_scan_tot(uint32_t* __restrict__ tot, int nb) {
+    __shared__ uint32_t wsum[SORT_WAVES];
+    __shared__ uint32_t carry;
+    if (threadIdx.x == 0) carry = 0;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int b0 = 0; b0 < nb; b0 += SORT_BLOCK) {
+        __syncthreads();
+        const int i = b0 + threadIdx.x;
+        const uint32_t v = i < nb ? tot[i] : 0;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
+        uint32_t pre = carry;
+        for (int k = 0; k < wid; ++k) pre += wsum[k];
+        if (i < nb) tot[i] = pre + x - v;
+        __syncthreads();
+        if (threadIdx.x == 0) for (int k = 0; k < SORT_WAVES; ++k) carry += wsum[k];
+    }
+}
+
+// Stable scatter of one pass: rank = digit base + block offset + rank inside the block in
+// input order (ballot match per wave, per-wave digit counts in LDS).
+template <class KT, int BITS>
+__global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                           KT* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                           int64_t n, int shift, const uint32_t* __restrict__ hist,
+                                                           const uint32_t* __restrict__ tot) {
+    constexpr int NB = 1 << BITS;
+    __shared__ uint32_t run[NB];
+    __shared__ uint32_t wh[SORT_WAVES][NB];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int d = threadIdx.x; d < NB; d += SORT_BLOCK) run[d] = tot[d] + hist[(int64_t)d * gridDim.x + blockIdx.x];
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int64_t b = lo; b < hi; b += SORT_BLOCK) {
+        for (int k = threadIdx.x; k < SORT_WAVES * NB; k += SORT_BLOCK) (&wh[0][0])[k] = 0;
+        __syncthreads();
+        const int64_t i = b + threadIdx.x;
+        const bool ok = i < hi;
+        const KT key = ok ? kin[i] : (KT)0;
+        const uint32_t val = ok ? vin[i] : 0;
+        const uint32_t d = (uint32_t)(key >> shift) & (NB - 1);
+        unsigned long long m = __ballot(ok);
+#pragma unroll
+        for (int bit = 0; bit < BITS; ++bit) {
+            const unsigned long long bb = __ballot((d >> bit) & 1);
+            m &= ((d >> bit) & 1) ? bb : ~bb;
+        }
+        const uint32_t r_in_wave = __popcll(m & lt);
+        if (ok && r_in_wave == 0) wh[wid][d] = __popcll(m);
+        __syncthreads();
+        uint32_t pre = 0;
+        for (int k = 0; k < wid; ++k) pre += wh[k][d];
+        if (ok) {
+            const uint32_t dst = run[d] + pre + r_in_wave;
+            kout[dst] = key;
+            vout[dst] = val;
+        }
+        __syncthreads();
+        for (int dd = threadIdx.x; dd < NB; dd += SORT_BLOCK) {
+            uint32_t t = 0;
+            for (int k = 0; k < SORT_WAVES; ++k) t += wh[k][dd];
+            run[dd] += t;
+        }
+        __syncthreads();
+    }
+}
+
+// ---- age-ordered memberships (load time)
+// Memberships of the nodes age[r], r in this block's share of [0, n).
+__global__ __launch_bounds__(SORT_BLOCK) void k_memb_count(NodeDev N, GroupDev G, const uint32_t* __restrict__ age,
+                                                           int64_t n, uint32_t* __restrict__ cnt) {
     __shared__ uint32_t tot;
     if (threadIdx.x == 0) tot = 0;
     __syncthreads();
-    const int64_t n = N.hi - N.lo;
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t lo = N.lo + (int64_t)blockIdx.x * per, hi = imin64(N.hi, lo + per);
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
     uint32_t c = 0;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += SORT_BLOCK)
+    for (int64_t r = lo + threadIdx.x; r < hi; r += SORT_BLOCK) {
+        const int64_t i = age[r];
         node_groups(N, G, N.flags[i], i, [&](uint32_t) { ++c; });
+    }
     atomicAdd(&tot, c);
     __syncthreads();
-    if (threadIdx.x == 0) hist[blockIdx.x] = tot;
+    if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
 }
 
 // Exclusive scan of n u32 in place by one workgroup; total to *total.
@@ -981,40 +1118,35 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_scan_small(uint32_t* __restrict_
     if (threadIdx.x == 0 && total) *total = carry;
 }
 
-// Pass 2: write memberships in node order (stable => ties resolve by node index).
-__global__ __launch_bounds__(SORT_BLOCK) void k_sort_expand(NodeDev N, GroupDev G, const uint32_t* __restrict__ base,
-                                                            int64_t ts_min, uint64_t ts_div,
-                                                            int R, uint64_t* __restrict__ keys,
-                                                            uint32_t* __restrict__ vals) {
+// Writes the memberships in age order (stable: a block's nodes in rank order, a node's
+// groups in label order): entry node, group code (group | dry bit), node flags.
+__global__ __launch_bounds__(SORT_BLOCK) void k_memb_expand(NodeDev N, GroupDev G, const uint32_t* __restrict__ age,
+                                                            int64_t n, const uint32_t* __restrict__ base,
+                                                            uint32_t* __restrict__ e_node, uint32_t* __restrict__ e_grp,
+                                                            uint32_t* __restrict__ e_flags) {
     __shared__ uint32_t wsum[SORT_WAVES];
     __shared__ uint32_t carry;
     if (threadIdx.x == 0) carry = base[blockIdx.x];
     __syncthreads();
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t n = N.hi - N.lo;
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t lo = N.lo + (int64_t)blockIdx.x * per, hi = imin64(N.hi, lo + per);
-    const uint64_t rmask = R >= 64 ? ~0ull : ((1ull << R) - 1);
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
     for (int64_t b = lo; b < hi; b += SORT_BLOCK) {
-        const int64_t i = b + threadIdx.x;
-        uint32_t c = 0;
-        uint32_t f = 0;
-        if (i < hi) { f = N.flags[i]; node_groups(N, G, f, i, [&](uint32_t) { ++c; }); }
-        uint32_t s = c;
-        for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(s, d, 64); if (lane >= d) s += y; }
-        if (lane == 63) wsum[wid] = s;
+        const int64_t r = b + threadIdx.x;
+        uint32_t c = 0, f = 0;
+        int64_t i = 0;
+        if (r < hi) { i = age[r]; f = N.flags[i]; node_groups(N, G, f, i, [&](uint32_t) { ++c; }); }
+        uint32_t x = c;
+        for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
+        if (lane == 63) wsum[wid] = x;
         __syncthreads();
-        uint32_t pos = carry + s - c;
+        uint32_t pos = carry + x - c;
         for (int k = 0; k < wid; ++k) pos += wsum[k];
-        if (i < hi && c) {
-            uint64_t off = (uint64_t)(N.created[i] - ts_min);
-            off = ts_div > 1 ? off / ts_div : off;
+        if (r < hi && c) {
             node_groups(N, G, f, i, [&](uint32_t mb) {
-                const uint32_t g = mg(mb);
-                const int cls = node_class(N, f, i, mb);
-                const uint64_t ts = cls == 1 ? (~off & rmask) : off;
-                keys[pos] = ((uint64_t)g << (R + 2)) | ((uint64_t)cls << R) | ts;
-                vals[pos] = (uint32_t)i;
+                e_node[pos] = (uint32_t)i;
+                e_grp[pos] = mb;
+                e_flags[pos] = f;
                 ++pos;
             });
         }
@@ -1024,74 +1156,30 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_sort_expand(NodeDev N, GroupDev 
     }
 }
 
-// One LSD pass, 8-bit digit at `shift`: per-block digit histogram.
-__global__ __launch_bounds__(SORT_BLOCK) void k_radix_hist(const uint64_t* __restrict__ keys, int64_t n, int shift,
-                                                           uint32_t* __restrict__ hist) {
-    __shared__ uint32_t h[256];
-    for (int i = threadIdx.x; i < 256; i += SORT_BLOCK) h[i] = 0;
-    __syncthreads();
-    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
-    for (int64_t i = lo + threadIdx.x; i < hi; i += SORT_BLOCK) atomicAdd(&h[(keys[i] >> shift) & 255], 1u);
-    __syncthreads();
-    for (int d = threadIdx.x; d < 256; d += SORT_BLOCK) hist[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
+// ---- per decision
+// filterNodes class of every membership (controller.go:125-150; dry groups: tracker only)
+// -> segment key (group << 2 | class), value node, in age order.
+__global__ __launch_bounds__(256) void k_memb_classify(NodeDev N, const uint32_t* __restrict__ e_node,
+                                                       const uint32_t* __restrict__ e_grp,
+                                                       const uint32_t* __restrict__ e_flags, int64_t n,
+                                                       uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t i = e_node[e], m = e_grp[e];
+    const int cls = node_class(N, e_flags[e], (int64_t)i, m);
+    keys[e] = (mg(m) << 2) | (uint32_t)cls;
+    vals[e] = i;
 }
 
-// Stable scatter: rank = digit offset of the block + rank inside the block in input order.
-__global__ __launch_bounds__(SORT_BLOCK) void k_radix_scatter(const uint64_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                              uint64_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                              int64_t n, int shift, const uint32_t* __restrict__ hist) {
-    __shared__ uint32_t run[256];
-    __shared__ uint32_t wh[SORT_WAVES][256];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int d = threadIdx.x; d < 256; d += SORT_BLOCK) run[d] = hist[(int64_t)d * gridDim.x + blockIdx.x];
-    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
-    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int64_t b = lo; b < hi; b += SORT_BLOCK) {
-        for (int k = threadIdx.x; k < SORT_WAVES * 256; k += SORT_BLOCK) (&wh[0][0])[k] = 0;
-        __syncthreads();
-        const int64_t i = b + threadIdx.x;
-        const bool ok = i < hi;
-        uint64_t key = ok ? kin[i] : 0;
-        uint32_t val = ok ? vin[i] : 0;
-        const uint32_t d = (uint32_t)(key >> shift) & 255;
-        unsigned long long m = __ballot(ok);
-#pragma unroll
-        for (int bit = 0; bit < 8; ++bit) {
-            const unsigned long long bb = __ballot((d >> bit) & 1);
-            m &= ((d >> bit) & 1) ? bb : ~bb;
-        }
-        const uint32_t r_in_wave = __popcll(m & lt);
-        if (ok && r_in_wave == 0) wh[wid][d] = __popcll(m);
-        __syncthreads();
-        uint32_t pre = 0;
-        for (int k = 0; k < wid; ++k) pre += wh[k][d];
-        if (ok) {
-            const uint32_t dst = run[d] + pre + r_in_wave;
-            kout[dst] = key;
-            vout[dst] = val;
-        }
-        __syncthreads();
-        for (int dd = threadIdx.x; dd < 256; dd += SORT_BLOCK) {
-            uint32_t t = 0;
-            for (int k = 0; k < SORT_WAVES; ++k) t += wh[k][dd];
-            run[dd] += t;
-        }
-        __syncthreads();
-    }
-}
-
-// Lower bound of each (group, class) prefix in the sorted keys: seg[g*3+cls].
-__global__ __launch_bounds__(256) void k_group_bounds(const uint64_t* __restrict__ keys, int64_t n, int key_shift,
-                                                      int32_t nseg, int64_t* __restrict__ seg) {
+// Start of each (group, class) segment in the partitioned keys: seg[s] = first key >= s.
+__global__ __launch_bounds__(256) void k_seg_bounds(const uint32_t* __restrict__ keys, int64_t n, int32_t nseg,
+                                                    int64_t* __restrict__ seg) {
     const int32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s > nseg) return;
-    const uint64_t target = (uint64_t)s;
     int64_t lo = 0, hi = n;
     while (lo < hi) {
         const int64_t mid = (lo + hi) >> 1;
-        if ((keys[mid] >> key_shift) < target) lo = mid + 1; else hi = mid;
+        if (keys[mid] < (uint32_t)s) lo = mid + 1; else hi = mid;
     }
     seg[s] = lo;
 }
@@ -1152,39 +1240,79 @@ hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* wor
     return hipGetLastError();
 }
 
-hipError_t launch_sort_count(const NodeDev& n, const GroupDev& g, int nblk, uint32_t* hist, hipStream_t st) {
-    hipLaunchKernelGGL(k_sort_count, dim3(nblk), dim3(SORT_BLOCK), 0, st, n, g, hist);
+namespace {
+int rs_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, (n + 8191) / 8192)); }
+
+template <class KT, int BITS>
+hipError_t rs_pass(const KT* kin, const uint32_t* vin, KT* kout, uint32_t* vout, int64_t n, int shift, uint32_t* hist,
+                   uint32_t* tot, hipStream_t st) {
+    const int nblk = rs_blocks(n), nb = 1 << BITS;
+    hipLaunchKernelGGL((k_rs_hist<KT, BITS>), dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, n, shift, hist);
+    hipLaunchKernelGGL(k_rs_scan_rows, dim3((nb + 3) / 4), dim3(256), 0, st, hist, nblk, nb, tot);
+    hipLaunchKernelGGL(k_rs_scan_tot, dim3(1), dim3(SORT_BLOCK), 0, st, tot, nb);
+    hipLaunchKernelGGL((k_rs_scatter<KT, BITS>), dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, vin, kout, vout, n, shift,
+                       hist, tot);
     return hipGetLastError();
 }
 
-hipError_t launch_scan_small(uint32_t* a, int n, uint32_t* total, hipStream_t st) {
-    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SORT_BLOCK), 0, st, a, n, total);
+// LSD passes over bits [0, bits) of keys[0] / vals[0] (ping-pong with [1]); returns the
+// buffer index holding the result.  8-bit digits, the last pass narrower when it can be.
+template <class KT>
+hipError_t rs_sort(KT* keys[2], uint32_t* vals[2], int64_t n, int bits, uint32_t* hist, uint32_t* tot, int* src,
+                   hipStream_t st) {
+    *src = 0;
+    for (int shift = 0; shift < bits; shift += 8) {
+        const int w = std::min(8, bits - shift);
+        hipError_t e = w <= 4 ? rs_pass<KT, 4>(keys[*src], vals[*src], keys[*src ^ 1], vals[*src ^ 1], n, shift, hist, tot, st)
+                              : rs_pass<KT, 8>(keys[*src], vals[*src], keys[*src ^ 1], vals[*src ^ 1], n, shift, hist, tot, st);
+        if (e != hipSuccess) return e;
+        *src ^= 1;
+    }
+    return hipSuccess;
+}
+}  // namespace
+
+size_t sort_hist_words(int64_t n) { return (size_t)256 * rs_blocks(n); }
+
+hipError_t launch_age_index(const NodeDev& nd, int64_t ts_min, uint64_t div, int R, uint64_t* keys64[2],
+                            uint32_t* vals[2], uint32_t* hist, uint32_t* tot, uint32_t** age_out, hipStream_t st) {
+    const int64_t n = nd.hi - nd.lo;
+    *age_out = vals[0];
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_age_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nd, nd.lo, n, ts_min, div,
+                       keys64[0], vals[0]);
+    int src = 0;
+    hipError_t e = rs_sort<uint64_t>(keys64, vals, n, R, hist, tot, &src, st);
+    *age_out = vals[src];
+    return e;
+}
+
+hipError_t launch_memb_count(const NodeDev& nd, const GroupDev& g, const uint32_t* age, int nblk, uint32_t* cnt,
+                             uint32_t* total, hipStream_t st) {
+    const int64_t n = nd.hi - nd.lo;
+    hipLaunchKernelGGL(k_memb_count, dim3(nblk), dim3(SORT_BLOCK), 0, st, nd, g, age, n, cnt);
+    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SORT_BLOCK), 0, st, cnt, nblk, total);
     return hipGetLastError();
 }
 
-hipError_t launch_sort_expand2(const NodeDev& n, const GroupDev& g, int nblk, const uint32_t* base,
-                               int64_t ts_min, uint64_t ts_div, int R, uint64_t* keys, uint32_t* vals,
-                               hipStream_t st) {
-    hipLaunchKernelGGL(k_sort_expand, dim3(nblk), dim3(SORT_BLOCK), 0, st, n, g, base, ts_min, ts_div, R,
-                       keys, vals);
+hipError_t launch_memb_expand(const NodeDev& nd, const GroupDev& g, const uint32_t* age, int nblk, const uint32_t* base,
+                              uint32_t* e_node, uint32_t* e_grp, uint32_t* e_flags, hipStream_t st) {
+    const int64_t n = nd.hi - nd.lo;
+    hipLaunchKernelGGL(k_memb_expand, dim3(nblk), dim3(SORT_BLOCK), 0, st, nd, g, age, n, base, e_node, e_grp, e_flags);
     return hipGetLastError();
 }
 
-hipError_t launch_radix_pass(const uint64_t* kin, const uint32_t* vin, uint64_t* kout, uint32_t* vout,
-                             int64_t n, int shift, int nblk, uint32_t* hist, hipStream_t st) {
-    hipLaunchKernelGGL(k_radix_hist, dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, n, shift, hist);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SORT_BLOCK), 0, st, hist, nblk * 256, (uint32_t*)nullptr);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_radix_scatter, dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, vin, kout, vout, n, shift, hist);
-    return hipGetLastError();
-}
-
-hipError_t launch_group_bounds(const uint64_t* keys, int64_t n, int key_shift, int32_t nseg, int64_t* seg,
-                               hipStream_t st) {
-    hipLaunchKernelGGL(k_group_bounds, dim3((nseg + 1 + 255) / 256), dim3(256), 0, st, keys, n, key_shift, nseg, seg);
+hipError_t launch_order(const NodeDev& nd, const uint32_t* e_node, const uint32_t* e_grp, const uint32_t* e_flags,
+                        int64_t n_e, int seg_bits, uint32_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t* tot,
+                        int32_t nseg, int64_t* seg, int* src, hipStream_t st) {
+    *src = 0;
+    if (n_e > 0) {
+        hipLaunchKernelGGL(k_memb_classify, dim3((unsigned)((n_e + 255) / 256)), dim3(256), 0, st, nd, e_node, e_grp,
+                           e_flags, n_e, keys[0], vals[0]);
+        hipError_t e = rs_sort<uint32_t>(keys, vals, n_e, seg_bits, hist, tot, src, st);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_seg_bounds, dim3((nseg + 1 + 255) / 256), dim3(256), 0, st, keys[*src], n_e, nseg, seg);
     return hipGetLastError();
 }
 

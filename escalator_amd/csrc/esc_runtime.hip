@@ -140,16 +140,21 @@ struct esc_ctx {
     double stage_ms[MAX_STAGES] = {};
     int n_stage_ev = 0;
     bool pending = false;
-    // sort
-    uint64_t* d_keys[2] = {nullptr, nullptr};
-    uint32_t* d_vals[2] = {nullptr, nullptr};
-    uint32_t* d_hist = nullptr;
-    uint32_t* d_total = nullptr;
+    // K5 ordering: the age index (built at load) and the per-decision partition
+    uint64_t* d_age_keys[2] = {nullptr, nullptr};            // creation offsets (index build)
+    uint32_t* d_age_vals[2] = {nullptr, nullptr};
+    uint32_t* d_age = nullptr;                                // nodes by creation time
+    uint32_t *d_e_node = nullptr, *d_e_grp = nullptr, *d_e_flags = nullptr;   // memberships, age order
+    uint32_t* d_okeys[2] = {nullptr, nullptr};               // (group << 2 | class), partitioned
+    uint32_t* d_ovals[2] = {nullptr, nullptr};
+    uint32_t *d_hist = nullptr, *d_tot = nullptr, *d_cnt = nullptr, *d_total = nullptr;
     int64_t* d_seg = nullptr;
-    int64_t sort_cap = 0, sort_n = 0;
-    int sort_src = 0;
-    int sort_R = 0;
+    int64_t n_memb = 0;
+    int order_src = 0, memb_blocks = 0;
+    uint64_t sort_div = 1;
+    int sort_R = 1;
     bool sorted = false;
+    std::vector<int64_t> h_created;                           // [lo, hi) creation times (tie order)
     // per-function drop-ins run on a one-group list context
     esc_ctx* list_ctx = nullptr;
 };
@@ -231,10 +236,62 @@ void release_work(esc_ctx* c) {
 }
 
 void release_sort(esc_ctx* c) {
-    for (int i = 0; i < 2; ++i) { dfree(c->d_keys[i]); dfree(c->d_vals[i]); }
-    dfree(c->d_hist); dfree(c->d_total); dfree(c->d_seg);
-    c->sort_cap = 0;
+    for (int i = 0; i < 2; ++i) {
+        dfree(c->d_age_keys[i]); dfree(c->d_age_vals[i]); dfree(c->d_okeys[i]); dfree(c->d_ovals[i]);
+    }
+    dfree(c->d_e_node); dfree(c->d_e_grp); dfree(c->d_e_flags);
+    dfree(c->d_hist); dfree(c->d_tot); dfree(c->d_cnt); dfree(c->d_total); dfree(c->d_seg);
+    c->d_age = nullptr;
+    c->n_memb = 0;
     c->sorted = false;
+}
+
+// The age index: this rank's node range sorted by creation time (LSD
+// radix sort of the creation offsets, divided by the largest of 1e9 / 1e6 / 1e3 that
+// divides them all — an exact order-preserving transform), and the group memberships of
+// the nodes listed in that order with their flags.  Built once per snapshot.
+int32_t build_age_index(esc_ctx* c) {
+    const GroupDev g = group_dev(c);
+    const NodeDev n = node_dev(c);
+    hipStream_t st = c->stream;
+    const int64_t nl = c->node_hi - c->node_lo;
+    const bool fresh = c->d_age_keys[0] == nullptr;
+    if (fresh) {
+        uint64_t div = 1;
+        for (uint64_t d : {1000000000ull, 1000000ull, 1000ull}) {
+            bool ok = true;
+            for (int64_t i = 0; i < nl && ok; ++i) ok = ((uint64_t)(c->h_created[i] - c->ts_min)) % d == 0;
+            if (ok) { div = d; break; }
+        }
+        c->sort_div = div;
+        c->sort_R = std::max(1, bit_width((uint64_t)(c->ts_max - c->ts_min) / div));
+        const size_t hw = std::max(sort_hist_words(nl), sort_hist_words(1) * 4);
+        for (int i = 0; i < 2; ++i) { HIP_TRY(dalloc(&c->d_age_keys[i], nl)); HIP_TRY(dalloc(&c->d_age_vals[i], nl)); }
+        HIP_TRY(dalloc(&c->d_hist, hw * 4));   // room for the membership passes too (n_memb <= 4 * n)
+        HIP_TRY(dalloc(&c->d_tot, 256));
+        HIP_TRY(dalloc(&c->d_total, 1));
+        HIP_TRY(dalloc(&c->d_seg, (size_t)4 * g.G + 1));
+        c->memb_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2 * c->cu_count, (nl + 4095) / 4096));
+        HIP_TRY(dalloc(&c->d_cnt, c->memb_blocks));
+    }
+    HIP_TRY(launch_age_index(n, c->ts_min, c->sort_div, c->sort_R, c->d_age_keys, c->d_age_vals, c->d_hist, c->d_tot,
+                             &c->d_age, st));
+    HIP_TRY(launch_memb_count(n, g, c->d_age, c->memb_blocks, c->d_cnt, c->d_total, st));
+    if (fresh) {
+        uint32_t total = 0;
+        HIP_TRY(hipMemcpyAsync(&total, c->d_total, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        c->n_memb = total;
+        HIP_TRY(dalloc(&c->d_e_node, total)); HIP_TRY(dalloc(&c->d_e_grp, total)); HIP_TRY(dalloc(&c->d_e_flags, total));
+        for (int i = 0; i < 2; ++i) { HIP_TRY(dalloc(&c->d_okeys[i], total)); HIP_TRY(dalloc(&c->d_ovals[i], total)); }
+        if (sort_hist_words(total) > std::max(sort_hist_words(nl), sort_hist_words(1) * 4)) {
+            dfree(c->d_hist);
+            HIP_TRY(dalloc(&c->d_hist, sort_hist_words(total)));
+        }
+    }
+    HIP_TRY(launch_memb_expand(n, g, c->d_age, c->memb_blocks, c->d_cnt, c->d_e_node, c->d_e_grp, c->d_e_flags, st));
+    c->sorted = false;
+    return ESC_OK;
 }
 
 // Pod accumulator slots: one per group pair + one for the default filter.
@@ -803,8 +860,9 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     c->node_hi = hi;
     c->ts_min = tmin;
     c->ts_max = tmax;
+    c->h_created.assign(s->created_ns + lo, s->created_ns + hi);
     c->nodes_loaded = true;
-    return ESC_OK;
+    return build_age_index(c);
 }
 
 int32_t esc_stream_bytes(const esc_ctx* c, int64_t* pod_bytes, int64_t* node_bytes) {
@@ -1018,55 +1076,27 @@ int32_t esc_sort_nodes(esc_ctx* c) {
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->nodes_loaded) return ESC_E_STATE;
     hipSetDevice(c->device);
-    const GroupDev g = group_dev(c);
-    const NodeDev n = node_dev(c);
-    hipStream_t st = c->stream;
-    const int64_t n_local = c->node_hi - c->node_lo;
-    // creation offsets: divide by the largest of 1e9/1e6/1e3 that divides them all
-    // (metav1.Time is whole seconds on the wire), an exact order-preserving transform
-    uint64_t div = 1;
-    if (n_local > 0) {
-        std::vector<int64_t> ts(n_local);
-        HIP_TRY(hipMemcpy(ts.data(), c->nodes.created + c->node_lo, n_local * 8, hipMemcpyDeviceToHost));
-        for (uint64_t d : {1000000000ull, 1000000ull, 1000ull}) {
-            bool ok = true;
-            for (int64_t i = 0; i < n_local && ok; ++i) ok = ((uint64_t)(ts[i] - c->ts_min)) % d == 0;
-            if (ok) { div = d; break; }
-        }
-    }
-    const int R = std::max(1, bit_width((uint64_t)(c->ts_max - c->ts_min) / div));
-    const int gbits = std::max(1, bit_width((uint64_t)(g.G - 1)));
-    if (R + 2 + gbits > 64) return ESC_E_LIMIT;
-    const int total_bits = R + 2 + gbits;
-    const int nblk = (int)std::max<int64_t>(1, std::min<int64_t>(2 * c->cu_count, (n_local + 4095) / 4096));
-    if (!c->d_hist) {
-        HIP_TRY(dalloc(&c->d_hist, (size_t)512 * 256 + 1));
-        HIP_TRY(dalloc(&c->d_total, 1));
-        HIP_TRY(dalloc(&c->d_seg, (size_t)4 * g.G + 1));
-    }
-    HIP_TRY(launch_sort_count(n, g, nblk, c->d_hist, st));
-    HIP_TRY(launch_scan_small(c->d_hist, nblk, c->d_total, st));
-    uint32_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, c->d_total, 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if ((int64_t)total > c->sort_cap) {
-        for (int i = 0; i < 2; ++i) { dfree(c->d_keys[i]); dfree(c->d_vals[i]); }
-        for (int i = 0; i < 2; ++i) { HIP_TRY(dalloc(&c->d_keys[i], total)); HIP_TRY(dalloc(&c->d_vals[i], total)); }
-        c->sort_cap = total;
-    }
-    HIP_TRY(launch_sort_expand2(n, g, nblk, c->d_hist, c->ts_min, div, R, c->d_keys[0], c->d_vals[0], st));
-    const int sblk = (int)std::max<int64_t>(1, std::min<int64_t>(512, ((int64_t)total + 8191) / 8192));
-    int src = 0;
-    for (int shift = 0; shift < total_bits; shift += 8) {
-        HIP_TRY(launch_radix_pass(c->d_keys[src], c->d_vals[src], c->d_keys[src ^ 1], c->d_vals[src ^ 1], total, shift,
-                                  sblk, c->d_hist, st));
-        src ^= 1;
-    }
-    HIP_TRY(launch_group_bounds(c->d_keys[src], total, R, 4 * g.G, c->d_seg, st));
-    c->sort_n = total;
-    c->sort_src = src;
-    c->sort_R = R;
+    const int G = c->gi.G;
+    const int seg_bits = std::max(1, bit_width((uint64_t)(4 * G - 1)));
+    HIP_TRY(launch_order(node_dev(c), c->d_e_node, c->d_e_grp, c->d_e_flags, c->n_memb, seg_bits, c->d_okeys,
+                         c->d_ovals, c->d_hist, c->d_tot, 4 * G, c->d_seg, &c->order_src, c->stream));
     c->sorted = true;
+    return ESC_OK;
+}
+
+int32_t esc_build_age_index(esc_ctx* c) {
+    if (!c) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->nodes_loaded) return ESC_E_STATE;
+    hipSetDevice(c->device);
+    return build_age_index(c);
+}
+
+int32_t esc_order_info(const esc_ctx* c, int64_t* n_memberships, int32_t* key_bits) {
+    if (!c || !n_memberships || !key_bits) return ESC_E_INVAL;
+    if (!c->nodes_loaded) return ESC_E_STATE;
+    *n_memberships = c->n_memb;
+    *key_bits = c->sort_R;
     return ESC_OK;
 }
 
@@ -1082,11 +1112,35 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
     const int64_t cnt = seg[1] - seg[0];
     if (n_out) *n_out = cnt;
     const int64_t m = std::min(cnt, cap);
-    if (m > 0) {
+    if (m <= 0) return ESC_OK;
+    const uint32_t* vals = c->d_ovals[c->order_src];
+    if (which == 0) {                                  // taintOldestN: the segment in age order
         std::vector<uint32_t> v(m);
-        HIP_TRY(hipMemcpy(v.data(), c->d_vals[c->sort_src] + seg[0], m * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(v.data(), vals + seg[0], m * 4, hipMemcpyDeviceToHost));
         for (int64_t i = 0; i < m; ++i) idx_out[i] = v[i];
+        return ESC_OK;
     }
+    // untaintNewestN: the segment backwards; equal creation times keep ascending snapshot
+    // index (the age index breaks ties that way), so read on until the tie run that
+    // straddles position m ends, then sort each run of equal times by index.
+    const int64_t lo_ts = c->node_lo;
+    auto ts = [&](uint32_t i) { return c->h_created[(int64_t)i - lo_ts]; };
+    int64_t take = std::min(cnt, m + 64);
+    std::vector<uint32_t> v;
+    for (;;) {
+        v.resize(take);
+        HIP_TRY(hipMemcpy(v.data(), vals + seg[1] - take, take * 4, hipMemcpyDeviceToHost));
+        std::reverse(v.begin(), v.end());
+        if (take == cnt || ts(v[take - 1]) != ts(v[m - 1])) break;
+        take = std::min(cnt, take * 2);
+    }
+    for (int64_t a = 0; a < m;) {
+        int64_t b = a + 1;
+        while (b < take && ts(v[b]) == ts(v[a])) ++b;
+        std::sort(v.begin() + a, v.begin() + b);
+        a = b;
+    }
+    for (int64_t i = 0; i < m; ++i) idx_out[i] = v[i];
     return ESC_OK;
 }
 

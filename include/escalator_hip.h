@@ -352,7 +352,17 @@ int32_t esc_stage_times(esc_ctx* ctx, double* ms_out, int32_t n);
  * Writes up to `cap` snapshot node indices; *n_out = number of members in that list.
  * Ties (equal timestamps) are broken by snapshot index (Go's sort.Sort is unstable,
  * so its tie order is not reproducible).                             */
-int32_t esc_sort_nodes(esc_ctx* ctx);          /* async: full segmented sort          */
+/* esc_load_nodes builds the AGE INDEX once per snapshot: the node range sorted by
+ * creation time (LSD radix sort) and the group memberships listed in that order.
+ * esc_sort_nodes (async, per decision) classifies every membership (filterNodes,
+ * controller.go:120-154) and stable-partitions by (group, class); a group's untainted
+ * segment is then oldest-first and its tainted one, read backwards, newest-first.
+ * esc_build_age_index rebuilds the index (snapshot ingestion; exposed for measurement). */
+int32_t esc_sort_nodes(esc_ctx* ctx);
+int32_t esc_build_age_index(esc_ctx* ctx);
+/* Size of the ordering problem: memberships of the node range and the bit width of the
+ * creation-offset keys the index sorts on. */
+int32_t esc_order_info(const esc_ctx* ctx, int64_t* n_memberships, int32_t* key_bits);
 int32_t esc_group_order(esc_ctx* ctx, int32_t group, int32_t which,
                         int64_t* idx_out, int64_t cap, int64_t* n_out);
 
