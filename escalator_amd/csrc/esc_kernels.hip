@@ -964,15 +964,43 @@ __global__ __launch_bounds__(256) void k_age_keys(NodeDev N, int64_t lo, int64_t
 template <class KT, int BITS>
 __global__ __launch_bounds__(SORT_BLOCK) void k_rs_hist(const KT* __restrict__ keys, int64_t n, int shift,
                                                         uint32_t* __restrict__ hist) {
+    // per wave: lanes with equal digits are matched with BITS ballots and the first of
+    // them adds the group's size to the wave's own counters (no atomics, no conflicts)
     constexpr int NB = 1 << BITS;
-    __shared__ uint32_t h[NB];
-    for (int i = threadIdx.x; i < NB; i += SORT_BLOCK) h[i] = 0;
+    __shared__ uint32_t wh[SORT_WAVES][NB];
+    for (int i = threadIdx.x; i < SORT_WAVES * NB; i += SORT_BLOCK) (&wh[0][0])[i] = 0;
     __syncthreads();
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
-    for (int64_t i = lo + threadIdx.x; i < hi; i += SORT_BLOCK) atomicAdd(&h[(uint32_t)(keys[i] >> shift) & (NB - 1)], 1u);
+    constexpr int U = 4;                                 // keys in flight per thread
+    for (int64_t b = lo; b < hi; b += (int64_t)SORT_BLOCK * U) {
+        KT k[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = b + (int64_t)u * SORT_BLOCK + threadIdx.x;
+            k[u] = i < hi ? keys[i] : (KT)0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool ok = b + (int64_t)u * SORT_BLOCK + threadIdx.x < hi;
+            const uint32_t d = (uint32_t)(k[u] >> shift) & (NB - 1);
+            unsigned long long m = __ballot(ok);
+#pragma unroll
+            for (int bit = 0; bit < BITS; ++bit) {
+                const unsigned long long bb = __ballot((d >> bit) & 1);
+                m &= ((d >> bit) & 1) ? bb : ~bb;
+            }
+            if (ok && (m & lt) == 0) wh[wid][d] += (uint32_t)__popcll(m);
+        }
+    }
     __syncthreads();
-    for (int d = threadIdx.x; d < NB; d += SORT_BLOCK) hist[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
+    for (int d = threadIdx.x; d < NB; d += SORT_BLOCK) {
+        uint32_t t = 0;
+        for (int k = 0; k < SORT_WAVES; ++k) t += wh[k][d];
+        hist[(int64_t)d * gridDim.x + blockIdx.x] = t;
+    }
 }
 
 // Exclusive scan of each digit's row hist[d][0..nblk) in place (one wave per digit) and the
@@ -1039,13 +1067,19 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    // the next chunk's key / value are loaded one iteration ahead
+    KT nkey = lo + (int64_t)threadIdx.x < hi ? kin[lo + threadIdx.x] : (KT)0;
+    uint32_t nval = lo + (int64_t)threadIdx.x < hi ? vin[lo + threadIdx.x] : 0;
     for (int64_t b = lo; b < hi; b += SORT_BLOCK) {
-        for (int k = threadIdx.x; k < SORT_WAVES * NB; k += SORT_BLOCK) (&wh[0][0])[k] = 0;
-        __syncthreads();
         const int64_t i = b + threadIdx.x;
         const bool ok = i < hi;
-        const KT key = ok ? kin[i] : (KT)0;
-        const uint32_t val = ok ? vin[i] : 0;
+        const KT key = nkey;
+        const uint32_t val = nval;
+        const int64_t ni = i + SORT_BLOCK;
+        nkey = ni < hi ? kin[ni] : (KT)0;
+        nval = ni < hi ? vin[ni] : 0;
+        for (int k = threadIdx.x; k < SORT_WAVES * NB; k += SORT_BLOCK) (&wh[0][0])[k] = 0;
+        __syncthreads();
         const uint32_t d = (uint32_t)(key >> shift) & (NB - 1);
         unsigned long long m = __ballot(ok);
 #pragma unroll
@@ -1257,16 +1291,28 @@ hipError_t rs_pass(const KT* kin, const uint32_t* vin, KT* kout, uint32_t* vout,
 
 // LSD passes over bits [0, bits) of keys[0] / vals[0] (ping-pong with [1]); returns the
 // buffer index holding the result.  8-bit digits, the last pass narrower when it can be.
+// The bits are split evenly over ceil(bits / 8) passes (9 bits -> 5 + 4, 34 -> 7 x 5):
+// narrower digits cost the scatter fewer LDS histogram words per element at equal traffic.
 template <class KT>
 hipError_t rs_sort(KT* keys[2], uint32_t* vals[2], int64_t n, int bits, uint32_t* hist, uint32_t* tot, int* src,
                    hipStream_t st) {
     *src = 0;
-    for (int shift = 0; shift < bits; shift += 8) {
-        const int w = std::min(8, bits - shift);
-        hipError_t e = w <= 4 ? rs_pass<KT, 4>(keys[*src], vals[*src], keys[*src ^ 1], vals[*src ^ 1], n, shift, hist, tot, st)
-                              : rs_pass<KT, 8>(keys[*src], vals[*src], keys[*src ^ 1], vals[*src ^ 1], n, shift, hist, tot, st);
+    const int passes = (bits + 7) / 8;
+    for (int p = 0, shift = 0; p < passes; ++p) {
+        const int w = (bits - shift + (passes - p) - 1) / (passes - p);
+        hipError_t e;
+        KT *ki = keys[*src], *ko = keys[*src ^ 1];
+        uint32_t *vi = vals[*src], *vo = vals[*src ^ 1];
+        switch (w) {
+            case 1: case 2: case 3: case 4: e = rs_pass<KT, 4>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+            case 5: e = rs_pass<KT, 5>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+            case 6: e = rs_pass<KT, 6>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+            case 7: e = rs_pass<KT, 7>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+            default: e = rs_pass<KT, 8>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+        }
         if (e != hipSuccess) return e;
         *src ^= 1;
+        shift += w;
     }
     return hipSuccess;
 }
