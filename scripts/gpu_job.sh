@@ -13,11 +13,19 @@ timeout -k 10 420 python -u -m pytest tests/ -m gpu -x -v --timeout 120 --timeou
 echo "[job] $(date) smoke" &&
 timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 &&
 echo "[job] $(date) bench" &&
-timeout -k 10 300 python -u scripts/k1_variants.py > gpurun_out/k1_variants_${TAG}.json 2>&1 && cat gpurun_out/k1_variants_${TAG}.json &&
+VARIANTS=${VARIANTS:-0,2,9,11,12,10} timeout -k 10 300 python -u scripts/k1_variants.py > gpurun_out/k1_variants_${TAG}.json 2>&1 && cat gpurun_out/k1_variants_${TAG}.json &&
 timeout -k 10 400 python -u bench.py --steps ${STEPS} --warmup 5 > gpurun_out/bench_${TAG}.json 2> gpurun_out/bench_${TAG}.err &&
 cat gpurun_out/bench_${TAG}.json &&
+echo "[job] $(date) config 5 orderings" &&
+timeout -k 10 300 python -u bench.py --config 5 --steps 20 --warmup 3 > gpurun_out/bench5_${TAG}.json 2> gpurun_out/bench5_${TAG}.err &&
+cat gpurun_out/bench5_${TAG}.json &&
+echo "[job] $(date) stream probe" &&
+hipcc --offload-arch=gfx950 -O3 -o /tmp/stream_probe scripts/stream_probe.hip &&
+timeout -k 10 120 /tmp/stream_probe > gpurun_out/stream_probe_${TAG}.json && cat gpurun_out/stream_probe_${TAG}.json &&
 echo "[job] $(date) rocprofv3 kernel trace" &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG} -o run \
     -- python3 bench.py --steps ${STEPS} --warmup 5 --no-cpu-baseline --no-parity \
     > gpurun_out/prof_${TAG}.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof5_${TAG} -o run \
+    -- python3 bench.py --config 5 --steps 20 --warmup 3 > gpurun_out/prof5_${TAG}.log 2>&1 &&
 echo "[job] $(date) done"
