@@ -177,11 +177,18 @@ def main():
     import escalator_amd as esc
     from escalator_amd.dist import Exchange, shard_range
 
+    # ESC_BENCH_BACKEND / ESC_BENCH_DEVICE: rehearsal knobs (gloo, every rank on one device)
+    # for exercising the N > 1 path on a one-GPU box; the driver's runs use the defaults.
+    backend = os.environ.get("ESC_BENCH_BACKEND", "nccl")
+    local = int(os.environ.get("ESC_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     lo, hi = shard_range(P, rank, world)
     nlo, nhi = shard_range(N, rank, world)
@@ -265,7 +272,9 @@ def main():
     records = P + N
     value = records * args.steps / elapsed
     decision_bytes = (pod_b + node_b) * world         # shards are near-equal; rank 0's x N
-    traffic = pmc_traffic("k_pod_reduce")
+    # PMC passes are taken on the single-GPU config-4 run (scripts/pmc_job.sh); a shard's
+    # K1 launch moves other bytes, so the committed figure applies to N = 1 only
+    traffic = pmc_traffic("k_pod_reduce") if world == 1 and args.config == 4 else None
     out = {
         "metric": "pod+node records evaluated/sec per scale decision & % HBM peak, 1/2/4/8 GPUs",
         "value": value,
