@@ -164,12 +164,16 @@ def main():
     ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS) + [5])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--pods", type=int, default=None, help="override the config's pod count (experiments)")
     args = ap.parse_args()
 
     if args.config == 5:
         return bench_order(args)
     rank, world, local = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1), ("LOCAL_RANK", 0)))
     cfg = dict(CONFIGS[args.config], cfg=args.config)
+    if args.pods:
+        cfg["P"] = args.pods
+        cfg["name"] += " [pods overridden: %d]" % args.pods
     P, N, G = cfg["P"], cfg["N"], cfg["G"]
 
     import numpy as np

@@ -58,7 +58,17 @@ struct PodDev {
 //    are exactly the entries of its pair, in snapshot order.  K2 reduces the entries per
 //    piece (a run of <= NODE_PIECE entries of one pair); this rank reduces pieces
 //    [pc_lo, pc_hi).  K3 joins each group to its pair's pieces.
+// Per-group node facts that are fixed for a loaded snapshot (esc_load_nodes): this rank's
+// piece range of the group's pair and allNodes[0] (controller.go:207-211) with its
+// allocatable, so K3 needs no dependent index chase.
+struct GroupNode {
+    int64_t first;             // lowest member node index (INT64_MAX: no member)
+    int64_t first_cpu, first_mem;
+    int64_t plo, phi;          // this rank's pieces of the group's pair
+};
+
 struct NodeDev {
+    const GroupNode* gnode;    // [G]
     const uint32_t* flags;
     const uint32_t* label0;
     const int64_t*  cpu;
@@ -102,6 +112,7 @@ struct GroupDev {
     const uint32_t* node_code; // [n_gp] pair id -> group code (K5)
     const uint32_t* code_list; // CODE_MULTI lists: [count, g...]
     const uint32_t* slot_readers; // [n_gp + 1] groups reading each pod slot in K3
+    const uint32_t* gslot;     // [G] the group's pod slot: its pair, or n_gp for the default group
     uint32_t n_gp;             // pod slots: pair ids [0, n_gp) + the default filter's slot n_gp
     int32_t G;
     uint32_t default_group;    // NONE when no group is named "default"
@@ -122,7 +133,9 @@ hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
                                int64_t* wide, hipStream_t st);
 hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows, int64_t* trk_acc, hipStream_t st);
-hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* pod_part, int nblk,
+constexpr int FOLD_SPLIT = 8;   // K3a: row ranges the K1 partials fold into (fold: [split][4][S] u64)
+hipError_t launch_pod_fold(const uint64_t* pod_part, int nblk, int64_t S, uint64_t* fold, hipStream_t st);
+hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* fold, int nsplit,
                           const int64_t* node_rows, int64_t* wide_pod, uint32_t* wp_cnt, int64_t* trk_acc,
                           int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);

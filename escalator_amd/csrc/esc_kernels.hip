@@ -751,9 +751,8 @@ __device__ __forceinline__ __int128 join_parts(uint64_t lo, uint64_t lo_carry, i
     return (__int128)(((unsigned __int128)lo_carry << 64) | lo) + ((__int128)hi << 32);
 }
 
-__device__ __forceinline__ void finalize(const GroupDev& G, const NodeDev& N, int32_t g,
-                                         const int64_t* __restrict__ w, int64_t first,
-                                         esc_group_decision* __restrict__ dec) {
+__device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn, int32_t g,
+                                         const int64_t* __restrict__ w, esc_group_decision& dec) {
     Totals t;
     int64_t flags = 0;
     if (!join_split(w[TW_POD_CPU_LO], w[TW_POD_CPU_HI], t.pod_cpu)) flags |= ESC_TF_POD_OVERFLOW;
@@ -765,11 +764,22 @@ __device__ __forceinline__ void finalize(const GroupDev& G, const NodeDev& N, in
     t.n_taint = w[TW_N_TAINT];
     t.n_cord = w[TW_N_CORD];
     t.n_nodes = t.n_unt + t.n_taint + t.n_cord;
-    t.first = first;
-    t.first_cpu = first != INT64_MAX ? N.cpu[first] : 0;
-    t.first_mem = first != INT64_MAX ? N.mem[first] : 0;
+    t.first = gn.first;
+    t.first_cpu = gn.first_cpu;
+    t.first_mem = gn.first_mem;
     t.flags = flags;
-    decide_one(G.params[g], t, dec[g]);
+    decide_one(G.params[g], t, dec);
+}
+
+// The decisions of 64 consecutive groups (sdec, LDS) stored by 256 threads as 16-B pieces
+// of one contiguous 4 KB run: the destination is pinned host memory (zero-copy), where
+// 8-B fields at a 64-B stride would each be a separate PCIe write.
+__device__ __forceinline__ void store_decisions(esc_group_decision* __restrict__ dec, int32_t g0, int32_t G,
+                                                const esc_group_decision* sdec) {
+    static_assert(sizeof(esc_group_decision) == 64, "decision record is 4 x 16 B");
+    const int ng = G - g0 < 64 ? G - g0 : 64;
+    if ((int)threadIdx.x < ng * 4)
+        reinterpret_cast<uint4*>(dec + g0)[threadIdx.x] = reinterpret_cast<const uint4*>(sdec)[threadIdx.x];
 }
 
 __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
@@ -777,6 +787,31 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 }
 
 }  // namespace
+
+// K3a: the K1 workgroups' packed slot partials summed column-wise — one thread per slot,
+// one of FOLD_SPLIT row ranges per grid row, coalesced 2 KB rows — into (cpu, count,
+// mem lo, mem carry) per split, so that K3 reads FOLD_SPLIT rows per slot instead of one
+// per K1 workgroup (41 MB for config 4).
+__global__ __launch_bounds__(256) void k_pod_fold(const uint64_t* __restrict__ part, int nblk, int64_t S,
+                                                  uint64_t* __restrict__ fold) {
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= S) return;
+    const int y = blockIdx.y;
+    const int b0 = nblk * y / FOLD_SPLIT, b1 = nblk * (y + 1) / FOLD_SPLIT;
+    uint64_t cpu = 0, cnt = 0, lo = 0, carry = 0;
+#pragma unroll 4
+    for (int b = b0; b < b1; ++b) {
+        const uint64_t c = ldnt(part + (int64_t)b * 2 * S + s), m = ldnt(part + ((int64_t)b * 2 + 1) * S + s);
+        cpu += c & CPU_MASK;
+        cnt += c >> CNT_SHIFT;
+        u128_add(lo, carry, m);
+    }
+    uint64_t* f = fold + (int64_t)y * 4 * S + s;
+    f[0] = cpu;
+    f[S] = cnt;
+    f[2 * S] = lo;
+    f[3 * S] = carry;
+}
 
 // One lane per group (64 groups per workgroup); the 16 waves split the group's pod
 // partial rows (K1 workgroups, coalesced reads of consecutive slots) and its pair's node
@@ -792,10 +827,10 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 // The wide pod row of a slot is read by every group of the slot; the last reader of a
 // non-zero row resets it for the next decision (wp_cnt, slot_readers).  A group's tracker
 // row has one reader and is reset by it.
-constexpr int CB_WAVES = 16;
+constexpr int CB_WAVES = 4;
 
 __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N,
-                                                           const uint64_t* __restrict__ pod_part, int nblk,
+                                                           const uint64_t* __restrict__ fold, int nsplit,
                                                            const int64_t* __restrict__ node_rows,
                                                            int64_t* __restrict__ wide_pod,
                                                            uint32_t* __restrict__ wp_cnt,
@@ -815,18 +850,18 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
 #pragma unroll
     for (int k = 0; k < NA; ++k) a[k] = 0;
     const int64_t S = G.n_gp + 1;
-    const int64_t slot = !ok ? 0 : ((uint32_t)g == G.default_group ? (int64_t)G.n_gp : (int64_t)G.gpair[g]);
-    const uint32_t q = ok ? G.gpair[g] : 0;
-    const uint32_t p0 = ok ? N.pp_off[q] : 0, p1 = ok ? N.pp_off[q + 1] : 0;
-    const int64_t plo = imax64((int64_t)p0, N.pc_lo), phi = imin64((int64_t)p1, N.pc_hi);   // this rank's share
+    const int64_t slot = ok ? (int64_t)G.gslot[g] : 0;
+    GroupNode gn;
+    gn.first = INT64_MAX; gn.first_cpu = gn.first_mem = 0; gn.plo = gn.phi = 0;
+    if (ok) gn = N.gnode[g];
+    const int64_t plo = gn.plo, phi = gn.phi;             // this rank's pieces of the pair
     if (ok) {
-#pragma unroll 4
-        for (int b = wid; b < nblk; b += CB_WAVES) {
-            const uint64_t c = pod_part[(int64_t)b * 2 * S + slot];
-            const uint64_t m = pod_part[((int64_t)b * 2 + 1) * S + slot];
-            a[0] += c & CPU_MASK;
-            a[1] += c >> CNT_SHIFT;
-            u128_add(a[2], a[3], m);
+        for (int y = wid; y < nsplit; y += CB_WAVES) {        // K3a's folded partials
+            const uint64_t* f = fold + (int64_t)y * 4 * S + slot;
+            a[0] += f[0];
+            a[1] += f[S];
+            u128_add(a[2], a[3], f[2 * S]);
+            a[3] += f[3 * S];
         }
         const int64_t np = N.n_pieces;
         for (int64_t p = plo + wid; p < phi; p += CB_WAVES) {
@@ -873,7 +908,8 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
             }
         }
     }
-    if (wid != 0 || !ok) return;
+    __shared__ esc_group_decision sdec[64];
+    if (wid == 0 && ok) {
     // wide pod row of the slot (agent-scope loads: written by K1's device-scope atomics)
     int64_t* wp = wide_pod + slot * WP_K;
     int64_t p[WP_K];
@@ -920,17 +956,23 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
     w[TW_N_UNT] = (int64_t)n_unt;
     w[TW_N_TAINT] = (int64_t)n_taint;
     w[TW_N_CORD] = (int64_t)n_cord;
-    const int64_t fst = p1 > p0 ? (int64_t)N.e_node[N.piece_off[p0]] : INT64_MAX;
-    firsts[g] = fst;
-    if (decide) finalize(G, N, g, w, fst, dec);
+    firsts[g] = gn.first;
+    if (decide) finalize(G, gn, g, w, sdec[lane]);
+    }
+    if (decide) {
+        __syncthreads();
+        store_decisions(dec, blockIdx.x * 64, G.G, sdec);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ words,
                                                 const int64_t* __restrict__ firsts,
                                                 esc_group_decision* __restrict__ dec) {
-    const int32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= G.G) return;
-    finalize(G, N, g, words + (int64_t)g * TW_K, firsts[g], dec);
+    __shared__ esc_group_decision sdec[64];
+    const int32_t g = blockIdx.x * 64 + (int32_t)threadIdx.x;
+    if (threadIdx.x < 64 && g < G.G) finalize(G, N.gnode[g], g, words + (int64_t)g * TW_K, sdec[threadIdx.x]);
+    __syncthreads();
+    store_decisions(dec, blockIdx.x * 64, G.G, sdec);
 }
 
 // ===================================================================== K5 ordering
@@ -1255,10 +1297,17 @@ hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows
     return hipGetLastError();
 }
 
-hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* pod_part, int nblk,
+hipError_t launch_pod_fold(const uint64_t* pod_part, int nblk, int64_t S, uint64_t* fold, hipStream_t st) {
+    if (nblk <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pod_fold, dim3((unsigned)((S + 255) / 256), FOLD_SPLIT), dim3(256), 0, st, pod_part, nblk, S,
+                       fold);
+    return hipGetLastError();
+}
+
+hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* fold, int nsplit,
                           const int64_t* node_rows, int64_t* wide_pod, uint32_t* wp_cnt, int64_t* trk_acc,
                           int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st) {
-    hipLaunchKernelGGL(k_combine, dim3((g.G + 63) / 64), dim3(CB_WAVES * 64), 0, st, g, n, pod_part, nblk,
+    hipLaunchKernelGGL(k_combine, dim3((g.G + 63) / 64), dim3(CB_WAVES * 64), 0, st, g, n, fold, nsplit,
                        node_rows, wide_pod, wp_cnt, trk_acc, words, first, decide ? 1 : 0, dec);
     return hipGetLastError();
 }
@@ -1270,7 +1319,7 @@ hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, h
 
 hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* words,
                          const int64_t* first, esc_group_decision* dec, hipStream_t st) {
-    hipLaunchKernelGGL(k_decide, dim3((g.G + 255) / 256), dim3(256), 0, st, g, n, words, first, dec);
+    hipLaunchKernelGGL(k_decide, dim3((g.G + 63) / 64), dim3(256), 0, st, g, n, words, first, dec);
     return hipGetLastError();
 }
 

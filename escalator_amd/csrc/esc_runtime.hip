@@ -72,7 +72,9 @@ struct NodeBuf {
     // pair-major entries, pieces, tracker by group, K2 rows
     uint32_t *e_flags = nullptr, *e_node = nullptr, *piece_off = nullptr, *piece_pair = nullptr, *pp_off = nullptr;
     int64_t *e_cpu = nullptr, *e_mem = nullptr, *rows = nullptr;
+    GroupNode* gnode = nullptr;
     void release() {
+        dfree(gnode);
         dfree(flags); dfree(label0); dfree(xl); dfree(xl_off); dfree(trk_start); dfree(cpu); dfree(mem);
         dfree(created); dfree(trk_node); dfree(trk_group);
         dfree(e_flags); dfree(e_node); dfree(piece_off); dfree(piece_pair); dfree(pp_off);
@@ -100,6 +102,7 @@ struct esc_ctx {
     uint8_t* d_dry = nullptr;
     GroupParams* d_params = nullptr;
     uint32_t *d_gpair = nullptr, *d_node_code = nullptr, *d_code_list = nullptr, *d_slot_readers = nullptr;
+    uint32_t* d_gslot = nullptr;
     // snapshot
     std::vector<PodBuf> pods;
     int n_replicas = 1, cur = 0;
@@ -115,6 +118,7 @@ struct esc_ctx {
     // work
     int nblk = 0;
     uint64_t* d_pod_part = nullptr;
+    uint64_t* d_fold = nullptr;                               // K3a output [FOLD_SPLIT][4][S]
     int64_t* d_wide_pod = nullptr;
     uint32_t* d_wp_cnt = nullptr;
     int64_t* d_trk_acc = nullptr;                             // [G][TA_K] dry-mode tracked sums
@@ -173,6 +177,7 @@ GroupDev group_dev(const esc_ctx* c) {
     g.node_code = c->d_node_code;
     g.code_list = c->d_code_list;
     g.slot_readers = c->d_slot_readers;
+    g.gslot = c->d_gslot;
     g.n_gp = c->gi.n_gp;
     g.G = c->gi.G;
     g.default_group = c->gi.default_group < 0 ? NONE : (uint32_t)c->gi.default_group;
@@ -195,6 +200,7 @@ PodDev pod_dev(const esc_ctx* c, int replica) {
 
 NodeDev node_dev(const esc_ctx* c) {
     NodeDev n;
+    n.gnode = c->nodes.gnode;
     n.flags = c->nodes.flags; n.label0 = c->nodes.label0; n.cpu = c->nodes.cpu; n.mem = c->nodes.mem;
     n.created = c->nodes.created; n.xl = c->nodes.xl; n.xl_off = c->nodes.xl_off;
     n.trk_node = c->nodes.trk_node; n.trk_group = c->nodes.trk_group; n.trk_start = c->nodes.trk_start;
@@ -224,7 +230,7 @@ void drop_graphs(esc_ctx* c) {
 }
 
 void release_work(esc_ctx* c) {
-    dfree(c->d_pod_part); dfree(c->d_wide_pod); dfree(c->d_wp_cnt); dfree(c->d_trk_acc);
+    dfree(c->d_pod_part); dfree(c->d_fold); dfree(c->d_wide_pod); dfree(c->d_wp_cnt); dfree(c->d_trk_acc);
     dfree(c->own_words); dfree(c->own_first); dfree(c->d_dec);
     c->d_words = nullptr;
     c->d_first = nullptr;
@@ -319,6 +325,7 @@ int32_t ensure_work(esc_ctx* c) {
     nblk = std::min<int64_t>(nblk, std::max(c->k_tiles, c->c_tiles));
     c->nblk = (int)nblk;
     HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * S));
+    HIP_TRY(dalloc(&c->d_fold, (size_t)FOLD_SPLIT * 4 * S));
     HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
     HIP_TRY(dalloc(&c->d_wp_cnt, (size_t)S));
     HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)S * WP_K * sizeof(int64_t)));
@@ -374,8 +381,9 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
         HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, st));
     }
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    HIP_TRY(launch_pod_fold(c->d_pod_part, nblk, pod_slots(c), c->d_fold, st));   // K3a
     esc_group_decision* dec = c->zero_copy ? c->h_dec_dev : c->d_dec;
-    HIP_TRY(launch_combine(g, n, c->d_pod_part, nblk, c->nodes.rows, c->d_wide_pod, c->d_wp_cnt, c->d_trk_acc,
+    HIP_TRY(launch_combine(g, n, c->d_fold, nblk ? FOLD_SPLIT : 0, c->nodes.rows, c->d_wide_pod, c->d_wp_cnt, c->d_trk_acc,
                            c->d_words, c->d_first, decide, dec, st));
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     if (copy_out && !c->zero_copy) {
@@ -477,12 +485,18 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     if (dalloc(&c->d_dry, G) || dalloc(&c->d_params, G)) return fail(ESC_E_NOMEM);
     const GroupIndex& gi = c->gi;
     if (dalloc(&c->d_gpair, G) || dalloc(&c->d_node_code, gi.n_gp) ||
-        dalloc(&c->d_code_list, gi.code_list.size()) || dalloc(&c->d_slot_readers, (size_t)gi.n_gp + 1))
+        dalloc(&c->d_code_list, gi.code_list.size()) || dalloc(&c->d_slot_readers, (size_t)gi.n_gp + 1) ||
+        dalloc(&c->d_gslot, G))
         return fail(ESC_E_NOMEM);
     // groups reading each pod slot in K3: the default group reads the default filter's
     // slot n_gp, every other group its pair's slot
     std::vector<uint32_t> readers((size_t)gi.n_gp + 1, 0);
-    for (int32_t g = 0; g < n_groups; ++g) ++readers[g == gi.default_group ? gi.n_gp : gi.gpair[g]];
+    std::vector<uint32_t> gslot(G);
+    for (int32_t g = 0; g < n_groups; ++g) {
+        gslot[g] = g == gi.default_group ? gi.n_gp : gi.gpair[g];
+        ++readers[gslot[g]];
+    }
+    if (hipMemcpy(c->d_gslot, gslot.data(), G * 4, hipMemcpyHostToDevice)) return fail(ESC_E_HIP);
     if (hipMemcpy(c->d_slot_readers, readers.data(), readers.size() * 4, hipMemcpyHostToDevice))
         return fail(ESC_E_HIP);
     if (hipMemcpy(c->d_gpair, gi.gpair.data(), G * 4, hipMemcpyHostToDevice) ||
@@ -510,7 +524,7 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         for (auto& b : c->pods) b.release();
         c->nodes.release();
         dfree(c->d_dry); dfree(c->d_params);
-        dfree(c->d_gpair); dfree(c->d_node_code); dfree(c->d_code_list); dfree(c->d_slot_readers);
+        dfree(c->d_gpair); dfree(c->d_node_code); dfree(c->d_code_list); dfree(c->d_slot_readers); dfree(c->d_gslot);
         for (int i = 0; i < MAX_STAGES; ++i)
             if (c->ev[i]) hipEventDestroy(c->ev[i]);
         if (c->side) hipStreamSynchronize(c->side);
@@ -848,6 +862,22 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     if (n_pieces) HIP_TRY(hipMemcpy(b.piece_pair, piece_pair.data(), piece_pair.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(b.pp_off, pp_off.data(), pp_off.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(dalloc(&b.rows, (size_t)std::max<int64_t>(n_pieces, 1) * NR_K));
+    {   // per-group facts fixed by this snapshot: this rank's pieces of the group's pair and
+        // allNodes[0] (controller.go:207-211) = the pair's first entry (lowest node index)
+        std::vector<GroupNode> gn(G);
+        for (uint32_t g = 0; g < G; ++g) {
+            const uint32_t q = c->gi.gpair[g], p0 = pp_off[q], p1 = pp_off[q + 1];
+            GroupNode& x = gn[g];
+            x.plo = std::max<int64_t>(p0, pc_lo);
+            x.phi = std::min<int64_t>(p1, pc_hi);
+            if (x.phi < x.plo) x.phi = x.plo;
+            x.first = p1 > p0 ? (int64_t)e_node[piece_off[p0]] : INT64_MAX;
+            x.first_cpu = p1 > p0 ? s->cpu[x.first] : 0;
+            x.first_mem = p1 > p0 ? s->mem[x.first] : 0;
+        }
+        HIP_TRY(dalloc(&b.gnode, gn.size()));
+        HIP_TRY(hipMemcpy(b.gnode, gn.data(), gn.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
+    }
     c->n_entries = E;
     c->n_pieces = n_pieces;
     c->pc_lo = pc_lo;
