@@ -54,6 +54,15 @@ class GroupDecision(C.Structure):
                 ("taint_status", i32), ("reserved", i32)]
 
 
+class GroupMetrics(C.Structure):
+    _fields_ = [(n, dbl) for n in ("nodes", "nodes_cordoned", "nodes_untainted", "nodes_tainted", "pods",
+                                   "cpu_request", "cpu_capacity", "mem_capacity", "mem_request",
+                                   "cpu_percent", "mem_percent")] + [("set_mask", u32), ("reserved", u32)]
+
+
+METRIC_NAMES = [n for n, _ in GroupMetrics._fields_[:11]]
+
+
 class KV(C.Structure):
     _fields_ = [("key", cstr), ("value", cstr)]
 
@@ -132,6 +141,8 @@ _SIGS = {
     "esc_run": (i32, [VP]),
     "esc_sync": (i32, [VP]),
     "esc_results": (i32, [VP, P(GroupTotals), P(GroupDecision)]),
+    "esc_set_metrics": (i32, [VP, i32]),
+    "esc_metrics_results": (i32, [VP, P(GroupMetrics)]),
     "esc_use_graph": (i32, [VP, i32]),
     "esc_force_wide": (i32, [VP, i32]),
     "esc_set_timing": (i32, [VP, i32]),

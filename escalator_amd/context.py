@@ -16,11 +16,13 @@ from . import _lib as L
 from .objects import groups_from_c, groups_to_c, nodes_to_c, pods_to_c, states_to_c
 
 TOTALS_DTYPE = np.dtype([(n, np.int64) for n, _ in L.GroupTotals._fields_])
+METRICS_DTYPE = np.dtype([(n, np.float64) for n in L.METRIC_NAMES] + [("set_mask", np.uint32), ("reserved", np.uint32)])
 DECISION_DTYPE = np.dtype({"names": [n for n, _ in L.GroupDecision._fields_],
                            "formats": [np.float64, np.float64, np.int64, np.int64, np.int64, np.int64,
                                        np.int32, np.int32, np.int32, np.int32]})
 assert TOTALS_DTYPE.itemsize == C.sizeof(L.GroupTotals)
 assert DECISION_DTYPE.itemsize == C.sizeof(L.GroupDecision)
+assert METRICS_DTYPE.itemsize == C.sizeof(L.GroupMetrics)
 
 _POD_FIELDS = [("flags", np.uint32, "n_pods"), ("cpu0", np.uint32, "n_pods"), ("mem0", np.int64, "n_pods"),
                ("pair0", np.uint32, "n_pods"), ("xc_cpu", np.int64, "n_xc"), ("xc_mem", np.int64, "n_xc"),
@@ -235,6 +237,16 @@ class Context:
         L.check(self.lib.esc_results(self.handle, t.ctypes.data_as(C.POINTER(L.GroupTotals)),
                                      d.ctypes.data_as(C.POINTER(L.GroupDecision))), "esc_results")
         return t, d
+
+    def set_metrics(self, on: bool = True):
+        """K4 also computes the per-group gauges scaleNodeGroup sets (§8f)."""
+        L.check(self.lib.esc_set_metrics(self.handle, int(on)), "esc_set_metrics")
+
+    def metrics(self) -> np.ndarray:
+        m = np.zeros(self.G, METRICS_DTYPE)
+        L.check(self.lib.esc_metrics_results(self.handle, m.ctypes.data_as(C.POINTER(L.GroupMetrics))),
+                "esc_metrics_results")
+        return m
 
     def decide_all(self, states: list[dict] | None = None):
         """One full decision (world == 1): totals and decisions for every group."""

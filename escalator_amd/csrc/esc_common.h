@@ -180,6 +180,33 @@ ESC_HD void decide_one(const GroupParams& p, const Totals& t, esc_group_decision
     }
 }
 
+// The gauges scaleNodeGroup sets in this run — controller.go:224-228 (before any gate),
+// :275-278 (after the min/max gates), :309-315 (after calcPercentUsage succeeded; 0 when
+// scaling up from 0).  Memory gauges are float64(Quantity.MilliValue() / 1000): the
+// wrapped ×1000 product, integer-divided (truncating) by 1000.
+ESC_HD void metrics_one(const Totals& t, const esc_group_decision& d, esc_group_metrics& m) {
+    m.nodes = (double)t.n_nodes;
+    m.nodes_cordoned = (double)t.n_cord;
+    m.nodes_untainted = (double)t.n_unt;
+    m.nodes_tainted = (double)t.n_taint;
+    m.pods = (double)t.n_pods;
+    m.cpu_request = m.cpu_capacity = m.mem_capacity = m.mem_request = 0.0;
+    m.cpu_percent = m.mem_percent = 0.0;
+    m.reserved = 0;
+    m.set_mask = ESC_M_NODES | ESC_M_NODES_CORDONED | ESC_M_NODES_UNTAINTED | ESC_M_NODES_TAINTED | ESC_M_PODS;
+    if (d.branch == ESC_BR_EMPTY || d.branch == ESC_BR_GATE) return;                    // :233-255
+    m.cpu_request = (double)t.pod_cpu;
+    m.cpu_capacity = (double)t.node_cpu;
+    m.mem_capacity = (double)(milli_mem(t.node_mem) / 1000);
+    m.mem_request = (double)(milli_mem(t.pod_mem) / 1000);
+    m.set_mask |= ESC_M_CPU_REQUEST | ESC_M_CPU_CAPACITY | ESC_M_MEM_CAPACITY | ESC_M_MEM_REQUEST;
+    if (d.branch == ESC_BR_BELOW_MIN || d.branch == ESC_BR_PCT_ERR) return;             // :281, :300
+    const bool from_zero = d.cpu_pct == MAX_FLOAT64 || d.mem_pct == MAX_FLOAT64;
+    m.cpu_percent = from_zero ? 0.0 : d.cpu_pct;
+    m.mem_percent = from_zero ? 0.0 : d.mem_pct;
+    m.set_mask |= ESC_M_CPU_PERCENT | ESC_M_MEM_PERCENT;
+}
+
 // ---------------------------------------------------------- pod flag helpers
 ESC_HD uint32_t pf_xreg(uint32_t f)  { return (f >> ESC_PF_XREG_SHIFT) & ESC_PF_CNT_MASK; }
 ESC_HD uint32_t pf_xinit(uint32_t f) { return (f >> ESC_PF_XINIT_SHIFT) & ESC_PF_CNT_MASK; }

@@ -113,6 +113,7 @@ struct GroupDev {
     const uint32_t* code_list; // CODE_MULTI lists: [count, g...]
     const uint32_t* slot_readers; // [n_gp + 1] groups reading each pod slot in K3
     const uint32_t* gslot;     // [G] the group's pod slot: its pair, or n_gp for the default group
+    esc_group_metrics* metrics; // [G] gauges written by K4, or null (esc_set_metrics)
     uint32_t n_gp;             // pod slots: pair ids [0, n_gp) + the default filter's slot n_gp
     int32_t G;
     uint32_t default_group;    // NONE when no group is named "default"

@@ -752,7 +752,8 @@ __device__ __forceinline__ __int128 join_parts(uint64_t lo, uint64_t lo_carry, i
 }
 
 __device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn, int32_t g,
-                                         const int64_t* __restrict__ w, esc_group_decision& dec) {
+                                         const int64_t* __restrict__ w, esc_group_decision& dec,
+                                         esc_group_metrics* __restrict__ met) {
     Totals t;
     int64_t flags = 0;
     if (!join_split(w[TW_POD_CPU_LO], w[TW_POD_CPU_HI], t.pod_cpu)) flags |= ESC_TF_POD_OVERFLOW;
@@ -769,6 +770,11 @@ __device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn,
     t.first_mem = gn.first_mem;
     t.flags = flags;
     decide_one(G.params[g], t, dec);
+    if (met) {
+        esc_group_metrics m;
+        metrics_one(t, dec, m);
+        met[g] = m;
+    }
 }
 
 // The decisions of 64 consecutive groups (sdec, LDS) stored by 256 threads as 16-B pieces
@@ -957,7 +963,7 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
     w[TW_N_TAINT] = (int64_t)n_taint;
     w[TW_N_CORD] = (int64_t)n_cord;
     firsts[g] = gn.first;
-    if (decide) finalize(G, gn, g, w, sdec[lane]);
+    if (decide) finalize(G, gn, g, w, sdec[lane], G.metrics);
     }
     if (decide) {
         __syncthreads();
@@ -970,7 +976,8 @@ __global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int
                                                 esc_group_decision* __restrict__ dec) {
     __shared__ esc_group_decision sdec[64];
     const int32_t g = blockIdx.x * 64 + (int32_t)threadIdx.x;
-    if (threadIdx.x < 64 && g < G.G) finalize(G, N.gnode[g], g, words + (int64_t)g * TW_K, sdec[threadIdx.x]);
+    if (threadIdx.x < 64 && g < G.G)
+        finalize(G, N.gnode[g], g, words + (int64_t)g * TW_K, sdec[threadIdx.x], G.metrics);
     __syncthreads();
     store_decisions(dec, blockIdx.x * 64, G.G, sdec);
 }

@@ -129,6 +129,8 @@ struct esc_ctx {
     esc_group_decision* h_dec_dev = nullptr;                 // device view of h_dec (zero-copy)
     bool zero_copy = true;                                    // K3/K4 write decisions to h_dec
     bool fork_nodes = true;                                   // K2 on the side stream, beside K1
+    bool want_metrics = false;                                // K4 also writes the gauges
+    esc_group_metrics* d_metrics = nullptr;
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int64_t *bound_words = nullptr, *bound_first = nullptr;  // caller-bound (RCCL) buffers
@@ -178,6 +180,7 @@ GroupDev group_dev(const esc_ctx* c) {
     g.code_list = c->d_code_list;
     g.slot_readers = c->d_slot_readers;
     g.gslot = c->d_gslot;
+    g.metrics = c->want_metrics ? c->d_metrics : nullptr;
     g.n_gp = c->gi.n_gp;
     g.G = c->gi.G;
     g.default_group = c->gi.default_group < 0 ? NONE : (uint32_t)c->gi.default_group;
@@ -231,7 +234,7 @@ void drop_graphs(esc_ctx* c) {
 
 void release_work(esc_ctx* c) {
     dfree(c->d_pod_part); dfree(c->d_fold); dfree(c->d_wide_pod); dfree(c->d_wp_cnt); dfree(c->d_trk_acc);
-    dfree(c->own_words); dfree(c->own_first); dfree(c->d_dec);
+    dfree(c->own_words); dfree(c->own_first); dfree(c->d_dec); dfree(c->d_metrics);
     c->d_words = nullptr;
     c->d_first = nullptr;
     if (c->h_dec) hipHostFree(c->h_dec);
@@ -337,6 +340,8 @@ int32_t ensure_work(esc_ctx* c) {
     c->d_words = c->bound_words ? c->bound_words : c->own_words;
     c->d_first = c->bound_first ? c->bound_first : c->own_first;
     HIP_TRY(dalloc(&c->d_dec, (size_t)G));
+    HIP_TRY(dalloc(&c->d_metrics, (size_t)G));
+    HIP_TRY(hipMemset(c->d_metrics, 0, (size_t)G * sizeof(esc_group_metrics)));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_dec), (size_t)G * sizeof(esc_group_decision)));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_dec_dev), c->h_dec, 0));
     c->work_ready = true;
@@ -913,6 +918,23 @@ int32_t esc_set_state(esc_ctx* c, const esc_group_state* st) {
     HIP_TRY(hipMemcpyAsync(c->d_params, c->params.data(), c->params.size() * sizeof(GroupParams),
                            hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    return ESC_OK;
+}
+
+int32_t esc_set_metrics(esc_ctx* c, int32_t enable) {
+    if (!c) return ESC_E_INVAL;
+    c->want_metrics = enable != 0;
+    drop_graphs(c);
+    return ESC_OK;
+}
+
+int32_t esc_metrics_results(esc_ctx* c, esc_group_metrics* out) {
+    if (!c || !out) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->work_ready || !c->want_metrics) return ESC_E_STATE;
+    int32_t rc = esc_sync(c);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(out, c->d_metrics, (size_t)c->gi.G * sizeof(esc_group_metrics), hipMemcpyDeviceToHost));
     return ESC_OK;
 }
 

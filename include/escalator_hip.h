@@ -128,6 +128,29 @@ typedef struct esc_group_decision {
     int32_t reserved;
 } esc_group_decision;
 
+/* Per-group gauges scaleNodeGroup sets on every run (pkg/metrics/metrics.go names;
+ * set at controller.go:224-228, :275-278, :309-315).  `set_mask` bit ESC_M_* = the gauge
+ * was Set this run; the others keep their previous value in the reference's registry
+ * (a gate or early return skips them).                                              */
+#define ESC_M_NODES          (1u << 0)   /* NodeGroupNodes            float64(len(allNodes))       */
+#define ESC_M_NODES_CORDONED (1u << 1)   /* NodeGroupNodesCordoned                                   */
+#define ESC_M_NODES_UNTAINTED (1u << 2)  /* NodeGroupNodesUntainted                                  */
+#define ESC_M_NODES_TAINTED  (1u << 3)   /* NodeGroupNodesTainted                                    */
+#define ESC_M_PODS           (1u << 4)   /* NodeGroupPods                                            */
+#define ESC_M_CPU_REQUEST    (1u << 5)   /* NodeGroupCPURequest      float64(cpuRequest.MilliValue()) */
+#define ESC_M_CPU_CAPACITY   (1u << 6)   /* NodeGroupCPUCapacity                                     */
+#define ESC_M_MEM_CAPACITY   (1u << 7)   /* NodeGroupMemCapacity     float64(memCapacity.MilliValue() / 1000) */
+#define ESC_M_MEM_REQUEST    (1u << 8)   /* NodeGroupMemRequest                                      */
+#define ESC_M_CPU_PERCENT    (1u << 9)   /* NodeGroupsCPUPercent     0 when scaling up from 0        */
+#define ESC_M_MEM_PERCENT    (1u << 10)  /* NodeGroupsMemPercent                                     */
+typedef struct esc_group_metrics {
+    double nodes, nodes_cordoned, nodes_untainted, nodes_tainted, pods;
+    double cpu_request, cpu_capacity, mem_capacity, mem_request;
+    double cpu_percent, mem_percent;
+    uint32_t set_mask;
+    uint32_t reserved;
+} esc_group_metrics;
+
 /* ---------------------------------------------------------- object-level input
  * What the cgo shim copies out of *v1.Pod / *v1.Node (no Go pointers retained).
  * Resource quantities arrive as Quantity.MilliValue() (cpu) and Quantity.Value()
@@ -339,6 +362,10 @@ int32_t esc_decide(esc_ctx* ctx);
 int32_t esc_run(esc_ctx* ctx);
 int32_t esc_sync(esc_ctx* ctx);
 int32_t esc_results(esc_ctx* ctx, esc_group_totals* totals, esc_group_decision* decisions);
+/* Metric gauges (§8f): computed by K4 beside the decisions when enabled (off by default;
+ * they stay in device memory until esc_metrics_results copies them out, after esc_sync). */
+int32_t esc_set_metrics(esc_ctx* ctx, int32_t enable);
+int32_t esc_metrics_results(esc_ctx* ctx, esc_group_metrics* out);
 int32_t esc_use_graph(esc_ctx* ctx, int32_t enable);
 int32_t esc_force_wide(esc_ctx* ctx, int32_t enable);   /* testing: always take the wide path */
 /* Last kernel's device time in ms per stage (timing mode), see DESIGN.md §6. */

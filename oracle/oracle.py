@@ -333,6 +333,34 @@ def untaint_newest_n(created_ns: list[int], n: int) -> list[int]:
 
 
 # ------------------------------------------------------ scaleNodeGroup (pure part)
+def go_div_trunc(a: int, b: int) -> int:
+    """Go's int64 '/' (truncates toward zero)."""
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b > 0) else -q
+
+
+def node_group_metrics(out: dict) -> dict:
+    """The gauges scaleNodeGroup Sets in the run that produced `out` (pkg/metrics/metrics.go):
+    controller.go:224-228 before any gate; :275-278 after the min/max gates
+    (float64(cpu.MilliValue()), float64(mem.MilliValue() / 1000)); :309-315 after a
+    successful calcPercentUsage (0 when scaling up from 0).  Absent key = not Set."""
+    m = {"nodes": float(out["n_nodes"]), "nodes_cordoned": float(out["n_cordoned"]),
+         "nodes_untainted": float(out["n_untainted"]), "nodes_tainted": float(out["n_tainted"]),
+         "pods": float(out["n_pods"])}
+    if out["branch"] in ("empty", "gate"):
+        return m
+    m["cpu_request"] = float(out["pod_cpu_m"])
+    m["cpu_capacity"] = float(out["node_cpu_m"])
+    m["mem_capacity"] = float(go_div_trunc(milli_value_mem(out["node_mem_b"]), 1000))
+    m["mem_request"] = float(go_div_trunc(milli_value_mem(out["pod_mem_b"]), 1000))
+    if out["branch"] in ("below_min", "pct_err"):
+        return m
+    from_zero = out["cpu_pct"] == MAX_FLOAT64 or out["mem_pct"] == MAX_FLOAT64
+    m["cpu_percent"] = 0.0 if from_zero else out["cpu_pct"]
+    m["mem_percent"] = 0.0 if from_zero else out["mem_pct"]
+    return m
+
+
 def scale_node_group(group: dict, state: dict, pods: list[dict], nodes: list[dict],
                      global_dry_mode: bool = False, tracker: list[str] | None = None) -> dict:
     """(*Controller).scaleNodeGroup — controller.go:192-397, decision arithmetic only.

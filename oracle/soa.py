@@ -138,3 +138,23 @@ def order(nodes: dict, groups: list[dict], group: int, which: int, node_lo: int 
     m = int(m)
     out = out[:m]
     return out if cap is None else out[:cap]
+
+
+METRIC_NAMES = ["nodes", "nodes_cordoned", "nodes_untainted", "nodes_tainted", "pods", "cpu_request",
+                "cpu_capacity", "mem_capacity", "mem_request", "cpu_percent", "mem_percent"]
+
+
+def metrics(tot: np.ndarray, df: np.ndarray, di: np.ndarray) -> list[dict]:
+    """Per-group gauges from the C oracle's totals and decisions, by the literal rules of
+    oracle.node_group_metrics (controller.go:224-228, :275-278, :309-315)."""
+    from oracle import oracle as O
+    out = []
+    for g in range(tot.shape[0]):
+        t = dict(zip(TOT_FIELDS, (int(x) for x in tot[g])))
+        run = {"n_nodes": t["n_nodes"], "n_cordoned": t["n_cordoned"], "n_untainted": t["n_untainted"],
+               "n_tainted": t["n_tainted"], "n_pods": t["n_pods"], "pod_cpu_m": t["pod_cpu_m"],
+               "pod_mem_b": t["pod_mem_b"], "node_cpu_m": t["node_cpu_m"], "node_mem_b": t["node_mem_b"],
+               "branch": BRANCH_NAMES[int(di[g, 5])], "cpu_pct": float(df[g, 0]), "mem_pct": float(df[g, 1])}
+        out.append(O.node_group_metrics(run))
+    return out
+

@@ -27,6 +27,16 @@ def esc():
     return escalator_amd
 
 
+def check_metrics(m, expected):
+    """GPU gauges (esc_metrics_results) == the oracle's, bit for bit, and the same set mask."""
+    from escalator_amd._lib import METRIC_NAMES
+    for g, e in enumerate(expected):
+        mask = sum(1 << k for k, n in enumerate(METRIC_NAMES) if n in e)
+        assert int(m["set_mask"][g]) == mask, (g, e)
+        for n, v in e.items():
+            assert _bits(m[n][g]) == _bits(v), (g, n, m[n][g], v)
+
+
 def check_against_c_oracle(tot, dec, otot, odf, odi):
     names = list(tot.dtype.names)
     for k, name in enumerate(soa.TOT_FIELDS):
@@ -151,9 +161,13 @@ def test_random_objects_vs_literal(esc, seed):
     ctx = esc.Context(groups)
     P, N = ctx.pack(pods, nodes, trackers)
     ctx.load(P, N)
+    ctx.set_metrics(True)
     for wide in (False, True):
         ctx.force_wide(wide)
         tot, dec = ctx.decide_all(states)
+        check_metrics(ctx.metrics(), [O.node_group_metrics(O.scale_node_group(groups[g], states[g], pods, nodes,
+                                                                              tracker=trackers.get(g, [])))
+                                      for g in range(G)])
         for g in range(G):
             L = O.scale_node_group(groups[g], states[g], pods, nodes, tracker=trackers.get(g, []))
             t, d = tot[g], dec[g]
@@ -207,6 +221,10 @@ def test_synthetic_vs_c_oracle(esc, cfg, P, N, G):
     ctx.run()
     tot, dec = ctx.results()
     check_against_c_oracle(tot, dec, otot, odf, odi)
+    ctx.force_wide(False)
+    ctx.set_metrics(True)
+    ctx.run()
+    check_metrics(ctx.metrics(), soa.metrics(otot, odf, odi))
 
 
 def test_synthetic_sort_vs_c_oracle(esc):
@@ -243,10 +261,12 @@ def test_sharded_two_contexts_host_exchange(esc):
     W = np.sum(words, axis=0)
     F = np.min(firsts, axis=0)
     for c, _ in ctxs:
+        c.set_metrics(True)
         c.exchange_upload(W, F)
         c.decide()
         tot, dec = c.results()
         check_against_c_oracle(tot, dec, otot, odf, odi)
+        check_metrics(c.metrics(), soa.metrics(otot, odf, odi))
 
 
 def test_determinism_repeat(esc):

@@ -171,3 +171,42 @@ def test_go_semantics_edges():
     assert d == O.INT64_MIN and err == O.ERR_NEG_DELTA
     with pytest.raises(O.QuantityOverflow):
         O.quantity_add(O.INT64_MAX, 1)
+
+
+def test_metrics_gauges_follow_scale_node_group_returns(golden):
+    """node_group_metrics: which gauges each return path of scaleNodeGroup Sets
+    (controller.go:224-228 always; :275-278 after the min/max gates; :309-315 after a
+    successful calcPercentUsage) on the reference's TestScaleNodeGroup cases.  The gauge
+    values themselves are not asserted by any reference test (parity unpinned beyond the
+    restatement)."""
+    always = {"nodes", "nodes_cordoned", "nodes_untainted", "nodes_tainted", "pods"}
+    req = {"cpu_request", "cpu_capacity", "mem_capacity", "mem_request"}
+    pct = {"cpu_percent", "mem_percent"}
+    seen = set()
+    for c in golden["controller"]["scale_node_group"]["cases"]:
+        if c.get("lister_error"):
+            continue
+        n_n, n_cpu, n_mem = c["nodes"]
+        n_p, p_cpu, p_mem = c["pods"]
+        out = O.scale_node_group(_default_group(c["opts"]), {}, build_test_pods(n_p, {"CPU": [p_cpu], "Mem": [p_mem]}),
+                                 build_test_nodes(n_n, {"CPU": n_cpu, "Mem": n_mem}))
+        m = O.node_group_metrics(out)
+        want = always | (req if out["branch"] not in ("empty", "gate") else set()) | \
+            (pct if out["branch"] not in ("empty", "gate", "below_min", "pct_err") else set())
+        assert set(m) == want, (c["name"], out["branch"], sorted(m))
+        assert m["nodes"] == float(n_n)
+        if "cpu_percent" in m and out["cpu_pct"] != O.MAX_FLOAT64:
+            assert m["cpu_percent"] == out["cpu_pct"]
+        seen.add(out["branch"])
+    assert len(seen) >= 3
+
+
+def test_metrics_memory_gauge_quirk():
+    """float64(mem.MilliValue() / 1000): the ×1000 product wraps in int64 before Go's
+    truncating division (unpinned; restated from apimachinery v0.22.5)."""
+    out = {"n_nodes": 1, "n_cordoned": 0, "n_untainted": 1, "n_tainted": 0, "n_pods": 1, "pod_cpu_m": 5,
+           "pod_mem_b": 1 << 62, "node_cpu_m": 7, "node_mem_b": 3, "branch": "none", "cpu_pct": 1.0, "mem_pct": 2.0}
+    m = O.node_group_metrics(out)
+    assert m["mem_capacity"] == 3.0
+    assert m["mem_request"] == float(O.go_div_trunc(O.wrap64((1 << 62) * 1000), 1000))
+    assert O.go_div_trunc(-1999, 1000) == -1 and O.go_div_trunc(1999, -1000) == -1
