@@ -141,6 +141,10 @@ _SIGS = {
     "esc_run": (i32, [VP]),
     "esc_sync": (i32, [VP]),
     "esc_results": (i32, [VP, P(GroupTotals), P(GroupDecision)]),
+    "esc_set_spare": (i32, [VP, dbl]),
+    "esc_pods_upsert": (i32, [VP, P(i64), P(PodSoA)]),
+    "esc_pods_delete": (i32, [VP, P(i64), i64]),
+    "esc_nodes_update": (i32, [VP, P(i64), i64, P(u32), P(i64), P(i64)]),
     "esc_set_metrics": (i32, [VP, i32]),
     "esc_metrics_results": (i32, [VP, P(GroupMetrics)]),
     "esc_use_graph": (i32, [VP, i32]),

@@ -164,6 +164,36 @@ class Context:
         hi = s.node_c.n_nodes if node_hi is None else node_hi
         L.check(self.lib.esc_load_nodes(self.handle, C.byref(s.node_c), node_lo, hi), "esc_load_nodes")
 
+    # ------------------------------------------------ incremental snapshot (§8f)
+    def set_spare(self, fraction: float):
+        """Spare slots per pod signature class at the next load (for pods_upsert)."""
+        L.check(self.lib.esc_set_spare(self.handle, float(fraction)), "esc_set_spare")
+
+    def pods_upsert(self, ids, pods: dict) -> int:
+        """Patch / insert packed pods (a `pack` result) under the given ids.  Returns the
+        ABI code: 0, or ESC_E_LIMIT when the batch does not fit in place (reload)."""
+        ids = np.ascontiguousarray(ids, np.int64)
+        ps, keep = pod_soa(pods)
+        rc = self.lib.esc_pods_upsert(self.handle, ids.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(ps))
+        if rc not in (0, L.ESC_E_LIMIT):
+            L.check(rc, "esc_pods_upsert")
+        return rc
+
+    def pods_delete(self, ids):
+        ids = np.ascontiguousarray(ids, np.int64)
+        L.check(self.lib.esc_pods_delete(self.handle, ids.ctypes.data_as(C.POINTER(C.c_int64)), len(ids)),
+                "esc_pods_delete")
+
+    def nodes_update(self, ids, flags, cpu, mem):
+        ids = np.ascontiguousarray(ids, np.int64)
+        f = np.ascontiguousarray(flags, np.uint32)
+        c_ = np.ascontiguousarray(cpu, np.int64)
+        m = np.ascontiguousarray(mem, np.int64)
+        L.check(self.lib.esc_nodes_update(self.handle, ids.ctypes.data_as(C.POINTER(C.c_int64)), len(ids),
+                                          f.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                          c_.ctypes.data_as(C.POINTER(C.c_int64)),
+                                          m.ctypes.data_as(C.POINTER(C.c_int64))), "esc_nodes_update")
+
     def stream_bytes(self) -> tuple[int, int]:
         """Algorithmic HBM bytes one decision streams on this rank: (K1 pods, K2 nodes)."""
         a, b = C.c_int64(), C.c_int64()

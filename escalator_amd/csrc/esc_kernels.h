@@ -140,6 +140,11 @@ hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* f
                           const int64_t* node_rows, int64_t* wide_pod, uint32_t* wp_cnt, int64_t* trk_acc,
                           int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
+struct PatchTargets {          // k_patch destinations: 4-byte arrays 0-5, 8-byte arrays 6-11
+    uint32_t* u32[6];
+    int64_t* i64[6];
+};
+hipError_t launch_patch(const PatchTargets& t, const uint64_t* where, const uint64_t* what, int64_t n, hipStream_t st);
 hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* words,
                          const int64_t* first, esc_group_decision* dec, hipStream_t st);
 

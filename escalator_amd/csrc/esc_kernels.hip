@@ -1267,6 +1267,21 @@ __global__ __launch_bounds__(256) void k_seg_bounds(const uint32_t* __restrict__
     seg[s] = lo;
 }
 
+// ===================================================================== snapshot patches
+// Incremental snapshot updates (esc_pods_upsert / esc_pods_delete / esc_nodes_update):
+// element writes into the resident arrays; where[i] = target << 60 | index, targets 0-5
+// are 4-byte arrays, 6-11 8-byte ones.  The host dedupes (target, index) first.
+__global__ __launch_bounds__(256) void k_patch(PatchTargets T, const uint64_t* __restrict__ where,
+                                               const uint64_t* __restrict__ what, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t w = where[i];
+    const uint32_t t = (uint32_t)(w >> 60);
+    const int64_t idx = (int64_t)(w & ((1ull << 60) - 1));
+    if (t < 6) T.u32[t][idx] = (uint32_t)what[i];
+    else T.i64[t - 6][idx] = (int64_t)what[i];
+}
+
 // ===================================================================== launchers
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st) {
@@ -1316,6 +1331,12 @@ hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* f
                           int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st) {
     hipLaunchKernelGGL(k_combine, dim3((g.G + 63) / 64), dim3(CB_WAVES * 64), 0, st, g, n, fold, nsplit,
                        node_rows, wide_pod, wp_cnt, trk_acc, words, first, decide ? 1 : 0, dec);
+    return hipGetLastError();
+}
+
+hipError_t launch_patch(const PatchTargets& t, const uint64_t* where, const uint64_t* what, int64_t n, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_patch, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, t, where, what, n);
     return hipGetLastError();
 }
 

@@ -163,6 +163,20 @@ struct esc_ctx {
     std::vector<int64_t> h_created;                           // [lo, hi) creation times (tie order)
     // per-function drop-ins run on a one-group list context
     esc_ctx* list_ctx = nullptr;
+    // incremental snapshot (§8f rank 1): where each loaded pod lives, free K slots
+    double spare_frac = 0.0;                                  // esc_set_spare
+    std::vector<int32_t> pod_cls;                             // by pod id: K class index, -1 C, -2 absent
+    std::vector<int64_t> pod_pos;                             // K: position in its class; C: base-array index
+    std::vector<std::vector<int64_t>> cls_free;               // per K class: free positions
+    std::vector<PodClass> h_cls;
+    std::vector<int> h_cls_of;                                // signature id -> class index (-1: none)
+    std::vector<uint32_t> h_cflags;                           // C-section flags (deletes keep the counts)
+    int64_t live_pods = 0, live_xc = 0, live_xp = 0;
+    // node state mirrors for esc_nodes_update
+    std::vector<uint32_t> h_nflags;
+    std::vector<int64_t> h_ncpu, h_nmem;
+    std::vector<uint32_t> ne_off, ne_pos;                     // node -> its pair-major entry positions
+    std::vector<GroupNode> h_gnode;
 };
 
 namespace esc {
@@ -628,14 +642,18 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     std::vector<int> cls_of(POD_CLASS_IDS, -1);
     int64_t kt = 0, xk = 0, pk = 0, kw = 0;
     for (int id = 0; id < POD_CLASS_IDS; ++id) {
-        if (!cnt[id]) continue;
+        // with spare slots requested every signature the K layout can hold gets a class, so
+        // that inserts of shapes absent at load still land in place
+        const bool holdable = (id / 32) + ((id / 8) % 4) + ((id / 4) % 2) <= 3;
+        if (!cnt[id] && !(c->spare_frac > 0 && holdable)) continue;
         PodClass k;
         std::memset(&k, 0, sizeof k);
         k.nxp = (uint32_t)(id % 4);
         k.ovh = (uint32_t)((id / 4) % 2);
         k.xinit = (uint32_t)((id / 8) % 4);
         k.xreg = (uint32_t)(id / 32);
-        const int64_t R = k.xreg + k.xinit + k.ovh, tiles = (cnt[id] + TILE - 1) / TILE;
+        const int64_t want = cnt[id] + (c->spare_frac > 0 ? std::max<int64_t>(1, (int64_t)(cnt[id] * c->spare_frac)) : 0);
+        const int64_t R = k.xreg + k.xinit + k.ovh, tiles = (want + TILE - 1) / TILE;
         k.t0 = kt;
         k.t1 = kt + tiles;
         k.xc0 = xk;
@@ -660,6 +678,8 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     std::vector<int64_t> hm(npad, 0), hxc(nxc_dev, 0), hxm(nxc_dev, 0);
     std::vector<uint32_t> hxp(nxp_dev, NONE);
     std::vector<uint32_t> xc_base(c_tiles + 1, 0), xp_base(c_tiles + 1, 0);
+    std::vector<int32_t> pod_cls(n);
+    std::vector<int64_t> pod_pos(n);
     {
         std::vector<int64_t> pos(POD_CLASS_IDS, 0);
         int64_t ic = 0;
@@ -673,6 +693,8 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
             if (id >= 0) {
                 const PodClass& k = cls[cls_of[id]];
                 const int64_t q = pos[id]++, rt = q / TILE, sl = q % TILE;
+                pod_cls[i] = cls_of[id];
+                pod_pos[i] = q;
                 const int64_t s64 = ((sl & 3) >> 1) * 128 + 2 * (sl >> 2) + (sl & 1);   // K1's pos64
                 d = (k.t0 + rt) * TILE + sl;
                 d64 = (k.t0 + rt) * TILE + s64;
@@ -685,6 +707,8 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
             } else {
                 if (ic % CTILE == 0) { xc_base[ic / CTILE] = (uint32_t)oc; xp_base[ic / CTILE] = (uint32_t)op; }
                 d = d64 = c0 + ic++;
+                pod_cls[i] = -1;
+                pod_pos[i] = d;
                 for (uint32_t j = 0; j < nc; ++j) { hxc[oc + j] = p->xc_cpu[rc + j]; hxm[oc + j] = p->xc_mem[rc + j]; }
                 for (uint32_t j = 0; j < nx; ++j) hxp[op + j] = p->xp_pair[rp + j];
                 oc += nc;
@@ -732,6 +756,22 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         if (!big.empty()) HIP_TRY(hipMemcpy(b.big, src(big.data(), a.big), big.size() * 4, kind));
         if (n_cls) HIP_TRY(hipMemcpy(b.cls, src(cls.data(), a.cls), n_cls * sizeof(PodClass), kind));
     }
+    // incremental-update bookkeeping: slot map, free K positions (padding and spare)
+    c->pod_cls.swap(pod_cls);
+    c->pod_pos.swap(pod_pos);
+    c->h_cls = cls;
+    c->h_cls_of = cls_of;
+    c->cls_free.assign(cls.size(), {});
+    for (int id = 0; id < POD_CLASS_IDS; ++id) {
+        const int ci = cls_of[id];
+        if (ci < 0) continue;
+        auto& fr = c->cls_free[ci];
+        for (int64_t q = (cls[ci].t1 - cls[ci].t0) * TILE - 1; q >= cnt[id]; --q) fr.push_back(q);
+    }
+    c->h_cflags.assign(hf.begin() + c0, hf.end());
+    c->live_pods = n;
+    c->live_xc = p->n_xc;
+    c->live_xp = p->n_xp;
     c->n_pods = n;
     c->k_tiles = k_tiles;
     c->k_weight = kw;
@@ -813,6 +853,14 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     }
     const int64_t n_pieces = (int64_t)piece_pair.size();
     piece_off.push_back((uint32_t)E);
+    // node -> its entry positions (esc_nodes_update patches the entries' copies)
+    std::vector<uint32_t> ne_off((size_t)n + 1, 0), ne_pos((size_t)std::max<int64_t>(E, 1));
+    for (int64_t k = 0; k < E; ++k) ++ne_off[(uint32_t)ent[k] + 1];
+    for (int64_t i = 0; i < n; ++i) ne_off[i + 1] += ne_off[i];
+    {
+        std::vector<uint32_t> fill(ne_off.begin(), ne_off.end() - 1);
+        for (int64_t k = 0; k < E; ++k) ne_pos[fill[(uint32_t)ent[k]]++] = (uint32_t)k;
+    }
     const uint32_t n_gp = c->gi.n_gp;
     std::vector<uint32_t> pp_off((size_t)n_gp + 1);
     for (uint32_t q = 0; q <= n_gp; ++q)
@@ -882,7 +930,13 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
         }
         HIP_TRY(dalloc(&b.gnode, gn.size()));
         HIP_TRY(hipMemcpy(b.gnode, gn.data(), gn.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
+        c->h_gnode.swap(gn);
     }
+    c->ne_off.swap(ne_off);
+    c->ne_pos.swap(ne_pos);
+    c->h_nflags.assign(s->flags, s->flags + n);
+    c->h_ncpu.assign(s->cpu, s->cpu + n);
+    c->h_nmem.assign(s->mem, s->mem + n);
     c->n_entries = E;
     c->n_pieces = n_pieces;
     c->pc_lo = pc_lo;
@@ -905,7 +959,7 @@ int32_t esc_stream_bytes(const esc_ctx* c, int64_t* pod_bytes, int64_t* node_byt
     if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
     // K1: flags 4 + cpu0 4 + mem0 8 + pair0 4 per pod, 16 per extra container record,
     // 4 per extra pair, 8 per C tile (record offsets); K2: see esc_load_nodes
-    *pod_bytes = c->n_pods * 20 + c->n_xc * 16 + c->n_xp * 4 + c->c_tiles * 8;
+    *pod_bytes = c->live_pods * 20 + c->live_xc * 16 + c->live_xp * 4 + c->c_tiles * 8;
     *node_bytes = c->node_bytes;
     return ESC_OK;
 }
@@ -1119,6 +1173,246 @@ int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* de
             }
         }
     }
+    return ESC_OK;
+}
+
+// ------------------------------------------------ incremental snapshot (§8f rank 1)
+}  // extern "C"
+
+namespace {
+
+struct Patches {
+    std::vector<uint64_t> where, what;
+    void add(uint32_t target, int64_t idx, uint64_t v) {
+        where.push_back(((uint64_t)target << 60) | (uint64_t)idx);
+        what.push_back(v);
+    }
+};
+
+// Applies a batch (last write per element wins) to `targets` of every replica.
+int32_t apply_patches(esc_ctx* c, Patches& P, const std::vector<PatchTargets>& targets) {
+    const int64_t n = (int64_t)P.where.size();
+    if (n == 0) return ESC_OK;
+    std::vector<int64_t> ord(n);
+    for (int64_t i = 0; i < n; ++i) ord[i] = i;
+    std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return P.where[a] < P.where[b]; });
+    std::vector<uint64_t> w, v;
+    for (int64_t k = 0; k < n; ++k) {
+        const int64_t i = ord[k];
+        if (k + 1 < n && P.where[ord[k + 1]] == P.where[i]) continue;      // a later write wins
+        w.push_back(P.where[i]);
+        v.push_back(P.what[i]);
+    }
+    uint64_t *dw = nullptr, *dv = nullptr;
+    HIP_TRY(dalloc(&dw, w.size()));
+    HIP_TRY(dalloc(&dv, v.size()));
+    int32_t rc = ESC_OK;
+    if (hipMemcpy(dw, w.data(), w.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(dv, v.data(), v.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+        rc = ESC_E_HIP;
+    for (const PatchTargets& t : targets)
+        if (!rc && launch_patch(t, dw, dv, (int64_t)w.size(), c->stream) != hipSuccess) rc = ESC_E_HIP;
+    if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = ESC_E_HIP;
+    dfree(dw);
+    dfree(dv);
+    return rc;
+}
+
+enum : uint32_t { PT_FLAGS = 0, PT_CPU0 = 1, PT_PAIR0 = 2, PT_XP = 3, PT_MEM0 = 6, PT_XC_CPU = 7, PT_XC_MEM = 8 };
+
+std::vector<PatchTargets> pod_targets(esc_ctx* c) {
+    std::vector<PatchTargets> v;
+    for (PodBuf& b : c->pods) {
+        PatchTargets t{};
+        t.u32[PT_FLAGS] = b.flags; t.u32[PT_CPU0] = b.cpu0; t.u32[PT_PAIR0] = b.pair0; t.u32[PT_XP] = b.xp;
+        t.i64[PT_MEM0 - 6] = b.mem0; t.i64[PT_XC_CPU - 6] = b.xc_cpu; t.i64[PT_XC_MEM - 6] = b.xc_mem;
+        v.push_back(t);
+    }
+    return v;
+}
+
+int sig_class_id(uint32_t f) {
+    const uint32_t xr = pf_xreg(f), xi = pf_xinit(f), ov = (f & ESC_PF_HAS_OVH) ? 1u : 0u, np = pf_xpair(f);
+    if (xr + xi + ov > 3 || np > 3) return -1;
+    return (int)(((xr * 4 + xi) * 2 + ov) * 4 + np);
+}
+
+// Removes pod `id` from the snapshot (its slot becomes padding: daemonset-flagged, which
+// every kernel skips; a C pod keeps its record counts so its tile's offsets stay valid).
+void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
+    const int32_t ci = c->pod_cls[id];
+    if (ci == -2) return;
+    if (ci == -1) {
+        const int64_t d = c->pod_pos[id];
+        uint32_t& f = c->h_cflags[d - c->k_tiles * TILE];
+        c->live_xc -= pf_xctr(f);
+        c->live_xp -= pf_xpair(f);
+        f |= ESC_PF_DAEMONSET;
+        P.add(PT_FLAGS, d, f);
+    } else {
+        const PodClass& k = c->h_cls[ci];
+        const int64_t q = c->pod_pos[id];
+        P.add(PT_FLAGS, (k.t0 + q / TILE) * TILE + q % TILE, ESC_PF_DAEMONSET);
+        c->cls_free[ci].push_back(q);
+        c->live_xc -= k.xreg + k.xinit + k.ovh;
+        c->live_xp -= k.nxp;
+    }
+    c->pod_cls[id] = -2;
+    --c->live_pods;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t esc_set_spare(esc_ctx* c, double fraction) {
+    if (!c || !(fraction >= 0.0) || fraction > 4.0) return ESC_E_INVAL;
+    c->spare_frac = fraction;                      // applies from the next esc_load_pods
+    return ESC_OK;
+}
+
+int32_t esc_pods_upsert(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
+    if (!c || !p || p->n_pods < 0 || (p->n_pods > 0 && (!ids || !p->flags || !p->cpu0 || !p->mem0 || !p->pair0)))
+        return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->pods_loaded) return ESC_E_STATE;
+    const int64_t n = p->n_pods;
+    // validate the batch and that every pod fits in place (all or nothing)
+    std::vector<int64_t> need(c->h_cls.size(), 0), rof(n), pof(n);
+    std::vector<int32_t> tgt(n);
+    uint64_t sc = 0, sp = 0;
+    std::vector<int64_t> seen(ids, ids + n);
+    std::sort(seen.begin(), seen.end());
+    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) return ESC_E_INVAL;   // one event per id
+    for (int64_t i = 0; i < n; ++i) {
+        if (ids[i] < 0 || ids[i] >= ((int64_t)1 << 31)) return ESC_E_INVAL;
+        const uint32_t f = p->flags[i], nx = pf_xpair(f), nc = pf_xctr(f);
+        uint32_t last = p->pair0[i];
+        if (last == NONE ? nx != 0 : last >= ESC_PAIR_LIMIT) return ESC_E_INVAL;
+        if (sp + nx > (uint64_t)p->n_xp || sc + nc > (uint64_t)p->n_xc) return ESC_E_INVAL;
+        for (uint32_t k = 0; k < nx; ++k) {
+            const uint32_t q = p->xp_pair[sp + k];
+            if (q >= ESC_PAIR_LIMIT || q <= last) return ESC_E_INVAL;
+            last = q;
+        }
+        rof[i] = (int64_t)sc;
+        pof[i] = (int64_t)sp;
+        sc += nc;
+        sp += nx;
+        const int sid = sig_class_id(f);
+        const int ci = sid < 0 ? -1 : c->h_cls_of[sid];
+        if (ci < 0) return ESC_E_LIMIT;            // C-section pod or a signature the layout has no class for
+        tgt[i] = ci;
+        const int64_t id = ids[i];
+        const bool in_place = id < (int64_t)c->pod_cls.size() && c->pod_cls[id] == ci;
+        if (!in_place) ++need[ci];
+    }
+    for (size_t ci = 0; ci < need.size(); ++ci)
+        if (need[ci] > (int64_t)c->cls_free[ci].size()) return ESC_E_LIMIT;   // spare exhausted: reload
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    Patches P;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t id = ids[i];
+        if (id >= (int64_t)c->pod_cls.size()) {
+            c->pod_cls.resize(id + 1, -2);
+            c->pod_pos.resize(id + 1, 0);
+        }
+        const int32_t ci = tgt[i];
+        if (c->pod_cls[id] != ci) {
+            remove_pod(c, id, P);
+            c->pod_cls[id] = ci;
+            c->pod_pos[id] = c->cls_free[ci].back();
+            c->cls_free[ci].pop_back();
+        } else {
+            --c->live_pods;                           // re-added below
+            const PodClass& k = c->h_cls[ci];
+            c->live_xc -= k.xreg + k.xinit + k.ovh;
+            c->live_xp -= k.nxp;
+        }
+        const PodClass& k = c->h_cls[ci];
+        const int64_t q = c->pod_pos[id], rt = q / TILE, sl = q % TILE;
+        const int64_t s64 = ((sl & 3) >> 1) * 128 + 2 * (sl >> 2) + (sl & 1);   // K1's pos64
+        const int64_t d = (k.t0 + rt) * TILE + sl, d64 = (k.t0 + rt) * TILE + s64;
+        const uint32_t f = p->flags[i], R = k.xreg + k.xinit + k.ovh;
+        P.add(PT_FLAGS, d, f);
+        P.add(PT_CPU0, d, p->cpu0[i]);
+        P.add(PT_PAIR0, d, p->pair0[i]);
+        P.add(PT_MEM0, d64, (uint64_t)p->mem0[i]);
+        for (uint32_t j = 0; j < R; ++j) {
+            const int64_t o = k.xc0 + (rt * R + j) * TILE + s64;
+            P.add(PT_XC_CPU, o, (uint64_t)p->xc_cpu[rof[i] + j]);
+            P.add(PT_XC_MEM, o, (uint64_t)p->xc_mem[rof[i] + j]);
+        }
+        for (uint32_t j = 0; j < k.nxp; ++j) P.add(PT_XP, k.xp0 + (rt * k.nxp + j) * TILE + sl, p->xp_pair[pof[i] + j]);
+        ++c->live_pods;
+        c->live_xc += R;
+        c->live_xp += k.nxp;
+    }
+    return apply_patches(c, P, pod_targets(c));
+}
+
+int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
+    if (!c || n < 0 || (n > 0 && !ids)) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->pods_loaded) return ESC_E_STATE;
+    for (int64_t i = 0; i < n; ++i)
+        if (ids[i] < 0 || ids[i] >= (int64_t)c->pod_cls.size()) return ESC_E_INVAL;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    Patches P;
+    for (int64_t i = 0; i < n; ++i) remove_pod(c, ids[i], P);
+    return apply_patches(c, P, pod_targets(c));
+}
+
+int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32_t* flags, const int64_t* cpu,
+                         const int64_t* mem) {
+    if (!c || n < 0 || (n > 0 && (!ids || !flags || !cpu || !mem))) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->nodes_loaded) return ESC_E_STATE;
+    const uint32_t mutable_bits = ESC_NF_UNSCHED | ESC_NF_TAINTED;
+    for (int64_t i = 0; i < n; ++i) {
+        if (ids[i] < 0 || ids[i] >= c->n_nodes) return ESC_E_INVAL;
+        if ((flags[i] ^ c->h_nflags[ids[i]]) & ~mutable_bits) return ESC_E_INVAL;   // labels / tracker: reload
+    }
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    enum : uint32_t { NT_FLAGS = 0, NT_EFLAGS = 1, NT_CPU = 6, NT_MEM = 7, NT_ECPU = 8, NT_EMEM = 9 };
+    Patches P;
+    bool first_changed = false;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t j = ids[i];
+        c->h_nflags[j] = flags[i];
+        c->h_ncpu[j] = cpu[i];
+        c->h_nmem[j] = mem[i];
+        P.add(NT_FLAGS, j, flags[i]);
+        P.add(NT_CPU, j, (uint64_t)cpu[i]);
+        P.add(NT_MEM, j, (uint64_t)mem[i]);
+        for (uint32_t e = c->ne_off[j]; e < c->ne_off[j + 1]; ++e) {
+            P.add(NT_EFLAGS, c->ne_pos[e], flags[i]);
+            P.add(NT_ECPU, c->ne_pos[e], (uint64_t)cpu[i]);
+            P.add(NT_EMEM, c->ne_pos[e], (uint64_t)mem[i]);
+        }
+    }
+    for (GroupNode& g : c->h_gnode)                  // allNodes[0]'s allocatable (controller.go:208)
+        if (g.first != INT64_MAX && (g.first_cpu != c->h_ncpu[g.first] || g.first_mem != c->h_nmem[g.first])) {
+            g.first_cpu = c->h_ncpu[g.first];
+            g.first_mem = c->h_nmem[g.first];
+            first_changed = true;
+        }
+    PatchTargets t{};
+    t.u32[NT_FLAGS] = c->nodes.flags; t.u32[NT_EFLAGS] = c->nodes.e_flags;
+    t.i64[NT_CPU - 6] = c->nodes.cpu; t.i64[NT_MEM - 6] = c->nodes.mem;
+    t.i64[NT_ECPU - 6] = c->nodes.e_cpu; t.i64[NT_EMEM - 6] = c->nodes.e_mem;
+    int32_t rc = apply_patches(c, P, {t});
+    if (rc) return rc;
+    if (first_changed)
+        HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
+    // the age index's membership list carries the node flags: re-list it (the order and
+    // the membership counts depend on creation times and labels only, both unchanged)
+    HIP_TRY(launch_memb_expand(node_dev(c), group_dev(c), c->d_age, c->memb_blocks, c->d_cnt, c->d_e_node,
+                               c->d_e_grp, c->d_e_flags, c->stream));
+    c->sorted = false;
     return ESC_OK;
 }
 

@@ -372,6 +372,23 @@ int32_t esc_force_wide(esc_ctx* ctx, int32_t enable);   /* testing: always take 
 int32_t esc_set_timing(esc_ctx* ctx, int32_t enable);
 int32_t esc_stage_times(esc_ctx* ctx, double* ms_out, int32_t n);
 
+/* ------------------------------------------- incremental snapshot (§8f rank 1)
+ * Informer-style events patch the resident snapshot in place instead of a reload
+ * (the reference re-lists every pod and node per group per decision through its
+ * informer caches, pkg/k8s/cache.go:16-56 -> pod_listers.go:33, node_listers.go:33).
+ * Pod ids are the indices of esc_load_pods' input; new ids (< 2^31) insert.  A pod
+ * lands in the spare slots of its record-signature class (esc_set_spare, before the
+ * load, reserves them); a batch that does not fit in place — spare exhausted, a pod
+ * with > 3 container records or > 3 extra pairs, or a signature absent at load —
+ * returns ESC_E_LIMIT with nothing applied, and the caller reloads.  Node events may
+ * change Spec.Unschedulable, the escalator taint and allocatable; label, creation-time
+ * or tracker changes need esc_load_nodes.  Every call completes before returning.    */
+int32_t esc_set_spare(esc_ctx* ctx, double fraction);       /* spare slots per K class, e.g. 0.05 */
+int32_t esc_pods_upsert(esc_ctx* ctx, const int64_t* ids, const esc_pod_soa* pods);
+int32_t esc_pods_delete(esc_ctx* ctx, const int64_t* ids, int64_t n);
+int32_t esc_nodes_update(esc_ctx* ctx, const int64_t* ids, int64_t n, const uint32_t* flags,
+                         const int64_t* cpu_m, const int64_t* mem_b);
+
 /* ----------------------------------------------------------------- ordering
  * K5: per-group creation-time order of the context's node shard (a18/a19):
  *   which 0: untainted members oldest-first (taintOldestN,   scale_down.go:171)

@@ -347,3 +347,97 @@ def test_node_index_split_within_pairs(esc, world):
         c.decide()
         tot, dec = c.results()
         check_against_c_oracle(tot, dec, otot, odf, odi)
+
+
+# ------------------------------------------------- incremental snapshot (§8f)
+def _packed_subset(P: dict, idx: list[int]) -> dict:
+    """The packed records of pods `idx` (in that order) out of a `pack` result."""
+    from escalator_amd.layout import NONE  # noqa: F401
+    f = P["flags"].astype(np.uint64)
+    nxc = ((f >> 8) & 0xFF) + ((f >> 16) & 0xFF) + ((f >> 4) & 1)
+    nxp = (f >> 24) & 0x3F
+    oc = np.concatenate([[0], np.cumsum(nxc)]).astype(np.int64)
+    op = np.concatenate([[0], np.cumsum(nxp)]).astype(np.int64)
+    out = {k: P[k][idx] for k in ("flags", "cpu0", "mem0", "pair0")}
+    out["xc_cpu"] = np.concatenate([P["xc_cpu"][oc[i]:oc[i + 1]] for i in idx] or [np.zeros(0, np.int64)])
+    out["xc_mem"] = np.concatenate([P["xc_mem"][oc[i]:oc[i + 1]] for i in idx] or [np.zeros(0, np.int64)])
+    out["xp_pair"] = np.concatenate([P["xp_pair"][op[i]:op[i + 1]] for i in idx] or [np.zeros(0, np.uint32)])
+    return out
+
+
+def _fits_k(P: dict, i: int) -> bool:
+    f = int(P["flags"][i])
+    return ((f >> 8) & 0xFF) + ((f >> 16) & 0xFF) + ((f >> 4) & 1) <= 3 and ((f >> 24) & 0x3F) <= 3
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_incremental_events_vs_literal(esc, seed):
+    """Pod upserts / deletes / inserts and node taint / cordon / allocatable events patch the
+    resident snapshot (esc_pods_upsert, esc_pods_delete, esc_nodes_update); every decision
+    and ordering then equals the literal oracle on the updated object lists."""
+    from escalator_amd._lib import ESC_E_LIMIT
+    rng = random.Random(7000 + seed)
+    G = rng.choice([3, 8])
+    groups = make_groups(rng, G, with_default=True)
+    pods = make_pods(rng, 400, groups, big_frac=0.0)
+    nodes = make_nodes(rng, 60, groups, big_frac=0.0)
+    states = make_states(rng, G)
+    ctx = esc.Context(groups)
+    ctx.set_spare(0.5)
+    P, N = ctx.pack(pods, nodes)
+    ctx.load(P, N)
+    live = {i: p for i, p in enumerate(pods)}
+    next_id = len(pods)
+    for rnd in range(3):
+        # pod events: deletes, in-place changes, inserts (only shapes the K layout holds)
+        ev_ids, ev_objs = [], []
+        for i in rng.sample(sorted(live), 30):
+            q = make_pods(rng, 1, groups, big_frac=0.0)[0]
+            ev_ids.append(i)
+            ev_objs.append(q)
+        for _ in range(20):
+            ev_ids.append(next_id)
+            ev_objs.append(make_pods(rng, 1, groups, big_frac=0.0)[0])
+            next_id += 1
+        Pe, _ = ctx.pack(ev_objs, [])
+        keep = [k for k in range(len(ev_ids)) if _fits_k(Pe, k)]
+        rc = ctx.pods_upsert([ev_ids[k] for k in keep], _packed_subset(Pe, keep))
+        assert rc == 0, rc
+        for k in keep:
+            live[ev_ids[k]] = ev_objs[k]
+        dels = rng.sample(sorted(live), 25)
+        ctx.pods_delete(dels)
+        for i in dels:
+            del live[i]
+        # node events: taint / cordon / allocatable
+        nid = rng.sample(range(len(nodes)), 12)
+        for j in nid:
+            nd = nodes[j]
+            nd["unschedulable"] = rng.random() < 0.3
+            nd["taints"] = ["atlassian.com/escalator"] if rng.random() < 0.4 else []
+            nd["cpu"] = rng.choice([0, 2000, 4000, 16000])
+            nd["mem"] = rng.choice([0, 8 << 30, 64 << 30])
+        _, Nn = ctx.pack([], nodes)
+        ctx.nodes_update(nid, Nn["flags"][nid], Nn["cpu"][nid], Nn["mem"][nid])
+        # decisions and orderings vs the literal oracle over the live objects
+        cur = [live[i] for i in sorted(live)]
+        tot, dec = ctx.decide_all(states)
+        ctx.sort_nodes()
+        for g in range(G):
+            L = O.scale_node_group(groups[g], states[g], cur, nodes)
+            t, d = tot[g], dec[g]
+            assert (t["n_pods"], t["n_nodes"], t["n_untainted"], t["n_tainted"], t["n_cordoned"]) == \
+                (L["n_pods"], L["n_nodes"], L["n_untainted"], L["n_tainted"], L["n_cordoned"]), (rnd, g)
+            assert (t["pod_cpu_m"], t["pod_mem_b"], t["node_cpu_m"], t["node_mem_b"]) == \
+                (L["pod_cpu_m"], L["pod_mem_b"], L["node_cpu_m"], L["node_mem_b"]), (rnd, g)
+            assert int(d["delta"]) == L["delta"] and _bits(d["cpu_pct"]) == _bits(L["cpu_pct"]), (rnd, g)
+            assert (int(d["cached_cpu_m"]), int(d["cached_mem_b"])) == (L["cached_cpu_m"], L["cached_mem_b"])
+            unt = L["untainted"]
+            assert list(ctx.group_order(g, 0)) == [unt[i] for i in O.oldest_first([nodes[i]["created_ns"] for i in unt])]
+    # more inserts than the spare holds: refused whole, nothing applied
+    many = make_pods(rng, 2000, groups, big_frac=0.0)
+    Pm, _ = ctx.pack(many, [])
+    keep = [k for k in range(len(many)) if _fits_k(Pm, k)]
+    before = ctx.decide_all(states)[0].tobytes()
+    assert ctx.pods_upsert([next_id + k for k in range(len(keep))], _packed_subset(Pm, keep)) == ESC_E_LIMIT
+    assert ctx.decide_all(states)[0].tobytes() == before
