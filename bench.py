@@ -126,10 +126,9 @@ def bench_order(args):
     parity = all(np.array_equal(ctx.group_order(g, w), soa.order(nodes, s.groups, g, w)) for g in (0, 37, 99)
                  for w in (0, 1))
     n_memb, R = ctx.order_info()
-    # bytes the ordering moves per membership: classify 12 read + 8 written; each 8-bit LSD
-    # pass over the (group << 2 | class) keys: 4 (histogram) + 8 read + 8 written
-    passes = -(-max(1, int(np.ceil(np.log2(4 * G)))) // 8)
-    order_bytes = n_memb * (20 + passes * 20)
+    # bytes the ordering moves per membership: classify (node, group, flags) 12 read + class
+    # 1 written; split: class 1 + node 4 read, node 4 written (esc_kernels.hip K5)
+    order_bytes = n_memb * 22
     idx_passes = -(-R // 8)
     index_bytes = N * (16 + idx_passes * 32)       # keys 8 + vals 4 per pass (hist 8 + r/w 24), + entries
     out = {
@@ -145,7 +144,7 @@ def bench_order(args):
         "data": "synthetic (esc_synth.cpp config 5: 10M nodes, 100 groups, unique ns creation times)",
         "config": {"workload": "config5: 10M nodes oldest-first / newest-first orderings, 100 node groups",
                    "nodes": N, "node_groups": G, "memberships": n_memb},
-        "roofline": {"bound": "hbm", "kernel": "per-decision ordering (classify + %d partition pass(es))" % passes,
+        "roofline": {"bound": "hbm", "kernel": "per-decision ordering (k_ord_count + k_ord_bases + k_ord_scatter)",
                      "achieved": order_bytes / (order_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": order_bytes / (order_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_decision": order_bytes},
         "age_index_build": {"ms": index_ms, "nodes_per_s": N / (index_ms * 1e-3), "key_bits": R,

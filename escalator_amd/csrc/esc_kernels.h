@@ -151,14 +151,27 @@ hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* wor
 // Ordering (K5), see esc_kernels.hip: the age index (once per snapshot) and the per-decision
 // (group, class) partition.
 size_t sort_hist_words(int64_t n);   // digit-histogram words one LSD pass over n keys needs
+struct OrdChunk {               // K5 per-decision chunk: memberships [start, end) of one group
+    uint32_t start, end, group, pad;
+};
+constexpr int ORD_CHUNK = 4096;
 hipError_t launch_age_index(const NodeDev& n, int64_t ts_min, uint64_t div, int R, uint64_t* keys64[2],
                             uint32_t* vals[2], uint32_t* hist, uint32_t* tot, uint32_t** age_out, hipStream_t st);
 hipError_t launch_memb_count(const NodeDev& n, const GroupDev& g, const uint32_t* age, int nblk, uint32_t* cnt,
                              uint32_t* total, hipStream_t st);
 hipError_t launch_memb_expand(const NodeDev& n, const GroupDev& g, const uint32_t* age, int nblk, const uint32_t* base,
                               uint32_t* e_node, uint32_t* e_grp, uint32_t* e_flags, hipStream_t st);
-hipError_t launch_order(const NodeDev& n, const uint32_t* e_node, const uint32_t* e_grp, const uint32_t* e_flags,
-                        int64_t n_e, int seg_bits, uint32_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t* tot,
-                        int32_t nseg, int64_t* seg, int* src, hipStream_t st);
+hipError_t launch_group_order(const uint32_t* e_grp, int64_t n_e, int32_t G, uint32_t* keys[2], uint32_t* vals[2],
+                              uint32_t* hist, uint32_t* tot, int64_t* starts, uint32_t** perm, uint32_t** gkeys,
+                              hipStream_t st);
+hipError_t launch_group_pos(const uint32_t* gkeys, int64_t n_e, const int64_t* starts, const uint32_t* pstart,
+                            uint32_t* gpos, hipStream_t st);
+hipError_t launch_group_gather(const uint32_t* perm, const uint32_t* gpos, int64_t n_e, const uint32_t* e_node,
+                               const uint32_t* e_grp, const uint32_t* e_flags, uint32_t* g_node, uint32_t* g_grp,
+                               uint32_t* g_flags, hipStream_t st);
+hipError_t launch_order(const NodeDev& n, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
+                        const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp, const uint32_t* g_flags,
+                        int64_t n_e, int32_t G, uint32_t* cls4, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,
+                        int64_t* seg, hipStream_t st);
 
 }  // namespace esc

@@ -1239,19 +1239,188 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_memb_expand(NodeDev N, GroupDev 
     }
 }
 
-// ---- per decision
-// filterNodes class of every membership (controller.go:125-150; dry groups: tracker only)
-// -> segment key (group << 2 | class), value node, in age order.
-__global__ __launch_bounds__(256) void k_memb_classify(NodeDev N, const uint32_t* __restrict__ e_node,
-                                                       const uint32_t* __restrict__ e_grp,
-                                                       const uint32_t* __restrict__ e_flags, int64_t n,
-                                                       uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+// ---- group order (load time): the age-ordered memberships stable-sorted by group, so
+// that every group's memberships are one contiguous run, oldest first.
+__global__ __launch_bounds__(256) void k_grp_keys(const uint32_t* __restrict__ e_grp, int64_t n,
+                                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
-    const uint32_t i = e_node[e], m = e_grp[e];
-    const int cls = node_class(N, e_flags[e], (int64_t)i, m);
-    keys[e] = (mg(m) << 2) | (uint32_t)cls;
-    vals[e] = i;
+    keys[e] = mg(e_grp[e]);
+    vals[e] = (uint32_t)e;
+}
+
+// Padded position of the e-th membership in group order: every group's run starts on a
+// multiple of 4 so that the per-decision split reads 16-B quads (padding: group NONE).
+__global__ __launch_bounds__(256) void k_grp_pos(const uint32_t* __restrict__ gkeys, int64_t n,
+                                                 const int64_t* __restrict__ starts, const uint32_t* __restrict__ pstart,
+                                                 uint32_t* __restrict__ gpos) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t g = gkeys[e];
+    gpos[e] = pstart[g] + (uint32_t)(e - starts[g]);
+}
+
+// Gathers the membership copies into (padded) group order (also after node events).
+__global__ __launch_bounds__(256) void k_grp_gather(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ gpos,
+                                                    int64_t n, const uint32_t* __restrict__ e_node,
+                                                    const uint32_t* __restrict__ e_grp,
+                                                    const uint32_t* __restrict__ e_flags, uint32_t* __restrict__ g_node,
+                                                    uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_flags) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const uint32_t k = perm[e], d = gpos[e];
+    g_node[d] = e_node[k];
+    g_grp[d] = e_grp[k];
+    g_flags[d] = e_flags[k];
+}
+
+// ---- per decision: inside every group's run, a stable 3-way split by filterNodes class
+// (controller.go:125-150; dry groups: tracker only).  Chunks never cross a group, so a
+// chunk's nodes go to three contiguous output streams; three passes:
+//   A  classify (12 B read, 1 B written) + per-chunk class counts,
+//   B  per group: chunk bases and the (group, class) segment bounds,
+//   C  per chunk: ballot ranks + wave prefix -> vals (5 B read, 4 B written, coalesced).
+constexpr int ORD_BLOCK = 256, ORD_WAVES = ORD_BLOCK / 64;
+
+__device__ __forceinline__ uint32_t ord_class(const NodeDev& N, uint32_t node, uint32_t grp, uint32_t f) {
+    return grp == NONE ? 3u : (uint32_t)node_class(N, f, (int64_t)node, grp);   // NONE: padding
+}
+
+// A: classes of the chunk's memberships (one u32 of 4 class bytes per quad) and the
+// chunk's count per class.  Quads: 16-B loads of node / group / flags per lane.
+__global__ __launch_bounds__(ORD_BLOCK) void k_ord_count(NodeDev N, const OrdChunk* __restrict__ chunks,
+                                                         const uint32_t* __restrict__ g_node,
+                                                         const uint32_t* __restrict__ g_grp,
+                                                         const uint32_t* __restrict__ g_flags,
+                                                         uint32_t* __restrict__ cls4, uint32_t* __restrict__ ccnt) {
+    __shared__ uint32_t red[ORD_WAVES][3];
+    const OrdChunk ch = chunks[blockIdx.x];
+    uint32_t c[3] = {0, 0, 0};
+    constexpr uint32_t STEP = 4 * ORD_BLOCK;
+    for (uint32_t b0 = ch.start + 4 * threadIdx.x; b0 < ch.end; b0 += 2 * STEP) {
+        uint4 nd[2], gr[2], fl[2];                      // two quads' loads in flight
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t b = b0 + h * STEP < ch.end ? b0 + h * STEP : b0;
+            nd[h] = ld4(g_node + b);
+            gr[h] = ld4(g_grp + b);
+            fl[h] = ld4(g_flags + b);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t b = b0 + h * STEP;
+            if (b >= ch.end) break;
+            uint32_t packed = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = b + j < ch.end ? ord_class(N, lane4(nd[h], j), lane4(gr[h], j), lane4(fl[h], j)) : 3u;
+                packed |= k << (8 * j);
+                c[0] += k == 0;
+                c[1] += k == 1;
+                c[2] += k == 2;
+            }
+            cls4[b >> 2] = packed;
+        }
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) c[k] += __shfl_xor(c[k], o, 64);
+    if (lane == 0) for (int k = 0; k < 3; ++k) red[wid][k] = c[k];
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        uint32_t t = 0;
+        for (int w = 0; w < ORD_WAVES; ++w) t += red[w][threadIdx.x];
+        ccnt[(int64_t)blockIdx.x * 3 + threadIdx.x] = t;
+    }
+}
+
+// B: one wave per group — class totals over the group's chunks, the (group, class)
+// segment bounds (seg[4g + class]), and every chunk's output base per class.
+__global__ __launch_bounds__(64) void k_ord_bases(const uint32_t* __restrict__ grp_off,
+                                                  const uint32_t* __restrict__ gch_off,
+                                                  const uint32_t* __restrict__ ccnt, int32_t G, int64_t n,
+                                                  uint32_t* __restrict__ cbase, int64_t* __restrict__ seg) {
+    const int32_t g = blockIdx.x;
+    const int lane = threadIdx.x;
+    if (g == G) { if (lane == 0) seg[4 * (int64_t)G] = n; return; }
+    const uint32_t q0 = gch_off[g], q1 = gch_off[g + 1];
+    uint32_t t[3] = {0, 0, 0};
+    for (uint32_t q = q0 + lane; q < q1; q += 64)
+        for (int k = 0; k < 3; ++k) t[k] += ccnt[(int64_t)q * 3 + k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) t[k] += __shfl_xor(t[k], o, 64);
+    uint32_t b[3];
+    b[0] = grp_off[g];
+    b[1] = b[0] + t[0];
+    b[2] = b[1] + t[1];
+    if (lane < 4) seg[4 * (int64_t)g + lane] = lane == 3 ? b[2] + t[2] : b[lane];
+    for (uint32_t q = q0; q < q1; q += 64) {          // chunk bases: exclusive wave scan per class
+        const uint32_t qq = q + lane;
+        uint32_t v[3];
+        for (int k = 0; k < 3; ++k) v[k] = qq < q1 ? ccnt[(int64_t)qq * 3 + k] : 0;
+        for (int k = 0; k < 3; ++k) {
+            uint32_t x = v[k];
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(x, o, 64);
+                if (lane >= o) x += y;
+            }
+            if (qq < q1) cbase[(int64_t)qq * 3 + k] = b[k] + x - v[k];
+            b[k] += __shfl(x, 63, 64);
+        }
+    }
+}
+
+// C: every chunk's nodes into its three class streams, stable: per lane 4 consecutive
+// memberships, per-class ranks from one packed DPP wave scan, wave offsets via LDS.
+__global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __restrict__ chunks,
+                                                           const uint32_t* __restrict__ cls4,
+                                                           const uint32_t* __restrict__ g_node,
+                                                           const uint32_t* __restrict__ cbase,
+                                                           uint32_t* __restrict__ vals) {
+    __shared__ uint32_t wt[ORD_WAVES];
+    __shared__ uint32_t rb[3];
+    const OrdChunk ch = chunks[blockIdx.x];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x < 3) rb[threadIdx.x] = cbase[(int64_t)blockIdx.x * 3 + threadIdx.x];
+    __syncthreads();
+    const uint32_t iters = (ch.end - ch.start + 4 * ORD_BLOCK - 1) / (4 * ORD_BLOCK);
+    for (uint32_t it = 0; it < iters; ++it) {
+        const uint32_t b = ch.start + it * 4 * ORD_BLOCK + 4 * threadIdx.x;
+        const bool ok = b < ch.end;
+        const uint32_t packed = ok ? cls4[b >> 2] : 0x03030303u;
+        const uint4 nd = ok ? ld4(g_node + b) : make_uint4(0, 0, 0, 0);
+        uint32_t v = 0;                                  // per-class counts, 10 bits each
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = (packed >> (8 * j)) & 0xFF;
+            if (k < 3) v += 1u << (10 * k);
+        }
+        const uint32_t inc = wave_incl_scan32(v);
+        if (lane == 63) wt[wid] = inc;
+        __syncthreads();
+        uint32_t pre = rb[0] | 0, p1 = rb[1], p2 = rb[2];
+        uint32_t wp = 0;
+        for (int w = 0; w < wid; ++w) wp += wt[w];
+        uint32_t ex = inc - v + wp;                       // my first slot per class, in this block step
+        uint32_t off[3] = {pre + (ex & 0x3FF), p1 + ((ex >> 10) & 0x3FF), p2 + (ex >> 20)};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = (packed >> (8 * j)) & 0xFF;
+            if (k < 3) vals[off[k]++] = lane4(nd, j);
+        }
+        __syncthreads();
+        if (threadIdx.x < 3) {
+            uint32_t t = 0;
+            for (int w = 0; w < ORD_WAVES; ++w) t += (wt[w] >> (10 * threadIdx.x)) & 0x3FF;
+            rb[threadIdx.x] += t;
+        }
+        __syncthreads();
+    }
 }
 
 // Start of each (group, class) segment in the partitioned keys: seg[s] = first key >= s.
@@ -1425,17 +1594,52 @@ hipError_t launch_memb_expand(const NodeDev& nd, const GroupDev& g, const uint32
     return hipGetLastError();
 }
 
-hipError_t launch_order(const NodeDev& nd, const uint32_t* e_node, const uint32_t* e_grp, const uint32_t* e_flags,
-                        int64_t n_e, int seg_bits, uint32_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t* tot,
-                        int32_t nseg, int64_t* seg, int* src, hipStream_t st) {
-    *src = 0;
-    if (n_e > 0) {
-        hipLaunchKernelGGL(k_memb_classify, dim3((unsigned)((n_e + 255) / 256)), dim3(256), 0, st, nd, e_node, e_grp,
-                           e_flags, n_e, keys[0], vals[0]);
-        hipError_t e = rs_sort<uint32_t>(keys, vals, n_e, seg_bits, hist, tot, src, st);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(k_seg_bounds, dim3((nseg + 1 + 255) / 256), dim3(256), 0, st, keys[*src], n_e, nseg, seg);
+hipError_t launch_group_order(const uint32_t* e_grp, int64_t n_e, int32_t G, uint32_t* keys[2], uint32_t* vals[2],
+                              uint32_t* hist, uint32_t* tot, int64_t* starts, uint32_t** perm, uint32_t** gkeys,
+                              hipStream_t st) {
+    *perm = vals[0];
+    *gkeys = keys[0];
+    if (n_e <= 0) return hipSuccess;
+    const unsigned nb = (unsigned)((n_e + 255) / 256);
+    hipLaunchKernelGGL(k_grp_keys, dim3(nb), dim3(256), 0, st, e_grp, n_e, keys[0], vals[0]);
+    int src = 0;
+    hipError_t e = rs_sort<uint32_t>(keys, vals, n_e, std::max(1, 32 - __builtin_clz((unsigned)std::max(1, G - 1))),
+                                     hist, tot, &src, st);
+    if (e != hipSuccess) return e;
+    *perm = vals[src];
+    *gkeys = keys[src];
+    hipLaunchKernelGGL(k_seg_bounds, dim3((G + 1 + 255) / 256), dim3(256), 0, st, keys[src], n_e, G, starts);
+    return hipGetLastError();
+}
+
+hipError_t launch_group_pos(const uint32_t* gkeys, int64_t n_e, const int64_t* starts, const uint32_t* pstart,
+                            uint32_t* gpos, hipStream_t st) {
+    if (n_e <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_grp_pos, dim3((unsigned)((n_e + 255) / 256)), dim3(256), 0, st, gkeys, n_e, starts, pstart,
+                       gpos);
+    return hipGetLastError();
+}
+
+hipError_t launch_group_gather(const uint32_t* perm, const uint32_t* gpos, int64_t n_e, const uint32_t* e_node,
+                               const uint32_t* e_grp, const uint32_t* e_flags, uint32_t* g_node, uint32_t* g_grp,
+                               uint32_t* g_flags, hipStream_t st) {
+    if (n_e <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_grp_gather, dim3((unsigned)((n_e + 255) / 256)), dim3(256), 0, st, perm, gpos, n_e, e_node,
+                       e_grp, e_flags, g_node, g_grp, g_flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_order(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
+                        const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp, const uint32_t* g_flags,
+                        int64_t n_e, int32_t G, uint32_t* cls4, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,
+                        int64_t* seg, hipStream_t st) {
+    if (n_chunks > 0)
+        hipLaunchKernelGGL(k_ord_count, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, g_node, g_grp,
+                           g_flags, cls4, ccnt);
+    hipLaunchKernelGGL(k_ord_bases, dim3(G + 1), dim3(64), 0, st, grp_off, gch_off, ccnt, G, n_e, cbase, seg);
+    if (n_chunks > 0)
+        hipLaunchKernelGGL(k_ord_scatter, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, chunks, cls4, g_node, cbase,
+                           vals);
     return hipGetLastError();
 }
 

@@ -157,6 +157,13 @@ struct esc_ctx {
     int64_t* d_seg = nullptr;
     int64_t n_memb = 0;
     int order_src = 0, memb_blocks = 0;
+    // group order of the memberships (per-decision 3-way split by class inside each group)
+    uint32_t *d_gperm = nullptr, *d_g_node = nullptr, *d_g_grp = nullptr, *d_g_flags = nullptr;
+    uint32_t *d_grp_off = nullptr, *d_gch_off = nullptr, *d_ccnt = nullptr, *d_cbase = nullptr;
+    uint32_t *d_gpos = nullptr, *d_pstart = nullptr, *d_cls4 = nullptr;
+    int64_t n_gpad = 0;                                       // padded group-order length
+    OrdChunk* d_chunks = nullptr;
+    int64_t n_chunks = 0;
     uint64_t sort_div = 1;
     int sort_R = 1;
     bool sorted = false;
@@ -263,6 +270,11 @@ void release_sort(esc_ctx* c) {
         dfree(c->d_age_keys[i]); dfree(c->d_age_vals[i]); dfree(c->d_okeys[i]); dfree(c->d_ovals[i]);
     }
     dfree(c->d_e_node); dfree(c->d_e_grp); dfree(c->d_e_flags);
+    dfree(c->d_gperm); dfree(c->d_g_node); dfree(c->d_g_grp); dfree(c->d_g_flags);
+    dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks);
+    dfree(c->d_gpos); dfree(c->d_pstart); dfree(c->d_cls4);
+    c->n_chunks = 0;
+    c->n_gpad = 0;
     dfree(c->d_hist); dfree(c->d_tot); dfree(c->d_cnt); dfree(c->d_total); dfree(c->d_seg);
     c->d_age = nullptr;
     c->n_memb = 0;
@@ -307,12 +319,63 @@ int32_t build_age_index(esc_ctx* c) {
         c->n_memb = total;
         HIP_TRY(dalloc(&c->d_e_node, total)); HIP_TRY(dalloc(&c->d_e_grp, total)); HIP_TRY(dalloc(&c->d_e_flags, total));
         for (int i = 0; i < 2; ++i) { HIP_TRY(dalloc(&c->d_okeys[i], total)); HIP_TRY(dalloc(&c->d_ovals[i], total)); }
-        if (sort_hist_words(total) > std::max(sort_hist_words(nl), sort_hist_words(1) * 4)) {
+        if (sort_hist_words(total) > std::max(sort_hist_words(nl), sort_hist_words(1) * 4) * 4) {
             dfree(c->d_hist);
             HIP_TRY(dalloc(&c->d_hist, sort_hist_words(total)));
         }
+        HIP_TRY(dalloc(&c->d_gperm, total)); HIP_TRY(dalloc(&c->d_gpos, total));
     }
     HIP_TRY(launch_memb_expand(n, g, c->d_age, c->memb_blocks, c->d_cnt, c->d_e_node, c->d_e_grp, c->d_e_flags, st));
+    // group order: each group's memberships one run, oldest first, starting on a multiple of
+    // 4 (16-B quads); chunks of <= ORD_CHUNK memberships inside a run drive the split
+    uint32_t *perm = nullptr, *gkeys = nullptr;
+    HIP_TRY(launch_group_order(c->d_e_grp, c->n_memb, g.G, c->d_okeys, c->d_ovals, c->d_hist, c->d_tot, c->d_seg,
+                               &perm, &gkeys, st));
+    if (c->n_memb) HIP_TRY(hipMemcpyAsync(c->d_gperm, perm, c->n_memb * 4, hipMemcpyDeviceToDevice, st));
+    std::vector<int64_t> starts((size_t)g.G + 1, 0);
+    if (c->n_memb) HIP_TRY(hipMemcpyAsync(starts.data(), c->d_seg, starts.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    starts[g.G] = c->n_memb;
+    std::vector<uint32_t> grp_off(g.G + 1), gch_off(g.G + 1), pstart(g.G + 1, 0);
+    std::vector<OrdChunk> chunks;
+    for (int32_t q = 0; q < g.G; ++q) {
+        const int64_t len = starts[q + 1] - starts[q];
+        pstart[q + 1] = pstart[q] + (uint32_t)((len + 3) & ~(int64_t)3);
+        grp_off[q] = (uint32_t)starts[q];
+        gch_off[q] = (uint32_t)chunks.size();
+        for (int64_t a = 0; a < len; a += ORD_CHUNK)
+            chunks.push_back({pstart[q] + (uint32_t)a, pstart[q] + (uint32_t)std::min<int64_t>(len, a + ORD_CHUNK),
+                              (uint32_t)q, 0u});
+    }
+    grp_off[g.G] = (uint32_t)c->n_memb;
+    gch_off[g.G] = (uint32_t)chunks.size();
+    const int64_t npad = pstart[g.G];
+    if (npad >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
+    if (fresh || npad != c->n_gpad) {
+        dfree(c->d_g_node); dfree(c->d_g_grp); dfree(c->d_g_flags); dfree(c->d_cls4);
+        HIP_TRY(dalloc(&c->d_g_node, npad)); HIP_TRY(dalloc(&c->d_g_grp, npad)); HIP_TRY(dalloc(&c->d_g_flags, npad));
+        HIP_TRY(dalloc(&c->d_cls4, (npad + 3) / 4));
+    }
+    c->n_gpad = npad;
+    if (npad) {
+        HIP_TRY(hipMemsetAsync(c->d_g_node, 0, npad * 4, st));
+        HIP_TRY(hipMemsetAsync(c->d_g_grp, 0xFF, npad * 4, st));     // padding: group NONE
+        HIP_TRY(hipMemsetAsync(c->d_g_flags, 0, npad * 4, st));
+    }
+    if (fresh || (int64_t)chunks.size() != c->n_chunks) {
+        dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks); dfree(c->d_pstart);
+        HIP_TRY(dalloc(&c->d_grp_off, grp_off.size())); HIP_TRY(dalloc(&c->d_gch_off, gch_off.size()));
+        HIP_TRY(dalloc(&c->d_ccnt, chunks.size() * 3)); HIP_TRY(dalloc(&c->d_cbase, chunks.size() * 3));
+        HIP_TRY(dalloc(&c->d_chunks, chunks.size())); HIP_TRY(dalloc(&c->d_pstart, pstart.size()));
+    }
+    c->n_chunks = (int64_t)chunks.size();
+    HIP_TRY(hipMemcpy(c->d_grp_off, grp_off.data(), grp_off.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_gch_off, gch_off.data(), gch_off.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_pstart, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice));
+    if (!chunks.empty()) HIP_TRY(hipMemcpy(c->d_chunks, chunks.data(), chunks.size() * sizeof(OrdChunk), hipMemcpyHostToDevice));
+    HIP_TRY(launch_group_pos(gkeys, c->n_memb, c->d_seg, c->d_pstart, c->d_gpos, st));
+    HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
+                                c->d_g_grp, c->d_g_flags, st));
     c->sorted = false;
     return ESC_OK;
 }
@@ -1412,6 +1475,8 @@ int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32
     // the membership counts depend on creation times and labels only, both unchanged)
     HIP_TRY(launch_memb_expand(node_dev(c), group_dev(c), c->d_age, c->memb_blocks, c->d_cnt, c->d_e_node,
                                c->d_e_grp, c->d_e_flags, c->stream));
+    HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
+                                c->d_g_grp, c->d_g_flags, c->stream));
     c->sorted = false;
     return ESC_OK;
 }
@@ -1422,10 +1487,10 @@ int32_t esc_sort_nodes(esc_ctx* c) {
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->nodes_loaded) return ESC_E_STATE;
     hipSetDevice(c->device);
-    const int G = c->gi.G;
-    const int seg_bits = std::max(1, bit_width((uint64_t)(4 * G - 1)));
-    HIP_TRY(launch_order(node_dev(c), c->d_e_node, c->d_e_grp, c->d_e_flags, c->n_memb, seg_bits, c->d_okeys,
-                         c->d_ovals, c->d_hist, c->d_tot, 4 * G, c->d_seg, &c->order_src, c->stream));
+    HIP_TRY(launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node, c->d_g_grp,
+                         c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase, c->d_ovals[0], c->d_seg,
+                         c->stream));
+    c->order_src = 0;
     c->sorted = true;
     return ESC_OK;
 }
