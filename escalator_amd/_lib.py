@@ -63,6 +63,10 @@ class GroupMetrics(C.Structure):
 METRIC_NAMES = [n for n, _ in GroupMetrics._fields_[:11]]
 
 
+class Removal(C.Structure):
+    _fields_ = [("n_candidates", i64), ("n_delete", i64), ("pods_remaining", i64), ("reserved", i64)]
+
+
 class KV(C.Structure):
     _fields_ = [("key", cstr), ("value", cstr)]
 
@@ -145,6 +149,9 @@ _SIGS = {
     "esc_pods_upsert": (i32, [VP, P(i64), P(PodSoA)]),
     "esc_pods_delete": (i32, [VP, P(i64), i64]),
     "esc_nodes_update": (i32, [VP, P(i64), i64, P(u32), P(i64), P(i64)]),
+    "esc_load_placement": (i32, [VP, P(u32), P(i64), P(C.c_uint8)]),
+    "esc_try_remove": (i32, [VP, i64, P(i64), P(i64), P(Removal)]),
+    "esc_removal_nodes": (i32, [VP, i32, P(i64), i64, P(i64)]),
     "esc_set_metrics": (i32, [VP, i32]),
     "esc_metrics_results": (i32, [VP, P(GroupMetrics)]),
     "esc_use_graph": (i32, [VP, i32]),

@@ -17,6 +17,7 @@ from .objects import groups_from_c, groups_to_c, nodes_to_c, pods_to_c, states_t
 
 TOTALS_DTYPE = np.dtype([(n, np.int64) for n, _ in L.GroupTotals._fields_])
 METRICS_DTYPE = np.dtype([(n, np.float64) for n in L.METRIC_NAMES] + [("set_mask", np.uint32), ("reserved", np.uint32)])
+REMOVAL_DTYPE = np.dtype([(n, np.int64) for n, _ in L.Removal._fields_])
 DECISION_DTYPE = np.dtype({"names": [n for n, _ in L.GroupDecision._fields_],
                            "formats": [np.float64, np.float64, np.int64, np.int64, np.int64, np.int64,
                                        np.int32, np.int32, np.int32, np.int32]})
@@ -283,6 +284,39 @@ class Context:
         self.set_state(states)
         self.run()
         return self.results()
+
+    # ------------------------------------------------ scale-down reaping (§8f rank 2)
+    def load_placement(self, pod_node, taint_s, no_delete):
+        """Bind the loaded pods to nodes (node index per pod id, NONE = none) and load each
+        node's escalator-taint time (Unix s, INT64_MIN = none) and no-delete flag
+        (objects.placement builds them).  pod_node=None refreshes the node facts only."""
+        t = np.ascontiguousarray(taint_s, np.int64)
+        nd = np.ascontiguousarray(no_delete, np.uint8)
+        pn = None if pod_node is None else np.ascontiguousarray(pod_node, np.uint32)
+        L.check(self.lib.esc_load_placement(self.handle, None if pn is None else pn.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                            t.ctypes.data_as(C.POINTER(C.c_int64)),
+                                            nd.ctypes.data_as(C.POINTER(C.c_uint8))), "esc_load_placement")
+
+    def try_remove(self, now_ns: int, soft_ns, hard_ns) -> np.ndarray:
+        """TryRemoveTaintedNodes for every group: (n_candidates, n_delete, pods_remaining)."""
+        s_ = np.ascontiguousarray(np.broadcast_to(np.asarray(soft_ns, np.int64), (self.G,)))
+        h_ = np.ascontiguousarray(np.broadcast_to(np.asarray(hard_ns, np.int64), (self.G,)))
+        out = np.zeros(self.G, REMOVAL_DTYPE)
+        L.check(self.lib.esc_try_remove(self.handle, int(now_ns), s_.ctypes.data_as(C.POINTER(C.c_int64)),
+                                        h_.ctypes.data_as(C.POINTER(C.c_int64)),
+                                        out.ctypes.data_as(C.POINTER(L.Removal))), "esc_try_remove")
+        return out
+
+    def removal_nodes(self, group: int) -> np.ndarray:
+        """Snapshot indices of the nodes the last try_remove deletes for `group`, in order."""
+        n = C.c_int64()
+        rc = self.lib.esc_removal_nodes(self.handle, group, None, 0, C.byref(n))
+        if rc not in (0, L.ESC_E_LIMIT):
+            L.check(rc, "esc_removal_nodes")
+        out = np.zeros(max(n.value, 1), np.int64)
+        L.check(self.lib.esc_removal_nodes(self.handle, group, out.ctypes.data_as(C.POINTER(C.c_int64)), len(out),
+                                           C.byref(n)), "esc_removal_nodes")
+        return out[:n.value]
 
     # ------------------------------------------------------------- ordering
     def sort_nodes(self):

@@ -140,6 +140,31 @@ hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* f
                           const int64_t* node_rows, int64_t* wide_pod, uint32_t* wp_cnt, int64_t* trk_acc,
                           int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
+// §8f rank 2: a loaded pod as seen by NodePodsRemaining, listed per node (runs in
+// node order).  p[0..2]: the pod's extra pairs (NONE-padded); a C pod with more than 3
+// has POD_REF_INDIRECT in flags and p[0] = offset, p[1] = count into xp.
+struct PodRef {
+    uint32_t flags, pair0, p[3];
+};
+constexpr uint32_t POD_REF_INDIRECT = 1u << 31;
+struct RemovalDev {
+    const int64_t* taint_s;    // [n_nodes] escalator-taint time (INT64_MIN: none / unparsable)
+    const uint8_t* no_delete;  // [n_nodes]
+    const uint32_t* nrun_off;  // [n_nodes + 1] runs of PodRef per node
+    const PodRef* refs;
+    const uint32_t* xp;        // C-pod extra pairs (indirect refs)
+    uint32_t* occ_pair;        // [entries] group pods on the node, by the entry's pair
+    uint32_t* occ_def;         // [entries] default-filter pods on the node
+    const int64_t* soft_ns;    // [G]
+    const int64_t* hard_ns;    // [G]
+    const uint32_t* rm_off;    // [G] offset of each group's deletable-node list
+    uint32_t* rm_list;
+    esc_removal* out;          // [G]
+    int64_t now_ns;
+};
+hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, int64_t n, PodRef* refs, hipStream_t st);
+hipError_t launch_try_remove(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st);
+
 struct PatchTargets {          // k_patch destinations: 4-byte arrays 0-5, 8-byte arrays 6-11
     uint32_t* u32[6];
     int64_t* i64[6];

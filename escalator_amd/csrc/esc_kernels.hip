@@ -1451,6 +1451,134 @@ __global__ __launch_bounds__(256) void k_patch(PatchTargets T, const uint64_t* _
     else T.i64[t - 6][idx] = (int64_t)what[i];
 }
 
+// ===================================================================== scale-down reaping
+// §8f rank 2: TryRemoveTaintedNodes (scale_down.go:51-136) for every group.
+namespace {
+// The pod behind device slot d, as a PodRef (pairs inline, or indirect for big C pods).
+__device__ PodRef podref_of(const PodDev& P, uint32_t d) {
+    PodRef r;
+    r.flags = P.flags[d];
+    r.pair0 = P.pair0[d];
+    r.p[0] = r.p[1] = r.p[2] = NONE;
+    const int64_t kpods = P.k_tiles * TILE;
+    if ((int64_t)d < kpods) {
+        const int64_t t = d / TILE, sl = d % TILE;
+        int lo = 0, hi = P.n_cls - 1;                      // class of tile t
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (P.cls[mid].t0 <= t) lo = mid; else hi = mid - 1;
+        }
+        const PodClass& C = P.cls[lo];
+        const int64_t rt = t - C.t0;
+        for (uint32_t k = 0; k < C.nxp && k < 3; ++k) r.p[k] = P.xp[C.xp0 + (rt * C.nxp + k) * TILE + sl];
+    } else {
+        const int64_t c = (int64_t)d - kpods, t = c / CTILE, l = c % CTILE;
+        uint32_t off = P.xp_base[t];
+        for (int64_t k = 0; k < l; ++k) off += pf_xpair(P.flags[kpods + t * CTILE + k]);
+        const uint32_t nx = pf_xpair(r.flags);
+        if (nx <= 3) {
+            for (uint32_t k = 0; k < nx; ++k) r.p[k] = P.xp[off + k];
+        } else {
+            r.flags |= POD_REF_INDIRECT;
+            r.p[0] = off;
+            r.p[1] = nx;
+        }
+    }
+    return r;
+}
+
+__device__ __forceinline__ bool podref_has(const PodRef& r, const uint32_t* xp, uint32_t q) {
+    if (r.pair0 == q) return true;
+    if (r.flags & POD_REF_INDIRECT) {
+        for (uint32_t k = 0; k < r.p[1]; ++k) if (xp[r.p[0] + k] == q) return true;
+        return false;
+    }
+    return r.p[0] == q || r.p[1] == q || r.p[2] == q;
+}
+
+// Go's time.Time.Sub saturates at the int64 Duration range.
+__device__ __forceinline__ int64_t go_sub_ns(int64_t now_ns, int64_t t_s) {
+    const __int128 d = (__int128)now_ns - (__int128)t_s * 1000000000;
+    return d > (__int128)INT64_MAX ? INT64_MAX : (d < (__int128)INT64_MIN ? INT64_MIN : (int64_t)d);
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_podref_fill(PodDev P, const uint32_t* __restrict__ run_slot, int64_t n,
+                                                     PodRef* __restrict__ refs) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) refs[i] = podref_of(P, run_slot[i]);
+}
+
+// K6: one wave per node piece; for each entry whose node is escalator-tainted and not
+// cordoned (the only nodes a wet group can reap), count the node's pods that the entry's
+// pair filter selects (NewPodAffinityFilterFunc: the pair among the pod's pairs, not a
+// daemonset) and that the default filter selects — NodePodsRemaining over the group's
+// NodeInfoMap, which only holds the group's own pods (controller.go:259, node_state.go:58).
+__global__ __launch_bounds__(256) void k_occupancy(NodeDev N, GroupDev G, RemovalDev R) {
+    const int64_t pc = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (pc >= N.n_pieces) return;
+    const uint32_t q = N.piece_pair[pc];
+    if (q >= G.n_gp) return;
+    for (uint32_t e = N.piece_off[pc]; e < N.piece_off[pc + 1]; ++e) {
+        const uint32_t f = N.e_flags[e];
+        if (!(f & ESC_NF_TAINTED) || (f & ESC_NF_UNSCHED)) continue;     // wave-uniform
+        const uint32_t j = N.e_node[e];
+        uint32_t cp = 0, cd = 0;
+        for (uint32_t k = R.nrun_off[j] + lane; k < R.nrun_off[j + 1]; k += 64) {
+            const PodRef r = R.refs[k];
+            if (r.flags & ESC_PF_DAEMONSET) continue;
+            cp += podref_has(r, R.xp, q) ? 1u : 0u;
+            cd += pf_default_ok(r.flags & ~POD_REF_INDIRECT) ? 1u : 0u;
+        }
+        for (int o = 32; o >= 1; o >>= 1) { cp += __shfl_xor(cp, o, 64); cd += __shfl_xor(cd, o, 64); }
+        if (lane == 0) { R.occ_pair[e] = cp; R.occ_def[e] = cd; }
+    }
+}
+
+// K7: one wave per group over its pair's entries in snapshot order: the reference's loop
+// over taintedNodes (scale_down.go:53-99) — safeFromDeletion, GetToBeRemovedTime,
+// soft / hard grace, NodeEmpty — then the deletable nodes compacted into the group's list
+// and NodePodsRemaining summed over them (:101-109).  Dry-mode groups delete nothing.
+__global__ __launch_bounds__(64) void k_try_remove(NodeDev N, GroupDev G, RemovalDev R) {
+    const int32_t g = blockIdx.x;
+    const int lane = threadIdx.x;
+    const uint32_t q = G.gpair[g];
+    const bool dry = G.dry[g] != 0, dflt = (uint32_t)g == G.default_group;
+    const int64_t e0 = N.piece_off[N.pp_off[q]], e1 = N.piece_off[N.pp_off[q + 1]];
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int64_t cand = 0, del = 0, pods = 0;
+    for (int64_t b = e0; b < e1; b += 64) {
+        const int64_t e = b + lane;
+        bool c = false, d = false;
+        uint32_t occ = 0, j = 0;
+        if (e < e1) {
+            const uint32_t f = N.e_flags[e];
+            j = N.e_node[e];
+            const uint32_t m = (uint32_t)g | (dry ? NODE_DRY_BIT : 0u);
+            c = node_class(N, f, (int64_t)j, m) == 1;                     // filterNodes: tainted
+            if (c && !dry && !R.no_delete[j] && R.taint_s[j] != INT64_MIN) {
+                const int64_t age = go_sub_ns(R.now_ns, R.taint_s[j]);
+                occ = dflt ? R.occ_def[e] : R.occ_pair[e];
+                d = age > R.soft_ns[g] && (occ == 0 || age > R.hard_ns[g]);
+            }
+        }
+        const unsigned long long md = __ballot(d);
+        if (d) R.rm_list[R.rm_off[g] + del + __popcll(md & lt)] = j;
+        del += __popcll(md);
+        cand += __popcll(__ballot(c));
+        pods += wave_sum64(d ? occ : 0);
+    }
+    if (lane == 0) {
+        esc_removal o;
+        o.n_candidates = cand;
+        o.n_delete = del;
+        o.pods_remaining = pods;
+        o.reserved = 0;
+        R.out[g] = o;
+    }
+}
+
 // ===================================================================== launchers
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, hipStream_t st) {
@@ -1500,6 +1628,19 @@ hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* f
                           int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st) {
     hipLaunchKernelGGL(k_combine, dim3((g.G + 63) / 64), dim3(CB_WAVES * 64), 0, st, g, n, fold, nsplit,
                        node_rows, wide_pod, wp_cnt, trk_acc, words, first, decide ? 1 : 0, dec);
+    return hipGetLastError();
+}
+
+hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, int64_t n, PodRef* refs, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_podref_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, run_slot, n, refs);
+    return hipGetLastError();
+}
+
+hipError_t launch_try_remove(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st) {
+    if (n.n_pieces > 0)
+        hipLaunchKernelGGL(k_occupancy, dim3((unsigned)((n.n_pieces + 3) / 4)), dim3(256), 0, st, n, g, r);
+    hipLaunchKernelGGL(k_try_remove, dim3(g.G), dim3(64), 0, st, n, g, r);
     return hipGetLastError();
 }
 

@@ -184,6 +184,18 @@ struct esc_ctx {
     std::vector<int64_t> h_ncpu, h_nmem;
     std::vector<uint32_t> ne_off, ne_pos;                     // node -> its pair-major entry positions
     std::vector<GroupNode> h_gnode;
+    // scale-down reaping (§8f rank 2): pods bound to nodes, per-node taint times
+    bool placed = false;                                      // pod binding current
+    bool node_removal = false;                                // taint times / no-delete loaded
+    PodRef* d_refs = nullptr;
+    uint32_t *d_nrun_off = nullptr, *d_occ_pair = nullptr, *d_occ_def = nullptr, *d_rm_off = nullptr,
+             *d_rm_list = nullptr;
+    int64_t *d_taint_s = nullptr, *d_soft = nullptr, *d_hard = nullptr;
+    uint8_t* d_no_delete = nullptr;
+    esc_removal* d_rm_out = nullptr;
+    std::vector<uint32_t> h_rm_off;                           // [G + 1]
+    std::vector<esc_removal> h_rm;
+    bool rm_valid = false;                                    // esc_try_remove results current
 };
 
 namespace esc {
@@ -263,6 +275,13 @@ void release_work(esc_ctx* c) {
     c->h_dec_dev = nullptr;
     c->work_ready = false;
     drop_graphs(c);
+}
+
+void release_placement(esc_ctx* c) {
+    dfree(c->d_refs); dfree(c->d_nrun_off); dfree(c->d_occ_pair); dfree(c->d_occ_def); dfree(c->d_rm_off);
+    dfree(c->d_rm_list); dfree(c->d_taint_s); dfree(c->d_soft); dfree(c->d_hard); dfree(c->d_no_delete);
+    dfree(c->d_rm_out);
+    c->placed = c->node_removal = c->rm_valid = false;
 }
 
 void release_sort(esc_ctx* c) {
@@ -603,6 +622,7 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         if (c->stream) hipStreamSynchronize(c->stream);
         release_work(c);
         release_sort(c);
+        release_placement(c);
         for (auto& b : c->pods) b.release();
         c->nodes.release();
         dfree(c->d_dry); dfree(c->d_params);
@@ -794,6 +814,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     drop_graphs(c);
     release_work(c);
     release_sort(c);
+    release_placement(c);
     for (auto& b : c->pods) b.release();
     c->pods.assign(c->n_replicas, PodBuf());
     for (int r = 0; r < c->n_replicas; ++r) {
@@ -946,6 +967,7 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     drop_graphs(c);
     release_work(c);
     release_sort(c);
+    release_placement(c);
     c->nodes.release();
     NodeBuf& b = c->nodes;
     HIP_TRY(dalloc(&b.flags, n)); HIP_TRY(dalloc(&b.label0, n)); HIP_TRY(dalloc(&b.cpu, n));
@@ -1374,6 +1396,7 @@ int32_t esc_pods_upsert(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
         if (need[ci] > (int64_t)c->cls_free[ci].size()) return ESC_E_LIMIT;   // spare exhausted: reload
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->placed = c->rm_valid = false;                // pods moved: esc_load_placement again
     Patches P;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t id = ids[i];
@@ -1425,6 +1448,7 @@ int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     Patches P;
     for (int64_t i = 0; i < n; ++i) remove_pod(c, ids[i], P);
+    c->placed = c->rm_valid = false;                // pods moved: esc_load_placement again
     return apply_patches(c, P, pod_targets(c));
 }
 
@@ -1440,6 +1464,7 @@ int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32
     }
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->rm_valid = false;
     enum : uint32_t { NT_FLAGS = 0, NT_EFLAGS = 1, NT_CPU = 6, NT_MEM = 7, NT_ECPU = 8, NT_EMEM = 9 };
     Patches P;
     bool first_changed = false;
@@ -1478,6 +1503,116 @@ int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32
     HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
                                 c->d_g_grp, c->d_g_flags, c->stream));
     c->sorted = false;
+    return ESC_OK;
+}
+
+// ------------------------------------------------ scale-down reaping (§8f rank 2)
+// esc_load_placement: CreateNodeNameToInfoMap (node_state.go:10-39) as runs of PodRef per
+// node (a host counting sort of the pods by node, then one gather of each pod's flags and
+// pairs from the resident layout), plus the per-node GetToBeRemovedTime / no-delete facts.
+int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* taint_s, const uint8_t* no_delete) {
+    if (!c || !taint_s || !no_delete) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->pods_loaded || !c->nodes_loaded || c->world != 1) return ESC_E_STATE;
+    if (!pod_node && !c->placed) return ESC_E_STATE;
+    const int64_t N = c->n_nodes, np = (int64_t)c->pod_cls.size();
+    if (pod_node)
+        for (int64_t i = 0; i < np; ++i)
+            if (pod_node[i] != NONE && (int64_t)pod_node[i] >= N) return ESC_E_INVAL;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const int32_t G = c->gi.G;
+    if (!c->d_taint_s) {
+        HIP_TRY(dalloc(&c->d_taint_s, std::max<int64_t>(N, 1)));
+        HIP_TRY(dalloc(&c->d_no_delete, std::max<int64_t>(N, 1)));
+        HIP_TRY(dalloc(&c->d_nrun_off, N + 1));
+        HIP_TRY(dalloc(&c->d_occ_pair, std::max<int64_t>(c->n_entries, 1)));
+        HIP_TRY(dalloc(&c->d_occ_def, std::max<int64_t>(c->n_entries, 1)));
+        HIP_TRY(dalloc(&c->d_soft, G)); HIP_TRY(dalloc(&c->d_hard, G));
+        HIP_TRY(dalloc(&c->d_rm_out, G)); HIP_TRY(dalloc(&c->d_rm_off, G));
+        // each group's deletable-node list can hold all of its pair's entries
+        std::vector<uint32_t> poff(c->n_pieces + 1), ppo(c->gi.n_gp + 1);
+        HIP_TRY(hipMemcpy(poff.data(), c->nodes.piece_off, poff.size() * 4, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(ppo.data(), c->nodes.pp_off, ppo.size() * 4, hipMemcpyDeviceToHost));
+        c->h_rm_off.assign(G + 1, 0);
+        for (int32_t g = 0; g < G; ++g) {
+            const uint32_t q = c->gi.gpair[g];
+            c->h_rm_off[g + 1] = c->h_rm_off[g] + (poff[ppo[q + 1]] - poff[ppo[q]]);
+        }
+        HIP_TRY(dalloc(&c->d_rm_list, std::max<uint32_t>(c->h_rm_off[G], 1)));
+        HIP_TRY(hipMemcpy(c->d_rm_off, c->h_rm_off.data(), (size_t)G * 4, hipMemcpyHostToDevice));
+        c->h_rm.assign(G, esc_removal{});
+    }
+    if (N) {
+        HIP_TRY(hipMemcpy(c->d_taint_s, taint_s, N * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_no_delete, no_delete, N, hipMemcpyHostToDevice));
+    }
+    if (pod_node) {
+        std::vector<uint32_t> off(N + 1, 0);
+        for (int64_t i = 0; i < np; ++i)
+            if (c->pod_cls[i] != -2 && pod_node[i] != NONE) ++off[pod_node[i] + 1];
+        for (int64_t j = 0; j < N; ++j) off[j + 1] += off[j];
+        const int64_t total = off[N];
+        std::vector<uint32_t> cur(off.begin(), off.end() - 1), slot(std::max<int64_t>(total, 1));
+        for (int64_t i = 0; i < np; ++i) {
+            const int32_t ci = c->pod_cls[i];
+            if (ci == -2 || pod_node[i] == NONE) continue;
+            int64_t d = c->pod_pos[i];                                  // C: already the slot
+            if (ci >= 0) d = (c->h_cls[ci].t0 + d / TILE) * TILE + d % TILE;
+            slot[cur[pod_node[i]]++] = (uint32_t)d;
+        }
+        dfree(c->d_refs);
+        uint32_t* d_slot = nullptr;
+        HIP_TRY(dalloc(&c->d_refs, std::max<int64_t>(total, 1)));
+        HIP_TRY(dalloc(&d_slot, slot.size()));
+        HIP_TRY(hipMemcpy(d_slot, slot.data(), slot.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_nrun_off, off.data(), (N + 1) * 4, hipMemcpyHostToDevice));
+        const hipError_t e = launch_podref_fill(pod_dev(c, c->cur), d_slot, total, c->d_refs, c->stream);
+        const hipError_t e2 = hipStreamSynchronize(c->stream);
+        dfree(d_slot);
+        HIP_TRY(e);
+        HIP_TRY(e2);
+        c->placed = true;
+    }
+    c->node_removal = true;
+    c->rm_valid = false;
+    return ESC_OK;
+}
+
+// esc_try_remove: K6 (node occupancy by group filter) + K7 (the per-group reaping pass).
+int32_t esc_try_remove(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, const int64_t* hard_ns, esc_removal* out) {
+    if (!c || !soft_ns || !hard_ns || !out) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->placed || !c->node_removal) return ESC_E_STATE;
+    const int32_t G = c->gi.G;
+    hipSetDevice(c->device);
+    HIP_TRY(hipMemcpyAsync(c->d_soft, soft_ns, (size_t)G * 8, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_hard, hard_ns, (size_t)G * 8, hipMemcpyHostToDevice, c->stream));
+    RemovalDev r;
+    r.taint_s = c->d_taint_s; r.no_delete = c->d_no_delete; r.nrun_off = c->d_nrun_off; r.refs = c->d_refs;
+    r.xp = c->pods[c->cur].xp;
+    r.occ_pair = c->d_occ_pair; r.occ_def = c->d_occ_def; r.soft_ns = c->d_soft; r.hard_ns = c->d_hard;
+    r.rm_off = c->d_rm_off; r.rm_list = c->d_rm_list; r.out = c->d_rm_out; r.now_ns = now_ns;
+    HIP_TRY(launch_try_remove(node_dev(c), group_dev(c), r, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_rm.data(), c->d_rm_out, (size_t)G * sizeof(esc_removal), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    std::memcpy(out, c->h_rm.data(), (size_t)G * sizeof(esc_removal));
+    c->rm_valid = true;
+    return ESC_OK;
+}
+
+int32_t esc_removal_nodes(esc_ctx* c, int32_t g, int64_t* idx, int64_t cap, int64_t* n_out) {
+    if (!c || !n_out || g < 0 || g >= c->gi.G || cap < 0 || (cap > 0 && !idx)) return ESC_E_INVAL;
+    if (!c->rm_valid) return ESC_E_STATE;
+    const int64_t n = c->h_rm[g].n_delete;
+    *n_out = n;
+    if (n > cap) return ESC_E_LIMIT;
+    if (!n) return ESC_OK;
+    std::vector<uint32_t> v(n);
+    hipSetDevice(c->device);
+    HIP_TRY(hipMemcpy(v.data(), c->d_rm_list + c->h_rm_off[g], n * 4, hipMemcpyDeviceToHost));
+    for (int64_t k = 0; k < n; ++k) idx[k] = v[k];
     return ESC_OK;
 }
 

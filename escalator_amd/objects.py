@@ -18,6 +18,7 @@ absent resource key.
 from __future__ import annotations
 
 import ctypes as C
+import re
 
 from . import _lib as L
 
@@ -172,3 +173,40 @@ def states_to_c(states: list[dict] | None, n: int):
         out[i] = L.GroupState(int(bool(st.get("locked", 0))), st.get("requested_nodes", 0),
                               st.get("cached_cpu_m", 0), st.get("cached_mem_b", 0))
     return out
+
+
+# ------------------------------------------------ scale-down reaping inputs (§8f rank 2)
+TO_BE_REMOVED_KEY = "atlassian.com/escalator"          # pkg/k8s/taint.go:31 (ToBeRemovedByAutoscalerKey)
+NO_DELETE_ANNOTATION = "atlassian.com/no-delete"       # pkg/controller/scale_down.go:22
+INT64_MIN, INT64_MAX = -(1 << 63), (1 << 63) - 1
+_NONE = 0xFFFFFFFF
+
+
+def taint_time(node: dict) -> int:
+    """GetToBeRemovedTime (pkg/k8s/taint.go:91-103) as Unix seconds: INT64_MIN when the
+    escalator taint is absent or its value is not a base-10 int64 (strconv.ParseInt)."""
+    if TO_BE_REMOVED_KEY not in (node.get("taints") or []):
+        return INT64_MIN
+    v = node.get("taint_value")
+    if not isinstance(v, str) or not re.fullmatch(r"[+-]?[0-9]+", v):
+        return INT64_MIN
+    t = int(v)
+    # INT64_MIN itself doubles as "no time": the one parseable value treated as absent
+    return t if INT64_MIN < t <= INT64_MAX else INT64_MIN
+
+
+def placement(pods: list[dict], nodes: list[dict]):
+    """Inputs of esc_load_placement from objects, in the packer's pod / node order:
+    each pod's Spec.NodeName as a node index (NONE when empty or not a listed node:
+    CreateNodeNameToInfoMap drops those, node_state.go:31-36), each node's escalator-taint
+    time and its no-delete annotation (safeFromDeletion, scale_down.go:39-46)."""
+    import numpy as np
+    index = {}
+    for j, n in enumerate(nodes):
+        index.setdefault(n.get("name", ""), j)
+    pod_node = np.array([index.get(p.get("node_name") or "", _NONE) if p.get("node_name") else _NONE
+                         for p in pods], np.uint32)
+    taint_s = np.array([taint_time(n) for n in nodes], np.int64)
+    no_delete = np.array([1 if (n.get("annotations") or {}).get(NO_DELETE_ANNOTATION, "") else 0 for n in nodes],
+                         np.uint8)
+    return pod_node, taint_s, no_delete

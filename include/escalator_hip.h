@@ -389,6 +389,30 @@ int32_t esc_pods_delete(esc_ctx* ctx, const int64_t* ids, int64_t n);
 int32_t esc_nodes_update(esc_ctx* ctx, const int64_t* ids, int64_t n, const uint32_t* flags,
                          const int64_t* cpu_m, const int64_t* mem_b);
 
+/* ------------------------------------------ scale-down reaping (§8f rank 2)
+ * TryRemoveTaintedNodes (pkg/controller/scale_down.go:51-136) with NodeEmpty /
+ * NodePodsRemaining over the group's NodeInfoMap (pkg/k8s/node_state.go:10-65), for every
+ * group at once.  esc_load_placement binds the loaded pods to nodes (Spec.NodeName as a
+ * snapshot node index, ESC_NONE when empty or not a known node — CreateNodeNameToInfoMap
+ * drops those) and gives each node its escalator-taint time (GetToBeRemovedTime,
+ * taint.go:91: Unix seconds, INT64_MIN when the taint is absent or its value does not
+ * parse) and its atlassian.com/no-delete annotation (non-empty = safe from deletion).
+ * Pod events (esc_pods_upsert / _delete) invalidate the binding (ESC_E_STATE until it is
+ * loaded again).  esc_try_remove then evaluates, per group, its tainted nodes in snapshot
+ * order: now - taintTime > soft grace and (NodeEmpty or > hard grace) -> delete (never in
+ * dry mode).  Single-rank contexts only.                                             */
+typedef struct esc_removal {
+    int64_t n_candidates;        /* the group's tainted nodes (filterNodes)                    */
+    int64_t n_delete;            /* len(toBeDeleted): TryRemoveTaintedNodes returns -n_delete  */
+    int64_t pods_remaining;      /* sum of NodePodsRemaining over them (NodeGroupPodsEvicted)  */
+    int64_t reserved;
+} esc_removal;
+int32_t esc_load_placement(esc_ctx* ctx, const uint32_t* pod_node, const int64_t* taint_unix_s,
+                           const uint8_t* no_delete);
+int32_t esc_try_remove(esc_ctx* ctx, int64_t now_unix_ns, const int64_t* soft_grace_ns,
+                       const int64_t* hard_grace_ns, esc_removal* out);
+int32_t esc_removal_nodes(esc_ctx* ctx, int32_t group, int64_t* idx_out, int64_t cap, int64_t* n_out);
+
 /* ----------------------------------------------------------------- ordering
  * K5: per-group creation-time order of the context's node shard (a18/a19):
  *   which 0: untainted members oldest-first (taintOldestN,   scale_down.go:171)

@@ -27,6 +27,8 @@ amd64's ``int(float64)`` conversion of NaN/Inf (0x8000000000000000).
 """
 from __future__ import annotations
 
+import re
+
 import math
 
 INT64_MIN = -(1 << 63)
@@ -225,6 +227,71 @@ def filter_nodes(dry_mode: bool, tracker: list[str], all_nodes: list[dict]):
             else:
                 unt.append(i)
     return unt, tnt, cor
+
+
+# ------------------------------------------------ pkg/k8s/node_state.go + taint.go:91
+def create_node_name_to_info_map(pods: list[dict], nodes: list[dict]) -> dict:
+    """CreateNodeNameToInfoMap — node_state.go:10-39: pods grouped by Spec.NodeName, then
+    node infos without a node ("" or unknown names: pods out of sync) removed."""
+    m: dict = {}
+    for p in pods:
+        m.setdefault(p.get("node_name", ""), {"node": None, "pods": []})["pods"].append(p)
+    for n in nodes:
+        m.setdefault(n["name"], {"node": None, "pods": []})["node"] = n
+    return {k: v for k, v in m.items() if v["node"] is not None}
+
+
+def node_pods_remaining(node: dict, info_map: dict | None) -> tuple[int, bool]:
+    """NodePodsRemaining — node_state.go:48-65: non-daemonset pods on the node, ok = the
+    node is in the map."""
+    if not info_map or node["name"] not in info_map:
+        return 0, False
+    return sum(1 for p in info_map[node["name"]]["pods"] if not pod_is_daemonset(p)), True
+
+
+def node_empty(node: dict, info_map: dict | None) -> bool:
+    """NodeEmpty — node_state.go:42-45."""
+    n, ok = node_pods_remaining(node, info_map)
+    return ok and n == 0
+
+
+def get_to_be_removed_time(node: dict):
+    """GetToBeRemovedTime — taint.go:91-103: the escalator taint's value as Unix seconds;
+    None when the taint is absent or its value does not parse (strconv.ParseInt)."""
+    if not has_to_be_removed_taint(node):
+        return None
+    v = node.get("taint_value")
+    if not isinstance(v, str) or not re.fullmatch(r"[+-]?[0-9]+", v):   # strconv.ParseInt(v, 10, 64)
+        return None
+    t = int(v)
+    return t if INT64_MIN <= t <= INT64_MAX else None
+
+
+def try_remove_tainted_nodes(group: dict, tainted: list[dict], pods_g: list[dict], all_nodes: list[dict],
+                             now_ns: int, soft_ns: int, hard_ns: int, dry_mode: bool) -> tuple[int, int, list[int]]:
+    """(*Controller).TryRemoveTaintedNodes — scale_down.go:51-136 (the cloud-provider and
+    API deletes stay with the host).  Returns (-len(toBeDeleted), podsRemaining summed over
+    them, indices into `tainted` of the nodes to delete)."""
+    info = create_node_name_to_info_map(pods_g, all_nodes)          # controller.go:259
+    out = []
+    for k, node in enumerate(tainted):
+        ann = node.get("annotations") or {}
+        if ann.get("atlassian.com/no-delete", ""):                   # safeFromDeletion :39-46
+            continue
+        t = get_to_be_removed_time(node)
+        if t is None:                                                # :65-69
+            continue
+        age = now_ns - t * 1_000_000_000                             # now.Sub(taintedTime)
+        if age > soft_ns:
+            if node_empty(node, info) or age > hard_ns:
+                if not dry_mode:
+                    out.append(k)
+    remaining = 0
+    for k in out:
+        n, ok = node_pods_remaining(tainted[k], info)
+        if ok:
+            remaining += n
+    return -len(out), remaining, out
 
 
 # ------------------------------------------------ pkg/controller/util.go

@@ -441,3 +441,75 @@ def test_incremental_events_vs_literal(esc, seed):
     before = ctx.decide_all(states)[0].tobytes()
     assert ctx.pods_upsert([next_id + k for k in range(len(keep))], _packed_subset(Pm, keep)) == ESC_E_LIMIT
     assert ctx.decide_all(states)[0].tobytes() == before
+
+
+# ------------------------------------------------ scale-down reaping (§8f rank 2)
+def _reaping_cluster(rng, G, n_pods, n_nodes):
+    groups = make_groups(rng, G, with_default=rng.random() < 0.7)
+    pods = make_pods(rng, n_pods, groups, big_frac=0.0)
+    nodes = make_nodes(rng, n_nodes, groups, big_frac=0.0)
+    now_s = 1_700_000_000
+    for nd in nodes:
+        if rng.random() < 0.4 and "atlassian.com/escalator" not in nd["taints"]:
+            nd["taints"] = nd["taints"] + ["atlassian.com/escalator"]
+        nd["taint_value"] = rng.choice([str(now_s - rng.randrange(0, 900)), str(now_s - rng.randrange(0, 900)),
+                                        "+%d" % (now_s - 400), "bad", "", "-5", "99999999999999999999", None])
+        if rng.random() < 0.1:
+            nd["annotations"] = {"atlassian.com/no-delete": rng.choice(["true", ""])}
+    for p in pods:
+        r = rng.random()
+        p["node_name"] = "" if r < 0.1 else ("ghost" if r < 0.15 else rng.choice(nodes)["name"])
+    return groups, pods, nodes, now_s * 1_000_000_000
+
+
+def _check_reaping(ctx, groups, pods, nodes, trackers, now_ns, soft, hard):
+    res = ctx.try_remove(now_ns, soft, hard)
+    for g, grp in enumerate(groups):
+        L = O.scale_node_group(grp, {}, pods, nodes, tracker=trackers.get(g, []))
+        pods_g = O.filtered_list(pods, O.group_pod_filter(grp))
+        all_nodes = [nodes[i] for i in range(len(nodes))
+                     if O.new_node_label_filter_func(grp.get("label_key", ""), grp.get("label_value", ""))(nodes[i])]
+        tainted = L["tainted"]
+        neg, remaining, ks = O.try_remove_tainted_nodes(grp, [nodes[i] for i in tainted], pods_g, all_nodes,
+                                                        now_ns, int(soft[g]), int(hard[g]), bool(grp.get("dry_mode")))
+        r = res[g]
+        assert int(r["n_candidates"]) == len(tainted), g
+        assert (-int(r["n_delete"]), int(r["pods_remaining"])) == (neg, remaining), (g, neg, remaining)
+        assert list(ctx.removal_nodes(g)) == [tainted[k] for k in ks], g
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_try_remove_tainted_vs_literal(esc, seed):
+    """TryRemoveTaintedNodes for every group at once (esc_load_placement + esc_try_remove):
+    deletion lists, counts and NodePodsRemaining sums equal the literal oracle, including
+    no-delete annotations, unparsable taint values, dry-mode groups, pods bound to no /
+    unknown nodes and nodes shared by several groups; pod events invalidate the binding."""
+    from escalator_amd.objects import placement
+    rng = random.Random(9100 + seed)
+    G = rng.choice([1, 4, 12])
+    groups, pods, nodes, now_ns = _reaping_cluster(rng, G, rng.choice([0, 300, 1500]), rng.choice([5, 60, 200]))
+    trackers = make_trackers(rng, groups, nodes)
+    ctx = esc.Context(groups)
+    P, N = ctx.pack(pods, nodes, trackers)
+    assert len(P["flags"]) == len(pods)
+    ctx.load(P, N)
+    pn, ts, nd = placement(pods, nodes)
+    ctx.load_placement(pn, ts, nd)
+    for _ in range(3):
+        soft = np.array([rng.choice([0, 60, 300, 600]) * 10**9 for _ in range(G)], np.int64)
+        hard = soft + np.array([rng.choice([0, 120, 600]) * 10**9 for _ in range(G)], np.int64)
+        _check_reaping(ctx, groups, pods, nodes, trackers, now_ns, soft, hard)
+    # node facts refreshed without re-binding pods
+    for x in rng.sample(nodes, min(len(nodes), 5)):
+        x["taint_value"] = str(now_ns // 10**9 - 5000)
+        x["annotations"] = {}
+    pn, ts, nd = placement(pods, nodes)
+    ctx.load_placement(None, ts, nd)
+    _check_reaping(ctx, groups, pods, nodes, trackers, now_ns, np.full(G, 60 * 10**9), np.full(G, 4000 * 10**9))
+    if pods:
+        ctx.pods_delete([0])
+        with pytest.raises(RuntimeError):
+            ctx.try_remove(now_ns, np.zeros(G, np.int64), np.zeros(G, np.int64))
+        del pods[0]
+        ctx.load_placement(np.r_[np.uint32(0xFFFFFFFF), pn[1:]], ts, nd)
+        _check_reaping(ctx, groups, pods, nodes, trackers, now_ns, np.full(G, 60 * 10**9), np.full(G, 4000 * 10**9))

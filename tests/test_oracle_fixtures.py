@@ -210,3 +210,54 @@ def test_metrics_memory_gauge_quirk():
     assert m["mem_capacity"] == 3.0
     assert m["mem_request"] == float(O.go_div_trunc(O.wrap64((1 << 62) * 1000), 1000))
     assert O.go_div_trunc(-1999, 1000) == -1 and O.go_div_trunc(1999, -1000) == -1
+
+
+# ------------------------------------------- §8f rank 2: node_state.go / TryRemoveTaintedNodes
+def _ns_golden():
+    import json
+    import os
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden", "node_state.json")))
+
+
+def test_create_node_name_to_info_map_fixtures():
+    for c in _ns_golden()["create_node_name_to_info_map"]:
+        nodes = [{"name": n} for n in c["nodes"]]
+        pods = [{"node_name": n, "owner_kinds": []} for n in c["pods"]]
+        m = O.create_node_name_to_info_map(pods, nodes)
+        assert len(m) == c["want_len"], c["name"]
+        assert sum(len(v["pods"]) for v in m.values()) == c["want_pods"], c["name"]
+
+
+def test_node_empty_and_pods_remaining_fixtures():
+    for c in _ns_golden()["node_state"]:
+        node = {"name": "node-1"}
+        pods = [{"node_name": "node-1", "owner_kinds": [p["owner"]] if p["owner"] else []} for p in c["pods"]]
+        m = None if c["empty_map"] else O.create_node_name_to_info_map(pods, [node])
+        assert O.node_empty(node, m) == c["empty"], c["name"]
+        assert O.node_pods_remaining(node, m) == (c["remaining"], c["ok"]), c["name"]
+
+
+def test_try_remove_tainted_nodes_fixtures():
+    g = _ns_golden()["try_remove_tainted_nodes"]
+    now_s = 1_700_000_000
+    for c in g["cases"]:
+        nodes = [{"name": "n%d" % i, "taints": ["atlassian.com/escalator"], "taint_value": str(now_s),
+                  "created_ns": i} for i in range(10)]
+        pods = [{"node_name": "", "owner_kinds": []} for _ in range(10)]
+        tainted = nodes[:c["n_tainted"]]
+        if c["annotate_first_tainted"]:
+            tainted[0]["annotations"] = {"atlassian.com/no-delete": "skip for testing"}
+        got, _, _ = O.try_remove_tainted_nodes({"name": "default"}, tainted, pods, nodes,
+                                                now_ns=now_s * 1_000_000_000 + 1, soft_ns=0, hard_ns=0,
+                                                dry_mode=False)
+        assert got == c["want"], c["name"]
+
+
+def test_to_be_removed_time_parse():
+    """strconv.ParseInt(v, 10, 64) semantics for the taint value (taint.go:95)."""
+    t = {"taints": ["atlassian.com/escalator"]}
+    assert O.get_to_be_removed_time(dict(t, taint_value="1700000000")) == 1700000000
+    assert O.get_to_be_removed_time(dict(t, taint_value="+12")) == 12
+    for bad in ("", " 12", "1_000", "12s", "9223372036854775808", None):
+        assert O.get_to_be_removed_time(dict(t, taint_value=bad)) is None, bad
+    assert O.get_to_be_removed_time({"taints": [], "taint_value": "12"}) is None
