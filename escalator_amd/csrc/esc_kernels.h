@@ -150,6 +150,8 @@ constexpr uint32_t POD_REF_INDIRECT = 1u << 31;
 struct RemovalDev {
     const int64_t* taint_s;    // [n_nodes] escalator-taint time (INT64_MIN: none / unparsable)
     const uint8_t* no_delete;  // [n_nodes]
+    const uint32_t* e_pair;    // [n_entries] pair of each pair-major entry
+    int64_t n_entries;
     const uint32_t* nrun_off;  // [n_nodes + 1] runs of PodRef per node
     const PodRef* refs;
     const uint32_t* xp;        // C-pod extra pairs (indirect refs)

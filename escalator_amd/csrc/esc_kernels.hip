@@ -1509,30 +1509,38 @@ __global__ __launch_bounds__(256) void k_podref_fill(PodDev P, const uint32_t* _
     if (i < n) refs[i] = podref_of(P, run_slot[i]);
 }
 
-// K6: one wave per node piece; for each entry whose node is escalator-tainted and not
-// cordoned (the only nodes a wet group can reap), count the node's pods that the entry's
-// pair filter selects (NewPodAffinityFilterFunc: the pair among the pod's pairs, not a
-// daemonset) and that the default filter selects — NodePodsRemaining over the group's
-// NodeInfoMap, which only holds the group's own pods (controller.go:259, node_state.go:58).
+// K6: one wave per 64 pair-major entries; the entries whose node is escalator-tainted and
+// not cordoned (the only nodes a wet group can reap) are taken in turn by the whole wave,
+// which counts the node's pods that the entry's pair filter selects
+// (NewPodAffinityFilterFunc: the pair among the pod's pairs) and that the default filter
+// selects, daemonsets excluded — NodePodsRemaining over the group's NodeInfoMap, which
+// only holds the group's own pods (controller.go:259, node_state.go:48-65).
 __global__ __launch_bounds__(256) void k_occupancy(NodeDev N, GroupDev G, RemovalDev R) {
-    const int64_t pc = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int64_t base = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64;
     const int lane = threadIdx.x & 63;
-    if (pc >= N.n_pieces) return;
-    const uint32_t q = N.piece_pair[pc];
-    if (q >= G.n_gp) return;
-    for (uint32_t e = N.piece_off[pc]; e < N.piece_off[pc + 1]; ++e) {
+    const int64_t e = base + lane;
+    bool want = false;
+    uint32_t j = 0, q = 0;
+    if (e < R.n_entries) {
         const uint32_t f = N.e_flags[e];
-        if (!(f & ESC_NF_TAINTED) || (f & ESC_NF_UNSCHED)) continue;     // wave-uniform
-        const uint32_t j = N.e_node[e];
+        q = R.e_pair[e];
+        j = N.e_node[e];
+        want = q < G.n_gp && (f & ESC_NF_TAINTED) && !(f & ESC_NF_UNSCHED);
+    }
+    unsigned long long m = __ballot(want);
+    while (m) {
+        const int k = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const uint32_t jk = __shfl(j, k, 64), qk = __shfl(q, k, 64);
         uint32_t cp = 0, cd = 0;
-        for (uint32_t k = R.nrun_off[j] + lane; k < R.nrun_off[j + 1]; k += 64) {
-            const PodRef r = R.refs[k];
+        for (uint32_t i = R.nrun_off[jk] + lane; i < R.nrun_off[jk + 1]; i += 64) {
+            const PodRef r = R.refs[i];
             if (r.flags & ESC_PF_DAEMONSET) continue;
-            cp += podref_has(r, R.xp, q) ? 1u : 0u;
+            cp += podref_has(r, R.xp, qk) ? 1u : 0u;
             cd += pf_default_ok(r.flags & ~POD_REF_INDIRECT) ? 1u : 0u;
         }
         for (int o = 32; o >= 1; o >>= 1) { cp += __shfl_xor(cp, o, 64); cd += __shfl_xor(cd, o, 64); }
-        if (lane == 0) { R.occ_pair[e] = cp; R.occ_def[e] = cd; }
+        if (lane == k) { R.occ_pair[e] = cp; R.occ_def[e] = cd; }
     }
 }
 
@@ -1638,8 +1646,8 @@ hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, int64_t
 }
 
 hipError_t launch_try_remove(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st) {
-    if (n.n_pieces > 0)
-        hipLaunchKernelGGL(k_occupancy, dim3((unsigned)((n.n_pieces + 3) / 4)), dim3(256), 0, st, n, g, r);
+    if (r.n_entries > 0)
+        hipLaunchKernelGGL(k_occupancy, dim3((unsigned)((r.n_entries + 255) / 256)), dim3(256), 0, st, n, g, r);
     hipLaunchKernelGGL(k_try_remove, dim3(g.G), dim3(64), 0, st, n, g, r);
     return hipGetLastError();
 }

@@ -188,6 +188,7 @@ struct esc_ctx {
     bool placed = false;                                      // pod binding current
     bool node_removal = false;                                // taint times / no-delete loaded
     PodRef* d_refs = nullptr;
+    uint32_t* d_e_pair = nullptr;
     uint32_t *d_nrun_off = nullptr, *d_occ_pair = nullptr, *d_occ_def = nullptr, *d_rm_off = nullptr,
              *d_rm_list = nullptr;
     int64_t *d_taint_s = nullptr, *d_soft = nullptr, *d_hard = nullptr;
@@ -278,7 +279,7 @@ void release_work(esc_ctx* c) {
 }
 
 void release_placement(esc_ctx* c) {
-    dfree(c->d_refs); dfree(c->d_nrun_off); dfree(c->d_occ_pair); dfree(c->d_occ_def); dfree(c->d_rm_off);
+    dfree(c->d_refs); dfree(c->d_e_pair); dfree(c->d_nrun_off); dfree(c->d_occ_pair); dfree(c->d_occ_def); dfree(c->d_rm_off);
     dfree(c->d_rm_list); dfree(c->d_taint_s); dfree(c->d_soft); dfree(c->d_hard); dfree(c->d_no_delete);
     dfree(c->d_rm_out);
     c->placed = c->node_removal = c->rm_valid = false;
@@ -1531,9 +1532,16 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
         HIP_TRY(dalloc(&c->d_soft, G)); HIP_TRY(dalloc(&c->d_hard, G));
         HIP_TRY(dalloc(&c->d_rm_out, G)); HIP_TRY(dalloc(&c->d_rm_off, G));
         // each group's deletable-node list can hold all of its pair's entries
-        std::vector<uint32_t> poff(c->n_pieces + 1), ppo(c->gi.n_gp + 1);
+        std::vector<uint32_t> poff(c->n_pieces + 1), ppo(c->gi.n_gp + 1), ppair(std::max<int64_t>(c->n_pieces, 1));
         HIP_TRY(hipMemcpy(poff.data(), c->nodes.piece_off, poff.size() * 4, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(ppo.data(), c->nodes.pp_off, ppo.size() * 4, hipMemcpyDeviceToHost));
+        if (c->n_pieces)
+            HIP_TRY(hipMemcpy(ppair.data(), c->nodes.piece_pair, c->n_pieces * 4, hipMemcpyDeviceToHost));
+        std::vector<uint32_t> epair(std::max<int64_t>(c->n_entries, 1), NONE);
+        for (int64_t pc = 0; pc < c->n_pieces; ++pc)
+            for (uint32_t e = poff[pc]; e < poff[pc + 1]; ++e) epair[e] = ppair[pc];
+        HIP_TRY(dalloc(&c->d_e_pair, epair.size()));
+        HIP_TRY(hipMemcpy(c->d_e_pair, epair.data(), epair.size() * 4, hipMemcpyHostToDevice));
         c->h_rm_off.assign(G + 1, 0);
         for (int32_t g = 0; g < G; ++g) {
             const uint32_t q = c->gi.gpair[g];
@@ -1589,6 +1597,7 @@ int32_t esc_try_remove(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, const
     HIP_TRY(hipMemcpyAsync(c->d_soft, soft_ns, (size_t)G * 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_hard, hard_ns, (size_t)G * 8, hipMemcpyHostToDevice, c->stream));
     RemovalDev r;
+    r.e_pair = c->d_e_pair; r.n_entries = c->n_entries;
     r.taint_s = c->d_taint_s; r.no_delete = c->d_no_delete; r.nrun_off = c->d_nrun_off; r.refs = c->d_refs;
     r.xp = c->pods[c->cur].xp;
     r.occ_pair = c->d_occ_pair; r.occ_def = c->d_occ_def; r.soft_ns = c->d_soft; r.hard_ns = c->d_hard;

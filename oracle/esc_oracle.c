@@ -19,6 +19,10 @@
  *   orc_decide      scaleNodeGroup's decision arithmetic (controller.go:192-351),
  *                   calcPercentUsage / calcScaleUpDelta (pkg/controller/util.go:13-81),
  *                   scaleDownTaint clamp (scale_down.go:138-158).
+ *   orc_try_remove  TryRemoveTaintedNodes (scale_down.go:51-136) for one group, with
+ *                   CreateNodeNameToInfoMap / NodePodsRemaining / NodeEmpty
+ *                   (node_state.go:10-65) over the pods' node bindings; reference-shaped
+ *                   (the group's pods rescanned per call).
  *   orc_order       taintOldestN / untaintNewestN orderings (scale_down.go:171-205,
  *                   scale_up.go:118-163, sort.go:6-39); ties by index (Go's sort.Sort
  *                   is unstable, so its tie order is not reproducible).
@@ -380,4 +384,58 @@ int64_t orc_order(int64_t n_nodes, const uint32_t* nflags, const uint32_t* label
     for (int64_t i = 0; i < m && i < cap; ++i) out[i] = v[i].idx;
     free(v);
     return m;
+}
+
+/* (*Controller).TryRemoveTaintedNodes — scale_down.go:51-136, one group.  The group's
+ * NodeInfoMap (controller.go:259 -> CreateNodeNameToInfoMap, node_state.go:10-39) is
+ * restated as occ[node] = the group's non-daemonset pods bound to the node
+ * (NodePodsRemaining, node_state.go:48-65; pods bound to no / an unknown node are dropped,
+ * node_state.go:31-36).  Then its tainted nodes (filterNodes, controller.go:125-150) in
+ * snapshot order: safeFromDeletion (:39-46), GetToBeRemovedTime (taint.go:91-103;
+ * taint_s INT64_MIN = none), now.Sub(taintedTime) (saturating, as time.Time.Sub) against
+ * the soft / hard grace (:71-99), deletions only when not in dry mode.
+ * res = {n_candidates, n_delete, pods_remaining}; out = deleted node indices.  */
+int64_t orc_try_remove(int64_t n_pods, const uint32_t* flags, const uint32_t* pair0, const uint32_t* xp,
+                       const uint32_t* pod_node, int64_t n_nodes, const uint32_t* nflags, const uint32_t* label0,
+                       const uint32_t* xl, const int32_t* tn, const int32_t* tg, int64_t n_trk,
+                       const int64_t* taint_s, const uint8_t* no_delete, const uint8_t* dry,
+                       const uint32_t* gpair, int32_t default_group, int32_t group, int64_t now_ns, int64_t soft_ns,
+                       int64_t hard_ns, int64_t* res, int64_t* out, int64_t cap) {
+    int64_t* occ = (int64_t*)calloc((size_t)n_nodes + 1, sizeof(int64_t));
+    if (!occ) return -1;
+    const uint32_t q = gpair[group];
+    uint64_t op = 0;
+    for (int64_t p = 0; p < n_pods; ++p) {
+        const uint32_t f = flags[p], nx = xpair(f);
+        int in = 0;
+        if (group == default_group) {
+            in = !(f & (PF_STATIC | PF_SEL | PF_AFF));                /* NewPodDefaultFilterFunc */
+        } else {
+            in = pair0[p] == q;                                         /* NewPodAffinityFilterFunc */
+            for (uint32_t k = 0; k < nx; ++k) in |= xp[op + k] == q;
+        }
+        op += nx;
+        if (!in || (f & PF_DS) || pod_node[p] == NONE) continue;        /* NodePodsRemaining skips DS */
+        occ[pod_node[p]]++;
+    }
+    int64_t cand = 0, del = 0, rem = 0, ql = 0;
+    for (int64_t i = 0; i < n_nodes; ++i) {
+        const uint32_t f = nflags[i];
+        int member = 0;
+        for (uint32_t k = 0; k <= xlbl(f); ++k) member |= (k == 0 ? label0[i] : xl[ql + k - 1]) == q;
+        ql += xlbl(f);
+        if (!member || node_class(f, dry[group], tn, tg, n_trk, i, group) != 1) continue;
+        ++cand;
+        if (no_delete[i] || taint_s[i] == INT64_MIN) continue;
+        const i128 d = (i128)now_ns - (i128)taint_s[i] * 1000000000;
+        const int64_t age = d > (i128)INT64_MAX ? INT64_MAX : d < (i128)INT64_MIN ? INT64_MIN : (int64_t)d;
+        if (age > soft_ns && (occ[i] == 0 || age > hard_ns) && !dry[group]) {
+            if (del < cap) out[del] = i;
+            ++del;
+            rem += occ[i];
+        }
+    }
+    res[0] = cand; res[1] = del; res[2] = rem;
+    free(occ);
+    return del;
 }

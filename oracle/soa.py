@@ -42,6 +42,7 @@ def lib():
         _lib.orc_totals.restype = C.c_int
         _lib.orc_ref_scan.restype = C.c_int
         _lib.orc_order.restype = C.c_int64
+        _lib.orc_try_remove.restype = C.c_int64
         _lib.orc_percent.restype = C.c_int
         _lib.orc_scale_up.restype = C.c_int
         _lib.orc_percent.argtypes = [C.c_int64] * 5 + [C.POINTER(C.c_double)] * 2
@@ -138,6 +139,31 @@ def order(nodes: dict, groups: list[dict], group: int, which: int, node_lo: int 
     m = int(m)
     out = out[:m]
     return out if cap is None else out[:cap]
+
+
+def try_remove(pods: dict, nodes: dict, groups: list[dict], pod_node, taint_s, no_delete, group: int,
+               now_ns: int, soft_ns: int, hard_ns: int):
+    """orc_try_remove: TryRemoveTaintedNodes for one group (scale_down.go:51-136) over a
+    packed snapshot.  Returns ((n_candidates, n_delete, pods_remaining), deleted indices)."""
+    t = group_tables(groups)
+    n = len(nodes["flags"])
+    res = np.zeros(3, np.int64)
+    out = np.zeros(max(n, 1), np.int64)
+    pn = np.ascontiguousarray(pod_node, np.uint32)
+    ts = np.ascontiguousarray(taint_s, np.int64)
+    nd = np.ascontiguousarray(no_delete, np.uint8)
+    m = lib().orc_try_remove(C.c_int64(len(pods["flags"])), _p(pods["flags"], C.c_uint32),
+                             _p(pods["pair0"], C.c_uint32), _p(pods["xp_pair"], C.c_uint32), _p(pn, C.c_uint32),
+                             C.c_int64(n), _p(nodes["flags"], C.c_uint32), _p(nodes["label0"], C.c_uint32),
+                             _p(nodes["xl_pair"], C.c_uint32), _p(nodes["trk_node"], C.c_int32),
+                             _p(nodes["trk_group"], C.c_int32), C.c_int64(len(nodes["trk_node"])),
+                             _p(ts, C.c_int64), _p(nd, C.c_uint8), _p(t["dry"], C.c_uint8),
+                             _p(t["gpair"], C.c_uint32), C.c_int32(t["default"]), C.c_int32(group),
+                             C.c_int64(now_ns), C.c_int64(soft_ns), C.c_int64(hard_ns), _p(res, C.c_int64),
+                             _p(out, C.c_int64), C.c_int64(len(out)))
+    if m < 0:
+        raise MemoryError("orc_try_remove")
+    return tuple(int(x) for x in res), out[:int(m)]
 
 
 METRIC_NAMES = ["nodes", "nodes_cordoned", "nodes_untainted", "nodes_tainted", "pods", "cpu_request",

@@ -130,3 +130,23 @@ def make_trackers(rng: random.Random, groups: list[dict], nodes: list[dict]) -> 
 def make_states(rng: random.Random, G: int) -> list[dict]:
     return [{"locked": rng.random() < 0.1, "requested_nodes": rng.randrange(0, 5),
              "cached_cpu_m": rng.choice([0, 4000]), "cached_mem_b": rng.choice([0, 8 << 30])} for _ in range(G)]
+
+
+def make_reaping_cluster(rng: random.Random, G: int, n_pods: int, n_nodes: int):
+    """A cluster for TryRemoveTaintedNodes: escalator taints with valid / unparsable
+    values, no-delete annotations, pods bound to listed, unknown and no nodes."""
+    groups = make_groups(rng, G, with_default=rng.random() < 0.7)
+    pods = make_pods(rng, n_pods, groups, big_frac=0.0)
+    nodes = make_nodes(rng, n_nodes, groups, big_frac=0.0)
+    now_s = 1_700_000_000
+    for nd in nodes:
+        if rng.random() < 0.4 and "atlassian.com/escalator" not in nd["taints"]:
+            nd["taints"] = nd["taints"] + ["atlassian.com/escalator"]
+        nd["taint_value"] = rng.choice([str(now_s - rng.randrange(0, 900)), str(now_s - rng.randrange(0, 900)),
+                                        "+%d" % (now_s - 400), "bad", "", "-5", "99999999999999999999", None])
+        if rng.random() < 0.1:
+            nd["annotations"] = {"atlassian.com/no-delete": rng.choice(["true", ""])}
+    for p in pods:
+        r = rng.random()
+        p["node_name"] = "" if r < 0.1 else ("ghost" if r < 0.15 else rng.choice(nodes)["name"])
+    return groups, pods, nodes, now_s * 1_000_000_000

@@ -11,7 +11,7 @@ import pytest
 from builders import build_test_node, build_test_nodes, build_test_pod, build_test_pods, unix_ns
 from oracle import oracle as O
 from oracle import soa
-from randobj import make_groups, make_nodes, make_pods, make_states, make_trackers
+from randobj import make_groups, make_nodes, make_pods, make_reaping_cluster, make_states, make_trackers
 
 pytestmark = pytest.mark.gpu
 soa.build()
@@ -444,24 +444,6 @@ def test_incremental_events_vs_literal(esc, seed):
 
 
 # ------------------------------------------------ scale-down reaping (§8f rank 2)
-def _reaping_cluster(rng, G, n_pods, n_nodes):
-    groups = make_groups(rng, G, with_default=rng.random() < 0.7)
-    pods = make_pods(rng, n_pods, groups, big_frac=0.0)
-    nodes = make_nodes(rng, n_nodes, groups, big_frac=0.0)
-    now_s = 1_700_000_000
-    for nd in nodes:
-        if rng.random() < 0.4 and "atlassian.com/escalator" not in nd["taints"]:
-            nd["taints"] = nd["taints"] + ["atlassian.com/escalator"]
-        nd["taint_value"] = rng.choice([str(now_s - rng.randrange(0, 900)), str(now_s - rng.randrange(0, 900)),
-                                        "+%d" % (now_s - 400), "bad", "", "-5", "99999999999999999999", None])
-        if rng.random() < 0.1:
-            nd["annotations"] = {"atlassian.com/no-delete": rng.choice(["true", ""])}
-    for p in pods:
-        r = rng.random()
-        p["node_name"] = "" if r < 0.1 else ("ghost" if r < 0.15 else rng.choice(nodes)["name"])
-    return groups, pods, nodes, now_s * 1_000_000_000
-
-
 def _check_reaping(ctx, groups, pods, nodes, trackers, now_ns, soft, hard):
     res = ctx.try_remove(now_ns, soft, hard)
     for g, grp in enumerate(groups):
@@ -487,7 +469,7 @@ def test_try_remove_tainted_vs_literal(esc, seed):
     from escalator_amd.objects import placement
     rng = random.Random(9100 + seed)
     G = rng.choice([1, 4, 12])
-    groups, pods, nodes, now_ns = _reaping_cluster(rng, G, rng.choice([0, 300, 1500]), rng.choice([5, 60, 200]))
+    groups, pods, nodes, now_ns = make_reaping_cluster(rng, G, rng.choice([0, 300, 1500]), rng.choice([5, 60, 200]))
     trackers = make_trackers(rng, groups, nodes)
     ctx = esc.Context(groups)
     P, N = ctx.pack(pods, nodes, trackers)

@@ -9,7 +9,7 @@ import pytest
 
 from oracle import oracle as O
 from oracle import soa
-from randobj import make_groups, make_nodes, make_pods, make_states, make_trackers
+from randobj import make_groups, make_nodes, make_pods, make_reaping_cluster, make_states, make_trackers
 
 soa.build()
 
@@ -75,6 +75,31 @@ def test_packer_c_oracle_vs_literal(seed):
         tn = L["tainted"]
         want = [tn[i] for i in O.newest_first([nodes[i]["created_ns"] for i in tn])]
         assert list(soa.order(N, groups, g, 1)) == want
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_c_oracle_try_remove_vs_literal(seed):
+    """orc_try_remove (used at full sizes) equals the fixture-pinned literal
+    TryRemoveTaintedNodes on random clusters, through the packer's pod / node order."""
+    from escalator_amd.objects import placement
+    rng = random.Random(4400 + seed)
+    G = rng.choice([1, 4, 12])
+    groups, pods, nodes, now_ns = make_reaping_cluster(rng, G, rng.choice([0, 200, 800]), rng.choice([5, 50, 150]))
+    trackers = make_trackers(rng, groups, nodes)
+    P, N = _ctx(groups).pack(pods, nodes, trackers)
+    pn, ts, nd = placement(pods, nodes)
+    for g, grp in enumerate(groups):
+        soft, hard = rng.choice([0, 60, 300]) * 10**9, rng.choice([300, 900]) * 10**9
+        L = O.scale_node_group(grp, {}, pods, nodes, tracker=trackers.get(g, []))
+        pods_g = O.filtered_list(pods, O.group_pod_filter(grp))
+        all_nodes = [n for n in nodes
+                     if O.new_node_label_filter_func(grp.get("label_key", ""), grp.get("label_value", ""))(n)]
+        tainted = L["tainted"]
+        neg, rem, ks = O.try_remove_tainted_nodes(grp, [nodes[i] for i in tainted], pods_g, all_nodes, now_ns,
+                                                  soft, hard, bool(grp.get("dry_mode")))
+        res, idx = soa.try_remove(P, N, groups, pn, ts, nd, g, now_ns, soft, hard)
+        assert res == (len(tainted), -neg, rem), g
+        assert list(idx) == [tainted[k] for k in ks], g
 
 
 def test_packer_list_mode_fixtures(golden):
