@@ -149,6 +149,8 @@ _SIGS = {
     "esc_pods_upsert": (i32, [VP, P(i64), P(PodSoA)]),
     "esc_pods_delete": (i32, [VP, P(i64), i64]),
     "esc_nodes_update": (i32, [VP, P(i64), i64, P(u32), P(i64), P(i64)]),
+    "esc_tracker_update": (i32, [VP, i32, P(i64), i64, P(i64), i64]),
+    "esc_tracker_list": (i32, [VP, i32, P(i64), i64, P(i64)]),
     "esc_load_placement": (i32, [VP, P(u32), P(i64), P(C.c_uint8)]),
     "esc_try_remove": (i32, [VP, i64, P(i64), P(i64), P(Removal)]),
     "esc_removal_nodes": (i32, [VP, i32, P(i64), i64, P(i64)]),

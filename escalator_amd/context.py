@@ -195,6 +195,24 @@ class Context:
                                           c_.ctypes.data_as(C.POINTER(C.c_int64)),
                                           m.ctypes.data_as(C.POINTER(C.c_int64))), "esc_nodes_update")
 
+    def tracker_update(self, group: int, add=(), remove=()):
+        """Dry-mode taintTracker change of one group in place (esc_tracker_update): the
+        nodes untaintNewestN deletes (scale_up.go:146-158), then the ones taintOldestN
+        appends (scale_down.go:197-200), as snapshot node indices."""
+        a = np.ascontiguousarray(add, np.int64)
+        r = np.ascontiguousarray(remove, np.int64)
+        L.check(self.lib.esc_tracker_update(self.handle, group, a.ctypes.data_as(C.POINTER(C.c_int64)), len(a),
+                                            r.ctypes.data_as(C.POINTER(C.c_int64)), len(r)), "esc_tracker_update")
+
+    def tracker_list(self, group: int) -> np.ndarray:
+        """Snapshot indices of the nodes `group`'s tracker holds, ascending."""
+        n = C.c_int64()
+        L.check(self.lib.esc_tracker_list(self.handle, group, None, 0, C.byref(n)), "esc_tracker_list")
+        out = np.zeros(n.value, np.int64)
+        L.check(self.lib.esc_tracker_list(self.handle, group, out.ctypes.data_as(C.POINTER(C.c_int64)), len(out),
+                                          C.byref(n)), "esc_tracker_list")
+        return out
+
     def stream_bytes(self) -> tuple[int, int]:
         """Algorithmic HBM bytes one decision streams on this rank: (K1 pods, K2 nodes)."""
         a, b = C.c_int64(), C.c_int64()

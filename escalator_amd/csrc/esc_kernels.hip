@@ -306,8 +306,10 @@ __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const 
                                       const PodClass& C, int64_t a, int64_t b, uint32_t lane) {
     constexpr int L = 5 + 4 * R + NXP;                   // 16-B loads per lane per tile
     // slots that fit the VGPR budget: 16 waves per CU leave 128 VGPRs a wave, 8 leave 256
-    constexpr int DS = NW >= 16 ? (L <= 7 ? 3 : (L <= 10 ? 2 : 1))
-                                : (4 * L * 4 <= 176 ? 4 : (4 * L * 3 <= 176 ? 3 : (4 * L * 2 <= 176 ? 2 : 1)));
+    constexpr int DS0 = NW >= 16 ? (L <= 7 ? 3 : (L <= 10 ? 2 : 1))
+                                 : (4 * L * 4 <= 176 ? 4 : (4 * L * 3 <= 176 ? 3 : (4 * L * 2 <= 176 ? 2 : 1)));
+    // timing knobs (ABLATE bits 6/7): cap the slots in flight at 2 / 3
+    constexpr int DS = (ABLATE & 64) ? (DS0 < 2 ? DS0 : 2) : ((ABLATE & 128) ? (DS0 < 3 ? DS0 : 3) : DS0);
     KTile<R, NXP> T[DS];
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
@@ -1596,6 +1598,8 @@ hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int
     switch (variant) {
         case 1: ESC_K1(512, 0, 2); break;
         case 2: ESC_K1(1024, 0, 3); break;
+        case 3: ESC_K1(512, 64, 3); break;       // <= 2 K tiles in flight per wave
+        case 4: ESC_K1(512, 128, 3); break;      // <= 3 K tiles in flight per wave
         // Timing-only ablations (wrong results; scripts/k1_variants.py), see k_pod_reduce.
         case 9: ESC_K1(512, 1, 3); break;        // LDS atomics replaced by a sink
         case 10: ESC_K1(512, 2, 3); break;       // C tiles only

@@ -184,6 +184,9 @@ struct esc_ctx {
     std::vector<int64_t> h_ncpu, h_nmem;
     std::vector<uint32_t> ne_off, ne_pos;                     // node -> its pair-major entry positions
     std::vector<GroupNode> h_gnode;
+    // dry-mode taintTracker mirror (§8f rank 4): (node << 32 | group), sorted, unique
+    std::vector<uint64_t> h_trk;
+    int64_t trk_cap = 0;                                      // device capacity of trk_node/_group
     // scale-down reaping (§8f rank 2): pods bound to nodes, per-node taint times
     bool placed = false;                                      // pod binding current
     bool node_removal = false;                                // taint times / no-delete loaded
@@ -1031,6 +1034,9 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     c->n_nodes = n;
     c->n_xl = s->n_xl;
     c->n_trk = s->n_trk;
+    c->trk_cap = s->n_trk;
+    c->h_trk.resize(s->n_trk);
+    for (int64_t k = 0; k < s->n_trk; ++k) c->h_trk[k] = ((uint64_t)(uint32_t)s->trk_node[k] << 32) | (uint32_t)s->trk_group[k];
     c->node_lo = lo;
     c->node_hi = hi;
     c->ts_min = tmin;
@@ -1347,6 +1353,50 @@ void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
     --c->live_pods;
 }
 
+// Writes the host mirrors (h_nflags / h_ncpu / h_nmem) of nodes `ids` to the device:
+// the node table, the nodes' pair-major K2 entries, allNodes[0]'s cached allocatable,
+// and the K5 membership list (re-listed: order and counts depend on creation times and
+// labels only, both unchanged).
+int32_t patch_nodes(esc_ctx* c, const std::vector<int64_t>& ids) {
+    c->rm_valid = false;
+    enum : uint32_t { NT_FLAGS = 0, NT_EFLAGS = 1, NT_CPU = 6, NT_MEM = 7, NT_ECPU = 8, NT_EMEM = 9 };
+    Patches P;
+    bool first_changed = false;
+    for (int64_t j : ids) {
+        const uint32_t f = c->h_nflags[j];
+        const uint64_t cpu = (uint64_t)c->h_ncpu[j], mem = (uint64_t)c->h_nmem[j];
+        P.add(NT_FLAGS, j, f);
+        P.add(NT_CPU, j, cpu);
+        P.add(NT_MEM, j, mem);
+        for (uint32_t e = c->ne_off[j]; e < c->ne_off[j + 1]; ++e) {
+            P.add(NT_EFLAGS, c->ne_pos[e], f);
+            P.add(NT_ECPU, c->ne_pos[e], cpu);
+            P.add(NT_EMEM, c->ne_pos[e], mem);
+        }
+    }
+    for (GroupNode& g : c->h_gnode)                  // allNodes[0]'s allocatable (controller.go:208)
+        if (g.first != INT64_MAX && (g.first_cpu != c->h_ncpu[g.first] || g.first_mem != c->h_nmem[g.first])) {
+            g.first_cpu = c->h_ncpu[g.first];
+            g.first_mem = c->h_nmem[g.first];
+            first_changed = true;
+        }
+    PatchTargets t{};
+    t.u32[NT_FLAGS] = c->nodes.flags; t.u32[NT_EFLAGS] = c->nodes.e_flags;
+    t.i64[NT_CPU - 6] = c->nodes.cpu; t.i64[NT_MEM - 6] = c->nodes.mem;
+    t.i64[NT_ECPU - 6] = c->nodes.e_cpu; t.i64[NT_EMEM - 6] = c->nodes.e_mem;
+    int32_t rc = apply_patches(c, P, {t});
+    if (rc) return rc;
+    if (first_changed)
+        HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
+    HIP_TRY(launch_memb_expand(node_dev(c), group_dev(c), c->d_age, c->memb_blocks, c->d_cnt, c->d_e_node,
+                               c->d_e_grp, c->d_e_flags, c->stream));
+    HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
+                                c->d_g_grp, c->d_g_flags, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->sorted = false;
+    return ESC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1458,52 +1508,112 @@ int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32
     if (!c || n < 0 || (n > 0 && (!ids || !flags || !cpu || !mem))) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->nodes_loaded) return ESC_E_STATE;
-    const uint32_t mutable_bits = ESC_NF_UNSCHED | ESC_NF_TAINTED;
+    // the tracker bit is the context's (esc_tracker_update), whatever the caller packed
+    const uint32_t mutable_bits = ESC_NF_UNSCHED | ESC_NF_TAINTED | ESC_NF_TRACKED;
     for (int64_t i = 0; i < n; ++i) {
         if (ids[i] < 0 || ids[i] >= c->n_nodes) return ESC_E_INVAL;
-        if ((flags[i] ^ c->h_nflags[ids[i]]) & ~mutable_bits) return ESC_E_INVAL;   // labels / tracker: reload
+        if ((flags[i] ^ c->h_nflags[ids[i]]) & ~mutable_bits) return ESC_E_INVAL;   // labels: reload
     }
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->rm_valid = false;
-    enum : uint32_t { NT_FLAGS = 0, NT_EFLAGS = 1, NT_CPU = 6, NT_MEM = 7, NT_ECPU = 8, NT_EMEM = 9 };
-    Patches P;
-    bool first_changed = false;
+    std::vector<int64_t> touched(ids, ids + n);
     for (int64_t i = 0; i < n; ++i) {
         const int64_t j = ids[i];
-        c->h_nflags[j] = flags[i];
+        c->h_nflags[j] = (flags[i] & ~ESC_NF_TRACKED) | (c->h_nflags[j] & ESC_NF_TRACKED);
         c->h_ncpu[j] = cpu[i];
         c->h_nmem[j] = mem[i];
-        P.add(NT_FLAGS, j, flags[i]);
-        P.add(NT_CPU, j, (uint64_t)cpu[i]);
-        P.add(NT_MEM, j, (uint64_t)mem[i]);
-        for (uint32_t e = c->ne_off[j]; e < c->ne_off[j + 1]; ++e) {
-            P.add(NT_EFLAGS, c->ne_pos[e], flags[i]);
-            P.add(NT_ECPU, c->ne_pos[e], (uint64_t)cpu[i]);
-            P.add(NT_EMEM, c->ne_pos[e], (uint64_t)mem[i]);
-        }
     }
-    for (GroupNode& g : c->h_gnode)                  // allNodes[0]'s allocatable (controller.go:208)
-        if (g.first != INT64_MAX && (g.first_cpu != c->h_ncpu[g.first] || g.first_mem != c->h_nmem[g.first])) {
-            g.first_cpu = c->h_ncpu[g.first];
-            g.first_mem = c->h_nmem[g.first];
-            first_changed = true;
-        }
-    PatchTargets t{};
-    t.u32[NT_FLAGS] = c->nodes.flags; t.u32[NT_EFLAGS] = c->nodes.e_flags;
-    t.i64[NT_CPU - 6] = c->nodes.cpu; t.i64[NT_MEM - 6] = c->nodes.mem;
-    t.i64[NT_ECPU - 6] = c->nodes.e_cpu; t.i64[NT_EMEM - 6] = c->nodes.e_mem;
-    int32_t rc = apply_patches(c, P, {t});
-    if (rc) return rc;
-    if (first_changed)
-        HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
-    // the age index's membership list carries the node flags: re-list it (the order and
-    // the membership counts depend on creation times and labels only, both unchanged)
-    HIP_TRY(launch_memb_expand(node_dev(c), group_dev(c), c->d_age, c->memb_blocks, c->d_cnt, c->d_e_node,
-                               c->d_e_grp, c->d_e_flags, c->stream));
-    HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
-                                c->d_g_grp, c->d_g_flags, c->stream));
+    return patch_nodes(c, touched);
+}
+
+// Dry-mode taintTracker bookkeeping (§8f rank 4).  The reference keeps per group a slice
+// of node names: taintOldestN appends in dry mode (scale_down.go:197-200), untaintNewestN
+// deletes the first equal name (scale_up.go:146-158) and filterNodes does a linear name
+// search per node (controller.go:126-138).  Here the tracker is the sorted (node, group)
+// list the kernels binary-index through trk_start; an update rewrites that list (a few
+// KB), and only the nodes whose ESC_NF_TRACKED bit flips are patched in the node table,
+// the pair-major entries and the K5 membership list.
+int32_t esc_tracker_update(esc_ctx* c, int32_t group, const int64_t* add, int64_t n_add, const int64_t* rm,
+                           int64_t n_rm) {
+    if (!c || n_add < 0 || n_rm < 0 || (n_add > 0 && !add) || (n_rm > 0 && !rm)) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->nodes_loaded) return ESC_E_STATE;
+    if (group < 0 || group >= c->gi.G) return ESC_E_INVAL;
+    auto key = [&](int64_t j) { return ((uint64_t)(uint32_t)j << 32) | (uint32_t)group; };
+    for (int64_t i = 0; i < n_rm; ++i) if (rm[i] < 0 || rm[i] >= c->n_nodes) return ESC_E_INVAL;
+    for (int64_t i = 0; i < n_add; ++i) if (add[i] < 0 || add[i] >= c->n_nodes) return ESC_E_INVAL;
+    // removals first (absent names are ignored, as untaintNewestN's deleteIndex == -1), then
+    // additions (a node already tracked by the group, or added twice, is refused: the
+    // reference only appends untainted, i.e. untracked, nodes)
+    std::vector<uint64_t> rk(n_rm), ak(n_add);
+    for (int64_t i = 0; i < n_rm; ++i) rk[i] = key(rm[i]);
+    for (int64_t i = 0; i < n_add; ++i) ak[i] = key(add[i]);
+    std::sort(rk.begin(), rk.end());
+    std::sort(ak.begin(), ak.end());
+    if (std::adjacent_find(ak.begin(), ak.end()) != ak.end()) return ESC_E_INVAL;
+    std::vector<uint64_t> kept;
+    kept.reserve(c->h_trk.size() + ak.size());
+    std::vector<int64_t> touched;
+    for (uint64_t k : c->h_trk) {
+        if (std::binary_search(rk.begin(), rk.end(), k)) touched.push_back((int64_t)(k >> 32));
+        else kept.push_back(k);
+    }
+    for (uint64_t k : ak)
+        if (std::binary_search(kept.begin(), kept.end(), k)) return ESC_E_INVAL;
+    for (uint64_t k : ak) touched.push_back((int64_t)(k >> 32));
+    std::vector<uint64_t> next(kept.size() + ak.size());
+    std::merge(kept.begin(), kept.end(), ak.begin(), ak.end(), next.begin());
+    const int64_t nt = (int64_t)next.size();
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    NodeBuf& b = c->nodes;
+    if (nt > c->trk_cap) {
+        const int64_t cap = std::max<int64_t>({nt, 2 * c->trk_cap, 1024});
+        dfree(b.trk_node); dfree(b.trk_group);
+        b.trk_node = nullptr; b.trk_group = nullptr;
+        HIP_TRY(dalloc(&b.trk_node, cap)); HIP_TRY(dalloc(&b.trk_group, cap));
+        c->trk_cap = cap;
+    }
+    std::vector<int32_t> tn(std::max<int64_t>(nt, 1)), tg(std::max<int64_t>(nt, 1));
+    std::vector<uint32_t> ts(std::max<int64_t>(c->n_nodes, 1), NONE);
+    for (int64_t k = nt - 1; k >= 0; --k) {
+        tn[k] = (int32_t)(next[k] >> 32);
+        tg[k] = (int32_t)(uint32_t)next[k];
+        ts[tn[k]] = (uint32_t)k;
+    }
+    if (nt) {
+        HIP_TRY(hipMemcpy(b.trk_node, tn.data(), nt * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(b.trk_group, tg.data(), nt * 4, hipMemcpyHostToDevice));
+    }
+    HIP_TRY(hipMemcpy(b.trk_start, ts.data(), ts.size() * 4, hipMemcpyHostToDevice));
+    c->h_trk.swap(next);
+    c->n_trk = nt;
+    drop_graphs(c);                                  // K2's grid and NodeDev carry n_trk
+    // ESC_NF_TRACKED = tracked by some group (controller.go:128 is per group; the kernels
+    // confirm the group through the list)
+    std::vector<int64_t> flip;
+    std::sort(touched.begin(), touched.end());
+    touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+    for (int64_t j : touched) {
+        const bool on = ts[j] != NONE;
+        const uint32_t f = on ? (c->h_nflags[j] | ESC_NF_TRACKED) : (c->h_nflags[j] & ~ESC_NF_TRACKED);
+        if (f != c->h_nflags[j]) { c->h_nflags[j] = f; flip.push_back(j); }
+    }
     c->sorted = false;
+    c->rm_valid = false;
+    return flip.empty() ? ESC_OK : patch_nodes(c, flip);
+}
+
+int32_t esc_tracker_list(const esc_ctx* c, int32_t group, int64_t* idx_out, int64_t cap, int64_t* n_out) {
+    if (!c || !n_out || cap < 0 || (cap > 0 && !idx_out)) return ESC_E_INVAL;
+    if (group < 0 || group >= c->gi.G) return ESC_E_INVAL;
+    int64_t m = 0;
+    for (uint64_t k : c->h_trk)
+        if ((int32_t)(uint32_t)k == group) {
+            if (m < cap) idx_out[m] = (int64_t)(k >> 32);
+            ++m;
+        }
+    *n_out = m;
     return ESC_OK;
 }
 

@@ -381,13 +381,29 @@ int32_t esc_stage_times(esc_ctx* ctx, double* ms_out, int32_t n);
  * load, reserves them); a batch that does not fit in place — spare exhausted, a pod
  * with > 3 container records or > 3 extra pairs, or a signature absent at load —
  * returns ESC_E_LIMIT with nothing applied, and the caller reloads.  Node events may
- * change Spec.Unschedulable, the escalator taint and allocatable; label, creation-time
- * or tracker changes need esc_load_nodes.  Every call completes before returning.    */
+ * change Spec.Unschedulable, the escalator taint and allocatable; label or creation-time
+ * changes need esc_load_nodes (tracker changes: esc_tracker_update).  Every call
+ * completes before returning.                                                       */
 int32_t esc_set_spare(esc_ctx* ctx, double fraction);       /* spare slots per K class, e.g. 0.05 */
 int32_t esc_pods_upsert(esc_ctx* ctx, const int64_t* ids, const esc_pod_soa* pods);
 int32_t esc_pods_delete(esc_ctx* ctx, const int64_t* ids, int64_t n);
 int32_t esc_nodes_update(esc_ctx* ctx, const int64_t* ids, int64_t n, const uint32_t* flags,
                          const int64_t* cpu_m, const int64_t* mem_b);
+
+/* ------------------------------------------- dry-mode taintTracker (§8f rank 4)
+ * nodeGroup.taintTracker (controller.go:35) as interned (node, group) pairs on the
+ * device.  In dry mode taintOldestN appends the names it "taints" (scale_down.go:197-200)
+ * and untaintNewestN deletes them (scale_up.go:146-158); filterNodes then splits a dry
+ * group's nodes by tracker membership (controller.go:126-138).  esc_tracker_update applies
+ * such a change for one group in place (no reload): `remove` first — nodes the group does
+ * not track are ignored, like untaintNewestN's deleteIndex == -1 — then `add`; adding a
+ * node the group already tracks (or twice) is ESC_E_INVAL with nothing applied (the
+ * reference only appends untracked nodes, so its slice never holds a duplicate).  The
+ * node's ESC_NF_TRACKED bit is maintained here: esc_nodes_update ignores the caller's.
+ * esc_tracker_list returns the group's tracked node indices, ascending.              */
+int32_t esc_tracker_update(esc_ctx* ctx, int32_t group, const int64_t* add, int64_t n_add,
+                           const int64_t* remove, int64_t n_remove);
+int32_t esc_tracker_list(const esc_ctx* ctx, int32_t group, int64_t* idx_out, int64_t cap, int64_t* n_out);
 
 /* ------------------------------------------ scale-down reaping (§8f rank 2)
  * TryRemoveTaintedNodes (pkg/controller/scale_down.go:51-136) with NodeEmpty /

@@ -46,6 +46,36 @@ __global__ __launch_bounds__(THREADS) void k_chunk(const uint4* __restrict__ p, 
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// S parallel streams (struct-of-arrays fields): the buffer is S equal arrays and every
+// workgroup reads the same relative share of each, U rounds of S loads in flight — the
+// K1 K-tile shape (flags, cpu0, pair0, mem0 x2, records) against one contiguous stream.
+template <int THREADS, int S, int U>
+__global__ __launch_bounds__(THREADS) void k_multi(const uint4* __restrict__ p, int64_t n16, uint32_t* out) {
+    const int64_t na = n16 / S;
+    const int64_t per = (na + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * per;
+    const int64_t hi = lo + per < na ? lo + per : na;
+    uint32_t acc = 0;
+    for (int64_t b = lo + threadIdx.x; b < hi; b += (int64_t)THREADS * U) {
+        uint4 v[U][S];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = b + (int64_t)u * THREADS;
+            const int64_t j = i < hi ? i : lo;
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+                const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p + (int64_t)k * na + j));
+                v[u][k] = make_uint4(t.x, t.y, t.z, t.w);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < S; ++k) acc ^= v[u][k].x ^ v[u][k].y ^ v[u][k].z ^ v[u][k].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 // Grid-stride (every wave walks the whole buffer at a stride of the grid).
 template <int THREADS, int U>
 __global__ __launch_bounds__(THREADS) void k_stride(const uint4* __restrict__ p, int64_t n16, uint32_t* out) {
@@ -116,6 +146,17 @@ int main() {
     RUN_CHUNK(256, 8, false, 8);
     RUN_CHUNK(256, 4, false, 16);
     RUN_CHUNK(256, 4, false, 64);
+    RUN_CHUNK(512, 4, true, 1);
+    RUN_CHUNK(512, 8, true, 1);
+#define RUN_MULTI(T, S, U)                                                                                \
+    rep("multi_t" #T "_s" #S "_u" #U,                                                                    \
+        time_ms([&] { hipLaunchKernelGGL((k_multi<T, S, U>), dim3(cus), dim3(T), 0, 0, p, n16, out); }, 10))
+    RUN_MULTI(512, 1, 4);
+    RUN_MULTI(512, 5, 1);
+    RUN_MULTI(512, 5, 2);
+    RUN_MULTI(512, 5, 4);
+    RUN_MULTI(512, 9, 2);
+    RUN_MULTI(1024, 5, 2);
 #define RUN_STRIDE(T, U, WPC)                                                                             \
     rep("stride_t" #T "_u" #U "_wgpercu" #WPC,                                                           \
         time_ms([&] { hipLaunchKernelGGL((k_stride<T, U>), dim3(cus * WPC), dim3(T), 0, 0, p, n16, out); }, 10))

@@ -495,3 +495,73 @@ def test_try_remove_tainted_vs_literal(esc, seed):
         del pods[0]
         ctx.load_placement(np.r_[np.uint32(0xFFFFFFFF), pn[1:]], ts, nd)
         _check_reaping(ctx, groups, pods, nodes, trackers, now_ns, np.full(G, 60 * 10**9), np.full(G, 4000 * 10**9))
+
+
+# ------------------------------------------------ dry-mode taintTracker (§8f rank 4)
+@pytest.mark.parametrize("seed", range(4))
+def test_tracker_updates_vs_literal(esc, seed):
+    """Dry-mode bookkeeping in place (esc_tracker_update): each round every dry group
+    "untaints" its newest tracked members and "taints" its oldest untracked ones, as
+    untaintNewestN / taintOldestN do in dry mode (scale_up.go:146-158,
+    scale_down.go:197-200); decisions, both orderings and the tracker lists then equal the
+    literal oracle over the updated name slices.  Wet groups' trackers are ignored."""
+    rng = random.Random(9700 + seed)
+    G = rng.choice([3, 8])
+    groups = make_groups(rng, G, with_default=True)
+    for g in rng.sample(range(G), max(1, G // 2)):
+        groups[g]["dry_mode"] = True
+    pods = make_pods(rng, 400, groups, big_frac=0.0)
+    nodes = make_nodes(rng, 80, groups, big_frac=0.0)
+    states = make_states(rng, G)
+    trackers = make_trackers(rng, groups, nodes)
+    ctx = esc.Context(groups)
+    P, N = ctx.pack(pods, nodes, trackers)
+    ctx.load(P, N)
+    idx = {nd["name"]: i for i, nd in enumerate(nodes)}
+    names = {g: list(trackers.get(g, [])) for g in range(G)}
+    ctx.use_graph(True)
+    for rnd in range(4):
+        tot, dec = ctx.decide_all(states)
+        ctx.sort_nodes()
+        for g in range(G):
+            L = O.scale_node_group(groups[g], states[g], pods, nodes, tracker=names[g])
+            t, d = tot[g], dec[g]
+            assert (t["n_untainted"], t["n_tainted"], t["n_cordoned"]) == \
+                (L["n_untainted"], L["n_tainted"], L["n_cordoned"]), (rnd, g)
+            assert (t["node_cpu_m"], t["node_mem_b"]) == (L["node_cpu_m"], L["node_mem_b"]), (rnd, g)
+            assert int(d["delta"]) == L["delta"] and _bits(d["cpu_pct"]) == _bits(L["cpu_pct"]), (rnd, g)
+            unt, tnt = L["untainted"], L["tainted"]
+            assert list(ctx.group_order(g, 0)) == [unt[i] for i in O.oldest_first([nodes[i]["created_ns"] for i in unt])]
+            assert list(ctx.group_order(g, 1)) == [tnt[i] for i in O.newest_first([nodes[i]["created_ns"] for i in tnt])]
+            assert list(ctx.tracker_list(g)) == sorted({idx[n] for n in names[g] if n in idx}), (rnd, g)
+        changes = []                                 # from this round's orderings
+        for g in range(G):
+            if groups[g].get("dry_mode"):
+                rm = list(ctx.group_order(g, 1))[:rng.randrange(0, 4)]
+                ad = list(ctx.group_order(g, 0))[:rng.randrange(0, 5)]
+            else:                                    # a wet group's tracker changes nothing
+                rm = rng.sample(range(len(nodes)), 2)
+                ad = [j for j in rng.sample(range(len(nodes)), 3) if nodes[j]["name"] not in names[g]]
+            changes.append((rm, ad))
+        for g, (rm, ad) in enumerate(changes):
+            ctx.tracker_update(g, add=ad, remove=rm)
+            for j in rm:                             # untaintNewestN: delete the first equal name
+                if nodes[j]["name"] in names[g]:
+                    names[g].remove(nodes[j]["name"])
+            names[g] += [nodes[j]["name"] for j in ad]
+        # node events keep the context's tracker bit whatever the caller packed
+        nid = rng.sample(range(len(nodes)), 6)
+        for j in nid:
+            nodes[j]["taints"] = ["atlassian.com/escalator"] if rng.random() < 0.5 else []
+        _, Nn = ctx.pack([], nodes)
+        ctx.nodes_update(nid, Nn["flags"][nid], Nn["cpu"][nid], Nn["mem"][nid])
+    # refused whole: re-adding a tracked node; removing an untracked one is a no-op
+    g = next((g for g in range(G) if ctx.tracker_list(g).size), None)
+    if g is not None:
+        before = list(ctx.tracker_list(g))
+        free = [j for j in range(len(nodes)) if j not in before]
+        with pytest.raises(RuntimeError):
+            ctx.tracker_update(g, add=free[:1] + before[:1])
+        assert list(ctx.tracker_list(g)) == before
+        ctx.tracker_update(g, remove=free[:3])
+        assert list(ctx.tracker_list(g)) == before
