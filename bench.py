@@ -6,7 +6,7 @@ of every group's decision to pinned host memory.  Default workload: BASELINE con
 (100M pods / 1M nodes / 10k node groups), sharded over the N GPUs (strong scaling: the
 snapshot is fixed, each GPU streams 1/N of it).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4|2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 4|2|3|5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -29,7 +29,7 @@ CONFIGS = {
 }
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # PMC passes (scripts/pmc_job.sh) of the kernels as built at this tag: HBM bytes per launch
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v5", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v8", "pmc_summary.json")
 
 
 def log(*a):
@@ -94,38 +94,100 @@ def cpu_baseline(cfg, G, seconds=12.0):
     }
 
 
+def init_dist():
+    """RANK / WORLD_SIZE / LOCAL_RANK from the launcher; one process per GPU over RCCL.
+    ESC_BENCH_BACKEND / ESC_BENCH_DEVICE: rehearsal knobs (gloo, every rank on one device)
+    for exercising the N > 1 path on a one-GPU box; the driver's runs use the defaults."""
+    import torch
+    rank, world, local = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1), ("LOCAL_RANK", 0)))
+    backend = os.environ.get("ESC_BENCH_BACKEND", "nccl")
+    local = int(os.environ.get("ESC_BENCH_DEVICE", local))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, world, local, dist, backend
+
+
 def bench_order(args):
     """BASELINE config #5: the scale-down / scale-up orderings over 10M nodes (taintOldestN
     scale_down.go:171, untaintNewestN scale_up.go:118).  Times (a) the per-decision ordering
-    (esc_sort_nodes: classify every membership, stable partition by (group, class)) and
-    (b) the age-index build it relies on (esc_build_age_index: LSD radix sort of the 10M
-    creation times + the memberships in age order, once per snapshot)."""
+    (esc_sort_nodes: classify every membership, stable 3-way split by class inside each
+    group's run) and (b) the age-index build it relies on (esc_build_age_index: LSD radix
+    sort of the creation times + the memberships in age order, once per snapshot).  On N
+    GPUs every rank orders its contiguous 1/N of the nodes (strong scaling); the taint /
+    untaint selections are the k-way merge of the ranks' per-group prefixes
+    (escalator_amd.dist.gather_orders, one all_gather), parity-checked against the
+    whole-snapshot order."""
     import numpy as np
+    import torch
     import escalator_amd as esc
+    from escalator_amd.dist import gather_orders, shard_range
     from oracle import soa
-    N, G = 10_000_000, 100
-    s = esc.Synth(100_000, N, G, config=5, seed=0xE5CA1A7E00000005, threads=16)
-    ctx = esc.Context(s)
-    ctx.load_synth(s)
+    rank, world, local, dist, backend = init_dist()
+    N, G, P = 10_000_000, 100, 100_000
+    lo, hi = shard_range(P, rank, world)
+    nlo, nhi = shard_range(N, rank, world)
+    s = esc.Synth(P, N, G, config=5, seed=0xE5CA1A7E00000005, p_lo=lo, p_hi=hi, threads=16)
+    ctx = esc.Context(s, device=local, rank=rank, world=world)
+    ctx.load_synth(s, pod_offset=lo, node_lo=nlo, node_hi=nhi)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
 
     def timed(fn, k):
         for _ in range(args.warmup):
             fn()
         ctx.sync()
+        torch.cuda.synchronize()
+        barrier()
         t0 = time.perf_counter()
         for _ in range(k):
             fn()
         ctx.sync()
-        return (time.perf_counter() - t0) / k * 1e3
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        if dist is not None:                      # max over ranks
+            e = torch.tensor([el], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+        return el / k * 1e3
 
     order_ms = timed(ctx.sort_nodes, args.steps)
     index_ms = timed(ctx.build_age_index, max(3, args.steps // 4))
     ctx.sort_nodes()
-    counts = [len(ctx.group_order(g, w)) for g in range(G) for w in (0, 1)]
-    nodes = s.nodes()
-    parity = all(np.array_equal(ctx.group_order(g, w), soa.order(nodes, s.groups, g, w)) for g in (0, 37, 99)
-                 for w in (0, 1))
     n_memb, R = ctx.order_info()
+    nodes = s.nodes()
+    check = (0, 37, 99)
+    if world == 1:
+        counts = [len(ctx.group_order(g, w)) for g in range(G) for w in (0, 1)]
+        parity = all(np.array_equal(ctx.group_order(g, w), soa.order(nodes, s.groups, g, w)) for g in check
+                     for w in (0, 1))
+        how = "bit-exact vs C oracle on groups 0, 37, 99 (both orders)"
+        sel_ms = None
+    else:
+        dev = torch.device("cuda", local) if backend == "nccl" else None
+        tot = torch.tensor([n_memb], dtype=torch.int64, device=dev if dev is not None else "cpu")
+        dist.all_reduce(tot)
+        n_memb = int(tot.item())
+        n_sel = 64
+        t0 = time.perf_counter()
+        merged = {w: gather_orders(ctx, w, n_sel, nodes["created_ns"], device=dev) for w in (0, 1)}
+        sel_ms = (time.perf_counter() - t0) * 1e3
+        counts = [len(merged[w][g]) for g in range(G) for w in (0, 1)]
+        parity = all(np.array_equal(merged[w][g], soa.order(nodes, s.groups, g, w, cap=n_sel)) for g in check
+                     for w in (0, 1))
+        how = ("merged first %d per group (all_gather of the ranks' prefixes) bit-exact vs the C oracle's "
+               "whole-snapshot order on groups 0, 37, 99 (both orders)" % n_sel)
+    if rank != 0:
+        dist.destroy_process_group()
+        return
     # bytes the ordering moves per membership: classify (node, group, flags) 12 read + class
     # 1 written; split: class 1 + node 4 read, node 4 written (esc_kernels.hip K5)
     order_bytes = n_memb * 22
@@ -135,24 +197,29 @@ def bench_order(args):
         "metric": "config5 node orderings: memberships ordered/sec per decision (taint/untaint selection)",
         "value": n_memb / (order_ms * 1e-3),
         "unit": "memberships/s",
-        "n_gpus": 1,
+        "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": order_ms,
         "higher_is_better": True,
+        "scaling": "strong",
         "dtype": "int64 keys",
         "data": "synthetic (esc_synth.cpp config 5: 10M nodes, 100 groups, unique ns creation times)",
         "config": {"workload": "config5: 10M nodes oldest-first / newest-first orderings, 100 node groups",
-                   "nodes": N, "node_groups": G, "memberships": n_memb},
+                   "nodes": N, "node_groups": G, "memberships": n_memb, "parallelism": "shard%d" % world},
         "roofline": {"bound": "hbm", "kernel": "per-decision ordering (k_ord_count + k_ord_bases + k_ord_scatter)",
-                     "achieved": order_bytes / (order_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": order_bytes / (order_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "bytes_per_decision": order_bytes},
+                     "achieved": order_bytes / (order_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                     "frac": order_bytes / (order_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
+                     "bytes_per_decision": order_bytes},
         "age_index_build": {"ms": index_ms, "nodes_per_s": N / (index_ms * 1e-3), "key_bits": R,
                             "lsd_passes": idx_passes, "GBps_moved": index_bytes / (index_ms * 1e-3) / 1e9},
+        "selection_merge_ms": sel_ms,
         "segments_nonempty": int(sum(1 for c in counts if c)),
-        "parity": "bit-exact vs C oracle on groups 0, 37, 99 (both orders)" if parity else "MISMATCH",
+        "parity": how if parity else "MISMATCH",
     }
     print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
 
 
 def main():
@@ -168,7 +235,6 @@ def main():
 
     if args.config == 5:
         return bench_order(args)
-    rank, world, local = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1), ("LOCAL_RANK", 0)))
     cfg = dict(CONFIGS[args.config], cfg=args.config)
     if args.pods:
         cfg["P"] = args.pods
@@ -180,18 +246,7 @@ def main():
     import escalator_amd as esc
     from escalator_amd.dist import Exchange, shard_range
 
-    # ESC_BENCH_BACKEND / ESC_BENCH_DEVICE: rehearsal knobs (gloo, every rank on one device)
-    # for exercising the N > 1 path on a one-GPU box; the driver's runs use the defaults.
-    backend = os.environ.get("ESC_BENCH_BACKEND", "nccl")
-    local = int(os.environ.get("ESC_BENCH_DEVICE", local))
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+    rank, world, local, dist, backend = init_dist()
 
     lo, hi = shard_range(P, rank, world)
     nlo, nhi = shard_range(N, rank, world)

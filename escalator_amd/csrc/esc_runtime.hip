@@ -827,6 +827,10 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         HIP_TRY(dalloc(&b.pair0, npad)); HIP_TRY(dalloc(&b.xc_cpu, nxc_dev)); HIP_TRY(dalloc(&b.xc_mem, nxc_dev));
         HIP_TRY(dalloc(&b.xp, nxp_dev)); HIP_TRY(dalloc(&b.xc_base, c_tiles + 1)); HIP_TRY(dalloc(&b.xp_base, c_tiles + 1));
         HIP_TRY(dalloc(&b.big, big.size())); HIP_TRY(dalloc(&b.cls, n_cls));
+        if (std::getenv("ESC_DEBUG_PTRS"))
+            fprintf(stderr, "[esc] replica %d flags %p cpu0 %p pair0 %p mem0 %p xc_cpu %p xc_mem %p xp %p\n", r,
+                    (void*)b.flags, (void*)b.cpu0, (void*)b.pair0, (void*)b.mem0, (void*)b.xc_cpu, (void*)b.xc_mem,
+                    (void*)b.xp);
         const hipMemcpyKind kind = r == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
         const PodBuf& a = c->pods[0];
         auto src = [&](const void* host, const void* dev) { return r == 0 ? host : dev; };

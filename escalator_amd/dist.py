@@ -70,3 +70,49 @@ def exchange_host(sum_arr, min_arr):
     dist.all_reduce(ts, op=dist.ReduceOp.SUM)
     dist.all_reduce(tm, op=dist.ReduceOp.MIN)
     return ts.numpy(), tm.numpy()
+
+
+# ------------------------------------------------ sharded orderings (config #5, 1-8 GPUs)
+def merge_orders(parts, created_ns, which: int, n: int):
+    """Global first `n` of one group's order from the ranks' local prefixes.
+
+    Every rank orders its contiguous node range (esc_sort_nodes over [lo, hi)) and
+    contributes the first `n` entries of its list; `which` 0 = untainted oldest-first
+    (taintOldestN, scale_down.go:171), 1 = tainted newest-first (untaintNewestN,
+    scale_up.go:118).  The global order is the k-way merge by creation time with ties by
+    ascending snapshot index — the single-rank tie rule — so the merged prefix equals the
+    single-GPU list bit for bit.  `parts` are int64 arrays of snapshot node indices."""
+    import numpy as np
+    idx = np.concatenate([np.asarray(p, np.int64) for p in parts]) if parts else np.zeros(0, np.int64)
+    if idx.size == 0:
+        return idx
+    t = np.asarray(created_ns, np.int64)[idx]
+    order = np.lexsort((idx, t if which == 0 else -t))   # -t: creation times are far from INT64_MIN
+    return idx[order[:n]]
+
+
+def gather_orders(ctx, which: int, n: int, created_ns, device=None):
+    """All ranks: each contributes the first `n` of every group's local order (one
+    all_gather of a [G, n + 1] int64 tensor: counts + indices, ≈ G·n·8 B per rank over
+    RCCL/xGMI or gloo); returns {group: merged global prefix} (identical on every rank)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    G = ctx.G
+    buf = np.full((G, n + 1), -1, np.int64)
+    for g in range(G):
+        loc = ctx.group_order(g, which, cap=n)[:n]
+        buf[g, 0] = len(loc)
+        buf[g, 1:1 + len(loc)] = loc
+    mine = torch.from_numpy(buf)
+    if device is not None:
+        mine = mine.to(device)
+    world = dist.get_world_size()
+    got = [torch.empty_like(mine) for _ in range(world)]
+    dist.all_gather(got, mine)
+    got = [x.cpu().numpy() for x in got]
+    out = {}
+    for g in range(G):
+        parts = [x[g, 1:1 + x[g, 0]] for x in got]
+        out[g] = merge_orders(parts, created_ns, which, n)
+    return out

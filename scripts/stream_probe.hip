@@ -76,6 +76,36 @@ __global__ __launch_bounds__(THREADS) void k_multi(const uint4* __restrict__ p, 
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// As k_multi, but stream k starts at k * (sp16 + ex16) (16-B units): power-of-two spacing
+// between the SoA arrays (ex16 = 0) against skewed bases — do separately allocated
+// arrays read at the same tile offset collide on HBM channels?
+template <int THREADS, int S, int U>
+__global__ __launch_bounds__(THREADS) void k_multi_sp(const uint4* __restrict__ p, int64_t na, int64_t sp16,
+                                                      int64_t ex16, uint32_t* out) {
+    const int64_t per = (na + gridDim.x - 1) / gridDim.x;
+    const int64_t lo = (int64_t)blockIdx.x * per;
+    const int64_t hi = lo + per < na ? lo + per : na;
+    uint32_t acc = 0;
+    for (int64_t b = lo + threadIdx.x; b < hi; b += (int64_t)THREADS * U) {
+        uint4 v[U][S];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = b + (int64_t)u * THREADS;
+            const int64_t j = i < hi ? i : lo;
+#pragma unroll
+            for (int k = 0; k < S; ++k) {
+                const v4u t = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p + (int64_t)k * (sp16 + ex16) + j));
+                v[u][k] = make_uint4(t.x, t.y, t.z, t.w);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < S; ++k) acc ^= v[u][k].x ^ v[u][k].y ^ v[u][k].z ^ v[u][k].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 // Grid-stride (every wave walks the whole buffer at a stride of the grid).
 template <int THREADS, int U>
 __global__ __launch_bounds__(THREADS) void k_stride(const uint4* __restrict__ p, int64_t n16, uint32_t* out) {
@@ -117,12 +147,13 @@ static float time_ms(F&& launch, int reps) {
 
 int main() {
     const int64_t bytes = 2400ll << 20;
+    const int64_t big = 3200ll << 20;                  // room for 5 streams 512 MB apart + skew
     const int64_t n16 = bytes / 16;
     uint4* p;
     uint32_t* out;
-    CK(hipMalloc(&p, bytes));
+    CK(hipMalloc(&p, big));
     CK(hipMalloc(&out, 4));
-    CK(hipMemset(p, 1, bytes));
+    CK(hipMemset(p, 1, big));
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     printf("{\"bytes\": %lld, \"cus\": %d, \"GBps\": {", (long long)bytes, cus);
@@ -157,6 +188,31 @@ int main() {
     RUN_MULTI(512, 5, 4);
     RUN_MULTI(512, 9, 2);
     RUN_MULTI(1024, 5, 2);
+    {   // 5 streams of 448 MB (2240 MB read) at 512 MB spacing + skew
+        const int64_t na = (448ll << 20) / 16, sp = (512ll << 20) / 16;
+        const int64_t mb = 2240ll << 20;
+        auto rep2 = [&](const char* name, float ms) {
+            printf("%s\"%s\": %.0f", first ? "" : ", ", name, mb / (ms * 1e-3) / 1e9);
+            first = false;
+            fflush(stdout);
+        };
+        for (int64_t ex : {0ll, 256ll, 4096ll, 65536ll, (1ll << 20) + 4096}) {
+            char name[64];
+            snprintf(name, sizeof name, "multi_sp512M_skew%lld_t512_s5_u2", (long long)ex);
+            rep2(name, time_ms([&] { hipLaunchKernelGGL((k_multi_sp<512, 5, 2>), dim3(cus), dim3(512), 0, 0, p, na, sp,
+                                                         ex / 16, out); }, 10));
+        }
+        // K1-like: arrays of 100M x 4 B rounded up to 2 MB (191 x 2 MB apart)
+        const int64_t sp191 = (191ll << 21) / 16, na191 = (382ll << 20) / 16;
+        const int64_t mb191 = 5 * (382ll << 20);
+        for (int64_t ex : {0ll, 4096ll}) {
+            char name[64];
+            snprintf(name, sizeof name, "multi_sp191x2M_skew%lld_t512_s5_u2", (long long)ex);
+            const float ms = time_ms([&] { hipLaunchKernelGGL((k_multi_sp<512, 5, 2>), dim3(cus), dim3(512), 0, 0, p, na191,
+                                                              sp191, ex / 16, out); }, 10);
+            printf(", \"%s\": %.0f", name, mb191 / (ms * 1e-3) / 1e9);
+        }
+    }
 #define RUN_STRIDE(T, U, WPC)                                                                             \
     rep("stride_t" #T "_u" #U "_wgpercu" #WPC,                                                           \
         time_ms([&] { hipLaunchKernelGGL((k_stride<T, U>), dim3(cus * WPC), dim3(T), 0, 0, p, n16, out); }, 10))

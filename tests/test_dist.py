@@ -57,3 +57,68 @@ def test_two_rank_exchange_equals_whole():
     sums = np.delete(t, [9, 10, 11], axis=1)
     assert np.array_equal(S[:, :-1], sums[:, :-1])        # flags column: OR semantics, all 0 here
     assert np.array_equal(F, want_first)
+
+
+class _RangeOrders:
+    """Stand-in for a context whose K5 streams nodes [lo, hi): group_order = the oracle's
+    order over that range (the GPU path is checked against the same oracle in test_gpu)."""
+
+    def __init__(self, nodes, groups, lo, hi):
+        self.nodes, self.groups, self.lo, self.hi, self.G = nodes, groups, lo, hi, len(groups)
+
+    def group_order(self, g, which, cap=None):
+        from oracle import soa
+        return soa.order(self.nodes, self.groups, g, which, self.lo, self.hi, cap)
+
+
+def _order_worker(rank, world, port, n, out):
+    import torch.distributed as dist
+    from escalator_amd.context import Synth
+    from escalator_amd.dist import gather_orders
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    N, G = 30_000, 12
+    s = Synth(1_000, N, G, config=5, seed=0xE5CA1A7E00000005)
+    nlo, nhi = shard_range(N, rank, world)
+    ctx = _RangeOrders(s.nodes(), s.groups, nlo, nhi)
+    res = {w: gather_orders(ctx, w, n, s.nodes()["created_ns"]) for w in (0, 1)}
+    if rank == 0:
+        out.put(res)
+    dist.destroy_process_group()
+
+
+def test_sharded_orderings_merge_to_whole():
+    """Config #5 on N ranks: every rank orders its node range, the per-group prefixes are
+    all-gathered and merged (escalator_amd.dist.gather_orders); the merged taint / untaint
+    selections equal the whole-snapshot orders."""
+    from escalator_amd.context import Synth
+    from oracle import soa
+    n = 50
+    for world in (2, 3):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_order_worker, args=(r, world, port, n, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        res = q.get(timeout=120)
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        full = Synth(1_000, 30_000, 12, config=5, seed=0xE5CA1A7E00000005)
+        for w in (0, 1):
+            for g in range(12):
+                want = soa.order(full.nodes(), full.groups, g, w, cap=n)
+                assert np.array_equal(res[w][g], want), (world, w, g)
+
+
+def test_merge_orders_ties_by_index():
+    """Equal creation times keep ascending snapshot index in both directions (the
+    single-rank rule), whichever rank holds them."""
+    from escalator_amd.dist import merge_orders
+    created = np.array([5, 3, 5, 3, 7, 5], np.int64)
+    parts = [np.array([1, 0, 2]), np.array([3, 5, 4])]            # each rank's local oldest-first
+    assert list(merge_orders(parts, created, 0, 6)) == [1, 3, 0, 2, 5, 4]
+    parts = [np.array([0, 2, 1]), np.array([4, 5, 3])]            # local newest-first
+    assert list(merge_orders(parts, created, 1, 4)) == [4, 0, 2, 5]
+    assert merge_orders([], created, 0, 3).size == 0
