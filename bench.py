@@ -188,9 +188,13 @@ def bench_order(args):
     if rank != 0:
         dist.destroy_process_group()
         return
-    # bytes the ordering moves per membership: classify (node, group, flags) 12 read + class
-    # 1 written; split: class 1 + node 4 read, node 4 written (esc_kernels.hip K5)
-    order_bytes = n_memb * 22
+    # algorithmic bytes per membership: read node, group, flags (12 B), write the node (4 B;
+    # an upper bound — cordoned nodes feed neither order).  The three-pass default moves 22 B
+    # (a class byte written and read back, the node read twice); the fused single pass
+    # (ESC_ORDER_FUSED=1) moves the 16 B.
+    fused = os.environ.get("ESC_ORDER_FUSED", "0") not in ("", "0")
+    order_bytes = n_memb * 16
+    moved_bytes = n_memb * (16 if fused else 22)
     idx_passes = -(-R // 8)
     index_bytes = N * (16 + idx_passes * 32)       # keys 8 + vals 4 per pass (hist 8 + r/w 24), + entries
     out = {
@@ -207,7 +211,9 @@ def bench_order(args):
         "data": "synthetic (esc_synth.cpp config 5: 10M nodes, 100 groups, unique ns creation times)",
         "config": {"workload": "config5: 10M nodes oldest-first / newest-first orderings, 100 node groups",
                    "nodes": N, "node_groups": G, "memberships": n_memb, "parallelism": "shard%d" % world},
-        "roofline": {"bound": "hbm", "kernel": "per-decision ordering (k_ord_count + k_ord_bases + k_ord_scatter)",
+        "roofline": {"bound": "hbm", "kernel": ("k_ord_fused (per-decision ordering, one pass)" if fused else
+                                                "per-decision ordering (k_ord_count + k_ord_bases + k_ord_scatter)"),
+                     "bytes_moved_per_decision": moved_bytes,
                      "achieved": order_bytes / (order_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                      "frac": order_bytes / (order_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
                      "bytes_per_decision": order_bytes},

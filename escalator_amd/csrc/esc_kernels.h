@@ -181,7 +181,12 @@ size_t sort_hist_words(int64_t n);   // digit-histogram words one LSD pass over 
 struct OrdChunk {               // K5 per-decision chunk: memberships [start, end) of one group
     uint32_t start, end, group, pad;
 };
-constexpr int ORD_CHUNK = 4096;
+constexpr int ORD_CHUNK = 4096;   // memberships per K5 chunk (three-pass default)
+hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
+                              const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
+                              const uint32_t* g_flags, unsigned long long* ticket, unsigned long long* status,
+                              uint32_t* vals, int64_t* seg, uint32_t* err, int64_t max_chunk, int ablate,
+                              hipStream_t st);
 hipError_t launch_age_index(const NodeDev& n, int64_t ts_min, uint64_t div, int R, uint64_t* keys64[2],
                             uint32_t* vals[2], uint32_t* hist, uint32_t* tot, uint32_t** age_out, hipStream_t st);
 hipError_t launch_memb_count(const NodeDev& n, const GroupDev& g, const uint32_t* age, int nblk, uint32_t* cnt,

@@ -1231,7 +1231,12 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_memb_expand(NodeDev N, GroupDev 
             node_groups(N, G, f, i, [&](uint32_t mb) {
                 e_node[pos] = (uint32_t)i;
                 e_grp[pos] = mb;
-                e_flags[pos] = f;
+                // a dry group's membership carries "tracked by this group" in the tracker
+                // bit (controller.go:126-138), so the per-decision split needs no lookup
+                e_flags[pos] = mdry(mb) ? ((f & ~ESC_NF_TRACKED) |
+                                           (((f & ESC_NF_TRACKED) && tracked(N, (int32_t)i, (int32_t)mg(mb)))
+                                                ? ESC_NF_TRACKED : 0u))
+                                        : f;
                 ++pos;
             });
         }
@@ -1284,8 +1289,13 @@ __global__ __launch_bounds__(256) void k_grp_gather(const uint32_t* __restrict__
 //   C  per chunk: ballot ranks + wave prefix -> vals (5 B read, 4 B written, coalesced).
 constexpr int ORD_BLOCK = 256, ORD_WAVES = ORD_BLOCK / 64;
 
-__device__ __forceinline__ uint32_t ord_class(const NodeDev& N, uint32_t node, uint32_t grp, uint32_t f) {
-    return grp == NONE ? 3u : (uint32_t)node_class(N, f, (int64_t)node, grp);   // NONE: padding
+// Membership flags: a dry group's membership has the tracker bit resolved for its group
+// (k_memb_expand), so no per-decision lookup is needed.
+__device__ __forceinline__ uint32_t ord_class(const NodeDev&, uint32_t, uint32_t grp, uint32_t f) {
+    if (grp == NONE) return 3u;                                                  // padding
+    if (mdry(grp)) return (f & ESC_NF_TRACKED) ? 1u : 0u;
+    if (f & ESC_NF_UNSCHED) return 2u;
+    return (f & ESC_NF_TAINTED) ? 1u : 0u;
 }
 
 // A: classes of the chunk's memberships (one u32 of 4 class bytes per quad) and the
@@ -1422,6 +1432,161 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __res
             rb[threadIdx.x] += t;
         }
         __syncthreads();
+    }
+}
+
+// Fused single pass (default): the per-decision order in one launch.  A chunk's block
+// classifies its <= 4096 memberships (12 B each), ranks classes 0 / 1 inside the chunk,
+// takes its exclusive per-class prefix within the group by decoupled look-back over the
+// group's earlier chunks, and writes untainted nodes forward from the group's start
+// (oldest first) and tainted nodes backward from the group's end (so that segment read
+// forward is newest first, untaintNewestN's order).  Cordoned nodes feed neither order
+// and are not written.  16 B per membership instead of the three-pass 22 B.
+// Chunks are taken in ticket order (one global counter), so a chunk's predecessors have
+// started before it spins on them; each status word carries the decision epoch
+// (ticket / n_chunks), so nothing needs resetting between decisions.  A look-back that
+// waits beyond a bound stops and raises *err (a lost predecessor would be a bug; the
+// bound keeps the grid finite whatever happens).
+namespace {
+constexpr uint64_t OST_AGG = 1, OST_INC = 2;
+constexpr int OST_CBITS = 27;
+constexpr uint64_t OST_CMASK = (1ull << OST_CBITS) - 1;
+__device__ __forceinline__ uint64_t ost_pack(uint32_t epoch, uint64_t flag, uint64_t n0, uint64_t n1) {
+    return ((uint64_t)(epoch & 0xFF) << 56) | (flag << 54) | ((n0 & OST_CMASK) << OST_CBITS) | (n1 & OST_CMASK);
+}
+}  // namespace
+
+template <int FB>
+__global__ __launch_bounds__(FB) void k_ord_fused(NodeDev N, const OrdChunk* __restrict__ chunks,
+                                                         int64_t n_chunks, const uint32_t* __restrict__ gch_off,
+                                                         const uint32_t* __restrict__ grp_off,
+                                                         const uint32_t* __restrict__ g_node,
+                                                         const uint32_t* __restrict__ g_grp,
+                                                         const uint32_t* __restrict__ g_flags,
+                                                         unsigned long long* __restrict__ ticket,
+                                                         unsigned long long* __restrict__ status,
+                                                         uint32_t* __restrict__ vals, int64_t* __restrict__ seg,
+                                                         uint32_t* __restrict__ err, int ablate) {
+    constexpr int ROUNDS = 4, FW = FB / 64;              // 4 quads per thread: 16 * FB memberships
+    __shared__ unsigned long long s_tk;
+    __shared__ uint32_t wt[ROUNDS][FW];
+    __shared__ uint32_t s_pre[2];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_tk = (ablate & 4) ? (unsigned long long)blockIdx.x : atomicAdd(ticket, 1ull);
+    __syncthreads();
+    const unsigned long long tk = s_tk;
+    const int64_t q = (int64_t)(tk % (unsigned long long)n_chunks);
+    const uint32_t epoch = (uint32_t)(tk / (unsigned long long)n_chunks);
+    const OrdChunk ch = chunks[q];
+    // classify: all four quads' loads in flight
+    uint4 nd[ROUNDS], gr[ROUNDS], fl[ROUNDS];
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        const uint32_t b = ch.start + r * 4 * FB + 4 * threadIdx.x;
+        const uint32_t bb = b < ch.end ? b : ch.start;
+        nd[r] = ld4(g_node + bb);
+        gr[r] = ld4(g_grp + bb);
+        fl[r] = ld4(g_flags + bb);
+    }
+    uint32_t cls = 0;                                     // 2 bits per membership
+    uint32_t v[ROUNDS];                                   // class 0 | class 1 << 16, per round
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        const uint32_t b = ch.start + r * 4 * FB + 4 * threadIdx.x;
+        v[r] = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = b + j < ch.end ? ord_class(N, lane4(nd[r], j), lane4(gr[r], j), lane4(fl[r], j)) : 3u;
+            cls |= k << (2 * (4 * r + j));
+            v[r] += k == 0 ? 1u : (k == 1 ? 0x10000u : 0u);
+        }
+        const uint32_t inc = wave_incl_scan32(v[r]);
+        if (lane == 63) wt[r][wid] = inc;
+        v[r] = inc - v[r];                                // exclusive, within the wave
+    }
+    __syncthreads();
+    // block prefix in membership order (round, wave, lane) and the chunk's aggregate
+    uint32_t agg = 0;
+    uint32_t pre[ROUNDS];
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r)
+#pragma unroll
+        for (int w = 0; w < FW; ++w) {
+            if (w == wid) pre[r] = agg;
+            agg += wt[r][w];
+        }
+    const uint32_t g = ch.group;
+    const uint32_t q0 = gch_off[g];
+    const uint64_t a0 = agg & 0xFFFF, a1 = agg >> 16;
+    if (threadIdx.x < 64) {                               // wave 0: publish, then look back
+        uint64_t p0 = 0, p1 = 0;
+        if ((uint32_t)q == q0 || (ablate & 1)) {        // ablate bit 0 (timing only): no look-back
+            if (lane == 0)
+                __hip_atomic_store(status + q, ost_pack(epoch, OST_INC, a0, a1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(status + q, ost_pack(epoch, OST_AGG, a0, a1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            // a window of 64 predecessors per round (lane l: chunk hi - l); the nearest
+            // inclusive word ends the walk once every chunk before it in the window is ready
+            int64_t hi = q - 1;
+            uint32_t spins = 0;
+            for (;;) {
+                const int64_t j = hi - lane;
+                const bool valid = j >= (int64_t)q0;
+                const uint64_t w = valid ? __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+                const uint32_t f = (uint32_t)((w >> 54) & 3);
+                const bool ready = valid && (uint32_t)(w >> 56) == (epoch & 0xFF) && f != 0;
+                const unsigned long long m_inc = __ballot(ready && f == OST_INC);
+                const unsigned long long m_wait = __ballot(valid && !ready);
+                const unsigned long long need = m_inc ? (m_inc & (~m_inc + 1)) * 2 - 1 : ~0ull;   // lanes up to the nearest INC
+                if (m_wait & need) {
+                    if (++spins > (1u << 22)) {
+                        if (lane == 0) atomicOr(err, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                const bool take = valid && ((need >> lane) & 1ull);
+                p0 += wave_sum64(take ? (w >> OST_CBITS) & OST_CMASK : 0);
+                p1 += wave_sum64(take ? w & OST_CMASK : 0);
+                if (m_inc || hi - 64 < (int64_t)q0) break;
+                hi -= 64;
+            }
+            if (lane == 0)
+                __hip_atomic_store(status + q, ost_pack(epoch, OST_INC, p0 + a0, p1 + a1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_pre[0] = (uint32_t)p0;
+            s_pre[1] = (uint32_t)p1;
+            if ((uint32_t)q + 1 == gch_off[g + 1]) {      // the group's last chunk: segment bounds
+                const int64_t s0 = grp_off[g], s3 = grp_off[g + 1];
+                seg[4 * (int64_t)g + 0] = s0;
+                seg[4 * (int64_t)g + 1] = s0 + (int64_t)(p0 + a0);
+                seg[4 * (int64_t)g + 2] = s3 - (int64_t)(p1 + a1);
+                seg[4 * (int64_t)g + 3] = s3;
+            }
+        }
+    }
+    __syncthreads();
+    if (ablate & 2) {                                    // timing only: no scatter
+        if (cls == 0x12345678u) vals[0] = 0;
+        return;
+    }
+    const uint32_t base0 = grp_off[g] + s_pre[0], last1 = grp_off[g + 1] - 1 - s_pre[1];
+#pragma unroll
+    for (int r = 0; r < ROUNDS; ++r) {
+        const uint32_t x = pre[r] + v[r];
+        uint32_t r0 = x & 0xFFFF, r1 = x >> 16;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = (cls >> (2 * (4 * r + j))) & 3u;
+            if (k == 0) vals[base0 + r0++] = lane4(nd[r], j);
+            else if (k == 1) vals[last1 - r1++] = lane4(nd[r], j);
+        }
     }
 }
 
@@ -1779,6 +1944,24 @@ hipError_t launch_group_gather(const uint32_t* perm, const uint32_t* gpos, int64
     if (n_e <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_grp_gather, dim3((unsigned)((n_e + 255) / 256)), dim3(256), 0, st, perm, gpos, n_e, e_node,
                        e_grp, e_flags, g_node, g_grp, g_flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
+                              const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
+                              const uint32_t* g_flags, unsigned long long* ticket, unsigned long long* status,
+                              uint32_t* vals, int64_t* seg, uint32_t* err, int64_t max_chunk, int ablate,
+                              hipStream_t st) {
+    if (n_chunks <= 0) return hipSuccess;
+    if (max_chunk > 16 * 512)                             // 1024 threads: up to 16384 per chunk
+        hipLaunchKernelGGL(k_ord_fused<1024>, dim3((unsigned)n_chunks), dim3(1024), 0, st, nd, chunks, n_chunks,
+                           gch_off, grp_off, g_node, g_grp, g_flags, ticket, status, vals, seg, err, ablate);
+    else if (max_chunk > 16 * 256)
+        hipLaunchKernelGGL(k_ord_fused<512>, dim3((unsigned)n_chunks), dim3(512), 0, st, nd, chunks, n_chunks,
+                           gch_off, grp_off, g_node, g_grp, g_flags, ticket, status, vals, seg, err, ablate);
+    else
+        hipLaunchKernelGGL(k_ord_fused<256>, dim3((unsigned)n_chunks), dim3(256), 0, st, nd, chunks, n_chunks,
+                           gch_off, grp_off, g_node, g_grp, g_flags, ticket, status, vals, seg, err, ablate);
     return hipGetLastError();
 }
 

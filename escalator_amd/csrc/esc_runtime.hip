@@ -163,7 +163,14 @@ struct esc_ctx {
     uint32_t *d_gpos = nullptr, *d_pstart = nullptr, *d_cls4 = nullptr;
     int64_t n_gpad = 0;                                       // padded group-order length
     OrdChunk* d_chunks = nullptr;
-    int64_t n_chunks = 0;
+    int64_t n_chunks = 0, max_chunk = 0;
+    bool order_fused = false;                                 // single-pass K5 (ESC_ORDER_FUSED=1), DESIGN.md §4
+    bool fused_fits = true;                                   // every group's run < 2^27 (look-back words)
+    bool fused_ran = false;                                   // layout of the last esc_sort_nodes
+    int order_ablate = 0;                                     // ESC_ORDER_ABLATE (timing-only knob)
+    int64_t ord_chunk = ORD_CHUNK;                            // memberships per K5 chunk (ESC_ORDER_CHUNK)
+    unsigned long long *d_oticket = nullptr, *d_ostat = nullptr;   // fused: chunk tickets, look-back words
+    uint32_t* d_oerr = nullptr;
     uint64_t sort_div = 1;
     int sort_R = 1;
     bool sorted = false;
@@ -295,6 +302,7 @@ void release_sort(esc_ctx* c) {
     dfree(c->d_e_node); dfree(c->d_e_grp); dfree(c->d_e_flags);
     dfree(c->d_gperm); dfree(c->d_g_node); dfree(c->d_g_grp); dfree(c->d_g_flags);
     dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks);
+    dfree(c->d_oticket); dfree(c->d_ostat); dfree(c->d_oerr);
     dfree(c->d_gpos); dfree(c->d_pstart); dfree(c->d_cls4);
     c->n_chunks = 0;
     c->n_gpad = 0;
@@ -366,11 +374,17 @@ int32_t build_age_index(esc_ctx* c) {
         pstart[q + 1] = pstart[q] + (uint32_t)((len + 3) & ~(int64_t)3);
         grp_off[q] = (uint32_t)starts[q];
         gch_off[q] = (uint32_t)chunks.size();
-        for (int64_t a = 0; a < len; a += ORD_CHUNK)
-            chunks.push_back({pstart[q] + (uint32_t)a, pstart[q] + (uint32_t)std::min<int64_t>(len, a + ORD_CHUNK),
+        for (int64_t a = 0; a < len; a += c->ord_chunk)
+            chunks.push_back({pstart[q] + (uint32_t)a, pstart[q] + (uint32_t)std::min<int64_t>(len, a + c->ord_chunk),
                               (uint32_t)q, 0u});
     }
     grp_off[g.G] = (uint32_t)c->n_memb;
+    c->fused_fits = true;
+    c->max_chunk = 0;
+    for (int32_t q = 0; q < g.G; ++q) {
+        if (starts[q + 1] - starts[q] >= ((int64_t)1 << 27)) c->fused_fits = false;
+        c->max_chunk = std::max<int64_t>(c->max_chunk, std::min<int64_t>(starts[q + 1] - starts[q], c->ord_chunk));
+    }
     gch_off[g.G] = (uint32_t)chunks.size();
     const int64_t npad = pstart[g.G];
     if (npad >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
@@ -390,7 +404,16 @@ int32_t build_age_index(esc_ctx* c) {
         HIP_TRY(dalloc(&c->d_grp_off, grp_off.size())); HIP_TRY(dalloc(&c->d_gch_off, gch_off.size()));
         HIP_TRY(dalloc(&c->d_ccnt, chunks.size() * 3)); HIP_TRY(dalloc(&c->d_cbase, chunks.size() * 3));
         HIP_TRY(dalloc(&c->d_chunks, chunks.size())); HIP_TRY(dalloc(&c->d_pstart, pstart.size()));
+        dfree(c->d_oticket); dfree(c->d_ostat); dfree(c->d_oerr);
+        HIP_TRY(dalloc(&c->d_oticket, 1)); HIP_TRY(dalloc(&c->d_ostat, chunks.size())); HIP_TRY(dalloc(&c->d_oerr, 1));
     }
+    // fused ordering: tickets restart at 0 (a decision consumes exactly n_chunks), status
+    // words at epoch 0 / not ready; groups without memberships get their (empty) segment
+    // bounds here, the others from their last chunk every decision
+    HIP_TRY(hipMemsetAsync(c->d_oticket, 0, 8, st));
+    HIP_TRY(hipMemsetAsync(c->d_ostat, 0, std::max<size_t>(chunks.size(), 1) * 8, st));
+    HIP_TRY(hipMemsetAsync(c->d_oerr, 0, 4, st));
+
     c->n_chunks = (int64_t)chunks.size();
     HIP_TRY(hipMemcpy(c->d_grp_off, grp_off.data(), grp_off.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_gch_off, gch_off.data(), gch_off.size() * 4, hipMemcpyHostToDevice));
@@ -399,6 +422,14 @@ int32_t build_age_index(esc_ctx* c) {
     HIP_TRY(launch_group_pos(gkeys, c->n_memb, c->d_seg, c->d_pstart, c->d_gpos, st));
     HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
                                 c->d_g_grp, c->d_g_flags, st));
+    {   // after k_grp_pos, which reads d_seg as the groups' unpadded starts
+        std::vector<int64_t> seg0((size_t)4 * g.G + 1);
+        for (int32_t q = 0; q < g.G; ++q)
+            for (int k = 0; k < 4; ++k) seg0[4 * (size_t)q + k] = grp_off[q];
+        seg0[4 * (size_t)g.G] = c->n_memb;
+        HIP_TRY(hipMemcpyAsync(c->d_seg, seg0.data(), seg0.size() * 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     c->sorted = false;
     return ESC_OK;
 }
@@ -556,6 +587,15 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     c->rank = rank;
     c->world = world;
     if (const char* v = std::getenv("ESC_K1_VARIANT")) c->k1_variant = std::atoi(v);
+    if (const char* v = std::getenv("ESC_ORDER_FUSED")) {
+        c->order_fused = std::atoi(v) != 0;
+        if (c->order_fused) c->ord_chunk = 8192;               // its best chunk on config 5
+    }
+    if (const char* v = std::getenv("ESC_ORDER_ABLATE")) c->order_ablate = std::atoi(v);
+    if (const char* v = std::getenv("ESC_ORDER_CHUNK")) {      // 4096 / 8192 / 16384 (measurement knob)
+        const int64_t k = std::atoll(v);
+        if (k == 4096 || k == 8192 || k == 16384) c->ord_chunk = k;
+    }
     c->gi.build(groups, n_groups);
     c->params.resize(n_groups);
     for (int32_t g = 0; g < n_groups; ++g) params_from(c->params[g], groups[g], nullptr);
@@ -1605,7 +1645,14 @@ int32_t esc_tracker_update(esc_ctx* c, int32_t group, const int64_t* add, int64_
     }
     c->sorted = false;
     c->rm_valid = false;
-    return flip.empty() ? ESC_OK : patch_nodes(c, flip);
+    if (!flip.empty()) return patch_nodes(c, flip);        // re-lists the memberships too
+    // the K5 membership copies carry each dry membership's tracker bit: re-list them
+    HIP_TRY(launch_memb_expand(node_dev(c), group_dev(c), c->d_age, c->memb_blocks, c->d_cnt, c->d_e_node,
+                               c->d_e_grp, c->d_e_flags, c->stream));
+    HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
+                                c->d_g_grp, c->d_g_flags, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ESC_OK;
 }
 
 int32_t esc_tracker_list(const esc_ctx* c, int32_t group, int64_t* idx_out, int64_t cap, int64_t* n_out) {
@@ -1745,9 +1792,15 @@ int32_t esc_sort_nodes(esc_ctx* c) {
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->nodes_loaded) return ESC_E_STATE;
     hipSetDevice(c->device);
-    HIP_TRY(launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node, c->d_g_grp,
-                         c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase, c->d_ovals[0], c->d_seg,
-                         c->stream));
+    c->fused_ran = c->order_fused && c->fused_fits;
+    if (c->fused_ran)
+        HIP_TRY(launch_order_fused(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node,
+                                   c->d_g_grp, c->d_g_flags, c->d_oticket, c->d_ostat, c->d_ovals[0], c->d_seg,
+                                   c->d_oerr, c->max_chunk, c->order_ablate, c->stream));
+    else
+        HIP_TRY(launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node,
+                             c->d_g_grp, c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase,
+                             c->d_ovals[0], c->d_seg, c->stream));
     c->order_src = 0;
     c->sorted = true;
     return ESC_OK;
@@ -1776,8 +1829,16 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
     if (!c->sorted) return ESC_E_STATE;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->fused_ran) {
+        uint32_t err = 0;
+        HIP_TRY(hipMemcpy(&err, c->d_oerr, 4, hipMemcpyDeviceToHost));
+        if (err) return ESC_E_HIP;                      // a look-back gave up: order not valid
+    }
+    // three-pass layout: class segments [b0, b1), [b1, b2) in age order; fused: untainted
+    // [s0, s1) in age order, tainted [s2, s3) newest first
+    const int64_t so = c->fused_ran ? 2 * (int64_t)which : (int64_t)which;
     int64_t seg[2];
-    HIP_TRY(hipMemcpy(seg, c->d_seg + 4 * (int64_t)group + which, 16, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(seg, c->d_seg + 4 * (int64_t)group + so, 16, hipMemcpyDeviceToHost));
     const int64_t cnt = seg[1] - seg[0];
     if (n_out) *n_out = cnt;
     const int64_t m = std::min(cnt, cap);
@@ -1798,8 +1859,12 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
     std::vector<uint32_t> v;
     for (;;) {
         v.resize(take);
-        HIP_TRY(hipMemcpy(v.data(), vals + seg[1] - take, take * 4, hipMemcpyDeviceToHost));
-        std::reverse(v.begin(), v.end());
+        if (c->fused_ran) {
+            HIP_TRY(hipMemcpy(v.data(), vals + seg[0], take * 4, hipMemcpyDeviceToHost));
+        } else {
+            HIP_TRY(hipMemcpy(v.data(), vals + seg[1] - take, take * 4, hipMemcpyDeviceToHost));
+            std::reverse(v.begin(), v.end());
+        }
         if (take == cnt || ts(v[take - 1]) != ts(v[m - 1])) break;
         take = std::min(cnt, take * 2);
     }

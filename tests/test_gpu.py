@@ -227,15 +227,37 @@ def test_synthetic_vs_c_oracle(esc, cfg, P, N, G):
     check_metrics(ctx.metrics(), soa.metrics(otot, odf, odi))
 
 
-def test_synthetic_sort_vs_c_oracle(esc):
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_synthetic_sort_vs_c_oracle(esc, fused, monkeypatch):
+    """Both K5 per-decision paths (three passes; ESC_ORDER_FUSED=1: one pass with
+    decoupled look-back across a group's chunks, several chunks per group here), repeated
+    decisions (look-back epochs) and a dry-mode tracker change in between."""
+    monkeypatch.setenv("ESC_ORDER_FUSED", fused)
     s = esc.Synth(10_000, 400_000, 100, config=5, seed=0xE5CA1A7E00000005)
     nodes = s.nodes()
     ctx = esc.Context(s)
     ctx.load_synth(s)
-    ctx.sort_nodes()
+    for _ in range(3):
+        ctx.sort_nodes()
     for g in list(range(0, 100, 7)) + [99]:
         for which in (0, 1):
             assert np.array_equal(ctx.group_order(g, which), soa.order(nodes, s.groups, g, which)), (g, which)
+    # a dry group's tracker changes in place; its split follows the new tracker
+    g = next(g for g, x in enumerate(s.groups) if x.get("dry_mode"))
+    members = _members_oldest(nodes, s.groups, g)
+    ctx.tracker_update(g, add=ctx.group_order(g, 0)[:500], remove=ctx.group_order(g, 1)[:100])
+    ctx.sort_nodes()
+    trk = set(ctx.tracker_list(g).tolist())
+    t = nodes["created_ns"]
+    assert ctx.group_order(g, 0).tolist() == [j for j in members if j not in trk]
+    assert ctx.group_order(g, 1).tolist() == sorted((j for j in members if j in trk), key=lambda j: (-int(t[j]), j))
+
+
+def _members_oldest(nodes, groups, g):
+    """All members of dry group g, oldest first (ties by index): the oracle's two lists merged."""
+    both = list(soa.order(nodes, groups, g, 0)) + list(soa.order(nodes, groups, g, 1))
+    t = nodes["created_ns"]
+    return sorted(both, key=lambda j: (int(t[j]), j))
 
 
 def test_sharded_two_contexts_host_exchange(esc):
