@@ -1387,52 +1387,69 @@ __global__ __launch_bounds__(64) void k_ord_bases(const uint32_t* __restrict__ g
     }
 }
 
-// C: every chunk's nodes into its three class streams, stable: per lane 4 consecutive
-// memberships, per-class ranks from one packed DPP wave scan, wave offsets via LDS.
+// C: every chunk's untainted and tainted nodes into their class segments, stable.  All of
+// the chunk's class bytes and node ids are loaded up front (4 steps of 1024 memberships,
+// 4 per lane); per-class ranks come from packed DPP wave scans; the nodes are staged in
+// LDS in output order (class 0 then class 1) and written out with consecutive lanes on
+// consecutive addresses.  Cordoned nodes (class 2) feed neither order and are not written.
 __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __restrict__ chunks,
                                                            const uint32_t* __restrict__ cls4,
                                                            const uint32_t* __restrict__ g_node,
                                                            const uint32_t* __restrict__ cbase,
                                                            uint32_t* __restrict__ vals) {
-    __shared__ uint32_t wt[ORD_WAVES];
-    __shared__ uint32_t rb[3];
+    constexpr int STEPS = ORD_CHUNK / (4 * ORD_BLOCK);
+    __shared__ uint32_t wt[STEPS][ORD_WAVES];
+    __shared__ uint32_t stage[ORD_CHUNK];
     const OrdChunk ch = chunks[blockIdx.x];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (threadIdx.x < 3) rb[threadIdx.x] = cbase[(int64_t)blockIdx.x * 3 + threadIdx.x];
-    __syncthreads();
-    const uint32_t iters = (ch.end - ch.start + 4 * ORD_BLOCK - 1) / (4 * ORD_BLOCK);
-    for (uint32_t it = 0; it < iters; ++it) {
-        const uint32_t b = ch.start + it * 4 * ORD_BLOCK + 4 * threadIdx.x;
+    uint32_t packed[STEPS];
+    uint4 nd[STEPS];
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {
+        const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
         const bool ok = b < ch.end;
-        const uint32_t packed = ok ? cls4[b >> 2] : 0x03030303u;
-        const uint4 nd = ok ? ld4(g_node + b) : make_uint4(0, 0, 0, 0);
-        uint32_t v = 0;                                  // per-class counts, 10 bits each
+        packed[st] = ok ? cls4[b >> 2] : 0x03030303u;
+        nd[st] = ld4(g_node + (ok ? b : ch.start));
+    }
+    uint32_t ex[STEPS];
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {
+        uint32_t v = 0;                                  // class 0 | class 1 << 16
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t k = (packed >> (8 * j)) & 0xFF;
-            if (k < 3) v += 1u << (10 * k);
+            const uint32_t k = (packed[st] >> (8 * j)) & 0xFF;
+            v += k == 0 ? 1u : (k == 1 ? 0x10000u : 0u);
         }
         const uint32_t inc = wave_incl_scan32(v);
-        if (lane == 63) wt[wid] = inc;
-        __syncthreads();
-        uint32_t pre = rb[0] | 0, p1 = rb[1], p2 = rb[2];
-        uint32_t wp = 0;
-        for (int w = 0; w < wid; ++w) wp += wt[w];
-        uint32_t ex = inc - v + wp;                       // my first slot per class, in this block step
-        uint32_t off[3] = {pre + (ex & 0x3FF), p1 + ((ex >> 10) & 0x3FF), p2 + (ex >> 20)};
+        if (lane == 63) wt[st][wid] = inc;
+        ex[st] = inc - v;
+    }
+    __syncthreads();
+    uint32_t tot = 0;                                    // chunk totals (packed)
+    uint32_t pre[STEPS];
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st)
+#pragma unroll
+        for (int w = 0; w < ORD_WAVES; ++w) {
+            if (w == wid) pre[st] = tot;
+            tot += wt[st][w];
+        }
+    const uint32_t n0 = tot & 0xFFFF, n1 = tot >> 16;
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {
+        const uint32_t x = pre[st] + ex[st];
+        uint32_t r0 = x & 0xFFFF, r1 = n0 + (x >> 16);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t k = (packed >> (8 * j)) & 0xFF;
-            if (k < 3) vals[off[k]++] = lane4(nd, j);
+            const uint32_t k = (packed[st] >> (8 * j)) & 0xFF;
+            if (k == 0) stage[r0++] = lane4(nd[st], j);
+            else if (k == 1) stage[r1++] = lane4(nd[st], j);
         }
-        __syncthreads();
-        if (threadIdx.x < 3) {
-            uint32_t t = 0;
-            for (int w = 0; w < ORD_WAVES; ++w) t += (wt[w] >> (10 * threadIdx.x)) & 0x3FF;
-            rb[threadIdx.x] += t;
-        }
-        __syncthreads();
     }
+    __syncthreads();
+    const uint32_t b0 = cbase[(int64_t)blockIdx.x * 3], b1 = cbase[(int64_t)blockIdx.x * 3 + 1];
+    for (uint32_t i = threadIdx.x; i < n0 + n1; i += ORD_BLOCK)
+        vals[i < n0 ? b0 + i : b1 + (i - n0)] = stage[i];
 }
 
 // Fused single pass (default): the per-decision order in one launch.  A chunk's block

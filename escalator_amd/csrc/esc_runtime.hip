@@ -596,6 +596,7 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
         const int64_t k = std::atoll(v);
         if (k == 4096 || k == 8192 || k == 16384) c->ord_chunk = k;
     }
+    if (!c->order_fused) c->ord_chunk = ORD_CHUNK;             // k_ord_scatter stages one ORD_CHUNK in LDS
     c->gi.build(groups, n_groups);
     c->params.resize(n_groups);
     for (int32_t g = 0; g < n_groups; ++g) params_from(c->params[g], groups[g], nullptr);
