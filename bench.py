@@ -212,7 +212,7 @@ def bench_order(args):
         "config": {"workload": "config5: 10M nodes oldest-first / newest-first orderings, 100 node groups",
                    "nodes": N, "node_groups": G, "memberships": n_memb, "parallelism": "shard%d" % world},
         "roofline": {"bound": "hbm", "kernel": ("k_ord_fused (per-decision ordering, one pass)" if fused else
-                                                "per-decision ordering (k_ord_count + k_ord_bases + k_ord_scatter)"),
+                                                "per-decision ordering (k_ord_count + k_ord_scatter)"),
                      "bytes_moved_per_decision": moved_bytes,
                      "achieved": order_bytes / (order_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                      "frac": order_bytes / (order_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),

@@ -1283,10 +1283,10 @@ __global__ __launch_bounds__(256) void k_grp_gather(const uint32_t* __restrict__
 
 // ---- per decision: inside every group's run, a stable 3-way split by filterNodes class
 // (controller.go:125-150; dry groups: tracker only).  Chunks never cross a group, so a
-// chunk's nodes go to three contiguous output streams; three passes:
+// chunk's untainted / tainted nodes go to two contiguous output streams; two passes:
 //   A  classify (12 B read, 1 B written) + per-chunk class counts,
-//   B  per group: chunk bases and the (group, class) segment bounds,
-//   C  per chunk: ballot ranks + wave prefix -> vals (5 B read, 4 B written, coalesced).
+//   C  per chunk: its bases from the group's chunk counts, DPP wave ranks, LDS staging
+//      -> vals (5 B read, <= 4 B written, coalesced), the group's segment bounds.
 constexpr int ORD_BLOCK = 256, ORD_WAVES = ORD_BLOCK / 64;
 
 // Membership flags: a dry group's membership has the tracker bit resolved for its group
@@ -1348,60 +1348,49 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_count(NodeDev N, const OrdChu
     }
 }
 
-// B: one wave per group — class totals over the group's chunks, the (group, class)
-// segment bounds (seg[4g + class]), and every chunk's output base per class.
-__global__ __launch_bounds__(64) void k_ord_bases(const uint32_t* __restrict__ grp_off,
-                                                  const uint32_t* __restrict__ gch_off,
-                                                  const uint32_t* __restrict__ ccnt, int32_t G, int64_t n,
-                                                  uint32_t* __restrict__ cbase, int64_t* __restrict__ seg) {
-    const int32_t g = blockIdx.x;
-    const int lane = threadIdx.x;
-    if (g == G) { if (lane == 0) seg[4 * (int64_t)G] = n; return; }
-    const uint32_t q0 = gch_off[g], q1 = gch_off[g + 1];
-    uint32_t t[3] = {0, 0, 0};
-    for (uint32_t q = q0 + lane; q < q1; q += 64)
-        for (int k = 0; k < 3; ++k) t[k] += ccnt[(int64_t)q * 3 + k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) t[k] += __shfl_xor(t[k], o, 64);
-    uint32_t b[3];
-    b[0] = grp_off[g];
-    b[1] = b[0] + t[0];
-    b[2] = b[1] + t[1];
-    if (lane < 4) seg[4 * (int64_t)g + lane] = lane == 3 ? b[2] + t[2] : b[lane];
-    for (uint32_t q = q0; q < q1; q += 64) {          // chunk bases: exclusive wave scan per class
-        const uint32_t qq = q + lane;
-        uint32_t v[3];
-        for (int k = 0; k < 3; ++k) v[k] = qq < q1 ? ccnt[(int64_t)qq * 3 + k] : 0;
-        for (int k = 0; k < 3; ++k) {
-            uint32_t x = v[k];
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
-            }
-            if (qq < q1) cbase[(int64_t)qq * 3 + k] = b[k] + x - v[k];
-            b[k] += __shfl(x, 63, 64);
-        }
-    }
-}
-
 // C: every chunk's untainted and tainted nodes into their class segments, stable.  All of
 // the chunk's class bytes and node ids are loaded up front (4 steps of 1024 memberships,
 // 4 per lane); per-class ranks come from packed DPP wave scans; the nodes are staged in
 // LDS in output order (class 0 then class 1) and written out with consecutive lanes on
 // consecutive addresses.  Cordoned nodes (class 2) feed neither order and are not written.
+// The chunk's output bases come from the class counts of its group's chunks (pass A):
+// wave 0 sums them (a group has few chunks), and the group's first chunk writes the
+// group's segment bounds (groups without memberships keep the bounds set at load).
 __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __restrict__ chunks,
                                                            const uint32_t* __restrict__ cls4,
                                                            const uint32_t* __restrict__ g_node,
-                                                           const uint32_t* __restrict__ cbase,
-                                                           uint32_t* __restrict__ vals) {
+                                                           const uint32_t* __restrict__ gch_off,
+                                                           const uint32_t* __restrict__ grp_off,
+                                                           const uint32_t* __restrict__ ccnt,
+                                                           uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
     constexpr int STEPS = ORD_CHUNK / (4 * ORD_BLOCK);
     __shared__ uint32_t wt[STEPS][ORD_WAVES];
     __shared__ uint32_t stage[ORD_CHUNK];
+    __shared__ uint32_t s_base[2];
     const OrdChunk ch = chunks[blockIdx.x];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (wid == 0) {
+        const uint32_t g = ch.group, q0 = gch_off[g], q1 = gch_off[g + 1], me = blockIdx.x;
+        uint32_t t0 = 0, t1 = 0, t2 = 0, p0 = 0, p1 = 0;
+        for (uint32_t q = q0 + lane; q < q1; q += 64) {
+            const uint32_t c0 = ccnt[(int64_t)q * 3], c1 = ccnt[(int64_t)q * 3 + 1], c2 = ccnt[(int64_t)q * 3 + 2];
+            t0 += c0; t1 += c1; t2 += c2;
+            if (q < me) { p0 += c0; p1 += c1; }
+        }
+        t0 = (uint32_t)wave_sum64(t0); t1 = (uint32_t)wave_sum64(t1); t2 = (uint32_t)wave_sum64(t2);
+        p0 = (uint32_t)wave_sum64(p0); p1 = (uint32_t)wave_sum64(p1);
+        const uint32_t s0 = grp_off[g];
+        if (lane == 0) {
+            s_base[0] = s0 + p0;
+            s_base[1] = s0 + t0 + p1;
+            if (me == q0) {
+                seg[4 * (int64_t)g + 0] = s0;
+                seg[4 * (int64_t)g + 1] = (int64_t)s0 + t0;
+                seg[4 * (int64_t)g + 2] = (int64_t)s0 + t0 + t1;
+                seg[4 * (int64_t)g + 3] = (int64_t)s0 + t0 + t1 + t2;
+            }
+        }
+    }
     uint32_t packed[STEPS];
     uint4 nd[STEPS];
 #pragma unroll
@@ -1447,7 +1436,7 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __res
         }
     }
     __syncthreads();
-    const uint32_t b0 = cbase[(int64_t)blockIdx.x * 3], b1 = cbase[(int64_t)blockIdx.x * 3 + 1];
+    const uint32_t b0 = s_base[0], b1 = s_base[1];
     for (uint32_t i = threadIdx.x; i < n0 + n1; i += ORD_BLOCK)
         vals[i < n0 ? b0 + i : b1 + (i - n0)] = stage[i];
 }
@@ -1989,10 +1978,9 @@ hipError_t launch_order(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chu
     if (n_chunks > 0)
         hipLaunchKernelGGL(k_ord_count, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, g_node, g_grp,
                            g_flags, cls4, ccnt);
-    hipLaunchKernelGGL(k_ord_bases, dim3(G + 1), dim3(64), 0, st, grp_off, gch_off, ccnt, G, n_e, cbase, seg);
     if (n_chunks > 0)
-        hipLaunchKernelGGL(k_ord_scatter, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, chunks, cls4, g_node, cbase,
-                           vals);
+        hipLaunchKernelGGL(k_ord_scatter, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, chunks, cls4, g_node, gch_off,
+                           grp_off, ccnt, vals, seg);
     return hipGetLastError();
 }
 

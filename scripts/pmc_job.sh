@@ -17,7 +17,7 @@ run() {   # prefix, regex, command, name, counters...
         --output-format csv -d gpurun_out/${pre}_${TAG}_${name} -o run -- $cmd > gpurun_out/${pre}_${TAG}_${name}.log 2>&1
 }
 K="k_pod_reduce|k_node_pieces|k_pod_fold|k_combine"
-S="k_ord_fused|k_ord_count|k_ord_bases|k_ord_scatter"
+S="k_ord_fused|k_ord_count|k_ord_scatter"
 run pmc "$K" "$CMD" fetch FETCH_SIZE &&
 run pmc "$K" "$CMD" write WRITE_SIZE &&
 run pmc "$K" "$CMD" sq SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD &&
