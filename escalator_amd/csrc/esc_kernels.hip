@@ -1309,17 +1309,18 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_count(NodeDev N, const OrdChu
     const OrdChunk ch = chunks[blockIdx.x];
     uint32_t c[3] = {0, 0, 0};
     constexpr uint32_t STEP = 4 * ORD_BLOCK;
-    for (uint32_t b0 = ch.start + 4 * threadIdx.x; b0 < ch.end; b0 += 2 * STEP) {
-        uint4 nd[2], gr[2], fl[2];                      // two quads' loads in flight
+    constexpr int H = ORD_CHUNK / STEP;                  // the whole chunk's quads in flight
+    for (uint32_t b0 = ch.start + 4 * threadIdx.x; b0 < ch.end; b0 += H * STEP) {
+        uint4 nd[H], gr[H], fl[H];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < H; ++h) {
             const uint32_t b = b0 + h * STEP < ch.end ? b0 + h * STEP : b0;
             nd[h] = ld4(g_node + b);
             gr[h] = ld4(g_grp + b);
             fl[h] = ld4(g_flags + b);
         }
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
+        for (int h = 0; h < H; ++h) {
             const uint32_t b = b0 + h * STEP;
             if (b >= ch.end) break;
             uint32_t packed = 0;
