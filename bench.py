@@ -272,7 +272,8 @@ def main():
         ctx.use_graph(True)
         step = ctx.run
     else:
-        ex = Exchange(ctx, device_collective=True)
+        ex = Exchange(ctx, device_collective=backend == "nccl")
+        ctx.use_graph(True)                       # the shard's K1/K2/K3 step replays as one graph
         step = ex.step
 
     def barrier():

@@ -139,7 +139,8 @@ struct esc_ctx {
     int k1_variant = 0;                                       // ESC_K1_VARIANT (measurement knob)
     // graph
     bool use_graph = false;
-    std::vector<hipGraphExec_t> graphs;
+    std::vector<hipGraphExec_t> graphs;                       // esc_run: whole decision (world 1)
+    std::vector<hipGraphExec_t> rgraphs;                      // esc_reduce: the shard's step (world > 1)
     // timing
     bool timing = false;
     hipEvent_t ev[MAX_STAGES] = {};
@@ -274,6 +275,35 @@ void drop_graphs(esc_ctx* c) {
     for (auto& g : c->graphs)
         if (g) hipGraphExecDestroy(g);
     c->graphs.clear();
+    for (auto& g : c->rgraphs)
+        if (g) hipGraphExecDestroy(g);
+    c->rgraphs.clear();
+}
+
+int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out);
+
+// Replays (capturing on first use) the per-replica graph of enqueue_step(r, decide, decide)
+// on the context's stream: one launch instead of the step's kernels, events and waits.
+int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool decide) {
+    const int nrep = (int)c->pods.size();
+    if ((int)gs.size() != nrep) {
+        for (auto& g : gs)
+            if (g) hipGraphExecDestroy(g);
+        gs.assign(nrep, nullptr);
+    }
+    if (!gs[r]) {
+        hipGraph_t graph = nullptr;
+        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        const int32_t rc = enqueue_step(c, r, decide, decide);
+        hipError_t e = hipStreamEndCapture(c->stream, &graph);
+        if (rc) { if (graph) hipGraphDestroy(graph); return rc; }
+        if (e != hipSuccess) return fail_hip(e, "hipStreamEndCapture");
+        e = hipGraphInstantiate(&gs[r], graph, nullptr, nullptr, 0);
+        hipGraphDestroy(graph);
+        if (e != hipSuccess) return fail_hip(e, "hipGraphInstantiate");
+    }
+    HIP_TRY(hipGraphLaunch(gs[r], c->stream));
+    return ESC_OK;
 }
 
 void release_work(esc_ctx* c) {
@@ -1160,10 +1190,11 @@ int32_t esc_reduce(esc_ctx* c) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
     hipSetDevice(c->device);
-    rc = enqueue_step(c, c->cur, false, false);
+    const int r = c->cur;
     c->cur = (c->cur + 1) % (int)c->pods.size();
     c->pending = true;
-    return rc;
+    if (!c->use_graph || c->timing) return enqueue_step(c, r, false, false);
+    return replay_step(c, c->rgraphs, r, false);
 }
 
 int32_t esc_exchange_buffers(esc_ctx* c, void** sum_buf, int64_t* sum_count, void** min_buf, int64_t* min_count) {
@@ -1235,21 +1266,9 @@ int32_t esc_run(esc_ctx* c) {
     const int nrep = (int)c->pods.size();
     c->cur = (c->cur + 1) % nrep;
     c->pending = true;
+    (void)nrep;
     if (!c->use_graph || c->timing) return enqueue_step(c, r, true, true);
-    if ((int)c->graphs.size() != nrep) { drop_graphs(c); c->graphs.assign(nrep, nullptr); }
-    if (!c->graphs[r]) {
-        hipGraph_t graph = nullptr;
-        HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-        rc = enqueue_step(c, r, true, true);
-        hipError_t e = hipStreamEndCapture(c->stream, &graph);
-        if (rc) { if (graph) hipGraphDestroy(graph); return rc; }
-        if (e != hipSuccess) return fail_hip(e, "hipStreamEndCapture");
-        e = hipGraphInstantiate(&c->graphs[r], graph, nullptr, nullptr, 0);
-        hipGraphDestroy(graph);
-        if (e != hipSuccess) return fail_hip(e, "hipGraphInstantiate");
-    }
-    HIP_TRY(hipGraphLaunch(c->graphs[r], c->stream));
-    return ESC_OK;
+    return replay_step(c, c->graphs, r, true);
 }
 
 int32_t esc_sync(esc_ctx* c) {

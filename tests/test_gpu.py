@@ -260,8 +260,10 @@ def _members_oldest(nodes, groups, g):
     return sorted(both, key=lambda j: (int(t[j]), j))
 
 
-def test_sharded_two_contexts_host_exchange(esc):
-    """Two ranks' shards on one device, exchanged through the host: == whole snapshot."""
+@pytest.mark.parametrize("graph", [False, True])
+def test_sharded_two_contexts_host_exchange(esc, graph):
+    """Three ranks' shards on one device, exchanged through the host: == whole snapshot
+    (graph: each shard's K1/K2/K3 step replayed from its captured graph, twice)."""
     from escalator_amd.dist import shard_range
     P, N, G = 300_000, 30_000, 1000
     full = esc.Synth(P, N, G, config=4, seed=11)
@@ -275,7 +277,9 @@ def test_sharded_two_contexts_host_exchange(esc):
         c = esc.Context(s, rank=r, world=3)
         c.load_synth(s, pod_offset=lo, node_lo=nlo, node_hi=nhi)
         c.set_state(full.states)
-        c.reduce()
+        c.use_graph(graph)
+        for _ in range(2 if graph else 1):
+            c.reduce()
         w, f = c.exchange_download()
         words.append(w)
         firsts.append(f)
