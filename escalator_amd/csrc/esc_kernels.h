@@ -126,11 +126,19 @@ enum WidePod : int { WP_CPU_LO = 0, WP_CPU_HI, WP_MEM_LO, WP_MEM_HI, WP_CNT, WP_
 enum TrkAcc : int { TA_CNT = 0, TA_CPU_LO, TA_CPU_HI, TA_MEM_LO, TA_MEM_HI, TA_K };
 
 // variant (ESC_K1_VARIANT, measurement knob): 0 = 512 threads (default: 8 waves per CU with
-// up to 256 VGPRs, 3-4 K tiles in flight per wave), 1 = two C tiles in flight, 2 = 1024
-// threads (16 waves, 128 VGPRs, 1-3 tiles in flight), 9.. = timing-only ablations (wrong
-// results, scripts/k1_variants.py).
+// up to 256 VGPRs, 3-4 K tiles in flight per wave, one static share per workgroup), 1 = two
+// C tiles in flight, 2 = 1024 threads (16 waves, 128 VGPRs, 1-3 tiles in flight), 5 = 512
+// threads with dynamic shares (below; parity-exact but slower: profiles/r01_v10), 9.. =
+// timing-only ablations (wrong results, scripts/k1_variants.py).
+// Dynamic shares (variant 5): the K tiles' weight is cut into nblk * K1_CHUNKS chunks; a workgroup
+// takes at most `cap` of them (K1_CHUNKS..K1_CHUNK_CAP, the packed LDS partials' exactness
+// bound, see ensure_work).  ticket: two u32 (next chunk, workgroups done), zero between launches —
+// the last workgroup to finish resets them.
+constexpr int K1_CHUNKS = 4;
+constexpr int K1_CHUNK_CAP = 8;
+bool k1_dynamic(int variant);
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
-                             uint64_t* part, int64_t* wide, hipStream_t st);
+                             uint64_t* part, int64_t* wide, uint32_t* ticket, int cap, hipStream_t st);
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
                                int64_t* wide, hipStream_t st);
 hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows, int64_t* trk_acc, hipStream_t st);

@@ -480,21 +480,36 @@ __device__ __forceinline__ void c_tile_exact(const PodDev& P, const GroupDev& G,
 // per-group partials stay in LDS and are flushed once.
 // ABLATE (timing-only builds): bit 0 LDS sink, bit 1 skip K tiles, bit 2 skip C tiles,
 // bit 5 loads only.
-template <int THREADS, int ABLATE = 0, int DC = 3>
+// DYN: the K tiles' weight is cut into gridDim.x * K1_CHUNKS chunks taken from a ticket
+// counter (at most `cap` per workgroup), so workgroups that stream faster take more
+// and the launch does not wait on the slowest static share; DYN 0: one static share each.
+template <int THREADS, int ABLATE = 0, int DC = 3, int DYN = 0>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
-                                                        int64_t* __restrict__ wide) {
+                                                        int64_t* __restrict__ wide,
+                                                        uint32_t* __restrict__ ticket, int cap) {
     constexpr int NW = THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
+    __shared__ uint32_t s_chunk;
     for (uint32_t i = threadIdx.x; i < 2 * gw; i += THREADS) lds[i] = 0;
-    __syncthreads();
     const PodSink<ABLATE> K{PodLds{lds, lds + gw, g0, gw}, PodWide{wide}};
     const uint32_t lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (!(ABLATE & 2)) {
+    const int64_t n_chunks = DYN ? (int64_t)gridDim.x * K1_CHUNKS : gridDim.x;
+    // every thread has read the previous ticket before thread 0 overwrites it
+    auto grab = [&]() -> int64_t {
+        __syncthreads();
+        if (threadIdx.x == 0) s_chunk = atomicAdd(ticket, 1u);
+        __syncthreads();
+        return (int64_t)__builtin_amdgcn_readfirstlane(s_chunk);
+    };
+    int64_t chunk = blockIdx.x;
+    if constexpr (DYN) chunk = grab();
+    else __syncthreads();
+    for (int taken = 1; !(ABLATE & 2) && chunk < n_chunks; ++taken) {
         // equal shares of work weight (bytes), not of tiles: a tile of a class with three
         // container records streams ~3.4x the bytes of a simple one
-        const int64_t wl = P.k_weight * blockIdx.x / gridDim.x, wh = P.k_weight * (blockIdx.x + 1) / gridDim.x;
+        const int64_t wl = P.k_weight * chunk / n_chunks, wh = P.k_weight * (chunk + 1) / n_chunks;
         for (int ci = 0; ci < P.n_cls; ++ci) {
             const PodClass C = load_class(P.cls, ci);
             if (C.w0 >= wh) break;
@@ -515,6 +530,8 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
                 default: break;
             }
         }
+        if (!DYN || taken >= cap) break;
+        chunk = grab();
     }
     if (!(ABLATE & 4)) {
         const int64_t per = (P.c_tiles + gridDim.x - 1) / gridDim.x;
@@ -559,6 +576,13 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
         out[i] = lds[i];
         out[S + i] = lds[gw + i];
+    }
+    if (DYN && threadIdx.x == 0) {
+        // every workgroup's last grab precedes its increment here: the last one resets
+        if (atomicAdd(ticket + 1, 1u) == gridDim.x - 1) {
+            __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(ticket + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 
@@ -1762,12 +1786,17 @@ __global__ __launch_bounds__(64) void k_try_remove(NodeDev N, GroupDev G, Remova
 }
 
 // ===================================================================== launchers
+bool k1_dynamic(int variant) { return variant == 5; }
+
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
-                             uint64_t* part, int64_t* wide, hipStream_t st) {
+                             uint64_t* part, int64_t* wide, uint32_t* ticket, int cap, hipStream_t st) {
     const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
-#define ESC_K1(T, A, DC)                                                                              \
-    hipLaunchKernelGGL((k_pod_reduce<T, A, DC>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, wide)
+#define ESC_K1(T, A, DC) ESC_K1D(T, A, DC, 0)
+#define ESC_K1D(T, A, DC, D)                                                                          \
+    hipLaunchKernelGGL((k_pod_reduce<T, A, DC, D>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, \
+                       wide, ticket, cap)
     switch (variant) {
+        case 5: ESC_K1D(512, 0, 3, 1); break;   // dynamic shares (measured slower)
         case 1: ESC_K1(512, 0, 2); break;
         case 2: ESC_K1(1024, 0, 3); break;
         case 3: ESC_K1(512, 64, 3); break;       // <= 2 K tiles in flight per wave
@@ -1781,6 +1810,7 @@ hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int
         default: ESC_K1(512, 0, 3); break;
     }
 #undef ESC_K1
+#undef ESC_K1D
     return hipGetLastError();
 }
 

@@ -121,6 +121,8 @@ struct esc_ctx {
     uint64_t* d_fold = nullptr;                               // K3a output [FOLD_SPLIT][4][S]
     int64_t* d_wide_pod = nullptr;
     uint32_t* d_wp_cnt = nullptr;
+    uint32_t* d_k1_ticket = nullptr;                          // K1 dynamic shares (next chunk, done)
+    int k1_cap = 0;                                           // K1 chunks per workgroup at most (0: static)
     int64_t* d_trk_acc = nullptr;                             // [G][TA_K] dry-mode tracked sums
     int64_t *d_words = nullptr, *d_first = nullptr;          // active exchange buffers
     int64_t *own_words = nullptr, *own_first = nullptr;      // context-owned ones
@@ -307,7 +309,7 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
 }
 
 void release_work(esc_ctx* c) {
-    dfree(c->d_pod_part); dfree(c->d_fold); dfree(c->d_wide_pod); dfree(c->d_wp_cnt); dfree(c->d_trk_acc);
+    dfree(c->d_pod_part); dfree(c->d_fold); dfree(c->d_wide_pod); dfree(c->d_wp_cnt); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
     dfree(c->own_words); dfree(c->own_first); dfree(c->d_dec); dfree(c->d_metrics);
     c->d_words = nullptr;
     c->d_first = nullptr;
@@ -479,19 +481,30 @@ int32_t ensure_work(esc_ctx* c) {
     int64_t nblk = c->cu_count * per_cu;
     // every workgroup takes 1/nblk of the K tiles' weight + ceil(c_tiles/nblk) C tiles;
     // keep that within PODS_PER_BLOCK_MAX (exactness of the packed LDS partials)
+    int64_t cap = 0;
     auto block_pods = [&](int64_t b) {
         // a weight share holds at most share / (lightest tile weight) + one partial tile
-        // per class
-        return ((c->k_weight + b - 1) / b / k_tile_weight(0, 0) + c->n_cls + 1) * TILE +
+        // per class; with dynamic shares a workgroup takes up to K1_CHUNK_CAP chunks of
+        // 1 / (b * K1_CHUNKS) each
+        const int64_t nch = b * K1_CHUNKS;
+        return cap * ((c->k_weight + nch - 1) / nch / k_tile_weight(0, 0) + c->n_cls + 1) * TILE +
                ((c->c_tiles + b - 1) / b) * CTILE;
     };
+    // the static share (cap K1_CHUNKS) sets the grid; dynamic shares then take the largest
+    // cap up to K1_CHUNK_CAP that keeps the bound (K1_CHUNKS = one static share: always)
+    cap = K1_CHUNKS;
     while (block_pods(nblk) > PODS_PER_BLOCK_MAX) nblk *= 2;
+    cap = K1_CHUNK_CAP;
+    while (cap > K1_CHUNKS && block_pods(nblk) > PODS_PER_BLOCK_MAX) --cap;
+    c->k1_cap = k1_dynamic(c->k1_variant) ? (int)cap : 0;
     nblk = std::min<int64_t>(nblk, std::max(c->k_tiles, c->c_tiles));
     c->nblk = (int)nblk;
     HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * S));
     HIP_TRY(dalloc(&c->d_fold, (size_t)FOLD_SPLIT * 4 * S));
     HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
     HIP_TRY(dalloc(&c->d_wp_cnt, (size_t)S));
+    HIP_TRY(dalloc(&c->d_k1_ticket, 2));
+    HIP_TRY(hipMemset(c->d_k1_ticket, 0, 2 * sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)S * WP_K * sizeof(int64_t)));
     HIP_TRY(hipMemset(c->d_wp_cnt, 0, (size_t)S * sizeof(uint32_t)));
     HIP_TRY(dalloc(&c->d_trk_acc, (size_t)G * TA_K));
@@ -533,7 +546,8 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
         const int32_t S = (int32_t)pod_slots(c);
         for (int32_t g0 = 0; g0 < S; g0 += POD_WINDOW_MAX) {           // LDS windows of pod slots
             const int32_t gw = std::min(POD_WINDOW_MAX, S - g0);
-            HIP_TRY(launch_pod_reduce(p, g, g0, gw, c->nblk, c->k1_variant, c->d_pod_part, c->d_wide_pod, st));
+            HIP_TRY(launch_pod_reduce(p, g, g0, gw, c->nblk, c->k1_variant, c->d_pod_part, c->d_wide_pod,
+                                      c->d_k1_ticket, c->k1_cap, st));
         }
         HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
         nblk = c->nblk;

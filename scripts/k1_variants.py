@@ -11,6 +11,7 @@ import numpy as np  # noqa: E402
 
 cfg = int(os.environ.get("CFG", 4))
 P, N, G = {4: (100_000_000, 1_000_000, 10_000), 2: (1_000_000, 10_000, 100), 3: (10_000_000, 100_000, 100)}[cfg]
+P = int(os.environ.get("PODS", P))            # a rank's shard at N > 1 (fixed-cost study)
 variants = [int(v) for v in os.environ.get("VARIANTS", "0,2,9,10,11").split(",")]
 rounds = int(os.environ.get("ROUNDS", 3))
 import escalator_amd as esc  # noqa: E402
@@ -46,4 +47,4 @@ for v in variants:
     ms = np.array(res[v])
     out[v] = {"median_ms": float(np.median(ms)), "min_ms": float(ms.min()),
               "GBps_median": bytes_k1 / (np.median(ms) * 1e-3) / 1e9}
-print(json.dumps({"config": cfg, "k1_bytes": int(bytes_k1), "variants": out}))
+print(json.dumps({"config": cfg, "pods": P, "k1_bytes": int(bytes_k1), "variants": out}))

@@ -227,6 +227,25 @@ def test_synthetic_vs_c_oracle(esc, cfg, P, N, G):
     check_metrics(ctx.metrics(), soa.metrics(otot, odf, odi))
 
 
+@pytest.mark.parametrize("variant", ["1", "2", "5"])
+def test_k1_variants_vs_c_oracle(esc, variant, monkeypatch):
+    """The exact K1 variants (ESC_K1_VARIANT: 1 two C tiles in flight, 2 1024 threads, 5
+    dynamic shares from the ticket counter — repeated launches check its reset)."""
+    monkeypatch.setenv("ESC_K1_VARIANT", variant)
+    s = esc.Synth(2_000_000, 20_000, 10_000, config=4, seed=0xE5CA1A7E00000004)
+    pods, nodes = s.pods(), s.nodes()
+    otot = soa.totals(pods, nodes, s.groups)
+    odf, odi = soa.decide(s.groups, s.states, otot)
+    ctx = esc.Context(s)
+    ctx.load_synth(s, replicas=2)
+    ctx.use_graph(True)
+    ctx.set_state(s.states)
+    for _ in range(4):
+        ctx.run()
+        tot, dec = ctx.results()
+        check_against_c_oracle(tot, dec, otot, odf, odi)
+
+
 @pytest.mark.parametrize("fused", ["0", "1"])
 def test_synthetic_sort_vs_c_oracle(esc, fused, monkeypatch):
     """Both K5 per-decision paths (three passes; ESC_ORDER_FUSED=1: one pass with
