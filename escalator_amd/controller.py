@@ -63,19 +63,87 @@ def untaint_newest_n(created_ns, n: int, device: int = 0) -> list[int]:
 
 
 class Controller:
-    """RunOnce over every node group as one GPU decision.
+    """RunOnce over every node group as one GPU decision, plus the actuation bookkeeping
+    the next run depends on.
 
     ``list_pods`` / ``list_nodes`` play the informer-backed listers
     (pkg/k8s/pod_listers.go:33, node_listers.go:33): callables returning the full
-    cluster lists (plain-dict records, escalator_amd/objects.py) or raising."""
+    cluster lists (plain-dict records, escalator_amd/objects.py) or raising.
 
-    def __init__(self, groups: list[dict], device: int = 0, dry_mode: bool = False):
+    Host state kept across runs, as the reference's NodeGroupState (controller.go:28-44):
+      * cached capacity of allNodes[0] (controller.go:207-211);
+      * the scale-up lock (scale_lock.go): ScaleUp locks it with the nodes it added
+        (scale_up.go:39); while ``clock() - lock_time < scale_up_cool_down_ns`` every run
+        returns ``requestedNodes`` (controller.go:317-323), after that it unlocks;
+      * the dry-mode taintTracker: taintOldestN appends the names it "taints"
+        (scale_down.go:197-200), untaintNewestN deletes the newest tracked names
+        (scale_up.go:146-158); filterNodes reads it on the next run (controller.go:126-138).
+    Wet-mode API writes (taint / untaint / cloud IncreaseSize) go to an optional
+    ``actuator`` with ``taint(group, idx) -> idx_ok``, ``untaint(group, idx) -> idx_ok`` and
+    ``increase_size(group, n) -> added``; without one every write succeeds and the cloud
+    group adds what was asked (the dry-mode path, scale_up.go:79-88)."""
+
+    def __init__(self, groups: list[dict], device: int = 0, dry_mode: bool = False, clock=None, actuator=None):
+        import time
         from .context import Context
         self.groups = [dict(g, dry_mode=bool(g.get("dry_mode")) or dry_mode) for g in groups]
         self.ctx = Context(self.groups, device=device)
         self.state = [{"locked": False, "requested_nodes": 0, "cached_cpu_m": 0, "cached_mem_b": 0}
                       for _ in groups]
+        self.lock_time = [None] * len(groups)          # scaleLock.lockTime (None: never locked)
         self.taint_tracker = {g: [] for g in range(len(groups))}
+        self.clock = clock or time.time_ns
+        self.actuator = actuator
+
+    def _lock_states(self, now: int):
+        """scaleLock.locked() (scale_lock.go:22-29) for every group, before the decision."""
+        for g, grp in enumerate(self.groups):
+            t = self.lock_time[g]
+            if t is not None and now - t < int(grp.get("scale_up_cool_down_ns", 0)):
+                self.state[g]["locked"] = True
+            else:                                          # unlock(): requestedNodes = 0
+                self.state[g]["locked"] = False
+                self.state[g]["requested_nodes"] = 0
+
+    def _scale_up(self, g: int, n: int, tainted: list[int], names: list[str], out: dict) -> int:
+        """ScaleUp (scale_up.go:14-46): untaintNewestN over the tainted nodes, the rest
+        from the cloud node group, then the lock."""
+        dry = self.groups[g]["dry_mode"]
+        picked = []
+        if tainted:                                        # scaleUpUntaint :98-116
+            order = self.ctx.group_order(g, 1)            # newest first (sort.go:27-39)
+            if dry:                                        # delete tracked names, newest first
+                trk = self.taint_tracker[g]
+                for j in order:
+                    if len(picked) >= n:
+                        break
+                    if names[j] in trk:
+                        trk.remove(names[j])
+                        picked.append(int(j))
+            else:
+                want = [int(j) for j in order[:max(n, 0)]]
+                picked = list(self.actuator.untaint(g, want)) if self.actuator else want
+        out["untainted_now"] = picked
+        rest = n - len(picked)
+        added = 0
+        if rest > 0:                                       # scaleUpCloudProviderNodeGroup :58-96
+            added = int(self.actuator.increase_size(g, rest)) if (self.actuator and not dry) else rest
+            if added > 0:
+                self.lock_time[g] = self.clock()           # scaleLock.lock(added) :39
+                self.state[g]["locked"] = True
+                self.state[g]["requested_nodes"] = added
+        out["added"] = added
+        return len(picked) + added
+
+    def _scale_down_taint(self, g: int, n: int, names: list[str], out: dict):
+        """scaleDownTaint -> taintOldestN (scale_down.go:138-205) with the clamped n."""
+        order = self.ctx.group_order(g, 0, cap=max(n, 0))  # untainted, oldest first
+        want = [int(j) for j in order[:max(n, 0)]]
+        if self.groups[g]["dry_mode"]:
+            self.taint_tracker[g] += [names[j] for j in want]
+            out["tainted_now"] = want
+        else:
+            out["tainted_now"] = list(self.actuator.taint(g, want)) if self.actuator else want
 
     def run_once(self, list_pods, list_nodes) -> list[dict]:
         try:
@@ -86,19 +154,32 @@ class Controller:
             nodes = list_nodes()
         except Exception as e:                   # controller.go:202-205
             return [{"delta": 0, "err": str(e)} for _ in self.groups]
-        trackers = {g: t for g, t in self.taint_tracker.items() if t}
+        self._lock_states(self.clock())
+        trackers = {g: list(t) for g, t in self.taint_tracker.items() if t}
         P, N = self.ctx.pack(pods, nodes, trackers)
         self.ctx.load(P, N)
         tot, dec = self.ctx.decide_all(self.state)
+        self.ctx.sort_nodes()
+        names = [n.get("name", "") for n in nodes]
         out = []
         for g in range(len(self.groups)):
             d = dec[g]
             self.state[g]["cached_cpu_m"] = int(d["cached_cpu_m"])        # controller.go:208-211
             self.state[g]["cached_mem_b"] = int(d["cached_mem_b"])
-            out.append({"delta": int(d["delta"]), "err": ERRORS.get(int(d["status"])),
-                        "branch": L.BRANCHES[int(d["branch"])], "cpu_pct": float(d["cpu_pct"]),
-                        "mem_pct": float(d["mem_pct"]), "n_to_taint": int(d["n_to_taint"]),
-                        "totals": {k: int(tot[g][k]) for k in tot.dtype.names}})
+            branch = L.BRANCHES[int(d["branch"])]
+            r = {"delta": int(d["delta"]), "err": ERRORS.get(int(d["status"])),
+                 "branch": branch, "cpu_pct": float(d["cpu_pct"]),
+                 "mem_pct": float(d["mem_pct"]), "n_to_taint": int(d["n_to_taint"]),
+                 "totals": {k: int(tot[g][k]) for k in tot.dtype.names},
+                 "tainted_now": [], "untainted_now": [], "added": 0}
+            tainted = self.ctx.group_order(g, 1) if int(tot["n_tainted"][g]) else []
+            if branch == "below_min":                                     # controller.go:281-295
+                r["delta"] = self._scale_up(g, r["delta"], list(tainted), names, r)
+            elif r["err"] is None and branch in ("fast_down", "slow_down") and int(d["taint_status"]) == 0:
+                self._scale_down_taint(g, r["n_to_taint"], names, r)      # controller.go:369-371
+            elif r["err"] is None and branch == "scale_up" and r["delta"] > 0:
+                self._scale_up(g, r["delta"], list(tainted), names, r)    # controller.go:372-375
+            out.append(r)
         return out
 
     def scale_node_group(self, name: str, list_pods, list_nodes) -> tuple[int, str | None]:

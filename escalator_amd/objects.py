@@ -201,9 +201,15 @@ def placement(pods: list[dict], nodes: list[dict]):
     CreateNodeNameToInfoMap drops those, node_state.go:31-36), each node's escalator-taint
     time and its no-delete annotation (safeFromDeletion, scale_down.go:39-46)."""
     import numpy as np
+    # CreateNodeNameToInfoMap is keyed by name: two nodes sharing one would share one
+    # NodeInfo (node_state.go:10-39).  Kubernetes node names are unique, so a duplicate is
+    # an input error here rather than a pod run silently attached to one of them.
     index = {}
     for j, n in enumerate(nodes):
-        index.setdefault(n.get("name", ""), j)
+        name = n.get("name", "")
+        if name in index:
+            raise ValueError("duplicate node name %r (nodes %d and %d)" % (name, index[name], j))
+        index[name] = j
     pod_node = np.array([index.get(p.get("node_name") or "", _NONE) if p.get("node_name") else _NONE
                          for p in pods], np.uint32)
     taint_s = np.array([taint_time(n) for n in nodes], np.int64)

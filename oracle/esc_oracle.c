@@ -439,3 +439,58 @@ int64_t orc_try_remove(int64_t n_pods, const uint32_t* flags, const uint32_t* pa
     free(occ);
     return del;
 }
+
+/* Every group's two orderings at once (the full-size config-5 check): one pass buckets
+ * each (node, group) membership of nodes [lo, hi) by (group, class) — classes 0
+ * untainted (oldest first) and 1 tainted (newest first), cordoned dropped — and each
+ * bucket is sorted as orc_order sorts.  off[2G + 1] (bucket g * 2 + which), idx[off[2G]].
+ * Two calls: idx == NULL only counts (fills off). */
+int64_t orc_order_all(int64_t n_nodes, const uint32_t* nflags, const uint32_t* label0, const int64_t* created,
+                      const uint32_t* xl, const int32_t* tn, const int32_t* tg, int64_t n_trk, int64_t lo, int64_t hi,
+                      const uint8_t* dry, const uint32_t* gpair, uint32_t n_gp, int32_t G, int64_t* off, int64_t* idx) {
+    PairIdx px;
+    if (pair_idx(&px, gpair, n_gp, G, -1)) return -1;
+    int64_t* cnt = (int64_t*)calloc((size_t)2 * G + 1, sizeof(int64_t));
+    KI* v = NULL;
+    if (!cnt) { pair_idx_free(&px); return -1; }
+    for (int pass = 0; pass < 2; ++pass) {
+        if (pass == 1) {
+            if (!idx) break;
+            v = (KI*)malloc(sizeof(KI) * (size_t)(off[2 * G] + 1));
+            if (!v) { free(cnt); pair_idx_free(&px); return -1; }
+            for (int64_t b = 0; b < 2 * (int64_t)G; ++b) cnt[b] = off[b];
+        }
+        uint64_t q = 0;
+        for (int64_t i = 0; i < lo && i < n_nodes; ++i) q += xlbl(nflags[i]);
+        for (int64_t i = lo; i < hi; ++i) {
+            const uint32_t f = nflags[i];
+            const uint32_t nx = xlbl(f);
+            for (uint32_t k = 0; k <= nx; ++k) {
+                const uint32_t pr = k == 0 ? label0[i] : xl[q++];
+                for (int32_t g = first_group(&px, pr); g >= 0; g = px.nxt[g]) {
+                    const int c = node_class(f, dry[g], tn, tg, n_trk, i, g);
+                    if (c > 1) continue;
+                    const int64_t b = 2 * (int64_t)g + c;
+                    if (pass == 0) { cnt[b]++; continue; }
+                    v[cnt[b]].key = c == 0 ? created[i] : -created[i];
+                    v[cnt[b]].idx = i;
+                    cnt[b]++;
+                }
+            }
+        }
+        if (pass == 0) {
+            off[0] = 0;
+            for (int64_t b = 0; b < 2 * (int64_t)G; ++b) off[b + 1] = off[b] + cnt[b];
+        }
+    }
+    if (v) {
+        for (int64_t b = 0; b < 2 * (int64_t)G; ++b) {
+            qsort(v + off[b], (size_t)(off[b + 1] - off[b]), sizeof(KI), cmp_ki);
+            for (int64_t k = off[b]; k < off[b + 1]; ++k) idx[k] = v[k].idx;
+        }
+        free(v);
+    }
+    free(cnt);
+    pair_idx_free(&px);
+    return off[2 * G];
+}

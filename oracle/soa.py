@@ -141,6 +141,27 @@ def order(nodes: dict, groups: list[dict], group: int, which: int, node_lo: int 
     return out if cap is None else out[:cap]
 
 
+def order_all(nodes: dict, groups: list[dict], node_lo: int = 0, node_hi: int | None = None) -> dict:
+    """orc_order_all: {(group, which): indices} for every group and both orders, one pass."""
+    t = group_tables(groups)
+    G = len(groups)
+    n = len(nodes["flags"])
+    hi = n if node_hi is None else node_hi
+    args = [C.c_int64(n), _p(nodes["flags"], C.c_uint32), _p(nodes["label0"], C.c_uint32),
+            _p(nodes["created_ns"], C.c_int64), _p(nodes["xl_pair"], C.c_uint32),
+            _p(nodes["trk_node"], C.c_int32), _p(nodes["trk_group"], C.c_int32),
+            C.c_int64(len(nodes["trk_node"])), C.c_int64(node_lo), C.c_int64(hi),
+            _p(t["dry"], C.c_uint8), _p(t["gpair"], C.c_uint32), C.c_uint32(len(t["pair_ids"])), C.c_int32(G)]
+    off = np.zeros(2 * G + 1, np.int64)
+    lib().orc_order_all.restype = C.c_int64
+    if lib().orc_order_all(*args, _p(off, C.c_int64), None) < 0:
+        raise MemoryError("orc_order_all")
+    idx = np.zeros(max(int(off[-1]), 1), np.int64)
+    if lib().orc_order_all(*args, _p(off, C.c_int64), _p(idx, C.c_int64)) < 0:
+        raise MemoryError("orc_order_all")
+    return {(g, w): idx[off[2 * g + w]:off[2 * g + w + 1]] for g in range(G) for w in (0, 1)}
+
+
 def try_remove(pods: dict, nodes: dict, groups: list[dict], pod_node, taint_s, no_delete, group: int,
                now_ns: int, soft_ns: int, hard_ns: int):
     """orc_try_remove: TryRemoveTaintedNodes for one group (scale_down.go:51-136) over a

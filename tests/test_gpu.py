@@ -610,3 +610,140 @@ def test_tracker_updates_vs_literal(esc, seed):
         assert list(ctx.tracker_list(g)) == before
         ctx.tracker_update(g, remove=free[:3])
         assert list(ctx.tracker_list(g)) == before
+
+
+# ------------------------------------------------ controller host state across runs
+def test_controller_dry_mode_tracker_across_scans(esc):
+    """Dry mode over several scans: taintOldestN appends the names it taints to
+    the tracker (scale_down.go:197-200), the next scan's filterNodes counts them as tainted
+    (controller.go:126-138), and a scale-up deletes the newest tracked names first
+    (untaintNewestN, scale_up.go:146-158).  Every scan equals the literal oracle run with
+    the tracker the reference would hold at that point."""
+    from escalator_amd.controller import Controller
+    opts = {"min_nodes": 5, "max_nodes": 100, "scale_up_pct": 70, "taint_lower_pct": 40, "taint_upper_pct": 60,
+            "fast_removal_rate": 4, "slow_removal_rate": 2, "dry_mode": True}
+    grp = _default_group(opts)
+    nodes = [dict(n, created_ns=1_000_000 + 7919 * ((i * 37) % 10)) for i, n in
+             enumerate(build_test_nodes(10, {"CPU": 2000, "Mem": 8000}))]
+    ctl = Controller([grp])
+    tracker = []                                    # the reference's nodeGroup.taintTracker
+    pods = []
+    expect_deltas = []
+    for scan in range(5):
+        if scan == 3:                               # load arrives: scale up, untaint newest
+            pods = build_test_pods(60, {"CPU": [500], "Mem": [1000]})
+        L = O.scale_node_group(grp, {}, pods, nodes, tracker=list(tracker))
+        r = ctl.run_once(lambda: pods, lambda: nodes)[0]
+        assert (r["totals"]["n_untainted"], r["totals"]["n_tainted"]) == (L["n_untainted"], L["n_tainted"]), scan
+        assert (r["branch"], r["delta"]) == (L["branch"], L["delta"]), (scan, r, L)
+        expect_deltas.append(L["delta"])
+        # the reference's actuation on its own lists
+        if L["delta"] < 0 and L["taint_err"] is None:
+            unt = L["untainted"]
+            picked = [unt[i] for i in O.taint_oldest_n([nodes[i]["created_ns"] for i in unt], L["n_to_taint"])]
+            tracker += [nodes[i]["name"] for i in picked]
+            assert r["tainted_now"] == picked, scan
+        elif L["delta"] > 0:
+            tn = L["tainted"]
+            picked = [tn[i] for i in O.newest_first([nodes[i]["created_ns"] for i in tn])][:L["delta"]]
+            for i in picked:
+                tracker.remove(nodes[i]["name"])
+            assert r["untainted_now"] == picked, scan
+        assert ctl.taint_tracker[0] == tracker, scan
+    assert expect_deltas[:3] == [-4, -4, -4] and expect_deltas[3] > 0
+
+
+def test_controller_scale_up_cool_down_lock(esc):
+    """ScaleUp locks the group with the nodes it added (scale_up.go:39); inside
+    ScaleUpCoolDownPeriod every run returns requestedNodes (controller.go:317-323,
+    scale_lock.go:22-29), afterwards the lock opens and the delta is computed again."""
+    from escalator_amd.controller import Controller
+    grp = _default_group({"min_nodes": 0, "max_nodes": 100, "scale_up_pct": 70, "taint_lower_pct": 40,
+                          "taint_upper_pct": 60, "fast_removal_rate": 4, "slow_removal_rate": 2,
+                          "scale_up_cool_down_ns": 60 * 10**9})
+    nodes = build_test_nodes(10, {"CPU": 2000, "Mem": 8000})
+    pods = build_test_pods(60, {"CPU": [500], "Mem": [1000]})
+    now = [1_700_000_000 * 10**9]
+    ctl = Controller([grp], clock=lambda: now[0])
+    r = ctl.run_once(lambda: pods, lambda: nodes)[0]
+    assert r["branch"] == "scale_up" and r["delta"] == 12 and r["added"] == 12
+    now[0] += 30 * 10**9                            # inside the cool-down: locked
+    r = ctl.run_once(lambda: pods, lambda: nodes)[0]
+    assert (r["branch"], r["delta"]) == ("locked", 12)
+    now[0] += 31 * 10**9                            # cool-down over: computed again
+    r = ctl.run_once(lambda: pods, lambda: nodes)[0]
+    assert (r["branch"], r["delta"]) == ("scale_up", 12)
+
+
+# ------------------------------------------------ filter truth tables through the HIP path
+def test_filter_truth_tables_through_hip(esc, golden):
+    """node_group_test.go:13-318 (NewPodAffinityFilterFunc, NewPodDefaultFilterFunc,
+    NewNodeLabelFilterFunc truth tables) through pack -> K1 / K2 -> per-group counts: a
+    one-group context holding only the case's pod (node) counts it iff the filter selects
+    it."""
+    fx = golden["controller"]
+    for c in fx["pod_affinity_filter"]["cases"]:
+        pod = build_test_pod(fx["pod_affinity_filter"]["pods"][c["pod"]])
+        ctx = esc.Context([{"name": "g", "label_key": c["key"], "label_value": c["value"], "max_nodes": 10}])
+        ctx.load(*ctx.pack([pod], []))
+        tot, _ = ctx.decide_all()
+        assert int(tot["n_pods"][0]) == int(c["want"]), c["name"]
+    for c in fx["pod_default_filter"]["cases"]:
+        pod = build_test_pod(fx["pod_default_filter"]["pods"][c["pod"]])
+        ctx = esc.Context([{"name": "default", "label_key": "k", "label_value": "v", "max_nodes": 10}])
+        ctx.load(*ctx.pack([pod], []))
+        tot, _ = ctx.decide_all()
+        assert int(tot["n_pods"][0]) == int(c["want"]), c["name"]
+    for c in fx["node_label_filter"]["cases"]:
+        node = build_test_node(fx["node_label_filter"]["nodes"][c["node"]])
+        ctx = esc.Context([{"name": "g", "label_key": c["key"], "label_value": c["value"], "max_nodes": 10}])
+        ctx.load(*ctx.pack([], [node]))
+        tot, _ = ctx.decide_all()
+        assert int(tot["n_nodes"][0]) == int(c["want"]), c["name"]
+        ctx.sort_nodes()
+        assert len(ctx.group_order(0, 0)) + len(ctx.group_order(0, 1)) + int(tot["n_cordoned"][0]) == int(c["want"])
+
+
+# ------------------------------------------------ BASELINE.json configs at their stated sizes
+def test_config3_full_size_vs_c_oracle(esc):
+    """BASELINE config #3 at its stated size: 10M pods / 100k nodes / 100 multi-instance-type
+    groups with slack (scale-up deltas and float64 percentages bit-exact)."""
+    s = esc.Synth(10_000_000, 100_000, 100, config=3, seed=0xE5CA1A7E00000003, threads=16)
+    pods, nodes = s.pods(), s.nodes()
+    otot = soa.totals(pods, nodes, s.groups)
+    odf, odi = soa.decide(s.groups, s.states, otot)
+    ctx = esc.Context(s)
+    ctx.load_synth(s, replicas=2)
+    ctx.use_graph(True)
+    ctx.set_state(s.states)
+    for _ in range(3):
+        ctx.run()
+        tot, dec = ctx.results()
+        check_against_c_oracle(tot, dec, otot, odf, odi)
+    assert (dec["branch"] == 7).sum() >= 50, "config 3 is tuned so that most groups scale up"
+
+
+def test_config5_full_size_orderings_vs_c_oracle(esc):
+    """BASELINE config #5 at its stated size: 10M nodes in 100 groups; every group's
+    taint order (untainted oldest first) and untaint order (tainted newest first) equal the
+    C oracle's, and the decision's totals too."""
+    s = esc.Synth(100_000, 10_000_000, 100, config=5, seed=0xE5CA1A7E00000005, threads=16)
+    pods, nodes = s.pods(), s.nodes()
+    want = soa.order_all(nodes, s.groups)
+    ctx = esc.Context(s)
+    ctx.load_synth(s)
+    ctx.set_state(s.states)
+    ctx.run()
+    tot, dec = ctx.results()
+    otot = soa.totals(pods, nodes, s.groups)
+    odf, odi = soa.decide(s.groups, s.states, otot)
+    check_against_c_oracle(tot, dec, otot, odf, odi)
+    for _ in range(2):
+        ctx.sort_nodes()
+    n = 0
+    for g in range(100):
+        for w in (0, 1):
+            got = ctx.group_order(g, w)
+            assert np.array_equal(got, want[(g, w)]), (g, w, len(got), len(want[(g, w)]))
+            n += len(got)
+    assert n > 9_000_000
