@@ -14,7 +14,8 @@ LIB_PATH = os.path.join(HERE, "libescalator_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "escalator_hip.h")
 
 ESC_OK = 0
-ESC_E_INVAL, ESC_E_HIP, ESC_E_NOMEM, ESC_E_LIMIT, ESC_E_STATE, ESC_E_NODEV = -1, -2, -3, -4, -5, -6
+ESC_E_INVAL, ESC_E_HIP, ESC_E_NOMEM, ESC_E_LIMIT, ESC_E_STATE, ESC_E_NODEV, ESC_E_COMM = -1, -2, -3, -4, -5, -6, -7
+ESC_COMM_ID_BYTES = 128
 ESC_NONE = 0xFFFFFFFF
 
 ESC_ST_OK, ESC_ST_ERR_MIN_NODES, ESC_ST_ERR_MAX_NODES, ESC_ST_ERR_DIV_ZERO = 0, 1, 2, 3
@@ -144,6 +145,10 @@ _SIGS = {
     "esc_decide": (i32, [VP]),
     "esc_run": (i32, [VP]),
     "esc_sync": (i32, [VP]),
+    "esc_comm_unique_id": (i32, [VP]),
+    "esc_comm_init": (i32, [VP, VP, i32, i32]),
+    "esc_exchange": (i32, [VP]),
+    "esc_step": (i32, [VP]),
     "esc_results": (i32, [VP, P(GroupTotals), P(GroupDecision)]),
     "esc_set_spare": (i32, [VP, dbl]),
     "esc_pods_upsert": (i32, [VP, P(i64), P(PodSoA)]),

@@ -253,6 +253,28 @@ class Context:
     def sync(self):
         L.check(self.lib.esc_sync(self.handle), "esc_sync")
 
+    # ------------------------------------------ RCCL exchange inside the library (§8e)
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """ncclGetUniqueId (rank 0); ship the bytes to the other ranks, then comm_init."""
+        buf = C.create_string_buffer(L.ESC_COMM_ID_BYTES)
+        L.check(L.load().esc_comm_unique_id(buf), "esc_comm_unique_id")
+        return buf.raw
+
+    def comm_init(self, uid: bytes, rank: int, world: int):
+        """ncclCommInitRank on the context's device (collective over the world's ranks)."""
+        assert len(uid) == L.ESC_COMM_ID_BYTES
+        buf = C.create_string_buffer(uid, L.ESC_COMM_ID_BYTES)
+        L.check(self.lib.esc_comm_init(self.handle, buf, rank, world), "esc_comm_init")
+
+    def exchange(self):
+        """ncclAllReduce(int64, SUM) of the pod words, in place, on the context's stream."""
+        L.check(self.lib.esc_exchange(self.handle), "esc_exchange")
+
+    def step(self):
+        """esc_reduce + esc_exchange + esc_decide (esc_run without a communicator)."""
+        L.check(self.lib.esc_step(self.handle), "esc_step")
+
     def exchange_buffers(self):
         sb, mb = C.c_void_p(), C.c_void_p()
         sc, mc = C.c_int64(), C.c_int64()

@@ -33,14 +33,14 @@ constexpr int64_t PODS_PER_BLOCK_MAX  = int64_t(1) << 20;  // keeps cpu|count<<4
 constexpr int CNT_SHIFT = 40;
 constexpr uint64_t CPU_MASK = (uint64_t(1) << CNT_SHIFT) - 1;
 
-// Exchanged per-group words (int64, all-reduced with SUM across ranks).  Every sum
-// travels split as lo = v & 0xffffffff, hi = v >> 32 (arithmetic) so the cross-rank
-// SUM cannot wrap and the exact total is recoverable (Quantity.Add's overflow check).
-enum TotWord : int {
-    TW_POD_CPU_LO = 0, TW_POD_CPU_HI, TW_POD_MEM_LO, TW_POD_MEM_HI, TW_N_PODS,
-    TW_NODE_CPU_LO, TW_NODE_CPU_HI, TW_NODE_MEM_LO, TW_NODE_MEM_HI,
-    TW_N_UNT, TW_N_TAINT, TW_N_CORD, TW_K
-};
+// Per-group pod words, all-reduced with SUM across ranks (the only exchange: every rank
+// reduces the whole node index itself).  Every sum travels split as
+// lo = v & 0xffffffff, hi = v >> 32 (arithmetic) so the cross-rank SUM cannot wrap and
+// the exact total is recoverable (Quantity.Add's overflow check).
+enum PodWord : int { PW_CPU_LO = 0, PW_CPU_HI, PW_MEM_LO, PW_MEM_HI, PW_N, PW_K };
+// Per-group node words (rank-local, exact): untainted capacity sums and the filterNodes
+// counts; NW_FLAGS carries ESC_TF_NODE_OVERFLOW.
+enum NodeWord : int { NW_CPU = 0, NW_MEM, NW_N_UNT, NW_N_TAINT, NW_N_CORD, NW_FLAGS, NW_K };
 
 // Device-side per-group parameters (from esc_group_spec + esc_group_state).
 struct GroupParams {

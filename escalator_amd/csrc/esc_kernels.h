@@ -146,7 +146,7 @@ constexpr int FOLD_SPLIT = 8;   // K3a: row ranges the K1 partials fold into (fo
 hipError_t launch_pod_fold(const uint64_t* pod_part, int nblk, int64_t S, uint64_t* fold, hipStream_t st);
 hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* fold, int nsplit,
                           const int64_t* node_rows, int64_t* wide_pod, uint32_t* wp_cnt, int64_t* trk_acc,
-                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st);
+                          int64_t* pwords, int64_t* nwords, bool decide, esc_group_decision* dec, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
 // §8f rank 2: a loaded pod as seen by NodePodsRemaining, listed per node (runs in
 // node order).  p[0..2]: the pod's extra pairs (NONE-padded); a C pod with more than 3
@@ -180,8 +180,8 @@ struct PatchTargets {          // k_patch destinations: 4-byte arrays 0-5, 8-byt
     int64_t* i64[6];
 };
 hipError_t launch_patch(const PatchTargets& t, const uint64_t* where, const uint64_t* what, int64_t n, hipStream_t st);
-hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* words,
-                         const int64_t* first, esc_group_decision* dec, hipStream_t st);
+hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords,
+                         const int64_t* nwords, esc_group_decision* dec, hipStream_t st);
 
 // Ordering (K5), see esc_kernels.hip: the age index (once per snapshot) and the per-decision
 // (group, class) partition.

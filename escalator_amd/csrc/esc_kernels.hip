@@ -301,7 +301,7 @@ __device__ __forceinline__ void k_sink(const KTile<R, NXP>& T) {   // loads-only
 // held (an L2 hit; never one address shared by every wave — that serialises on one
 // channel: 0.9 ms instead of 0.4 ms for config 4), so that every load is unconditional
 // and the compiler's vmcnt accounting never waits early.
-template <int R, int NXP, int NW, int ABLATE>
+template <int R, int NXP, int NW, int ABLATE, int ST>
 __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const PodSink<ABLATE>& K,
                                       const PodClass& C, int64_t a, int64_t b, uint32_t lane) {
     constexpr int L = 5 + 4 * R + NXP;                   // 16-B loads per lane per tile
@@ -313,14 +313,14 @@ __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const 
     KTile<R, NXP> T[DS];
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
-        const int64_t u = a + (int64_t)d * NW;
+        const int64_t u = a + (int64_t)d * ST;
         k_load(P, C, u < b ? u : a, lane, T[d]);
         __builtin_amdgcn_sched_barrier(0);            // slots issue in order (see below)
     }
-    for (int64_t t = a; t < b; t += (int64_t)DS * NW) {
+    for (int64_t t = a; t < b; t += (int64_t)DS * ST) {
 #pragma unroll
         for (int d = 0; d < DS; ++d) {
-            const int64_t u = t + (int64_t)d * NW;
+            const int64_t u = t + (int64_t)d * ST;
             if (u < b) {                                       // wave-uniform
                 if constexpr (ABLATE & 32) k_sink(T[d]);
                 else k_process<R, NXP, ABLATE>(G, K, C, T[d]);
@@ -328,7 +328,7 @@ __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const 
             // keep slot d's refill after its use: hoisting it would make the next slots'
             // waits count it (vmcnt is in order) and drain the pipeline
             __builtin_amdgcn_sched_barrier(0);
-            const int64_t nu = u + (int64_t)DS * NW;
+            const int64_t nu = u + (int64_t)DS * ST;
             k_load(P, C, nu < b ? nu : (u < b ? u : a), lane, T[d]);
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -483,7 +483,7 @@ __device__ __forceinline__ void c_tile_exact(const PodDev& P, const GroupDev& G,
 // DYN: the K tiles' weight is cut into gridDim.x * K1_CHUNKS chunks taken from a ticket
 // counter (at most `cap` per workgroup), so workgroups that stream faster take more
 // and the launch does not wait on the slowest static share; DYN 0: one static share each.
-template <int THREADS, int ABLATE = 0, int DC = 3, int DYN = 0>
+template <int THREADS, int ABLATE = 0, int DC = 3, int DYN = 0, int WS = 0>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
                                                         int64_t* __restrict__ wide,
@@ -495,7 +495,9 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     const PodSink<ABLATE> K{PodLds{lds, lds + gw, g0, gw}, PodWide{wide}};
     const uint32_t lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t n_chunks = DYN ? (int64_t)gridDim.x * K1_CHUNKS : gridDim.x;
+    // WS: every wave takes its own contiguous share of the K weight (a wave's restarts at
+    // class boundaries then idle only that wave, the WG's other waves keep streaming)
+    const int64_t n_chunks = DYN ? (int64_t)gridDim.x * K1_CHUNKS : (WS ? (int64_t)gridDim.x * NW : gridDim.x);
     // every thread has read the previous ticket before thread 0 overwrites it
     auto grab = [&]() -> int64_t {
         __syncthreads();
@@ -503,7 +505,7 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
         __syncthreads();
         return (int64_t)__builtin_amdgcn_readfirstlane(s_chunk);
     };
-    int64_t chunk = blockIdx.x;
+    int64_t chunk = WS ? (int64_t)blockIdx.x * NW + wid : blockIdx.x;
     if constexpr (DYN) chunk = grab();
     else __syncthreads();
     for (int taken = 1; !(ABLATE & 2) && chunk < n_chunks; ++taken) {
@@ -517,11 +519,11 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
             const int64_t n = C.t1 - C.t0;
             const int64_t i0 = imin64(n, imax64(0, (wl - C.w0 + C.wt - 1) / C.wt));
             const int64_t i1 = imin64(n, imax64(0, (wh - C.w0 + C.wt - 1) / C.wt));
-            const int64_t a = C.t0 + i0 + wid, b = C.t0 + i1;
+            const int64_t a = C.t0 + i0 + (WS ? 0 : wid), b = C.t0 + i1;
             if (a >= b) continue;
             switch (C.kind) {
 #define ESC_KRUN(RR, XX) \
-    case RR * 4 + XX: k_run<RR, XX, NW, ABLATE>(P, G, K, C, a, b, lane); break;
+    case RR * 4 + XX: k_run<RR, XX, NW, ABLATE, (WS ? 1 : NW)>(P, G, K, C, a, b, lane); break;
                 ESC_KRUN(0, 0) ESC_KRUN(0, 1) ESC_KRUN(0, 2) ESC_KRUN(0, 3)
                 ESC_KRUN(1, 0) ESC_KRUN(1, 1) ESC_KRUN(1, 2) ESC_KRUN(1, 3)
                 ESC_KRUN(2, 0) ESC_KRUN(2, 1) ESC_KRUN(2, 2) ESC_KRUN(2, 3)
@@ -778,18 +780,18 @@ __device__ __forceinline__ __int128 join_parts(uint64_t lo, uint64_t lo_carry, i
 }
 
 __device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn, int32_t g,
-                                         const int64_t* __restrict__ w, esc_group_decision& dec,
-                                         esc_group_metrics* __restrict__ met) {
+                                         const int64_t* __restrict__ pw, const int64_t* __restrict__ nw,
+                                         esc_group_decision& dec, esc_group_metrics* __restrict__ met) {
     Totals t;
-    int64_t flags = 0;
-    if (!join_split(w[TW_POD_CPU_LO], w[TW_POD_CPU_HI], t.pod_cpu)) flags |= ESC_TF_POD_OVERFLOW;
-    if (!join_split(w[TW_POD_MEM_LO], w[TW_POD_MEM_HI], t.pod_mem)) flags |= ESC_TF_POD_OVERFLOW;
-    t.n_pods = w[TW_N_PODS];
-    if (!join_split(w[TW_NODE_CPU_LO], w[TW_NODE_CPU_HI], t.node_cpu)) flags |= ESC_TF_NODE_OVERFLOW;
-    if (!join_split(w[TW_NODE_MEM_LO], w[TW_NODE_MEM_HI], t.node_mem)) flags |= ESC_TF_NODE_OVERFLOW;
-    t.n_unt = w[TW_N_UNT];
-    t.n_taint = w[TW_N_TAINT];
-    t.n_cord = w[TW_N_CORD];
+    int64_t flags = nw[NW_FLAGS];
+    if (!join_split(pw[PW_CPU_LO], pw[PW_CPU_HI], t.pod_cpu)) flags |= ESC_TF_POD_OVERFLOW;
+    if (!join_split(pw[PW_MEM_LO], pw[PW_MEM_HI], t.pod_mem)) flags |= ESC_TF_POD_OVERFLOW;
+    t.n_pods = pw[PW_N];
+    t.node_cpu = nw[NW_CPU];
+    t.node_mem = nw[NW_MEM];
+    t.n_unt = nw[NW_N_UNT];
+    t.n_taint = nw[NW_N_TAINT];
+    t.n_cord = nw[NW_N_CORD];
     t.n_nodes = t.n_unt + t.n_taint + t.n_cord;
     t.first = gn.first;
     t.first_cpu = gn.first_cpu;
@@ -867,8 +869,8 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
                                                            int64_t* __restrict__ wide_pod,
                                                            uint32_t* __restrict__ wp_cnt,
                                                            int64_t* __restrict__ trk_acc,
-                                                           int64_t* __restrict__ words,
-                                                           int64_t* __restrict__ firsts, int decide,
+                                                           int64_t* __restrict__ pwords,
+                                                           int64_t* __restrict__ nwords, int decide,
                                                            esc_group_decision* __restrict__ dec) {
     // a: 0 pod cpu, 1 pod count, 2-3 pod mem (lo, carry), 4-6 untainted / tainted /
     //    cordoned counts, then node sums as (lo, carry, hi) triples: 7-9 untainted cpu,
@@ -957,13 +959,13 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
             __hip_atomic_store(wp_cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    int64_t* w = words + (int64_t)g * TW_K;
+    int64_t* pw = pwords + (int64_t)g * PW_K;
     const __int128 pcpu = (__int128)a[0] + ((__int128)p[WP_CPU_HI] << 32) + (__int128)p[WP_CPU_LO];
     const __int128 pmem = (__int128)(((unsigned __int128)a[3] << 64) | a[2]) + ((__int128)p[WP_MEM_HI] << 32) +
                           (__int128)p[WP_MEM_LO];
-    split_store(w, TW_POD_CPU_LO, pcpu);
-    split_store(w, TW_POD_MEM_LO, pmem);
-    w[TW_N_PODS] = (int64_t)a[1] + p[WP_CNT];
+    split_store(pw, PW_CPU_LO, pcpu);
+    split_store(pw, PW_MEM_LO, pmem);
+    pw[PW_N] = (int64_t)a[1] + p[WP_CNT];
     __int128 ncpu, nmem;
     uint64_t n_unt = a[4], n_taint = a[5], n_cord = a[6];
     if (!G.dry[g]) {
@@ -983,13 +985,17 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
         n_taint = (uint64_t)tr[TA_CNT];
         n_cord = 0;
     }
-    split_store(w, TW_NODE_CPU_LO, ncpu);
-    split_store(w, TW_NODE_MEM_LO, nmem);
-    w[TW_N_UNT] = (int64_t)n_unt;
-    w[TW_N_TAINT] = (int64_t)n_taint;
-    w[TW_N_CORD] = (int64_t)n_cord;
-    firsts[g] = gn.first;
-    if (decide) finalize(G, gn, g, w, sdec[lane], G.metrics);
+    // the node words stay on this rank: every rank reduces the whole node index
+    int64_t* nw = nwords + (int64_t)g * NW_K;
+    const bool n_ok = ncpu >= (__int128)INT64_MIN && ncpu <= (__int128)INT64_MAX &&
+                      nmem >= (__int128)INT64_MIN && nmem <= (__int128)INT64_MAX;
+    nw[NW_CPU] = (int64_t)ncpu;
+    nw[NW_MEM] = (int64_t)nmem;
+    nw[NW_N_UNT] = (int64_t)n_unt;
+    nw[NW_N_TAINT] = (int64_t)n_taint;
+    nw[NW_N_CORD] = (int64_t)n_cord;
+    nw[NW_FLAGS] = n_ok ? 0 : ESC_TF_NODE_OVERFLOW;
+    if (decide) finalize(G, gn, g, pw, nw, sdec[lane], G.metrics);
     }
     if (decide) {
         __syncthreads();
@@ -997,13 +1003,14 @@ __global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N
     }
 }
 
-__global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ words,
-                                                const int64_t* __restrict__ firsts,
+__global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ pwords,
+                                                const int64_t* __restrict__ nwords,
                                                 esc_group_decision* __restrict__ dec) {
     __shared__ esc_group_decision sdec[64];
     const int32_t g = blockIdx.x * 64 + (int32_t)threadIdx.x;
     if (threadIdx.x < 64 && g < G.G)
-        finalize(G, N.gnode[g], g, words + (int64_t)g * TW_K, sdec[threadIdx.x], G.metrics);
+        finalize(G, N.gnode[g], g, pwords + (int64_t)g * PW_K, nwords + (int64_t)g * NW_K, sdec[threadIdx.x],
+                 G.metrics);
     __syncthreads();
     store_decisions(dec, blockIdx.x * 64, G.G, sdec);
 }
@@ -1792,10 +1799,13 @@ hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int
                              uint64_t* part, int64_t* wide, uint32_t* ticket, int cap, hipStream_t st) {
     const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
 #define ESC_K1(T, A, DC) ESC_K1D(T, A, DC, 0)
-#define ESC_K1D(T, A, DC, D)                                                                          \
-    hipLaunchKernelGGL((k_pod_reduce<T, A, DC, D>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, \
+#define ESC_K1D(T, A, DC, D) ESC_K1W(T, A, DC, D, 0)
+#define ESC_K1W(T, A, DC, D, W)                                                                       \
+    hipLaunchKernelGGL((k_pod_reduce<T, A, DC, D, W>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, \
                        wide, ticket, cap)
     switch (variant) {
+        case 6: ESC_K1W(512, 0, 3, 0, 1); break;   // per-wave shares of the K weight
+        case 14: ESC_K1W(512, 4 | 32, 3, 0, 1); break;   // per-wave shares, K tiles, loads only
         case 5: ESC_K1D(512, 0, 3, 1); break;   // dynamic shares (measured slower)
         case 1: ESC_K1(512, 0, 2); break;
         case 2: ESC_K1(1024, 0, 3); break;
@@ -1811,6 +1821,7 @@ hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int
     }
 #undef ESC_K1
 #undef ESC_K1D
+#undef ESC_K1W
     return hipGetLastError();
 }
 
@@ -1839,9 +1850,9 @@ hipError_t launch_pod_fold(const uint64_t* pod_part, int nblk, int64_t S, uint64
 
 hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* fold, int nsplit,
                           const int64_t* node_rows, int64_t* wide_pod, uint32_t* wp_cnt, int64_t* trk_acc,
-                          int64_t* words, int64_t* first, bool decide, esc_group_decision* dec, hipStream_t st) {
+                          int64_t* pwords, int64_t* nwords, bool decide, esc_group_decision* dec, hipStream_t st) {
     hipLaunchKernelGGL(k_combine, dim3((g.G + 63) / 64), dim3(CB_WAVES * 64), 0, st, g, n, fold, nsplit,
-                       node_rows, wide_pod, wp_cnt, trk_acc, words, first, decide ? 1 : 0, dec);
+                       node_rows, wide_pod, wp_cnt, trk_acc, pwords, nwords, decide ? 1 : 0, dec);
     return hipGetLastError();
 }
 
@@ -1869,9 +1880,9 @@ hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, h
     return hipGetLastError();
 }
 
-hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* words,
-                         const int64_t* first, esc_group_decision* dec, hipStream_t st) {
-    hipLaunchKernelGGL(k_decide, dim3((g.G + 63) / 64), dim3(256), 0, st, g, n, words, first, dec);
+hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords,
+                         const int64_t* nwords, esc_group_decision* dec, hipStream_t st) {
+    hipLaunchKernelGGL(k_decide, dim3((g.G + 63) / 64), dim3(256), 0, st, g, n, pwords, nwords, dec);
     return hipGetLastError();
 }
 

@@ -6,7 +6,9 @@
 // and an optional hipGraph of the whole decision step.  The only host<->device
 // traffic per decision is the launch (a graph replay for one rank) and the copy of the
 // per-group decisions back to pinned host memory.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -38,6 +40,11 @@ thread_local char g_last_error[256];
 int32_t fail_hip(hipError_t e, const char* what) {
     std::snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, hipGetErrorString(e));
     return e == hipErrorOutOfMemory ? ESC_E_NOMEM : ESC_E_HIP;
+}
+
+int32_t fail_comm(const char* what, const char* why) {
+    std::snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, why);
+    return ESC_E_COMM;
 }
 
 template <class T>
@@ -82,6 +89,39 @@ struct NodeBuf {
     }
 };
 
+// RCCL is resolved at first use: the copy already mapped into the process if there is one
+// (PyTorch-ROCm ships its own librccl, and two RCCL instances in one process would each
+// run their own proxy threads), else the system librccl.so.1.  Hosts that never exchange
+// (world 1, the per-function drop-ins) need no RCCL at all.
+struct RcclApi {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    bool ok = false;
+};
+
+const RcclApi& rccl() {
+    static const RcclApi api = [] {
+        RcclApi a;
+        void* h = nullptr;
+        for (const char* n : {"librccl.so", "librccl.so.1"})
+            if ((h = dlopen(n, RTLD_NOW | RTLD_NOLOAD)) != nullptr) break;
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+        if (!h) return a;
+        a.get_unique_id = reinterpret_cast<decltype(a.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        a.init_rank = reinterpret_cast<decltype(a.init_rank)>(dlsym(h, "ncclCommInitRank"));
+        a.all_reduce = reinterpret_cast<decltype(a.all_reduce)>(dlsym(h, "ncclAllReduce"));
+        a.destroy = reinterpret_cast<decltype(a.destroy)>(dlsym(h, "ncclCommDestroy"));
+        a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
+        a.ok = a.get_unique_id && a.init_rank && a.all_reduce && a.destroy && a.error_string;
+        return a;
+    }();
+    return api;
+}
+
 int bit_width(uint64_t v) {
     int b = 0;
     while (v) { ++b; v >>= 1; }
@@ -124,8 +164,9 @@ struct esc_ctx {
     uint32_t* d_k1_ticket = nullptr;                          // K1 dynamic shares (next chunk, done)
     int k1_cap = 0;                                           // K1 chunks per workgroup at most (0: static)
     int64_t* d_trk_acc = nullptr;                             // [G][TA_K] dry-mode tracked sums
-    int64_t *d_words = nullptr, *d_first = nullptr;          // active exchange buffers
-    int64_t *own_words = nullptr, *own_first = nullptr;      // context-owned ones
+    int64_t* d_pwords = nullptr;                              // active exchange buffer [G][PW_K]
+    int64_t* own_pwords = nullptr;                            // the context-owned one
+    int64_t* d_nwords = nullptr;                              // [G][NW_K] rank-local node words
     esc_group_decision* d_dec = nullptr;
     esc_group_decision* h_dec = nullptr;
     esc_group_decision* h_dec_dev = nullptr;                 // device view of h_dec (zero-copy)
@@ -135,7 +176,8 @@ struct esc_ctx {
     esc_group_metrics* d_metrics = nullptr;
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    int64_t *bound_words = nullptr, *bound_first = nullptr;  // caller-bound (RCCL) buffers
+    int64_t* bound_pwords = nullptr;                          // caller-bound exchange buffer
+    void* comm = nullptr;                                     // RCCL communicator (esc_comm_init)
     bool work_ready = false;
     bool force_wide = false;
     int k1_variant = 0;                                       // ESC_K1_VARIANT (measurement knob)
@@ -310,9 +352,8 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
 
 void release_work(esc_ctx* c) {
     dfree(c->d_pod_part); dfree(c->d_fold); dfree(c->d_wide_pod); dfree(c->d_wp_cnt); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
-    dfree(c->own_words); dfree(c->own_first); dfree(c->d_dec); dfree(c->d_metrics);
-    c->d_words = nullptr;
-    c->d_first = nullptr;
+    dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_metrics);
+    c->d_pwords = nullptr;
     if (c->h_dec) hipHostFree(c->h_dec);
     c->h_dec = nullptr;
     c->h_dec_dev = nullptr;
@@ -509,10 +550,9 @@ int32_t ensure_work(esc_ctx* c) {
     HIP_TRY(hipMemset(c->d_wp_cnt, 0, (size_t)S * sizeof(uint32_t)));
     HIP_TRY(dalloc(&c->d_trk_acc, (size_t)G * TA_K));
     HIP_TRY(hipMemset(c->d_trk_acc, 0, (size_t)G * TA_K * sizeof(int64_t)));
-    HIP_TRY(dalloc(&c->own_words, (size_t)G * TW_K));
-    HIP_TRY(dalloc(&c->own_first, (size_t)G));
-    c->d_words = c->bound_words ? c->bound_words : c->own_words;
-    c->d_first = c->bound_first ? c->bound_first : c->own_first;
+    HIP_TRY(dalloc(&c->own_pwords, (size_t)G * PW_K));
+    HIP_TRY(dalloc(&c->d_nwords, (size_t)G * NW_K));
+    c->d_pwords = c->bound_pwords ? c->bound_pwords : c->own_pwords;
     HIP_TRY(dalloc(&c->d_dec, (size_t)G));
     HIP_TRY(dalloc(&c->d_metrics, (size_t)G));
     HIP_TRY(hipMemset(c->d_metrics, 0, (size_t)G * sizeof(esc_group_metrics)));
@@ -564,7 +604,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     HIP_TRY(launch_pod_fold(c->d_pod_part, nblk, pod_slots(c), c->d_fold, st));   // K3a
     esc_group_decision* dec = c->zero_copy ? c->h_dec_dev : c->d_dec;
     HIP_TRY(launch_combine(g, n, c->d_fold, nblk ? FOLD_SPLIT : 0, c->nodes.rows, c->d_wide_pod, c->d_wp_cnt, c->d_trk_acc,
-                           c->d_words, c->d_first, decide, dec, st));
+                           c->d_pwords, c->d_nwords, decide, dec, st));
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     if (copy_out && !c->zero_copy) {
         HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)g.G * sizeof(esc_group_decision),
@@ -598,6 +638,7 @@ const char* esc_strerror(int32_t code) {
         case ESC_E_LIMIT: return "input exceeds an encoding limit";
         case ESC_E_STATE: return "call order violated";
         case ESC_E_NODEV: return "no gfx950 device available";
+        case ESC_E_COMM: return g_last_error[0] ? g_last_error : "RCCL unavailable or a collective failed";
         default: return "unknown error";
     }
 }
@@ -709,6 +750,8 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
     if (c->has_device) {
         hipSetDevice(c->device);
         if (c->stream) hipStreamSynchronize(c->stream);
+        if (c->comm && rccl().ok) rccl().destroy(reinterpret_cast<ncclComm_t>(c->comm));
+        c->comm = nullptr;
         release_work(c);
         release_sort(c);
         release_placement(c);
@@ -1042,11 +1085,10 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     std::vector<uint32_t> pp_off((size_t)n_gp + 1);
     for (uint32_t q = 0; q <= n_gp; ++q)
         pp_off[q] = (uint32_t)(std::lower_bound(piece_pair.begin(), piece_pair.end(), q) - piece_pair.begin());
-    auto piece_at = [&](int64_t r) {                 // first piece starting at or after E*r/world
-        const uint64_t e0 = (uint64_t)((__int128)E * r / c->world);
-        return (int64_t)(std::lower_bound(piece_off.begin(), piece_off.end() - 1, (uint32_t)e0) - piece_off.begin());
-    };
-    const int64_t pc_lo = piece_at(c->rank), pc_hi = c->rank + 1 == c->world ? n_pieces : piece_at(c->rank + 1);
+    // Every rank reduces the whole index: the node words then need no
+    // exchange and only the pods' per-group words cross xGMI.  The node table is resident
+    // on every rank anyway (K5 orders its [lo, hi) share; allNodes[0] is global).
+    const int64_t pc_lo = 0, pc_hi = n_pieces;
     int64_t node_bytes = 0;                          // algorithmic bytes K2 streams per decision
     for (int64_t p = pc_lo; p < pc_hi; ++p) {
         node_bytes += 8;                             // piece_pair + piece_off
@@ -1214,8 +1256,8 @@ int32_t esc_reduce(esc_ctx* c) {
 int32_t esc_exchange_buffers(esc_ctx* c, void** sum_buf, int64_t* sum_count, void** min_buf, int64_t* min_count) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
-    if (sum_buf) *sum_buf = c->d_words;
-    if (sum_count) *sum_count = (int64_t)c->gi.G * TW_K;
+    if (sum_buf) *sum_buf = c->d_pwords;
+    if (sum_count) *sum_count = (int64_t)c->gi.G * PW_K;
     // allNodes[0] is resolved from the pair-major index every rank holds in full, so the
     // first-member words need no MIN exchange in this build
     if (min_buf) *min_buf = nullptr;
@@ -1226,12 +1268,9 @@ int32_t esc_exchange_buffers(esc_ctx* c, void** sum_buf, int64_t* sum_count, voi
 int32_t esc_bind_exchange_buffers(esc_ctx* c, void* sum_buf, void* min_buf) {
     if (!c || (!sum_buf && min_buf)) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
-    c->bound_words = reinterpret_cast<int64_t*>(sum_buf);
-    c->bound_first = reinterpret_cast<int64_t*>(min_buf);
-    if (c->work_ready) {
-        c->d_words = c->bound_words ? c->bound_words : c->own_words;
-        c->d_first = c->bound_first ? c->bound_first : c->own_first;
-    }
+    if (min_buf) return ESC_E_INVAL;                  // min_count is 0: nothing to MIN-exchange
+    c->bound_pwords = reinterpret_cast<int64_t*>(sum_buf);
+    if (c->work_ready) c->d_pwords = c->bound_pwords ? c->bound_pwords : c->own_pwords;
     drop_graphs(c);
     return ESC_OK;
 }
@@ -1243,7 +1282,7 @@ int32_t esc_exchange_download(esc_ctx* c, int64_t* sum_out, int64_t* min_out) {
     (void)min_out;                                   // min_count is 0: nothing to MIN-exchange
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(sum_out, c->d_words, (size_t)c->gi.G * TW_K * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(sum_out, c->d_pwords, (size_t)c->gi.G * PW_K * 8, hipMemcpyDeviceToHost));
     return ESC_OK;
 }
 
@@ -1254,7 +1293,7 @@ int32_t esc_exchange_upload(esc_ctx* c, const int64_t* sum_in, const int64_t* mi
     (void)min_in;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(c->d_words, sum_in, (size_t)c->gi.G * TW_K * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_pwords, sum_in, (size_t)c->gi.G * PW_K * 8, hipMemcpyHostToDevice));
     return ESC_OK;
 }
 
@@ -1262,7 +1301,7 @@ int32_t esc_decide(esc_ctx* c) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
     hipSetDevice(c->device);
-    HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_words, c->d_first,
+    HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_pwords, c->d_nwords,
                           c->zero_copy ? c->h_dec_dev : c->d_dec, c->stream));
     if (!c->zero_copy)
         HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)c->gi.G * sizeof(esc_group_decision),
@@ -1283,6 +1322,55 @@ int32_t esc_run(esc_ctx* c) {
     (void)nrep;
     if (!c->use_graph || c->timing) return enqueue_step(c, r, true, true);
     return replay_step(c, c->graphs, r, true);
+}
+
+// ------------------------------------------------- RCCL exchange (§8e) inside the library
+int32_t esc_comm_unique_id(void* id_out) {
+    if (!id_out) return ESC_E_INVAL;
+    if (!rccl().ok) return fail_comm("esc_comm_unique_id", "librccl not found");
+    ncclUniqueId id;
+    const ncclResult_t r = rccl().get_unique_id(&id);
+    if (r != ncclSuccess) return fail_comm("ncclGetUniqueId", rccl().error_string(r));
+    static_assert(sizeof(ncclUniqueId) == ESC_COMM_ID_BYTES, "RCCL unique id size");
+    std::memcpy(id_out, &id, sizeof id);
+    return ESC_OK;
+}
+
+int32_t esc_comm_init(esc_ctx* c, const void* id, int32_t rank, int32_t world) {
+    if (!c || !id) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (rank != c->rank || world != c->world || c->comm) return ESC_E_STATE;
+    if (!rccl().ok) return fail_comm("esc_comm_init", "librccl not found");
+    hipSetDevice(c->device);
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = rccl().init_rank(&comm, world, uid, rank);
+    if (r != ncclSuccess) return fail_comm("ncclCommInitRank", rccl().error_string(r));
+    c->comm = comm;
+    return ESC_OK;
+}
+
+int32_t esc_exchange(esc_ctx* c) {
+    int32_t rc = check_ready(c);
+    if (rc) return rc;
+    if (!c->comm) return ESC_E_STATE;
+    hipSetDevice(c->device);
+    // int64 SUM is exact in any order: the words are split lo32 / hi
+    const ncclResult_t r = rccl().all_reduce(c->d_pwords, c->d_pwords, (size_t)c->gi.G * PW_K, ncclInt64, ncclSum,
+                                             reinterpret_cast<ncclComm_t>(c->comm), c->stream);
+    if (r != ncclSuccess) return fail_comm("ncclAllReduce", rccl().error_string(r));
+    c->pending = true;
+    return ESC_OK;
+}
+
+int32_t esc_step(esc_ctx* c) {
+    int32_t rc = check_ready(c);
+    if (rc) return rc;
+    if (!c->comm) return c->world == 1 ? esc_run(c) : ESC_E_STATE;
+    if ((rc = esc_reduce(c)) != ESC_OK) return rc;
+    if ((rc = esc_exchange(c)) != ESC_OK) return rc;
+    return esc_decide(c);
 }
 
 int32_t esc_sync(esc_ctx* c) {
@@ -1312,35 +1400,32 @@ int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* de
     const int32_t G = c->gi.G;
     if (decisions) std::memcpy(decisions, c->h_dec, (size_t)G * sizeof(esc_group_decision));
     if (totals) {
-        std::vector<int64_t> w((size_t)G * TW_K), f((size_t)G);
-        HIP_TRY(hipMemcpy(w.data(), c->d_words, w.size() * 8, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(f.data(), c->d_first, f.size() * 8, hipMemcpyDeviceToHost));
-        std::vector<int64_t> ncpu, nmem;
+        std::vector<int64_t> w((size_t)G * PW_K), nw((size_t)G * NW_K);
+        HIP_TRY(hipMemcpy(w.data(), c->d_pwords, w.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(nw.data(), c->d_nwords, nw.size() * 8, hipMemcpyDeviceToHost));
         for (int32_t g = 0; g < G; ++g) {
-            const int64_t* x = &w[(size_t)g * TW_K];
+            const int64_t* x = &w[(size_t)g * PW_K];
+            const int64_t* y = &nw[(size_t)g * NW_K];
             esc_group_totals& t = totals[g];
             auto join = [&](int k, int64_t& out) {
                 const __int128 v = ((__int128)x[k + 1] << 32) + (__int128)x[k];
                 out = (int64_t)v;
                 return v >= (__int128)INT64_MIN && v <= (__int128)INT64_MAX;
             };
-            t.flags = 0;
-            if (!join(TW_POD_CPU_LO, t.pod_cpu_m)) t.flags |= ESC_TF_POD_OVERFLOW;
-            if (!join(TW_POD_MEM_LO, t.pod_mem_b)) t.flags |= ESC_TF_POD_OVERFLOW;
-            t.n_pods = x[TW_N_PODS];
-            if (!join(TW_NODE_CPU_LO, t.node_cpu_m)) t.flags |= ESC_TF_NODE_OVERFLOW;
-            if (!join(TW_NODE_MEM_LO, t.node_mem_b)) t.flags |= ESC_TF_NODE_OVERFLOW;
-            t.n_untainted = x[TW_N_UNT];
-            t.n_tainted = x[TW_N_TAINT];
-            t.n_cordoned = x[TW_N_CORD];
+            t.flags = y[NW_FLAGS];
+            if (!join(PW_CPU_LO, t.pod_cpu_m)) t.flags |= ESC_TF_POD_OVERFLOW;
+            if (!join(PW_MEM_LO, t.pod_mem_b)) t.flags |= ESC_TF_POD_OVERFLOW;
+            t.n_pods = x[PW_N];
+            t.node_cpu_m = y[NW_CPU];
+            t.node_mem_b = y[NW_MEM];
+            t.n_untainted = y[NW_N_UNT];
+            t.n_tainted = y[NW_N_TAINT];
+            t.n_cordoned = y[NW_N_CORD];
             t.n_nodes = t.n_untainted + t.n_tainted + t.n_cordoned;
-            t.first_node = f[g] == INT64_MAX ? -1 : f[g];
-            t.first_cpu_m = 0;
-            t.first_mem_b = 0;
-            if (t.first_node >= 0) {
-                HIP_TRY(hipMemcpy(&t.first_cpu_m, c->nodes.cpu + t.first_node, 8, hipMemcpyDeviceToHost));
-                HIP_TRY(hipMemcpy(&t.first_mem_b, c->nodes.mem + t.first_node, 8, hipMemcpyDeviceToHost));
-            }
+            const int64_t first = c->h_gnode[g].first;
+            t.first_node = first == INT64_MAX ? -1 : first;
+            t.first_cpu_m = t.first_node >= 0 ? c->h_ncpu[t.first_node] : 0;
+            t.first_mem_b = t.first_node >= 0 ? c->h_nmem[t.first_node] : 0;
         }
     }
     return ESC_OK;

@@ -1,17 +1,19 @@
-"""One process per GPU: sharded snapshot + one exchange of the per-group int64 words.
+"""One process per GPU: sharded pods + one exchange of the pods' per-group int64 words.
 
 The reference has no parallelism (groups run sequentially,
-controller.go:416).  Here every rank holds a contiguous shard of the pod SoA and reduces
-its 1/world share of the node index; the per-group words are all-reduced with SUM — over
-RCCL/xGMI with the ``nccl`` backend (the words live in a torch tensor bound as the
-context's exchange buffer, stream-ordered), or host-staged over ``gloo``.  int64 addition
-is associative, so any reduction order gives bit-identical totals; every rank then runs
-K4 on the same words.  The first-member words (allNodes[0]) need no exchange in this
-build (the context reports min_count 0); a MIN all-reduce runs only if one is asked for.
+controller.go:416).  Here every rank holds a contiguous shard of the pod SoA and the whole
+node table (it reduces the node index itself, so only the pods' words cross ranks); the
+per-group pod words are all-reduced with SUM — by the library's own RCCL communicator
+(esc_comm_init / esc_exchange: ncclAllReduce over xGMI on the context's stream), or
+host-staged over ``gloo``.  int64 addition is associative and the words are split lo32 /
+hi, so any reduction order gives bit-identical totals; every rank then runs K4 on the
+same words.
 """
 from __future__ import annotations
 
 import os
+
+import numpy as np
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -28,7 +30,13 @@ def env_rank() -> tuple[int, int, int]:
 
 
 class Exchange:
-    """Per-decision exchange of one context's words across the process group."""
+    """Per-decision exchange of one context's pod words across the process group.
+
+    device_collective: the library's own RCCL communicator (esc_comm_init; rank 0's
+    unique id travels over the torch.distributed group), one in-place
+    ncclAllReduce(int64, SUM) on the context's stream between K3 and K4 (esc_step) — the
+    path a Go host drives through the C ABI alone.  Otherwise host-staged over the group
+    (gloo): download, all_reduce, upload."""
 
     def __init__(self, ctx, device_collective: bool):
         import torch
@@ -36,39 +44,36 @@ class Exchange:
         self.ctx, self.dist, self.torch = ctx, dist, torch
         self.device_collective = device_collective
         (_, sc), (_, mc) = ctx.exchange_buffers()
-        self.min_count = mc
+        assert mc == 0, "the node words are reduced on every rank: nothing to MIN-exchange"
         if device_collective:
-            dev = torch.device("cuda", torch.cuda.current_device())
-            self.words = torch.zeros(sc, dtype=torch.int64, device=dev)
-            self.first = torch.zeros(mc, dtype=torch.int64, device=dev) if mc else None
-            ctx.bind_exchange(self.words.data_ptr(), self.first.data_ptr() if mc else None)
-            ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+            rank, world = dist.get_rank(), dist.get_world_size()
+            obj = [ctx.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            ctx.comm_init(obj[0], rank, world)
 
     def step(self):
-        """K1+K2+K3 on this shard, exchange, K4 (all stream-ordered for RCCL)."""
-        self.ctx.reduce()
+        """K1+K2+K3 on this shard, exchange, K4."""
         if self.device_collective:
-            self.dist.all_reduce(self.words, op=self.dist.ReduceOp.SUM)
-            if self.min_count:
-                self.dist.all_reduce(self.first, op=self.dist.ReduceOp.MIN)
-        else:
-            s, m = self.ctx.exchange_download()
-            ts, tm = self.torch.from_numpy(s), self.torch.from_numpy(m)
-            self.dist.all_reduce(ts, op=self.dist.ReduceOp.SUM)
-            if self.min_count:
-                self.dist.all_reduce(tm, op=self.dist.ReduceOp.MIN)
-            self.ctx.exchange_upload(ts.numpy(), tm.numpy())
+            self.ctx.step()
+            return
+        self.ctx.reduce()
+        s, _ = self.ctx.exchange_download()
+        ts = self.torch.from_numpy(s)
+        self.dist.all_reduce(ts, op=self.dist.ReduceOp.SUM)
+        self.ctx.exchange_upload(ts.numpy(), np.zeros(0, np.int64))
         self.ctx.decide()
 
 
 def exchange_host(sum_arr, min_arr):
-    """Host-side SUM/MIN all-reduce of numpy int64 arrays (gloo) — used by the CPU tests."""
+    """Host-side SUM (and, when non-empty, MIN) all-reduce of numpy int64 arrays (gloo) —
+    used by the CPU tests."""
     import torch
     import torch.distributed as dist
     ts = torch.from_numpy(sum_arr.copy())
     tm = torch.from_numpy(min_arr.copy())
     dist.all_reduce(ts, op=dist.ReduceOp.SUM)
-    dist.all_reduce(tm, op=dist.ReduceOp.MIN)
+    if tm.numel():
+        dist.all_reduce(tm, op=dist.ReduceOp.MIN)
     return ts.numpy(), tm.numpy()
 
 

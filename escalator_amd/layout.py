@@ -7,7 +7,7 @@ per 64-pod C tile (pods with more than 3 extra container records or more than 3 
 pairs; all other pods sit in homogeneous 256-pod K tiles that need no offsets).
 K2 reads the node index once per decision: 24 B per (label pair, node) entry of a pair
 some group selects (flags 4 + cpu 8 + mem 8 + node 4) and 8 B per piece (offset + pair);
-a rank reads the pieces that start in its 1/world share of the entries.
+every rank reads the whole index (only the pods' words are exchanged).
 """
 import numpy as np
 
@@ -48,7 +48,5 @@ def node_bytes(nodes: dict, n_gp: int, rank: int = 0, world: int = 1) -> int:
     p_start = np.repeat(starts, n_pc) + NODE_PIECE * (np.arange(n_pc.sum()) - np.repeat(np.cumsum(n_pc) - n_pc, n_pc))
     p_len = np.diff(np.r_[p_start, E])
     p_pair = q[p_start]
-    lo = E * rank // world
-    hi = E * (rank + 1) // world if rank + 1 < world else E + 1
-    mine = (p_start >= lo) & (p_start < hi)
-    return int(8 * mine.sum() + 24 * p_len[mine & (p_pair < n_gp)].sum())
+    del rank, world                      # rank-independent: every rank reduces all pieces
+    return int(8 * len(p_start) + 24 * p_len[p_pair < n_gp].sum())

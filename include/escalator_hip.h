@@ -42,6 +42,7 @@ extern "C" {
 #define ESC_E_LIMIT    -4   /* input exceeds a documented encoding limit              */
 #define ESC_E_STATE    -5   /* call order violated (e.g. decide before load)          */
 #define ESC_E_NODEV    -6   /* library loaded without a usable gfx950 device          */
+#define ESC_E_COMM     -7   /* RCCL not loadable, or an RCCL call failed               */
 
 /* ------------------------------------------------------- per-group status codes
  * esc_status_string(code) returns the reference's error text verbatim.            */
@@ -337,10 +338,11 @@ int32_t esc_stream_bytes(const esc_ctx* ctx, int64_t* pod_bytes, int64_t* node_b
 /* ------------------------------------------------------------ scale decision
  * esc_reduce     : async. Per-shard group totals (K1 pods + K2 nodes + combine).
  * esc_exchange_buffers: device buffers to all-reduce between esc_reduce and esc_decide:
- *                  sum_buf  int64[sum_count]  with op SUM,
+ *                  sum_buf  int64[sum_count]  with op SUM: the pods' per-group words
+ *                  (G x 5: cpu and memory split lo32 / hi, count),
  *                  min_buf  int64[min_count]  with op MIN (min_count 0 = nothing to
- *                  exchange: this build resolves allNodes[0] from the node index
- *                  every rank holds, so min_buf is NULL).
+ *                  exchange: every rank reduces the whole node index and resolves
+ *                  allNodes[0] from it, so min_buf is NULL).
  * esc_decide     : async. K4 decide on the (exchanged) totals; results land in the
  *                  context's host buffers after esc_sync.
  * esc_run        : esc_reduce + esc_decide for world == 1, optionally graph-captured.
@@ -361,6 +363,20 @@ int32_t esc_exchange_upload(esc_ctx* ctx, const int64_t* sum_in, const int64_t* 
 int32_t esc_decide(esc_ctx* ctx);
 int32_t esc_run(esc_ctx* ctx);
 int32_t esc_sync(esc_ctx* ctx);
+/* RCCL exchange inside the library (replaces the sequential per-group loop
+ * of RunOnce, pkg/controller/controller.go:416-445, by one sharded decision).  One process
+ * per GPU: rank 0 calls esc_comm_unique_id and ships the ESC_COMM_ID_BYTES bytes to the
+ * other ranks over any host channel; every rank then calls esc_comm_init (collective,
+ * blocking until all ranks joined; rank / world must equal the context's).  esc_exchange
+ * enqueues ncclAllReduce(int64, SUM) of the pod words (esc_exchange_buffers) in place on
+ * the context's stream; esc_step = esc_reduce + esc_exchange + esc_decide (esc_run when
+ * world == 1 and no communicator was set up).  The library resolves librccl at run time
+ * (the copy already loaded in the process, else librccl.so.1).                         */
+#define ESC_COMM_ID_BYTES 128
+int32_t esc_comm_unique_id(void* id_out);
+int32_t esc_comm_init(esc_ctx* ctx, const void* id, int32_t rank, int32_t world);
+int32_t esc_exchange(esc_ctx* ctx);
+int32_t esc_step(esc_ctx* ctx);
 int32_t esc_results(esc_ctx* ctx, esc_group_totals* totals, esc_group_decision* decisions);
 /* Metric gauges (§8f): computed by K4 beside the decisions when enabled (off by default;
  * they stay in device memory until esc_metrics_results copies them out, after esc_sync). */

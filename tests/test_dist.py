@@ -1,5 +1,6 @@
-"""CPU, world_size 2 over gloo: sharding + the SUM/MIN exchange reproduce the
-whole-snapshot totals (the same exchange the N-GPU bench performs over RCCL)."""
+"""CPU, world_size 2 over gloo: sharded pods + the SUM exchange of the pods' per-group
+words reproduce the whole-snapshot totals (the exchange the N-GPU decision performs with
+ncclAllReduce inside the library); every rank reduces the whole node table itself."""
 import os
 import socket
 
@@ -26,14 +27,12 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     P, N, G = 40_000, 3_000, 64
     lo, hi = shard_range(P, rank, world)
-    nlo, nhi = shard_range(N, rank, world)
     s = Synth(P, N, G, config=4, seed=5, p_lo=lo, p_hi=hi)
-    t = soa.totals(s.pods(), s.nodes(), s.groups, node_lo=nlo, node_hi=nhi)
-    first = np.where(t[:, 9] < 0, np.iinfo(np.int64).max, t[:, 9])
-    sums = np.delete(t, [9, 10, 11], axis=1)
-    S, F = exchange_host(sums, first)
+    t = soa.totals(s.pods(), s.nodes(), s.groups)        # this rank's pods, every node
+    S, F = exchange_host(np.ascontiguousarray(t[:, 0:3]), np.zeros(0, np.int64))
+    nodes_local = np.ascontiguousarray(t[:, 3:12])
     if rank == 0:
-        out.put((S, F))
+        out.put((S, nodes_local))
     dist.destroy_process_group()
 
 
@@ -47,16 +46,14 @@ def test_two_rank_exchange_equals_whole():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    S, F = q.get(timeout=120)
+    S, NL = q.get(timeout=120)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     full = Synth(40_000, 3_000, 64, config=4, seed=5)
     t = soa.totals(full.pods(), full.nodes(), full.groups)
-    want_first = np.where(t[:, 9] < 0, np.iinfo(np.int64).max, t[:, 9])
-    sums = np.delete(t, [9, 10, 11], axis=1)
-    assert np.array_equal(S[:, :-1], sums[:, :-1])        # flags column: OR semantics, all 0 here
-    assert np.array_equal(F, want_first)
+    assert np.array_equal(S, t[:, 0:3])                    # pod cpu, mem, count: SUM over ranks
+    assert np.array_equal(NL, t[:, 3:12])                  # node words and allNodes[0]: rank-local
 
 
 class _RangeOrders:

@@ -747,3 +747,27 @@ def test_config5_full_size_orderings_vs_c_oracle(esc):
             assert np.array_equal(got, want[(g, w)]), (g, w, len(got), len(want[(g, w)]))
             n += len(got)
     assert n > 9_000_000
+
+
+# ------------------------------------------------ RCCL exchange inside the library (§8e)
+@pytest.mark.parametrize("graph", [False, True])
+def test_rccl_step_world1_vs_c_oracle(esc, graph):
+    """esc_comm_unique_id -> esc_comm_init -> esc_step (K1 + K2 + K3 on the shard, the
+    in-place ncclAllReduce(int64, SUM) of the pod words on the context's stream, K4) at
+    world 1: the RCCL code path a Go host drives through the C ABI alone."""
+    s = esc.Synth(2_000_000, 20_000, 10_000, config=4, seed=0xE5CA1A7E00000004)
+    otot = soa.totals(s.pods(), s.nodes(), s.groups)
+    odf, odi = soa.decide(s.groups, s.states, otot)
+    ctx = esc.Context(s, rank=0, world=1)
+    ctx.load_synth(s, replicas=2)
+    ctx.use_graph(graph)
+    ctx.set_state(s.states)
+    uid = esc.Context.comm_unique_id()
+    assert len(uid) == 128
+    ctx.comm_init(uid, 0, 1)
+    for _ in range(3):
+        ctx.step()
+        tot, dec = ctx.results()
+        check_against_c_oracle(tot, dec, otot, odf, odi)
+    (sb, sc), (mb, mc) = ctx.exchange_buffers()
+    assert sc == 5 * 10_000 and mc == 0 and mb is None
