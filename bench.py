@@ -370,7 +370,7 @@ def main():
         "node_bytes_per_decision": node_b,
         # stages timed in order on one stream (timing mode); "d2h" only when the decisions
         # are copied rather than written to pinned host memory by K3 (zero-copy)
-        "stage_ms": {k: float(v) for k, v in zip(["k_pod_reduce", "k_node_pieces", "k_combine", "d2h"], stage_mean)
+        "stage_ms": {k: float(v) for k, v in zip(["k_pod_reduce", "k_node_pieces", "k_fold_decide", "d2h"], stage_mean)
                      if v > 0} if world == 1 else None,
         "parity": parity,
     }

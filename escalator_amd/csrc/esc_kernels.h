@@ -22,6 +22,7 @@ struct PodClass {
 // weight (16-B loads per lane) of a K tile with R records and NXP extra pairs per pod
 constexpr uint32_t k_tile_weight(uint32_t R, uint32_t NXP) { return 5 + 4 * R + NXP; }
 constexpr int POD_CLASS_IDS = 128;   // signatures with <= 3 extra records and <= 3 extra pairs
+constexpr int K1_SEGS = 4;           // class runs per K1 workgroup in the work plan (at most)
 
 // Device view of a pod shard.  Two sections of the same arrays, made at load
 // (esc_load_pods; sums are order-independent):
@@ -41,6 +42,10 @@ struct PodDev {
     const PodClass* cls;       // [n_cls] K classes, in tile order
     const uint32_t* xc_base;   // [c_tiles + 1] extra-container offset of each C tile
     const uint32_t* xp_base;   // [c_tiles + 1] extra-pair offset
+    // K1 work plan (ensure_work): per workgroup up to K1_SEGS runs of one
+    // class, {t0 | class << 48, t1} (t1 == 0: unused), balanced in work weight, at most two
+    // class boundaries per workgroup.  Null: the weight-range shares of variant 7.
+    const int64_t* seg;
     int32_t n_cls;
     int64_t k_tiles;           // K section: pods [0, k_tiles * 256)
     int64_t k_weight;          // total work weight of the K tiles (K1 splits it evenly)
@@ -114,6 +119,7 @@ struct GroupDev {
     const uint32_t* slot_readers; // [n_gp + 1] groups reading each pod slot in K3
     const uint32_t* gslot;     // [G] the group's pod slot: its pair, or n_gp for the default group
     esc_group_metrics* metrics; // [G] gauges written by K4, or null (esc_set_metrics)
+    int64_t sp;                // K1 partial row stride: pod slots rounded up to FC_COL
     uint32_t n_gp;             // pod slots: pair ids [0, n_gp) + the default filter's slot n_gp
     int32_t G;
     uint32_t default_group;    // NONE when no group is named "default"
@@ -142,11 +148,21 @@ hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
                                int64_t* wide, hipStream_t st);
 hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows, int64_t* trk_acc, hipStream_t st);
-constexpr int FOLD_SPLIT = 8;   // K3a: row ranges the K1 partials fold into (fold: [split][4][S] u64)
-hipError_t launch_pod_fold(const uint64_t* pod_part, int nblk, int64_t S, uint64_t* fold, hipStream_t st);
-hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* fold, int nsplit,
-                          const int64_t* node_rows, int64_t* wide_pod, uint32_t* wp_cnt, int64_t* trk_acc,
-                          int64_t* pwords, int64_t* nwords, bool decide, esc_group_decision* dec, hipStream_t st);
+// K3 (k_fold_decide): fold of the K1 partials + group join + decide in one launch.
+constexpr int FC_COL = 128;            // pod slots per K3 column (one 16-B wave-load of a row)
+struct FoldPlan {
+    const uint64_t* part;              // K1 partials: row b = cc[sp], mem[sp] at part + 2 * sp * b
+    int nblk, split;                   // K1 rows; row ranges per column (grid.y)
+    int64_t sp;                        // slots per partial row, a multiple of FC_COL
+    int64_t n_col;                     // columns (grid.x)
+    uint64_t* scratch;                 // [n_col][split][4][FC_COL] block folds
+    uint32_t* col_cnt;                 // [n_col] arrivals (the last block resets its word)
+    const uint32_t* col_off;           // [n_col + 1] the column's groups in col_groups
+    const uint32_t* col_groups;        // group ids ordered by pod slot, then id
+};
+hipError_t launch_fold_decide(const GroupDev& g, const NodeDev& n, const FoldPlan& f, const int64_t* node_rows,
+                              int64_t* wide_pod, int64_t* trk_acc, int64_t* pwords, int64_t* nwords, bool decide,
+                              esc_group_decision* dec, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
 // §8f rank 2: a loaded pod as seen by NodePodsRemaining, listed per node (runs in
 // node order).  p[0..2]: the pod's extra pairs (NONE-padded); a C pod with more than 3

@@ -508,6 +508,30 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     int64_t chunk = WS ? (int64_t)blockIdx.x * NW + wid : blockIdx.x;
     if constexpr (DYN) chunk = grab();
     else __syncthreads();
+    // the host's work plan: this workgroup's class runs, every wave interleaved over each
+    typedef __attribute__((address_space(4))) const int64_t ci64;
+    if (P.seg && !DYN && !WS && !(ABLATE & 2)) {
+        const ci64* sg = (const ci64*)P.seg + (int64_t)blockIdx.x * (2 * K1_SEGS);
+#pragma unroll 1
+        for (int k = 0; k < K1_SEGS; ++k) {
+            const int64_t t0c = sg[2 * k], b = sg[2 * k + 1];
+            if (b == 0) break;
+            const PodClass C = load_class(P.cls, (int)(t0c >> 48));
+            const int64_t a = (t0c & ((1ll << 48) - 1)) + wid;
+            if (a >= b) continue;
+            switch (C.kind) {
+#define ESC_KRUN(RR, XX) \
+    case RR * 4 + XX: k_run<RR, XX, NW, ABLATE, NW>(P, G, K, C, a, b, lane); break;
+                ESC_KRUN(0, 0) ESC_KRUN(0, 1) ESC_KRUN(0, 2) ESC_KRUN(0, 3)
+                ESC_KRUN(1, 0) ESC_KRUN(1, 1) ESC_KRUN(1, 2) ESC_KRUN(1, 3)
+                ESC_KRUN(2, 0) ESC_KRUN(2, 1) ESC_KRUN(2, 2) ESC_KRUN(2, 3)
+                ESC_KRUN(3, 0) ESC_KRUN(3, 1) ESC_KRUN(3, 2) ESC_KRUN(3, 3)
+#undef ESC_KRUN
+                default: break;
+            }
+        }
+        chunk = n_chunks;                                // skip the weight-range walk
+    }
     for (int taken = 1; !(ABLATE & 2) && chunk < n_chunks; ++taken) {
         // equal shares of work weight (bytes), not of tiles: a tile of a class with three
         // container records streams ~3.4x the bytes of a simple one
@@ -573,7 +597,7 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
         }
     }
     __syncthreads();
-    const int64_t S = G.n_gp + 1;
+    const int64_t S = G.sp;                                  // row stride (K3 reads whole columns)
     uint64_t* out = part + (int64_t)blockIdx.x * 2 * S + g0;
     for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
         out[i] = lds[i];
@@ -822,184 +846,229 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 
 }  // namespace
 
-// K3a: the K1 workgroups' packed slot partials summed column-wise — one thread per slot,
-// one of FOLD_SPLIT row ranges per grid row, coalesced 2 KB rows — into (cpu, count,
-// mem lo, mem carry) per split, so that K3 reads FOLD_SPLIT rows per slot instead of one
-// per K1 workgroup (41 MB for config 4).
-__global__ __launch_bounds__(256) void k_pod_fold(const uint64_t* __restrict__ part, int nblk, int64_t S,
-                                                  uint64_t* __restrict__ fold) {
-    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (s >= S) return;
-    const int y = blockIdx.y;
-    const int b0 = nblk * y / FOLD_SPLIT, b1 = nblk * (y + 1) / FOLD_SPLIT;
-    uint64_t cpu = 0, cnt = 0, lo = 0, carry = 0;
-#pragma unroll 4
-    for (int b = b0; b < b1; ++b) {
-        const uint64_t c = ldnt(part + (int64_t)b * 2 * S + s), m = ldnt(part + ((int64_t)b * 2 + 1) * S + s);
-        cpu += c & CPU_MASK;
-        cnt += c >> CNT_SHIFT;
-        u128_add(lo, carry, m);
-    }
-    uint64_t* f = fold + (int64_t)y * 4 * S + s;
-    f[0] = cpu;
-    f[S] = cnt;
-    f[2 * S] = lo;
-    f[3 * S] = carry;
-}
-
-// One lane per group (64 groups per workgroup); the 16 waves split the group's pod
-// partial rows (K1 workgroups, coalesced reads of consecutive slots) and its pair's node
-// piece rows, three LDS rounds merge the waves, and wave 0 adds the wide and tracker
-// accumulators and writes the exchanged words.
+// K3 (k_fold_decide): the K1 workgroups' slot partials folded, joined to the groups and
+// decided, in ONE launch.  Grid = columns of FC_COL slots x `split` row ranges.  Every
+// block sums its rows of its column (16-B loads: a wave-load covers the column's 128 slots
+// of one row; every row of the block in flight at once) and publishes the result (sc1
+// stores, drained, then one agent-scope ticket add per block: MI355X_MICROARCH.md
+// § visibility, the first row of the hand-off table).  The block whose add comes last sums
+// the column's `split` results (sc1 loads) and evaluates every group whose pod slot lies
+// in the column (col_off / col_groups): the slot's sums + its wide (exact-path) row, the
+// pieces of the group's node pair (4 waves split them), the dry-mode tracker sums, then
+// K4 (decide_one) for one rank.  No block waits on another: only arrivals are counted.
 //  - pods: the group's slot is its pair (NewPodAffinityFilterFunc, node_group.go:218) or,
 //    for the group named "default", the default filter's slot (client.go:58-64);
 //  - nodes: the pieces of the group's pair (NewNodeLabelFilterFunc, node_group.go:278);
 //    wet groups take the filterNodes classes, dry groups (controller.go:126-138) take
 //    every member as untainted (cordoned ones included) except the tracked members;
-//  - allNodes[0] (controller.go:208): the first entry of the pair = lowest node index
-//    (every rank holds every piece's offsets, so this needs no exchange).
-// The wide pod row of a slot is read by every group of the slot; the last reader of a
-// non-zero row resets it for the next decision (wp_cnt, slot_readers).  A group's tracker
-// row has one reader and is reset by it.
-constexpr int CB_WAVES = 4;
+//  - allNodes[0] (controller.go:208): the pair's first entry (GroupNode, set at load).
+namespace {
+constexpr int FD_WAVES = 4;
 
-__global__ __launch_bounds__(CB_WAVES * 64) void k_combine(GroupDev G, NodeDev N,
-                                                           const uint64_t* __restrict__ fold, int nsplit,
-                                                           const int64_t* __restrict__ node_rows,
-                                                           int64_t* __restrict__ wide_pod,
-                                                           uint32_t* __restrict__ wp_cnt,
-                                                           int64_t* __restrict__ trk_acc,
-                                                           int64_t* __restrict__ pwords,
-                                                           int64_t* __restrict__ nwords, int decide,
-                                                           esc_group_decision* __restrict__ dec) {
-    // a: 0 pod cpu, 1 pod count, 2-3 pod mem (lo, carry), 4-6 untainted / tainted /
-    //    cordoned counts, then node sums as (lo, carry, hi) triples: 7-9 untainted cpu,
-    //    10-12 untainted mem, 13-15 every-member cpu, 16-18 every-member mem
-    constexpr int NA = 19, NPH = 7;
-    __shared__ uint64_t red[CB_WAVES][NPH][64];
+__device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+}  // namespace
+
+__global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeDev N, FoldPlan F,
+                                                                 const int64_t* __restrict__ node_rows,
+                                                                 int64_t* __restrict__ wide_pod,
+                                                                 int64_t* __restrict__ trk_acc,
+                                                                 int64_t* __restrict__ pwords,
+                                                                 int64_t* __restrict__ nwords, int decide,
+                                                                 esc_group_decision* __restrict__ dec) {
+    __shared__ uint64_t red[FD_WAVES][8][64];
+    __shared__ uint64_t tot[4][FC_COL];                 // per slot: cpu, count, mem lo, mem carry
+    __shared__ int64_t wtot[WP_K][FC_COL];              // per slot: its wide row
+    __shared__ esc_group_decision sdec[64];
+    __shared__ uint32_t s_last;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int32_t g = blockIdx.x * 64 + lane;
-    const bool ok = g < G.G;
-    uint64_t a[NA];
+    const int col = blockIdx.x, y = blockIdx.y;
+    const int64_t s0 = (int64_t)col * FC_COL;
+    // ---- fold: rows [b0, b1) of the column, every row of the block in flight at once
+    {
+        uint64_t cp[2] = {0, 0}, cn[2] = {0, 0}, ml[2] = {0, 0}, mc[2] = {0, 0};
+        const int b0 = F.nblk * y / F.split, b1 = F.nblk * (y + 1) / F.split;
+        constexpr int U = 4;
+        for (int b = b0 + wid; b < b1; b += FD_WAVES * U) {
+            ulonglong2 c[U], m[U];
 #pragma unroll
-    for (int k = 0; k < NA; ++k) a[k] = 0;
-    const int64_t S = G.n_gp + 1;
-    const int64_t slot = ok ? (int64_t)G.gslot[g] : 0;
-    GroupNode gn;
-    gn.first = INT64_MAX; gn.first_cpu = gn.first_mem = 0; gn.plo = gn.phi = 0;
-    if (ok) gn = N.gnode[g];
-    const int64_t plo = gn.plo, phi = gn.phi;             // this rank's pieces of the pair
-    if (ok) {
-        for (int y = wid; y < nsplit; y += CB_WAVES) {        // K3a's folded partials
-            const uint64_t* f = fold + (int64_t)y * 4 * S + slot;
-            a[0] += f[0];
-            a[1] += f[S];
-            u128_add(a[2], a[3], f[2 * S]);
-            a[3] += f[3 * S];
+            for (int u = 0; u < U; ++u) {
+                const int bb = b + FD_WAVES * u < b1 ? b + FD_WAVES * u : b;
+                const int64_t* row = reinterpret_cast<const int64_t*>(F.part) + (int64_t)bb * 2 * F.sp + s0 + 2 * lane;
+                c[u] = ld2(row);
+                m[u] = ld2(row + F.sp);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (b + FD_WAVES * u >= b1) break;
+                cp[0] += c[u].x & CPU_MASK; cn[0] += c[u].x >> CNT_SHIFT;
+                cp[1] += c[u].y & CPU_MASK; cn[1] += c[u].y >> CNT_SHIFT;
+                u128_add(ml[0], mc[0], m[u].x);
+                u128_add(ml[1], mc[1], m[u].y);
+            }
         }
-        const int64_t np = N.n_pieces;
-        for (int64_t p = plo + wid; p < phi; p += CB_WAVES) {
-            const int64_t* r = node_rows + p;
-            u128_add(a[7], a[8], (uint64_t)r[NR_UCPU_LO * np]); a[9] += (uint64_t)r[NR_UCPU_HI * np];
-            u128_add(a[10], a[11], (uint64_t)r[NR_UMEM_LO * np]); a[12] += (uint64_t)r[NR_UMEM_HI * np];
-            u128_add(a[13], a[14], (uint64_t)r[NR_ACPU_LO * np]); a[15] += (uint64_t)r[NR_ACPU_HI * np];
-            u128_add(a[16], a[17], (uint64_t)r[NR_AMEM_LO * np]); a[18] += (uint64_t)r[NR_AMEM_HI * np];
-            const uint64_t cn = (uint64_t)r[NR_COUNTS * np];
-            a[4] += cn & NR_CNT_MASK;
-            a[5] += (cn >> NR_CNT_BITS) & NR_CNT_MASK;
-            a[6] += cn >> (2 * NR_CNT_BITS);
-        }
-    }
-    // round 1: words 0-6 (plain sums except the pod mem pair)
-#pragma unroll
-    for (int k = 0; k < NPH; ++k) red[wid][k][lane] = a[k];
-    __syncthreads();
-    if (wid == 0) {
-        for (int w = 1; w < CB_WAVES; ++w) {
-            a[0] += red[w][0][lane];
-            a[1] += red[w][1][lane];
-            u128_add(a[2], a[3], red[w][2][lane]); a[3] += red[w][3][lane];
-            a[4] += red[w][4][lane];
-            a[5] += red[w][5][lane];
-            a[6] += red[w][6][lane];
-        }
-    }
-    // rounds 2, 3: the (lo, carry, hi) triples 7-12 and 13-18
-#pragma unroll
-    for (int r0 = 7; r0 < NA; r0 += 6) {
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 6; ++k) red[wid][k][lane] = a[r0 + k];
+        red[wid][0][lane] = cp[0]; red[wid][1][lane] = cp[1]; red[wid][2][lane] = cn[0]; red[wid][3][lane] = cn[1];
+        red[wid][4][lane] = ml[0]; red[wid][5][lane] = ml[1]; red[wid][6][lane] = mc[0]; red[wid][7][lane] = mc[1];
         __syncthreads();
         if (wid == 0) {
-            for (int w = 1; w < CB_WAVES; ++w) {
+            for (int w = 1; w < FD_WAVES; ++w) {
+                cp[0] += red[w][0][lane]; cp[1] += red[w][1][lane]; cn[0] += red[w][2][lane]; cn[1] += red[w][3][lane];
+                u128_add(ml[0], mc[0], red[w][4][lane]); mc[0] += red[w][6][lane];
+                u128_add(ml[1], mc[1], red[w][5][lane]); mc[1] += red[w][7][lane];
+            }
+            uint64_t* o = F.scratch + ((int64_t)col * F.split + y) * 4 * FC_COL + 2 * lane;
 #pragma unroll
-                for (int k = 0; k < 6; k += 3) {
-                    u128_add(a[r0 + k], a[r0 + k + 1], red[w][k][lane]);
-                    a[r0 + k + 1] += red[w][k + 1][lane];
-                    a[r0 + k + 2] += red[w][k + 2][lane];
+            for (int j = 0; j < 2; ++j) {
+                st_sc1(o + j, cp[j]);
+                st_sc1(o + FC_COL + j, cn[j]);
+                st_sc1(o + 2 * FC_COL + j, ml[j]);
+                st_sc1(o + 3 * FC_COL + j, mc[j]);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the storing wave drains, then signals
+            if (lane == 0) {
+                const uint32_t old = __hip_atomic_fetch_add(F.col_cnt + col, 1u, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+                s_last = old + 1 == (uint32_t)F.split;
+            }
+        }
+        __syncthreads();
+        if (!s_last) return;
+    }
+    // ---- the column's last arrival: sum the `split` block folds (sc1 loads), add the wide rows
+    if (threadIdx.x == 0) __hip_atomic_store(F.col_cnt + col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    {
+        const int sl = threadIdx.x & (FC_COL - 1), half = threadIdx.x >> 7;   // words {0,1} or {2,3}
+        uint64_t a0 = 0, a1 = 0;
+        for (int q = 0; q < F.split; ++q) {
+            const uint64_t* o = F.scratch + ((int64_t)col * F.split + q) * 4 * FC_COL + sl;
+            const uint64_t x0 = ld_sc1(o + (2 * half) * FC_COL), x1 = ld_sc1(o + (2 * half + 1) * FC_COL);
+            if (half == 0) { a0 += x0; a1 += x1; }
+            else { u128_add(a0, a1, x0); a1 += x1; }
+        }
+        tot[2 * half][sl] = a0;
+        tot[2 * half + 1][sl] = a1;
+        if (half == 0) {
+            const int64_t slot = s0 + sl;
+            int64_t p[WP_K] = {0, 0, 0, 0, 0};
+            if (slot <= (int64_t)G.n_gp) {
+                int64_t* wp = wide_pod + slot * WP_K;
+#pragma unroll
+                for (int k = 0; k < WP_K; ++k) p[k] = ld_agent(wp + k);
+                if ((p[0] | p[1] | p[2] | p[3] | p[4]) != 0)      // every reader is in this block: reset
+#pragma unroll
+                    for (int k = 0; k < WP_K; ++k)
+                        __hip_atomic_store(wp + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int k = 0; k < WP_K; ++k) wtot[k][sl] = p[k];
+        }
+    }
+    __syncthreads();
+    // ---- the column's groups, 64 at a time (lane = group); 4 waves split each group's pieces
+    const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
+    for (uint32_t base = ga; base < gb; base += 64) {
+        const bool ok = base + lane < gb;
+        const int32_t g = ok ? (int32_t)F.col_groups[base + lane] : 0;
+        constexpr int NA = 15;   // 0-2 counts; node sums (lo, carry, hi): 3-5 unt cpu, 6-8 unt mem, 9-11 all cpu, 12-14 all mem
+        uint64_t a[NA];
+#pragma unroll
+        for (int k = 0; k < NA; ++k) a[k] = 0;
+        GroupNode gn;
+        gn.first = INT64_MAX; gn.first_cpu = gn.first_mem = 0; gn.plo = gn.phi = 0;
+        if (ok) gn = N.gnode[g];
+        {
+            const int64_t np = N.n_pieces;
+            for (int64_t pc = gn.plo + wid; pc < gn.phi; pc += FD_WAVES) {
+                const int64_t* r = node_rows + pc;
+                u128_add(a[3], a[4], (uint64_t)r[NR_UCPU_LO * np]); a[5] += (uint64_t)r[NR_UCPU_HI * np];
+                u128_add(a[6], a[7], (uint64_t)r[NR_UMEM_LO * np]); a[8] += (uint64_t)r[NR_UMEM_HI * np];
+                u128_add(a[9], a[10], (uint64_t)r[NR_ACPU_LO * np]); a[11] += (uint64_t)r[NR_ACPU_HI * np];
+                u128_add(a[12], a[13], (uint64_t)r[NR_AMEM_LO * np]); a[14] += (uint64_t)r[NR_AMEM_HI * np];
+                const uint64_t cn = (uint64_t)r[NR_COUNTS * np];
+                a[0] += cn & NR_CNT_MASK;
+                a[1] += (cn >> NR_CNT_BITS) & NR_CNT_MASK;
+                a[2] += cn >> (2 * NR_CNT_BITS);
+            }
+        }
+        // merge the waves: counts, then the (lo, carry, hi) triples in two rounds
+#pragma unroll
+        for (int r0 = 0; r0 < NA; r0 += (r0 == 0 ? 3 : 6)) {
+            const int nk = r0 == 0 ? 3 : 6;
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                if (k < nk) red[wid][k][lane] = a[r0 + k];
+            __syncthreads();
+            if (wid == 0) {
+                for (int w = 1; w < FD_WAVES; ++w) {
+                    if (r0 == 0) {
+                        a[0] += red[w][0][lane]; a[1] += red[w][1][lane]; a[2] += red[w][2][lane];
+                    } else {
+#pragma unroll
+                        for (int k = 0; k < 6; k += 3) {
+                            u128_add(a[r0 + k], a[r0 + k + 1], red[w][k][lane]);
+                            a[r0 + k + 1] += red[w][k + 1][lane];
+                            a[r0 + k + 2] += red[w][k + 2][lane];
+                        }
+                    }
                 }
             }
         }
-    }
-    __shared__ esc_group_decision sdec[64];
-    if (wid == 0 && ok) {
-    // wide pod row of the slot (agent-scope loads: written by K1's device-scope atomics)
-    int64_t* wp = wide_pod + slot * WP_K;
-    int64_t p[WP_K];
+        if (wid == 0 && ok) {
+            const int sl = (int)((int64_t)G.gslot[g] - s0);
+            int64_t* pw = pwords + (int64_t)g * PW_K;
+            const __int128 pcpu = (__int128)tot[0][sl] + ((__int128)wtot[WP_CPU_HI][sl] << 32) + (__int128)wtot[WP_CPU_LO][sl];
+            const __int128 pmem = (__int128)(((unsigned __int128)tot[3][sl] << 64) | tot[2][sl]) +
+                                  ((__int128)wtot[WP_MEM_HI][sl] << 32) + (__int128)wtot[WP_MEM_LO][sl];
+            split_store(pw, PW_CPU_LO, pcpu);
+            split_store(pw, PW_MEM_LO, pmem);
+            pw[PW_N] = (int64_t)tot[1][sl] + wtot[WP_CNT][sl];
+            __int128 ncpu, nmem;
+            uint64_t n_unt = a[0], n_taint = a[1], n_cord = a[2];
+            if (!G.dry[g]) {
+                ncpu = join_parts(a[3], a[4], (int64_t)a[5]);
+                nmem = join_parts(a[6], a[7], (int64_t)a[8]);
+            } else {
+                // dry mode (controller.go:126-138): untainted = every member but the tracked ones
+                int64_t* t = trk_acc + (int64_t)g * TA_K;
+                int64_t tr[TA_K];
 #pragma unroll
-    for (int k = 0; k < WP_K; ++k) p[k] = ld_agent(wp + k);
-    if ((p[0] | p[1] | p[2] | p[3] | p[4]) != 0) {
-        __threadfence();
-        const uint32_t seen = atomicAdd(wp_cnt + slot, 1u) + 1u;
-        if (seen == G.slot_readers[slot]) {             // every reader has its copy: reset
-#pragma unroll
-            for (int k = 0; k < WP_K; ++k)
-                __hip_atomic_store(wp + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(wp_cnt + slot, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (int k = 0; k < TA_K; ++k)
+                    tr[k] = __hip_atomic_exchange(t + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ncpu = join_parts(a[9], a[10], (int64_t)a[11]) - (((__int128)tr[TA_CPU_HI] << 32) + (__int128)tr[TA_CPU_LO]);
+                nmem = join_parts(a[12], a[13], (int64_t)a[14]) - (((__int128)tr[TA_MEM_HI] << 32) + (__int128)tr[TA_MEM_LO]);
+                const uint64_t n_all = n_unt + n_taint + n_cord;
+                n_unt = n_all - (uint64_t)tr[TA_CNT];
+                n_taint = (uint64_t)tr[TA_CNT];
+                n_cord = 0;
+            }
+            // the node words stay on this rank: every rank reduces the whole node index
+            int64_t* nw = nwords + (int64_t)g * NW_K;
+            const bool n_ok = ncpu >= (__int128)INT64_MIN && ncpu <= (__int128)INT64_MAX &&
+                              nmem >= (__int128)INT64_MIN && nmem <= (__int128)INT64_MAX;
+            nw[NW_CPU] = (int64_t)ncpu;
+            nw[NW_MEM] = (int64_t)nmem;
+            nw[NW_N_UNT] = (int64_t)n_unt;
+            nw[NW_N_TAINT] = (int64_t)n_taint;
+            nw[NW_N_CORD] = (int64_t)n_cord;
+            nw[NW_FLAGS] = n_ok ? 0 : ESC_TF_NODE_OVERFLOW;
+            if (decide) finalize(G, gn, g, pw, nw, sdec[lane], G.metrics);
         }
-    }
-    int64_t* pw = pwords + (int64_t)g * PW_K;
-    const __int128 pcpu = (__int128)a[0] + ((__int128)p[WP_CPU_HI] << 32) + (__int128)p[WP_CPU_LO];
-    const __int128 pmem = (__int128)(((unsigned __int128)a[3] << 64) | a[2]) + ((__int128)p[WP_MEM_HI] << 32) +
-                          (__int128)p[WP_MEM_LO];
-    split_store(pw, PW_CPU_LO, pcpu);
-    split_store(pw, PW_MEM_LO, pmem);
-    pw[PW_N] = (int64_t)a[1] + p[WP_CNT];
-    __int128 ncpu, nmem;
-    uint64_t n_unt = a[4], n_taint = a[5], n_cord = a[6];
-    if (!G.dry[g]) {
-        ncpu = join_parts(a[7], a[8], (int64_t)a[9]);
-        nmem = join_parts(a[10], a[11], (int64_t)a[12]);
-    } else {
-        // dry mode (controller.go:126-138): untainted = every member but the tracked ones
-        int64_t* t = trk_acc + (int64_t)g * TA_K;
-        int64_t tr[TA_K];
-#pragma unroll
-        for (int k = 0; k < TA_K; ++k)
-            tr[k] = __hip_atomic_exchange(t + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ncpu = join_parts(a[13], a[14], (int64_t)a[15]) - (((__int128)tr[TA_CPU_HI] << 32) + (__int128)tr[TA_CPU_LO]);
-        nmem = join_parts(a[16], a[17], (int64_t)a[18]) - (((__int128)tr[TA_MEM_HI] << 32) + (__int128)tr[TA_MEM_LO]);
-        const uint64_t n_all = n_unt + n_taint + n_cord;
-        n_unt = n_all - (uint64_t)tr[TA_CNT];
-        n_taint = (uint64_t)tr[TA_CNT];
-        n_cord = 0;
-    }
-    // the node words stay on this rank: every rank reduces the whole node index
-    int64_t* nw = nwords + (int64_t)g * NW_K;
-    const bool n_ok = ncpu >= (__int128)INT64_MIN && ncpu <= (__int128)INT64_MAX &&
-                      nmem >= (__int128)INT64_MIN && nmem <= (__int128)INT64_MAX;
-    nw[NW_CPU] = (int64_t)ncpu;
-    nw[NW_MEM] = (int64_t)nmem;
-    nw[NW_N_UNT] = (int64_t)n_unt;
-    nw[NW_N_TAINT] = (int64_t)n_taint;
-    nw[NW_N_CORD] = (int64_t)n_cord;
-    nw[NW_FLAGS] = n_ok ? 0 : ESC_TF_NODE_OVERFLOW;
-    if (decide) finalize(G, gn, g, pw, nw, sdec[lane], G.metrics);
-    }
-    if (decide) {
-        __syncthreads();
-        store_decisions(dec, blockIdx.x * 64, G.G, sdec);
+        if (decide) {
+            __syncthreads();
+            const uint32_t n = gb - base < 64 ? gb - base : 64;
+            const uint32_t g0 = F.col_groups[base], gl = F.col_groups[base + n - 1];
+            if (gl - g0 + 1 == n) {
+                store_decisions(dec, (int32_t)g0, (int32_t)(g0 + n), sdec);        // one contiguous run
+            } else if (threadIdx.x < n * 4) {
+                const uint32_t k = threadIdx.x >> 2, part = threadIdx.x & 3;
+                reinterpret_cast<uint4*>(dec + F.col_groups[base + k])[part] = reinterpret_cast<const uint4*>(sdec)[threadIdx.x];
+            }
+        }
     }
 }
 
@@ -1841,18 +1910,11 @@ hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows
     return hipGetLastError();
 }
 
-hipError_t launch_pod_fold(const uint64_t* pod_part, int nblk, int64_t S, uint64_t* fold, hipStream_t st) {
-    if (nblk <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_pod_fold, dim3((unsigned)((S + 255) / 256), FOLD_SPLIT), dim3(256), 0, st, pod_part, nblk, S,
-                       fold);
-    return hipGetLastError();
-}
-
-hipError_t launch_combine(const GroupDev& g, const NodeDev& n, const uint64_t* fold, int nsplit,
-                          const int64_t* node_rows, int64_t* wide_pod, uint32_t* wp_cnt, int64_t* trk_acc,
-                          int64_t* pwords, int64_t* nwords, bool decide, esc_group_decision* dec, hipStream_t st) {
-    hipLaunchKernelGGL(k_combine, dim3((g.G + 63) / 64), dim3(CB_WAVES * 64), 0, st, g, n, fold, nsplit,
-                       node_rows, wide_pod, wp_cnt, trk_acc, pwords, nwords, decide ? 1 : 0, dec);
+hipError_t launch_fold_decide(const GroupDev& g, const NodeDev& n, const FoldPlan& f, const int64_t* node_rows,
+                              int64_t* wide_pod, int64_t* trk_acc, int64_t* pwords, int64_t* nwords, bool decide,
+                              esc_group_decision* dec, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_decide, dim3((unsigned)f.n_col, (unsigned)f.split), dim3(FD_WAVES * 64), 0, st, g, n, f,
+                       node_rows, wide_pod, trk_acc, pwords, nwords, decide ? 1 : 0, dec);
     return hipGetLastError();
 }
 

@@ -158,10 +158,14 @@ struct esc_ctx {
     // work
     int nblk = 0;
     uint64_t* d_pod_part = nullptr;
-    uint64_t* d_fold = nullptr;                               // K3a output [FOLD_SPLIT][4][S]
+    uint64_t* d_fold = nullptr;                               // K3 block folds [n_col][split][4][FC_COL]
+    uint32_t* d_col_cnt = nullptr;                            // K3 column arrivals
+    uint32_t *d_col_off = nullptr, *d_col_groups = nullptr;   // K3: groups by pod slot column
+    int fold_split = 1;
     int64_t* d_wide_pod = nullptr;
     uint32_t* d_wp_cnt = nullptr;
     uint32_t* d_k1_ticket = nullptr;                          // K1 dynamic shares (next chunk, done)
+    int64_t* d_k1seg = nullptr;                               // K1 work plan [nblk][K1_SEGS][2]
     int k1_cap = 0;                                           // K1 chunks per workgroup at most (0: static)
     int64_t* d_trk_acc = nullptr;                             // [G][TA_K] dry-mode tracked sums
     int64_t* d_pwords = nullptr;                              // active exchange buffer [G][PW_K]
@@ -260,6 +264,10 @@ const GroupIndex* ctx_group_index(const esc_ctx* ctx) { return &ctx->gi; }
 
 namespace {
 
+// K1 partial row stride: the pod slots (one per group pair + the default filter's)
+// rounded up to whole K3 columns.
+int64_t slot_stride(const esc_ctx* c) { return ((int64_t)c->gi.n_gp + 1 + FC_COL - 1) / FC_COL * FC_COL; }
+
 GroupDev group_dev(const esc_ctx* c) {
     GroupDev g;
     g.dry = c->d_dry;
@@ -271,6 +279,7 @@ GroupDev group_dev(const esc_ctx* c) {
     g.gslot = c->d_gslot;
     g.metrics = c->want_metrics ? c->d_metrics : nullptr;
     g.n_gp = c->gi.n_gp;
+    g.sp = slot_stride(c);
     g.G = c->gi.G;
     g.default_group = c->gi.default_group < 0 ? NONE : (uint32_t)c->gi.default_group;
     return g;
@@ -283,6 +292,8 @@ PodDev pod_dev(const esc_ctx* c, int replica) {
     p.xc_cpu = b.xc_cpu; p.xc_mem = b.xc_mem; p.xp = b.xp;
     p.xc_base = b.xc_base; p.xp_base = b.xp_base;
     p.cls = b.cls;
+    p.seg = (c->k1_variant == 5 || c->k1_variant == 6 || c->k1_variant == 7 || c->k1_variant == 14) ? nullptr
+                                                                                                    : c->d_k1seg;
     p.n_cls = c->n_cls;
     p.k_tiles = c->k_tiles;
     p.k_weight = c->k_weight;
@@ -351,7 +362,7 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
 }
 
 void release_work(esc_ctx* c) {
-    dfree(c->d_pod_part); dfree(c->d_fold); dfree(c->d_wide_pod); dfree(c->d_wp_cnt); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
+    dfree(c->d_k1seg); dfree(c->d_pod_part); dfree(c->d_fold); dfree(c->d_col_cnt); dfree(c->d_wide_pod); dfree(c->d_wp_cnt); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
     dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_metrics);
     c->d_pwords = nullptr;
     if (c->h_dec) hipHostFree(c->h_dec);
@@ -507,6 +518,75 @@ int32_t build_age_index(esc_ctx* c) {
     return ESC_OK;
 }
 
+// K1 work plan: every workgroup's K tiles as at most K1_SEGS runs of one
+// class, balanced in work weight (16-B loads), with at most two class boundaries per
+// workgroup.  A class run restarts the workgroup's load pipeline (its first tiles' full
+// latency, every wave at once), so the old weight-range shares, which let a workgroup
+// cross every small class in its range (up to 4 runs at 12.5M pods), set the launch's
+// tail.  Classes lighter than one share ("small") are each placed whole into one
+// workgroup, beside a chunk of a large class that does not end there; large classes are
+// cut at tile boundaries following the cumulative weight target, so rounding never drifts.
+std::vector<int64_t> plan_k1(const std::vector<PodClass>& cls, int64_t W, int64_t nblk) {
+    std::vector<int64_t> seg((size_t)nblk * K1_SEGS * 2, 0);
+    if (W <= 0 || nblk <= 0) return seg;
+    std::vector<int> big, small;
+    for (int i = 0; i < (int)cls.size(); ++i) {
+        const int64_t w = (cls[i].t1 - cls[i].t0) * (int64_t)cls[i].wt;
+        if (w == 0) continue;
+        (w * nblk < W ? small : big).push_back(i);
+    }
+    std::sort(small.begin(), small.end(), [&](int a, int b) {
+        return (cls[a].t1 - cls[a].t0) * cls[a].wt > (cls[b].t1 - cls[b].t0) * cls[b].wt;
+    });
+    size_t bi = 0, si = 0;
+    int64_t toff = 0, cum = 0;
+    const int64_t n_small = (int64_t)small.size();
+    for (int64_t k = 0; k < nblk; ++k) {
+        int ns = 0;
+        auto add = [&](int ci, int64_t a, int64_t b) {
+            int64_t* e = &seg[((size_t)k * K1_SEGS + ns) * 2];
+            e[0] = a | ((int64_t)ci << 48);
+            e[1] = b;
+            ++ns;
+        };
+        const int64_t end = k + 1 == nblk ? W : (int64_t)((__int128)W * (k + 1) / nblk);
+        // spread the small classes over the grid, one per workgroup, where the large stream
+        // has no boundary inside this workgroup
+        if (si < small.size() && k >= (int64_t)si * nblk / std::max<int64_t>(n_small, 1)) {
+            const PodClass& q = cls[small[si]];
+            const int64_t wq = (q.t1 - q.t0) * q.wt;
+            bool fits = bi >= big.size();
+            if (!fits) {
+                const PodClass& c = cls[big[bi]];
+                fits = (c.t1 - c.t0 - toff) * (int64_t)c.wt >= end - cum - wq;
+            }
+            if (fits || k + 1 == nblk || nblk - k <= n_small - (int64_t)si) {
+                add(small[si], q.t0, q.t1);
+                cum += wq;
+                ++si;
+            }
+        }
+        while (bi < big.size() && (cum < end || k + 1 == nblk) && ns < K1_SEGS) {
+            const PodClass& c = cls[big[bi]];
+            const int64_t rem = c.t1 - c.t0 - toff;
+            int64_t take = k + 1 == nblk ? rem : std::min(rem, (end - cum + c.wt / 2) / (int64_t)c.wt);
+            if (take <= 0) break;
+            add(big[bi], c.t0 + toff, c.t0 + toff + take);
+            toff += take;
+            cum += take * (int64_t)c.wt;
+            if (toff == c.t1 - c.t0) { ++bi; toff = 0; }
+        }
+        while (k + 1 == nblk && si < small.size() && ns < K1_SEGS) {   // leftovers (never in practice)
+            const PodClass& q = cls[small[si++]];
+            add((int)(&q - cls.data()), q.t0, q.t1);
+        }
+    }
+    // a grid smaller than the class count can leave tiles unplanned: no plan then (K1 falls
+    // back to the weight-range shares)
+    if (bi < big.size() || si < small.size()) seg.clear();
+    return seg;
+}
+
 // Pod accumulator slots: one per group pair + one for the default filter.
 int64_t pod_slots(const esc_ctx* c) { return (int64_t)c->gi.n_gp + 1; }
 
@@ -539,9 +619,34 @@ int32_t ensure_work(esc_ctx* c) {
     while (cap > K1_CHUNKS && block_pods(nblk) > PODS_PER_BLOCK_MAX) --cap;
     c->k1_cap = k1_dynamic(c->k1_variant) ? (int)cap : 0;
     nblk = std::min<int64_t>(nblk, std::max(c->k_tiles, c->c_tiles));
+    std::vector<int64_t> plan;
+    for (;;) {            // the plan's own per-workgroup pod counts must keep the LDS words exact
+        plan = plan_k1(c->h_cls, c->k_weight, std::max<int64_t>(nblk, 1));
+        if (plan.empty()) break;
+        int64_t worst = 0;
+        for (int64_t b = 0; b < nblk; ++b) {
+            int64_t pods = ((c->c_tiles + nblk - 1) / nblk) * CTILE;
+            for (int k = 0; k < K1_SEGS; ++k) {
+                const int64_t* e = &plan[((size_t)b * K1_SEGS + k) * 2];
+                if (e[1]) pods += (e[1] - (e[0] & ((1ll << 48) - 1))) * TILE;
+            }
+            worst = std::max(worst, pods);
+        }
+        if (worst <= PODS_PER_BLOCK_MAX || nblk >= std::max(c->k_tiles, c->c_tiles)) break;
+        nblk *= 2;
+    }
     c->nblk = (int)nblk;
-    HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * S));
-    HIP_TRY(dalloc(&c->d_fold, (size_t)FOLD_SPLIT * 4 * S));
+    if (!plan.empty()) {
+        HIP_TRY(dalloc(&c->d_k1seg, plan.size()));
+        HIP_TRY(hipMemcpy(c->d_k1seg, plan.data(), plan.size() * 8, hipMemcpyHostToDevice));
+    }
+    const int64_t SP = slot_stride(c), n_col = SP / FC_COL;
+    HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * SP));
+    // K3: ~16 K1 rows per block, every one in flight (4 per wave)
+    c->fold_split = (int)std::max<int64_t>(1, std::min<int64_t>(64, (nblk + 15) / 16));
+    HIP_TRY(dalloc(&c->d_fold, (size_t)n_col * c->fold_split * 4 * FC_COL));
+    HIP_TRY(dalloc(&c->d_col_cnt, (size_t)n_col));
+    HIP_TRY(hipMemset(c->d_col_cnt, 0, (size_t)n_col * sizeof(uint32_t)));
     HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
     HIP_TRY(dalloc(&c->d_wp_cnt, (size_t)S));
     HIP_TRY(dalloc(&c->d_k1_ticket, 2));
@@ -601,10 +706,19 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
         HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, st));
     }
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-    HIP_TRY(launch_pod_fold(c->d_pod_part, nblk, pod_slots(c), c->d_fold, st));   // K3a
     esc_group_decision* dec = c->zero_copy ? c->h_dec_dev : c->d_dec;
-    HIP_TRY(launch_combine(g, n, c->d_fold, nblk ? FOLD_SPLIT : 0, c->nodes.rows, c->d_wide_pod, c->d_wp_cnt, c->d_trk_acc,
-                           c->d_pwords, c->d_nwords, decide, dec, st));
+    FoldPlan f;
+    f.part = c->d_pod_part;
+    f.nblk = nblk;
+    f.split = c->fold_split;
+    f.sp = slot_stride(c);
+    f.n_col = f.sp / FC_COL;
+    f.scratch = c->d_fold;
+    f.col_cnt = c->d_col_cnt;
+    f.col_off = c->d_col_off;
+    f.col_groups = c->d_col_groups;
+    HIP_TRY(launch_fold_decide(g, n, f, c->nodes.rows, c->d_wide_pod, c->d_trk_acc, c->d_pwords, c->d_nwords, decide,
+                               dec, st));
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     if (copy_out && !c->zero_copy) {
         HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)g.G * sizeof(esc_group_decision),
@@ -728,6 +842,17 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
         ++readers[gslot[g]];
     }
     if (hipMemcpy(c->d_gslot, gslot.data(), G * 4, hipMemcpyHostToDevice)) return fail(ESC_E_HIP);
+    {   // K3: the groups of every column of FC_COL pod slots, ordered by (slot, group)
+        const int64_t n_col = slot_stride(c) / FC_COL;
+        std::vector<uint32_t> off((size_t)n_col + 1, 0), order(G);
+        for (size_t g = 0; g < G; ++g) { order[g] = (uint32_t)g; ++off[gslot[g] / FC_COL + 1]; }
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return gslot[a] < gslot[b]; });
+        for (int64_t k = 0; k < n_col; ++k) off[k + 1] += off[k];
+        if (dalloc(&c->d_col_off, off.size()) || dalloc(&c->d_col_groups, G)) return fail(ESC_E_NOMEM);
+        if (hipMemcpy(c->d_col_off, off.data(), off.size() * 4, hipMemcpyHostToDevice) ||
+            hipMemcpy(c->d_col_groups, order.data(), G * 4, hipMemcpyHostToDevice))
+            return fail(ESC_E_HIP);
+    }
     if (hipMemcpy(c->d_slot_readers, readers.data(), readers.size() * 4, hipMemcpyHostToDevice))
         return fail(ESC_E_HIP);
     if (hipMemcpy(c->d_gpair, gi.gpair.data(), G * 4, hipMemcpyHostToDevice) ||
@@ -759,6 +884,7 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         c->nodes.release();
         dfree(c->d_dry); dfree(c->d_params);
         dfree(c->d_gpair); dfree(c->d_node_code); dfree(c->d_code_list); dfree(c->d_slot_readers); dfree(c->d_gslot);
+        dfree(c->d_col_off); dfree(c->d_col_groups);
         for (int i = 0; i < MAX_STAGES; ++i)
             if (c->ev[i]) hipEventDestroy(c->ev[i]);
         if (c->side) hipStreamSynchronize(c->side);
