@@ -116,7 +116,6 @@ struct GroupDev {
     const uint32_t* gpair;     // [G] group -> its pair id (K3 joins pod slots / node pieces to groups)
     const uint32_t* node_code; // [n_gp] pair id -> group code (K5)
     const uint32_t* code_list; // CODE_MULTI lists: [count, g...]
-    const uint32_t* slot_readers; // [n_gp + 1] groups reading each pod slot in K3
     const uint32_t* gslot;     // [G] the group's pod slot: its pair, or n_gp for the default group
     esc_group_metrics* metrics; // [G] gauges written by K4, or null (esc_set_metrics)
     int64_t sp;                // K1 partial row stride: pod slots rounded up to FC_COL
@@ -126,7 +125,7 @@ struct GroupDev {
 };
 
 // Wide (exact, any-range) pod accumulators: global int64 atomics, one row per pod slot.
-// K3 reads them and the last reader of a non-zero row resets it (wp_cnt).
+// K3 reads them and resets a non-zero row (every reader of a slot is in one K3 workgroup).
 enum WidePod : int { WP_CPU_LO = 0, WP_CPU_HI, WP_MEM_LO, WP_MEM_HI, WP_CNT, WP_K };
 // Per dry-mode group: the tracked members' count and split sums (K2 adds, K3 resets).
 enum TrkAcc : int { TA_CNT = 0, TA_CPU_LO, TA_CPU_HI, TA_MEM_LO, TA_MEM_HI, TA_K };
@@ -148,21 +147,36 @@ hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
                                int64_t* wide, hipStream_t st);
 hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows, int64_t* trk_acc, hipStream_t st);
-// K3 (k_fold_decide): fold of the K1 partials + group join + decide in one launch.
+// Compact decision record (32 B) that K3 / K4 write to pinned host memory each decision
+// instead of the ABI's 64-B esc_group_decision: esc_results rebuilds the full record on the
+// host (the cached capacity from its node mirror: allNodes[0]'s allocatable when the group
+// has nodes, else the state's, controller.go:207-211) and copies the full record, which
+// the kernels also keep in device memory, for a group whose delta or n_to_taint leaves int32.
+struct DecCompact {
+    double cpu_pct, mem_pct;
+    int32_t delta, n_to_taint;
+    uint8_t status, branch, taint_status, wide;
+    uint32_t pad;
+};
+static_assert(sizeof(DecCompact) == 32, "compact decision is 2 x 16 B");
+
+// K2b (k_node_groups): every group's final node words from K2's piece rows (side stream).
+hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t* node_rows, int64_t* trk_acc,
+                              int64_t* nwords, hipStream_t st);
+// K3 (k_fold_decide): fold of the K1 partials + group join + decide, one workgroup per column.
 constexpr int FC_COL = 128;            // pod slots per K3 column (one 16-B wave-load of a row)
 struct FoldPlan {
     const uint64_t* part;              // K1 partials: row b = cc[sp], mem[sp] at part + 2 * sp * b
-    int nblk, split;                   // K1 rows; row ranges per column (grid.y)
+    int nblk;                          // K1 rows
     int64_t sp;                        // slots per partial row, a multiple of FC_COL
-    int64_t n_col;                     // columns (grid.x)
-    uint64_t* scratch;                 // [n_col][split][4][FC_COL] block folds
-    uint32_t* col_cnt;                 // [n_col] arrivals (the last block resets its word)
+    int64_t n_col;                     // columns (grid)
     const uint32_t* col_off;           // [n_col + 1] the column's groups in col_groups
     const uint32_t* col_groups;        // group ids ordered by pod slot, then id
+    int ablate;                        // ESC_K3_ABLATE (timing-only knob)
 };
-hipError_t launch_fold_decide(const GroupDev& g, const NodeDev& n, const FoldPlan& f, const int64_t* node_rows,
-                              int64_t* wide_pod, int64_t* trk_acc, int64_t* pwords, int64_t* nwords, bool decide,
-                              esc_group_decision* dec, hipStream_t st);
+hipError_t launch_fold_decide(const GroupDev& g, const NodeDev& n, const FoldPlan& f, int64_t* wide_pod,
+                              int64_t* pwords, const int64_t* nwords, bool decide, esc_group_decision* dec,
+                              DecCompact* cdec, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
 // §8f rank 2: a loaded pod as seen by NodePodsRemaining, listed per node (runs in
 // node order).  p[0..2]: the pod's extra pairs (NONE-padded); a C pod with more than 3
@@ -197,7 +211,7 @@ struct PatchTargets {          // k_patch destinations: 4-byte arrays 0-5, 8-byt
 };
 hipError_t launch_patch(const PatchTargets& t, const uint64_t* where, const uint64_t* what, int64_t n, hipStream_t st);
 hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords,
-                         const int64_t* nwords, esc_group_decision* dec, hipStream_t st);
+                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st);
 
 // Ordering (K5), see esc_kernels.hip: the age index (once per snapshot) and the per-decision
 // (group, class) partition.

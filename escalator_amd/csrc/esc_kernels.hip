@@ -829,15 +829,41 @@ __device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn,
     }
 }
 
-// The decisions of 64 consecutive groups (sdec, LDS) stored by 256 threads as 16-B pieces
-// of one contiguous 4 KB run: the destination is pinned host memory (zero-copy), where
-// 8-B fields at a 64-B stride would each be a separate PCIe write.
-__device__ __forceinline__ void store_decisions(esc_group_decision* __restrict__ dec, int32_t g0, int32_t G,
-                                                const esc_group_decision* sdec) {
+__device__ __forceinline__ DecCompact compact_of(const esc_group_decision& d) {
+    DecCompact c;
+    c.cpu_pct = d.cpu_pct;
+    c.mem_pct = d.mem_pct;
+    const bool fits = d.delta == (int64_t)(int32_t)d.delta && d.n_to_taint == (int64_t)(int32_t)d.n_to_taint;
+    c.delta = (int32_t)d.delta;
+    c.n_to_taint = (int32_t)d.n_to_taint;
+    c.status = (uint8_t)d.status;
+    c.branch = (uint8_t)d.branch;
+    c.taint_status = (uint8_t)d.taint_status;
+    c.wide = fits ? 0 : 1;
+    c.pad = 0;
+    return c;
+}
+
+__device__ __forceinline__ void store_full(esc_group_decision* dst, const esc_group_decision& d) {
     static_assert(sizeof(esc_group_decision) == 64, "decision record is 4 x 16 B");
-    const int ng = G - g0 < 64 ? G - g0 : 64;
-    if ((int)threadIdx.x < ng * 4)
-        reinterpret_cast<uint4*>(dec + g0)[threadIdx.x] = reinterpret_cast<const uint4*>(sdec)[threadIdx.x];
+    const uint4* s = reinterpret_cast<const uint4*>(&d);
+    uint4* o = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = s[k];
+}
+
+// The compact decisions of n groups staged in LDS (sc), written as 16-B pieces: one
+// contiguous run when the groups are consecutive ids (g0 ..), else per group (ids[k]).
+// The destination is pinned host memory (zero-copy), where scattered narrow fields would
+// each be a PCIe write.
+__device__ __forceinline__ void store_compact(DecCompact* __restrict__ cdec, const DecCompact* sc, uint32_t n,
+                                              bool seq, uint32_t g0, const uint32_t* ids, uint32_t tid,
+                                              uint32_t nthreads) {
+    const uint4* src = reinterpret_cast<const uint4*>(sc);
+    for (uint32_t i = tid; i < n * 2; i += nthreads) {
+        const uint32_t k = i >> 1;
+        reinterpret_cast<uint4*>(cdec + (seq ? g0 + k : ids[k]))[i & 1] = src[i];
+    }
 }
 
 __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
@@ -846,179 +872,192 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 
 }  // namespace
 
-// K3 (k_fold_decide): the K1 workgroups' slot partials folded, joined to the groups and
-// decided, in ONE launch.  Grid = columns of FC_COL slots x `split` row ranges.  Every
-// block sums its rows of its column (16-B loads: a wave-load covers the column's 128 slots
-// of one row; every row of the block in flight at once) and publishes the result (sc1
-// stores, drained, then one agent-scope ticket add per block: MI355X_MICROARCH.md
-// § visibility, the first row of the hand-off table).  The block whose add comes last sums
-// the column's `split` results (sc1 loads) and evaluates every group whose pod slot lies
-// in the column (col_off / col_groups): the slot's sums + its wide (exact-path) row, the
-// pieces of the group's node pair (4 waves split them), the dry-mode tracker sums, then
-// K4 (decide_one) for one rank.  No block waits on another: only arrivals are counted.
-//  - pods: the group's slot is its pair (NewPodAffinityFilterFunc, node_group.go:218) or,
-//    for the group named "default", the default filter's slot (client.go:58-64);
-//  - nodes: the pieces of the group's pair (NewNodeLabelFilterFunc, node_group.go:278);
-//    wet groups take the filterNodes classes, dry groups (controller.go:126-138) take
-//    every member as untainted (cordoned ones included) except the tracked members;
-//  - allNodes[0] (controller.go:208): the pair's first entry (GroupNode, set at load).
-namespace {
-constexpr int FD_WAVES = 4;
+// K2b (k_node_groups, side stream, beside K1): every group's node words from its pair's
+// K2 piece rows — NewNodeLabelFilterFunc (node_group.go:278) + filterNodes
+// (controller.go:120-154) + CalculateNodesCapacityTotal(untainted) (util.go:41-51): wet
+// groups take the filterNodes classes, dry groups (controller.go:126-138) every member as
+// untainted (cordoned ones included) except the tracked members (K2's tracker sums, read
+// and reset here).  64 groups per block, the 4 waves split each group's pieces.  Every
+// rank reduces the whole node index, so these words are final (never exchanged).
+constexpr int NG_WAVES = 4;
 
-__device__ __forceinline__ void st_sc1(uint64_t* p, uint64_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_sc1(const uint64_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-}  // namespace
-
-__global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeDev N, FoldPlan F,
-                                                                 const int64_t* __restrict__ node_rows,
-                                                                 int64_t* __restrict__ wide_pod,
-                                                                 int64_t* __restrict__ trk_acc,
-                                                                 int64_t* __restrict__ pwords,
-                                                                 int64_t* __restrict__ nwords, int decide,
-                                                                 esc_group_decision* __restrict__ dec) {
-    __shared__ uint64_t red[FD_WAVES][8][64];
-    __shared__ uint64_t tot[4][FC_COL];                 // per slot: cpu, count, mem lo, mem carry
-    __shared__ int64_t wtot[WP_K][FC_COL];              // per slot: its wide row
-    __shared__ esc_group_decision sdec[64];
-    __shared__ uint32_t s_last;
+__global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeDev N,
+                                                               const int64_t* __restrict__ node_rows,
+                                                               int64_t* __restrict__ trk_acc,
+                                                               int64_t* __restrict__ nwords) {
+    __shared__ uint64_t red[NG_WAVES][6][64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int col = blockIdx.x, y = blockIdx.y;
-    const int64_t s0 = (int64_t)col * FC_COL;
-    // ---- fold: rows [b0, b1) of the column, every row of the block in flight at once
-    {
-        uint64_t cp[2] = {0, 0}, cn[2] = {0, 0}, ml[2] = {0, 0}, mc[2] = {0, 0};
-        const int b0 = F.nblk * y / F.split, b1 = F.nblk * (y + 1) / F.split;
-        constexpr int U = 4;
-        for (int b = b0 + wid; b < b1; b += FD_WAVES * U) {
-            ulonglong2 c[U], m[U];
+    const int32_t g = blockIdx.x * 64 + lane;
+    const bool ok = g < G.G;
+    constexpr int NA = 15;   // 0-2 counts; node sums (lo, carry, hi): 3-5 unt cpu, 6-8 unt mem, 9-11 all cpu, 12-14 all mem
+    uint64_t a[NA];
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int bb = b + FD_WAVES * u < b1 ? b + FD_WAVES * u : b;
-                const int64_t* row = reinterpret_cast<const int64_t*>(F.part) + (int64_t)bb * 2 * F.sp + s0 + 2 * lane;
-                c[u] = ld2(row);
-                m[u] = ld2(row + F.sp);
-            }
+    for (int k = 0; k < NA; ++k) a[k] = 0;
+    int64_t plo = 0, phi = 0;
+    if (ok) { plo = N.gnode[g].plo; phi = N.gnode[g].phi; }
+    const int64_t np = N.n_pieces;
+#pragma unroll 2
+    for (int64_t pc = plo + wid; pc < phi; pc += NG_WAVES) {
+        const int64_t* r = node_rows + pc;
+        u128_add(a[3], a[4], (uint64_t)r[NR_UCPU_LO * np]); a[5] += (uint64_t)r[NR_UCPU_HI * np];
+        u128_add(a[6], a[7], (uint64_t)r[NR_UMEM_LO * np]); a[8] += (uint64_t)r[NR_UMEM_HI * np];
+        u128_add(a[9], a[10], (uint64_t)r[NR_ACPU_LO * np]); a[11] += (uint64_t)r[NR_ACPU_HI * np];
+        u128_add(a[12], a[13], (uint64_t)r[NR_AMEM_LO * np]); a[14] += (uint64_t)r[NR_AMEM_HI * np];
+        const uint64_t cn = (uint64_t)r[NR_COUNTS * np];
+        a[0] += cn & NR_CNT_MASK;
+        a[1] += (cn >> NR_CNT_BITS) & NR_CNT_MASK;
+        a[2] += cn >> (2 * NR_CNT_BITS);
+    }
+    // merge the waves: counts, then the (lo, carry, hi) triples in two rounds
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (b + FD_WAVES * u >= b1) break;
-                cp[0] += c[u].x & CPU_MASK; cn[0] += c[u].x >> CNT_SHIFT;
-                cp[1] += c[u].y & CPU_MASK; cn[1] += c[u].y >> CNT_SHIFT;
-                u128_add(ml[0], mc[0], m[u].x);
-                u128_add(ml[1], mc[1], m[u].y);
-            }
-        }
-        red[wid][0][lane] = cp[0]; red[wid][1][lane] = cp[1]; red[wid][2][lane] = cn[0]; red[wid][3][lane] = cn[1];
-        red[wid][4][lane] = ml[0]; red[wid][5][lane] = ml[1]; red[wid][6][lane] = mc[0]; red[wid][7][lane] = mc[1];
+    for (int r0 = 0; r0 < NA; r0 += (r0 == 0 ? 3 : 6)) {
+        const int nk = r0 == 0 ? 3 : 6;
+        if (r0) __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            if (k < nk) red[wid][k][lane] = a[r0 + k];
         __syncthreads();
         if (wid == 0) {
-            for (int w = 1; w < FD_WAVES; ++w) {
-                cp[0] += red[w][0][lane]; cp[1] += red[w][1][lane]; cn[0] += red[w][2][lane]; cn[1] += red[w][3][lane];
-                u128_add(ml[0], mc[0], red[w][4][lane]); mc[0] += red[w][6][lane];
-                u128_add(ml[1], mc[1], red[w][5][lane]); mc[1] += red[w][7][lane];
-            }
-            uint64_t* o = F.scratch + ((int64_t)col * F.split + y) * 4 * FC_COL + 2 * lane;
+            for (int w = 1; w < NG_WAVES; ++w) {
+                if (r0 == 0) {
+                    a[0] += red[w][0][lane]; a[1] += red[w][1][lane]; a[2] += red[w][2][lane];
+                } else {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
-                st_sc1(o + j, cp[j]);
-                st_sc1(o + FC_COL + j, cn[j]);
-                st_sc1(o + 2 * FC_COL + j, ml[j]);
-                st_sc1(o + 3 * FC_COL + j, mc[j]);
-            }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the storing wave drains, then signals
-            if (lane == 0) {
-                const uint32_t old = __hip_atomic_fetch_add(F.col_cnt + col, 1u, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT);
-                s_last = old + 1 == (uint32_t)F.split;
-            }
-        }
-        __syncthreads();
-        if (!s_last) return;
-    }
-    // ---- the column's last arrival: sum the `split` block folds (sc1 loads), add the wide rows
-    if (threadIdx.x == 0) __hip_atomic_store(F.col_cnt + col, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    {
-        const int sl = threadIdx.x & (FC_COL - 1), half = threadIdx.x >> 7;   // words {0,1} or {2,3}
-        uint64_t a0 = 0, a1 = 0;
-        for (int q = 0; q < F.split; ++q) {
-            const uint64_t* o = F.scratch + ((int64_t)col * F.split + q) * 4 * FC_COL + sl;
-            const uint64_t x0 = ld_sc1(o + (2 * half) * FC_COL), x1 = ld_sc1(o + (2 * half + 1) * FC_COL);
-            if (half == 0) { a0 += x0; a1 += x1; }
-            else { u128_add(a0, a1, x0); a1 += x1; }
-        }
-        tot[2 * half][sl] = a0;
-        tot[2 * half + 1][sl] = a1;
-        if (half == 0) {
-            const int64_t slot = s0 + sl;
-            int64_t p[WP_K] = {0, 0, 0, 0, 0};
-            if (slot <= (int64_t)G.n_gp) {
-                int64_t* wp = wide_pod + slot * WP_K;
-#pragma unroll
-                for (int k = 0; k < WP_K; ++k) p[k] = ld_agent(wp + k);
-                if ((p[0] | p[1] | p[2] | p[3] | p[4]) != 0)      // every reader is in this block: reset
-#pragma unroll
-                    for (int k = 0; k < WP_K; ++k)
-                        __hip_atomic_store(wp + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-#pragma unroll
-            for (int k = 0; k < WP_K; ++k) wtot[k][sl] = p[k];
-        }
-    }
-    __syncthreads();
-    // ---- the column's groups, 64 at a time (lane = group); 4 waves split each group's pieces
-    const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
-    for (uint32_t base = ga; base < gb; base += 64) {
-        const bool ok = base + lane < gb;
-        const int32_t g = ok ? (int32_t)F.col_groups[base + lane] : 0;
-        constexpr int NA = 15;   // 0-2 counts; node sums (lo, carry, hi): 3-5 unt cpu, 6-8 unt mem, 9-11 all cpu, 12-14 all mem
-        uint64_t a[NA];
-#pragma unroll
-        for (int k = 0; k < NA; ++k) a[k] = 0;
-        GroupNode gn;
-        gn.first = INT64_MAX; gn.first_cpu = gn.first_mem = 0; gn.plo = gn.phi = 0;
-        if (ok) gn = N.gnode[g];
-        {
-            const int64_t np = N.n_pieces;
-            for (int64_t pc = gn.plo + wid; pc < gn.phi; pc += FD_WAVES) {
-                const int64_t* r = node_rows + pc;
-                u128_add(a[3], a[4], (uint64_t)r[NR_UCPU_LO * np]); a[5] += (uint64_t)r[NR_UCPU_HI * np];
-                u128_add(a[6], a[7], (uint64_t)r[NR_UMEM_LO * np]); a[8] += (uint64_t)r[NR_UMEM_HI * np];
-                u128_add(a[9], a[10], (uint64_t)r[NR_ACPU_LO * np]); a[11] += (uint64_t)r[NR_ACPU_HI * np];
-                u128_add(a[12], a[13], (uint64_t)r[NR_AMEM_LO * np]); a[14] += (uint64_t)r[NR_AMEM_HI * np];
-                const uint64_t cn = (uint64_t)r[NR_COUNTS * np];
-                a[0] += cn & NR_CNT_MASK;
-                a[1] += (cn >> NR_CNT_BITS) & NR_CNT_MASK;
-                a[2] += cn >> (2 * NR_CNT_BITS);
-            }
-        }
-        // merge the waves: counts, then the (lo, carry, hi) triples in two rounds
-#pragma unroll
-        for (int r0 = 0; r0 < NA; r0 += (r0 == 0 ? 3 : 6)) {
-            const int nk = r0 == 0 ? 3 : 6;
-            __syncthreads();
-#pragma unroll
-            for (int k = 0; k < 6; ++k)
-                if (k < nk) red[wid][k][lane] = a[r0 + k];
-            __syncthreads();
-            if (wid == 0) {
-                for (int w = 1; w < FD_WAVES; ++w) {
-                    if (r0 == 0) {
-                        a[0] += red[w][0][lane]; a[1] += red[w][1][lane]; a[2] += red[w][2][lane];
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < 6; k += 3) {
-                            u128_add(a[r0 + k], a[r0 + k + 1], red[w][k][lane]);
-                            a[r0 + k + 1] += red[w][k + 1][lane];
-                            a[r0 + k + 2] += red[w][k + 2][lane];
-                        }
+                    for (int k = 0; k < 6; k += 3) {
+                        u128_add(a[r0 + k], a[r0 + k + 1], red[w][k][lane]);
+                        a[r0 + k + 1] += red[w][k + 1][lane];
+                        a[r0 + k + 2] += red[w][k + 2][lane];
                     }
                 }
             }
         }
-        if (wid == 0 && ok) {
+    }
+    if (wid != 0 || !ok) return;
+    __int128 ncpu, nmem;
+    uint64_t n_unt = a[0], n_taint = a[1], n_cord = a[2];
+    if (!G.dry[g]) {
+        ncpu = join_parts(a[3], a[4], (int64_t)a[5]);
+        nmem = join_parts(a[6], a[7], (int64_t)a[8]);
+    } else {
+        int64_t* t = trk_acc + (int64_t)g * TA_K;
+        int64_t tr[TA_K];
+#pragma unroll
+        for (int k = 0; k < TA_K; ++k)
+            tr[k] = __hip_atomic_exchange(t + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ncpu = join_parts(a[9], a[10], (int64_t)a[11]) - (((__int128)tr[TA_CPU_HI] << 32) + (__int128)tr[TA_CPU_LO]);
+        nmem = join_parts(a[12], a[13], (int64_t)a[14]) - (((__int128)tr[TA_MEM_HI] << 32) + (__int128)tr[TA_MEM_LO]);
+        const uint64_t n_all = n_unt + n_taint + n_cord;
+        n_unt = n_all - (uint64_t)tr[TA_CNT];
+        n_taint = (uint64_t)tr[TA_CNT];
+        n_cord = 0;
+    }
+    int64_t* nw = nwords + (int64_t)g * NW_K;
+    const bool n_ok = ncpu >= (__int128)INT64_MIN && ncpu <= (__int128)INT64_MAX &&
+                      nmem >= (__int128)INT64_MIN && nmem <= (__int128)INT64_MAX;
+    nw[NW_CPU] = (int64_t)ncpu;
+    nw[NW_MEM] = (int64_t)nmem;
+    nw[NW_N_UNT] = (int64_t)n_unt;
+    nw[NW_N_TAINT] = (int64_t)n_taint;
+    nw[NW_N_CORD] = (int64_t)n_cord;
+    nw[NW_FLAGS] = n_ok ? 0 : ESC_TF_NODE_OVERFLOW;
+}
+
+// K3 (k_fold_decide): the K1 workgroups' slot partials folded and joined to the groups, in
+// ONE launch with no hand-off between workgroups: one 1024-thread workgroup per column of
+// FC_COL pod slots reads every K1 row of its column (16-B loads, a wave-load covers the 128
+// slots of one row, 16 waves x up to 16 rows in flight: ~0.5 MB per CU, read back from the
+// Infinity Cache K1 just wrote it through), merges the waves in LDS, adds the slots' wide
+// (exact-path) rows, and evaluates every group whose pod slot lies in the column
+// (col_off / col_groups): pod words, then K4 (decide_one) for one rank.  The group inputs
+// that do not depend on the fold (node words from K2b, GroupNode, parameters) are loaded
+// before the fold's loads are consumed.
+//  - pods: the group's slot is its pair (NewPodAffinityFilterFunc, node_group.go:218) or,
+//    for the group named "default", the default filter's slot (client.go:58-64);
+//  - allNodes[0] (controller.go:208): the pair's first entry (GroupNode, set at load).
+namespace {
+constexpr int FD_WAVES = 16;
+constexpr int FD_U = 16;                 // K1 rows per wave in flight
+}  // namespace
+
+__global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeDev N, FoldPlan F,
+                                                                 int64_t* __restrict__ wide_pod,
+                                                                 int64_t* __restrict__ pwords,
+                                                                 const int64_t* __restrict__ nwords, int decide,
+                                                                 esc_group_decision* __restrict__ dec,
+                                                                 DecCompact* __restrict__ cdec, int ablate) {
+    // ablate (timing-only, wrong results): 1 no group phase, 4 no fold loads
+    __shared__ uint64_t red[FD_WAVES][8][64];            // 64 KB
+    __shared__ uint64_t tot[4][FC_COL];                 // per slot: cpu, count, mem lo, mem carry
+    __shared__ int64_t wtot[WP_K][FC_COL];              // per slot: its wide row
+    __shared__ DecCompact sdec[FC_COL];
+    __shared__ uint32_t s_seq;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int col = blockIdx.x;
+    const int64_t s0 = (int64_t)col * FC_COL;
+    const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
+    // ---- the group inputs that do not depend on the fold: first pass's groups, issued now
+    const uint32_t me = threadIdx.x;
+    if (me == 0) s_seq = 1u;
+    // ---- fold: every K1 row of the column; wave w takes rows w, w + 16, ...
+    uint64_t cp[2] = {0, 0}, cn[2] = {0, 0}, ml[2] = {0, 0}, mc[2] = {0, 0};
+    const int nrows = (ablate & 4) ? 0 : F.nblk;
+    for (int b = wid; b < nrows; b += FD_WAVES * FD_U) {
+        ulonglong2 c[FD_U], m[FD_U];
+#pragma unroll
+        for (int u = 0; u < FD_U; ++u) {
+            const int bb = b + FD_WAVES * u < nrows ? b + FD_WAVES * u : b;
+            const int64_t* row = reinterpret_cast<const int64_t*>(F.part) + (int64_t)bb * 2 * F.sp + s0 + 2 * lane;
+            c[u] = ld2(row);
+            m[u] = ld2(row + F.sp);
+        }
+#pragma unroll
+        for (int u = 0; u < FD_U; ++u) {
+            if (b + FD_WAVES * u >= nrows) break;
+            cp[0] += c[u].x & CPU_MASK; cn[0] += c[u].x >> CNT_SHIFT;
+            cp[1] += c[u].y & CPU_MASK; cn[1] += c[u].y >> CNT_SHIFT;
+            u128_add(ml[0], mc[0], m[u].x);
+            u128_add(ml[1], mc[1], m[u].y);
+        }
+    }
+    red[wid][0][lane] = cp[0]; red[wid][1][lane] = cp[1]; red[wid][2][lane] = cn[0]; red[wid][3][lane] = cn[1];
+    red[wid][4][lane] = ml[0]; red[wid][5][lane] = ml[1]; red[wid][6][lane] = mc[0]; red[wid][7][lane] = mc[1];
+    // the slots' wide rows (threads 0-127), read and reset (every reader is in this block)
+    int64_t p[WP_K] = {0, 0, 0, 0, 0};
+    if (me < FC_COL && s0 + me <= (int64_t)G.n_gp) {
+        int64_t* wp = wide_pod + (s0 + me) * WP_K;
+#pragma unroll
+        for (int k = 0; k < WP_K; ++k) p[k] = ld_agent(wp + k);
+        if ((p[0] | p[1] | p[2] | p[3] | p[4]) != 0)
+#pragma unroll
+            for (int k = 0; k < WP_K; ++k)
+                __hip_atomic_store(wp + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (wid < 2) {                                        // wave 0: slots 2l, 2l+1 words 0/1; wave 1: mem words
+        const int j = lane;
+        uint64_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
+        for (int w = 0; w < FD_WAVES; ++w) {
+            if (wid == 0) {
+                x0 += red[w][0][j]; x1 += red[w][1][j]; y0 += red[w][2][j]; y1 += red[w][3][j];
+            } else {
+                u128_add(x0, y0, red[w][4][j]); y0 += red[w][6][j];
+                u128_add(x1, y1, red[w][5][j]); y1 += red[w][7][j];
+            }
+        }
+        if (wid == 0) { tot[0][2 * j] = x0; tot[0][2 * j + 1] = x1; tot[1][2 * j] = y0; tot[1][2 * j + 1] = y1; }
+        else { tot[2][2 * j] = x0; tot[2][2 * j + 1] = x1; tot[3][2 * j] = y0; tot[3][2 * j + 1] = y1; }
+    }
+    if (me < FC_COL)
+#pragma unroll
+        for (int k = 0; k < WP_K; ++k) wtot[k][me] = p[k];
+    __syncthreads();
+    if (ablate & 1) return;
+    // ---- the column's groups, one thread each (a column holds ~FC_COL groups)
+    for (uint32_t base = ga; base < gb; base += FD_WAVES * 64) {
+        const bool ok = base + me < gb;
+        const int32_t g = ok ? (int32_t)F.col_groups[base + me] : 0;
+        if (ok) {
+            if (g != (int32_t)F.col_groups[base] + (int32_t)me) s_seq = 0u;
             const int sl = (int)((int64_t)G.gslot[g] - s0);
             int64_t* pw = pwords + (int64_t)g * PW_K;
             const __int128 pcpu = (__int128)tot[0][sl] + ((__int128)wtot[WP_CPU_HI][sl] << 32) + (__int128)wtot[WP_CPU_LO][sl];
@@ -1027,61 +1066,37 @@ __global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeD
             split_store(pw, PW_CPU_LO, pcpu);
             split_store(pw, PW_MEM_LO, pmem);
             pw[PW_N] = (int64_t)tot[1][sl] + wtot[WP_CNT][sl];
-            __int128 ncpu, nmem;
-            uint64_t n_unt = a[0], n_taint = a[1], n_cord = a[2];
-            if (!G.dry[g]) {
-                ncpu = join_parts(a[3], a[4], (int64_t)a[5]);
-                nmem = join_parts(a[6], a[7], (int64_t)a[8]);
-            } else {
-                // dry mode (controller.go:126-138): untainted = every member but the tracked ones
-                int64_t* t = trk_acc + (int64_t)g * TA_K;
-                int64_t tr[TA_K];
-#pragma unroll
-                for (int k = 0; k < TA_K; ++k)
-                    tr[k] = __hip_atomic_exchange(t + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ncpu = join_parts(a[9], a[10], (int64_t)a[11]) - (((__int128)tr[TA_CPU_HI] << 32) + (__int128)tr[TA_CPU_LO]);
-                nmem = join_parts(a[12], a[13], (int64_t)a[14]) - (((__int128)tr[TA_MEM_HI] << 32) + (__int128)tr[TA_MEM_LO]);
-                const uint64_t n_all = n_unt + n_taint + n_cord;
-                n_unt = n_all - (uint64_t)tr[TA_CNT];
-                n_taint = (uint64_t)tr[TA_CNT];
-                n_cord = 0;
+            if (decide) {
+                esc_group_decision d;
+                finalize(G, N.gnode[g], g, pw, nwords + (int64_t)g * NW_K, d, G.metrics);
+                store_full(dec + g, d);                       // device copy of the full record
+                if (me < FC_COL) sdec[me] = compact_of(d);
+                else cdec[g] = compact_of(d);
             }
-            // the node words stay on this rank: every rank reduces the whole node index
-            int64_t* nw = nwords + (int64_t)g * NW_K;
-            const bool n_ok = ncpu >= (__int128)INT64_MIN && ncpu <= (__int128)INT64_MAX &&
-                              nmem >= (__int128)INT64_MIN && nmem <= (__int128)INT64_MAX;
-            nw[NW_CPU] = (int64_t)ncpu;
-            nw[NW_MEM] = (int64_t)nmem;
-            nw[NW_N_UNT] = (int64_t)n_unt;
-            nw[NW_N_TAINT] = (int64_t)n_taint;
-            nw[NW_N_CORD] = (int64_t)n_cord;
-            nw[NW_FLAGS] = n_ok ? 0 : ESC_TF_NODE_OVERFLOW;
-            if (decide) finalize(G, gn, g, pw, nw, sdec[lane], G.metrics);
         }
         if (decide) {
             __syncthreads();
-            const uint32_t n = gb - base < 64 ? gb - base : 64;
-            const uint32_t g0 = F.col_groups[base], gl = F.col_groups[base + n - 1];
-            if (gl - g0 + 1 == n) {
-                store_decisions(dec, (int32_t)g0, (int32_t)(g0 + n), sdec);        // one contiguous run
-            } else if (threadIdx.x < n * 4) {
-                const uint32_t k = threadIdx.x >> 2, part = threadIdx.x & 3;
-                reinterpret_cast<uint4*>(dec + F.col_groups[base + k])[part] = reinterpret_cast<const uint4*>(sdec)[threadIdx.x];
-            }
+            const uint32_t n = gb - base < FC_COL ? gb - base : FC_COL;
+            store_compact(cdec, sdec, n, s_seq != 0, F.col_groups[base], F.col_groups + base, me, FD_WAVES * 64);
+            __syncthreads();
         }
     }
 }
 
 __global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ pwords,
                                                 const int64_t* __restrict__ nwords,
-                                                esc_group_decision* __restrict__ dec) {
-    __shared__ esc_group_decision sdec[64];
-    const int32_t g = blockIdx.x * 64 + (int32_t)threadIdx.x;
-    if (threadIdx.x < 64 && g < G.G)
-        finalize(G, N.gnode[g], g, pwords + (int64_t)g * PW_K, nwords + (int64_t)g * NW_K, sdec[threadIdx.x],
-                 G.metrics);
+                                                esc_group_decision* __restrict__ dec, DecCompact* __restrict__ cdec) {
+    __shared__ DecCompact sc[256];
+    const int32_t g0 = blockIdx.x * 256, g = g0 + (int32_t)threadIdx.x;
+    if (g < G.G) {
+        esc_group_decision d;
+        finalize(G, N.gnode[g], g, pwords + (int64_t)g * PW_K, nwords + (int64_t)g * NW_K, d, G.metrics);
+        store_full(dec + g, d);
+        sc[threadIdx.x] = compact_of(d);
+    }
     __syncthreads();
-    store_decisions(dec, blockIdx.x * 64, G.G, sdec);
+    const uint32_t n = G.G - g0 < 256 ? (uint32_t)(G.G - g0) : 256u;
+    store_compact(cdec, sc, n, true, (uint32_t)g0, nullptr, threadIdx.x, 256);
 }
 
 // ===================================================================== K5 ordering
@@ -1910,11 +1925,18 @@ hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows
     return hipGetLastError();
 }
 
-hipError_t launch_fold_decide(const GroupDev& g, const NodeDev& n, const FoldPlan& f, const int64_t* node_rows,
-                              int64_t* wide_pod, int64_t* trk_acc, int64_t* pwords, int64_t* nwords, bool decide,
-                              esc_group_decision* dec, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_decide, dim3((unsigned)f.n_col, (unsigned)f.split), dim3(FD_WAVES * 64), 0, st, g, n, f,
-                       node_rows, wide_pod, trk_acc, pwords, nwords, decide ? 1 : 0, dec);
+hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t* node_rows, int64_t* trk_acc,
+                              int64_t* nwords, hipStream_t st) {
+    hipLaunchKernelGGL(k_node_groups, dim3((g.G + 63) / 64), dim3(NG_WAVES * 64), 0, st, g, n, node_rows, trk_acc,
+                       nwords);
+    return hipGetLastError();
+}
+
+hipError_t launch_fold_decide(const GroupDev& g, const NodeDev& n, const FoldPlan& f, int64_t* wide_pod,
+                              int64_t* pwords, const int64_t* nwords, bool decide, esc_group_decision* dec,
+                              DecCompact* cdec, hipStream_t st) {
+    hipLaunchKernelGGL(k_fold_decide, dim3((unsigned)f.n_col), dim3(FD_WAVES * 64), 0, st, g, n, f, wide_pod, pwords,
+                       nwords, decide ? 1 : 0, dec, cdec, f.ablate);
     return hipGetLastError();
 }
 
@@ -1943,8 +1965,8 @@ hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, h
 }
 
 hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords,
-                         const int64_t* nwords, esc_group_decision* dec, hipStream_t st) {
-    hipLaunchKernelGGL(k_decide, dim3((g.G + 63) / 64), dim3(256), 0, st, g, n, pwords, nwords, dec);
+                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st) {
+    hipLaunchKernelGGL(k_decide, dim3((g.G + 255) / 256), dim3(256), 0, st, g, n, pwords, nwords, dec, cdec);
     return hipGetLastError();
 }
 

@@ -141,7 +141,7 @@ struct esc_ctx {
     // device group tables
     uint8_t* d_dry = nullptr;
     GroupParams* d_params = nullptr;
-    uint32_t *d_gpair = nullptr, *d_node_code = nullptr, *d_code_list = nullptr, *d_slot_readers = nullptr;
+    uint32_t *d_gpair = nullptr, *d_node_code = nullptr, *d_code_list = nullptr;
     uint32_t* d_gslot = nullptr;
     // snapshot
     std::vector<PodBuf> pods;
@@ -158,12 +158,9 @@ struct esc_ctx {
     // work
     int nblk = 0;
     uint64_t* d_pod_part = nullptr;
-    uint64_t* d_fold = nullptr;                               // K3 block folds [n_col][split][4][FC_COL]
-    uint32_t* d_col_cnt = nullptr;                            // K3 column arrivals
     uint32_t *d_col_off = nullptr, *d_col_groups = nullptr;   // K3: groups by pod slot column
-    int fold_split = 1;
+    int k3_ablate = 0;                                        // ESC_K3_ABLATE (timing-only knob)
     int64_t* d_wide_pod = nullptr;
-    uint32_t* d_wp_cnt = nullptr;
     uint32_t* d_k1_ticket = nullptr;                          // K1 dynamic shares (next chunk, done)
     int64_t* d_k1seg = nullptr;                               // K1 work plan [nblk][K1_SEGS][2]
     int k1_cap = 0;                                           // K1 chunks per workgroup at most (0: static)
@@ -171,10 +168,11 @@ struct esc_ctx {
     int64_t* d_pwords = nullptr;                              // active exchange buffer [G][PW_K]
     int64_t* own_pwords = nullptr;                            // the context-owned one
     int64_t* d_nwords = nullptr;                              // [G][NW_K] rank-local node words
-    esc_group_decision* d_dec = nullptr;
-    esc_group_decision* h_dec = nullptr;
-    esc_group_decision* h_dec_dev = nullptr;                 // device view of h_dec (zero-copy)
-    bool zero_copy = true;                                    // K3/K4 write decisions to h_dec
+    esc_group_decision* d_dec = nullptr;                     // full records (device)
+    DecCompact* d_cdec = nullptr;                             // compact records (device; no zero-copy)
+    DecCompact* h_cdec = nullptr;                             // compact records (pinned host)
+    DecCompact* h_cdec_dev = nullptr;                         // device view of h_cdec (zero-copy)
+    bool zero_copy = true;                                    // K3/K4 write compact decisions to h_cdec
     bool fork_nodes = true;                                   // K2 on the side stream, beside K1
     bool want_metrics = false;                                // K4 also writes the gauges
     esc_group_metrics* d_metrics = nullptr;
@@ -275,7 +273,6 @@ GroupDev group_dev(const esc_ctx* c) {
     g.gpair = c->d_gpair;
     g.node_code = c->d_node_code;
     g.code_list = c->d_code_list;
-    g.slot_readers = c->d_slot_readers;
     g.gslot = c->d_gslot;
     g.metrics = c->want_metrics ? c->d_metrics : nullptr;
     g.n_gp = c->gi.n_gp;
@@ -362,12 +359,12 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
 }
 
 void release_work(esc_ctx* c) {
-    dfree(c->d_k1seg); dfree(c->d_pod_part); dfree(c->d_fold); dfree(c->d_col_cnt); dfree(c->d_wide_pod); dfree(c->d_wp_cnt); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
-    dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_metrics);
+    dfree(c->d_k1seg); dfree(c->d_pod_part); dfree(c->d_wide_pod); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
+    dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_cdec); dfree(c->d_metrics);
     c->d_pwords = nullptr;
-    if (c->h_dec) hipHostFree(c->h_dec);
-    c->h_dec = nullptr;
-    c->h_dec_dev = nullptr;
+    if (c->h_cdec) hipHostFree(c->h_cdec);
+    c->h_cdec = nullptr;
+    c->h_cdec_dev = nullptr;
     c->work_ready = false;
     drop_graphs(c);
 }
@@ -642,17 +639,11 @@ int32_t ensure_work(esc_ctx* c) {
     }
     const int64_t SP = slot_stride(c), n_col = SP / FC_COL;
     HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * SP));
-    // K3: ~16 K1 rows per block, every one in flight (4 per wave)
-    c->fold_split = (int)std::max<int64_t>(1, std::min<int64_t>(64, (nblk + 15) / 16));
-    HIP_TRY(dalloc(&c->d_fold, (size_t)n_col * c->fold_split * 4 * FC_COL));
-    HIP_TRY(dalloc(&c->d_col_cnt, (size_t)n_col));
-    HIP_TRY(hipMemset(c->d_col_cnt, 0, (size_t)n_col * sizeof(uint32_t)));
+    (void)n_col;
     HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
-    HIP_TRY(dalloc(&c->d_wp_cnt, (size_t)S));
     HIP_TRY(dalloc(&c->d_k1_ticket, 2));
     HIP_TRY(hipMemset(c->d_k1_ticket, 0, 2 * sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)S * WP_K * sizeof(int64_t)));
-    HIP_TRY(hipMemset(c->d_wp_cnt, 0, (size_t)S * sizeof(uint32_t)));
     HIP_TRY(dalloc(&c->d_trk_acc, (size_t)G * TA_K));
     HIP_TRY(hipMemset(c->d_trk_acc, 0, (size_t)G * TA_K * sizeof(int64_t)));
     HIP_TRY(dalloc(&c->own_pwords, (size_t)G * PW_K));
@@ -661,8 +652,9 @@ int32_t ensure_work(esc_ctx* c) {
     HIP_TRY(dalloc(&c->d_dec, (size_t)G));
     HIP_TRY(dalloc(&c->d_metrics, (size_t)G));
     HIP_TRY(hipMemset(c->d_metrics, 0, (size_t)G * sizeof(esc_group_metrics)));
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_dec), (size_t)G * sizeof(esc_group_decision)));
-    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_dec_dev), c->h_dec, 0));
+    HIP_TRY(dalloc(&c->d_cdec, (size_t)G));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_cdec), (size_t)G * sizeof(DecCompact)));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_cdec_dev), c->h_cdec, 0));
     c->work_ready = true;
     return ESC_OK;
 }
@@ -699,30 +691,28 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     }
     if (fork) {
         HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, c->side));
+        HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, c->side));
         HIP_TRY(hipEventRecord(c->ev_join, c->side));
         HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
     } else {
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
         HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, st));
+        HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, st));
     }
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-    esc_group_decision* dec = c->zero_copy ? c->h_dec_dev : c->d_dec;
+    DecCompact* cdec = c->zero_copy ? c->h_cdec_dev : c->d_cdec;
     FoldPlan f;
     f.part = c->d_pod_part;
     f.nblk = nblk;
-    f.split = c->fold_split;
     f.sp = slot_stride(c);
     f.n_col = f.sp / FC_COL;
-    f.scratch = c->d_fold;
-    f.col_cnt = c->d_col_cnt;
     f.col_off = c->d_col_off;
     f.col_groups = c->d_col_groups;
-    HIP_TRY(launch_fold_decide(g, n, f, c->nodes.rows, c->d_wide_pod, c->d_trk_acc, c->d_pwords, c->d_nwords, decide,
-                               dec, st));
+    f.ablate = c->k3_ablate;
+    HIP_TRY(launch_fold_decide(g, n, f, c->d_wide_pod, c->d_pwords, c->d_nwords, decide, c->d_dec, cdec, st));
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     if (copy_out && !c->zero_copy) {
-        HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)g.G * sizeof(esc_group_decision),
-                               hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)g.G * sizeof(DecCompact), hipMemcpyDeviceToHost, st));
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     }
     c->n_stage_ev = e;
@@ -791,6 +781,7 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
         if (c->order_fused) c->ord_chunk = 8192;               // its best chunk on config 5
     }
     if (const char* v = std::getenv("ESC_ORDER_ABLATE")) c->order_ablate = std::atoi(v);
+    if (const char* v = std::getenv("ESC_K3_ABLATE")) c->k3_ablate = std::atoi(v);
     if (const char* v = std::getenv("ESC_ORDER_CHUNK")) {      // 4096 / 8192 / 16384 (measurement knob)
         const int64_t k = std::atoll(v);
         if (k == 4096 || k == 8192 || k == 16384) c->ord_chunk = k;
@@ -830,17 +821,13 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     if (dalloc(&c->d_dry, G) || dalloc(&c->d_params, G)) return fail(ESC_E_NOMEM);
     const GroupIndex& gi = c->gi;
     if (dalloc(&c->d_gpair, G) || dalloc(&c->d_node_code, gi.n_gp) ||
-        dalloc(&c->d_code_list, gi.code_list.size()) || dalloc(&c->d_slot_readers, (size_t)gi.n_gp + 1) ||
+        dalloc(&c->d_code_list, gi.code_list.size()) ||
         dalloc(&c->d_gslot, G))
         return fail(ESC_E_NOMEM);
-    // groups reading each pod slot in K3: the default group reads the default filter's
-    // slot n_gp, every other group its pair's slot
-    std::vector<uint32_t> readers((size_t)gi.n_gp + 1, 0);
+    // each group's pod slot in K3: the default group reads the default filter's slot
+    // n_gp, every other group its pair's slot
     std::vector<uint32_t> gslot(G);
-    for (int32_t g = 0; g < n_groups; ++g) {
-        gslot[g] = g == gi.default_group ? gi.n_gp : gi.gpair[g];
-        ++readers[gslot[g]];
-    }
+    for (int32_t g = 0; g < n_groups; ++g) gslot[g] = g == gi.default_group ? gi.n_gp : gi.gpair[g];
     if (hipMemcpy(c->d_gslot, gslot.data(), G * 4, hipMemcpyHostToDevice)) return fail(ESC_E_HIP);
     {   // K3: the groups of every column of FC_COL pod slots, ordered by (slot, group)
         const int64_t n_col = slot_stride(c) / FC_COL;
@@ -853,8 +840,6 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
             hipMemcpy(c->d_col_groups, order.data(), G * 4, hipMemcpyHostToDevice))
             return fail(ESC_E_HIP);
     }
-    if (hipMemcpy(c->d_slot_readers, readers.data(), readers.size() * 4, hipMemcpyHostToDevice))
-        return fail(ESC_E_HIP);
     if (hipMemcpy(c->d_gpair, gi.gpair.data(), G * 4, hipMemcpyHostToDevice) ||
         hipMemcpy(c->d_node_code, gi.node_code.data(), gi.n_gp * 4, hipMemcpyHostToDevice) ||
         (!gi.code_list.empty() &&
@@ -883,7 +868,7 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         for (auto& b : c->pods) b.release();
         c->nodes.release();
         dfree(c->d_dry); dfree(c->d_params);
-        dfree(c->d_gpair); dfree(c->d_node_code); dfree(c->d_code_list); dfree(c->d_slot_readers); dfree(c->d_gslot);
+        dfree(c->d_gpair); dfree(c->d_node_code); dfree(c->d_code_list); dfree(c->d_gslot);
         dfree(c->d_col_off); dfree(c->d_col_groups);
         for (int i = 0; i < MAX_STAGES; ++i)
             if (c->ev[i]) hipEventDestroy(c->ev[i]);
@@ -1427,11 +1412,11 @@ int32_t esc_decide(esc_ctx* c) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
     hipSetDevice(c->device);
-    HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_pwords, c->d_nwords,
-                          c->zero_copy ? c->h_dec_dev : c->d_dec, c->stream));
+    HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_pwords, c->d_nwords, c->d_dec,
+                          c->zero_copy ? c->h_cdec_dev : c->d_cdec, c->stream));
     if (!c->zero_copy)
-        HIP_TRY(hipMemcpyAsync(c->h_dec, c->d_dec, (size_t)c->gi.G * sizeof(esc_group_decision),
-                               hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)c->gi.G * sizeof(DecCompact), hipMemcpyDeviceToHost,
+                               c->stream));
     c->pending = true;
     return ESC_OK;
 }
@@ -1524,7 +1509,29 @@ int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* de
     int32_t rc = esc_sync(c);
     if (rc) return rc;
     const int32_t G = c->gi.G;
-    if (decisions) std::memcpy(decisions, c->h_dec, (size_t)G * sizeof(esc_group_decision));
+    if (decisions) {
+        // the compact records -> esc_group_decision (cached capacity: allNodes[0]'s allocatable
+        // when the group has nodes, else the state's, controller.go:207-211)
+        for (int32_t g = 0; g < G; ++g) {
+            const DecCompact& x = c->h_cdec[g];
+            esc_group_decision& d = decisions[g];
+            if (x.wide) {                                // delta / n_to_taint beyond int32
+                HIP_TRY(hipMemcpy(&d, c->d_dec + g, sizeof d, hipMemcpyDeviceToHost));
+                continue;
+            }
+            d.cpu_pct = x.cpu_pct;
+            d.mem_pct = x.mem_pct;
+            d.delta = x.delta;
+            d.n_to_taint = x.n_to_taint;
+            const GroupNode& gn = c->h_gnode[g];
+            d.cached_cpu_m = gn.first != INT64_MAX ? gn.first_cpu : c->params[g].cached_cpu;
+            d.cached_mem_b = gn.first != INT64_MAX ? gn.first_mem : c->params[g].cached_mem;
+            d.status = x.status;
+            d.branch = x.branch;
+            d.taint_status = x.taint_status;
+            d.reserved = 0;
+        }
+    }
     if (totals) {
         std::vector<int64_t> w((size_t)G * PW_K), nw((size_t)G * NW_K);
         HIP_TRY(hipMemcpy(w.data(), c->d_pwords, w.size() * 8, hipMemcpyDeviceToHost));

@@ -771,3 +771,23 @@ def test_rccl_step_world1_vs_c_oracle(esc, graph):
         check_against_c_oracle(tot, dec, otot, odf, odi)
     (sb, sc), (mb, mc) = ctx.exchange_buffers()
     assert sc == 5 * 10_000 and mc == 0 and mb is None
+
+
+def test_decision_beyond_int32_round_trips(esc):
+    """The decisions travel to the host as compact 32-B records (delta, n_to_taint as
+    int32); a scale-up from zero against a tiny cached capacity gives a delta beyond int32
+    (calcScaleUpDelta, util.go:21-31) and must come back exact through the full record."""
+    groups = [{"name": "a", "label_key": "k", "label_value": "v", "max_nodes": 100, "scale_up_pct": 70,
+               "taint_lower_pct": 40, "taint_upper_pct": 60},
+              {"name": "b", "label_key": "k", "label_value": "w", "max_nodes": 100, "scale_up_pct": 70}]
+    pods = [{"containers": [{"cpu": 1 << 30, "mem": 1 << 20}], "node_selector": {"k": "v"}} for _ in range(20)]
+    pods += [{"containers": [{"cpu": 500, "mem": 1000}], "node_selector": {"k": "w"}} for _ in range(5)]
+    states = [{"cached_cpu_m": 1, "cached_mem_b": 1}, {}]
+    ctx = esc.Context(groups)
+    ctx.load(*ctx.pack(pods, []))
+    tot, dec = ctx.decide_all(states)
+    for g in range(2):
+        L = O.scale_node_group(groups[g], states[g], pods, [])
+        assert int(dec["delta"][g]) == L["delta"] and esc._lib.BRANCHES[dec["branch"][g]] == L["branch"], (g, L)
+        assert (int(dec["cached_cpu_m"][g]), int(dec["cached_mem_b"][g])) == (L["cached_cpu_m"], L["cached_mem_b"])
+    assert int(dec["delta"][0]) > (1 << 31)
