@@ -13,6 +13,8 @@
  *                   (node_listers.go:33, pkg/controller/controller.go:120-154,
  *                   util.go:41-51), allNodes[0] (controller.go:208-211).  Exact sums in
  *                   __int128 (Quantity.Add's checked int64 add -> overflow flag).
+ *   orc_totals_par  orc_totals over n host threads (OpenMP): the optimised all-core
+ *                   "B-opt" CPU baseline of BASELINE.md §4.
  *   orc_ref_scan    the same totals computed the way the reference computes them: one
  *                   full scan of every pod per group (controller.go:416 loops groups,
  *                   each List() rescans everything) — the "port" CPU baseline.
@@ -38,6 +40,7 @@
  * Build: gcc -O2 -ffp-contract=off (oracle/Makefile).
  */
 #include <math.h>
+#include <omp.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -189,6 +192,81 @@ int orc_totals(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, cons
     pair_idx_free(&np);
     free(a);
     return 0;
+}
+
+/* The "B-opt" CPU baseline: orc_totals' single
+ * pass split over n_threads host threads (OpenMP), each with private per-group
+ * accumulators merged at the end.  Pod ranges start at record offsets found by a parallel
+ * count + prefix of the per-pod record counts.  Same outputs as orc_totals. */
+int orc_totals_par(int64_t n_pods, const uint32_t* flags, const uint32_t* cpu0, const int64_t* mem0,
+                   const uint32_t* pair0, const int64_t* xc_cpu, const int64_t* xc_mem, const uint32_t* xp,
+                   int64_t n_nodes, const uint32_t* nflags, const uint32_t* label0, const int64_t* ncpu,
+                   const int64_t* nmem, const uint32_t* xl, const int32_t* tn, const int32_t* tg, int64_t n_trk,
+                   int64_t node_lo, int64_t node_hi, int32_t G, int32_t default_group, const uint32_t* gpair,
+                   uint32_t n_gp, const uint8_t* dry, int32_t n_threads, int64_t* out) {
+    if (n_threads < 1) n_threads = 1;
+    const int T = n_threads;
+    Acc* acc = (Acc*)calloc((size_t)G * (size_t)T, sizeof(Acc));
+    uint64_t* oc0 = (uint64_t*)calloc((size_t)T + 1, sizeof(uint64_t));
+    uint64_t* op0 = (uint64_t*)calloc((size_t)T + 1, sizeof(uint64_t));
+    PairIdx pp, np;
+    if (!acc || !oc0 || !op0 || pair_idx(&pp, gpair, n_gp, G, default_group) || pair_idx(&np, gpair, n_gp, G, -1))
+        return -1;
+    for (int64_t k = 0; k < (int64_t)G * T; ++k) acc[k].first = -1;
+    int rc = 0;
+#pragma omp parallel num_threads(T)
+    {
+        const int t = omp_get_thread_num();
+        const int64_t lo = n_pods * t / T, hi = n_pods * (t + 1) / T;
+        uint64_t c = 0, q = 0;
+        for (int64_t p = lo; p < hi; ++p) { c += xctr(flags[p]); q += xpair(flags[p]); }
+        oc0[t + 1] = c;
+        op0[t + 1] = q;
+#pragma omp barrier
+#pragma omp single
+        for (int k = 0; k < T; ++k) { oc0[k + 1] += oc0[k]; op0[k + 1] += op0[k]; }
+        Acc* a = acc + (size_t)G * t;
+        uint64_t oc = oc0[t], op = op0[t];
+        for (int64_t p = lo; p < hi; ++p) {
+            const uint32_t f = flags[p];
+            if (f & PF_DS) { oc += xctr(f); op += xpair(f); continue; }
+            int64_t cpu, mem;
+            pod_request(f, cpu0[p], mem0[p], xc_cpu, xc_mem, &oc, &cpu, &mem);
+            if (default_group >= 0 && !(f & (PF_STATIC | PF_SEL | PF_AFF))) {
+                a[default_group].pcpu += cpu; a[default_group].pmem += mem; a[default_group].npod++;
+            }
+            const uint32_t nx = xpair(f);
+            for (uint32_t k = 0; k <= nx; ++k) {
+                const uint32_t pr = k == 0 ? pair0[p] : xp[op++];
+                for (int32_t g = first_group(&pp, pr); g >= 0; g = pp.nxt[g]) {
+                    a[g].pcpu += cpu; a[g].pmem += mem; a[g].npod++;
+                }
+            }
+        }
+        /* nodes: contiguous thread ranges, so the lowest thread with a member holds allNodes[0] */
+        const int64_t span = node_hi - node_lo;
+        node_pass(a, node_lo + span * t / T, node_lo + span * (t + 1) / T, nflags, label0, ncpu, nmem, xl, tn, tg,
+                  n_trk, dry, n_nodes, &np);
+#pragma omp barrier
+        /* merge: thread t owns groups [G*t/T, G*(t+1)/T) */
+        for (int32_t g = (int32_t)((int64_t)G * t / T); g < (int32_t)((int64_t)G * (t + 1) / T); ++g) {
+            Acc s = acc[g];
+            for (int k = 1; k < T; ++k) {
+                const Acc* b = &acc[(size_t)G * k + g];
+                s.pcpu += b->pcpu; s.pmem += b->pmem; s.ncpu += b->ncpu; s.nmem += b->nmem;
+                s.npod += b->npod; s.nunt += b->nunt; s.ntaint += b->ntaint; s.ncord += b->ncord;
+                if (s.first < 0) s.first = b->first;
+            }
+            acc[g] = s;
+        }
+    }
+    emit_out(acc, G, ncpu, nmem, out);
+    pair_idx_free(&pp);
+    pair_idx_free(&np);
+    free(acc);
+    free(oc0);
+    free(op0);
+    return rc;
 }
 
 /* Reference-shaped: every group rescans every pod and re-evaluates its filter and the

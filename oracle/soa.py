@@ -40,6 +40,7 @@ def lib():
             build()
         _lib = C.CDLL(LIB)
         _lib.orc_totals.restype = C.c_int
+        _lib.orc_totals_par.restype = C.c_int
         _lib.orc_ref_scan.restype = C.c_int
         _lib.orc_order.restype = C.c_int64
         _lib.orc_try_remove.restype = C.c_int64
@@ -77,8 +78,9 @@ TOT_FIELDS = ["pod_cpu_m", "pod_mem_b", "n_pods", "node_cpu_m", "node_mem_b", "n
 
 
 def totals(pods: dict, nodes: dict, groups: list[dict], node_lo: int = 0, node_hi: int | None = None,
-           reference_shaped: bool = False, g_range: tuple[int, int] | None = None) -> np.ndarray:
-    """int64 [G, 13] in esc_group_totals order."""
+           reference_shaped: bool = False, g_range: tuple[int, int] | None = None,
+           threads: int = 0) -> np.ndarray:
+    """int64 [G, 13] in esc_group_totals order.  threads > 0: orc_totals_par (OpenMP)."""
     t = group_tables(groups)
     G = t["G"]
     out = np.zeros((G, 13), np.int64)
@@ -93,6 +95,10 @@ def totals(pods: dict, nodes: dict, groups: list[dict], node_lo: int = 0, node_h
         lo, hi_g = g_range or (0, G)
         rc = lib().orc_ref_scan(*pa, *na, C.c_int32(G), C.c_int32(t["default"]), _p(t["gpair"], C.c_uint32),
                                 _p(t["dry"], C.c_uint8), C.c_int32(lo), C.c_int32(hi_g), _p(out, C.c_int64))
+    elif threads > 0:
+        rc = lib().orc_totals_par(*pa, *na, C.c_int64(node_lo), C.c_int64(hi), C.c_int32(G),
+                                  C.c_int32(t["default"]), _p(t["gpair"], C.c_uint32), C.c_uint32(t["n_gp"]),
+                                  _p(t["dry"], C.c_uint8), C.c_int32(threads), _p(out, C.c_int64))
     else:
         rc = lib().orc_totals(*pa, *na, C.c_int64(node_lo), C.c_int64(hi), C.c_int32(G), C.c_int32(t["default"]),
                               _p(t["gpair"], C.c_uint32), C.c_uint32(t["n_gp"]), _p(t["dry"], C.c_uint8),
