@@ -10,7 +10,9 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libescalator_hip.so")
+# ESC_LIB_PATH: an alternative build of the same library (the host-sanitizer build of
+# scripts/asan_check.sh); the default is the in-tree gfx950 build.
+LIB_PATH = os.environ.get("ESC_LIB_PATH") or os.path.join(HERE, "libescalator_hip.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "escalator_hip.h")
 
 ESC_OK = 0
@@ -201,10 +203,11 @@ def load():
         # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64, so when torch
         # is installed it is loaded first and the library binds to that runtime (loading
         # /opt/rocm's first and torch's second leaves two runtimes that disagree on devices).
-        try:
-            import torch  # noqa: F401
-        except ImportError:
-            pass
+        if not os.environ.get("ESC_NO_TORCH_PRELOAD"):   # sanitizer runs keep torch out
+            try:
+                import torch  # noqa: F401
+            except ImportError:
+                pass
         lib = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             f = getattr(lib, name)

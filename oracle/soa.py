@@ -19,7 +19,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+LIB = os.environ.get("ESC_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 NONE = 0xFFFFFFFF
 BRANCH_NAMES = ["empty", "gate", "below_min", "pct_err", "locked", "fast_down", "slow_down", "scale_up", "none"]
 STATUS_ERR = {0: None, 1: "node count less than the minimum", 2: "node count larger than the maximum",
