@@ -281,6 +281,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--pods", type=int, default=None, help="override the config's pod count (experiments)")
+    ap.add_argument("--no-order", action="store_true",
+                    help="leave the K5 ordering out of the decision (ablation; BASELINE.md §2 includes it)")
     args = ap.parse_args()
 
     if args.config == 5:
@@ -308,6 +310,8 @@ def main():
     ctx = esc.Context(s, device=local, rank=rank, world=world)
     ctx.load_synth(s, pod_offset=lo, node_lo=nlo, node_hi=nhi, replicas=replicas)
     ctx.set_state(s.states)
+    ctx.set_order_in_step(not args.no_order)          # oldest-first ordering is part of a decision
+    n_memb = ctx.order_info()[0]
     pod_b, node_b = stream_bytes(ctx, s, rank, world)
     log("rank %d: shard pods [%d,%d) nodes [%d,%d), %.1f MB x %d replicas, setup %.1fs" %
         (rank, lo, hi, nlo, nhi, shard_bytes / 1e6, replicas, time.time() - t0))
@@ -357,6 +361,9 @@ def main():
         stages.append(st)
     ctx.set_timing(False)
     k1_ms = float(np.mean(k1))
+    stage_names = (["k_pod_reduce", "k_node_pieces", "k_fold_decide"] +
+                   (["d2h"] if os.environ.get("ESC_NO_ZEROCOPY", "0") not in ("", "0") else []) +
+                   ([] if args.no_order else ["k_order"]))
     stage_mean = np.mean(np.array(stages), axis=0)
 
     parity = None
@@ -374,7 +381,13 @@ def main():
             ok &= np.array_equal(dec["cpu_pct"].view(np.uint64), odf[:, 0].view(np.uint64))
             ok &= np.array_equal(dec["mem_pct"].view(np.uint64), odf[:, 1].view(np.uint64))
             ok &= np.array_equal(dec["delta"], odi[:, 0])
-            parity = ("bit-exact vs C oracle, all %d groups%s" % (G, "" if world == 1 else
+            if not args.no_order:                 # this rank's node range, three groups, both orders
+                for g in (0, G // 2, G - 1):
+                    for w in (0, 1):
+                        ok &= np.array_equal(ctx.group_order(g, w),
+                                             soa.order(full.nodes(), full.groups, g, w, node_lo=nlo, node_hi=nhi))
+            parity = ("bit-exact vs C oracle, all %d groups%s%s" % (
+                      G, "" if args.no_order else " (orderings: groups 0, G/2, G-1, both orders)", "" if world == 1 else
                       " (rank 0 after the RCCL exchange, oracle over the unsharded snapshot)")
                       if ok else "MISMATCH vs C oracle")
 
@@ -387,7 +400,8 @@ def main():
     achieved = algo / (k1_ms * 1e-3) / 1e9
     records = P + N
     value = records * args.steps / elapsed
-    decision_bytes = (pod_b + node_b) * world         # shards are near-equal; rank 0's x N
+    # shards are near-equal: rank 0's bytes x N (pods, the node index, the orderings)
+    decision_bytes = (pod_b + node_b + (0 if args.no_order else n_memb * 16)) * world
     # PMC passes are taken on the single-GPU config-4 run (scripts/pmc_job.sh); a shard's
     # K1 launch moves other bytes, so the committed figure applies to N = 1 only
     traffic = pmc_traffic("k_pod_reduce") if world == 1 and args.config == 4 else None
@@ -414,8 +428,10 @@ def main():
         "node_bytes_per_decision": node_b,
         # stages timed in order on one stream (timing mode); "d2h" only when the decisions
         # are copied rather than written to pinned host memory by K3 (zero-copy)
-        "stage_ms": {k: float(v) for k, v in zip(["k_pod_reduce", "k_node_pieces", "k_fold_decide", "d2h"], stage_mean)
-                     if v > 0} if world == 1 else None,
+        "stage_ms": {k: float(v) for k, v in zip(stage_names, stage_mean) if v > 0} if world == 1 else None,
+        "ordering": None if args.no_order else {
+            "kernels": "k_ord_count + k_ord_scatter on the side stream beside K1 (esc_set_order_in_step)",
+            "memberships": n_memb, "algorithmic_bytes": n_memb * 16},
         "parity": parity,
     }
     if world == 1 and not args.no_cpu_baseline:

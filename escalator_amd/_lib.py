@@ -168,6 +168,7 @@ _SIGS = {
     "esc_set_timing": (i32, [VP, i32]),
     "esc_stage_times": (i32, [VP, P(dbl), i32]),
     "esc_sort_nodes": (i32, [VP]),
+    "esc_set_order_in_step": (i32, [VP, i32]),
     "esc_build_age_index": (i32, [VP]),
     "esc_order_info": (i32, [VP, P(i64), P(i32)]),
     "esc_group_order": (i32, [VP, i32, i32, P(i64), i64, P(i64)]),

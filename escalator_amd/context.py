@@ -362,6 +362,10 @@ class Context:
     def sort_nodes(self):
         L.check(self.lib.esc_sort_nodes(self.handle), "esc_sort_nodes")
 
+    def set_order_in_step(self, on: bool = True):
+        """Run the K5 ordering inside every decision (beside K1, in the step's graph)."""
+        L.check(self.lib.esc_set_order_in_step(self.handle, int(bool(on))), "esc_set_order_in_step")
+
     def order_info(self) -> tuple[int, int]:
         """(memberships of the node range, creation-key bits of the age index)."""
         n, b = C.c_int64(), C.c_int32()

@@ -27,6 +27,10 @@
 
 #include "esc_kernels.h"
 
+#ifndef ESC_PART
+#define ESC_PART 0
+#endif
+
 namespace esc {
 
 namespace {
@@ -612,6 +616,72 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     }
 }
 
+// ============================================================ K1 launchers by part
+// The K1 template is instantiated once per (variant, 16 record shapes): the production
+// variant in part 0 (with every other kernel), the exact alternatives (1, 2, 5, 6) in
+// part 1 and the timing-only ablations in part 2, each its own translation unit so the
+// build compiles them in parallel (Makefile; part 2 only with ABLATIONS=1).
+#define ESC_K1(T, A, DC) ESC_K1D(T, A, DC, 0)
+#define ESC_K1D(T, A, DC, D) ESC_K1W(T, A, DC, D, 0)
+#define ESC_K1W(T, A, DC, D, W)                                                                       \
+    hipLaunchKernelGGL((k_pod_reduce<T, A, DC, D, W>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, \
+                       wide, ticket, cap)
+#define ESC_K1_ARGS const PodDev &p, const GroupDev &g, int32_t g0, int32_t gw, int nblk, int variant, uint64_t *part, \
+                    int64_t *wide, uint32_t *ticket, int cap, hipStream_t st
+hipError_t launch_pod_reduce_alt(ESC_K1_ARGS);
+hipError_t launch_pod_reduce_ablation(ESC_K1_ARGS) __attribute__((weak));
+
+#if ESC_PART == 0
+bool k1_dynamic(int variant) { return variant == 5; }
+
+hipError_t launch_pod_reduce(ESC_K1_ARGS) {
+    const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
+    switch (variant) {
+        case 0: ESC_K1(512, 0, 3); break;
+        case 1: case 2: case 5: case 6:
+            return launch_pod_reduce_alt(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, st);
+        default:                                  // timing-only ablations (ABLATIONS=1 build)
+            if (!launch_pod_reduce_ablation) return hipErrorInvalidValue;
+            return launch_pod_reduce_ablation(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, st);
+    }
+    return hipGetLastError();
+}
+#elif ESC_PART == 1
+hipError_t launch_pod_reduce_alt(ESC_K1_ARGS) {
+    const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
+    switch (variant) {
+        case 6: ESC_K1W(512, 0, 3, 0, 1); break;   // per-wave shares of the K weight
+        case 5: ESC_K1D(512, 0, 3, 1); break;      // dynamic shares (measured slower)
+        case 1: ESC_K1(512, 0, 2); break;
+        case 2: ESC_K1(1024, 0, 3); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+#elif ESC_PART == 2
+hipError_t launch_pod_reduce_ablation(ESC_K1_ARGS) {
+    const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
+    switch (variant) {
+        case 14: ESC_K1W(512, 4 | 32, 3, 0, 1); break;   // per-wave shares, K tiles, loads only
+        case 3: ESC_K1(512, 64, 3); break;       // <= 2 K tiles in flight per wave
+        case 4: ESC_K1(512, 128, 3); break;      // <= 3 K tiles in flight per wave
+        // Timing-only ablations (wrong results; scripts/k1_variants.py), see k_pod_reduce.
+        case 9: ESC_K1(512, 1, 3); break;        // LDS atomics replaced by a sink
+        case 10: ESC_K1(512, 2, 3); break;       // C tiles only
+        case 11: ESC_K1(512, 4, 3); break;       // K tiles only
+        case 12: ESC_K1(512, 4 | 32, 3); break;  // K tiles, loads only
+        case 13: ESC_K1(512, 2 | 32, 3); break;  // C tiles, loads only
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+#endif
+#undef ESC_K1
+#undef ESC_K1D
+#undef ESC_K1W
+#undef ESC_K1_ARGS
+
+#if ESC_PART == 0
 // C tiles with more than 128 extra records of a kind (listed by the host at load):
 // one wave per tile, records read from memory, exact wide accumulation.
 __global__ __launch_bounds__(64) void k_pod_bigtiles(PodDev P, GroupDev G, const uint32_t* __restrict__ tiles,
@@ -1877,38 +1947,6 @@ __global__ __launch_bounds__(64) void k_try_remove(NodeDev N, GroupDev G, Remova
 }
 
 // ===================================================================== launchers
-bool k1_dynamic(int variant) { return variant == 5; }
-
-hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
-                             uint64_t* part, int64_t* wide, uint32_t* ticket, int cap, hipStream_t st) {
-    const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
-#define ESC_K1(T, A, DC) ESC_K1D(T, A, DC, 0)
-#define ESC_K1D(T, A, DC, D) ESC_K1W(T, A, DC, D, 0)
-#define ESC_K1W(T, A, DC, D, W)                                                                       \
-    hipLaunchKernelGGL((k_pod_reduce<T, A, DC, D, W>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, \
-                       wide, ticket, cap)
-    switch (variant) {
-        case 6: ESC_K1W(512, 0, 3, 0, 1); break;   // per-wave shares of the K weight
-        case 14: ESC_K1W(512, 4 | 32, 3, 0, 1); break;   // per-wave shares, K tiles, loads only
-        case 5: ESC_K1D(512, 0, 3, 1); break;   // dynamic shares (measured slower)
-        case 1: ESC_K1(512, 0, 2); break;
-        case 2: ESC_K1(1024, 0, 3); break;
-        case 3: ESC_K1(512, 64, 3); break;       // <= 2 K tiles in flight per wave
-        case 4: ESC_K1(512, 128, 3); break;      // <= 3 K tiles in flight per wave
-        // Timing-only ablations (wrong results; scripts/k1_variants.py), see k_pod_reduce.
-        case 9: ESC_K1(512, 1, 3); break;        // LDS atomics replaced by a sink
-        case 10: ESC_K1(512, 2, 3); break;       // C tiles only
-        case 11: ESC_K1(512, 4, 3); break;       // K tiles only
-        case 12: ESC_K1(512, 4 | 32, 3); break;  // K tiles, loads only
-        case 13: ESC_K1(512, 2 | 32, 3); break;  // C tiles, loads only
-        default: ESC_K1(512, 0, 3); break;
-    }
-#undef ESC_K1
-#undef ESC_K1D
-#undef ESC_K1W
-    return hipGetLastError();
-}
-
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
                                int64_t* wide, hipStream_t st) {
     if (n_big <= 0) return hipSuccess;
@@ -2109,5 +2147,7 @@ hipError_t launch_order(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chu
                            grp_off, ccnt, vals, seg);
     return hipGetLastError();
 }
+
+#endif  // ESC_PART == 0
 
 }  // namespace esc

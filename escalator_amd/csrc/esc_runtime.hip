@@ -174,6 +174,7 @@ struct esc_ctx {
     DecCompact* h_cdec_dev = nullptr;                         // device view of h_cdec (zero-copy)
     bool zero_copy = true;                                    // K3/K4 write compact decisions to h_cdec
     bool fork_nodes = true;                                   // K2 on the side stream, beside K1
+    bool order_in_step = false;                               // K5 ordering inside every decision
     bool want_metrics = false;                                // K4 also writes the gauges
     esc_group_metrics* d_metrics = nullptr;
     hipStream_t side = nullptr;
@@ -333,6 +334,13 @@ void drop_graphs(esc_ctx* c) {
 }
 
 int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out);
+
+// K5 per-decision ordering (classify + stable split of every group's age-ordered
+// memberships) on stream st; the two-pass kernels (the fused one needs its ticket reset).
+hipError_t enqueue_order(esc_ctx* c, hipStream_t st) {
+    return launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node, c->d_g_grp,
+                        c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase, c->d_ovals[0], c->d_seg, st);
+}
 
 // Replays (capturing on first use) the per-replica graph of enqueue_step(r, decide, decide)
 // on the context's stream: one launch instead of the step's kernels, events and waits.
@@ -692,6 +700,9 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     if (fork) {
         HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, c->side));
         HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, c->side));
+        // the orderings (taintOldestN / untaintNewestN inputs) depend on the node flags
+        // only: they run on the side stream too, beside K1
+        if (c->order_in_step) HIP_TRY(enqueue_order(c, c->side));
         HIP_TRY(hipEventRecord(c->ev_join, c->side));
         HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
     } else {
@@ -713,6 +724,10 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     if (copy_out && !c->zero_copy) {
         HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)g.G * sizeof(DecCompact), hipMemcpyDeviceToHost, st));
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    }
+    if (c->order_in_step && !fork) {                  // in order (timing mode): its own stage, last
+        HIP_TRY(enqueue_order(c, st));
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     }
     c->n_stage_ev = e;
@@ -1360,6 +1375,8 @@ int32_t esc_reduce(esc_ctx* c) {
     const int r = c->cur;
     c->cur = (c->cur + 1) % (int)c->pods.size();
     c->pending = true;
+    c->fused_ran = false;
+    if (c->order_in_step) { c->order_src = 0; c->sorted = true; }
     if (!c->use_graph || c->timing) return enqueue_step(c, r, false, false);
     return replay_step(c, c->rgraphs, r, false);
 }
@@ -1431,8 +1448,17 @@ int32_t esc_run(esc_ctx* c) {
     c->cur = (c->cur + 1) % nrep;
     c->pending = true;
     (void)nrep;
+    c->fused_ran = false;
+    if (c->order_in_step) { c->order_src = 0; c->sorted = true; }
     if (!c->use_graph || c->timing) return enqueue_step(c, r, true, true);
     return replay_step(c, c->graphs, r, true);
+}
+
+int32_t esc_set_order_in_step(esc_ctx* c, int32_t enable) {
+    if (!c) return ESC_E_INVAL;
+    c->order_in_step = enable != 0;
+    drop_graphs(c);
+    return ESC_OK;
 }
 
 // ------------------------------------------------- RCCL exchange (§8e) inside the library

@@ -459,6 +459,12 @@ int32_t esc_removal_nodes(esc_ctx* ctx, int32_t group, int64_t* idx_out, int64_t
  * segment is then oldest-first and its tainted one, read backwards, newest-first.
  * esc_build_age_index rebuilds the index (snapshot ingestion; exposed for measurement). */
 int32_t esc_sort_nodes(esc_ctx* ctx);
+/* Include the per-decision ordering in every decision (esc_run / esc_reduce / esc_step):
+ * it runs on the side stream beside K1 (it reads node flags only) and is captured in the
+ * decision's graph; esc_group_order is then valid after each decision without a separate
+ * esc_sort_nodes (one decision = membership, sums, percentages, deltas
+ * and oldest-first ordering). */
+int32_t esc_set_order_in_step(esc_ctx* ctx, int32_t enable);
 int32_t esc_build_age_index(esc_ctx* ctx);
 /* Size of the ordering problem: memberships of the node range and the bit width of the
  * creation-offset keys the index sorts on. */

@@ -272,6 +272,43 @@ def test_synthetic_sort_vs_c_oracle(esc, fused, monkeypatch):
     assert ctx.group_order(g, 1).tolist() == sorted((j for j in members if j in trk), key=lambda j: (-int(t[j]), j))
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_order_in_step_vs_c_oracle(esc, graph):
+    """esc_set_order_in_step: the K5 ordering inside every decision (side stream beside K1,
+    captured in the decision graph) — orders valid after esc_run with no esc_sort_nodes,
+    also after node events patch the flags, and the decision itself unchanged."""
+    s = esc.Synth(300_000, 200_000, 100, config=5, seed=0xE5CA1A7E00000005)
+    pods, nodes = s.pods(), s.nodes()
+    ctx = esc.Context(s)
+    ctx.load_synth(s, replicas=2)
+    ctx.use_graph(graph)
+    ctx.set_state(s.states)
+    ctx.set_order_in_step(True)
+    otot = soa.totals(pods, nodes, s.groups)
+    odf, odi = soa.decide(s.groups, s.states, otot)
+    for _ in range(3):
+        ctx.run()
+        tot, dec = ctx.results()
+        check_against_c_oracle(tot, dec, otot, odf, odi)
+    full = soa.order_all(nodes, s.groups)
+    for g in range(100):
+        for which in (0, 1):
+            assert np.array_equal(ctx.group_order(g, which), full[(g, which)]), (g, which)
+    # node events (cordon / taint flips) then one more decision: orders follow the flags
+    rng = np.random.default_rng(5)
+    ids = rng.choice(len(nodes["flags"]), 2000, replace=False).astype(np.int64)
+    flags = nodes["flags"].copy()
+    flags[ids] ^= rng.integers(1, 4, len(ids)).astype(np.uint32) & 3
+    ctx.nodes_update(ids, flags[ids], nodes["cpu"][ids], nodes["mem"][ids])
+    n2 = dict(nodes, flags=flags)
+    ctx.run()
+    ctx.results()
+    full = soa.order_all(n2, s.groups)
+    for g in range(0, 100, 3):
+        for which in (0, 1):
+            assert np.array_equal(ctx.group_order(g, which), full[(g, which)]), (g, which)
+
+
 def _members_oldest(nodes, groups, g):
     """All members of dry group g, oldest first (ties by index): the oracle's two lists merged."""
     both = list(soa.order(nodes, groups, g, 0)) + list(soa.order(nodes, groups, g, 1))
