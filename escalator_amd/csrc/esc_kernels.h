@@ -220,6 +220,17 @@ struct OrdChunk {               // K5 per-decision chunk: memberships [start, en
     uint32_t start, end, group, pad;
 };
 constexpr int ORD_CHUNK = 4096;   // memberships per K5 chunk (three-pass default)
+// Group-order padding slot of group g: g | MEMB_PAD (class 3, skipped).  Every group owns a
+// region of the group-order arrays: its memberships oldest first, then padding (the round-up
+// to whole 16-B quads and the spare slots node additions take).
+constexpr uint32_t MEMB_PAD = 0x80000000u;
+// Small groups (region <= ORD_CHUNK) are packed whole into chunks ordered in one pass.
+hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* grp_off,
+                               const uint32_t* g_node, const uint32_t* g_grp, const uint32_t* g_flags,
+                               uint32_t* vals, int64_t* seg, hipStream_t st);
+// Fills the padding of every group's region (after its `len` memberships) with g | MEMB_PAD.
+hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_grp,
+                             uint32_t* g_node, uint32_t* g_flags, hipStream_t st);
 hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
                               const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
                               const uint32_t* g_flags, unsigned long long* ticket, unsigned long long* status,

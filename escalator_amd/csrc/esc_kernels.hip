@@ -1477,7 +1477,7 @@ constexpr int ORD_BLOCK = 256, ORD_WAVES = ORD_BLOCK / 64;
 // Membership flags: a dry group's membership has the tracker bit resolved for its group
 // (k_memb_expand), so no per-decision lookup is needed.
 __device__ __forceinline__ uint32_t ord_class(const NodeDev&, uint32_t, uint32_t grp, uint32_t f) {
-    if (grp == NONE) return 3u;                                                  // padding
+    if ((grp & MEMB_PAD) || (f & ESC_NF_ABSENT)) return 3u;                      // padding, deleted node
     if (mdry(grp)) return (f & ESC_NF_TRACKED) ? 1u : 0u;
     if (f & ESC_NF_UNSCHED) return 2u;
     return (f & ESC_NF_TAINTED) ? 1u : 0u;
@@ -1625,6 +1625,144 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __res
     const uint32_t b0 = s_base[0], b1 = s_base[1];
     for (uint32_t i = threadIdx.x; i < n0 + n1; i += ORD_BLOCK)
         vals[i < n0 ? b0 + i : b1 + (i - n0)] = stage[i];
+}
+
+// Small groups packed whole into one chunk (<= ORD_CHUNK memberships, regions start on
+// quads): one pass, no cross-chunk prefix.  Classes are counted by one packed 64-bit block
+// scan (class 0 | class 1 << 21 | class 2 << 42) in membership order; a group's base is the
+// scan value at its region's first quad (hp, indexed by quad), its class totals come from
+// its region's last quad (tt), and the output segment of group g is [grp_off[g], ...):
+// class 0 then class 1, i.e. the chunk's own slots — so the nodes are staged in LDS and the
+// chunk written back coalesced.  The last quad of each group writes its segment bounds.
+__device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long y = __shfl_up(v, d, 64);
+        if (lane >= d) v += y;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdChunk* __restrict__ chunks,
+                                                          const uint32_t* __restrict__ grp_off,
+                                                          const uint32_t* __restrict__ g_node,
+                                                          const uint32_t* __restrict__ g_grp,
+                                                          const uint32_t* __restrict__ g_flags,
+                                                          uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
+    constexpr int STEPS = ORD_CHUNK / (4 * ORD_BLOCK);
+    constexpr int NQ = ORD_CHUNK / 4;
+    constexpr int C1 = 21, C2 = 42;
+    constexpr unsigned long long M = (1ull << C1) - 1;
+    __shared__ unsigned long long wt[STEPS][ORD_WAVES];
+    __shared__ unsigned long long hp[NQ];                // scan value at each group's first quad
+    __shared__ unsigned long long tt[NQ];                // each group's totals, at its first quad
+    __shared__ uint32_t stage[ORD_CHUNK];
+    const OrdChunk ch = chunks[blockIdx.x];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint4 nd[STEPS], gr[STEPS], fl[STEPS];
+    uint32_t grp[STEPS];
+    bool ok[STEPS];
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {
+        const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
+        ok[st] = b < ch.end;
+        const uint32_t bb = ok[st] ? b : ch.start;
+        nd[st] = ld4(g_node + bb);
+        gr[st] = ld4(g_grp + bb);
+        fl[st] = ld4(g_flags + bb);
+    }
+    uint32_t cls[STEPS];
+    unsigned long long ex[STEPS];
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {
+        grp[st] = gr[st].x;                              // a quad lies in one group's region
+        unsigned long long v = 0;
+        cls[st] = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = ok[st] ? ord_class(N, lane4(nd[st], j), lane4(gr[st], j), lane4(fl[st], j)) : 3u;
+            cls[st] |= k << (8 * j);
+            v += k == 0 ? 1ull : (k == 1 ? (1ull << C1) : (k == 2 ? (1ull << C2) : 0ull));
+        }
+        const unsigned long long inc = wave_incl_scan64(v);
+        if (lane == 63) wt[st][wid] = inc;
+        ex[st] = inc - v;
+    }
+    __syncthreads();
+    unsigned long long tot = 0, pre[STEPS];
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st)
+#pragma unroll
+        for (int w = 0; w < ORD_WAVES; ++w) {
+            if (w == wid) pre[st] = tot;
+            tot += wt[st][w];
+        }
+    // group heads publish their base; every quad then finds its group's head by address
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {
+        ex[st] += pre[st];                               // exclusive scan value of this quad
+        const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
+        if (ok[st] && b == grp_off[mg(grp[st])]) hp[(b - ch.start) >> 2] = ex[st];
+    }
+    __syncthreads();
+    uint32_t hq[STEPS];
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {
+        const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
+        if (!ok[st]) continue;
+        const uint32_t g = mg(grp[st]);
+        hq[st] = (grp_off[g] - ch.start) >> 2;
+        const uint32_t end = grp_off[g + 1];
+        if (b + 4 == end) {                              // the group's last quad: totals + bounds
+            unsigned long long inc = ex[st];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t k = (cls[st] >> (8 * j)) & 0xFF;
+                inc += k == 0 ? 1ull : (k == 1 ? (1ull << C1) : (k == 2 ? (1ull << C2) : 0ull));
+            }
+            const unsigned long long t = inc - hp[hq[st]];
+            tt[hq[st]] = t;
+            const int64_t s0 = grp_off[g], t0 = (int64_t)(t & M), t1 = (int64_t)((t >> C1) & M), t2 = (int64_t)(t >> C2);
+            seg[4 * (int64_t)g + 0] = s0;
+            seg[4 * (int64_t)g + 1] = s0 + t0;
+            seg[4 * (int64_t)g + 2] = s0 + t0 + t1;
+            seg[4 * (int64_t)g + 3] = s0 + t0 + t1 + t2;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {
+        if (!ok[st]) continue;
+        const unsigned long long base = hp[hq[st]], t = tt[hq[st]];
+        const uint32_t s0 = (hq[st] << 2);               // the group's first slot, chunk-relative
+        const uint32_t t0 = (uint32_t)(t & M);
+        uint32_t r0 = (uint32_t)((ex[st] - base) & M), r1 = (uint32_t)(((ex[st] - base) >> C1) & M);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t k = (cls[st] >> (8 * j)) & 0xFF;
+            if (k == 0) stage[s0 + r0++] = lane4(nd[st], j);
+            else if (k == 1) stage[s0 + t0 + r1++] = lane4(nd[st], j);
+        }
+    }
+    __syncthreads();
+    const uint32_t n = ch.end - ch.start;
+    for (uint32_t i = 4 * threadIdx.x; i < n; i += 4 * ORD_BLOCK)
+        *reinterpret_cast<uint4*>(vals + ch.start + i) = *reinterpret_cast<const uint4*>(stage + i);
+}
+
+// Region padding: g | MEMB_PAD after each group's memberships (node 0, flags 0).
+__global__ __launch_bounds__(256) void k_region_pad(const uint32_t* __restrict__ pstart,
+                                                    const uint32_t* __restrict__ plen, int32_t G,
+                                                    uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_node,
+                                                    uint32_t* __restrict__ g_flags) {
+    const int32_t g = blockIdx.x;
+    if (g >= G) return;
+    for (uint32_t i = pstart[g] + plen[g] + threadIdx.x; i < pstart[g + 1]; i += blockDim.x) {
+        g_grp[i] = (uint32_t)g | MEMB_PAD;
+        g_node[i] = 0;
+        g_flags[i] = 0;
+    }
 }
 
 // Fused single pass (default): the per-decision order in one launch.  A chunk's block
@@ -2132,6 +2270,22 @@ hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t
     else
         hipLaunchKernelGGL(k_ord_fused<256>, dim3((unsigned)n_chunks), dim3(256), 0, st, nd, chunks, n_chunks,
                            gch_off, grp_off, g_node, g_grp, g_flags, ticket, status, vals, seg, err, ablate);
+    return hipGetLastError();
+}
+
+hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* grp_off,
+                               const uint32_t* g_node, const uint32_t* g_grp, const uint32_t* g_flags,
+                               uint32_t* vals, int64_t* seg, hipStream_t st) {
+    if (n_chunks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ord_packed, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, grp_off, g_node,
+                       g_grp, g_flags, vals, seg);
+    return hipGetLastError();
+}
+
+hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_grp,
+                             uint32_t* g_node, uint32_t* g_flags, hipStream_t st) {
+    if (G <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_region_pad, dim3((unsigned)G), dim3(256), 0, st, pstart, plen, G, g_grp, g_node, g_flags);
     return hipGetLastError();
 }
 

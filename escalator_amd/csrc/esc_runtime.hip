@@ -208,7 +208,12 @@ struct esc_ctx {
     // group order of the memberships (per-decision 3-way split by class inside each group)
     uint32_t *d_gperm = nullptr, *d_g_node = nullptr, *d_g_grp = nullptr, *d_g_flags = nullptr;
     uint32_t *d_grp_off = nullptr, *d_gch_off = nullptr, *d_ccnt = nullptr, *d_cbase = nullptr;
-    uint32_t *d_gpos = nullptr, *d_pstart = nullptr, *d_cls4 = nullptr;
+    uint32_t *d_gpos = nullptr, *d_pstart = nullptr, *d_cls4 = nullptr, *d_plen = nullptr;
+    uint32_t* d_ord = nullptr;                                // K5 output, in the group regions
+    OrdChunk* d_pchunks = nullptr;                            // packed chunks of small groups
+    int64_t n_pchunks = 0;
+    std::vector<uint32_t> h_pstart, h_plen;                   // group regions: start, memberships
+    std::vector<uint32_t> h_gch_off;                          // group -> its split chunks (big groups)
     int64_t n_gpad = 0;                                       // padded group-order length
     OrdChunk* d_chunks = nullptr;
     int64_t n_chunks = 0, max_chunk = 0;
@@ -338,8 +343,12 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out);
 // K5 per-decision ordering (classify + stable split of every group's age-ordered
 // memberships) on stream st; the two-pass kernels (the fused one needs its ticket reset).
 hipError_t enqueue_order(esc_ctx* c, hipStream_t st) {
-    return launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node, c->d_g_grp,
-                        c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase, c->d_ovals[0], c->d_seg, st);
+    const hipError_t e = launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node,
+                                      c->d_g_grp, c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase,
+                                      c->d_ord, c->d_seg, st);
+    if (e != hipSuccess) return e;
+    return launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->d_grp_off, c->d_g_node, c->d_g_grp,
+                               c->d_g_flags, c->d_ord, c->d_seg, st);
 }
 
 // Replays (capturing on first use) the per-replica graph of enqueue_step(r, decide, decide)
@@ -392,7 +401,8 @@ void release_sort(esc_ctx* c) {
     dfree(c->d_gperm); dfree(c->d_g_node); dfree(c->d_g_grp); dfree(c->d_g_flags);
     dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks);
     dfree(c->d_oticket); dfree(c->d_ostat); dfree(c->d_oerr);
-    dfree(c->d_gpos); dfree(c->d_pstart); dfree(c->d_cls4);
+    dfree(c->d_gpos); dfree(c->d_pstart); dfree(c->d_cls4); dfree(c->d_plen); dfree(c->d_ord); dfree(c->d_pchunks);
+    c->n_pchunks = 0;
     c->n_chunks = 0;
     c->n_gpad = 0;
     dfree(c->d_hist); dfree(c->d_tot); dfree(c->d_cnt); dfree(c->d_total); dfree(c->d_seg);
@@ -456,45 +466,76 @@ int32_t build_age_index(esc_ctx* c) {
     if (c->n_memb) HIP_TRY(hipMemcpyAsync(starts.data(), c->d_seg, starts.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     starts[g.G] = c->n_memb;
-    std::vector<uint32_t> grp_off(g.G + 1), gch_off(g.G + 1), pstart(g.G + 1, 0);
-    std::vector<OrdChunk> chunks;
+    // every group's region: its memberships (oldest first), then padding to whole quads plus
+    // the spare slots node additions take (esc_set_spare); the per-decision output uses the
+    // same positions (grp_off = region starts)
+    std::vector<uint32_t> gch_off(g.G + 1), pstart(g.G + 1, 0), plen(std::max<int32_t>(g.G, 1), 0);
     for (int32_t q = 0; q < g.G; ++q) {
         const int64_t len = starts[q + 1] - starts[q];
-        pstart[q + 1] = pstart[q] + (uint32_t)((len + 3) & ~(int64_t)3);
-        grp_off[q] = (uint32_t)starts[q];
-        gch_off[q] = (uint32_t)chunks.size();
-        for (int64_t a = 0; a < len; a += c->ord_chunk)
-            chunks.push_back({pstart[q] + (uint32_t)a, pstart[q] + (uint32_t)std::min<int64_t>(len, a + c->ord_chunk),
-                              (uint32_t)q, 0u});
+        const int64_t spare = c->spare_frac > 0 ? (int64_t)std::ceil((double)len * c->spare_frac) + 4 : 0;
+        plen[q] = (uint32_t)len;
+        const int64_t reg = (len + spare + 3) & ~(int64_t)3;
+        if ((int64_t)pstart[q] + reg >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
+        pstart[q + 1] = pstart[q] + (uint32_t)reg;
     }
-    grp_off[g.G] = (uint32_t)c->n_memb;
+    // chunks: a group whose region exceeds ORD_CHUNK is split (two-pass or fused kernels,
+    // chunk prefix across the group); smaller groups are packed whole, several per chunk,
+    // and ordered in one pass (k_ord_packed)
+    std::vector<OrdChunk> chunks, pchunks;
+    uint32_t pk_lo = 0, pk_hi = 0;
+    auto flush_packed = [&]() {
+        if (pk_hi > pk_lo) pchunks.push_back({pk_lo, pk_hi, NONE, 1u});
+        pk_lo = pk_hi;
+    };
+    for (int32_t q = 0; q < g.G; ++q) {
+        const uint32_t reg = pstart[q + 1] - pstart[q];
+        gch_off[q] = (uint32_t)chunks.size();
+        if (reg == 0) continue;
+        if (reg > (uint32_t)ORD_CHUNK) {
+            flush_packed();
+            pk_lo = pk_hi = pstart[q + 1];
+            for (int64_t a = 0; a < reg; a += c->ord_chunk)
+                chunks.push_back({pstart[q] + (uint32_t)a, pstart[q] + (uint32_t)std::min<int64_t>(reg, a + c->ord_chunk),
+                                  (uint32_t)q, 0u});
+            continue;
+        }
+        if (pk_hi - pk_lo + reg > (uint32_t)ORD_CHUNK) flush_packed();
+        if (pk_hi == pk_lo) pk_lo = pk_hi = pstart[q];
+        pk_hi = pstart[q + 1];
+    }
+    flush_packed();
+    gch_off[g.G] = (uint32_t)chunks.size();
     c->fused_fits = true;
     c->max_chunk = 0;
     for (int32_t q = 0; q < g.G; ++q) {
-        if (starts[q + 1] - starts[q] >= ((int64_t)1 << 27)) c->fused_fits = false;
-        c->max_chunk = std::max<int64_t>(c->max_chunk, std::min<int64_t>(starts[q + 1] - starts[q], c->ord_chunk));
+        if (pstart[q + 1] - pstart[q] >= (1u << 27)) c->fused_fits = false;
+        if (gch_off[q + 1] > gch_off[q])
+            c->max_chunk = std::max<int64_t>(c->max_chunk, std::min<int64_t>(pstart[q + 1] - pstart[q], c->ord_chunk));
     }
-    gch_off[g.G] = (uint32_t)chunks.size();
     const int64_t npad = pstart[g.G];
-    if (npad >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
     if (fresh || npad != c->n_gpad) {
-        dfree(c->d_g_node); dfree(c->d_g_grp); dfree(c->d_g_flags); dfree(c->d_cls4);
+        dfree(c->d_g_node); dfree(c->d_g_grp); dfree(c->d_g_flags); dfree(c->d_cls4); dfree(c->d_ord);
         HIP_TRY(dalloc(&c->d_g_node, npad)); HIP_TRY(dalloc(&c->d_g_grp, npad)); HIP_TRY(dalloc(&c->d_g_flags, npad));
-        HIP_TRY(dalloc(&c->d_cls4, (npad + 3) / 4));
+        HIP_TRY(dalloc(&c->d_cls4, (npad + 3) / 4)); HIP_TRY(dalloc(&c->d_ord, npad));
     }
     c->n_gpad = npad;
     if (npad) {
         HIP_TRY(hipMemsetAsync(c->d_g_node, 0, npad * 4, st));
-        HIP_TRY(hipMemsetAsync(c->d_g_grp, 0xFF, npad * 4, st));     // padding: group NONE
+        HIP_TRY(hipMemsetAsync(c->d_g_grp, 0xFF, npad * 4, st));
         HIP_TRY(hipMemsetAsync(c->d_g_flags, 0, npad * 4, st));
     }
-    if (fresh || (int64_t)chunks.size() != c->n_chunks) {
-        dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks); dfree(c->d_pstart);
-        HIP_TRY(dalloc(&c->d_grp_off, grp_off.size())); HIP_TRY(dalloc(&c->d_gch_off, gch_off.size()));
-        HIP_TRY(dalloc(&c->d_ccnt, chunks.size() * 3)); HIP_TRY(dalloc(&c->d_cbase, chunks.size() * 3));
-        HIP_TRY(dalloc(&c->d_chunks, chunks.size())); HIP_TRY(dalloc(&c->d_pstart, pstart.size()));
+    if (fresh || (int64_t)chunks.size() != c->n_chunks || (int64_t)pchunks.size() != c->n_pchunks) {
+        dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks);
+        dfree(c->d_pstart); dfree(c->d_plen); dfree(c->d_pchunks);
+        HIP_TRY(dalloc(&c->d_grp_off, pstart.size())); HIP_TRY(dalloc(&c->d_gch_off, gch_off.size()));
+        HIP_TRY(dalloc(&c->d_ccnt, std::max<size_t>(chunks.size(), 1) * 3));
+        HIP_TRY(dalloc(&c->d_cbase, std::max<size_t>(chunks.size(), 1) * 3));
+        HIP_TRY(dalloc(&c->d_chunks, std::max<size_t>(chunks.size(), 1)));
+        HIP_TRY(dalloc(&c->d_pchunks, std::max<size_t>(pchunks.size(), 1)));
+        HIP_TRY(dalloc(&c->d_pstart, pstart.size())); HIP_TRY(dalloc(&c->d_plen, plen.size()));
         dfree(c->d_oticket); dfree(c->d_ostat); dfree(c->d_oerr);
-        HIP_TRY(dalloc(&c->d_oticket, 1)); HIP_TRY(dalloc(&c->d_ostat, chunks.size())); HIP_TRY(dalloc(&c->d_oerr, 1));
+        HIP_TRY(dalloc(&c->d_oticket, 1)); HIP_TRY(dalloc(&c->d_ostat, std::max<size_t>(chunks.size(), 1)));
+        HIP_TRY(dalloc(&c->d_oerr, 1));
     }
     // fused ordering: tickets restart at 0 (a decision consumes exactly n_chunks), status
     // words at epoch 0 / not ready; groups without memberships get their (empty) segment
@@ -504,21 +545,29 @@ int32_t build_age_index(esc_ctx* c) {
     HIP_TRY(hipMemsetAsync(c->d_oerr, 0, 4, st));
 
     c->n_chunks = (int64_t)chunks.size();
-    HIP_TRY(hipMemcpy(c->d_grp_off, grp_off.data(), grp_off.size() * 4, hipMemcpyHostToDevice));
+    c->n_pchunks = (int64_t)pchunks.size();
+    HIP_TRY(hipMemcpy(c->d_grp_off, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_gch_off, gch_off.data(), gch_off.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->d_pstart, pstart.data(), pstart.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_plen, plen.data(), plen.size() * 4, hipMemcpyHostToDevice));
     if (!chunks.empty()) HIP_TRY(hipMemcpy(c->d_chunks, chunks.data(), chunks.size() * sizeof(OrdChunk), hipMemcpyHostToDevice));
+    if (!pchunks.empty())
+        HIP_TRY(hipMemcpy(c->d_pchunks, pchunks.data(), pchunks.size() * sizeof(OrdChunk), hipMemcpyHostToDevice));
     HIP_TRY(launch_group_pos(gkeys, c->n_memb, c->d_seg, c->d_pstart, c->d_gpos, st));
     HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
                                 c->d_g_grp, c->d_g_flags, st));
+    HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_grp, c->d_g_node, c->d_g_flags, st));
     {   // after k_grp_pos, which reads d_seg as the groups' unpadded starts
         std::vector<int64_t> seg0((size_t)4 * g.G + 1);
         for (int32_t q = 0; q < g.G; ++q)
-            for (int k = 0; k < 4; ++k) seg0[4 * (size_t)q + k] = grp_off[q];
-        seg0[4 * (size_t)g.G] = c->n_memb;
+            for (int k = 0; k < 4; ++k) seg0[4 * (size_t)q + k] = pstart[q];
+        seg0[4 * (size_t)g.G] = npad;
         HIP_TRY(hipMemcpyAsync(c->d_seg, seg0.data(), seg0.size() * 8, hipMemcpyHostToDevice, st));
         HIP_TRY(hipStreamSynchronize(st));
     }
+    c->h_pstart.swap(pstart);
+    c->h_plen.swap(plen);
+    c->h_gch_off.swap(gch_off);
     c->sorted = false;
     return ESC_OK;
 }
@@ -2071,14 +2120,15 @@ int32_t esc_sort_nodes(esc_ctx* c) {
     if (!c->nodes_loaded) return ESC_E_STATE;
     hipSetDevice(c->device);
     c->fused_ran = c->order_fused && c->fused_fits;
-    if (c->fused_ran)
+    if (c->fused_ran) {
         HIP_TRY(launch_order_fused(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node,
-                                   c->d_g_grp, c->d_g_flags, c->d_oticket, c->d_ostat, c->d_ovals[0], c->d_seg,
+                                   c->d_g_grp, c->d_g_flags, c->d_oticket, c->d_ostat, c->d_ord, c->d_seg,
                                    c->d_oerr, c->max_chunk, c->order_ablate, c->stream));
-    else
-        HIP_TRY(launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node,
-                             c->d_g_grp, c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase,
-                             c->d_ovals[0], c->d_seg, c->stream));
+        HIP_TRY(launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->d_grp_off, c->d_g_node, c->d_g_grp,
+                                    c->d_g_flags, c->d_ord, c->d_seg, c->stream));
+    } else {
+        HIP_TRY(enqueue_order(c, c->stream));
+    }
     c->order_src = 0;
     c->sorted = true;
     return ESC_OK;
@@ -2114,14 +2164,16 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
     }
     // three-pass layout: class segments [b0, b1), [b1, b2) in age order; fused: untainted
     // [s0, s1) in age order, tainted [s2, s3) newest first
-    const int64_t so = c->fused_ran ? 2 * (int64_t)which : (int64_t)which;
+    // packed (small) groups always take the three-pass layout
+    const bool fused_g = c->fused_ran && c->h_gch_off[group + 1] > c->h_gch_off[group];
+    const int64_t so = fused_g ? 2 * (int64_t)which : (int64_t)which;
     int64_t seg[2];
     HIP_TRY(hipMemcpy(seg, c->d_seg + 4 * (int64_t)group + so, 16, hipMemcpyDeviceToHost));
     const int64_t cnt = seg[1] - seg[0];
     if (n_out) *n_out = cnt;
     const int64_t m = std::min(cnt, cap);
     if (m <= 0) return ESC_OK;
-    const uint32_t* vals = c->d_ovals[c->order_src];
+    const uint32_t* vals = c->d_ord;
     if (which == 0) {                                  // taintOldestN: the segment in age order
         std::vector<uint32_t> v(m);
         HIP_TRY(hipMemcpy(v.data(), vals + seg[0], m * 4, hipMemcpyDeviceToHost));
@@ -2137,7 +2189,7 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
     std::vector<uint32_t> v;
     for (;;) {
         v.resize(take);
-        if (c->fused_ran) {
+        if (fused_g) {
             HIP_TRY(hipMemcpy(v.data(), vals + seg[0], take * 4, hipMemcpyDeviceToHost));
         } else {
             HIP_TRY(hipMemcpy(v.data(), vals + seg[1] - take, take * 4, hipMemcpyDeviceToHost));

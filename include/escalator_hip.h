@@ -248,6 +248,7 @@ typedef struct esc_node_obj {
 #define ESC_NF_UNSCHED     (1u << 0)   /* Spec.Unschedulable           controller.go:141 */
 #define ESC_NF_TAINTED     (1u << 1)   /* has atlassian.com/escalator  taint.go:31,80    */
 #define ESC_NF_TRACKED     (1u << 2)   /* in some group's dry-mode taintTracker controller.go:128 */
+#define ESC_NF_ABSENT      (1u << 3)   /* the slot holds no node (deleted, or a spare slot); owned by the context */
 #define ESC_NF_XLBL_SHIFT  8           /* bits 8..15: extra label pairs (xl_pair)                */
 
 typedef struct esc_pod_soa {
