@@ -224,10 +224,13 @@ constexpr int ORD_CHUNK = 4096;   // memberships per K5 chunk (three-pass defaul
 // region of the group-order arrays: its memberships oldest first, then padding (the round-up
 // to whole 16-B quads and the spare slots node additions take).
 constexpr uint32_t MEMB_PAD = 0x80000000u;
-// Small groups (region <= ORD_CHUNK) are packed whole into chunks ordered in one pass.
-hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* grp_off,
-                               const uint32_t* g_node, const uint32_t* g_grp, const uint32_t* g_flags,
-                               uint32_t* vals, int64_t* seg, hipStream_t st);
+// Small groups (region <= ORD_CHUNK) are packed whole into chunks ordered in one pass:
+// chunks [0, n_small) of groups with regions <= ORD_PCHUNK, packed up to ORD_PCHUNK
+// memberships (more, shorter blocks), then chunks of up to ORD_CHUNK.
+constexpr int ORD_PCHUNK = 1024;
+hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, int64_t n_small,
+                               const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
+                               const uint32_t* g_flags, uint32_t* vals, int64_t* seg, hipStream_t st);
 // Fills the padding of every group's region (after its `len` memberships) with g | MEMB_PAD.
 hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_grp,
                              uint32_t* g_node, uint32_t* g_flags, hipStream_t st);

@@ -745,6 +745,7 @@ __device__ __forceinline__ bool tracked(const NodeDev& N, int32_t node, int32_t 
 // filterNodes classification (controller.go:125-150): 0 untainted, 1 tainted, 2 cordoned.
 // Dry mode separates only tracker members; cordoned nodes are not split out there.
 __device__ __forceinline__ int node_class(const NodeDev& N, uint32_t f, int64_t i, uint32_t m) {
+    if (f & ESC_NF_ABSENT) return 3;                 // no node: in no class
     if (mdry(m)) return ((f & ESC_NF_TRACKED) && tracked(N, (int32_t)i, (int32_t)mg(m))) ? 1 : 0;
     if (f & ESC_NF_UNSCHED) return 2;
     return (f & ESC_NF_TAINTED) ? 1 : 0;
@@ -755,6 +756,7 @@ __device__ __forceinline__ int node_class(const NodeDev& N, uint32_t f, int64_t 
 template <class F>
 __device__ __forceinline__ void node_groups(const NodeDev& N, const GroupDev& G, uint32_t f, int64_t i,
                                             F&& emit) {
+    if (f & ESC_NF_ABSENT) return;                   // a free / deleted slot is in no group
     for_code(G, node_code(G, N.label0[i]), emit);
     const uint32_t nx = nf_xlbl(f);
     if (nx) {
@@ -784,6 +786,7 @@ constexpr int K2_WAVES = 4;
 struct PieceAcc {
     unsigned long long ucl = 0, uch = 0, uml = 0, umh = 0, acl = 0, ach = 0, aml = 0, amh = 0, cnt = 0;
     __device__ __forceinline__ void add(uint32_t f, int64_t c, int64_t m) {
+        if (f & ESC_NF_ABSENT) return;               // spare entry or deleted node
         const unsigned long long cl = (uint64_t)c & 0xFFFFFFFFull, ml = (uint64_t)m & 0xFFFFFFFFull;
         const unsigned long long chh = (unsigned long long)(c >> 32), mhh = (unsigned long long)(m >> 32);
         acl += cl; ach += chh; aml += ml; amh += mhh;
@@ -1644,20 +1647,21 @@ __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long lon
     return v;
 }
 
+template <int STEPS>
 __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdChunk* __restrict__ chunks,
                                                           const uint32_t* __restrict__ grp_off,
                                                           const uint32_t* __restrict__ g_node,
                                                           const uint32_t* __restrict__ g_grp,
                                                           const uint32_t* __restrict__ g_flags,
                                                           uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
-    constexpr int STEPS = ORD_CHUNK / (4 * ORD_BLOCK);
-    constexpr int NQ = ORD_CHUNK / 4;
+    constexpr int CAP = STEPS * 4 * ORD_BLOCK;           // memberships per chunk
+    constexpr int NQ = CAP / 4;
     constexpr int C1 = 21, C2 = 42;
     constexpr unsigned long long M = (1ull << C1) - 1;
     __shared__ unsigned long long wt[STEPS][ORD_WAVES];
     __shared__ unsigned long long hp[NQ];                // scan value at each group's first quad
     __shared__ unsigned long long tt[NQ];                // each group's totals, at its first quad
-    __shared__ uint32_t stage[ORD_CHUNK];
+    __shared__ uint32_t stage[CAP];
     const OrdChunk ch = chunks[blockIdx.x];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint4 nd[STEPS], gr[STEPS], fl[STEPS];
@@ -2022,7 +2026,7 @@ __global__ __launch_bounds__(256) void k_occupancy(NodeDev N, GroupDev G, Remova
         const uint32_t f = N.e_flags[e];
         q = R.e_pair[e];
         j = N.e_node[e];
-        want = q < G.n_gp && (f & ESC_NF_TAINTED) && !(f & ESC_NF_UNSCHED);
+        want = q < G.n_gp && (f & ESC_NF_TAINTED) && !(f & (ESC_NF_UNSCHED | ESC_NF_ABSENT));
     }
     unsigned long long m = __ballot(want);
     while (m) {
@@ -2273,12 +2277,17 @@ hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t
     return hipGetLastError();
 }
 
-hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* grp_off,
-                               const uint32_t* g_node, const uint32_t* g_grp, const uint32_t* g_flags,
-                               uint32_t* vals, int64_t* seg, hipStream_t st) {
+hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, int64_t n_small,
+                               const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
+                               const uint32_t* g_flags, uint32_t* vals, int64_t* seg, hipStream_t st) {
     if (n_chunks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_ord_packed, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, grp_off, g_node,
-                       g_grp, g_flags, vals, seg);
+    // chunks [0, n_small) hold <= ORD_PCHUNK memberships, the rest <= ORD_CHUNK
+    if (n_small > 0)
+        hipLaunchKernelGGL(k_ord_packed<ORD_PCHUNK / (4 * ORD_BLOCK)>, dim3((unsigned)n_small), dim3(ORD_BLOCK), 0, st,
+                           nd, chunks, grp_off, g_node, g_grp, g_flags, vals, seg);
+    if (n_chunks > n_small)
+        hipLaunchKernelGGL(k_ord_packed<ORD_CHUNK / (4 * ORD_BLOCK)>, dim3((unsigned)(n_chunks - n_small)),
+                           dim3(ORD_BLOCK), 0, st, nd, chunks + n_small, grp_off, g_node, g_grp, g_flags, vals, seg);
     return hipGetLastError();
 }
 

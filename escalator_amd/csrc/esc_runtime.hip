@@ -211,7 +211,7 @@ struct esc_ctx {
     uint32_t *d_gpos = nullptr, *d_pstart = nullptr, *d_cls4 = nullptr, *d_plen = nullptr;
     uint32_t* d_ord = nullptr;                                // K5 output, in the group regions
     OrdChunk* d_pchunks = nullptr;                            // packed chunks of small groups
-    int64_t n_pchunks = 0;
+    int64_t n_pchunks = 0, n_psmall = 0;                      // all / those <= ORD_PCHUNK (first)
     std::vector<uint32_t> h_pstart, h_plen;                   // group regions: start, memberships
     std::vector<uint32_t> h_gch_off;                          // group -> its split chunks (big groups)
     int64_t n_gpad = 0;                                       // padded group-order length
@@ -228,6 +228,13 @@ struct esc_ctx {
     int sort_R = 1;
     bool sorted = false;
     std::vector<int64_t> h_created;                           // [lo, hi) creation times (tie order)
+    // node informer events (§8f rank 1): capacity and host mirrors for in-place add / delete
+    int64_t n_cap = 0, xl_used = 0, xl_cap = 0, age_n = -1;
+    bool tail_owner = true;                                   // this rank's K5 range ends at the table's end
+    std::vector<uint32_t> h_label0, h_xl_off, h_xl;           // node labels (pair ids)
+    std::vector<uint32_t> h_e_node;                           // pair-major entry -> node (NONE: spare)
+    std::vector<uint32_t> pair_next, pair_end;                // group pair -> next spare entry, range end
+    std::vector<uint32_t> h_gn;                               // group regions' nodes (lazy mirror of d_g_node)
     // per-function drop-ins run on a one-group list context
     esc_ctx* list_ctx = nullptr;
     // incremental snapshot (§8f rank 1): where each loaded pod lives, free K slots
@@ -347,7 +354,7 @@ hipError_t enqueue_order(esc_ctx* c, hipStream_t st) {
                                       c->d_g_grp, c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase,
                                       c->d_ord, c->d_seg, st);
     if (e != hipSuccess) return e;
-    return launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->d_grp_off, c->d_g_node, c->d_g_grp,
+    return launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_node, c->d_g_grp,
                                c->d_g_flags, c->d_ord, c->d_seg, st);
 }
 
@@ -420,8 +427,15 @@ int32_t build_age_index(esc_ctx* c) {
     const NodeDev n = node_dev(c);
     hipStream_t st = c->stream;
     const int64_t nl = c->node_hi - c->node_lo;
+    if (c->d_age_keys[0] && c->age_n != nl) release_sort(c);   // the range grew (esc_nodes_add)
     const bool fresh = c->d_age_keys[0] == nullptr;
     if (fresh) {
+        c->age_n = nl;
+        c->h_gn.clear();
+        if (nl) {                                    // creation-time range of the node range
+            c->ts_min = *std::min_element(c->h_created.begin(), c->h_created.end());
+            c->ts_max = *std::max_element(c->h_created.begin(), c->h_created.end());
+        }
         uint64_t div = 1;
         for (uint64_t d : {1000000000ull, 1000000ull, 1000ull}) {
             bool ok = true;
@@ -481,29 +495,46 @@ int32_t build_age_index(esc_ctx* c) {
     // chunks: a group whose region exceeds ORD_CHUNK is split (two-pass or fused kernels,
     // chunk prefix across the group); smaller groups are packed whole, several per chunk,
     // and ordered in one pass (k_ord_packed)
-    std::vector<OrdChunk> chunks, pchunks;
-    uint32_t pk_lo = 0, pk_hi = 0;
-    auto flush_packed = [&]() {
+    std::vector<OrdChunk> chunks, pchunks, pbig;
+    uint32_t pk_lo = 0, pk_hi = 0, qk_lo = 0, qk_hi = 0;
+    auto flush_small = [&]() {
         if (pk_hi > pk_lo) pchunks.push_back({pk_lo, pk_hi, NONE, 1u});
         pk_lo = pk_hi;
+    };
+    auto flush_mid = [&]() {
+        if (qk_hi > qk_lo) pbig.push_back({qk_lo, qk_hi, NONE, 1u});
+        qk_lo = qk_hi;
     };
     for (int32_t q = 0; q < g.G; ++q) {
         const uint32_t reg = pstart[q + 1] - pstart[q];
         gch_off[q] = (uint32_t)chunks.size();
         if (reg == 0) continue;
         if (reg > (uint32_t)ORD_CHUNK) {
-            flush_packed();
-            pk_lo = pk_hi = pstart[q + 1];
+            flush_small();
+            flush_mid();
+            pk_lo = pk_hi = qk_lo = qk_hi = pstart[q + 1];
             for (int64_t a = 0; a < reg; a += c->ord_chunk)
                 chunks.push_back({pstart[q] + (uint32_t)a, pstart[q] + (uint32_t)std::min<int64_t>(reg, a + c->ord_chunk),
                                   (uint32_t)q, 0u});
             continue;
         }
-        if (pk_hi - pk_lo + reg > (uint32_t)ORD_CHUNK) flush_packed();
+        if (reg > (uint32_t)ORD_PCHUNK) {          // mid-size: packed up to ORD_CHUNK
+            flush_small();
+            if (qk_hi - qk_lo + reg > (uint32_t)ORD_CHUNK || qk_hi != pstart[q]) flush_mid();
+            if (qk_hi == qk_lo) qk_lo = qk_hi = pstart[q];
+            qk_hi = pstart[q + 1];
+            pk_lo = pk_hi = pstart[q + 1];
+            continue;
+        }
+        if (pk_hi - pk_lo + reg > (uint32_t)ORD_PCHUNK || pk_hi != pstart[q]) flush_small();
         if (pk_hi == pk_lo) pk_lo = pk_hi = pstart[q];
         pk_hi = pstart[q + 1];
+        qk_lo = qk_hi = pstart[q + 1];
     }
-    flush_packed();
+    flush_small();
+    flush_mid();
+    c->n_psmall = (int64_t)pchunks.size();
+    pchunks.insert(pchunks.end(), pbig.begin(), pbig.end());
     gch_off[g.G] = (uint32_t)chunks.size();
     c->fused_fits = true;
     c->max_chunk = 0;
@@ -1223,11 +1254,27 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     // in its 1/world share of the entries.
     std::vector<uint64_t> ent;
     ent.reserve((size_t)n + (size_t)s->n_xl);
+    const uint32_t n_gp0 = c->gi.n_gp;
+    std::vector<int64_t> pair_cnt(n_gp0, 0);
     for (int64_t i = 0; i < n; ++i) {
+        if (s->flags[i] & ESC_NF_ABSENT) return ESC_E_INVAL;   // the context owns that bit
         if (s->label0[i] == NONE) continue;
         ent.push_back(((uint64_t)s->label0[i] << 32) | (uint64_t)i);
+        if (s->label0[i] < n_gp0) ++pair_cnt[s->label0[i]];
         const uint32_t nx = nf_xlbl(s->flags[i]);
-        for (uint32_t k = 0; k < nx; ++k) ent.push_back(((uint64_t)s->xl_pair[xl_off[i] + k] << 32) | (uint64_t)i);
+        for (uint32_t k = 0; k < nx; ++k) {
+            const uint32_t q = s->xl_pair[xl_off[i] + k];
+            ent.push_back(((uint64_t)q << 32) | (uint64_t)i);
+            if (q < n_gp0) ++pair_cnt[q];
+        }
+    }
+    // spare entries (esc_set_spare): after each group pair's entries, flagged ESC_NF_ABSENT,
+    // taken in order by added nodes (whose indices are above every loaded one, so a
+    // pair's entries stay in snapshot order)
+    const double sf = c->spare_frac;
+    for (uint32_t q = 0; q < n_gp0 && sf > 0; ++q) {
+        const int64_t sp = (int64_t)std::ceil((double)pair_cnt[q] * sf) + 4;
+        for (int64_t k = 0; k < sp; ++k) ent.push_back(((uint64_t)q << 32) | 0xFFFFFFFFull);
     }
     std::sort(ent.begin(), ent.end());
     const int64_t E = (int64_t)ent.size();
@@ -1241,6 +1288,12 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
             piece_off.push_back((uint32_t)k);
             piece_pair.push_back(q);
         }
+        if (i == NONE) {                             // spare entry
+            e_flags[k] = ESC_NF_ABSENT;
+            e_node[k] = NONE;
+            e_cpu[k] = e_mem[k] = 0;
+            continue;
+        }
         e_flags[k] = s->flags[i];
         e_node[k] = i;
         e_cpu[k] = s->cpu[i];
@@ -1250,12 +1303,15 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     piece_off.push_back((uint32_t)E);
     // node -> its entry positions (esc_nodes_update patches the entries' copies)
     std::vector<uint32_t> ne_off((size_t)n + 1, 0), ne_pos((size_t)std::max<int64_t>(E, 1));
-    for (int64_t k = 0; k < E; ++k) ++ne_off[(uint32_t)ent[k] + 1];
+    for (int64_t k = 0; k < E; ++k)
+        if ((uint32_t)ent[k] != NONE) ++ne_off[(uint32_t)ent[k] + 1];
     for (int64_t i = 0; i < n; ++i) ne_off[i + 1] += ne_off[i];
     {
         std::vector<uint32_t> fill(ne_off.begin(), ne_off.end() - 1);
-        for (int64_t k = 0; k < E; ++k) ne_pos[fill[(uint32_t)ent[k]]++] = (uint32_t)k;
+        for (int64_t k = 0; k < E; ++k)
+            if ((uint32_t)ent[k] != NONE) ne_pos[fill[(uint32_t)ent[k]]++] = (uint32_t)k;
     }
+    ne_pos.resize(ne_off[n]);
     const uint32_t n_gp = c->gi.n_gp;
     std::vector<uint32_t> pp_off((size_t)n_gp + 1);
     for (uint32_t q = 0; q <= n_gp; ++q)
@@ -1270,7 +1326,8 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
         if (piece_pair[p] < n_gp) node_bytes += 24 * (int64_t)(piece_off[p + 1] - piece_off[p]);
     }
     // dry-mode tracker: each tracked node's first entry (the (node, group) list is node-sorted)
-    std::vector<uint32_t> trk_start(std::max<int64_t>(n, 1), NONE);
+    std::vector<uint32_t> trk_start(std::max<int64_t>(n + (sf > 0 ? (int64_t)std::ceil((double)n * sf) + 64 : 0), 1),
+                                    NONE);
     for (int64_t k = s->n_trk - 1; k >= 0; --k) trk_start[s->trk_node[k]] = (uint32_t)k;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
@@ -1279,10 +1336,21 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     release_sort(c);
     release_placement(c);
     c->nodes.release();
+    // capacity for added nodes (esc_nodes_add): table slots and extra-label words
+    const int64_t n_cap = n + (sf > 0 ? (int64_t)std::ceil((double)n * sf) + 64 : 0);
+    const int64_t xl_cap = s->n_xl + (sf > 0 ? (int64_t)std::ceil((double)s->n_xl * sf) + 256 : 0);
+    if (n_cap >= (int64_t)0x7FFFFFFF) return ESC_E_LIMIT;
     NodeBuf& b = c->nodes;
-    HIP_TRY(dalloc(&b.flags, n)); HIP_TRY(dalloc(&b.label0, n)); HIP_TRY(dalloc(&b.cpu, n));
-    HIP_TRY(dalloc(&b.mem, n)); HIP_TRY(dalloc(&b.created, n)); HIP_TRY(dalloc(&b.xl, s->n_xl));
-    HIP_TRY(dalloc(&b.xl_off, n)); HIP_TRY(dalloc(&b.trk_node, s->n_trk)); HIP_TRY(dalloc(&b.trk_group, s->n_trk));
+    HIP_TRY(dalloc(&b.flags, n_cap)); HIP_TRY(dalloc(&b.label0, n_cap)); HIP_TRY(dalloc(&b.cpu, n_cap));
+    HIP_TRY(dalloc(&b.mem, n_cap)); HIP_TRY(dalloc(&b.created, n_cap)); HIP_TRY(dalloc(&b.xl, xl_cap));
+    HIP_TRY(dalloc(&b.xl_off, n_cap)); HIP_TRY(dalloc(&b.trk_node, s->n_trk)); HIP_TRY(dalloc(&b.trk_group, s->n_trk));
+    if (n_cap > n) {                                 // free slots: absent, no labels
+        std::vector<uint32_t> fa(n_cap - n, ESC_NF_ABSENT), la(n_cap - n, NONE);
+        HIP_TRY(hipMemcpy(b.flags + n, fa.data(), fa.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(b.label0 + n, la.data(), la.size() * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemset(b.cpu + n, 0, (n_cap - n) * 8)); HIP_TRY(hipMemset(b.mem + n, 0, (n_cap - n) * 8));
+        HIP_TRY(hipMemset(b.created + n, 0, (n_cap - n) * 8)); HIP_TRY(hipMemset(b.xl_off + n, 0, (n_cap - n) * 4));
+    }
     if (n) {
         HIP_TRY(hipMemcpy(b.flags, s->flags, n * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(b.label0, s->label0, n * 4, hipMemcpyHostToDevice));
@@ -1319,19 +1387,43 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
             x.plo = std::max<int64_t>(p0, pc_lo);
             x.phi = std::min<int64_t>(p1, pc_hi);
             if (x.phi < x.plo) x.phi = x.plo;
-            x.first = p1 > p0 ? (int64_t)e_node[piece_off[p0]] : INT64_MAX;
-            x.first_cpu = p1 > p0 ? s->cpu[x.first] : 0;
-            x.first_mem = p1 > p0 ? s->mem[x.first] : 0;
+            const bool any = p1 > p0 && e_node[piece_off[p0]] != NONE;     // not only spare entries
+            x.first = any ? (int64_t)e_node[piece_off[p0]] : INT64_MAX;
+            x.first_cpu = any ? s->cpu[x.first] : 0;
+            x.first_mem = any ? s->mem[x.first] : 0;
         }
         HIP_TRY(dalloc(&b.gnode, gn.size()));
         HIP_TRY(hipMemcpy(b.gnode, gn.data(), gn.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
         c->h_gnode.swap(gn);
     }
+    // host mirrors for node events (table slots up to the capacity)
+    c->pair_next.assign(n_gp, 0);
+    c->pair_end.assign(n_gp, 0);
+    for (uint32_t q = 0; q < n_gp; ++q) {
+        const uint32_t a = piece_off[pp_off[q]], z = piece_off[pp_off[q + 1]];
+        c->pair_end[q] = z;
+        c->pair_next[q] = a + (uint32_t)pair_cnt[q];
+    }
+    c->h_e_node.swap(e_node);
+    c->h_e_node.resize(E);
     c->ne_off.swap(ne_off);
     c->ne_pos.swap(ne_pos);
     c->h_nflags.assign(s->flags, s->flags + n);
     c->h_ncpu.assign(s->cpu, s->cpu + n);
     c->h_nmem.assign(s->mem, s->mem + n);
+    c->h_label0.assign(s->label0, s->label0 + n);
+    c->h_xl_off.assign(xl_off.begin(), xl_off.begin() + n);
+    c->h_xl.assign(s->xl_pair, s->xl_pair + s->n_xl);
+    c->h_nflags.resize(n_cap, ESC_NF_ABSENT);
+    c->h_ncpu.resize(n_cap, 0);
+    c->h_nmem.resize(n_cap, 0);
+    c->h_label0.resize(n_cap, NONE);
+    c->h_xl_off.resize(n_cap, 0);
+    c->n_cap = n_cap;
+    c->xl_used = s->n_xl;
+    c->xl_cap = xl_cap;
+    c->tail_owner = hi == n;
+    c->h_gn.clear();
     c->n_entries = E;
     c->n_pieces = n_pieces;
     c->pc_lo = pc_lo;
@@ -2124,7 +2216,7 @@ int32_t esc_sort_nodes(esc_ctx* c) {
         HIP_TRY(launch_order_fused(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node,
                                    c->d_g_grp, c->d_g_flags, c->d_oticket, c->d_ostat, c->d_ord, c->d_seg,
                                    c->d_oerr, c->max_chunk, c->order_ablate, c->stream));
-        HIP_TRY(launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->d_grp_off, c->d_g_node, c->d_g_grp,
+        HIP_TRY(launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_node, c->d_g_grp,
                                     c->d_g_flags, c->d_ord, c->d_seg, c->stream));
     } else {
         HIP_TRY(enqueue_order(c, c->stream));

@@ -272,12 +272,13 @@ def test_synthetic_sort_vs_c_oracle(esc, fused, monkeypatch):
     assert ctx.group_order(g, 1).tolist() == sorted((j for j in members if j in trk), key=lambda j: (-int(t[j]), j))
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_order_in_step_vs_c_oracle(esc, graph):
+@pytest.mark.parametrize("graph,N", [(False, 200_000), (True, 200_000), (True, 30_000), (True, 700_000)])
+def test_order_in_step_vs_c_oracle(esc, graph, N):
     """esc_set_order_in_step: the K5 ordering inside every decision (side stream beside K1,
     captured in the decision graph) — orders valid after esc_run with no esc_sort_nodes,
-    also after node events patch the flags, and the decision itself unchanged."""
-    s = esc.Synth(300_000, 200_000, 100, config=5, seed=0xE5CA1A7E00000005)
+    also after node events patch the flags, and the decision itself unchanged.  Group sizes
+    cover the packed chunk kinds (<= 1024 and <= 4096 memberships) and the split one."""
+    s = esc.Synth(300_000, N, 100, config=5, seed=0xE5CA1A7E00000005)
     pods, nodes = s.pods(), s.nodes()
     ctx = esc.Context(s)
     ctx.load_synth(s, replicas=2)
@@ -296,7 +297,7 @@ def test_order_in_step_vs_c_oracle(esc, graph):
             assert np.array_equal(ctx.group_order(g, which), full[(g, which)]), (g, which)
     # node events (cordon / taint flips) then one more decision: orders follow the flags
     rng = np.random.default_rng(5)
-    ids = rng.choice(len(nodes["flags"]), 2000, replace=False).astype(np.int64)
+    ids = rng.choice(len(nodes["flags"]), min(2000, N // 10), replace=False).astype(np.int64)
     flags = nodes["flags"].copy()
     flags[ids] ^= rng.integers(1, 4, len(ids)).astype(np.uint32) & 3
     ctx.nodes_update(ids, flags[ids], nodes["cpu"][ids], nodes["mem"][ids])
