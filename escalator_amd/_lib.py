@@ -156,6 +156,8 @@ _SIGS = {
     "esc_pods_upsert": (i32, [VP, P(i64), P(PodSoA)]),
     "esc_pods_delete": (i32, [VP, P(i64), i64]),
     "esc_nodes_update": (i32, [VP, P(i64), i64, P(u32), P(i64), P(i64)]),
+    "esc_nodes_add": (i32, [VP, P(NodeSoA), P(i64)]),
+    "esc_nodes_delete": (i32, [VP, P(i64), i64]),
     "esc_tracker_update": (i32, [VP, i32, P(i64), i64, P(i64), i64]),
     "esc_tracker_list": (i32, [VP, i32, P(i64), i64, P(i64)]),
     "esc_load_placement": (i32, [VP, P(u32), P(i64), P(C.c_uint8)]),

@@ -195,6 +195,23 @@ class Context:
                                           c_.ctypes.data_as(C.POINTER(C.c_int64)),
                                           m.ctypes.data_as(C.POINTER(C.c_int64))), "esc_nodes_update")
 
+    def nodes_add(self, nodes: dict) -> np.ndarray:
+        """Node informer Add events (cache.go:37-56): packed nodes (n_trk = 0) appended in
+        place; returns their snapshot indices.  EscError(ESC_E_LIMIT) when the spare room is short."""
+        n = len(nodes["flags"])
+        ns, keep = node_soa(nodes)
+        out = np.zeros(max(n, 1), np.int64)
+        L.check(self.lib.esc_nodes_add(self.handle, C.byref(ns), out.ctypes.data_as(C.POINTER(C.c_int64))),
+                "esc_nodes_add")
+        del keep
+        return out[:n]
+
+    def nodes_delete(self, ids):
+        """Node informer Delete events: the nodes' slots become absent."""
+        ids = np.ascontiguousarray(ids, np.int64)
+        L.check(self.lib.esc_nodes_delete(self.handle, ids.ctypes.data_as(C.POINTER(C.c_int64)), len(ids)),
+                "esc_nodes_delete")
+
     def tracker_update(self, group: int, add=(), remove=()):
         """Dry-mode taintTracker change of one group in place (esc_tracker_update): the
         nodes untaintNewestN deletes (scale_up.go:146-158), then the ones taintOldestN

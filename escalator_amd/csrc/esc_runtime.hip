@@ -234,6 +234,8 @@ struct esc_ctx {
     std::vector<uint32_t> h_label0, h_xl_off, h_xl;           // node labels (pair ids)
     std::vector<uint32_t> h_e_node;                           // pair-major entry -> node (NONE: spare)
     std::vector<uint32_t> pair_next, pair_end;                // group pair -> next spare entry, range end
+    std::vector<uint32_t> pair_lo;                            // group pair -> its first entry
+    uint32_t nodes_piece_lo(uint32_t q) const { return pair_lo[q]; }
     std::vector<uint32_t> h_gn;                               // group regions' nodes (lazy mirror of d_g_node)
     // per-function drop-ins run on a one-group list context
     esc_ctx* list_ctx = nullptr;
@@ -1399,9 +1401,11 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     // host mirrors for node events (table slots up to the capacity)
     c->pair_next.assign(n_gp, 0);
     c->pair_end.assign(n_gp, 0);
+    c->pair_lo.assign(n_gp, 0);
     for (uint32_t q = 0; q < n_gp; ++q) {
         const uint32_t a = piece_off[pp_off[q]], z = piece_off[pp_off[q + 1]];
         c->pair_end[q] = z;
+        c->pair_lo[q] = a;
         c->pair_next[q] = a + (uint32_t)pair_cnt[q];
     }
     c->h_e_node.swap(e_node);
@@ -1816,13 +1820,123 @@ void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
     --c->live_pods;
 }
 
+// ---- node events: host views of the node memberships and the K5 group regions
+// Groups of node j (its label pairs through the node codes, dry bit included), as the
+// kernels' node_groups lists them.
+void node_membs(const esc_ctx* c, int64_t j, std::vector<uint32_t>& out) {
+    out.clear();
+    if (c->h_nflags[j] & ESC_NF_ABSENT) return;
+    auto add = [&](uint32_t q) {
+        if (q >= c->gi.n_gp) return;
+        const uint32_t code = c->gi.node_code[q];
+        if (code < CODE_MULTI) out.push_back(code);
+        else if (code != NONE) {
+            const uint32_t* l = c->gi.code_list.data() + (code & ~CODE_MULTI);
+            for (uint32_t k = 1; k <= l[0]; ++k) out.push_back(l[k]);
+        }
+    };
+    add(c->h_label0[j]);
+    const uint32_t nx = nf_xlbl(c->h_nflags[j]);
+    for (uint32_t k = 0; k < nx; ++k) add(c->h_xl[c->h_xl_off[j] + k]);
+}
+
+// Groups of a node given its label pairs (before it is in the mirrors).
+void node_membs_from(const esc_ctx* c, uint32_t label0, uint32_t nx, const uint32_t* xl, std::vector<uint32_t>& out) {
+    out.clear();
+    auto add = [&](uint32_t q) {
+        if (q >= c->gi.n_gp) return;
+        const uint32_t code = c->gi.node_code[q];
+        if (code < CODE_MULTI) out.push_back(code);
+        else if (code != NONE) {
+            const uint32_t* l = c->gi.code_list.data() + (code & ~CODE_MULTI);
+            for (uint32_t k = 1; k <= l[0]; ++k) out.push_back(l[k]);
+        }
+    };
+    add(label0);
+    for (uint32_t k = 0; k < nx; ++k) add(xl[k]);
+}
+
+// The K5 copy of node j's flags for membership mb: a dry group's copy carries "tracked by
+// this group" in the tracker bit (as k_memb_expand lists it).
+uint32_t memb_flags(const esc_ctx* c, int64_t j, uint32_t mb) {
+    const uint32_t f = c->h_nflags[j];
+    if (!(mb & NODE_DRY_BIT)) return f;
+    const uint64_t key = ((uint64_t)(uint32_t)j << 32) | (mb & NODE_GROUP_MASK);
+    const bool tr = (f & ESC_NF_TRACKED) && std::binary_search(c->h_trk.begin(), c->h_trk.end(), key);
+    return (f & ~ESC_NF_TRACKED) | (tr ? ESC_NF_TRACKED : 0u);
+}
+
+int64_t created_of(const esc_ctx* c, uint32_t j) { return c->h_created[(int64_t)j - c->node_lo]; }
+
+// Host mirror of the regions' node ids (fetched once, then kept in step with every patch).
+int32_t ensure_gn(esc_ctx* c) {
+    if ((int64_t)c->h_gn.size() == c->n_gpad) return ESC_OK;
+    c->h_gn.resize(c->n_gpad);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->n_gpad) HIP_TRY(hipMemcpy(c->h_gn.data(), c->d_g_node, c->n_gpad * 4, hipMemcpyDeviceToHost));
+    return ESC_OK;
+}
+
+// Position of node j's membership in group g's region (regions are ordered by creation
+// time, ties by index), or -1.
+int64_t region_pos(const esc_ctx* c, uint32_t g, uint32_t j) {
+    const uint32_t a = c->h_pstart[g], z = a + c->h_plen[g];
+    const int64_t t = created_of(c, j);
+    const uint32_t* b = c->h_gn.data();
+    const uint32_t* it = std::lower_bound(b + a, b + z, j, [&](uint32_t x, uint32_t y) {
+        const int64_t tx = created_of(c, x);
+        return tx < t || (tx == t && x < y);
+    });
+    return (it != b + z && *it == j) ? (int64_t)(it - b) : -1;
+}
+
+enum : uint32_t { NT_FLAGS = 0, NT_EFLAGS = 1, NT_LABEL0 = 2, NT_XLOFF = 3, NT_ENODE = 4, NT_XL = 5, NT_CPU = 6,
+                  NT_MEM = 7, NT_ECPU = 8, NT_EMEM = 9, NT_CREATED = 10 };
+
+PatchTargets node_targets(esc_ctx* c) {
+    PatchTargets t{};
+    t.u32[NT_FLAGS] = c->nodes.flags; t.u32[NT_EFLAGS] = c->nodes.e_flags; t.u32[NT_LABEL0] = c->nodes.label0;
+    t.u32[NT_XLOFF] = c->nodes.xl_off; t.u32[NT_ENODE] = c->nodes.e_node; t.u32[NT_XL] = c->nodes.xl;
+    t.i64[NT_CPU - 6] = c->nodes.cpu; t.i64[NT_MEM - 6] = c->nodes.mem;
+    t.i64[NT_ECPU - 6] = c->nodes.e_cpu; t.i64[NT_EMEM - 6] = c->nodes.e_mem;
+    t.i64[NT_CREATED - 6] = c->nodes.created;
+    return t;
+}
+
+// K5 region copies of the memberships of nodes `ids` (their flags, as the split reads them).
+int32_t patch_regions(esc_ctx* c, const std::vector<int64_t>& ids) {
+    if (!c->n_gpad) return ESC_OK;
+    int32_t rc = ensure_gn(c);
+    if (rc) return rc;
+    Patches P;
+    std::vector<uint32_t> mb;
+    for (int64_t j : ids) {
+        if (j < c->node_lo || j >= c->node_hi) continue;            // outside this rank's K5 range
+        const bool gone = (c->h_nflags[j] & ESC_NF_ABSENT) != 0;
+        if (gone) {                                                   // the memberships it had
+            uint32_t f = c->h_nflags[j];
+            c->h_nflags[j] &= ~ESC_NF_ABSENT;
+            node_membs(c, j, mb);
+            c->h_nflags[j] = f;
+        } else {
+            node_membs(c, j, mb);
+        }
+        for (uint32_t m : mb) {
+            const int64_t pos = region_pos(c, m & NODE_GROUP_MASK, (uint32_t)j);
+            if (pos < 0) return ESC_E_HIP;                            // mirror out of step: never expected
+            P.add(0, pos, gone ? ESC_NF_ABSENT : memb_flags(c, j, m));
+        }
+    }
+    PatchTargets t{};
+    t.u32[0] = c->d_g_flags;
+    return apply_patches(c, P, {t});
+}
+
 // Writes the host mirrors (h_nflags / h_ncpu / h_nmem) of nodes `ids` to the device:
 // the node table, the nodes' pair-major K2 entries, allNodes[0]'s cached allocatable,
-// and the K5 membership list (re-listed: order and counts depend on creation times and
-// labels only, both unchanged).
+// and the K5 region copies (looked up by creation time: no re-listing).
 int32_t patch_nodes(esc_ctx* c, const std::vector<int64_t>& ids) {
     c->rm_valid = false;
-    enum : uint32_t { NT_FLAGS = 0, NT_EFLAGS = 1, NT_CPU = 6, NT_MEM = 7, NT_ECPU = 8, NT_EMEM = 9 };
     Patches P;
     bool first_changed = false;
     for (int64_t j : ids) {
@@ -1843,20 +1957,44 @@ int32_t patch_nodes(esc_ctx* c, const std::vector<int64_t>& ids) {
             g.first_mem = c->h_nmem[g.first];
             first_changed = true;
         }
-    PatchTargets t{};
-    t.u32[NT_FLAGS] = c->nodes.flags; t.u32[NT_EFLAGS] = c->nodes.e_flags;
-    t.i64[NT_CPU - 6] = c->nodes.cpu; t.i64[NT_MEM - 6] = c->nodes.mem;
-    t.i64[NT_ECPU - 6] = c->nodes.e_cpu; t.i64[NT_EMEM - 6] = c->nodes.e_mem;
-    int32_t rc = apply_patches(c, P, {t});
+    int32_t rc = apply_patches(c, P, {node_targets(c)});
     if (rc) return rc;
     if (first_changed)
         HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
-    HIP_TRY(launch_memb_expand(node_dev(c), group_dev(c), c->d_age, c->memb_blocks, c->d_cnt, c->d_e_node,
-                               c->d_e_grp, c->d_e_flags, c->stream));
-    HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
-                                c->d_g_grp, c->d_g_flags, c->stream));
+    rc = patch_regions(c, ids);
+    if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->sorted = false;
+    return ESC_OK;
+}
+
+// The tracker list (sorted (node << 32 | group)) and its per-node first-entry index on the
+// device; graphs are dropped (K2's grid and NodeDev carry n_trk).
+int32_t write_tracker(esc_ctx* c, std::vector<uint64_t>& next) {
+    const int64_t nt = (int64_t)next.size();
+    NodeBuf& b = c->nodes;
+    if (nt > c->trk_cap) {
+        const int64_t cap = std::max<int64_t>({nt, 2 * c->trk_cap, 1024});
+        dfree(b.trk_node); dfree(b.trk_group);
+        b.trk_node = nullptr; b.trk_group = nullptr;
+        HIP_TRY(dalloc(&b.trk_node, cap)); HIP_TRY(dalloc(&b.trk_group, cap));
+        c->trk_cap = cap;
+    }
+    std::vector<int32_t> tn(std::max<int64_t>(nt, 1)), tg(std::max<int64_t>(nt, 1));
+    std::vector<uint32_t> ts(std::max<int64_t>(c->n_cap, 1), NONE);
+    for (int64_t k = nt - 1; k >= 0; --k) {
+        tn[k] = (int32_t)(next[k] >> 32);
+        tg[k] = (int32_t)(uint32_t)next[k];
+        ts[tn[k]] = (uint32_t)k;
+    }
+    if (nt) {
+        HIP_TRY(hipMemcpy(b.trk_node, tn.data(), nt * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(b.trk_group, tg.data(), nt * 4, hipMemcpyHostToDevice));
+    }
+    HIP_TRY(hipMemcpy(b.trk_start, ts.data(), ts.size() * 4, hipMemcpyHostToDevice));
+    c->h_trk.swap(next);
+    c->n_trk = nt;
+    drop_graphs(c);
     return ESC_OK;
 }
 
@@ -1974,7 +2112,7 @@ int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32
     // the tracker bit is the context's (esc_tracker_update), whatever the caller packed
     const uint32_t mutable_bits = ESC_NF_UNSCHED | ESC_NF_TAINTED | ESC_NF_TRACKED;
     for (int64_t i = 0; i < n; ++i) {
-        if (ids[i] < 0 || ids[i] >= c->n_nodes) return ESC_E_INVAL;
+        if (ids[i] < 0 || ids[i] >= c->n_nodes || (c->h_nflags[ids[i]] & ESC_NF_ABSENT)) return ESC_E_INVAL;
         if ((flags[i] ^ c->h_nflags[ids[i]]) & ~mutable_bits) return ESC_E_INVAL;   // labels: reload
     }
     hipSetDevice(c->device);
@@ -1987,6 +2125,226 @@ int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32
         c->h_nmem[j] = mem[i];
     }
     return patch_nodes(c, touched);
+}
+
+// Node informer events that add or delete nodes (pkg/k8s/cache.go:37-56 feeds the
+// reference's node lister).  Added nodes take the next snapshot indices (listed after every
+// loaded node, so allNodes[0] and each pair's entries keep snapshot order), spare entries
+// of their label pairs (K2), and slots of their groups' K5 regions, inserted at their place
+// by creation time; a deleted node's slot becomes ESC_NF_ABSENT everywhere (no kernel
+// counts it) and its tracker entries are dropped.  All or nothing: ESC_E_LIMIT when the
+// spare room (esc_set_spare before esc_load_nodes) does not hold the batch.
+int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
+    if (!c || !s || s->n_nodes < 0 || (s->n_nodes > 0 && (!ids_out || !s->flags || !s->label0 || !s->cpu || !s->mem ||
+                                                          !s->created_ns)))
+        return ESC_E_INVAL;
+    if (s->n_trk != 0 || (s->n_xl > 0 && !s->xl_pair)) return ESC_E_INVAL;   // trackers: esc_tracker_update
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->nodes_loaded) return ESC_E_STATE;
+    const int64_t n = s->n_nodes;
+    if (n == 0) return ESC_OK;
+    if (c->n_nodes + n > c->n_cap || c->xl_used + s->n_xl > c->xl_cap) return ESC_E_LIMIT;
+    // validate, and count the spare room the batch needs (entries per pair, region slots)
+    const uint32_t n_gp = c->gi.n_gp;
+    std::vector<int64_t> xo(n);
+    std::vector<uint32_t> need_e(n_gp, 0);
+    std::unordered_map<uint32_t, uint32_t> need_r;
+    std::vector<uint32_t> mb;
+    uint64_t sx = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint32_t f = s->flags[i], nx = nf_xlbl(f);
+        if (f & (ESC_NF_TRACKED | ESC_NF_ABSENT)) return ESC_E_INVAL;
+        uint32_t last = s->label0[i];
+        if (last == NONE ? nx != 0 : last >= ESC_PAIR_LIMIT) return ESC_E_INVAL;
+        if (sx + nx > (uint64_t)s->n_xl) return ESC_E_INVAL;
+        for (uint32_t k = 0; k < nx; ++k) {
+            const uint32_t q = s->xl_pair[sx + k];
+            if (q >= ESC_PAIR_LIMIT || q <= last) return ESC_E_INVAL;
+            last = q;
+        }
+        xo[i] = (int64_t)sx;
+        auto count = [&](uint32_t q) {
+            if (q >= n_gp) return;
+            ++need_e[q];
+        };
+        count(s->label0[i]);
+        for (uint32_t k = 0; k < nx; ++k) count(s->xl_pair[sx + k]);
+        sx += nx;
+    }
+    if ((int64_t)sx != s->n_xl) return ESC_E_INVAL;
+    for (uint32_t q = 0; q < n_gp; ++q)
+        if (need_e[q] && c->pair_next[q] + need_e[q] > c->pair_end[q]) return ESC_E_LIMIT;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // the K5 regions this rank orders (the tail of the node table is the last rank's)
+    const bool k5 = c->tail_owner && c->n_gpad > 0;
+    if (k5) {
+        int32_t rc = ensure_gn(c);
+        if (rc) return rc;
+    }
+    // host mirrors of the new nodes (their memberships are read from these)
+    const int64_t j0 = c->n_nodes;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t j = j0 + i;
+        c->h_nflags[j] = s->flags[i];
+        c->h_ncpu[j] = s->cpu[i];
+        c->h_nmem[j] = s->mem[i];
+        c->h_label0[j] = s->label0[i];
+        c->h_xl_off[j] = (uint32_t)(c->xl_used + xo[i]);
+    }
+    if (k5) {
+        for (int64_t i = 0; i < n; ++i) {
+            node_membs_from(c, s->label0[i], nf_xlbl(s->flags[i]), s->xl_pair + xo[i], mb);
+            for (uint32_t m : mb) ++need_r[m & NODE_GROUP_MASK];
+        }
+        for (const auto& kv : need_r)
+            if ((int64_t)c->h_plen[kv.first] + kv.second > (int64_t)(c->h_pstart[kv.first + 1] - c->h_pstart[kv.first])) {
+                for (int64_t i = 0; i < n; ++i) c->h_nflags[j0 + i] = ESC_NF_ABSENT;   // undo
+                return ESC_E_LIMIT;
+            }
+    }
+    // commit: node table, extra labels, pair-major entries, allNodes[0]
+    c->h_xl.insert(c->h_xl.end(), s->xl_pair, s->xl_pair + s->n_xl);
+    Patches P;
+    bool first_changed = false;
+    std::vector<uint32_t> pairs;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t j = j0 + i;
+        const uint32_t f = s->flags[i];
+        P.add(NT_FLAGS, j, f);
+        P.add(NT_LABEL0, j, s->label0[i]);
+        P.add(NT_XLOFF, j, c->h_xl_off[j]);
+        P.add(NT_CPU, j, (uint64_t)s->cpu[i]);
+        P.add(NT_MEM, j, (uint64_t)s->mem[i]);
+        P.add(NT_CREATED, j, (uint64_t)s->created_ns[i]);
+        for (uint32_t k = 0; k < nf_xlbl(f); ++k) P.add(NT_XL, c->h_xl_off[j] + k, s->xl_pair[xo[i] + k]);
+        pairs.clear();
+        if (s->label0[i] < n_gp) pairs.push_back(s->label0[i]);
+        for (uint32_t k = 0; k < nf_xlbl(f); ++k)
+            if (s->xl_pair[xo[i] + k] < n_gp) pairs.push_back(s->xl_pair[xo[i] + k]);
+        for (uint32_t q : pairs) {
+            const uint32_t e = c->pair_next[q]++;
+            P.add(NT_EFLAGS, e, f);
+            P.add(NT_ENODE, e, (uint32_t)j);
+            P.add(NT_ECPU, e, (uint64_t)s->cpu[i]);
+            P.add(NT_EMEM, e, (uint64_t)s->mem[i]);
+            c->h_e_node[e] = (uint32_t)j;
+            c->ne_pos.push_back(e);
+            const uint32_t code = c->gi.node_code[q];
+            auto first_of = [&](uint32_t g) {
+                GroupNode& x = c->h_gnode[g];
+                if (x.first == INT64_MAX) {           // the group's first member (controller.go:208)
+                    x.first = j;
+                    x.first_cpu = s->cpu[i];
+                    x.first_mem = s->mem[i];
+                    first_changed = true;
+                }
+            };
+            if (code < CODE_MULTI) first_of(code & NODE_GROUP_MASK);
+            else if (code != NONE) {
+                const uint32_t* l = c->gi.code_list.data() + (code & ~CODE_MULTI);
+                for (uint32_t k = 1; k <= l[0]; ++k) first_of(l[k] & NODE_GROUP_MASK);
+            }
+        }
+        c->ne_off.push_back((uint32_t)c->ne_pos.size());
+        ids_out[i] = j;
+    }
+    c->xl_used += s->n_xl;
+    c->n_nodes += n;
+    c->placed = c->rm_valid = false;                 // esc_load_placement again (node runs)
+    int32_t rc = apply_patches(c, P, {node_targets(c)});
+    if (rc) return rc;
+    if (first_changed)
+        HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
+    if (k5) {
+        // K5: insert each new membership at its place by (creation time, index) in its
+        // group's region; every group touched is rewritten from its first insertion on
+        for (int64_t i = 0; i < n; ++i) c->h_created.push_back(s->created_ns[i]);
+        c->node_hi = c->n_nodes;
+        std::unordered_map<uint32_t, std::vector<uint32_t>> add_by_g;
+        for (int64_t i = 0; i < n; ++i) {
+            node_membs(c, j0 + i, mb);
+            for (uint32_t m : mb) add_by_g[m & NODE_GROUP_MASK].push_back((uint32_t)(j0 + i));
+        }
+        auto less = [&](uint32_t x, uint32_t y) {
+            const int64_t tx = created_of(c, x), ty = created_of(c, y);
+            return tx < ty || (tx == ty && x < y);
+        };
+        std::vector<uint32_t> buf_n, buf_g, buf_f;
+        for (auto& kv : add_by_g) {
+            const uint32_t g = kv.first;
+            std::vector<uint32_t>& nw = kv.second;
+            std::sort(nw.begin(), nw.end(), less);
+            const uint32_t a = c->h_pstart[g], len = c->h_plen[g];
+            uint32_t* run = c->h_gn.data() + a;
+            const uint32_t from = (uint32_t)(std::upper_bound(run, run + len, nw.front(), less) - run);
+            std::vector<uint32_t> merged(len - from + nw.size());
+            std::merge(run + from, run + len, nw.begin(), nw.end(), merged.begin(), less);
+            std::copy(merged.begin(), merged.end(), run + from);
+            c->h_plen[g] = len + (uint32_t)nw.size();
+            const uint32_t mbit = (uint32_t)g | (c->params[g].dry ? NODE_DRY_BIT : 0u);
+            buf_n.assign(merged.begin(), merged.end());
+            buf_g.assign(merged.size(), mbit);
+            buf_f.resize(merged.size());
+            for (size_t k = 0; k < merged.size(); ++k)
+                buf_f[k] = (c->h_nflags[merged[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT : memb_flags(c, merged[k], mbit);
+            const size_t bytes = merged.size() * 4;
+            HIP_TRY(hipMemcpyAsync(c->d_g_node + a + from, buf_n.data(), bytes, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(hipMemcpyAsync(c->d_g_grp + a + from, buf_g.data(), bytes, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(hipMemcpyAsync(c->d_g_flags + a + from, buf_f.data(), bytes, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+        }
+    }
+    c->sorted = false;
+    return ESC_OK;
+}
+
+int32_t esc_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
+    if (!c || n < 0 || (n > 0 && !ids)) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->nodes_loaded) return ESC_E_STATE;
+    std::vector<int64_t> del(ids, ids + n);
+    std::sort(del.begin(), del.end());
+    if (std::adjacent_find(del.begin(), del.end()) != del.end()) return ESC_E_INVAL;
+    for (int64_t j : del)
+        if (j < 0 || j >= c->n_nodes || (c->h_nflags[j] & ESC_NF_ABSENT)) return ESC_E_INVAL;
+    if (n == 0) return ESC_OK;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // tracker entries of the deleted nodes go (a re-added name is re-tracked by the host)
+    std::vector<uint64_t> next;
+    next.reserve(c->h_trk.size());
+    for (uint64_t k : c->h_trk)
+        if (!std::binary_search(del.begin(), del.end(), (int64_t)(k >> 32))) next.push_back(k);
+    if (next.size() != c->h_trk.size()) {
+        int32_t rc = write_tracker(c, next);
+        if (rc) return rc;
+    }
+    for (int64_t j : del) c->h_nflags[j] = (c->h_nflags[j] & ~ESC_NF_TRACKED) | ESC_NF_ABSENT;
+    // allNodes[0] of the groups whose first member went: the next live entry of the pair
+    bool first_changed = false;
+    for (int32_t g = 0; g < c->gi.G; ++g) {
+        GroupNode& x = c->h_gnode[g];
+        if (x.first == INT64_MAX || !(c->h_nflags[x.first] & ESC_NF_ABSENT)) continue;
+        const uint32_t q = c->gi.gpair[g];
+        const uint32_t a = c->nodes_piece_lo(q), z = c->pair_next.empty() ? a : c->pair_next[q];
+        x.first = INT64_MAX;
+        x.first_cpu = x.first_mem = 0;
+        for (uint32_t e = a; e < z; ++e) {
+            const uint32_t j = c->h_e_node[e];
+            if (j != NONE && !(c->h_nflags[j] & ESC_NF_ABSENT)) {
+                x.first = j;
+                x.first_cpu = c->h_ncpu[j];
+                x.first_mem = c->h_nmem[j];
+                break;
+            }
+        }
+        first_changed = true;
+    }
+    if (first_changed)
+        HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
+    c->placed = c->rm_valid = false;
+    return patch_nodes(c, del);
 }
 
 // Dry-mode taintTracker bookkeeping (§8f rank 4).  The reference keeps per group a slice
@@ -2004,7 +2362,8 @@ int32_t esc_tracker_update(esc_ctx* c, int32_t group, const int64_t* add, int64_
     if (group < 0 || group >= c->gi.G) return ESC_E_INVAL;
     auto key = [&](int64_t j) { return ((uint64_t)(uint32_t)j << 32) | (uint32_t)group; };
     for (int64_t i = 0; i < n_rm; ++i) if (rm[i] < 0 || rm[i] >= c->n_nodes) return ESC_E_INVAL;
-    for (int64_t i = 0; i < n_add; ++i) if (add[i] < 0 || add[i] >= c->n_nodes) return ESC_E_INVAL;
+    for (int64_t i = 0; i < n_add; ++i)
+        if (add[i] < 0 || add[i] >= c->n_nodes || (c->h_nflags[add[i]] & ESC_NF_ABSENT)) return ESC_E_INVAL;
     // removals first (absent names are ignored, as untaintNewestN's deleteIndex == -1), then
     // additions (a node already tracked by the group, or added twice, is refused: the
     // reference only appends untainted, i.e. untracked, nodes)
@@ -2026,50 +2385,28 @@ int32_t esc_tracker_update(esc_ctx* c, int32_t group, const int64_t* add, int64_
     for (uint64_t k : ak) touched.push_back((int64_t)(k >> 32));
     std::vector<uint64_t> next(kept.size() + ak.size());
     std::merge(kept.begin(), kept.end(), ak.begin(), ak.end(), next.begin());
-    const int64_t nt = (int64_t)next.size();
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    NodeBuf& b = c->nodes;
-    if (nt > c->trk_cap) {
-        const int64_t cap = std::max<int64_t>({nt, 2 * c->trk_cap, 1024});
-        dfree(b.trk_node); dfree(b.trk_group);
-        b.trk_node = nullptr; b.trk_group = nullptr;
-        HIP_TRY(dalloc(&b.trk_node, cap)); HIP_TRY(dalloc(&b.trk_group, cap));
-        c->trk_cap = cap;
-    }
-    std::vector<int32_t> tn(std::max<int64_t>(nt, 1)), tg(std::max<int64_t>(nt, 1));
-    std::vector<uint32_t> ts(std::max<int64_t>(c->n_nodes, 1), NONE);
-    for (int64_t k = nt - 1; k >= 0; --k) {
-        tn[k] = (int32_t)(next[k] >> 32);
-        tg[k] = (int32_t)(uint32_t)next[k];
-        ts[tn[k]] = (uint32_t)k;
-    }
-    if (nt) {
-        HIP_TRY(hipMemcpy(b.trk_node, tn.data(), nt * 4, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(b.trk_group, tg.data(), nt * 4, hipMemcpyHostToDevice));
-    }
-    HIP_TRY(hipMemcpy(b.trk_start, ts.data(), ts.size() * 4, hipMemcpyHostToDevice));
-    c->h_trk.swap(next);
-    c->n_trk = nt;
-    drop_graphs(c);                                  // K2's grid and NodeDev carry n_trk
+    int32_t rc = write_tracker(c, next);
+    if (rc) return rc;
     // ESC_NF_TRACKED = tracked by some group (controller.go:128 is per group; the kernels
     // confirm the group through the list)
     std::vector<int64_t> flip;
     std::sort(touched.begin(), touched.end());
     touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
     for (int64_t j : touched) {
-        const bool on = ts[j] != NONE;
+        const uint64_t lo = (uint64_t)(uint32_t)j << 32;
+        const auto it = std::lower_bound(c->h_trk.begin(), c->h_trk.end(), lo);
+        const bool on = it != c->h_trk.end() && (*it >> 32) == (uint64_t)(uint32_t)j;
         const uint32_t f = on ? (c->h_nflags[j] | ESC_NF_TRACKED) : (c->h_nflags[j] & ~ESC_NF_TRACKED);
         if (f != c->h_nflags[j]) { c->h_nflags[j] = f; flip.push_back(j); }
     }
     c->sorted = false;
     c->rm_valid = false;
-    if (!flip.empty()) return patch_nodes(c, flip);        // re-lists the memberships too
-    // the K5 membership copies carry each dry membership's tracker bit: re-list them
-    HIP_TRY(launch_memb_expand(node_dev(c), group_dev(c), c->d_age, c->memb_blocks, c->d_cnt, c->d_e_node,
-                               c->d_e_grp, c->d_e_flags, c->stream));
-    HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
-                                c->d_g_grp, c->d_g_flags, c->stream));
+    if (!flip.empty()) return patch_nodes(c, touched);     // node table + entries + K5 copies
+    // the K5 copies carry each dry membership's tracker bit: patch the touched nodes'
+    rc = patch_regions(c, touched);
+    if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
     return ESC_OK;
 }

@@ -401,11 +401,24 @@ int32_t esc_stage_times(esc_ctx* ctx, double* ms_out, int32_t n);
  * change Spec.Unschedulable, the escalator taint and allocatable; label or creation-time
  * changes need esc_load_nodes (tracker changes: esc_tracker_update).  Every call
  * completes before returning.                                                       */
-int32_t esc_set_spare(esc_ctx* ctx, double fraction);       /* spare slots per K class, e.g. 0.05 */
+int32_t esc_set_spare(esc_ctx* ctx, double fraction);       /* spare room: per K pod class (esc_load_pods),
+                                                                node slots / entries / K5 regions (esc_load_nodes) */
 int32_t esc_pods_upsert(esc_ctx* ctx, const int64_t* ids, const esc_pod_soa* pods);
 int32_t esc_pods_delete(esc_ctx* ctx, const int64_t* ids, int64_t n);
 int32_t esc_nodes_update(esc_ctx* ctx, const int64_t* ids, int64_t n, const uint32_t* flags,
                          const int64_t* cpu_m, const int64_t* mem_b);
+/* Node additions and deletions (the node informer's Add / Delete, pkg/k8s/cache.go:37-56)
+ * in place.  esc_set_spare(f) before esc_load_nodes reserves room: table slots, spare
+ * pair-major entries per group label pair and spare slots in every group's K5 region.
+ * esc_nodes_add appends the nodes (packed like esc_load_nodes' input, n_trk = 0, no
+ * ESC_NF_TRACKED) at the next snapshot indices, returned in ids_out: the lister order
+ * lists them after every loaded node.  esc_nodes_delete removes nodes by index: the slot
+ * becomes ESC_NF_ABSENT (no kernel counts it, allNodes[0] moves to the group's next
+ * member) and its dry-mode tracker entries are dropped (a host that re-adds a tracked
+ * name re-applies it with esc_tracker_update).  Both invalidate esc_load_placement; an
+ * add that does not fit returns ESC_E_LIMIT with nothing applied (reload). */
+int32_t esc_nodes_add(esc_ctx* ctx, const esc_node_soa* nodes, int64_t* ids_out);
+int32_t esc_nodes_delete(esc_ctx* ctx, const int64_t* ids, int64_t n);
 
 /* ------------------------------------------- dry-mode taintTracker (§8f rank 4)
  * nodeGroup.taintTracker (controller.go:35) as interned (node, group) pairs on the

@@ -310,6 +310,117 @@ def test_order_in_step_vs_c_oracle(esc, graph, N):
             assert np.array_equal(ctx.group_order(g, which), full[(g, which)]), (g, which)
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_node_add_delete_vs_literal(esc, seed):
+    """Node informer Add / Delete events in place (esc_nodes_add / esc_nodes_delete): after
+    every round of deletions and additions (creation times older, newer and equal to the
+    loaded ones), the totals, allNodes[0], decisions and both orderings equal the literal
+    oracle over the live nodes in snapshot order; half the seeds decide through the graph
+    with the ordering in the step."""
+    rng = random.Random(9100 + seed)
+    G = rng.choice([3, 8, 20])
+    groups = make_groups(rng, G, with_default=rng.random() < 0.6)
+    pods = make_pods(rng, 300, groups, big_frac=0.0)
+    nodes = make_nodes(rng, rng.choice([40, 120]), groups, big_frac=0.0)
+    trackers = make_trackers(rng, groups, nodes)
+    states = make_states(rng, G)
+    ctx = esc.Context(groups)
+    ctx.set_spare(1.0)
+    P, N = ctx.pack(pods, nodes, trackers)
+    ctx.load(P, N)
+    in_step = seed % 2 == 1
+    if in_step:
+        ctx.use_graph(True)
+        ctx.set_order_in_step(True)
+    live = dict(enumerate(nodes))
+    pflags = {j: int(N["flags"][j]) for j in live}
+    hw = base = len(nodes)
+    for rnd in range(5):
+        dels = rng.sample(sorted(live), k=min(len(live), rng.randrange(0, 12)))
+        if dels:
+            ctx.nodes_delete(dels)
+            for j in dels:
+                del live[j]
+        new = make_nodes(rng, rng.randrange(0, 14), groups, big_frac=0.0)
+        for k, nd in enumerate(new):
+            nd["name"] = "r%d-new%d" % (rnd, k)
+        if new:
+            _, packed = ctx.pack([], new)
+            try:
+                ids = ctx.nodes_add(packed)
+            except esc._lib.EscError as e:                            # spare room short: reload
+                assert e.code == esc._lib.ESC_E_LIMIT
+                lst = [live[j] for j in sorted(live)] + new
+                P, N = ctx.pack(pods, lst, trackers)
+                ctx.load(P, N)
+                live = dict(enumerate(lst))
+                pflags = {j: int(N["flags"][j]) for j in live}
+                hw = base = len(lst)
+            else:
+                assert list(ids) == list(range(hw, hw + len(new)))      # next snapshot indices
+                hw += len(new)
+                for k, (j, nd) in enumerate(zip(ids, new)):
+                    live[int(j)] = nd
+                    pflags[int(j)] = int(packed["flags"][k])
+        idx = sorted(live)
+        lst = [live[j] for j in idx]
+        tot, dec = ctx.decide_all(states)
+        if not in_step:
+            ctx.sort_nodes()
+        for g in range(G):
+            L = O.scale_node_group(groups[g], states[g], pods, lst, tracker=trackers.get(g, []))
+            t, d = tot[g], dec[g]
+            first = idx[L["first_node"]] if L["first_node"] >= 0 else -1
+            assert (t["n_pods"], t["n_nodes"], t["n_untainted"], t["n_tainted"], t["n_cordoned"], t["first_node"]) == \
+                (L["n_pods"], L["n_nodes"], L["n_untainted"], L["n_tainted"], L["n_cordoned"], first), (rnd, g)
+            if L["pod_cpu_m"] is not None:
+                assert (t["node_cpu_m"], t["node_mem_b"]) == (L["node_cpu_m"], L["node_mem_b"]), (rnd, g)
+            assert esc._lib.BRANCHES[d["branch"]] == L["branch"], (rnd, g)
+            assert int(d["delta"]) == L["delta"] and int(d["n_to_taint"]) == L["n_to_taint"], (rnd, g)
+            assert _bits(d["cpu_pct"]) == _bits(L["cpu_pct"]) and _bits(d["mem_pct"]) == _bits(L["mem_pct"])
+            assert (int(d["cached_cpu_m"]), int(d["cached_mem_b"])) == (L["cached_cpu_m"], L["cached_mem_b"])
+            unt, tn = L["untainted"], L["tainted"]
+            assert list(ctx.group_order(g, 0)) == \
+                [idx[unt[i]] for i in O.oldest_first([lst[k]["created_ns"] for k in unt])], (rnd, g)
+            assert list(ctx.group_order(g, 1)) == \
+                [idx[tn[i]] for i in O.newest_first([lst[k]["created_ns"] for k in tn])], (rnd, g)
+    # cordon / taint updates of added nodes, then a full rebuild of the age index agrees
+    added = [j for j in live if j >= base]
+    if added:
+        flags = np.array([pflags[j] | 2 for j in added], np.uint32)      # + the escalator taint
+        cpu = np.array([live[j].get("cpu") or 0 for j in added], np.int64)
+        mem = np.array([live[j].get("mem") or 0 for j in added], np.int64)
+        ctx.nodes_update(np.array(added, np.int64), flags, cpu, mem)
+        for j in added:
+            live[j] = dict(live[j], taints=["atlassian.com/escalator"])
+        ctx.decide_all(states)
+        if not in_step:
+            ctx.sort_nodes()
+        before = {(g, w): list(ctx.group_order(g, w)) for g in range(G) for w in (0, 1)}
+        ctx.build_age_index()
+        ctx.sort_nodes()
+        assert before == {(g, w): list(ctx.group_order(g, w)) for g in range(G) for w in (0, 1)}
+
+
+def test_node_add_limit_all_or_nothing(esc):
+    """A batch that does not fit the spare room is refused whole (ESC_E_LIMIT)."""
+    groups = [{"name": "a", "label_key": "k", "label_value": "v", "max_nodes": 1000}]
+    nodes = [{"name": "n%d" % i, "labels": {"k": "v"}, "cpu": 1000, "mem": 1000, "created_ns": i} for i in range(8)]
+    ctx = esc.Context(groups)
+    ctx.set_spare(0.01)
+    ctx.load(*ctx.pack([], nodes))
+    more = [{"name": "m%d" % i, "labels": {"k": "v"}, "cpu": 1, "mem": 1, "created_ns": 100 + i} for i in range(64)]
+    _, packed = ctx.pack([], more)
+    with pytest.raises(esc._lib.EscError):
+        ctx.nodes_add(packed)
+    tot, _ = ctx.decide_all()
+    assert tot["n_nodes"][0] == 8 and tot["node_cpu_m"][0] == 8000
+    _, packed = ctx.pack([], more[:3])
+    assert list(ctx.nodes_add(packed)) == [8, 9, 10]
+    tot, _ = ctx.decide_all()
+    assert tot["n_nodes"][0] == 11 and tot["node_cpu_m"][0] == 8003
+
+
 def _members_oldest(nodes, groups, g):
     """All members of dry group g, oldest first (ties by index): the oracle's two lists merged."""
     both = list(soa.order(nodes, groups, g, 0)) + list(soa.order(nodes, groups, g, 1))
