@@ -2270,7 +2270,7 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
             const int64_t tx = created_of(c, x), ty = created_of(c, y);
             return tx < ty || (tx == ty && x < y);
         };
-        std::vector<uint32_t> buf_n, buf_g, buf_f;
+        Patches R;                                   // one scatter for every touched region
         for (auto& kv : add_by_g) {
             const uint32_t g = kv.first;
             std::vector<uint32_t>& nw = kv.second;
@@ -2283,17 +2283,17 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
             std::copy(merged.begin(), merged.end(), run + from);
             c->h_plen[g] = len + (uint32_t)nw.size();
             const uint32_t mbit = (uint32_t)g | (c->params[g].dry ? NODE_DRY_BIT : 0u);
-            buf_n.assign(merged.begin(), merged.end());
-            buf_g.assign(merged.size(), mbit);
-            buf_f.resize(merged.size());
-            for (size_t k = 0; k < merged.size(); ++k)
-                buf_f[k] = (c->h_nflags[merged[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT : memb_flags(c, merged[k], mbit);
-            const size_t bytes = merged.size() * 4;
-            HIP_TRY(hipMemcpyAsync(c->d_g_node + a + from, buf_n.data(), bytes, hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(hipMemcpyAsync(c->d_g_grp + a + from, buf_g.data(), bytes, hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(hipMemcpyAsync(c->d_g_flags + a + from, buf_f.data(), bytes, hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
+            for (size_t k = 0; k < merged.size(); ++k) {
+                const int64_t pos = (int64_t)a + from + (int64_t)k;
+                R.add(0, pos, merged[k]);
+                R.add(1, pos, mbit);
+                R.add(2, pos, (c->h_nflags[merged[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT : memb_flags(c, merged[k], mbit));
+            }
         }
+        PatchTargets t{};
+        t.u32[0] = c->d_g_node; t.u32[1] = c->d_g_grp; t.u32[2] = c->d_g_flags;
+        rc = apply_patches(c, R, {t});
+        if (rc) return rc;
     }
     c->sorted = false;
     return ESC_OK;

@@ -8,7 +8,8 @@ times (a) batches of in-place pod upserts (the pods' own records re-sent under t
 the common "status changed" event), (b) batches of deletes followed by re-inserts of the
 same records (slot recycling), (c) node taint / allocatable updates, and (d) one full
 decision after the events; the decision is checked bit-exact against the C oracle on the
-unchanged snapshot content.  Prints one JSON line."""
+unchanged snapshot content.  Then (e) node deletions and additions (the same records
+re-added as new nodes).  Prints one JSON line."""
 import argparse
 import json
 import os
@@ -26,6 +27,7 @@ def main():
     ap.add_argument("--pods", type=int, default=100_000_000)
     ap.add_argument("--batch", type=int, default=1_000_000)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--node-batch", type=int, default=1000)
     args = ap.parse_args()
     import escalator_amd as esc
     from oracle import soa
@@ -33,7 +35,7 @@ def main():
     s = esc.Synth(P, N, G, config=4, seed=0xE5CA1A7E00000004, threads=16)
     pods, nodes = s.pods(), s.nodes()
     ctx = esc.Context(s)
-    ctx.set_spare(0.05)
+    ctx.set_spare(0.05)                               # pod classes, node slots / entries / K5 regions
     t0 = time.perf_counter()
     ctx.load_synth(s)
     load_s = time.perf_counter() - t0
@@ -76,12 +78,52 @@ def main():
     odf, odi = soa.decide(s.groups, s.states, otot)
     ok = all(np.array_equal(tot[n], otot[:, k]) for k, n in enumerate(soa.TOT_FIELDS[:12]))
     ok &= np.array_equal(dec["delta"], odi[:, 0])
+    # node informer Add / Delete (esc_nodes_add / esc_nodes_delete): delete a batch of nodes,
+    # then add the same records back as new nodes (next snapshot indices); parity of these
+    # rounds is covered by tests/test_gpu.py::test_node_add_delete_vs_literal
+    xo = np.concatenate([[0], np.cumsum((nodes["flags"].astype(np.int64) >> 8) & 0xFF)]).astype(np.int64)
+
+    def node_subset(idx):
+        out = {k: nodes[k][idx] for k in ("flags", "label0", "cpu", "mem", "created_ns")}
+        out["flags"] = out["flags"] & ~np.uint32(4)              # the tracker bit is the context's
+        xi = np.concatenate([np.arange(xo[i], xo[i + 1]) for i in idx]) if len(idx) else np.zeros(0, np.int64)
+        out["xl_pair"] = nodes["xl_pair"][xi]
+        out["trk_node"] = np.zeros(0, np.int32)
+        out["trk_group"] = np.zeros(0, np.int32)
+        return out
+
+    nb = max(1, args.node_batch)
+    live, src = np.arange(N), np.arange(N)            # snapshot index, record it holds
+    res["node_delete_s"], res["node_add_s"] = [], []
+    for r in range(args.rounds + 1):                  # round 0 warms the host mirrors
+        pick = np.sort(rng.choice(len(live), size=nb, replace=False))
+        ids = live[pick]
+        rec = node_subset(src[pick])
+        t0 = time.perf_counter()
+        ctx.nodes_delete(ids)
+        t_del = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        new = ctx.nodes_add(rec)
+        t_add = time.perf_counter() - t0
+        live = np.concatenate([np.delete(live, pick), new])
+        src = np.concatenate([np.delete(src, pick), src[pick]])
+        if r:
+            res["node_delete_s"].append(t_del)
+            res["node_add_s"].append(t_add)
+    t0 = time.perf_counter()
+    ctx.run()
+    ctx.sync()
+    decide_after_s = time.perf_counter() - t0
     out = {"metric": "incremental snapshot events applied per second (config 4 resident)",
            "pods": P, "batch": args.batch, "full_load_s": load_s,
            "pod_upserts_per_s": args.batch / float(np.median(res["upsert_in_place_s"])),
            "pod_deletes_per_s": args.batch / float(np.median(res["delete_s"])),
            "pod_reinserts_per_s": args.batch / float(np.median(res["reinsert_s"])),
            "node_updates_per_s": (args.batch // 10) / float(np.median(res["node_update_s"])),
+           "node_batch": nb,
+           "node_deletes_per_s": nb / float(np.median(res["node_delete_s"])),
+           "node_adds_per_s": nb / float(np.median(res["node_add_s"])),
+           "decision_after_node_events_s": decide_after_s,
            "raw_s": res,
            "parity_after_events": "bit-exact vs C oracle (10000 groups)" if ok else "MISMATCH"}
     print(json.dumps(out), flush=True)
