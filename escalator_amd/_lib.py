@@ -162,6 +162,12 @@ _SIGS = {
     "esc_tracker_list": (i32, [VP, i32, P(i64), i64, P(i64)]),
     "esc_load_placement": (i32, [VP, P(u32), P(i64), P(C.c_uint8)]),
     "esc_try_remove": (i32, [VP, i64, P(i64), P(i64), P(Removal)]),
+    "esc_pods_bind": (i32, [VP, P(i64), P(u32), i64]),
+    "esc_reap_occupancy": (i32, [VP]),
+    "esc_reap_buffer": (i32, [VP, P(VP), P(i64)]),
+    "esc_reap_download": (i32, [VP, P(u32)]),
+    "esc_reap_upload": (i32, [VP, P(u32)]),
+    "esc_reap_finish": (i32, [VP, i64, P(i64), P(i64), P(Removal)]),
     "esc_removal_nodes": (i32, [VP, i32, P(i64), i64, P(i64)]),
     "esc_set_metrics": (i32, [VP, i32]),
     "esc_metrics_results": (i32, [VP, P(GroupMetrics)]),

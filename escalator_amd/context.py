@@ -364,6 +364,37 @@ class Context:
                                         out.ctypes.data_as(C.POINTER(L.Removal))), "esc_try_remove")
         return out
 
+    def pods_bind(self, ids, pod_node):
+        """Spec.NodeName changes of pods (node index, NONE = unbound): the placement follows."""
+        ids = np.ascontiguousarray(ids, np.int64)
+        pn = np.ascontiguousarray(pod_node, np.uint32)
+        L.check(self.lib.esc_pods_bind(self.handle, ids.ctypes.data_as(C.POINTER(C.c_int64)),
+                                       pn.ctypes.data_as(C.POINTER(C.c_uint32)), len(ids)), "esc_pods_bind")
+
+    # the sharded reaping steps (esc_try_remove does all three, with the RCCL sum)
+    def reap_occupancy(self):
+        L.check(self.lib.esc_reap_occupancy(self.handle), "esc_reap_occupancy")
+
+    def reap_download(self) -> np.ndarray:
+        buf, n = C.c_void_p(), C.c_int64()
+        L.check(self.lib.esc_reap_buffer(self.handle, C.byref(buf), C.byref(n)), "esc_reap_buffer")
+        out = np.zeros(max(n.value, 1), np.uint32)
+        L.check(self.lib.esc_reap_download(self.handle, out.ctypes.data_as(C.POINTER(C.c_uint32))), "esc_reap_download")
+        return out[:n.value]
+
+    def reap_upload(self, words):
+        w = np.ascontiguousarray(words, np.uint32)
+        L.check(self.lib.esc_reap_upload(self.handle, w.ctypes.data_as(C.POINTER(C.c_uint32))), "esc_reap_upload")
+
+    def reap_finish(self, now_ns: int, soft_ns, hard_ns) -> np.ndarray:
+        s_ = np.ascontiguousarray(np.broadcast_to(np.asarray(soft_ns, np.int64), (self.G,)))
+        h_ = np.ascontiguousarray(np.broadcast_to(np.asarray(hard_ns, np.int64), (self.G,)))
+        out = np.zeros(self.G, REMOVAL_DTYPE)
+        L.check(self.lib.esc_reap_finish(self.handle, int(now_ns), s_.ctypes.data_as(C.POINTER(C.c_int64)),
+                                         h_.ctypes.data_as(C.POINTER(C.c_int64)),
+                                         out.ctypes.data_as(C.POINTER(L.Removal))), "esc_reap_finish")
+        return out
+
     def removal_nodes(self, group: int) -> np.ndarray:
         """Snapshot indices of the nodes the last try_remove deletes for `group`, in order."""
         n = C.c_int64()

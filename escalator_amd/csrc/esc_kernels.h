@@ -190,7 +190,8 @@ struct RemovalDev {
     const uint8_t* no_delete;  // [n_nodes]
     const uint32_t* e_pair;    // [n_entries] pair of each pair-major entry
     int64_t n_entries;
-    const uint32_t* nrun_off;  // [n_nodes + 1] runs of PodRef per node
+    const uint32_t* nrun_off;  // [n_nodes + 1] runs of PodRef per node (capacity)
+    const uint32_t* nrun_len;  // [n_nodes] PodRefs in each run
     const PodRef* refs;
     const uint32_t* xp;        // C-pod extra pairs (indirect refs)
     uint32_t* occ_pair;        // [entries] group pods on the node, by the entry's pair
@@ -202,8 +203,10 @@ struct RemovalDev {
     esc_removal* out;          // [G]
     int64_t now_ns;
 };
-hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, int64_t n, PodRef* refs, hipStream_t st);
-hipError_t launch_try_remove(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st);
+hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, const uint32_t* run_pos, int64_t n, PodRef* refs,
+                              hipStream_t st);
+hipError_t launch_occupancy(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st);   // K6
+hipError_t launch_try_remove(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st);  // K7
 
 struct PatchTargets {          // k_patch destinations: 4-byte arrays 0-5, 8-byte arrays 6-11
     uint32_t* u32[6];

@@ -2004,10 +2004,12 @@ __device__ __forceinline__ int64_t go_sub_ns(int64_t now_ns, int64_t t_s) {
 }
 }  // namespace
 
+// PodRef of the pod in each listed slot, at position i (a whole placement) or run_pos[i]
+// (pod events patching runs in place).
 __global__ __launch_bounds__(256) void k_podref_fill(PodDev P, const uint32_t* __restrict__ run_slot, int64_t n,
-                                                     PodRef* __restrict__ refs) {
+                                                     const uint32_t* __restrict__ run_pos, PodRef* __restrict__ refs) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) refs[i] = podref_of(P, run_slot[i]);
+    if (i < n) refs[run_pos ? (int64_t)run_pos[i] : i] = podref_of(P, run_slot[i]);
 }
 
 // K6: one wave per 64 pair-major entries; the entries whose node is escalator-tainted and
@@ -2027,6 +2029,7 @@ __global__ __launch_bounds__(256) void k_occupancy(NodeDev N, GroupDev G, Remova
         q = R.e_pair[e];
         j = N.e_node[e];
         want = q < G.n_gp && (f & ESC_NF_TAINTED) && !(f & (ESC_NF_UNSCHED | ESC_NF_ABSENT));
+        if (!want) { R.occ_pair[e] = 0; R.occ_def[e] = 0; }   // defined words for the cross-rank SUM
     }
     unsigned long long m = __ballot(want);
     while (m) {
@@ -2034,7 +2037,7 @@ __global__ __launch_bounds__(256) void k_occupancy(NodeDev N, GroupDev G, Remova
         m &= m - 1;
         const uint32_t jk = __shfl(j, k, 64), qk = __shfl(q, k, 64);
         uint32_t cp = 0, cd = 0;
-        for (uint32_t i = R.nrun_off[jk] + lane; i < R.nrun_off[jk + 1]; i += 64) {
+        for (uint32_t i = R.nrun_off[jk] + lane; i < R.nrun_off[jk] + R.nrun_len[jk]; i += 64) {
             const PodRef r = R.refs[i];
             if (r.flags & ESC_PF_DAEMONSET) continue;
             cp += podref_has(r, R.xp, qk) ? 1u : 0u;
@@ -2120,15 +2123,20 @@ hipError_t launch_fold_decide(const GroupDev& g, const NodeDev& n, const FoldPla
     return hipGetLastError();
 }
 
-hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, int64_t n, PodRef* refs, hipStream_t st) {
+hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, const uint32_t* run_pos, int64_t n, PodRef* refs,
+                              hipStream_t st) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_podref_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, run_slot, n, refs);
+    hipLaunchKernelGGL(k_podref_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, run_slot, n, run_pos, refs);
+    return hipGetLastError();
+}
+
+hipError_t launch_occupancy(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st) {
+    if (r.n_entries > 0)
+        hipLaunchKernelGGL(k_occupancy, dim3((unsigned)((r.n_entries + 255) / 256)), dim3(256), 0, st, n, g, r);
     return hipGetLastError();
 }
 
 hipError_t launch_try_remove(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st) {
-    if (r.n_entries > 0)
-        hipLaunchKernelGGL(k_occupancy, dim3((unsigned)((r.n_entries + 255) / 256)), dim3(256), 0, st, n, g, r);
     hipLaunchKernelGGL(k_try_remove, dim3(g.G), dim3(64), 0, st, n, g, r);
     return hipGetLastError();
 }

@@ -261,14 +261,20 @@ struct esc_ctx {
     bool node_removal = false;                                // taint times / no-delete loaded
     PodRef* d_refs = nullptr;
     uint32_t* d_e_pair = nullptr;
-    uint32_t *d_nrun_off = nullptr, *d_occ_pair = nullptr, *d_occ_def = nullptr, *d_rm_off = nullptr,
-             *d_rm_list = nullptr;
+    uint32_t *d_nrun_off = nullptr, *d_nrun_len = nullptr, *d_occ = nullptr, *d_rm_off = nullptr,
+             *d_rm_list = nullptr;                             // d_occ: [2][n_entries] (pair, default)
+    // host mirror of the placement: runs per node (capacity offsets, lengths), the pod at
+    // each run position, each pod's node and run position (pod events keep them current)
+    std::vector<uint32_t> h_run_off, h_run_len, h_pod_node;
+    std::vector<int32_t> h_run_pod;
+    std::vector<int64_t> h_pod_rpos;
     int64_t *d_taint_s = nullptr, *d_soft = nullptr, *d_hard = nullptr;
     uint8_t* d_no_delete = nullptr;
     esc_removal* d_rm_out = nullptr;
     std::vector<uint32_t> h_rm_off;                           // [G + 1]
     std::vector<esc_removal> h_rm;
     bool rm_valid = false;                                    // esc_try_remove results current
+    int64_t rm_nodes = -1;                                    // node count the reaping buffers are sized for
 };
 
 namespace esc {
@@ -396,7 +402,7 @@ void release_work(esc_ctx* c) {
 }
 
 void release_placement(esc_ctx* c) {
-    dfree(c->d_refs); dfree(c->d_e_pair); dfree(c->d_nrun_off); dfree(c->d_occ_pair); dfree(c->d_occ_def); dfree(c->d_rm_off);
+    dfree(c->d_refs); dfree(c->d_e_pair); dfree(c->d_nrun_off); dfree(c->d_nrun_len); dfree(c->d_occ); dfree(c->d_rm_off);
     dfree(c->d_rm_list); dfree(c->d_taint_s); dfree(c->d_soft); dfree(c->d_hard); dfree(c->d_no_delete);
     dfree(c->d_rm_out);
     c->placed = c->node_removal = c->rm_valid = false;
@@ -1820,6 +1826,91 @@ void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
     --c->live_pods;
 }
 
+// Device slot of live pod `id` in the resident layout (K section: class tiles; C section:
+// its position).
+int64_t pod_slot(const esc_ctx* c, int64_t id) {
+    const int32_t ci = c->pod_cls[id];
+    const int64_t d = c->pod_pos[id];
+    return ci >= 0 ? (c->h_cls[ci].t0 + d / TILE) * TILE + d % TILE : d;
+}
+
+RemovalDev removal_dev(const esc_ctx* c, int64_t now_ns) {
+    RemovalDev r;
+    r.e_pair = c->d_e_pair; r.n_entries = c->n_entries;
+    r.taint_s = c->d_taint_s; r.no_delete = c->d_no_delete;
+    r.nrun_off = c->d_nrun_off; r.nrun_len = c->d_nrun_len; r.refs = c->d_refs;
+    r.xp = c->pods[c->cur].xp;
+    r.occ_pair = c->d_occ; r.occ_def = c->d_occ + std::max<int64_t>(c->n_entries, 0);
+    r.soft_ns = c->d_soft; r.hard_ns = c->d_hard;
+    r.rm_off = c->d_rm_off; r.rm_list = c->d_rm_list; r.out = c->d_rm_out; r.now_ns = now_ns;
+    return r;
+}
+
+// Placement upkeep under pod events (§8f rank 2): a bound pod's PodRef lives in its node's
+// run; removal swaps the run's last PodRef into the hole, binding appends.  `touched`
+// collects pods whose PodRef must be (re)written (new position or new slot), `runs` the
+// nodes whose run length changed; sync_placement writes both after the pod data patches.
+void run_remove(esc_ctx* c, int64_t id, std::vector<int64_t>& touched, std::vector<uint32_t>& runs) {
+    if (id >= (int64_t)c->h_pod_rpos.size() || c->h_pod_rpos[id] < 0) return;
+    const uint32_t j = c->h_pod_node[id];
+    const int64_t pos = c->h_pod_rpos[id], last = (int64_t)c->h_run_off[j] + c->h_run_len[j] - 1;
+    if (pos != last) {
+        const int32_t moved = c->h_run_pod[last];
+        c->h_run_pod[pos] = moved;
+        c->h_pod_rpos[moved] = pos;
+        touched.push_back(moved);
+    }
+    c->h_run_pod[last] = -1;
+    --c->h_run_len[j];
+    runs.push_back(j);
+    c->h_pod_rpos[id] = -1;
+    c->h_pod_node[id] = NONE;
+}
+
+bool run_append(esc_ctx* c, int64_t id, uint32_t j, std::vector<int64_t>& touched, std::vector<uint32_t>& runs) {
+    if (c->h_run_len[j] >= c->h_run_off[j + 1] - c->h_run_off[j]) return false;
+    const int64_t pos = (int64_t)c->h_run_off[j] + c->h_run_len[j]++;
+    c->h_run_pod[pos] = (int32_t)id;
+    c->h_pod_rpos[id] = pos;
+    c->h_pod_node[id] = j;
+    touched.push_back(id);
+    runs.push_back(j);
+    return true;
+}
+
+int32_t sync_placement(esc_ctx* c, std::vector<int64_t>& touched, std::vector<uint32_t>& runs) {
+    std::sort(touched.begin(), touched.end());
+    touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+    std::vector<uint32_t> pos, slot;
+    for (int64_t id : touched)
+        if (id < (int64_t)c->h_pod_rpos.size() && c->h_pod_rpos[id] >= 0 && c->pod_cls[id] != -2) {
+            pos.push_back((uint32_t)c->h_pod_rpos[id]);
+            slot.push_back((uint32_t)pod_slot(c, id));
+        }
+    if (!pos.empty()) {
+        uint32_t *dp = nullptr, *ds = nullptr;
+        HIP_TRY(dalloc(&dp, pos.size()));
+        HIP_TRY(dalloc(&ds, slot.size()));
+        hipError_t e = hipMemcpy(dp, pos.data(), pos.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(ds, slot.data(), slot.size() * 4, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = launch_podref_fill(pod_dev(c, c->cur), ds, dp, (int64_t)pos.size(), c->d_refs, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        dfree(dp);
+        dfree(ds);
+        HIP_TRY(e);
+    }
+    if (!runs.empty()) {
+        Patches P;
+        for (uint32_t j : runs) P.add(0, j, c->h_run_len[j]);
+        PatchTargets t{};
+        t.u32[0] = c->d_nrun_len;
+        int32_t rc = apply_patches(c, P, {t});
+        if (rc) return rc;
+    }
+    c->rm_valid = false;
+    return ESC_OK;
+}
+
 // ---- node events: host views of the node memberships and the K5 group regions
 // Groups of node j (its label pairs through the node codes, dry bit included), as the
 // kernels' node_groups lists them.
@@ -2048,7 +2139,7 @@ int32_t esc_pods_upsert(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
         if (need[ci] > (int64_t)c->cls_free[ci].size()) return ESC_E_LIMIT;   // spare exhausted: reload
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    c->placed = c->rm_valid = false;                // pods moved: esc_load_placement again
+    c->rm_valid = false;
     Patches P;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t id = ids[i];
@@ -2087,7 +2178,12 @@ int32_t esc_pods_upsert(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
         c->live_xc += R;
         c->live_xp += k.nxp;
     }
-    return apply_patches(c, P, pod_targets(c));
+    int32_t rc = apply_patches(c, P, pod_targets(c));
+    if (rc || !c->placed) return rc;
+    // a bound pod keeps its node; its PodRef follows the new record (and slot)
+    std::vector<int64_t> touched(ids, ids + n);
+    std::vector<uint32_t> runs;
+    return sync_placement(c, touched, runs);
 }
 
 int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
@@ -2099,9 +2195,54 @@ int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     Patches P;
-    for (int64_t i = 0; i < n; ++i) remove_pod(c, ids[i], P);
-    c->placed = c->rm_valid = false;                // pods moved: esc_load_placement again
-    return apply_patches(c, P, pod_targets(c));
+    std::vector<int64_t> touched;
+    std::vector<uint32_t> runs;
+    for (int64_t i = 0; i < n; ++i) {
+        if (c->placed && c->pod_cls[ids[i]] != -2) run_remove(c, ids[i], touched, runs);   // leaves its node
+        remove_pod(c, ids[i], P);
+    }
+    c->rm_valid = false;
+    int32_t rc = apply_patches(c, P, pod_targets(c));
+    if (rc || !c->placed) return rc;
+    return sync_placement(c, touched, runs);
+}
+
+// Spec.NodeName of pods (the informer's pod Update once the scheduler binds a pod, or a
+// pod leaving its node): moves each pod's PodRef between node runs (node_state.go:10-39
+// builds the same map per decision).  NONE = unbound.  All or nothing: ESC_E_LIMIT when a
+// node's run has no room left (esc_load_placement again).
+int32_t esc_pods_bind(esc_ctx* c, const int64_t* ids, const uint32_t* pod_node, int64_t n) {
+    if (!c || n < 0 || (n > 0 && (!ids || !pod_node))) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->placed) return ESC_E_STATE;
+    std::vector<int64_t> seen(ids, ids + n);
+    std::sort(seen.begin(), seen.end());
+    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) return ESC_E_INVAL;
+    std::unordered_map<uint32_t, int64_t> need;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t id = ids[i];
+        if (id < 0 || id >= (int64_t)c->pod_cls.size() || c->pod_cls[id] == -2) return ESC_E_INVAL;
+        if (pod_node[i] != NONE && ((int64_t)pod_node[i] >= c->n_nodes || (c->h_nflags[pod_node[i]] & ESC_NF_ABSENT)))
+            return ESC_E_INVAL;
+        const uint32_t old = id < (int64_t)c->h_pod_node.size() ? c->h_pod_node[id] : NONE;
+        if (old != NONE) --need[old];
+        if (pod_node[i] != NONE) ++need[pod_node[i]];
+    }
+    for (const auto& kv : need)
+        if (kv.second > 0 && c->h_run_len[kv.first] + kv.second > c->h_run_off[kv.first + 1] - c->h_run_off[kv.first])
+            return ESC_E_LIMIT;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((int64_t)c->h_pod_node.size() < (int64_t)c->pod_cls.size()) {
+        c->h_pod_node.resize(c->pod_cls.size(), NONE);
+        c->h_pod_rpos.resize(c->pod_cls.size(), -1);
+    }
+    std::vector<int64_t> touched;
+    std::vector<uint32_t> runs;
+    for (int64_t i = 0; i < n; ++i) run_remove(c, ids[i], touched, runs);      // removals first: room
+    for (int64_t i = 0; i < n; ++i)
+        if (pod_node[i] != NONE && !run_append(c, ids[i], pod_node[i], touched, runs)) return ESC_E_HIP;
+    return sync_placement(c, touched, runs);
 }
 
 int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32_t* flags, const int64_t* cpu,
@@ -2431,7 +2572,7 @@ int32_t esc_tracker_list(const esc_ctx* c, int32_t group, int64_t* idx_out, int6
 int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* taint_s, const uint8_t* no_delete) {
     if (!c || !taint_s || !no_delete) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
-    if (!c->pods_loaded || !c->nodes_loaded || c->world != 1) return ESC_E_STATE;
+    if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
     if (!pod_node && !c->placed) return ESC_E_STATE;
     const int64_t N = c->n_nodes, np = (int64_t)c->pod_cls.size();
     if (pod_node)
@@ -2440,12 +2581,13 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     const int32_t G = c->gi.G;
-    if (!c->d_taint_s) {
+    if (!c->d_taint_s || c->rm_nodes != N) {
+        // per-node facts and the per-entry occupancy words, sized for this node table
+        dfree(c->d_taint_s); dfree(c->d_no_delete); dfree(c->d_occ); dfree(c->d_e_pair);
+        dfree(c->d_soft); dfree(c->d_hard); dfree(c->d_rm_out); dfree(c->d_rm_off); dfree(c->d_rm_list);
         HIP_TRY(dalloc(&c->d_taint_s, std::max<int64_t>(N, 1)));
         HIP_TRY(dalloc(&c->d_no_delete, std::max<int64_t>(N, 1)));
-        HIP_TRY(dalloc(&c->d_nrun_off, N + 1));
-        HIP_TRY(dalloc(&c->d_occ_pair, std::max<int64_t>(c->n_entries, 1)));
-        HIP_TRY(dalloc(&c->d_occ_def, std::max<int64_t>(c->n_entries, 1)));
+        HIP_TRY(dalloc(&c->d_occ, 2 * std::max<int64_t>(c->n_entries, 1)));
         HIP_TRY(dalloc(&c->d_soft, G)); HIP_TRY(dalloc(&c->d_hard, G));
         HIP_TRY(dalloc(&c->d_rm_out, G)); HIP_TRY(dalloc(&c->d_rm_off, G));
         // each group's deletable-node list can hold all of its pair's entries
@@ -2467,36 +2609,53 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
         HIP_TRY(dalloc(&c->d_rm_list, std::max<uint32_t>(c->h_rm_off[G], 1)));
         HIP_TRY(hipMemcpy(c->d_rm_off, c->h_rm_off.data(), (size_t)G * 4, hipMemcpyHostToDevice));
         c->h_rm.assign(G, esc_removal{});
+        c->rm_nodes = N;
     }
     if (N) {
         HIP_TRY(hipMemcpy(c->d_taint_s, taint_s, N * 8, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c->d_no_delete, no_delete, N, hipMemcpyHostToDevice));
     }
     if (pod_node) {
-        std::vector<uint32_t> off(N + 1, 0);
+        // runs of PodRefs per node, each with spare room (esc_set_spare) for pods bound later
+        std::vector<uint32_t> cnt(N, 0);
         for (int64_t i = 0; i < np; ++i)
-            if (c->pod_cls[i] != -2 && pod_node[i] != NONE) ++off[pod_node[i] + 1];
-        for (int64_t j = 0; j < N; ++j) off[j + 1] += off[j];
-        const int64_t total = off[N];
-        std::vector<uint32_t> cur(off.begin(), off.end() - 1), slot(std::max<int64_t>(total, 1));
-        for (int64_t i = 0; i < np; ++i) {
-            const int32_t ci = c->pod_cls[i];
-            if (ci == -2 || pod_node[i] == NONE) continue;
-            int64_t d = c->pod_pos[i];                                  // C: already the slot
-            if (ci >= 0) d = (c->h_cls[ci].t0 + d / TILE) * TILE + d % TILE;
-            slot[cur[pod_node[i]]++] = (uint32_t)d;
+            if (c->pod_cls[i] != -2 && pod_node[i] != NONE) ++cnt[pod_node[i]];
+        std::vector<uint32_t> off(N + 1, 0);
+        for (int64_t j = 0; j < N; ++j) {
+            const uint64_t cap = cnt[j] + (c->spare_frac > 0 ? (uint64_t)std::ceil(cnt[j] * c->spare_frac) + 2 : 0);
+            if ((uint64_t)off[j] + cap >= 0xFFFFFFFFull) return ESC_E_LIMIT;
+            off[j + 1] = off[j] + (uint32_t)cap;
         }
-        dfree(c->d_refs);
+        const int64_t total = off[N];
+        std::vector<uint32_t> len(std::max<int64_t>(N, 1), 0), slot(std::max<int64_t>(total, 1), 0);
+        c->h_run_pod.assign(std::max<int64_t>(total, 1), -1);
+        c->h_pod_node.assign(np, NONE);
+        c->h_pod_rpos.assign(np, -1);
+        for (int64_t i = 0; i < np; ++i) {
+            if (c->pod_cls[i] == -2 || pod_node[i] == NONE) continue;
+            const uint32_t j = pod_node[i];
+            const uint32_t pos = off[j] + len[j]++;
+            slot[pos] = (uint32_t)pod_slot(c, i);
+            c->h_run_pod[pos] = (int32_t)i;
+            c->h_pod_node[i] = j;
+            c->h_pod_rpos[i] = pos;
+        }
+        dfree(c->d_refs); dfree(c->d_nrun_off); dfree(c->d_nrun_len);
         uint32_t* d_slot = nullptr;
         HIP_TRY(dalloc(&c->d_refs, std::max<int64_t>(total, 1)));
+        HIP_TRY(dalloc(&c->d_nrun_off, N + 1));
+        HIP_TRY(dalloc(&c->d_nrun_len, std::max<int64_t>(N, 1)));
         HIP_TRY(dalloc(&d_slot, slot.size()));
         HIP_TRY(hipMemcpy(d_slot, slot.data(), slot.size() * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c->d_nrun_off, off.data(), (N + 1) * 4, hipMemcpyHostToDevice));
-        const hipError_t e = launch_podref_fill(pod_dev(c, c->cur), d_slot, total, c->d_refs, c->stream);
+        HIP_TRY(hipMemcpy(c->d_nrun_len, len.data(), len.size() * 4, hipMemcpyHostToDevice));
+        const hipError_t e = launch_podref_fill(pod_dev(c, c->cur), d_slot, nullptr, total, c->d_refs, c->stream);
         const hipError_t e2 = hipStreamSynchronize(c->stream);
         dfree(d_slot);
         HIP_TRY(e);
         HIP_TRY(e2);
+        c->h_run_off.swap(off);
+        c->h_run_len.swap(len);
         c->placed = true;
     }
     c->node_removal = true;
@@ -2504,8 +2663,48 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
     return ESC_OK;
 }
 
-// esc_try_remove: K6 (node occupancy by group filter) + K7 (the per-group reaping pass).
-int32_t esc_try_remove(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, const int64_t* hard_ns, esc_removal* out) {
+// K6 (node occupancy by group filter over this rank's pods) — the first half of
+// esc_try_remove; with several ranks the occupancy words are summed across ranks before K7.
+int32_t esc_reap_occupancy(esc_ctx* c) {
+    if (!c) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->placed || !c->node_removal) return ESC_E_STATE;
+    hipSetDevice(c->device);
+    HIP_TRY(launch_occupancy(node_dev(c), group_dev(c), removal_dev(c, 0), c->stream));
+    c->rm_valid = false;
+    return ESC_OK;
+}
+
+int32_t esc_reap_buffer(esc_ctx* c, void** buf, int64_t* n_words) {
+    if (!c || !buf || !n_words) return ESC_E_INVAL;
+    if (!c->placed) return ESC_E_STATE;
+    *buf = c->d_occ;
+    *n_words = 2 * c->n_entries;
+    return ESC_OK;
+}
+
+int32_t esc_reap_download(esc_ctx* c, uint32_t* out) {
+    if (!c || !out) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->placed) return ESC_E_STATE;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->n_entries) HIP_TRY(hipMemcpy(out, c->d_occ, 2 * c->n_entries * 4, hipMemcpyDeviceToHost));
+    return ESC_OK;
+}
+
+int32_t esc_reap_upload(esc_ctx* c, const uint32_t* in) {
+    if (!c || !in) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->placed) return ESC_E_STATE;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->n_entries) HIP_TRY(hipMemcpy(c->d_occ, in, 2 * c->n_entries * 4, hipMemcpyHostToDevice));
+    return ESC_OK;
+}
+
+// K7 over the (summed) occupancy: the per-group reaping pass.
+int32_t esc_reap_finish(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, const int64_t* hard_ns, esc_removal* out) {
     if (!c || !soft_ns || !hard_ns || !out) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->placed || !c->node_removal) return ESC_E_STATE;
@@ -2513,19 +2712,30 @@ int32_t esc_try_remove(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, const
     hipSetDevice(c->device);
     HIP_TRY(hipMemcpyAsync(c->d_soft, soft_ns, (size_t)G * 8, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_hard, hard_ns, (size_t)G * 8, hipMemcpyHostToDevice, c->stream));
-    RemovalDev r;
-    r.e_pair = c->d_e_pair; r.n_entries = c->n_entries;
-    r.taint_s = c->d_taint_s; r.no_delete = c->d_no_delete; r.nrun_off = c->d_nrun_off; r.refs = c->d_refs;
-    r.xp = c->pods[c->cur].xp;
-    r.occ_pair = c->d_occ_pair; r.occ_def = c->d_occ_def; r.soft_ns = c->d_soft; r.hard_ns = c->d_hard;
-    r.rm_off = c->d_rm_off; r.rm_list = c->d_rm_list; r.out = c->d_rm_out; r.now_ns = now_ns;
-    HIP_TRY(launch_try_remove(node_dev(c), group_dev(c), r, c->stream));
+    HIP_TRY(launch_try_remove(node_dev(c), group_dev(c), removal_dev(c, now_ns), c->stream));
     HIP_TRY(hipMemcpyAsync(c->h_rm.data(), c->d_rm_out, (size_t)G * sizeof(esc_removal), hipMemcpyDeviceToHost,
                            c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     std::memcpy(out, c->h_rm.data(), (size_t)G * sizeof(esc_removal));
     c->rm_valid = true;
     return ESC_OK;
+}
+
+// esc_try_remove: K6 (node occupancy by group filter) + the cross-rank SUM of the occupancy
+// words over the context's RCCL communicator when there are several ranks + K7.
+int32_t esc_try_remove(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, const int64_t* hard_ns, esc_removal* out) {
+    if (!c || !soft_ns || !hard_ns || !out) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (c->world > 1 && !c->comm) return ESC_E_STATE;  // host-staged: esc_reap_occupancy / _download / _upload / _finish
+    int32_t rc = esc_reap_occupancy(c);
+    if (rc) return rc;
+    if (c->world > 1) {
+        hipSetDevice(c->device);
+        const ncclResult_t r = rccl().all_reduce(c->d_occ, c->d_occ, (size_t)(2 * c->n_entries), ncclUint32, ncclSum,
+                                                 reinterpret_cast<ncclComm_t>(c->comm), c->stream);
+        if (r != ncclSuccess) return fail_comm("ncclAllReduce", rccl().error_string(r));
+    }
+    return esc_reap_finish(c, now_ns, soft_ns, hard_ns, out);
 }
 
 int32_t esc_removal_nodes(esc_ctx* c, int32_t g, int64_t* idx, int64_t cap, int64_t* n_out) {

@@ -64,6 +64,22 @@ class Exchange:
         self.ctx.decide()
 
 
+def try_remove(ctx, now_ns: int, soft_ns, hard_ns, device_collective: bool):
+    """TryRemoveTaintedNodes (scale_down.go:51-136) on a pod-sharded context: K6 counts the
+    rank's own pods per tainted node, the occupancy words are SUM-all-reduced (uint32) —
+    inside the library over RCCL (esc_try_remove) or host-staged over the process group —
+    then K7 runs on every rank over the same words, so every rank gets the same deletions."""
+    if device_collective:
+        return ctx.try_remove(now_ns, soft_ns, hard_ns)
+    import torch
+    import torch.distributed as dist
+    ctx.reap_occupancy()
+    w = torch.from_numpy(ctx.reap_download().astype(np.int64))
+    dist.all_reduce(w, op=dist.ReduceOp.SUM)
+    ctx.reap_upload(w.numpy().astype(np.uint32))
+    return ctx.reap_finish(now_ns, soft_ns, hard_ns)
+
+
 def exchange_host(sum_arr, min_arr):
     """Host-side SUM (and, when non-empty, MIN) all-reduce of numpy int64 arrays (gloo) —
     used by the CPU tests."""

@@ -443,10 +443,17 @@ int32_t esc_tracker_list(const esc_ctx* ctx, int32_t group, int64_t* idx_out, in
  * drops those) and gives each node its escalator-taint time (GetToBeRemovedTime,
  * taint.go:91: Unix seconds, INT64_MIN when the taint is absent or its value does not
  * parse) and its atlassian.com/no-delete annotation (non-empty = safe from deletion).
- * Pod events (esc_pods_upsert / _delete) invalidate the binding (ESC_E_STATE until it is
- * loaded again).  esc_try_remove then evaluates, per group, its tainted nodes in snapshot
- * order: now - taintTime > soft grace and (NodeEmpty or > hard grace) -> delete (never in
- * dry mode).  Single-rank contexts only.                                             */
+ * Pod events keep the binding current: esc_pods_upsert rewrites a bound pod's reference,
+ * esc_pods_delete drops it, esc_pods_bind moves pods between nodes (runs per node keep
+ * esc_set_spare room; ESC_E_LIMIT when a run is full).  Node additions / deletions need
+ * esc_load_placement again (ESC_E_STATE until then).  esc_try_remove then evaluates, per
+ * group, its tainted nodes in snapshot order: now - taintTime > soft grace and (NodeEmpty
+ * or > hard grace) -> delete (never in dry mode).
+ * Several ranks (each holding its pod shard): the per-node occupancy is this rank's pods
+ * only, so esc_try_remove sums the occupancy words across ranks over the context's RCCL
+ * communicator (esc_comm_init) between K6 and K7; hosts with their own collective use
+ * esc_reap_occupancy, SUM-all-reduce esc_reap_buffer's uint32 words (or
+ * esc_reap_download / esc_reap_upload), then esc_reap_finish.                        */
 typedef struct esc_removal {
     int64_t n_candidates;        /* the group's tainted nodes (filterNodes)                    */
     int64_t n_delete;            /* len(toBeDeleted): TryRemoveTaintedNodes returns -n_delete  */
@@ -457,6 +464,13 @@ int32_t esc_load_placement(esc_ctx* ctx, const uint32_t* pod_node, const int64_t
                            const uint8_t* no_delete);
 int32_t esc_try_remove(esc_ctx* ctx, int64_t now_unix_ns, const int64_t* soft_grace_ns,
                        const int64_t* hard_grace_ns, esc_removal* out);
+int32_t esc_pods_bind(esc_ctx* ctx, const int64_t* ids, const uint32_t* pod_node, int64_t n);
+int32_t esc_reap_occupancy(esc_ctx* ctx);
+int32_t esc_reap_buffer(esc_ctx* ctx, void** buf, int64_t* n_words);
+int32_t esc_reap_download(esc_ctx* ctx, uint32_t* out);
+int32_t esc_reap_upload(esc_ctx* ctx, const uint32_t* in);
+int32_t esc_reap_finish(esc_ctx* ctx, int64_t now_unix_ns, const int64_t* soft_grace_ns,
+                        const int64_t* hard_grace_ns, esc_removal* out);
 int32_t esc_removal_nodes(esc_ctx* ctx, int32_t group, int64_t* idx_out, int64_t cap, int64_t* n_out);
 
 /* ----------------------------------------------------------------- ordering

@@ -659,7 +659,7 @@ def test_try_remove_tainted_vs_literal(esc, seed):
     """TryRemoveTaintedNodes for every group at once (esc_load_placement + esc_try_remove):
     deletion lists, counts and NodePodsRemaining sums equal the literal oracle, including
     no-delete annotations, unparsable taint values, dry-mode groups, pods bound to no /
-    unknown nodes and nodes shared by several groups; pod events invalidate the binding."""
+    unknown nodes and nodes shared by several groups; a pod delete keeps the binding."""
     from escalator_amd.objects import placement
     rng = random.Random(9100 + seed)
     G = rng.choice([1, 4, 12])
@@ -682,13 +682,126 @@ def test_try_remove_tainted_vs_literal(esc, seed):
     pn, ts, nd = placement(pods, nodes)
     ctx.load_placement(None, ts, nd)
     _check_reaping(ctx, groups, pods, nodes, trackers, now_ns, np.full(G, 60 * 10**9), np.full(G, 4000 * 10**9))
-    if pods:
+    if pods:                                      # a pod event keeps the binding current
         ctx.pods_delete([0])
-        with pytest.raises(RuntimeError):
-            ctx.try_remove(now_ns, np.zeros(G, np.int64), np.zeros(G, np.int64))
         del pods[0]
-        ctx.load_placement(np.r_[np.uint32(0xFFFFFFFF), pn[1:]], ts, nd)
         _check_reaping(ctx, groups, pods, nodes, trackers, now_ns, np.full(G, 60 * 10**9), np.full(G, 4000 * 10**9))
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_reaping_follows_pod_events(esc, seed):
+    """The placement survives pod events (§8f rank 2): upserts rewrite a bound pod's
+    reference (its record and slot may change), deletes drop it, esc_pods_bind moves pods
+    between nodes / binds new pods; TryRemoveTaintedNodes then equals the literal oracle on
+    the live pods with their current Spec.NodeName."""
+    from escalator_amd.objects import placement
+    rng = random.Random(9300 + seed)
+    G = rng.choice([2, 6, 12])
+    groups, pods, nodes, now_ns = make_reaping_cluster(rng, G, 600, rng.choice([20, 80]))
+    trackers = make_trackers(rng, groups, nodes)
+    ctx = esc.Context(groups)
+    ctx.set_spare(0.5)
+    P, N = ctx.pack(pods, nodes, trackers)
+    ctx.load(P, N)
+    pn, ts, nd = placement(pods, nodes)
+    ctx.load_placement(pn, ts, nd)
+    index = {n["name"]: j for j, n in enumerate(nodes)}
+    live = dict(enumerate(pods))
+    next_id = len(pods)
+    soft = np.array([rng.choice([0, 60, 300]) * 10**9 for _ in range(G)], np.int64)
+    hard = soft + np.array([rng.choice([0, 600]) * 10**9 for _ in range(G)], np.int64)
+    for rnd in range(4):
+        # upserts of existing pods (new records; some move node) and inserts of new pods
+        ev_ids, ev_objs = [], []
+        for i in rng.sample(sorted(live), min(len(live), 40)):
+            q = make_pods(rng, 1, groups, big_frac=0.0)[0]
+            q["node_name"] = live[i]["node_name"] if rng.random() < 0.7 else rng.choice(nodes)["name"]
+            ev_ids.append(i)
+            ev_objs.append(q)
+        for _ in range(25):
+            q = make_pods(rng, 1, groups, big_frac=0.0)[0]
+            q["node_name"] = rng.choice(nodes)["name"] if rng.random() < 0.8 else ""
+            ev_ids.append(next_id)
+            ev_objs.append(q)
+            next_id += 1
+        Pe, _ = ctx.pack(ev_objs, [])
+        keep = [k for k in range(len(ev_ids)) if _fits_k(Pe, k)]
+        assert ctx.pods_upsert([ev_ids[k] for k in keep], _packed_subset(Pe, keep)) == 0
+        bind_ids, bind_to = [], []
+        for k in keep:
+            i, q = ev_ids[k], ev_objs[k]
+            old = live[i]["node_name"] if i in live else ""
+            live[i] = q
+            if q["node_name"] != old:
+                bind_ids.append(i)
+                bind_to.append(index.get(q["node_name"], 0xFFFFFFFF) if q["node_name"] else 0xFFFFFFFF)
+        def bind(ids_, to_):
+            try:
+                ctx.pods_bind(ids_, to_)
+            except esc._lib.EscError as e:            # a node's run is full: re-bind everything
+                assert e.code == esc._lib.ESC_E_LIMIT
+                full = np.full(next_id, 0xFFFFFFFF, np.uint32)
+                for i_, t_ in zip(ids_, to_):
+                    live[i_] = dict(live[i_], node_name=nodes[t_]["name"] if t_ != 0xFFFFFFFF else "")
+                for i_, q_ in live.items():
+                    if q_.get("node_name") in index:
+                        full[i_] = index[q_["node_name"]]
+                ctx.load_placement(full, ts, nd)
+
+        if bind_ids:
+            bind(bind_ids, bind_to)
+        dels = rng.sample(sorted(live), 30)
+        ctx.pods_delete(dels)
+        for i in dels:
+            del live[i]
+        # pods rescheduled to other nodes (or unbound) without a record change
+        mv = rng.sample(sorted(live), 20)
+        to = [rng.choice(nodes)["name"] if rng.random() < 0.85 else "" for _ in mv]
+        bind(mv, [index[t] if t else 0xFFFFFFFF for t in to])
+        for i, t in zip(mv, to):
+            live[i] = dict(live[i], node_name=t)
+        cur = [live[i] for i in sorted(live)]
+        _check_reaping(ctx, groups, cur, nodes, trackers, now_ns, soft, hard)
+
+
+@pytest.mark.parametrize("graphless", [True])
+def test_reaping_sharded_host_exchange(esc, graphless):
+    """Reaping over three pod shards on one device: each rank's K6 counts its own pods per
+    tainted node, the occupancy words are summed through the host (esc_reap_download /
+    _upload — the sum RCCL does in esc_try_remove), and every rank's K7 gives the
+    single-context deletions (and the literal oracle's)."""
+    from escalator_amd.dist import shard_range
+    from escalator_amd.objects import placement
+    rng = random.Random(9400)
+    G = 8
+    groups, pods, nodes, now_ns = make_reaping_cluster(rng, G, 1500, 120)
+    trackers = make_trackers(rng, groups, nodes)
+    pn, ts, nd = placement(pods, nodes)
+    soft = np.full(G, 60 * 10**9, np.int64)
+    hard = np.full(G, 4000 * 10**9, np.int64)
+    one = esc.Context(groups)
+    P, N = one.pack(pods, nodes, trackers)
+    one.load(P, N)
+    one.load_placement(pn, ts, nd)
+    want = one.try_remove(now_ns, soft, hard)
+    world = 3
+    ctxs = []
+    for r in range(world):
+        lo, hi = shard_range(len(pods), r, world)
+        c = esc.Context(groups, rank=r, world=world)
+        Pr, Nr = c.pack(pods[lo:hi], nodes, trackers)
+        c.load(Pr, Nr, pod_offset=lo)
+        c.load_placement(pn[lo:hi], ts, nd)
+        c.reap_occupancy()
+        ctxs.append(c)
+    total = sum(c.reap_download().astype(np.int64) for c in ctxs).astype(np.uint32)
+    for c in ctxs:
+        c.reap_upload(total)
+        got = c.reap_finish(now_ns, soft, hard)
+        assert got.tobytes() == want.tobytes()
+        for g in range(G):
+            assert list(c.removal_nodes(g)) == list(one.removal_nodes(g))
+    _check_reaping(one, groups, pods, nodes, trackers, now_ns, soft, hard)
 
 
 # ------------------------------------------------ dry-mode taintTracker (§8f rank 4)
