@@ -540,6 +540,46 @@ func (x *Context) NodesUpdate(ids []int64, flags []uint32, cpuMilli, memBytes []
 		(*C.int64_t)(unsafe.Pointer(&memBytes[0]))))
 }
 
+// NodesAdd applies node Add events (cache.go:37-56): the nodes are packed and appended at
+// the next snapshot indices, returned in order.  ErrReload when the spare room is short.
+func (x *Context) NodesAdd(nodes []*v1.Node) ([]int64, error) {
+	ids := make([]int64, len(nodes)+1)
+	if len(nodes) == 0 {
+		return nil, nil
+	}
+	err := x.pack(nil, nodes, nil, false, func(_ *C.esc_pod_soa, ns *C.esc_node_soa) error {
+		rc := C.esc_nodes_add(x.c, ns, (*C.int64_t)(unsafe.Pointer(&ids[0])))
+		if rc == C.ESC_E_LIMIT {
+			return ErrReload
+		}
+		return rcErr("esc_nodes_add", rc)
+	})
+	return ids[:len(nodes)], err
+}
+
+// NodesDelete applies node Delete events by snapshot index.
+func (x *Context) NodesDelete(ids []int64) error {
+	if len(ids) == 0 {
+		return nil
+	}
+	return rcErr("esc_nodes_delete", C.esc_nodes_delete(x.c, (*C.int64_t)(unsafe.Pointer(&ids[0])), C.int64_t(len(ids))))
+}
+
+// PodsBind records Spec.NodeName changes (the scheduler bound a pod, or it left its node):
+// node snapshot indices, 0xFFFFFFFF for none.  ErrReload when a node's run is full
+// (LoadPlacement again).
+func (x *Context) PodsBind(ids []int64, nodeIdx []uint32) error {
+	if len(ids) == 0 || len(ids) != len(nodeIdx) {
+		return nil
+	}
+	rc := C.esc_pods_bind(x.c, (*C.int64_t)(unsafe.Pointer(&ids[0])), (*C.uint32_t)(unsafe.Pointer(&nodeIdx[0])),
+		C.int64_t(len(ids)))
+	if rc == C.ESC_E_LIMIT {
+		return ErrReload
+	}
+	return rcErr("esc_pods_bind", rc)
+}
+
 // TrackerUpdate applies one dry-mode group's taintTracker change in place: taintOldestN
 // appends (scale_down.go:197-200), untaintNewestN deletes (scale_up.go:146-158).
 func (x *Context) TrackerUpdate(g int, add, remove []int64) error {
