@@ -142,8 +142,43 @@ enum TrkAcc : int { TA_CNT = 0, TA_CPU_LO, TA_CPU_HI, TA_MEM_LO, TA_MEM_HI, TA_K
 constexpr int K1_CHUNKS = 4;
 constexpr int K1_CHUNK_CAP = 8;
 bool k1_dynamic(int variant);
+struct DecCompact;
+// K1 with the fold fused (one LDS window, every workgroup co-resident): after flushing its
+// partial row each workgroup arrives at a grid barrier (a 64-bit counter that only grows:
+// the barrier of decision k completes at k * nblk arrivals) and then folds its own slice
+// of pod slots over every row — the whole chip folds instead of one column per workgroup —
+// and writes the pod words of the groups whose slot lies in the slice.  `arrive == null`:
+// no fold (k_fold_decide folds).  A barrier that does not complete in bounded time sets
+// *err (the host then falls back to the separate fold).
+struct K1Fold {
+    unsigned long long* arrive;
+    uint32_t* err;
+    int64_t* pwords;             // [G][PW_K] (the exchange words)
+    const uint32_t* goff;        // [nblk + 1] groups of each workgroup's slice in `groups`
+    const uint32_t* groups;      // group ids ordered by pod slot
+    int64_t n_slots;             // pod slots: n_gp + 1
+    // the fused decide (one rank): K1's fold (pod words) and k_node_groups on the side
+    // stream (node words) each publish a group's words with write-through stores and then
+    // count an arrival on the group's counter; the second arrival (odd old value) decides
+    // the group — nobody waits.  Null: k_decide decides after the join.
+    uint32_t* arrive_g;
+    const int64_t* nwords;
+    const GroupNode* gnode;
+    esc_group_decision* dec;
+    DecCompact* cdec;
+};
+struct NGDecide {               // k_node_groups' side of the fused decide (see K1Fold)
+    uint32_t* arrive_g;         // null: no fused decide
+    const int64_t* pwords;
+    esc_group_decision* dec;
+    DecCompact* cdec;
+};
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
-                             uint64_t* part, int64_t* wide, uint32_t* ticket, int cap, hipStream_t st);
+                             uint64_t* part, int64_t* wide, uint32_t* ticket, int cap, const K1Fold& fold,
+                             hipStream_t st);
+// Workgroups of the K1 launch that fit on one CU at once (the fused fold's co-residency bound).
+int k1_blocks_per_cu(int gw);
+constexpr int K1_FOLD_LDS = 4 * 512 * 8 + 3 * 512 * 16;   // the fold's LDS use (bytes, 512 threads)
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
                                int64_t* wide, hipStream_t st);
 hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows, int64_t* trk_acc, hipStream_t st);
@@ -162,7 +197,7 @@ static_assert(sizeof(DecCompact) == 32, "compact decision is 2 x 16 B");
 
 // K2b (k_node_groups): every group's final node words from K2's piece rows (side stream).
 hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t* node_rows, int64_t* trk_acc,
-                              int64_t* nwords, hipStream_t st);
+                              int64_t* nwords, const NGDecide& nd, hipStream_t st);
 // K3 (k_fold_decide): fold of the K1 partials + group join + decide, one workgroup per column.
 constexpr int FC_COL = 128;            // pod slots per K3 column (one 16-B wave-load of a row)
 struct FoldPlan {

@@ -487,11 +487,194 @@ __device__ __forceinline__ void c_tile_exact(const PodDev& P, const GroupDev& G,
 // DYN: the K tiles' weight is cut into gridDim.x * K1_CHUNKS chunks taken from a ticket
 // counter (at most `cap` per workgroup), so workgroups that stream faster take more
 // and the launch does not wait on the slowest static share; DYN 0: one static share each.
+namespace {
+// ---- K4 decision helpers (K1's fused decide, k_fold_decide, k_decide)
+// Exact total from split words; false when it is outside int64 (Quantity -> inf.Dec).
+__device__ __forceinline__ bool join_split(int64_t lo_sum, int64_t hi_sum, int64_t& out) {
+    const __int128 t = ((__int128)hi_sum << 32) + (__int128)lo_sum;
+    out = (int64_t)t;
+    return t >= (__int128)INT64_MIN && t <= (__int128)INT64_MAX;
+}
+
+__device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn, int32_t g,
+                                         const int64_t* __restrict__ pw, const int64_t* __restrict__ nw,
+                                         esc_group_decision& dec, esc_group_metrics* __restrict__ met) {
+    Totals t;
+    int64_t flags = nw[NW_FLAGS];
+    if (!join_split(pw[PW_CPU_LO], pw[PW_CPU_HI], t.pod_cpu)) flags |= ESC_TF_POD_OVERFLOW;
+    if (!join_split(pw[PW_MEM_LO], pw[PW_MEM_HI], t.pod_mem)) flags |= ESC_TF_POD_OVERFLOW;
+    t.n_pods = pw[PW_N];
+    t.node_cpu = nw[NW_CPU];
+    t.node_mem = nw[NW_MEM];
+    t.n_unt = nw[NW_N_UNT];
+    t.n_taint = nw[NW_N_TAINT];
+    t.n_cord = nw[NW_N_CORD];
+    t.n_nodes = t.n_unt + t.n_taint + t.n_cord;
+    t.first = gn.first;
+    t.first_cpu = gn.first_cpu;
+    t.first_mem = gn.first_mem;
+    t.flags = flags;
+    decide_one(G.params[g], t, dec);
+    if (met) {
+        esc_group_metrics m;
+        metrics_one(t, dec, m);
+        met[g] = m;
+    }
+}
+
+__device__ __forceinline__ DecCompact compact_of(const esc_group_decision& d) {
+    DecCompact c;
+    c.cpu_pct = d.cpu_pct;
+    c.mem_pct = d.mem_pct;
+    const bool fits = d.delta == (int64_t)(int32_t)d.delta && d.n_to_taint == (int64_t)(int32_t)d.n_to_taint;
+    c.delta = (int32_t)d.delta;
+    c.n_to_taint = (int32_t)d.n_to_taint;
+    c.status = (uint8_t)d.status;
+    c.branch = (uint8_t)d.branch;
+    c.taint_status = (uint8_t)d.taint_status;
+    c.wide = fits ? 0 : 1;
+    c.pad = 0;
+    return c;
+}
+
+__device__ __forceinline__ void store_full(esc_group_decision* dst, const esc_group_decision& d) {
+    static_assert(sizeof(esc_group_decision) == 64, "decision record is 4 x 16 B");
+    const uint4* s = reinterpret_cast<const uint4*>(&d);
+    uint4* o = reinterpret_cast<uint4*>(dst);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = s[k];
+}
+
+// One group's decision from its pod / node words: the full record to device memory, the
+// compact one to the decision buffer.
+__device__ __forceinline__ void decide_store(const GroupDev& G, const GroupNode& gn, int32_t g, const int64_t* pw,
+                                             const int64_t* nw, esc_group_decision* dec, DecCompact* cdec) {
+    esc_group_decision d;
+    finalize(G, gn, g, pw, nw, d, G.metrics);
+    store_full(dec + g, d);
+    const DecCompact cd = compact_of(d);
+    const uint4* src = reinterpret_cast<const uint4*>(&cd);
+    uint4* dst = reinterpret_cast<uint4*>(cdec + g);
+    dst[0] = src[0];
+    dst[1] = src[1];
+}
+}  // namespace
+
+// The fused fold (K1Fold): grid barrier, then this workgroup's slice of pod slots summed
+// over every partial row (+ the slots' exact wide rows, read and reset), then the pod words
+// of the slice's groups.  `lds` is free again here (the window was flushed).
+template <int THREADS>
+__device__ __forceinline__ void k1_fold(const GroupDev& G, const K1Fold& F, const uint64_t* __restrict__ part,
+                                        int64_t* __restrict__ wide, uint64_t* lds) {
+    // The partial rows were written with agent-scope (write-through) stores and are read
+    // with agent-scope loads, so no L2 write-back / invalidate is needed (an agent-scope
+    // release fence costs a buffer_wbl2 per wave: +90 us on config 4): every wave waits for
+    // its stores to complete, then one arrival per workgroup.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ uint32_t s_ok;
+    if (threadIdx.x == 0) {
+        const unsigned long long n = gridDim.x;
+        const unsigned long long old = __hip_atomic_fetch_add(F.arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long target = (old / n + 1) * n;
+        uint32_t spins = 0, ok = 1;
+        while (__hip_atomic_load(F.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (++spins > (1u << 22)) { atomicOr(F.err, 1u); ok = 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) return;
+    const int64_t nb = gridDim.x, b = blockIdx.x;
+    const int64_t lo = F.n_slots * b / nb, hi = F.n_slots * (b + 1) / nb;
+    const int W = (int)(hi - lo);
+    if (W <= 0) return;
+    // the host enables the fold only when every slice has at most THREADS slots
+    const int RG = THREADS / W;                          // rows folded in parallel per slot
+    const int t = threadIdx.x, sl = t % W, rg = t / W;
+    uint64_t cpu = 0, cnt = 0, ml = 0, mc = 0;
+    if (rg < RG) {
+        constexpr int U = 8;                             // rows in flight per thread
+        for (int64_t r0 = rg; r0 < nb; r0 += (int64_t)RG * U) {
+            uint64_t cc[U], mm[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t r = r0 + (int64_t)u * RG;
+                const uint64_t* row = part + (r < nb ? r : r0) * 2 * G.sp + lo + sl;
+                cc[u] = __hip_atomic_load(row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                mm[u] = __hip_atomic_load(row + G.sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (r0 + (int64_t)u * RG >= nb) break;
+                cpu += cc[u] & CPU_MASK;
+                cnt += cc[u] >> CNT_SHIFT;
+                ml += mm[u];
+                mc += ml < mm[u] ? 1u : 0u;
+            }
+        }
+    }
+    // reduce the row groups: lds[k * THREADS + t]
+    lds[0 * THREADS + t] = cpu; lds[1 * THREADS + t] = cnt; lds[2 * THREADS + t] = ml; lds[3 * THREADS + t] = mc;
+    __syncthreads();
+    __int128* tot = reinterpret_cast<__int128*>(lds + 4 * THREADS);   // per slot: cpu, mem (exact), count
+    if (t < W) {
+        uint64_t a = 0, n = 0, lo2 = 0, carry = 0;
+        for (int k = 0; k < RG; ++k) {
+            const int u = k * W + t;
+            a += lds[u]; n += lds[THREADS + u];
+            const uint64_t m = lds[2 * THREADS + u];
+            lo2 += m;
+            carry += (lo2 < m ? 1u : 0u) + lds[3 * THREADS + u];
+        }
+        int64_t* wp = wide + (lo + t) * WP_K;
+        int64_t w[WP_K];
+#pragma unroll
+        for (int k = 0; k < WP_K; ++k) w[k] = __hip_atomic_load(wp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((w[0] | w[1] | w[2] | w[3] | w[4]) != 0)
+#pragma unroll
+            for (int k = 0; k < WP_K; ++k) __hip_atomic_store(wp + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        tot[3 * t + 0] = (__int128)a + ((__int128)w[WP_CPU_HI] << 32) + (__int128)w[WP_CPU_LO];
+        tot[3 * t + 1] = (__int128)(((unsigned __int128)carry << 64) | lo2) + ((__int128)w[WP_MEM_HI] << 32) +
+                         (__int128)w[WP_MEM_LO];
+        tot[3 * t + 2] = (__int128)n + w[WP_CNT];
+    }
+    for (uint32_t i = F.goff[b] + t; i < F.goff[b + 1]; i += THREADS) {
+        const uint32_t g = F.groups[i];
+        const int k = (int)((int64_t)G.gslot[g] - lo);
+        const __int128 pc = tot[3 * k], pm = tot[3 * k + 1];
+        int64_t w[PW_K];
+        w[PW_CPU_LO] = (int64_t)((unsigned __int128)pc & 0xFFFFFFFFull);
+        w[PW_CPU_HI] = (int64_t)(pc >> 32);
+        w[PW_MEM_LO] = (int64_t)((unsigned __int128)pm & 0xFFFFFFFFull);
+        w[PW_MEM_HI] = (int64_t)(pm >> 32);
+        w[PW_N] = (int64_t)tot[3 * k + 2];
+        int64_t* pw = F.pwords + (int64_t)g * PW_K;
+        if (!F.arrive_g) {
+#pragma unroll
+            for (int q = 0; q < PW_K; ++q) pw[q] = w[q];
+            continue;
+        }
+#pragma unroll
+        for (int q = 0; q < PW_K; ++q) __hip_atomic_store(pw + q, w[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t old = __hip_atomic_fetch_add(F.arrive_g + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old & 1u) {                                  // the node words are already published
+            int64_t nw[NW_K];
+#pragma unroll
+            for (int q = 0; q < NW_K; ++q)
+                nw[q] = __hip_atomic_load(F.nwords + (int64_t)g * NW_K + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            decide_store(G, F.gnode[g], (int32_t)g, w, nw, F.dec, F.cdec);
+        }
+    }
+}
+
 template <int THREADS, int ABLATE = 0, int DC = 3, int DYN = 0, int WS = 0>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
                                                         int64_t* __restrict__ wide,
-                                                        uint32_t* __restrict__ ticket, int cap) {
+                                                        uint32_t* __restrict__ ticket, int cap, K1Fold FF) {
     constexpr int NW = THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     __shared__ uint32_t s_chunk;
@@ -603,9 +786,16 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     __syncthreads();
     const int64_t S = G.sp;                                  // row stride (K3 reads whole columns)
     uint64_t* out = part + (int64_t)blockIdx.x * 2 * S + g0;
-    for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
-        out[i] = lds[i];
-        out[S + i] = lds[gw + i];
+    if (!DYN && !ABLATE && FF.arrive) {               // fused fold: write-through (agent-scope) stores
+        for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
+            __hip_atomic_store(out + i, lds[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(out + S + i, lds[gw + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else {
+        for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
+            out[i] = lds[i];
+            out[S + i] = lds[gw + i];
+        }
     }
     if (DYN && threadIdx.x == 0) {
         // every workgroup's last grab precedes its increment here: the last one resets
@@ -613,6 +803,9 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
             __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(ticket + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+    }
+    if constexpr (!DYN && !ABLATE) {
+        if (FF.arrive) k1_fold<THREADS>(G, FF, part, wide, lds);
     }
 }
 
@@ -625,24 +818,33 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
 #define ESC_K1D(T, A, DC, D) ESC_K1W(T, A, DC, D, 0)
 #define ESC_K1W(T, A, DC, D, W)                                                                       \
     hipLaunchKernelGGL((k_pod_reduce<T, A, DC, D, W>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, \
-                       wide, ticket, cap)
+                       wide, ticket, cap, fold)
 #define ESC_K1_ARGS const PodDev &p, const GroupDev &g, int32_t g0, int32_t gw, int nblk, int variant, uint64_t *part, \
-                    int64_t *wide, uint32_t *ticket, int cap, hipStream_t st
+                    int64_t *wide, uint32_t *ticket, int cap, const K1Fold &fold, hipStream_t st
 hipError_t launch_pod_reduce_alt(ESC_K1_ARGS);
 hipError_t launch_pod_reduce_ablation(ESC_K1_ARGS) __attribute__((weak));
 
 #if ESC_PART == 0
 bool k1_dynamic(int variant) { return variant == 5; }
 
+int k1_blocks_per_cu(int gw) {
+    int nb = 0;
+    const size_t lds = std::max<size_t>((size_t)gw * 2 * sizeof(uint64_t), (size_t)K1_FOLD_LDS);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pod_reduce<512, 0, 3, 0, 0>, 512, lds) != hipSuccess)
+        return 0;
+    return nb;
+}
+
 hipError_t launch_pod_reduce(ESC_K1_ARGS) {
-    const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
+    size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
+    if (fold.arrive && lds < (size_t)K1_FOLD_LDS) lds = K1_FOLD_LDS;
     switch (variant) {
         case 0: ESC_K1(512, 0, 3); break;
         case 1: case 2: case 5: case 6:
-            return launch_pod_reduce_alt(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, st);
+            return launch_pod_reduce_alt(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, K1Fold{}, st);
         default:                                  // timing-only ablations (ABLATIONS=1 build)
             if (!launch_pod_reduce_ablation) return hipErrorInvalidValue;
-            return launch_pod_reduce_ablation(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, st);
+            return launch_pod_reduce_ablation(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, K1Fold{}, st);
     }
     return hipGetLastError();
 }
@@ -864,66 +1066,14 @@ __device__ __forceinline__ void split_store(int64_t* w, int k, __int128 t) {
     w[k + 1] = (int64_t)(t >> 32);
 }
 
-// Exact total from split words; false when it is outside int64 (Quantity -> inf.Dec).
-__device__ __forceinline__ bool join_split(int64_t lo_sum, int64_t hi_sum, int64_t& out) {
-    const __int128 t = ((__int128)hi_sum << 32) + (__int128)lo_sum;
-    out = (int64_t)t;
-    return t >= (__int128)INT64_MIN && t <= (__int128)INT64_MAX;
-}
 
 // (unsigned 128-bit sum of lo32 parts, int64 sum of hi parts) -> the exact total
 __device__ __forceinline__ __int128 join_parts(uint64_t lo, uint64_t lo_carry, int64_t hi) {
     return (__int128)(((unsigned __int128)lo_carry << 64) | lo) + ((__int128)hi << 32);
 }
 
-__device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn, int32_t g,
-                                         const int64_t* __restrict__ pw, const int64_t* __restrict__ nw,
-                                         esc_group_decision& dec, esc_group_metrics* __restrict__ met) {
-    Totals t;
-    int64_t flags = nw[NW_FLAGS];
-    if (!join_split(pw[PW_CPU_LO], pw[PW_CPU_HI], t.pod_cpu)) flags |= ESC_TF_POD_OVERFLOW;
-    if (!join_split(pw[PW_MEM_LO], pw[PW_MEM_HI], t.pod_mem)) flags |= ESC_TF_POD_OVERFLOW;
-    t.n_pods = pw[PW_N];
-    t.node_cpu = nw[NW_CPU];
-    t.node_mem = nw[NW_MEM];
-    t.n_unt = nw[NW_N_UNT];
-    t.n_taint = nw[NW_N_TAINT];
-    t.n_cord = nw[NW_N_CORD];
-    t.n_nodes = t.n_unt + t.n_taint + t.n_cord;
-    t.first = gn.first;
-    t.first_cpu = gn.first_cpu;
-    t.first_mem = gn.first_mem;
-    t.flags = flags;
-    decide_one(G.params[g], t, dec);
-    if (met) {
-        esc_group_metrics m;
-        metrics_one(t, dec, m);
-        met[g] = m;
-    }
-}
 
-__device__ __forceinline__ DecCompact compact_of(const esc_group_decision& d) {
-    DecCompact c;
-    c.cpu_pct = d.cpu_pct;
-    c.mem_pct = d.mem_pct;
-    const bool fits = d.delta == (int64_t)(int32_t)d.delta && d.n_to_taint == (int64_t)(int32_t)d.n_to_taint;
-    c.delta = (int32_t)d.delta;
-    c.n_to_taint = (int32_t)d.n_to_taint;
-    c.status = (uint8_t)d.status;
-    c.branch = (uint8_t)d.branch;
-    c.taint_status = (uint8_t)d.taint_status;
-    c.wide = fits ? 0 : 1;
-    c.pad = 0;
-    return c;
-}
 
-__device__ __forceinline__ void store_full(esc_group_decision* dst, const esc_group_decision& d) {
-    static_assert(sizeof(esc_group_decision) == 64, "decision record is 4 x 16 B");
-    const uint4* s = reinterpret_cast<const uint4*>(&d);
-    uint4* o = reinterpret_cast<uint4*>(dst);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = s[k];
-}
 
 // The compact decisions of n groups staged in LDS (sc), written as 16-B pieces: one
 // contiguous run when the groups are consecutive ids (g0 ..), else per group (ids[k]).
@@ -943,6 +1093,7 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+
 }  // namespace
 
 // K2b (k_node_groups, side stream, beside K1): every group's node words from its pair's
@@ -957,7 +1108,7 @@ constexpr int NG_WAVES = 4;
 __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeDev N,
                                                                const int64_t* __restrict__ node_rows,
                                                                int64_t* __restrict__ trk_acc,
-                                                               int64_t* __restrict__ nwords) {
+                                                               int64_t* __restrict__ nwords, NGDecide D) {
     __shared__ uint64_t red[NG_WAVES][6][64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int32_t g = blockIdx.x * 64 + lane;
@@ -1005,7 +1156,7 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
             }
         }
     }
-    if (wid != 0 || !ok) return;
+    if (wid == 0 && ok) {
     __int128 ncpu, nmem;
     uint64_t n_unt = a[0], n_taint = a[1], n_cord = a[2];
     if (!G.dry[g]) {
@@ -1027,12 +1178,27 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
     int64_t* nw = nwords + (int64_t)g * NW_K;
     const bool n_ok = ncpu >= (__int128)INT64_MIN && ncpu <= (__int128)INT64_MAX &&
                       nmem >= (__int128)INT64_MIN && nmem <= (__int128)INT64_MAX;
-    nw[NW_CPU] = (int64_t)ncpu;
-    nw[NW_MEM] = (int64_t)nmem;
-    nw[NW_N_UNT] = (int64_t)n_unt;
-    nw[NW_N_TAINT] = (int64_t)n_taint;
-    nw[NW_N_CORD] = (int64_t)n_cord;
-    nw[NW_FLAGS] = n_ok ? 0 : ESC_TF_NODE_OVERFLOW;
+    const int64_t v[6] = {(int64_t)ncpu, (int64_t)nmem, (int64_t)n_unt, (int64_t)n_taint, (int64_t)n_cord,
+                          n_ok ? 0 : ESC_TF_NODE_OVERFLOW};
+    static_assert(NW_CPU == 0 && NW_MEM == 1 && NW_N_UNT == 2 && NW_N_TAINT == 3 && NW_N_CORD == 4 && NW_FLAGS == 5,
+                  "node word order");
+    if (!D.arrive_g) {
+#pragma unroll
+        for (int k = 0; k < 6; ++k) nw[k] = v[k];
+    } else {                                             // fused decide: publish, then arrive
+#pragma unroll
+        for (int k = 0; k < 6; ++k) __hip_atomic_store(nw + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t old = __hip_atomic_fetch_add(D.arrive_g + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old & 1u) {                                  // K1 published the pod words first
+            int64_t pw[PW_K];
+#pragma unroll
+            for (int k = 0; k < PW_K; ++k)
+                pw[k] = __hip_atomic_load(D.pwords + (int64_t)g * PW_K + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            decide_store(G, N.gnode[g], g, pw, v, D.dec, D.cdec);
+        }
+    }
+    }
 }
 
 // K3 (k_fold_decide): the K1 workgroups' slot partials folded and joined to the groups, in
@@ -2109,9 +2275,9 @@ hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows
 }
 
 hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t* node_rows, int64_t* trk_acc,
-                              int64_t* nwords, hipStream_t st) {
+                              int64_t* nwords, const NGDecide& nd, hipStream_t st) {
     hipLaunchKernelGGL(k_node_groups, dim3((g.G + 63) / 64), dim3(NG_WAVES * 64), 0, st, g, n, node_rows, trk_acc,
-                       nwords);
+                       nwords, nd);
     return hipGetLastError();
 }
 

@@ -164,6 +164,11 @@ struct esc_ctx {
     uint32_t* d_k1_ticket = nullptr;                          // K1 dynamic shares (next chunk, done)
     int64_t* d_k1seg = nullptr;                               // K1 work plan [nblk][K1_SEGS][2]
     int k1_cap = 0;                                           // K1 chunks per workgroup at most (0: static)
+    bool k1_fold = false;                                     // the fold fused into K1 (K1Fold)
+    bool k1_fold_allowed = false;                             // ESC_FUSED_FOLD=1 (off: DESIGN.md §8b), not after a timeout
+    unsigned long long* d_k1_arrive = nullptr;
+    uint32_t* d_arrive_g = nullptr;                           // per-group arrivals (fused decide)
+    uint32_t *d_k1_err = nullptr, *d_k1_goff = nullptr;
     int64_t* d_trk_acc = nullptr;                             // [G][TA_K] dry-mode tracked sums
     int64_t* d_pwords = nullptr;                              // active exchange buffer [G][PW_K]
     int64_t* own_pwords = nullptr;                            // the context-owned one
@@ -392,6 +397,8 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
 
 void release_work(esc_ctx* c) {
     dfree(c->d_k1seg); dfree(c->d_pod_part); dfree(c->d_wide_pod); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
+    dfree(c->d_k1_arrive); dfree(c->d_k1_err); dfree(c->d_k1_goff); dfree(c->d_arrive_g);
+    c->k1_fold = false;
     dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_cdec); dfree(c->d_metrics);
     c->d_pwords = nullptr;
     if (c->h_cdec) hipHostFree(c->h_cdec);
@@ -737,6 +744,35 @@ int32_t ensure_work(esc_ctx* c) {
     HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * SP));
     (void)n_col;
     HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
+    {   // the fold fused into K1: one LDS window, slices of <= 512 slots, every workgroup
+        // co-resident (the grid barrier), the production variant
+        const int per = k1_blocks_per_cu(gw);
+        c->k1_fold = c->k1_fold_allowed && c->k1_variant == 0 && S <= POD_WINDOW_MAX && nblk > 0 &&
+                     (S + nblk - 1) / nblk <= 512 && per > 0 && nblk <= (int64_t)per * c->cu_count;
+        if (c->k1_fold) {
+            std::vector<uint32_t> gslot(G), order(G);
+            for (int32_t g = 0; g < G; ++g) {
+                gslot[g] = g == c->gi.default_group ? c->gi.n_gp : c->gi.gpair[g];
+                order[g] = (uint32_t)g;
+            }
+            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return gslot[a] < gslot[b]; });
+            std::vector<uint32_t> goff(nblk + 1);
+            for (int64_t b = 0; b <= nblk; ++b) {
+                const int64_t lo = S * b / nblk;
+                goff[b] = (uint32_t)(std::lower_bound(order.begin(), order.end(), (uint32_t)lo,
+                                                      [&](uint32_t g, uint32_t v) { return gslot[g] < v; }) -
+                                     order.begin());
+            }
+            HIP_TRY(dalloc(&c->d_k1_goff, goff.size()));
+            HIP_TRY(hipMemcpy(c->d_k1_goff, goff.data(), goff.size() * 4, hipMemcpyHostToDevice));
+            HIP_TRY(dalloc(&c->d_k1_arrive, 1));
+            HIP_TRY(dalloc(&c->d_arrive_g, G));
+            HIP_TRY(dalloc(&c->d_k1_err, 1));
+            HIP_TRY(hipMemset(c->d_k1_arrive, 0, 8));
+            HIP_TRY(hipMemset(c->d_arrive_g, 0, (size_t)G * 4));
+            HIP_TRY(hipMemset(c->d_k1_err, 0, 4));
+        }
+    }
     HIP_TRY(dalloc(&c->d_k1_ticket, 2));
     HIP_TRY(hipMemset(c->d_k1_ticket, 0, 2 * sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)S * WP_K * sizeof(int64_t)));
@@ -772,22 +808,46 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
         HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
     }
     int nblk = 0;
+    const bool fused = c->k1_fold && !c->force_wide && c->nblk;
+    // the decision inside K1 too when the node words come from the side stream beside it
+    const bool fdec = fused && decide && fork && c->world == 1;
+    DecCompact* cdec = c->zero_copy ? c->h_cdec_dev : c->d_cdec;
     if (c->force_wide) {
         if (c->k_tiles + c->c_tiles) HIP_TRY(launch_wide_pods(pod_dev(c, r), g, c->d_wide_pod, st));
     } else if (c->nblk) {
         const PodDev p = pod_dev(c, r);
         const int32_t S = (int32_t)pod_slots(c);
+        K1Fold fold{};
+        if (fused) {
+            // the big C tiles add to the wide rows the fold reads: they go first
+            HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
+            fold.arrive = c->d_k1_arrive;
+            fold.err = c->d_k1_err;
+            fold.pwords = c->d_pwords;
+            fold.goff = c->d_k1_goff;
+            fold.groups = c->d_col_groups;
+            fold.n_slots = S;
+            if (fdec) {
+                fold.arrive_g = c->d_arrive_g;
+                fold.nwords = c->d_nwords;
+                fold.gnode = n.gnode;
+                fold.dec = c->d_dec;
+                fold.cdec = cdec;
+            }
+        }
         for (int32_t g0 = 0; g0 < S; g0 += POD_WINDOW_MAX) {           // LDS windows of pod slots
             const int32_t gw = std::min(POD_WINDOW_MAX, S - g0);
             HIP_TRY(launch_pod_reduce(p, g, g0, gw, c->nblk, c->k1_variant, c->d_pod_part, c->d_wide_pod,
-                                      c->d_k1_ticket, c->k1_cap, st));
+                                      c->d_k1_ticket, c->k1_cap, fold, st));
         }
-        HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
+        if (!fused) HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
         nblk = c->nblk;
     }
     if (fork) {
         HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, c->side));
-        HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, c->side));
+        NGDecide nd{};
+        if (fdec) nd = NGDecide{c->d_arrive_g, c->d_pwords, c->d_dec, cdec};
+        HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, nd, c->side));
         // the orderings (taintOldestN / untaintNewestN inputs) depend on the node flags
         // only: they run on the side stream too, beside K1
         if (c->order_in_step) HIP_TRY(enqueue_order(c, c->side));
@@ -796,10 +856,9 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     } else {
         if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
         HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, st));
-        HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, st));
+        HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, NGDecide{}, st));
     }
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-    DecCompact* cdec = c->zero_copy ? c->h_cdec_dev : c->d_cdec;
     FoldPlan f;
     f.part = c->d_pod_part;
     f.nblk = nblk;
@@ -808,7 +867,11 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     f.col_off = c->d_col_off;
     f.col_groups = c->d_col_groups;
     f.ablate = c->k3_ablate;
-    HIP_TRY(launch_fold_decide(g, n, f, c->d_wide_pod, c->d_pwords, c->d_nwords, decide, c->d_dec, cdec, st));
+    if (fused) {                                     // pod words from K1: the decision alone
+        if (decide && !fdec) HIP_TRY(launch_decide(g, n, c->d_pwords, c->d_nwords, c->d_dec, cdec, st));
+    } else {
+        HIP_TRY(launch_fold_decide(g, n, f, c->d_wide_pod, c->d_pwords, c->d_nwords, decide, c->d_dec, cdec, st));
+    }
     if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
     if (copy_out && !c->zero_copy) {
         HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)g.G * sizeof(DecCompact), hipMemcpyDeviceToHost, st));
@@ -919,6 +982,7 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
         return fail(ESC_E_HIP);
     if (const char* v = std::getenv("ESC_NO_FORK")) c->fork_nodes = std::atoi(v) == 0;
+    if (const char* v = std::getenv("ESC_FUSED_FOLD")) c->k1_fold_allowed = std::atoi(v) != 0;
     if (const char* v = std::getenv("ESC_NO_ZEROCOPY")) c->zero_copy = std::atoi(v) == 0;
     const size_t G = (size_t)n_groups;
     if (dalloc(&c->d_dry, G) || dalloc(&c->d_params, G)) return fail(ESC_E_NOMEM);
@@ -1666,6 +1730,17 @@ int32_t esc_sync(esc_ctx* c) {
     if (!c->has_device) return ESC_E_NODEV;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->k1_fold && c->pending) {
+        uint32_t err = 0;
+        HIP_TRY(hipMemcpy(&err, c->d_k1_err, 4, hipMemcpyDeviceToHost));
+        if (err) {                                   // a grid barrier gave up: results invalid,
+            c->k1_fold_allowed = false;              // the separate fold from now on
+            release_work(c);
+            std::snprintf(g_last_error, sizeof g_last_error, "K1 fused-fold barrier timed out (fold disabled; rerun)");
+            c->pending = false;
+            return ESC_E_HIP;
+        }
+    }
     if (c->timing && c->pending && c->n_stage_ev > 1) {
         float ms = 0;
         for (int i = 0; i + 1 < c->n_stage_ev; ++i) {
