@@ -323,6 +323,7 @@ def main():
         ex = Exchange(ctx, device_collective=backend == "nccl")
         ctx.use_graph(True)                       # the shard's K1/K2/K3 step replays as one graph
         step = ex.step
+    ctx.k1_calibrate(10)                          # K1 shares to this device's rates (untimed, once per load)
 
     def barrier():
         if dist is not None:

@@ -258,6 +258,20 @@ class Context:
         L.check(self.lib.esc_stage_times(self.handle, a, 8))
         return list(a)
 
+    def k1_calibrate(self, rounds: int = 4):
+        """Balances K1's per-workgroup shares to this device's measured streaming rates
+        (esc_k1_calibrate; results unchanged)."""
+        L.check(self.lib.esc_k1_calibrate(self.handle, int(rounds)), "esc_k1_calibrate")
+
+    def k1_trace(self):
+        """Per-workgroup K1 timestamps of the last decision (diagnostics):
+        uint64 [nblk, 8] = start, K tiles done, C tiles done, flushed (100 MHz ticks), HW_ID, XCC_ID."""
+        n = C.c_int64(0)
+        L.check(self.lib.esc_k1_trace(self.handle, None, 0, C.byref(n)))
+        a = np.zeros((n.value, 8), dtype=np.uint64)
+        L.check(self.lib.esc_k1_trace(self.handle, a.ctypes.data_as(C.POINTER(C.c_uint64)), a.size, C.byref(n)))
+        return a
+
     def run(self):
         L.check(self.lib.esc_run(self.handle), "esc_run")
 

@@ -9,30 +9,56 @@
 namespace esc {
 
 // A class of homogeneous pod tiles: every pod of the class has the same record
-// signature (extra regular containers, init containers, overhead, extra pairs), so record
-// k of a tile's 256 pods is one contiguous 256-entry row.
+// signature (extra regular containers, init containers, overhead, extra pairs), so every
+// field and record k of a tile's 256 pods is one contiguous 256-entry row.
 struct PodClass {
     int64_t t0, t1;            // tiles [t0, t1) of the K section
-    int64_t xc0, xp0;          // first record-row entry of tile t0 (xc_cpu / xc_mem, xp)
+    int64_t kb0, rsv;          // u32-word offset of tile t0's block in the K-block array
     int64_t w0;                // K1 work weight of the tiles before t0
     uint32_t xreg, xinit, ovh, nxp;
     uint32_t kind;             // (xreg + xinit + ovh) * 4 + nxp: selects K1's pipeline
-    uint32_t wt;               // work weight of one tile: its 16-B loads per lane
+    uint32_t wt;               // work weight of one tile: its 16-B loads per lane (= block KB)
 };
 // weight (16-B loads per lane) of a K tile with R records and NXP extra pairs per pod
 constexpr uint32_t k_tile_weight(uint32_t R, uint32_t NXP) { return 5 + 4 * R + NXP; }
 constexpr int POD_CLASS_IDS = 128;   // signatures with <= 3 extra records and <= 3 extra pairs
 constexpr int K1_SEGS = 4;           // class runs per K1 workgroup in the work plan (at most)
 
-// Device view of a pod shard.  Two sections of the same arrays, made at load
-// (esc_load_pods; sums are order-independent):
+// K blocks (tile-major K section).  Tile t of a class is ONE contiguous block of wt KB
+// (wt = 5 + 4R + NXP): a wave streams a tile as wt consecutive 1-KB wave-loads from one
+// address range instead of wt loads from 4 + 2R + 1 separate arrays (the SoA streams cost
+// 6.5 % at 100 M pods and 4 % at 12.5 M in scripts/k1_shape_probe.hip, profiles/r02_v8).
+// Word offsets inside a block (u32 words; 8-byte rows are 512 words = 256 entries):
+//   flags [0, 256)  cpu0 [256, 512)  mem0 [512, 1024)  pair0 [1024, 1280)
+//   record k: cpu [1280 + 1024k, +512), mem [+512, +1024)   extra pair k: [1280 + 1024R + 256k, +256)
+// 4-byte rows hold pod s at entry s; 8-byte rows at pos64(s) = (s%4/2)*128 + 2(s/4) + s%2,
+// so that lane l's 16-B load of either width covers its pods 4l..4l+3 and every wave-load
+// reads one contiguous 1 KB.
+constexpr int KB_CPU0 = 256, KB_MEM0 = 512, KB_PAIR0 = 1024, KB_REC = 1280;
+__host__ __device__ inline int64_t kb_pos64(int64_t s) { return ((s & 3) >> 1) * 128 + 2 * (s >> 2) + (s & 1); }
+// first word of tile t's block (t a tile of class C)
+__host__ __device__ inline int64_t kb_block(const PodClass& C, int64_t t) { return C.kb0 + (t - C.t0) * (int64_t)C.wt * 256; }
+__host__ __device__ inline uint32_t kb_nrec(const PodClass& C) { return C.xreg + C.xinit + C.ovh; }
+// 8-byte element index (into the array viewed as int64) of record k's cpu (mem: +256) of pod s
+__host__ __device__ inline int64_t kb_rec64(int64_t blk, uint32_t k, int64_t s) {
+    return (blk + KB_REC + 1024 * (int64_t)k) / 2 + kb_pos64(s);
+}
+__host__ __device__ inline int64_t kb_xp(const PodClass& C, int64_t blk, uint32_t k, int64_t s) {
+    return blk + KB_REC + 1024 * (int64_t)kb_nrec(C) + 256 * (int64_t)k + s;
+}
+
+// Device view of a pod shard.  Two sections, made at load (esc_load_pods; sums are
+// order-independent):
 //  - K: pods with at most 3 extra container records and at most 3 extra pairs, grouped by
-//    record signature into 256-pod tiles (4 pods per lane, every array a 16-B load);
-//  - C: the others, in 64-pod tiles (1 per lane) whose extra records are contiguous per
-//    tile (xc_base / xp_base).
-// Padding pods carry ESC_PF_DAEMONSET.
+//    record signature into 256-pod tiles, each tile one contiguous block (kb, above);
+//  - C: the others, in 64-pod tiles (1 per lane) in their own SoA arrays (flags .. pair0
+//    indexed from the C section's start), whose extra records are contiguous per tile
+//    (xc_base / xp_base into xc_cpu / xc_mem / xp).
+// Pod slot numbering (the host's and the reaping's): K pod s of tile t = t * 256 + s, C pod
+// i = k_tiles * 256 + i.  Padding pods carry ESC_PF_DAEMONSET.
 struct PodDev {
-    const uint32_t* flags;
+    const uint32_t* kb;        // K blocks
+    const uint32_t* flags;     // C section
     const uint32_t* cpu0;
     const int64_t*  mem0;
     const uint32_t* pair0;
@@ -166,6 +192,10 @@ struct K1Fold {
     const GroupNode* gnode;
     esc_group_decision* dec;
     DecCompact* cdec;
+    // per workgroup 8 words (esc_k1_trace; the share calibration reads words 0-1):
+    // s_memrealtime (100 MHz) at start, after the K tiles, after the C tiles, after the
+    // flush; HW_ID, XCC_ID
+    uint64_t* trace;
 };
 struct NGDecide {               // k_node_groups' side of the fused decide (see K1Fold)
     uint32_t* arrive_g;         // null: no fused decide
@@ -199,7 +229,7 @@ static_assert(sizeof(DecCompact) == 32, "compact decision is 2 x 16 B");
 hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t* node_rows, int64_t* trk_acc,
                               int64_t* nwords, const NGDecide& nd, hipStream_t st);
 // K3 (k_fold_decide): fold of the K1 partials + group join + decide, one workgroup per column.
-constexpr int FC_COL = 128;            // pod slots per K3 column (one 16-B wave-load of a row)
+constexpr int FC_COL = 32;             // pod slots per K3 column (a 256-B piece of each K1 row)
 struct FoldPlan {
     const uint64_t* part;              // K1 partials: row b = cc[sp], mem[sp] at part + 2 * sp * b
     int nblk;                          // K1 rows
@@ -257,6 +287,7 @@ size_t sort_hist_words(int64_t n);   // digit-histogram words one LSD pass over 
 struct OrdChunk {               // K5 per-decision chunk: memberships [start, end) of one group
     uint32_t start, end, group, pad;
 };
+constexpr uint32_t ORD_CHUNK_DRY = 2u;   // OrdChunk::pad bit of a split chunk: its group is in dry mode
 constexpr int ORD_CHUNK = 4096;   // memberships per K5 chunk (three-pass default)
 // Group-order padding slot of group g: g | MEMB_PAD (class 3, skipped).  Every group owns a
 // region of the group-order arrays: its memberships oldest first, then padding (the round-up

@@ -216,7 +216,7 @@ typedef __attribute__((address_space(4))) const PodClass cPodClass;   // scalar 
 __device__ __forceinline__ PodClass load_class(const PodClass* cls, int i) {
     const cPodClass* q = (const cPodClass*)cls + i;
     PodClass k;
-    k.t0 = q->t0; k.t1 = q->t1; k.xc0 = q->xc0; k.xp0 = q->xp0;
+    k.t0 = q->t0; k.t1 = q->t1; k.kb0 = q->kb0; k.rsv = 0;
     k.w0 = q->w0;
     k.xreg = q->xreg; k.xinit = q->xinit; k.ovh = q->ovh; k.nxp = q->nxp; k.kind = q->kind; k.wt = q->wt;
     return k;
@@ -226,28 +226,29 @@ __device__ __forceinline__ PodClass load_class(const PodClass* cls, int i) {
 // (j / 2) * 128 + 2l + j % 2 of the 8-byte ones (pos64), so that every wave-load of either
 // width reads one contiguous 1 KB (an 8-byte array read as lanes x 4 consecutive pods would
 // stride 32 B and double the requests per byte).
-__device__ __forceinline__ int64_t pos64(uint32_t s) { return ((s & 3) >> 1) * 128 + 2 * (s >> 2) + (s & 1); }
 
+// One tile = one contiguous block (esc_kernels.h, K blocks): every load below is lane l's
+// 16 B at a compile-time offset from the block's first word.
 template <int R, int NXP>
 __device__ __forceinline__ void k_load(const PodDev& P, const PodClass& C, int64_t t, uint32_t lane,
                                        KTile<R, NXP>& T) {
-    const int64_t p0 = t * TILE + lane * PODS_PER_LANE, q0 = t * TILE + lane * 2;
-    T.f = ld4(P.flags + p0);
-    T.c = ld4(P.cpu0 + p0);
-    T.m[0] = ld2(P.mem0 + q0);
-    T.m[1] = ld2(P.mem0 + q0 + 128);
-    T.p = ld4(P.pair0 + p0);
-    const int64_t rt = t - C.t0;
+    constexpr int64_t BW = (int64_t)k_tile_weight(R, NXP) * 256;        // block words
+    const uint32_t* b = P.kb + C.kb0 + (t - C.t0) * BW + lane * 4;
+    auto l8 = [&](int off) { return ld2(reinterpret_cast<const int64_t*>(b + off)); };
+    T.f = ld4(b);
+    T.c = ld4(b + KB_CPU0);
+    T.m[0] = l8(KB_MEM0);
+    T.m[1] = l8(KB_MEM0 + 256);
+    T.p = ld4(b + KB_PAIR0);
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        const int64_t o = C.xc0 + (rt * R + k) * TILE + lane * 2;
-        T.rc[k][0] = ld2(P.xc_cpu + o);
-        T.rc[k][1] = ld2(P.xc_cpu + o + 128);
-        T.rm[k][0] = ld2(P.xc_mem + o);
-        T.rm[k][1] = ld2(P.xc_mem + o + 128);
+        T.rc[k][0] = l8(KB_REC + 1024 * k);
+        T.rc[k][1] = l8(KB_REC + 1024 * k + 256);
+        T.rm[k][0] = l8(KB_REC + 1024 * k + 512);
+        T.rm[k][1] = l8(KB_REC + 1024 * k + 768);
     }
 #pragma unroll
-    for (int k = 0; k < NXP; ++k) T.rq[k] = ld4(P.xp + C.xp0 + (rt * NXP + k) * TILE + lane * PODS_PER_LANE);
+    for (int k = 0; k < NXP; ++k) T.rq[k] = ld4(b + KB_REC + 1024 * R + 256 * k);
 }
 
 // ComputePodResourceRequest (scheduler/types.go:72-89) for each of the lane's 4 pods:
@@ -373,7 +374,7 @@ struct CTile {
 // record arrays carry one element of padding), so the compiler's vmcnt accounting can
 // leave a second tile's loads in flight while the first is processed.
 __device__ __forceinline__ void c_load(const PodDev& P, int64_t t, uint32_t lane, const TileBases& b, CTile& T) {
-    const int64_t i = P.k_tiles * TILE + t * CTILE + lane;
+    const int64_t i = t * CTILE + lane;                  // C arrays start at the C section
     T.b = b;
     T.f = ldnt(P.flags + i);
     T.c = ldnt(P.cpu0 + i);
@@ -459,7 +460,7 @@ __device__ __forceinline__ void c_process(const GroupDev& G, const PodSink<ABLAT
 // Exact (any-range) evaluation of one C tile from memory, one pod per lane.
 __device__ __forceinline__ void c_tile_exact(const PodDev& P, const GroupDev& G, int64_t t, uint32_t lane,
                                              int64_t* __restrict__ wide) {
-    const int64_t i = P.k_tiles * TILE + t * CTILE + lane;
+    const int64_t i = t * CTILE + lane;
     const uint32_t f = P.flags[i];
     const uint32_t nxc = pf_xctr(f), nxp = pf_xpair(f);
     uint32_t oc = P.xc_base[t] + wave_incl_scan32(nxc) - nxc;
@@ -678,6 +679,12 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     constexpr int NW = THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     __shared__ uint32_t s_chunk;
+    uint64_t* const trace = FF.trace ? FF.trace + (int64_t)blockIdx.x * 8 : nullptr;
+    if (trace && threadIdx.x == 0) {
+        trace[0] = __builtin_amdgcn_s_memrealtime();
+        trace[4] = (uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
+        trace[5] = (uint64_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
+    }
     for (uint32_t i = threadIdx.x; i < 2 * gw; i += THREADS) lds[i] = 0;
     const PodSink<ABLATE> K{PodLds{lds, lds + gw, g0, gw}, PodWide{wide}};
     const uint32_t lane = threadIdx.x & 63;
@@ -746,6 +753,10 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
         if (!DYN || taken >= cap) break;
         chunk = grab();
     }
+    if (trace) {
+        __syncthreads();
+        if (threadIdx.x == 0) trace[1] = __builtin_amdgcn_s_memrealtime();
+    }
     if (!(ABLATE & 4)) {
         const int64_t per = (P.c_tiles + gridDim.x - 1) / gridDim.x;
         const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(lo + per, P.c_tiles);
@@ -784,6 +795,7 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
         }
     }
     __syncthreads();
+    if (trace && threadIdx.x == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
     const int64_t S = G.sp;                                  // row stride (K3 reads whole columns)
     uint64_t* out = part + (int64_t)blockIdx.x * 2 * S + g0;
     if (!DYN && !ABLATE && FF.arrive) {               // fused fold: write-through (agent-scope) stores
@@ -796,6 +808,11 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
             out[i] = lds[i];
             out[S + i] = lds[gw + i];
         }
+    }
+    if (trace) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) trace[3] = __builtin_amdgcn_s_memrealtime();
     }
     if (DYN && threadIdx.x == 0) {
         // every workgroup's last grab precedes its increment here: the last one resets
@@ -827,6 +844,12 @@ hipError_t launch_pod_reduce_ablation(ESC_K1_ARGS) __attribute__((weak));
 #if ESC_PART == 0
 bool k1_dynamic(int variant) { return variant == 5; }
 
+static K1Fold trace_only(const K1Fold& f) {
+    K1Fold t{};
+    t.trace = f.trace;
+    return t;
+}
+
 int k1_blocks_per_cu(int gw) {
     int nb = 0;
     const size_t lds = std::max<size_t>((size_t)gw * 2 * sizeof(uint64_t), (size_t)K1_FOLD_LDS);
@@ -841,10 +864,11 @@ hipError_t launch_pod_reduce(ESC_K1_ARGS) {
     switch (variant) {
         case 0: ESC_K1(512, 0, 3); break;
         case 1: case 2: case 5: case 6:
-            return launch_pod_reduce_alt(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, K1Fold{}, st);
+            return launch_pod_reduce_alt(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, trace_only(fold), st);
         default:                                  // timing-only ablations (ABLATIONS=1 build)
             if (!launch_pod_reduce_ablation) return hipErrorInvalidValue;
-            return launch_pod_reduce_ablation(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, K1Fold{}, st);
+            return launch_pod_reduce_ablation(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, trace_only(fold),
+                                              st);
     }
     return hipGetLastError();
 }
@@ -897,23 +921,24 @@ namespace {
 __device__ __forceinline__ void k_tile_exact(const PodDev& P, const GroupDev& G, const PodClass& C, int64_t t,
                                              uint32_t lane, int64_t* __restrict__ wide) {
     const PodWide acc{wide};
-    const uint32_t R = C.xreg + C.xinit + C.ovh;
-    const int64_t rt = t - C.t0;
+    const uint32_t R = kb_nrec(C);
+    const int64_t blk = kb_block(C, t);
+    const int64_t* kb64 = reinterpret_cast<const int64_t*>(P.kb);
     for (int j = 0; j < PODS_PER_LANE; ++j) {
         const uint32_t s = lane * PODS_PER_LANE + j;
-        const int64_t i = t * TILE + s, i64 = t * TILE + pos64(s);
-        const uint32_t f = P.flags[i];
+        const uint32_t f = P.kb[blk + s];
         if (f & ESC_PF_DAEMONSET) continue;
-        uint64_t cpu = P.cpu0[i], mem = (uint64_t)P.mem0[i64];
+        uint64_t cpu = P.kb[blk + KB_CPU0 + s], mem = (uint64_t)kb64[(blk + KB_MEM0) / 2 + kb_pos64(s)];
         for (uint32_t k = 0; k < R; ++k) {
-            const int64_t o = C.xc0 + (rt * R + k) * TILE + pos64(s);
-            apply_rec(k, R, C.xreg, C.xreg + C.xinit, (unsigned long long)P.xc_cpu[o],
-                      (unsigned long long)P.xc_mem[o], cpu, mem);
+            const int64_t o = kb_rec64(blk, k, s);
+            apply_rec(k, R, C.xreg, C.xreg + C.xinit, (unsigned long long)kb64[o],
+                      (unsigned long long)kb64[o + 256], cpu, mem);
         }
+        const uint32_t q0 = P.kb[blk + KB_PAIR0 + s];
         if (pf_default_ok(f) && G.default_group != NONE) acc.add(G.n_gp, (int64_t)cpu, (int64_t)mem);
-        if (P.pair0[i] < G.n_gp) acc.add(P.pair0[i], (int64_t)cpu, (int64_t)mem);
+        if (q0 < G.n_gp) acc.add(q0, (int64_t)cpu, (int64_t)mem);
         for (uint32_t k = 0; k < C.nxp; ++k) {
-            const uint32_t q = P.xp[C.xp0 + (rt * C.nxp + k) * TILE + s];
+            const uint32_t q = P.kb[kb_xp(C, blk, k, s)];
             if (q < G.n_gp) acc.add(q, (int64_t)cpu, (int64_t)mem);
         }
     }
@@ -1202,20 +1227,24 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
 }
 
 // K3 (k_fold_decide): the K1 workgroups' slot partials folded and joined to the groups, in
-// ONE launch with no hand-off between workgroups: one 1024-thread workgroup per column of
-// FC_COL pod slots reads every K1 row of its column (16-B loads, a wave-load covers the 128
-// slots of one row, 16 waves x up to 16 rows in flight: ~0.5 MB per CU, read back from the
-// Infinity Cache K1 just wrote it through), merges the waves in LDS, adds the slots' wide
-// (exact-path) rows, and evaluates every group whose pod slot lies in the column
-// (col_off / col_groups): pod words, then K4 (decide_one) for one rank.  The group inputs
-// that do not depend on the fold (node words from K2b, GroupNode, parameters) are loaded
-// before the fold's loads are consumed.
+// ONE launch with no hand-off between workgroups: one 256-thread workgroup per column of
+// FC_COL pod slots reads every K1 row of its column (16-B loads; a wave-load covers
+// FD_RPL rows of FC_COL slots, 4 waves x FD_U wave-loads in flight: every row of a
+// 256-workgroup K1 grid in one round, read back from the Infinity Cache K1 just wrote it
+// through), merges the lanes and waves in LDS, adds the slots' wide (exact-path) rows, and
+// evaluates every group whose pod slot lies in the column (col_off / col_groups): pod
+// words, then K4 (decide_one) for one rank.  Narrow columns give ~n_gp / 32 workgroups
+// (313 at 10 k groups) so the whole chip folds: 128-slot columns left 79 CUs reading
+// 0.5 MB each (18.6 us at 12.5 M pods, profiles/r02_v3).
 //  - pods: the group's slot is its pair (NewPodAffinityFilterFunc, node_group.go:218) or,
 //    for the group named "default", the default filter's slot (client.go:58-64);
 //  - allNodes[0] (controller.go:208): the pair's first entry (GroupNode, set at load).
 namespace {
-constexpr int FD_WAVES = 16;
-constexpr int FD_U = 16;                 // K1 rows per wave in flight
+constexpr int FD_WAVES = 4;
+constexpr int FD_U = 16;                 // wave-loads per wave in flight (each array)
+constexpr int FD_HL = FC_COL / 2;        // lanes per row (2 slots per 16-B lane load)
+constexpr int FD_RPL = 64 / FD_HL;       // K1 rows per wave-load
+static_assert(FD_RPL * FD_HL == 64 && FD_WAVES >= 2, "fold lane map");
 }  // namespace
 
 __global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeDev N, FoldPlan F,
@@ -1225,33 +1254,36 @@ __global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeD
                                                                  esc_group_decision* __restrict__ dec,
                                                                  DecCompact* __restrict__ cdec, int ablate) {
     // ablate (timing-only, wrong results): 1 no group phase, 4 no fold loads
-    __shared__ uint64_t red[FD_WAVES][8][64];            // 64 KB
+    __shared__ uint64_t red[FD_WAVES][8][64];            // 16 KB
     __shared__ uint64_t tot[4][FC_COL];                 // per slot: cpu, count, mem lo, mem carry
     __shared__ int64_t wtot[WP_K][FC_COL];              // per slot: its wide row
     __shared__ DecCompact sdec[FC_COL];
     __shared__ uint32_t s_seq;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int sub = lane / FD_HL, hl = lane % FD_HL;
     const int col = blockIdx.x;
     const int64_t s0 = (int64_t)col * FC_COL;
     const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
-    // ---- the group inputs that do not depend on the fold: first pass's groups, issued now
     const uint32_t me = threadIdx.x;
     if (me == 0) s_seq = 1u;
-    // ---- fold: every K1 row of the column; wave w takes rows w, w + 16, ...
+    // ---- fold: every K1 row of the column; wave w's load u covers rows
+    //      (w + FD_WAVES * u) * FD_RPL + sub
     uint64_t cp[2] = {0, 0}, cn[2] = {0, 0}, ml[2] = {0, 0}, mc[2] = {0, 0};
     const int nrows = (ablate & 4) ? 0 : F.nblk;
-    for (int b = wid; b < nrows; b += FD_WAVES * FD_U) {
+    constexpr int STEP = FD_WAVES * FD_U * FD_RPL;
+    for (int b = wid * FD_RPL + sub; b - sub < nrows; b += STEP) {
         ulonglong2 c[FD_U], m[FD_U];
 #pragma unroll
         for (int u = 0; u < FD_U; ++u) {
-            const int bb = b + FD_WAVES * u < nrows ? b + FD_WAVES * u : b;
-            const int64_t* row = reinterpret_cast<const int64_t*>(F.part) + (int64_t)bb * 2 * F.sp + s0 + 2 * lane;
+            const int r = b + FD_WAVES * FD_RPL * u;
+            const int bb = r < nrows ? r : 0;
+            const int64_t* row = reinterpret_cast<const int64_t*>(F.part) + (int64_t)bb * 2 * F.sp + s0 + 2 * hl;
             c[u] = ld2(row);
             m[u] = ld2(row + F.sp);
         }
 #pragma unroll
         for (int u = 0; u < FD_U; ++u) {
-            if (b + FD_WAVES * u >= nrows) break;
+            if (b + FD_WAVES * FD_RPL * u >= nrows) continue;
             cp[0] += c[u].x & CPU_MASK; cn[0] += c[u].x >> CNT_SHIFT;
             cp[1] += c[u].y & CPU_MASK; cn[1] += c[u].y >> CNT_SHIFT;
             u128_add(ml[0], mc[0], m[u].x);
@@ -1260,7 +1292,7 @@ __global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeD
     }
     red[wid][0][lane] = cp[0]; red[wid][1][lane] = cp[1]; red[wid][2][lane] = cn[0]; red[wid][3][lane] = cn[1];
     red[wid][4][lane] = ml[0]; red[wid][5][lane] = ml[1]; red[wid][6][lane] = mc[0]; red[wid][7][lane] = mc[1];
-    // the slots' wide rows (threads 0-127), read and reset (every reader is in this block)
+    // the slots' wide rows (threads < FC_COL), read and reset (every reader is in this block)
     int64_t p[WP_K] = {0, 0, 0, 0, 0};
     if (me < FC_COL && s0 + me <= (int64_t)G.n_gp) {
         int64_t* wp = wide_pod + (s0 + me) * WP_K;
@@ -1272,15 +1304,19 @@ __global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeD
                 __hip_atomic_store(wp + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
-    if (wid < 2) {                                        // wave 0: slots 2l, 2l+1 words 0/1; wave 1: mem words
+    if (wid < 2 && lane < FD_HL) {                       // wave 0: slots 2l, 2l+1 words 0/1; wave 1: mem words
         const int j = lane;
         uint64_t x0 = 0, x1 = 0, y0 = 0, y1 = 0;
         for (int w = 0; w < FD_WAVES; ++w) {
-            if (wid == 0) {
-                x0 += red[w][0][j]; x1 += red[w][1][j]; y0 += red[w][2][j]; y1 += red[w][3][j];
-            } else {
-                u128_add(x0, y0, red[w][4][j]); y0 += red[w][6][j];
-                u128_add(x1, y1, red[w][5][j]); y1 += red[w][7][j];
+#pragma unroll
+            for (int q = 0; q < FD_RPL; ++q) {
+                const int l = q * FD_HL + j;
+                if (wid == 0) {
+                    x0 += red[w][0][l]; x1 += red[w][1][l]; y0 += red[w][2][l]; y1 += red[w][3][l];
+                } else {
+                    u128_add(x0, y0, red[w][4][l]); y0 += red[w][6][l];
+                    u128_add(x1, y1, red[w][5][l]); y1 += red[w][7][l];
+                }
             }
         }
         if (wid == 0) { tot[0][2 * j] = x0; tot[0][2 * j + 1] = x1; tot[1][2 * j] = y0; tot[1][2 * j + 1] = y1; }
@@ -1653,24 +1689,24 @@ __device__ __forceinline__ uint32_t ord_class(const NodeDev&, uint32_t, uint32_t
 }
 
 // A: classes of the chunk's memberships (one u32 of 4 class bytes per quad) and the
-// chunk's count per class.  Quads: 16-B loads of node / group / flags per lane.
+// chunk's count per class.  A split chunk holds one group's memberships, so the class is a
+// function of the flags alone (4 B per membership): the group's dry mode comes with the
+// chunk (OrdChunk::pad & ORD_CHUNK_DRY) and region padding is flagged ESC_NF_ABSENT
+// (k_region_pad) like a deleted node.  Quads: one 16-B load of flags per lane.
 __global__ __launch_bounds__(ORD_BLOCK) void k_ord_count(NodeDev N, const OrdChunk* __restrict__ chunks,
-                                                         const uint32_t* __restrict__ g_node,
-                                                         const uint32_t* __restrict__ g_grp,
                                                          const uint32_t* __restrict__ g_flags,
                                                          uint32_t* __restrict__ cls4, uint32_t* __restrict__ ccnt) {
     __shared__ uint32_t red[ORD_WAVES][3];
     const OrdChunk ch = chunks[blockIdx.x];
+    const uint32_t gword = (ch.pad & ORD_CHUNK_DRY) ? NODE_DRY_BIT : 0u;   // ord_class's group word
     uint32_t c[3] = {0, 0, 0};
     constexpr uint32_t STEP = 4 * ORD_BLOCK;
     constexpr int H = ORD_CHUNK / STEP;                  // the whole chunk's quads in flight
     for (uint32_t b0 = ch.start + 4 * threadIdx.x; b0 < ch.end; b0 += H * STEP) {
-        uint4 nd[H], gr[H], fl[H];
+        uint4 fl[H];
 #pragma unroll
         for (int h = 0; h < H; ++h) {
             const uint32_t b = b0 + h * STEP < ch.end ? b0 + h * STEP : b0;
-            nd[h] = ld4(g_node + b);
-            gr[h] = ld4(g_grp + b);
             fl[h] = ld4(g_flags + b);
         }
 #pragma unroll
@@ -1680,7 +1716,7 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_count(NodeDev N, const OrdChu
             uint32_t packed = 0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t k = b + j < ch.end ? ord_class(N, lane4(nd[h], j), lane4(gr[h], j), lane4(fl[h], j)) : 3u;
+                const uint32_t k = b + j < ch.end ? ord_class(N, 0u, gword, lane4(fl[h], j)) : 3u;
                 packed |= k << (8 * j);
                 c[0] += k == 0;
                 c[1] += k == 1;
@@ -1931,7 +1967,7 @@ __global__ __launch_bounds__(256) void k_region_pad(const uint32_t* __restrict__
     for (uint32_t i = pstart[g] + plen[g] + threadIdx.x; i < pstart[g + 1]; i += blockDim.x) {
         g_grp[i] = (uint32_t)g | MEMB_PAD;
         g_node[i] = 0;
-        g_flags[i] = 0;
+        g_flags[i] = ESC_NF_ABSENT;                     // class 3 from the flags alone (k_ord_count)
     }
 }
 
@@ -2124,8 +2160,6 @@ namespace {
 // The pod behind device slot d, as a PodRef (pairs inline, or indirect for big C pods).
 __device__ PodRef podref_of(const PodDev& P, uint32_t d) {
     PodRef r;
-    r.flags = P.flags[d];
-    r.pair0 = P.pair0[d];
     r.p[0] = r.p[1] = r.p[2] = NONE;
     const int64_t kpods = P.k_tiles * TILE;
     if ((int64_t)d < kpods) {
@@ -2136,12 +2170,16 @@ __device__ PodRef podref_of(const PodDev& P, uint32_t d) {
             if (P.cls[mid].t0 <= t) lo = mid; else hi = mid - 1;
         }
         const PodClass& C = P.cls[lo];
-        const int64_t rt = t - C.t0;
-        for (uint32_t k = 0; k < C.nxp && k < 3; ++k) r.p[k] = P.xp[C.xp0 + (rt * C.nxp + k) * TILE + sl];
+        const int64_t blk = kb_block(C, t);
+        r.flags = P.kb[blk + sl];
+        r.pair0 = P.kb[blk + KB_PAIR0 + sl];
+        for (uint32_t k = 0; k < C.nxp && k < 3; ++k) r.p[k] = P.kb[kb_xp(C, blk, k, sl)];
     } else {
         const int64_t c = (int64_t)d - kpods, t = c / CTILE, l = c % CTILE;
+        r.flags = P.flags[c];
+        r.pair0 = P.pair0[c];
         uint32_t off = P.xp_base[t];
-        for (int64_t k = 0; k < l; ++k) off += pf_xpair(P.flags[kpods + t * CTILE + k]);
+        for (int64_t k = 0; k < l; ++k) off += pf_xpair(P.flags[t * CTILE + k]);
         const uint32_t nx = pf_xpair(r.flags);
         if (nx <= 3) {
             for (uint32_t k = 0; k < nx; ++k) r.p[k] = P.xp[off + k];
@@ -2477,8 +2515,8 @@ hipError_t launch_order(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chu
                         int64_t n_e, int32_t G, uint32_t* cls4, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,
                         int64_t* seg, hipStream_t st) {
     if (n_chunks > 0)
-        hipLaunchKernelGGL(k_ord_count, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, g_node, g_grp,
-                           g_flags, cls4, ccnt);
+        hipLaunchKernelGGL(k_ord_count, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, g_flags, cls4,
+                           ccnt);
     if (n_chunks > 0)
         hipLaunchKernelGGL(k_ord_scatter, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, chunks, cls4, g_node, gch_off,
                            grp_off, ccnt, vals, seg);

@@ -61,12 +61,13 @@ void dfree(T*& p) {
 }
 
 struct PodBuf {
+    uint32_t* kb = nullptr;                      // K blocks (tile-major K section)
     uint32_t *flags = nullptr, *cpu0 = nullptr, *pair0 = nullptr, *xp = nullptr, *xc_base = nullptr,
              *xp_base = nullptr, *big = nullptr;
     int64_t *mem0 = nullptr, *xc_cpu = nullptr, *xc_mem = nullptr;
     PodClass* cls = nullptr;
     void release() {
-        dfree(flags); dfree(cpu0); dfree(pair0); dfree(xp); dfree(xc_base); dfree(xp_base); dfree(big);
+        dfree(kb); dfree(flags); dfree(cpu0); dfree(pair0); dfree(xp); dfree(xc_base); dfree(xp_base); dfree(big);
         dfree(mem0); dfree(xc_cpu); dfree(xc_mem); dfree(cls);
     }
 };
@@ -163,8 +164,10 @@ struct esc_ctx {
     int64_t* d_wide_pod = nullptr;
     uint32_t* d_k1_ticket = nullptr;                          // K1 dynamic shares (next chunk, done)
     int64_t* d_k1seg = nullptr;                               // K1 work plan [nblk][K1_SEGS][2]
+    std::vector<double> k1_share;                             // calibrated K1 shares (esc_k1_calibrate)
     int k1_cap = 0;                                           // K1 chunks per workgroup at most (0: static)
     bool k1_fold = false;                                     // the fold fused into K1 (K1Fold)
+    uint64_t* d_k1_trace = nullptr;                           // K1 per-workgroup timestamps (esc_k1_trace)
     bool k1_fold_allowed = false;                             // ESC_FUSED_FOLD=1 (off: DESIGN.md §8b), not after a timeout
     unsigned long long* d_k1_arrive = nullptr;
     uint32_t* d_arrive_g = nullptr;                           // per-group arrivals (fused decide)
@@ -311,6 +314,7 @@ GroupDev group_dev(const esc_ctx* c) {
 PodDev pod_dev(const esc_ctx* c, int replica) {
     const PodBuf& b = c->pods[replica];
     PodDev p;
+    p.kb = b.kb;
     p.flags = b.flags; p.cpu0 = b.cpu0; p.mem0 = b.mem0; p.pair0 = b.pair0;
     p.xc_cpu = b.xc_cpu; p.xc_mem = b.xc_mem; p.xp = b.xp;
     p.xc_base = b.xc_base; p.xp_base = b.xp_base;
@@ -397,6 +401,7 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
 
 void release_work(esc_ctx* c) {
     dfree(c->d_k1seg); dfree(c->d_pod_part); dfree(c->d_wide_pod); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
+    dfree(c->d_k1_trace);
     dfree(c->d_k1_arrive); dfree(c->d_k1_err); dfree(c->d_k1_goff); dfree(c->d_arrive_g);
     c->k1_fold = false;
     dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_cdec); dfree(c->d_metrics);
@@ -530,7 +535,7 @@ int32_t build_age_index(esc_ctx* c) {
             pk_lo = pk_hi = qk_lo = qk_hi = pstart[q + 1];
             for (int64_t a = 0; a < reg; a += c->ord_chunk)
                 chunks.push_back({pstart[q] + (uint32_t)a, pstart[q] + (uint32_t)std::min<int64_t>(reg, a + c->ord_chunk),
-                                  (uint32_t)q, 0u});
+                                  (uint32_t)q, c->params[q].dry ? ORD_CHUNK_DRY : 0u});
             continue;
         }
         if (reg > (uint32_t)ORD_PCHUNK) {          // mid-size: packed up to ORD_CHUNK
@@ -626,9 +631,37 @@ int32_t build_age_index(esc_ctx* c) {
 // tail.  Classes lighter than one share ("small") are each placed whole into one
 // workgroup, beside a chunk of a large class that does not end there; large classes are
 // cut at tile boundaries following the cumulative weight target, so rounding never drifts.
-std::vector<int64_t> plan_k1(const std::vector<PodClass>& cls, int64_t W, int64_t nblk) {
+//
+// `share` (calibrated, esc_k1_calibrate): workgroup k's fraction of the weight; empty = equal.
+std::vector<int64_t> plan_k1(const std::vector<PodClass>& cls, int64_t W, int64_t nblk,
+                             const std::vector<double>& share);
+
+// Largest pod count one workgroup of `plan` sees (K runs + its C tiles).
+int64_t plan_worst(const esc_ctx* c, const std::vector<int64_t>& plan, int64_t nblk) {
+    int64_t worst = 0;
+    for (int64_t b = 0; b < nblk; ++b) {
+        int64_t pods = ((c->c_tiles + nblk - 1) / nblk) * CTILE;
+        for (int k = 0; k < K1_SEGS; ++k) {
+            const int64_t* e = &plan[((size_t)b * K1_SEGS + k) * 2];
+            if (e[1]) pods += (e[1] - (e[0] & ((1ll << 48) - 1))) * TILE;
+        }
+        worst = std::max(worst, pods);
+    }
+    return worst;
+}
+
+std::vector<int64_t> plan_k1(const std::vector<PodClass>& cls, int64_t W, int64_t nblk,
+                             const std::vector<double>& share) {
     std::vector<int64_t> seg((size_t)nblk * K1_SEGS * 2, 0);
     if (W <= 0 || nblk <= 0) return seg;
+    std::vector<int64_t> cut(nblk + 1, 0);                // cumulative weight targets
+    const bool eq = (int64_t)share.size() != nblk;
+    double acc = 0;
+    for (int64_t k = 0; k < nblk; ++k) {
+        acc += eq ? 1.0 / (double)nblk : share[k];
+        cut[k + 1] = eq ? (int64_t)((__int128)W * (k + 1) / nblk) : (int64_t)std::llround(acc * (double)W);
+    }
+    cut[nblk] = W;
     std::vector<int> big, small;
     for (int i = 0; i < (int)cls.size(); ++i) {
         const int64_t w = (cls[i].t1 - cls[i].t0) * (int64_t)cls[i].wt;
@@ -649,7 +682,7 @@ std::vector<int64_t> plan_k1(const std::vector<PodClass>& cls, int64_t W, int64_
             e[1] = b;
             ++ns;
         };
-        const int64_t end = k + 1 == nblk ? W : (int64_t)((__int128)W * (k + 1) / nblk);
+        const int64_t end = cut[k + 1];
         // spread the small classes over the grid, one per workgroup, where the large stream
         // has no boundary inside this workgroup
         if (si < small.size() && k >= (int64_t)si * nblk / std::max<int64_t>(n_small, 1)) {
@@ -721,18 +754,10 @@ int32_t ensure_work(esc_ctx* c) {
     nblk = std::min<int64_t>(nblk, std::max(c->k_tiles, c->c_tiles));
     std::vector<int64_t> plan;
     for (;;) {            // the plan's own per-workgroup pod counts must keep the LDS words exact
-        plan = plan_k1(c->h_cls, c->k_weight, std::max<int64_t>(nblk, 1));
+        if ((int64_t)c->k1_share.size() != nblk) c->k1_share.clear();
+        plan = plan_k1(c->h_cls, c->k_weight, std::max<int64_t>(nblk, 1), c->k1_share);
         if (plan.empty()) break;
-        int64_t worst = 0;
-        for (int64_t b = 0; b < nblk; ++b) {
-            int64_t pods = ((c->c_tiles + nblk - 1) / nblk) * CTILE;
-            for (int k = 0; k < K1_SEGS; ++k) {
-                const int64_t* e = &plan[((size_t)b * K1_SEGS + k) * 2];
-                if (e[1]) pods += (e[1] - (e[0] & ((1ll << 48) - 1))) * TILE;
-            }
-            worst = std::max(worst, pods);
-        }
-        if (worst <= PODS_PER_BLOCK_MAX || nblk >= std::max(c->k_tiles, c->c_tiles)) break;
+        if (plan_worst(c, plan, nblk) <= PODS_PER_BLOCK_MAX || nblk >= std::max(c->k_tiles, c->c_tiles)) break;
         nblk *= 2;
     }
     c->nblk = (int)nblk;
@@ -740,6 +765,8 @@ int32_t ensure_work(esc_ctx* c) {
         HIP_TRY(dalloc(&c->d_k1seg, plan.size()));
         HIP_TRY(hipMemcpy(c->d_k1seg, plan.data(), plan.size() * 8, hipMemcpyHostToDevice));
     }
+    HIP_TRY(dalloc(&c->d_k1_trace, (size_t)std::max<int64_t>(nblk, 1) * 8));
+    HIP_TRY(hipMemset(c->d_k1_trace, 0, (size_t)std::max<int64_t>(nblk, 1) * 64));
     const int64_t SP = slot_stride(c), n_col = SP / FC_COL;
     HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * SP));
     (void)n_col;
@@ -818,6 +845,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
         const PodDev p = pod_dev(c, r);
         const int32_t S = (int32_t)pod_slots(c);
         K1Fold fold{};
+        fold.trace = c->d_k1_trace;
         if (fused) {
             // the big C tiles add to the wide rows the fold reads: they go first
             HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
@@ -983,6 +1011,7 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
         return fail(ESC_E_HIP);
     if (const char* v = std::getenv("ESC_NO_FORK")) c->fork_nodes = std::atoi(v) == 0;
     if (const char* v = std::getenv("ESC_FUSED_FOLD")) c->k1_fold_allowed = std::atoi(v) != 0;
+
     if (const char* v = std::getenv("ESC_NO_ZEROCOPY")) c->zero_copy = std::atoi(v) == 0;
     const size_t G = (size_t)n_groups;
     if (dalloc(&c->d_dry, G) || dalloc(&c->d_params, G)) return fail(ESC_E_NOMEM);
@@ -1133,7 +1162,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     }
     std::vector<PodClass> cls;
     std::vector<int> cls_of(POD_CLASS_IDS, -1);
-    int64_t kt = 0, xk = 0, pk = 0, kw = 0;
+    int64_t kt = 0, kbw = 0, kw = 0;
     for (int id = 0; id < POD_CLASS_IDS; ++id) {
         // with spare slots requested every signature the K layout can hold gets a class, so
         // that inserts of shapes absent at load still land in place
@@ -1149,27 +1178,35 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         const int64_t R = k.xreg + k.xinit + k.ovh, tiles = (want + TILE - 1) / TILE;
         k.t0 = kt;
         k.t1 = kt + tiles;
-        k.xc0 = xk;
-        k.xp0 = pk;
         k.kind = (uint32_t)(R * 4 + k.nxp);
         k.wt = k_tile_weight((uint32_t)R, k.nxp);
+        k.kb0 = kbw;
         k.w0 = kw;
         kw += tiles * k.wt;
         kt += tiles;
-        xk += tiles * R * TILE;
-        pk += tiles * (int64_t)k.nxp * TILE;
+        kbw += tiles * (int64_t)k.wt * 256;
         cls_of[id] = (int)cls.size();
         cls.push_back(k);
     }
     const int64_t k_tiles = kt, c_tiles = (n_c + CTILE - 1) / CTILE;
-    const int64_t c0 = k_tiles * TILE, npad = c0 + c_tiles * CTILE;
-    // record arrays: K rows, then the C records; one element of padding (K1 clamps its
-    // unconditional C record loads)
-    const int64_t nxc_dev = xk + (int64_t)sc_c + 1, nxp_dev = pk + (int64_t)sp_c + 1;
+    const int64_t c0 = k_tiles * TILE, npad = c_tiles * CTILE;   // C arrays: the C section only
+    // C record arrays; one element of padding (K1 clamps its unconditional C record loads)
+    const int64_t nxc_dev = (int64_t)sc_c + 1, nxp_dev = (int64_t)sp_c + 1;
     if (nxc_dev >= (int64_t)0xFFFFFFFF || nxp_dev >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
     std::vector<uint32_t> hf(npad, ESC_PF_DAEMONSET), hc(npad, 0), hp(npad, NONE);
     std::vector<int64_t> hm(npad, 0), hxc(nxc_dev, 0), hxm(nxc_dev, 0);
     std::vector<uint32_t> hxp(nxp_dev, NONE);
+    // K blocks: padding pods are daemonset-flagged with no pairs, padding records 0
+    std::vector<uint32_t> hkb((size_t)kbw, 0);
+    for (const PodClass& k : cls)
+        for (int64_t t = k.t0; t < k.t1; ++t) {
+            const int64_t blk = kb_block(k, t);
+            std::fill(hkb.begin() + blk, hkb.begin() + blk + TILE, ESC_PF_DAEMONSET);
+            std::fill(hkb.begin() + blk + KB_PAIR0, hkb.begin() + blk + KB_PAIR0 + TILE, NONE);
+            const int64_t x0 = kb_xp(k, blk, 0, 0);
+            std::fill(hkb.begin() + x0, hkb.begin() + x0 + (int64_t)k.nxp * TILE, NONE);
+        }
+    int64_t* hkb64 = reinterpret_cast<int64_t*>(hkb.data());
     std::vector<uint32_t> xc_base(c_tiles + 1, 0), xp_base(c_tiles + 1, 0);
     std::vector<int32_t> pod_cls(n);
     std::vector<int64_t> pod_pos(n);
@@ -1177,39 +1214,40 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         std::vector<int64_t> pos(POD_CLASS_IDS, 0);
         int64_t ic = 0;
         uint64_t rc = 0, rp = 0;                          // the pod's records in the input
-        uint64_t oc = (uint64_t)xk, op = (uint64_t)pk;    // C record cursors
+        uint64_t oc = 0, op = 0;                          // C record cursors
         for (int64_t i = 0; i < n; ++i) {
             const uint32_t f = p->flags[i];
             const uint32_t nx = pf_xpair(f), nc = pf_xctr(f);
             const int id = class_id(f);
-            int64_t d, d64;                               // slot in the 4- / 8-byte arrays
             if (id >= 0) {
                 const PodClass& k = cls[cls_of[id]];
-                const int64_t q = pos[id]++, rt = q / TILE, sl = q % TILE;
+                const int64_t q = pos[id]++, sl = q % TILE;
                 pod_cls[i] = cls_of[id];
                 pod_pos[i] = q;
-                const int64_t s64 = ((sl & 3) >> 1) * 128 + 2 * (sl >> 2) + (sl & 1);   // K1's pos64
-                d = (k.t0 + rt) * TILE + sl;
-                d64 = (k.t0 + rt) * TILE + s64;
+                const int64_t blk = kb_block(k, k.t0 + q / TILE);
+                hkb[blk + sl] = f;
+                hkb[blk + KB_CPU0 + sl] = p->cpu0[i];
+                hkb64[(blk + KB_MEM0) / 2 + kb_pos64(sl)] = p->mem0[i];
+                hkb[blk + KB_PAIR0 + sl] = p->pair0[i];
                 for (uint32_t j = 0; j < nc; ++j) {
-                    const int64_t o = k.xc0 + (rt * nc + j) * TILE + s64;
-                    hxc[o] = p->xc_cpu[rc + j];
-                    hxm[o] = p->xc_mem[rc + j];
+                    const int64_t o = kb_rec64(blk, j, sl);
+                    hkb64[o] = p->xc_cpu[rc + j];
+                    hkb64[o + 256] = p->xc_mem[rc + j];
                 }
-                for (uint32_t j = 0; j < nx; ++j) hxp[k.xp0 + (rt * nx + j) * TILE + sl] = p->xp_pair[rp + j];
+                for (uint32_t j = 0; j < nx; ++j) hkb[kb_xp(k, blk, j, sl)] = p->xp_pair[rp + j];
             } else {
                 if (ic % CTILE == 0) { xc_base[ic / CTILE] = (uint32_t)oc; xp_base[ic / CTILE] = (uint32_t)op; }
-                d = d64 = c0 + ic++;
+                const int64_t d = ic++;                   // C-array index (slot c0 + d)
                 pod_cls[i] = -1;
-                pod_pos[i] = d;
+                pod_pos[i] = c0 + d;
                 for (uint32_t j = 0; j < nc; ++j) { hxc[oc + j] = p->xc_cpu[rc + j]; hxm[oc + j] = p->xc_mem[rc + j]; }
                 for (uint32_t j = 0; j < nx; ++j) hxp[op + j] = p->xp_pair[rp + j];
                 oc += nc;
                 op += nx;
+                hf[d] = f; hc[d] = p->cpu0[i]; hm[d] = p->mem0[i]; hp[d] = p->pair0[i];
             }
             rc += nc;
             rp += nx;
-            hf[d] = f; hc[d] = p->cpu0[i]; hm[d64] = p->mem0[i]; hp[d] = p->pair0[i];
         }
         xc_base[c_tiles] = (uint32_t)oc;
         xp_base[c_tiles] = (uint32_t)op;
@@ -1229,6 +1267,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     c->pods.assign(c->n_replicas, PodBuf());
     for (int r = 0; r < c->n_replicas; ++r) {
         PodBuf& b = c->pods[r];
+        HIP_TRY(dalloc(&b.kb, std::max<int64_t>(kbw, 4)));
         HIP_TRY(dalloc(&b.flags, npad)); HIP_TRY(dalloc(&b.cpu0, npad)); HIP_TRY(dalloc(&b.mem0, npad));
         HIP_TRY(dalloc(&b.pair0, npad)); HIP_TRY(dalloc(&b.xc_cpu, nxc_dev)); HIP_TRY(dalloc(&b.xc_mem, nxc_dev));
         HIP_TRY(dalloc(&b.xp, nxp_dev)); HIP_TRY(dalloc(&b.xc_base, c_tiles + 1)); HIP_TRY(dalloc(&b.xp_base, c_tiles + 1));
@@ -1240,6 +1279,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         const hipMemcpyKind kind = r == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
         const PodBuf& a = c->pods[0];
         auto src = [&](const void* host, const void* dev) { return r == 0 ? host : dev; };
+        if (kbw) HIP_TRY(hipMemcpy(b.kb, src(hkb.data(), a.kb), kbw * 4, kind));
         if (npad) {
             HIP_TRY(hipMemcpy(b.flags, src(hf.data(), a.flags), npad * 4, kind));
             HIP_TRY(hipMemcpy(b.cpu0, src(hc.data(), a.cpu0), npad * 4, kind));
@@ -1266,7 +1306,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         auto& fr = c->cls_free[ci];
         for (int64_t q = (cls[ci].t1 - cls[ci].t0) * TILE - 1; q >= cnt[id]; --q) fr.push_back(q);
     }
-    c->h_cflags.assign(hf.begin() + c0, hf.end());
+    c->h_cflags.assign(hf.begin(), hf.end());
     c->live_pods = n;
     c->live_xc = p->n_xc;
     c->live_xp = p->n_xp;
@@ -1583,6 +1623,73 @@ int32_t esc_stage_times(esc_ctx* c, double* ms, int32_t n) {
     return ESC_OK;
 }
 
+// K1 share calibration.  The K1 workgroups stream equal bytes at unequal rates, and the
+// rates are a stable property of the grid position on a device: at 100 M pods the slowest
+// workgroup's K phase took 1.14x the mean (odd XCDs ~5 % slower than even ones, plus a
+// within-XCD spread), and the per-workgroup durations correlate 0.9-0.98 between
+// decisions and 0.96-0.99 between processes (profiles/r02_v8/k1_trace_stability_*.json).
+// Each round runs one decision, reads every workgroup's K-phase time (trace words 0-1) and
+// scales each share by sqrt(mean time / its time) (a damped step: a share that moves also
+// changes which tiles — classes of other costs — the workgroup streams); the plan with
+// the lowest slowest-workgroup time seen is kept.  The grid and the per-workgroup pod bound
+// do not change, and sums are order-independent, so every result is unchanged; the graphs
+// read the plan from device memory, so they stay valid.
+int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
+    int32_t rc = check_ready(c);
+    if (rc) return rc;
+    if (rounds < 0) return ESC_E_INVAL;
+    hipSetDevice(c->device);
+    const int64_t nblk = c->nblk;
+    if (!c->d_k1seg || nblk <= 1 || c->force_wide || rounds == 0) return ESC_OK;   // nothing to balance
+    std::vector<uint64_t> tr((size_t)nblk * 8);
+    std::vector<double> share = c->k1_share, best;
+    if ((int64_t)share.size() != nblk) share.assign(nblk, 1.0 / (double)nblk);
+    double best_max = 0;
+    auto upload = [&](const std::vector<double>& sh) -> int32_t {
+        std::vector<int64_t> plan = plan_k1(c->h_cls, c->k_weight, nblk, sh);
+        if (plan.empty() || plan_worst(c, plan, nblk) > PODS_PER_BLOCK_MAX) return 1;
+        HIP_TRY(hipMemcpy(c->d_k1seg, plan.data(), plan.size() * 8, hipMemcpyHostToDevice));
+        c->k1_share = sh;
+        return ESC_OK;
+    };
+    for (int32_t r = 0; r <= rounds; ++r) {
+        rc = c->world == 1 ? esc_run(c) : esc_reduce(c);
+        if (!rc) rc = esc_sync(c);
+        if (rc) return rc;
+        HIP_TRY(hipMemcpy(tr.data(), c->d_k1_trace, tr.size() * 8, hipMemcpyDeviceToHost));
+        std::vector<double> t(nblk);
+        double mean = 0, mx = 0;
+        for (int64_t b = 0; b < nblk; ++b) {
+            t[b] = (double)(int64_t)(tr[b * 8 + 1] - tr[b * 8 + 0]);
+            if (!(t[b] > 0)) return ESC_OK;             // no K phase measured: keep the plan
+            mean += t[b] / (double)nblk;
+            mx = std::max(mx, t[b]);
+        }
+        if (best.empty() || mx < best_max) { best = share; best_max = mx; }
+        if (r == rounds) break;
+        std::vector<double> next(nblk);
+        double sum = 0;
+        for (int64_t b = 0; b < nblk; ++b) sum += (next[b] = share[b] * std::sqrt(mean / t[b]));
+        for (double& x : next) x /= sum;
+        if (upload(next) != ESC_OK) break;               // outside the exactness bound: stop here
+        share = next;
+    }
+    if (best != c->k1_share) {
+        rc = upload(best);
+        if (rc < 0) return rc;
+    }
+    return ESC_OK;
+}
+
+int32_t esc_k1_trace(esc_ctx* c, uint64_t* out, int64_t cap, int64_t* n_out) {
+    if (!c || !n_out || cap < 0 || (cap > 0 && !out)) return ESC_E_INVAL;
+    if (!c->d_k1_trace) return ESC_E_STATE;
+    *n_out = c->nblk;
+    const int64_t w = std::min<int64_t>(cap, (int64_t)c->nblk * 8);
+    if (w > 0) HIP_TRY(hipMemcpy(out, c->d_k1_trace, (size_t)w * 8, hipMemcpyDeviceToHost));
+    return ESC_OK;
+}
+
 int32_t esc_reduce(esc_ctx* c) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
@@ -1858,7 +1965,9 @@ int32_t apply_patches(esc_ctx* c, Patches& P, const std::vector<PatchTargets>& t
     return rc;
 }
 
-enum : uint32_t { PT_FLAGS = 0, PT_CPU0 = 1, PT_PAIR0 = 2, PT_XP = 3, PT_MEM0 = 6, PT_XC_CPU = 7, PT_XC_MEM = 8 };
+// C-section arrays (C index) and the K blocks as 4- and 8-byte words
+enum : uint32_t { PT_FLAGS = 0, PT_CPU0 = 1, PT_PAIR0 = 2, PT_XP = 3, PT_KB32 = 4, PT_MEM0 = 6, PT_XC_CPU = 7,
+                  PT_XC_MEM = 8, PT_KB64 = 9 };
 
 std::vector<PatchTargets> pod_targets(esc_ctx* c) {
     std::vector<PatchTargets> v;
@@ -1866,6 +1975,7 @@ std::vector<PatchTargets> pod_targets(esc_ctx* c) {
         PatchTargets t{};
         t.u32[PT_FLAGS] = b.flags; t.u32[PT_CPU0] = b.cpu0; t.u32[PT_PAIR0] = b.pair0; t.u32[PT_XP] = b.xp;
         t.i64[PT_MEM0 - 6] = b.mem0; t.i64[PT_XC_CPU - 6] = b.xc_cpu; t.i64[PT_XC_MEM - 6] = b.xc_mem;
+        t.u32[PT_KB32] = b.kb; t.i64[PT_KB64 - 6] = reinterpret_cast<int64_t*>(b.kb);
         v.push_back(t);
     }
     return v;
@@ -1883,8 +1993,8 @@ void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
     const int32_t ci = c->pod_cls[id];
     if (ci == -2) return;
     if (ci == -1) {
-        const int64_t d = c->pod_pos[id];
-        uint32_t& f = c->h_cflags[d - c->k_tiles * TILE];
+        const int64_t d = c->pod_pos[id] - c->k_tiles * TILE;    // C-array index
+        uint32_t& f = c->h_cflags[d];
         c->live_xc -= pf_xctr(f);
         c->live_xp -= pf_xpair(f);
         f |= ESC_PF_DAEMONSET;
@@ -1892,7 +2002,7 @@ void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
     } else {
         const PodClass& k = c->h_cls[ci];
         const int64_t q = c->pod_pos[id];
-        P.add(PT_FLAGS, (k.t0 + q / TILE) * TILE + q % TILE, ESC_PF_DAEMONSET);
+        P.add(PT_KB32, kb_block(k, k.t0 + q / TILE) + q % TILE, ESC_PF_DAEMONSET);
         c->cls_free[ci].push_back(q);
         c->live_xc -= k.xreg + k.xinit + k.ovh;
         c->live_xp -= k.nxp;
@@ -2235,20 +2345,19 @@ int32_t esc_pods_upsert(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
             c->live_xp -= k.nxp;
         }
         const PodClass& k = c->h_cls[ci];
-        const int64_t q = c->pod_pos[id], rt = q / TILE, sl = q % TILE;
-        const int64_t s64 = ((sl & 3) >> 1) * 128 + 2 * (sl >> 2) + (sl & 1);   // K1's pos64
-        const int64_t d = (k.t0 + rt) * TILE + sl, d64 = (k.t0 + rt) * TILE + s64;
-        const uint32_t f = p->flags[i], R = k.xreg + k.xinit + k.ovh;
-        P.add(PT_FLAGS, d, f);
-        P.add(PT_CPU0, d, p->cpu0[i]);
-        P.add(PT_PAIR0, d, p->pair0[i]);
-        P.add(PT_MEM0, d64, (uint64_t)p->mem0[i]);
+        const int64_t q = c->pod_pos[id], sl = q % TILE;
+        const int64_t blk = kb_block(k, k.t0 + q / TILE);
+        const uint32_t f = p->flags[i], R = kb_nrec(k);
+        P.add(PT_KB32, blk + sl, f);
+        P.add(PT_KB32, blk + KB_CPU0 + sl, p->cpu0[i]);
+        P.add(PT_KB32, blk + KB_PAIR0 + sl, p->pair0[i]);
+        P.add(PT_KB64, (blk + KB_MEM0) / 2 + kb_pos64(sl), (uint64_t)p->mem0[i]);
         for (uint32_t j = 0; j < R; ++j) {
-            const int64_t o = k.xc0 + (rt * R + j) * TILE + s64;
-            P.add(PT_XC_CPU, o, (uint64_t)p->xc_cpu[rof[i] + j]);
-            P.add(PT_XC_MEM, o, (uint64_t)p->xc_mem[rof[i] + j]);
+            const int64_t o = kb_rec64(blk, j, sl);
+            P.add(PT_KB64, o, (uint64_t)p->xc_cpu[rof[i] + j]);
+            P.add(PT_KB64, o + 256, (uint64_t)p->xc_mem[rof[i] + j]);
         }
-        for (uint32_t j = 0; j < k.nxp; ++j) P.add(PT_XP, k.xp0 + (rt * k.nxp + j) * TILE + sl, p->xp_pair[pof[i] + j]);
+        for (uint32_t j = 0; j < k.nxp; ++j) P.add(PT_KB32, kb_xp(k, blk, j, sl), p->xp_pair[pof[i] + j]);
         ++c->live_pods;
         c->live_xc += R;
         c->live_xp += k.nxp;

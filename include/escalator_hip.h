@@ -388,6 +388,14 @@ int32_t esc_force_wide(esc_ctx* ctx, int32_t enable);   /* testing: always take 
 /* Last kernel's device time in ms per stage (timing mode), see DESIGN.md §6. */
 int32_t esc_set_timing(esc_ctx* ctx, int32_t enable);
 int32_t esc_stage_times(esc_ctx* ctx, double* ms_out, int32_t n);
+/* K1 records per workgroup 8 words (s_memrealtime ticks at 100 MHz at start / after the K
+ * tiles / after the C tiles / after the flush, HW_ID, XCC_ID, 0, 0) of the last decision;
+ * this copies them out (after esc_sync).  *n_out = workgroups; ESC_E_STATE before a run. */
+int32_t esc_k1_trace(esc_ctx* ctx, uint64_t* out, int64_t cap_words, int64_t* n_out);
+/* Calibrates K1's work split on this device: `rounds` decisions, each moving
+ * every workgroup's share of the pod bytes toward its measured streaming rate.  Results are
+ * unchanged (integer sums are order-independent); call once after loading a snapshot. */
+int32_t esc_k1_calibrate(esc_ctx* ctx, int32_t rounds);
 
 /* ------------------------------------------- incremental snapshot (§8f rank 1)
  * Informer-style events patch the resident snapshot in place instead of a reload

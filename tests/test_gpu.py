@@ -251,6 +251,30 @@ def test_fold_paths_vs_c_oracle(esc, fused, cfg, P, N, G, monkeypatch):
         check_against_c_oracle(tot, dec, otot, odf, odi)
 
 
+@pytest.mark.parametrize("cfg,P,N,G", [(4, 2_000_000, 20_000, 10_000), (2, 1_000_000, 10_000, 100),
+                                       (3, 2_000_000, 20_000, 100)])
+def test_k1_calibrated_shares_vs_c_oracle(esc, cfg, P, N, G):
+    """esc_k1_calibrate moves K1's per-workgroup shares to the measured rates: the plan
+    changes, every tile is still taken exactly once (totals and decisions bit-exact before
+    and after, through the captured graph, which reads the plan from device memory), and
+    the per-workgroup K phase is timed (trace words 0-1)."""
+    s = esc.Synth(P, N, G, config=cfg, seed=0xE5CA1A7E00000000 + cfg)
+    otot = soa.totals(s.pods(), s.nodes(), s.groups)
+    odf, odi = soa.decide(s.groups, s.states, otot)
+    ctx = esc.Context(s)
+    ctx.load_synth(s, replicas=2)
+    ctx.use_graph(True)
+    ctx.set_state(s.states)
+    ctx.run()
+    check_against_c_oracle(*ctx.results(), otot, odf, odi)
+    ctx.k1_calibrate(3)
+    tr = ctx.k1_trace()
+    assert tr.shape[0] > 1 and np.all(tr[:, 1] >= tr[:, 0])
+    for _ in range(3):
+        ctx.run()
+        check_against_c_oracle(*ctx.results(), otot, odf, odi)
+
+
 @pytest.mark.parametrize("variant", ["1", "2", "5"])
 def test_k1_variants_vs_c_oracle(esc, variant, monkeypatch):
     """The exact K1 variants (ESC_K1_VARIANT: 1 two C tiles in flight, 2 1024 threads, 5
