@@ -29,7 +29,7 @@ CONFIGS = {
 }
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # PMC passes (scripts/pmc_job.sh) of the kernels as built at this tag: HBM bytes per launch
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v10", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_v10", "pmc_summary.json")
 
 
 def log(*a):
@@ -281,6 +281,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--pods", type=int, default=None, help="override the config's pod count (experiments)")
+    ap.add_argument("--graph", action="store_true",
+                    help="replay each step from a captured hipGraph (default: enqueue its three kernels directly; "
+                         "a graph launch left ~8 us idle between back-to-back decisions, profiles/r02_v10)")
     ap.add_argument("--no-order", action="store_true",
                     help="leave the K5 ordering out of the decision (ablation; BASELINE.md §2 includes it)")
     args = ap.parse_args()
@@ -317,11 +320,11 @@ def main():
         (rank, lo, hi, nlo, nhi, shard_bytes / 1e6, replicas, time.time() - t0))
 
     if world == 1:
-        ctx.use_graph(True)
+        ctx.use_graph(args.graph)
         step = ctx.run
     else:
         ex = Exchange(ctx, device_collective=backend == "nccl")
-        ctx.use_graph(True)                       # the shard's K1/K2/K3 step replays as one graph
+        ctx.use_graph(args.graph)          # the shard's K1 / tail / node-groups step as one graph
         step = ex.step
     ctx.k1_calibrate(10)                          # K1 shares to this device's rates (untimed, once per load)
 
@@ -362,9 +365,10 @@ def main():
         stages.append(st)
     ctx.set_timing(False)
     k1_ms = float(np.mean(k1))
-    stage_names = (["k_pod_reduce", "k_node_pieces", "k_fold_decide"] +
-                   (["d2h"] if os.environ.get("ESC_NO_ZEROCOPY", "0") not in ("", "0") else []) +
-                   ([] if args.no_order else ["k_order"]))
+    # stages of enqueue_step in timing mode: K1, the fused tail (fold + node pieces + packed
+    # small-group orderings), the remaining ordering kernels, node groups + decide, [copy]
+    stage_names = (["k_pod_reduce", "k_step_tail", "k_order_split", "k_node_groups_decide"] +
+                   (["d2h"] if os.environ.get("ESC_NO_ZEROCOPY", "0") not in ("", "0") else []))
     stage_mean = np.mean(np.array(stages), axis=0)
 
     parity = None

@@ -120,7 +120,10 @@ struct NodeDev {
     const uint32_t* piece_off; // [n_pieces + 1] entry offsets
     const uint32_t* piece_pair;// [n_pieces]
     const uint32_t* pp_off;    // [n_gp + 1]: pieces of group pair q are [pp_off[q], pp_off[q+1])
-    int64_t n_pieces, pc_lo, pc_hi;
+    // K2 work: span w = this rank's group-pair pieces [span_off[w], span_off[w + 1]), about
+    // NODE_SPAN entries each (several small pieces, or one large), one wave per span
+    const uint32_t* span_off;  // [n_spans + 1]
+    int64_t n_pieces, pc_lo, pc_hi, n_spans;
 };
 
 // K2 output row per piece (int64 words, stored word-major: rows[word * n_pieces + piece]).
@@ -133,6 +136,7 @@ enum NodeRow : int {
     NR_K
 };
 constexpr int NODE_PIECE = 1024;
+constexpr int NODE_SPAN = 256;         // entries per K2 wave (whole pieces)
 constexpr int NR_CNT_BITS = 21;
 constexpr uint64_t NR_CNT_MASK = (uint64_t(1) << NR_CNT_BITS) - 1;
 
@@ -169,49 +173,23 @@ constexpr int K1_CHUNKS = 4;
 constexpr int K1_CHUNK_CAP = 8;
 bool k1_dynamic(int variant);
 struct DecCompact;
-// K1 with the fold fused (one LDS window, every workgroup co-resident): after flushing its
-// partial row each workgroup arrives at a grid barrier (a 64-bit counter that only grows:
-// the barrier of decision k completes at k * nblk arrivals) and then folds its own slice
-// of pod slots over every row — the whole chip folds instead of one column per workgroup —
-// and writes the pod words of the groups whose slot lies in the slice.  `arrive == null`:
-// no fold (k_fold_decide folds).  A barrier that does not complete in bounded time sets
-// *err (the host then falls back to the separate fold).
-struct K1Fold {
-    unsigned long long* arrive;
-    uint32_t* err;
-    int64_t* pwords;             // [G][PW_K] (the exchange words)
-    const uint32_t* goff;        // [nblk + 1] groups of each workgroup's slice in `groups`
-    const uint32_t* groups;      // group ids ordered by pod slot
-    int64_t n_slots;             // pod slots: n_gp + 1
-    // the fused decide (one rank): K1's fold (pod words) and k_node_groups on the side
-    // stream (node words) each publish a group's words with write-through stores and then
-    // count an arrival on the group's counter; the second arrival (odd old value) decides
-    // the group — nobody waits.  Null: k_decide decides after the join.
-    uint32_t* arrive_g;
-    const int64_t* nwords;
-    const GroupNode* gnode;
-    esc_group_decision* dec;
-    DecCompact* cdec;
-    // per workgroup 8 words (esc_k1_trace; the share calibration reads words 0-1):
-    // s_memrealtime (100 MHz) at start, after the K tiles, after the C tiles, after the
-    // flush; HW_ID, XCC_ID
+// K1 diagnostics.  trace: per workgroup 8 words (esc_k1_trace; the share calibration reads words
+// 0-1): s_memrealtime (100 MHz) at start, after the K tiles, after the C tiles, after the
+// flush; HW_ID, XCC_ID.
+struct K1Diag {
     uint64_t* trace;
 };
-struct NGDecide {               // k_node_groups' side of the fused decide (see K1Fold)
-    uint32_t* arrive_g;         // null: no fused decide
+// k_node_groups' decision (one rank, or after the exchange): null dec = node words only.
+struct NGDecide {
     const int64_t* pwords;
     esc_group_decision* dec;
     DecCompact* cdec;
 };
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
-                             uint64_t* part, int64_t* wide, uint32_t* ticket, int cap, const K1Fold& fold,
+                             uint64_t* part, int64_t* wide, uint32_t* ticket, int cap, const K1Diag& diag,
                              hipStream_t st);
-// Workgroups of the K1 launch that fit on one CU at once (the fused fold's co-residency bound).
-int k1_blocks_per_cu(int gw);
-constexpr int K1_FOLD_LDS = 4 * 512 * 8 + 3 * 512 * 16;   // the fold's LDS use (bytes, 512 threads)
 hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_t* tiles, int64_t n_big,
                                int64_t* wide, hipStream_t st);
-hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows, int64_t* trk_acc, hipStream_t st);
 // Compact decision record (32 B) that K3 / K4 write to pinned host memory each decision
 // instead of the ABI's 64-B esc_group_decision: esc_results rebuilds the full record on the
 // host (the cached capacity from its node mirror: allNodes[0]'s allocatable when the group
@@ -225,10 +203,13 @@ struct DecCompact {
 };
 static_assert(sizeof(DecCompact) == 32, "compact decision is 2 x 16 B");
 
-// K2b (k_node_groups): every group's final node words from K2's piece rows (side stream).
+// K2b + K4 (k_node_groups): every group's final node words from K2's piece rows, then
+// (nd.dec != null) the decisions.  K4 alone (k_decide): after an exchange.
+hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords,
+                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st);
 hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t* node_rows, int64_t* trk_acc,
                               int64_t* nwords, const NGDecide& nd, hipStream_t st);
-// K3 (k_fold_decide): fold of the K1 partials + group join + decide, one workgroup per column.
+// K3 fold (a role of k_step_tail): the K1 partials of FC_COL pod slots per block.
 constexpr int FC_COL = 32;             // pod slots per K3 column (a 256-B piece of each K1 row)
 struct FoldPlan {
     const uint64_t* part;              // K1 partials: row b = cc[sp], mem[sp] at part + 2 * sp * b
@@ -239,9 +220,14 @@ struct FoldPlan {
     const uint32_t* col_groups;        // group ids ordered by pod slot, then id
     int ablate;                        // ESC_K3_ABLATE (timing-only knob)
 };
-hipError_t launch_fold_decide(const GroupDev& g, const NodeDev& n, const FoldPlan& f, int64_t* wide_pod,
-                              int64_t* pwords, const int64_t* nwords, bool decide, esc_group_decision* dec,
-                              DecCompact* cdec, hipStream_t st);
+struct OrdChunk;
+// The step's tail in one launch (esc_kernels.hip k_step_tail): the K3 fold into the pod
+// words, K2's dry-mode tracker entries (+ its piece rows when `spans`: no K1 ran) and,
+// with n_small > 0, the K5 ordering of the packed small-group chunks [0, n_small).
+hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
+                            int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
+                            const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
+                            const uint32_t* g_flags, uint32_t* vals, int64_t* seg, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
 // §8f rank 2: a loaded pod as seen by NodePodsRemaining, listed per node (runs in
 // node order).  p[0..2]: the pod's extra pairs (NONE-padded); a C pod with more than 3
@@ -278,8 +264,7 @@ struct PatchTargets {          // k_patch destinations: 4-byte arrays 0-5, 8-byt
     int64_t* i64[6];
 };
 hipError_t launch_patch(const PatchTargets& t, const uint64_t* where, const uint64_t* what, int64_t n, hipStream_t st);
-hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords,
-                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st);
+
 
 // Ordering (K5), see esc_kernels.hip: the age index (once per snapshot) and the per-decision
 // (group, class) partition.

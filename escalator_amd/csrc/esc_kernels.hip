@@ -6,16 +6,17 @@
 //                      16-B-per-lane coalesced loads (4 pods per lane, 256 per wave), int64
 //                      per-group partials privatised in LDS (ds_add_u64), flushed once per
 //                      workgroup.  HBM-bound; no MFMA (nothing is a contraction).
-//  K2 k_node_pieces  : FilteredNodesLister.List + filterNodes (controller.go:120) +
+//  K2 node pieces    : (k_step_tail) FilteredNodesLister.List + filterNodes (controller.go:120) +
 //                      CalculateNodesCapacityTotal(untainted) (util.go:41) over the
 //                      pair-major node entries: one wave per piece, register sums, one
 //                      row per piece.  No LDS, no atomics, exact for any int64 input.
-//  K3 k_combine      : joins every group to its pod slot and its pair's node pieces, sums
-//                      the partials into the exchanged int64 words (+ allNodes[0],
-//                      controller.go:208, and the dry-mode tracker); for one rank it also
-//                      runs K4.
-//  K4 k_decide       : calcPercentUsage / switch / calcScaleUpDelta / scaleDownTaint clamp
-//                      (util.go:13-81, controller.go:233-351, scale_down.go:138-158).
+//  K3 fold           : (k_step_tail) the K1 partials of every pod slot summed into each
+//                      group's pod words (int64 split lo32 / hi, exchanged when sharded);
+//                      K2 and the packed K5 chunks run as other blocks of the same launch.
+//  K2b+K4 k_node_groups: each group's node words from its pair's pieces (+ allNodes[0],
+//                      controller.go:208, and the dry-mode tracker), then calcPercentUsage /
+//                      switch / calcScaleUpDelta / scaleDownTaint clamp (util.go:13-81,
+//                      controller.go:233-351, scale_down.go:138-158).
 //  K5 ordering       : taintOldestN / untaintNewestN (scale_down.go:171, scale_up.go:118,
 //                      sort.go:18,33): an age index (LSD radix sort of creation times,
 //                      once per snapshot) + a per-decision stable partition by
@@ -477,6 +478,74 @@ __device__ __forceinline__ void c_tile_exact(const PodDev& P, const GroupDev& G,
 
 }  // namespace
 
+// ------------------------------------------------------------------ K2 spans
+// (k_step_tail's piece role; inside K1's first window they cost K1 as much as they saved in
+// the tail: +20 us, profiles/r02_v10)
+namespace {
+// Adds one entry to the piece accumulators: its wet class (filterNodes,
+// controller.go:141-150: Spec.Unschedulable first, then the escalator taint) and the
+// every-member sums used by dry-mode groups.
+struct PieceAcc {
+    unsigned long long ucl = 0, uch = 0, uml = 0, umh = 0, acl = 0, ach = 0, aml = 0, amh = 0, cnt = 0;
+    __device__ __forceinline__ void add(uint32_t f, int64_t c, int64_t m) {
+        if (f & ESC_NF_ABSENT) return;               // spare entry or deleted node
+        const unsigned long long cl = (uint64_t)c & 0xFFFFFFFFull, ml = (uint64_t)m & 0xFFFFFFFFull;
+        const unsigned long long chh = (unsigned long long)(c >> 32), mhh = (unsigned long long)(m >> 32);
+        acl += cl; ach += chh; aml += ml; amh += mhh;
+        const int cls = (f & ESC_NF_UNSCHED) ? 2 : ((f & ESC_NF_TAINTED) ? 1 : 0);
+        if (cls == 0) { ucl += cl; uch += chh; uml += ml; umh += mhh; }
+        cnt += 1ull << (NR_CNT_BITS * cls);
+    }
+};
+
+// K2 span w (one wave; see node_piece_block).
+__device__ __forceinline__ void node_span(const NodeDev& N, int64_t* __restrict__ rows, int64_t w, int lane) {
+    if (w >= N.n_spans) return;
+    typedef __attribute__((address_space(4))) const uint32_t cu32n;
+    const cu32n* poff = (const cu32n*)N.piece_off;
+    const uint32_t p0 = ((const cu32n*)N.span_off)[w], p1 = ((const cu32n*)N.span_off)[w + 1];
+    const uint32_t z = poff[p1];
+    uint32_t p = p0, ps = poff[p0], pe = poff[p0 + 1];
+    PieceAcc acc;
+    auto flush = [&]() {                             // piece p's row, then the next piece
+        const unsigned long long v[NR_K] = {wave_sum64(acc.ucl), wave_sum64(acc.uch), wave_sum64(acc.uml),
+                                            wave_sum64(acc.umh), wave_sum64(acc.acl), wave_sum64(acc.ach),
+                                            wave_sum64(acc.aml), wave_sum64(acc.amh), wave_sum64(acc.cnt)};
+        unsigned long long x = 0;
+#pragma unroll
+        for (int k = 0; k < NR_K; ++k) x = lane == k ? v[k] : x;
+        if (lane < NR_K) rows[(int64_t)lane * N.n_pieces + p] = (int64_t)x;
+        acc = PieceAcc();
+        ++p;
+        ps = pe;
+        if (p < p1) pe = poff[p + 1];
+    };
+    constexpr int U = 4;
+    for (uint32_t base = ps; base < z; base += 64 * U) {
+        uint32_t f[U];
+        int64_t c[U], m[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = base + u * 64 + lane, ii = i < z ? i : z - 1;
+            f[u] = ldnt(N.e_flags + ii);
+            c[u] = ldnt(N.e_cpu + ii);
+            m[u] = ldnt(N.e_mem + ii);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t lo = base + u * 64, i = lo + lane;
+            if (lo >= z) break;
+            for (;;) {                                   // wave-uniform: p, ps, pe
+                if (i >= ps && i < pe && i < z) acc.add(f[u], c[u], m[u]);
+                if (p >= p1 || pe > lo + 63) break;      // piece p goes on in the next load
+                flush();
+            }
+        }
+    }
+    while (p < p1) flush();                          // the span's last piece(s)
+}
+}  // namespace
+
 // =====================================================================  K1 (fast)
 // Each workgroup takes an equal contiguous share of the K tiles' work weight (16-B loads)
 // and of the C tiles.  K tiles: the share is walked class by class (the class table is sorted by tile), each
@@ -489,7 +558,7 @@ __device__ __forceinline__ void c_tile_exact(const PodDev& P, const GroupDev& G,
 // counter (at most `cap` per workgroup), so workgroups that stream faster take more
 // and the launch does not wait on the slowest static share; DYN 0: one static share each.
 namespace {
-// ---- K4 decision helpers (K1's fused decide, k_fold_decide, k_decide)
+// ---- K4 decision helpers (k_node_groups' decide)
 // Exact total from split words; false when it is outside int64 (Quantity -> inf.Dec).
 __device__ __forceinline__ bool join_split(int64_t lo_sum, int64_t hi_sum, int64_t& out) {
     const __int128 t = ((__int128)hi_sum << 32) + (__int128)lo_sum;
@@ -561,121 +630,11 @@ __device__ __forceinline__ void decide_store(const GroupDev& G, const GroupNode&
 }
 }  // namespace
 
-// The fused fold (K1Fold): grid barrier, then this workgroup's slice of pod slots summed
-// over every partial row (+ the slots' exact wide rows, read and reset), then the pod words
-// of the slice's groups.  `lds` is free again here (the window was flushed).
-template <int THREADS>
-__device__ __forceinline__ void k1_fold(const GroupDev& G, const K1Fold& F, const uint64_t* __restrict__ part,
-                                        int64_t* __restrict__ wide, uint64_t* lds) {
-    // The partial rows were written with agent-scope (write-through) stores and are read
-    // with agent-scope loads, so no L2 write-back / invalidate is needed (an agent-scope
-    // release fence costs a buffer_wbl2 per wave: +90 us on config 4): every wave waits for
-    // its stores to complete, then one arrival per workgroup.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    __shared__ uint32_t s_ok;
-    if (threadIdx.x == 0) {
-        const unsigned long long n = gridDim.x;
-        const unsigned long long old = __hip_atomic_fetch_add(F.arrive, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned long long target = (old / n + 1) * n;
-        uint32_t spins = 0, ok = 1;
-        while (__hip_atomic_load(F.arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (++spins > (1u << 22)) { atomicOr(F.err, 1u); ok = 0; break; }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        s_ok = ok;
-    }
-    __syncthreads();
-    if (!s_ok) return;
-    const int64_t nb = gridDim.x, b = blockIdx.x;
-    const int64_t lo = F.n_slots * b / nb, hi = F.n_slots * (b + 1) / nb;
-    const int W = (int)(hi - lo);
-    if (W <= 0) return;
-    // the host enables the fold only when every slice has at most THREADS slots
-    const int RG = THREADS / W;                          // rows folded in parallel per slot
-    const int t = threadIdx.x, sl = t % W, rg = t / W;
-    uint64_t cpu = 0, cnt = 0, ml = 0, mc = 0;
-    if (rg < RG) {
-        constexpr int U = 8;                             // rows in flight per thread
-        for (int64_t r0 = rg; r0 < nb; r0 += (int64_t)RG * U) {
-            uint64_t cc[U], mm[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t r = r0 + (int64_t)u * RG;
-                const uint64_t* row = part + (r < nb ? r : r0) * 2 * G.sp + lo + sl;
-                cc[u] = __hip_atomic_load(row, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                mm[u] = __hip_atomic_load(row + G.sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (r0 + (int64_t)u * RG >= nb) break;
-                cpu += cc[u] & CPU_MASK;
-                cnt += cc[u] >> CNT_SHIFT;
-                ml += mm[u];
-                mc += ml < mm[u] ? 1u : 0u;
-            }
-        }
-    }
-    // reduce the row groups: lds[k * THREADS + t]
-    lds[0 * THREADS + t] = cpu; lds[1 * THREADS + t] = cnt; lds[2 * THREADS + t] = ml; lds[3 * THREADS + t] = mc;
-    __syncthreads();
-    __int128* tot = reinterpret_cast<__int128*>(lds + 4 * THREADS);   // per slot: cpu, mem (exact), count
-    if (t < W) {
-        uint64_t a = 0, n = 0, lo2 = 0, carry = 0;
-        for (int k = 0; k < RG; ++k) {
-            const int u = k * W + t;
-            a += lds[u]; n += lds[THREADS + u];
-            const uint64_t m = lds[2 * THREADS + u];
-            lo2 += m;
-            carry += (lo2 < m ? 1u : 0u) + lds[3 * THREADS + u];
-        }
-        int64_t* wp = wide + (lo + t) * WP_K;
-        int64_t w[WP_K];
-#pragma unroll
-        for (int k = 0; k < WP_K; ++k) w[k] = __hip_atomic_load(wp + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((w[0] | w[1] | w[2] | w[3] | w[4]) != 0)
-#pragma unroll
-            for (int k = 0; k < WP_K; ++k) __hip_atomic_store(wp + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        tot[3 * t + 0] = (__int128)a + ((__int128)w[WP_CPU_HI] << 32) + (__int128)w[WP_CPU_LO];
-        tot[3 * t + 1] = (__int128)(((unsigned __int128)carry << 64) | lo2) + ((__int128)w[WP_MEM_HI] << 32) +
-                         (__int128)w[WP_MEM_LO];
-        tot[3 * t + 2] = (__int128)n + w[WP_CNT];
-    }
-    for (uint32_t i = F.goff[b] + t; i < F.goff[b + 1]; i += THREADS) {
-        const uint32_t g = F.groups[i];
-        const int k = (int)((int64_t)G.gslot[g] - lo);
-        const __int128 pc = tot[3 * k], pm = tot[3 * k + 1];
-        int64_t w[PW_K];
-        w[PW_CPU_LO] = (int64_t)((unsigned __int128)pc & 0xFFFFFFFFull);
-        w[PW_CPU_HI] = (int64_t)(pc >> 32);
-        w[PW_MEM_LO] = (int64_t)((unsigned __int128)pm & 0xFFFFFFFFull);
-        w[PW_MEM_HI] = (int64_t)(pm >> 32);
-        w[PW_N] = (int64_t)tot[3 * k + 2];
-        int64_t* pw = F.pwords + (int64_t)g * PW_K;
-        if (!F.arrive_g) {
-#pragma unroll
-            for (int q = 0; q < PW_K; ++q) pw[q] = w[q];
-            continue;
-        }
-#pragma unroll
-        for (int q = 0; q < PW_K; ++q) __hip_atomic_store(pw + q, w[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t old = __hip_atomic_fetch_add(F.arrive_g + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old & 1u) {                                  // the node words are already published
-            int64_t nw[NW_K];
-#pragma unroll
-            for (int q = 0; q < NW_K; ++q)
-                nw[q] = __hip_atomic_load(F.nwords + (int64_t)g * NW_K + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            decide_store(G, F.gnode[g], (int32_t)g, w, nw, F.dec, F.cdec);
-        }
-    }
-}
-
 template <int THREADS, int ABLATE = 0, int DC = 3, int DYN = 0, int WS = 0>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
                                                         int64_t* __restrict__ wide,
-                                                        uint32_t* __restrict__ ticket, int cap, K1Fold FF) {
+                                                        uint32_t* __restrict__ ticket, int cap, K1Diag FF) {
     constexpr int NW = THREADS / 64;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds[];
     __shared__ uint32_t s_chunk;
@@ -798,16 +757,9 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     if (trace && threadIdx.x == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
     const int64_t S = G.sp;                                  // row stride (K3 reads whole columns)
     uint64_t* out = part + (int64_t)blockIdx.x * 2 * S + g0;
-    if (!DYN && !ABLATE && FF.arrive) {               // fused fold: write-through (agent-scope) stores
-        for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
-            __hip_atomic_store(out + i, lds[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(out + S + i, lds[gw + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    } else {
-        for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
-            out[i] = lds[i];
-            out[S + i] = lds[gw + i];
-        }
+    for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
+        out[i] = lds[i];
+        out[S + i] = lds[gw + i];
     }
     if (trace) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -821,9 +773,6 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
             __hip_atomic_store(ticket + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if constexpr (!DYN && !ABLATE) {
-        if (FF.arrive) k1_fold<THREADS>(G, FF, part, wide, lds);
-    }
 }
 
 // ============================================================ K1 launchers by part
@@ -835,39 +784,26 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
 #define ESC_K1D(T, A, DC, D) ESC_K1W(T, A, DC, D, 0)
 #define ESC_K1W(T, A, DC, D, W)                                                                       \
     hipLaunchKernelGGL((k_pod_reduce<T, A, DC, D, W>), dim3(nblk), dim3(T), lds, st, p, g, g0, (uint32_t)gw, part, \
-                       wide, ticket, cap, fold)
+                       wide, ticket, cap, diag)
 #define ESC_K1_ARGS const PodDev &p, const GroupDev &g, int32_t g0, int32_t gw, int nblk, int variant, uint64_t *part, \
-                    int64_t *wide, uint32_t *ticket, int cap, const K1Fold &fold, hipStream_t st
+                    int64_t *wide, uint32_t *ticket, int cap, const K1Diag &diag, hipStream_t st
 hipError_t launch_pod_reduce_alt(ESC_K1_ARGS);
 hipError_t launch_pod_reduce_ablation(ESC_K1_ARGS) __attribute__((weak));
 
 #if ESC_PART == 0
 bool k1_dynamic(int variant) { return variant == 5; }
 
-static K1Fold trace_only(const K1Fold& f) {
-    K1Fold t{};
-    t.trace = f.trace;
-    return t;
-}
 
-int k1_blocks_per_cu(int gw) {
-    int nb = 0;
-    const size_t lds = std::max<size_t>((size_t)gw * 2 * sizeof(uint64_t), (size_t)K1_FOLD_LDS);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_pod_reduce<512, 0, 3, 0, 0>, 512, lds) != hipSuccess)
-        return 0;
-    return nb;
-}
 
 hipError_t launch_pod_reduce(ESC_K1_ARGS) {
-    size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
-    if (fold.arrive && lds < (size_t)K1_FOLD_LDS) lds = K1_FOLD_LDS;
+    const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
     switch (variant) {
         case 0: ESC_K1(512, 0, 3); break;
         case 1: case 2: case 5: case 6:
-            return launch_pod_reduce_alt(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, trace_only(fold), st);
+            return launch_pod_reduce_alt(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, diag, st);
         default:                                  // timing-only ablations (ABLATIONS=1 build)
             if (!launch_pod_reduce_ablation) return hipErrorInvalidValue;
-            return launch_pod_reduce_ablation(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, trace_only(fold),
+            return launch_pod_reduce_ablation(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, diag,
                                               st);
     }
     return hipGetLastError();
@@ -1007,39 +943,24 @@ __device__ __forceinline__ bool node_has_pair(const NodeDev& N, int64_t i, uint3
 
 constexpr int K2_WAVES = 4;
 
-// Adds one entry to the piece accumulators: its wet class (filterNodes,
-// controller.go:141-150: Spec.Unschedulable first, then the escalator taint) and the
-// every-member sums used by dry-mode groups.
-struct PieceAcc {
-    unsigned long long ucl = 0, uch = 0, uml = 0, umh = 0, acl = 0, ach = 0, aml = 0, amh = 0, cnt = 0;
-    __device__ __forceinline__ void add(uint32_t f, int64_t c, int64_t m) {
-        if (f & ESC_NF_ABSENT) return;               // spare entry or deleted node
-        const unsigned long long cl = (uint64_t)c & 0xFFFFFFFFull, ml = (uint64_t)m & 0xFFFFFFFFull;
-        const unsigned long long chh = (unsigned long long)(c >> 32), mhh = (unsigned long long)(m >> 32);
-        acl += cl; ach += chh; aml += ml; amh += mhh;
-        const int cls = (f & ESC_NF_UNSCHED) ? 2 : ((f & ESC_NF_TAINTED) ? 1 : 0);
-        if (cls == 0) { ucl += cl; uch += chh; uml += ml; umh += mhh; }
-        cnt += 1ull << (NR_CNT_BITS * cls);
-    }
-};
 
 }  // namespace
 
-// One wave per piece of this rank's range [pc_lo, pc_hi): <= NODE_PIECE entries of one
-// label pair, 24 B per entry streamed coalesced, two 64-entry rounds in flight per
-// iteration, wave sums by butterfly, one NR_K-word row per piece stored word-major
-// (rows[k * n_pieces + p], so K3's lanes read consecutive pieces coalesced).  Pieces of
-// pairs no group selects (ids >= n_gp) are skipped.
+// K2: the pieces of this rank's group pairs (<= NODE_PIECE entries of one label pair each,
+// 20 B per entry streamed coalesced) reduced to one NR_K-word row per piece, stored
+// word-major (rows[k * n_pieces + p], so k_node_groups' lanes read consecutive pieces
+// coalesced).  Pieces of pairs no group selects (ids >= n_gp) are in no span.
 // Blocks past the pieces take the dry-mode tracker entries (controller.go:128-133): a
 // (node, dry group) entry whose node is a member of the group and lies in this rank's
 // share of the group's pieces adds the node to the group's tracked sums (trk_acc, global
 // atomics: a few thousand entries), which K3 reads and resets.
-__global__ __launch_bounds__(K2_WAVES * 64) void k_node_pieces(NodeDev N, GroupDev G, int64_t nb_pieces,
-                                                               int64_t* __restrict__ rows,
-                                                               int64_t* __restrict__ trk_acc) {
+namespace {
+
+__device__ __forceinline__ void node_piece_block(const NodeDev& N, const GroupDev& G, int64_t nb_pieces,
+                                                 int64_t* __restrict__ rows, int64_t* __restrict__ trk_acc, int64_t blk) {
     const int lane = threadIdx.x & 63;
-    if ((int64_t)blockIdx.x >= nb_pieces) {
-        const int64_t k = ((int64_t)blockIdx.x - nb_pieces) * (K2_WAVES * 64) + threadIdx.x;
+    if (blk >= nb_pieces) {
+        const int64_t k = (blk - nb_pieces) * (K2_WAVES * 64) + threadIdx.x;
         if (k >= N.n_trk) return;
         const int32_t j = N.trk_node[k], g = N.trk_group[k];
         if (!G.dry[g]) return;                       // wet groups ignore the tracker
@@ -1057,29 +978,14 @@ __global__ __launch_bounds__(K2_WAVES * 64) void k_node_pieces(NodeDev N, GroupD
         g_add(r + TA_MEM_HI, m >> 32);
         return;
     }
-    const int64_t p = N.pc_lo + (int64_t)blockIdx.x * K2_WAVES + (threadIdx.x >> 6);
-    if (p >= N.pc_hi) return;
-    if (N.piece_pair[p] >= G.n_gp) return;
-    const uint32_t a = N.piece_off[p], b = N.piece_off[p + 1];
-    PieceAcc acc;
-    for (uint32_t i = a + lane; i < b; i += 128) {
-        const uint32_t j = i + 64;
-        const bool has_j = j < b;
-        const uint32_t jj = has_j ? j : i;
-        const uint32_t f0 = N.e_flags[i], f1 = N.e_flags[jj];
-        const int64_t c0 = N.e_cpu[i], c1 = N.e_cpu[jj];
-        const int64_t m0 = N.e_mem[i], m1 = N.e_mem[jj];
-        acc.add(f0, c0, m0);
-        if (has_j) acc.add(f1, c1, m1);
-    }
-    const unsigned long long v[NR_K] = {wave_sum64(acc.ucl), wave_sum64(acc.uch), wave_sum64(acc.uml),
-                                        wave_sum64(acc.umh), wave_sum64(acc.acl), wave_sum64(acc.ach),
-                                        wave_sum64(acc.aml), wave_sum64(acc.amh), wave_sum64(acc.cnt)};
-    unsigned long long w = 0;
-#pragma unroll
-    for (int k = 0; k < NR_K; ++k) w = lane == k ? v[k] : w;
-    if (lane < NR_K) rows[(int64_t)lane * N.n_pieces + p] = (int64_t)w;
+    // one wave per span of whole pieces (~NODE_SPAN entries): the span's entries stream
+    // coalesced, U wave-loads in flight; a lane adds its entry to the piece whose range
+    // holds it, and every piece that ends inside a wave-load is reduced (butterflies) and
+    // stored there — small pieces share a wave instead of taking one each (a wave per
+    // ~110-entry piece was latency-bound: 25 us for 26 MB at config 4)
+    node_span(N, rows, blk * K2_WAVES + (threadIdx.x >> 6), lane);
 }
+}  // namespace
 
 // ===================================================================== K3 / K4
 namespace {
@@ -1121,13 +1027,16 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 
 }  // namespace
 
-// K2b (k_node_groups, side stream, beside K1): every group's node words from its pair's
-// K2 piece rows — NewNodeLabelFilterFunc (node_group.go:278) + filterNodes
+// K2b + K4 (k_node_groups, last kernel of the step): every group's node words from its
+// pair's K2 piece rows — NewNodeLabelFilterFunc (node_group.go:278) + filterNodes
 // (controller.go:120-154) + CalculateNodesCapacityTotal(untainted) (util.go:41-51): wet
 // groups take the filterNodes classes, dry groups (controller.go:126-138) every member as
 // untainted (cordoned ones included) except the tracked members (K2's tracker sums, read
 // and reset here).  64 groups per block, the 4 waves split each group's pieces.  Every
-// rank reduces the whole node index, so these words are final (never exchanged).
+// rank reduces the whole node index, so these words are final (never exchanged).  With a
+// decision target (D.dec) the block then decides its groups (K4: the pod words are final —
+// this rank's fold, or the exchanged sums) and writes the compact records to the decision
+// buffer as one contiguous run.
 constexpr int NG_WAVES = 4;
 
 __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeDev N,
@@ -1135,6 +1044,7 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
                                                                int64_t* __restrict__ trk_acc,
                                                                int64_t* __restrict__ nwords, NGDecide D) {
     __shared__ uint64_t red[NG_WAVES][6][64];
+    __shared__ DecCompact sdec[64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int32_t g = blockIdx.x * 64 + lane;
     const bool ok = g < G.G;
@@ -1207,35 +1117,49 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
                           n_ok ? 0 : ESC_TF_NODE_OVERFLOW};
     static_assert(NW_CPU == 0 && NW_MEM == 1 && NW_N_UNT == 2 && NW_N_TAINT == 3 && NW_N_CORD == 4 && NW_FLAGS == 5,
                   "node word order");
-    if (!D.arrive_g) {
 #pragma unroll
-        for (int k = 0; k < 6; ++k) nw[k] = v[k];
-    } else {                                             // fused decide: publish, then arrive
-#pragma unroll
-        for (int k = 0; k < 6; ++k) __hip_atomic_store(nw + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t old = __hip_atomic_fetch_add(D.arrive_g + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old & 1u) {                                  // K1 published the pod words first
-            int64_t pw[PW_K];
-#pragma unroll
-            for (int k = 0; k < PW_K; ++k)
-                pw[k] = __hip_atomic_load(D.pwords + (int64_t)g * PW_K + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            decide_store(G, N.gnode[g], g, pw, v, D.dec, D.cdec);
-        }
+    for (int k = 0; k < 6; ++k) nw[k] = v[k];
+    if (D.dec) {
+        esc_group_decision d;
+        finalize(G, N.gnode[g], g, D.pwords + (int64_t)g * PW_K, v, d, G.metrics);
+        store_full(D.dec + g, d);
+        sdec[lane] = compact_of(d);
     }
+    }
+    if (D.dec) {                                         // contiguous 16-B pieces (PCIe writes)
+        __syncthreads();
+        const int32_t g0 = blockIdx.x * 64;
+        const uint32_t n = G.G - g0 < 64 ? (uint32_t)(G.G - g0) : 64u;
+        store_compact(D.cdec, sdec, n, true, (uint32_t)g0, nullptr, threadIdx.x, NG_WAVES * 64);
     }
 }
 
-// K3 (k_fold_decide): the K1 workgroups' slot partials folded and joined to the groups, in
-// ONE launch with no hand-off between workgroups: one 256-thread workgroup per column of
-// FC_COL pod slots reads every K1 row of its column (16-B loads; a wave-load covers
+// K4 alone (esc_decide after an exchange): the node words are this rank's (k_node_groups
+// ran in the step), the pod words the exchanged sums.
+__global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ pwords,
+                                                const int64_t* __restrict__ nwords,
+                                                esc_group_decision* __restrict__ dec, DecCompact* __restrict__ cdec) {
+    __shared__ DecCompact sc[256];
+    const int32_t g0 = blockIdx.x * 256, g = g0 + (int32_t)threadIdx.x;
+    if (g < G.G) {
+        esc_group_decision d;
+        finalize(G, N.gnode[g], g, pwords + (int64_t)g * PW_K, nwords + (int64_t)g * NW_K, d, G.metrics);
+        store_full(dec + g, d);
+        sc[threadIdx.x] = compact_of(d);
+    }
+    __syncthreads();
+    const uint32_t n = G.G - g0 < 256 ? (uint32_t)(G.G - g0) : 256u;
+    store_compact(cdec, sc, n, true, (uint32_t)g0, nullptr, threadIdx.x, 256);
+}
+
+// K3 fold (fold_col, a role of k_step_tail): the K1 workgroups' slot partials folded and
+// joined to the groups with no hand-off between workgroups: one 256-thread block per column
+// of FC_COL pod slots reads every K1 row of its column (16-B loads; a wave-load covers
 // FD_RPL rows of FC_COL slots, 4 waves x FD_U wave-loads in flight: every row of a
 // 256-workgroup K1 grid in one round, read back from the Infinity Cache K1 just wrote it
 // through), merges the lanes and waves in LDS, adds the slots' wide (exact-path) rows, and
-// evaluates every group whose pod slot lies in the column (col_off / col_groups): pod
-// words, then K4 (decide_one) for one rank.  Narrow columns give ~n_gp / 32 workgroups
-// (313 at 10 k groups) so the whole chip folds: 128-slot columns left 79 CUs reading
-// 0.5 MB each (18.6 us at 12.5 M pods, profiles/r02_v3).
+// writes the pod words of every group whose pod slot lies in the column (col_off /
+// col_groups).  Narrow columns give ~n_gp / 32 blocks (313 at 10 k groups).
 //  - pods: the group's slot is its pair (NewPodAffinityFilterFunc, node_group.go:218) or,
 //    for the group named "default", the default filter's slot (client.go:58-64);
 //  - allNodes[0] (controller.go:208): the pair's first entry (GroupNode, set at load).
@@ -1247,25 +1171,19 @@ constexpr int FD_RPL = 64 / FD_HL;       // K1 rows per wave-load
 static_assert(FD_RPL * FD_HL == 64 && FD_WAVES >= 2, "fold lane map");
 }  // namespace
 
-__global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeDev N, FoldPlan F,
-                                                                 int64_t* __restrict__ wide_pod,
-                                                                 int64_t* __restrict__ pwords,
-                                                                 const int64_t* __restrict__ nwords, int decide,
-                                                                 esc_group_decision* __restrict__ dec,
-                                                                 DecCompact* __restrict__ cdec, int ablate) {
-    // ablate (timing-only, wrong results): 1 no group phase, 4 no fold loads
+namespace {
+__device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, int64_t* __restrict__ wide_pod,
+                                         int64_t* __restrict__ pwords, int col) {
+    // F.ablate (timing-only, wrong results): 1 no group phase, 4 no fold loads
+    const int ablate = F.ablate;
     __shared__ uint64_t red[FD_WAVES][8][64];            // 16 KB
     __shared__ uint64_t tot[4][FC_COL];                 // per slot: cpu, count, mem lo, mem carry
     __shared__ int64_t wtot[WP_K][FC_COL];              // per slot: its wide row
-    __shared__ DecCompact sdec[FC_COL];
-    __shared__ uint32_t s_seq;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int sub = lane / FD_HL, hl = lane % FD_HL;
-    const int col = blockIdx.x;
     const int64_t s0 = (int64_t)col * FC_COL;
     const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
     const uint32_t me = threadIdx.x;
-    if (me == 0) s_seq = 1u;
     // ---- fold: every K1 row of the column; wave w's load u covers rows
     //      (w + FD_WAVES * u) * FD_RPL + sub
     uint64_t cp[2] = {0, 0}, cn[2] = {0, 0}, ml[2] = {0, 0}, mc[2] = {0, 0};
@@ -1327,12 +1245,11 @@ __global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeD
         for (int k = 0; k < WP_K; ++k) wtot[k][me] = p[k];
     __syncthreads();
     if (ablate & 1) return;
-    // ---- the column's groups, one thread each (a column holds ~FC_COL groups)
+    // ---- the column's groups' pod words, one thread each (a column holds ~FC_COL groups)
     for (uint32_t base = ga; base < gb; base += FD_WAVES * 64) {
         const bool ok = base + me < gb;
         const int32_t g = ok ? (int32_t)F.col_groups[base + me] : 0;
         if (ok) {
-            if (g != (int32_t)F.col_groups[base] + (int32_t)me) s_seq = 0u;
             const int sl = (int)((int64_t)G.gslot[g] - s0);
             int64_t* pw = pwords + (int64_t)g * PW_K;
             const __int128 pcpu = (__int128)tot[0][sl] + ((__int128)wtot[WP_CPU_HI][sl] << 32) + (__int128)wtot[WP_CPU_LO][sl];
@@ -1341,38 +1258,11 @@ __global__ __launch_bounds__(FD_WAVES * 64) void k_fold_decide(GroupDev G, NodeD
             split_store(pw, PW_CPU_LO, pcpu);
             split_store(pw, PW_MEM_LO, pmem);
             pw[PW_N] = (int64_t)tot[1][sl] + wtot[WP_CNT][sl];
-            if (decide) {
-                esc_group_decision d;
-                finalize(G, N.gnode[g], g, pw, nwords + (int64_t)g * NW_K, d, G.metrics);
-                store_full(dec + g, d);                       // device copy of the full record
-                if (me < FC_COL) sdec[me] = compact_of(d);
-                else cdec[g] = compact_of(d);
-            }
-        }
-        if (decide) {
-            __syncthreads();
-            const uint32_t n = gb - base < FC_COL ? gb - base : FC_COL;
-            store_compact(cdec, sdec, n, s_seq != 0, F.col_groups[base], F.col_groups + base, me, FD_WAVES * 64);
-            __syncthreads();
         }
     }
 }
+}  // namespace
 
-__global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ pwords,
-                                                const int64_t* __restrict__ nwords,
-                                                esc_group_decision* __restrict__ dec, DecCompact* __restrict__ cdec) {
-    __shared__ DecCompact sc[256];
-    const int32_t g0 = blockIdx.x * 256, g = g0 + (int32_t)threadIdx.x;
-    if (g < G.G) {
-        esc_group_decision d;
-        finalize(G, N.gnode[g], g, pwords + (int64_t)g * PW_K, nwords + (int64_t)g * NW_K, d, G.metrics);
-        store_full(dec + g, d);
-        sc[threadIdx.x] = compact_of(d);
-    }
-    __syncthreads();
-    const uint32_t n = G.G - g0 < 256 ? (uint32_t)(G.G - g0) : 256u;
-    store_compact(cdec, sc, n, true, (uint32_t)g0, nullptr, threadIdx.x, 256);
-}
 
 // ===================================================================== K5 ordering
 // taintOldestN / untaintNewestN (scale_down.go:171, scale_up.go:118) order a group's
@@ -1850,12 +1740,12 @@ __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long lon
 }
 
 template <int STEPS>
-__global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdChunk* __restrict__ chunks,
-                                                          const uint32_t* __restrict__ grp_off,
-                                                          const uint32_t* __restrict__ g_node,
-                                                          const uint32_t* __restrict__ g_grp,
-                                                          const uint32_t* __restrict__ g_flags,
-                                                          uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
+__device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChunk* __restrict__ chunks,
+                                                 const uint32_t* __restrict__ grp_off,
+                                                 const uint32_t* __restrict__ g_node,
+                                                 const uint32_t* __restrict__ g_grp,
+                                                 const uint32_t* __restrict__ g_flags,
+                                                 uint32_t* __restrict__ vals, int64_t* __restrict__ seg, int64_t blk) {
     constexpr int CAP = STEPS * 4 * ORD_BLOCK;           // memberships per chunk
     constexpr int NQ = CAP / 4;
     constexpr int C1 = 21, C2 = 42;
@@ -1864,7 +1754,7 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdCh
     __shared__ unsigned long long hp[NQ];                // scan value at each group's first quad
     __shared__ unsigned long long tt[NQ];                // each group's totals, at its first quad
     __shared__ uint32_t stage[CAP];
-    const OrdChunk ch = chunks[blockIdx.x];
+    const OrdChunk ch = chunks[blk];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint4 nd[STEPS], gr[STEPS], fl[STEPS];
     uint32_t grp[STEPS];
@@ -1955,6 +1845,44 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdCh
     const uint32_t n = ch.end - ch.start;
     for (uint32_t i = 4 * threadIdx.x; i < n; i += 4 * ORD_BLOCK)
         *reinterpret_cast<uint4*>(vals + ch.start + i) = *reinterpret_cast<const uint4*>(stage + i);
+}
+
+template <int STEPS>
+__global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdChunk* __restrict__ chunks,
+                                                          const uint32_t* __restrict__ grp_off,
+                                                          const uint32_t* __restrict__ g_node,
+                                                          const uint32_t* __restrict__ g_grp,
+                                                          const uint32_t* __restrict__ g_flags,
+                                                          uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
+    ord_packed_block<STEPS>(N, chunks, grp_off, g_node, g_grp, g_flags, vals, seg, blockIdx.x);
+}
+
+// The step's tail in ONE launch (horizontal fusion; every role is 256 threads and none
+// waits on another): blocks [0, n_col) fold the K1 partials into the pod words (fold_col),
+// the next ones reduce the node pieces and the dry-mode tracker entries (K2,
+// node_piece_block), the last ones order the packed small groups (K5, ord_packed_block).
+// Before, K2 and K5 ran on a side stream beside K1: K1 holds every CU's LDS and its loads
+// starve K2's latency-bound waves, so the side chain ended after K1 and the cross-stream
+// join cost ~10 us more (profiles/r02_v9 timeline): ~45 us after K1 at any pod count.
+__global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPlan F, int64_t* __restrict__ wide_pod,
+                                                   int64_t* __restrict__ pwords, int64_t nb_pieces, int64_t n_piece_blk,
+                                                   int64_t* __restrict__ rows, int64_t* __restrict__ trk_acc,
+                                                   const OrdChunk* __restrict__ chunks, const uint32_t* __restrict__ grp_off,
+                                                   const uint32_t* __restrict__ g_node, const uint32_t* __restrict__ g_grp,
+                                                   const uint32_t* __restrict__ g_flags, uint32_t* __restrict__ vals,
+                                                   int64_t* __restrict__ seg) {
+    static_assert(FD_WAVES * 64 == 256 && K2_WAVES * 64 == 256 && ORD_BLOCK == 256, "one block size for every role");
+    const int64_t b = blockIdx.x;
+    // F.ablate (ESC_K3_ABLATE, timing-only, wrong results): 8 / 16 / 32 skip the fold /
+    // node-piece / ordering role
+    if (b < F.n_col) {
+        if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)b);
+    } else if (b < F.n_col + n_piece_blk) {
+        if (!(F.ablate & 16)) node_piece_block(N, G, nb_pieces, rows, trk_acc, b - F.n_col);
+    } else if (!(F.ablate & 32)) {
+        ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, g_node, g_grp, g_flags, vals, seg,
+                                                       b - F.n_col - n_piece_blk);
+    }
 }
 
 // Region padding: g | MEMB_PAD after each group's memberships (node 0, flags 0).
@@ -2303,15 +2231,6 @@ hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_
     return hipGetLastError();
 }
 
-hipError_t launch_node_pieces(const NodeDev& n, const GroupDev& g, int64_t* rows, int64_t* trk_acc, hipStream_t st) {
-    const int64_t np = n.pc_hi - n.pc_lo;
-    const int64_t nb = (np + K2_WAVES - 1) / K2_WAVES;
-    const int64_t nt = (n.n_trk + K2_WAVES * 64 - 1) / (K2_WAVES * 64);
-    if (nb + nt <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_node_pieces, dim3((unsigned)(nb + nt)), dim3(K2_WAVES * 64), 0, st, n, g, nb, rows, trk_acc);
-    return hipGetLastError();
-}
-
 hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t* node_rows, int64_t* trk_acc,
                               int64_t* nwords, const NGDecide& nd, hipStream_t st) {
     hipLaunchKernelGGL(k_node_groups, dim3((g.G + 63) / 64), dim3(NG_WAVES * 64), 0, st, g, n, node_rows, trk_acc,
@@ -2319,11 +2238,22 @@ hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t
     return hipGetLastError();
 }
 
-hipError_t launch_fold_decide(const GroupDev& g, const NodeDev& n, const FoldPlan& f, int64_t* wide_pod,
-                              int64_t* pwords, const int64_t* nwords, bool decide, esc_group_decision* dec,
-                              DecCompact* cdec, hipStream_t st) {
-    hipLaunchKernelGGL(k_fold_decide, dim3((unsigned)f.n_col), dim3(FD_WAVES * 64), 0, st, g, n, f, wide_pod, pwords,
-                       nwords, decide ? 1 : 0, dec, cdec, f.ablate);
+hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords,
+                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st) {
+    hipLaunchKernelGGL(k_decide, dim3((g.G + 255) / 256), dim3(256), 0, st, g, n, pwords, nwords, dec, cdec);
+    return hipGetLastError();
+}
+
+hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
+                            int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
+                            const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
+                            const uint32_t* g_flags, uint32_t* vals, int64_t* seg, hipStream_t st) {
+    const int64_t nb = spans ? (n.n_spans + K2_WAVES - 1) / K2_WAVES : 0;      // else K1 made the rows
+    const int64_t nt = (n.n_trk + K2_WAVES * 64 - 1) / (K2_WAVES * 64);
+    const int64_t grid = f.n_col + nb + nt + std::max<int64_t>(n_small, 0);
+    if (grid <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_step_tail, dim3((unsigned)grid), dim3(256), 0, st, g, n, f, wide_pod, pwords, nb, nb + nt, rows,
+                       trk_acc, chunks, grp_off, g_node, g_grp, g_flags, vals, seg);
     return hipGetLastError();
 }
 
@@ -2356,11 +2286,6 @@ hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, h
     return hipGetLastError();
 }
 
-hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords,
-                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st) {
-    hipLaunchKernelGGL(k_decide, dim3((g.G + 255) / 256), dim3(256), 0, st, g, n, pwords, nwords, dec, cdec);
-    return hipGetLastError();
-}
 
 namespace {
 int rs_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, (n + 8191) / 8192)); }

@@ -79,13 +79,14 @@ struct NodeBuf {
     int32_t *trk_node = nullptr, *trk_group = nullptr;
     // pair-major entries, pieces, tracker by group, K2 rows
     uint32_t *e_flags = nullptr, *e_node = nullptr, *piece_off = nullptr, *piece_pair = nullptr, *pp_off = nullptr;
+    uint32_t* span_off = nullptr;                // K2 waves' piece ranges
     int64_t *e_cpu = nullptr, *e_mem = nullptr, *rows = nullptr;
     GroupNode* gnode = nullptr;
     void release() {
         dfree(gnode);
         dfree(flags); dfree(label0); dfree(xl); dfree(xl_off); dfree(trk_start); dfree(cpu); dfree(mem);
         dfree(created); dfree(trk_node); dfree(trk_group);
-        dfree(e_flags); dfree(e_node); dfree(piece_off); dfree(piece_pair); dfree(pp_off);
+        dfree(e_flags); dfree(e_node); dfree(piece_off); dfree(piece_pair); dfree(pp_off); dfree(span_off);
         dfree(e_cpu); dfree(e_mem); dfree(rows);
     }
 };
@@ -153,7 +154,7 @@ struct esc_ctx {
     bool pods_loaded = false;
     NodeBuf nodes;
     int64_t n_nodes = 0, n_xl = 0, n_trk = 0, node_lo = 0, node_hi = 0;
-    int64_t n_entries = 0, n_pieces = 0, pc_lo = 0, pc_hi = 0, node_bytes = 0;
+    int64_t n_entries = 0, n_pieces = 0, pc_lo = 0, pc_hi = 0, node_bytes = 0, n_spans = 0;
     int64_t ts_min = 0, ts_max = 0;
     bool nodes_loaded = false;
     // work
@@ -166,12 +167,7 @@ struct esc_ctx {
     int64_t* d_k1seg = nullptr;                               // K1 work plan [nblk][K1_SEGS][2]
     std::vector<double> k1_share;                             // calibrated K1 shares (esc_k1_calibrate)
     int k1_cap = 0;                                           // K1 chunks per workgroup at most (0: static)
-    bool k1_fold = false;                                     // the fold fused into K1 (K1Fold)
     uint64_t* d_k1_trace = nullptr;                           // K1 per-workgroup timestamps (esc_k1_trace)
-    bool k1_fold_allowed = false;                             // ESC_FUSED_FOLD=1 (off: DESIGN.md §8b), not after a timeout
-    unsigned long long* d_k1_arrive = nullptr;
-    uint32_t* d_arrive_g = nullptr;                           // per-group arrivals (fused decide)
-    uint32_t *d_k1_err = nullptr, *d_k1_goff = nullptr;
     int64_t* d_trk_acc = nullptr;                             // [G][TA_K] dry-mode tracked sums
     int64_t* d_pwords = nullptr;                              // active exchange buffer [G][PW_K]
     int64_t* own_pwords = nullptr;                            // the context-owned one
@@ -181,12 +177,9 @@ struct esc_ctx {
     DecCompact* h_cdec = nullptr;                             // compact records (pinned host)
     DecCompact* h_cdec_dev = nullptr;                         // device view of h_cdec (zero-copy)
     bool zero_copy = true;                                    // K3/K4 write compact decisions to h_cdec
-    bool fork_nodes = true;                                   // K2 on the side stream, beside K1
     bool order_in_step = false;                               // K5 ordering inside every decision
     bool want_metrics = false;                                // K4 also writes the gauges
     esc_group_metrics* d_metrics = nullptr;
-    hipStream_t side = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     int64_t* bound_pwords = nullptr;                          // caller-bound exchange buffer
     void* comm = nullptr;                                     // RCCL communicator (esc_comm_init)
     bool work_ready = false;
@@ -339,6 +332,7 @@ NodeDev node_dev(const esc_ctx* c) {
     n.e_flags = c->nodes.e_flags; n.e_cpu = c->nodes.e_cpu; n.e_mem = c->nodes.e_mem; n.e_node = c->nodes.e_node;
     n.piece_off = c->nodes.piece_off; n.piece_pair = c->nodes.piece_pair; n.pp_off = c->nodes.pp_off;
     n.n_pieces = c->n_pieces; n.pc_lo = c->pc_lo; n.pc_hi = c->pc_hi;
+    n.span_off = c->nodes.span_off; n.n_spans = c->n_spans;
     return n;
 }
 
@@ -402,8 +396,6 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
 void release_work(esc_ctx* c) {
     dfree(c->d_k1seg); dfree(c->d_pod_part); dfree(c->d_wide_pod); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
     dfree(c->d_k1_trace);
-    dfree(c->d_k1_arrive); dfree(c->d_k1_err); dfree(c->d_k1_goff); dfree(c->d_arrive_g);
-    c->k1_fold = false;
     dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_cdec); dfree(c->d_metrics);
     c->d_pwords = nullptr;
     if (c->h_cdec) hipHostFree(c->h_cdec);
@@ -771,35 +763,6 @@ int32_t ensure_work(esc_ctx* c) {
     HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * SP));
     (void)n_col;
     HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
-    {   // the fold fused into K1: one LDS window, slices of <= 512 slots, every workgroup
-        // co-resident (the grid barrier), the production variant
-        const int per = k1_blocks_per_cu(gw);
-        c->k1_fold = c->k1_fold_allowed && c->k1_variant == 0 && S <= POD_WINDOW_MAX && nblk > 0 &&
-                     (S + nblk - 1) / nblk <= 512 && per > 0 && nblk <= (int64_t)per * c->cu_count;
-        if (c->k1_fold) {
-            std::vector<uint32_t> gslot(G), order(G);
-            for (int32_t g = 0; g < G; ++g) {
-                gslot[g] = g == c->gi.default_group ? c->gi.n_gp : c->gi.gpair[g];
-                order[g] = (uint32_t)g;
-            }
-            std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return gslot[a] < gslot[b]; });
-            std::vector<uint32_t> goff(nblk + 1);
-            for (int64_t b = 0; b <= nblk; ++b) {
-                const int64_t lo = S * b / nblk;
-                goff[b] = (uint32_t)(std::lower_bound(order.begin(), order.end(), (uint32_t)lo,
-                                                      [&](uint32_t g, uint32_t v) { return gslot[g] < v; }) -
-                                     order.begin());
-            }
-            HIP_TRY(dalloc(&c->d_k1_goff, goff.size()));
-            HIP_TRY(hipMemcpy(c->d_k1_goff, goff.data(), goff.size() * 4, hipMemcpyHostToDevice));
-            HIP_TRY(dalloc(&c->d_k1_arrive, 1));
-            HIP_TRY(dalloc(&c->d_arrive_g, G));
-            HIP_TRY(dalloc(&c->d_k1_err, 1));
-            HIP_TRY(hipMemset(c->d_k1_arrive, 0, 8));
-            HIP_TRY(hipMemset(c->d_arrive_g, 0, (size_t)G * 4));
-            HIP_TRY(hipMemset(c->d_k1_err, 0, 4));
-        }
-    }
     HIP_TRY(dalloc(&c->d_k1_ticket, 2));
     HIP_TRY(hipMemset(c->d_k1_ticket, 0, 2 * sizeof(uint32_t)));
     HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)S * WP_K * sizeof(int64_t)));
@@ -818,75 +781,45 @@ int32_t ensure_work(esc_ctx* c) {
     return ESC_OK;
 }
 
-// Enqueue K1 + K2 + K3 (and K4 + the decisions when decide) for replica r.  K2 (nodes)
-// runs on the side stream beside K1 (it needs no LDS, so its waves fit next to K1's
-// workgroups) and K3 joins both; with timing on, the stages run in order on one stream so
-// that each has its own events.  Decisions go straight to pinned host memory (zero-copy)
-// unless disabled, in which case a copy follows K3.
+// Enqueue one step for replica r on the context's stream, three launches in order:
+//   K1  the pod pass (LDS windows of pod slots; the exact paths when needed),
+//   tail k_step_tail: the K3 fold into the pod words + K2 (node piece rows, dry-mode
+//        tracker entries) + the K5 ordering of the packed small groups when the ordering is
+//        in the step,
+//   D   k_node_groups: the node words, then K4 + the decisions when `decide` (one rank;
+//        after an exchange esc_decide launches K4 alone).
+// The ordering's remaining kernels (split groups, mid-size packed chunks) follow the tail.
+// Everything is on one stream: K1 fills every CU's LDS, so nothing overlaps it usefully,
+// and a cross-stream join cost ~10 us per step.  With timing on each
+// stage has its own events.  Decisions go straight to pinned host memory (zero-copy)
+// unless disabled, in which case a copy follows.
 int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     const GroupDev g = group_dev(c);
     const NodeDev n = node_dev(c);
     hipStream_t st = c->stream;
-    const bool fork = c->fork_nodes && !c->timing && c->side;
     int e = 0;
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-    if (fork) {
-        HIP_TRY(hipEventRecord(c->ev_fork, st));
-        HIP_TRY(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-    }
-    int nblk = 0;
-    const bool fused = c->k1_fold && !c->force_wide && c->nblk;
-    // the decision inside K1 too when the node words come from the side stream beside it
-    const bool fdec = fused && decide && fork && c->world == 1;
+    auto mark = [&]() -> int32_t {
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+        return ESC_OK;
+    };
     DecCompact* cdec = c->zero_copy ? c->h_cdec_dev : c->d_cdec;
+    if (int32_t rc = mark()) return rc;
+    int nblk = 0;
     if (c->force_wide) {
         if (c->k_tiles + c->c_tiles) HIP_TRY(launch_wide_pods(pod_dev(c, r), g, c->d_wide_pod, st));
     } else if (c->nblk) {
         const PodDev p = pod_dev(c, r);
         const int32_t S = (int32_t)pod_slots(c);
-        K1Fold fold{};
-        fold.trace = c->d_k1_trace;
-        if (fused) {
-            // the big C tiles add to the wide rows the fold reads: they go first
-            HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
-            fold.arrive = c->d_k1_arrive;
-            fold.err = c->d_k1_err;
-            fold.pwords = c->d_pwords;
-            fold.goff = c->d_k1_goff;
-            fold.groups = c->d_col_groups;
-            fold.n_slots = S;
-            if (fdec) {
-                fold.arrive_g = c->d_arrive_g;
-                fold.nwords = c->d_nwords;
-                fold.gnode = n.gnode;
-                fold.dec = c->d_dec;
-                fold.cdec = cdec;
-            }
-        }
         for (int32_t g0 = 0; g0 < S; g0 += POD_WINDOW_MAX) {           // LDS windows of pod slots
             const int32_t gw = std::min(POD_WINDOW_MAX, S - g0);
+            const K1Diag diag{c->d_k1_trace};
             HIP_TRY(launch_pod_reduce(p, g, g0, gw, c->nblk, c->k1_variant, c->d_pod_part, c->d_wide_pod,
-                                      c->d_k1_ticket, c->k1_cap, fold, st));
+                                      c->d_k1_ticket, c->k1_cap, diag, st));
         }
-        if (!fused) HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
+        HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
         nblk = c->nblk;
     }
-    if (fork) {
-        HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, c->side));
-        NGDecide nd{};
-        if (fdec) nd = NGDecide{c->d_arrive_g, c->d_pwords, c->d_dec, cdec};
-        HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, nd, c->side));
-        // the orderings (taintOldestN / untaintNewestN inputs) depend on the node flags
-        // only: they run on the side stream too, beside K1
-        if (c->order_in_step) HIP_TRY(enqueue_order(c, c->side));
-        HIP_TRY(hipEventRecord(c->ev_join, c->side));
-        HIP_TRY(hipStreamWaitEvent(st, c->ev_join, 0));
-    } else {
-        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-        HIP_TRY(launch_node_pieces(n, g, c->nodes.rows, c->d_trk_acc, st));
-        HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, NGDecide{}, st));
-    }
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    if (int32_t rc = mark()) return rc;
     FoldPlan f;
     f.part = c->d_pod_part;
     f.nblk = nblk;
@@ -895,19 +828,28 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     f.col_off = c->d_col_off;
     f.col_groups = c->d_col_groups;
     f.ablate = c->k3_ablate;
-    if (fused) {                                     // pod words from K1: the decision alone
-        if (decide && !fdec) HIP_TRY(launch_decide(g, n, c->d_pwords, c->d_nwords, c->d_dec, cdec, st));
-    } else {
-        HIP_TRY(launch_fold_decide(g, n, f, c->d_wide_pod, c->d_pwords, c->d_nwords, decide, c->d_dec, cdec, st));
+    const bool ord = c->order_in_step;
+    HIP_TRY(launch_step_tail(g, n, f, true, c->d_wide_pod, c->d_pwords, c->nodes.rows, c->d_trk_acc, c->d_pchunks,
+                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_node, c->d_g_grp, c->d_g_flags, c->d_ord,
+                             c->d_seg, st));
+    if (int32_t rc = mark()) return rc;
+    if (ord) {                                       // split groups, mid-size packed chunks
+        HIP_TRY(launch_order(n, c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node, c->d_g_grp,
+                             c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase, c->d_ord, c->d_seg,
+                             st));
+        HIP_TRY(launch_order_packed(n, c->d_pchunks + c->n_psmall, c->n_pchunks - c->n_psmall, 0, c->d_grp_off,
+                                    c->d_g_node, c->d_g_grp, c->d_g_flags, c->d_ord, c->d_seg, st));
     }
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+    if (int32_t rc = mark()) return rc;
+    // D reads and resets the tracker sums the tail accumulated (once per step); a sharded
+    // step (no decide) computes the node words only and esc_decide runs K4 after the exchange
+    NGDecide nd{};
+    if (decide) nd = NGDecide{c->d_pwords, c->d_dec, cdec};
+    HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, nd, st));
+    if (int32_t rc = mark()) return rc;
     if (copy_out && !c->zero_copy) {
         HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)g.G * sizeof(DecCompact), hipMemcpyDeviceToHost, st));
-        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
-    }
-    if (c->order_in_step && !fork) {                  // in order (timing mode): its own stage, last
-        HIP_TRY(enqueue_order(c, st));
-        if (c->timing) HIP_TRY(hipEventRecord(c->ev[e++], st));
+        if (int32_t rc = mark()) return rc;
     }
     c->n_stage_ev = e;
     return ESC_OK;
@@ -1005,12 +947,6 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     c->own_stream = true;
     for (int i = 0; i < MAX_STAGES; ++i)
         if (hipEventCreate(&c->ev[i]) != hipSuccess) return fail(ESC_E_HIP);
-    if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess)
-        return fail(ESC_E_HIP);
-    if (const char* v = std::getenv("ESC_NO_FORK")) c->fork_nodes = std::atoi(v) == 0;
-    if (const char* v = std::getenv("ESC_FUSED_FOLD")) c->k1_fold_allowed = std::atoi(v) != 0;
 
     if (const char* v = std::getenv("ESC_NO_ZEROCOPY")) c->zero_copy = std::atoi(v) == 0;
     const size_t G = (size_t)n_groups;
@@ -1068,10 +1004,6 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         dfree(c->d_col_off); dfree(c->d_col_groups);
         for (int i = 0; i < MAX_STAGES; ++i)
             if (c->ev[i]) hipEventDestroy(c->ev[i]);
-        if (c->side) hipStreamSynchronize(c->side);
-        if (c->ev_fork) hipEventDestroy(c->ev_fork);
-        if (c->ev_join) hipEventDestroy(c->ev_join);
-        if (c->side) hipStreamDestroy(c->side);
         if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     }
     delete c;
@@ -1437,6 +1369,19 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
         node_bytes += 8;                             // piece_pair + piece_off
         if (piece_pair[p] < n_gp) node_bytes += 24 * (int64_t)(piece_off[p + 1] - piece_off[p]);
     }
+    // K2 spans: consecutive whole pieces of the group pairs (a prefix: pieces are pair-sorted
+    // and ids >= n_gp come last), ~NODE_SPAN entries per wave
+    std::vector<uint32_t> span_off(1, (uint32_t)pc_lo);
+    {
+        int64_t p_end = pc_lo, acc = 0;
+        while (p_end < pc_hi && piece_pair[p_end] < n_gp) ++p_end;
+        for (int64_t p = pc_lo; p < p_end; ++p) {
+            const int64_t len = (int64_t)piece_off[p + 1] - piece_off[p];
+            if (acc > 0 && acc + len > NODE_SPAN) { span_off.push_back((uint32_t)p); acc = 0; }
+            acc += len;
+        }
+        if (p_end > pc_lo) span_off.push_back((uint32_t)p_end);
+    }
     // dry-mode tracker: each tracked node's first entry (the (node, group) list is node-sorted)
     std::vector<uint32_t> trk_start(std::max<int64_t>(n + (sf > 0 ? (int64_t)std::ceil((double)n * sf) + 64 : 0), 1),
                                     NONE);
@@ -1489,6 +1434,8 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     HIP_TRY(hipMemcpy(b.piece_off, piece_off.data(), piece_off.size() * 4, hipMemcpyHostToDevice));
     if (n_pieces) HIP_TRY(hipMemcpy(b.piece_pair, piece_pair.data(), piece_pair.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(b.pp_off, pp_off.data(), pp_off.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(dalloc(&b.span_off, span_off.size()));
+    HIP_TRY(hipMemcpy(b.span_off, span_off.data(), span_off.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(dalloc(&b.rows, (size_t)std::max<int64_t>(n_pieces, 1) * NR_K));
     {   // per-group facts fixed by this snapshot: this rank's pieces of the group's pair and
         // allNodes[0] (controller.go:207-211) = the pair's first entry (lowest node index)
@@ -1540,6 +1487,7 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     c->h_gn.clear();
     c->n_entries = E;
     c->n_pieces = n_pieces;
+    c->n_spans = (int64_t)span_off.size() - 1;
     c->pc_lo = pc_lo;
     c->pc_hi = pc_hi;
     c->node_bytes = node_bytes;
@@ -1751,6 +1699,7 @@ int32_t esc_decide(esc_ctx* c) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
     hipSetDevice(c->device);
+    // K4 over the (exchanged) pod words and this rank's node words (computed in the step)
     HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_pwords, c->d_nwords, c->d_dec,
                           c->zero_copy ? c->h_cdec_dev : c->d_cdec, c->stream));
     if (!c->zero_copy)
@@ -1837,17 +1786,6 @@ int32_t esc_sync(esc_ctx* c) {
     if (!c->has_device) return ESC_E_NODEV;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->k1_fold && c->pending) {
-        uint32_t err = 0;
-        HIP_TRY(hipMemcpy(&err, c->d_k1_err, 4, hipMemcpyDeviceToHost));
-        if (err) {                                   // a grid barrier gave up: results invalid,
-            c->k1_fold_allowed = false;              // the separate fold from now on
-            release_work(c);
-            std::snprintf(g_last_error, sizeof g_last_error, "K1 fused-fold barrier timed out (fold disabled; rerun)");
-            c->pending = false;
-            return ESC_E_HIP;
-        }
-    }
     if (c->timing && c->pending && c->n_stage_ev > 1) {
         float ms = 0;
         for (int i = 0; i + 1 < c->n_stage_ev; ++i) {

@@ -16,7 +16,7 @@ run() {   # prefix, regex, command, name, counters...
     timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$rx" \
         --output-format csv -d gpurun_out/${pre}_${TAG}_${name} -o run -- $cmd > gpurun_out/${pre}_${TAG}_${name}.log 2>&1
 }
-K="k_pod_reduce|k_node_pieces|k_pod_fold|k_combine"
+K="k_pod_reduce|k_step_tail|k_node_groups"
 S="k_ord_fused|k_ord_count|k_ord_scatter"
 run pmc "$K" "$CMD" fetch FETCH_SIZE &&
 run pmc "$K" "$CMD" write WRITE_SIZE &&

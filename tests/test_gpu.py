@@ -227,16 +227,12 @@ def test_synthetic_vs_c_oracle(esc, cfg, P, N, G):
     check_metrics(ctx.metrics(), soa.metrics(otot, odf, odi))
 
 
-@pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("cfg,P,N,G", [(2, 1_000_000, 10_000, 100), (4, 2_000_000, 20_000, 10_000),
                                        (4, 300, 50, 10_000), (1, 1000, 50, 1)])
-def test_fold_paths_vs_c_oracle(esc, fused, cfg, P, N, G, monkeypatch):
-    """The fold fused into K1 (ESC_FUSED_FOLD=1: grid barrier, every workgroup folds its
-    slice of pod slots, K1 and k_node_groups decide each group at its second arrival) and the
-    separate fold kernel (default) give the same bit-exact totals and decisions, over
-    repeated graph replays (the barrier and arrival counters only grow) and with the exact
-    wide path forced in between."""
-    monkeypatch.setenv("ESC_FUSED_FOLD", fused)
+def test_step_graph_and_wide_vs_c_oracle(esc, cfg, P, N, G):
+    """The step (K1, the fused tail k_step_tail: fold + node pieces, then node groups +
+    decide) gives bit-exact totals and decisions over repeated graph replays and with the
+    exact wide path forced in between (the wide rows are read and reset by the fold)."""
     s = esc.Synth(P, N, G, config=cfg, seed=0xE5CA1A7E00000000 + cfg)
     otot = soa.totals(s.pods(), s.nodes(), s.groups)
     odf, odi = soa.decide(s.groups, s.states, otot)
