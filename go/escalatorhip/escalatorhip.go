@@ -358,6 +358,13 @@ func (x *Context) Load(pods []*v1.Pod, podOffset int64, nodes []*v1.Node, nodeLo
 	})
 }
 
+// Calibrate balances the pod pass's per-workgroup shares to this GPU's measured streaming
+// rates (esc_k1_calibrate: `rounds` untimed decisions with the current state; results are
+// unchanged).  Call it once after Load and the first RunOnce's state.
+func (x *Context) Calibrate(rounds int) error {
+	return rcErr("esc_k1_calibrate", C.esc_k1_calibrate(x.c, C.int32_t(rounds)))
+}
+
 // RunOnce evaluates scaleNodeGroup's decision for every group at once (controller.go:192-351):
 // listers + filters + sums + filterNodes + cached capacity + gates + percentages + delta +
 // the scale-down clamp.  With a communicator (CommInit) the per-group pod sums are

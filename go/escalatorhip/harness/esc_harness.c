@@ -10,6 +10,7 @@
  *   (*Context).Load     esc_packer_create, esc_packer_add_pods, esc_packer_add_nodes,
  *                       esc_packer_set_tracker (dry-mode groups), esc_packer_view,
  *                       esc_load_pods, esc_load_nodes, esc_packer_destroy
+ *   (*Context).Calibrate esc_k1_calibrate (once, after the first state)
  *   (*Context).RunOnce  esc_set_state, esc_step, esc_sync, esc_results,
  *                       esc_sort_nodes, esc_group_order (taintOldestN / untaintNewestN)
  *   CalculatePodsRequestsTotal / CalculateNodesCapacityTotal
@@ -287,6 +288,7 @@ int main(int argc, char** argv) {
 
     /* (*Context).RunOnce */
     device_call("esc_set_state", esc_set_state(ctx, states));
+    device_call("esc_k1_calibrate", esc_k1_calibrate(ctx, 2));     /* (*Context).Calibrate */
     device_call("esc_step", esc_step(ctx));
     device_call("esc_sync", esc_sync(ctx));
     esc_group_totals* tot = cal((size_t)G, sizeof(esc_group_totals));
