@@ -104,6 +104,28 @@ __device__ __forceinline__ uint32_t wave_incl_scan32(uint32_t v) {
 
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0; }
 
+// Sum over the wave's 64 lanes of a 64-bit value with DPP (VALU only, no LDS round trips):
+// the inclusive-scan pattern of wave_incl_scan32 on both halves, total read from lane 63.
+// (The __shfl_xor butterfly is 12 dependent ds_bpermute per value; K2's 9-value piece
+// reductions spent most of their time waiting on them.)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ unsigned long long dpp64(unsigned long long v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROW_MASK, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROW_MASK, 0xF, false);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long wave_total64(unsigned long long v) {
+    v += dpp64<0x111, 0xF>(v);
+    v += dpp64<0x112, 0xF>(v);
+    v += dpp64<0x114, 0xF>(v);
+    v += dpp64<0x118, 0xF>(v);
+    v += dpp64<0x142, 0xA>(v);
+    v += dpp64<0x143, 0xC>(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63);
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 __device__ __forceinline__ unsigned long long shfl64(unsigned long long v, int src) {
     return __shfl(v, src, 64);
 }
@@ -502,25 +524,29 @@ struct PieceAcc {
 __device__ __forceinline__ void node_span(const NodeDev& N, int64_t* __restrict__ rows, int64_t w, int lane) {
     if (w >= N.n_spans) return;
     typedef __attribute__((address_space(4))) const uint32_t cu32n;
-    const cu32n* poff = (const cu32n*)N.piece_off;
     const uint32_t p0 = ((const cu32n*)N.span_off)[w], p1 = ((const cu32n*)N.span_off)[w + 1];
-    const uint32_t z = poff[p1];
-    uint32_t p = p0, ps = poff[p0], pe = poff[p0 + 1];
+    // the span's <= 64 piece bounds, one per lane (a span has <= 63 pieces), read with
+    // readlane: no dependent load per piece
+    const uint32_t np = p1 - p0;
+    const uint32_t bound = N.piece_off[p0 + (lane < (int)np ? (uint32_t)lane : np)];
+    auto off = [&](uint32_t k) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)bound, (int)k); };
+    const uint32_t z = off(np);
+    uint32_t p = p0, ps = off(0), pe = off(1);
     PieceAcc acc;
     auto flush = [&]() {                             // piece p's row, then the next piece
-        const unsigned long long v[NR_K] = {wave_sum64(acc.ucl), wave_sum64(acc.uch), wave_sum64(acc.uml),
-                                            wave_sum64(acc.umh), wave_sum64(acc.acl), wave_sum64(acc.ach),
-                                            wave_sum64(acc.aml), wave_sum64(acc.amh), wave_sum64(acc.cnt)};
+        const unsigned long long v[NR_K] = {wave_total64(acc.ucl), wave_total64(acc.uch), wave_total64(acc.uml),
+                                            wave_total64(acc.umh), wave_total64(acc.acl), wave_total64(acc.ach),
+                                            wave_total64(acc.aml), wave_total64(acc.amh), wave_total64(acc.cnt)};
         unsigned long long x = 0;
 #pragma unroll
         for (int k = 0; k < NR_K; ++k) x = lane == k ? v[k] : x;
-        if (lane < NR_K) rows[(int64_t)lane * N.n_pieces + p] = (int64_t)x;
+        if (rows && lane < NR_K) rows[(int64_t)lane * N.n_pieces + p] = (int64_t)x;
         acc = PieceAcc();
         ++p;
         ps = pe;
-        if (p < p1) pe = poff[p + 1];
+        if (p < p1) pe = off(p + 1 - p0);
     };
-    constexpr int U = 4;
+    constexpr int U = 8;                             // a NODE_SPAN span's loads in one round
     for (uint32_t base = ps; base < z; base += 64 * U) {
         uint32_t f[U];
         int64_t c[U], m[U];
@@ -1729,13 +1755,14 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __res
 // its region's last quad (tt), and the output segment of group g is [grp_off[g], ...):
 // class 0 then class 1, i.e. the chunk's own slots — so the nodes are staged in LDS and the
 // chunk written back coalesced.  The last quad of each group writes its segment bounds.
+// Inclusive 64-bit scan over the wave with DPP (see wave_total64).
 __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const unsigned long long y = __shfl_up(v, d, 64);
-        if (lane >= d) v += y;
-    }
+    v += dpp64<0x111, 0xF>(v);
+    v += dpp64<0x112, 0xF>(v);
+    v += dpp64<0x114, 0xF>(v);
+    v += dpp64<0x118, 0xF>(v);
+    v += dpp64<0x142, 0xA>(v);
+    v += dpp64<0x143, 0xC>(v);
     return v;
 }
 
@@ -1874,11 +1901,13 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
     static_assert(FD_WAVES * 64 == 256 && K2_WAVES * 64 == 256 && ORD_BLOCK == 256, "one block size for every role");
     const int64_t b = blockIdx.x;
     // F.ablate (ESC_K3_ABLATE, timing-only, wrong results): 8 / 16 / 32 skip the fold /
-    // node-piece / ordering role
+    // node-piece / ordering role, 64 the dry-mode tracker blocks, 128 K2's row stores
     if (b < F.n_col) {
         if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)b);
     } else if (b < F.n_col + n_piece_blk) {
-        if (!(F.ablate & 16)) node_piece_block(N, G, nb_pieces, rows, trk_acc, b - F.n_col);
+        // 64: skip the tracker blocks (timing only)
+        if (!(F.ablate & 16) && !((F.ablate & 64) && b - F.n_col >= nb_pieces))
+            node_piece_block(N, G, nb_pieces, (F.ablate & 128) ? nullptr : rows, trk_acc, b - F.n_col);
     } else if (!(F.ablate & 32)) {
         ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, g_node, g_grp, g_flags, vals, seg,
                                                        b - F.n_col - n_piece_blk);

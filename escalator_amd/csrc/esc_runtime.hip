@@ -1370,15 +1370,18 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
         if (piece_pair[p] < n_gp) node_bytes += 24 * (int64_t)(piece_off[p + 1] - piece_off[p]);
     }
     // K2 spans: consecutive whole pieces of the group pairs (a prefix: pieces are pair-sorted
-    // and ids >= n_gp come last), ~NODE_SPAN entries per wave
+    // and ids >= n_gp come last), <= NODE_SPAN entries (or one larger piece) and <= 63
+    // pieces per wave
     std::vector<uint32_t> span_off(1, (uint32_t)pc_lo);
     {
         int64_t p_end = pc_lo, acc = 0;
         while (p_end < pc_hi && piece_pair[p_end] < n_gp) ++p_end;
+        int64_t np = 0;
         for (int64_t p = pc_lo; p < p_end; ++p) {
             const int64_t len = (int64_t)piece_off[p + 1] - piece_off[p];
-            if (acc > 0 && acc + len > NODE_SPAN) { span_off.push_back((uint32_t)p); acc = 0; }
+            if (acc > 0 && (acc + len > NODE_SPAN || np == 63)) { span_off.push_back((uint32_t)p); acc = 0; np = 0; }
             acc += len;
+            ++np;
         }
         if (p_end > pc_lo) span_off.push_back((uint32_t)p_end);
     }
