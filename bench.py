@@ -239,8 +239,12 @@ def bench_order(args):
     fused = os.environ.get("ESC_ORDER_FUSED", "0") not in ("", "0")
     order_bytes = n_memb * 16
     moved_bytes = n_memb * (16 if fused else 22)
-    idx_passes = -(-R // 8)
-    index_bytes = N * (16 + idx_passes * 32)       # keys 8 + vals 4 per pass (hist 8 + r/w 24), + entries
+    # the index build: node table read twice (count, list: flags, label, created ~24 B),
+    # each membership written once (16 B key + value), LSD passes of <= 8 bits over the
+    # (group << R | creation offset) keys (hist: 8 B read; scatter: 16 B read + 16 B
+    # written), then read once more (16 B) into the regions (12 B written)
+    idx_passes = -(-(R + max(1, (G - 1).bit_length())) // 8)
+    index_bytes = N * 2 * 24 + n_memb * (16 + idx_passes * 40 + 16 + 12)
     out = {
         "metric": "config5 node orderings: memberships ordered/sec per decision (taint/untaint selection)",
         "value": n_memb / (order_ms * 1e-3),

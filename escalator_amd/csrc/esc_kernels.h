@@ -293,19 +293,17 @@ hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t
                               const uint32_t* g_flags, unsigned long long* ticket, unsigned long long* status,
                               uint32_t* vals, int64_t* seg, uint32_t* err, int64_t max_chunk, int ablate,
                               hipStream_t st);
-hipError_t launch_age_index(const NodeDev& n, int64_t ts_min, uint64_t div, int R, uint64_t* keys64[2],
-                            uint32_t* vals[2], uint32_t* hist, uint32_t* tot, uint32_t** age_out, hipStream_t st);
-hipError_t launch_memb_count(const NodeDev& n, const GroupDev& g, const uint32_t* age, int nblk, uint32_t* cnt,
-                             uint32_t* total, hipStream_t st);
-hipError_t launch_memb_expand(const NodeDev& n, const GroupDev& g, const uint32_t* age, int nblk, const uint32_t* base,
-                              uint32_t* e_node, uint32_t* e_grp, uint32_t* e_flags, hipStream_t st);
-hipError_t launch_group_order(const uint32_t* e_grp, int64_t n_e, int32_t G, uint32_t* keys[2], uint32_t* vals[2],
-                              uint32_t* hist, uint32_t* tot, int64_t* starts, uint32_t** perm, uint32_t** gkeys,
-                              hipStream_t st);
-hipError_t launch_group_pos(const uint32_t* gkeys, int64_t n_e, const int64_t* starts, const uint32_t* pstart,
-                            uint32_t* gpos, hipStream_t st);
-hipError_t launch_group_gather(const uint32_t* perm, const uint32_t* gpos, int64_t n_e, const uint32_t* e_node,
-                               const uint32_t* e_grp, const uint32_t* e_flags, uint32_t* g_node, uint32_t* g_grp,
+// The age index (load time): memberships counted per block of nodes (scan: cnt = block
+// bases, *total), listed with (group << R | creation offset) keys and (node | flags << 32)
+// values, LSD-sorted (result in keys[*src] / vals[*src]), group starts; then written into
+// the groups' padded regions.
+hipError_t launch_memb_count(const NodeDev& n, const GroupDev& g, int nblk, uint32_t* cnt, uint32_t* total,
+                             hipStream_t st);
+hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const uint32_t* base, int64_t n_memb,
+                           int64_t ts_min, uint64_t div, int R, int gbits, uint64_t* keys[2], uint64_t* vals[2],
+                           uint32_t* hist, uint32_t* tot, int64_t* starts, int* src, hipStream_t st);
+hipError_t launch_region_write(const uint64_t* keys, const uint64_t* vals, int64_t n_memb, int R, const GroupDev& g,
+                               const int64_t* starts, const uint32_t* pstart, uint32_t* g_node, uint32_t* g_grp,
                                uint32_t* g_flags, hipStream_t st);
 hipError_t launch_order(const NodeDev& n, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
                         const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp, const uint32_t* g_flags,

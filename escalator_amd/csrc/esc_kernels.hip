@@ -1294,9 +1294,10 @@ __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, i
 // taintOldestN / untaintNewestN (scale_down.go:171, scale_up.go:118) order a group's
 // untainted (tainted) nodes by CreationTimestamp (sort.go:6-39).  Creation times and
 // label memberships are immutable, so the snapshot carries an AGE INDEX built once per
-// load (esc_load_nodes): this rank's nodes sorted by creation time (a full LSD radix sort
-// of the creation offsets, ties by snapshot index), and their group memberships listed in
-// that order with a copy of the node flags (like K2's pair-major entries).  Per decision
+// load (esc_load_nodes): every group membership of this rank's nodes, with a copy of the
+// node's flags, in (group, creation time, snapshot index) order — one LSD radix sort of
+// 64-bit (group | creation offset) keys carrying (node | flags) as the value over the
+// memberships listed in snapshot order, so no pass gathers at random.  Per decision
 // only the class can change (taint / cordon / dry-mode tracker), so ordering = classify
 // every membership and stable-partition by (group, class): LSD radix passes over the
 // segment id alone.  A segment then lists its nodes oldest first; newest first is the
@@ -1306,14 +1307,10 @@ constexpr int SORT_BLOCK = 1024;
 constexpr int SORT_WAVES = SORT_BLOCK / 64;
 }
 
-// Creation offsets of nodes [lo, lo + n) (divided by div when exact) and their indices.
-__global__ __launch_bounds__(256) void k_age_keys(NodeDev N, int64_t lo, int64_t n, int64_t ts_min, uint64_t div,
-                                                  uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t off = (uint64_t)(N.created[lo + i] - ts_min);
-    keys[i] = div > 1 ? off / div : off;
-    vals[i] = (uint32_t)(lo + i);
+// Creation offset of node i (divided by div when exact): the low key bits of its memberships.
+__device__ __forceinline__ uint64_t age_key(const NodeDev& N, int64_t i, int64_t ts_min, uint64_t div) {
+    const uint64_t off = (uint64_t)(N.created[i] - ts_min);
+    return div > 1 ? off / div : off;
 }
 
 // ---- LSD radix sort building blocks (stable), BITS-bit digits, KT = uint64_t or uint32_t.
@@ -1411,9 +1408,9 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scan_tot(uint32_t* __restrict
 
 // Stable scatter of one pass: rank = digit base + block offset + rank inside the block in
 // input order (ballot match per wave, per-wave digit counts in LDS).
-template <class KT, int BITS>
-__global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                           KT* __restrict__ kout, uint32_t* __restrict__ vout,
+template <class KT, class VT, int BITS>
+__global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict__ kin, const VT* __restrict__ vin,
+                                                           KT* __restrict__ kout, VT* __restrict__ vout,
                                                            int64_t n, int shift, const uint32_t* __restrict__ hist,
                                                            const uint32_t* __restrict__ tot) {
     constexpr int NB = 1 << BITS;
@@ -1426,15 +1423,15 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     // the next chunk's key / value are loaded one iteration ahead
     KT nkey = lo + (int64_t)threadIdx.x < hi ? kin[lo + threadIdx.x] : (KT)0;
-    uint32_t nval = lo + (int64_t)threadIdx.x < hi ? vin[lo + threadIdx.x] : 0;
+    VT nval = lo + (int64_t)threadIdx.x < hi ? vin[lo + threadIdx.x] : (VT)0;
     for (int64_t b = lo; b < hi; b += SORT_BLOCK) {
         const int64_t i = b + threadIdx.x;
         const bool ok = i < hi;
         const KT key = nkey;
-        const uint32_t val = nval;
+        const VT val = nval;
         const int64_t ni = i + SORT_BLOCK;
         nkey = ni < hi ? kin[ni] : (KT)0;
-        nval = ni < hi ? vin[ni] : 0;
+        nval = ni < hi ? vin[ni] : (VT)0;
         for (int k = threadIdx.x; k < SORT_WAVES * NB; k += SORT_BLOCK) (&wh[0][0])[k] = 0;
         __syncthreads();
         const uint32_t d = (uint32_t)(key >> shift) & (NB - 1);
@@ -1464,10 +1461,11 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
     }
 }
 
-// ---- age-ordered memberships (load time)
-// Memberships of the nodes age[r], r in this block's share of [0, n).
-__global__ __launch_bounds__(SORT_BLOCK) void k_memb_count(NodeDev N, GroupDev G, const uint32_t* __restrict__ age,
-                                                           int64_t n, uint32_t* __restrict__ cnt) {
+// ---- the age index (load time): memberships listed in snapshot order (streaming over
+// the node table), then sorted by (group, creation offset) with (node | flags << 32)
+// carried along, then written into the groups' padded regions (streaming).
+// Memberships of the nodes of this block's share of [0, n) (snapshot order).
+__global__ __launch_bounds__(SORT_BLOCK) void k_memb_count(NodeDev N, GroupDev G, int64_t n, uint32_t* __restrict__ cnt) {
     __shared__ uint32_t tot;
     if (threadIdx.x == 0) tot = 0;
     __syncthreads();
@@ -1475,7 +1473,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_memb_count(NodeDev N, GroupDev G
     const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
     uint32_t c = 0;
     for (int64_t r = lo + threadIdx.x; r < hi; r += SORT_BLOCK) {
-        const int64_t i = age[r];
+        const int64_t i = N.lo + r;
         node_groups(N, G, N.flags[i], i, [&](uint32_t) { ++c; });
     }
     atomicAdd(&tot, c);
@@ -1509,12 +1507,13 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_scan_small(uint32_t* __restrict_
     if (threadIdx.x == 0 && total) *total = carry;
 }
 
-// Writes the memberships in age order (stable: a block's nodes in rank order, a node's
-// groups in label order): entry node, group code (group | dry bit), node flags.
-__global__ __launch_bounds__(SORT_BLOCK) void k_memb_expand(NodeDev N, GroupDev G, const uint32_t* __restrict__ age,
-                                                            int64_t n, const uint32_t* __restrict__ base,
-                                                            uint32_t* __restrict__ e_node, uint32_t* __restrict__ e_grp,
-                                                            uint32_t* __restrict__ e_flags) {
+// Lists the memberships in snapshot order (a block's nodes in order, a node's groups in
+// label order): key = group << R | creation offset (R bits), value = node | membership
+// flags << 32 — a dry group's membership carries "tracked by this group" in the tracker
+// bit (controller.go:126-138), so the per-decision split needs no lookup.
+__global__ __launch_bounds__(SORT_BLOCK) void k_memb_keys(NodeDev N, GroupDev G, int64_t n, const uint32_t* __restrict__ base,
+                                                          int64_t ts_min, uint64_t div, int R,
+                                                          uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
     __shared__ uint32_t wsum[SORT_WAVES];
     __shared__ uint32_t carry;
     if (threadIdx.x == 0) carry = base[blockIdx.x];
@@ -1525,66 +1524,58 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_memb_expand(NodeDev N, GroupDev 
     for (int64_t b = lo; b < hi; b += SORT_BLOCK) {
         const int64_t r = b + threadIdx.x;
         uint32_t c = 0, f = 0;
-        int64_t i = 0;
-        if (r < hi) { i = age[r]; f = N.flags[i]; node_groups(N, G, f, i, [&](uint32_t) { ++c; }); }
-        uint32_t x = c;
-        for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
+        const int64_t i = N.lo + r;
+        if (r < hi) { f = N.flags[i]; node_groups(N, G, f, i, [&](uint32_t) { ++c; }); }
+        const uint32_t x = wave_incl_scan32(c);
         if (lane == 63) wsum[wid] = x;
         __syncthreads();
         uint32_t pos = carry + x - c;
         for (int k = 0; k < wid; ++k) pos += wsum[k];
         if (r < hi && c) {
+            const uint64_t ak = age_key(N, i, ts_min, div);
             node_groups(N, G, f, i, [&](uint32_t mb) {
-                e_node[pos] = (uint32_t)i;
-                e_grp[pos] = mb;
-                // a dry group's membership carries "tracked by this group" in the tracker
-                // bit (controller.go:126-138), so the per-decision split needs no lookup
-                e_flags[pos] = mdry(mb) ? ((f & ~ESC_NF_TRACKED) |
-                                           (((f & ESC_NF_TRACKED) && tracked(N, (int32_t)i, (int32_t)mg(mb)))
-                                                ? ESC_NF_TRACKED : 0u))
-                                        : f;
+                const uint32_t mf = mdry(mb) ? ((f & ~ESC_NF_TRACKED) |
+                                                (((f & ESC_NF_TRACKED) && tracked(N, (int32_t)i, (int32_t)mg(mb)))
+                                                     ? ESC_NF_TRACKED : 0u))
+                                             : f;
+                keys[pos] = ((uint64_t)mg(mb) << R) | ak;
+                vals[pos] = (uint64_t)(uint32_t)i | ((uint64_t)mf << 32);
                 ++pos;
             });
         }
         __syncthreads();
-        if (threadIdx.x == 0) { uint32_t t = 0; for (int k = 0; k < SORT_WAVES; ++k) t += wsum[k]; carry += t; }
+        if (threadIdx.x == 0) { uint32_t s = 0; for (int k = 0; k < SORT_WAVES; ++k) s += wsum[k]; carry += s; }
         __syncthreads();
     }
 }
 
-// ---- group order (load time): the age-ordered memberships stable-sorted by group, so
-// that every group's memberships are one contiguous run, oldest first.
-__global__ __launch_bounds__(256) void k_grp_keys(const uint32_t* __restrict__ e_grp, int64_t n,
-                                                  uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
-    keys[e] = mg(e_grp[e]);
-    vals[e] = (uint32_t)e;
+// First sorted membership of every group s in [0, G] (key >> R = group).
+__global__ __launch_bounds__(256) void k_group_bounds(const uint64_t* __restrict__ keys, int64_t n, int R, int32_t G,
+                                                      int64_t* __restrict__ seg) {
+    const int32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s > G) return;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((keys[mid] >> R) < (uint64_t)s) lo = mid + 1; else hi = mid;
+    }
+    seg[s] = lo;
 }
 
-// Padded position of the e-th membership in group order: every group's run starts on a
-// multiple of 4 so that the per-decision split reads 16-B quads (padding: group NONE).
-__global__ __launch_bounds__(256) void k_grp_pos(const uint32_t* __restrict__ gkeys, int64_t n,
-                                                 const int64_t* __restrict__ starts, const uint32_t* __restrict__ pstart,
-                                                 uint32_t* __restrict__ gpos) {
+// Sorted memberships into the groups' padded regions (streaming): position pstart[g] +
+// rank inside the group; node, group word (group | dry bit), flags.
+__global__ __launch_bounds__(256) void k_region_write(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ vals,
+                                                      int64_t n, int R, GroupDev G, const int64_t* __restrict__ seg,
+                                                      const uint32_t* __restrict__ pstart, uint32_t* __restrict__ g_node,
+                                                      uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_flags) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= n) return;
-    const uint32_t g = gkeys[e];
-    gpos[e] = pstart[g] + (uint32_t)(e - starts[g]);
-}
-
-// Gathers the membership copies into (padded) group order (also after node events).
-__global__ __launch_bounds__(256) void k_grp_gather(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ gpos,
-                                                    int64_t n, const uint32_t* __restrict__ e_node,
-                                                    const uint32_t* __restrict__ e_grp,
-                                                    const uint32_t* __restrict__ e_flags, uint32_t* __restrict__ g_node,
-                                                    uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_flags) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
-    const uint32_t k = perm[e], d = gpos[e];
-    g_node[d] = e_node[k];
-    g_grp[d] = e_grp[k];
-    g_flags[d] = e_flags[k];
+    const uint32_t g = (uint32_t)(keys[e] >> R);
+    const uint64_t v = vals[e];
+    const int64_t d = (int64_t)pstart[g] + (e - seg[g]);
+    g_node[d] = (uint32_t)v;
+    g_grp[d] = g | (G.dry[g] ? NODE_DRY_BIT : 0u);
+    g_flags[d] = (uint32_t)(v >> 32);
 }
 
 // ---- per decision: inside every group's run, a stable 3-way split by filterNodes class
@@ -1596,7 +1587,7 @@ __global__ __launch_bounds__(256) void k_grp_gather(const uint32_t* __restrict__
 constexpr int ORD_BLOCK = 256, ORD_WAVES = ORD_BLOCK / 64;
 
 // Membership flags: a dry group's membership has the tracker bit resolved for its group
-// (k_memb_expand), so no per-decision lookup is needed.
+// (k_memb_keys), so no per-decision lookup is needed.
 __device__ __forceinline__ uint32_t ord_class(const NodeDev&, uint32_t, uint32_t grp, uint32_t f) {
     if ((grp & MEMB_PAD) || (f & ESC_NF_ABSENT)) return 3u;                      // padding, deleted node
     if (mdry(grp)) return (f & ESC_NF_TRACKED) ? 1u : 0u;
@@ -2084,17 +2075,6 @@ __global__ __launch_bounds__(FB) void k_ord_fused(NodeDev N, const OrdChunk* __r
 }
 
 // Start of each (group, class) segment in the partitioned keys: seg[s] = first key >= s.
-__global__ __launch_bounds__(256) void k_seg_bounds(const uint32_t* __restrict__ keys, int64_t n, int32_t nseg,
-                                                    int64_t* __restrict__ seg) {
-    const int32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s > nseg) return;
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (keys[mid] < (uint32_t)s) lo = mid + 1; else hi = mid;
-    }
-    seg[s] = lo;
-}
 
 // ===================================================================== snapshot patches
 // Incremental snapshot updates (esc_pods_upsert / esc_pods_delete / esc_nodes_update):
@@ -2319,24 +2299,24 @@ hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, h
 namespace {
 int rs_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, (n + 8191) / 8192)); }
 
-template <class KT, int BITS>
-hipError_t rs_pass(const KT* kin, const uint32_t* vin, KT* kout, uint32_t* vout, int64_t n, int shift, uint32_t* hist,
+template <class KT, class VT, int BITS>
+hipError_t rs_pass(const KT* kin, const VT* vin, KT* kout, VT* vout, int64_t n, int shift, uint32_t* hist,
                    uint32_t* tot, hipStream_t st) {
     const int nblk = rs_blocks(n), nb = 1 << BITS;
     hipLaunchKernelGGL((k_rs_hist<KT, BITS>), dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, n, shift, hist);
     hipLaunchKernelGGL(k_rs_scan_rows, dim3((nb + 3) / 4), dim3(256), 0, st, hist, nblk, nb, tot);
     hipLaunchKernelGGL(k_rs_scan_tot, dim3(1), dim3(SORT_BLOCK), 0, st, tot, nb);
-    hipLaunchKernelGGL((k_rs_scatter<KT, BITS>), dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, vin, kout, vout, n, shift,
+    hipLaunchKernelGGL((k_rs_scatter<KT, VT, BITS>), dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, vin, kout, vout, n, shift,
                        hist, tot);
     return hipGetLastError();
 }
 
 // LSD passes over bits [0, bits) of keys[0] / vals[0] (ping-pong with [1]); returns the
 // buffer index holding the result.  8-bit digits, the last pass narrower when it can be.
-// The bits are split evenly over ceil(bits / 8) passes (9 bits -> 5 + 4, 34 -> 7 x 5):
+// The bits are split evenly over ceil(bits / 8) passes (9 bits -> 5 + 4, 41 -> 7 x 5 + 6):
 // narrower digits cost the scatter fewer LDS histogram words per element at equal traffic.
-template <class KT>
-hipError_t rs_sort(KT* keys[2], uint32_t* vals[2], int64_t n, int bits, uint32_t* hist, uint32_t* tot, int* src,
+template <class KT, class VT>
+hipError_t rs_sort(KT* keys[2], VT* vals[2], int64_t n, int bits, uint32_t* hist, uint32_t* tot, int* src,
                    hipStream_t st) {
     *src = 0;
     const int passes = (bits + 7) / 8;
@@ -2344,13 +2324,13 @@ hipError_t rs_sort(KT* keys[2], uint32_t* vals[2], int64_t n, int bits, uint32_t
         const int w = (bits - shift + (passes - p) - 1) / (passes - p);
         hipError_t e;
         KT *ki = keys[*src], *ko = keys[*src ^ 1];
-        uint32_t *vi = vals[*src], *vo = vals[*src ^ 1];
+        VT *vi = vals[*src], *vo = vals[*src ^ 1];
         switch (w) {
-            case 1: case 2: case 3: case 4: e = rs_pass<KT, 4>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
-            case 5: e = rs_pass<KT, 5>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
-            case 6: e = rs_pass<KT, 6>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
-            case 7: e = rs_pass<KT, 7>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
-            default: e = rs_pass<KT, 8>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+            case 1: case 2: case 3: case 4: e = rs_pass<KT, VT, 4>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+            case 5: e = rs_pass<KT, VT, 5>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+            case 6: e = rs_pass<KT, VT, 6>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+            case 7: e = rs_pass<KT, VT, 7>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+            default: e = rs_pass<KT, VT, 8>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
         }
         if (e != hipSuccess) return e;
         *src ^= 1;
@@ -2362,66 +2342,36 @@ hipError_t rs_sort(KT* keys[2], uint32_t* vals[2], int64_t n, int bits, uint32_t
 
 size_t sort_hist_words(int64_t n) { return (size_t)256 * rs_blocks(n); }
 
-hipError_t launch_age_index(const NodeDev& nd, int64_t ts_min, uint64_t div, int R, uint64_t* keys64[2],
-                            uint32_t* vals[2], uint32_t* hist, uint32_t* tot, uint32_t** age_out, hipStream_t st) {
+hipError_t launch_memb_count(const NodeDev& nd, const GroupDev& g, int nblk, uint32_t* cnt, uint32_t* total,
+                             hipStream_t st) {
     const int64_t n = nd.hi - nd.lo;
-    *age_out = vals[0];
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_age_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, nd, nd.lo, n, ts_min, div,
-                       keys64[0], vals[0]);
-    int src = 0;
-    hipError_t e = rs_sort<uint64_t>(keys64, vals, n, R, hist, tot, &src, st);
-    *age_out = vals[src];
-    return e;
-}
-
-hipError_t launch_memb_count(const NodeDev& nd, const GroupDev& g, const uint32_t* age, int nblk, uint32_t* cnt,
-                             uint32_t* total, hipStream_t st) {
-    const int64_t n = nd.hi - nd.lo;
-    hipLaunchKernelGGL(k_memb_count, dim3(nblk), dim3(SORT_BLOCK), 0, st, nd, g, age, n, cnt);
+    hipLaunchKernelGGL(k_memb_count, dim3(nblk), dim3(SORT_BLOCK), 0, st, nd, g, n, cnt);
     hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SORT_BLOCK), 0, st, cnt, nblk, total);
     return hipGetLastError();
 }
 
-hipError_t launch_memb_expand(const NodeDev& nd, const GroupDev& g, const uint32_t* age, int nblk, const uint32_t* base,
-                              uint32_t* e_node, uint32_t* e_grp, uint32_t* e_flags, hipStream_t st) {
+hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const uint32_t* base, int64_t n_memb,
+                           int64_t ts_min, uint64_t div, int R, int gbits, uint64_t* keys[2], uint64_t* vals[2],
+                           uint32_t* hist, uint32_t* tot, int64_t* starts, int* src, hipStream_t st) {
+    *src = 0;
     const int64_t n = nd.hi - nd.lo;
-    hipLaunchKernelGGL(k_memb_expand, dim3(nblk), dim3(SORT_BLOCK), 0, st, nd, g, age, n, base, e_node, e_grp, e_flags);
+    if (n > 0)
+        hipLaunchKernelGGL(k_memb_keys, dim3(nblk), dim3(SORT_BLOCK), 0, st, nd, g, n, base, ts_min, div, R, keys[0],
+                           vals[0]);
+    if (n_memb > 0) {
+        const hipError_t e = rs_sort<uint64_t, uint64_t>(keys, vals, n_memb, R + gbits, hist, tot, src, st);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(k_group_bounds, dim3((g.G + 1 + 255) / 256), dim3(256), 0, st, keys[*src], n_memb, R, g.G, starts);
     return hipGetLastError();
 }
 
-hipError_t launch_group_order(const uint32_t* e_grp, int64_t n_e, int32_t G, uint32_t* keys[2], uint32_t* vals[2],
-                              uint32_t* hist, uint32_t* tot, int64_t* starts, uint32_t** perm, uint32_t** gkeys,
-                              hipStream_t st) {
-    *perm = vals[0];
-    *gkeys = keys[0];
-    if (n_e <= 0) return hipSuccess;
-    const unsigned nb = (unsigned)((n_e + 255) / 256);
-    hipLaunchKernelGGL(k_grp_keys, dim3(nb), dim3(256), 0, st, e_grp, n_e, keys[0], vals[0]);
-    int src = 0;
-    hipError_t e = rs_sort<uint32_t>(keys, vals, n_e, std::max(1, 32 - __builtin_clz((unsigned)std::max(1, G - 1))),
-                                     hist, tot, &src, st);
-    if (e != hipSuccess) return e;
-    *perm = vals[src];
-    *gkeys = keys[src];
-    hipLaunchKernelGGL(k_seg_bounds, dim3((G + 1 + 255) / 256), dim3(256), 0, st, keys[src], n_e, G, starts);
-    return hipGetLastError();
-}
-
-hipError_t launch_group_pos(const uint32_t* gkeys, int64_t n_e, const int64_t* starts, const uint32_t* pstart,
-                            uint32_t* gpos, hipStream_t st) {
-    if (n_e <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_grp_pos, dim3((unsigned)((n_e + 255) / 256)), dim3(256), 0, st, gkeys, n_e, starts, pstart,
-                       gpos);
-    return hipGetLastError();
-}
-
-hipError_t launch_group_gather(const uint32_t* perm, const uint32_t* gpos, int64_t n_e, const uint32_t* e_node,
-                               const uint32_t* e_grp, const uint32_t* e_flags, uint32_t* g_node, uint32_t* g_grp,
+hipError_t launch_region_write(const uint64_t* keys, const uint64_t* vals, int64_t n_memb, int R, const GroupDev& g,
+                               const int64_t* starts, const uint32_t* pstart, uint32_t* g_node, uint32_t* g_grp,
                                uint32_t* g_flags, hipStream_t st) {
-    if (n_e <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_grp_gather, dim3((unsigned)((n_e + 255) / 256)), dim3(256), 0, st, perm, gpos, n_e, e_node,
-                       e_grp, e_flags, g_node, g_grp, g_flags);
+    if (n_memb <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_region_write, dim3((unsigned)((n_memb + 255) / 256)), dim3(256), 0, st, keys, vals, n_memb, R, g,
+                       starts, pstart, g_node, g_grp, g_flags);
     return hipGetLastError();
 }
 

@@ -196,20 +196,18 @@ struct esc_ctx {
     int n_stage_ev = 0;
     bool pending = false;
     // K5 ordering: the age index (built at load) and the per-decision partition
-    uint64_t* d_age_keys[2] = {nullptr, nullptr};            // creation offsets (index build)
-    uint32_t* d_age_vals[2] = {nullptr, nullptr};
-    uint32_t* d_age = nullptr;                                // nodes by creation time
-    uint32_t *d_e_node = nullptr, *d_e_grp = nullptr, *d_e_flags = nullptr;   // memberships, age order
-    uint32_t* d_okeys[2] = {nullptr, nullptr};               // (group << 2 | class), partitioned
-    uint32_t* d_ovals[2] = {nullptr, nullptr};
+    uint64_t* d_mkeys[2] = {nullptr, nullptr};               // index build: (group | creation offset)
+    uint64_t* d_mvals[2] = {nullptr, nullptr};               //              (node | flags << 32)
+    int64_t mcap = 0;                                         // their capacity (memberships)
+    bool age_built = false;
     uint32_t *d_hist = nullptr, *d_tot = nullptr, *d_cnt = nullptr, *d_total = nullptr;
     int64_t* d_seg = nullptr;
     int64_t n_memb = 0;
     int order_src = 0, memb_blocks = 0;
     // group order of the memberships (per-decision 3-way split by class inside each group)
-    uint32_t *d_gperm = nullptr, *d_g_node = nullptr, *d_g_grp = nullptr, *d_g_flags = nullptr;
+    uint32_t *d_g_node = nullptr, *d_g_grp = nullptr, *d_g_flags = nullptr;
     uint32_t *d_grp_off = nullptr, *d_gch_off = nullptr, *d_ccnt = nullptr, *d_cbase = nullptr;
-    uint32_t *d_gpos = nullptr, *d_pstart = nullptr, *d_cls4 = nullptr, *d_plen = nullptr;
+    uint32_t *d_pstart = nullptr, *d_cls4 = nullptr, *d_plen = nullptr;
     uint32_t* d_ord = nullptr;                                // K5 output, in the group regions
     OrdChunk* d_pchunks = nullptr;                            // packed chunks of small groups
     int64_t n_pchunks = 0, n_psmall = 0;                      // all / those <= ORD_PCHUNK (first)
@@ -413,34 +411,34 @@ void release_placement(esc_ctx* c) {
 }
 
 void release_sort(esc_ctx* c) {
-    for (int i = 0; i < 2; ++i) {
-        dfree(c->d_age_keys[i]); dfree(c->d_age_vals[i]); dfree(c->d_okeys[i]); dfree(c->d_ovals[i]);
-    }
-    dfree(c->d_e_node); dfree(c->d_e_grp); dfree(c->d_e_flags);
-    dfree(c->d_gperm); dfree(c->d_g_node); dfree(c->d_g_grp); dfree(c->d_g_flags);
+    for (int i = 0; i < 2; ++i) { dfree(c->d_mkeys[i]); dfree(c->d_mvals[i]); }
+    c->mcap = 0;
+    c->age_built = false;
+    dfree(c->d_g_node); dfree(c->d_g_grp); dfree(c->d_g_flags);
     dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks);
     dfree(c->d_oticket); dfree(c->d_ostat); dfree(c->d_oerr);
-    dfree(c->d_gpos); dfree(c->d_pstart); dfree(c->d_cls4); dfree(c->d_plen); dfree(c->d_ord); dfree(c->d_pchunks);
+    dfree(c->d_pstart); dfree(c->d_cls4); dfree(c->d_plen); dfree(c->d_ord); dfree(c->d_pchunks);
     c->n_pchunks = 0;
     c->n_chunks = 0;
     c->n_gpad = 0;
     dfree(c->d_hist); dfree(c->d_tot); dfree(c->d_cnt); dfree(c->d_total); dfree(c->d_seg);
-    c->d_age = nullptr;
     c->n_memb = 0;
     c->sorted = false;
 }
 
-// The age index: this rank's node range sorted by creation time (LSD
-// radix sort of the creation offsets, divided by the largest of 1e9 / 1e6 / 1e3 that
-// divides them all — an exact order-preserving transform), and the group memberships of
-// the nodes listed in that order with their flags.  Built once per snapshot.
+// The age index: every group membership of this rank's node range, in
+// (group, creation time, snapshot index) order, with its flags — one LSD radix sort of
+// (group << R | creation offset) keys (the offsets divided by the largest of 1e9 / 1e6 /
+// 1e3 that divides them all — an exact order-preserving transform) over the memberships
+// listed in snapshot order (stable: equal times keep index order), carrying (node | flags)
+// as the value, so no pass gathers at random.  Built once per snapshot.
 int32_t build_age_index(esc_ctx* c) {
     const GroupDev g = group_dev(c);
     const NodeDev n = node_dev(c);
     hipStream_t st = c->stream;
     const int64_t nl = c->node_hi - c->node_lo;
-    if (c->d_age_keys[0] && c->age_n != nl) release_sort(c);   // the range grew (esc_nodes_add)
-    const bool fresh = c->d_age_keys[0] == nullptr;
+    if (c->age_built && c->age_n != nl) release_sort(c);   // the range grew (esc_nodes_add)
+    const bool fresh = !c->age_built;
     if (fresh) {
         c->age_n = nl;
         c->h_gn.clear();
@@ -456,40 +454,36 @@ int32_t build_age_index(esc_ctx* c) {
         }
         c->sort_div = div;
         c->sort_R = std::max(1, bit_width((uint64_t)(c->ts_max - c->ts_min) / div));
-        const size_t hw = std::max(sort_hist_words(nl), sort_hist_words(1) * 4);
-        for (int i = 0; i < 2; ++i) { HIP_TRY(dalloc(&c->d_age_keys[i], nl)); HIP_TRY(dalloc(&c->d_age_vals[i], nl)); }
-        HIP_TRY(dalloc(&c->d_hist, hw * 4));   // room for the membership passes too (n_memb <= 4 * n)
+        if (c->sort_R + bit_width((uint64_t)std::max<int32_t>(g.G - 1, 1)) > 64) return ESC_E_LIMIT;
         HIP_TRY(dalloc(&c->d_tot, 256));
         HIP_TRY(dalloc(&c->d_total, 1));
         HIP_TRY(dalloc(&c->d_seg, (size_t)4 * g.G + 1));
         c->memb_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2 * c->cu_count, (nl + 4095) / 4096));
         HIP_TRY(dalloc(&c->d_cnt, c->memb_blocks));
+        c->age_built = true;
     }
-    HIP_TRY(launch_age_index(n, c->ts_min, c->sort_div, c->sort_R, c->d_age_keys, c->d_age_vals, c->d_hist, c->d_tot,
-                             &c->d_age, st));
-    HIP_TRY(launch_memb_count(n, g, c->d_age, c->memb_blocks, c->d_cnt, c->d_total, st));
-    if (fresh) {
-        uint32_t total = 0;
-        HIP_TRY(hipMemcpyAsync(&total, c->d_total, 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        c->n_memb = total;
-        HIP_TRY(dalloc(&c->d_e_node, total)); HIP_TRY(dalloc(&c->d_e_grp, total)); HIP_TRY(dalloc(&c->d_e_flags, total));
-        for (int i = 0; i < 2; ++i) { HIP_TRY(dalloc(&c->d_okeys[i], total)); HIP_TRY(dalloc(&c->d_ovals[i], total)); }
-        if (sort_hist_words(total) > std::max(sort_hist_words(nl), sort_hist_words(1) * 4) * 4) {
-            dfree(c->d_hist);
-            HIP_TRY(dalloc(&c->d_hist, sort_hist_words(total)));
+    // count (block bases) -> the memberships in snapshot order -> sort -> group starts
+    HIP_TRY(launch_memb_count(n, g, c->memb_blocks, c->d_cnt, c->d_total, st));
+    uint32_t total = 0;
+    HIP_TRY(hipMemcpyAsync(&total, c->d_total, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    c->n_memb = total;
+    if ((int64_t)total > c->mcap || !c->d_hist) {
+        for (int i = 0; i < 2; ++i) {
+            dfree(c->d_mkeys[i]); dfree(c->d_mvals[i]);
+            HIP_TRY(dalloc(&c->d_mkeys[i], std::max<int64_t>(total, 1)));
+            HIP_TRY(dalloc(&c->d_mvals[i], std::max<int64_t>(total, 1)));
         }
-        HIP_TRY(dalloc(&c->d_gperm, total)); HIP_TRY(dalloc(&c->d_gpos, total));
+        c->mcap = std::max<int64_t>(total, 1);
+        dfree(c->d_hist);
+        HIP_TRY(dalloc(&c->d_hist, std::max(sort_hist_words(c->mcap), sort_hist_words(1) * 4)));
     }
-    HIP_TRY(launch_memb_expand(n, g, c->d_age, c->memb_blocks, c->d_cnt, c->d_e_node, c->d_e_grp, c->d_e_flags, st));
-    // group order: each group's memberships one run, oldest first, starting on a multiple of
-    // 4 (16-B quads); chunks of <= ORD_CHUNK memberships inside a run drive the split
-    uint32_t *perm = nullptr, *gkeys = nullptr;
-    HIP_TRY(launch_group_order(c->d_e_grp, c->n_memb, g.G, c->d_okeys, c->d_ovals, c->d_hist, c->d_tot, c->d_seg,
-                               &perm, &gkeys, st));
-    if (c->n_memb) HIP_TRY(hipMemcpyAsync(c->d_gperm, perm, c->n_memb * 4, hipMemcpyDeviceToDevice, st));
+    const int gbits = bit_width((uint64_t)std::max<int32_t>(g.G - 1, 1));
+    int src = 0;
+    HIP_TRY(launch_age_sort(n, g, c->memb_blocks, c->d_cnt, c->n_memb, c->ts_min, c->sort_div, c->sort_R, gbits,
+                            c->d_mkeys, c->d_mvals, c->d_hist, c->d_tot, c->d_seg, &src, st));
     std::vector<int64_t> starts((size_t)g.G + 1, 0);
-    if (c->n_memb) HIP_TRY(hipMemcpyAsync(starts.data(), c->d_seg, starts.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(starts.data(), c->d_seg, starts.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     starts[g.G] = c->n_memb;
     // every group's region: its memberships (oldest first), then padding to whole quads plus
@@ -596,11 +590,10 @@ int32_t build_age_index(esc_ctx* c) {
     if (!chunks.empty()) HIP_TRY(hipMemcpy(c->d_chunks, chunks.data(), chunks.size() * sizeof(OrdChunk), hipMemcpyHostToDevice));
     if (!pchunks.empty())
         HIP_TRY(hipMemcpy(c->d_pchunks, pchunks.data(), pchunks.size() * sizeof(OrdChunk), hipMemcpyHostToDevice));
-    HIP_TRY(launch_group_pos(gkeys, c->n_memb, c->d_seg, c->d_pstart, c->d_gpos, st));
-    HIP_TRY(launch_group_gather(c->d_gperm, c->d_gpos, c->n_memb, c->d_e_node, c->d_e_grp, c->d_e_flags, c->d_g_node,
-                                c->d_g_grp, c->d_g_flags, st));
+    HIP_TRY(launch_region_write(c->d_mkeys[src], c->d_mvals[src], c->n_memb, c->sort_R, g, c->d_seg, c->d_pstart,
+                                c->d_g_node, c->d_g_grp, c->d_g_flags, st));
     HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_grp, c->d_g_node, c->d_g_flags, st));
-    {   // after k_grp_pos, which reads d_seg as the groups' unpadded starts
+    {   // after k_region_write, which reads d_seg as the groups' unpadded starts
         std::vector<int64_t> seg0((size_t)4 * g.G + 1);
         for (int32_t q = 0; q < g.G; ++q)
             for (int k = 0; k < 4; ++k) seg0[4 * (size_t)q + k] = pstart[q];
