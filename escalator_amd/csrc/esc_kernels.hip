@@ -114,6 +114,9 @@ __device__ __forceinline__ unsigned long long dpp64(unsigned long long v) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, ROW_MASK, 0xF, false);
     return ((unsigned long long)hi << 32) | lo;
 }
+__device__ __forceinline__ uint32_t wave_total32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan32(v), 63);
+}
 __device__ __forceinline__ unsigned long long wave_total64(unsigned long long v) {
     v += dpp64<0x111, 0xF>(v);
     v += dpp64<0x112, 0xF>(v);
@@ -2172,27 +2175,42 @@ __global__ __launch_bounds__(256) void k_occupancy(NodeDev N, GroupDev G, Remova
         want = q < G.n_gp && (f & ESC_NF_TAINTED) && !(f & (ESC_NF_UNSCHED | ESC_NF_ABSENT));
         if (!want) { R.occ_pair[e] = 0; R.occ_def[e] = 0; }   // defined words for the cross-rank SUM
     }
+    // the wave's wet-tainted entries two at a time: both nodes' PodRef runs are loaded
+    // before either is reduced (DPP sums, no ds_bpermute chains)
     unsigned long long m = __ballot(want);
     while (m) {
-        const int k = __ffsll((long long)m) - 1;
+        const int k0 = __ffsll((long long)m) - 1;
         m &= m - 1;
-        const uint32_t jk = __shfl(j, k, 64), qk = __shfl(q, k, 64);
-        uint32_t cp = 0, cd = 0;
-        for (uint32_t i = R.nrun_off[jk] + lane; i < R.nrun_off[jk] + R.nrun_len[jk]; i += 64) {
-            const PodRef r = R.refs[i];
-            if (r.flags & ESC_PF_DAEMONSET) continue;
-            cp += podref_has(r, R.xp, qk) ? 1u : 0u;
-            cd += pf_default_ok(r.flags & ~POD_REF_INDIRECT) ? 1u : 0u;
+        const int k1 = m ? __ffsll((long long)m) - 1 : -1;
+        if (m) m &= m - 1;
+        const uint32_t j0 = (uint32_t)__builtin_amdgcn_readlane((int)j, k0), q0 = (uint32_t)__builtin_amdgcn_readlane((int)q, k0);
+        const uint32_t j1 = k1 >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)j, k1) : j0;
+        const uint32_t q1 = k1 >= 0 ? (uint32_t)__builtin_amdgcn_readlane((int)q, k1) : q0;
+        const uint32_t a0 = R.nrun_off[j0], n0 = R.nrun_len[j0];
+        const uint32_t a1 = R.nrun_off[j1], n1 = k1 >= 0 ? R.nrun_len[j1] : 0u;
+        uint32_t cp0 = 0, cd0 = 0, cp1 = 0, cd1 = 0;
+        const uint32_t nmax = n0 > n1 ? n0 : n1;
+        for (uint32_t i = lane; i < nmax; i += 64) {
+            PodRef r0, r1;
+            if (i < n0) r0 = R.refs[a0 + i];
+            if (i < n1) r1 = R.refs[a1 + i];
+            if (i < n0 && !(r0.flags & ESC_PF_DAEMONSET)) {
+                cp0 += podref_has(r0, R.xp, q0) ? 1u : 0u;
+                cd0 += pf_default_ok(r0.flags & ~POD_REF_INDIRECT) ? 1u : 0u;
+            }
+            if (i < n1 && !(r1.flags & ESC_PF_DAEMONSET)) {
+                cp1 += podref_has(r1, R.xp, q1) ? 1u : 0u;
+                cd1 += pf_default_ok(r1.flags & ~POD_REF_INDIRECT) ? 1u : 0u;
+            }
         }
-        for (int o = 32; o >= 1; o >>= 1) { cp += __shfl_xor(cp, o, 64); cd += __shfl_xor(cd, o, 64); }
-        if (lane == k) { R.occ_pair[e] = cp; R.occ_def[e] = cd; }
+        cp0 = wave_total32(cp0); cd0 = wave_total32(cd0);
+        if (lane == k0) { R.occ_pair[e] = cp0; R.occ_def[e] = cd0; }
+        if (k1 >= 0) {
+            cp1 = wave_total32(cp1); cd1 = wave_total32(cd1);
+            if (lane == k1) { R.occ_pair[e] = cp1; R.occ_def[e] = cd1; }
+        }
     }
 }
-
-// K7: one wave per group over its pair's entries in snapshot order: the reference's loop
-// over taintedNodes (scale_down.go:53-99) — safeFromDeletion, GetToBeRemovedTime,
-// soft / hard grace, NodeEmpty — then the deletable nodes compacted into the group's list
-// and NodePodsRemaining summed over them (:101-109).  Dry-mode groups delete nothing.
 __global__ __launch_bounds__(64) void k_try_remove(NodeDev N, GroupDev G, RemovalDev R) {
     const int32_t g = blockIdx.x;
     const int lane = threadIdx.x;
@@ -2220,7 +2238,7 @@ __global__ __launch_bounds__(64) void k_try_remove(NodeDev N, GroupDev G, Remova
         if (d) R.rm_list[R.rm_off[g] + del + __popcll(md & lt)] = j;
         del += __popcll(md);
         cand += __popcll(__ballot(c));
-        pods += wave_sum64(d ? occ : 0);
+        pods += (int64_t)wave_total64(d ? (unsigned long long)occ : 0ull);
     }
     if (lane == 0) {
         esc_removal o;

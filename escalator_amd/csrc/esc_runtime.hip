@@ -271,7 +271,8 @@ struct esc_ctx {
     uint8_t* d_no_delete = nullptr;
     esc_removal* d_rm_out = nullptr;
     std::vector<uint32_t> h_rm_off;                           // [G + 1]
-    std::vector<esc_removal> h_rm;
+    esc_removal* h_rm = nullptr;                              // K7 results (pinned copy)
+    std::vector<int64_t> h_soft, h_hard;                      // grace periods last uploaded
     bool rm_valid = false;                                    // esc_try_remove results current
     int64_t rm_nodes = -1;                                    // node count the reaping buffers are sized for
 };
@@ -407,6 +408,9 @@ void release_placement(esc_ctx* c) {
     dfree(c->d_refs); dfree(c->d_e_pair); dfree(c->d_nrun_off); dfree(c->d_nrun_len); dfree(c->d_occ); dfree(c->d_rm_off);
     dfree(c->d_rm_list); dfree(c->d_taint_s); dfree(c->d_soft); dfree(c->d_hard); dfree(c->d_no_delete);
     dfree(c->d_rm_out);
+    if (c->h_rm) { hipHostFree(c->h_rm); c->h_rm = nullptr; }
+    c->h_soft.clear();
+    c->h_hard.clear();
     c->placed = c->node_removal = c->rm_valid = false;
 }
 
@@ -2726,7 +2730,10 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
         }
         HIP_TRY(dalloc(&c->d_rm_list, std::max<uint32_t>(c->h_rm_off[G], 1)));
         HIP_TRY(hipMemcpy(c->d_rm_off, c->h_rm_off.data(), (size_t)G * 4, hipMemcpyHostToDevice));
-        c->h_rm.assign(G, esc_removal{});
+        if (c->h_rm) { hipHostFree(c->h_rm); c->h_rm = nullptr; }
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_rm), (size_t)std::max<int32_t>(G, 1) * sizeof(esc_removal)));
+        c->h_soft.clear();
+        c->h_hard.clear();
         c->rm_nodes = N;
     }
     if (N) {
@@ -2828,13 +2835,22 @@ int32_t esc_reap_finish(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, cons
     if (!c->placed || !c->node_removal) return ESC_E_STATE;
     const int32_t G = c->gi.G;
     hipSetDevice(c->device);
-    HIP_TRY(hipMemcpyAsync(c->d_soft, soft_ns, (size_t)G * 8, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_hard, hard_ns, (size_t)G * 8, hipMemcpyHostToDevice, c->stream));
+    // the grace periods are node-group options: uploaded when they change
+    const bool same = (int32_t)c->h_soft.size() == G && (int32_t)c->h_hard.size() == G &&
+                      std::memcmp(c->h_soft.data(), soft_ns, (size_t)G * 8) == 0 &&
+                      std::memcmp(c->h_hard.data(), hard_ns, (size_t)G * 8) == 0;
+    if (!same) {
+        c->h_soft.assign(soft_ns, soft_ns + G);
+        c->h_hard.assign(hard_ns, hard_ns + G);
+        HIP_TRY(hipMemcpyAsync(c->d_soft, c->h_soft.data(), (size_t)G * 8, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->d_hard, c->h_hard.data(), (size_t)G * 8, hipMemcpyHostToDevice, c->stream));
+    }
+    // K7's per-group records come back by one DMA copy into pinned memory (one 32-B
+    // record per group is too small a write for zero-copy over PCIe)
     HIP_TRY(launch_try_remove(node_dev(c), group_dev(c), removal_dev(c, now_ns), c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_rm.data(), c->d_rm_out, (size_t)G * sizeof(esc_removal), hipMemcpyDeviceToHost,
-                           c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_rm, c->d_rm_out, (size_t)G * sizeof(esc_removal), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    std::memcpy(out, c->h_rm.data(), (size_t)G * sizeof(esc_removal));
+    std::memcpy(out, c->h_rm, (size_t)G * sizeof(esc_removal));
     c->rm_valid = true;
     return ESC_OK;
 }
