@@ -330,7 +330,7 @@ def main():
         ex = Exchange(ctx, device_collective=backend == "nccl")
         ctx.use_graph(args.graph)          # the shard's K1 / tail / node-groups step as one graph
         step = ex.step
-    ctx.k1_calibrate(10)                          # K1 shares to this device's rates (untimed, once per load)
+    ctx.k1_calibrate(16)                          # K1 shares to this device's rates (untimed, once per load)
 
     def barrier():
         if dist is not None:

@@ -1576,7 +1576,7 @@ int32_t esc_stage_times(esc_ctx* c, double* ms, int32_t n) {
 // workgroup's K phase took 1.14x the mean (odd XCDs ~5 % slower than even ones, plus a
 // within-XCD spread), and the per-workgroup durations correlate 0.9-0.98 between
 // decisions and 0.96-0.99 between processes (profiles/r02_v8/k1_trace_stability_*.json).
-// Each round runs one decision, reads every workgroup's K-phase time (trace words 0-1) and
+// Each round runs three decisions, averages every workgroup's K-phase time (trace words 0-1) and
 // scales each share by sqrt(mean time / its time) (a damped step: a share that moves also
 // changes which tiles — classes of other costs — the workgroup streams); the plan with
 // the lowest slowest-workgroup time seen is kept.  The grid and the per-workgroup pod bound
@@ -1600,16 +1600,22 @@ int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
         c->k1_share = sh;
         return ESC_OK;
     };
+    constexpr int REPS = 3;                              // decisions averaged per round (noise ~1-4 %)
     for (int32_t r = 0; r <= rounds; ++r) {
-        rc = c->world == 1 ? esc_run(c) : esc_reduce(c);
-        if (!rc) rc = esc_sync(c);
-        if (rc) return rc;
-        HIP_TRY(hipMemcpy(tr.data(), c->d_k1_trace, tr.size() * 8, hipMemcpyDeviceToHost));
-        std::vector<double> t(nblk);
+        std::vector<double> t(nblk, 0.0);
+        for (int k = 0; k < REPS; ++k) {
+            rc = c->world == 1 ? esc_run(c) : esc_reduce(c);
+            if (!rc) rc = esc_sync(c);
+            if (rc) return rc;
+            HIP_TRY(hipMemcpy(tr.data(), c->d_k1_trace, tr.size() * 8, hipMemcpyDeviceToHost));
+            for (int64_t b = 0; b < nblk; ++b) {
+                const double d = (double)(int64_t)(tr[b * 8 + 1] - tr[b * 8 + 0]);
+                if (!(d > 0)) return ESC_OK;            // no K phase measured: keep the plan
+                t[b] += d / REPS;
+            }
+        }
         double mean = 0, mx = 0;
         for (int64_t b = 0; b < nblk; ++b) {
-            t[b] = (double)(int64_t)(tr[b * 8 + 1] - tr[b * 8 + 0]);
-            if (!(t[b] > 0)) return ESC_OK;             // no K phase measured: keep the plan
             mean += t[b] / (double)nblk;
             mx = std::max(mx, t[b]);
         }

@@ -12,8 +12,8 @@ tail -2 $OUT/pytest_gpu.log
 timeout -k 10 300 python bench.py --no-cpu-baseline > $OUT/bench.json 2> $OUT/b.err || { tail $OUT/b.err; exit 1; }
 timeout -k 10 240 python bench.py --pods 12500000 --steps 50 --warmup 10 --no-cpu-baseline --no-parity \
      > $OUT/bench_p12.5M.json 2> $OUT/p.err || { tail $OUT/p.err; exit 1; }
-CALIBRATE=10 PODS=12500000 VARIANTS=0 timeout -k 10 200 python -u scripts/k1_trace.py > $OUT/trace_p12.5M.json 2> $OUT/t12.err || { tail $OUT/t12.err; exit 1; }
-CALIBRATE=10 PODS=100000000 VARIANTS=0 timeout -k 10 300 python -u scripts/k1_trace.py > $OUT/trace_p100M.json 2> $OUT/t100.err || { tail $OUT/t100.err; exit 1; }
+CALIBRATE=16 PODS=12500000 VARIANTS=0 timeout -k 10 200 python -u scripts/k1_trace.py > $OUT/trace_p12.5M.json 2> $OUT/t12.err || { tail $OUT/t12.err; exit 1; }
+CALIBRATE=16 PODS=100000000 VARIANTS=0 timeout -k 10 300 python -u scripts/k1_trace.py > $OUT/trace_p100M.json 2> $OUT/t100.err || { tail $OUT/t100.err; exit 1; }
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_p12 -o run \
     -- python3 bench.py --pods 12500000 --steps 50 --warmup 10 --no-cpu-baseline --no-parity > $OUT/prof_p12.log 2>&1 || exit 1
 find $OUT/prof_p12 -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats_p12.csv \;
