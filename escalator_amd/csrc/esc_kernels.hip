@@ -786,9 +786,17 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     if (trace && threadIdx.x == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
     const int64_t S = G.sp;                                  // row stride (K3 reads whole columns)
     uint64_t* out = part + (int64_t)blockIdx.x * 2 * S + g0;
-    for (uint32_t i = threadIdx.x; i < gw; i += THREADS) {
-        out[i] = lds[i];
-        out[S + i] = lds[gw + i];
+    // 16-B nontemporal stores (rows and g0 are 16-B aligned: S is a multiple of FC_COL)
+    typedef uint64_t v2u64s __attribute__((ext_vector_type(2)));
+    for (uint32_t i = 2 * threadIdx.x; i < gw; i += 2 * THREADS) {
+        if (i + 1 < gw) {
+            const v2u64s a = {lds[i], lds[i + 1]}, m = {lds[gw + i], lds[gw + i + 1]};
+            __builtin_nontemporal_store(a, reinterpret_cast<v2u64s*>(out + i));
+            __builtin_nontemporal_store(m, reinterpret_cast<v2u64s*>(out + S + i));
+        } else {
+            out[i] = lds[i];
+            out[S + i] = lds[gw + i];
+        }
     }
     if (trace) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1739,7 +1747,7 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __res
     __syncthreads();
     const uint32_t b0 = s_base[0], b1 = s_base[1];
     for (uint32_t i = threadIdx.x; i < n0 + n1; i += ORD_BLOCK)
-        vals[i < n0 ? b0 + i : b1 + (i - n0)] = stage[i];
+        __builtin_nontemporal_store(stage[i], vals + (i < n0 ? b0 + i : b1 + (i - n0)));   // read by the host only
 }
 
 // Small groups packed whole into one chunk (<= ORD_CHUNK memberships, regions start on
@@ -1865,7 +1873,7 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
     __syncthreads();
     const uint32_t n = ch.end - ch.start;
     for (uint32_t i = 4 * threadIdx.x; i < n; i += 4 * ORD_BLOCK)
-        *reinterpret_cast<uint4*>(vals + ch.start + i) = *reinterpret_cast<const uint4*>(stage + i);
+        __builtin_nontemporal_store(*reinterpret_cast<const v4u32*>(stage + i), reinterpret_cast<v4u32*>(vals + ch.start + i));
 }
 
 template <int STEPS>

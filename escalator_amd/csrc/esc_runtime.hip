@@ -27,6 +27,7 @@ namespace {
 
 constexpr int LDS_BYTES = 160 * 1024;
 constexpr int POD_WINDOW_MAX = LDS_BYTES / 16;      // groups whose pod partials fit in LDS
+static_assert(POD_WINDOW_MAX % 2 == 0 && FC_COL % 2 == 0, "K1's 16-B partial-row stores need even window starts");
 constexpr int MAX_STAGES = 8;
 
 #define HIP_TRY(x)                                              \
