@@ -288,6 +288,9 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="replay each step from a captured hipGraph (default: enqueue its three kernels directly; "
                          "a graph launch left ~8 us idle between back-to-back decisions, profiles/r02_v10)")
+    ap.add_argument("--shard-of", type=int, default=1, metavar="W",
+                    help="at N=1: run rank 0's shard of a W-GPU job (1/W of the pods and of the nodes) with no "
+                         "exchange -- the per-rank device time of an N=W run (experiments; no parity check)")
     ap.add_argument("--no-order", action="store_true",
                     help="leave the K5 ordering out of the decision (ablation; BASELINE.md §2 includes it)")
     args = ap.parse_args()
@@ -309,6 +312,11 @@ def main():
 
     lo, hi = shard_range(P, rank, world)
     nlo, nhi = shard_range(N, rank, world)
+    if world == 1 and args.shard_of > 1:
+        lo, hi = shard_range(P, 0, args.shard_of)
+        nlo, nhi = shard_range(N, 0, args.shard_of)
+        cfg["name"] += " [rank 0 of %d, no exchange]" % args.shard_of
+        args.no_parity = True
     t0 = time.time()
     s = esc.Synth(P, N, G, config=args.config, seed=0xE5CA1A7E00000000 + args.config, p_lo=lo, p_hi=hi, threads=16)
     from escalator_amd import layout
@@ -319,7 +327,7 @@ def main():
     ctx.set_state(s.states)
     ctx.set_order_in_step(not args.no_order)          # oldest-first ordering is part of a decision
     n_memb = ctx.order_info()[0]
-    pod_b, node_b = stream_bytes(ctx, s, rank, world)
+    pod_b, node_b = stream_bytes(ctx, s, rank, args.shard_of if world == 1 else world)
     log("rank %d: shard pods [%d,%d) nodes [%d,%d), %.1f MB x %d replicas, setup %.1fs" %
         (rank, lo, hi, nlo, nhi, shard_bytes / 1e6, replicas, time.time() - t0))
 
