@@ -447,7 +447,7 @@ def main():
         # are copied rather than written to pinned host memory by K3 (zero-copy)
         "stage_ms": {k: float(v) for k, v in zip(stage_names, stage_mean) if v > 0} if world == 1 else None,
         "ordering": None if args.no_order else {
-            "kernels": "k_ord_packed (groups <= 4096 memberships, one pass) + k_ord_count / k_ord_scatter (larger groups), on the side stream beside K1 (esc_set_order_in_step)",
+            "kernels": "groups of <= 1024 memberships packed as blocks of k_step_tail (one pass); larger groups by k_ord_count + k_ord_scatter after it; all on the context's one stream (esc_set_order_in_step)",
             "memberships": n_memb, "algorithmic_bytes": n_memb * 16},
         "parity": parity,
     }
