@@ -446,6 +446,8 @@ def main():
         # stages timed in order on one stream (timing mode); "d2h" only when the decisions
         # are copied rather than written to pinned host memory by K3 (zero-copy)
         "stage_ms": {k: float(v) for k, v in zip(stage_names, stage_mean) if v > 0} if world == 1 else None,
+        "stage_note": ("HIP events between the step's launches, timing mode (each event pair adds a few us); "
+                       "k_order_split launches nothing when every group is packed into the tail (config 4)"),
         "ordering": None if args.no_order else {
             "kernels": "groups of <= 1024 memberships packed as blocks of k_step_tail (one pass); larger groups by k_ord_count + k_ord_scatter after it; all on the context's one stream (esc_set_order_in_step)",
             "memberships": n_memb, "algorithmic_bytes": n_memb * 16},
