@@ -100,15 +100,17 @@ def cpu_baseline(cfg, G, full=None, seconds=12.0):
         pods, nodes = full.pods(), full.nodes()
         n_rec = len(pods["flags"]) + len(nodes["flags"])
         soa.totals(pods, nodes, full.groups, threads=threads)          # warm the pages
-        reps, t0 = 0, time.perf_counter()
-        while reps < 3 or time.perf_counter() - t0 < 3.0:
+        ts, t0 = [], time.perf_counter()
+        while len(ts) < 10 or time.perf_counter() - t0 < 3.0:
+            t1 = time.perf_counter()
             soa.totals(pods, nodes, full.groups, threads=threads)
-            reps += 1
-        dt = (time.perf_counter() - t0) / reps
+            ts.append(time.perf_counter() - t1)
+        dt = float(np.median(ts))
         out["value"] = n_rec / dt
+        out["spread"] = [n_rec / max(ts), n_rec / min(ts)]
         out["sample"] = ("B-opt: oracle/esc_oracle.c orc_totals_par (single pass over the SoA snapshot, per-thread "
-                         "group accumulators, OpenMP) over the full %d-record snapshot on %d threads, %d passes, "
-                         "%.3f s per decision" % (n_rec, threads, reps, dt))
+                         "group accumulators, OpenMP) over the full %d-record snapshot on %d threads, median of %d "
+                         "passes, %.3f s per decision" % (n_rec, threads, len(ts), dt))
     P_s, N_s = 2_000_000, 20_000
     s = Synth(P_s, N_s, G, config=cfg["cfg"], seed=0xE5CA1A7E00000000 + cfg["cfg"], threads=16)
     pods, nodes = s.pods(), s.nodes()
@@ -175,10 +177,9 @@ def bench_order(args):
     rank, world, local, dist, backend = init_dist()
     N, G, P = 10_000_000, 100, 100_000
     lo, hi = shard_range(P, rank, world)
-    nlo, nhi = shard_range(N, rank, world)
     s = esc.Synth(P, N, G, config=5, seed=0xE5CA1A7E00000005, p_lo=lo, p_hi=hi, threads=16)
     ctx = esc.Context(s, device=local, rank=rank, world=world)
-    ctx.load_synth(s, pod_offset=lo, node_lo=nlo, node_hi=nhi)
+    ctx.load_synth(s, pod_offset=lo)          # every rank orders the groups whose pairs it owns
 
     def barrier():
         if dist is not None:
@@ -276,6 +277,62 @@ def bench_order(args):
         dist.destroy_process_group()
 
 
+def host_side(esc, ctx_dev):
+    """BASELINE.md §2's host-side figures: the K0 packer over object structs (esc_synth_objects:
+    what the cgo shim fills from *v1.Pod / *v1.Node) of BASELINE config #2, in objects/s on
+    one host thread; and one per-call drop-in esc_pods_requests_total (pkg/k8s/util.go:27:
+    pack + upload + reduce + results on the GPU) over 1000 of those pods (config #1's size)."""
+    import ctypes as C
+    import numpy as np
+    from escalator_amd import _lib as L
+    s = esc.Synth(1_000_000, 10_000, 100, config=2, seed=0xE5CA1A7E00000002, threads=16)
+    po, n, no, nn = s.objects()
+    host = esc.Context(s.groups, device=-1)
+    times = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        host.pack_objects(po, n, no, nn)
+        times.append(time.perf_counter() - t0)
+    t_pack = float(np.median(times))
+    mem, cpu = C.c_int64(), C.c_int64()
+    lib = ctx_dev.lib
+    L.check(lib.esc_pods_requests_total(ctx_dev.handle, po, 1000, C.byref(mem), C.byref(cpu)))   # warm
+    calls = []
+    for _ in range(20):
+        t0 = time.perf_counter()
+        L.check(lib.esc_pods_requests_total(ctx_dev.handle, po, 1000, C.byref(mem), C.byref(cpu)))
+        calls.append(time.perf_counter() - t0)
+    return {"packer_objects_per_s": (n + nn) / t_pack,
+            "packer_sample": "esc_packer_add_pods + _add_nodes + _view over config #2's %d pod and %d node "
+                             "objects (esc_synth_objects), one host thread, median of 3: %.3f s" % (n, nn, t_pack),
+            "dropin_pods_requests_total_ms": float(np.median(calls)) * 1e3,
+            "dropin_sample": "esc_pods_requests_total over 1000 pod objects per call (pack, upload, K1, "
+                             "results), median of 20 calls"}
+
+
+def upload_ms(s, device):
+    """Host -> device copy of the snapshot's SoA arrays (pageable numpy memory, the form a
+    host packs into), through torch on the device: what one decision would add if the
+    snapshot were not resident ('including H2D upload')."""
+    import numpy as np
+    import torch
+    arrs = [a for d in (s.pods(), s.nodes()) for a in d.values() if a.size]
+    total = sum(a.nbytes for a in arrs)
+    buf = torch.empty(total, dtype=torch.uint8, device=device)
+    ts = []
+    for _ in range(3):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        off = 0
+        for a in arrs:
+            buf[off:off + a.nbytes].copy_(torch.from_numpy(a.view(np.uint8)), non_blocking=False)
+            off += a.nbytes
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    del buf
+    return float(np.median(ts)) * 1e3, total
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -284,13 +341,17 @@ def main():
     ap.add_argument("--config", type=int, default=4, choices=sorted(CONFIGS) + [5])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-side packer / upload figures")
     ap.add_argument("--pods", type=int, default=None, help="override the config's pod count (experiments)")
     ap.add_argument("--graph", action="store_true",
                     help="replay each step from a captured hipGraph (default: enqueue its three kernels directly; "
                          "a graph launch left ~8 us idle between back-to-back decisions, profiles/r02_v10)")
     ap.add_argument("--shard-of", type=int, default=1, metavar="W",
-                    help="at N=1: run rank 0's shard of a W-GPU job (1/W of the pods and of the nodes) with no "
-                         "exchange -- the per-rank device time of an N=W run (experiments; no parity check)")
+                    help="at N=1: run rank 0's shard of a W-GPU job (1/W of the pods, the node side of the pairs "
+                         "rank 0 owns) with no exchange -- the per-rank device time of an N=W run (no parity check)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="one process drives --gpus devices through ONE multi-device context (esc_ctx_create_multi: "
+                         "the Go host's drop-in shape; ESC_BENCH_DEVICES=0,0 rehearses it on one GPU)")
     ap.add_argument("--no-order", action="store_true",
                     help="leave the K5 ordering out of the decision (ablation; BASELINE.md §2 includes it)")
     args = ap.parse_args()
@@ -308,36 +369,64 @@ def main():
     import escalator_amd as esc
     from escalator_amd.dist import Exchange, shard_range
 
-    rank, world, local, dist, backend = init_dist()
+    multi = None
+    if args.single_process and args.gpus > 1:
+        env = os.environ.get("ESC_BENCH_DEVICES")
+        multi = [int(x) for x in env.split(",")] if env else list(range(args.gpus))
+        rank, world, local, dist, backend = 0, 1, multi[0], None, "multi"
+        torch.cuda.set_device(local)
+    else:
+        rank, world, local, dist, backend = init_dist()
+    n_gpus = len(multi) if multi else world
 
     lo, hi = shard_range(P, rank, world)
-    nlo, nhi = shard_range(N, rank, world)
-    if world == 1 and args.shard_of > 1:
+    shard_rank, shard_world = rank, world
+    if world == 1 and args.shard_of > 1 and not multi:
         lo, hi = shard_range(P, 0, args.shard_of)
-        nlo, nhi = shard_range(N, 0, args.shard_of)
+        shard_rank, shard_world = 0, args.shard_of
         cfg["name"] += " [rank 0 of %d, no exchange]" % args.shard_of
         args.no_parity = True
     t0 = time.time()
     s = esc.Synth(P, N, G, config=args.config, seed=0xE5CA1A7E00000000 + args.config, p_lo=lo, p_hi=hi, threads=16)
     from escalator_amd import layout
-    shard_bytes = layout.pod_bytes(s.pods()["flags"], s.pod_c.n_xc, s.pod_c.n_xp)
+    shard_bytes = layout.pod_bytes(s.pods()["flags"], s.pod_c.n_xc, s.pod_c.n_xp) // (len(multi) if multi else 1)
     replicas = int(max(1, min(8, -(-1_000_000_000 // max(shard_bytes, 1)))))   # >= 1 GB resident: HBM-served
-    ctx = esc.Context(s, device=local, rank=rank, world=world)
-    ctx.load_synth(s, pod_offset=lo, node_lo=nlo, node_hi=nhi, replicas=replicas)
+    if multi:
+        ctx = esc.Context(s, devices=multi)
+    else:
+        ctx = esc.Context(s, device=local, rank=shard_rank, world=shard_world)
+    t_load = time.perf_counter()
+    ctx.load_synth(s, pod_offset=lo, replicas=replicas)
+    load_ms = (time.perf_counter() - t_load) * 1e3
     ctx.set_state(s.states)
     ctx.set_order_in_step(not args.no_order)          # oldest-first ordering is part of a decision
     n_memb = ctx.order_info()[0]
-    pod_b, node_b = stream_bytes(ctx, s, rank, args.shard_of if world == 1 else world)
-    log("rank %d: shard pods [%d,%d) nodes [%d,%d), %.1f MB x %d replicas, setup %.1fs" %
-        (rank, lo, hi, nlo, nhi, shard_bytes / 1e6, replicas, time.time() - t0))
+    if multi:
+        pod_b, node_b = ctx.stream_bytes()            # every device's shard
+    else:
+        pod_b, node_b = stream_bytes(ctx, s, shard_rank, shard_world)
+    log("rank %d: shard pods [%d,%d), %.1f MB x %d replicas, setup %.1fs" %
+        (rank, lo, hi, shard_bytes / 1e6, replicas, time.time() - t0))
 
-    if world == 1:
-        ctx.use_graph(args.graph)
+    exchange = None
+    if multi:
+        step = ctx.step
+        exchange = "rccl (esc_ctx_create_multi: ncclCommInitAll, one ncclAllReduce per device in a group call)" \
+            if len(set(multi)) == len(multi) and os.environ.get("ESC_EXCHANGE") != "peer" else \
+            "peer (esc_ctx_create_multi: every device sums the others' words over peer-mapped memory)"
+    elif world == 1 and shard_world > 1:
+        def step():                        # rank 0's device work of an N-GPU step, without the SUM
+            ctx.reduce()
+            ctx.decide()
+    elif world == 1:
         step = ctx.run
     else:
         ex = Exchange(ctx, device_collective=backend == "nccl")
-        ctx.use_graph(args.graph)          # the shard's K1 / tail / node-groups step as one graph
         step = ex.step
+        exchange = ("rccl (esc_comm_init + esc_step: ncclAllReduce on the context's stream)" if backend == "nccl"
+                    else "host-staged over torch.distributed %s" % backend)
+    ctx.use_graph(args.graph)
+    rccl_ranks = ctx.comm_size() if (multi or (world > 1 and backend == "nccl")) else None
     ctx.k1_calibrate(16)                          # K1 shares to this device's rates (untimed, once per load)
 
     def barrier():
@@ -359,12 +448,13 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        e = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     ms_per_step = elapsed / args.steps * 1e3
 
-    # Per-kernel device time of K1 (the dominant kernel), HIP events on the context's stream.
+    # Per-kernel device time of K1 (the dominant kernel), HIP events on the context's stream
+    # (a multi-device context: device 0's).
     kp = min(args.steps, 10)
     ctx.set_timing(True)
     k1 = []
@@ -378,8 +468,8 @@ def main():
     ctx.set_timing(False)
     k1_ms = float(np.mean(k1))
     # stages of enqueue_step in timing mode: K1, the fused tail (fold + node pieces + packed
-    # small-group orderings), the remaining ordering kernels, node groups + decide, [copy]
-    stage_names = (["k_pod_reduce", "k_step_tail", "k_order_split", "k_node_groups_decide"] +
+    # small-group orderings), the remaining ordering kernels, node groups (+ decide), [copy]
+    stage_names = (["k_pod_reduce", "k_step_tail", "k_order_split", "k_node_groups"] +
                    (["d2h"] if os.environ.get("ESC_NO_ZEROCOPY", "0") not in ("", "0") else []))
     stage_mean = np.mean(np.array(stages), axis=0)
 
@@ -392,20 +482,23 @@ def main():
             tot, dec = ctx.results()
             full = s if world == 1 else esc.Synth(P, N, G, config=args.config, seed=0xE5CA1A7E00000000 + args.config,
                                                  threads=16)
-            otot = soa.totals(full.pods(), full.nodes(), full.groups)
+            otot = soa.totals(full.pods(), full.nodes(), full.groups, threads=16)
             odf, odi = soa.decide(full.groups, full.states, otot)
             ok = all(np.array_equal(tot[n], otot[:, k]) for k, n in enumerate(soa.TOT_FIELDS[:12]))
             ok &= np.array_equal(dec["cpu_pct"].view(np.uint64), odf[:, 0].view(np.uint64))
             ok &= np.array_equal(dec["mem_pct"].view(np.uint64), odf[:, 1].view(np.uint64))
             ok &= np.array_equal(dec["delta"], odi[:, 0])
-            if not args.no_order:                 # this rank's node range, three groups, both orders
-                for g in (0, G // 2, G - 1):
+            checked = []
+            if not args.no_order:                 # three groups this rank can answer, both orders
+                mine = [g for g in range(G) if multi or ctx.group_owner(g) == rank]
+                for g in sorted(set([mine[0], mine[len(mine) // 2], mine[-1]])) if mine else []:
+                    checked.append(g)
                     for w in (0, 1):
-                        ok &= np.array_equal(ctx.group_order(g, w),
-                                             soa.order(full.nodes(), full.groups, g, w, node_lo=nlo, node_hi=nhi))
+                        ok &= np.array_equal(ctx.group_order(g, w), soa.order(full.nodes(), full.groups, g, w))
             parity = ("bit-exact vs C oracle, all %d groups%s%s" % (
-                      G, "" if args.no_order else " (orderings: groups 0, G/2, G-1, both orders)", "" if world == 1 else
-                      " (rank 0 after the RCCL exchange, oracle over the unsharded snapshot)")
+                      G, "" if args.no_order else " (orderings: groups %s, both orders)" % checked,
+                      "" if n_gpus == 1 else " (rank 0 after the exchange over %d ranks, oracle over the unsharded "
+                                             "snapshot)" % n_gpus)
                       if ok else "MISMATCH vs C oracle")
 
     if rank != 0:
@@ -413,20 +506,22 @@ def main():
             dist.destroy_process_group()
         return
 
-    algo = pod_b
+    # K1's algorithmic bytes per launch on device 0 (its share of the pods)
+    algo = pod_b // (len(multi) if multi else 1)
     achieved = algo / (k1_ms * 1e-3) / 1e9
     records = P + N
     value = records * args.steps / elapsed
-    # shards are near-equal: rank 0's bytes x N (pods, the node index, the orderings)
-    decision_bytes = (pod_b + node_b + (0 if args.no_order else n_memb * 16)) * world
+    # shards are near-equal: rank 0's bytes x N (pods, the node index, the orderings); a
+    # multi-device context reports every device's bytes already
+    decision_bytes = (pod_b + node_b + (0 if args.no_order else n_memb * 16)) * (1 if multi else world)
     # PMC passes are taken on the single-GPU config-4 run (scripts/pmc_job.sh); a shard's
     # K1 launch moves other bytes, so the committed figure applies to N = 1 only
-    traffic = pmc_traffic("k_pod_reduce") if world == 1 and args.config == 4 else None
+    traffic = pmc_traffic("k_pod_reduce") if n_gpus == 1 and shard_world == 1 and args.config == 4 else None
     out = {
         "metric": "pod+node records evaluated/sec per scale decision & % HBM peak, 1/2/4/8 GPUs",
         "value": value,
         "unit": "records/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
@@ -436,13 +531,16 @@ def main():
         "dtype": "int64",
         "data": "synthetic (deterministic counter-hash generator, escalator_amd/csrc/esc_synth.cpp)",
         "config": {"workload": cfg["name"], "pods": P, "nodes": N, "node_groups": G,
-                   "parallelism": "shard%d" % world, "replicas_rotated": replicas},
-        "hbm_frac_decision": decision_bytes / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9 * world),
+                   "parallelism": ("single-process x%d" % n_gpus) if multi else "shard%d" % world,
+                   "replicas_rotated": replicas},
+        "hbm_frac_decision": decision_bytes / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9 * n_gpus),
         "roofline": {"bound": "hbm", "kernel": "k_pod_reduce", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) if traffic else None,
                      "algorithmic_bytes_per_launch": algo, "launch_ms": k1_ms},
         "node_bytes_per_decision": node_b,
+        "exchange": exchange,
+        "rccl_ranks": rccl_ranks,
         # stages timed in order on one stream (timing mode); "d2h" only when the decisions
         # are copied rather than written to pinned host memory by K3 (zero-copy)
         "stage_ms": {k: float(v) for k, v in zip(stage_names, stage_mean) if v > 0} if world == 1 else None,
@@ -453,7 +551,15 @@ def main():
             "memberships": n_memb, "algorithmic_bytes": n_memb * 16},
         "parity": parity,
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if not args.no_host and n_gpus == 1 and shard_world == 1:
+        up_ms, up_bytes = upload_ms(s, torch.device("cuda", local))
+        out["snapshot_load"] = {"esc_load_ms": load_ms, "h2d_ms": up_ms, "h2d_bytes": up_bytes,
+                                "ms_per_step_with_h2d": ms_per_step + up_ms,
+                                "note": "esc_load_ms: esc_load_pods + esc_load_nodes (host layout, the H2D copies of "
+                                        "every replica, the age index), once per snapshot; h2d_ms: the SoA's "
+                                        "pageable host -> HBM copy alone, what a non-resident decision would add"}
+        out["host_side"] = host_side(esc, ctx)
+    if world == 1 and shard_world == 1 and not multi and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, G, full=s)
     print(json.dumps(out), flush=True)
     if dist is not None:

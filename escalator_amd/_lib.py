@@ -122,6 +122,11 @@ _SIGS = {
     "esc_status_string": (cstr, [i32]),
     "esc_taint_error": (i32, [i64, i32, C.c_char_p, i32]),
     "esc_ctx_create": (i32, [P(GroupSpec), i32, i32, i32, i32, P(VP)]),
+    "esc_ctx_create_multi": (i32, [P(GroupSpec), i32, P(i32), i32, P(VP)]),
+    "esc_ctx_counts": (i32, [VP, P(i64), P(i64)]),
+    "esc_group_owner": (i32, [VP, i32, P(i32)]),
+    "esc_node_owner_ranges": (i32, [VP, P(NodeSoA), i32, P(u32)]),
+    "esc_comm_size": (i32, [VP, P(i32)]),
     "esc_ctx_destroy": (i32, [VP]),
     "esc_ctx_set_stream": (i32, [VP, VP]),
     "esc_ctx_num_groups": (i32, [VP]),
@@ -192,6 +197,7 @@ _SIGS = {
     "esc_synth_groups": (i32, [VP, P(P(GroupSpec)), P(i32)]),
     "esc_synth_states": (i32, [VP, P(P(GroupState))]),
     "esc_synth_view": (i32, [VP, P(PodSoA), P(NodeSoA)]),
+    "esc_synth_objects": (i32, [VP, P(P(PodObj)), P(i64), P(P(NodeObj)), P(i64)]),
 }
 
 _lib = None

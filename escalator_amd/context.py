@@ -90,6 +90,16 @@ class Synth:
         self.node_c = L.NodeSoA()
         L.check(self.lib.esc_synth_view(self.handle, C.byref(self.pod_c), C.byref(self.node_c)))
 
+    def objects(self):
+        """The snapshot as object structs (esc_synth_objects, built once, owned by the
+        handle): (pod objects, n_pods, node objects, n_nodes) as ctypes pointers — the input
+        of the K0 packer (esc_packer_add_pods / _add_nodes)."""
+        po, no = C.POINTER(L.PodObj)(), C.POINTER(L.NodeObj)()
+        npd, nnd = C.c_int64(), C.c_int64()
+        L.check(self.lib.esc_synth_objects(self.handle, C.byref(po), C.byref(npd), C.byref(no), C.byref(nnd)),
+                "esc_synth_objects")
+        return po, npd.value, no, nnd.value
+
     def pods(self) -> dict:
         return _view(self.pod_c, _POD_FIELDS)
 
@@ -109,9 +119,13 @@ class Synth:
 
 
 class Context:
-    """One device snapshot + the batched decision over every group."""
+    """One device snapshot + the batched decision over every group.
 
-    def __init__(self, groups, device: int = 0, rank: int = 0, world: int = 1):
+    ``devices=[d0, d1, ...]``: one context driving several devices from this process
+    (esc_ctx_create_multi — pods sharded over the devices, the exchange internal); a device
+    listed more than once selects the peer exchange (several shards on one GPU)."""
+
+    def __init__(self, groups, device: int = 0, rank: int = 0, world: int = 1, devices=None):
         self.lib = L.load()
         if isinstance(groups, Synth):
             spec_ptr, self._gkeep, self.G = groups.specs, None, groups.n_groups
@@ -121,12 +135,37 @@ class Context:
             spec_ptr, self.G = spec_arr, len(groups)
             self.groups = list(groups)
         self.handle = C.c_void_p()
-        L.check(self.lib.esc_ctx_create(spec_ptr, self.G, device, rank, world, C.byref(self.handle)),
-                "esc_ctx_create")
+        if devices is not None:
+            dv = (C.c_int32 * len(devices))(*devices)
+            L.check(self.lib.esc_ctx_create_multi(spec_ptr, self.G, dv, len(devices), C.byref(self.handle)),
+                    "esc_ctx_create_multi")
+            self.devices = list(devices)
+        else:
+            L.check(self.lib.esc_ctx_create(spec_ptr, self.G, device, rank, world, C.byref(self.handle)),
+                    "esc_ctx_create")
+            self.devices = None
         self.world = world
         self._keep = []
 
     # ------------------------------------------------------------- loading
+    def pack_objects(self, pod_objs, n_pods: int, node_objs, n_nodes: int, trackers: dict | None = None):
+        """K0 packer over object structs already in C memory (Synth.objects): packed SoA
+        (numpy copies).  trackers: {group: [node names]} (nodeGroup.taintTracker)."""
+        pk = C.c_void_p()
+        L.check(self.lib.esc_packer_create(self.handle, C.byref(pk)), "esc_packer_create")
+        try:
+            L.check(self.lib.esc_packer_add_pods(pk, pod_objs, n_pods), "esc_packer_add_pods")
+            L.check(self.lib.esc_packer_add_nodes(pk, node_objs, n_nodes), "esc_packer_add_nodes")
+            for g, names in (trackers or {}).items():
+                arr = (C.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+                L.check(self.lib.esc_packer_set_tracker(pk, g, arr, len(names)), "esc_packer_set_tracker")
+            ps, ns = L.PodSoA(), L.NodeSoA()
+            L.check(self.lib.esc_packer_view(pk, C.byref(ps), C.byref(ns)), "esc_packer_view")
+            return ({k: v.copy() for k, v in _view(ps, _POD_FIELDS).items()},
+                    {k: v.copy() for k, v in _view(ns, _NODE_FIELDS).items()})
+        finally:
+            self.lib.esc_packer_destroy(pk)
+
     def pack(self, pods: list[dict], nodes: list[dict], trackers: dict | None = None, list_mode: bool = False):
         """K0 packer: objects -> packed SoA (numpy copies)."""
         pk = C.c_void_p()
@@ -149,21 +188,47 @@ class Context:
             self.lib.esc_packer_destroy(pk)
         return pods_np, nodes_np
 
-    def load(self, pods: dict, nodes: dict, pod_offset: int = 0, node_lo: int = 0, node_hi: int | None = None,
-             replicas: int = 1):
+    def load(self, pods: dict, nodes: dict, pod_offset: int = 0, replicas: int = 1):
+        """This rank's pod shard (global indices from pod_offset) and the whole node table
+        (every rank holds it; its share of the node work is the pairs it owns)."""
         L.check(self.lib.esc_set_replicas(self.handle, replicas), "esc_set_replicas")
         ps, k1 = pod_soa(pods)
         ns, k2 = node_soa(nodes)
         L.check(self.lib.esc_load_pods(self.handle, C.byref(ps), pod_offset), "esc_load_pods")
-        hi = len(nodes["flags"]) if node_hi is None else node_hi
-        L.check(self.lib.esc_load_nodes(self.handle, C.byref(ns), node_lo, hi), "esc_load_nodes")
+        L.check(self.lib.esc_load_nodes(self.handle, C.byref(ns), 0, len(nodes["flags"])), "esc_load_nodes")
 
-    def load_synth(self, s: Synth, pod_offset: int = 0, node_lo: int = 0, node_hi: int | None = None,
-                   replicas: int = 1):
+    def load_synth(self, s: Synth, pod_offset: int = 0, replicas: int = 1):
         L.check(self.lib.esc_set_replicas(self.handle, replicas), "esc_set_replicas")
         L.check(self.lib.esc_load_pods(self.handle, C.byref(s.pod_c), pod_offset), "esc_load_pods")
-        hi = s.node_c.n_nodes if node_hi is None else node_hi
-        L.check(self.lib.esc_load_nodes(self.handle, C.byref(s.node_c), node_lo, hi), "esc_load_nodes")
+        L.check(self.lib.esc_load_nodes(self.handle, C.byref(s.node_c), 0, s.node_c.n_nodes), "esc_load_nodes")
+
+    def counts(self) -> tuple[int, int]:
+        """(pod ids, node slots): the sizes of load_placement's per-pod / per-node arrays."""
+        a, b = C.c_int64(), C.c_int64()
+        L.check(self.lib.esc_ctx_counts(self.handle, C.byref(a), C.byref(b)), "esc_ctx_counts")
+        return a.value, b.value
+
+    def group_owner(self, group: int) -> int:
+        """The rank (device index of a multi-device context) owning the group's node side."""
+        r = C.c_int32()
+        L.check(self.lib.esc_group_owner(self.handle, group, C.byref(r)), "esc_group_owner")
+        return r.value
+
+    def comm_size(self) -> int:
+        """Ranks of the context's communicator (ncclCommCount), or the devices of a
+        multi-device context."""
+        r = C.c_int32()
+        L.check(self.lib.esc_comm_size(self.handle, C.byref(r)), "esc_comm_size")
+        return r.value
+
+    def owner_ranges(self, nodes: dict, world: int) -> np.ndarray:
+        """The owner split of the node side for `world` ranks (host only): rank r owns group
+        pairs [q[r], q[r + 1])."""
+        ns, keep = node_soa(nodes)
+        out = np.zeros(world + 1, np.uint32)
+        L.check(self.lib.esc_node_owner_ranges(self.handle, C.byref(ns), world,
+                                               out.ctypes.data_as(C.POINTER(C.c_uint32))), "esc_node_owner_ranges")
+        return out
 
     # ------------------------------------------------ incremental snapshot (§8f)
     def set_spare(self, fraction: float):

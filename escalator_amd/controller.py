@@ -62,6 +62,38 @@ def untaint_newest_n(created_ns, n: int, device: int = 0) -> list[int]:
     return _order(created_ns, n, False, device)
 
 
+class SimulatedCloud:
+    """The actuator used when none is given: every Kubernetes write succeeds, and the
+    cloud node group behaves like the reference tests' mock (pkg/test/cloud_provider.go):
+    TargetSize is the group's listed node count and MaxSize its ``max_nodes``;
+    IncreaseSize and DeleteNodes succeed."""
+
+    def __init__(self, groups):
+        self.groups = groups
+        self.size = [0] * len(groups)
+
+    def observe(self, g: int, n_nodes: int):
+        self.size[g] = int(n_nodes)
+
+    def taint(self, g: int, node: int) -> bool:
+        return True
+
+    def untaint(self, g: int, node: int) -> bool:
+        return True
+
+    def target_size(self, g: int) -> int:
+        return self.size[g]
+
+    def max_size(self, g: int) -> int:
+        return int(self.groups[g].get("max_nodes", 0))
+
+    def increase_size(self, g: int, n: int):
+        self.size[g] += n
+
+    def delete_nodes(self, g: int, nodes: list[int]):
+        self.size[g] -= len(nodes)
+
+
 class Controller:
     """RunOnce over every node group as one GPU decision, plus the actuation bookkeeping
     the next run depends on.
@@ -78,10 +110,17 @@ class Controller:
       * the dry-mode taintTracker: taintOldestN appends the names it "taints"
         (scale_down.go:197-200), untaintNewestN deletes the newest tracked names
         (scale_up.go:146-158); filterNodes reads it on the next run (controller.go:126-138).
-    Wet-mode API writes (taint / untaint / cloud IncreaseSize) go to an optional
-    ``actuator`` with ``taint(group, idx) -> idx_ok``, ``untaint(group, idx) -> idx_ok`` and
-    ``increase_size(group, n) -> added``; without one every write succeeds and the cloud
-    group adds what was asked (the dry-mode path, scale_up.go:79-88)."""
+
+    Actuation follows the reference's walk: taintOldestN / untaintNewestN go down the GPU
+    ordering one node at a time and skip a node whose API write fails until n writes
+    succeeded (scale_down.go:179-202, scale_up.go:127-160); the cloud add is clamped to
+    MaxSize - TargetSize (calculateNodesToAdd, scale_up.go:48-56) in wet and dry mode, and a
+    clamp <= 0 is scaleUpCloudProviderNodeGroup's error without a lock (scale_up.go:66-74);
+    TryRemoveTaintedNodes (scale_down.go:51-136) runs before tainting and in the no-change
+    branch (controller.go:369-383) on the GPU's reaping pass.  The ``actuator`` provides
+    ``taint(g, node) -> bool``, ``untaint(g, node) -> bool``, ``target_size(g)``,
+    ``max_size(g)``, ``increase_size(g, n)`` and ``delete_nodes(g, nodes)`` (raising on an
+    API error); without one a ``SimulatedCloud`` stands in (every write succeeds)."""
 
     def __init__(self, groups: list[dict], device: int = 0, dry_mode: bool = False, clock=None, actuator=None):
         import time
@@ -93,7 +132,7 @@ class Controller:
         self.lock_time = [None] * len(groups)          # scaleLock.lockTime (None: never locked)
         self.taint_tracker = {g: [] for g in range(len(groups))}
         self.clock = clock or time.time_ns
-        self.actuator = actuator
+        self.actuator = actuator if actuator is not None else SimulatedCloud(self.groups)
 
     def _lock_states(self, now: int):
         """scaleLock.locked() (scale_lock.go:22-29) for every group, before the decision."""
@@ -105,45 +144,75 @@ class Controller:
                 self.state[g]["locked"] = False
                 self.state[g]["requested_nodes"] = 0
 
-    def _scale_up(self, g: int, n: int, tainted: list[int], names: list[str], out: dict) -> int:
+    def _scale_up(self, g: int, n: int, tainted: list[int], names: list[str], out: dict):
         """ScaleUp (scale_up.go:14-46): untaintNewestN over the tainted nodes, the rest
-        from the cloud node group, then the lock."""
+        from the cloud node group (clamped to its MaxSize), then the lock.  Returns
+        (nodes brought up, error-or-None)."""
         dry = self.groups[g]["dry_mode"]
         picked = []
         if tainted:                                        # scaleUpUntaint :98-116
             order = self.ctx.group_order(g, 1)            # newest first (sort.go:27-39)
-            if dry:                                        # delete tracked names, newest first
-                trk = self.taint_tracker[g]
-                for j in order:
-                    if len(picked) >= n:
-                        break
+            for j in order:                                # untaintNewestN :127-160
+                if len(picked) >= n:
+                    break
+                j = int(j)
+                if dry:                                    # delete the tracked name, if any
+                    trk = self.taint_tracker[g]
                     if names[j] in trk:
                         trk.remove(names[j])
-                        picked.append(int(j))
-            else:
-                want = [int(j) for j in order[:max(n, 0)]]
-                picked = list(self.actuator.untaint(g, want)) if self.actuator else want
+                        picked.append(j)
+                elif self.actuator.untaint(g, j):          # a failed write moves on
+                    picked.append(j)
         out["untainted_now"] = picked
         rest = n - len(picked)
-        added = 0
-        if rest > 0:                                       # scaleUpCloudProviderNodeGroup :58-96
-            added = int(self.actuator.increase_size(g, rest)) if (self.actuator and not dry) else rest
-            if added > 0:
-                self.lock_time[g] = self.clock()           # scaleLock.lock(added) :39
-                self.state[g]["locked"] = True
-                self.state[g]["requested_nodes"] = added
-        out["added"] = added
-        return len(picked) + added
+        out["added"] = 0
+        if rest <= 0:
+            return len(picked), None
+        # scaleUpCloudProviderNodeGroup :58-96 with calculateNodesToAdd :48-56
+        target, mx = int(self.actuator.target_size(g)), int(self.actuator.max_size(g))
+        add = mx - target if target + rest > mx else rest
+        if add <= 0:
+            return 0, ("refusing to scaleup up beyond the maximum size of the autoscaling group "
+                       "(TargetSize: %d; MaxNodes: %d). Taking no action" % (target, int(self.groups[g].get("max_nodes", 0))))
+        if not dry:
+            try:
+                self.actuator.increase_size(g, add)
+            except Exception as e:                         # :84-87
+                return 0, str(e)
+        self.lock_time[g] = self.clock()                   # scaleLock.lock(added) :39
+        self.state[g]["locked"] = True
+        self.state[g]["requested_nodes"] = add
+        out["added"] = add
+        return len(picked) + add, None
 
     def _scale_down_taint(self, g: int, n: int, names: list[str], out: dict):
-        """scaleDownTaint -> taintOldestN (scale_down.go:138-205) with the clamped n."""
-        order = self.ctx.group_order(g, 0, cap=max(n, 0))  # untainted, oldest first
-        want = [int(j) for j in order[:max(n, 0)]]
-        if self.groups[g]["dry_mode"]:
-            self.taint_tracker[g] += [names[j] for j in want]
-            out["tainted_now"] = want
-        else:
-            out["tainted_now"] = list(self.actuator.taint(g, want)) if self.actuator else want
+        """scaleDownTaint -> taintOldestN (scale_down.go:138-205) with the clamped n: the
+        untainted nodes oldest first until n taints succeeded."""
+        dry = self.groups[g]["dry_mode"]
+        picked = []
+        for j in self.ctx.group_order(g, 0):
+            if len(picked) >= max(n, 0):
+                break
+            j = int(j)
+            if dry:
+                self.taint_tracker[g].append(names[j])
+                picked.append(j)
+            elif self.actuator.taint(g, j):
+                picked.append(j)
+        out["tainted_now"] = picked
+
+    def _reap(self, g: int, out: dict):
+        """TryRemoveTaintedNodes (scale_down.go:51-136): the GPU pass's toBeDeleted list
+        for the group, handed to the cloud node group (DeleteNodes) in wet mode."""
+        n = int(self._removal[g]["n_delete"])
+        nodes = [int(j) for j in self.ctx.removal_nodes(g)] if n else []
+        out["removed"] = nodes
+        out["pods_evicted"] = int(self._removal[g]["pods_remaining"]) if n else 0
+        if nodes and not self.groups[g]["dry_mode"]:
+            try:
+                self.actuator.delete_nodes(g, nodes)
+            except Exception as e:
+                out["reap_err"] = str(e)
 
     def run_once(self, list_pods, list_nodes) -> list[dict]:
         try:
@@ -154,31 +223,46 @@ class Controller:
             nodes = list_nodes()
         except Exception as e:                   # controller.go:202-205
             return [{"delta": 0, "err": str(e)} for _ in self.groups]
-        self._lock_states(self.clock())
+        from .objects import placement
+        now = self.clock()
+        self._lock_states(now)
         trackers = {g: list(t) for g, t in self.taint_tracker.items() if t}
         P, N = self.ctx.pack(pods, nodes, trackers)
         self.ctx.load(P, N)
         tot, dec = self.ctx.decide_all(self.state)
         self.ctx.sort_nodes()
+        # CreateNodeNameToInfoMap (controller.go:259) + the reaping pass for every group
+        self.ctx.load_placement(*placement(pods, nodes))
+        soft = [int(grp.get("soft_delete_grace_ns", 0)) for grp in self.groups]
+        hard = [int(grp.get("hard_delete_grace_ns", 0)) for grp in self.groups]
+        self._removal = self.ctx.try_remove(now, soft, hard)
         names = [n.get("name", "") for n in nodes]
         out = []
         for g in range(len(self.groups)):
             d = dec[g]
             self.state[g]["cached_cpu_m"] = int(d["cached_cpu_m"])        # controller.go:208-211
             self.state[g]["cached_mem_b"] = int(d["cached_mem_b"])
+            if hasattr(self.actuator, "observe"):
+                self.actuator.observe(g, int(tot["n_nodes"][g]))
             branch = L.BRANCHES[int(d["branch"])]
             r = {"delta": int(d["delta"]), "err": ERRORS.get(int(d["status"])),
                  "branch": branch, "cpu_pct": float(d["cpu_pct"]),
                  "mem_pct": float(d["mem_pct"]), "n_to_taint": int(d["n_to_taint"]),
                  "totals": {k: int(tot[g][k]) for k in tot.dtype.names},
-                 "tainted_now": [], "untainted_now": [], "added": 0}
+                 "tainted_now": [], "untainted_now": [], "added": 0, "removed": [], "pods_evicted": 0}
             tainted = self.ctx.group_order(g, 1) if int(tot["n_tainted"][g]) else []
             if branch == "below_min":                                     # controller.go:281-295
-                r["delta"] = self._scale_up(g, r["delta"], list(tainted), names, r)
-            elif r["err"] is None and branch in ("fast_down", "slow_down") and int(d["taint_status"]) == 0:
-                self._scale_down_taint(g, r["n_to_taint"], names, r)      # controller.go:369-371
+                r["delta"], r["err"] = self._scale_up(g, r["delta"], list(tainted), names, r)
+            elif r["err"] is None and branch in ("fast_down", "slow_down"):
+                self._reap(g, r)                                          # ScaleDown: reap first
+                if int(d["taint_status"]) == 0:
+                    self._scale_down_taint(g, r["n_to_taint"], names, r)  # controller.go:369-371
+                else:
+                    r["action_err"] = "taint clamp"                       # scale_down.go:150-154
             elif r["err"] is None and branch == "scale_up" and r["delta"] > 0:
-                self._scale_up(g, r["delta"], list(tainted), names, r)    # controller.go:372-375
+                _, r["action_err"] = self._scale_up(g, r["delta"], list(tainted), names, r)   # controller.go:372-375
+            elif r["err"] is None and branch == "none":
+                self._reap(g, r)                                          # controller.go:377-383
             out.append(r)
         return out
 

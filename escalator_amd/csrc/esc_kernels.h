@@ -82,16 +82,19 @@ struct PodDev {
 //
 // Two layouts of the same records, both resident on every rank:
 //  - the node table in snapshot order: flags, label pairs, allocatable, creation time.
-//    K5 (ordering) streams nodes [lo, hi) of it; K3 reads allNodes[0]'s capacity.
+//    The K5 age index is listed from it (nodes [lo, hi) = the whole table), keeping the
+//    memberships of this rank's groups; K3 reads allNodes[0]'s capacity.
 //  - the pair-major entries: one entry per (label pair, node), sorted by (pair, node)
 //    at load (e_flags / e_cpu / e_mem / e_node).  NewNodeLabelFilterFunc
 //    (node_group.go:278) is "(K_g, V_g) in the node's label pairs", so a group's members
 //    are exactly the entries of its pair, in snapshot order.  K2 reduces the entries per
-//    piece (a run of <= NODE_PIECE entries of one pair); this rank reduces pieces
-//    [pc_lo, pc_hi).  K3 joins each group to its pair's pieces.
+//    piece (a run of <= NODE_PIECE entries of one pair); this rank reduces the pieces
+//    [pc_lo, pc_hi) of the pairs [q_lo, q_hi) it owns.  K3 joins each group to its pair's
+//    pieces.
 // Per-group node facts that are fixed for a loaded snapshot (esc_load_nodes): this rank's
-// piece range of the group's pair and allNodes[0] (controller.go:207-211) with its
-// allocatable, so K3 needs no dependent index chase.
+// piece range of the group's pair (empty when another rank owns the pair) and allNodes[0]
+// (controller.go:207-211, from the whole table on every rank) with its allocatable, so K3
+// needs no dependent index chase.
 struct GroupNode {
     int64_t first;             // lowest member node index (INT64_MAX: no member)
     int64_t first_cpu, first_mem;
@@ -124,6 +127,9 @@ struct NodeDev {
     // NODE_SPAN entries each (several small pieces, or one large), one wave per span
     const uint32_t* span_off;  // [n_spans + 1]
     int64_t n_pieces, pc_lo, pc_hi, n_spans;
+    // the group pairs this rank owns: their pieces [pc_lo, pc_hi) are its K2
+    // work, their groups' memberships its K5 age index; [0, n_gp) with one rank
+    uint32_t q_lo, q_hi;
 };
 
 // K2 output row per piece (int64 words, stored word-major: rows[word * n_pieces + piece]).
@@ -179,11 +185,13 @@ struct DecCompact;
 struct K1Diag {
     uint64_t* trace;
 };
-// k_node_groups' decision (one rank, or after the exchange): null dec = node words only.
+// k_node_groups' decision (one rank without an exchange): null dec = the node words only,
+// written as exchange words (NX_K per group) to nx for the SUM and k_decide.
 struct NGDecide {
     const int64_t* pwords;
     esc_group_decision* dec;
     DecCompact* cdec;
+    int64_t* nx;
 };
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, uint32_t* ticket, int cap, const K1Diag& diag,
@@ -205,8 +213,14 @@ static_assert(sizeof(DecCompact) == 32, "compact decision is 2 x 16 B");
 
 // K2b + K4 (k_node_groups): every group's final node words from K2's piece rows, then
 // (nd.dec != null) the decisions.  K4 alone (k_decide): after an exchange.
-hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords,
-                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st);
+// k_decide reads the exchanged pod words (pwords, G x PW_K) and node words (nx, G x NX_K)
+// and writes the final node words (nwords, G x NW_K, for esc_results) besides the decisions.
+hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords, const int64_t* nx,
+                         int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st);
+// Peer exchange of a multi-device context (esc_ctx_create_multi): dst[i] = sum of src[k][i]
+// over the n_src buffers (peer-mapped device memory), int64 or uint32 words.
+hipError_t launch_peer_sum64(const int64_t* const* src, int n_src, int64_t* dst, int64_t n, hipStream_t st);
+hipError_t launch_peer_sum32(const uint32_t* const* src, int n_src, uint32_t* dst, int64_t n, hipStream_t st);
 hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t* node_rows, int64_t* trk_acc,
                               int64_t* nwords, const NGDecide& nd, hipStream_t st);
 // K3 fold (a role of k_step_tail): the K1 partials of FC_COL pod slots per block.

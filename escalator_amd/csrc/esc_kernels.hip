@@ -55,13 +55,6 @@ __device__ __forceinline__ ulonglong2 ld2(const int64_t* p) {
 template <class T>
 __device__ __forceinline__ T ldnt(const T* p) { return __builtin_nontemporal_load(p); }
 
-__device__ __forceinline__ void lds_add(uint64_t* a, uint64_t v) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v);
-}
-__device__ __forceinline__ void g_add(int64_t* a, int64_t v) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v);
-}
-
 // Effective request of one pod — ComputePodResourceRequest, scheduler/types.go:72-89:
 // regular containers summed (Resource.Add, plain int64 += wraps), then max with every
 // init container (SetMaxResource; an absent key is INT64_MIN so max() ignores it),
@@ -953,15 +946,19 @@ __device__ __forceinline__ int node_class(const NodeDev& N, uint32_t f, int64_t 
 
 // Groups a node belongs to: NewNodeLabelFilterFunc (node_group.go:278) over its label
 // pairs, resolved through the node pair table (K5).
+// Only the groups of the pairs this rank owns (NodeDev q_lo / q_hi).
 template <class F>
 __device__ __forceinline__ void node_groups(const NodeDev& N, const GroupDev& G, uint32_t f, int64_t i,
                                             F&& emit) {
     if (f & ESC_NF_ABSENT) return;                   // a free / deleted slot is in no group
-    for_code(G, node_code(G, N.label0[i]), emit);
+    auto pair = [&](uint32_t q) {
+        if (q >= N.q_lo && q < N.q_hi) for_code(G, node_code(G, q), emit);
+    };
+    pair(N.label0[i]);
     const uint32_t nx = nf_xlbl(f);
     if (nx) {
         const uint32_t q = N.xl_off[i];
-        for (uint32_t k = 0; k < nx; ++k) for_code(G, node_code(G, N.xl[q + k]), emit);
+        for (uint32_t k = 0; k < nx; ++k) pair(N.xl[q + k]);
     }
 }
 
@@ -1069,11 +1066,12 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 // (controller.go:120-154) + CalculateNodesCapacityTotal(untainted) (util.go:41-51): wet
 // groups take the filterNodes classes, dry groups (controller.go:126-138) every member as
 // untainted (cordoned ones included) except the tracked members (K2's tracker sums, read
-// and reset here).  64 groups per block, the 4 waves split each group's pieces.  Every
-// rank reduces the whole node index, so these words are final (never exchanged).  With a
-// decision target (D.dec) the block then decides its groups (K4: the pod words are final —
-// this rank's fold, or the exchanged sums) and writes the compact records to the decision
-// buffer as one contiguous run.
+// and reset here).  64 groups per block, the 4 waves split each group's pieces.  A rank
+// reduces only the pieces of the pairs it owns, so a group's words are exact on its owner
+// and zero elsewhere.  With a decision target (D.dec: one rank, no exchange) the block then
+// decides its groups (K4 on this rank's fold) and writes the compact records to the
+// decision buffer as one contiguous run; otherwise it writes the words to the exchange
+// buffer (D.nx) and k_decide runs after the SUM.
 constexpr int NG_WAVES = 4;
 
 __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeDev N,
@@ -1147,15 +1145,23 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
         n_taint = (uint64_t)tr[TA_CNT];
         n_cord = 0;
     }
-    int64_t* nw = nwords + (int64_t)g * NW_K;
     const bool n_ok = ncpu >= (__int128)INT64_MIN && ncpu <= (__int128)INT64_MAX &&
                       nmem >= (__int128)INT64_MIN && nmem <= (__int128)INT64_MAX;
     const int64_t v[6] = {(int64_t)ncpu, (int64_t)nmem, (int64_t)n_unt, (int64_t)n_taint, (int64_t)n_cord,
                           n_ok ? 0 : ESC_TF_NODE_OVERFLOW};
     static_assert(NW_CPU == 0 && NW_MEM == 1 && NW_N_UNT == 2 && NW_N_TAINT == 3 && NW_N_CORD == 4 && NW_FLAGS == 5,
                   "node word order");
+    if (!D.dec) {                                    // exchange words: zero unless this rank owns the pair
+        int64_t* x = D.nx + (int64_t)g * NX_K;
+        x[NX_CPU] = v[0];
+        x[NX_MEM] = v[1];
+        x[NX_CNT] = (int64_t)((uint64_t)n_unt | ((uint64_t)n_taint << 32));
+        x[NX_CORD] = (int64_t)((uint64_t)n_cord | ((uint64_t)v[5] << 32));
+    } else {
+        int64_t* nw = nwords + (int64_t)g * NW_K;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) nw[k] = v[k];
+        for (int k = 0; k < 6; ++k) nw[k] = v[k];
+    }
     if (D.dec) {
         esc_group_decision d;
         finalize(G, N.gnode[g], g, D.pwords + (int64_t)g * PW_K, v, d, G.metrics);
@@ -1171,16 +1177,24 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
     }
 }
 
-// K4 alone (esc_decide after an exchange): the node words are this rank's (k_node_groups
-// ran in the step), the pod words the exchanged sums.
+// K4 alone (esc_decide after an exchange): the pod and node words are the exchanged sums
+// (the node words exact from their owner rank); the final node words are kept for
+// esc_results.
 __global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ pwords,
-                                                const int64_t* __restrict__ nwords,
+                                                const int64_t* __restrict__ nx, int64_t* __restrict__ nwords,
                                                 esc_group_decision* __restrict__ dec, DecCompact* __restrict__ cdec) {
     __shared__ DecCompact sc[256];
     const int32_t g0 = blockIdx.x * 256, g = g0 + (int32_t)threadIdx.x;
     if (g < G.G) {
+        const int64_t* x = nx + (int64_t)g * NX_K;
+        const uint64_t cnt = (uint64_t)x[NX_CNT], cf = (uint64_t)x[NX_CORD];
+        const int64_t v[NW_K] = {x[NX_CPU], x[NX_MEM], (int64_t)(cnt & 0xFFFFFFFFull), (int64_t)(cnt >> 32),
+                                 (int64_t)(cf & 0xFFFFFFFFull), (int64_t)(cf >> 32)};
+        int64_t* nw = nwords + (int64_t)g * NW_K;
+#pragma unroll
+        for (int k = 0; k < NW_K; ++k) nw[k] = v[k];
         esc_group_decision d;
-        finalize(G, N.gnode[g], g, pwords + (int64_t)g * PW_K, nwords + (int64_t)g * NW_K, d, G.metrics);
+        finalize(G, N.gnode[g], g, pwords + (int64_t)g * PW_K, v, d, G.metrics);
         store_full(dec + g, d);
         sc[threadIdx.x] = compact_of(d);
     }
@@ -2273,10 +2287,46 @@ hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t
     return hipGetLastError();
 }
 
-hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords,
-                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st) {
-    hipLaunchKernelGGL(k_decide, dim3((g.G + 255) / 256), dim3(256), 0, st, g, n, pwords, nwords, dec, cdec);
+hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords, const int64_t* nx,
+                         int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st) {
+    hipLaunchKernelGGL(k_decide, dim3((g.G + 255) / 256), dim3(256), 0, st, g, n, pwords, nx, nwords, dec, cdec);
     return hipGetLastError();
+}
+
+namespace {
+constexpr int PEER_MAX = 16;
+template <class T>
+struct PeerSrc {
+    const T* p[PEER_MAX];
+};
+// dst = the sum of every source buffer (the sources are other devices' memory, peer-mapped,
+// or the same device's): 16-B loads where the words allow, one pass.
+template <class T>
+__global__ __launch_bounds__(256) void k_peer_sum(PeerSrc<T> S, int n_src, T* __restrict__ dst, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        T a = 0;
+        for (int k = 0; k < n_src; ++k) a += S.p[k][i];
+        dst[i] = a;
+    }
+}
+template <class T>
+hipError_t peer_sum(const T* const* src, int n_src, T* dst, int64_t n, hipStream_t st) {
+    if (n_src < 1 || n_src > PEER_MAX) return hipErrorInvalidValue;
+    if (n <= 0) return hipSuccess;
+    PeerSrc<T> S{};
+    for (int k = 0; k < n_src; ++k) S.p[k] = src[k];
+    const unsigned blocks = (unsigned)std::min<int64_t>(1024, (n + 255) / 256);
+    hipLaunchKernelGGL(k_peer_sum<T>, dim3(blocks), dim3(256), 0, st, S, n_src, dst, n);
+    return hipGetLastError();
+}
+}  // namespace
+
+hipError_t launch_peer_sum64(const int64_t* const* src, int n_src, int64_t* dst, int64_t n, hipStream_t st) {
+    return peer_sum<int64_t>(src, n_src, dst, n, st);
+}
+hipError_t launch_peer_sum32(const uint32_t* const* src, int n_src, uint32_t* dst, int64_t n, hipStream_t st) {
+    return peer_sum<uint32_t>(src, n_src, dst, n, st);
 }
 
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,

@@ -15,11 +15,14 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <thread>
+#include <type_traits>
 #include <string>
 #include <vector>
 
 #include "esc_internal.h"
 #include "esc_kernels.h"
+#include "esc_multi.h"
 
 using namespace esc;
 
@@ -37,16 +40,6 @@ constexpr int MAX_STAGES = 8;
     } while (0)
 
 thread_local char g_last_error[256];
-
-int32_t fail_hip(hipError_t e, const char* what) {
-    std::snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, hipGetErrorString(e));
-    return e == hipErrorOutOfMemory ? ESC_E_NOMEM : ESC_E_HIP;
-}
-
-int32_t fail_comm(const char* what, const char* why) {
-    std::snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, why);
-    return ESC_E_COMM;
-}
 
 template <class T>
 hipError_t dalloc(T** p, size_t n) {
@@ -92,18 +85,18 @@ struct NodeBuf {
     }
 };
 
-// RCCL is resolved at first use: the copy already mapped into the process if there is one
-// (PyTorch-ROCm ships its own librccl, and two RCCL instances in one process would each
-// run their own proxy threads), else the system librccl.so.1.  Hosts that never exchange
-// (world 1, the per-function drop-ins) need no RCCL at all.
-struct RcclApi {
-    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
-    decltype(&ncclCommInitRank) init_rank = nullptr;
-    decltype(&ncclAllReduce) all_reduce = nullptr;
-    decltype(&ncclCommDestroy) destroy = nullptr;
-    decltype(&ncclGetErrorString) error_string = nullptr;
-    bool ok = false;
-};
+}  // namespace
+
+namespace esc {
+int32_t fail_hip(hipError_t e, const char* what) {
+    std::snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, hipGetErrorString(e));
+    return e == hipErrorOutOfMemory ? ESC_E_NOMEM : ESC_E_HIP;
+}
+
+int32_t fail_comm(const char* what, const char* why) {
+    std::snprintf(g_last_error, sizeof g_last_error, "%s: %s", what, why);
+    return ESC_E_COMM;
+}
 
 const RcclApi& rccl() {
     static const RcclApi api = [] {
@@ -114,16 +107,25 @@ const RcclApi& rccl() {
         if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
         if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
         if (!h) return a;
-        a.get_unique_id = reinterpret_cast<decltype(a.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
-        a.init_rank = reinterpret_cast<decltype(a.init_rank)>(dlsym(h, "ncclCommInitRank"));
-        a.all_reduce = reinterpret_cast<decltype(a.all_reduce)>(dlsym(h, "ncclAllReduce"));
-        a.destroy = reinterpret_cast<decltype(a.destroy)>(dlsym(h, "ncclCommDestroy"));
-        a.error_string = reinterpret_cast<decltype(a.error_string)>(dlsym(h, "ncclGetErrorString"));
-        a.ok = a.get_unique_id && a.init_rank && a.all_reduce && a.destroy && a.error_string;
+        auto sym = [&](auto& f, const char* name) { f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name)); };
+        sym(a.get_unique_id, "ncclGetUniqueId");
+        sym(a.init_rank, "ncclCommInitRank");
+        sym(a.init_all, "ncclCommInitAll");
+        sym(a.all_reduce, "ncclAllReduce");
+        sym(a.group_start, "ncclGroupStart");
+        sym(a.group_end, "ncclGroupEnd");
+        sym(a.count, "ncclCommCount");
+        sym(a.destroy, "ncclCommDestroy");
+        sym(a.error_string, "ncclGetErrorString");
+        a.ok = a.get_unique_id && a.init_rank && a.init_all && a.all_reduce && a.group_start && a.group_end && a.count &&
+               a.destroy && a.error_string;
         return a;
     }();
     return api;
 }
+}  // namespace esc
+
+namespace {
 
 int bit_width(uint64_t v) {
     int b = 0;
@@ -158,6 +160,9 @@ struct esc_ctx {
     int64_t n_entries = 0, n_pieces = 0, pc_lo = 0, pc_hi = 0, node_bytes = 0, n_spans = 0;
     int64_t ts_min = 0, ts_max = 0;
     bool nodes_loaded = false;
+    uint32_t q_lo = 0, q_hi = 0;                              // the group pairs this rank owns (§7)
+    std::vector<uint32_t> q_bounds;                           // every rank's first owned pair, + n_gp
+    std::vector<int64_t> pair_live;                           // group pair -> live node entries
     // work
     int nblk = 0;
     uint64_t* d_pod_part = nullptr;
@@ -170,7 +175,7 @@ struct esc_ctx {
     int k1_cap = 0;                                           // K1 chunks per workgroup at most (0: static)
     uint64_t* d_k1_trace = nullptr;                           // K1 per-workgroup timestamps (esc_k1_trace)
     int64_t* d_trk_acc = nullptr;                             // [G][TA_K] dry-mode tracked sums
-    int64_t* d_pwords = nullptr;                              // active exchange buffer [G][PW_K]
+    int64_t* d_pwords = nullptr;                              // active exchange buffer [G][PW_K] + [G][NX_K]
     int64_t* own_pwords = nullptr;                            // the context-owned one
     int64_t* d_nwords = nullptr;                              // [G][NW_K] rank-local node words
     esc_group_decision* d_dec = nullptr;                     // full records (device)
@@ -213,6 +218,7 @@ struct esc_ctx {
     OrdChunk* d_pchunks = nullptr;                            // packed chunks of small groups
     int64_t n_pchunks = 0, n_psmall = 0;                      // all / those <= ORD_PCHUNK (first)
     std::vector<uint32_t> h_pstart, h_plen;                   // group regions: start, memberships
+    std::vector<uint32_t> h_pcap;                             // every group's region capacity (owned or not)
     std::vector<uint32_t> h_gch_off;                          // group -> its split chunks (big groups)
     int64_t n_gpad = 0;                                       // padded group-order length
     OrdChunk* d_chunks = nullptr;
@@ -230,7 +236,6 @@ struct esc_ctx {
     std::vector<int64_t> h_created;                           // [lo, hi) creation times (tie order)
     // node informer events (§8f rank 1): capacity and host mirrors for in-place add / delete
     int64_t n_cap = 0, xl_used = 0, xl_cap = 0, age_n = -1;
-    bool tail_owner = true;                                   // this rank's K5 range ends at the table's end
     std::vector<uint32_t> h_label0, h_xl_off, h_xl;           // node labels (pair ids)
     std::vector<uint32_t> h_e_node;                           // pair-major entry -> node (NONE: spare)
     std::vector<uint32_t> pair_next, pair_end;                // group pair -> next spare entry, range end
@@ -239,6 +244,9 @@ struct esc_ctx {
     std::vector<uint32_t> h_gn;                               // group regions' nodes (lazy mirror of d_g_node)
     // per-function drop-ins run on a one-group list context
     esc_ctx* list_ctx = nullptr;
+    // single-process multi-device context (esc_ctx_create_multi): every call dispatches to
+    // its per-device contexts (esc_multi.hip); null for a per-device context
+    esc::esc_multi_state* multi = nullptr;
     // incremental snapshot (§8f rank 1): where each loaded pod lives, free K slots
     double spare_frac = 0.0;                                  // esc_set_spare
     std::vector<int32_t> pod_cls;                             // by pod id: K class index, -1 C, -2 absent
@@ -280,6 +288,10 @@ struct esc_ctx {
 
 namespace esc {
 const GroupIndex* ctx_group_index(const esc_ctx* ctx) { return &ctx->gi; }
+esc_multi_state* ctx_multi(const esc_ctx* c) { return c->multi; }
+void ctx_set_multi(esc_ctx* c, esc_multi_state* m) { c->multi = m; }
+hipStream_t ctx_stream(const esc_ctx* c) { return c->stream; }
+int ctx_device(const esc_ctx* c) { return c->device; }
 }
 
 namespace {
@@ -287,6 +299,11 @@ namespace {
 // K1 partial row stride: the pod slots (one per group pair + the default filter's)
 // rounded up to whole K3 columns.
 int64_t slot_stride(const esc_ctx* c) { return ((int64_t)c->gi.n_gp + 1 + FC_COL - 1) / FC_COL * FC_COL; }
+
+// The exchange buffer (SUM across ranks): the pods' words [G][PW_K], then the node words
+// [G][NX_K].
+constexpr int XW_K = PW_K + NX_K;
+int64_t* node_xwords(const esc_ctx* c) { return c->d_pwords + (int64_t)c->gi.G * PW_K; }
 
 GroupDev group_dev(const esc_ctx* c) {
     GroupDev g;
@@ -333,6 +350,7 @@ NodeDev node_dev(const esc_ctx* c) {
     n.piece_off = c->nodes.piece_off; n.piece_pair = c->nodes.piece_pair; n.pp_off = c->nodes.pp_off;
     n.n_pieces = c->n_pieces; n.pc_lo = c->pc_lo; n.pc_hi = c->pc_hi;
     n.span_off = c->nodes.span_off; n.n_spans = c->n_spans;
+    n.q_lo = c->q_lo; n.q_hi = c->q_hi;
     return n;
 }
 
@@ -494,12 +512,23 @@ int32_t build_age_index(esc_ctx* c) {
     // every group's region: its memberships (oldest first), then padding to whole quads plus
     // the spare slots node additions take (esc_set_spare); the per-decision output uses the
     // same positions (grp_off = region starts)
-    std::vector<uint32_t> gch_off(g.G + 1), pstart(g.G + 1, 0), plen(std::max<int32_t>(g.G, 1), 0);
+    // Every group's length and capacity come from the host's live entry counts, identically on
+    // every rank (node additions check the capacity of every group they touch, owned or not,
+    // so that all ranks accept or refuse a batch alike); only the groups of the
+    // pairs this rank owns get a device region.
+    std::vector<uint32_t> gch_off(g.G + 1), pstart(g.G + 1, 0), plen(std::max<int32_t>(g.G, 1), 0),
+        pcap(std::max<int32_t>(g.G, 1), 0);
     for (int32_t q = 0; q < g.G; ++q) {
-        const int64_t len = starts[q + 1] - starts[q];
+        const uint32_t gp = c->gi.gpair[q];
+        const bool own = gp >= c->q_lo && gp < c->q_hi;
+        const int64_t len = c->pair_live[gp];
+        if (starts[q + 1] - starts[q] != (own ? len : 0)) return fail_hip(hipErrorUnknown, "age index: membership count");
         const int64_t spare = c->spare_frac > 0 ? (int64_t)std::ceil((double)len * c->spare_frac) + 4 : 0;
+        const int64_t cap = (len + spare + 3) & ~(int64_t)3;
+        if (cap >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
         plen[q] = (uint32_t)len;
-        const int64_t reg = (len + spare + 3) & ~(int64_t)3;
+        pcap[q] = (uint32_t)cap;
+        const int64_t reg = own ? cap : 0;
         if ((int64_t)pstart[q] + reg >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
         pstart[q + 1] = pstart[q] + (uint32_t)reg;
     }
@@ -608,6 +637,7 @@ int32_t build_age_index(esc_ctx* c) {
     }
     c->h_pstart.swap(pstart);
     c->h_plen.swap(plen);
+    c->h_pcap.swap(pcap);
     c->h_gch_off.swap(gch_off);
     c->sorted = false;
     return ESC_OK;
@@ -710,6 +740,46 @@ std::vector<int64_t> plan_k1(const std::vector<PodClass>& cls, int64_t W, int64_
     return seg;
 }
 
+// The group pairs [lo, hi) rank `rank` of `world` owns: pair q (weight =
+// its node entries + OWN_PAD, for the per-pair work that does not scale with entries) goes
+// to rank floor(S_q * world / W), S_q the weight of the pairs before q and W the total —
+// contiguous ranges in pair order, balanced by weight, computed from the whole table, so
+// every rank derives the same split (escalator_amd/layout.py owner_ranges restates it).
+constexpr int64_t OWN_PAD = 64;
+void owned_pairs(const std::vector<int64_t>& cnt, int32_t world, int32_t rank, uint32_t& lo, uint32_t& hi) {
+    const uint32_t n = (uint32_t)cnt.size();
+    lo = 0;
+    hi = n;
+    if (world <= 1) return;
+    __int128 W = 0;
+    for (int64_t x : cnt) W += x + OWN_PAD;
+    __int128 S = 0;
+    lo = hi = n;
+    bool have_lo = false;
+    for (uint32_t q = 0; q < n; ++q) {
+        const int64_t r = (int64_t)(S * world / W);
+        if (!have_lo && r >= rank) { lo = q; have_lo = true; }
+        if (r >= (int64_t)rank + 1) { hi = q; break; }
+        S += cnt[q] + OWN_PAD;
+    }
+    if (!have_lo) lo = hi;
+}
+
+// Live node entries per group pair of a packed node table (the weights of owned_pairs).
+std::vector<int64_t> pair_counts(const esc_ctx* c, const esc_node_soa* s) {
+    const uint32_t n_gp = c->gi.n_gp;
+    std::vector<int64_t> cnt(n_gp, 0);
+    int64_t x = 0;
+    for (int64_t i = 0; i < s->n_nodes; ++i) {
+        if (s->label0[i] < n_gp) ++cnt[s->label0[i]];
+        const uint32_t nx = nf_xlbl(s->flags[i]);
+        for (uint32_t k = 0; k < nx; ++k)
+            if (s->xl_pair[x + k] < n_gp) ++cnt[s->xl_pair[x + k]];
+        x += nx;
+    }
+    return cnt;
+}
+
 // Pod accumulator slots: one per group pair + one for the default filter.
 int64_t pod_slots(const esc_ctx* c) { return (int64_t)c->gi.n_gp + 1; }
 
@@ -766,7 +836,7 @@ int32_t ensure_work(esc_ctx* c) {
     HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)S * WP_K * sizeof(int64_t)));
     HIP_TRY(dalloc(&c->d_trk_acc, (size_t)G * TA_K));
     HIP_TRY(hipMemset(c->d_trk_acc, 0, (size_t)G * TA_K * sizeof(int64_t)));
-    HIP_TRY(dalloc(&c->own_pwords, (size_t)G * PW_K));
+    HIP_TRY(dalloc(&c->own_pwords, (size_t)G * XW_K));
     HIP_TRY(dalloc(&c->d_nwords, (size_t)G * NW_K));
     c->d_pwords = c->bound_pwords ? c->bound_pwords : c->own_pwords;
     HIP_TRY(dalloc(&c->d_dec, (size_t)G));
@@ -841,8 +911,8 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     if (int32_t rc = mark()) return rc;
     // D reads and resets the tracker sums the tail accumulated (once per step); a sharded
     // step (no decide) computes the node words only and esc_decide runs K4 after the exchange
-    NGDecide nd{};
-    if (decide) nd = NGDecide{c->d_pwords, c->d_dec, cdec};
+    NGDecide nd{nullptr, nullptr, nullptr, node_xwords(c)};
+    if (decide) nd = NGDecide{c->d_pwords, c->d_dec, cdec, nullptr};
     HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, nd, st));
     if (int32_t rc = mark()) return rc;
     if (copy_out && !c->zero_copy) {
@@ -857,6 +927,7 @@ int32_t check_ready(esc_ctx* c) {
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
+    hipSetDevice(c->device);          // a multi-device host drives several contexts from one thread
     return ensure_work(c);
 }
 
@@ -986,6 +1057,7 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
 
 int32_t esc_ctx_destroy(esc_ctx* c) {
     if (!c) return ESC_OK;
+    if (c->multi) esc::multi_destroy(c);                    // the devices' contexts and communicators
     if (c->list_ctx) esc_ctx_destroy(c->list_ctx);
     if (c->has_device) {
         hipSetDevice(c->device);
@@ -1009,6 +1081,7 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
 }
 
 int32_t esc_ctx_set_stream(esc_ctx* c, void* hip_stream) {
+    if (c && c->multi) return ESC_E_STATE;              // the devices' contexts own their streams
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     hipSetDevice(c->device);
@@ -1035,12 +1108,14 @@ uint32_t esc_ctx_pair_id(const esc_ctx* c, const char* key, const char* value) {
 int32_t esc_ctx_num_group_pairs(const esc_ctx* c) { return c ? (int32_t)c->gi.n_gp : 0; }
 
 int32_t esc_set_replicas(esc_ctx* c, int32_t n) {
+    if (c && c->multi) return esc::multi_set_replicas(c, n);
     if (!c || n < 1 || n > 64) return ESC_E_INVAL;
     c->n_replicas = n;              // applies from the next esc_load_pods
     return ESC_OK;
 }
 
 int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
+    if (c && c->multi) return esc::multi_load_pods(c, p, global_offset);
     if (!c || !p || p->n_pods < 0) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     const int64_t n = p->n_pods;
@@ -1255,7 +1330,9 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
 }
 
 int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi) {
-    if (!c || !s || s->n_nodes < 0 || lo < 0 || hi < lo || hi > s->n_nodes) return ESC_E_INVAL;
+    if (c && c->multi) return esc::multi_load_nodes(c, s, lo, hi);
+    // every rank holds the whole table; its share is the pairs it owns
+    if (!c || !s || s->n_nodes < 0 || lo != 0 || hi != s->n_nodes) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     const int64_t n = s->n_nodes;
     if (n >= (int64_t)0x7FFFFFFF) return ESC_E_LIMIT;
@@ -1358,10 +1435,14 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     std::vector<uint32_t> pp_off((size_t)n_gp + 1);
     for (uint32_t q = 0; q <= n_gp; ++q)
         pp_off[q] = (uint32_t)(std::lower_bound(piece_pair.begin(), piece_pair.end(), q) - piece_pair.begin());
-    // Every rank reduces the whole index: the node words then need no
-    // exchange and only the pods' per-group words cross xGMI.  The node table is resident
-    // on every rank anyway (K5 orders its [lo, hi) share; allNodes[0] is global).
-    const int64_t pc_lo = 0, pc_hi = n_pieces;
+    // This rank's share of the index: the pieces of the group pairs it owns, a
+    // contiguous pair range balanced by entry count, the same split on every rank.  Its K2
+    // streams only those, its node words are exact for those groups and zero for the others
+    // (the SUM exchange carries them), and its K5 orders those groups.  The whole table stays
+    // resident on every rank: allNodes[0] and the reaping read it.
+    uint32_t q_lo = 0, q_hi = n_gp;
+    owned_pairs(pair_cnt, c->world, c->rank, q_lo, q_hi);
+    const int64_t pc_lo = pp_off[q_lo], pc_hi = pp_off[q_hi];
     int64_t node_bytes = 0;                          // algorithmic bytes K2 streams per decision
     for (int64_t p = pc_lo; p < pc_hi; ++p) {
         node_bytes += 8;                             // piece_pair + piece_off
@@ -1484,7 +1565,15 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     c->n_cap = n_cap;
     c->xl_used = s->n_xl;
     c->xl_cap = xl_cap;
-    c->tail_owner = hi == n;
+    c->q_lo = q_lo;
+    c->q_hi = q_hi;
+    c->q_bounds.assign((size_t)c->world + 1, n_gp);
+    for (int32_t r = 0; r < c->world; ++r) {
+        uint32_t a = 0, b = 0;
+        owned_pairs(pair_cnt, c->world, r, a, b);
+        c->q_bounds[r] = a;
+    }
+    c->pair_live = pair_cnt;
     c->h_gn.clear();
     c->n_entries = E;
     c->n_pieces = n_pieces;
@@ -1508,6 +1597,7 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
 }
 
 int32_t esc_stream_bytes(const esc_ctx* c, int64_t* pod_bytes, int64_t* node_bytes) {
+    if (c && c->multi) return esc::multi_stream_bytes(c, pod_bytes, node_bytes);
     if (!c || !pod_bytes || !node_bytes) return ESC_E_INVAL;
     if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
     // K1: flags 4 + cpu0 4 + mem0 8 + pair0 4 per pod, 16 per extra container record,
@@ -1518,6 +1608,7 @@ int32_t esc_stream_bytes(const esc_ctx* c, int64_t* pod_bytes, int64_t* node_byt
 }
 
 int32_t esc_set_state(esc_ctx* c, const esc_group_state* st) {
+    if (c && c->multi) return esc::multi_set_state(c, st);
     if (!c) return ESC_E_INVAL;
     for (int32_t g = 0; g < c->gi.G; ++g) params_from(c->params[g], c->gi.groups[g].spec, st ? st + g : nullptr);
     if (!c->has_device) return ESC_OK;
@@ -1529,6 +1620,7 @@ int32_t esc_set_state(esc_ctx* c, const esc_group_state* st) {
 }
 
 int32_t esc_set_metrics(esc_ctx* c, int32_t enable) {
+    if (c && c->multi) return esc::multi_each(c, esc_set_metrics, enable);
     if (!c) return ESC_E_INVAL;
     c->want_metrics = enable != 0;
     drop_graphs(c);
@@ -1536,6 +1628,7 @@ int32_t esc_set_metrics(esc_ctx* c, int32_t enable) {
 }
 
 int32_t esc_metrics_results(esc_ctx* c, esc_group_metrics* out) {
+    if (c && c->multi) return esc_metrics_results(esc::multi_sub(c, 0), out);
     if (!c || !out) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->work_ready || !c->want_metrics) return ESC_E_STATE;
@@ -1546,6 +1639,7 @@ int32_t esc_metrics_results(esc_ctx* c, esc_group_metrics* out) {
 }
 
 int32_t esc_use_graph(esc_ctx* c, int32_t enable) {
+    if (c && c->multi) return esc::multi_each(c, esc_use_graph, enable);
     if (!c) return ESC_E_INVAL;
     c->use_graph = enable != 0;
     if (!c->use_graph) drop_graphs(c);
@@ -1553,6 +1647,7 @@ int32_t esc_use_graph(esc_ctx* c, int32_t enable) {
 }
 
 int32_t esc_force_wide(esc_ctx* c, int32_t enable) {
+    if (c && c->multi) return esc::multi_each(c, esc_force_wide, enable);
     if (!c) return ESC_E_INVAL;
     c->force_wide = enable != 0;
     drop_graphs(c);
@@ -1560,6 +1655,7 @@ int32_t esc_force_wide(esc_ctx* c, int32_t enable) {
 }
 
 int32_t esc_set_timing(esc_ctx* c, int32_t enable) {
+    if (c && c->multi) return esc::multi_each(c, esc_set_timing, enable);
     if (!c) return ESC_E_INVAL;
     c->timing = enable != 0;
     drop_graphs(c);
@@ -1567,6 +1663,7 @@ int32_t esc_set_timing(esc_ctx* c, int32_t enable) {
 }
 
 int32_t esc_stage_times(esc_ctx* c, double* ms, int32_t n) {
+    if (c && c->multi) return esc_stage_times(esc::multi_sub(c, 0), ms, n);
     if (!c || !ms || n <= 0) return ESC_E_INVAL;
     for (int i = 0; i < n && i < MAX_STAGES; ++i) ms[i] = c->stage_ms[i];
     return ESC_OK;
@@ -1584,6 +1681,7 @@ int32_t esc_stage_times(esc_ctx* c, double* ms, int32_t n) {
 // do not change, and sums are order-independent, so every result is unchanged; the graphs
 // read the plan from device memory, so they stay valid.
 int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
+    if (c && c->multi) return esc::multi_k1_calibrate(c, rounds);
     int32_t rc = check_ready(c);
     if (rc) return rc;
     if (rounds < 0) return ESC_E_INVAL;
@@ -1637,15 +1735,18 @@ int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
 }
 
 int32_t esc_k1_trace(esc_ctx* c, uint64_t* out, int64_t cap, int64_t* n_out) {
+    if (c && c->multi) return esc_k1_trace(esc::multi_sub(c, 0), out, cap, n_out);
     if (!c || !n_out || cap < 0 || (cap > 0 && !out)) return ESC_E_INVAL;
     if (!c->d_k1_trace) return ESC_E_STATE;
     *n_out = c->nblk;
+    hipSetDevice(c->device);
     const int64_t w = std::min<int64_t>(cap, (int64_t)c->nblk * 8);
     if (w > 0) HIP_TRY(hipMemcpy(out, c->d_k1_trace, (size_t)w * 8, hipMemcpyDeviceToHost));
     return ESC_OK;
 }
 
 int32_t esc_reduce(esc_ctx* c) {
+    if (c && c->multi) return ESC_E_STATE;             // the exchange is internal: esc_step
     int32_t rc = check_ready(c);
     if (rc) return rc;
     hipSetDevice(c->device);
@@ -1659,11 +1760,12 @@ int32_t esc_reduce(esc_ctx* c) {
 }
 
 int32_t esc_exchange_buffers(esc_ctx* c, void** sum_buf, int64_t* sum_count, void** min_buf, int64_t* min_count) {
+    if (c && c->multi) return ESC_E_STATE;
     int32_t rc = check_ready(c);
     if (rc) return rc;
     if (sum_buf) *sum_buf = c->d_pwords;
-    if (sum_count) *sum_count = (int64_t)c->gi.G * PW_K;
-    // allNodes[0] is resolved from the pair-major index every rank holds in full, so the
+    if (sum_count) *sum_count = (int64_t)c->gi.G * XW_K;
+    // allNodes[0] is resolved from the whole node table every rank holds, so the
     // first-member words need no MIN exchange in this build
     if (min_buf) *min_buf = nullptr;
     if (min_count) *min_count = 0;
@@ -1671,6 +1773,7 @@ int32_t esc_exchange_buffers(esc_ctx* c, void** sum_buf, int64_t* sum_count, voi
 }
 
 int32_t esc_bind_exchange_buffers(esc_ctx* c, void* sum_buf, void* min_buf) {
+    if (c && c->multi) return ESC_E_STATE;
     if (!c || (!sum_buf && min_buf)) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (min_buf) return ESC_E_INVAL;                  // min_count is 0: nothing to MIN-exchange
@@ -1681,33 +1784,36 @@ int32_t esc_bind_exchange_buffers(esc_ctx* c, void* sum_buf, void* min_buf) {
 }
 
 int32_t esc_exchange_download(esc_ctx* c, int64_t* sum_out, int64_t* min_out) {
+    if (c && c->multi) return ESC_E_STATE;
     int32_t rc = check_ready(c);
     if (rc) return rc;
     if (!sum_out) return ESC_E_INVAL;
     (void)min_out;                                   // min_count is 0: nothing to MIN-exchange
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(sum_out, c->d_pwords, (size_t)c->gi.G * PW_K * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(sum_out, c->d_pwords, (size_t)c->gi.G * XW_K * 8, hipMemcpyDeviceToHost));
     return ESC_OK;
 }
 
 int32_t esc_exchange_upload(esc_ctx* c, const int64_t* sum_in, const int64_t* min_in) {
+    if (c && c->multi) return ESC_E_STATE;
     int32_t rc = check_ready(c);
     if (rc) return rc;
     if (!sum_in) return ESC_E_INVAL;
     (void)min_in;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(c->d_pwords, sum_in, (size_t)c->gi.G * PW_K * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_pwords, sum_in, (size_t)c->gi.G * XW_K * 8, hipMemcpyHostToDevice));
     return ESC_OK;
 }
 
 int32_t esc_decide(esc_ctx* c) {
+    if (c && c->multi) return ESC_E_STATE;
     int32_t rc = check_ready(c);
     if (rc) return rc;
     hipSetDevice(c->device);
-    // K4 over the (exchanged) pod words and this rank's node words (computed in the step)
-    HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_pwords, c->d_nwords, c->d_dec,
+    // K4 over the exchanged pod and node words
+    HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_pwords, node_xwords(c), c->d_nwords, c->d_dec,
                           c->zero_copy ? c->h_cdec_dev : c->d_cdec, c->stream));
     if (!c->zero_copy)
         HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)c->gi.G * sizeof(DecCompact), hipMemcpyDeviceToHost,
@@ -1717,6 +1823,7 @@ int32_t esc_decide(esc_ctx* c) {
 }
 
 int32_t esc_run(esc_ctx* c) {
+    if (c && c->multi) return esc::multi_step(c);
     int32_t rc = check_ready(c);
     if (rc) return rc;
     if (c->world != 1) return ESC_E_STATE;            // multi-rank: reduce, exchange, decide
@@ -1733,6 +1840,7 @@ int32_t esc_run(esc_ctx* c) {
 }
 
 int32_t esc_set_order_in_step(esc_ctx* c, int32_t enable) {
+    if (c && c->multi) return esc::multi_each(c, esc_set_order_in_step, enable);
     if (!c) return ESC_E_INVAL;
     c->order_in_step = enable != 0;
     drop_graphs(c);
@@ -1752,6 +1860,7 @@ int32_t esc_comm_unique_id(void* id_out) {
 }
 
 int32_t esc_comm_init(esc_ctx* c, const void* id, int32_t rank, int32_t world) {
+    if (c && c->multi) return ESC_E_STATE;              // esc_ctx_create_multi made its communicators
     if (!c || !id) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (rank != c->rank || world != c->world || c->comm) return ESC_E_STATE;
@@ -1767,12 +1876,14 @@ int32_t esc_comm_init(esc_ctx* c, const void* id, int32_t rank, int32_t world) {
 }
 
 int32_t esc_exchange(esc_ctx* c) {
+    if (c && c->multi) return ESC_E_STATE;
     int32_t rc = check_ready(c);
     if (rc) return rc;
     if (!c->comm) return ESC_E_STATE;
     hipSetDevice(c->device);
-    // int64 SUM is exact in any order: the words are split lo32 / hi
-    const ncclResult_t r = rccl().all_reduce(c->d_pwords, c->d_pwords, (size_t)c->gi.G * PW_K, ncclInt64, ncclSum,
+    // int64 SUM is exact in any order: the pod words are split lo32 / hi, the node words are
+    // non-zero on their owner rank only
+    const ncclResult_t r = rccl().all_reduce(c->d_pwords, c->d_pwords, (size_t)c->gi.G * XW_K, ncclInt64, ncclSum,
                                              reinterpret_cast<ncclComm_t>(c->comm), c->stream);
     if (r != ncclSuccess) return fail_comm("ncclAllReduce", rccl().error_string(r));
     c->pending = true;
@@ -1780,6 +1891,7 @@ int32_t esc_exchange(esc_ctx* c) {
 }
 
 int32_t esc_step(esc_ctx* c) {
+    if (c && c->multi) return esc::multi_step(c);
     int32_t rc = check_ready(c);
     if (rc) return rc;
     if (!c->comm) return c->world == 1 ? esc_run(c) : ESC_E_STATE;
@@ -1789,6 +1901,7 @@ int32_t esc_step(esc_ctx* c) {
 }
 
 int32_t esc_sync(esc_ctx* c) {
+    if (c && c->multi) return esc::multi_sync(c);
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     hipSetDevice(c->device);
@@ -1807,6 +1920,7 @@ int32_t esc_sync(esc_ctx* c) {
 }
 
 int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* decisions) {
+    if (c && c->multi) return esc::multi_results(c, totals, decisions);
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->work_ready) return ESC_E_STATE;
@@ -2089,6 +2203,12 @@ uint32_t memb_flags(const esc_ctx* c, int64_t j, uint32_t mb) {
 
 int64_t created_of(const esc_ctx* c, uint32_t j) { return c->h_created[(int64_t)j - c->node_lo]; }
 
+// Does this rank own group g's node side (its pair in [q_lo, q_hi))?
+bool owns_group(const esc_ctx* c, uint32_t g) {
+    const uint32_t q = c->gi.gpair[g];
+    return q >= c->q_lo && q < c->q_hi;
+}
+
 // Host mirror of the regions' node ids (fetched once, then kept in step with every patch).
 int32_t ensure_gn(esc_ctx* c) {
     if ((int64_t)c->h_gn.size() == c->n_gpad) return ESC_OK;
@@ -2132,7 +2252,6 @@ int32_t patch_regions(esc_ctx* c, const std::vector<int64_t>& ids) {
     Patches P;
     std::vector<uint32_t> mb;
     for (int64_t j : ids) {
-        if (j < c->node_lo || j >= c->node_hi) continue;            // outside this rank's K5 range
         const bool gone = (c->h_nflags[j] & ESC_NF_ABSENT) != 0;
         if (gone) {                                                   // the memberships it had
             uint32_t f = c->h_nflags[j];
@@ -2143,6 +2262,7 @@ int32_t patch_regions(esc_ctx* c, const std::vector<int64_t>& ids) {
             node_membs(c, j, mb);
         }
         for (uint32_t m : mb) {
+            if (!owns_group(c, m & NODE_GROUP_MASK)) continue;          // another rank's K5 region
             const int64_t pos = region_pos(c, m & NODE_GROUP_MASK, (uint32_t)j);
             if (pos < 0) return ESC_E_HIP;                            // mirror out of step: never expected
             P.add(0, pos, gone ? ESC_NF_ABSENT : memb_flags(c, j, m));
@@ -2224,12 +2344,23 @@ int32_t write_tracker(esc_ctx* c, std::vector<uint64_t>& next) {
 extern "C" {
 
 int32_t esc_set_spare(esc_ctx* c, double fraction) {
+    if (c && c->multi) { for (int i = 0; esc::multi_sub(c, i); ++i) if (int32_t rc = esc_set_spare(esc::multi_sub(c, i), fraction)) return rc; return ESC_OK; }
     if (!c || !(fraction >= 0.0) || fraction > 4.0) return ESC_E_INVAL;
     c->spare_frac = fraction;                      // applies from the next esc_load_pods
     return ESC_OK;
 }
 
-int32_t esc_pods_upsert(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
+}  // extern "C"
+
+namespace {
+// esc_pods_upsert in two phases, so that a multi-device context can check every device's
+// share of a batch before it applies any (all or nothing across devices too).
+struct UpsertPlan {
+    std::vector<int64_t> rof, pof;   // each pod's first record / extra pair in the batch
+    std::vector<int32_t> tgt;        // its K class
+};
+
+int32_t upsert_plan(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, UpsertPlan& u) {
     if (!c || !p || p->n_pods < 0 || (p->n_pods > 0 && (!ids || !p->flags || !p->cpu0 || !p->mem0 || !p->pair0)))
         return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
@@ -2267,6 +2398,17 @@ int32_t esc_pods_upsert(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
     }
     for (size_t ci = 0; ci < need.size(); ++ci)
         if (need[ci] > (int64_t)c->cls_free[ci].size()) return ESC_E_LIMIT;   // spare exhausted: reload
+    u.rof.swap(rof);
+    u.pof.swap(pof);
+    u.tgt.swap(tgt);
+    return ESC_OK;
+}
+
+int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const UpsertPlan& u) {
+    const int64_t n = p->n_pods;
+    const std::vector<int64_t>& rof = u.rof;
+    const std::vector<int64_t>& pof = u.pof;
+    const std::vector<int32_t>& tgt = u.tgt;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->rm_valid = false;
@@ -2315,7 +2457,52 @@ int32_t esc_pods_upsert(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
     return sync_placement(c, touched, runs);
 }
 
+// esc_pods_bind's checks (ids, nodes, room in the runs) without applying anything.
+int32_t bind_check(esc_ctx* c, const int64_t* ids, const uint32_t* pod_node, int64_t n) {
+    if (!c || n < 0 || (n > 0 && (!ids || !pod_node))) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->placed) return ESC_E_STATE;
+    std::vector<int64_t> seen(ids, ids + n);
+    std::sort(seen.begin(), seen.end());
+    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) return ESC_E_INVAL;
+    std::unordered_map<uint32_t, int64_t> need;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t id = ids[i];
+        if (id < 0 || id >= (int64_t)c->pod_cls.size() || c->pod_cls[id] == -2) return ESC_E_INVAL;
+        if (pod_node[i] != NONE && ((int64_t)pod_node[i] >= c->n_nodes || (c->h_nflags[pod_node[i]] & ESC_NF_ABSENT)))
+            return ESC_E_INVAL;
+        const uint32_t old = id < (int64_t)c->h_pod_node.size() ? c->h_pod_node[id] : NONE;
+        if (old != NONE) --need[old];
+        if (pod_node[i] != NONE) ++need[pod_node[i]];
+    }
+    for (const auto& kv : need)
+        if (kv.second > 0 && c->h_run_len[kv.first] + kv.second > c->h_run_off[kv.first + 1] - c->h_run_off[kv.first])
+            return ESC_E_LIMIT;
+    return ESC_OK;
+}
+}  // namespace
+
+namespace esc {
+int32_t pods_upsert_check(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
+    UpsertPlan u;
+    return upsert_plan(c, ids, p, u);
+}
+int32_t pods_bind_check(esc_ctx* c, const int64_t* ids, const uint32_t* pod_node, int64_t n) {
+    return bind_check(c, ids, pod_node, n);
+}
+}  // namespace esc
+
+extern "C" {
+
+int32_t esc_pods_upsert(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
+    if (c && c->multi) return multi_pods_upsert(c, ids, p);
+    UpsertPlan u;
+    const int32_t rc = upsert_plan(c, ids, p, u);
+    return rc ? rc : upsert_apply(c, ids, p, u);
+}
+
 int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
+    if (c && c->multi) return esc::multi_pods_delete(c, ids, n);
     if (!c || n < 0 || (n > 0 && !ids)) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->pods_loaded) return ESC_E_STATE;
@@ -2341,25 +2528,8 @@ int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
 // builds the same map per decision).  NONE = unbound.  All or nothing: ESC_E_LIMIT when a
 // node's run has no room left (esc_load_placement again).
 int32_t esc_pods_bind(esc_ctx* c, const int64_t* ids, const uint32_t* pod_node, int64_t n) {
-    if (!c || n < 0 || (n > 0 && (!ids || !pod_node))) return ESC_E_INVAL;
-    if (!c->has_device) return ESC_E_NODEV;
-    if (!c->placed) return ESC_E_STATE;
-    std::vector<int64_t> seen(ids, ids + n);
-    std::sort(seen.begin(), seen.end());
-    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) return ESC_E_INVAL;
-    std::unordered_map<uint32_t, int64_t> need;
-    for (int64_t i = 0; i < n; ++i) {
-        const int64_t id = ids[i];
-        if (id < 0 || id >= (int64_t)c->pod_cls.size() || c->pod_cls[id] == -2) return ESC_E_INVAL;
-        if (pod_node[i] != NONE && ((int64_t)pod_node[i] >= c->n_nodes || (c->h_nflags[pod_node[i]] & ESC_NF_ABSENT)))
-            return ESC_E_INVAL;
-        const uint32_t old = id < (int64_t)c->h_pod_node.size() ? c->h_pod_node[id] : NONE;
-        if (old != NONE) --need[old];
-        if (pod_node[i] != NONE) ++need[pod_node[i]];
-    }
-    for (const auto& kv : need)
-        if (kv.second > 0 && c->h_run_len[kv.first] + kv.second > c->h_run_off[kv.first + 1] - c->h_run_off[kv.first])
-            return ESC_E_LIMIT;
+    if (c && c->multi) return multi_pods_bind(c, ids, pod_node, n);
+    if (int32_t rc = bind_check(c, ids, pod_node, n)) return rc;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     if ((int64_t)c->h_pod_node.size() < (int64_t)c->pod_cls.size()) {
@@ -2376,6 +2546,7 @@ int32_t esc_pods_bind(esc_ctx* c, const int64_t* ids, const uint32_t* pod_node, 
 
 int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32_t* flags, const int64_t* cpu,
                          const int64_t* mem) {
+    if (c && c->multi) return esc::multi_nodes_update(c, ids, n, flags, cpu, mem);
     if (!c || n < 0 || (n > 0 && (!ids || !flags || !cpu || !mem))) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->nodes_loaded) return ESC_E_STATE;
@@ -2405,6 +2576,7 @@ int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32
 // counts it) and its tracker entries are dropped.  All or nothing: ESC_E_LIMIT when the
 // spare room (esc_set_spare before esc_load_nodes) does not hold the batch.
 int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
+    if (c && c->multi) return esc::multi_nodes_add(c, s, ids_out);
     if (!c || !s || s->n_nodes < 0 || (s->n_nodes > 0 && (!ids_out || !s->flags || !s->label0 || !s->cpu || !s->mem ||
                                                           !s->created_ns)))
         return ESC_E_INVAL;
@@ -2446,9 +2618,11 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
         if (need_e[q] && c->pair_next[q] + need_e[q] > c->pair_end[q]) return ESC_E_LIMIT;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    // the K5 regions this rank orders (the tail of the node table is the last rank's)
-    const bool k5 = c->tail_owner && c->n_gpad > 0;
-    if (k5) {
+    // K5 regions: every rank checks the capacity of every group the batch touches (the host
+    // knows them all), so that all ranks accept or refuse alike; it inserts into the regions
+    // of the groups it owns
+    const bool k5 = c->age_built && !c->h_pcap.empty();
+    if (k5 && c->n_gpad > 0) {
         int32_t rc = ensure_gn(c);
         if (rc) return rc;
     }
@@ -2468,7 +2642,7 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
             for (uint32_t m : mb) ++need_r[m & NODE_GROUP_MASK];
         }
         for (const auto& kv : need_r)
-            if ((int64_t)c->h_plen[kv.first] + kv.second > (int64_t)(c->h_pstart[kv.first + 1] - c->h_pstart[kv.first])) {
+            if ((int64_t)c->h_plen[kv.first] + kv.second > (int64_t)c->h_pcap[kv.first]) {
                 for (int64_t i = 0; i < n; ++i) c->h_nflags[j0 + i] = ESC_NF_ABSENT;   // undo
                 return ESC_E_LIMIT;
             }
@@ -2494,6 +2668,7 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
             if (s->xl_pair[xo[i] + k] < n_gp) pairs.push_back(s->xl_pair[xo[i] + k]);
         for (uint32_t q : pairs) {
             const uint32_t e = c->pair_next[q]++;
+            ++c->pair_live[q];
             P.add(NT_EFLAGS, e, f);
             P.add(NT_ENODE, e, (uint32_t)j);
             P.add(NT_ECPU, e, (uint64_t)s->cpu[i]);
@@ -2526,15 +2701,20 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
     if (rc) return rc;
     if (first_changed)
         HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
+    for (int64_t i = 0; i < n; ++i) c->h_created.push_back(s->created_ns[i]);
+    c->node_hi = c->n_nodes;
     if (k5) {
         // K5: insert each new membership at its place by (creation time, index) in its
-        // group's region; every group touched is rewritten from its first insertion on
-        for (int64_t i = 0; i < n; ++i) c->h_created.push_back(s->created_ns[i]);
-        c->node_hi = c->n_nodes;
+        // group's region (the groups this rank owns; the others only count it); every group
+        // touched is rewritten from its first insertion on
         std::unordered_map<uint32_t, std::vector<uint32_t>> add_by_g;
         for (int64_t i = 0; i < n; ++i) {
             node_membs(c, j0 + i, mb);
-            for (uint32_t m : mb) add_by_g[m & NODE_GROUP_MASK].push_back((uint32_t)(j0 + i));
+            for (uint32_t m : mb) {
+                const uint32_t g = m & NODE_GROUP_MASK;
+                if (owns_group(c, g)) add_by_g[g].push_back((uint32_t)(j0 + i));
+                else ++c->h_plen[g];
+            }
         }
         auto less = [&](uint32_t x, uint32_t y) {
             const int64_t tx = created_of(c, x), ty = created_of(c, y);
@@ -2570,6 +2750,7 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
 }
 
 int32_t esc_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
+    if (c && c->multi) return esc::multi_nodes_delete(c, ids, n);
     if (!c || n < 0 || (n > 0 && !ids)) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->nodes_loaded) return ESC_E_STATE;
@@ -2590,7 +2771,12 @@ int32_t esc_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
         int32_t rc = write_tracker(c, next);
         if (rc) return rc;
     }
-    for (int64_t j : del) c->h_nflags[j] = (c->h_nflags[j] & ~ESC_NF_TRACKED) | ESC_NF_ABSENT;
+    for (int64_t j : del) {
+        auto drop = [&](uint32_t q) { if (q < c->gi.n_gp) --c->pair_live[q]; };   // live entries (owner split)
+        drop(c->h_label0[j]);
+        for (uint32_t k = 0; k < nf_xlbl(c->h_nflags[j]); ++k) drop(c->h_xl[c->h_xl_off[j] + k]);
+        c->h_nflags[j] = (c->h_nflags[j] & ~ESC_NF_TRACKED) | ESC_NF_ABSENT;
+    }
     // allNodes[0] of the groups whose first member went: the next live entry of the pair
     bool first_changed = false;
     for (int32_t g = 0; g < c->gi.G; ++g) {
@@ -2626,6 +2812,7 @@ int32_t esc_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
 // the pair-major entries and the K5 membership list.
 int32_t esc_tracker_update(esc_ctx* c, int32_t group, const int64_t* add, int64_t n_add, const int64_t* rm,
                            int64_t n_rm) {
+    if (c && c->multi) return esc::multi_tracker_update(c, group, add, n_add, rm, n_rm);
     if (!c || n_add < 0 || n_rm < 0 || (n_add > 0 && !add) || (n_rm > 0 && !rm)) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->nodes_loaded) return ESC_E_STATE;
@@ -2682,6 +2869,7 @@ int32_t esc_tracker_update(esc_ctx* c, int32_t group, const int64_t* add, int64_
 }
 
 int32_t esc_tracker_list(const esc_ctx* c, int32_t group, int64_t* idx_out, int64_t cap, int64_t* n_out) {
+    if (c && c->multi) return esc_tracker_list(esc::multi_sub(c, 0), group, idx_out, cap, n_out);
     if (!c || !n_out || cap < 0 || (cap > 0 && !idx_out)) return ESC_E_INVAL;
     if (group < 0 || group >= c->gi.G) return ESC_E_INVAL;
     int64_t m = 0;
@@ -2699,6 +2887,7 @@ int32_t esc_tracker_list(const esc_ctx* c, int32_t group, int64_t* idx_out, int6
 // node (a host counting sort of the pods by node, then one gather of each pod's flags and
 // pairs from the resident layout), plus the per-node GetToBeRemovedTime / no-delete facts.
 int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* taint_s, const uint8_t* no_delete) {
+    if (c && c->multi) return esc::multi_load_placement(c, pod_node, taint_s, no_delete);
     if (!c || !taint_s || !no_delete) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
@@ -2798,6 +2987,7 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
 // K6 (node occupancy by group filter over this rank's pods) — the first half of
 // esc_try_remove; with several ranks the occupancy words are summed across ranks before K7.
 int32_t esc_reap_occupancy(esc_ctx* c) {
+    if (c && c->multi) return ESC_E_STATE;              // esc_try_remove exchanges internally
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->placed || !c->node_removal) return ESC_E_STATE;
@@ -2808,6 +2998,7 @@ int32_t esc_reap_occupancy(esc_ctx* c) {
 }
 
 int32_t esc_reap_buffer(esc_ctx* c, void** buf, int64_t* n_words) {
+    if (c && c->multi) return ESC_E_STATE;
     if (!c || !buf || !n_words) return ESC_E_INVAL;
     if (!c->placed) return ESC_E_STATE;
     *buf = c->d_occ;
@@ -2816,6 +3007,7 @@ int32_t esc_reap_buffer(esc_ctx* c, void** buf, int64_t* n_words) {
 }
 
 int32_t esc_reap_download(esc_ctx* c, uint32_t* out) {
+    if (c && c->multi) return ESC_E_STATE;
     if (!c || !out) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->placed) return ESC_E_STATE;
@@ -2826,6 +3018,7 @@ int32_t esc_reap_download(esc_ctx* c, uint32_t* out) {
 }
 
 int32_t esc_reap_upload(esc_ctx* c, const uint32_t* in) {
+    if (c && c->multi) return ESC_E_STATE;
     if (!c || !in) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->placed) return ESC_E_STATE;
@@ -2837,6 +3030,7 @@ int32_t esc_reap_upload(esc_ctx* c, const uint32_t* in) {
 
 // K7 over the (summed) occupancy: the per-group reaping pass.
 int32_t esc_reap_finish(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, const int64_t* hard_ns, esc_removal* out) {
+    if (c && c->multi) return ESC_E_STATE;
     if (!c || !soft_ns || !hard_ns || !out) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->placed || !c->node_removal) return ESC_E_STATE;
@@ -2865,6 +3059,7 @@ int32_t esc_reap_finish(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, cons
 // esc_try_remove: K6 (node occupancy by group filter) + the cross-rank SUM of the occupancy
 // words over the context's RCCL communicator when there are several ranks + K7.
 int32_t esc_try_remove(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, const int64_t* hard_ns, esc_removal* out) {
+    if (c && c->multi) return esc::multi_try_remove(c, now_ns, soft_ns, hard_ns, out);
     if (!c || !soft_ns || !hard_ns || !out) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (c->world > 1 && !c->comm) return ESC_E_STATE;  // host-staged: esc_reap_occupancy / _download / _upload / _finish
@@ -2880,6 +3075,7 @@ int32_t esc_try_remove(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, const
 }
 
 int32_t esc_removal_nodes(esc_ctx* c, int32_t g, int64_t* idx, int64_t cap, int64_t* n_out) {
+    if (c && c->multi) return esc_removal_nodes(esc::multi_sub(c, 0), g, idx, cap, n_out);
     if (!c || !n_out || g < 0 || g >= c->gi.G || cap < 0 || (cap > 0 && !idx)) return ESC_E_INVAL;
     if (!c->rm_valid) return ESC_E_STATE;
     const int64_t n = c->h_rm[g].n_delete;
@@ -2895,6 +3091,7 @@ int32_t esc_removal_nodes(esc_ctx* c, int32_t g, int64_t* idx, int64_t cap, int6
 
 // ----------------------------------------------------------------- ordering
 int32_t esc_sort_nodes(esc_ctx* c) {
+    if (c && c->multi) return esc::multi_each(c, [](esc_ctx* x, int32_t) { return esc_sort_nodes(x); }, 0);
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->nodes_loaded) return ESC_E_STATE;
@@ -2915,6 +3112,7 @@ int32_t esc_sort_nodes(esc_ctx* c) {
 }
 
 int32_t esc_build_age_index(esc_ctx* c) {
+    if (c && c->multi) return esc::multi_each(c, [](esc_ctx* x, int32_t) { return esc_build_age_index(x); }, 0);
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->nodes_loaded) return ESC_E_STATE;
@@ -2923,6 +3121,7 @@ int32_t esc_build_age_index(esc_ctx* c) {
 }
 
 int32_t esc_order_info(const esc_ctx* c, int64_t* n_memberships, int32_t* key_bits) {
+    if (c && c->multi) return esc::multi_order_info(c, n_memberships, key_bits);
     if (!c || !n_memberships || !key_bits) return ESC_E_INVAL;
     if (!c->nodes_loaded) return ESC_E_STATE;
     *n_memberships = c->n_memb;
@@ -2931,6 +3130,7 @@ int32_t esc_order_info(const esc_ctx* c, int64_t* n_memberships, int32_t* key_bi
 }
 
 int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_out, int64_t cap, int64_t* n_out) {
+    if (c && c->multi) return esc::multi_group_order(c, group, which, idx_out, cap, n_out);
     if (!c || group < 0 || group >= c->gi.G || (which != 0 && which != 1) || cap < 0 || (cap > 0 && !idx_out))
         return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
@@ -3027,6 +3227,7 @@ int32_t run_list(esc_ctx* L, const esc_pod_obj* pods, int64_t np, const esc_node
 }  // namespace
 
 int32_t esc_pods_requests_total(esc_ctx* c, const esc_pod_obj* pods, int64_t n, int64_t* mem_b, int64_t* cpu_m) {
+    if (c && c->multi) return esc_pods_requests_total(esc::multi_sub(c, 0), pods, n, mem_b, cpu_m);
     if (!c || n < 0 || (n > 0 && !pods) || !mem_b || !cpu_m) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     esc_ctx* L = nullptr;
@@ -3042,6 +3243,7 @@ int32_t esc_pods_requests_total(esc_ctx* c, const esc_pod_obj* pods, int64_t n, 
 }
 
 int32_t esc_nodes_capacity_total(esc_ctx* c, const esc_node_obj* nodes, int64_t n, int64_t* mem_b, int64_t* cpu_m) {
+    if (c && c->multi) return esc_nodes_capacity_total(esc::multi_sub(c, 0), nodes, n, mem_b, cpu_m);
     if (!c || n < 0 || (n > 0 && !nodes) || !mem_b || !cpu_m) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     esc_ctx* L = nullptr;
@@ -3058,6 +3260,7 @@ int32_t esc_nodes_capacity_total(esc_ctx* c, const esc_node_obj* nodes, int64_t 
 
 int32_t esc_order_by_creation(esc_ctx* c, const int64_t* created_ns, int64_t n, int32_t oldest, int64_t n_take,
                               int64_t* idx_out) {
+    if (c && c->multi) return esc_order_by_creation(esc::multi_sub(c, 0), created_ns, n, oldest, n_take, idx_out);
     if (!c || n < 0 || (n > 0 && !created_ns) || (n_take > 0 && !idx_out)) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     esc_ctx* L = nullptr;
@@ -3079,6 +3282,51 @@ int32_t esc_order_by_creation(esc_ctx* c, const int64_t* created_ns, int64_t n, 
     int64_t cnt = 0;
     if (!rc) rc = esc_group_order(L, 0, oldest ? 0 : 1, idx_out, std::max<int64_t>(0, std::min(n_take, n)), &cnt);
     return rc;
+}
+
+// ------------------------------------------------------- sizes, ownership, communicators
+int32_t esc_ctx_counts(const esc_ctx* c, int64_t* n_pod_ids, int64_t* n_nodes) {
+    if (!c || !n_pod_ids || !n_nodes) return ESC_E_INVAL;
+    if (c->multi) return esc::multi_counts(c, n_pod_ids, n_nodes);
+    *n_pod_ids = c->pods_loaded ? (int64_t)c->pod_cls.size() : 0;
+    *n_nodes = c->nodes_loaded ? c->n_nodes : 0;
+    return ESC_OK;
+}
+
+int32_t esc_group_owner(const esc_ctx* c, int32_t group, int32_t* rank) {
+    if (!c || !rank || group < 0 || group >= c->gi.G) return ESC_E_INVAL;
+    if (c->multi) return esc_group_owner(esc::multi_sub(c, 0), group, rank);   // every device knows the split
+    if (!c->nodes_loaded) return ESC_E_STATE;
+    const uint32_t q = c->gi.gpair[group];
+    *rank = (int32_t)(std::upper_bound(c->q_bounds.begin(), c->q_bounds.end() - 1, q) - c->q_bounds.begin()) - 1;
+    return ESC_OK;
+}
+
+int32_t esc_node_owner_ranges(const esc_ctx* c, const esc_node_soa* s, int32_t world, uint32_t* q_bounds) {
+    if (!c || !s || !q_bounds || world < 1 || s->n_nodes < 0) return ESC_E_INVAL;
+    if (s->n_nodes > 0 && (!s->flags || !s->label0 || (s->n_xl > 0 && !s->xl_pair))) return ESC_E_INVAL;
+    int64_t sx = 0;
+    for (int64_t i = 0; i < s->n_nodes; ++i) sx += nf_xlbl(s->flags[i]);
+    if (sx != s->n_xl) return ESC_E_INVAL;
+    const std::vector<int64_t> cnt = pair_counts(c, s);
+    for (int32_t r = 0; r < world; ++r) {
+        uint32_t a = 0, b = 0;
+        owned_pairs(cnt, world, r, a, b);
+        q_bounds[r] = a;
+    }
+    q_bounds[world] = c->gi.n_gp;
+    return ESC_OK;
+}
+
+int32_t esc_comm_size(const esc_ctx* c, int32_t* ranks) {
+    if (!c || !ranks) return ESC_E_INVAL;
+    if (c->multi) { *ranks = esc::multi_size(c); return ESC_OK; }
+    if (!c->comm) return ESC_E_STATE;
+    int n = 0;
+    const ncclResult_t r = rccl().count(reinterpret_cast<ncclComm_t>(c->comm), &n);
+    if (r != ncclSuccess) return fail_comm("ncclCommCount", rccl().error_string(r));
+    *ranks = n;
+    return ESC_OK;
 }
 
 // ------------------------------------------------------- scalar decision math

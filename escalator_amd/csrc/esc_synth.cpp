@@ -65,6 +65,17 @@ struct esc_synth {
     uint64_t default_bp = 0;        // basis points of pods that carry no selector at all
     int64_t mem_mib_max = 16384;    // per-container memory request range (MiB)
     HostSnapshot s;
+    // object-level form of the same snapshot (esc_synth_objects), built on first use
+    struct Objects {
+        bool built = false;
+        std::vector<esc_pod_obj> pods;
+        std::vector<esc_node_obj> nodes;
+        std::vector<esc_kv> kvs;
+        std::vector<esc_selector_expr> exprs;
+        std::vector<const char*> vals;
+        std::vector<esc_request> reqs;
+        std::vector<std::string> values, node_names;
+    } obj;
 };
 
 namespace {
@@ -73,6 +84,13 @@ struct PodDesc {
     uint32_t pred = 0;
     uint32_t heads[16];                                 // selected pair ids
     int nheads = 0;
+    // the object-level routes of the heads (esc_synth_objects): nodeSelector pairs, the
+    // "In" values of the required node-affinity term, and the other object facts
+    uint32_t sel[4], aff[8];
+    int nsel = 0, naff = 0;
+    bool not_in = false, pod_aff = false, zone = false;
+    void add_sel(uint32_t h) { if (nsel < 4) sel[nsel++] = h; add_head(h); }
+    void add_aff(uint32_t h) { if (naff < 8) aff[naff++] = h; add_head(h); }
     int n_reg = 0, n_init = 0;
     bool ovh = false;
     int64_t cpu[4], mem[4], icpu = 0, imem = 0, ocpu = 0, omem = 0;
@@ -102,15 +120,16 @@ void gen_pod(const esc_synth& S, int64_t i, PodDesc& d) {
     if (S.p.config == 1) {                              // 1 group, every non-DS pod selects it
         if (r < 500) d.pred |= ESC_PF_DAEMONSET;
         d.pred |= ESC_PF_HAS_SEL;
-        d.add_head(S.pair_of[0]);
+        d.add_sel(S.pair_of[0]);
     } else if (r < 500) {                               // daemonset with a selector
         d.pred |= ESC_PF_DAEMONSET | ESC_PF_HAS_SEL;
-        if (nnd) d.add_head(S.pair_of[pick(1)]);
+        if (nnd) d.add_sel(S.pair_of[pick(1)]);
     } else if (r < 550) {                               // static pod, no selector
         d.pred |= ESC_PF_STATIC;
     } else if (r < 550 + S.default_bp) {                // default-group pod (~one group's share)
     } else if (r < 570 + S.default_bp) {                // PodAffinity only: blocks default, no pairs
         d.pred |= ESC_PF_AFF_BLOCK;
+        d.pod_aff = true;
     } else if (nnd) {
         const uint64_t sub = rnd(seed, 1, i, 2) % 100;
         const int32_t g1 = pick(3);
@@ -121,29 +140,29 @@ void gen_pod(const esc_synth& S, int64_t i, PodDesc& d) {
         };
         if (sub < 70) {                                 // nodeSelector only
             d.pred |= ESC_PF_HAS_SEL;
-            d.add_head(S.pair_of[g1]);
+            d.add_sel(S.pair_of[g1]);
         } else if (sub < 90) {                          // affinity In with 1-3 values
             d.pred |= ESC_PF_AFF_BLOCK;
             const int nv = 1 + (int)(rnd(seed, 1, i, 4) % 3);
-            d.add_head(aff_head(g1));
-            if (nv > 1) d.add_head(aff_head(pick(5)));
-            if (nv > 2) d.add_head(aff_head(pick(6)));
+            d.add_aff(aff_head(g1));
+            if (nv > 1) d.add_aff(aff_head(pick(5)));
+            if (nv > 2) d.add_aff(aff_head(pick(6)));
         } else {                                        // both (duplicate pair -> counted once)
             d.pred |= ESC_PF_HAS_SEL | ESC_PF_AFF_BLOCK;
-            d.add_head(S.pair_of[g1]);
-            d.add_head(aff_head(g1));
-            d.add_head(aff_head(pick(7)));
+            d.add_sel(S.pair_of[g1]);
+            d.add_aff(aff_head(g1));
+            d.add_aff(aff_head(pick(7)));
         }
         const uint64_t x = rnd(seed, 1, i, 8) % 1000;
-        if (x < 10) d.pred |= ESC_PF_AFF_BLOCK;         // extra NotIn expression (ignored)
+        if (x < 10) { d.pred |= ESC_PF_AFF_BLOCK; d.not_in = true; }   // extra NotIn expression (ignored)
         if (x >= 100 && x < 150 && !S.pool_groups.empty()) {   // extra "pool" selector
             d.pred |= ESC_PF_HAS_SEL;
             int32_t gp = S.pool_groups[rnd(seed, 1, i, 9) % S.pool_groups.size()];
-            d.add_head(S.pair_of[S.canon[gp]]);
+            d.add_sel(S.pair_of[S.canon[gp]]);
         }
-        if (x >= 200 && x < 300) d.pred |= ESC_PF_HAS_SEL;     // "zone" selector: no group key, not carried
+        if (x >= 200 && x < 300) { d.pred |= ESC_PF_HAS_SEL; d.zone = true; }   // "zone" selector: no group key, not carried
         if (x >= 300 && x < 330)                                // a customer value no group has
-            d.add_head(other_pair(S, K_CUSTOMER, (uint32_t)S.p.n_groups + (uint32_t)(rnd(seed, 1, i, 11) % 1000)));
+            d.add_aff(other_pair(S, K_CUSTOMER, (uint32_t)S.p.n_groups + (uint32_t)(rnd(seed, 1, i, 11) % 1000)));
     }
     std::sort(d.heads, d.heads + d.nheads);
     // Containers: 90% one, 6% two, 3% three, 1% two + one init + overhead.
@@ -377,6 +396,141 @@ void gen_nodes(esc_synth& S) {
     }
 }
 
+// (key, value) strings of pair id q (a group pair, or one of the generator's other values).
+struct PairNames {
+    std::vector<const char*> key, val;                 // group pairs
+    const esc_synth* S;
+    const char* k(uint32_t q) const {
+        if (q < key.size()) return key[q];
+        return ((q - key.size()) / ((uint32_t)S->p.n_groups + 2000u)) == K_POOL ? "pool" : "customer";
+    }
+    const char* v(uint32_t q) const {
+        if (q < val.size()) return val[q];
+        return S->obj.values[(q - val.size()) % ((uint32_t)S->p.n_groups + 2000u)].c_str();
+    }
+};
+
+// The esc_pod_obj / esc_node_obj fields each generated record stands for (what the cgo
+// shim copies out of *v1.Pod / *v1.Node): owner kinds, the config.source annotation, a
+// nodeSelector, a required node-affinity term ("In" values per key, an ignored NotIn),
+// PodAffinity, containers.  Packing them reproduces the generator's snapshot up to the
+// numbering of values no group selects and to flag bits no filter reads differently
+// (tests/test_pack_parity.py compares totals).
+void build_objects(esc_synth& S) {
+    auto& O = S.obj;
+    const uint32_t G = (uint32_t)S.p.n_groups, nv = G + 2000u;
+    O.values.resize(nv);
+    for (uint32_t v = 0; v < nv; ++v) O.values[v] = (v < G ? "g" : "x") + std::to_string(v);
+    PairNames pn;
+    pn.S = &S;
+    pn.key.assign(S.gi.n_gp, "");
+    pn.val.assign(S.gi.n_gp, "");
+    for (int32_t g = (int32_t)G - 1; g >= 0; --g) { pn.key[S.gi.gpair[g]] = S.keys[g].c_str(); pn.val[S.gi.gpair[g]] = S.values[g].c_str(); }
+    static const char* const kind_ds[] = {"DaemonSet"};
+    static const char* const kind_rs[] = {"ReplicaSet"};
+    static const char* const taint_esc[] = {"atlassian.com/escalator"};
+    const int64_t n = S.p_hi - S.p_lo;
+    // pass 1: sizes
+    std::vector<int64_t> nkv(n + 1, 0), nex(n + 1, 0), nva(n + 1, 0), nrq(n + 1, 0);
+    parallel_for(n, std::max(1, S.p.n_threads), [&](int64_t lo, int64_t hi, int) {
+        for (int64_t k = lo; k < hi; ++k) {
+            PodDesc d;
+            gen_pod(S, S.p_lo + k, d);
+            nkv[k] = d.nsel + (d.zone ? 1 : 0);
+            nex[k] = 3;                                         // In per key (<= 2 keys), NotIn
+            nva[k] = d.naff + d.nsel + 1;                       // a selector key given twice moves here
+            nrq[k] = d.n_reg + d.n_init;
+        }
+    });
+    auto scan = [](std::vector<int64_t>& v) { int64_t a = 0; for (auto& x : v) { const int64_t t = x; x = a; a += t; } };
+    scan(nkv); scan(nex); scan(nva); scan(nrq);
+    const HostSnapshot& h = S.s;
+    const int64_t nn = (int64_t)h.nflags.size();
+    O.pods.assign(n, esc_pod_obj{});
+    O.kvs.resize(std::max<int64_t>(nkv[n] + 2 * nn + (int64_t)h.xl.size(), 1));   // pods', then the nodes' labels
+    O.exprs.resize(std::max<int64_t>(nex[n], 1));
+    O.vals.resize(std::max<int64_t>(nva[n], 1));
+    O.reqs.resize(std::max<int64_t>(nrq[n], 1));
+    parallel_for(n, std::max(1, S.p.n_threads), [&](int64_t lo, int64_t hi, int) {
+        for (int64_t k = lo; k < hi; ++k) {
+            PodDesc d;
+            gen_pod(S, S.p_lo + k, d);
+            esc_pod_obj& o = O.pods[k];
+            const bool ds = (d.pred & ESC_PF_DAEMONSET) != 0;
+            o.owner_kinds = ds ? kind_ds : kind_rs;
+            o.n_owner_kinds = 1;
+            o.has_config_source = (d.pred & ESC_PF_STATIC) ? 1 : 0;
+            o.config_source = o.has_config_source ? "file" : "";
+            esc_kv* kv = O.kvs.data() + nkv[k];
+            esc_selector_expr* ex = O.exprs.data() + nex[k];
+            const char** va = O.vals.data() + nva[k];
+            int nk = 0, ne = 0, nvv = 0;
+            for (int i = 0; i < d.nsel; ++i) {                  // a key twice goes to the affinity term
+                bool dup = false;
+                for (int j = 0; j < nk; ++j) dup |= std::strcmp(kv[j].key, pn.k(d.sel[i])) == 0;
+                if (dup) { d.aff[d.naff < 8 ? d.naff++ : 7] = d.sel[i]; continue; }
+                kv[nk++] = esc_kv{pn.k(d.sel[i]), pn.v(d.sel[i])};
+            }
+            if (d.zone) kv[nk++] = esc_kv{"zone", "z1"};
+            o.node_selector = kv;
+            o.n_node_selector = nk;
+            for (const char* key : {"customer", "pool"}) {      // one In expression per key
+                const int first = nvv;
+                for (int i = 0; i < d.naff; ++i)
+                    if (std::strcmp(pn.k(d.aff[i]), key) == 0 && nvv < (int)(nva[k + 1] - nva[k])) va[nvv++] = pn.v(d.aff[i]);
+                if (nvv > first) ex[ne++] = esc_selector_expr{key, "In", va + first, nvv - first, 0};
+            }
+            if (d.not_in && nvv < (int)(nva[k + 1] - nva[k])) {
+                va[nvv] = "z9";
+                ex[ne++] = esc_selector_expr{"zone", "NotIn", va + nvv, 1, 0};
+                ++nvv;
+            }
+            o.exprs = ex;
+            o.n_exprs = ne;
+            o.has_affinity = (ne > 0 || d.pod_aff) ? 1 : 0;
+            o.has_node_affinity = ne > 0 ? 1 : 0;
+            o.has_required = ne > 0 ? 1 : 0;
+            o.has_pod_affinity = d.pod_aff ? 1 : 0;
+            esc_request* rq = O.reqs.data() + nrq[k];
+            for (int i = 0; i < d.n_reg; ++i)
+                rq[i] = esc_request{d.cpu[i], d.mem[i], d.cpu[i] != 0, d.mem[i] != 0};
+            o.containers = rq;
+            o.n_containers = d.n_reg;
+            if (d.n_init) rq[d.n_reg] = esc_request{d.icpu, d.imem, 1, 1};
+            o.init_containers = d.n_init ? rq + d.n_reg : nullptr;
+            o.n_init_containers = d.n_init;
+            o.has_overhead = d.ovh ? 1 : 0;
+            o.overhead = esc_request{d.ocpu, d.omem, d.ovh ? 1 : 0, d.ovh ? 1 : 0};
+        }
+    });
+    // nodes: name, label pairs (+ a zone label no group filters on), cordon, the escalator
+    // taint, allocatable, creation time
+    std::vector<int64_t> xo(nn + 1, 0);
+    for (int64_t j = 0; j < nn; ++j) xo[j + 1] = xo[j] + nf_xlbl(h.nflags[j]);
+    const int64_t kv0 = nkv[n];
+    O.nodes.assign(nn, esc_node_obj{});
+    O.node_names.resize(nn);
+    for (int64_t j = 0; j < nn; ++j) O.node_names[j] = "node-" + std::to_string(j);
+    for (int64_t j = 0, kp = kv0; j < nn; ++j) {
+        esc_node_obj& o = O.nodes[j];
+        o.name = O.node_names[j].c_str();
+        esc_kv* kv = O.kvs.data() + kp;
+        int nk = 0;
+        if (h.label0[j] != NONE) kv[nk++] = esc_kv{pn.k(h.label0[j]), pn.v(h.label0[j])};
+        for (int64_t x = xo[j]; x < xo[j + 1]; ++x) kv[nk++] = esc_kv{pn.k(h.xl[x]), pn.v(h.xl[x])};
+        kv[nk++] = esc_kv{"zone", (j % 3 == 0) ? "z0" : (j % 3 == 1 ? "z1" : "z2")};
+        kp += nk;
+        o.labels = kv;
+        o.n_labels = nk;
+        o.unschedulable = (h.nflags[j] & ESC_NF_UNSCHED) ? 1 : 0;
+        o.taint_keys = (h.nflags[j] & ESC_NF_TAINTED) ? taint_esc : nullptr;
+        o.n_taints = (h.nflags[j] & ESC_NF_TAINTED) ? 1 : 0;
+        o.allocatable = esc_request{h.ncpu[j], h.nmem[j], 1, 1};
+        o.created_unix_ns = h.created[j];
+    }
+    O.built = true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -422,6 +576,23 @@ int32_t esc_synth_states(const esc_synth* s, const esc_group_state** states) {
 int32_t esc_synth_view(const esc_synth* s, esc_pod_soa* pods, esc_node_soa* nodes) {
     if (!s) return ESC_E_INVAL;
     s->s.view(pods, nodes);
+    return ESC_OK;
+}
+
+int32_t esc_synth_objects(esc_synth* s, const esc_pod_obj** pods, int64_t* n_pods, const esc_node_obj** nodes,
+                          int64_t* n_nodes) {
+    if (!s || !pods || !n_pods || !nodes || !n_nodes) return ESC_E_INVAL;
+    if (!s->obj.built) {
+        try {
+            build_objects(*s);
+        } catch (const std::bad_alloc&) {
+            return ESC_E_NOMEM;
+        }
+    }
+    *pods = s->obj.pods.data();
+    *n_pods = (int64_t)s->obj.pods.size();
+    *nodes = s->obj.nodes.data();
+    *n_nodes = (int64_t)s->obj.nodes.size();
     return ESC_OK;
 }
 

@@ -1,13 +1,17 @@
-"""One process per GPU: sharded pods + one exchange of the pods' per-group int64 words.
+"""One process per GPU: sharded pods, the node side split by pair ownership, and one SUM
+exchange of the per-group words.
 
 The reference has no parallelism (groups run sequentially,
 controller.go:416).  Here every rank holds a contiguous shard of the pod SoA and the whole
-node table (it reduces the node index itself, so only the pods' words cross ranks); the
-per-group pod words are all-reduced with SUM — by the library's own RCCL communicator
+node table; it reduces and orders the node side of the group pairs it owns (a contiguous
+pair range balanced by node entries, the same split on every rank).  The
+per-group words — the pods' sums split lo32 / hi, and the node words, exact on the owner
+and zero elsewhere — are all-reduced with SUM: by the library's own RCCL communicator
 (esc_comm_init / esc_exchange: ncclAllReduce over xGMI on the context's stream), or
-host-staged over ``gloo``.  int64 addition is associative and the words are split lo32 /
-hi, so any reduction order gives bit-identical totals; every rank then runs K4 on the
-same words.
+host-staged over ``gloo``.  int64 addition is associative, so any reduction order gives
+bit-identical totals; every rank then runs K4 on the same words.  (One process driving
+every GPU is ``Context(..., devices=[...])``: the same sharding with the exchange inside
+the library.)
 """
 from __future__ import annotations
 
@@ -34,9 +38,9 @@ class Exchange:
 
     device_collective: the library's own RCCL communicator (esc_comm_init; rank 0's
     unique id travels over the torch.distributed group), one in-place
-    ncclAllReduce(int64, SUM) on the context's stream between K3 and K4 (esc_step) — the
-    path a Go host drives through the C ABI alone.  Otherwise host-staged over the group
-    (gloo): download, all_reduce, upload."""
+    ncclAllReduce(int64, SUM) of the pods' and node words on the context's stream between
+    the shard step and K4 (esc_step) — the path a Go host drives through the C ABI alone.
+    Otherwise host-staged over the group (gloo): download, all_reduce, upload."""
 
     def __init__(self, ctx, device_collective: bool):
         import torch
@@ -44,7 +48,7 @@ class Exchange:
         self.ctx, self.dist, self.torch = ctx, dist, torch
         self.device_collective = device_collective
         (_, sc), (_, mc) = ctx.exchange_buffers()
-        assert mc == 0, "the node words are reduced on every rank: nothing to MIN-exchange"
+        assert mc == 0, "allNodes[0] comes from the whole node table on every rank: nothing to MIN-exchange"
         if device_collective:
             rank, world = dist.get_rank(), dist.get_world_size()
             obj = [ctx.comm_unique_id() if rank == 0 else None]
@@ -95,14 +99,14 @@ def exchange_host(sum_arr, min_arr):
 
 # ------------------------------------------------ sharded orderings (config #5, 1-8 GPUs)
 def merge_orders(parts, created_ns, which: int, n: int):
-    """Global first `n` of one group's order from the ranks' local prefixes.
+    """Global first `n` of one group's order from the ranks' prefixes.
 
-    Every rank orders its contiguous node range (esc_sort_nodes over [lo, hi)) and
-    contributes the first `n` entries of its list; `which` 0 = untainted oldest-first
-    (taintOldestN, scale_down.go:171), 1 = tainted newest-first (untaintNewestN,
-    scale_up.go:118).  The global order is the k-way merge by creation time with ties by
-    ascending snapshot index — the single-rank tie rule — so the merged prefix equals the
-    single-GPU list bit for bit.  `parts` are int64 arrays of snapshot node indices."""
+    The rank owning the group's pair orders all of its members (esc_sort_nodes), the
+    others contribute nothing; `which` 0 = untainted oldest-first (taintOldestN,
+    scale_down.go:171), 1 = tainted newest-first (untaintNewestN, scale_up.go:118).  The
+    merge by creation time with ties by ascending snapshot index — the single-rank tie rule
+    — is the general k-way merge, so it also joins prefixes of disjoint node ranges.
+    `parts` are int64 arrays of snapshot node indices."""
     import numpy as np
     idx = np.concatenate([np.asarray(p, np.int64) for p in parts]) if parts else np.zeros(0, np.int64)
     if idx.size == 0:

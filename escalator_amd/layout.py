@@ -6,8 +6,9 @@ K1 reads the pod shard once per decision: per pod flags 4 + cpu0 4 + mem0 8 + pa
 per 64-pod C tile (pods with more than 3 extra container records or more than 3 extra
 pairs; all other pods sit in homogeneous 256-pod K tiles that need no offsets).
 K2 reads the node index once per decision: 24 B per (label pair, node) entry of a pair
-some group selects (flags 4 + cpu 8 + mem 8 + node 4) and 8 B per piece (offset + pair);
-every rank reads the whole index (only the pods' words are exchanged).
+some group selects (flags 4 + cpu 8 + mem 8 + node 4) and 8 B per piece (offset + pair).
+With several ranks each reads the pieces of the group pairs it owns (``owner_ranges``:
+contiguous pair ranges balanced by entry count).
 """
 import numpy as np
 
@@ -36,6 +37,33 @@ def node_entries(nodes: dict) -> np.ndarray:
     return np.sort(pairs, kind="stable")
 
 
+OWN_PAD = 64          # per-pair weight beside its entries (esc_runtime.hip owned_pairs)
+
+
+def pair_counts(nodes: dict, n_gp: int) -> np.ndarray:
+    """Node entries of every group pair (ids < n_gp)."""
+    q = node_entries(nodes)
+    return np.bincount(q[q < n_gp].astype(np.int64), minlength=n_gp)[:n_gp]
+
+
+def owner_ranges(nodes: dict, n_gp: int, world: int) -> list[int]:
+    """The owner split of the node side: pair q, weighted by its entries +
+    OWN_PAD, goes to rank floor(S_q * world / W) with S_q the weight before q and W the
+    total; returns q_bounds (rank r owns pairs [q_bounds[r], q_bounds[r + 1]))."""
+    if world <= 1:
+        return [0, n_gp]
+    w = [int(x) + OWN_PAD for x in pair_counts(nodes, n_gp)]
+    W = sum(w)
+    owner, S = [], 0
+    for x in w:
+        owner.append(S * world // W)
+        S += x
+    bounds = []
+    for r in range(world):
+        bounds.append(next((q for q, o in enumerate(owner) if o >= r), n_gp))
+    return bounds + [n_gp]
+
+
 def node_bytes(nodes: dict, n_gp: int, rank: int = 0, world: int = 1) -> int:
     q = node_entries(nodes)
     E = len(q)
@@ -48,5 +76,6 @@ def node_bytes(nodes: dict, n_gp: int, rank: int = 0, world: int = 1) -> int:
     p_start = np.repeat(starts, n_pc) + NODE_PIECE * (np.arange(n_pc.sum()) - np.repeat(np.cumsum(n_pc) - n_pc, n_pc))
     p_len = np.diff(np.r_[p_start, E])
     p_pair = q[p_start]
-    del rank, world                      # rank-independent: every rank reduces all pieces
-    return int(8 * len(p_start) + 24 * p_len[p_pair < n_gp].sum())
+    b = owner_ranges(nodes, n_gp, world)
+    mine = (p_pair >= b[rank]) & (p_pair < b[rank + 1])
+    return int(8 * int(mine.sum()) + 24 * int(p_len[mine].sum()))

@@ -92,23 +92,42 @@ func (a *arena) free() {
 	a.ptrs = nil
 }
 
+// ptr is &s[0], or nil for an empty slice: &s[0] of a zero-length slice panics, and the
+// ABI takes NULL with a zero count for every array (include/escalator_hip.h conventions).
+// Every slice handed to C goes through it.
+func ptr[T any](s []T) *T {
+	if len(s) == 0 {
+		return nil
+	}
+	return &s[0]
+}
+
+// cslice is n zeroed elements of C memory owned by the arena, or nil when n == 0.
+func cslice[T any](a *arena, n int) []T {
+	if n == 0 {
+		return nil
+	}
+	var z T
+	return unsafe.Slice((*T)(a.alloc(n, unsafe.Sizeof(z))), n)
+}
+
 func (a *arena) cstrs(ss []string) **C.char {
-	arr := (*[1 << 28]*C.char)(a.alloc(len(ss), unsafe.Sizeof((*C.char)(nil))))[:len(ss):len(ss)]
+	arr := cslice[*C.char](a, len(ss))
 	for i, s := range ss {
 		arr[i] = a.cstr(s)
 	}
-	return &arr[0]
+	return ptr(arr)
 }
 
 func (a *arena) kvs(m map[string]string) (*C.esc_kv, C.int32_t) {
-	arr := (*[1 << 28]C.esc_kv)(a.alloc(len(m), C.sizeof_esc_kv))[:len(m):len(m)]
+	arr := cslice[C.esc_kv](a, len(m))
 	i := 0
 	for k, v := range m { // map order is irrelevant: pairs are interned and de-duplicated
 		arr[i].key = a.cstr(k)
 		arr[i].value = a.cstr(v)
 		i++
 	}
-	return &arr[0], C.int32_t(len(m))
+	return ptr(arr), C.int32_t(len(m))
 }
 
 // request copies one ResourceList: cpu as MilliValue, memory as Value, with presence flags
@@ -127,11 +146,11 @@ func request(rl v1.ResourceList) C.esc_request {
 }
 
 func (a *arena) requests(cs []v1.Container) (*C.esc_request, C.int32_t) {
-	arr := (*[1 << 28]C.esc_request)(a.alloc(len(cs), C.sizeof_esc_request))[:len(cs):len(cs)]
+	arr := cslice[C.esc_request](a, len(cs))
 	for i := range cs {
 		arr[i] = request(cs[i].Resources.Requests) // types.go:74-83
 	}
-	return &arr[0], C.int32_t(len(cs))
+	return ptr(arr), C.int32_t(len(cs))
 }
 
 // podObj copies the fields the hot path reads from a pod (esc_pod_obj).
@@ -176,9 +195,9 @@ func (a *arena) podObj(p *v1.Pod, o *C.esc_pod_obj) {
 			}
 		}
 	}
-	arr := (*[1 << 28]C.esc_selector_expr)(a.alloc(len(exprs), C.sizeof_esc_selector_expr))[:len(exprs):len(exprs)]
+	arr := cslice[C.esc_selector_expr](a, len(exprs))
 	copy(arr, exprs)
-	o.exprs = &arr[0]
+	o.exprs = ptr(arr)
 	o.n_exprs = C.int32_t(len(exprs))
 	o.containers, o.n_containers = a.requests(p.Spec.Containers)
 	o.init_containers, o.n_init_containers = a.requests(p.Spec.InitContainers)
@@ -206,19 +225,19 @@ func (a *arena) nodeObj(n *v1.Node, o *C.esc_node_obj) {
 }
 
 func (a *arena) pods(pods []*v1.Pod) (*C.esc_pod_obj, C.int64_t) {
-	objs := (*[1 << 28]C.esc_pod_obj)(a.alloc(len(pods), C.sizeof_esc_pod_obj))[:len(pods):len(pods)]
+	objs := cslice[C.esc_pod_obj](a, len(pods))
 	for i, p := range pods {
 		a.podObj(p, &objs[i])
 	}
-	return &objs[0], C.int64_t(len(pods))
+	return ptr(objs), C.int64_t(len(pods))
 }
 
 func (a *arena) nodes(nodes []*v1.Node) (*C.esc_node_obj, C.int64_t) {
-	objs := (*[1 << 28]C.esc_node_obj)(a.alloc(len(nodes), C.sizeof_esc_node_obj))[:len(nodes):len(nodes)]
+	objs := cslice[C.esc_node_obj](a, len(nodes))
 	for i, n := range nodes {
 		a.nodeObj(n, &objs[i])
 	}
-	return &objs[0], C.int64_t(len(nodes))
+	return ptr(objs), C.int64_t(len(nodes))
 }
 
 // ---------------------------------------------------------------------- context
@@ -269,8 +288,35 @@ type Context struct {
 // NewContext creates the context for groups (fixed for its lifetime, client.go:55-64).
 // rank/world describe the sharding when one process drives each GPU.
 func NewContext(groups []GroupSpec, device, rank, world int) (*Context, error) {
+	return newContext(groups, func(specs *C.esc_group_spec, n C.int32_t, out **C.esc_ctx) C.int32_t {
+		return C.esc_ctx_create(specs, n, C.int32_t(device), C.int32_t(rank), C.int32_t(world), out)
+	})
+}
+
+// NewContextMulti creates ONE context driving every listed GPU from this process
+// (esc_ctx_create_multi): the pods are sharded over the devices, each owns the node side
+// of a range of groups, and RunOnce's exchange is an ncclAllReduce per device inside one
+// RCCL group call — the reference stays one process with one informer set
+// (cmd/main.go:187, controller.go:416-445).
+func NewContextMulti(groups []GroupSpec, devices []int) (*Context, error) {
+	if len(devices) == 0 {
+		return nil, fmt.Errorf("escalatorhip: no devices")
+	}
+	dev := make([]C.int32_t, len(devices))
+	for i, d := range devices {
+		dev[i] = C.int32_t(d)
+	}
+	return newContext(groups, func(specs *C.esc_group_spec, n C.int32_t, out **C.esc_ctx) C.int32_t {
+		return C.esc_ctx_create_multi(specs, n, ptr(dev), C.int32_t(len(dev)), out)
+	})
+}
+
+func newContext(groups []GroupSpec, create func(*C.esc_group_spec, C.int32_t, **C.esc_ctx) C.int32_t) (*Context, error) {
+	if len(groups) == 0 {
+		return nil, fmt.Errorf("escalatorhip: no node groups")
+	}
 	x := &Context{groups: groups}
-	specs := (*[1 << 20]C.esc_group_spec)(x.names.alloc(len(groups), C.sizeof_esc_group_spec))[:len(groups):len(groups)]
+	specs := cslice[C.esc_group_spec](&x.names, len(groups))
 	for i, g := range groups {
 		s := &specs[i]
 		s.name = x.names.cstr(g.Name)
@@ -287,8 +333,8 @@ func NewContext(groups []GroupSpec, device, rank, world int) (*Context, error) {
 			s.dry_mode = 1
 		}
 	}
-	x.cspecs = unsafe.Pointer(&specs[0])
-	rc := C.esc_ctx_create(&specs[0], C.int32_t(len(groups)), C.int32_t(device), C.int32_t(rank), C.int32_t(world), &x.c)
+	x.cspecs = unsafe.Pointer(ptr(specs))
+	rc := create(ptr(specs), C.int32_t(len(groups)), &x.c)
 	if rc != C.ESC_OK {
 		x.names.free()
 		return nil, rcErr("esc_ctx_create", rc)
@@ -346,15 +392,15 @@ func (x *Context) pack(pods []*v1.Pod, nodes []*v1.Node, trackers map[int][]stri
 }
 
 // Load replaces the resident snapshot with the listers' current pods and nodes (this
-// rank's pod shard starting at global index podOffset; the full node list, of which the
-// ordering covers [nodeLo, nodeHi)).  trackers holds the dry-mode groups' taintTracker.
-func (x *Context) Load(pods []*v1.Pod, podOffset int64, nodes []*v1.Node, nodeLo, nodeHi int64,
-	trackers map[int][]string) error {
+// rank's pod shard starting at global index podOffset — every pod for a NewContextMulti
+// context — and the full node list, which every rank holds).  trackers holds the dry-mode
+// groups' taintTracker.
+func (x *Context) Load(pods []*v1.Pod, podOffset int64, nodes []*v1.Node, trackers map[int][]string) error {
 	return x.pack(pods, nodes, trackers, false, func(ps *C.esc_pod_soa, ns *C.esc_node_soa) error {
 		if rc := C.esc_load_pods(x.c, ps, C.int64_t(podOffset)); rc != C.ESC_OK {
 			return rcErr("esc_load_pods", rc)
 		}
-		return rcErr("esc_load_nodes", C.esc_load_nodes(x.c, ns, C.int64_t(nodeLo), C.int64_t(nodeHi)))
+		return rcErr("esc_load_nodes", C.esc_load_nodes(x.c, ns, 0, ns.n_nodes))
 	})
 }
 
@@ -383,7 +429,7 @@ func (x *Context) RunOnce(states []GroupState) ([]Decision, error) {
 		cst[g].cached_cpu_m = C.int64_t(s.CachedCPUMilli)
 		cst[g].cached_mem_b = C.int64_t(s.CachedMemBytes)
 	}
-	if rc := C.esc_set_state(x.c, &cst[0]); rc != C.ESC_OK {
+	if rc := C.esc_set_state(x.c, ptr(cst)); rc != C.ESC_OK {
 		return nil, rcErr("esc_set_state", rc)
 	}
 	if rc := C.esc_step(x.c); rc != C.ESC_OK {
@@ -394,7 +440,7 @@ func (x *Context) RunOnce(states []GroupState) ([]Decision, error) {
 	}
 	tot := make([]C.esc_group_totals, G)
 	dec := make([]C.esc_group_decision, G)
-	if rc := C.esc_results(x.c, &tot[0], &dec[0]); rc != C.ESC_OK {
+	if rc := C.esc_results(x.c, ptr(tot), ptr(dec)); rc != C.ESC_OK {
 		return nil, rcErr("esc_results", rc)
 	}
 	out := make([]Decision, G)
@@ -412,9 +458,9 @@ func (x *Context) RunOnce(states []GroupState) ([]Decision, error) {
 		}
 		if d.taint_status == C.ESC_ST_ERR_TAINT_MIN { // scale_down.go:150-154
 			buf := make([]byte, 160)
-			C.esc_taint_error(t.n_untainted, C.int32_t(x.groups[g].MinNodes), (*C.char)(unsafe.Pointer(&buf[0])),
+			C.esc_taint_error(t.n_untainted, C.int32_t(x.groups[g].MinNodes), (*C.char)(unsafe.Pointer(ptr(buf))),
 				C.int32_t(len(buf)))
-			out[g].TaintErr = errors.New(C.GoString((*C.char)(unsafe.Pointer(&buf[0]))))
+			out[g].TaintErr = errors.New(C.GoString((*C.char)(unsafe.Pointer(ptr(buf)))))
 		}
 	}
 	return out, nil
@@ -434,7 +480,7 @@ func (x *Context) Order(g int, oldest bool, n int) ([]int64, error) {
 	}
 	idx := make([]int64, n+1)
 	var got C.int64_t
-	rc := C.esc_group_order(x.c, C.int32_t(g), which, (*C.int64_t)(unsafe.Pointer(&idx[0])), C.int64_t(n), &got)
+	rc := C.esc_group_order(x.c, C.int32_t(g), which, (*C.int64_t)(unsafe.Pointer(ptr(idx))), C.int64_t(n), &got)
 	if rc != C.ESC_OK {
 		return nil, rcErr("esc_group_order", rc)
 	}
@@ -496,7 +542,7 @@ func CalcScaleUpDelta(untainted int, cpuPercent, memPercent float64, cpuRequest,
 // CommUniqueID is called on rank 0; its bytes go to every other rank over any host channel.
 func CommUniqueID() ([]byte, error) {
 	id := make([]byte, C.ESC_COMM_ID_BYTES)
-	rc := C.esc_comm_unique_id(unsafe.Pointer(&id[0]))
+	rc := C.esc_comm_unique_id(unsafe.Pointer(ptr(id)))
 	return id, rcErr("esc_comm_unique_id", rc)
 }
 
@@ -516,11 +562,14 @@ func (x *Context) CommInit(id []byte, rank, world int) error {
 var ErrReload = errors.New(C.GoString(C.esc_strerror(C.ESC_E_LIMIT)))
 
 func (x *Context) PodsUpsert(ids []int64, pods []*v1.Pod) error {
-	if len(ids) != len(pods) || len(ids) == 0 {
+	if len(ids) != len(pods) {
+		return fmt.Errorf("escalatorhip: %d ids for %d pods", len(ids), len(pods))
+	}
+	if len(ids) == 0 {
 		return nil
 	}
 	return x.pack(pods, nil, nil, false, func(ps *C.esc_pod_soa, _ *C.esc_node_soa) error {
-		rc := C.esc_pods_upsert(x.c, (*C.int64_t)(unsafe.Pointer(&ids[0])), ps)
+		rc := C.esc_pods_upsert(x.c, (*C.int64_t)(unsafe.Pointer(ptr(ids))), ps)
 		if rc == C.ESC_E_LIMIT {
 			return ErrReload
 		}
@@ -530,21 +579,18 @@ func (x *Context) PodsUpsert(ids []int64, pods []*v1.Pod) error {
 
 // PodsDelete removes pods by snapshot index.
 func (x *Context) PodsDelete(ids []int64) error {
-	if len(ids) == 0 {
-		return nil
-	}
-	return rcErr("esc_pods_delete", C.esc_pods_delete(x.c, (*C.int64_t)(unsafe.Pointer(&ids[0])), C.int64_t(len(ids))))
+	return rcErr("esc_pods_delete", C.esc_pods_delete(x.c, (*C.int64_t)(unsafe.Pointer(ptr(ids))), C.int64_t(len(ids))))
 }
 
 // NodesUpdate applies node watch events that change Spec.Unschedulable, the escalator
 // taint or Status.Allocatable (flags are ESC_NF_* bits).
 func (x *Context) NodesUpdate(ids []int64, flags []uint32, cpuMilli, memBytes []int64) error {
-	if len(ids) == 0 {
-		return nil
+	if len(flags) != len(ids) || len(cpuMilli) != len(ids) || len(memBytes) != len(ids) {
+		return fmt.Errorf("escalatorhip: NodesUpdate needs one flags / cpu / memory entry per id")
 	}
-	return rcErr("esc_nodes_update", C.esc_nodes_update(x.c, (*C.int64_t)(unsafe.Pointer(&ids[0])), C.int64_t(len(ids)),
-		(*C.uint32_t)(unsafe.Pointer(&flags[0])), (*C.int64_t)(unsafe.Pointer(&cpuMilli[0])),
-		(*C.int64_t)(unsafe.Pointer(&memBytes[0]))))
+	return rcErr("esc_nodes_update", C.esc_nodes_update(x.c, (*C.int64_t)(unsafe.Pointer(ptr(ids))), C.int64_t(len(ids)),
+		(*C.uint32_t)(unsafe.Pointer(ptr(flags))), (*C.int64_t)(unsafe.Pointer(ptr(cpuMilli))),
+		(*C.int64_t)(unsafe.Pointer(ptr(memBytes)))))
 }
 
 // NodesAdd applies node Add events (cache.go:37-56): the nodes are packed and appended at
@@ -555,7 +601,7 @@ func (x *Context) NodesAdd(nodes []*v1.Node) ([]int64, error) {
 		return nil, nil
 	}
 	err := x.pack(nil, nodes, nil, false, func(_ *C.esc_pod_soa, ns *C.esc_node_soa) error {
-		rc := C.esc_nodes_add(x.c, ns, (*C.int64_t)(unsafe.Pointer(&ids[0])))
+		rc := C.esc_nodes_add(x.c, ns, (*C.int64_t)(unsafe.Pointer(ptr(ids))))
 		if rc == C.ESC_E_LIMIT {
 			return ErrReload
 		}
@@ -566,20 +612,17 @@ func (x *Context) NodesAdd(nodes []*v1.Node) ([]int64, error) {
 
 // NodesDelete applies node Delete events by snapshot index.
 func (x *Context) NodesDelete(ids []int64) error {
-	if len(ids) == 0 {
-		return nil
-	}
-	return rcErr("esc_nodes_delete", C.esc_nodes_delete(x.c, (*C.int64_t)(unsafe.Pointer(&ids[0])), C.int64_t(len(ids))))
+	return rcErr("esc_nodes_delete", C.esc_nodes_delete(x.c, (*C.int64_t)(unsafe.Pointer(ptr(ids))), C.int64_t(len(ids))))
 }
 
 // PodsBind records Spec.NodeName changes (the scheduler bound a pod, or it left its node):
 // node snapshot indices, 0xFFFFFFFF for none.  ErrReload when a node's run is full
 // (LoadPlacement again).
 func (x *Context) PodsBind(ids []int64, nodeIdx []uint32) error {
-	if len(ids) == 0 || len(ids) != len(nodeIdx) {
-		return nil
+	if len(ids) != len(nodeIdx) {
+		return fmt.Errorf("escalatorhip: %d ids for %d node indices", len(ids), len(nodeIdx))
 	}
-	rc := C.esc_pods_bind(x.c, (*C.int64_t)(unsafe.Pointer(&ids[0])), (*C.uint32_t)(unsafe.Pointer(&nodeIdx[0])),
+	rc := C.esc_pods_bind(x.c, (*C.int64_t)(unsafe.Pointer(ptr(ids))), (*C.uint32_t)(unsafe.Pointer(ptr(nodeIdx))),
 		C.int64_t(len(ids)))
 	if rc == C.ESC_E_LIMIT {
 		return ErrReload
@@ -590,13 +633,7 @@ func (x *Context) PodsBind(ids []int64, nodeIdx []uint32) error {
 // TrackerUpdate applies one dry-mode group's taintTracker change in place: taintOldestN
 // appends (scale_down.go:197-200), untaintNewestN deletes (scale_up.go:146-158).
 func (x *Context) TrackerUpdate(g int, add, remove []int64) error {
-	var pa, pr *C.int64_t
-	if len(add) > 0 {
-		pa = (*C.int64_t)(unsafe.Pointer(&add[0]))
-	}
-	if len(remove) > 0 {
-		pr = (*C.int64_t)(unsafe.Pointer(&remove[0]))
-	}
+	pa, pr := (*C.int64_t)(unsafe.Pointer(ptr(add))), (*C.int64_t)(unsafe.Pointer(ptr(remove)))
 	return rcErr("esc_tracker_update", C.esc_tracker_update(x.c, C.int32_t(g), pa, C.int64_t(len(add)), pr,
 		C.int64_t(len(remove))))
 }
@@ -612,21 +649,34 @@ type Removal struct {
 // 0xFFFFFFFF when empty or unknown — CreateNodeNameToInfoMap drops those, node_state.go:27-36)
 // and gives each node its escalator-taint time (GetToBeRemovedTime, taint.go:91) and its
 // no-delete annotation (scale_down.go:39-46).
+// podNode may be nil to refresh the per-node facts only (the binding is kept current by
+// PodsUpsert / PodsDelete / PodsBind).  The library reads one entry per pod id and per node
+// slot (esc_ctx_counts), so shorter slices are refused here instead of being over-read.
 func (x *Context) LoadPlacement(podNode []uint32, taintUnixS []int64, noDelete []uint8) error {
-	var pn *C.uint32_t
-	if len(podNode) > 0 {
-		pn = (*C.uint32_t)(unsafe.Pointer(&podNode[0]))
+	var nPods, nNodes C.int64_t
+	if rc := C.esc_ctx_counts(x.c, &nPods, &nNodes); rc != C.ESC_OK {
+		return rcErr("esc_ctx_counts", rc)
 	}
-	return rcErr("esc_load_placement", C.esc_load_placement(x.c, pn, (*C.int64_t)(unsafe.Pointer(&taintUnixS[0])),
-		(*C.uint8_t)(unsafe.Pointer(&noDelete[0]))))
+	if podNode != nil && int64(len(podNode)) != int64(nPods) {
+		return fmt.Errorf("escalatorhip: LoadPlacement: %d pod entries for %d pod ids", len(podNode), nPods)
+	}
+	if int64(len(taintUnixS)) != int64(nNodes) || int64(len(noDelete)) != int64(nNodes) {
+		return fmt.Errorf("escalatorhip: LoadPlacement: %d taint times / %d no-delete flags for %d nodes",
+			len(taintUnixS), len(noDelete), nNodes)
+	}
+	return rcErr("esc_load_placement", C.esc_load_placement(x.c, (*C.uint32_t)(unsafe.Pointer(ptr(podNode))),
+		(*C.int64_t)(unsafe.Pointer(ptr(taintUnixS))), (*C.uint8_t)(unsafe.Pointer(ptr(noDelete)))))
 }
 
 // TryRemove evaluates TryRemoveTaintedNodes for every group at once; DeleteList(g) gives
 // the group's toBeDeleted nodes in the reference's order.
 func (x *Context) TryRemove(nowUnixNano int64, softGraceNs, hardGraceNs []int64) ([]Removal, error) {
+	if len(softGraceNs) != len(x.groups) || len(hardGraceNs) != len(x.groups) {
+		return nil, fmt.Errorf("escalatorhip: TryRemove needs one soft / hard grace period per group (%d)", len(x.groups))
+	}
 	out := make([]C.esc_removal, len(x.groups))
-	rc := C.esc_try_remove(x.c, C.int64_t(nowUnixNano), (*C.int64_t)(unsafe.Pointer(&softGraceNs[0])),
-		(*C.int64_t)(unsafe.Pointer(&hardGraceNs[0])), &out[0])
+	rc := C.esc_try_remove(x.c, C.int64_t(nowUnixNano), (*C.int64_t)(unsafe.Pointer(ptr(softGraceNs))),
+		(*C.int64_t)(unsafe.Pointer(ptr(hardGraceNs))), ptr(out))
 	if rc != C.ESC_OK {
 		return nil, rcErr("esc_try_remove", rc)
 	}
@@ -641,7 +691,7 @@ func (x *Context) TryRemove(nowUnixNano int64, softGraceNs, hardGraceNs []int64)
 func (x *Context) DeleteList(g int, n int64) ([]int64, error) {
 	idx := make([]int64, n+1)
 	var got C.int64_t
-	rc := C.esc_removal_nodes(x.c, C.int32_t(g), (*C.int64_t)(unsafe.Pointer(&idx[0])), C.int64_t(n), &got)
+	rc := C.esc_removal_nodes(x.c, C.int32_t(g), (*C.int64_t)(unsafe.Pointer(ptr(idx))), C.int64_t(n), &got)
 	if rc != C.ESC_OK {
 		return nil, rcErr("esc_removal_nodes", rc)
 	}

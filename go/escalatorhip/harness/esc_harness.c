@@ -7,6 +7,8 @@
  * host would run is exercised end to end:
  *
  *   NewContext          esc_ctx_create
+ *   NewContextMulti     esc_ctx_create_multi (argv[2] = number of shards: the device of
+ *                       the input listed that many times, the peer exchange on one GPU)
  *   (*Context).Load     esc_packer_create, esc_packer_add_pods, esc_packer_add_nodes,
  *                       esc_packer_set_tracker (dry-mode groups), esc_packer_view,
  *                       esc_load_pods, esc_load_nodes, esc_packer_destroy
@@ -94,6 +96,10 @@ static void* cal(size_t n, size_t sz) {
     return p;
 }
 
+/* Arrays handed to the library: NULL when empty, as the cgo shim's ptr() passes them (the
+ * ABI takes NULL with a zero count for every array). */
+static void* arr(size_t n, size_t sz) { return n ? cal(n, sz) : NULL; }
+
 static esc_request req(rd_t* r) {
     esc_request q;
     q.cpu_m = num(r);
@@ -107,13 +113,13 @@ static esc_request req(rd_t* r) {
 static void read_pod(rd_t* r, esc_pod_obj* o) {
     memset(o, 0, sizeof(*o));
     o->n_owner_kinds = (int32_t)num(r);
-    const char** kinds = cal((size_t)o->n_owner_kinds, sizeof(char*));
+    const char** kinds = arr((size_t)o->n_owner_kinds, sizeof(char*));
     for (int i = 0; i < o->n_owner_kinds; i++) kinds[i] = str(r);
     o->owner_kinds = kinds;
     o->has_config_source = (int32_t)num(r);
     o->config_source = str(r);
     o->n_node_selector = (int32_t)num(r);
-    esc_kv* sel = cal((size_t)o->n_node_selector, sizeof(esc_kv));
+    esc_kv* sel = arr((size_t)o->n_node_selector, sizeof(esc_kv));
     for (int i = 0; i < o->n_node_selector; i++) { sel[i].key = str(r); sel[i].value = str(r); }
     o->node_selector = sel;
     o->has_affinity = (int32_t)num(r);
@@ -122,23 +128,23 @@ static void read_pod(rd_t* r, esc_pod_obj* o) {
     o->has_pod_anti_affinity = (int32_t)num(r);
     o->has_required = (int32_t)num(r);
     o->n_exprs = (int32_t)num(r);
-    esc_selector_expr* ex = cal((size_t)o->n_exprs, sizeof(esc_selector_expr));
+    esc_selector_expr* ex = arr((size_t)o->n_exprs, sizeof(esc_selector_expr));
     for (int i = 0; i < o->n_exprs; i++) {
         ex[i].key = str(r);
         ex[i].op = str(r);
         ex[i].n_values = (int32_t)num(r);
-        const char** vals = cal((size_t)ex[i].n_values, sizeof(char*));
+        const char** vals = arr((size_t)ex[i].n_values, sizeof(char*));
         for (int v = 0; v < ex[i].n_values; v++) vals[v] = str(r);
         ex[i].values = vals;
         ex[i].term = (int32_t)num(r);
     }
     o->exprs = ex;
     o->n_containers = (int32_t)num(r);
-    esc_request* cs = cal((size_t)o->n_containers, sizeof(esc_request));
+    esc_request* cs = arr((size_t)o->n_containers, sizeof(esc_request));
     for (int i = 0; i < o->n_containers; i++) cs[i] = req(r);
     o->containers = cs;
     o->n_init_containers = (int32_t)num(r);
-    esc_request* ic = cal((size_t)o->n_init_containers, sizeof(esc_request));
+    esc_request* ic = arr((size_t)o->n_init_containers, sizeof(esc_request));
     for (int i = 0; i < o->n_init_containers; i++) ic[i] = req(r);
     o->init_containers = ic;
     o->has_overhead = (int32_t)num(r);
@@ -149,12 +155,12 @@ static void read_node(rd_t* r, esc_node_obj* o) {
     memset(o, 0, sizeof(*o));
     o->name = str(r);
     o->n_labels = (int32_t)num(r);
-    esc_kv* lb = cal((size_t)o->n_labels, sizeof(esc_kv));
+    esc_kv* lb = arr((size_t)o->n_labels, sizeof(esc_kv));
     for (int i = 0; i < o->n_labels; i++) { lb[i].key = str(r); lb[i].value = str(r); }
     o->labels = lb;
     o->unschedulable = (int32_t)num(r);
     o->n_taints = (int32_t)num(r);
-    const char** tk = cal((size_t)o->n_taints, sizeof(char*));
+    const char** tk = arr((size_t)o->n_taints, sizeof(char*));
     for (int i = 0; i < o->n_taints; i++) tk[i] = str(r);
     o->taint_keys = tk;
     o->allocatable = req(r);
@@ -188,7 +194,9 @@ static uint64_t bits(double d) {
 }
 
 int main(int argc, char** argv) {
-    if (argc != 2) die("usage: esc_harness <input>");
+    if (argc != 2 && argc != 3) die("usage: esc_harness <input> [shards]");
+    const int32_t shards = argc == 3 ? (int32_t)atoi(argv[2]) : 0;
+    if (argc == 3 && (shards < 1 || shards > 16)) die("shards must be 1..16");
     FILE* f = fopen(argv[1], "rb");
     if (!f) die("cannot open input");
     rd_t r = {0};
@@ -228,11 +236,11 @@ int main(int argc, char** argv) {
     }
     expect(&r, "pods");
     int64_t P = num(&r);
-    esc_pod_obj* pods = cal((size_t)P, sizeof(esc_pod_obj));
+    esc_pod_obj* pods = arr((size_t)P, sizeof(esc_pod_obj));
     for (int64_t i = 0; i < P; i++) read_pod(&r, &pods[i]);
     expect(&r, "nodes");
     int64_t N = num(&r);
-    esc_node_obj* nodes = cal((size_t)N, sizeof(esc_node_obj));
+    esc_node_obj* nodes = arr((size_t)N, sizeof(esc_node_obj));
     for (int64_t i = 0; i < N; i++) read_node(&r, &nodes[i]);
     expect(&r, "trackers");
     int32_t T = (int32_t)num(&r);
@@ -242,7 +250,7 @@ int main(int argc, char** argv) {
     for (int t = 0; t < T; t++) {
         trk_group[t] = (int32_t)num(&r);
         trk_n[t] = num(&r);
-        trk_names[t] = cal((size_t)trk_n[t], sizeof(char*));
+        trk_names[t] = arr((size_t)trk_n[t], sizeof(char*));
         for (int64_t i = 0; i < trk_n[t]; i++) trk_names[t][i] = str(&r);
     }
     expect(&r, "end");
@@ -250,10 +258,18 @@ int main(int argc, char** argv) {
     if (esc_abi_version() != ESC_ABI_VERSION) die("ABI version mismatch");
     printf("abi %d\n", esc_abi_version());
 
-    /* NewContext */
+    /* NewContext / NewContextMulti */
     esc_ctx* ctx = NULL;
-    int32_t rc = esc_ctx_create(groups, G, device, 0, 1, &ctx);
-    if (device_call("esc_ctx_create", rc)) return 0;
+    int32_t rc;
+    if (shards) {
+        int32_t devs[16];
+        for (int i = 0; i < shards; i++) devs[i] = device;
+        rc = esc_ctx_create_multi(groups, G, devs, shards, &ctx);
+        if (device_call("esc_ctx_create_multi", rc)) return 0;
+    } else {
+        rc = esc_ctx_create(groups, G, device, 0, 1, &ctx);
+        if (device_call("esc_ctx_create", rc)) return 0;
+    }
 
     /* scalar math (calcPercentUsage / calcScaleUpDelta): host-only, runs without a device */
     {

@@ -13,9 +13,13 @@
  *     are carried as ESC_ST_* codes whose esc_status_string() is the reference's text
  *     verbatim.
  *   - Caller-owned input arrays are read during the call only and never retained (the
- *     cgo pointer-passing rule).  Outputs go to caller-allocated buffers.
- *   - One esc_ctx per process / device, driven from one thread (the reference's RunOnce
- *     is a single goroutine, pkg/controller/controller.go:416).
+ *     cgo pointer-passing rule).  Outputs go to caller-allocated buffers.  Every array
+ *     argument (and every array inside the object / SoA structs) may be NULL when its
+ *     count is 0.
+ *   - An esc_ctx is driven from one thread (the reference's RunOnce is a single
+ *     goroutine, pkg/controller/controller.go:416).  Either one context per device and
+ *     process (esc_ctx_create + esc_comm_init), or one context for several devices in one
+ *     process (esc_ctx_create_multi: the fan-out and the exchange are internal).
  *
  * Hot path: group membership (a1-a7), per-pod effective requests (a8),
  * per-group int64 sums (a9, a10), node classification (a11), first-node capacity (a12),
@@ -32,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ESC_ABI_VERSION 3
+#define ESC_ABI_VERSION 4
 
 /* ---------------------------------------------------------------- return codes */
 #define ESC_OK          0
@@ -288,13 +292,29 @@ int32_t     esc_taint_error(int64_t n_untainted, int32_t min_nodes, char* buf, i
 /* ------------------------------------------------------------------- context
  * Groups are fixed for the context's lifetime (the reference builds its listers once,
  * pkg/controller/client.go:55-64).  rank/world describe the sharding when one process
- * drives each GPU; the per-group int64 exchange itself is done by the caller's
- * collective (RCCL via torch.distributed, or ncclAllReduce in a cgo host) on the
- * buffers returned by esc_exchange_buffers.                                         */
+ * drives each GPU: rank r holds a contiguous shard of the pods and the whole node table,
+ * of which it reduces and orders the node side of the group pairs it owns (a contiguous
+ * pair range balanced by node entries, the same split on every rank: esc_group_owner,
+ * DESIGN.md §7).  The per-group words are summed across ranks inside the library
+ * (esc_comm_init + esc_step) or by the caller's collective on esc_exchange_buffers.
+ * device < 0 creates a host-only context (packer, scalar math, esc_node_owner_ranges). */
 typedef struct esc_ctx esc_ctx;
 
 int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t device,
                        int32_t rank, int32_t world, esc_ctx** out);
+/* One context driving n_dev devices from one thread: rank i of n_dev on
+ * devices[i], one communicator set from ncclCommInitAll, and every call below fanned out
+ * internally — esc_load_pods splits the pods into n_dev contiguous shards, esc_step /
+ * esc_run enqueue every device's shard step, the ncclAllReduce of the exchange words inside
+ * ncclGroupStart / ncclGroupEnd and every device's decision; pod events are routed to the
+ * shard holding the id, node events reach every device; esc_group_order answers from the
+ * owner device.  The per-device calls esc_reduce, esc_exchange*, esc_decide, esc_comm_init,
+ * esc_reap_* and esc_ctx_set_stream return ESC_E_STATE on it.  A device listed twice (or
+ * ESC_EXCHANGE=peer) selects the peer exchange instead of RCCL: every device sums the others'
+ * words over peer-mapped memory (a one-GPU machine runs several shards this way).
+ * Replaces the sequential per-group loop of RunOnce, pkg/controller/controller.go:416-445. */
+int32_t esc_ctx_create_multi(const esc_group_spec* groups, int32_t n_groups, const int32_t* devices,
+                             int32_t n_dev, esc_ctx** out);
 int32_t esc_ctx_destroy(esc_ctx* ctx);
 int32_t esc_ctx_set_stream(esc_ctx* ctx, void* hip_stream);   /* NULL = ctx-owned stream */
 int32_t esc_ctx_num_groups(const esc_ctx* ctx);
@@ -323,10 +343,10 @@ int32_t esc_packer_view(esc_packer* pk, esc_pod_soa* pods, esc_node_soa* nodes);
 
 /* -------------------------------------------------------------- device snapshot
  * esc_load_pods: copies this rank's pod shard (global pod indices [offset, offset+n)).
- * esc_load_nodes: copies the full node table and builds its pair-major index (one
- *   entry per (label pair, node), sorted by pair then node — DESIGN.md §3); the
- *   decision reduces this rank's 1/world share of the index; the ordering (K5)
- *   streams nodes [lo, hi).                                                         */
+ * esc_load_nodes: copies the full node table (lo = 0, hi = n_nodes: every rank holds it)
+ *   and builds its pair-major index (one entry per (label pair, node), sorted by pair then
+ *   node — DESIGN.md §3); the decision reduces the pieces of the pairs this rank owns, and
+ *   the age index (K5) lists the memberships of their groups.                        */
 int32_t esc_load_pods(esc_ctx* ctx, const esc_pod_soa* pods, int64_t global_offset);
 int32_t esc_load_nodes(esc_ctx* ctx, const esc_node_soa* nodes, int64_t lo, int64_t hi);
 /* Number of device-resident copies of the pod shard to rotate through on successive
@@ -335,14 +355,24 @@ int32_t esc_set_replicas(esc_ctx* ctx, int32_t n_replicas);
 /* Algorithmic HBM bytes one decision streams on this rank: K1 (pod shard) and K2
  * (this rank's node index share).  DESIGN.md §6; cross-checked by escalator_amd/layout.py. */
 int32_t esc_stream_bytes(const esc_ctx* ctx, int64_t* pod_bytes, int64_t* node_bytes);
+/* Sizes a host's per-pod and per-node arrays must match (esc_load_placement): pod ids
+ * (esc_load_pods' count plus inserted ids) and node snapshot slots (loaded + added). */
+int32_t esc_ctx_counts(const esc_ctx* ctx, int64_t* n_pod_ids, int64_t* n_nodes);
+/* The rank that owns `group`'s node side: its totals' node words, its orderings
+ * (esc_group_order answers on that rank; the others report 0 members). */
+int32_t esc_group_owner(const esc_ctx* ctx, int32_t group, int32_t* rank);
+/* The owner split as esc_load_nodes computes it, on the host only (no device needed):
+ * q_bounds[r] = first group pair of rank r, q_bounds[world] = number of group pairs. */
+int32_t esc_node_owner_ranges(const esc_ctx* ctx, const esc_node_soa* nodes, int32_t world, uint32_t* q_bounds);
 
 /* ------------------------------------------------------------ scale decision
  * esc_reduce     : async. Per-shard group totals (K1 pods + K2 nodes + combine).
  * esc_exchange_buffers: device buffers to all-reduce between esc_reduce and esc_decide:
  *                  sum_buf  int64[sum_count]  with op SUM: the pods' per-group words
- *                  (G x 5: cpu and memory split lo32 / hi, count),
+ *                  (G x 5: cpu and memory split lo32 / hi, count), then the node words
+ *                  (G x 4, exact on the group's owner rank and zero elsewhere),
  *                  min_buf  int64[min_count]  with op MIN (min_count 0 = nothing to
- *                  exchange: every rank reduces the whole node index and resolves
+ *                  exchange: every rank holds the whole node table and resolves
  *                  allNodes[0] from it, so min_buf is NULL).
  * esc_decide     : async. K4 decide on the (exchanged) totals; results land in the
  *                  context's host buffers after esc_sync.
@@ -378,6 +408,8 @@ int32_t esc_comm_unique_id(void* id_out);
 int32_t esc_comm_init(esc_ctx* ctx, const void* id, int32_t rank, int32_t world);
 int32_t esc_exchange(esc_ctx* ctx);
 int32_t esc_step(esc_ctx* ctx);
+/* Ranks of the context's communicator (ncclCommCount; a multi-device context: its devices). */
+int32_t esc_comm_size(const esc_ctx* ctx, int32_t* ranks);
 int32_t esc_results(esc_ctx* ctx, esc_group_totals* totals, esc_group_decision* decisions);
 /* Metric gauges (§8f): computed by K4 beside the decisions when enabled (off by default;
  * they stay in device memory until esc_metrics_results copies them out, after esc_sync). */
@@ -424,7 +456,9 @@ int32_t esc_nodes_update(esc_ctx* ctx, const int64_t* ids, int64_t n, const uint
  * becomes ESC_NF_ABSENT (no kernel counts it, allNodes[0] moves to the group's next
  * member) and its dry-mode tracker entries are dropped (a host that re-adds a tracked
  * name re-applies it with esc_tracker_update).  Both invalidate esc_load_placement; an
- * add that does not fit returns ESC_E_LIMIT with nothing applied (reload). */
+ * add that does not fit returns ESC_E_LIMIT with nothing applied (reload).  Every check
+ * depends on the node table alone, which every rank holds, so all ranks of a sharded job
+ * accept or refuse the same batch. */
 int32_t esc_nodes_add(esc_ctx* ctx, const esc_node_soa* nodes, int64_t* ids_out);
 int32_t esc_nodes_delete(esc_ctx* ctx, const int64_t* ids, int64_t n);
 
@@ -496,10 +530,11 @@ int32_t esc_removal_nodes(esc_ctx* ctx, int32_t group, int64_t* idx_out, int64_t
  * esc_build_age_index rebuilds the index (snapshot ingestion; exposed for measurement). */
 int32_t esc_sort_nodes(esc_ctx* ctx);
 /* Include the per-decision ordering in every decision (esc_run / esc_reduce / esc_step):
- * it runs on the side stream beside K1 (it reads node flags only) and is captured in the
- * decision's graph; esc_group_order is then valid after each decision without a separate
- * esc_sort_nodes (one decision = membership, sums, percentages, deltas
- * and oldest-first ordering). */
+ * the packed small groups are ordered by blocks of the step's fused tail launch (after K1,
+ * beside the fold and K2), the larger groups by the split kernels right after it, all on
+ * the context's one stream (and in its graph when esc_use_graph); esc_group_order is then
+ * valid after each decision without a separate esc_sort_nodes (one
+ * decision = membership, sums, percentages, deltas and oldest-first ordering). */
 int32_t esc_set_order_in_step(esc_ctx* ctx, int32_t enable);
 int32_t esc_build_age_index(esc_ctx* ctx);
 /* Size of the ordering problem: memberships of the node range and the bit width of the
@@ -554,6 +589,10 @@ int32_t esc_synth_destroy(esc_synth* s);
 int32_t esc_synth_groups(const esc_synth* s, const esc_group_spec** groups, int32_t* n);
 int32_t esc_synth_states(const esc_synth* s, const esc_group_state** states);
 int32_t esc_synth_view(const esc_synth* s, esc_pod_soa* pods, esc_node_soa* nodes);
+/* The same snapshot as object structs (what the cgo shim fills from *v1.Pod / *v1.Node), for
+ * timing the K0 packer and checking it against the generator; owned by the handle. */
+int32_t esc_synth_objects(esc_synth* s, const esc_pod_obj** pods, int64_t* n_pods, const esc_node_obj** nodes,
+                          int64_t* n_nodes);
 
 #ifdef __cplusplus
 }

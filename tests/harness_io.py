@@ -106,8 +106,11 @@ def write_input(path: str, groups, states, pods, nodes, trackers=None, device: i
         fh.write("\n".join(lines) + "\n")
 
 
-def run(path: str, timeout: int = 120) -> dict:
-    out = subprocess.run([HARNESS, path], check=True, capture_output=True, text=True, timeout=timeout).stdout
+def run(path: str, timeout: int = 120, shards: int = 0) -> dict:
+    """shards > 0: the NewContextMulti sequence (esc_ctx_create_multi over `shards` copies of
+    the input's device)."""
+    args = [HARNESS, path] + ([str(shards)] if shards else [])
+    out = subprocess.run(args, check=True, capture_output=True, text=True, timeout=timeout).stdout
     res = {"totals": {}, "decision": {}, "status": {}, "order": {}, "nodev": None, "lines": out}
     for line in out.splitlines():
         w = line.split(" ")

@@ -1,6 +1,10 @@
-"""CPU, world_size 2 over gloo: sharded pods + the SUM exchange of the pods' per-group
-words reproduce the whole-snapshot totals (the exchange the N-GPU decision performs with
-ncclAllReduce inside the library); every rank reduces the whole node table itself."""
+"""CPU, world_size 2 / 3 over gloo: the N-GPU exchange — sharded pods, the node side split
+by pair ownership, one SUM of the per-group words — reproduces the whole-snapshot totals.
+
+No GPU here, so each rank's words are restated from the C oracle in the library's layout
+(the pods' words split lo32 / hi; the node words exact on the group's owner
+rank, escalator_amd.layout.owner_ranges, and zero elsewhere); the GPU suite checks the
+library's own words against the same layout (tests/test_gpu_multi.py)."""
 import os
 import socket
 
@@ -18,6 +22,45 @@ def _free_port():
     return p
 
 
+def exchange_words(tot_shard: np.ndarray, tot_all: np.ndarray, groups, nodes, rank: int, world: int) -> np.ndarray:
+    """One rank's exchange words (esc_exchange_buffers layout): [G][5] pods (cpu lo, cpu hi,
+    mem lo, mem hi, count) from its pod shard, then [G][4] nodes (cpu, mem, unt | taint << 32,
+    cord | flags << 32) for the groups whose pairs it owns."""
+    from escalator_amd import layout
+    from oracle import soa
+    t = soa.group_tables(groups)
+    G = len(groups)
+    pw = np.zeros((G, 5), np.int64)
+    for k, col in ((0, 0), (2, 1)):
+        v = tot_shard[:, col].astype(object)
+        pw[:, k] = [int(x) & 0xFFFFFFFF for x in v]
+        pw[:, k + 1] = [int(x) >> 32 for x in v]
+    pw[:, 4] = tot_shard[:, 2]
+    b = layout.owner_ranges(nodes, len(t["pair_ids"]), world)
+    own = (np.asarray(t["gpair"]) >= b[rank]) & (np.asarray(t["gpair"]) < b[rank + 1])
+    F = soa.TOT_FIELDS
+    nx = np.zeros((G, 4), np.int64)
+    nx[:, 0] = tot_all[:, F.index("node_cpu_m")]
+    nx[:, 1] = tot_all[:, F.index("node_mem_b")]
+    nx[:, 2] = tot_all[:, F.index("n_untainted")] | (tot_all[:, F.index("n_tainted")] << 32)
+    nx[:, 3] = tot_all[:, F.index("n_cordoned")]
+    nx[~own] = 0
+    return np.concatenate([pw.ravel(), nx.ravel()])
+
+
+def decode_words(W: np.ndarray, G: int) -> np.ndarray:
+    """The exchanged words back to (pod cpu, pod mem, pods, node cpu, node mem, unt, taint, cord)."""
+    pw = W[:G * 5].reshape(G, 5).astype(object)
+    nx = W[G * 5:].reshape(G, 4)
+    out = np.zeros((G, 8), np.int64)
+    out[:, 0] = [int(a) + (int(b) << 32) for a, b in zip(pw[:, 0], pw[:, 1])]
+    out[:, 1] = [int(a) + (int(b) << 32) for a, b in zip(pw[:, 2], pw[:, 3])]
+    out[:, 2] = W[:G * 5].reshape(G, 5)[:, 4]
+    out[:, 3], out[:, 4] = nx[:, 0], nx[:, 1]
+    out[:, 5], out[:, 6], out[:, 7] = nx[:, 2] & 0xFFFFFFFF, nx[:, 2] >> 32, nx[:, 3] & 0xFFFFFFFF
+    return out
+
+
 def _worker(rank, world, port, out):
     import torch.distributed as dist
     from escalator_amd.context import Synth
@@ -29,43 +72,72 @@ def _worker(rank, world, port, out):
     lo, hi = shard_range(P, rank, world)
     s = Synth(P, N, G, config=4, seed=5, p_lo=lo, p_hi=hi)
     t = soa.totals(s.pods(), s.nodes(), s.groups)        # this rank's pods, every node
-    S, F = exchange_host(np.ascontiguousarray(t[:, 0:3]), np.zeros(0, np.int64))
-    nodes_local = np.ascontiguousarray(t[:, 3:12])
+    w = exchange_words(t, t, s.groups, s.nodes(), rank, world)
+    S, _ = exchange_host(w, np.zeros(0, np.int64))
     if rank == 0:
-        out.put((S, nodes_local))
+        out.put(S)
     dist.destroy_process_group()
 
 
-def test_two_rank_exchange_equals_whole():
+def test_two_and_three_rank_exchange_equals_whole():
     from escalator_amd.context import Synth
     from oracle import soa
     assert [shard_range(10, r, 3) for r in range(3)] == [(0, 4), (4, 7), (7, 10)]
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    S, NL = q.get(timeout=120)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
     full = Synth(40_000, 3_000, 64, config=4, seed=5)
     t = soa.totals(full.pods(), full.nodes(), full.groups)
-    assert np.array_equal(S, t[:, 0:3])                    # pod cpu, mem, count: SUM over ranks
-    assert np.array_equal(NL, t[:, 3:12])                  # node words and allNodes[0]: rank-local
+    F = soa.TOT_FIELDS
+    want = t[:, [F.index(k) for k in ("pod_cpu_m", "pod_mem_b", "n_pods", "node_cpu_m", "node_mem_b",
+                                      "n_untainted", "n_tainted", "n_cordoned")]]
+    for world in (2, 3):
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        S = q.get(timeout=120)
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        assert np.array_equal(decode_words(S, 64), want), world
 
 
-class _RangeOrders:
-    """Stand-in for a context whose K5 streams nodes [lo, hi): group_order = the oracle's
-    order over that range (the GPU path is checked against the same oracle in test_gpu)."""
+def test_owner_split_library_equals_restatement():
+    """The library's owner split (esc_node_owner_ranges, host only) == layout.owner_ranges,
+    and it covers every pair exactly once, in rank order."""
+    from escalator_amd import layout
+    from escalator_amd.context import Context, Synth
+    from oracle import soa
+    for cfg, P, N, G in ((4, 1000, 30_000, 2000), (5, 1000, 100_000, 100), (2, 1000, 5_000, 7)):
+        s = Synth(P, N, G, config=cfg, seed=cfg)
+        ctx = Context(s.groups, device=-1)
+        n_gp = len(soa.group_tables(s.groups)["pair_ids"])
+        for world in (1, 2, 3, 8, 16):
+            b = [int(x) for x in ctx.owner_ranges(s.nodes(), world)]
+            assert b == layout.owner_ranges(s.nodes(), n_gp, world), (cfg, world)
+            assert b[0] == 0 and b[-1] == n_gp and b == sorted(b)
+        # ranks' node bytes add up to the whole index's
+        assert sum(layout.node_bytes(s.nodes(), n_gp, r, 8) for r in range(8)) == layout.node_bytes(s.nodes(), n_gp)
 
-    def __init__(self, nodes, groups, lo, hi):
-        self.nodes, self.groups, self.lo, self.hi, self.G = nodes, groups, lo, hi, len(groups)
+
+class _OwnerOrders:
+    """Stand-in for a context on rank r: K5 orders the groups whose pairs the rank owns
+    (layout.owner_ranges), group_order of another rank's group has no members — the oracle's
+    order (the GPU path is checked against the same oracle in test_gpu)."""
+
+    def __init__(self, nodes, groups, rank, world):
+        from escalator_amd import layout
+        from oracle import soa
+        t = soa.group_tables(groups)
+        b = layout.owner_ranges(nodes, len(t["pair_ids"]), world)
+        self.own = [b[rank] <= q < b[rank + 1] for q in t["gpair"]]
+        self.nodes, self.groups, self.G = nodes, groups, len(groups)
 
     def group_order(self, g, which, cap=None):
         from oracle import soa
-        return soa.order(self.nodes, self.groups, g, which, self.lo, self.hi, cap)
+        if not self.own[g]:
+            return np.zeros(0, np.int64)
+        return soa.order(self.nodes, self.groups, g, which, cap=cap)
 
 
 def _order_worker(rank, world, port, n, out):
@@ -76,8 +148,7 @@ def _order_worker(rank, world, port, n, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     N, G = 30_000, 12
     s = Synth(1_000, N, G, config=5, seed=0xE5CA1A7E00000005)
-    nlo, nhi = shard_range(N, rank, world)
-    ctx = _RangeOrders(s.nodes(), s.groups, nlo, nhi)
+    ctx = _OwnerOrders(s.nodes(), s.groups, rank, world)
     res = {w: gather_orders(ctx, w, n, s.nodes()["created_ns"]) for w in (0, 1)}
     if rank == 0:
         out.put(res)
@@ -85,8 +156,8 @@ def _order_worker(rank, world, port, n, out):
 
 
 def test_sharded_orderings_merge_to_whole():
-    """Config #5 on N ranks: every rank orders its node range, the per-group prefixes are
-    all-gathered and merged (escalator_amd.dist.gather_orders); the merged taint / untaint
+    """Config #5 on N ranks: every rank orders the groups it owns, the per-group prefixes
+    are all-gathered (escalator_amd.dist.gather_orders); the gathered taint / untaint
     selections equal the whole-snapshot orders."""
     from escalator_amd.context import Synth
     from oracle import soa

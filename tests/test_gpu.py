@@ -485,9 +485,8 @@ def test_sharded_two_contexts_host_exchange(esc, graph):
     for r in range(3):
         lo, hi = shard_range(P, r, 3)
         s = esc.Synth(P, N, G, config=4, seed=11, p_lo=lo, p_hi=hi)
-        nlo, nhi = shard_range(N, r, 3)
         c = esc.Context(s, rank=r, world=3)
-        c.load_synth(s, pod_offset=lo, node_lo=nlo, node_hi=nhi)
+        c.load_synth(s, pod_offset=lo)
         c.set_state(full.states)
         c.use_graph(graph)
         for _ in range(2 if graph else 1):
@@ -1029,6 +1028,27 @@ def test_config3_full_size_vs_c_oracle(esc):
     assert (dec["branch"] == 7).sum() >= 50, "config 3 is tuned so that most groups scale up"
 
 
+def test_config4_full_size_vs_c_oracle(esc):
+    """BASELINE config #4 at its stated size on one GPU: 100M pods / 1M nodes / 10k groups;
+    every group's totals and decision, and three groups' orderings, equal the C oracle
+    (the check bench.py makes, here in the GPU suite)."""
+    s = esc.Synth(100_000_000, 1_000_000, 10_000, config=4, seed=0xE5CA1A7E00000004, threads=16)
+    pods, nodes = s.pods(), s.nodes()
+    otot = soa.totals(pods, nodes, s.groups, threads=16)
+    odf, odi = soa.decide(s.groups, s.states, otot)
+    ctx = esc.Context(s)
+    ctx.load_synth(s)
+    ctx.set_state(s.states)
+    ctx.set_order_in_step(True)
+    for _ in range(2):
+        ctx.run()
+        tot, dec = ctx.results()
+        check_against_c_oracle(tot, dec, otot, odf, odi)
+    for g in (0, 5_000, 9_999):
+        for w in (0, 1):
+            assert np.array_equal(ctx.group_order(g, w), soa.order(nodes, s.groups, g, w)), (g, w)
+
+
 def test_config5_full_size_orderings_vs_c_oracle(esc):
     """BASELINE config #5 at its stated size: 10M nodes in 100 groups; every group's
     taint order (untainted oldest first) and untaint order (tainted newest first) equal the
@@ -1076,7 +1096,8 @@ def test_rccl_step_world1_vs_c_oracle(esc, graph):
         tot, dec = ctx.results()
         check_against_c_oracle(tot, dec, otot, odf, odi)
     (sb, sc), (mb, mc) = ctx.exchange_buffers()
-    assert sc == 5 * 10_000 and mc == 0 and mb is None
+    assert sc == (5 + 4) * 10_000 and mc == 0 and mb is None
+    assert ctx.comm_size() == 1
 
 
 def test_decision_beyond_int32_round_trips(esc):

@@ -46,13 +46,15 @@ def test_harness_host_only_stops_at_device_call(harness, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(6))
-def test_harness_shim_sequence_vs_literal(harness, tmp_path, seed):
+@pytest.mark.parametrize("seed,shards", [(s, 0) for s in range(6)] + [(1, 1), (2, 2), (5, 3)])
+def test_harness_shim_sequence_vs_literal(harness, tmp_path, seed, shards):
+    """seed 0 is the empty cluster (every array NULL); shards > 0 runs the NewContextMulti
+    sequence (one context over `shards` copies of device 0)."""
     from escalator_amd._lib import BRANCHES
     groups, states, pods, nodes, trackers = _cluster(seed)
     path = str(tmp_path / "in.txt")
     H.write_input(path, groups, states, pods, nodes, trackers, device=0)
-    r = H.run(path)
+    r = H.run(path, shards=shards)
     assert r["nodev"] is None and r["lines"].rstrip().endswith("done")
     for g, spec in enumerate(groups):
         L = O.scale_node_group(spec, states[g], pods, nodes, tracker=trackers.get(g, []))

@@ -170,3 +170,25 @@ def test_scalar_math_matches_literal():
                                                  C.byref(d))
                 want, err = O.calc_scale_up_delta(c[4], a.value, b.value, c[0], c[1], cached[0], cached[1], thr)
                 assert d.value == want and (st == 4) == (err is not None), (c, thr, cached)
+
+
+def test_packer_over_generator_objects_equals_generator():
+    """The generator's snapshot as object structs (esc_synth_objects: owner kinds, the
+    config.source annotation, nodeSelector, required node-affinity "In" / "NotIn"
+    expressions, PodAffinity, containers, labels, cordon, taints, allocatable) packed by K0
+    gives the generator's packed snapshot's totals for every group (the pair ids of values
+    no group selects are numbered differently, which no filter can see)."""
+    from escalator_amd.context import Context, Synth
+    for cfg, P, N, G in ((2, 60_000, 2_000, 100), (4, 40_000, 3_000, 700), (3, 30_000, 1_000, 20)):
+        s = Synth(P, N, G, config=cfg, seed=cfg + 40, threads=4)
+        po, n, no, nn = s.objects()
+        assert (n, nn) == (P, N)
+        nodes = s.nodes()
+        trk = {}
+        for j, g in zip(nodes["trk_node"], nodes["trk_group"]):
+            trk.setdefault(int(g), []).append("node-%d" % j)
+        ctx = Context(s.groups, device=-1)
+        Pk, Nk = ctx.pack_objects(po, n, no, nn, trk)
+        pods = s.pods()
+        assert np.array_equal(Pk["pair0"] < 0x7FFFFFFF, pods["pair0"] < 0x7FFFFFFF)
+        assert np.array_equal(soa.totals(Pk, Nk, s.groups), soa.totals(pods, nodes, s.groups)), cfg
