@@ -55,6 +55,38 @@ __device__ __forceinline__ ulonglong2 ld2(const int64_t* p) {
 template <class T>
 __device__ __forceinline__ T ldnt(const T* p) { return __builtin_nontemporal_load(p); }
 
+// Buffer loads through a wave-uniform descriptor (nontemporal: aux 2 = nt on gfx950).  An
+// offset at or past the descriptor's size returns zeros without touching memory: K1's
+// pipeline refills past the end of a run cost no traffic.
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc rsrc(const void* base, int64_t bytes) {
+    const uint64_t b = reinterpret_cast<uint64_t>(base);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+    const uint32_t n = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)bytes);
+    void* p = reinterpret_cast<void*>(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(p, 0, (int)n, 0x00020000);
+}
+__device__ __forceinline__ uint4 ldb4(Rsrc rs, uint32_t off) {
+    const v4u32 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 2);
+    return make_uint4(t.x, t.y, t.z, t.w);
+}
+__device__ __forceinline__ ulonglong2 ldb2(Rsrc rs, uint32_t off) {
+    const v4u32 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 2);
+    ulonglong2 r;
+    r.x = ((uint64_t)t.y << 32) | t.x;
+    r.y = ((uint64_t)t.w << 32) | t.z;
+    return r;
+}
+constexpr uint32_t RUN_OOB = 0x7FFF0000u;     // a tile offset past every run (K1 runs are < 2 GB)
+
+__device__ __forceinline__ void lds_add(uint64_t* a, uint64_t v) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v);
+}
+__device__ __forceinline__ void g_add(int64_t* a, int64_t v) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a), (unsigned long long)v);
+}
+
 // Effective request of one pod — ComputePodResourceRequest, scheduler/types.go:72-89:
 // regular containers summed (Resource.Add, plain int64 += wraps), then max with every
 // init container (SetMaxResource; an absent key is INT64_MIN so max() ignores it),
@@ -247,27 +279,26 @@ __device__ __forceinline__ PodClass load_class(const PodClass* cls, int i) {
 // stride 32 B and double the requests per byte).
 
 // One tile = one contiguous block (esc_kernels.h, K blocks): every load below is lane l's
-// 16 B at a compile-time offset from the block's first word.
+// 16 B at a compile-time offset from the block's first word, through the run's descriptor
+// (`to` = the tile's byte offset in the run; RUN_OOB past its end: zeros, no traffic).
 template <int R, int NXP>
-__device__ __forceinline__ void k_load(const PodDev& P, const PodClass& C, int64_t t, uint32_t lane,
-                                       KTile<R, NXP>& T) {
-    constexpr int64_t BW = (int64_t)k_tile_weight(R, NXP) * 256;        // block words
-    const uint32_t* b = P.kb + C.kb0 + (t - C.t0) * BW + lane * 4;
-    auto l8 = [&](int off) { return ld2(reinterpret_cast<const int64_t*>(b + off)); };
-    T.f = ld4(b);
-    T.c = ld4(b + KB_CPU0);
-    T.m[0] = l8(KB_MEM0);
-    T.m[1] = l8(KB_MEM0 + 256);
-    T.p = ld4(b + KB_PAIR0);
+__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP>& T) {
+    const uint32_t o = to + lane * 16;
+    auto w = [&](int words) { return o + 4u * (uint32_t)words; };
+    T.f = ldb4(rs, o);
+    T.c = ldb4(rs, w(KB_CPU0));
+    T.m[0] = ldb2(rs, w(KB_MEM0));
+    T.m[1] = ldb2(rs, w(KB_MEM0 + 256));
+    T.p = ldb4(rs, w(KB_PAIR0));
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        T.rc[k][0] = l8(KB_REC + 1024 * k);
-        T.rc[k][1] = l8(KB_REC + 1024 * k + 256);
-        T.rm[k][0] = l8(KB_REC + 1024 * k + 512);
-        T.rm[k][1] = l8(KB_REC + 1024 * k + 768);
+        T.rc[k][0] = ldb2(rs, w(KB_REC + 1024 * k));
+        T.rc[k][1] = ldb2(rs, w(KB_REC + 1024 * k + 256));
+        T.rm[k][0] = ldb2(rs, w(KB_REC + 1024 * k + 512));
+        T.rm[k][1] = ldb2(rs, w(KB_REC + 1024 * k + 768));
     }
 #pragma unroll
-    for (int k = 0; k < NXP; ++k) T.rq[k] = ld4(b + KB_REC + 1024 * R + 256 * k);
+    for (int k = 0; k < NXP; ++k) T.rq[k] = ldb4(rs, w(KB_REC + 1024 * R + 256 * k));
 }
 
 // ComputePodResourceRequest (scheduler/types.go:72-89) for each of the lane's 4 pods:
@@ -321,14 +352,18 @@ __device__ __forceinline__ void k_sink(const KTile<R, NXP>& T) {   // loads-only
 
 // Tiles a, a + NW, ... (< b) of one class for this wave: a rolling pipeline of DS tile
 // slots (slot d is processed, then refilled with the tile DS rounds ahead).  DS follows
-// the tile's register footprint.  Refills past the end re-read the tile the slot just
-// held (an L2 hit; never one address shared by every wave — that serialises on one
-// channel: 0.9 ms instead of 0.4 ms for config 4), so that every load is unconditional
-// and the compiler's vmcnt accounting never waits early.
+// the tile's register footprint.  Every load is unconditional, so the compiler's vmcnt
+// accounting never waits early; the refills past the end go through the wave's run
+// descriptor at an offset past its size, which returns zeros without a memory access (they
+// used to re-read the slot's last tile: 1.2x K1's algorithmic fetch at 12.5 M pods).
 template <int R, int NXP, int NW, int ABLATE, int ST>
 __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const PodSink<ABLATE>& K,
                                       const PodClass& C, int64_t a, int64_t b, uint32_t lane) {
     constexpr int L = 5 + 4 * R + NXP;                   // 16-B loads per lane per tile
+    constexpr int64_t BW = (int64_t)k_tile_weight(R, NXP) * 256;        // block words
+    // the wave's run: tiles [a, b) -> bytes [0, (b - a) * BW * 4) of its descriptor
+    const Rsrc rs = rsrc(P.kb + C.kb0 + (a - C.t0) * BW, (b - a) * BW * 4);
+    auto off = [&](int64_t u) { return u < b ? (uint32_t)((u - a) * BW * 4) : RUN_OOB; };
     // slots that fit the VGPR budget: 16 waves per CU leave 128 VGPRs a wave, 8 leave 256
     constexpr int DS0 = NW >= 16 ? (L <= 7 ? 3 : (L <= 10 ? 2 : 1))
                                  : (4 * L * 4 <= 176 ? 4 : (4 * L * 3 <= 176 ? 3 : (4 * L * 2 <= 176 ? 2 : 1)));
@@ -337,8 +372,7 @@ __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const 
     KTile<R, NXP> T[DS];
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
-        const int64_t u = a + (int64_t)d * ST;
-        k_load(P, C, u < b ? u : a, lane, T[d]);
+        k_load(rs, off(a + (int64_t)d * ST), lane, T[d]);
         __builtin_amdgcn_sched_barrier(0);            // slots issue in order (see below)
     }
     for (int64_t t = a; t < b; t += (int64_t)DS * ST) {
@@ -352,8 +386,7 @@ __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const 
             // keep slot d's refill after its use: hoisting it would make the next slots'
             // waits count it (vmcnt is in order) and drain the pipeline
             __builtin_amdgcn_sched_barrier(0);
-            const int64_t nu = u + (int64_t)DS * ST;
-            k_load(P, C, nu < b ? nu : (u < b ? u : a), lane, T[d]);
+            k_load(rs, off(u + (int64_t)DS * ST), lane, T[d]);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
