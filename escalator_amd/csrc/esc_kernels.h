@@ -16,12 +16,17 @@ struct PodClass {
     int64_t kb0, rsv;          // u32-word offset of tile t0's block in the K-block array
     int64_t w0;                // K1 work weight of the tiles before t0
     uint32_t xreg, xinit, ovh, nxp;
-    uint32_t kind;             // (xreg + xinit + ovh) * 4 + nxp: selects K1's pipeline
+    uint32_t kind;             // packed * 16 + (xreg + xinit + ovh) * 4 + nxp: selects K1's pipeline
     uint32_t wt;               // work weight of one tile: its 16-B loads per lane (= block KB)
+    uint32_t packed;           // 1: the packed block layout (kp_*, below)
+    uint32_t pad;
 };
 // weight (16-B loads per lane) of a K tile with R records and NXP extra pairs per pod
-constexpr uint32_t k_tile_weight(uint32_t R, uint32_t NXP) { return 5 + 4 * R + NXP; }
-constexpr int POD_CLASS_IDS = 128;   // signatures with <= 3 extra records and <= 3 extra pairs
+constexpr uint32_t k_tile_weight(uint32_t R, uint32_t NXP, uint32_t packed = 0) {
+    return packed ? 3 + 2 * R + NXP : 5 + 4 * R + NXP;
+}
+constexpr int POD_SIG_IDS = 128;     // signatures with <= 3 extra records and <= 3 extra pairs
+constexpr int POD_CLASS_IDS = 256;   // class id = signature | packed << 7
 constexpr int K1_SEGS = 4;           // class runs per K1 workgroup in the work plan (at most)
 
 // K blocks (tile-major K section).  Tile t of a class is ONE contiguous block of wt KB
@@ -43,8 +48,100 @@ __host__ __device__ inline uint32_t kb_nrec(const PodClass& C) { return C.xreg +
 __host__ __device__ inline int64_t kb_rec64(int64_t blk, uint32_t k, int64_t s) {
     return (blk + KB_REC + 1024 * (int64_t)k) / 2 + kb_pos64(s);
 }
+// Packed K blocks (PodClass::packed): the same tile-major block with every value of a pod
+// that fits its range packed, 12 B per pod instead of 20 and 8 B per record instead of 16
+// (DESIGN.md §3):
+//   word  [0, 256)            pair0 (bits 0..27, KP_PAIR_NONE = no pair) | the pod's own flag
+//                             bits DAEMONSET, STATIC, HAS_SEL, AFF_BLOCK at bits 28..31 (every
+//                             other flag bit is the class signature's)
+//   u64   [256, 768)          cpu0 | mem0 << 20 at kb_pos64(s)
+//   u64   record k            [768 + 512k, +512): cpu | mem << 20 (an init container's absent
+//                             key: cpu field KP_CPU_ABSENT / mem field KP_MEM_ABSENT = INT64_MIN)
+//   u32   extra pair k        [768 + 512R + 256k, +256), as in the plain layout
+// A pod is packed when cpu0 and every record cpu are in [0, 2^20 - 1), mem0 and every record
+// mem in [0, 2^44 - 1) (an init record's key may instead be absent) and pair0 < 2^28 - 1:
+// the range of K1's LDS fast path, so nothing that fits it is left unpacked; others keep
+// the plain layout of their signature.
+constexpr int KP_CM0 = 256, KP_REC = 768;
+constexpr uint32_t KP_FLAG_SHIFT = 28;
+constexpr uint32_t KP_PAIR_NONE = (1u << KP_FLAG_SHIFT) - 1;
+constexpr uint32_t KP_POD_FLAGS = ESC_PF_DAEMONSET | ESC_PF_STATIC | ESC_PF_HAS_SEL | ESC_PF_AFF_BLOCK;
+constexpr int KP_CPU_BITS = 20;
+constexpr uint64_t KP_CPU_ABSENT = (uint64_t(1) << KP_CPU_BITS) - 1;
+constexpr uint64_t KP_MEM_ABSENT = (uint64_t(1) << 44) - 1;
+// the word a freed / padding slot holds in the first row (plain: the flags; packed: pair0|flags)
+__host__ __device__ inline uint32_t kb_free_word(const PodClass& C) {
+    return C.packed ? (ESC_PF_DAEMONSET << KP_FLAG_SHIFT) | KP_PAIR_NONE : ESC_PF_DAEMONSET;
+}
 __host__ __device__ inline int64_t kb_xp(const PodClass& C, int64_t blk, uint32_t k, int64_t s) {
+    if (C.packed) return blk + KP_REC + 512 * (int64_t)kb_nrec(C) + 256 * (int64_t)k + s;
     return blk + KB_REC + 1024 * (int64_t)kb_nrec(C) + 256 * (int64_t)k + s;
+}
+// packed 8-byte value of a (cpu, mem) pair; init: an absent key becomes its field's sentinel
+__host__ __device__ inline bool kp_val_fits(int64_t cpu, int64_t mem, bool init) {
+    const bool c = (cpu >= 0 && (uint64_t)cpu < KP_CPU_ABSENT) || (init && cpu == INT64_MIN);
+    const bool m = (mem >= 0 && (uint64_t)mem < KP_MEM_ABSENT) || (init && mem == INT64_MIN);
+    return c && m;
+}
+__host__ __device__ inline uint64_t kp_val(int64_t cpu, int64_t mem) {
+    const uint64_t c = cpu == INT64_MIN ? KP_CPU_ABSENT : (uint64_t)cpu;
+    const uint64_t m = mem == INT64_MIN ? KP_MEM_ABSENT : (uint64_t)mem;
+    return c | (m << KP_CPU_BITS);
+}
+__host__ __device__ inline int64_t kp_cpu(uint64_t v) {
+    const uint64_t c = v & KP_CPU_ABSENT;
+    return c == KP_CPU_ABSENT ? INT64_MIN : (int64_t)c;
+}
+__host__ __device__ inline int64_t kp_mem(uint64_t v) {
+    const uint64_t m = v >> KP_CPU_BITS;
+    return m == KP_MEM_ABSENT ? INT64_MIN : (int64_t)m;
+}
+__host__ __device__ inline uint32_t kp_word(uint32_t flags, uint32_t pair0) {
+    return ((flags & KP_POD_FLAGS) << KP_FLAG_SHIFT) | (pair0 == NONE ? KP_PAIR_NONE : pair0);
+}
+__host__ __device__ inline uint32_t kp_pair0(uint32_t w) {
+    const uint32_t q = w & KP_PAIR_NONE;
+    return q == KP_PAIR_NONE ? NONE : q;
+}
+// full ESC_PF_* flags of a packed pod: its own bits + the class signature
+__host__ __device__ inline uint32_t kp_flags(const PodClass& C, uint32_t w) {
+    return (w >> KP_FLAG_SHIFT) | (C.ovh ? ESC_PF_HAS_OVH : 0u) | (C.xreg << ESC_PF_XREG_SHIFT) |
+           (C.xinit << ESC_PF_XINIT_SHIFT) | (C.nxp << ESC_PF_XPAIR_SHIFT);
+}
+// Does the pod fit the packed layout?  (xc_cpu / xc_mem: its extra records, regular, then
+// init, then overhead, as esc_pod_soa lists them.)
+__host__ __device__ inline bool kp_fits(uint32_t f, uint32_t cpu0, int64_t mem0, uint32_t pair0, const int64_t* xc_cpu,
+                                        const int64_t* xc_mem) {
+    if (!(pair0 == NONE || pair0 < KP_PAIR_NONE) || !kp_val_fits((int64_t)cpu0, mem0, false)) return false;
+    const uint32_t nreg = pf_xreg(f), ninit = pf_xinit(f), n = pf_xctr(f);
+    for (uint32_t k = 0; k < n; ++k)
+        if (!kp_val_fits(xc_cpu[k], xc_mem[k], k >= nreg && k < nreg + ninit)) return false;
+    return true;
+}
+// Every word a K-class pod occupies in its tile (load and in-place upserts): put(is64, index
+// in u32 words (is64 false) or in 8-byte elements (true), value).
+template <class Put>
+__host__ __device__ inline void kb_write_pod(const PodClass& C, int64_t blk, int64_t sl, uint32_t f, uint32_t cpu0,
+                                             int64_t mem0, uint32_t pair0, const int64_t* xc_cpu,
+                                             const int64_t* xc_mem, const uint32_t* xp, Put&& put) {
+    const uint32_t R = kb_nrec(C);
+    if (C.packed) {
+        put(false, blk + sl, kp_word(f, pair0));
+        put(true, (blk + KP_CM0) / 2 + kb_pos64(sl), kp_val((int64_t)cpu0, mem0));
+        for (uint32_t k = 0; k < R; ++k)
+            put(true, (blk + KP_REC + 512 * (int64_t)k) / 2 + kb_pos64(sl), kp_val(xc_cpu[k], xc_mem[k]));
+    } else {
+        put(false, blk + sl, f);
+        put(false, blk + KB_CPU0 + sl, cpu0);
+        put(true, (blk + KB_MEM0) / 2 + kb_pos64(sl), (uint64_t)mem0);
+        put(false, blk + KB_PAIR0 + sl, pair0);
+        for (uint32_t k = 0; k < R; ++k) {
+            const int64_t o = kb_rec64(blk, k, sl);
+            put(true, o, (uint64_t)xc_cpu[k]);
+            put(true, o + 256, (uint64_t)xc_mem[k]);
+        }
+    }
+    for (uint32_t k = 0; k < C.nxp; ++k) put(false, kb_xp(C, blk, k, sl), xp[k]);
 }
 
 // Device view of a pod shard.  Two sections, made at load (esc_load_pods; sums are

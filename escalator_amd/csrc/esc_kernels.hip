@@ -31,6 +31,9 @@
 #ifndef ESC_PART
 #define ESC_PART 0
 #endif
+#ifndef K1_PK_DS
+#define K1_PK_DS 6      // packed K tiles in flight per K1 wave (at most; the VGPR budget may allow fewer)
+#endif
 
 namespace esc {
 
@@ -248,11 +251,20 @@ __device__ __forceinline__ bool in_range(uint64_t cpu, uint64_t mem) {
 // record k of a tile's pods is one 256-entry row and every array — the pods' own fields
 // and each record / pair row — is one 16-B load per lane (4 pods per lane).  No per-pod
 // offsets, no cross-lane moves, wave-uniform record semantics.
+template <int R, int NXP, int PK>
+struct KTile;
 template <int R, int NXP>
-struct KTile {
+struct KTile<R, NXP, 0> {            // plain block
     uint4 f, c, p;
     ulonglong2 m[2];
     ulonglong2 rc[R > 0 ? R : 1][2], rm[R > 0 ? R : 1][2];
+    uint4 rq[NXP > 0 ? NXP : 1];
+};
+template <int R, int NXP>
+struct KTile<R, NXP, 1> {            // packed block (esc_kernels.h, kp_*)
+    uint4 a;                         // pair0 | pod flags << 28
+    ulonglong2 cm[2];                // cpu0 | mem0 << 20
+    ulonglong2 r[R > 0 ? R : 1][2];  // records, cpu | mem << 20
     uint4 rq[NXP > 0 ? NXP : 1];
 };
 
@@ -282,7 +294,23 @@ __device__ __forceinline__ PodClass load_class(const PodClass* cls, int i) {
 // 16 B at a compile-time offset from the block's first word, through the run's descriptor
 // (`to` = the tile's byte offset in the run; RUN_OOB past its end: zeros, no traffic).
 template <int R, int NXP>
-__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP>& T) {
+__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP, 1>& T) {
+    const uint32_t o = to + lane * 16;
+    auto w = [&](int words) { return o + 4u * (uint32_t)words; };
+    T.a = ldb4(rs, o);
+    T.cm[0] = ldb2(rs, w(KP_CM0));
+    T.cm[1] = ldb2(rs, w(KP_CM0 + 256));
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        T.r[k][0] = ldb2(rs, w(KP_REC + 512 * k));
+        T.r[k][1] = ldb2(rs, w(KP_REC + 512 * k + 256));
+    }
+#pragma unroll
+    for (int k = 0; k < NXP; ++k) T.rq[k] = ldb4(rs, w(KP_REC + 512 * R + 256 * k));
+}
+
+template <int R, int NXP>
+__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP, 0>& T) {
     const uint32_t o = to + lane * 16;
     auto w = [&](int words) { return o + 4u * (uint32_t)words; };
     T.f = ldb4(rs, o);
@@ -305,9 +333,45 @@ __device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTil
 // records [0, xreg) are regular containers (add), [xreg, xreg + xinit) init containers
 // (max; an absent key is INT64_MIN), the last the overhead (add), with Go's wrapping
 // int64 +=; then the pod's memberships (node_group.go:218-275).
+// The same for a packed block: values unpacked in registers (an init record's absent key
+// — its field's sentinel — takes no part in the max, as INT64_MIN would not).
 template <int R, int NXP, int ABLATE>
 __device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLATE>& K, const PodClass& C,
-                                          const KTile<R, NXP>& T) {
+                                          const KTile<R, NXP, 1>& T) {
+    const uint32_t init_end = C.xreg + C.xinit;
+#pragma unroll
+    for (int j = 0; j < PODS_PER_LANE; ++j) {
+        const uint32_t a = lane4(T.a, j);
+        if (a & (ESC_PF_DAEMONSET << KP_FLAG_SHIFT)) continue;      // node_group.go:221, :259
+        const uint64_t cm = lane4(T.cm, j);
+        uint64_t cpu = cm & KP_CPU_ABSENT, mem = cm >> KP_CPU_BITS;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const uint64_t v = lane4(T.r[k], j);
+            const uint64_t c = v & KP_CPU_ABSENT, m = v >> KP_CPU_BITS;
+            if ((uint32_t)k < C.xreg || (uint32_t)k >= init_end) {
+                cpu += c;
+                mem += m;
+            } else {                                   // values and sums are >= 0 here
+                cpu = (c == KP_CPU_ABSENT || cpu >= c) ? cpu : c;
+                mem = (m == KP_MEM_ABSENT || mem >= m) ? mem : m;
+            }
+        }
+        const bool in = in_range(cpu, mem);
+        if ((a >> KP_FLAG_SHIFT) == 0 && G.default_group != NONE) K.add(G.n_gp, cpu, mem, in);   // pf_default_ok
+        const uint32_t q0 = a & KP_PAIR_NONE;
+        if (q0 < G.n_gp) K.add(q0, cpu, mem, in);
+#pragma unroll
+        for (int k = 0; k < NXP; ++k) {
+            const uint32_t q = lane4(T.rq[k], j);
+            if (q < G.n_gp) K.add(q, cpu, mem, in);
+        }
+    }
+}
+
+template <int R, int NXP, int ABLATE>
+__device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLATE>& K, const PodClass& C,
+                                          const KTile<R, NXP, 0>& T) {
     const uint32_t init_end = C.xreg + C.xinit;
 #pragma unroll
     for (int j = 0; j < PODS_PER_LANE; ++j) {
@@ -338,7 +402,20 @@ __device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLAT
 }
 
 template <int R, int NXP>
-__device__ __forceinline__ void k_sink(const KTile<R, NXP>& T) {   // loads-only ablation
+__device__ __forceinline__ void k_sink(const KTile<R, NXP, 1>& T) {   // loads-only ablation
+    uint32_t x = T.a.x ^ T.a.y ^ T.a.z ^ T.a.w;
+    uint64_t y = T.cm[0].x ^ T.cm[0].y ^ T.cm[1].x ^ T.cm[1].y;
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) y ^= T.r[k][h].x ^ T.r[k][h].y;
+#pragma unroll
+    for (int k = 0; k < NXP; ++k) x ^= T.rq[k].x ^ T.rq[k].y ^ T.rq[k].z ^ T.rq[k].w;
+    asm volatile("" :: "v"(x), "v"(y));
+}
+
+template <int R, int NXP>
+__device__ __forceinline__ void k_sink(const KTile<R, NXP, 0>& T) {   // loads-only ablation
     uint32_t x = T.f.x ^ T.f.y ^ T.f.z ^ T.f.w ^ T.c.x ^ T.c.y ^ T.c.z ^ T.c.w ^ T.p.x ^ T.p.y ^ T.p.z ^ T.p.w;
     uint64_t y = T.m[0].x ^ T.m[0].y ^ T.m[1].x ^ T.m[1].y;
 #pragma unroll
@@ -356,20 +433,22 @@ __device__ __forceinline__ void k_sink(const KTile<R, NXP>& T) {   // loads-only
 // accounting never waits early; the refills past the end go through the wave's run
 // descriptor at an offset past its size, which returns zeros without a memory access (they
 // used to re-read the slot's last tile: 1.2x K1's algorithmic fetch at 12.5 M pods).
-template <int R, int NXP, int NW, int ABLATE, int ST>
+template <int R, int NXP, int PK, int NW, int ABLATE, int ST>
 __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const PodSink<ABLATE>& K,
                                       const PodClass& C, int64_t a, int64_t b, uint32_t lane) {
-    constexpr int L = 5 + 4 * R + NXP;                   // 16-B loads per lane per tile
-    constexpr int64_t BW = (int64_t)k_tile_weight(R, NXP) * 256;        // block words
+    constexpr int L = (int)k_tile_weight(R, NXP, PK);    // 16-B loads per lane per tile
+    constexpr int64_t BW = (int64_t)L * 256;             // block words
     // the wave's run: tiles [a, b) -> bytes [0, (b - a) * BW * 4) of its descriptor
     const Rsrc rs = rsrc(P.kb + C.kb0 + (a - C.t0) * BW, (b - a) * BW * 4);
     auto off = [&](int64_t u) { return u < b ? (uint32_t)((u - a) * BW * 4) : RUN_OOB; };
     // slots that fit the VGPR budget: 16 waves per CU leave 128 VGPRs a wave, 8 leave 256
+    // (a packed tile is smaller, so more of them are in flight: up to K1_PK_DS)
+    constexpr int DSM = PK ? K1_PK_DS : 4;
     constexpr int DS0 = NW >= 16 ? (L <= 7 ? 3 : (L <= 10 ? 2 : 1))
-                                 : (4 * L * 4 <= 176 ? 4 : (4 * L * 3 <= 176 ? 3 : (4 * L * 2 <= 176 ? 2 : 1)));
+                                 : (176 / (4 * L) >= DSM ? DSM : (176 / (4 * L) >= 1 ? 176 / (4 * L) : 1));
     // timing knobs (ABLATE bits 6/7): cap the slots in flight at 2 / 3
     constexpr int DS = (ABLATE & 64) ? (DS0 < 2 ? DS0 : 2) : ((ABLATE & 128) ? (DS0 < 3 ? DS0 : 3) : DS0);
-    KTile<R, NXP> T[DS];
+    KTile<R, NXP, PK> T[DS];
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
         k_load(rs, off(a + (int64_t)d * ST), lane, T[d]);
@@ -685,6 +764,13 @@ __device__ __forceinline__ void decide_store(const GroupDev& G, const GroupNode&
 }
 }  // namespace
 
+// Every K1 pipeline: (packed, records, extra pairs) of the K classes (PodClass::kind).
+#define ESC_KRUN_SHAPES(PK)                                                     \
+    ESC_KRUN(PK, 0, 0) ESC_KRUN(PK, 0, 1) ESC_KRUN(PK, 0, 2) ESC_KRUN(PK, 0, 3) \
+    ESC_KRUN(PK, 1, 0) ESC_KRUN(PK, 1, 1) ESC_KRUN(PK, 1, 2) ESC_KRUN(PK, 1, 3) \
+    ESC_KRUN(PK, 2, 0) ESC_KRUN(PK, 2, 1) ESC_KRUN(PK, 2, 2) ESC_KRUN(PK, 2, 3) \
+    ESC_KRUN(PK, 3, 0) ESC_KRUN(PK, 3, 1) ESC_KRUN(PK, 3, 2) ESC_KRUN(PK, 3, 3)
+#define ESC_KRUN_ALL ESC_KRUN_SHAPES(0) ESC_KRUN_SHAPES(1)
 template <int THREADS, int ABLATE = 0, int DC = 3, int DYN = 0, int WS = 0>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
@@ -728,12 +814,9 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
             const int64_t a = (t0c & ((1ll << 48) - 1)) + wid;
             if (a >= b) continue;
             switch (C.kind) {
-#define ESC_KRUN(RR, XX) \
-    case RR * 4 + XX: k_run<RR, XX, NW, ABLATE, NW>(P, G, K, C, a, b, lane); break;
-                ESC_KRUN(0, 0) ESC_KRUN(0, 1) ESC_KRUN(0, 2) ESC_KRUN(0, 3)
-                ESC_KRUN(1, 0) ESC_KRUN(1, 1) ESC_KRUN(1, 2) ESC_KRUN(1, 3)
-                ESC_KRUN(2, 0) ESC_KRUN(2, 1) ESC_KRUN(2, 2) ESC_KRUN(2, 3)
-                ESC_KRUN(3, 0) ESC_KRUN(3, 1) ESC_KRUN(3, 2) ESC_KRUN(3, 3)
+#define ESC_KRUN(PK, RR, XX) \
+    case PK * 16 + RR * 4 + XX: k_run<RR, XX, PK, NW, ABLATE, NW>(P, G, K, C, a, b, lane); break;
+                ESC_KRUN_ALL
 #undef ESC_KRUN
                 default: break;
             }
@@ -754,12 +837,9 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
             const int64_t a = C.t0 + i0 + (WS ? 0 : wid), b = C.t0 + i1;
             if (a >= b) continue;
             switch (C.kind) {
-#define ESC_KRUN(RR, XX) \
-    case RR * 4 + XX: k_run<RR, XX, NW, ABLATE, (WS ? 1 : NW)>(P, G, K, C, a, b, lane); break;
-                ESC_KRUN(0, 0) ESC_KRUN(0, 1) ESC_KRUN(0, 2) ESC_KRUN(0, 3)
-                ESC_KRUN(1, 0) ESC_KRUN(1, 1) ESC_KRUN(1, 2) ESC_KRUN(1, 3)
-                ESC_KRUN(2, 0) ESC_KRUN(2, 1) ESC_KRUN(2, 2) ESC_KRUN(2, 3)
-                ESC_KRUN(3, 0) ESC_KRUN(3, 1) ESC_KRUN(3, 2) ESC_KRUN(3, 3)
+#define ESC_KRUN(PK, RR, XX) \
+    case PK * 16 + RR * 4 + XX: k_run<RR, XX, PK, NW, ABLATE, (WS ? 1 : NW)>(P, G, K, C, a, b, lane); break;
+                ESC_KRUN_ALL
 #undef ESC_KRUN
                 default: break;
             }
@@ -862,7 +942,7 @@ hipError_t launch_pod_reduce(ESC_K1_ARGS) {
     const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
     switch (variant) {
         case 0: ESC_K1(512, 0, 3); break;
-        case 1: case 2: case 5: case 6:
+        case 5:
             return launch_pod_reduce_alt(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, diag, st);
         default:                                  // timing-only ablations (ABLATIONS=1 build)
             if (!launch_pod_reduce_ablation) return hipErrorInvalidValue;
@@ -875,10 +955,10 @@ hipError_t launch_pod_reduce(ESC_K1_ARGS) {
 hipError_t launch_pod_reduce_alt(ESC_K1_ARGS) {
     const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
     switch (variant) {
-        case 6: ESC_K1W(512, 0, 3, 0, 1); break;   // per-wave shares of the K weight
-        case 5: ESC_K1D(512, 0, 3, 1); break;      // dynamic shares (measured slower)
-        case 1: ESC_K1(512, 0, 2); break;
-        case 2: ESC_K1(1024, 0, 3); break;
+        // dynamic shares (measured slower).  (Variants 1: two C tiles in
+        // flight, 2: 1024 threads, 6: per-wave shares were measured and dropped in round 3:
+        // each doubled the build once the packed pipelines joined the plain ones.)
+        case 5: ESC_K1D(512, 0, 3, 1); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -925,15 +1005,30 @@ __device__ __forceinline__ void k_tile_exact(const PodDev& P, const GroupDev& G,
     const int64_t* kb64 = reinterpret_cast<const int64_t*>(P.kb);
     for (int j = 0; j < PODS_PER_LANE; ++j) {
         const uint32_t s = lane * PODS_PER_LANE + j;
-        const uint32_t f = P.kb[blk + s];
+        const uint32_t w0 = P.kb[blk + s];
+        const uint32_t f = C.packed ? kp_flags(C, w0) : w0;
         if (f & ESC_PF_DAEMONSET) continue;
-        uint64_t cpu = P.kb[blk + KB_CPU0 + s], mem = (uint64_t)kb64[(blk + KB_MEM0) / 2 + kb_pos64(s)];
-        for (uint32_t k = 0; k < R; ++k) {
-            const int64_t o = kb_rec64(blk, k, s);
-            apply_rec(k, R, C.xreg, C.xreg + C.xinit, (unsigned long long)kb64[o],
-                      (unsigned long long)kb64[o + 256], cpu, mem);
+        uint64_t cpu, mem;
+        if (C.packed) {
+            const uint64_t v = (uint64_t)kb64[(blk + KP_CM0) / 2 + kb_pos64(s)];
+            cpu = (uint64_t)kp_cpu(v);
+            mem = (uint64_t)kp_mem(v);
+        } else {
+            cpu = P.kb[blk + KB_CPU0 + s];
+            mem = (uint64_t)kb64[(blk + KB_MEM0) / 2 + kb_pos64(s)];
         }
-        const uint32_t q0 = P.kb[blk + KB_PAIR0 + s];
+        for (uint32_t k = 0; k < R; ++k) {
+            if (C.packed) {
+                const uint64_t v = (uint64_t)kb64[(blk + KP_REC + 512 * (int64_t)k) / 2 + kb_pos64(s)];
+                apply_rec(k, R, C.xreg, C.xreg + C.xinit, (unsigned long long)kp_cpu(v),
+                          (unsigned long long)kp_mem(v), cpu, mem);
+            } else {
+                const int64_t o = kb_rec64(blk, k, s);
+                apply_rec(k, R, C.xreg, C.xreg + C.xinit, (unsigned long long)kb64[o],
+                          (unsigned long long)kb64[o + 256], cpu, mem);
+            }
+        }
+        const uint32_t q0 = C.packed ? kp_pair0(w0) : P.kb[blk + KB_PAIR0 + s];
         if (pf_default_ok(f) && G.default_group != NONE) acc.add(G.n_gp, (int64_t)cpu, (int64_t)mem);
         if (q0 < G.n_gp) acc.add(q0, (int64_t)cpu, (int64_t)mem);
         for (uint32_t k = 0; k < C.nxp; ++k) {
@@ -2166,8 +2261,9 @@ __device__ PodRef podref_of(const PodDev& P, uint32_t d) {
         }
         const PodClass& C = P.cls[lo];
         const int64_t blk = kb_block(C, t);
-        r.flags = P.kb[blk + sl];
-        r.pair0 = P.kb[blk + KB_PAIR0 + sl];
+        const uint32_t w0 = P.kb[blk + sl];
+        r.flags = C.packed ? kp_flags(C, w0) : w0;
+        r.pair0 = C.packed ? kp_pair0(w0) : P.kb[blk + KB_PAIR0 + sl];
         for (uint32_t k = 0; k < C.nxp && k < 3; ++k) r.p[k] = P.kb[kb_xp(C, blk, k, sl)];
     } else {
         const int64_t c = (int64_t)d - kpods, t = c / CTILE, l = c % CTILE;

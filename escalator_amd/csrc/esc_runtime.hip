@@ -256,6 +256,7 @@ struct esc_ctx {
     std::vector<int> h_cls_of;                                // signature id -> class index (-1: none)
     std::vector<uint32_t> h_cflags;                           // C-section flags (deletes keep the counts)
     int64_t live_pods = 0, live_xc = 0, live_xp = 0;
+    int64_t live_pk_pods = 0, live_pk_xc = 0;   // of them in packed K classes
     // node state mirrors for esc_nodes_update
     std::vector<uint32_t> h_nflags;
     std::vector<int64_t> h_ncpu, h_nmem;
@@ -295,6 +296,17 @@ int ctx_device(const esc_ctx* c) { return c->device; }
 }
 
 namespace {
+
+// K class of a pod: its record signature (at most 3 extra container
+// records and 3 extra pairs; -1: the C section) | packed << 7 when its values fit the packed
+// block (kp_fits).  xc_cpu / xc_mem: the pod's own records (null when it has none).
+int pod_class_id(uint32_t f, uint32_t cpu0, int64_t mem0, uint32_t pair0, const int64_t* xc_cpu,
+                 const int64_t* xc_mem) {
+    const uint32_t xr = pf_xreg(f), xi = pf_xinit(f), ov = (f & ESC_PF_HAS_OVH) ? 1u : 0u, np = pf_xpair(f);
+    if (xr + xi + ov > 3 || np > 3) return -1;
+    const int sig = (int)(((xr * 4 + xi) * 2 + ov) * 4 + np);
+    return kp_fits(f, cpu0, mem0, pair0, xc_cpu, xc_mem) ? sig | POD_SIG_IDS : sig;
+}
 
 // K1 partial row stride: the pod slots (one per group pair + the default filter's)
 // rounded up to whole K3 columns.
@@ -1146,45 +1158,52 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     // per-tile rows; the rest go to 64-pod C tiles with per-tile record offsets.  Sums are
     // order-independent, so the placement changes no result.  Padding pods carry
     // ESC_PF_DAEMONSET, padding records are 0 and padding pairs NONE.
-    auto class_id = [](uint32_t f) -> int {
-        const uint32_t xr = pf_xreg(f), xi = pf_xinit(f), ov = (f & ESC_PF_HAS_OVH) ? 1u : 0u, np = pf_xpair(f);
-        if (xr + xi + ov > 3 || np > 3) return -1;
-        return (int)(((xr * 4 + xi) * 2 + ov) * 4 + np);
-    };
+    // class id = record signature | packed << 7 (the pod's values fit the packed block,
+    // esc_kernels.h kp_fits; the packed class is listed first so that K1 streams it first)
+    std::vector<int16_t> pid(n);
     std::vector<int64_t> cnt(POD_CLASS_IDS, 0);
     uint64_t sc_c = 0, sp_c = 0;
     int64_t n_c = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        const uint32_t f = p->flags[i];
-        const int id = class_id(f);
-        if (id >= 0) {
-            ++cnt[id];
-        } else {
-            ++n_c;
-            sc_c += pf_xctr(f);
-            sp_c += pf_xpair(f);
+    {
+        uint64_t rc = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            const uint32_t f = p->flags[i];
+            const int id = pod_class_id(f, p->cpu0[i], p->mem0[i], p->pair0[i], p->xc_cpu ? p->xc_cpu + rc : nullptr,
+                                        p->xc_mem ? p->xc_mem + rc : nullptr);
+            pid[i] = (int16_t)id;
+            rc += pf_xctr(f);
+            if (id >= 0) {
+                ++cnt[id];
+            } else {
+                ++n_c;
+                sc_c += pf_xctr(f);
+                sp_c += pf_xpair(f);
+            }
         }
     }
     std::vector<PodClass> cls;
     std::vector<int> cls_of(POD_CLASS_IDS, -1);
     int64_t kt = 0, kbw = 0, kw = 0;
-    for (int id = 0; id < POD_CLASS_IDS; ++id) {
+    for (int ord = 0; ord < POD_CLASS_IDS; ++ord) {
+        const int id = ord ^ POD_SIG_IDS;                 // packed classes first
+        const int sig = id % POD_SIG_IDS;
         // with spare slots requested every signature the K layout can hold gets a class, so
         // that inserts of shapes absent at load still land in place
-        const bool holdable = (id / 32) + ((id / 8) % 4) + ((id / 4) % 2) <= 3;
+        const bool holdable = (sig / 32) + ((sig / 8) % 4) + ((sig / 4) % 2) <= 3;
         if (!cnt[id] && !(c->spare_frac > 0 && holdable)) continue;
         PodClass k;
         std::memset(&k, 0, sizeof k);
-        k.nxp = (uint32_t)(id % 4);
-        k.ovh = (uint32_t)((id / 4) % 2);
-        k.xinit = (uint32_t)((id / 8) % 4);
-        k.xreg = (uint32_t)(id / 32);
+        k.nxp = (uint32_t)(sig % 4);
+        k.ovh = (uint32_t)((sig / 4) % 2);
+        k.xinit = (uint32_t)((sig / 8) % 4);
+        k.xreg = (uint32_t)(sig / 32);
+        k.packed = id >= POD_SIG_IDS ? 1u : 0u;
         const int64_t want = cnt[id] + (c->spare_frac > 0 ? std::max<int64_t>(1, (int64_t)(cnt[id] * c->spare_frac)) : 0);
         const int64_t R = k.xreg + k.xinit + k.ovh, tiles = (want + TILE - 1) / TILE;
         k.t0 = kt;
         k.t1 = kt + tiles;
-        k.kind = (uint32_t)(R * 4 + k.nxp);
-        k.wt = k_tile_weight((uint32_t)R, k.nxp);
+        k.kind = (uint32_t)(k.packed * 16 + R * 4 + k.nxp);
+        k.wt = k_tile_weight((uint32_t)R, k.nxp, k.packed);
         k.kb0 = kbw;
         k.w0 = kw;
         kw += tiles * k.wt;
@@ -1206,8 +1225,8 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     for (const PodClass& k : cls)
         for (int64_t t = k.t0; t < k.t1; ++t) {
             const int64_t blk = kb_block(k, t);
-            std::fill(hkb.begin() + blk, hkb.begin() + blk + TILE, ESC_PF_DAEMONSET);
-            std::fill(hkb.begin() + blk + KB_PAIR0, hkb.begin() + blk + KB_PAIR0 + TILE, NONE);
+            std::fill(hkb.begin() + blk, hkb.begin() + blk + TILE, kb_free_word(k));
+            if (!k.packed) std::fill(hkb.begin() + blk + KB_PAIR0, hkb.begin() + blk + KB_PAIR0 + TILE, NONE);
             const int64_t x0 = kb_xp(k, blk, 0, 0);
             std::fill(hkb.begin() + x0, hkb.begin() + x0 + (int64_t)k.nxp * TILE, NONE);
         }
@@ -1223,23 +1242,18 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         for (int64_t i = 0; i < n; ++i) {
             const uint32_t f = p->flags[i];
             const uint32_t nx = pf_xpair(f), nc = pf_xctr(f);
-            const int id = class_id(f);
+            const int id = pid[i];
             if (id >= 0) {
                 const PodClass& k = cls[cls_of[id]];
                 const int64_t q = pos[id]++, sl = q % TILE;
                 pod_cls[i] = cls_of[id];
                 pod_pos[i] = q;
                 const int64_t blk = kb_block(k, k.t0 + q / TILE);
-                hkb[blk + sl] = f;
-                hkb[blk + KB_CPU0 + sl] = p->cpu0[i];
-                hkb64[(blk + KB_MEM0) / 2 + kb_pos64(sl)] = p->mem0[i];
-                hkb[blk + KB_PAIR0 + sl] = p->pair0[i];
-                for (uint32_t j = 0; j < nc; ++j) {
-                    const int64_t o = kb_rec64(blk, j, sl);
-                    hkb64[o] = p->xc_cpu[rc + j];
-                    hkb64[o + 256] = p->xc_mem[rc + j];
-                }
-                for (uint32_t j = 0; j < nx; ++j) hkb[kb_xp(k, blk, j, sl)] = p->xp_pair[rp + j];
+                kb_write_pod(k, blk, sl, f, p->cpu0[i], p->mem0[i], p->pair0[i], nc ? p->xc_cpu + rc : nullptr,
+                             nc ? p->xc_mem + rc : nullptr, nx ? p->xp_pair + rp : nullptr, [&](bool is64, int64_t at, uint64_t v) {
+                                 if (is64) hkb64[at] = (int64_t)v;
+                                 else hkb[at] = (uint32_t)v;
+                             });
             } else {
                 if (ic % CTILE == 0) { xc_base[ic / CTILE] = (uint32_t)oc; xp_base[ic / CTILE] = (uint32_t)op; }
                 const int64_t d = ic++;                   // C-array index (slot c0 + d)
@@ -1315,6 +1329,12 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     c->live_pods = n;
     c->live_xc = p->n_xc;
     c->live_xp = p->n_xp;
+    c->live_pk_pods = c->live_pk_xc = 0;
+    for (int id = POD_SIG_IDS; id < POD_CLASS_IDS; ++id) {
+        if (cls_of[id] < 0) continue;
+        c->live_pk_pods += cnt[id];
+        c->live_pk_xc += cnt[id] * (int64_t)kb_nrec(cls[cls_of[id]]);
+    }
     c->n_pods = n;
     c->k_tiles = k_tiles;
     c->k_weight = kw;
@@ -1601,8 +1621,10 @@ int32_t esc_stream_bytes(const esc_ctx* c, int64_t* pod_bytes, int64_t* node_byt
     if (!c || !pod_bytes || !node_bytes) return ESC_E_INVAL;
     if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
     // K1: flags 4 + cpu0 4 + mem0 8 + pair0 4 per pod, 16 per extra container record,
-    // 4 per extra pair, 8 per C tile (record offsets); K2: see esc_load_nodes
-    *pod_bytes = c->live_pods * 20 + c->live_xc * 16 + c->live_xp * 4 + c->c_tiles * 8;
+    // 4 per extra pair, 8 per C tile (record offsets); a pod of a packed class 12 B + 8 per
+    // record (esc_kernels.h, kp_*); K2: see esc_load_nodes
+    *pod_bytes = c->live_pods * 20 + c->live_xc * 16 + c->live_xp * 4 + c->c_tiles * 8 - c->live_pk_pods * 8 -
+                 c->live_pk_xc * 8;
     *node_bytes = c->node_bytes;
     return ESC_OK;
 }
@@ -2040,12 +2062,6 @@ std::vector<PatchTargets> pod_targets(esc_ctx* c) {
     return v;
 }
 
-int sig_class_id(uint32_t f) {
-    const uint32_t xr = pf_xreg(f), xi = pf_xinit(f), ov = (f & ESC_PF_HAS_OVH) ? 1u : 0u, np = pf_xpair(f);
-    if (xr + xi + ov > 3 || np > 3) return -1;
-    return (int)(((xr * 4 + xi) * 2 + ov) * 4 + np);
-}
-
 // Removes pod `id` from the snapshot (its slot becomes padding: daemonset-flagged, which
 // every kernel skips; a C pod keeps its record counts so its tile's offsets stay valid).
 void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
@@ -2061,10 +2077,11 @@ void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
     } else {
         const PodClass& k = c->h_cls[ci];
         const int64_t q = c->pod_pos[id];
-        P.add(PT_KB32, kb_block(k, k.t0 + q / TILE) + q % TILE, ESC_PF_DAEMONSET);
+        P.add(PT_KB32, kb_block(k, k.t0 + q / TILE) + q % TILE, kb_free_word(k));
         c->cls_free[ci].push_back(q);
         c->live_xc -= k.xreg + k.xinit + k.ovh;
         c->live_xp -= k.nxp;
+        if (k.packed) { --c->live_pk_pods; c->live_pk_xc -= k.xreg + k.xinit + k.ovh; }
     }
     c->pod_cls[id] = -2;
     --c->live_pods;
@@ -2388,7 +2405,8 @@ int32_t upsert_plan(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, Upsert
         pof[i] = (int64_t)sp;
         sc += nc;
         sp += nx;
-        const int sid = sig_class_id(f);
+        const int sid = pod_class_id(f, p->cpu0[i], p->mem0[i], p->pair0[i], nc ? p->xc_cpu + sc - nc : nullptr,
+                                     nc ? p->xc_mem + sc - nc : nullptr);
         const int ci = sid < 0 ? -1 : c->h_cls_of[sid];
         if (ci < 0) return ESC_E_LIMIT;            // C-section pod or a signature the layout has no class for
         tgt[i] = ci;
@@ -2430,24 +2448,19 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
             const PodClass& k = c->h_cls[ci];
             c->live_xc -= k.xreg + k.xinit + k.ovh;
             c->live_xp -= k.nxp;
+            if (k.packed) { --c->live_pk_pods; c->live_pk_xc -= k.xreg + k.xinit + k.ovh; }
         }
         const PodClass& k = c->h_cls[ci];
         const int64_t q = c->pod_pos[id], sl = q % TILE;
         const int64_t blk = kb_block(k, k.t0 + q / TILE);
         const uint32_t f = p->flags[i], R = kb_nrec(k);
-        P.add(PT_KB32, blk + sl, f);
-        P.add(PT_KB32, blk + KB_CPU0 + sl, p->cpu0[i]);
-        P.add(PT_KB32, blk + KB_PAIR0 + sl, p->pair0[i]);
-        P.add(PT_KB64, (blk + KB_MEM0) / 2 + kb_pos64(sl), (uint64_t)p->mem0[i]);
-        for (uint32_t j = 0; j < R; ++j) {
-            const int64_t o = kb_rec64(blk, j, sl);
-            P.add(PT_KB64, o, (uint64_t)p->xc_cpu[rof[i] + j]);
-            P.add(PT_KB64, o + 256, (uint64_t)p->xc_mem[rof[i] + j]);
-        }
-        for (uint32_t j = 0; j < k.nxp; ++j) P.add(PT_KB32, kb_xp(k, blk, j, sl), p->xp_pair[pof[i] + j]);
+        kb_write_pod(k, blk, sl, f, p->cpu0[i], p->mem0[i], p->pair0[i], R ? p->xc_cpu + rof[i] : nullptr,
+                     R ? p->xc_mem + rof[i] : nullptr, k.nxp ? p->xp_pair + pof[i] : nullptr,
+                     [&](bool is64, int64_t at, uint64_t v) { P.add(is64 ? PT_KB64 : PT_KB32, at, v); });
         ++c->live_pods;
         c->live_xc += R;
         c->live_xp += k.nxp;
+        if (k.packed) { ++c->live_pk_pods; c->live_pk_xc += R; }
     }
     int32_t rc = apply_patches(c, P, pod_targets(c));
     if (rc || !c->placed) return rc;

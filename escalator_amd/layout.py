@@ -4,7 +4,9 @@ restatement of what ``esc_stream_bytes`` reports, used to cross-check it.
 K1 reads the pod shard once per decision: per pod flags 4 + cpu0 4 + mem0 8 + pair0 4 B,
 16 B per extra container record, 4 B per extra selector pair, and 8 B of record offsets
 per 64-pod C tile (pods with more than 3 extra container records or more than 3 extra
-pairs; all other pods sit in homogeneous 256-pod K tiles that need no offsets).
+pairs; all other pods sit in homogeneous 256-pod K tiles that need no offsets).  A K pod
+whose values fit the packed block (``packed_mask``) takes 12 B (pair0 | flags 4, cpu0 | mem0
+8) and 8 B per record.
 K2 reads the node index once per decision: 24 B per (label pair, node) entry of a pair
 some group selects (flags 4 + cpu 8 + mem 8 + node 4) and 8 B per piece (offset + pair).
 With several ranks each reads the pieces of the group pairs it owns (``owner_ranges``:
@@ -24,10 +26,50 @@ def complex_pods(flags: np.ndarray) -> int:
     return int(np.count_nonzero((recs > 3) | (((f >> 24) & 0x3F) > 3)))
 
 
-def pod_bytes(flags: np.ndarray, n_xc: int, n_xp: int) -> int:
-    n = len(flags)
-    c_tiles = (complex_pods(flags) + 63) // 64
-    return n * 20 + int(n_xc) * 16 + int(n_xp) * 4 + c_tiles * 8
+KP_CPU_ABSENT = (1 << 20) - 1      # packed K blocks (esc_kernels.h kp_*): field ranges / sentinels
+KP_MEM_ABSENT = (1 << 44) - 1
+KP_PAIR_NONE = (1 << 28) - 1
+INT64_MIN = -(1 << 63)
+
+
+def packed_mask(pods: dict) -> np.ndarray:
+    """Pods of a K class whose values fit the packed block: cpu0 and every record cpu in
+    [0, 2^20 - 1), mem0 and every record mem in [0, 2^44 - 1) (an init container's key may be
+    absent, INT64_MIN, instead) and pair0 NONE or < 2^28 - 1."""
+    f = np.asarray(pods["flags"], np.uint64)
+    nreg, ninit = (f >> 8) & 0xFF, (f >> 16) & 0xFF
+    nrec = (nreg + ninit + ((f >> 4) & 1)).astype(np.int64)
+    kcls = (nrec <= 3) & (((f >> 24) & 0x3F) <= 3)
+    cpu0 = np.asarray(pods["cpu0"], np.int64)
+    mem0 = np.asarray(pods["mem0"], np.int64)
+    pair0 = np.asarray(pods["pair0"], np.uint32)
+    ok = kcls & (cpu0 < KP_CPU_ABSENT) & (mem0 >= 0) & (mem0 < KP_MEM_ABSENT)
+    ok &= (pair0 == NONE) | (pair0 < KP_PAIR_NONE)
+    n_rec = int(nrec.sum())
+    if n_rec:
+        xc = np.asarray(pods["xc_cpu"], np.int64)[:n_rec]
+        xm = np.asarray(pods["xc_mem"], np.int64)[:n_rec]
+        owner = np.repeat(np.arange(len(f), dtype=np.int64), nrec)
+        k = np.arange(n_rec, dtype=np.int64) - np.repeat(np.cumsum(nrec) - nrec, nrec)
+        init = (k >= nreg.astype(np.int64)[owner]) & (k < (nreg + ninit).astype(np.int64)[owner])
+        rc = ((xc >= 0) & (xc < KP_CPU_ABSENT)) | (init & (xc == INT64_MIN))
+        rm = ((xm >= 0) & (xm < KP_MEM_ABSENT)) | (init & (xm == INT64_MIN))
+        bad = np.bincount(owner[~(rc & rm)], minlength=len(f)) > 0
+        ok &= ~bad
+    return ok
+
+
+def pod_bytes(pods: dict, lo: int = 0, hi: int | None = None) -> int:
+    """K1's algorithmic bytes for pods [lo, hi) of a snapshot (one shard)."""
+    f = np.asarray(pods["flags"], np.uint64)
+    hi = len(f) if hi is None else hi
+    nrec = (((f >> 8) & 0xFF) + ((f >> 16) & 0xFF) + ((f >> 4) & 1)).astype(np.int64)[lo:hi]
+    nxp = ((f >> 24) & 0x3F).astype(np.int64)[lo:hi]
+    pk = packed_mask(pods)[lo:hi]
+    c_tiles = (complex_pods(f[lo:hi]) + 63) // 64
+    plain = (20 + 16 * nrec + 4 * nxp)[~pk].sum()
+    packed = (12 + 8 * nrec + 4 * nxp)[pk].sum()
+    return int(plain + packed + c_tiles * 8)
 
 
 def node_entries(nodes: dict) -> np.ndarray:

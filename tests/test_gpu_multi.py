@@ -52,13 +52,9 @@ def test_multi_device_context_vs_c_oracle(esc, devices):
             assert np.array_equal(ctx.group_order(g, w), soa.order(s.nodes(), s.groups, g, w)), (g, w)
     pb, nb = ctx.stream_bytes()
     from escalator_amd import layout
-    f = s.pods()["flags"].astype(np.uint64)
-    nxc = ((f >> 8) & 0xFF) + ((f >> 16) & 0xFF) + ((f >> 4) & 1)
-    nxp = (f >> 24) & 0x3F
     k = len(devices)
     cuts = [P * i // k for i in range(k + 1)]
-    assert pb == sum(layout.pod_bytes(f[a:b], int(nxc[a:b].sum()), int(nxp[a:b].sum()))
-                     for a, b in zip(cuts, cuts[1:]))
+    assert pb == sum(layout.pod_bytes(s.pods(), a, b) for a, b in zip(cuts, cuts[1:]))
     n_gp = len(soa.group_tables(s.groups)["pair_ids"])
     assert nb == layout.node_bytes(s.nodes(), n_gp, 0, 1)       # the shards' node shares add up to the index
 
