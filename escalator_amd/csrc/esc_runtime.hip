@@ -191,6 +191,9 @@ struct esc_ctx {
     bool work_ready = false;
     bool force_wide = false;
     int k1_variant = 0;                                       // ESC_K1_VARIANT (measurement knob)
+    // K pods of a class are laid out in order of pair0 / pod_sort (0: input order), so that a
+    // K1 workgroup's share touches few pod-slot columns; ESC_POD_SORT
+    uint32_t pod_sort = 0;
     // graph
     bool use_graph = false;
     std::vector<hipGraphExec_t> graphs;                       // esc_run: whole decision (world 1)
@@ -993,6 +996,7 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     c->rank = rank;
     c->world = world;
     if (const char* v = std::getenv("ESC_K1_VARIANT")) c->k1_variant = std::atoi(v);
+    if (const char* v = std::getenv("ESC_POD_SORT")) c->pod_sort = (uint32_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("ESC_ORDER_FUSED")) {
         c->order_fused = std::atoi(v) != 0;
         if (c->order_fused) c->ord_chunk = 8192;               // its best chunk on config 5
@@ -1234,8 +1238,23 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     std::vector<uint32_t> xc_base(c_tiles + 1, 0), xp_base(c_tiles + 1, 0);
     std::vector<int32_t> pod_cls(n);
     std::vector<int64_t> pod_pos(n);
+    // positions inside each class: counting sort by bucket = pair0 / pod_sort (NONE and
+    // pairs no group selects last); input order inside a bucket
+    const uint32_t sw = c->pod_sort, n_gp = c->gi.n_gp;
+    const int64_t nbk = sw ? (int64_t)(n_gp / sw) + 2 : 1;
+    auto bucket = [&](uint32_t q0) -> int64_t { return sw ? (q0 < n_gp ? (int64_t)(q0 / sw) : nbk - 1) : 0; };
+    std::vector<std::vector<int64_t>> next(POD_CLASS_IDS);
+    for (int id = 0; id < POD_CLASS_IDS; ++id)
+        if (cnt[id]) next[id].assign(nbk, 0);
+    if (sw) {
+        for (int64_t i = 0; i < n; ++i)
+            if (pid[i] >= 0) ++next[pid[i]][bucket(p->pair0[i])];
+        for (auto& v : next) {
+            int64_t acc = 0;
+            for (int64_t& x : v) { const int64_t t = x; x = acc; acc += t; }
+        }
+    }
     {
-        std::vector<int64_t> pos(POD_CLASS_IDS, 0);
         int64_t ic = 0;
         uint64_t rc = 0, rp = 0;                          // the pod's records in the input
         uint64_t oc = 0, op = 0;                          // C record cursors
@@ -1245,7 +1264,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
             const int id = pid[i];
             if (id >= 0) {
                 const PodClass& k = cls[cls_of[id]];
-                const int64_t q = pos[id]++, sl = q % TILE;
+                const int64_t q = next[id][bucket(p->pair0[i])]++, sl = q % TILE;
                 pod_cls[i] = cls_of[id];
                 pod_pos[i] = q;
                 const int64_t blk = kb_block(k, k.t0 + q / TILE);
