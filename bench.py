@@ -428,6 +428,10 @@ def main():
     ctx.use_graph(args.graph)
     rccl_ranks = ctx.comm_size() if (multi or (world > 1 and backend == "nccl")) else None
     ctx.k1_calibrate(16)                          # K1 shares to this device's rates (untimed, once per load)
+    fe, ff = ctx.k1_flush_entries()
+    k1_partials = {"entries": fe, "whole_row_entries": ff, "bytes": fe * 512,
+                   "note": "512-B pod-slot column partials K1 writes and K3 reads per decision (compact flush: "
+                           "only the columns a workgroup's share touches, DESIGN.md §4)"}
 
     def barrier():
         if dist is not None:
@@ -538,6 +542,7 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) if traffic else None,
                      "algorithmic_bytes_per_launch": algo, "launch_ms": k1_ms},
+        "k1_partials": k1_partials,
         "node_bytes_per_decision": node_b,
         "exchange": exchange,
         "rccl_ranks": rccl_ranks,

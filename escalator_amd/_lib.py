@@ -182,6 +182,7 @@ _SIGS = {
     "esc_stage_times": (i32, [VP, P(dbl), i32]),
     "esc_k1_trace": (i32, [VP, P(C.c_uint64), i64, P(i64)]),
     "esc_k1_calibrate": (i32, [VP, i32]),
+    "esc_k1_flush_entries": (i32, [VP, P(i64), P(i64)]),
     "esc_sort_nodes": (i32, [VP]),
     "esc_set_order_in_step": (i32, [VP, i32]),
     "esc_build_age_index": (i32, [VP]),

@@ -328,6 +328,12 @@ class Context:
         (esc_k1_calibrate; results unchanged)."""
         L.check(self.lib.esc_k1_calibrate(self.handle, int(rounds)), "esc_k1_calibrate")
 
+    def k1_flush_entries(self) -> tuple[int, int]:
+        """(512-B column partials K1 flushes per decision, entries of a whole-row flush)."""
+        a, b = C.c_int64(), C.c_int64()
+        L.check(self.lib.esc_k1_flush_entries(self.handle, C.byref(a), C.byref(b)), "esc_k1_flush_entries")
+        return a.value, b.value
+
     def k1_trace(self):
         """Per-workgroup K1 timestamps of the last decision (diagnostics):
         uint64 [nblk, 8] = start, K tiles done, C tiles done, flushed (100 MHz ticks), HW_ID, XCC_ID."""

@@ -169,6 +169,13 @@ struct PodDev {
     // class, {t0 | class << 48, t1} (t1 == 0: unused), balanced in work weight, at most two
     // class boundaries per workgroup.  Null: the weight-range shares of variant 7.
     const int64_t* seg;
+    // Compact K1 flush: workgroup b writes only the pod-slot columns its share
+    // touches, wg_cols[b * n_col + i] = {column, destination} for i < wg_off[b] (n_col = the
+    // columns of a partial row), each destination a 64-word partial (32 cpu|count words, 32
+    // mem words) that K3 finds through FoldPlan::col_rows.  Null: every row flushed whole (no
+    // static plan).
+    const uint2* wg_cols;
+    const uint32_t* wg_off;
     int32_t n_cls;
     int64_t k_tiles;           // K section: pods [0, k_tiles * 256)
     int64_t k_weight;          // total work weight of the K tiles (K1 splits it evenly)
@@ -329,8 +336,13 @@ struct FoldPlan {
     int64_t n_col;                     // columns (grid)
     const uint32_t* col_off;           // [n_col + 1] the column's groups in col_groups
     const uint32_t* col_groups;        // group ids ordered by pod slot, then id
+    const uint32_t* col_rows;          // compact flush: [n_col + 1] partial entries of each column (null: nblk rows)
     int ablate;                        // ESC_K3_ABLATE (timing-only knob)
 };
+// The pod-slot columns each K1 workgroup's share touches (compact flush): bitmap words of
+// tw u32 per workgroup, from the same work plan as K1 (daemonset pods skipped: they add
+// nothing; the default filter's column always).
+hipError_t launch_touch(const PodDev& p, const GroupDev& g, int nblk, int tw, uint32_t* bits, hipStream_t st);
 struct OrdChunk;
 // The step's tail in one launch (esc_kernels.hip k_step_tail): the K3 fold into the pod
 // words, K2's dry-mode tracker entries (+ its piece rows when `spans`: no K1 ran) and,

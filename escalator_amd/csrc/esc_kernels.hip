@@ -294,7 +294,7 @@ __device__ __forceinline__ PodClass load_class(const PodClass* cls, int i) {
 // 16 B at a compile-time offset from the block's first word, through the run's descriptor
 // (`to` = the tile's byte offset in the run; RUN_OOB past its end: zeros, no traffic).
 template <int R, int NXP>
-__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP, 1>& T) {
+__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP, 1>& T, const PodClass&) {
     const uint32_t o = to + lane * 16;
     auto w = [&](int words) { return o + 4u * (uint32_t)words; };
     T.a = ldb4(rs, o);
@@ -309,9 +309,13 @@ __device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTil
     for (int k = 0; k < NXP; ++k) T.rq[k] = ldb4(rs, w(KP_REC + 512 * R + 256 * k));
 }
 
+// Plain blocks (pods outside the packed ranges: rare) go through ONE pipeline for every
+// shape: R and NXP are the maxima (3, 3) and the class's own counts select the rows; the
+// rows it lacks load through the descriptor's out-of-range offset (zeros, no traffic).
 template <int R, int NXP>
-__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP, 0>& T) {
+__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP, 0>& T, const PodClass& C) {
     const uint32_t o = to + lane * 16;
+    const uint32_t nr = kb_nrec(C);
     auto w = [&](int words) { return o + 4u * (uint32_t)words; };
     T.f = ldb4(rs, o);
     T.c = ldb4(rs, w(KB_CPU0));
@@ -320,13 +324,15 @@ __device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTil
     T.p = ldb4(rs, w(KB_PAIR0));
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        T.rc[k][0] = ldb2(rs, w(KB_REC + 1024 * k));
-        T.rc[k][1] = ldb2(rs, w(KB_REC + 1024 * k + 256));
-        T.rm[k][0] = ldb2(rs, w(KB_REC + 1024 * k + 512));
-        T.rm[k][1] = ldb2(rs, w(KB_REC + 1024 * k + 768));
+        const bool on = (uint32_t)k < nr;
+        T.rc[k][0] = ldb2(rs, on ? w(KB_REC + 1024 * k) : RUN_OOB);
+        T.rc[k][1] = ldb2(rs, on ? w(KB_REC + 1024 * k + 256) : RUN_OOB);
+        T.rm[k][0] = ldb2(rs, on ? w(KB_REC + 1024 * k + 512) : RUN_OOB);
+        T.rm[k][1] = ldb2(rs, on ? w(KB_REC + 1024 * k + 768) : RUN_OOB);
     }
 #pragma unroll
-    for (int k = 0; k < NXP; ++k) T.rq[k] = ldb4(rs, w(KB_REC + 1024 * R + 256 * k));
+    for (int k = 0; k < NXP; ++k)
+        T.rq[k] = ldb4(rs, (uint32_t)k < C.nxp ? o + 4u * (KB_REC + 1024u * nr + 256u * (uint32_t)k) : RUN_OOB);
 }
 
 // ComputePodResourceRequest (scheduler/types.go:72-89) for each of the lane's 4 pods:
@@ -396,7 +402,7 @@ __device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLAT
 #pragma unroll
         for (int k = 0; k < NXP; ++k) {
             const uint32_t q = lane4(T.rq[k], j);
-            if (q < G.n_gp) K.add(q, cpu, mem, in);
+            if ((uint32_t)k < C.nxp && q < G.n_gp) K.add(q, cpu, mem, in);   // rows past the class's: zeros
         }
     }
 }
@@ -436,8 +442,8 @@ __device__ __forceinline__ void k_sink(const KTile<R, NXP, 0>& T) {   // loads-o
 template <int R, int NXP, int PK, int NW, int ABLATE, int ST>
 __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const PodSink<ABLATE>& K,
                                       const PodClass& C, int64_t a, int64_t b, uint32_t lane) {
-    constexpr int L = (int)k_tile_weight(R, NXP, PK);    // 16-B loads per lane per tile
-    constexpr int64_t BW = (int64_t)L * 256;             // block words
+    constexpr int L = (int)k_tile_weight(R, NXP, PK);    // 16-B loads per lane per tile (plain: at most)
+    const int64_t BW = (int64_t)C.wt * 256;              // block words
     // the wave's run: tiles [a, b) -> bytes [0, (b - a) * BW * 4) of its descriptor
     const Rsrc rs = rsrc(P.kb + C.kb0 + (a - C.t0) * BW, (b - a) * BW * 4);
     auto off = [&](int64_t u) { return u < b ? (uint32_t)((u - a) * BW * 4) : RUN_OOB; };
@@ -451,7 +457,7 @@ __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const 
     KTile<R, NXP, PK> T[DS];
 #pragma unroll
     for (int d = 0; d < DS; ++d) {
-        k_load(rs, off(a + (int64_t)d * ST), lane, T[d]);
+        k_load(rs, off(a + (int64_t)d * ST), lane, T[d], C);
         __builtin_amdgcn_sched_barrier(0);            // slots issue in order (see below)
     }
     for (int64_t t = a; t < b; t += (int64_t)DS * ST) {
@@ -465,7 +471,7 @@ __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const 
             // keep slot d's refill after its use: hoisting it would make the next slots'
             // waits count it (vmcnt is in order) and drain the pipeline
             __builtin_amdgcn_sched_barrier(0);
-            k_load(rs, off(u + (int64_t)DS * ST), lane, T[d]);
+            k_load(rs, off(u + (int64_t)DS * ST), lane, T[d], C);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -770,7 +776,11 @@ __device__ __forceinline__ void decide_store(const GroupDev& G, const GroupNode&
     ESC_KRUN(PK, 1, 0) ESC_KRUN(PK, 1, 1) ESC_KRUN(PK, 1, 2) ESC_KRUN(PK, 1, 3) \
     ESC_KRUN(PK, 2, 0) ESC_KRUN(PK, 2, 1) ESC_KRUN(PK, 2, 2) ESC_KRUN(PK, 2, 3) \
     ESC_KRUN(PK, 3, 0) ESC_KRUN(PK, 3, 1) ESC_KRUN(PK, 3, 2) ESC_KRUN(PK, 3, 3)
-#define ESC_KRUN_ALL ESC_KRUN_SHAPES(0) ESC_KRUN_SHAPES(1)
+// plain blocks: one generic pipeline (k_load above) for the 16 plain kinds
+#define ESC_KRUN_PLAIN                                                                          \
+    case 0: case 1: case 2: case 3: case 4: case 5: case 6: case 7:                            \
+    case 8: case 9: case 10: case 11: case 12: case 13: case 14: ESC_KRUN(0, 3, 3)   /* = case 15 */
+#define ESC_KRUN_ALL ESC_KRUN_SHAPES(1) ESC_KRUN_PLAIN
 template <int THREADS, int ABLATE = 0, int DC = 3, int DYN = 0, int WS = 0>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
@@ -785,8 +795,24 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
         trace[4] = (uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID
         trace[5] = (uint64_t)__builtin_amdgcn_s_getreg(20 | (31 << 11));   // HW_REG_XCC_ID
     }
-    for (uint32_t i = threadIdx.x; i < 2 * gw; i += THREADS) lds[i] = 0;
-    const PodSink<ABLATE> K{PodLds{lds, lds + gw, g0, gw}, PodWide{wide}};
+    // cpu|count words [0, gwp), mem words [gwp, 2 gwp): whole FC_COL columns per half, so the
+    // compact flush reads a column's 16 B per lane unconditionally (ds_read_b128, no conflicts)
+    const uint32_t gwp = (gw + FC_COL - 1) / FC_COL * FC_COL;
+    for (uint32_t i = threadIdx.x; i < 2 * gwp; i += THREADS) lds[i] = 0;
+    const PodSink<ABLATE> K{PodLds{lds, lds + gwp, g0, gw}, PodWide{wide}};
+    // compact flush: this workgroup's entry range and the descriptors of its first 32 rounds,
+    // fetched now so the flush does not wait on them (see the flush)
+    // (entries of workgroup b: wg_cols[b * n_col + i], i < wg_off[b]; fixed-stride, so the two
+    // loads do not depend on each other and nothing waits on them before the flush)
+    const int64_t n_col = G.sp / FC_COL;
+    const uint2* fcols = P.wg_cols + (int64_t)blockIdx.x * n_col;
+    uint32_t fe1 = 0;
+    uint2 fdv = make_uint2(0xFFFFFFFFu, 0u);
+    if (P.wg_off) {
+        fe1 = P.wg_off[blockIdx.x];
+        const uint32_t li = 2 * (threadIdx.x >> 6) + (threadIdx.x & 1) + ((threadIdx.x & 63) >> 1) * (THREADS / 32);
+        if (li < n_col) fdv = fcols[li];
+    }
     const uint32_t lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // WS: every wave takes its own contiguous share of the K weight (a wave's restarts at
@@ -894,14 +920,45 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     uint64_t* out = part + (int64_t)blockIdx.x * 2 * S + g0;
     // 16-B nontemporal stores (rows and g0 are 16-B aligned: S is a multiple of FC_COL)
     typedef uint64_t v2u64s __attribute__((ext_vector_type(2)));
+    if (P.wg_off) {
+        // compact: the columns this share touches, 32 threads per column (16 write the
+        // cpu|count words, 16 the mem words), each to its own 64-word entry
+        // Wave w takes entries e0 + 2w + {0, 1} + (THREADS / 32) k; lane 2k + h holds the
+        // descriptor of round k, half h (fetched at the start for rounds 0..31, by one load
+        // per 32 rounds after that) and hands it out by readlane.
+        const uint32_t e0 = 0, e1 = fe1;
+        const uint32_t h = threadIdx.x & 31, j = 2 * (h & 15), half = h >> 4, eh = (threadIdx.x >> 5) & 1;
+        constexpr uint32_t EPR = THREADS / 32;                         // entries per round
+        const uint32_t wb = e0 + 2 * (uint32_t)wid;
+        for (uint32_t r0 = 0; wb + r0 * EPR < e1; r0 += 32) {
+            uint2 dv = fdv;
+            if (r0) {
+                const uint32_t li = wb + (lane & 1) + (r0 + (lane >> 1)) * EPR;
+                dv = li < e1 ? fcols[li] : make_uint2(0xFFFFFFFFu, 0u);
+            }
+#pragma unroll 4
+            for (uint32_t k = 0; k < 32; ++k) {
+                if (wb + (r0 + k) * EPR >= e1) break;                  // wave-uniform
+                const uint32_t x0 = __builtin_amdgcn_readlane(dv.x, 2 * k), x1 = __builtin_amdgcn_readlane(dv.x, 2 * k + 1);
+                const uint32_t y0 = __builtin_amdgcn_readlane(dv.y, 2 * k), y1 = __builtin_amdgcn_readlane(dv.y, 2 * k + 1);
+                const uint32_t col = eh ? x1 : x0, dst = eh ? y1 : y0;
+                if (wb + (r0 + k) * EPR + eh >= e1) continue;          // past the list (second entry)
+                const int64_t c0 = (int64_t)col * FC_COL - g0;         // column start in this window
+                if (c0 < 0 || c0 >= (int64_t)gw) continue;             // the column is in another window
+                const v2u64s v = *reinterpret_cast<const v2u64s*>(lds + half * gwp + c0 + j);
+                __builtin_nontemporal_store(v, reinterpret_cast<v2u64s*>(part + (int64_t)dst * 2 * FC_COL +
+                                                                         half * FC_COL + j));
+            }
+        }
+    } else
     for (uint32_t i = 2 * threadIdx.x; i < gw; i += 2 * THREADS) {
         if (i + 1 < gw) {
-            const v2u64s a = {lds[i], lds[i + 1]}, m = {lds[gw + i], lds[gw + i + 1]};
+            const v2u64s a = {lds[i], lds[i + 1]}, m = {lds[gwp + i], lds[gwp + i + 1]};
             __builtin_nontemporal_store(a, reinterpret_cast<v2u64s*>(out + i));
             __builtin_nontemporal_store(m, reinterpret_cast<v2u64s*>(out + S + i));
         } else {
             out[i] = lds[i];
-            out[S + i] = lds[gw + i];
+            out[S + i] = lds[gwp + i];
         }
     }
     if (trace) {
@@ -939,7 +996,7 @@ bool k1_dynamic(int variant) { return variant == 5; }
 
 
 hipError_t launch_pod_reduce(ESC_K1_ARGS) {
-    const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
+    const size_t lds = (size_t)(gw + FC_COL - 1) / FC_COL * FC_COL * 2 * sizeof(uint64_t);
     switch (variant) {
         case 0: ESC_K1(512, 0, 3); break;
         case 5:
@@ -953,7 +1010,7 @@ hipError_t launch_pod_reduce(ESC_K1_ARGS) {
 }
 #elif ESC_PART == 1
 hipError_t launch_pod_reduce_alt(ESC_K1_ARGS) {
-    const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
+    const size_t lds = (size_t)(gw + FC_COL - 1) / FC_COL * FC_COL * 2 * sizeof(uint64_t);
     switch (variant) {
         // dynamic shares (measured slower).  (Variants 1: two C tiles in
         // flight, 2: 1024 threads, 6: per-wave shares were measured and dropped in round 3:
@@ -965,7 +1022,7 @@ hipError_t launch_pod_reduce_alt(ESC_K1_ARGS) {
 }
 #elif ESC_PART == 2
 hipError_t launch_pod_reduce_ablation(ESC_K1_ARGS) {
-    const size_t lds = (size_t)gw * 2 * sizeof(uint64_t);
+    const size_t lds = (size_t)(gw + FC_COL - 1) / FC_COL * FC_COL * 2 * sizeof(uint64_t);
     switch (variant) {
         case 14: ESC_K1W(512, 4 | 32, 3, 0, 1); break;   // per-wave shares, K tiles, loads only
         case 3: ESC_K1(512, 64, 3); break;       // <= 2 K tiles in flight per wave
@@ -992,6 +1049,55 @@ hipError_t launch_pod_reduce_ablation(ESC_K1_ARGS) {
 __global__ __launch_bounds__(64) void k_pod_bigtiles(PodDev P, GroupDev G, const uint32_t* __restrict__ tiles,
                                                      int64_t* __restrict__ wide) {
     c_tile_exact(P, G, tiles[blockIdx.x], threadIdx.x, wide);
+}
+
+// Touched pod-slot columns of every K1 workgroup's share (compact flush, launch_touch): the
+// K1 plan's class runs and K1's C-tile share, walked pod by pod (once per plan, not per
+// decision).  Daemonset pods of K tiles add nothing and are skipped (an upsert that later
+// fills such a slot marks its columns on the host); C tiles are taken whole (a superset).
+__global__ __launch_bounds__(256) void k_touch(PodDev P, GroupDev G, int tw, uint32_t* __restrict__ bits) {
+    extern __shared__ uint32_t tb[];
+    for (int i = threadIdx.x; i < tw; i += 256) tb[i] = 0;
+    __syncthreads();
+    auto mark = [&](uint32_t slot) {
+        const uint32_t col = slot / FC_COL;
+        atomicOr(&tb[col >> 5], 1u << (col & 31));
+    };
+    const int64_t* sg = P.seg + (int64_t)blockIdx.x * (2 * K1_SEGS);
+    for (int k = 0; k < K1_SEGS; ++k) {
+        const int64_t t0c = sg[2 * k], b = sg[2 * k + 1];
+        if (b == 0) break;
+        const PodClass C = P.cls[(int)(t0c >> 48)];
+        const int64_t a = t0c & ((1ll << 48) - 1);
+        for (int64_t i = threadIdx.x; i < (b - a) * TILE; i += 256) {
+            const int64_t blk = kb_block(C, a + i / TILE), s = i % TILE;
+            const uint32_t w0 = P.kb[blk + s];
+            if ((C.packed ? kp_flags(C, w0) : w0) & ESC_PF_DAEMONSET) continue;
+            const uint32_t q0 = C.packed ? kp_pair0(w0) : P.kb[blk + KB_PAIR0 + s];
+            if (q0 < G.n_gp) mark(q0);
+            for (uint32_t x = 0; x < C.nxp; ++x) {
+                const uint32_t q = P.kb[kb_xp(C, blk, x, s)];
+                if (q < G.n_gp) mark(q);
+            }
+        }
+    }
+    const int64_t per = (P.c_tiles + gridDim.x - 1) / gridDim.x;       // K1's C-tile share
+    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(lo + per, P.c_tiles);
+    if (lo < hi) {
+        for (int64_t i = lo * CTILE + threadIdx.x; i < hi * CTILE; i += 256)
+            if (P.pair0[i] < G.n_gp) mark(P.pair0[i]);
+        for (int64_t i = P.xp_base[lo] + threadIdx.x; i < (int64_t)P.xp_base[hi]; i += 256)
+            if (P.xp[i] < G.n_gp) mark(P.xp[i]);
+    }
+    if (threadIdx.x == 0 && G.default_group != NONE) mark(G.n_gp);
+    __syncthreads();
+    for (int i = threadIdx.x; i < tw; i += 256) bits[(int64_t)blockIdx.x * tw + i] = tb[i];
+}
+
+hipError_t launch_touch(const PodDev& p, const GroupDev& g, int nblk, int tw, uint32_t* bits, hipStream_t st) {
+    if (nblk <= 0 || !p.seg) return hipSuccess;
+    hipLaunchKernelGGL(k_touch, dim3(nblk), dim3(256), (size_t)tw * 4, st, p, g, tw, bits);
+    return hipGetLastError();
 }
 
 // =====================================================================  K1 (wide)
@@ -1366,7 +1472,21 @@ __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, i
     // ---- fold: every K1 row of the column; wave w's load u covers rows
     //      (w + FD_WAVES * u) * FD_RPL + sub
     uint64_t cp[2] = {0, 0}, cn[2] = {0, 0}, ml[2] = {0, 0}, mc[2] = {0, 0};
-    const int nrows = (ablate & 4) ? 0 : F.nblk;
+    // compact flush: the column's own entries (64 words each: cpu|count, then mem), else
+    // column col of every K1 row
+    const int64_t* pbase = reinterpret_cast<const int64_t*>(F.part);
+    int64_t rstride = 2 * F.sp, mo = F.sp;
+    int nrows = F.nblk;
+    if (F.col_rows) {
+        const uint32_t r0 = F.col_rows[col];
+        nrows = (int)(F.col_rows[col + 1] - r0);
+        pbase += (int64_t)r0 * 2 * FC_COL;
+        rstride = 2 * FC_COL;
+        mo = FC_COL;
+    } else {
+        pbase += s0;
+    }
+    if (ablate & 4) nrows = 0;
     constexpr int STEP = FD_WAVES * FD_U * FD_RPL;
     for (int b = wid * FD_RPL + sub; b - sub < nrows; b += STEP) {
         ulonglong2 c[FD_U], m[FD_U];
@@ -1374,9 +1494,9 @@ __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, i
         for (int u = 0; u < FD_U; ++u) {
             const int r = b + FD_WAVES * FD_RPL * u;
             const int bb = r < nrows ? r : 0;
-            const int64_t* row = reinterpret_cast<const int64_t*>(F.part) + (int64_t)bb * 2 * F.sp + s0 + 2 * hl;
+            const int64_t* row = pbase + (int64_t)bb * rstride + 2 * hl;
             c[u] = ld2(row);
-            m[u] = ld2(row + F.sp);
+            m[u] = ld2(row + mo);
         }
 #pragma unroll
         for (int u = 0; u < FD_U; ++u) {

@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -171,6 +172,18 @@ struct esc_ctx {
     int64_t* d_wide_pod = nullptr;
     uint32_t* d_k1_ticket = nullptr;                          // K1 dynamic shares (next chunk, done)
     int64_t* d_k1seg = nullptr;                               // K1 work plan [nblk][K1_SEGS][2]
+    // Compact K1 flush: the pod-slot columns each workgroup's share touches
+    // (bitmap of touch_tw u32 per workgroup, kept current by pod upserts), as per-workgroup
+    // {column, entry} lists and per-column entry ranges on the device.
+    bool touch_on = false;
+    bool full_flush = false;                                  // ESC_K1_FULL_FLUSH=1 (measurement knob)
+    int touch_tw = 0;
+    std::vector<uint32_t> h_touch;
+    std::vector<std::array<int64_t, 3>> h_tile_wg;            // {first tile, end tile, workgroup}, sorted
+    uint32_t* d_touch = nullptr;
+    uint2* d_wg_cols = nullptr;
+    uint32_t* d_wg_off = nullptr;
+    uint32_t* d_col_rows = nullptr;
     std::vector<double> k1_share;                             // calibrated K1 shares (esc_k1_calibrate)
     int k1_cap = 0;                                           // K1 chunks per workgroup at most (0: static)
     uint64_t* d_k1_trace = nullptr;                           // K1 per-workgroup timestamps (esc_k1_trace)
@@ -193,7 +206,7 @@ struct esc_ctx {
     int k1_variant = 0;                                       // ESC_K1_VARIANT (measurement knob)
     // K pods of a class are laid out in order of pair0 / pod_sort (0: input order), so that a
     // K1 workgroup's share touches few pod-slot columns; ESC_POD_SORT
-    uint32_t pod_sort = 0;
+    uint32_t pod_sort = FC_COL;   // one K3 column per bucket (exact pair order serialises K1's LDS atomics: 0.65 ms)
     // graph
     bool use_graph = false;
     std::vector<hipGraphExec_t> graphs;                       // esc_run: whole decision (world 1)
@@ -346,6 +359,8 @@ PodDev pod_dev(const esc_ctx* c, int replica) {
     p.cls = b.cls;
     p.seg = (c->k1_variant == 5 || c->k1_variant == 6 || c->k1_variant == 7 || c->k1_variant == 14) ? nullptr
                                                                                                     : c->d_k1seg;
+    p.wg_cols = c->touch_on ? c->d_wg_cols : nullptr;
+    p.wg_off = c->touch_on ? c->d_wg_off : nullptr;
     p.n_cls = c->n_cls;
     p.k_tiles = c->k_tiles;
     p.k_weight = c->k_weight;
@@ -429,6 +444,8 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
 void release_work(esc_ctx* c) {
     dfree(c->d_k1seg); dfree(c->d_pod_part); dfree(c->d_wide_pod); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
     dfree(c->d_k1_trace);
+    dfree(c->d_touch); dfree(c->d_wg_cols); dfree(c->d_wg_off); dfree(c->d_col_rows);
+    c->touch_on = false;
     dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_cdec); dfree(c->d_metrics);
     c->d_pwords = nullptr;
     if (c->h_cdec) hipHostFree(c->h_cdec);
@@ -798,13 +815,86 @@ std::vector<int64_t> pair_counts(const esc_ctx* c, const esc_node_soa* s) {
 // Pod accumulator slots: one per group pair + one for the default filter.
 int64_t pod_slots(const esc_ctx* c) { return (int64_t)c->gi.n_gp + 1; }
 
+// Compact K1 flush lists from the touch bitmap: per column its entries (one per workgroup
+// touching it, in workgroup order), per workgroup its {column, entry} list (fixed stride of
+// n_col entries) and length.
+int32_t touch_upload(esc_ctx* c) {
+    const int64_t nblk = c->nblk, tw = c->touch_tw, n_col = slot_stride(c) / FC_COL;
+    std::vector<uint32_t> col_rows(n_col + 1, 0), wg_cnt(nblk, 0);
+    std::vector<uint2> cols((size_t)nblk * n_col, make_uint2(0xFFFFFFFFu, 0u));
+    for (int64_t b = 0; b < nblk; ++b)
+        for (int64_t w = 0; w < tw; ++w)
+            for (uint32_t x = c->h_touch[b * tw + w]; x; x &= x - 1) {
+                const int64_t col = w * 32 + __builtin_ctz(x);
+                if (col < n_col) ++col_rows[col + 1];
+            }
+    for (int64_t k = 0; k < n_col; ++k) col_rows[k + 1] += col_rows[k];
+    std::vector<uint32_t> next(col_rows.begin(), col_rows.end() - 1);
+    for (int64_t b = 0; b < nblk; ++b)
+        for (int64_t w = 0; w < tw; ++w)
+            for (uint32_t x = c->h_touch[b * tw + w]; x; x &= x - 1) {
+                const int64_t col = w * 32 + __builtin_ctz(x);
+                if (col < n_col) cols[b * n_col + wg_cnt[b]++] = make_uint2((uint32_t)col, next[col]++);
+            }
+    HIP_TRY(hipMemcpy(c->d_col_rows, col_rows.data(), col_rows.size() * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_wg_off, wg_cnt.data(), wg_cnt.size() * 4, hipMemcpyHostToDevice));
+    if (!cols.empty()) HIP_TRY(hipMemcpy(c->d_wg_cols, cols.data(), cols.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    return ESC_OK;
+}
+
+// (Re)computes the touched columns of the current K1 plan (after ensure_work and every plan
+// change of esc_k1_calibrate): k_touch on the device, the lists on the host.  Off (every
+// row flushed whole) without a static plan (dynamic shares) or with ESC_K1_FULL_FLUSH.
+int32_t touch_refresh(esc_ctx* c, const std::vector<int64_t>& plan) {
+    const PodDev p0 = pod_dev(c, 0);
+    const bool on = !plan.empty() && p0.seg && !c->full_flush && c->nblk > 0 && !c->pods.empty();
+    if (on != c->touch_on) drop_graphs(c);             // the captured steps hold the flush mode
+    c->touch_on = false;
+    if (!on) return ESC_OK;
+    c->h_tile_wg.clear();
+    for (int64_t b = 0; b < c->nblk; ++b)
+        for (int k = 0; k < K1_SEGS; ++k) {
+            const int64_t* e = &plan[((size_t)b * K1_SEGS + k) * 2];
+            if (e[1] == 0) break;
+            c->h_tile_wg.push_back({e[0] & ((1ll << 48) - 1), e[1], b});
+        }
+    std::sort(c->h_tile_wg.begin(), c->h_tile_wg.end());
+    c->h_touch.assign((size_t)c->nblk * c->touch_tw, 0);
+    HIP_TRY(launch_touch(p0, group_dev(c), c->nblk, c->touch_tw, c->d_touch, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_touch.data(), c->d_touch, c->h_touch.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (int32_t rc = touch_upload(c)) return rc;
+    c->touch_on = true;
+    return ESC_OK;
+}
+
+// Marks the columns a pod written into K slot q of class ci adds to (esc_pods_upsert);
+// true when its workgroup did not touch one of them yet (the lists need an upload).
+bool touch_mark(esc_ctx* c, int32_t ci, int64_t q, uint32_t f, uint32_t pair0, const uint32_t* xp) {
+    if (!c->touch_on || (f & ESC_PF_DAEMONSET)) return false;
+    const int64_t t = c->h_cls[ci].t0 + q / TILE;
+    auto it = std::upper_bound(c->h_tile_wg.begin(), c->h_tile_wg.end(), std::array<int64_t, 3>{t, INT64_MAX, INT64_MAX});
+    if (it == c->h_tile_wg.begin() || t >= (it - 1)->at(1)) return false;   // a tile no workgroup streams (none)
+    uint32_t* row = c->h_touch.data() + (size_t)(it - 1)->at(2) * c->touch_tw;
+    bool grew = false;
+    auto mark = [&](uint32_t slot) {
+        const uint32_t col = slot / FC_COL, bit = 1u << (col & 31);
+        if (!(row[col >> 5] & bit)) { row[col >> 5] |= bit; grew = true; }
+    };
+    const uint32_t n_gp = c->gi.n_gp;
+    if (pair0 < n_gp) mark(pair0);
+    for (uint32_t k = 0; k < pf_xpair(f); ++k)
+        if (xp[k] < n_gp) mark(xp[k]);
+    return grew;
+}
+
 // Grid geometry for the current snapshot.
 int32_t ensure_work(esc_ctx* c) {
     if (c->work_ready) return ESC_OK;
     const int32_t G = c->gi.G;
     const int64_t S = pod_slots(c);
     const int gw = (int)std::min<int64_t>(S, POD_WINDOW_MAX);
-    const int lds = gw * 16;
+    const int lds = (gw + FC_COL - 1) / FC_COL * FC_COL * 16;   // K1's two LDS halves, whole columns each
     const int max_blocks = c->k1_variant == 2 ? 2 : 4;   // 2048 threads per CU
     const int per_cu = std::max(1, std::min(max_blocks, LDS_BYTES / std::max(lds, 1)));
     int64_t nblk = c->cu_count * per_cu;
@@ -844,7 +934,6 @@ int32_t ensure_work(esc_ctx* c) {
     HIP_TRY(hipMemset(c->d_k1_trace, 0, (size_t)std::max<int64_t>(nblk, 1) * 64));
     const int64_t SP = slot_stride(c), n_col = SP / FC_COL;
     HIP_TRY(dalloc(&c->d_pod_part, (size_t)std::max<int64_t>(nblk, 1) * 2 * SP));
-    (void)n_col;
     HIP_TRY(dalloc(&c->d_wide_pod, (size_t)S * WP_K));
     HIP_TRY(dalloc(&c->d_k1_ticket, 2));
     HIP_TRY(hipMemset(c->d_k1_ticket, 0, 2 * sizeof(uint32_t)));
@@ -860,7 +949,15 @@ int32_t ensure_work(esc_ctx* c) {
     HIP_TRY(dalloc(&c->d_cdec, (size_t)G));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_cdec), (size_t)G * sizeof(DecCompact)));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_cdec_dev), c->h_cdec, 0));
+    // compact flush: every workgroup may touch every column at most once, so the lists and
+    // the entries fit the full-row buffers' sizes
+    c->touch_tw = (int)((n_col + 31) / 32);
+    HIP_TRY(dalloc(&c->d_touch, (size_t)std::max<int64_t>(nblk, 1) * c->touch_tw));
+    HIP_TRY(dalloc(&c->d_wg_cols, (size_t)std::max<int64_t>(nblk, 1) * n_col));
+    HIP_TRY(dalloc(&c->d_wg_off, (size_t)nblk + 1));
+    HIP_TRY(dalloc(&c->d_col_rows, (size_t)n_col + 1));
     c->work_ready = true;
+    if (int32_t rc = touch_refresh(c, plan)) return rc;
     return ESC_OK;
 }
 
@@ -910,6 +1007,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     f.n_col = f.sp / FC_COL;
     f.col_off = c->d_col_off;
     f.col_groups = c->d_col_groups;
+    f.col_rows = nblk && c->touch_on ? c->d_col_rows : nullptr;
     f.ablate = c->k3_ablate;
     const bool ord = c->order_in_step;
     HIP_TRY(launch_step_tail(g, n, f, true, c->d_wide_pod, c->d_pwords, c->nodes.rows, c->d_trk_acc, c->d_pchunks,
@@ -997,6 +1095,7 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     c->world = world;
     if (const char* v = std::getenv("ESC_K1_VARIANT")) c->k1_variant = std::atoi(v);
     if (const char* v = std::getenv("ESC_POD_SORT")) c->pod_sort = (uint32_t)std::max(0, std::atoi(v));
+    if (const char* v = std::getenv("ESC_K1_FULL_FLUSH")) c->full_flush = std::atoi(v) != 0;
     if (const char* v = std::getenv("ESC_ORDER_FUSED")) {
         c->order_fused = std::atoi(v) != 0;
         if (c->order_fused) c->ord_chunk = 8192;               // its best chunk on config 5
@@ -1738,7 +1837,7 @@ int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
         if (plan.empty() || plan_worst(c, plan, nblk) > PODS_PER_BLOCK_MAX) return 1;
         HIP_TRY(hipMemcpy(c->d_k1seg, plan.data(), plan.size() * 8, hipMemcpyHostToDevice));
         c->k1_share = sh;
-        return ESC_OK;
+        return touch_refresh(c, plan);
     };
     constexpr int REPS = 3;                              // decisions averaged per round (noise ~1-4 %)
     for (int32_t r = 0; r <= rounds; ++r) {
@@ -1772,6 +1871,29 @@ int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
         rc = upload(best);
         if (rc < 0) return rc;
     }
+    return ESC_OK;
+}
+
+int32_t esc_k1_flush_entries(const esc_ctx* c, int64_t* entries, int64_t* full) {
+    if (!c || !entries || !full) return ESC_E_INVAL;
+    if (c->multi) {
+        int64_t e = 0, f = 0;
+        for (int i = 0; esc::multi_sub(const_cast<esc_ctx*>(c), i); ++i) {
+            int64_t a, b;
+            if (int32_t rc = esc_k1_flush_entries(esc::multi_sub(const_cast<esc_ctx*>(c), i), &a, &b)) return rc;
+            e += a;
+            f += b;
+        }
+        *entries = e;
+        *full = f;
+        return ESC_OK;
+    }
+    if (!c->work_ready) return ESC_E_STATE;
+    const int64_t n_col = slot_stride(c) / FC_COL;
+    *full = (int64_t)c->nblk * n_col;
+    int64_t e = 0;
+    for (uint32_t x : c->h_touch) e += __builtin_popcount(x);
+    *entries = c->touch_on ? e : *full;
     return ESC_OK;
 }
 
@@ -2450,6 +2572,7 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->rm_valid = false;
     Patches P;
+    bool touch_grew = false;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t id = ids[i];
         if (id >= (int64_t)c->pod_cls.size()) {
@@ -2476,12 +2599,14 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
         kb_write_pod(k, blk, sl, f, p->cpu0[i], p->mem0[i], p->pair0[i], R ? p->xc_cpu + rof[i] : nullptr,
                      R ? p->xc_mem + rof[i] : nullptr, k.nxp ? p->xp_pair + pof[i] : nullptr,
                      [&](bool is64, int64_t at, uint64_t v) { P.add(is64 ? PT_KB64 : PT_KB32, at, v); });
+        touch_grew |= touch_mark(c, ci, q, f, p->pair0[i], k.nxp ? p->xp_pair + pof[i] : nullptr);
         ++c->live_pods;
         c->live_xc += R;
         c->live_xp += k.nxp;
         if (k.packed) { ++c->live_pk_pods; c->live_pk_xc += R; }
     }
     int32_t rc = apply_patches(c, P, pod_targets(c));
+    if (!rc && touch_grew) rc = touch_upload(c);
     if (rc || !c->placed) return rc;
     // a bound pod keeps its node; its PodRef follows the new record (and slot)
     std::vector<int64_t> touched(ids, ids + n);

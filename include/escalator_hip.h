@@ -428,6 +428,10 @@ int32_t esc_k1_trace(esc_ctx* ctx, uint64_t* out, int64_t cap_words, int64_t* n_
  * every workgroup's share of the pod bytes toward its measured streaming rate.  Results are
  * unchanged (integer sums are order-independent); call once after loading a snapshot. */
 int32_t esc_k1_calibrate(esc_ctx* ctx, int32_t rounds);
+/* K1's partial flush: *entries = 512-B column partials K1 writes (and K3 reads)
+ * per decision, *full = entries of a whole-row flush (workgroups x pod-slot columns); equal
+ * when the compact flush is off.  Multi-device: summed over the devices. */
+int32_t esc_k1_flush_entries(const esc_ctx* ctx, int64_t* entries, int64_t* full);
 
 /* ------------------------------------------- incremental snapshot (§8f rank 1)
  * Informer-style events patch the resident snapshot in place instead of a reload
