@@ -2853,7 +2853,7 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
     }
     c->xl_used += s->n_xl;
     c->n_nodes += n;
-    c->placed = c->rm_valid = false;                 // esc_load_placement again (node runs)
+    c->rm_valid = false;            // the placement stays: every table slot has a run and facts
     int32_t rc = apply_patches(c, P, {node_targets(c)});
     if (rc) return rc;
     if (first_changed)
@@ -2956,7 +2956,9 @@ int32_t esc_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
     }
     if (first_changed)
         HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
-    c->placed = c->rm_valid = false;
+    // the placement stays: a deleted node's entries are absent (K6 / K7 skip them) and its
+    // pods' PodRefs stay in its run until they are rebound or deleted
+    c->rm_valid = false;
     return patch_nodes(c, del);
 }
 
@@ -3056,12 +3058,20 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     const int32_t G = c->gi.G;
-    if (!c->d_taint_s || c->rm_nodes != N) {
+    // per-node arrays cover every table slot (n_cap), so that nodes added later
+    // (esc_nodes_add) have facts (none until refreshed) and an empty run of their own
+    const int64_t NC = std::max<int64_t>(c->n_cap, N);
+    if (!c->d_taint_s || c->rm_nodes != NC) {
         // per-node facts and the per-entry occupancy words, sized for this node table
         dfree(c->d_taint_s); dfree(c->d_no_delete); dfree(c->d_occ); dfree(c->d_e_pair);
         dfree(c->d_soft); dfree(c->d_hard); dfree(c->d_rm_out); dfree(c->d_rm_off); dfree(c->d_rm_list);
-        HIP_TRY(dalloc(&c->d_taint_s, std::max<int64_t>(N, 1)));
-        HIP_TRY(dalloc(&c->d_no_delete, std::max<int64_t>(N, 1)));
+        HIP_TRY(dalloc(&c->d_taint_s, std::max<int64_t>(NC, 1)));
+        HIP_TRY(dalloc(&c->d_no_delete, std::max<int64_t>(NC, 1)));
+        if (NC > N) {
+            const std::vector<int64_t> none(NC - N, INT64_MIN);
+            HIP_TRY(hipMemcpy(c->d_taint_s + N, none.data(), (NC - N) * 8, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemset(c->d_no_delete + N, 0, NC - N));
+        }
         HIP_TRY(dalloc(&c->d_occ, 2 * std::max<int64_t>(c->n_entries, 1)));
         HIP_TRY(dalloc(&c->d_soft, G)); HIP_TRY(dalloc(&c->d_hard, G));
         HIP_TRY(dalloc(&c->d_rm_out, G)); HIP_TRY(dalloc(&c->d_rm_off, G));
@@ -3087,7 +3097,7 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_rm), (size_t)std::max<int32_t>(G, 1) * sizeof(esc_removal)));
         c->h_soft.clear();
         c->h_hard.clear();
-        c->rm_nodes = N;
+        c->rm_nodes = NC;
     }
     if (N) {
         HIP_TRY(hipMemcpy(c->d_taint_s, taint_s, N * 8, hipMemcpyHostToDevice));
@@ -3095,17 +3105,25 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
     }
     if (pod_node) {
         // runs of PodRefs per node, each with spare room (esc_set_spare) for pods bound later
-        std::vector<uint32_t> cnt(N, 0);
+        std::vector<uint32_t> cnt(NC, 0);
+        int64_t bound = 0, live = 0;
         for (int64_t i = 0; i < np; ++i)
-            if (c->pod_cls[i] != -2 && pod_node[i] != NONE) ++cnt[pod_node[i]];
-        std::vector<uint32_t> off(N + 1, 0);
-        for (int64_t j = 0; j < N; ++j) {
-            const uint64_t cap = cnt[j] + (c->spare_frac > 0 ? (uint64_t)std::ceil(cnt[j] * c->spare_frac) + 2 : 0);
+            if (c->pod_cls[i] != -2 && pod_node[i] != NONE) { ++cnt[pod_node[i]]; ++bound; }
+        for (int64_t j = 0; j < N; ++j) live += (c->h_nflags[j] & ESC_NF_ABSENT) ? 0 : 1;
+        // room for pods bound later: a node's own count with the spare fraction on top, and at
+        // least the mean pods per node with the spare fraction on top — what a lightly loaded
+        // node, or a table slot with no node yet (added later), gets; the scheduler fills those
+        const uint64_t cap_new = c->spare_frac > 0
+            ? (uint64_t)std::ceil((double)bound / (double)std::max<int64_t>(live, 1) * (1.0 + c->spare_frac)) + 4 : 0;
+        std::vector<uint32_t> off(NC + 1, 0);
+        for (int64_t j = 0; j < NC; ++j) {
+            const uint64_t own = cnt[j] + (c->spare_frac > 0 ? (uint64_t)std::ceil(cnt[j] * c->spare_frac) + 2 : 0);
+            const uint64_t cap = j >= N ? cap_new : std::max(own, cap_new);
             if ((uint64_t)off[j] + cap >= 0xFFFFFFFFull) return ESC_E_LIMIT;
             off[j + 1] = off[j] + (uint32_t)cap;
         }
-        const int64_t total = off[N];
-        std::vector<uint32_t> len(std::max<int64_t>(N, 1), 0), slot(std::max<int64_t>(total, 1), 0);
+        const int64_t total = off[NC];
+        std::vector<uint32_t> len(std::max<int64_t>(NC, 1), 0), slot(std::max<int64_t>(total, 1), 0);
         c->h_run_pod.assign(std::max<int64_t>(total, 1), -1);
         c->h_pod_node.assign(np, NONE);
         c->h_pod_rpos.assign(np, -1);
@@ -3121,11 +3139,11 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
         dfree(c->d_refs); dfree(c->d_nrun_off); dfree(c->d_nrun_len);
         uint32_t* d_slot = nullptr;
         HIP_TRY(dalloc(&c->d_refs, std::max<int64_t>(total, 1)));
-        HIP_TRY(dalloc(&c->d_nrun_off, N + 1));
-        HIP_TRY(dalloc(&c->d_nrun_len, std::max<int64_t>(N, 1)));
+        HIP_TRY(dalloc(&c->d_nrun_off, NC + 1));
+        HIP_TRY(dalloc(&c->d_nrun_len, std::max<int64_t>(NC, 1)));
         HIP_TRY(dalloc(&d_slot, slot.size()));
         HIP_TRY(hipMemcpy(d_slot, slot.data(), slot.size() * 4, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(c->d_nrun_off, off.data(), (N + 1) * 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(c->d_nrun_off, off.data(), (NC + 1) * 4, hipMemcpyHostToDevice));
         HIP_TRY(hipMemcpy(c->d_nrun_len, len.data(), len.size() * 4, hipMemcpyHostToDevice));
         const hipError_t e = launch_podref_fill(pod_dev(c, c->cur), d_slot, nullptr, total, c->d_refs, c->stream);
         const hipError_t e2 = hipStreamSynchronize(c->stream);

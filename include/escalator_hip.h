@@ -459,8 +459,10 @@ int32_t esc_nodes_update(esc_ctx* ctx, const int64_t* ids, int64_t n, const uint
  * lists them after every loaded node.  esc_nodes_delete removes nodes by index: the slot
  * becomes ESC_NF_ABSENT (no kernel counts it, allNodes[0] moves to the group's next
  * member) and its dry-mode tracker entries are dropped (a host that re-adds a tracked
- * name re-applies it with esc_tracker_update).  Both invalidate esc_load_placement; an
- * add that does not fit returns ESC_E_LIMIT with nothing applied (reload).  Every check
+ * name re-applies it with esc_tracker_update).  Both keep esc_load_placement's binding
+ * (an added node starts with no pods, no taint time and no no-delete flag until
+ * esc_pods_bind / a node-facts refresh); an add that does not fit returns ESC_E_LIMIT
+ * with nothing applied (reload).  Every check
  * depends on the node table alone, which every rank holds, so all ranks of a sharded job
  * accept or refuse the same batch. */
 int32_t esc_nodes_add(esc_ctx* ctx, const esc_node_soa* nodes, int64_t* ids_out);
@@ -491,8 +493,11 @@ int32_t esc_tracker_list(const esc_ctx* ctx, int32_t group, int64_t* idx_out, in
  * parse) and its atlassian.com/no-delete annotation (non-empty = safe from deletion).
  * Pod events keep the binding current: esc_pods_upsert rewrites a bound pod's reference,
  * esc_pods_delete drops it, esc_pods_bind moves pods between nodes (runs per node keep
- * esc_set_spare room; ESC_E_LIMIT when a run is full).  Node additions / deletions need
- * esc_load_placement again (ESC_E_STATE until then).  esc_try_remove then evaluates, per
+ * esc_set_spare room; ESC_E_LIMIT when a run is full).  Node additions / deletions keep
+ * it: every node-table slot (esc_set_spare's free slots included) has a run and facts, a
+ * free slot's run sized for the mean pods per node plus the spare fraction; refresh the
+ * facts (esc_load_placement with pod_node NULL, n_nodes entries: the table as it is now,
+ * deleted slots included) when taints change.  esc_try_remove then evaluates, per
  * group, its tainted nodes in snapshot order: now - taintTime > soft grace and (NodeEmpty
  * or > hard grace) -> delete (never in dry mode).
  * Several ranks (each holding its pod shard): the per-node occupancy is this rank's pods

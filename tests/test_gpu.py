@@ -807,6 +807,118 @@ def test_reaping_follows_pod_events(esc, seed):
         _check_reaping(ctx, groups, cur, nodes, trackers, now_ns, soft, hard)
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_reaping_across_node_events(esc, seed):
+    """The placement survives node informer events (§8f rank 2): node deletes, node adds
+    (their pods bound with esc_pods_bind into the runs reserved for new table slots), pod
+    moves and a node-facts refresh, with no esc_load_placement of the pods in between;
+    TryRemoveTaintedNodes equals the literal oracle on the live nodes in snapshot order."""
+    from escalator_amd.objects import placement, taint_time, NO_DELETE_ANNOTATION
+    NONE = 0xFFFFFFFF
+    rng = random.Random(9500 + seed)
+    G = rng.choice([2, 6, 12])
+    groups, pods, nodes, now_ns = make_reaping_cluster(rng, G, 500, rng.choice([30, 90]))
+    trackers = make_trackers(rng, groups, nodes)
+    ctx = esc.Context(groups)
+    ctx.set_spare(2.0)
+    P, N = ctx.pack(pods, nodes, trackers)
+    ctx.load(P, N)
+    pn, ts, nd = placement(pods, nodes)
+    ctx.load_placement(pn, ts, nd)
+    live = dict(enumerate(nodes))
+    index = {x["name"]: j for j, x in live.items()}
+    pod_live = dict(enumerate(pods))
+    soft = np.array([rng.choice([0, 60, 300]) * 10**9 for _ in range(G)], np.int64)
+    hard = soft + np.array([rng.choice([0, 600]) * 10**9 for _ in range(G)], np.int64)
+    now_s = now_ns // 10**9
+    reloads = []
+    hw = len(nodes)                                          # table slots in use (deleted included)
+    for rnd in range(5):
+        dels = rng.sample(sorted(live), k=min(len(live) - 1, rng.randrange(0, 6)))
+        if dels:
+            ctx.nodes_delete(dels)
+            for j in dels:
+                del index[live.pop(j)["name"]]
+        new = make_nodes(rng, rng.randrange(1, 8), groups, big_frac=0.0)
+        for k, x in enumerate(new):
+            x["name"] = "r%d-new%d" % (rnd, k)
+            if rng.random() < 0.6 and "atlassian.com/escalator" not in x["taints"]:
+                x["taints"] = x["taints"] + ["atlassian.com/escalator"]
+            x["taint_value"] = rng.choice([str(now_s - rng.randrange(0, 900)), "bad", None])
+            if rng.random() < 0.15:
+                x["annotations"] = {NO_DELETE_ANNOTATION: "true"}
+        _, packed = ctx.pack([], new)
+        try:
+            ids = [int(j) for j in ctx.nodes_add(packed)]
+        except esc._lib.EscError as e:                       # spare room short: reload all
+            assert e.code == esc._lib.ESC_E_LIMIT
+            order = sorted(live)
+            lst = [live[j] for j in order] + new
+            P, N = ctx.pack([pod_live[i] for i in sorted(pod_live)], lst, trackers)
+            ctx.load(P, N)
+            pod_live = dict(enumerate(pod_live[i] for i in sorted(pod_live)))
+            live = dict(enumerate(lst))
+            index = {x["name"]: j for j, x in live.items()}
+            ctx.load_placement(*placement([pod_live[i] for i in sorted(pod_live)], lst))
+            hw = len(lst)
+            reloads.append(("nodes_add", rnd))
+        else:
+            assert ids == list(range(hw, hw + len(new)))
+            hw += len(new)
+            for j, x in zip(ids, new):
+                live[j] = x
+                index[x["name"]] = j
+        # pods rescheduled: about the mean pods per node onto each new node (round robin),
+        # others onto existing nodes or unbound
+        names = [x["name"] for x in new if x["name"] in index]
+        mv = rng.sample(sorted(pod_live), 6 * len(names) + 20)
+        to = [names[k % len(names)] if k < 6 * len(names) else
+              (live[rng.choice(sorted(live))]["name"] if rng.random() < 0.85 else "") for k in range(len(mv))]
+        try:
+            ctx.pods_bind(mv, [index[t] if t else NONE for t in to])
+        except esc._lib.EscError as e:                       # a run is full: re-bind everything
+            assert e.code == esc._lib.ESC_E_LIMIT
+            for i, t in zip(mv, to):
+                pod_live[i] = dict(pod_live[i], node_name=t)
+            full = np.full(max(pod_live) + 1, NONE, np.uint32)
+            for i, q in pod_live.items():
+                full[i] = index.get(q.get("node_name") or "", NONE)
+            ctx.load_placement(full, *_facts(live, hw, taint_time))
+            reloads.append(("pods_bind", rnd))
+        for i, t in zip(mv, to):
+            pod_live[i] = dict(pod_live[i], node_name=t)
+        # the node facts (taint times, no-delete) of every table slot, the new nodes' included
+        ctx.load_placement(None, *_facts(live, hw, taint_time))
+        idx = sorted(live)
+        lst = [live[j] for j in idx]
+        cur = [pod_live[i] for i in sorted(pod_live)]
+        res = ctx.try_remove(now_ns, soft, hard)
+        for g, grp in enumerate(groups):
+            L = O.scale_node_group(grp, {}, cur, lst, tracker=trackers.get(g, []))
+            pods_g = O.filtered_list(cur, O.group_pod_filter(grp))
+            all_nodes = [x for x in lst if O.new_node_label_filter_func(grp.get("label_key", ""),
+                                                                        grp.get("label_value", ""))(x)]
+            tainted = L["tainted"]
+            neg, remaining, ks = O.try_remove_tainted_nodes(grp, [lst[i] for i in tainted], pods_g, all_nodes, now_ns,
+                                                            int(soft[g]), int(hard[g]), bool(grp.get("dry_mode")))
+            r = res[g]
+            assert int(r["n_candidates"]) == len(tainted), (rnd, g)
+            assert (-int(r["n_delete"]), int(r["pods_remaining"])) == (neg, remaining), (rnd, g)
+            assert list(ctx.removal_nodes(g)) == [idx[tainted[k]] for k in ks], (rnd, g)
+    assert not reloads, reloads
+
+
+def _facts(live, hw, taint_time):
+    """esc_load_placement's node facts over table slots [0, hw) (deleted slots: none)."""
+    from escalator_amd.objects import NO_DELETE_ANNOTATION
+    ts = np.full(hw, np.iinfo(np.int64).min, np.int64)
+    nd = np.zeros(hw, np.uint8)
+    for j, x in live.items():
+        ts[j] = taint_time(x)
+        nd[j] = 1 if (x.get("annotations") or {}).get(NO_DELETE_ANNOTATION, "") else 0
+    return ts, nd
+
+
 @pytest.mark.parametrize("graphless", [True])
 def test_reaping_sharded_host_exchange(esc, graphless):
     """Reaping over three pod shards on one device: each rank's K6 counts its own pods per
