@@ -271,6 +271,9 @@ struct esc_ctx {
     std::vector<PodClass> h_cls;
     std::vector<int> h_cls_of;                                // signature id -> class index (-1: none)
     std::vector<uint32_t> h_cflags;                           // C-section flags (deletes keep the counts)
+    std::vector<int64_t> c_free;                              // free C slots (C-array index), room in h_cflags
+    std::vector<uint32_t> h_cused;                            // a C slot's pod's own records | pairs << 16
+    std::vector<uint32_t> h_xc_base, h_xp_base;               // C tiles' record / pair offsets
     int64_t live_pods = 0, live_xc = 0, live_xp = 0;
     int64_t live_pk_pods = 0, live_pk_xc = 0;   // of them in packed K classes
     // node state mirrors for esc_nodes_update
@@ -312,6 +315,12 @@ int ctx_device(const esc_ctx* c) { return c->device; }
 }
 
 namespace {
+
+// Spare C slots (esc_load_pods with esc_set_spare): room per slot, slots per 64-pod tile.
+constexpr int CS_SLOTS = 16, CS_XREG = 4, CS_XINIT = 2, CS_REC = CS_XREG + CS_XINIT + 1, CS_XP = 6;
+static_assert(CS_SLOTS * CS_REC <= 128 && CS_SLOTS * CS_XP <= 128, "a spare C tile stays on K1's C path");
+constexpr uint32_t CS_FLAGS = ESC_PF_DAEMONSET | ESC_PF_HAS_OVH | (uint32_t)CS_XREG << ESC_PF_XREG_SHIFT |
+                              (uint32_t)CS_XINIT << ESC_PF_XINIT_SHIFT | (uint32_t)CS_XP << ESC_PF_XPAIR_SHIFT;
 
 // K class of a pod: its record signature (at most 3 extra container
 // records and 3 extra pairs; -1: the C section) | packed << 7 when its values fit the packed
@@ -888,6 +897,24 @@ bool touch_mark(esc_ctx* c, int32_t ci, int64_t q, uint32_t f, uint32_t pair0, c
     return grew;
 }
 
+// The same for a pod written into C slot d (K1 and k_touch give workgroup b the C tiles
+// [b * per, (b + 1) * per), per = ceil(c_tiles / nblk)).
+bool touch_mark_c(esc_ctx* c, int64_t d, uint32_t f, uint32_t pair0, const uint32_t* xp) {
+    if (!c->touch_on || (f & ESC_PF_DAEMONSET) || c->nblk <= 0) return false;
+    const int64_t per = (c->c_tiles + c->nblk - 1) / c->nblk, b = (d / CTILE) / std::max<int64_t>(per, 1);
+    uint32_t* row = c->h_touch.data() + (size_t)b * c->touch_tw;
+    bool grew = false;
+    auto mark = [&](uint32_t slot) {
+        const uint32_t col = slot / FC_COL, bit = 1u << (col & 31);
+        if (!(row[col >> 5] & bit)) { row[col >> 5] |= bit; grew = true; }
+    };
+    const uint32_t n_gp = c->gi.n_gp;
+    if (pair0 < n_gp) mark(pair0);
+    for (uint32_t k = 0; k < pf_xpair(f); ++k)
+        if (xp[k] < n_gp) mark(xp[k]);
+    return grew;
+}
+
 // Grid geometry for the current snapshot.
 int32_t ensure_work(esc_ctx* c) {
     if (c->work_ready) return ESC_OK;
@@ -1315,10 +1342,16 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         cls_of[id] = (int)cls.size();
         cls.push_back(k);
     }
-    const int64_t k_tiles = kt, c_tiles = (n_c + CTILE - 1) / CTILE;
+    // spare C slots (esc_set_spare): tiles of CS_SLOTS free slots, each with room for a pod of
+    // up to CS_XREG regular and CS_XINIT init containers, an overhead and CS_XP extra pairs
+    // (the tile's other slots hold nothing, so no tile passes the C path's 128 records of a
+    // kind); an upsert of a pod outside the K classes (or of a full K class) takes one
+    const int64_t n_cs = c->spare_frac > 0 ? std::max<int64_t>(CS_SLOTS, (int64_t)std::ceil((double)n_c * c->spare_frac)) : 0;
+    const int64_t c_real = (n_c + CTILE - 1) / CTILE, cs_tiles = (n_cs + CS_SLOTS - 1) / CS_SLOTS;
+    const int64_t k_tiles = kt, c_tiles = c_real + cs_tiles;
     const int64_t c0 = k_tiles * TILE, npad = c_tiles * CTILE;   // C arrays: the C section only
     // C record arrays; one element of padding (K1 clamps its unconditional C record loads)
-    const int64_t nxc_dev = (int64_t)sc_c + 1, nxp_dev = (int64_t)sp_c + 1;
+    const int64_t nxc_dev = (int64_t)sc_c + cs_tiles * CS_SLOTS * CS_REC + 1, nxp_dev = (int64_t)sp_c + cs_tiles * CS_SLOTS * CS_XP + 1;
     if (nxc_dev >= (int64_t)0xFFFFFFFF || nxp_dev >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
     std::vector<uint32_t> hf(npad, ESC_PF_DAEMONSET), hc(npad, 0), hp(npad, NONE);
     std::vector<int64_t> hm(npad, 0), hxc(nxc_dev, 0), hxm(nxc_dev, 0);
@@ -1386,6 +1419,19 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
             rc += nc;
             rp += nx;
         }
+        for (int64_t t = c_real; t < c_tiles; ++t) {         // spare C tiles: free slots with room
+            xc_base[t] = (uint32_t)oc;
+            xp_base[t] = (uint32_t)op;
+            for (int l = 0; l < CS_SLOTS; ++l) {
+                hf[t * CTILE + l] = CS_FLAGS;
+                for (int k = 0; k < CS_REC; ++k) {       // neutral records: 0 added, init keys absent
+                    const bool init = k >= CS_XREG && k < CS_XREG + CS_XINIT;
+                    hxc[oc + k] = hxm[oc + k] = init ? INT64_MIN : 0;
+                }
+                oc += CS_REC;
+                op += CS_XP;                             // hxp is NONE already
+            }
+        }
         xc_base[c_tiles] = (uint32_t)oc;
         xp_base[c_tiles] = (uint32_t)op;
     }
@@ -1444,6 +1490,14 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         for (int64_t q = (cls[ci].t1 - cls[ci].t0) * TILE - 1; q >= cnt[id]; --q) fr.push_back(q);
     }
     c->h_cflags.assign(hf.begin(), hf.end());
+    c->h_xc_base = xc_base;
+    c->h_xp_base = xp_base;
+    c->c_free.clear();
+    for (int64_t t = c_tiles - 1; t >= c_real; --t)
+        for (int l = CS_SLOTS - 1; l >= 0; --l) c->c_free.push_back(t * CTILE + l);
+    c->h_cused.assign(npad, 0);
+    for (int64_t d = 0; d < npad; ++d)
+        if (!(hf[d] & ESC_PF_DAEMONSET) || d < n_c) c->h_cused[d] = pf_xctr(hf[d]) | pf_xpair(hf[d]) << 16;
     c->live_pods = n;
     c->live_xc = p->n_xc;
     c->live_xp = p->n_xp;
@@ -2211,10 +2265,12 @@ void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
     if (ci == -1) {
         const int64_t d = c->pod_pos[id] - c->k_tiles * TILE;    // C-array index
         uint32_t& f = c->h_cflags[d];
-        c->live_xc -= pf_xctr(f);
-        c->live_xp -= pf_xpair(f);
+        c->live_xc -= c->h_cused[d] & 0xFFFF;
+        c->live_xp -= c->h_cused[d] >> 16;
+        c->h_cused[d] = 0;
         f |= ESC_PF_DAEMONSET;
         P.add(PT_FLAGS, d, f);
+        c->c_free.push_back(d);                           // its room (counts) stays: reusable
     } else {
         const PodClass& k = c->h_cls[ci];
         const int64_t q = c->pod_pos[id];
@@ -2515,8 +2571,62 @@ namespace {
 // share of a batch before it applies any (all or nothing across devices too).
 struct UpsertPlan {
     std::vector<int64_t> rof, pof;   // each pod's first record / extra pair in the batch
-    std::vector<int32_t> tgt;        // its K class
+    std::vector<int32_t> tgt;        // its K class, or -1: the C slot cslot
+    std::vector<int64_t> cslot;
 };
+
+// Does C slot room `cf` (counts of a slot's flags) hold a pod with flags f?  Its records
+// and pairs take the slot's first positions of each kind, the rest stay neutral.
+bool c_room(uint32_t cf, uint32_t f) {
+    return pf_xreg(f) <= pf_xreg(cf) && pf_xinit(f) <= pf_xinit(cf) && (!(f & ESC_PF_HAS_OVH) || (cf & ESC_PF_HAS_OVH)) &&
+           pf_xpair(f) <= pf_xpair(cf);
+}
+
+bool touch_mark_c(esc_ctx* c, int64_t d, uint32_t f, uint32_t pair0, const uint32_t* xp);
+
+// Writes pod i of the batch into C slot d (its room: the slot's flags' counts; the pod's
+// records and pairs first of each kind, the rest neutral — 0 for added records, absent keys
+// for init containers, NONE for pairs).  True when K1's touched columns grew.
+bool upsert_c(esc_ctx* c, int64_t id, int64_t d, const esc_pod_soa* p, int64_t i, int64_t rof, int64_t pof, Patches& P) {
+    const int64_t c0 = c->k_tiles * TILE;
+    if (!(c->pod_cls[id] == -1 && c->pod_pos[id] - c0 == d)) {
+        remove_pod(c, id, P);
+        auto it = std::find(c->c_free.begin(), c->c_free.end(), d);
+        if (it != c->c_free.end()) c->c_free.erase(it);
+        c->pod_cls[id] = -1;
+        c->pod_pos[id] = c0 + d;
+    } else {
+        --c->live_pods;                                   // re-added below
+        c->live_xc -= c->h_cused[d] & 0xFFFF;
+        c->live_xp -= c->h_cused[d] >> 16;
+    }
+    const uint32_t f = p->flags[i], cf = c->h_cflags[d];
+    const uint32_t nf = (cf & ~KP_POD_FLAGS) | (f & KP_POD_FLAGS);
+    const int64_t t = d / CTILE;
+    uint32_t ro = c->h_xc_base[t], po = c->h_xp_base[t];
+    for (int64_t k = t * CTILE; k < d; ++k) { ro += pf_xctr(c->h_cflags[k]); po += pf_xpair(c->h_cflags[k]); }
+    P.add(PT_FLAGS, d, nf);
+    P.add(PT_CPU0, d, p->cpu0[i]);
+    P.add(PT_MEM0, d, (uint64_t)p->mem0[i]);
+    P.add(PT_PAIR0, d, p->pair0[i]);
+    const uint32_t xr = pf_xreg(f), xi = pf_xinit(f), ov = (f & ESC_PF_HAS_OVH) ? 1u : 0u;
+    auto rec = [&](uint32_t at, bool have, int64_t src, int64_t neutral) {
+        P.add(PT_XC_CPU, at, (uint64_t)(have ? p->xc_cpu[src] : neutral));
+        P.add(PT_XC_MEM, at, (uint64_t)(have ? p->xc_mem[src] : neutral));
+    };
+    uint32_t o = ro;
+    for (uint32_t k = 0; k < pf_xreg(cf); ++k) rec(o++, k < xr, rof + k, 0);
+    for (uint32_t k = 0; k < pf_xinit(cf); ++k) rec(o++, k < xi, rof + xr + k, INT64_MIN);
+    if (cf & ESC_PF_HAS_OVH) rec(o++, ov != 0, rof + xr + xi, 0);
+    const uint32_t nx = pf_xpair(f);
+    for (uint32_t k = 0; k < pf_xpair(cf); ++k) P.add(PT_XP, po + k, k < nx ? p->xp_pair[pof + k] : NONE);
+    c->h_cflags[d] = nf;
+    c->h_cused[d] = (xr + xi + ov) | nx << 16;
+    ++c->live_pods;
+    c->live_xc += xr + xi + ov;
+    c->live_xp += nx;
+    return touch_mark_c(c, d, f, p->pair0[i], nx ? p->xp_pair + pof : nullptr);
+}
 
 int32_t upsert_plan(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, UpsertPlan& u) {
     if (!c || !p || p->n_pods < 0 || (p->n_pods > 0 && (!ids || !p->flags || !p->cpu0 || !p->mem0 || !p->pair0)))
@@ -2525,8 +2635,10 @@ int32_t upsert_plan(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, Upsert
     if (!c->pods_loaded) return ESC_E_STATE;
     const int64_t n = p->n_pods;
     // validate the batch and that every pod fits in place (all or nothing)
-    std::vector<int64_t> need(c->h_cls.size(), 0), rof(n), pof(n);
+    std::vector<int64_t> need(c->h_cls.size(), 0), rof(n), pof(n), cslot(n, -1);
     std::vector<int32_t> tgt(n);
+    std::vector<char> taken(c->c_free.size(), 0);          // free C slots this batch takes
+    const int64_t c0 = c->k_tiles * TILE;
     uint64_t sc = 0, sp = 0;
     std::vector<int64_t> seen(ids, ids + n);
     std::sort(seen.begin(), seen.end());
@@ -2548,18 +2660,36 @@ int32_t upsert_plan(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, Upsert
         sp += nx;
         const int sid = pod_class_id(f, p->cpu0[i], p->mem0[i], p->pair0[i], nc ? p->xc_cpu + sc - nc : nullptr,
                                      nc ? p->xc_mem + sc - nc : nullptr);
-        const int ci = sid < 0 ? -1 : c->h_cls_of[sid];
-        if (ci < 0) return ESC_E_LIMIT;            // C-section pod or a signature the layout has no class for
-        tgt[i] = ci;
+        int ci = sid < 0 ? -1 : c->h_cls_of[sid];
         const int64_t id = ids[i];
-        const bool in_place = id < (int64_t)c->pod_cls.size() && c->pod_cls[id] == ci;
-        if (!in_place) ++need[ci];
+        const bool known = id < (int64_t)c->pod_cls.size();
+        if (ci >= 0 && !(known && c->pod_cls[id] == ci)) {
+            if (need[ci] < (int64_t)c->cls_free[ci].size()) ++need[ci];
+            else ci = -1;                                  // its class is full: a C slot
+        }
+        tgt[i] = ci;
+        if (ci >= 0) continue;
+        // a C slot: its own (when it has room), else a free one with room
+        if (known && c->pod_cls[id] == -1 && c_room(c->h_cflags[c->pod_pos[id] - c0], f)) {
+            cslot[i] = c->pod_pos[id] - c0;
+            continue;
+        }
+        for (int64_t k = (int64_t)c->c_free.size() - 1; k >= 0 && cslot[i] < 0; --k)
+            if (!taken[k] && c_room(c->h_cflags[c->c_free[k]], f)) {
+                taken[k] = 1;
+                cslot[i] = c->c_free[k];
+            }
+        if (cslot[i] < 0) {                                // no room in place: reload
+            if (std::getenv("ESC_DEBUG_UPSERT"))
+                fprintf(stderr, "[esc] upsert %lld: no C room for flags %08x (class %d, free C slots %zu)\n",
+                        (long long)id, f, sid, c->c_free.size());
+            return ESC_E_LIMIT;
+        }
     }
-    for (size_t ci = 0; ci < need.size(); ++ci)
-        if (need[ci] > (int64_t)c->cls_free[ci].size()) return ESC_E_LIMIT;   // spare exhausted: reload
     u.rof.swap(rof);
     u.pof.swap(pof);
     u.tgt.swap(tgt);
+    u.cslot.swap(cslot);
     return ESC_OK;
 }
 
@@ -2580,6 +2710,10 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
             c->pod_pos.resize(id + 1, 0);
         }
         const int32_t ci = tgt[i];
+        if (ci < 0) {
+            touch_grew |= upsert_c(c, id, u.cslot[i], p, i, rof[i], pof[i], P);
+            continue;
+        }
         if (c->pod_cls[id] != ci) {
             remove_pod(c, id, P);
             c->pod_cls[id] = ci;

@@ -439,9 +439,11 @@ int32_t esc_k1_flush_entries(const esc_ctx* ctx, int64_t* entries, int64_t* full
  * informer caches, pkg/k8s/cache.go:16-56 -> pod_listers.go:33, node_listers.go:33).
  * Pod ids are the indices of esc_load_pods' input; new ids (< 2^31) insert.  A pod
  * lands in the spare slots of its record-signature class (esc_set_spare, before the
- * load, reserves them); a batch that does not fit in place — spare exhausted, a pod
- * with > 3 container records or > 3 extra pairs, or a signature absent at load —
- * returns ESC_E_LIMIT with nothing applied, and the caller reloads.  Node events may
+ * load, reserves them); a pod with > 3 container records or > 3 extra pairs (or whose
+ * class is full) stays in its own C-section slot when that has room, else takes a spare
+ * C slot (room for 4 extra regular and 2 init containers, an overhead and 6 extra pairs;
+ * unused records stay neutral).  A batch that does not fit in place returns ESC_E_LIMIT
+ * with nothing applied, and the caller reloads.  Node events may
  * change Spec.Unschedulable, the escalator taint and allocatable; label or creation-time
  * changes need esc_load_nodes (tracker changes: esc_tracker_update).  Every call
  * completes before returning.                                                       */

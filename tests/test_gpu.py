@@ -680,6 +680,69 @@ def test_incremental_events_vs_literal(esc, seed):
     assert ctx.decide_all(states)[0].tobytes() == before
 
 
+@pytest.mark.parametrize("seed", range(4))
+def test_c_pod_events_vs_literal(esc, seed):
+    """Upserts of pods outside the K classes (more than 3 extra container records: the C
+    section) patch in place (§8f rank 1): into the pod's own C slot when it has room, else
+    into a spare C slot (esc_set_spare), whose unused records stay neutral; pods change
+    between the K and C sections, are deleted and re-inserted.  Every decision then equals
+    the literal oracle; a pod bigger than any free slot's room is refused whole."""
+    from escalator_amd._lib import ESC_E_LIMIT
+    from randobj import _req
+    rng = random.Random(7300 + seed)
+    G = rng.choice([3, 8])
+    groups = make_groups(rng, G, with_default=True)
+
+    def c_pod(n_reg=5):                      # 5 containers (4 extra records, + init / overhead): a C pod
+        q = make_pods(rng, 1, groups, big_frac=0.0)[0]
+        # (a first container with a negative cpu is not inline: 5 extra records, more than a
+        # spare slot's room, so big values only from the second one on)
+        q["containers"] = [_req(rng, k > 0 and rng.random() < 0.05) for k in range(n_reg)]
+        return q
+
+    pods = make_pods(rng, 300, groups, big_frac=0.02) + [c_pod() for _ in range(40)]
+    nodes = make_nodes(rng, 60, groups, big_frac=0.0)
+    states = make_states(rng, G)
+    ctx = esc.Context(groups)
+    ctx.set_spare(2.0)                       # spare C room: max(16, 2 x 40) slots
+    P, N = ctx.pack(pods, nodes)
+    assert sum(not _fits_k(P, k) for k in range(len(pods))) >= 40
+    ctx.load(P, N)
+    live = dict(enumerate(pods))
+    next_id = len(pods)
+    for rnd in range(3):
+        ev_ids, ev_objs = [], []
+        for i in rng.sample(sorted(live), 16):               # K <-> C changes of existing pods
+            ev_ids.append(i)
+            ev_objs.append(c_pod() if rng.random() < 0.6 else make_pods(rng, 1, groups, big_frac=0.02)[0])
+        for _ in range(6):                                   # new C pods
+            ev_ids.append(next_id)
+            ev_objs.append(c_pod())
+            next_id += 1
+        Pe, _ = ctx.pack(ev_objs, [])
+        assert ctx.pods_upsert(ev_ids, Pe) == 0, rnd
+        for i, q in zip(ev_ids, ev_objs):
+            live[i] = q
+        dels = rng.sample(sorted(live), 12)
+        ctx.pods_delete(dels)
+        for i in dels:
+            del live[i]
+        cur = [live[i] for i in sorted(live)]
+        tot, dec = ctx.decide_all(states)
+        for g in range(G):
+            L = O.scale_node_group(groups[g], states[g], cur, nodes)
+            t, d = tot[g], dec[g]
+            assert t["n_pods"] == L["n_pods"], (rnd, g)
+            assert (t["pod_cpu_m"], t["pod_mem_b"]) == (L["pod_cpu_m"], L["pod_mem_b"]) or L["pod_cpu_m"] is None, (rnd, g)
+            assert esc._lib.BRANCHES[d["branch"]] == L["branch"], (rnd, g)
+            assert int(d["delta"]) == L["delta"] and _bits(d["cpu_pct"]) == _bits(L["cpu_pct"]), (rnd, g)
+    # a pod with more containers than any free C slot holds: nothing applied
+    before = ctx.decide_all(states)[0].tobytes()
+    Pb, _ = ctx.pack([c_pod(9)], [])
+    assert ctx.pods_upsert([next_id], Pb) == ESC_E_LIMIT
+    assert ctx.decide_all(states)[0].tobytes() == before
+
+
 # ------------------------------------------------ scale-down reaping (§8f rank 2)
 def _check_reaping(ctx, groups, pods, nodes, trackers, now_ns, soft, hard):
     res = ctx.try_remove(now_ns, soft, hard)
