@@ -42,8 +42,8 @@ def stream_bytes(ctx, s, rank, world) -> tuple[int, int]:
     from escalator_amd import layout
     from oracle import soa
     pb, nb = ctx.stream_bytes()
-    assert pb == layout.pod_bytes(s.pods()), "K1 bytes"
     n_gp = len(soa.group_tables(s.groups)["pair_ids"])
+    assert pb == layout.pod_bytes(s.pods(), n_gp), "K1 bytes"
     assert nb == layout.node_bytes(s.nodes(), n_gp, rank, world), "K2 bytes"
     return pb, nb
 
@@ -389,7 +389,8 @@ def main():
     t0 = time.time()
     s = esc.Synth(P, N, G, config=args.config, seed=0xE5CA1A7E00000000 + args.config, p_lo=lo, p_hi=hi, threads=16)
     from escalator_amd import layout
-    shard_bytes = layout.pod_bytes(s.pods()) // (len(multi) if multi else 1)
+    from oracle import soa as _soa
+    shard_bytes = layout.pod_bytes(s.pods(), len(_soa.group_tables(s.groups)["pair_ids"])) // (len(multi) if multi else 1)
     replicas = int(max(1, min(8, -(-1_000_000_000 // max(shard_bytes, 1)))))   # >= 1 GB resident: HBM-served
     if multi:
         ctx = esc.Context(s, devices=multi)

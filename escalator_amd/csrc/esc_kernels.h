@@ -18,15 +18,15 @@ struct PodClass {
     uint32_t xreg, xinit, ovh, nxp;
     uint32_t kind;             // packed * 16 + (xreg + xinit + ovh) * 4 + nxp: selects K1's pipeline
     uint32_t wt;               // work weight of one tile: its 16-B loads per lane (= block KB)
-    uint32_t packed;           // 1: the packed block layout (kp_*, below)
+    uint32_t packed;           // 0 plain, 1 packed (12 B / pod), 2 packed small (8 B / pod): kp_*, kp8_* below
     uint32_t pad;
 };
 // weight (16-B loads per lane) of a K tile with R records and NXP extra pairs per pod
 constexpr uint32_t k_tile_weight(uint32_t R, uint32_t NXP, uint32_t packed = 0) {
-    return packed ? 3 + 2 * R + NXP : 5 + 4 * R + NXP;
+    return packed == 2 ? 2 + 2 * R + NXP : (packed ? 3 + 2 * R + NXP : 5 + 4 * R + NXP);
 }
 constexpr int POD_SIG_IDS = 128;     // signatures with <= 3 extra records and <= 3 extra pairs
-constexpr int POD_CLASS_IDS = 256;   // class id = signature | packed << 7
+constexpr int POD_CLASS_IDS = 384;   // class id = signature | packed << 7
 constexpr int K1_SEGS = 4;           // class runs per K1 workgroup in the work plan (at most)
 
 // K blocks (tile-major K section).  Tile t of a class is ONE contiguous block of wt KB
@@ -69,13 +69,39 @@ constexpr uint32_t KP_POD_FLAGS = ESC_PF_DAEMONSET | ESC_PF_STATIC | ESC_PF_HAS_
 constexpr int KP_CPU_BITS = 20;
 constexpr uint64_t KP_CPU_ABSENT = (uint64_t(1) << KP_CPU_BITS) - 1;
 constexpr uint64_t KP_MEM_ABSENT = (uint64_t(1) << 44) - 1;
-// the word a freed / padding slot holds in the first row (plain: the flags; packed: pair0|flags)
-__host__ __device__ inline uint32_t kb_free_word(const PodClass& C) {
-    return C.packed ? (ESC_PF_DAEMONSET << KP_FLAG_SHIFT) | KP_PAIR_NONE : ESC_PF_DAEMONSET;
+// Packed small K blocks (PodClass::packed == 2): a pod whose packed values also have
+// cpu0 < 2^14 m and mem0 < 2^34 B (16 cores, 16 GiB in its first container: most pods), in
+// a context with fewer than 2^14 - 1 group pairs, is ONE u64 (8 B):
+//   u64   [0, 512)            cpu0 | mem0 << 14 | pair0 << 48 (14 bits; KP8_PAIR_NONE: no
+//                             pair, or one no group selects) | daemonset << 62 |
+//                             blocks-default << 63 (static, has-selector or affinity: the
+//                             default filter's other conditions, node_group.go:263-273)
+//   u64   record k            [512 + 512k, +512): as in the packed block
+//   u32   extra pair k        [512 + 512R + 256k, +256)
+constexpr int KP8_REC = 512;
+constexpr int KP8_CPU_BITS = 14, KP8_MEM_BITS = 34, KP8_PAIR_SHIFT = 48;
+constexpr uint64_t KP8_CPU_MASK = (uint64_t(1) << KP8_CPU_BITS) - 1;
+constexpr uint64_t KP8_MEM_MASK = (uint64_t(1) << KP8_MEM_BITS) - 1;
+constexpr uint32_t KP8_PAIR_NONE = (1u << 14) - 1;
+constexpr uint64_t KP8_DS = uint64_t(1) << 62, KP8_NODEF = uint64_t(1) << 63;
+__host__ __device__ inline bool kp8_fits(uint32_t cpu0, int64_t mem0) {
+    return (uint64_t)cpu0 <= KP8_CPU_MASK && mem0 >= 0 && (uint64_t)mem0 <= KP8_MEM_MASK;
+}
+__host__ __device__ inline uint64_t kp8_word(uint32_t f, uint32_t cpu0, int64_t mem0, uint32_t pair0) {
+    const uint64_t q = pair0 < KP8_PAIR_NONE ? pair0 : KP8_PAIR_NONE;
+    return (uint64_t)cpu0 | (uint64_t)mem0 << KP8_CPU_BITS | q << KP8_PAIR_SHIFT | ((f & ESC_PF_DAEMONSET) ? KP8_DS : 0) |
+           ((f & (ESC_PF_STATIC | ESC_PF_HAS_SEL | ESC_PF_AFF_BLOCK)) ? KP8_NODEF : 0);
 }
 __host__ __device__ inline int64_t kb_xp(const PodClass& C, int64_t blk, uint32_t k, int64_t s) {
+    if (C.packed == 2) return blk + KP8_REC + 512 * (int64_t)kb_nrec(C) + 256 * (int64_t)k + s;
     if (C.packed) return blk + KP_REC + 512 * (int64_t)kb_nrec(C) + 256 * (int64_t)k + s;
     return blk + KB_REC + 1024 * (int64_t)kb_nrec(C) + 256 * (int64_t)k + s;
+}
+// A freed / padding slot: daemonset-flagged, no pair (put as in kb_write_pod below).
+template <class Put>
+__host__ __device__ inline void kb_write_free(const PodClass& C, int64_t blk, int64_t sl, Put&& put) {
+    if (C.packed == 2) put(true, blk / 2 + kb_pos64(sl), KP8_DS | (uint64_t)KP8_PAIR_NONE << KP8_PAIR_SHIFT);
+    else put(false, blk + sl, C.packed ? (ESC_PF_DAEMONSET << KP_FLAG_SHIFT) | KP_PAIR_NONE : ESC_PF_DAEMONSET);
 }
 // packed 8-byte value of a (cpu, mem) pair; init: an absent key becomes its field's sentinel
 __host__ __device__ inline bool kp_val_fits(int64_t cpu, int64_t mem, bool init) {
@@ -118,6 +144,53 @@ __host__ __device__ inline bool kp_fits(uint32_t f, uint32_t cpu0, int64_t mem0,
         if (!kp_val_fits(xc_cpu[k], xc_mem[k], k >= nreg && k < nreg + ninit)) return false;
     return true;
 }
+// The head of K pod s of the block at word blk, any layout: ESC_PF_* flags (the class
+// signature's counts included; a packed small pod's static / has-selector / affinity bits
+// read back as ESC_PF_HAS_SEL), pair0 (NONE: none, or no group's in a small block) and the
+// first container's cpu / mem; kp_rec: record k's cpu / mem (an absent init key INT64_MIN).
+struct KHead {
+    uint32_t flags, pair0;
+    int64_t cpu0, mem0;
+};
+__host__ __device__ inline KHead kb_head(const PodClass& C, const uint32_t* kb, int64_t blk, int64_t s) {
+    KHead h;
+    const int64_t* kb64 = reinterpret_cast<const int64_t*>(kb);
+    if (C.packed == 2) {
+        const uint64_t w = (uint64_t)kb64[blk / 2 + kb_pos64(s)];
+        h.flags = kp_flags(C, 0) | ((w & KP8_DS) ? ESC_PF_DAEMONSET : 0u) | ((w & KP8_NODEF) ? ESC_PF_HAS_SEL : 0u);
+        const uint32_t q = (uint32_t)(w >> KP8_PAIR_SHIFT) & KP8_PAIR_NONE;
+        h.pair0 = q == KP8_PAIR_NONE ? NONE : q;
+        h.cpu0 = (int64_t)(w & KP8_CPU_MASK);
+        h.mem0 = (int64_t)((w >> KP8_CPU_BITS) & KP8_MEM_MASK);
+    } else if (C.packed) {
+        const uint32_t w0 = kb[blk + s];
+        const uint64_t v = (uint64_t)kb64[(blk + KP_CM0) / 2 + kb_pos64(s)];
+        h.flags = kp_flags(C, w0);
+        h.pair0 = kp_pair0(w0);
+        h.cpu0 = kp_cpu(v);
+        h.mem0 = kp_mem(v);
+    } else {
+        h.flags = kb[blk + s];
+        h.pair0 = kb[blk + KB_PAIR0 + s];
+        h.cpu0 = kb[blk + KB_CPU0 + s];
+        h.mem0 = kb64[(blk + KB_MEM0) / 2 + kb_pos64(s)];
+    }
+    return h;
+}
+__host__ __device__ inline void kb_rec(const PodClass& C, const uint32_t* kb, int64_t blk, uint32_t k, int64_t s,
+                                       int64_t& cpu, int64_t& mem) {
+    const int64_t* kb64 = reinterpret_cast<const int64_t*>(kb);
+    if (C.packed) {
+        const uint64_t v = (uint64_t)kb64[(blk + (C.packed == 2 ? KP8_REC : KP_REC) + 512 * (int64_t)k) / 2 + kb_pos64(s)];
+        cpu = kp_cpu(v);
+        mem = kp_mem(v);
+    } else {
+        const int64_t o = kb_rec64(blk, k, s);
+        cpu = kb64[o];
+        mem = kb64[o + 256];
+    }
+}
+
 // Every word a K-class pod occupies in its tile (load and in-place upserts): put(is64, index
 // in u32 words (is64 false) or in 8-byte elements (true), value).
 template <class Put>
@@ -125,7 +198,11 @@ __host__ __device__ inline void kb_write_pod(const PodClass& C, int64_t blk, int
                                              int64_t mem0, uint32_t pair0, const int64_t* xc_cpu,
                                              const int64_t* xc_mem, const uint32_t* xp, Put&& put) {
     const uint32_t R = kb_nrec(C);
-    if (C.packed) {
+    if (C.packed == 2) {
+        put(true, blk / 2 + kb_pos64(sl), kp8_word(f, cpu0, mem0, pair0));
+        for (uint32_t k = 0; k < R; ++k)
+            put(true, (blk + KP8_REC + 512 * (int64_t)k) / 2 + kb_pos64(sl), kp_val(xc_cpu[k], xc_mem[k]));
+    } else if (C.packed) {
         put(false, blk + sl, kp_word(f, pair0));
         put(true, (blk + KP_CM0) / 2 + kb_pos64(sl), kp_val((int64_t)cpu0, mem0));
         for (uint32_t k = 0; k < R; ++k)

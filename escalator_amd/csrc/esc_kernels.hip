@@ -34,6 +34,9 @@
 #ifndef K1_PK_DS
 #define K1_PK_DS 6      // packed K tiles in flight per K1 wave (at most; the VGPR budget may allow fewer)
 #endif
+#ifndef K1_PK8_DS
+#define K1_PK8_DS 8     // packed small K tiles in flight per K1 wave (at most)
+#endif
 
 namespace esc {
 
@@ -261,6 +264,12 @@ struct KTile<R, NXP, 0> {            // plain block
     uint4 rq[NXP > 0 ? NXP : 1];
 };
 template <int R, int NXP>
+struct KTile<R, NXP, 2> {            // packed small block (esc_kernels.h, kp8_*)
+    ulonglong2 w[2];                 // cpu0 | mem0 << 14 | pair0 << 48 | flags << 62
+    ulonglong2 r[R > 0 ? R : 1][2];  // records, cpu | mem << 20
+    uint4 rq[NXP > 0 ? NXP : 1];
+};
+template <int R, int NXP>
 struct KTile<R, NXP, 1> {            // packed block (esc_kernels.h, kp_*)
     uint4 a;                         // pair0 | pod flags << 28
     ulonglong2 cm[2];                // cpu0 | mem0 << 20
@@ -294,19 +303,39 @@ __device__ __forceinline__ PodClass load_class(const PodClass* cls, int i) {
 // 16 B at a compile-time offset from the block's first word, through the run's descriptor
 // (`to` = the tile's byte offset in the run; RUN_OOB past its end: zeros, no traffic).
 template <int R, int NXP>
-__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP, 1>& T, const PodClass&) {
+__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP, 2>& T, const PodClass&) {
     const uint32_t o = to + lane * 16;
+    auto w = [&](int words) { return o + 4u * (uint32_t)words; };
+    T.w[0] = ldb2(rs, o);
+    T.w[1] = ldb2(rs, w(256));
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        T.r[k][0] = ldb2(rs, w(KP8_REC + 512 * k));
+        T.r[k][1] = ldb2(rs, w(KP8_REC + 512 * k + 256));
+    }
+#pragma unroll
+    for (int k = 0; k < NXP; ++k) T.rq[k] = ldb4(rs, w(KP8_REC + 512 * R + 256 * k));
+}
+
+// Packed (12-B) blocks: since the small blocks take most pods, one pipeline for every
+// shape (R = NXP = 3 at most, the class's counts select the rows, as for plain blocks).
+template <int R, int NXP>
+__device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTile<R, NXP, 1>& T, const PodClass& C) {
+    const uint32_t o = to + lane * 16;
+    const uint32_t nr = kb_nrec(C);
     auto w = [&](int words) { return o + 4u * (uint32_t)words; };
     T.a = ldb4(rs, o);
     T.cm[0] = ldb2(rs, w(KP_CM0));
     T.cm[1] = ldb2(rs, w(KP_CM0 + 256));
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-        T.r[k][0] = ldb2(rs, w(KP_REC + 512 * k));
-        T.r[k][1] = ldb2(rs, w(KP_REC + 512 * k + 256));
+        const bool on = (uint32_t)k < nr;
+        T.r[k][0] = ldb2(rs, on ? w(KP_REC + 512 * k) : RUN_OOB);
+        T.r[k][1] = ldb2(rs, on ? w(KP_REC + 512 * k + 256) : RUN_OOB);
     }
 #pragma unroll
-    for (int k = 0; k < NXP; ++k) T.rq[k] = ldb4(rs, w(KP_REC + 512 * R + 256 * k));
+    for (int k = 0; k < NXP; ++k)
+        T.rq[k] = ldb4(rs, (uint32_t)k < C.nxp ? o + 4u * (KP_REC + 512u * nr + 256u * (uint32_t)k) : RUN_OOB);
 }
 
 // Plain blocks (pods outside the packed ranges: rare) go through ONE pipeline for every
@@ -370,6 +399,40 @@ __device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLAT
 #pragma unroll
         for (int k = 0; k < NXP; ++k) {
             const uint32_t q = lane4(T.rq[k], j);
+            if ((uint32_t)k < C.nxp && q < G.n_gp) K.add(q, cpu, mem, in);   // rows past the class's: zeros
+        }
+    }
+}
+
+// The packed small block: one u64 per pod (kp8_*), records as in the packed block.
+template <int R, int NXP, int ABLATE>
+__device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLATE>& K, const PodClass& C,
+                                          const KTile<R, NXP, 2>& T) {
+    const uint32_t init_end = C.xreg + C.xinit;
+#pragma unroll
+    for (int j = 0; j < PODS_PER_LANE; ++j) {
+        const uint64_t w = lane4(T.w, j);
+        if (w & KP8_DS) continue;                                    // node_group.go:221, :259
+        uint64_t cpu = w & KP8_CPU_MASK, mem = (w >> KP8_CPU_BITS) & KP8_MEM_MASK;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+            const uint64_t v = lane4(T.r[k], j);
+            const uint64_t c = v & KP_CPU_ABSENT, m = v >> KP_CPU_BITS;
+            if ((uint32_t)k < C.xreg || (uint32_t)k >= init_end) {
+                cpu += c;
+                mem += m;
+            } else {                                   // values and sums are >= 0 here
+                cpu = (c == KP_CPU_ABSENT || cpu >= c) ? cpu : c;
+                mem = (m == KP_MEM_ABSENT || mem >= m) ? mem : m;
+            }
+        }
+        const bool in = in_range(cpu, mem);
+        if (!(w & KP8_NODEF) && G.default_group != NONE) K.add(G.n_gp, cpu, mem, in);   // pf_default_ok
+        const uint32_t q0 = (uint32_t)(w >> KP8_PAIR_SHIFT) & KP8_PAIR_NONE;
+        if (q0 < G.n_gp) K.add(q0, cpu, mem, in);
+#pragma unroll
+        for (int k = 0; k < NXP; ++k) {
+            const uint32_t q = lane4(T.rq[k], j);
             if (q < G.n_gp) K.add(q, cpu, mem, in);
         }
     }
@@ -405,6 +468,19 @@ __device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLAT
             if ((uint32_t)k < C.nxp && q < G.n_gp) K.add(q, cpu, mem, in);   // rows past the class's: zeros
         }
     }
+}
+
+template <int R, int NXP>
+__device__ __forceinline__ void k_sink(const KTile<R, NXP, 2>& T) {   // loads-only ablation
+    uint64_t y = T.w[0].x ^ T.w[0].y ^ T.w[1].x ^ T.w[1].y;
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) y ^= T.r[k][h].x ^ T.r[k][h].y;
+#pragma unroll
+    for (int k = 0; k < NXP; ++k) x ^= T.rq[k].x ^ T.rq[k].y ^ T.rq[k].z ^ T.rq[k].w;
+    asm volatile("" :: "v"(x), "v"(y));
 }
 
 template <int R, int NXP>
@@ -449,7 +525,7 @@ __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const 
     auto off = [&](int64_t u) { return u < b ? (uint32_t)((u - a) * BW * 4) : RUN_OOB; };
     // slots that fit the VGPR budget: 16 waves per CU leave 128 VGPRs a wave, 8 leave 256
     // (a packed tile is smaller, so more of them are in flight: up to K1_PK_DS)
-    constexpr int DSM = PK ? K1_PK_DS : 4;
+    constexpr int DSM = PK == 2 ? K1_PK8_DS : (PK ? K1_PK_DS : 4);
     constexpr int DS0 = NW >= 16 ? (L <= 7 ? 3 : (L <= 10 ? 2 : 1))
                                  : (176 / (4 * L) >= DSM ? DSM : (176 / (4 * L) >= 1 ? 176 / (4 * L) : 1));
     // timing knobs (ABLATE bits 6/7): cap the slots in flight at 2 / 3
@@ -780,7 +856,11 @@ __device__ __forceinline__ void decide_store(const GroupDev& G, const GroupNode&
 #define ESC_KRUN_PLAIN                                                                          \
     case 0: case 1: case 2: case 3: case 4: case 5: case 6: case 7:                            \
     case 8: case 9: case 10: case 11: case 12: case 13: case 14: ESC_KRUN(0, 3, 3)   /* = case 15 */
-#define ESC_KRUN_ALL ESC_KRUN_SHAPES(1) ESC_KRUN_PLAIN
+// packed (12-B) blocks: one generic pipeline for their 16 kinds too
+#define ESC_KRUN_PK1                                                                            \
+    case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23:                    \
+    case 24: case 25: case 26: case 27: case 28: case 29: case 30: ESC_KRUN(1, 3, 3)   /* = case 31 */
+#define ESC_KRUN_ALL ESC_KRUN_SHAPES(2) ESC_KRUN_PK1 ESC_KRUN_PLAIN
 template <int THREADS, int ABLATE = 0, int DC = 3, int DYN = 0, int WS = 0>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
@@ -1071,10 +1151,9 @@ __global__ __launch_bounds__(256) void k_touch(PodDev P, GroupDev G, int tw, uin
         const int64_t a = t0c & ((1ll << 48) - 1);
         for (int64_t i = threadIdx.x; i < (b - a) * TILE; i += 256) {
             const int64_t blk = kb_block(C, a + i / TILE), s = i % TILE;
-            const uint32_t w0 = P.kb[blk + s];
-            if ((C.packed ? kp_flags(C, w0) : w0) & ESC_PF_DAEMONSET) continue;
-            const uint32_t q0 = C.packed ? kp_pair0(w0) : P.kb[blk + KB_PAIR0 + s];
-            if (q0 < G.n_gp) mark(q0);
+            const KHead hd = kb_head(C, P.kb, blk, s);
+            if (hd.flags & ESC_PF_DAEMONSET) continue;
+            if (hd.pair0 < G.n_gp) mark(hd.pair0);
             for (uint32_t x = 0; x < C.nxp; ++x) {
                 const uint32_t q = P.kb[kb_xp(C, blk, x, s)];
                 if (q < G.n_gp) mark(q);
@@ -1108,35 +1187,18 @@ __device__ __forceinline__ void k_tile_exact(const PodDev& P, const GroupDev& G,
     const PodWide acc{wide};
     const uint32_t R = kb_nrec(C);
     const int64_t blk = kb_block(C, t);
-    const int64_t* kb64 = reinterpret_cast<const int64_t*>(P.kb);
     for (int j = 0; j < PODS_PER_LANE; ++j) {
         const uint32_t s = lane * PODS_PER_LANE + j;
-        const uint32_t w0 = P.kb[blk + s];
-        const uint32_t f = C.packed ? kp_flags(C, w0) : w0;
-        if (f & ESC_PF_DAEMONSET) continue;
-        uint64_t cpu, mem;
-        if (C.packed) {
-            const uint64_t v = (uint64_t)kb64[(blk + KP_CM0) / 2 + kb_pos64(s)];
-            cpu = (uint64_t)kp_cpu(v);
-            mem = (uint64_t)kp_mem(v);
-        } else {
-            cpu = P.kb[blk + KB_CPU0 + s];
-            mem = (uint64_t)kb64[(blk + KB_MEM0) / 2 + kb_pos64(s)];
-        }
+        const KHead h = kb_head(C, P.kb, blk, s);
+        if (h.flags & ESC_PF_DAEMONSET) continue;
+        uint64_t cpu = (uint64_t)h.cpu0, mem = (uint64_t)h.mem0;
         for (uint32_t k = 0; k < R; ++k) {
-            if (C.packed) {
-                const uint64_t v = (uint64_t)kb64[(blk + KP_REC + 512 * (int64_t)k) / 2 + kb_pos64(s)];
-                apply_rec(k, R, C.xreg, C.xreg + C.xinit, (unsigned long long)kp_cpu(v),
-                          (unsigned long long)kp_mem(v), cpu, mem);
-            } else {
-                const int64_t o = kb_rec64(blk, k, s);
-                apply_rec(k, R, C.xreg, C.xreg + C.xinit, (unsigned long long)kb64[o],
-                          (unsigned long long)kb64[o + 256], cpu, mem);
-            }
+            int64_t rc, rm;
+            kb_rec(C, P.kb, blk, k, s, rc, rm);
+            apply_rec(k, R, C.xreg, C.xreg + C.xinit, (unsigned long long)rc, (unsigned long long)rm, cpu, mem);
         }
-        const uint32_t q0 = C.packed ? kp_pair0(w0) : P.kb[blk + KB_PAIR0 + s];
-        if (pf_default_ok(f) && G.default_group != NONE) acc.add(G.n_gp, (int64_t)cpu, (int64_t)mem);
-        if (q0 < G.n_gp) acc.add(q0, (int64_t)cpu, (int64_t)mem);
+        if (pf_default_ok(h.flags) && G.default_group != NONE) acc.add(G.n_gp, (int64_t)cpu, (int64_t)mem);
+        if (h.pair0 < G.n_gp) acc.add(h.pair0, (int64_t)cpu, (int64_t)mem);
         for (uint32_t k = 0; k < C.nxp; ++k) {
             const uint32_t q = P.kb[kb_xp(C, blk, k, s)];
             if (q < G.n_gp) acc.add(q, (int64_t)cpu, (int64_t)mem);
@@ -2381,9 +2443,9 @@ __device__ PodRef podref_of(const PodDev& P, uint32_t d) {
         }
         const PodClass& C = P.cls[lo];
         const int64_t blk = kb_block(C, t);
-        const uint32_t w0 = P.kb[blk + sl];
-        r.flags = C.packed ? kp_flags(C, w0) : w0;
-        r.pair0 = C.packed ? kp_pair0(w0) : P.kb[blk + KB_PAIR0 + sl];
+        const KHead hd = kb_head(C, P.kb, blk, sl);
+        r.flags = hd.flags;
+        r.pair0 = hd.pair0;
         for (uint32_t k = 0; k < C.nxp && k < 3; ++k) r.p[k] = P.kb[kb_xp(C, blk, k, sl)];
     } else {
         const int64_t c = (int64_t)d - kpods, t = c / CTILE, l = c % CTILE;

@@ -275,7 +275,9 @@ struct esc_ctx {
     std::vector<uint32_t> h_cused;                            // a C slot's pod's own records | pairs << 16
     std::vector<uint32_t> h_xc_base, h_xp_base;               // C tiles' record / pair offsets
     int64_t live_pods = 0, live_xc = 0, live_xp = 0;
-    int64_t live_pk_pods = 0, live_pk_xc = 0;   // of them in packed K classes
+    int64_t live_pk_pods = 0, live_pk_xc = 0;   // of them in packed K classes (either size)
+    int64_t live_p8_pods = 0;                   // of them in packed small K classes
+    int64_t c_tiles_loaded = 0;                 // C tiles of loaded pods (the spare C tiles excluded)
     // node state mirrors for esc_nodes_update
     std::vector<uint32_t> h_nflags;
     std::vector<int64_t> h_ncpu, h_nmem;
@@ -323,14 +325,17 @@ constexpr uint32_t CS_FLAGS = ESC_PF_DAEMONSET | ESC_PF_HAS_OVH | (uint32_t)CS_X
                               (uint32_t)CS_XINIT << ESC_PF_XINIT_SHIFT | (uint32_t)CS_XP << ESC_PF_XPAIR_SHIFT;
 
 // K class of a pod: its record signature (at most 3 extra container
-// records and 3 extra pairs; -1: the C section) | packed << 7 when its values fit the packed
-// block (kp_fits).  xc_cpu / xc_mem: the pod's own records (null when it has none).
+// records and 3 extra pairs; -1: the C section) | packed << 7: 1 when its values fit the
+// packed block (kp_fits), 2 when they also fit the packed small block (kp8_fits, in a context
+// with fewer than KP8_PAIR_NONE group pairs).  xc_cpu / xc_mem: the pod's own records (null
+// when it has none).
 int pod_class_id(uint32_t f, uint32_t cpu0, int64_t mem0, uint32_t pair0, const int64_t* xc_cpu,
-                 const int64_t* xc_mem) {
+                 const int64_t* xc_mem, uint32_t n_gp) {
     const uint32_t xr = pf_xreg(f), xi = pf_xinit(f), ov = (f & ESC_PF_HAS_OVH) ? 1u : 0u, np = pf_xpair(f);
     if (xr + xi + ov > 3 || np > 3) return -1;
     const int sig = (int)(((xr * 4 + xi) * 2 + ov) * 4 + np);
-    return kp_fits(f, cpu0, mem0, pair0, xc_cpu, xc_mem) ? sig | POD_SIG_IDS : sig;
+    if (!kp_fits(f, cpu0, mem0, pair0, xc_cpu, xc_mem)) return sig;
+    return sig | (n_gp < KP8_PAIR_NONE && kp8_fits(cpu0, mem0) ? 2 : 1) * POD_SIG_IDS;
 }
 
 // K1 partial row stride: the pod slots (one per group pair + the default filter's)
@@ -1299,7 +1304,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         for (int64_t i = 0; i < n; ++i) {
             const uint32_t f = p->flags[i];
             const int id = pod_class_id(f, p->cpu0[i], p->mem0[i], p->pair0[i], p->xc_cpu ? p->xc_cpu + rc : nullptr,
-                                        p->xc_mem ? p->xc_mem + rc : nullptr);
+                                        p->xc_mem ? p->xc_mem + rc : nullptr, c->gi.n_gp);
             pid[i] = (int16_t)id;
             rc += pf_xctr(f);
             if (id >= 0) {
@@ -1315,7 +1320,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     std::vector<int> cls_of(POD_CLASS_IDS, -1);
     int64_t kt = 0, kbw = 0, kw = 0;
     for (int ord = 0; ord < POD_CLASS_IDS; ++ord) {
-        const int id = ord ^ POD_SIG_IDS;                 // packed classes first
+        const int id = POD_CLASS_IDS - POD_SIG_IDS * (ord / POD_SIG_IDS + 1) + ord % POD_SIG_IDS;   // small, packed, plain
         const int sig = id % POD_SIG_IDS;
         // with spare slots requested every signature the K layout can hold gets a class, so
         // that inserts of shapes absent at load still land in place
@@ -1327,7 +1332,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         k.ovh = (uint32_t)((sig / 4) % 2);
         k.xinit = (uint32_t)((sig / 8) % 4);
         k.xreg = (uint32_t)(sig / 32);
-        k.packed = id >= POD_SIG_IDS ? 1u : 0u;
+        k.packed = (uint32_t)(id / POD_SIG_IDS);
         const int64_t want = cnt[id] + (c->spare_frac > 0 ? std::max<int64_t>(1, (int64_t)(cnt[id] * c->spare_frac)) : 0);
         const int64_t R = k.xreg + k.xinit + k.ovh, tiles = (want + TILE - 1) / TILE;
         k.t0 = kt;
@@ -1361,7 +1366,11 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     for (const PodClass& k : cls)
         for (int64_t t = k.t0; t < k.t1; ++t) {
             const int64_t blk = kb_block(k, t);
-            std::fill(hkb.begin() + blk, hkb.begin() + blk + TILE, kb_free_word(k));
+            for (int64_t sl = 0; sl < TILE; ++sl)
+                kb_write_free(k, blk, sl, [&](bool is64, int64_t at, uint64_t v) {
+                    if (is64) reinterpret_cast<int64_t*>(hkb.data())[at] = (int64_t)v;
+                    else hkb[at] = (uint32_t)v;
+                });
             if (!k.packed) std::fill(hkb.begin() + blk + KB_PAIR0, hkb.begin() + blk + KB_PAIR0 + TILE, NONE);
             const int64_t x0 = kb_xp(k, blk, 0, 0);
             std::fill(hkb.begin() + x0, hkb.begin() + x0 + (int64_t)k.nxp * TILE, NONE);
@@ -1501,17 +1510,19 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     c->live_pods = n;
     c->live_xc = p->n_xc;
     c->live_xp = p->n_xp;
-    c->live_pk_pods = c->live_pk_xc = 0;
+    c->live_pk_pods = c->live_pk_xc = c->live_p8_pods = 0;
     for (int id = POD_SIG_IDS; id < POD_CLASS_IDS; ++id) {
         if (cls_of[id] < 0) continue;
         c->live_pk_pods += cnt[id];
         c->live_pk_xc += cnt[id] * (int64_t)kb_nrec(cls[cls_of[id]]);
+        if (id >= 2 * POD_SIG_IDS) c->live_p8_pods += cnt[id];
     }
     c->n_pods = n;
     c->k_tiles = k_tiles;
     c->k_weight = kw;
     c->n_cls = (int32_t)n_cls;
     c->c_tiles = c_tiles;
+    c->c_tiles_loaded = c_real;
     c->n_big = (int64_t)big.size();
     c->n_xc = p->n_xc;
     c->n_xp = p->n_xp;
@@ -1794,9 +1805,10 @@ int32_t esc_stream_bytes(const esc_ctx* c, int64_t* pod_bytes, int64_t* node_byt
     if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
     // K1: flags 4 + cpu0 4 + mem0 8 + pair0 4 per pod, 16 per extra container record,
     // 4 per extra pair, 8 per C tile (record offsets); a pod of a packed class 12 B + 8 per
-    // record (esc_kernels.h, kp_*); K2: see esc_load_nodes
-    *pod_bytes = c->live_pods * 20 + c->live_xc * 16 + c->live_xp * 4 + c->c_tiles * 8 - c->live_pk_pods * 8 -
-                 c->live_pk_xc * 8;
+    // record, of a packed small class 8 B + 8 per record (esc_kernels.h, kp_*, kp8_*); K2:
+    // see esc_load_nodes
+    *pod_bytes = c->live_pods * 20 + c->live_xc * 16 + c->live_xp * 4 + c->c_tiles_loaded * 8 - c->live_pk_pods * 8 -
+                 c->live_pk_xc * 8 - c->live_p8_pods * 4;
     *node_bytes = c->node_bytes;
     return ESC_OK;
 }
@@ -2274,11 +2286,13 @@ void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
     } else {
         const PodClass& k = c->h_cls[ci];
         const int64_t q = c->pod_pos[id];
-        P.add(PT_KB32, kb_block(k, k.t0 + q / TILE) + q % TILE, kb_free_word(k));
+        kb_write_free(k, kb_block(k, k.t0 + q / TILE), q % TILE,
+                      [&](bool is64, int64_t at, uint64_t v) { P.add(is64 ? PT_KB64 : PT_KB32, at, v); });
         c->cls_free[ci].push_back(q);
         c->live_xc -= k.xreg + k.xinit + k.ovh;
         c->live_xp -= k.nxp;
         if (k.packed) { --c->live_pk_pods; c->live_pk_xc -= k.xreg + k.xinit + k.ovh; }
+        if (k.packed == 2) --c->live_p8_pods;
     }
     c->pod_cls[id] = -2;
     --c->live_pods;
@@ -2659,7 +2673,7 @@ int32_t upsert_plan(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, Upsert
         sc += nc;
         sp += nx;
         const int sid = pod_class_id(f, p->cpu0[i], p->mem0[i], p->pair0[i], nc ? p->xc_cpu + sc - nc : nullptr,
-                                     nc ? p->xc_mem + sc - nc : nullptr);
+                                     nc ? p->xc_mem + sc - nc : nullptr, c->gi.n_gp);
         int ci = sid < 0 ? -1 : c->h_cls_of[sid];
         const int64_t id = ids[i];
         const bool known = id < (int64_t)c->pod_cls.size();
@@ -2725,6 +2739,7 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
             c->live_xc -= k.xreg + k.xinit + k.ovh;
             c->live_xp -= k.nxp;
             if (k.packed) { --c->live_pk_pods; c->live_pk_xc -= k.xreg + k.xinit + k.ovh; }
+        if (k.packed == 2) --c->live_p8_pods;
         }
         const PodClass& k = c->h_cls[ci];
         const int64_t q = c->pod_pos[id], sl = q % TILE;
@@ -2738,6 +2753,7 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
         c->live_xc += R;
         c->live_xp += k.nxp;
         if (k.packed) { ++c->live_pk_pods; c->live_pk_xc += R; }
+        if (k.packed == 2) ++c->live_p8_pods;
     }
     int32_t rc = apply_patches(c, P, pod_targets(c));
     if (!rc && touch_grew) rc = touch_upload(c);

@@ -6,7 +6,8 @@ K1 reads the pod shard once per decision: per pod flags 4 + cpu0 4 + mem0 8 + pa
 per 64-pod C tile (pods with more than 3 extra container records or more than 3 extra
 pairs; all other pods sit in homogeneous 256-pod K tiles that need no offsets).  A K pod
 whose values fit the packed block (``packed_mask``) takes 12 B (pair0 | flags 4, cpu0 | mem0
-8) and 8 B per record.
+8) and 8 B per record; one that also fits the packed small block (``small_mask``) 8 B
+(cpu0 | mem0 | pair0 | flags in one u64) and 8 B per record.
 K2 reads the node index once per decision: 24 B per (label pair, node) entry of a pair
 some group selects (flags 4 + cpu 8 + mem 8 + node 4) and 8 B per piece (offset + pair).
 With several ranks each reads the pieces of the group pairs it owns (``owner_ranges``:
@@ -59,17 +60,35 @@ def packed_mask(pods: dict) -> np.ndarray:
     return ok
 
 
-def pod_bytes(pods: dict, lo: int = 0, hi: int | None = None) -> int:
-    """K1's algorithmic bytes for pods [lo, hi) of a snapshot (one shard)."""
+KP8_CPU_MAX = (1 << 14) - 1       # packed small block (kp8_*): cpu0, mem0 ranges, pair-id field
+KP8_MEM_MAX = (1 << 34) - 1
+KP8_PAIR_NONE = (1 << 14) - 1
+
+
+def small_mask(pods: dict, n_gp: int) -> np.ndarray:
+    """Packed pods that also fit the packed small block: cpu0 < 2^14, mem0 < 2^34, in a
+    context with fewer than 2^14 - 1 group pairs."""
+    if n_gp >= KP8_PAIR_NONE:
+        return np.zeros(len(pods["flags"]), bool)
+    cpu0 = np.asarray(pods["cpu0"], np.int64)
+    mem0 = np.asarray(pods["mem0"], np.int64)
+    return packed_mask(pods) & (cpu0 <= KP8_CPU_MAX) & (mem0 >= 0) & (mem0 <= KP8_MEM_MAX)
+
+
+def pod_bytes(pods: dict, n_gp: int, lo: int = 0, hi: int | None = None) -> int:
+    """K1's algorithmic bytes for pods [lo, hi) of a snapshot (one shard) in a context with
+    n_gp group pairs."""
     f = np.asarray(pods["flags"], np.uint64)
     hi = len(f) if hi is None else hi
     nrec = (((f >> 8) & 0xFF) + ((f >> 16) & 0xFF) + ((f >> 4) & 1)).astype(np.int64)[lo:hi]
     nxp = ((f >> 24) & 0x3F).astype(np.int64)[lo:hi]
     pk = packed_mask(pods)[lo:hi]
+    sm = small_mask(pods, n_gp)[lo:hi]
     c_tiles = (complex_pods(f[lo:hi]) + 63) // 64
     plain = (20 + 16 * nrec + 4 * nxp)[~pk].sum()
-    packed = (12 + 8 * nrec + 4 * nxp)[pk].sum()
-    return int(plain + packed + c_tiles * 8)
+    packed = (12 + 8 * nrec + 4 * nxp)[pk & ~sm].sum()
+    small = (8 + 8 * nrec + 4 * nxp)[sm].sum()
+    return int(plain + packed + small + c_tiles * 8)
 
 
 def node_entries(nodes: dict) -> np.ndarray:

@@ -18,7 +18,8 @@ import escalator_amd as esc  # noqa: E402
 
 s = esc.Synth(P, N, G, config=cfg, seed=0xE5CA1A7E00000000 + cfg, threads=16)
 from escalator_amd import layout  # noqa: E402
-bytes_k1 = layout.pod_bytes(s.pods())
+from oracle import soa
+bytes_k1 = layout.pod_bytes(s.pods(), len(soa.group_tables(s.groups)["pair_ids"]))
 ctxs = {}
 for v in variants:
     os.environ["ESC_K1_VARIANT"] = str(v)

@@ -48,9 +48,9 @@ def _req(rng, big=False):
         r["cpu"] = rng.choice([(1 << 20) + rng.randrange(100), (1 << 33), -rng.randrange(1, 1000)])
     if big and rng.random() < 0.5:
         r["mem"] = rng.choice([(1 << 44) + 7, (1 << 50), -rng.randrange(1, 1 << 20)])
-    if big and rng.random() < 0.3:           # the packed K block's edges (kp_fits): just in / just out
-        r["cpu"] = rng.choice([(1 << 20) - 2, (1 << 20) - 1])
-        r["mem"] = rng.choice([(1 << 44) - 2, (1 << 44) - 1])
+    if big and rng.random() < 0.3:           # the packed K blocks' edges (kp_fits, kp8_fits): just in / out
+        r["cpu"] = rng.choice([(1 << 14) - 1, 1 << 14, (1 << 20) - 2, (1 << 20) - 1])
+        r["mem"] = rng.choice([(1 << 34) - 1, 1 << 34, (1 << 44) - 2, (1 << 44) - 1])
     return r
 
 

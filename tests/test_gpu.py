@@ -570,7 +570,7 @@ def test_node_index_split_within_pairs(esc, world):
         c = esc.Context(s, rank=r, world=world)
         c.load_synth(s, pod_offset=lo)
         pb, nb = c.stream_bytes()
-        assert pb == layout.pod_bytes(s.pods())
+        assert pb == layout.pod_bytes(s.pods(), n_gp)
         assert nb == layout.node_bytes(s.nodes(), n_gp, r, world)
         c.set_state(full.states)
         c.reduce()
@@ -678,6 +678,61 @@ def test_incremental_events_vs_literal(esc, seed):
     before = ctx.decide_all(states)[0].tobytes()
     assert ctx.pods_upsert([next_id + k for k in range(len(keep))], _packed_subset(Pm, keep)) == ESC_E_LIMIT
     assert ctx.decide_all(states)[0].tobytes() == before
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_k_block_formats_vs_literal(esc, seed):
+    """Pods at the edges of the three K block formats (plain; packed: cpu < 2^20 - 1, mem <
+    2^44 - 1; packed small: first container cpu < 2^14, mem < 2^34) and init containers with
+    absent keys, through the layout and upserts that move pods between formats: totals and
+    decisions equal the literal oracle, and esc_stream_bytes the restated format bytes."""
+    from escalator_amd import layout
+    from randobj import _req
+    rng = random.Random(7600 + seed)
+    G = rng.choice([3, 12])
+    groups = make_groups(rng, G, with_default=True)
+    edges_c = [0, 1, (1 << 14) - 1, 1 << 14, (1 << 20) - 2, (1 << 20) - 1, -1, None]
+    edges_m = [0, 1, (1 << 34) - 1, 1 << 34, (1 << 44) - 2, (1 << 44) - 1, -1, None]
+
+    def edge_pod():
+        q = make_pods(rng, 1, groups, big_frac=0.0)[0]
+        reqs = q["containers"] + q["init_containers"]
+        for r in reqs:
+            if rng.random() < 0.5:
+                r["cpu"] = rng.choice(edges_c)
+            if rng.random() < 0.5:
+                r["mem"] = rng.choice(edges_m)
+        return q
+
+    pods = [edge_pod() for _ in range(400)]
+    nodes = make_nodes(rng, 40, groups, big_frac=0.0)
+    states = make_states(rng, G)
+    ctx = esc.Context(groups)
+    ctx.set_spare(1.0)
+    P, N = ctx.pack(pods, nodes)
+    ctx.load(P, N)
+    n_gp = ctx.lib.esc_ctx_num_group_pairs(ctx.handle)
+    live = dict(enumerate(pods))
+    for rnd in range(3):
+        if rnd:
+            ids = rng.sample(sorted(live), 60)
+            objs = [edge_pod() for _ in ids]
+            Pe, _ = ctx.pack(objs, [])
+            assert ctx.pods_upsert(ids, Pe) == 0
+            for i, q in zip(ids, objs):
+                live[i] = q
+        cur = [live[i] for i in sorted(live)]
+        tot, dec = ctx.decide_all(states)
+        for g in range(G):
+            L = O.scale_node_group(groups[g], states[g], cur, nodes)
+            t, d = tot[g], dec[g]
+            assert t["n_pods"] == L["n_pods"], (rnd, g)
+            if L["pod_cpu_m"] is not None:
+                assert (t["pod_cpu_m"], t["pod_mem_b"]) == (L["pod_cpu_m"], L["pod_mem_b"]), (rnd, g)
+            assert esc._lib.BRANCHES[d["branch"]] == L["branch"], (rnd, g)
+            assert int(d["delta"]) == L["delta"] and _bits(d["cpu_pct"]) == _bits(L["cpu_pct"]), (rnd, g)
+        if rnd == 0:
+            assert ctx.stream_bytes()[0] == layout.pod_bytes(P, n_gp)
 
 
 @pytest.mark.parametrize("seed", range(4))

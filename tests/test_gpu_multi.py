@@ -54,8 +54,8 @@ def test_multi_device_context_vs_c_oracle(esc, devices):
     from escalator_amd import layout
     k = len(devices)
     cuts = [P * i // k for i in range(k + 1)]
-    assert pb == sum(layout.pod_bytes(s.pods(), a, b) for a, b in zip(cuts, cuts[1:]))
     n_gp = len(soa.group_tables(s.groups)["pair_ids"])
+    assert pb == sum(layout.pod_bytes(s.pods(), n_gp, a, b) for a, b in zip(cuts, cuts[1:]))
     assert nb == layout.node_bytes(s.nodes(), n_gp, 0, 1)       # the shards' node shares add up to the index
 
 
