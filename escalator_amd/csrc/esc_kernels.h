@@ -76,6 +76,8 @@ constexpr uint64_t KP_MEM_ABSENT = (uint64_t(1) << 44) - 1;
 //                             pair, or one no group selects) | daemonset << 62 |
 //                             blocks-default << 63 (static, has-selector or affinity: the
 //                             default filter's other conditions, node_group.go:263-273)
+//                             A daemonset pod (and a free slot) is stored with no pairs and
+//                             blocks-default set, so K1 adds it nowhere without a test.
 //   u64   record k            [512 + 512k, +512): as in the packed block
 //   u32   extra pair k        [512 + 512R + 256k, +256)
 constexpr int KP8_REC = 512;
@@ -88,8 +90,9 @@ __host__ __device__ inline bool kp8_fits(uint32_t cpu0, int64_t mem0) {
     return (uint64_t)cpu0 <= KP8_CPU_MASK && mem0 >= 0 && (uint64_t)mem0 <= KP8_MEM_MASK;
 }
 __host__ __device__ inline uint64_t kp8_word(uint32_t f, uint32_t cpu0, int64_t mem0, uint32_t pair0) {
-    const uint64_t q = pair0 < KP8_PAIR_NONE ? pair0 : KP8_PAIR_NONE;
-    return (uint64_t)cpu0 | (uint64_t)mem0 << KP8_CPU_BITS | q << KP8_PAIR_SHIFT | ((f & ESC_PF_DAEMONSET) ? KP8_DS : 0) |
+    const bool ds = (f & ESC_PF_DAEMONSET) != 0;
+    const uint64_t q = pair0 < KP8_PAIR_NONE && !ds ? pair0 : KP8_PAIR_NONE;
+    return (uint64_t)cpu0 | (uint64_t)mem0 << KP8_CPU_BITS | q << KP8_PAIR_SHIFT | (ds ? KP8_DS | KP8_NODEF : 0) |
            ((f & (ESC_PF_STATIC | ESC_PF_HAS_SEL | ESC_PF_AFF_BLOCK)) ? KP8_NODEF : 0);
 }
 __host__ __device__ inline int64_t kb_xp(const PodClass& C, int64_t blk, uint32_t k, int64_t s) {
@@ -100,8 +103,12 @@ __host__ __device__ inline int64_t kb_xp(const PodClass& C, int64_t blk, uint32_
 // A freed / padding slot: daemonset-flagged, no pair (put as in kb_write_pod below).
 template <class Put>
 __host__ __device__ inline void kb_write_free(const PodClass& C, int64_t blk, int64_t sl, Put&& put) {
-    if (C.packed == 2) put(true, blk / 2 + kb_pos64(sl), KP8_DS | (uint64_t)KP8_PAIR_NONE << KP8_PAIR_SHIFT);
-    else put(false, blk + sl, C.packed ? (ESC_PF_DAEMONSET << KP_FLAG_SHIFT) | KP_PAIR_NONE : ESC_PF_DAEMONSET);
+    if (C.packed == 2) {
+        put(true, blk / 2 + kb_pos64(sl), KP8_DS | KP8_NODEF | (uint64_t)KP8_PAIR_NONE << KP8_PAIR_SHIFT);
+        for (uint32_t k = 0; k < C.nxp; ++k) put(false, kb_xp(C, blk, k, sl), NONE);   // no pairs (see kp8_word)
+    } else {
+        put(false, blk + sl, C.packed ? (ESC_PF_DAEMONSET << KP_FLAG_SHIFT) | KP_PAIR_NONE : ESC_PF_DAEMONSET);
+    }
 }
 // packed 8-byte value of a (cpu, mem) pair; init: an absent key becomes its field's sentinel
 __host__ __device__ inline bool kp_val_fits(int64_t cpu, int64_t mem, bool init) {
@@ -218,7 +225,8 @@ __host__ __device__ inline void kb_write_pod(const PodClass& C, int64_t blk, int
             put(true, o + 256, (uint64_t)xc_mem[k]);
         }
     }
-    for (uint32_t k = 0; k < C.nxp; ++k) put(false, kb_xp(C, blk, k, sl), xp[k]);
+    const bool no_pairs = C.packed == 2 && (f & ESC_PF_DAEMONSET);   // (see kp8_word)
+    for (uint32_t k = 0; k < C.nxp; ++k) put(false, kb_xp(C, blk, k, sl), no_pairs ? NONE : xp[k]);
 }
 
 // Device view of a pod shard.  Two sections, made at load (esc_load_pods; sums are

@@ -209,6 +209,8 @@ struct PodLds {          // fast path: LDS partials of a group window
     uint64_t* mem;
     int32_t g0;
     uint32_t gw;
+    uint32_t plim;       // pair slots of this window: pair q is slot q - g0 when that is < plim
+    uint32_t dslot;      // the default filter's slot in this window, or NONE (none / another window)
     __device__ __forceinline__ void add(uint32_t g, uint64_t vcc, uint64_t vmem) const {
         const uint32_t i = g - (uint32_t)g0;
         if (i < gw) { lds_add(cc + i, vcc); lds_add(mem + i, vmem); }
@@ -411,8 +413,9 @@ __device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLAT
     const uint32_t init_end = C.xreg + C.xinit;
 #pragma unroll
     for (int j = 0; j < PODS_PER_LANE; ++j) {
+        // (a daemonset pod, node_group.go:221 / :259, is stored with no pairs and
+        // blocks-default set: it is added nowhere, no test needed)
         const uint64_t w = lane4(T.w, j);
-        if (w & KP8_DS) continue;                                    // node_group.go:221, :259
         uint64_t cpu = w & KP8_CPU_MASK, mem = (w >> KP8_CPU_BITS) & KP8_MEM_MASK;
 #pragma unroll
         for (int k = 0; k < R; ++k) {
@@ -426,14 +429,37 @@ __device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLAT
                 mem = (m == KP_MEM_ABSENT || mem >= m) ? mem : m;
             }
         }
-        const bool in = in_range(cpu, mem);
-        if (!(w & KP8_NODEF) && G.default_group != NONE) K.add(G.n_gp, cpu, mem, in);   // pf_default_ok
+        // without records the pod is inside the LDS range by construction (2^14, 2^34)
+        const bool in = R == 0 ? true : in_range(cpu, mem);
         const uint32_t q0 = (uint32_t)(w >> KP8_PAIR_SHIFT) & KP8_PAIR_NONE;
-        if (q0 < G.n_gp) K.add(q0, cpu, mem, in);
+        if (in) {
+            if constexpr (ABLATE & 1) {
+                asm volatile("" :: "v"(q0), "v"(cpu), "v"(mem));
+            } else {
+                // slot adds straight to LDS: pair q is slot q - g0 of this window when below
+                // plim (NONE and pairs no group selects are above it), the default slot
+                // when the pod passes the default filter (pf_default_ok)
+                const uint64_t vcc = cpu | (1ull << CNT_SHIFT);
+                if (K.acc.dslot != NONE && !(w & KP8_NODEF)) {
+                    lds_add(K.acc.cc + K.acc.dslot, vcc);
+                    lds_add(K.acc.mem + K.acc.dslot, mem);
+                }
+                const uint32_t i0 = q0 - (uint32_t)K.acc.g0;
+                if (i0 < K.acc.plim) { lds_add(K.acc.cc + i0, vcc); lds_add(K.acc.mem + i0, mem); }
 #pragma unroll
-        for (int k = 0; k < NXP; ++k) {
-            const uint32_t q = lane4(T.rq[k], j);
-            if (q < G.n_gp) K.add(q, cpu, mem, in);
+                for (int k = 0; k < NXP; ++k) {
+                    const uint32_t i = lane4(T.rq[k], j) - (uint32_t)K.acc.g0;
+                    if (i < K.acc.plim) { lds_add(K.acc.cc + i, vcc); lds_add(K.acc.mem + i, mem); }
+                }
+            }
+        } else {                                       // outside the LDS range: the exact words
+            if (!(w & KP8_NODEF) && G.default_group != NONE) K.add(G.n_gp, cpu, mem, false);
+            if (q0 < G.n_gp) K.add(q0, cpu, mem, false);
+#pragma unroll
+            for (int k = 0; k < NXP; ++k) {
+                const uint32_t q = lane4(T.rq[k], j);
+                if (q < G.n_gp) K.add(q, cpu, mem, false);
+            }
         }
     }
 }
@@ -519,7 +545,9 @@ template <int R, int NXP, int PK, int NW, int ABLATE, int ST>
 __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const PodSink<ABLATE>& K,
                                       const PodClass& C, int64_t a, int64_t b, uint32_t lane) {
     constexpr int L = (int)k_tile_weight(R, NXP, PK);    // 16-B loads per lane per tile (plain: at most)
-    const int64_t BW = (int64_t)C.wt * 256;              // block words
+    // block words: a compile-time constant for the specialised (packed small) shapes, the
+    // class's own for the generic pipelines
+    const int64_t BW = PK == 2 ? (int64_t)L * 256 : (int64_t)C.wt * 256;
     // the wave's run: tiles [a, b) -> bytes [0, (b - a) * BW * 4) of its descriptor
     const Rsrc rs = rsrc(P.kb + C.kb0 + (a - C.t0) * BW, (b - a) * BW * 4);
     auto off = [&](int64_t u) { return u < b ? (uint32_t)((u - a) * BW * 4) : RUN_OOB; };
@@ -879,7 +907,9 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     // compact flush reads a column's 16 B per lane unconditionally (ds_read_b128, no conflicts)
     const uint32_t gwp = (gw + FC_COL - 1) / FC_COL * FC_COL;
     for (uint32_t i = threadIdx.x; i < 2 * gwp; i += THREADS) lds[i] = 0;
-    const PodSink<ABLATE> K{PodLds{lds, lds + gwp, g0, gw}, PodWide{wide}};
+    const uint32_t plim = (int64_t)G.n_gp <= (int64_t)g0 ? 0u : (uint32_t)imin64((int64_t)gw, (int64_t)G.n_gp - g0);
+    const uint32_t dslot = (G.default_group != NONE && G.n_gp - (uint32_t)g0 < gw) ? G.n_gp - (uint32_t)g0 : NONE;
+    const PodSink<ABLATE> K{PodLds{lds, lds + gwp, g0, gw, plim, dslot}, PodWide{wide}};
     // compact flush: this workgroup's entry range and the descriptors of its first 32 rounds,
     // fetched now so the flush does not wait on them (see the flush)
     // (entries of workgroup b: wg_cols[b * n_col + i], i < wg_off[b]; fixed-stride, so the two
