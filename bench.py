@@ -29,7 +29,7 @@ CONFIGS = {
 }
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # PMC passes (scripts/pmc_job.sh) of the kernels as built at this tag: HBM bytes per launch
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_pk2", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_p8c", "pmc_summary.json")
 
 
 def log(*a):
