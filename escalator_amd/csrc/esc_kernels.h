@@ -21,10 +21,13 @@ struct PodClass {
     uint32_t packed;           // 0 plain, 1 packed (12 B / pod), 2 packed small (8 B / pod): kp_*, kp8_* below
     uint32_t pad;
 };
-// weight (16-B loads per lane) of a K tile with R records and NXP extra pairs per pod
+// weight of a K tile with R records and NXP extra pairs per pod: its block size in half-KB
+// units (128 u32 words; the packed small block's u16 pair rows are half a KB each)
 constexpr uint32_t k_tile_weight(uint32_t R, uint32_t NXP, uint32_t packed = 0) {
-    return packed == 2 ? 2 + 2 * R + NXP : (packed ? 3 + 2 * R + NXP : 5 + 4 * R + NXP);
+    return packed == 2 ? 4 + 4 * R + NXP : (packed ? 2 * (3 + 2 * R + NXP) : 2 * (5 + 4 * R + NXP));
 }
+constexpr uint32_t K_TILE_WEIGHT_MIN = 4;   // the lightest tile (packed small, no records or pairs)
+constexpr int64_t KB_UNIT = 128;            // u32 words per weight unit
 constexpr int POD_SIG_IDS = 128;     // signatures with <= 3 extra records and <= 3 extra pairs
 constexpr int POD_CLASS_IDS = 384;   // class id = signature | packed << 7
 constexpr int K1_SEGS = 4;           // class runs per K1 workgroup in the work plan (at most)
@@ -42,7 +45,7 @@ constexpr int K1_SEGS = 4;           // class runs per K1 workgroup in the work 
 constexpr int KB_CPU0 = 256, KB_MEM0 = 512, KB_PAIR0 = 1024, KB_REC = 1280;
 __host__ __device__ inline int64_t kb_pos64(int64_t s) { return ((s & 3) >> 1) * 128 + 2 * (s >> 2) + (s & 1); }
 // first word of tile t's block (t a tile of class C)
-__host__ __device__ inline int64_t kb_block(const PodClass& C, int64_t t) { return C.kb0 + (t - C.t0) * (int64_t)C.wt * 256; }
+__host__ __device__ inline int64_t kb_block(const PodClass& C, int64_t t) { return C.kb0 + (t - C.t0) * (int64_t)C.wt * KB_UNIT; }
 __host__ __device__ inline uint32_t kb_nrec(const PodClass& C) { return C.xreg + C.xinit + C.ovh; }
 // 8-byte element index (into the array viewed as int64) of record k's cpu (mem: +256) of pod s
 __host__ __device__ inline int64_t kb_rec64(int64_t blk, uint32_t k, int64_t s) {
@@ -79,7 +82,8 @@ constexpr uint64_t KP_MEM_ABSENT = (uint64_t(1) << 44) - 1;
 //                             A daemonset pod (and a free slot) is stored with no pairs and
 //                             blocks-default set, so K1 adds it nowhere without a test.
 //   u64   record k            [512 + 512k, +512): as in the packed block
-//   u32   extra pair k        [512 + 512R + 256k, +256)
+//   u16   extra pair k        [512 + 512R + 128k, +128) words: pod s at u16 index s (0xFFFF:
+//                             none, or one no group selects)
 constexpr int KP8_REC = 512;
 constexpr int KP8_CPU_BITS = 14, KP8_MEM_BITS = 34, KP8_PAIR_SHIFT = 48;
 constexpr uint64_t KP8_CPU_MASK = (uint64_t(1) << KP8_CPU_BITS) - 1;
@@ -95,19 +99,36 @@ __host__ __device__ inline uint64_t kp8_word(uint32_t f, uint32_t cpu0, int64_t 
     return (uint64_t)cpu0 | (uint64_t)mem0 << KP8_CPU_BITS | q << KP8_PAIR_SHIFT | (ds ? KP8_DS | KP8_NODEF : 0) |
            ((f & (ESC_PF_STATIC | ESC_PF_HAS_SEL | ESC_PF_AFF_BLOCK)) ? KP8_NODEF : 0);
 }
+// extra pair k of pod s: its u32-word index (plain and packed blocks) or, in a packed small
+// block, its u16 index (kb_pair reads either)
+constexpr uint32_t KP8_XP_NONE = 0xFFFFu;
 __host__ __device__ inline int64_t kb_xp(const PodClass& C, int64_t blk, uint32_t k, int64_t s) {
-    if (C.packed == 2) return blk + KP8_REC + 512 * (int64_t)kb_nrec(C) + 256 * (int64_t)k + s;
+    if (C.packed == 2) return (blk + KP8_REC + 512 * (int64_t)kb_nrec(C) + 128 * (int64_t)k) * 2 + s;
     if (C.packed) return blk + KP_REC + 512 * (int64_t)kb_nrec(C) + 256 * (int64_t)k + s;
     return blk + KB_REC + 1024 * (int64_t)kb_nrec(C) + 256 * (int64_t)k + s;
 }
+// the first u32 word of the extra-pair rows of the block at blk, and their size in words
+__host__ __device__ inline int64_t kb_xp_row0(const PodClass& C, int64_t blk) {
+    if (C.packed == 2) return blk + KP8_REC + 512 * (int64_t)kb_nrec(C);
+    return kb_xp(C, blk, 0, 0);
+}
+__host__ __device__ inline int64_t kb_xp_words(const PodClass& C) { return (int64_t)C.nxp * (C.packed == 2 ? 128 : 256); }
+__host__ __device__ inline uint32_t kb_pair(const PodClass& C, const uint32_t* kb, int64_t blk, uint32_t k, int64_t s) {
+    if (C.packed == 2) {
+        const uint32_t q = reinterpret_cast<const uint16_t*>(kb)[kb_xp(C, blk, k, s)];
+        return q == KP8_XP_NONE ? NONE : q;
+    }
+    return kb[kb_xp(C, blk, k, s)];
+}
 // A freed / padding slot: daemonset-flagged, no pair (put as in kb_write_pod below).
+// put(width, index, value): width 8 = int64 element index, 4 = u32 word, 2 = u16 element.
 template <class Put>
 __host__ __device__ inline void kb_write_free(const PodClass& C, int64_t blk, int64_t sl, Put&& put) {
     if (C.packed == 2) {
-        put(true, blk / 2 + kb_pos64(sl), KP8_DS | KP8_NODEF | (uint64_t)KP8_PAIR_NONE << KP8_PAIR_SHIFT);
-        for (uint32_t k = 0; k < C.nxp; ++k) put(false, kb_xp(C, blk, k, sl), NONE);   // no pairs (see kp8_word)
+        put(8, blk / 2 + kb_pos64(sl), KP8_DS | KP8_NODEF | (uint64_t)KP8_PAIR_NONE << KP8_PAIR_SHIFT);
+        for (uint32_t k = 0; k < C.nxp; ++k) put(2, kb_xp(C, blk, k, sl), KP8_XP_NONE);   // no pairs (see kp8_word)
     } else {
-        put(false, blk + sl, C.packed ? (ESC_PF_DAEMONSET << KP_FLAG_SHIFT) | KP_PAIR_NONE : ESC_PF_DAEMONSET);
+        put(4, blk + sl, C.packed ? (ESC_PF_DAEMONSET << KP_FLAG_SHIFT) | KP_PAIR_NONE : ESC_PF_DAEMONSET);
     }
 }
 // packed 8-byte value of a (cpu, mem) pair; init: an absent key becomes its field's sentinel
@@ -198,35 +219,39 @@ __host__ __device__ inline void kb_rec(const PodClass& C, const uint32_t* kb, in
     }
 }
 
-// Every word a K-class pod occupies in its tile (load and in-place upserts): put(is64, index
-// in u32 words (is64 false) or in 8-byte elements (true), value).
+// Every word a K-class pod occupies in its tile (load and in-place upserts): put(width,
+// index, value) as for kb_write_free.
 template <class Put>
 __host__ __device__ inline void kb_write_pod(const PodClass& C, int64_t blk, int64_t sl, uint32_t f, uint32_t cpu0,
                                              int64_t mem0, uint32_t pair0, const int64_t* xc_cpu,
                                              const int64_t* xc_mem, const uint32_t* xp, Put&& put) {
     const uint32_t R = kb_nrec(C);
     if (C.packed == 2) {
-        put(true, blk / 2 + kb_pos64(sl), kp8_word(f, cpu0, mem0, pair0));
+        put(8, blk / 2 + kb_pos64(sl), kp8_word(f, cpu0, mem0, pair0));
         for (uint32_t k = 0; k < R; ++k)
-            put(true, (blk + KP8_REC + 512 * (int64_t)k) / 2 + kb_pos64(sl), kp_val(xc_cpu[k], xc_mem[k]));
+            put(8, (blk + KP8_REC + 512 * (int64_t)k) / 2 + kb_pos64(sl), kp_val(xc_cpu[k], xc_mem[k]));
     } else if (C.packed) {
-        put(false, blk + sl, kp_word(f, pair0));
-        put(true, (blk + KP_CM0) / 2 + kb_pos64(sl), kp_val((int64_t)cpu0, mem0));
+        put(4, blk + sl, kp_word(f, pair0));
+        put(8, (blk + KP_CM0) / 2 + kb_pos64(sl), kp_val((int64_t)cpu0, mem0));
         for (uint32_t k = 0; k < R; ++k)
-            put(true, (blk + KP_REC + 512 * (int64_t)k) / 2 + kb_pos64(sl), kp_val(xc_cpu[k], xc_mem[k]));
+            put(8, (blk + KP_REC + 512 * (int64_t)k) / 2 + kb_pos64(sl), kp_val(xc_cpu[k], xc_mem[k]));
     } else {
-        put(false, blk + sl, f);
-        put(false, blk + KB_CPU0 + sl, cpu0);
-        put(true, (blk + KB_MEM0) / 2 + kb_pos64(sl), (uint64_t)mem0);
-        put(false, blk + KB_PAIR0 + sl, pair0);
+        put(4, blk + sl, f);
+        put(4, blk + KB_CPU0 + sl, cpu0);
+        put(8, (blk + KB_MEM0) / 2 + kb_pos64(sl), (uint64_t)mem0);
+        put(4, blk + KB_PAIR0 + sl, pair0);
         for (uint32_t k = 0; k < R; ++k) {
             const int64_t o = kb_rec64(blk, k, sl);
-            put(true, o, (uint64_t)xc_cpu[k]);
-            put(true, o + 256, (uint64_t)xc_mem[k]);
+            put(8, o, (uint64_t)xc_cpu[k]);
+            put(8, o + 256, (uint64_t)xc_mem[k]);
         }
     }
-    const bool no_pairs = C.packed == 2 && (f & ESC_PF_DAEMONSET);   // (see kp8_word)
-    for (uint32_t k = 0; k < C.nxp; ++k) put(false, kb_xp(C, blk, k, sl), no_pairs ? NONE : xp[k]);
+    if (C.packed == 2) {                       // u16 pairs; a daemonset pod has none (kp8_word)
+        for (uint32_t k = 0; k < C.nxp; ++k)
+            put(2, kb_xp(C, blk, k, sl), (f & ESC_PF_DAEMONSET) || xp[k] >= KP8_XP_NONE ? KP8_XP_NONE : xp[k]);
+    } else {
+        for (uint32_t k = 0; k < C.nxp; ++k) put(4, kb_xp(C, blk, k, sl), xp[k]);
+    }
 }
 
 // Device view of a pod shard.  Two sections, made at load (esc_load_pods; sums are
@@ -467,9 +492,10 @@ hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, const u
 hipError_t launch_occupancy(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st);   // K6
 hipError_t launch_try_remove(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st);  // K7
 
-struct PatchTargets {          // k_patch destinations: 4-byte arrays 0-5, 8-byte arrays 6-11
+struct PatchTargets {          // k_patch destinations: 4-byte arrays 0-5, 8-byte arrays 6-11, 2-byte 12-13
     uint32_t* u32[6];
     int64_t* i64[6];
+    uint16_t* u16[2];
 };
 hipError_t launch_patch(const PatchTargets& t, const uint64_t* where, const uint64_t* what, int64_t n, hipStream_t st);
 

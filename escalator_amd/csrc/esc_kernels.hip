@@ -77,6 +77,10 @@ __device__ __forceinline__ uint4 ldb4(Rsrc rs, uint32_t off) {
     const v4u32 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 2);
     return make_uint4(t.x, t.y, t.z, t.w);
 }
+__device__ __forceinline__ uint2 ldb8(Rsrc rs, uint32_t off) {     // 8 B per lane
+    const auto t = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)off, 0, 2);
+    return make_uint2(t[0], t[1]);
+}
 __device__ __forceinline__ ulonglong2 ldb2(Rsrc rs, uint32_t off) {
     const v4u32 t = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 2);
     ulonglong2 r;
@@ -269,7 +273,7 @@ template <int R, int NXP>
 struct KTile<R, NXP, 2> {            // packed small block (esc_kernels.h, kp8_*)
     ulonglong2 w[2];                 // cpu0 | mem0 << 14 | pair0 << 48 | flags << 62
     ulonglong2 r[R > 0 ? R : 1][2];  // records, cpu | mem << 20
-    uint4 rq[NXP > 0 ? NXP : 1];
+    uint2 rq[NXP > 0 ? NXP : 1];     // u16 pairs, 4 per lane
 };
 template <int R, int NXP>
 struct KTile<R, NXP, 1> {            // packed block (esc_kernels.h, kp_*)
@@ -279,6 +283,10 @@ struct KTile<R, NXP, 1> {            // packed block (esc_kernels.h, kp_*)
     uint4 rq[NXP > 0 ? NXP : 1];
 };
 
+// pod j's u16 pair of a packed small block's 8-B lane load (0xFFFF: none -> above every slot)
+__device__ __forceinline__ uint32_t kp8_xp(const uint2& v, int j) {
+    return ((j < 2 ? v.x : v.y) >> (16 * (j & 1))) & 0xFFFFu;
+}
 __device__ __forceinline__ uint32_t lane4(const uint4& v, int j) {
     return j == 0 ? v.x : (j == 1 ? v.y : (j == 2 ? v.z : v.w));
 }
@@ -316,7 +324,7 @@ __device__ __forceinline__ void k_load(Rsrc rs, uint32_t to, uint32_t lane, KTil
         T.r[k][1] = ldb2(rs, w(KP8_REC + 512 * k + 256));
     }
 #pragma unroll
-    for (int k = 0; k < NXP; ++k) T.rq[k] = ldb4(rs, w(KP8_REC + 512 * R + 256 * k));
+    for (int k = 0; k < NXP; ++k) T.rq[k] = ldb8(rs, to + lane * 8 + 4u * (KP8_REC + 512 * R + 128 * k));
 }
 
 // Packed (12-B) blocks: since the small blocks take most pods, one pipeline for every
@@ -448,7 +456,7 @@ __device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLAT
                 if (i0 < K.acc.plim) { lds_add(K.acc.cc + i0, vcc); lds_add(K.acc.mem + i0, mem); }
 #pragma unroll
                 for (int k = 0; k < NXP; ++k) {
-                    const uint32_t i = lane4(T.rq[k], j) - (uint32_t)K.acc.g0;
+                    const uint32_t i = kp8_xp(T.rq[k], j) - (uint32_t)K.acc.g0;
                     if (i < K.acc.plim) { lds_add(K.acc.cc + i, vcc); lds_add(K.acc.mem + i, mem); }
                 }
             }
@@ -457,7 +465,7 @@ __device__ __forceinline__ void k_process(const GroupDev& G, const PodSink<ABLAT
             if (q0 < G.n_gp) K.add(q0, cpu, mem, false);
 #pragma unroll
             for (int k = 0; k < NXP; ++k) {
-                const uint32_t q = lane4(T.rq[k], j);
+                const uint32_t q = kp8_xp(T.rq[k], j);
                 if (q < G.n_gp) K.add(q, cpu, mem, false);
             }
         }
@@ -505,7 +513,7 @@ __device__ __forceinline__ void k_sink(const KTile<R, NXP, 2>& T) {   // loads-o
 #pragma unroll
         for (int h = 0; h < 2; ++h) y ^= T.r[k][h].x ^ T.r[k][h].y;
 #pragma unroll
-    for (int k = 0; k < NXP; ++k) x ^= T.rq[k].x ^ T.rq[k].y ^ T.rq[k].z ^ T.rq[k].w;
+    for (int k = 0; k < NXP; ++k) x ^= T.rq[k].x ^ T.rq[k].y;
     asm volatile("" :: "v"(x), "v"(y));
 }
 
@@ -544,18 +552,21 @@ __device__ __forceinline__ void k_sink(const KTile<R, NXP, 0>& T) {   // loads-o
 template <int R, int NXP, int PK, int NW, int ABLATE, int ST>
 __device__ __forceinline__ void k_run(const PodDev& P, const GroupDev& G, const PodSink<ABLATE>& K,
                                       const PodClass& C, int64_t a, int64_t b, uint32_t lane) {
-    constexpr int L = (int)k_tile_weight(R, NXP, PK);    // 16-B loads per lane per tile (plain: at most)
+    constexpr int W = (int)k_tile_weight(R, NXP, PK);    // block size, half-KB units (generic: at most)
+    // VGPRs a tile slot holds: 4 per 16-B load, 2 per 8-B one (the packed small pair rows)
+    constexpr int L = PK == 2 ? (4 + 4 * R + NXP) : W / 2;
     // block words: a compile-time constant for the specialised (packed small) shapes, the
     // class's own for the generic pipelines
-    const int64_t BW = PK == 2 ? (int64_t)L * 256 : (int64_t)C.wt * 256;
+    const int64_t BW = PK == 2 ? (int64_t)W * KB_UNIT : (int64_t)C.wt * KB_UNIT;
     // the wave's run: tiles [a, b) -> bytes [0, (b - a) * BW * 4) of its descriptor
     const Rsrc rs = rsrc(P.kb + C.kb0 + (a - C.t0) * BW, (b - a) * BW * 4);
     auto off = [&](int64_t u) { return u < b ? (uint32_t)((u - a) * BW * 4) : RUN_OOB; };
     // slots that fit the VGPR budget: 16 waves per CU leave 128 VGPRs a wave, 8 leave 256
     // (a packed tile is smaller, so more of them are in flight: up to K1_PK_DS)
     constexpr int DSM = PK == 2 ? K1_PK8_DS : (PK ? K1_PK_DS : 4);
+    constexpr int VG = PK == 2 ? 2 * L : 4 * L;
     constexpr int DS0 = NW >= 16 ? (L <= 7 ? 3 : (L <= 10 ? 2 : 1))
-                                 : (176 / (4 * L) >= DSM ? DSM : (176 / (4 * L) >= 1 ? 176 / (4 * L) : 1));
+                                 : (176 / VG >= DSM ? DSM : (176 / VG >= 1 ? 176 / VG : 1));
     // timing knobs (ABLATE bits 6/7): cap the slots in flight at 2 / 3
     constexpr int DS = (ABLATE & 64) ? (DS0 < 2 ? DS0 : 2) : ((ABLATE & 128) ? (DS0 < 3 ? DS0 : 3) : DS0);
     KTile<R, NXP, PK> T[DS];
@@ -1185,7 +1196,7 @@ __global__ __launch_bounds__(256) void k_touch(PodDev P, GroupDev G, int tw, uin
             if (hd.flags & ESC_PF_DAEMONSET) continue;
             if (hd.pair0 < G.n_gp) mark(hd.pair0);
             for (uint32_t x = 0; x < C.nxp; ++x) {
-                const uint32_t q = P.kb[kb_xp(C, blk, x, s)];
+                const uint32_t q = kb_pair(C, P.kb, blk, x, s);
                 if (q < G.n_gp) mark(q);
             }
         }
@@ -1230,7 +1241,7 @@ __device__ __forceinline__ void k_tile_exact(const PodDev& P, const GroupDev& G,
         if (pf_default_ok(h.flags) && G.default_group != NONE) acc.add(G.n_gp, (int64_t)cpu, (int64_t)mem);
         if (h.pair0 < G.n_gp) acc.add(h.pair0, (int64_t)cpu, (int64_t)mem);
         for (uint32_t k = 0; k < C.nxp; ++k) {
-            const uint32_t q = P.kb[kb_xp(C, blk, k, s)];
+            const uint32_t q = kb_pair(C, P.kb, blk, k, s);
             if (q < G.n_gp) acc.add(q, (int64_t)cpu, (int64_t)mem);
         }
     }
@@ -2453,7 +2464,8 @@ __global__ __launch_bounds__(256) void k_patch(PatchTargets T, const uint64_t* _
     const uint32_t t = (uint32_t)(w >> 60);
     const int64_t idx = (int64_t)(w & ((1ull << 60) - 1));
     if (t < 6) T.u32[t][idx] = (uint32_t)what[i];
-    else T.i64[t - 6][idx] = (int64_t)what[i];
+    else if (t < 12) T.i64[t - 6][idx] = (int64_t)what[i];
+    else T.u16[t - 12][idx] = (uint16_t)what[i];
 }
 
 // ===================================================================== scale-down reaping
@@ -2476,7 +2488,7 @@ __device__ PodRef podref_of(const PodDev& P, uint32_t d) {
         const KHead hd = kb_head(C, P.kb, blk, sl);
         r.flags = hd.flags;
         r.pair0 = hd.pair0;
-        for (uint32_t k = 0; k < C.nxp && k < 3; ++k) r.p[k] = P.kb[kb_xp(C, blk, k, sl)];
+        for (uint32_t k = 0; k < C.nxp && k < 3; ++k) r.p[k] = kb_pair(C, P.kb, blk, k, sl);
     } else {
         const int64_t c = (int64_t)d - kpods, t = c / CTILE, l = c % CTILE;
         r.flags = P.flags[c];

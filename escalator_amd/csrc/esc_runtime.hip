@@ -276,7 +276,7 @@ struct esc_ctx {
     std::vector<uint32_t> h_xc_base, h_xp_base;               // C tiles' record / pair offsets
     int64_t live_pods = 0, live_xc = 0, live_xp = 0;
     int64_t live_pk_pods = 0, live_pk_xc = 0;   // of them in packed K classes (either size)
-    int64_t live_p8_pods = 0;                   // of them in packed small K classes
+    int64_t live_p8_pods = 0, live_p8_xp = 0;   // of them in packed small K classes, their extra pairs
     int64_t c_tiles_loaded = 0;                 // C tiles of loaded pods (the spare C tiles excluded)
     // node state mirrors for esc_nodes_update
     std::vector<uint32_t> h_nflags;
@@ -317,6 +317,13 @@ int ctx_device(const esc_ctx* c) { return c->device; }
 }
 
 namespace {
+
+// A kb_write_pod / kb_write_free put into the host copy of the K blocks.
+void put_kb(std::vector<uint32_t>& kb, int width, int64_t at, uint64_t v) {
+    if (width == 8) reinterpret_cast<int64_t*>(kb.data())[at] = (int64_t)v;
+    else if (width == 4) kb[at] = (uint32_t)v;
+    else reinterpret_cast<uint16_t*>(kb.data())[at] = (uint16_t)v;
+}
 
 // Spare C slots (esc_load_pods with esc_set_spare): room per slot, slots per 64-pod tile.
 constexpr int CS_SLOTS = 16, CS_XREG = 4, CS_XINIT = 2, CS_REC = CS_XREG + CS_XINIT + 1, CS_XP = 6;
@@ -938,7 +945,7 @@ int32_t ensure_work(esc_ctx* c) {
         // per class; with dynamic shares a workgroup takes up to K1_CHUNK_CAP chunks of
         // 1 / (b * K1_CHUNKS) each
         const int64_t nch = b * K1_CHUNKS;
-        return cap * ((c->k_weight + nch - 1) / nch / k_tile_weight(0, 0) + c->n_cls + 1) * TILE +
+        return cap * ((c->k_weight + nch - 1) / nch / K_TILE_WEIGHT_MIN + c->n_cls + 1) * TILE +
                ((c->c_tiles + b - 1) / b) * CTILE;
     };
     // the static share (cap K1_CHUNKS) sets the grid; dynamic shares then take the largest
@@ -1343,7 +1350,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         k.w0 = kw;
         kw += tiles * k.wt;
         kt += tiles;
-        kbw += tiles * (int64_t)k.wt * 256;
+        kbw += tiles * (int64_t)k.wt * KB_UNIT;
         cls_of[id] = (int)cls.size();
         cls.push_back(k);
     }
@@ -1367,15 +1374,11 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         for (int64_t t = k.t0; t < k.t1; ++t) {
             const int64_t blk = kb_block(k, t);
             for (int64_t sl = 0; sl < TILE; ++sl)
-                kb_write_free(k, blk, sl, [&](bool is64, int64_t at, uint64_t v) {
-                    if (is64) reinterpret_cast<int64_t*>(hkb.data())[at] = (int64_t)v;
-                    else hkb[at] = (uint32_t)v;
-                });
+                kb_write_free(k, blk, sl, [&](int width, int64_t at, uint64_t v) { put_kb(hkb, width, at, v); });
             if (!k.packed) std::fill(hkb.begin() + blk + KB_PAIR0, hkb.begin() + blk + KB_PAIR0 + TILE, NONE);
-            const int64_t x0 = kb_xp(k, blk, 0, 0);
-            std::fill(hkb.begin() + x0, hkb.begin() + x0 + (int64_t)k.nxp * TILE, NONE);
+            const int64_t x0 = kb_xp_row0(k, blk);         // no pairs (u32 or u16 NONE)
+            std::fill(hkb.begin() + x0, hkb.begin() + x0 + kb_xp_words(k), NONE);
         }
-    int64_t* hkb64 = reinterpret_cast<int64_t*>(hkb.data());
     std::vector<uint32_t> xc_base(c_tiles + 1, 0), xp_base(c_tiles + 1, 0);
     std::vector<int32_t> pod_cls(n);
     std::vector<int64_t> pod_pos(n);
@@ -1410,10 +1413,8 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
                 pod_pos[i] = q;
                 const int64_t blk = kb_block(k, k.t0 + q / TILE);
                 kb_write_pod(k, blk, sl, f, p->cpu0[i], p->mem0[i], p->pair0[i], nc ? p->xc_cpu + rc : nullptr,
-                             nc ? p->xc_mem + rc : nullptr, nx ? p->xp_pair + rp : nullptr, [&](bool is64, int64_t at, uint64_t v) {
-                                 if (is64) hkb64[at] = (int64_t)v;
-                                 else hkb[at] = (uint32_t)v;
-                             });
+                             nc ? p->xc_mem + rc : nullptr, nx ? p->xp_pair + rp : nullptr,
+                             [&](int width, int64_t at, uint64_t v) { put_kb(hkb, width, at, v); });
             } else {
                 if (ic % CTILE == 0) { xc_base[ic / CTILE] = (uint32_t)oc; xp_base[ic / CTILE] = (uint32_t)op; }
                 const int64_t d = ic++;                   // C-array index (slot c0 + d)
@@ -1510,12 +1511,12 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     c->live_pods = n;
     c->live_xc = p->n_xc;
     c->live_xp = p->n_xp;
-    c->live_pk_pods = c->live_pk_xc = c->live_p8_pods = 0;
+    c->live_pk_pods = c->live_pk_xc = c->live_p8_pods = c->live_p8_xp = 0;
     for (int id = POD_SIG_IDS; id < POD_CLASS_IDS; ++id) {
         if (cls_of[id] < 0) continue;
         c->live_pk_pods += cnt[id];
         c->live_pk_xc += cnt[id] * (int64_t)kb_nrec(cls[cls_of[id]]);
-        if (id >= 2 * POD_SIG_IDS) c->live_p8_pods += cnt[id];
+        if (id >= 2 * POD_SIG_IDS) { c->live_p8_pods += cnt[id]; c->live_p8_xp += cnt[id] * (int64_t)cls[cls_of[id]].nxp; }
     }
     c->n_pods = n;
     c->k_tiles = k_tiles;
@@ -1805,10 +1806,11 @@ int32_t esc_stream_bytes(const esc_ctx* c, int64_t* pod_bytes, int64_t* node_byt
     if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
     // K1: flags 4 + cpu0 4 + mem0 8 + pair0 4 per pod, 16 per extra container record,
     // 4 per extra pair, 8 per C tile (record offsets); a pod of a packed class 12 B + 8 per
-    // record, of a packed small class 8 B + 8 per record (esc_kernels.h, kp_*, kp8_*); K2:
+    // record, of a packed small class 8 B + 8 per record + 2 per extra pair (esc_kernels.h,
+    // kp_*, kp8_*); K2:
     // see esc_load_nodes
     *pod_bytes = c->live_pods * 20 + c->live_xc * 16 + c->live_xp * 4 + c->c_tiles_loaded * 8 - c->live_pk_pods * 8 -
-                 c->live_pk_xc * 8 - c->live_p8_pods * 4;
+                 c->live_pk_xc * 8 - c->live_p8_pods * 4 - c->live_p8_xp * 2;
     *node_bytes = c->node_bytes;
     return ESC_OK;
 }
@@ -2255,7 +2257,9 @@ int32_t apply_patches(esc_ctx* c, Patches& P, const std::vector<PatchTargets>& t
 
 // C-section arrays (C index) and the K blocks as 4- and 8-byte words
 enum : uint32_t { PT_FLAGS = 0, PT_CPU0 = 1, PT_PAIR0 = 2, PT_XP = 3, PT_KB32 = 4, PT_MEM0 = 6, PT_XC_CPU = 7,
-                  PT_XC_MEM = 8, PT_KB64 = 9 };
+                  PT_XC_MEM = 8, PT_KB64 = 9, PT_KB16 = 12 };
+// the K-block patch target of a kb_write_pod / kb_write_free put of the given width
+uint32_t pt_kb(int width) { return width == 8 ? PT_KB64 : (width == 4 ? PT_KB32 : PT_KB16); }
 
 std::vector<PatchTargets> pod_targets(esc_ctx* c) {
     std::vector<PatchTargets> v;
@@ -2264,6 +2268,7 @@ std::vector<PatchTargets> pod_targets(esc_ctx* c) {
         t.u32[PT_FLAGS] = b.flags; t.u32[PT_CPU0] = b.cpu0; t.u32[PT_PAIR0] = b.pair0; t.u32[PT_XP] = b.xp;
         t.i64[PT_MEM0 - 6] = b.mem0; t.i64[PT_XC_CPU - 6] = b.xc_cpu; t.i64[PT_XC_MEM - 6] = b.xc_mem;
         t.u32[PT_KB32] = b.kb; t.i64[PT_KB64 - 6] = reinterpret_cast<int64_t*>(b.kb);
+        t.u16[PT_KB16 - 12] = reinterpret_cast<uint16_t*>(b.kb);
         v.push_back(t);
     }
     return v;
@@ -2287,12 +2292,12 @@ void remove_pod(esc_ctx* c, int64_t id, Patches& P) {
         const PodClass& k = c->h_cls[ci];
         const int64_t q = c->pod_pos[id];
         kb_write_free(k, kb_block(k, k.t0 + q / TILE), q % TILE,
-                      [&](bool is64, int64_t at, uint64_t v) { P.add(is64 ? PT_KB64 : PT_KB32, at, v); });
+                      [&](int width, int64_t at, uint64_t v) { P.add(pt_kb(width), at, v); });
         c->cls_free[ci].push_back(q);
         c->live_xc -= k.xreg + k.xinit + k.ovh;
         c->live_xp -= k.nxp;
         if (k.packed) { --c->live_pk_pods; c->live_pk_xc -= k.xreg + k.xinit + k.ovh; }
-        if (k.packed == 2) --c->live_p8_pods;
+        if (k.packed == 2) { --c->live_p8_pods; c->live_p8_xp -= k.nxp; }
     }
     c->pod_cls[id] = -2;
     --c->live_pods;
@@ -2739,7 +2744,7 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
             c->live_xc -= k.xreg + k.xinit + k.ovh;
             c->live_xp -= k.nxp;
             if (k.packed) { --c->live_pk_pods; c->live_pk_xc -= k.xreg + k.xinit + k.ovh; }
-        if (k.packed == 2) --c->live_p8_pods;
+        if (k.packed == 2) { --c->live_p8_pods; c->live_p8_xp -= k.nxp; }
         }
         const PodClass& k = c->h_cls[ci];
         const int64_t q = c->pod_pos[id], sl = q % TILE;
@@ -2747,13 +2752,13 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
         const uint32_t f = p->flags[i], R = kb_nrec(k);
         kb_write_pod(k, blk, sl, f, p->cpu0[i], p->mem0[i], p->pair0[i], R ? p->xc_cpu + rof[i] : nullptr,
                      R ? p->xc_mem + rof[i] : nullptr, k.nxp ? p->xp_pair + pof[i] : nullptr,
-                     [&](bool is64, int64_t at, uint64_t v) { P.add(is64 ? PT_KB64 : PT_KB32, at, v); });
+                     [&](int width, int64_t at, uint64_t v) { P.add(pt_kb(width), at, v); });
         touch_grew |= touch_mark(c, ci, q, f, p->pair0[i], k.nxp ? p->xp_pair + pof[i] : nullptr);
         ++c->live_pods;
         c->live_xc += R;
         c->live_xp += k.nxp;
         if (k.packed) { ++c->live_pk_pods; c->live_pk_xc += R; }
-        if (k.packed == 2) ++c->live_p8_pods;
+        if (k.packed == 2) { ++c->live_p8_pods; c->live_p8_xp += k.nxp; }
     }
     int32_t rc = apply_patches(c, P, pod_targets(c));
     if (!rc && touch_grew) rc = touch_upload(c);

@@ -7,7 +7,7 @@ per 64-pod C tile (pods with more than 3 extra container records or more than 3 
 pairs; all other pods sit in homogeneous 256-pod K tiles that need no offsets).  A K pod
 whose values fit the packed block (``packed_mask``) takes 12 B (pair0 | flags 4, cpu0 | mem0
 8) and 8 B per record; one that also fits the packed small block (``small_mask``) 8 B
-(cpu0 | mem0 | pair0 | flags in one u64) and 8 B per record.
+(cpu0 | mem0 | pair0 | flags in one u64), 8 B per record and 2 B per extra pair.
 K2 reads the node index once per decision: 24 B per (label pair, node) entry of a pair
 some group selects (flags 4 + cpu 8 + mem 8 + node 4) and 8 B per piece (offset + pair).
 With several ranks each reads the pieces of the group pairs it owns (``owner_ranges``:
@@ -87,7 +87,7 @@ def pod_bytes(pods: dict, n_gp: int, lo: int = 0, hi: int | None = None) -> int:
     c_tiles = (complex_pods(f[lo:hi]) + 63) // 64
     plain = (20 + 16 * nrec + 4 * nxp)[~pk].sum()
     packed = (12 + 8 * nrec + 4 * nxp)[pk & ~sm].sum()
-    small = (8 + 8 * nrec + 4 * nxp)[sm].sum()
+    small = (8 + 8 * nrec + 2 * nxp)[sm].sum()
     return int(plain + packed + small + c_tiles * 8)
 
 

@@ -26,6 +26,8 @@ for v in variants:
     c = esc.Context(s)
     c.load_synth(s, replicas=1 if cfg == 4 else 8)
     c.set_state(s.states)
+    if os.environ.get("CALIBRATE", "0") != "0":      # calibrated shares (as the bench runs K1)
+        c.k1_calibrate(int(os.environ["CALIBRATE"]))
     c.set_timing(True)
     ctxs[v] = c
 res = {v: [] for v in variants}
