@@ -489,7 +489,14 @@ struct RemovalDev {
 };
 hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, const uint32_t* run_pos, int64_t n, PodRef* refs,
                               hipStream_t st);
-hipError_t launch_occupancy(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st);   // K6
+// K6: the occupancy words of every live pair-major entry (esc_load_placement; pod and node
+// events then keep them current through launch_occ_delta instead of a recount per call).
+hipError_t launch_occupancy(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st);
+// The occupancy change of n PodRef placements: the PodRef at run position pos[i], on node
+// node[i], added (sign +1) to or removed (-1) from the words of the node's entries
+// (ne_off / ne_pos: node -> its entry positions).
+hipError_t launch_occ_delta(const GroupDev& g, const RemovalDev& r, const uint32_t* ne_off, const uint32_t* ne_pos,
+                            const uint32_t* pos, const uint32_t* node, int64_t n, int sign, hipStream_t st);
 hipError_t launch_try_remove(const NodeDev& n, const GroupDev& g, const RemovalDev& r, hipStream_t st);  // K7
 
 struct PatchTargets {          // k_patch destinations: 4-byte arrays 0-5, 8-byte arrays 6-11, 2-byte 12-13

@@ -2547,10 +2547,12 @@ __global__ __launch_bounds__(256) void k_occupancy(NodeDev N, GroupDev G, Remova
         const uint32_t f = N.e_flags[e];
         q = R.e_pair[e];
         j = N.e_node[e];
-        want = q < G.n_gp && (f & ESC_NF_TAINTED) && !(f & (ESC_NF_UNSCHED | ESC_NF_ABSENT));
-        if (!want) { R.occ_pair[e] = 0; R.occ_def[e] = 0; }   // defined words for the cross-rank SUM
+        // every live entry: the words are kept current by events from here on, and any
+        // node may become wet-tainted later
+        want = q < G.n_gp && !(f & ESC_NF_ABSENT);
+        if (!want) { R.occ_pair[e] = 0; R.occ_def[e] = 0; }
     }
-    // the wave's wet-tainted entries two at a time: both nodes' PodRef runs are loaded
+    // the wave's entries two at a time: both nodes' PodRef runs are loaded
     // before either is reduced (DPP sums, no ds_bpermute chains)
     unsigned long long m = __ballot(want);
     while (m) {
@@ -2584,6 +2586,23 @@ __global__ __launch_bounds__(256) void k_occupancy(NodeDev N, GroupDev G, Remova
             cp1 = wave_total32(cp1); cd1 = wave_total32(cd1);
             if (lane == k1) { R.occ_pair[e] = cp1; R.occ_def[e] = cd1; }
         }
+    }
+}
+
+// Occupancy deltas of pod events (launch_occ_delta): one thread per PodRef placement.
+__global__ __launch_bounds__(256) void k_occ_delta(GroupDev G, RemovalDev R, const uint32_t* __restrict__ ne_off,
+                                                   const uint32_t* __restrict__ ne_pos, const uint32_t* __restrict__ pos,
+                                                   const uint32_t* __restrict__ node, int64_t n, int sign) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const PodRef r = R.refs[pos[i]];
+    if (r.flags & ESC_PF_DAEMONSET) return;                   // NodePodsRemaining skips daemonsets
+    const bool dflt = pf_default_ok(r.flags & ~POD_REF_INDIRECT);
+    const uint32_t j = node[i], d = (uint32_t)sign;
+    for (uint32_t k = ne_off[j]; k < ne_off[j + 1]; ++k) {
+        const uint32_t e = ne_pos[k];
+        if (podref_has(r, R.xp, R.e_pair[e])) atomicAdd(R.occ_pair + e, d);
+        if (dflt) atomicAdd(R.occ_def + e, d);
     }
 }
 __global__ __launch_bounds__(64) void k_try_remove(NodeDev N, GroupDev G, RemovalDev R) {
@@ -2699,6 +2718,14 @@ hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, const u
                               hipStream_t st) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_podref_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, p, run_slot, n, run_pos, refs);
+    return hipGetLastError();
+}
+
+hipError_t launch_occ_delta(const GroupDev& g, const RemovalDev& r, const uint32_t* ne_off, const uint32_t* ne_pos,
+                            const uint32_t* pos, const uint32_t* node, int64_t n, int sign, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_occ_delta, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, g, r, ne_off, ne_pos, pos, node, n,
+                       sign);
     return hipGetLastError();
 }
 

@@ -282,6 +282,13 @@ struct esc_ctx {
     std::vector<uint32_t> h_nflags;
     std::vector<int64_t> h_ncpu, h_nmem;
     std::vector<uint32_t> ne_off, ne_pos;                     // node -> its pair-major entry positions
+    // The reaping occupancy words, maintained by pod / node events once esc_load_placement
+    // counted them (K6 no longer runs per call): d_occ at one rank; with several ranks the
+    // maintained local words are d_occ_local and d_occ is the exchange buffer.
+    uint32_t* d_occ_local = nullptr;
+    uint32_t* d_ne_off = nullptr;                             // device copies of ne_off / ne_pos
+    uint32_t* d_ne_pos = nullptr;
+    int64_t ne_dev_nodes = -1, ne_dev_pos = -1;
     std::vector<GroupNode> h_gnode;
     // dry-mode taintTracker mirror (§8f rank 4): (node << 32 | group), sorted, unique
     std::vector<uint64_t> h_trk;
@@ -478,6 +485,8 @@ void release_work(esc_ctx* c) {
 
 void release_placement(esc_ctx* c) {
     dfree(c->d_refs); dfree(c->d_e_pair); dfree(c->d_nrun_off); dfree(c->d_nrun_len); dfree(c->d_occ); dfree(c->d_rm_off);
+    dfree(c->d_occ_local); dfree(c->d_ne_off); dfree(c->d_ne_pos);
+    c->ne_dev_nodes = c->ne_dev_pos = -1;
     dfree(c->d_rm_list); dfree(c->d_taint_s); dfree(c->d_soft); dfree(c->d_hard); dfree(c->d_no_delete);
     dfree(c->d_rm_out);
     if (c->h_rm) { hipHostFree(c->h_rm); c->h_rm = nullptr; }
@@ -2311,6 +2320,75 @@ int64_t pod_slot(const esc_ctx* c, int64_t id) {
     return ci >= 0 ? (c->h_cls[ci].t0 + d / TILE) * TILE + d % TILE : d;
 }
 
+RemovalDev removal_dev(const esc_ctx* c, int64_t now_ns);
+
+// The maintained occupancy words (see esc_ctx::d_occ_local) as K6 / the deltas address them.
+RemovalDev occ_dev(const esc_ctx* c) {
+    RemovalDev r = removal_dev(c, 0);
+    uint32_t* o = c->d_occ_local ? c->d_occ_local : c->d_occ;
+    r.occ_pair = o;
+    r.occ_def = o + std::max<int64_t>(c->n_entries, 0);
+    return r;
+}
+
+// Device copy of the node -> entries map (node slots up to n_cap, entries up to n_entries).
+int32_t ensure_ne_dev(esc_ctx* c) {
+    const int64_t nn = (int64_t)c->ne_off.size() - 1, np = (int64_t)c->ne_pos.size();
+    if (nn == c->ne_dev_nodes && np == c->ne_dev_pos) return ESC_OK;
+    if (!c->d_ne_off) {
+        HIP_TRY(dalloc(&c->d_ne_off, (size_t)std::max<int64_t>(c->n_cap, nn) + 1));
+        HIP_TRY(dalloc(&c->d_ne_pos, (size_t)std::max<int64_t>(c->n_entries, std::max<int64_t>(np, 1))));
+    }
+    std::vector<uint32_t> off(c->ne_off);
+    off.resize((size_t)std::max<int64_t>(c->n_cap, nn) + 1, c->ne_off.back());   // free slots: no entries
+    HIP_TRY(hipMemcpy(c->d_ne_off, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+    if (np) HIP_TRY(hipMemcpy(c->d_ne_pos, c->ne_pos.data(), (size_t)np * 4, hipMemcpyHostToDevice));
+    c->ne_dev_nodes = nn;
+    c->ne_dev_pos = np;
+    return ESC_OK;
+}
+
+// K6 over every live entry into the maintained words (esc_load_placement).
+int32_t occ_recount(esc_ctx* c) {
+    if (int32_t rc = ensure_ne_dev(c)) return rc;
+    HIP_TRY(launch_occupancy(node_dev(c), group_dev(c), occ_dev(c), c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ESC_OK;
+}
+
+// The PodRefs now at run positions pos (on nodes node) added to (+1) or removed from (-1)
+// the maintained occupancy words: called before the runs change for the pods an event
+// moves or drops, and after for the pods it binds or rewrites.
+int32_t occ_delta(esc_ctx* c, const std::vector<uint32_t>& pos, const std::vector<uint32_t>& node, int sign) {
+    if (!c->placed || pos.empty()) return ESC_OK;
+    if (int32_t rc = ensure_ne_dev(c)) return rc;
+    uint32_t *dp = nullptr, *dn = nullptr;
+    HIP_TRY(dalloc(&dp, pos.size()));
+    HIP_TRY(dalloc(&dn, node.size()));
+    hipError_t e = hipMemcpy(dp, pos.data(), pos.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dn, node.data(), node.size() * 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = launch_occ_delta(group_dev(c), occ_dev(c), c->d_ne_off, c->d_ne_pos, dp, dn, (int64_t)pos.size(), sign, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    dfree(dp);
+    dfree(dn);
+    HIP_TRY(e);
+    return ESC_OK;
+}
+
+// (position, node) of every bound pod among ids
+void bound_of(const esc_ctx* c, const int64_t* ids, int64_t n, std::vector<uint32_t>& pos, std::vector<uint32_t>& node) {
+    pos.clear();
+    node.clear();
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t id = ids[i];
+        if (id >= 0 && id < (int64_t)c->h_pod_rpos.size() && c->h_pod_rpos[id] >= 0) {
+            pos.push_back((uint32_t)c->h_pod_rpos[id]);
+            node.push_back(c->h_pod_node[id]);
+        }
+    }
+}
+
 RemovalDev removal_dev(const esc_ctx* c, int64_t now_ns) {
     RemovalDev r;
     r.e_pair = c->d_e_pair; r.n_entries = c->n_entries;
@@ -2763,10 +2841,15 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
     int32_t rc = apply_patches(c, P, pod_targets(c));
     if (!rc && touch_grew) rc = touch_upload(c);
     if (rc || !c->placed) return rc;
-    // a bound pod keeps its node; its PodRef follows the new record (and slot)
+    // a bound pod keeps its node; its PodRef follows the new record (and slot), and its
+    // occupancy contribution with it
+    std::vector<uint32_t> bpos, bnode;
+    bound_of(c, ids, n, bpos, bnode);
+    if (int32_t r2 = occ_delta(c, bpos, bnode, -1)) return r2;
     std::vector<int64_t> touched(ids, ids + n);
     std::vector<uint32_t> runs;
-    return sync_placement(c, touched, runs);
+    if (int32_t r2 = sync_placement(c, touched, runs)) return r2;
+    return occ_delta(c, bpos, bnode, +1);
 }
 
 // esc_pods_bind's checks (ids, nodes, room in the runs) without applying anything.
@@ -2825,6 +2908,14 @@ int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
     Patches P;
     std::vector<int64_t> touched;
     std::vector<uint32_t> runs;
+    if (c->placed) {                                 // the deleted pods leave their nodes' occupancy
+        std::vector<int64_t> live_ids;
+        for (int64_t i = 0; i < n; ++i)
+            if (c->pod_cls[ids[i]] != -2) live_ids.push_back(ids[i]);
+        std::vector<uint32_t> bpos, bnode;
+        bound_of(c, live_ids.data(), (int64_t)live_ids.size(), bpos, bnode);
+        if (int32_t rc = occ_delta(c, bpos, bnode, -1)) return rc;
+    }
     for (int64_t i = 0; i < n; ++i) {
         if (c->placed && c->pod_cls[ids[i]] != -2) run_remove(c, ids[i], touched, runs);   // leaves its node
         remove_pod(c, ids[i], P);
@@ -2850,10 +2941,15 @@ int32_t esc_pods_bind(esc_ctx* c, const int64_t* ids, const uint32_t* pod_node, 
     }
     std::vector<int64_t> touched;
     std::vector<uint32_t> runs;
+    std::vector<uint32_t> bpos, bnode;
+    bound_of(c, ids, n, bpos, bnode);                // the pods leave their old nodes' occupancy
+    if (int32_t rc = occ_delta(c, bpos, bnode, -1)) return rc;
     for (int64_t i = 0; i < n; ++i) run_remove(c, ids[i], touched, runs);      // removals first: room
     for (int64_t i = 0; i < n; ++i)
         if (pod_node[i] != NONE && !run_append(c, ids[i], pod_node[i], touched, runs)) return ESC_E_HIP;
-    return sync_placement(c, touched, runs);
+    if (int32_t rc = sync_placement(c, touched, runs)) return rc;
+    bound_of(c, ids, n, bpos, bnode);                // and join their new ones'
+    return occ_delta(c, bpos, bnode, +1);
 }
 
 int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32_t* flags, const int64_t* cpu,
@@ -3218,7 +3314,7 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
     const int64_t NC = std::max<int64_t>(c->n_cap, N);
     if (!c->d_taint_s || c->rm_nodes != NC) {
         // per-node facts and the per-entry occupancy words, sized for this node table
-        dfree(c->d_taint_s); dfree(c->d_no_delete); dfree(c->d_occ); dfree(c->d_e_pair);
+        dfree(c->d_taint_s); dfree(c->d_no_delete); dfree(c->d_occ); dfree(c->d_e_pair); dfree(c->d_occ_local);
         dfree(c->d_soft); dfree(c->d_hard); dfree(c->d_rm_out); dfree(c->d_rm_off); dfree(c->d_rm_list);
         HIP_TRY(dalloc(&c->d_taint_s, std::max<int64_t>(NC, 1)));
         HIP_TRY(dalloc(&c->d_no_delete, std::max<int64_t>(NC, 1)));
@@ -3228,6 +3324,8 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
             HIP_TRY(hipMemset(c->d_no_delete + N, 0, NC - N));
         }
         HIP_TRY(dalloc(&c->d_occ, 2 * std::max<int64_t>(c->n_entries, 1)));
+        if (c->world > 1) HIP_TRY(dalloc(&c->d_occ_local, 2 * std::max<int64_t>(c->n_entries, 1)));
+        c->placed = false;                             // the occupancy words are recounted below
         HIP_TRY(dalloc(&c->d_soft, G)); HIP_TRY(dalloc(&c->d_hard, G));
         HIP_TRY(dalloc(&c->d_rm_out, G)); HIP_TRY(dalloc(&c->d_rm_off, G));
         // each group's deletable-node list can hold all of its pair's entries
@@ -3307,6 +3405,7 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
         HIP_TRY(e2);
         c->h_run_off.swap(off);
         c->h_run_len.swap(len);
+        if (int32_t rc = occ_recount(c)) return rc;
         c->placed = true;
     }
     c->node_removal = true;
@@ -3322,7 +3421,10 @@ int32_t esc_reap_occupancy(esc_ctx* c) {
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->placed || !c->node_removal) return ESC_E_STATE;
     hipSetDevice(c->device);
-    HIP_TRY(launch_occupancy(node_dev(c), group_dev(c), removal_dev(c, 0), c->stream));
+    // the words are current (events maintain them); with several ranks this rank's words
+    // go into the exchange buffer the SUM works on
+    if (c->d_occ_local && c->n_entries)
+        HIP_TRY(hipMemcpyAsync(c->d_occ, c->d_occ_local, (size_t)(2 * c->n_entries) * 4, hipMemcpyDeviceToDevice, c->stream));
     c->rm_valid = false;
     return ESC_OK;
 }
