@@ -234,18 +234,19 @@ def bench_order(args):
         dist.destroy_process_group()
         return
     # algorithmic bytes per membership: read node, group, flags (12 B), write the node (4 B;
-    # an upper bound — cordoned nodes feed neither order).  The three-pass default moves 22 B
-    # (a class byte written and read back, the node read twice); the fused single pass
-    # (ESC_ORDER_FUSED=1) moves the 16 B.
+    # an upper bound — cordoned nodes feed neither order).  The two-pass default moves 14 B
+    # (classify: flags 4 read, a class byte written; split: the class byte and the node
+    # read, the node written — the group is implied by the region, PMC in
+    # profiles/r03_k5/pmc_config5.json); the fused single pass (ESC_ORDER_FUSED=1) 16 B.
     fused = os.environ.get("ESC_ORDER_FUSED", "0") not in ("", "0")
     order_bytes = n_memb * 16
-    moved_bytes = n_memb * (16 if fused else 22)
-    # the index build: node table read twice (count, list: flags, label, created ~24 B),
-    # each membership written once (16 B key + value), LSD passes of <= 8 bits over the
-    # (group << R | creation offset) keys (hist: 8 B read; scatter: 16 B read + 16 B
-    # written), then read once more (16 B) into the regions (12 B written)
+    moved_bytes = n_memb * (16 if fused else 14)
+    # the index build: node table read twice (count: flags, label 8 B; list: flags, label,
+    # created 16 B), each membership written once (12 B: 8-B key, 4-B node | flags value),
+    # LSD passes of <= 8 bits over the (group << R | creation offset) keys (hist: 8 B read;
+    # scatter: 12 B read + 12 B written), the last pass writing the regions instead (12 B)
     idx_passes = -(-(R + max(1, (G - 1).bit_length())) // 8)
-    index_bytes = N * 2 * 24 + n_memb * (16 + idx_passes * 40 + 16 + 12)
+    index_bytes = N * 24 + n_memb * (12 + idx_passes * 32)
     out = {
         "metric": "config5 node orderings: memberships ordered/sec per decision (taint/untaint selection)",
         "value": n_memb / (order_ms * 1e-3),

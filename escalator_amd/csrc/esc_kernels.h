@@ -540,12 +540,20 @@ hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t
 // the groups' padded regions.
 hipError_t launch_memb_count(const NodeDev& n, const GroupDev& g, int nblk, uint32_t* cnt, uint32_t* total,
                              hipStream_t st);
+// The age index's destination: every group's padded region (k_rs_scatter<FINAL>).
+struct RegionSink {
+    const int64_t* seg;        // sorted start of group g's memberships (host-computed)
+    const uint32_t* pstart;    // region start of group g
+    const uint32_t* plen;      // memberships of group g
+    const uint8_t* dry;
+    uint32_t *g_node, *g_grp, *g_flags;
+    uint32_t* err;             // set when a membership falls outside its group's count
+    int32_t G;
+    int R;                     // creation-offset bits (key = group << R | offset)
+};
 hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const uint32_t* base, int64_t n_memb,
-                           int64_t ts_min, uint64_t div, int R, int gbits, uint64_t* keys[2], uint64_t* vals[2],
-                           uint32_t* hist, uint32_t* tot, int64_t* starts, int* src, hipStream_t st);
-hipError_t launch_region_write(const uint64_t* keys, const uint64_t* vals, int64_t n_memb, int R, const GroupDev& g,
-                               const int64_t* starts, const uint32_t* pstart, uint32_t* g_node, uint32_t* g_grp,
-                               uint32_t* g_flags, hipStream_t st);
+                           int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, uint64_t* keys[2], uint32_t* vals[2],
+                           uint32_t* hist, uint32_t* tot, const RegionSink& S, hipStream_t st);
 hipError_t launch_order(const NodeDev& n, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
                         const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp, const uint32_t* g_flags,
                         int64_t n_e, int32_t G, uint32_t* cls4, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,

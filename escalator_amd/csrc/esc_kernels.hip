@@ -28,6 +28,9 @@
 
 #include "esc_kernels.h"
 
+#ifndef MK_ABL
+#define MK_ABL 0                                     // k_memb_keys ablations (timing only)
+#endif
 #ifndef ESC_PART
 #define ESC_PART 0
 #endif
@@ -1684,11 +1687,17 @@ constexpr int SORT_WAVES = SORT_BLOCK / 64;
 }
 
 // Creation offset of node i (divided by div when exact): the low key bits of its memberships.
-__device__ __forceinline__ uint64_t age_key(const NodeDev& N, int64_t i, int64_t ts_min, uint64_t div) {
-    const uint64_t off = (uint64_t)(N.created[i] - ts_min);
-    return div > 1 ? off / div : off;
+// x / d for the creation-time divisors the host picks (1, 10^3, 10^6, 10^9): divisions by
+// constants (multiply-high) instead of the 64-bit division routine.
+__device__ __forceinline__ uint64_t div_pow10(uint64_t x, uint64_t d) {
+    switch (d) {
+        case 1: return x;
+        case 1000ull: return x / 1000ull;
+        case 1000000ull: return x / 1000000ull;
+        case 1000000000ull: return x / 1000000000ull;
+        default: return x / d;
+    }
 }
-
 // ---- LSD radix sort building blocks (stable), BITS-bit digits, KT = uint64_t or uint32_t.
 // hist is digit-major: hist[d * nblk + b] = keys of block b with digit d.
 template <class KT, int BITS>
@@ -1704,7 +1713,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_hist(const KT* __restrict__ k
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
-    constexpr int U = 4;                                 // keys in flight per thread
+    constexpr int U = 8;                                 // keys in flight per thread
     for (int64_t b = lo; b < hi; b += (int64_t)SORT_BLOCK * U) {
         KT k[U];
 #pragma unroll
@@ -1782,57 +1791,122 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scan_tot(uint32_t* __restrict
     }
 }
 
-// Stable scatter of one pass: rank = digit base + block offset + rank inside the block in
-// input order (ballot match per wave, per-wave digit counts in LDS).
-template <class KT, class VT, int BITS>
+// Stable scatter of one pass, a chunk of RS_U * SORT_BLOCK keys at a time: ranks from
+// ballot matching per wave and per-(round, wave) digit counts; the chunk is reordered by
+// digit in LDS and written out in per-digit runs (stored straight from the ranking, a
+// wave's 64 keys went to ~64 different buckets: 8-B scattered stores, 1.6x write traffic).
+// A membership's sort value: node | its flags' low four bits (UNSCHED, TAINTED, TRACKED
+// resolved for the group, ABSENT: all the per-decision split reads) << 28.  4 B instead of
+// node | flags << 32: every LSD pass moves 8 B less per membership.
+constexpr uint32_t MEMB_FLAG_SHIFT = 28, MEMB_NODE_MASK = (1u << MEMB_FLAG_SHIFT) - 1;
+// Sorted membership at position p (key = group << R | offset, value as above)
+// into its group's region: pstart[g] + p - seg[g].  The sorted starts seg are the host's
+// (live entries per pair); a position outside the group's [0, len) means the device listed a
+// different count, and is flagged in *err instead of written.
+__device__ __forceinline__ void region_put(const RegionSink& S, uint32_t p, uint64_t key, uint32_t v) {
+    const uint32_t g = (uint32_t)(key >> S.R);
+    const int64_t r = (int64_t)p - S.seg[g];
+    if (g >= (uint32_t)S.G || r < 0 || r >= (int64_t)S.plen[g]) { *S.err = 1u; return; }
+    const int64_t d = (int64_t)S.pstart[g] + r;
+    S.g_node[d] = v & MEMB_NODE_MASK;
+    S.g_grp[d] = g | (S.dry[g] ? NODE_DRY_BIT : 0u);
+    S.g_flags[d] = v >> MEMB_FLAG_SHIFT;
+}
+
+// FINAL (the age index's last pass): a key's sorted position goes straight into its group's
+// padded region (RegionSink) instead of the key / value arrays.
+constexpr int RS_U = 2;
+template <class KT, class VT, int BITS, bool FINAL>
 __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict__ kin, const VT* __restrict__ vin,
                                                            KT* __restrict__ kout, VT* __restrict__ vout,
                                                            int64_t n, int shift, const uint32_t* __restrict__ hist,
-                                                           const uint32_t* __restrict__ tot) {
-    constexpr int NB = 1 << BITS;
-    __shared__ uint32_t run[NB];
-    __shared__ uint32_t wh[SORT_WAVES][NB];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int d = threadIdx.x; d < NB; d += SORT_BLOCK) run[d] = tot[d] + hist[(int64_t)d * gridDim.x + blockIdx.x];
+                                                           const uint32_t* __restrict__ tot, RegionSink sink) {
+    constexpr int NB = 1 << BITS, S = RS_U * SORT_WAVES, CH = RS_U * SORT_BLOCK;
+    static_assert(NB <= SORT_BLOCK, "one thread per digit");
+    __shared__ uint32_t run[NB];                         // output position of the digit's next key
+    __shared__ uint32_t lst[NB];                         // the digit's first slot in the chunk
+    __shared__ uint32_t wh[S][NB];                       // (round, wave) digit counts -> offsets
+    __shared__ uint32_t ws[SORT_WAVES];
+    __shared__ KT sk[CH];
+    __shared__ VT sv[CH];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, t = threadIdx.x;
+    if (t < NB) run[t] = tot[t] + hist[(int64_t)t * gridDim.x + blockIdx.x];
+    for (int e = t; e < S * NB; e += SORT_BLOCK) (&wh[0][0])[e] = 0;
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    // the next chunk's key / value are loaded one iteration ahead
-    KT nkey = lo + (int64_t)threadIdx.x < hi ? kin[lo + threadIdx.x] : (KT)0;
-    VT nval = lo + (int64_t)threadIdx.x < hi ? vin[lo + threadIdx.x] : (VT)0;
-    for (int64_t b = lo; b < hi; b += SORT_BLOCK) {
-        const int64_t i = b + threadIdx.x;
-        const bool ok = i < hi;
-        const KT key = nkey;
-        const VT val = nval;
-        const int64_t ni = i + SORT_BLOCK;
-        nkey = ni < hi ? kin[ni] : (KT)0;
-        nval = ni < hi ? vin[ni] : (VT)0;
-        for (int k = threadIdx.x; k < SORT_WAVES * NB; k += SORT_BLOCK) (&wh[0][0])[k] = 0;
-        __syncthreads();
-        const uint32_t d = (uint32_t)(key >> shift) & (NB - 1);
-        unsigned long long m = __ballot(ok);
+    uint32_t dtot = 0;                                   // this thread's digit: keys in the last chunk
+    KT key[RS_U];
+    VT val[RS_U];
 #pragma unroll
-        for (int bit = 0; bit < BITS; ++bit) {
-            const unsigned long long bb = __ballot((d >> bit) & 1);
-            m &= ((d >> bit) & 1) ? bb : ~bb;
+    for (int u = 0; u < RS_U; ++u) {
+        const int64_t i = lo + u * SORT_BLOCK + t;
+        key[u] = i < hi ? kin[i] : (KT)0;
+        val[u] = i < hi ? vin[i] : (VT)0;
+    }
+    __syncthreads();
+    for (int64_t b = lo; b < hi; b += CH) {
+        uint32_t d[RS_U], r[RS_U];
+        bool ok[RS_U];
+#pragma unroll
+        for (int u = 0; u < RS_U; ++u) {
+            ok[u] = b + u * SORT_BLOCK + t < hi;
+            d[u] = (uint32_t)(key[u] >> shift) & (NB - 1);
+            unsigned long long m = __ballot(ok[u]);
+#pragma unroll
+            for (int bit = 0; bit < BITS; ++bit) {
+                const unsigned long long bb = __ballot((d[u] >> bit) & 1);
+                m &= ((d[u] >> bit) & 1) ? bb : ~bb;
+            }
+            r[u] = __popcll(m & lt);
+            if (ok[u] && r[u] == 0) wh[u * SORT_WAVES + wid][d[u]] = __popcll(m);
         }
-        const uint32_t r_in_wave = __popcll(m & lt);
-        if (ok && r_in_wave == 0) wh[wid][d] = __popcll(m);
         __syncthreads();
-        uint32_t pre = 0;
-        for (int k = 0; k < wid; ++k) pre += wh[k][d];
-        if (ok) {
-            const uint32_t dst = run[d] + pre + r_in_wave;
-            kout[dst] = key;
-            vout[dst] = val;
+        // per digit: offsets of the (round, wave) segments, the digit's count; the previous
+        // chunk's count moves run on (its write-out has finished)
+        uint32_t c = 0;
+        if (t < NB) {
+            run[t] += dtot;
+#pragma unroll 8
+            for (int s = 0; s < S; ++s) { const uint32_t v = wh[s][t]; wh[s][t] = c; c += v; }
+            dtot = c;
+        }
+        const uint32_t x = wave_incl_scan32(c);          // digits in thread order (0 past NB)
+        if (lane == 63) ws[wid] = x;
+        __syncthreads();
+        if (t < NB) {
+            uint32_t p = x - dtot;
+            for (int k = 0; k < wid; ++k) p += ws[k];
+            lst[t] = p;
         }
         __syncthreads();
-        for (int dd = threadIdx.x; dd < NB; dd += SORT_BLOCK) {
-            uint32_t t = 0;
-            for (int k = 0; k < SORT_WAVES; ++k) t += wh[k][dd];
-            run[dd] += t;
+#pragma unroll
+        for (int u = 0; u < RS_U; ++u)
+            if (ok[u]) {
+                const uint32_t s = lst[d[u]] + wh[u * SORT_WAVES + wid][d[u]] + r[u];
+                sk[s] = key[u];
+                sv[s] = val[u];
+            }
+        __syncthreads();
+        // the next chunk's keys in flight during the write-out
+#pragma unroll
+        for (int u = 0; u < RS_U; ++u) {
+            const int64_t i = b + CH + u * SORT_BLOCK + t;
+            key[u] = i < hi ? kin[i] : (KT)0;
+            val[u] = i < hi ? vin[i] : (VT)0;
         }
+        const int cn = (int)imin64(CH, hi - b);
+        for (int e = t; e < cn; e += SORT_BLOCK) {
+            const KT kk = sk[e];
+            const uint32_t dd = (uint32_t)(kk >> shift) & (NB - 1);
+            const uint32_t g = run[dd] + (uint32_t)e - lst[dd];
+            if constexpr (FINAL) region_put(sink, g, kk, sv[e]);
+            else {
+                kout[g] = kk;
+                vout[g] = sv[e];
+            }
+        }
+        for (int e = t; e < S * NB; e += SORT_BLOCK) (&wh[0][0])[e] = 0;
         __syncthreads();
     }
 }
@@ -1841,16 +1915,88 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
 // the node table), then sorted by (group, creation offset) with (node | flags << 32)
 // carried along, then written into the groups' padded regions (streaming).
 // Memberships of the nodes of this block's share of [0, n) (snapshot order).
-__global__ __launch_bounds__(SORT_BLOCK) void k_memb_count(NodeDev N, GroupDev G, int64_t n, uint32_t* __restrict__ cnt) {
+// (node_groups with the node's flags and the group code of its label0 already loaded,
+// memb_codes)
+template <class F>
+__device__ __forceinline__ void node_groups_c0(const NodeDev& N, const GroupDev& G, uint32_t f, int64_t i, uint32_t c0,
+                                               F&& emit) {
+    if (f & ESC_NF_ABSENT) return;
+    for_code(G, c0, emit);
+    const uint32_t nx = nf_xlbl(f);
+    if (nx) {
+        const uint32_t q = N.xl_off[i];
+        for (uint32_t k = 0; k < nx; ++k) {
+            const uint32_t p = N.xl[q + k];
+            if (p >= N.q_lo && p < N.q_hi) for_code(G, node_code(G, p), emit);
+        }
+    }
+}
+constexpr int MEMB_U = 4;                            // consecutive nodes per thread per round
+constexpr int MEMB_BLOCK = 512, MEMB_WAVES = MEMB_BLOCK / 64;
+// LDS staging of one round's memberships (1.5 per node; a round with more stores directly)
+constexpr int MEMB_CAP = MEMB_BLOCK * MEMB_U * 3 / 2;
+// A block's share of the node range: whole groups of MEMB_U nodes, so a thread's nodes start
+// on a 16-B boundary (the node arrays start at node 0: N.lo == 0, one rank holds the table).
+__device__ __forceinline__ int64_t memb_share(int64_t n) {
+    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    return (per + MEMB_U - 1) / MEMB_U * MEMB_U;
+}
+// Flags, label0 (and creation times) of nodes [r0, r0 + MEMB_U) with 16-B loads when all are
+// below hi (absent / NONE past it).
+__device__ __forceinline__ void memb_load(const NodeDev& N, int64_t r0, int64_t hi, uint32_t (&f)[MEMB_U],
+                                          uint32_t (&l0)[MEMB_U], int64_t* cr) {
+    const int64_t i0 = N.lo + r0;
+    if (r0 + MEMB_U <= hi && (i0 & 3) == 0) {
+        const uint4 a = *reinterpret_cast<const uint4*>(N.flags + i0), b = *reinterpret_cast<const uint4*>(N.label0 + i0);
+        f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+        l0[0] = b.x; l0[1] = b.y; l0[2] = b.z; l0[3] = b.w;
+        if (cr) {
+            const longlong2 c0 = *reinterpret_cast<const longlong2*>(N.created + i0);
+            const longlong2 c1 = *reinterpret_cast<const longlong2*>(N.created + i0 + 2);
+            cr[0] = c0.x; cr[1] = c0.y; cr[2] = c1.x; cr[3] = c1.y;
+        }
+        return;
+    }
+#pragma unroll
+    for (int u = 0; u < MEMB_U; ++u) {
+        const bool ok = r0 + u < hi;
+        f[u] = ok ? N.flags[i0 + u] : ESC_NF_ABSENT;
+        l0[u] = ok ? N.label0[i0 + u] : NONE;
+        if (cr) cr[u] = ok ? N.created[i0 + u] : 0;
+    }
+}
+
+// The group codes of the MEMB_U nodes' first labels, loaded together (unconditional loads
+// at a clamped index: in branches they went out one after another).
+__device__ __forceinline__ void memb_codes(const NodeDev& N, const GroupDev& G, const uint32_t (&f)[MEMB_U],
+                                           const uint32_t (&l0)[MEMB_U], uint32_t (&c0)[MEMB_U]) {
+#pragma unroll
+    for (int u = 0; u < MEMB_U; ++u) {
+        const uint32_t q = l0[u];
+        const bool ok = !(f[u] & ESC_NF_ABSENT) && q >= N.q_lo && q < N.q_hi && q < G.n_gp;
+        c0[u] = G.n_gp ? G.node_code[ok ? q : 0u] : NONE;
+        if (!ok) c0[u] = NONE;
+    }
+}
+
+// Each thread takes MEMB_U consecutive nodes per round, their flags and labels loaded
+// before any is looked at (the listing is latency-bound: one node per thread per round
+// left a chain of dependent loads per 1024 nodes).
+__global__ __launch_bounds__(MEMB_BLOCK) void k_memb_count(NodeDev N, GroupDev G, int64_t n, uint32_t* __restrict__ cnt) {
     __shared__ uint32_t tot;
     if (threadIdx.x == 0) tot = 0;
     __syncthreads();
-    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const int64_t per = memb_share(n);
     const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
     uint32_t c = 0;
-    for (int64_t r = lo + threadIdx.x; r < hi; r += SORT_BLOCK) {
-        const int64_t i = N.lo + r;
-        node_groups(N, G, N.flags[i], i, [&](uint32_t) { ++c; });
+    for (int64_t b = lo; b < hi; b += (int64_t)MEMB_BLOCK * MEMB_U) {
+        uint32_t f[MEMB_U], l0[MEMB_U];
+        memb_load(N, b + (int64_t)threadIdx.x * MEMB_U, hi, f, l0, nullptr);
+        uint32_t c0[MEMB_U];
+        memb_codes(N, G, f, l0, c0);
+#pragma unroll
+        for (int u = 0; u < MEMB_U; ++u)
+            node_groups_c0(N, G, f[u], N.lo + b + (int64_t)threadIdx.x * MEMB_U + u, c0[u], [&](uint32_t) { ++c; });
     }
     atomicAdd(&tot, c);
     __syncthreads();
@@ -1887,71 +2033,89 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_scan_small(uint32_t* __restrict_
 // label order): key = group << R | creation offset (R bits), value = node | membership
 // flags << 32 — a dry group's membership carries "tracked by this group" in the tracker
 // bit (controller.go:126-138), so the per-decision split needs no lookup.
-__global__ __launch_bounds__(SORT_BLOCK) void k_memb_keys(NodeDev N, GroupDev G, int64_t n, const uint32_t* __restrict__ base,
-                                                          int64_t ts_min, uint64_t div, int R,
-                                                          uint64_t* __restrict__ keys, uint64_t* __restrict__ vals) {
-    __shared__ uint32_t wsum[SORT_WAVES];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) carry = base[blockIdx.x];
-    __syncthreads();
+template <int ABL>                                   // ABL != 0: timing ablations (MK_ABL builds)
+__global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G, int64_t n, const uint32_t* __restrict__ base,
+                                                          int64_t cap, int64_t ts_min, uint64_t div, int R,
+                                                          uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    // A round's memberships are staged in LDS and written out as two contiguous streams:
+    // stored straight from the walk, a wave's 8-B stores land ~4 entries apart per lane and
+    // the listing took 5x its store-free time (measured, r03_mk).
+    __shared__ uint32_t wsum[MEMB_WAVES];
+    __shared__ uint64_t sk[MEMB_CAP];
+    __shared__ uint32_t sv[MEMB_CAP];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+    uint32_t carry = base[blockIdx.x];
+    const int64_t per = memb_share(n);
     const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
-    for (int64_t b = lo; b < hi; b += SORT_BLOCK) {
-        const int64_t r = b + threadIdx.x;
-        uint32_t c = 0, f = 0;
-        const int64_t i = N.lo + r;
-        if (r < hi) { f = N.flags[i]; node_groups(N, G, f, i, [&](uint32_t) { ++c; }); }
+    for (int64_t b = lo; b < hi; b += (int64_t)MEMB_BLOCK * MEMB_U) {
+        // MEMB_U consecutive nodes per thread (snapshot order = thread order), loads first
+        const int64_t r0 = b + (int64_t)threadIdx.x * MEMB_U;
+        uint32_t f[MEMB_U], l0[MEMB_U];
+        int64_t cr[MEMB_U];
+        memb_load(N, r0, hi, f, l0, cr);
+        uint32_t c0[MEMB_U];
+        memb_codes(N, G, f, l0, c0);
+        // a tracked node's first tracker entry, loaded with the codes (most tracked nodes are
+        // tracked by one group: the per-membership lookup then needs nothing more)
+        uint32_t tk[MEMB_U];
+        int32_t tn[MEMB_U], tg[MEMB_U];
+#pragma unroll
+        for (int u = 0; u < MEMB_U; ++u) tk[u] = (f[u] & ESC_NF_TRACKED) ? N.trk_start[N.lo + r0 + u] : NONE;
+#pragma unroll
+        for (int u = 0; u < MEMB_U; ++u) {
+            const bool v = tk[u] != NONE && (int64_t)tk[u] < N.n_trk;
+            tn[u] = v ? N.trk_node[tk[u]] : -1;
+            tg[u] = v ? N.trk_group[tk[u]] : -1;
+        }
+        uint32_t c = 0;
+        if constexpr (ABL == 2) {
+#pragma unroll
+            for (int u = 0; u < MEMB_U; ++u) c += (f[u] & ESC_NF_ABSENT) ? 0u : 1u;
+        } else {
+#pragma unroll
+            for (int u = 0; u < MEMB_U; ++u) node_groups_c0(N, G, f[u], N.lo + r0 + u, c0[u], [&](uint32_t) { ++c; });
+        }
         const uint32_t x = wave_incl_scan32(c);
         if (lane == 63) wsum[wid] = x;
         __syncthreads();
-        uint32_t pos = carry + x - c;
-        for (int k = 0; k < wid; ++k) pos += wsum[k];
-        if (r < hi && c) {
-            const uint64_t ak = age_key(N, i, ts_min, div);
-            node_groups(N, G, f, i, [&](uint32_t mb) {
-                const uint32_t mf = mdry(mb) ? ((f & ~ESC_NF_TRACKED) |
-                                                (((f & ESC_NF_TRACKED) && tracked(N, (int32_t)i, (int32_t)mg(mb)))
-                                                     ? ESC_NF_TRACKED : 0u))
-                                             : f;
-                keys[pos] = ((uint64_t)mg(mb) << R) | ak;
-                vals[pos] = (uint64_t)(uint32_t)i | ((uint64_t)mf << 32);
+        uint32_t pos = x - c, total = 0;
+#pragma unroll
+        for (int k = 0; k < MEMB_WAVES; ++k) {
+            const uint32_t s = wsum[k];
+            pos += k < wid ? s : 0u;
+            total += s;
+        }
+        const bool stage = total <= (uint32_t)MEMB_CAP;   // block-uniform
+#pragma unroll
+        for (int u = 0; u < MEMB_U; ++u) {
+            const int64_t i = N.lo + r0 + u;
+            const uint64_t off = (uint64_t)(cr[u] - ts_min);
+            const uint64_t ak = ABL == 3 ? off : div_pow10(off, div);
+            const uint32_t fu = f[u];
+            node_groups_c0(N, G, fu, i, c0[u], [&](uint32_t mb) {
+                bool tr = false;
+                if (ABL != 5 && mdry(mb) && (fu & ESC_NF_TRACKED))
+                    tr = (tn[u] == (int32_t)i && tg[u] == (int32_t)mg(mb)) || tracked(N, (int32_t)i, (int32_t)mg(mb));
+                const uint32_t mf = mdry(mb) ? ((fu & ~ESC_NF_TRACKED) | (tr ? ESC_NF_TRACKED : 0u)) : fu;
+                const uint64_t kw = ((uint64_t)mg(mb) << R) | ak;
+                const uint32_t vw = (uint32_t)i | ((mf & 0xFu) << MEMB_FLAG_SHIFT);
+                if constexpr (ABL == 2 || ABL == 4) asm volatile("" :: "v"(kw), "v"(vw));
+                else {
+                    if (stage) { sk[pos] = kw; sv[pos] = vw; }
+                    else if (carry + pos < cap) { keys[carry + pos] = kw; vals[carry + pos] = vw; }
+                }
                 ++pos;
             });
         }
         __syncthreads();
-        if (threadIdx.x == 0) { uint32_t s = 0; for (int k = 0; k < SORT_WAVES; ++k) s += wsum[k]; carry += s; }
+        if (stage && ABL != 1 && ABL != 2 && ABL != 4)
+            for (uint32_t e = threadIdx.x; e < total && carry + e < cap; e += MEMB_BLOCK) {
+                keys[carry + e] = sk[e];
+                vals[carry + e] = sv[e];
+            }
+        carry += total;
         __syncthreads();
     }
-}
-
-// First sorted membership of every group s in [0, G] (key >> R = group).
-__global__ __launch_bounds__(256) void k_group_bounds(const uint64_t* __restrict__ keys, int64_t n, int R, int32_t G,
-                                                      int64_t* __restrict__ seg) {
-    const int32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s > G) return;
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((keys[mid] >> R) < (uint64_t)s) lo = mid + 1; else hi = mid;
-    }
-    seg[s] = lo;
-}
-
-// Sorted memberships into the groups' padded regions (streaming): position pstart[g] +
-// rank inside the group; node, group word (group | dry bit), flags.
-__global__ __launch_bounds__(256) void k_region_write(const uint64_t* __restrict__ keys, const uint64_t* __restrict__ vals,
-                                                      int64_t n, int R, GroupDev G, const int64_t* __restrict__ seg,
-                                                      const uint32_t* __restrict__ pstart, uint32_t* __restrict__ g_node,
-                                                      uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_flags) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
-    const uint32_t g = (uint32_t)(keys[e] >> R);
-    const uint64_t v = vals[e];
-    const int64_t d = (int64_t)pstart[g] + (e - seg[g]);
-    g_node[d] = (uint32_t)v;
-    g_grp[d] = g | (G.dry[g] ? NODE_DRY_BIT : 0u);
-    g_flags[d] = (uint32_t)(v >> 32);
 }
 
 // ---- per decision: inside every group's run, a stable 3-way split by filterNodes class
@@ -2755,38 +2919,50 @@ hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, h
 namespace {
 int rs_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, (n + 8191) / 8192)); }
 
-template <class KT, class VT, int BITS>
+template <class KT, class VT, int BITS, bool FINAL = false>
 hipError_t rs_pass(const KT* kin, const VT* vin, KT* kout, VT* vout, int64_t n, int shift, uint32_t* hist,
-                   uint32_t* tot, hipStream_t st) {
+                   uint32_t* tot, const RegionSink& S, hipStream_t st) {
     const int nblk = rs_blocks(n), nb = 1 << BITS;
     hipLaunchKernelGGL((k_rs_hist<KT, BITS>), dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, n, shift, hist);
     hipLaunchKernelGGL(k_rs_scan_rows, dim3((nb + 3) / 4), dim3(256), 0, st, hist, nblk, nb, tot);
     hipLaunchKernelGGL(k_rs_scan_tot, dim3(1), dim3(SORT_BLOCK), 0, st, tot, nb);
-    hipLaunchKernelGGL((k_rs_scatter<KT, VT, BITS>), dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, vin, kout, vout, n, shift,
-                       hist, tot);
+    hipLaunchKernelGGL((k_rs_scatter<KT, VT, BITS, FINAL>), dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, vin, kout, vout, n,
+                       shift, hist, tot, S);
     return hipGetLastError();
 }
 
 // LSD passes over bits [0, bits) of keys[0] / vals[0] (ping-pong with [1]); returns the
-// buffer index holding the result.  8-bit digits, the last pass narrower when it can be.
+// buffer index holding the result (the last pass writes the regions of S instead).
 // The bits are split evenly over ceil(bits / 8) passes (9 bits -> 5 + 4, 41 -> 7 x 5 + 6):
 // narrower digits cost the scatter fewer LDS histogram words per element at equal traffic.
 template <class KT, class VT>
 hipError_t rs_sort(KT* keys[2], VT* vals[2], int64_t n, int bits, uint32_t* hist, uint32_t* tot, int* src,
-                   hipStream_t st) {
+                   const RegionSink& S, hipStream_t st) {
     *src = 0;
+    // digits of at most 8 bits (9-bit digits were measured: the scatter's per-chunk digit
+    // bookkeeping grows with the bins, 5 passes of 8-9 bits took longer than 6 of 6-7)
     const int passes = (bits + 7) / 8;
     for (int p = 0, shift = 0; p < passes; ++p) {
         const int w = (bits - shift + (passes - p) - 1) / (passes - p);
         hipError_t e;
         KT *ki = keys[*src], *ko = keys[*src ^ 1];
         VT *vi = vals[*src], *vo = vals[*src ^ 1];
-        switch (w) {
-            case 1: case 2: case 3: case 4: e = rs_pass<KT, VT, 4>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
-            case 5: e = rs_pass<KT, VT, 5>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
-            case 6: e = rs_pass<KT, VT, 6>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
-            case 7: e = rs_pass<KT, VT, 7>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
-            default: e = rs_pass<KT, VT, 8>(ki, vi, ko, vo, n, shift, hist, tot, st); break;
+        if (p + 1 < passes) {
+            switch (w) {
+                case 1: case 2: case 3: case 4: e = rs_pass<KT, VT, 4>(ki, vi, ko, vo, n, shift, hist, tot, S, st); break;
+                case 5: e = rs_pass<KT, VT, 5>(ki, vi, ko, vo, n, shift, hist, tot, S, st); break;
+                case 6: e = rs_pass<KT, VT, 6>(ki, vi, ko, vo, n, shift, hist, tot, S, st); break;
+                case 7: e = rs_pass<KT, VT, 7>(ki, vi, ko, vo, n, shift, hist, tot, S, st); break;
+                default: e = rs_pass<KT, VT, 8>(ki, vi, ko, vo, n, shift, hist, tot, S, st); break;
+            }
+        } else {
+            switch (w) {
+                case 1: case 2: case 3: case 4: e = rs_pass<KT, VT, 4, true>(ki, vi, ko, vo, n, shift, hist, tot, S, st); break;
+                case 5: e = rs_pass<KT, VT, 5, true>(ki, vi, ko, vo, n, shift, hist, tot, S, st); break;
+                case 6: e = rs_pass<KT, VT, 6, true>(ki, vi, ko, vo, n, shift, hist, tot, S, st); break;
+                case 7: e = rs_pass<KT, VT, 7, true>(ki, vi, ko, vo, n, shift, hist, tot, S, st); break;
+                default: e = rs_pass<KT, VT, 8, true>(ki, vi, ko, vo, n, shift, hist, tot, S, st); break;
+            }
         }
         if (e != hipSuccess) return e;
         *src ^= 1;
@@ -2801,33 +2977,35 @@ size_t sort_hist_words(int64_t n) { return (size_t)256 * rs_blocks(n); }
 hipError_t launch_memb_count(const NodeDev& nd, const GroupDev& g, int nblk, uint32_t* cnt, uint32_t* total,
                              hipStream_t st) {
     const int64_t n = nd.hi - nd.lo;
-    hipLaunchKernelGGL(k_memb_count, dim3(nblk), dim3(SORT_BLOCK), 0, st, nd, g, n, cnt);
+    hipLaunchKernelGGL(k_memb_count, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, cnt);
     hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SORT_BLOCK), 0, st, cnt, nblk, total);
     return hipGetLastError();
 }
 
 hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const uint32_t* base, int64_t n_memb,
-                           int64_t ts_min, uint64_t div, int R, int gbits, uint64_t* keys[2], uint64_t* vals[2],
-                           uint32_t* hist, uint32_t* tot, int64_t* starts, int* src, hipStream_t st) {
-    *src = 0;
+                           int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, uint64_t* keys[2], uint32_t* vals[2],
+                           uint32_t* hist, uint32_t* tot, const RegionSink& S, hipStream_t st) {
     const int64_t n = nd.hi - nd.lo;
+#if MK_ABL
+    // timing ablations: LDS staging without the write-out (1), no stores and no group walk
+    // in the count (2), no division (3), no stores (4), no tracker lookups (5); those that
+    // store are overwritten by the real listing that follows
+    if (n > 0) {
+        hipLaunchKernelGGL(k_memb_keys<1>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0], vals[0]);
+        hipLaunchKernelGGL(k_memb_keys<2>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0], vals[0]);
+        hipLaunchKernelGGL(k_memb_keys<3>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0], vals[0]);
+        hipLaunchKernelGGL(k_memb_keys<4>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0], vals[0]);
+        hipLaunchKernelGGL(k_memb_keys<5>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0], vals[0]);
+    }
+#endif
     if (n > 0)
-        hipLaunchKernelGGL(k_memb_keys, dim3(nblk), dim3(SORT_BLOCK), 0, st, nd, g, n, base, ts_min, div, R, keys[0],
+        hipLaunchKernelGGL(k_memb_keys<0>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0],
                            vals[0]);
     if (n_memb > 0) {
-        const hipError_t e = rs_sort<uint64_t, uint64_t>(keys, vals, n_memb, R + gbits, hist, tot, src, st);
+        int src = 0;
+        const hipError_t e = rs_sort<uint64_t, uint32_t>(keys, vals, n_memb, R + gbits, hist, tot, &src, S, st);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(k_group_bounds, dim3((g.G + 1 + 255) / 256), dim3(256), 0, st, keys[*src], n_memb, R, g.G, starts);
-    return hipGetLastError();
-}
-
-hipError_t launch_region_write(const uint64_t* keys, const uint64_t* vals, int64_t n_memb, int R, const GroupDev& g,
-                               const int64_t* starts, const uint32_t* pstart, uint32_t* g_node, uint32_t* g_grp,
-                               uint32_t* g_flags, hipStream_t st) {
-    if (n_memb <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_region_write, dim3((unsigned)((n_memb + 255) / 256)), dim3(256), 0, st, keys, vals, n_memb, R, g,
-                       starts, pstart, g_node, g_grp, g_flags);
     return hipGetLastError();
 }
 

@@ -219,10 +219,10 @@ struct esc_ctx {
     bool pending = false;
     // K5 ordering: the age index (built at load) and the per-decision partition
     uint64_t* d_mkeys[2] = {nullptr, nullptr};               // index build: (group | creation offset)
-    uint64_t* d_mvals[2] = {nullptr, nullptr};               //              (node | flags << 32)
+    uint32_t* d_mvals[2] = {nullptr, nullptr};               //              (node | flags << 28)
     int64_t mcap = 0;                                         // their capacity (memberships)
     bool age_built = false;
-    uint32_t *d_hist = nullptr, *d_tot = nullptr, *d_cnt = nullptr, *d_total = nullptr;
+    uint32_t *d_hist = nullptr, *d_tot = nullptr, *d_cnt = nullptr, *d_total = nullptr, *d_ierr = nullptr;
     int64_t* d_seg = nullptr;
     int64_t n_memb = 0;
     int order_src = 0, memb_blocks = 0;
@@ -506,7 +506,7 @@ void release_sort(esc_ctx* c) {
     c->n_pchunks = 0;
     c->n_chunks = 0;
     c->n_gpad = 0;
-    dfree(c->d_hist); dfree(c->d_tot); dfree(c->d_cnt); dfree(c->d_total); dfree(c->d_seg);
+    dfree(c->d_hist); dfree(c->d_tot); dfree(c->d_cnt); dfree(c->d_total); dfree(c->d_ierr); dfree(c->d_seg);
     c->n_memb = 0;
     c->sorted = false;
 }
@@ -540,18 +540,36 @@ int32_t build_age_index(esc_ctx* c) {
         c->sort_div = div;
         c->sort_R = std::max(1, bit_width((uint64_t)(c->ts_max - c->ts_min) / div));
         if (c->sort_R + bit_width((uint64_t)std::max<int32_t>(g.G - 1, 1)) > 64) return ESC_E_LIMIT;
+        if (c->node_hi >= ((int64_t)1 << 28)) return ESC_E_LIMIT;   // node | flags << 28 sort values
         HIP_TRY(dalloc(&c->d_tot, 256));
         HIP_TRY(dalloc(&c->d_total, 1));
+        HIP_TRY(dalloc(&c->d_ierr, 1));
         HIP_TRY(dalloc(&c->d_seg, (size_t)4 * g.G + 1));
-        c->memb_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(2 * c->cu_count, (nl + 4095) / 4096));
+        // 512-thread listing blocks (48 KB LDS staging each): 3 per CU, >= 2048 nodes each
+        c->memb_blocks = (int)std::max<int64_t>(1, std::min<int64_t>(3 * c->cu_count, (nl + 2047) / 2048));
         HIP_TRY(dalloc(&c->d_cnt, c->memb_blocks));
         c->age_built = true;
     }
+    // Every group's membership count is the live entry count of its pair (the host's), so
+    // the total and the sorted groups' starts need no round trip; the device's own counts
+    // are compared with them on a fresh build (and on every build with ESC_CHECK_INDEX=1).
+    std::vector<int64_t> starts((size_t)g.G + 1, 0);
+    for (int32_t q = 0; q < g.G; ++q) {
+        const uint32_t gp = c->gi.gpair[q];
+        starts[q + 1] = starts[q] + ((gp >= c->q_lo && gp < c->q_hi) ? c->pair_live[gp] : 0);
+    }
+    if (starts[g.G] > (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
+    const uint32_t total = (uint32_t)starts[g.G];
+    static const bool check_env = std::getenv("ESC_CHECK_INDEX") && std::atoi(std::getenv("ESC_CHECK_INDEX")) != 0;
+    const bool check = fresh || check_env;
     // count (block bases) -> the memberships in snapshot order -> sort -> group starts
     HIP_TRY(launch_memb_count(n, g, c->memb_blocks, c->d_cnt, c->d_total, st));
-    uint32_t total = 0;
-    HIP_TRY(hipMemcpyAsync(&total, c->d_total, 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if (check) {
+        uint32_t dev_total = 0;
+        HIP_TRY(hipMemcpyAsync(&dev_total, c->d_total, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (dev_total != total) return fail_hip(hipErrorUnknown, "age index: membership total");
+    }
     c->n_memb = total;
     if ((int64_t)total > c->mcap || !c->d_hist) {
         for (int i = 0; i < 2; ++i) {
@@ -563,14 +581,6 @@ int32_t build_age_index(esc_ctx* c) {
         dfree(c->d_hist);
         HIP_TRY(dalloc(&c->d_hist, std::max(sort_hist_words(c->mcap), sort_hist_words(1) * 4)));
     }
-    const int gbits = bit_width((uint64_t)std::max<int32_t>(g.G - 1, 1));
-    int src = 0;
-    HIP_TRY(launch_age_sort(n, g, c->memb_blocks, c->d_cnt, c->n_memb, c->ts_min, c->sort_div, c->sort_R, gbits,
-                            c->d_mkeys, c->d_mvals, c->d_hist, c->d_tot, c->d_seg, &src, st));
-    std::vector<int64_t> starts((size_t)g.G + 1, 0);
-    HIP_TRY(hipMemcpyAsync(starts.data(), c->d_seg, starts.size() * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    starts[g.G] = c->n_memb;
     // every group's region: its memberships (oldest first), then padding to whole quads plus
     // the spare slots node additions take (esc_set_spare); the per-decision output uses the
     // same positions (grp_off = region starts)
@@ -584,7 +594,6 @@ int32_t build_age_index(esc_ctx* c) {
         const uint32_t gp = c->gi.gpair[q];
         const bool own = gp >= c->q_lo && gp < c->q_hi;
         const int64_t len = c->pair_live[gp];
-        if (starts[q + 1] - starts[q] != (own ? len : 0)) return fail_hip(hipErrorUnknown, "age index: membership count");
         const int64_t spare = c->spare_frac > 0 ? (int64_t)std::ceil((double)len * c->spare_frac) + 4 : 0;
         const int64_t cap = (len + spare + 3) & ~(int64_t)3;
         if (cap >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
@@ -652,11 +661,8 @@ int32_t build_age_index(esc_ctx* c) {
         HIP_TRY(dalloc(&c->d_cls4, (npad + 3) / 4)); HIP_TRY(dalloc(&c->d_ord, npad));
     }
     c->n_gpad = npad;
-    if (npad) {
-        HIP_TRY(hipMemsetAsync(c->d_g_node, 0, npad * 4, st));
-        HIP_TRY(hipMemsetAsync(c->d_g_grp, 0xFF, npad * 4, st));
-        HIP_TRY(hipMemsetAsync(c->d_g_flags, 0, npad * 4, st));
-    }
+    // no clearing: the sort's last pass fills every group's [start, start + len), k_region_pad the
+    // rest of its region
     if (fresh || (int64_t)chunks.size() != c->n_chunks || (int64_t)pchunks.size() != c->n_pchunks) {
         dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks);
         dfree(c->d_pstart); dfree(c->d_plen); dfree(c->d_pchunks);
@@ -686,10 +692,22 @@ int32_t build_age_index(esc_ctx* c) {
     if (!chunks.empty()) HIP_TRY(hipMemcpy(c->d_chunks, chunks.data(), chunks.size() * sizeof(OrdChunk), hipMemcpyHostToDevice));
     if (!pchunks.empty())
         HIP_TRY(hipMemcpy(c->d_pchunks, pchunks.data(), pchunks.size() * sizeof(OrdChunk), hipMemcpyHostToDevice));
-    HIP_TRY(launch_region_write(c->d_mkeys[src], c->d_mvals[src], c->n_memb, c->sort_R, g, c->d_seg, c->d_pstart,
-                                c->d_g_node, c->d_g_grp, c->d_g_flags, st));
+    // the listing and the sort; its last pass writes the regions at the host's sorted starts
+    HIP_TRY(hipMemcpyAsync(c->d_seg, starts.data(), starts.size() * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(c->d_ierr, 0, 4, st));
+    const int gbits = bit_width((uint64_t)std::max<int32_t>(g.G - 1, 1));
+    RegionSink sink{c->d_seg, c->d_pstart, c->d_plen, c->d_dry, c->d_g_node, c->d_g_grp, c->d_g_flags, c->d_ierr,
+                    g.G, c->sort_R};
+    HIP_TRY(launch_age_sort(n, g, c->memb_blocks, c->d_cnt, c->n_memb, c->mcap, c->ts_min, c->sort_div, c->sort_R,
+                            gbits, c->d_mkeys, c->d_mvals, c->d_hist, c->d_tot, sink, st));
     HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_grp, c->d_g_node, c->d_g_flags, st));
-    {   // after k_region_write, which reads d_seg as the groups' unpadded starts
+    if (check) {
+        uint32_t err = 0;
+        HIP_TRY(hipMemcpyAsync(&err, c->d_ierr, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (err) return fail_hip(hipErrorUnknown, "age index: membership count");
+    }
+    {   // after the sort's last pass, which reads d_seg as the groups' unpadded starts
         std::vector<int64_t> seg0((size_t)4 * g.G + 1);
         for (int32_t q = 0; q < g.G; ++q)
             for (int k = 0; k < 4; ++k) seg0[4 * (size_t)q + k] = pstart[q];

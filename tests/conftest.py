@@ -7,6 +7,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
+# the age-index build compares the device's membership counts with the host's on every build
+os.environ.setdefault("ESC_CHECK_INDEX", "1")
 
 
 def pytest_configure(config):
