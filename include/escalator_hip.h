@@ -538,7 +538,11 @@ int32_t esc_removal_nodes(esc_ctx* ctx, int32_t group, int64_t* idx_out, int64_t
  * esc_sort_nodes (async, per decision) classifies every membership (filterNodes,
  * controller.go:120-154) and stable-partitions by (group, class); a group's untainted
  * segment is then oldest-first and its tainted one, read backwards, newest-first.
- * esc_build_age_index rebuilds the index (snapshot ingestion; exposed for measurement). */
+ * esc_build_age_index rebuilds the index (snapshot ingestion; exposed for measurement).
+ * The index carries node indices in 28 bits: a node table of 2^28 slots or more returns
+ * ESC_E_LIMIT.  Its group starts come from the host's live entry counts; the device's own
+ * counts are checked against them on a fresh build (every build with ESC_CHECK_INDEX=1),
+ * a mismatch returning ESC_E_HIP.                                                       */
 int32_t esc_sort_nodes(esc_ctx* ctx);
 /* Include the per-decision ordering in every decision (esc_run / esc_reduce / esc_step):
  * the packed small groups are ordered by blocks of the step's fused tail launch (after K1,
