@@ -65,6 +65,20 @@ def main():
     for _ in range(args.steps):
         res = ctx.try_remove(now_ns, soft, hard)
     call_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    # the same call through the C ABI with the argument and result arrays made once (what a
+    # cgo caller does): the Python wrapper's share of call_ms is the difference
+    import ctypes as C
+    from escalator_amd import _lib as L
+    s_arr = np.full(G, soft, np.int64)
+    h_arr = np.full(G, hard, np.int64)
+    o_arr = np.empty(G, esc.context.REMOVAL_DTYPE)
+    ps, ph = s_arr.ctypes.data_as(C.POINTER(C.c_int64)), h_arr.ctypes.data_as(C.POINTER(C.c_int64))
+    po = o_arr.ctypes.data_as(C.POINTER(L.Removal))
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        L.check(ctx.lib.esc_try_remove(ctx.handle, int(now_ns), ps, ph, po), "esc_try_remove")
+    abi_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    assert np.array_equal(o_arr, res)
 
     # pod rescheduling events (esc_pods_bind) keep the occupancy words current: time a
     # batch, then one call again (its result is the one checked below)
@@ -113,6 +127,7 @@ def main():
         "value": G / (call_ms * 1e-3),
         "unit": "groups/s",
         "ms_per_call": call_ms,
+        "ms_per_call_abi": abi_ms,          # the same call with arrays made once (C-ABI caller)
         "steps": args.steps,
         "data": "synthetic (esc_synth.cpp config 4 + random pod bindings / taint times)",
         "config": {"workload": "config4: 100M pods / 1M nodes / 10k groups", "pods": P, "nodes": N,
