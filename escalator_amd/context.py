@@ -443,7 +443,7 @@ class Context:
         """TryRemoveTaintedNodes for every group: (n_candidates, n_delete, pods_remaining)."""
         s_ = np.ascontiguousarray(np.broadcast_to(np.asarray(soft_ns, np.int64), (self.G,)))
         h_ = np.ascontiguousarray(np.broadcast_to(np.asarray(hard_ns, np.int64), (self.G,)))
-        out = np.zeros(self.G, REMOVAL_DTYPE)
+        out = np.empty(self.G, REMOVAL_DTYPE)          # every record is written
         L.check(self.lib.esc_try_remove(self.handle, int(now_ns), s_.ctypes.data_as(C.POINTER(C.c_int64)),
                                         h_.ctypes.data_as(C.POINTER(C.c_int64)),
                                         out.ctypes.data_as(C.POINTER(L.Removal))), "esc_try_remove")

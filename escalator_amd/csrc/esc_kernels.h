@@ -469,6 +469,11 @@ struct PodRef {
     uint32_t flags, pair0, p[3];
 };
 constexpr uint32_t POD_REF_INDIRECT = 1u << 31;
+// K7's per-group record on the device (esc_removal widened on the host)
+struct RmRec {
+    uint32_t n_candidates, n_delete;
+    int64_t pods_remaining;
+};
 struct RemovalDev {
     const int64_t* taint_s;    // [n_nodes] escalator-taint time (INT64_MIN: none / unparsable)
     const uint8_t* no_delete;  // [n_nodes]
@@ -484,7 +489,7 @@ struct RemovalDev {
     const int64_t* hard_ns;    // [G]
     const uint32_t* rm_off;    // [G] offset of each group's deletable-node list
     uint32_t* rm_list;
-    esc_removal* out;          // [G]
+    RmRec* out;                // [G]
     int64_t now_ns;
 };
 hipError_t launch_podref_fill(const PodDev& p, const uint32_t* run_slot, const uint32_t* run_pos, int64_t n, PodRef* refs,

@@ -2769,43 +2769,45 @@ __global__ __launch_bounds__(256) void k_occ_delta(GroupDev G, RemovalDev R, con
         if (dflt) atomicAdd(R.occ_def + e, d);
     }
 }
+// One wave per group over its pair's entries (pair-major, e_flags / e_node / the occupancy
+// word contiguous), the next 64 entries' loads in flight while this chunk's nodes' taint
+// times are read: one dependent load per chunk instead of two.  The record goes back
+// compact (RmRec, 16 B; the host widens it to esc_removal).
 __global__ __launch_bounds__(64) void k_try_remove(NodeDev N, GroupDev G, RemovalDev R) {
     const int32_t g = blockIdx.x;
     const int lane = threadIdx.x;
     const uint32_t q = G.gpair[g];
     const bool dry = G.dry[g] != 0, dflt = (uint32_t)g == G.default_group;
+    const uint32_t* __restrict__ occw = dflt ? R.occ_def : R.occ_pair;
     const int64_t e0 = N.piece_off[N.pp_off[q]], e1 = N.piece_off[N.pp_off[q + 1]];
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    int64_t cand = 0, del = 0, pods = 0;
+    const uint32_t m = (uint32_t)g | (dry ? NODE_DRY_BIT : 0u);
+    const int64_t soft = R.soft_ns[g], hard = R.hard_ns[g];
+    uint32_t cand = 0, del = 0;
+    int64_t pods = 0;
+    uint32_t f = ESC_NF_ABSENT, j = 0, o = 0;
+    if (e0 + lane < e1) { f = N.e_flags[e0 + lane]; j = N.e_node[e0 + lane]; o = occw[e0 + lane]; }
     for (int64_t b = e0; b < e1; b += 64) {
-        const int64_t e = b + lane;
-        bool c = false, d = false;
-        uint32_t occ = 0, j = 0;
-        if (e < e1) {
-            const uint32_t f = N.e_flags[e];
-            j = N.e_node[e];
-            const uint32_t m = (uint32_t)g | (dry ? NODE_DRY_BIT : 0u);
-            c = node_class(N, f, (int64_t)j, m) == 1;                     // filterNodes: tainted
-            if (c && !dry && !R.no_delete[j] && R.taint_s[j] != INT64_MIN) {
-                const int64_t age = go_sub_ns(R.now_ns, R.taint_s[j]);
-                occ = dflt ? R.occ_def[e] : R.occ_pair[e];
-                d = age > R.soft_ns[g] && (occ == 0 || age > R.hard_ns[g]);
+        const int64_t en = b + 64 + lane;
+        uint32_t nf = ESC_NF_ABSENT, nj = 0, no = 0;
+        if (en < e1) { nf = N.e_flags[en]; nj = N.e_node[en]; no = occw[en]; }
+        const bool c = node_class(N, f, (int64_t)j, m) == 1;          // filterNodes: tainted (absent: 3)
+        bool d = false;
+        if (c && !dry) {
+            const int64_t ts = R.taint_s[j];
+            if (!R.no_delete[j] && ts != INT64_MIN) {
+                const int64_t age = go_sub_ns(R.now_ns, ts);
+                d = age > soft && (o == 0 || age > hard);
             }
         }
         const unsigned long long md = __ballot(d);
         if (d) R.rm_list[R.rm_off[g] + del + __popcll(md & lt)] = j;
-        del += __popcll(md);
-        cand += __popcll(__ballot(c));
-        pods += (int64_t)wave_total64(d ? (unsigned long long)occ : 0ull);
+        del += (uint32_t)__popcll(md);
+        cand += (uint32_t)__popcll(__ballot(c));
+        pods += (int64_t)wave_total64(d ? (unsigned long long)o : 0ull);
+        f = nf; j = nj; o = no;
     }
-    if (lane == 0) {
-        esc_removal o;
-        o.n_candidates = cand;
-        o.n_delete = del;
-        o.pods_remaining = pods;
-        o.reserved = 0;
-        R.out[g] = o;
-    }
+    if (lane == 0) R.out[g] = RmRec{cand, del, pods};
 }
 
 // ===================================================================== launchers

@@ -307,9 +307,9 @@ struct esc_ctx {
     std::vector<int64_t> h_pod_rpos;
     int64_t *d_taint_s = nullptr, *d_soft = nullptr, *d_hard = nullptr;
     uint8_t* d_no_delete = nullptr;
-    esc_removal* d_rm_out = nullptr;
+    RmRec* d_rm_out = nullptr;
     std::vector<uint32_t> h_rm_off;                           // [G + 1]
-    esc_removal* h_rm = nullptr;                              // K7 results (pinned copy)
+    RmRec* h_rm = nullptr;                                    // K7 results (pinned copy)
     std::vector<int64_t> h_soft, h_hard;                      // grace periods last uploaded
     bool rm_valid = false;                                    // esc_try_remove results current
     int64_t rm_nodes = -1;                                    // node count the reaping buffers are sized for
@@ -3365,7 +3365,7 @@ int32_t esc_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* 
         HIP_TRY(dalloc(&c->d_rm_list, std::max<uint32_t>(c->h_rm_off[G], 1)));
         HIP_TRY(hipMemcpy(c->d_rm_off, c->h_rm_off.data(), (size_t)G * 4, hipMemcpyHostToDevice));
         if (c->h_rm) { hipHostFree(c->h_rm); c->h_rm = nullptr; }
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_rm), (size_t)std::max<int32_t>(G, 1) * sizeof(esc_removal)));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_rm), (size_t)std::max<int32_t>(G, 1) * sizeof(RmRec)));
         c->h_soft.clear();
         c->h_hard.clear();
         c->rm_nodes = NC;
@@ -3499,9 +3499,15 @@ int32_t esc_reap_finish(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, cons
     // K7's per-group records come back by one DMA copy into pinned memory (one 32-B
     // record per group is too small a write for zero-copy over PCIe)
     HIP_TRY(launch_try_remove(node_dev(c), group_dev(c), removal_dev(c, now_ns), c->stream));
-    HIP_TRY(hipMemcpyAsync(c->h_rm, c->d_rm_out, (size_t)G * sizeof(esc_removal), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_rm, c->d_rm_out, (size_t)G * sizeof(RmRec), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    std::memcpy(out, c->h_rm, (size_t)G * sizeof(esc_removal));
+    for (int32_t g = 0; g < G; ++g) {
+        const RmRec& s = c->h_rm[g];
+        out[g].n_candidates = s.n_candidates;
+        out[g].n_delete = s.n_delete;
+        out[g].pods_remaining = s.pods_remaining;
+        out[g].reserved = 0;
+    }
     c->rm_valid = true;
     return ESC_OK;
 }
