@@ -21,6 +21,9 @@ cat $OUT/bench.json
 timeout -k 10 240 python bench.py --pods 12500000 --steps 50 --warmup 10 --no-cpu-baseline --no-parity \
     > $OUT/bench_p12.5M.json 2> $OUT/bench_p12.5M.err || { tail $OUT/bench_p12.5M.err; exit 1; }
 cat $OUT/bench_p12.5M.json
+timeout -k 10 300 python bench.py --shard-of 8 --steps 50 --warmup 10 --no-cpu-baseline \
+    > $OUT/bench_shard8.json 2> $OUT/bench_shard8.err || { tail $OUT/bench_shard8.err; exit 1; }
+cut -c1-600 $OUT/bench_shard8.json
 echo "[job] $(date) config 5"
 timeout -k 10 300 python -u bench.py --config 5 --steps 20 --warmup 3 > $OUT/bench5.json 2> $OUT/bench5.err || { tail $OUT/bench5.err; exit 1; }
 cat $OUT/bench5.json
