@@ -519,7 +519,10 @@ struct OrdChunk {               // K5 per-decision chunk: memberships [start, en
     uint32_t start, end, group, pad;
 };
 constexpr uint32_t ORD_CHUNK_DRY = 2u;   // OrdChunk::pad bit of a split chunk: its group is in dry mode
-constexpr int ORD_CHUNK = 4096;   // memberships per K5 chunk (three-pass default)
+#ifndef ESC_ORD_CHUNK
+#define ESC_ORD_CHUNK 4096         // (timing builds may override)
+#endif
+constexpr int ORD_CHUNK = ESC_ORD_CHUNK;   // memberships per K5 chunk (three-pass default)
 // Group-order padding slot of group g: g | MEMB_PAD (class 3, skipped).  Every group owns a
 // region of the group-order arrays: its memberships oldest first, then padding (the round-up
 // to whole 16-B quads and the spare slots node additions take).

@@ -10,5 +10,10 @@ HIPCC=/opt/rocm/bin/hipcc
 FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Wall -Wno-unused-function -Wno-unused-value -Wno-unused-result -I../../include -I."
 $HIPCC $FL "$@" -DESC_PART=0 -c esc_kernels.hip -o $B/esc_kernels.o
 O=../../build/csrc
-$HIPCC --offload-arch=gfx950 -shared -fPIC -o ../libescalator_hip_$NAME.so $B/esc_kernels.o $O/esc_runtime.o \
+RT=$O/esc_runtime.o
+if [ -n "$REBUILD_RT" ]; then            # flags that change the runtime's view too (e.g. -DESC_ORD_CHUNK)
+    $HIPCC $FL "$@" -c esc_runtime.hip -o $B/esc_runtime.o
+    RT=$B/esc_runtime.o
+fi
+$HIPCC --offload-arch=gfx950 -shared -fPIC -o ../libescalator_hip_$NAME.so $B/esc_kernels.o $RT \
     $O/esc_multi.o $O/esc_kernels_p1.o $O/esc_pack.o $O/esc_synth.o -pthread
