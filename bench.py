@@ -140,12 +140,54 @@ def cpu_baseline(cfg, G, full=None, seconds=12.0):
     return out
 
 
-def init_dist():
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def worker_command(argv: list[str], n: int, port: int) -> list[str]:
+    """The launch of `n` ranks of this script (one process per GPU, RANK / WORLD_SIZE /
+    LOCAL_RANK / MASTER_* in their env), the shape the driver uses for its N > 1 runs."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def needs_launch(gpus: int, single_process: bool, env=None) -> bool:
+    """`--gpus N` (N > 1) run without a launcher: this process must start the N ranks itself
+    (the one-process-per-GPU shape), unless --single-process drives the devices from here."""
+    env = os.environ if env is None else env
+    return gpus > 1 and not single_process and "WORLD_SIZE" not in env
+
+
+def launch_workers(argv: list[str], n: int) -> int:
+    """Start the N ranks as child processes (nothing in this process has touched the GPU:
+    torch is not imported yet) and return their launcher's exit code."""
+    import subprocess
+    cmd = worker_command(argv, n, _free_port())
+    log("bench: --gpus %d without a launcher: starting %d ranks (%s)" % (n, n, " ".join(cmd[1:8])))
+    return subprocess.call(cmd)
+
+
+def check_world(gpus: int, world: int, single_process: bool) -> None:
+    """Fail loudly when the ranks running do not match --gpus (a run would otherwise print
+    another N's numbers under this N)."""
+    if single_process:
+        return
+    if world != gpus:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d ranks are running" % (gpus, world))
+
+
+def init_dist(gpus: int = 1):
     """RANK / WORLD_SIZE / LOCAL_RANK from the launcher; one process per GPU over RCCL.
     ESC_BENCH_BACKEND / ESC_BENCH_DEVICE: rehearsal knobs (gloo, every rank on one device)
     for exercising the N > 1 path on a one-GPU box; the driver's runs use the defaults."""
     import torch
     rank, world, local = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1), ("LOCAL_RANK", 0)))
+    check_world(gpus, world, False)
     backend = os.environ.get("ESC_BENCH_BACKEND", "nccl")
     local = int(os.environ.get("ESC_BENCH_DEVICE", local))
     torch.cuda.set_device(local)
@@ -174,7 +216,7 @@ def bench_order(args):
     import escalator_amd as esc
     from escalator_amd.dist import gather_orders, shard_range
     from oracle import soa
-    rank, world, local, dist, backend = init_dist()
+    rank, world, local, dist, backend = init_dist(args.gpus)
     N, G, P = 10_000_000, 100, 100_000
     lo, hi = shard_range(P, rank, world)
     s = esc.Synth(P, N, G, config=5, seed=0xE5CA1A7E00000005, p_lo=lo, p_hi=hi, threads=16)
@@ -233,6 +275,8 @@ def bench_order(args):
     if rank != 0:
         dist.destroy_process_group()
         return
+    if world != args.gpus:
+        raise SystemExit("bench: n_gpus %d != --gpus %d" % (world, args.gpus))
     # algorithmic bytes per membership: read node, group, flags (12 B), write the node (4 B;
     # an upper bound — cordoned nodes feed neither order).  The two-pass default moves 14 B
     # (classify: flags 4 read, a class byte written; split: the class byte and the node
@@ -281,11 +325,14 @@ def bench_order(args):
 def host_side(esc, ctx_dev):
     """BASELINE.md §2's host-side figures: the K0 packer over object structs (esc_synth_objects:
     what the cgo shim fills from *v1.Pod / *v1.Node) of BASELINE config #2, in objects/s on
-    one host thread; and one per-call drop-in esc_pods_requests_total (pkg/k8s/util.go:27:
-    pack + upload + reduce + results on the GPU) over 1000 of those pods (config #1's size)."""
+    one host thread; and the per-call drop-in esc_pods_requests_total (pkg/k8s/util.go:27:
+    the slice's records into reused pinned buffers, one kernel reading them zero-copy, the
+    exact sums back) over config #1's 1000 pod objects, beside the single-thread C oracle
+    (orc_totals) over the same pods' SoA."""
     import ctypes as C
     import numpy as np
     from escalator_amd import _lib as L
+    from oracle import soa
     s = esc.Synth(1_000_000, 10_000, 100, config=2, seed=0xE5CA1A7E00000002, threads=16)
     po, n, no, nn = s.objects()
     host = esc.Context(s.groups, device=-1)
@@ -295,20 +342,56 @@ def host_side(esc, ctx_dev):
         host.pack_objects(po, n, no, nn)
         times.append(time.perf_counter() - t0)
     t_pack = float(np.median(times))
+    c1 = esc.Synth(1000, 50, 1, config=1, seed=0xE5CA1A7E00000001)
+    pa, na, o1, m1 = c1.objects()
+    # what scaleNodeGroup hands CalculatePodsRequestsTotal: the group's filtered pods
+    # (controller.go:194, :262): not a daemonset, and the group's pair among the pod's pairs
+    sp = c1.pods()
+    f = sp["flags"].astype(np.int64)
+    nxp = (f >> 24) & 0x3F
+    xo = np.concatenate([[0], np.cumsum(nxp)])
+    sel = [i for i in range(na) if not (f[i] & 1) and (sp["pair0"][i] == 0 or
+                                                       0 in sp["xp_pair"][xo[i]:xo[i + 1]])]
+    p1 = (L.PodObj * max(len(sel), 1))()
+    for j, i in enumerate(sel):
+        p1[j] = pa[i]
+    n1 = len(sel)
     mem, cpu = C.c_int64(), C.c_int64()
     lib = ctx_dev.lib
-    L.check(lib.esc_pods_requests_total(ctx_dev.handle, po, 1000, C.byref(mem), C.byref(cpu)))   # warm
+    L.check(lib.esc_pods_requests_total(ctx_dev.handle, p1, n1, C.byref(mem), C.byref(cpu)))   # warm
     calls = []
-    for _ in range(20):
+    for _ in range(200):
         t0 = time.perf_counter()
-        L.check(lib.esc_pods_requests_total(ctx_dev.handle, po, 1000, C.byref(mem), C.byref(cpu)))
+        L.check(lib.esc_pods_requests_total(ctx_dev.handle, p1, n1, C.byref(mem), C.byref(cpu)))
         calls.append(time.perf_counter() - t0)
+    ncalls = []
+    for _ in range(200):
+        t0 = time.perf_counter()
+        L.check(lib.esc_nodes_capacity_total(ctx_dev.handle, o1, m1, C.byref(mem), C.byref(cpu)))
+        ncalls.append(time.perf_counter() - t0)
+    fn = soa.totals_fn(c1.pods(), c1.nodes(), c1.groups)
+    fn()
+    reps, t0 = 2000, time.perf_counter()
+    for _ in range(reps):
+        fn()
+    t_orc = (time.perf_counter() - t0) / reps
+    want = fn()[0]
+    L.check(lib.esc_pods_requests_total(ctx_dev.handle, p1, n1, C.byref(mem), C.byref(cpu)))
+    assert int(want[2]) == n1, "config #1 filter restatement"
     return {"packer_objects_per_s": (n + nn) / t_pack,
             "packer_sample": "esc_packer_add_pods + _add_nodes + _view over config #2's %d pod and %d node "
                              "objects (esc_synth_objects), one host thread, median of 3: %.3f s" % (n, nn, t_pack),
             "dropin_pods_requests_total_ms": float(np.median(calls)) * 1e3,
-            "dropin_sample": "esc_pods_requests_total over 1000 pod objects per call (pack, upload, K1, "
-                             "results), median of 20 calls"}
+            "dropin_pods_requests_total_p90_ms": float(np.percentile(calls, 90)) * 1e3,
+            "dropin_nodes_capacity_total_ms": float(np.median(ncalls)) * 1e3,
+            "dropin_oracle_1thread_ms": t_orc * 1e3,
+            "dropin_parity": bool(cpu.value == want[0] and mem.value == want[1]),
+            "dropin_sample": "config #1 (1000 pods, 50 nodes, 1 group): esc_pods_requests_total over the group's "
+                             "%d filtered pod objects (what scaleNodeGroup passes, controller.go:262) / "
+                             "esc_nodes_capacity_total over the 50 nodes per call (records into reused "
+                             "pinned buffers, one k_list_sum launch reading them zero-copy, sums back), median of "
+                             "200 calls; oracle: orc_totals over the same pods' SoA on one thread (every group's "
+                             "totals, arguments marshalled once), mean of %d calls" % (n1, reps)}
 
 
 def upload_ms(s, device):
@@ -355,8 +438,18 @@ def main():
                          "the Go host's drop-in shape; ESC_BENCH_DEVICES=0,0 rehearses it on one GPU)")
     ap.add_argument("--no-order", action="store_true",
                     help="leave the K5 ordering out of the decision (ablation; BASELINE.md §2 includes it)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="print this rank's RANK / WORLD_SIZE and exit before any GPU call (tests the launch)")
     args = ap.parse_args()
 
+    if needs_launch(args.gpus, args.single_process):
+        return launch_workers(sys.argv[1:], args.gpus)
+    if args.launch_check:
+        rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+        check_world(args.gpus, world, args.single_process)
+        print(json.dumps({"rank": rank, "world": world, "local_rank": int(os.environ.get("LOCAL_RANK", 0))}),
+              flush=True)
+        return 0
     if args.config == 5:
         return bench_order(args)
     cfg = dict(CONFIGS[args.config], cfg=args.config)
@@ -377,7 +470,7 @@ def main():
         rank, world, local, dist, backend = 0, 1, multi[0], None, "multi"
         torch.cuda.set_device(local)
     else:
-        rank, world, local, dist, backend = init_dist()
+        rank, world, local, dist, backend = init_dist(args.gpus)
     n_gpus = len(multi) if multi else world
 
     lo, hi = shard_range(P, rank, world)
@@ -568,10 +661,12 @@ def main():
         out["host_side"] = host_side(esc, ctx)
     if world == 1 and shard_world == 1 and not multi and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, G, full=s)
+    if n_gpus != args.gpus or (rccl_ranks is not None and rccl_ranks != args.gpus):
+        raise SystemExit("bench: n_gpus %d / rccl_ranks %s != --gpus %d" % (n_gpus, rccl_ranks, args.gpus))
     print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -61,4 +61,14 @@ struct HostSnapshot {
     void view(esc_pod_soa* p, esc_node_soa* n) const;
 };
 
+// Per-call drop-ins over object slices (esc_list.hip): reusable pinned buffers and one
+// small kernel per call, no snapshot layout (esc_pods_requests_total, util.go:27;
+// esc_nodes_capacity_total, util.go:41).  stream: the context's hipStream_t.
+struct ListReducer;
+int32_t list_pods_requests_total(ListReducer*& r, int device, void* stream, const esc_pod_obj* pods, int64_t n,
+                                 int64_t* mem_b, int64_t* cpu_m);
+int32_t list_nodes_capacity_total(ListReducer*& r, int device, void* stream, const esc_node_obj* nodes, int64_t n,
+                                  int64_t* mem_b, int64_t* cpu_m);
+void list_reducer_free(ListReducer*& r);
+
 }  // namespace esc

@@ -258,8 +258,10 @@ struct esc_ctx {
     std::vector<uint32_t> pair_lo;                            // group pair -> its first entry
     uint32_t nodes_piece_lo(uint32_t q) const { return pair_lo[q]; }
     std::vector<uint32_t> h_gn;                               // group regions' nodes (lazy mirror of d_g_node)
-    // per-function drop-ins run on a one-group list context
+    // per-function drop-ins: the list reducer (esc_list.hip); esc_order_by_creation runs
+    // on a one-group list context
     esc_ctx* list_ctx = nullptr;
+    esc::ListReducer* lred = nullptr;
     // single-process multi-device context (esc_ctx_create_multi): every call dispatches to
     // its per-device contexts (esc_multi.hip); null for a per-device context
     esc::esc_multi_state* multi = nullptr;
@@ -1240,6 +1242,7 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
     if (!c) return ESC_OK;
     if (c->multi) esc::multi_destroy(c);                    // the devices' contexts and communicators
     if (c->list_ctx) esc_ctx_destroy(c->list_ctx);
+    list_reducer_free(c->lred);
     if (c->has_device) {
         hipSetDevice(c->device);
         if (c->stream) hipStreamSynchronize(c->stream);
@@ -2816,6 +2819,15 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->rm_valid = false;
+    // A bound pod keeps its node and its run position; its occupancy contribution is taken
+    // out while the device still holds its OLD record: a PodRef with more than 3 extra pairs
+    // reads them through the pod's xp offset, which the patches below rewrite (or hand to
+    // another pod of this batch).  The same order as esc_pods_delete.
+    std::vector<uint32_t> bpos, bnode;
+    if (c->placed) {
+        bound_of(c, ids, n, bpos, bnode);
+        if (int32_t r2 = occ_delta(c, bpos, bnode, -1)) return r2;
+    }
     Patches P;
     bool touch_grew = false;
     for (int64_t i = 0; i < n; ++i) {
@@ -2859,11 +2871,7 @@ int32_t upsert_apply(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, const
     int32_t rc = apply_patches(c, P, pod_targets(c));
     if (!rc && touch_grew) rc = touch_upload(c);
     if (rc || !c->placed) return rc;
-    // a bound pod keeps its node; its PodRef follows the new record (and slot), and its
-    // occupancy contribution with it
-    std::vector<uint32_t> bpos, bnode;
-    bound_of(c, ids, n, bpos, bnode);
-    if (int32_t r2 = occ_delta(c, bpos, bnode, -1)) return r2;
+    // its PodRef follows the new record (and slot), and the occupancy with it
     std::vector<int64_t> touched(ids, ids + n);
     std::vector<uint32_t> runs;
     if (int32_t r2 = sync_placement(c, touched, runs)) return r2;
@@ -3661,57 +3669,20 @@ int32_t list_context(esc_ctx* c, esc_ctx** out) {
     return ESC_OK;
 }
 
-int32_t run_list(esc_ctx* L, const esc_pod_obj* pods, int64_t np, const esc_node_obj* nodes, int64_t nn,
-                 esc_group_totals* t) {
-    esc_packer* pk = nullptr;
-    int32_t rc = esc_packer_create(L, &pk);
-    if (rc) return rc;
-    esc_packer_set_list_mode(pk, 1);
-    rc = esc_packer_add_pods(pk, pods, np);
-    if (!rc) rc = esc_packer_add_nodes(pk, nodes, nn);
-    esc_pod_soa ps;
-    esc_node_soa ns;
-    if (!rc) rc = esc_packer_view(pk, &ps, &ns);
-    if (!rc) rc = esc_load_pods(L, &ps, 0);
-    if (!rc) rc = esc_load_nodes(L, &ns, 0, ns.n_nodes);
-    esc_packer_destroy(pk);
-    if (!rc) rc = esc_run(L);
-    if (!rc) rc = esc_results(L, t, nullptr);
-    return rc;
-}
-
 }  // namespace
 
 int32_t esc_pods_requests_total(esc_ctx* c, const esc_pod_obj* pods, int64_t n, int64_t* mem_b, int64_t* cpu_m) {
     if (c && c->multi) return esc_pods_requests_total(esc::multi_sub(c, 0), pods, n, mem_b, cpu_m);
     if (!c || n < 0 || (n > 0 && !pods) || !mem_b || !cpu_m) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
-    esc_ctx* L = nullptr;
-    int32_t rc = list_context(c, &L);
-    if (rc) return rc;
-    esc_group_totals t;
-    rc = run_list(L, pods, n, nullptr, 0, &t);
-    if (rc) return rc;
-    if (t.flags & ESC_TF_POD_OVERFLOW) return ESC_E_LIMIT;
-    *mem_b = t.pod_mem_b;
-    *cpu_m = t.pod_cpu_m;
-    return ESC_OK;
+    return list_pods_requests_total(c->lred, c->device, c->stream, pods, n, mem_b, cpu_m);
 }
 
 int32_t esc_nodes_capacity_total(esc_ctx* c, const esc_node_obj* nodes, int64_t n, int64_t* mem_b, int64_t* cpu_m) {
     if (c && c->multi) return esc_nodes_capacity_total(esc::multi_sub(c, 0), nodes, n, mem_b, cpu_m);
     if (!c || n < 0 || (n > 0 && !nodes) || !mem_b || !cpu_m) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
-    esc_ctx* L = nullptr;
-    int32_t rc = list_context(c, &L);
-    if (rc) return rc;
-    esc_group_totals t;
-    rc = run_list(L, nullptr, 0, nodes, n, &t);
-    if (rc) return rc;
-    if (t.flags & ESC_TF_NODE_OVERFLOW) return ESC_E_LIMIT;
-    *mem_b = t.node_mem_b;
-    *cpu_m = t.node_cpu_m;
-    return ESC_OK;
+    return list_nodes_capacity_total(c->lred, c->device, c->stream, nodes, n, mem_b, cpu_m);
 }
 
 int32_t esc_order_by_creation(esc_ctx* c, const int64_t* created_ns, int64_t n, int32_t oldest, int64_t n_take,

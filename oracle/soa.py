@@ -108,6 +108,31 @@ def totals(pods: dict, nodes: dict, groups: list[dict], node_lo: int = 0, node_h
     return out
 
 
+def totals_fn(pods: dict, nodes: dict, groups: list[dict]):
+    """A zero-argument callable running orc_totals (one thread) over the snapshot, its
+    arguments marshalled once: the per-call CPU time of the oracle for bench.py's
+    cpu_baseline figures (ctypes call overhead included, ~1 us)."""
+    t = group_tables(groups)
+    G = t["G"]
+    out = np.zeros((G, 13), np.int64)
+    arrs = {k: np.ascontiguousarray(v) for k, v in list(pods.items())}
+    narrs = {k: np.ascontiguousarray(v) for k, v in list(nodes.items())}
+    args = [C.c_int64(len(arrs["flags"])), _p(arrs["flags"], C.c_uint32), _p(arrs["cpu0"], C.c_uint32),
+            _p(arrs["mem0"], C.c_int64), _p(arrs["pair0"], C.c_uint32), _p(arrs["xc_cpu"], C.c_int64),
+            _p(arrs["xc_mem"], C.c_int64), _p(arrs["xp_pair"], C.c_uint32)]
+    args += _node_args(narrs) + [_p(narrs["xl_pair"], C.c_uint32), _p(narrs["trk_node"], C.c_int32),
+                                 _p(narrs["trk_group"], C.c_int32), C.c_int64(len(narrs["trk_node"]))]
+    args += [C.c_int64(0), C.c_int64(len(narrs["flags"])), C.c_int32(G), C.c_int32(t["default"]),
+             _p(t["gpair"], C.c_uint32), C.c_uint32(t["n_gp"]), _p(t["dry"], C.c_uint8), _p(out, C.c_int64)]
+    f = lib().orc_totals
+    keep = (arrs, narrs, t, out)
+
+    def run():
+        assert f(*args) == 0 and keep
+        return out
+    return run
+
+
 def params(groups: list[dict], states: list[dict] | None) -> np.ndarray:
     out = np.zeros((len(groups), 12), np.int64)
     for g, s in enumerate(groups):

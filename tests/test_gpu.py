@@ -69,6 +69,40 @@ def test_fixture_nodes_capacity_total(esc, golden):
         assert k8s.calculate_nodes_capacity_total(nodes) == (c["mem"], c["cpu"]), c["name"]
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_dropin_lists_vs_literal(esc, seed):
+    """The per-call drop-ins (esc_list.hip: pinned buffers reused across calls, one kernel)
+    over random slices — absent / zero / negative / huge requests, init containers,
+    overhead, daemonsets (the Go functions take the slice as given: no filter) — equal the
+    literal CalculatePodsRequestsTotal / CalculateNodesCapacityTotal; sizes from empty to
+    many workgroups, repeated calls on one context, growth of the buffers; a total outside
+    int64 raises OverflowError (the reference's Quantity would move to inf.Dec)."""
+    from escalator_amd import k8s
+    rng = random.Random(8800 + seed)
+    groups = make_groups(rng, 3, with_default=True)
+    for n in (0, 1, 7, 1000, 3000, 40_000, 1000):
+        pods = make_pods(rng, n, groups, big_frac=0.05 if n < 5000 else 0.0)
+        try:
+            want = O.calculate_pods_requests_total(pods)
+        except O.QuantityOverflow:
+            want = None
+        if want is None:
+            t = [O.compute_pod_resource_request(p) for p in pods]
+            exact = (sum(m for _, m in t), sum(c for c, _ in t))
+            if all(-(1 << 63) <= v < (1 << 63) for v in exact):
+                want = exact                    # order-independent exact total (unpinned: see DESIGN.md §2)
+        if want is None:
+            with pytest.raises(OverflowError):
+                k8s.calculate_pods_requests_total(pods)
+        else:
+            assert k8s.calculate_pods_requests_total(pods) == want, n
+        nodes = make_nodes(rng, max(n // 20, 0), groups, big_frac=0.0)
+        assert k8s.calculate_nodes_capacity_total(nodes) == O.calculate_nodes_capacity_total(nodes), n
+    big = [build_test_pod({"CPU": [1 << 62], "Mem": [1 << 62]})] * 3
+    with pytest.raises(OverflowError):
+        k8s.calculate_pods_requests_total(big)
+
+
 def test_fixture_orderings(esc, golden):
     from escalator_amd import controller
     fx = golden["controller"]
@@ -923,6 +957,66 @@ def test_reaping_follows_pod_events(esc, seed):
             live[i] = dict(live[i], node_name=t)
         cur = [live[i] for i in sorted(live)]
         _check_reaping(ctx, groups, cur, nodes, trackers, now_ns, soft, hard)
+
+
+def _many_pair_pod(rng, groups, node_name):
+    """A pod outside the K classes by its pairs: one node-affinity `In` term over 5-7 values
+    of one group key (4-6 extra pairs: > 3, so its PodRef reads them through its xp offset;
+    <= 6, a spare C slot's room)."""
+    q = make_pods(rng, 1, groups, big_frac=0.0)[0]
+    keyed = [g for g in groups if g["label_key"]]
+    k = rng.choice(keyed)["label_key"] if keyed else "customer"
+    vals = sorted({g["label_value"] for g in groups if g["label_key"] == k} | {"x%d" % i for i in range(9)})
+    rng.shuffle(vals)
+    q["node_selector"] = None
+    q["owner_kinds"] = []
+    q["affinity"] = {"node_affinity": {"required": [[{"key": k, "op": "In", "values": vals[:rng.randrange(5, 8)]}]]},
+                     "pod_affinity": False, "pod_anti_affinity": False}
+    q["node_name"] = node_name
+    return q
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_reaping_follows_c_pod_upserts(esc, seed):
+    """upserts of BOUND pods with more than 3 extra pairs (C section, indirect
+    PodRefs) whose pairs change, K <-> C moves and C-slot reuse inside one batch: the node
+    occupancy words follow (the old contribution leaves before the record is patched), so
+    TryRemoveTaintedNodes equals the literal oracle on the live pods."""
+    from escalator_amd.objects import placement
+    rng = random.Random(9700 + seed)
+    G = rng.choice([4, 8])
+    groups, pods, nodes, now_ns = make_reaping_cluster(rng, G, 300, 30)
+    pods += [_many_pair_pod(rng, groups, rng.choice(nodes)["name"]) for _ in range(60)]
+    trackers = make_trackers(rng, groups, nodes)
+    ctx = esc.Context(groups)
+    ctx.set_spare(2.0)
+    P, N = ctx.pack(pods, nodes, trackers)
+    assert sum(not _fits_k(P, k) for k in range(len(pods))) >= 60
+    ctx.load(P, N)
+    pn, ts, nd = placement(pods, nodes)
+    ctx.load_placement(pn, ts, nd)
+    live = dict(enumerate(pods))
+    soft = np.full(G, 60 * 10**9, np.int64)
+    hard = np.full(G, 4000 * 10**9, np.int64)
+    _check_reaping(ctx, groups, [live[i] for i in sorted(live)], nodes, trackers, now_ns, soft, hard)
+    for rnd in range(4):
+        bound = [i for i in sorted(live) if live[i]["node_name"] and not _fits_k(P, i)]
+        ev_ids, ev_objs = [], []
+        for i in rng.sample(bound, min(len(bound), 20)):       # C pods: new pairs (or into K), same node
+            q = _many_pair_pod(rng, groups, live[i]["node_name"]) if rng.random() < 0.7 else \
+                dict(make_pods(rng, 1, groups, big_frac=0.0)[0], node_name=live[i]["node_name"])
+            ev_ids.append(i)
+            ev_objs.append(q)
+        kb = [i for i in sorted(live) if live[i]["node_name"] and i not in ev_ids]
+        for i in rng.sample(kb, min(len(kb), 10)):             # K pods into C (may reuse a slot freed above)
+            ev_ids.append(i)
+            ev_objs.append(_many_pair_pod(rng, groups, live[i]["node_name"]))
+        Pe, _ = ctx.pack(ev_objs, [])
+        assert ctx.pods_upsert(ev_ids, Pe) == 0, rnd
+        for i, q in zip(ev_ids, ev_objs):
+            live[i] = q
+        P, _ = ctx.pack([live[i] for i in range(len(pods))], [])     # which ids are C pods now
+        _check_reaping(ctx, groups, [live[i] for i in sorted(live)], nodes, trackers, now_ns, soft, hard)
 
 
 @pytest.mark.parametrize("seed", range(4))
