@@ -28,8 +28,11 @@ CONFIGS = {
             name="config4: 100M pods / 1M nodes / 10k node groups (BASELINE.json configs[3]), sharded over N GPUs"),
 }
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# PMC passes (scripts/pmc_job.sh) of the kernels as built at this tag: HBM bytes per launch
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03_p8c", "pmc_summary.json")
+# rocprofv3 kernel-trace + PMC passes of this same command (scripts/job_r04c.sh), reduced to
+# the timed launches by scripts/prof_summary.py: HBM bytes per K1 launch, by workload
+PROF_DIR = os.path.join(ROOT, "profiles", "r04_prof")
+PMC_SUMMARY = {(4, 1): os.path.join(PROF_DIR, "summary_full.json"),       # (config, shard-of)
+               (4, 8): os.path.join(PROF_DIR, "summary_shard8.json")}
 
 
 def log(*a):
@@ -48,17 +51,16 @@ def stream_bytes(ctx, s, rank, world) -> tuple[int, int]:
     return pb, nb
 
 
-def pmc_traffic(kernel: str):
-    """HBM bytes per launch of `kernel` from the committed PMC summary (or None)."""
+def pmc_traffic(kernel: str, key):
+    """HBM bytes per launch of `kernel` over the timed launches, from the committed PMC
+    summary of this workload (or None), and that summary's path."""
+    path = PMC_SUMMARY.get(key)
     try:
-        with open(PMC_SUMMARY) as f:
+        with open(path) as f:
             d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    for name, v in d.items():
-        if kernel in name:
-            return v.get("hbm_bytes")
-    return None
+    except (OSError, ValueError, TypeError):
+        return None, None
+    return d.get("kernels", {}).get(kernel, {}).get("hbm_bytes"), os.path.relpath(path, ROOT)
 
 
 def cpu_model() -> str:
@@ -572,6 +574,16 @@ def main():
                    (["d2h"] if os.environ.get("ESC_NO_ZEROCOPY", "0") not in ("", "0") else []))
     stage_mean = np.mean(np.array(stages), axis=0)
 
+    # BASELINE.md §2 logical bytes: this rank's pods (every pod for a multi-device context),
+    # its ordered memberships (the groups it owns) -- summed over the ranks -- and the node
+    # table once
+    from escalator_amd import layout as _layout
+    md = np.array([_layout.baseline_md_pod_bytes(s.pods()), 0 if args.no_order else n_memb], np.int64)
+    if dist is not None:
+        tmd = torch.from_numpy(md).to("cuda" if backend == "nccl" else "cpu")
+        dist.all_reduce(tmd)
+        md = tmd.cpu().numpy()
+
     parity = None
     if not args.no_parity:
         # rank 0 checks its decision (after the exchange) against the C oracle over the
@@ -615,7 +627,14 @@ def main():
     decision_bytes = (pod_b + node_b + (0 if args.no_order else n_memb * 16)) * (1 if multi else world)
     # PMC passes are taken on the single-GPU config-4 run (scripts/pmc_job.sh); a shard's
     # K1 launch moves other bytes, so the committed figure applies to N = 1 only
-    traffic = pmc_traffic("k_pod_reduce") if n_gpus == 1 and shard_world == 1 and args.config == 4 else None
+    traffic, traffic_src = (pmc_traffic("k_pod_reduce", (args.config, shard_world))
+                            if n_gpus == 1 and not args.pods else (None, None))
+    # BASELINE.md §2's definition of the metric's bytes (the uncompressed reference-shaped
+    # SoA; the north star's "% of aggregate HBM" is quoted on it), beside the physical frac
+    nmd = _layout.baseline_md_node_bytes(s.nodes())
+    bmd = {"pods": int(md[0]), "nodes": nmd, "orderings": 12 * int(md[1]), "total": int(md[0]) + nmd + 12 * int(md[1])}
+    frac_md = bmd["total"] / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9 * n_gpus)
+    probe = ctx.hbm_probe() if n_gpus == 1 else None
     out = {
         "metric": "pod+node records evaluated/sec per scale decision & % HBM peak, 1/2/4/8 GPUs",
         "value": value,
@@ -635,8 +654,16 @@ def main():
         "hbm_frac_decision": decision_bytes / (ms_per_step * 1e-3) / (HBM_PEAK_GBS * 1e9 * n_gpus),
         "roofline": {"bound": "hbm", "kernel": "k_pod_reduce", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) if traffic else None,
-                     "algorithmic_bytes_per_launch": algo, "launch_ms": k1_ms},
+                     "traffic_source": traffic_src if traffic else None,
+                     "algorithmic_bytes_per_launch": algo, "launch_ms": k1_ms,
+                     "box_read_ceiling_GBps": probe,
+                     "frac_of_box_ceiling": achieved / probe if probe else None},
+        "frac_baseline_md": frac_md,
+        "baseline_md_bytes": dict(bmd, note="BASELINE.md §2 logical bytes (uncompressed reference-shaped SoA: 33 B/pod "
+                                            "at C=S=1, 24 + 4 L B/node, 12 B per ordered membership) over the generated "
+                                            "arrays, all ranks; frac_baseline_md = total / ms_per_step / (n_gpus x 8 TB/s) "
+                                            "(> 1 possible: the resident format is packed, see roofline for the physical "
+                                            "bytes)"),
         "k1_partials": k1_partials,
         "node_bytes_per_decision": node_b,
         "exchange": exchange,

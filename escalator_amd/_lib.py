@@ -163,6 +163,8 @@ _SIGS = {
     "esc_nodes_update": (i32, [VP, P(i64), i64, P(u32), P(i64), P(i64)]),
     "esc_nodes_add": (i32, [VP, P(NodeSoA), P(i64)]),
     "esc_nodes_delete": (i32, [VP, P(i64), i64]),
+    "esc_nodes_relabel": (i32, [VP, P(i64), P(NodeSoA)]),
+    "esc_hbm_probe": (i32, [VP, i64, i32, P(C.c_double)]),
     "esc_tracker_update": (i32, [VP, i32, P(i64), i64, P(i64), i64]),
     "esc_tracker_list": (i32, [VP, i32, P(i64), i64, P(i64)]),
     "esc_load_placement": (i32, [VP, P(u32), P(i64), P(C.c_uint8)]),

@@ -271,6 +271,17 @@ class Context:
         del keep
         return out[:n]
 
+    def nodes_relabel(self, ids, nodes: dict):
+        """Node informer Update events with any field changed, labels and creation time
+        included (esc_nodes_relabel): `nodes` = the packed new records of the nodes `ids`
+        (n_trk = 0).  EscError(ESC_E_LIMIT) when the spare room is short (reload)."""
+        ids = np.ascontiguousarray(ids, np.int64)
+        assert len(ids) == len(nodes["flags"])
+        ns, keep = node_soa(nodes)
+        L.check(self.lib.esc_nodes_relabel(self.handle, ids.ctypes.data_as(C.POINTER(C.c_int64)), C.byref(ns)),
+                "esc_nodes_relabel")
+        del keep
+
     def nodes_delete(self, ids):
         """Node informer Delete events: the nodes' slots become absent."""
         ids = np.ascontiguousarray(ids, np.int64)
@@ -333,6 +344,12 @@ class Context:
         a, b = C.c_int64(), C.c_int64()
         L.check(self.lib.esc_k1_flush_entries(self.handle, C.byref(a), C.byref(b)), "esc_k1_flush_entries")
         return a.value, b.value
+
+    def hbm_probe(self, nbytes: int = 2 << 30, reps: int = 10) -> float:
+        """The device's practical HBM read rate (GB/s) in K1's access shape (esc_hbm_probe)."""
+        v = C.c_double()
+        L.check(self.lib.esc_hbm_probe(self.handle, int(nbytes), int(reps), C.byref(v)), "esc_hbm_probe")
+        return v.value
 
     def k1_trace(self):
         """Per-workgroup K1 timestamps of the last decision (diagnostics):

@@ -62,6 +62,12 @@ def untaint_newest_n(created_ns, n: int, device: int = 0) -> list[int]:
     return _order(created_ns, n, False, device)
 
 
+# The methods Controller calls on its actuator (per node: taint / untaint return whether the
+# API write succeeded; the cloud node group's TargetSize / MaxSize / IncreaseSize /
+# DeleteNodes, cloudprovider/interface.go:45-80)
+ACTUATOR_METHODS = ("taint", "untaint", "target_size", "max_size", "increase_size", "delete_nodes")
+
+
 class SimulatedCloud:
     """The actuator used when none is given: every Kubernetes write succeeds, and the
     cloud node group behaves like the reference tests' mock (pkg/test/cloud_provider.go):
@@ -133,6 +139,12 @@ class Controller:
         self.taint_tracker = {g: [] for g in range(len(groups))}
         self.clock = clock or time.time_ns
         self.actuator = actuator if actuator is not None else SimulatedCloud(self.groups)
+        # the actuator protocol (per-node taint/untaint -> bool, the cloud group's sizes):
+        # refused here rather than by an AttributeError after a decision
+        missing = [m for m in ACTUATOR_METHODS if not callable(getattr(self.actuator, m, None))]
+        if missing:
+            raise TypeError("actuator %r lacks %s (the protocol: %s; see INTEGRATION.md §5)" %
+                            (type(self.actuator).__name__, ", ".join(missing), ", ".join(ACTUATOR_METHODS)))
 
     def _lock_states(self, now: int):
         """scaleLock.locked() (scale_lock.go:22-29) for every group, before the decision."""
@@ -253,16 +265,19 @@ class Controller:
             tainted = self.ctx.group_order(g, 1) if int(tot["n_tainted"][g]) else []
             if branch == "below_min":                                     # controller.go:281-295
                 r["delta"], r["err"] = self._scale_up(g, r["delta"], list(tainted), names, r)
-            elif r["err"] is None and branch in ("fast_down", "slow_down"):
-                self._reap(g, r)                                          # ScaleDown: reap first
-                if int(d["taint_status"]) == 0:
-                    self._scale_down_taint(g, r["n_to_taint"], names, r)  # controller.go:369-371
+            elif r["err"] is None and branch in ("fast_down", "slow_down", "scale_up", "none"):
+                # the action switch is on nodesDelta's sign, whichever branch computed it
+                # (controller.go:367-383; a scale-up from zero can compute 0)
+                if r["delta"] < 0:
+                    self._reap(g, r)                                      # ScaleDown: reap first
+                    if int(d["taint_status"]) == 0:
+                        self._scale_down_taint(g, r["n_to_taint"], names, r)   # controller.go:368-371
+                    else:
+                        r["action_err"] = "taint clamp"                   # scale_down.go:150-154
+                elif r["delta"] > 0:
+                    _, r["action_err"] = self._scale_up(g, r["delta"], list(tainted), names, r)   # :372-375
                 else:
-                    r["action_err"] = "taint clamp"                       # scale_down.go:150-154
-            elif r["err"] is None and branch == "scale_up" and r["delta"] > 0:
-                _, r["action_err"] = self._scale_up(g, r["delta"], list(tainted), names, r)   # controller.go:372-375
-            elif r["err"] is None and branch == "none":
-                self._reap(g, r)                                          # controller.go:377-383
+                    self._reap(g, r)                                      # default: controller.go:377-383
             out.append(r)
         return out
 

@@ -70,5 +70,7 @@ int32_t list_pods_requests_total(ListReducer*& r, int device, void* stream, cons
 int32_t list_nodes_capacity_total(ListReducer*& r, int device, void* stream, const esc_node_obj* nodes, int64_t n,
                                   int64_t* mem_b, int64_t* cpu_m);
 void list_reducer_free(ListReducer*& r);
+// esc_hbm_probe's streaming read (esc_list.hip)
+int32_t hbm_probe(int device, void* stream, int64_t bytes, int32_t reps, double* gbps);
 
 }  // namespace esc

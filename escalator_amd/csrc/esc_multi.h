@@ -39,6 +39,7 @@ int32_t fail_hip(hipError_t e, const char* what);
 // check phases of esc_pods_upsert / esc_pods_bind (nothing applied)
 int32_t pods_upsert_check(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p);
 int32_t pods_bind_check(esc_ctx* c, const int64_t* ids, const uint32_t* pod_node, int64_t n);
+int32_t nodes_relabel_check(esc_ctx* c, const int64_t* ids, const esc_node_soa* s);
 
 // ---- the multi-device context: every ABI call on it dispatches to these (esc_multi.hip)
 void multi_destroy(esc_ctx* c);
@@ -60,6 +61,7 @@ int32_t multi_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint
                            const int64_t* mem);
 int32_t multi_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out);
 int32_t multi_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n);
+int32_t multi_nodes_relabel(esc_ctx* c, const int64_t* ids, const esc_node_soa* s);
 int32_t multi_tracker_update(esc_ctx* c, int32_t group, const int64_t* add, int64_t n_add, const int64_t* rm,
                              int64_t n_rm);
 int32_t multi_load_placement(esc_ctx* c, const uint32_t* pod_node, const int64_t* taint_s, const uint8_t* no_delete);

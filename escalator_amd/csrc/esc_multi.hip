@@ -43,6 +43,9 @@ struct esc_multi_state {
     std::vector<uint32_t*> psum32;
     int64_t psum32_n = 0;
     std::vector<hipEvent_t> ev_done, ev_read;
+    // a node event applied on some devices but failed on a later one: the devices' node
+    // tables differ, so decisions are refused (ESC_E_STATE) until the nodes are reloaded
+    bool diverged = false;
 };
 
 namespace {
@@ -248,7 +251,9 @@ int32_t multi_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset)
 }
 
 int32_t multi_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi) {
-    return par(c, [&](int i) { return esc_load_nodes(M(c).subs[i], s, lo, hi); });
+    const int32_t rc = par(c, [&](int i) { return esc_load_nodes(M(c).subs[i], s, lo, hi); });
+    M(c).diverged = rc != ESC_OK && nsub(c) > 1;             // some devices may hold the new table
+    return rc;
 }
 
 int32_t multi_stream_bytes(const esc_ctx* c, int64_t* pod_bytes, int64_t* node_bytes) {
@@ -271,6 +276,7 @@ int32_t multi_set_state(esc_ctx* c, const esc_group_state* st) {
 // words), the SUM across the devices (RCCL group call, or the peer exchange), every
 // device's K4.  Asynchronous like esc_run; esc_sync / esc_results wait.
 int32_t multi_step(esc_ctx* c) {
+    if (M(c).diverged) return ESC_E_STATE;
     if (int32_t rc = seq(c, [&](int i) { return esc_reduce(M(c).subs[i]); })) return rc;
     if (int32_t rc = exchange_words(c)) return rc;
     return seq(c, [&](int i) { return esc_decide(M(c).subs[i]); });
@@ -372,16 +378,37 @@ int32_t multi_pods_bind(esc_ctx* c, const int64_t* ids, const uint32_t* pod_node
 }
 
 // Node events reach every device (each holds the whole node table); their checks depend
-// on that table only, so the devices accept or refuse a batch alike.
+// on that table only, so the devices accept or refuse a batch alike: device
+// 0's refusal leaves every device untouched.  A failure on a later device (a HIP error after
+// device 0 applied the batch) leaves the tables different: the context is marked diverged
+// and refuses decisions until esc_load_nodes.
+template <class F>
+int32_t node_event(esc_ctx* c, F&& f) {
+    esc_multi_state& m = M(c);
+    if (m.diverged) return ESC_E_STATE;
+    for (int i = 0; i < nsub(c); ++i)
+        if (int32_t rc = f(i)) {
+            if (i > 0) m.diverged = true;
+            return i > 0 ? (int32_t)ESC_E_STATE : rc;
+        }
+    return ESC_OK;
+}
+
 int32_t multi_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32_t* flags, const int64_t* cpu,
                            const int64_t* mem) {
-    return seq(c, [&](int i) { return esc_nodes_update(M(c).subs[i], ids, n, flags, cpu, mem); });
+    return node_event(c, [&](int i) { return esc_nodes_update(M(c).subs[i], ids, n, flags, cpu, mem); });
+}
+
+int32_t multi_nodes_relabel(esc_ctx* c, const int64_t* ids, const esc_node_soa* s) {
+    if (M(c).diverged) return ESC_E_STATE;
+    if (int32_t rc = nodes_relabel_check(M(c).subs[0], ids, s)) return rc;   // nothing applied anywhere
+    return node_event(c, [&](int i) { return esc_nodes_relabel(M(c).subs[i], ids, s); });
 }
 
 int32_t multi_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
     if (!s || s->n_nodes < 0 || (s->n_nodes > 0 && !ids_out)) return ESC_E_INVAL;
     std::vector<int64_t> tmp((size_t)std::max<int64_t>(s->n_nodes, 1));
-    return seq(c, [&](int i) {
+    return node_event(c, [&](int i) {
         int64_t* out = i == 0 ? ids_out : tmp.data();
         const int32_t rc = esc_nodes_add(M(c).subs[i], s, out);
         if (rc == ESC_OK && i > 0 && s->n_nodes > 0 && std::memcmp(out, ids_out, (size_t)s->n_nodes * 8) != 0)
@@ -391,12 +418,12 @@ int32_t multi_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
 }
 
 int32_t multi_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
-    return seq(c, [&](int i) { return esc_nodes_delete(M(c).subs[i], ids, n); });
+    return node_event(c, [&](int i) { return esc_nodes_delete(M(c).subs[i], ids, n); });
 }
 
 int32_t multi_tracker_update(esc_ctx* c, int32_t group, const int64_t* add, int64_t n_add, const int64_t* rm,
                              int64_t n_rm) {
-    return seq(c, [&](int i) { return esc_tracker_update(M(c).subs[i], group, add, n_add, rm, n_rm); });
+    return node_event(c, [&](int i) { return esc_tracker_update(M(c).subs[i], group, add, n_add, rm, n_rm); });
 }
 
 // ------------------------------------------------------------------------ reaping

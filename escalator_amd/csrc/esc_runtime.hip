@@ -2605,6 +2605,84 @@ int32_t patch_regions(esc_ctx* c, const std::vector<int64_t>& ids) {
     return apply_patches(c, P, {t});
 }
 
+// allNodes[0] (controller.go:207-211) of a group with pair q: its lowest live member,
+// over every entry of the pair (a relabelled node's entry sits after the others, so the
+// pair's entries are not always in index order).
+void pair_first(const esc_ctx* c, uint32_t q, GroupNode& x) {
+    const uint32_t a = c->pair_lo[q], z = c->pair_next.empty() ? a : c->pair_next[q];
+    x.first = INT64_MAX;
+    x.first_cpu = x.first_mem = 0;
+    for (uint32_t e = a; e < z; ++e) {
+        const uint32_t j = c->h_e_node[e];
+        if (j != NONE && (int64_t)j < x.first && !(c->h_nflags[j] & ESC_NF_ABSENT)) x.first = j;
+    }
+    if (x.first != INT64_MAX) {
+        x.first_cpu = c->h_ncpu[x.first];
+        x.first_mem = c->h_nmem[x.first];
+    }
+}
+
+// Patch targets of the K5 regions: node id, group code, flags copy.
+PatchTargets region_targets(esc_ctx* c) {
+    PatchTargets t{};
+    t.u32[0] = c->d_g_node; t.u32[1] = c->d_g_grp; t.u32[2] = c->d_g_flags;
+    return t;
+}
+
+// Node events, K5 regions: insert the nodes `add_by_g[g]` into the regions of the groups g
+// (owned by this rank) at their place by (creation time, index); every touched region is
+// rewritten from its first insertion on (one scatter for all of them, into R).
+void regions_insert(esc_ctx* c, std::unordered_map<uint32_t, std::vector<uint32_t>>& add_by_g, Patches& R) {
+    auto less = [&](uint32_t x, uint32_t y) {
+        const int64_t tx = created_of(c, x), ty = created_of(c, y);
+        return tx < ty || (tx == ty && x < y);
+    };
+    for (auto& kv : add_by_g) {
+        const uint32_t g = kv.first;
+        std::vector<uint32_t>& nw = kv.second;
+        if (nw.empty()) continue;
+        std::sort(nw.begin(), nw.end(), less);
+        const uint32_t a = c->h_pstart[g], len = c->h_plen[g];
+        uint32_t* run = c->h_gn.data() + a;
+        const uint32_t from = (uint32_t)(std::upper_bound(run, run + len, nw.front(), less) - run);
+        std::vector<uint32_t> merged(len - from + nw.size());
+        std::merge(run + from, run + len, nw.begin(), nw.end(), merged.begin(), less);
+        std::copy(merged.begin(), merged.end(), run + from);
+        c->h_plen[g] = len + (uint32_t)nw.size();
+        const uint32_t mbit = (uint32_t)g | (c->params[g].dry ? NODE_DRY_BIT : 0u);
+        for (size_t k = 0; k < merged.size(); ++k) {
+            const int64_t pos = (int64_t)a + from + (int64_t)k;
+            R.add(0, pos, merged[k]);
+            R.add(1, pos, mbit);
+            R.add(2, pos, (c->h_nflags[merged[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT : memb_flags(c, merged[k], mbit));
+        }
+    }
+}
+
+// Node events, K5 regions: take node j's membership out of group g's region (owned by this
+// rank; found by the node's CURRENT creation time): the region's tail moves up one slot and
+// its last slot becomes padding (g | MEMB_PAD, absent), as k_region_pad writes it.
+bool region_remove(esc_ctx* c, uint32_t g, uint32_t j, Patches& R) {
+    const int64_t pos = region_pos(c, g, j);
+    if (pos < 0) return false;
+    const uint32_t a = c->h_pstart[g], len = c->h_plen[g];
+    const int64_t last = (int64_t)a + len - 1;
+    uint32_t* gn = c->h_gn.data();
+    const uint32_t mbit = (uint32_t)g | (c->params[g].dry ? NODE_DRY_BIT : 0u);
+    for (int64_t k = pos; k < last; ++k) {
+        gn[k] = gn[k + 1];
+        R.add(0, k, gn[k]);
+        R.add(1, k, mbit);
+        R.add(2, k, (c->h_nflags[gn[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT : memb_flags(c, gn[k], mbit));
+    }
+    gn[last] = 0;
+    R.add(0, last, 0);
+    R.add(1, last, (uint32_t)g | MEMB_PAD);
+    R.add(2, last, ESC_NF_ABSENT);
+    c->h_plen[g] = len - 1;
+    return true;
+}
+
 // Writes the host mirrors (h_nflags / h_ncpu / h_nmem) of nodes `ids` to the device:
 // the node table, the nodes' pair-major K2 entries, allNodes[0]'s cached allocatable,
 // and the K5 region copies (looked up by creation time: no re-listing).
@@ -2619,6 +2697,7 @@ int32_t patch_nodes(esc_ctx* c, const std::vector<int64_t>& ids) {
         P.add(NT_CPU, j, cpu);
         P.add(NT_MEM, j, mem);
         for (uint32_t e = c->ne_off[j]; e < c->ne_off[j + 1]; ++e) {
+            if (c->h_e_node[c->ne_pos[e]] != (uint32_t)j) continue;   // an entry a relabel retired
             P.add(NT_EFLAGS, c->ne_pos[e], f);
             P.add(NT_ECPU, c->ne_pos[e], cpu);
             P.add(NT_EMEM, c->ne_pos[e], mem);
@@ -3150,32 +3229,9 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
                 else ++c->h_plen[g];
             }
         }
-        auto less = [&](uint32_t x, uint32_t y) {
-            const int64_t tx = created_of(c, x), ty = created_of(c, y);
-            return tx < ty || (tx == ty && x < y);
-        };
         Patches R;                                   // one scatter for every touched region
-        for (auto& kv : add_by_g) {
-            const uint32_t g = kv.first;
-            std::vector<uint32_t>& nw = kv.second;
-            std::sort(nw.begin(), nw.end(), less);
-            const uint32_t a = c->h_pstart[g], len = c->h_plen[g];
-            uint32_t* run = c->h_gn.data() + a;
-            const uint32_t from = (uint32_t)(std::upper_bound(run, run + len, nw.front(), less) - run);
-            std::vector<uint32_t> merged(len - from + nw.size());
-            std::merge(run + from, run + len, nw.begin(), nw.end(), merged.begin(), less);
-            std::copy(merged.begin(), merged.end(), run + from);
-            c->h_plen[g] = len + (uint32_t)nw.size();
-            const uint32_t mbit = (uint32_t)g | (c->params[g].dry ? NODE_DRY_BIT : 0u);
-            for (size_t k = 0; k < merged.size(); ++k) {
-                const int64_t pos = (int64_t)a + from + (int64_t)k;
-                R.add(0, pos, merged[k]);
-                R.add(1, pos, mbit);
-                R.add(2, pos, (c->h_nflags[merged[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT : memb_flags(c, merged[k], mbit));
-            }
-        }
-        PatchTargets t{};
-        t.u32[0] = c->d_g_node; t.u32[1] = c->d_g_grp; t.u32[2] = c->d_g_flags;
+        regions_insert(c, add_by_g, R);
+        PatchTargets t = region_targets(c);
         rc = apply_patches(c, R, {t});
         if (rc) return rc;
     }
@@ -3216,19 +3272,7 @@ int32_t esc_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
     for (int32_t g = 0; g < c->gi.G; ++g) {
         GroupNode& x = c->h_gnode[g];
         if (x.first == INT64_MAX || !(c->h_nflags[x.first] & ESC_NF_ABSENT)) continue;
-        const uint32_t q = c->gi.gpair[g];
-        const uint32_t a = c->nodes_piece_lo(q), z = c->pair_next.empty() ? a : c->pair_next[q];
-        x.first = INT64_MAX;
-        x.first_cpu = x.first_mem = 0;
-        for (uint32_t e = a; e < z; ++e) {
-            const uint32_t j = c->h_e_node[e];
-            if (j != NONE && !(c->h_nflags[j] & ESC_NF_ABSENT)) {
-                x.first = j;
-                x.first_cpu = c->h_ncpu[j];
-                x.first_mem = c->h_nmem[j];
-                break;
-            }
-        }
+        pair_first(c, c->gi.gpair[g], x);
         first_changed = true;
     }
     if (first_changed)
@@ -3238,6 +3282,273 @@ int32_t esc_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
     c->rm_valid = false;
     return patch_nodes(c, del);
 }
+
+// Node informer Update events that change a node's LABELS or CREATION TIME (besides its
+// flags and allocatable).  The reference re-reads every node's labels on every List
+// (NewNodeLabelFilterFunc node_group.go:278-287 through FilteredNodesLister.List
+// node_listers.go:33-48, fed by the informer cache.go:37-56), so a relabelled node simply
+// moves between groups on the next scan.  Here the node keeps its snapshot index and:
+//  - its pair-major entries of pairs it no longer carries are retired (absent, no node) and
+//    entries of the group pairs it now carries are taken from their pairs' spare room (as
+//    esc_nodes_add does); the node -> entries map follows;
+//  - allNodes[0] of every group whose pair gained or lost the node is recomputed (lowest
+//    live member);
+//  - its K5 memberships leave the regions of the groups it left (the region closes up) and
+//    join the regions of the groups it joined at their place by creation time (a creation
+//    time change moves it in every region);
+//  - with a placement loaded, its pods' occupancy contributions leave the old entries and
+//    join the new ones (k_occ_delta).
+// All or nothing: ESC_E_LIMIT when the spare entries, extra-label words or region slots do
+// not hold the batch (nothing applied; reload).
+namespace {
+
+struct RelabelPlan {
+    std::vector<std::vector<uint32_t>> old_m, new_m;          // memberships (group | dry bit)
+    std::vector<int64_t> xo;                                  // each node's first new extra label
+    std::vector<uint8_t> moved;                               // creation time changed
+};
+
+// group pairs (ids < n_gp) of a label set, ascending
+void group_pairs(uint32_t n_gp, uint32_t label0, uint32_t nx, const uint32_t* xl, std::vector<uint32_t>& out) {
+    out.clear();
+    if (label0 < n_gp) out.push_back(label0);
+    for (uint32_t k = 0; k < nx; ++k)
+        if (xl[k] < n_gp) out.push_back(xl[k]);
+}
+
+// the group pair of pair-major entry e (NONE: a pair no group uses)
+uint32_t entry_pair(const esc_ctx* c, uint32_t e) {
+    const uint32_t n_gp = c->gi.n_gp;
+    if (!n_gp || e >= c->pair_end[n_gp - 1]) return NONE;
+    const uint32_t q = (uint32_t)(std::upper_bound(c->pair_lo.begin(), c->pair_lo.end(), e) - c->pair_lo.begin()) - 1;
+    return e < c->pair_end[q] ? q : NONE;
+}
+
+int32_t relabel_plan(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, RelabelPlan& u) {
+    if (!c || !s || s->n_nodes < 0 || (s->n_nodes > 0 && (!ids || !s->flags || !s->label0 || !s->cpu || !s->mem ||
+                                                          !s->created_ns)))
+        return ESC_E_INVAL;
+    if (s->n_trk != 0 || (s->n_xl > 0 && !s->xl_pair)) return ESC_E_INVAL;   // trackers: esc_tracker_update
+    if (!c->has_device) return ESC_E_NODEV;
+    if (!c->nodes_loaded) return ESC_E_STATE;
+    const int64_t n = s->n_nodes;
+    std::vector<int64_t> seen(ids, ids + n);
+    std::sort(seen.begin(), seen.end());
+    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end()) return ESC_E_INVAL;
+    const uint32_t n_gp = c->gi.n_gp;
+    u.old_m.assign(n, {});
+    u.new_m.assign(n, {});
+    u.xo.assign(n, 0);
+    u.moved.assign(n, 0);
+    std::unordered_map<uint32_t, int64_t> need_e;
+    std::unordered_map<uint32_t, int64_t> need_r;
+    std::vector<uint32_t> oq, nq;
+    uint64_t sx = 0, xl_grow = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t j = ids[i];
+        if (j < 0 || j >= c->n_nodes || (c->h_nflags[j] & ESC_NF_ABSENT)) return ESC_E_INVAL;
+        const uint32_t f = s->flags[i], nx = nf_xlbl(f);
+        if (f & ESC_NF_ABSENT) return ESC_E_INVAL;
+        uint32_t last = s->label0[i];
+        if (last == NONE ? nx != 0 : last >= ESC_PAIR_LIMIT) return ESC_E_INVAL;
+        if (sx + nx > (uint64_t)s->n_xl) return ESC_E_INVAL;
+        for (uint32_t k = 0; k < nx; ++k) {
+            const uint32_t q = s->xl_pair[sx + k];
+            if (q >= ESC_PAIR_LIMIT || q <= last) return ESC_E_INVAL;
+            last = q;
+        }
+        u.xo[i] = (int64_t)sx;
+        if (nx > nf_xlbl(c->h_nflags[j])) xl_grow += nx;
+        // entries: the group pairs the node gains
+        group_pairs(n_gp, c->h_label0[j], nf_xlbl(c->h_nflags[j]), c->h_xl.data() + c->h_xl_off[j], oq);
+        group_pairs(n_gp, s->label0[i], nx, s->xl_pair + sx, nq);
+        for (uint32_t q : nq)
+            if (!std::binary_search(oq.begin(), oq.end(), q)) ++need_e[q];
+        // K5 regions: memberships left / joined (all of them when the creation time moved)
+        node_membs(c, j, u.old_m[i]);
+        node_membs_from(c, s->label0[i], nx, s->xl_pair + sx, u.new_m[i]);
+        u.moved[i] = s->created_ns[i] != created_of(c, (uint32_t)j);
+        for (uint32_t m : u.old_m[i])
+            if (u.moved[i] || std::find(u.new_m[i].begin(), u.new_m[i].end(), m) == u.new_m[i].end())
+                --need_r[m & NODE_GROUP_MASK];
+        for (uint32_t m : u.new_m[i])
+            if (u.moved[i] || std::find(u.old_m[i].begin(), u.old_m[i].end(), m) == u.old_m[i].end())
+                ++need_r[m & NODE_GROUP_MASK];
+        sx += nx;
+    }
+    if ((int64_t)sx != s->n_xl) return ESC_E_INVAL;
+    if (c->xl_used + (int64_t)xl_grow > c->xl_cap) return ESC_E_LIMIT;
+    for (const auto& kv : need_e)
+        if ((int64_t)c->pair_next[kv.first] + kv.second > (int64_t)c->pair_end[kv.first]) return ESC_E_LIMIT;
+    if (c->age_built && !c->h_pcap.empty())
+        for (const auto& kv : need_r)
+            if ((int64_t)c->h_plen[kv.first] + kv.second > (int64_t)c->h_pcap[kv.first]) return ESC_E_LIMIT;
+    return ESC_OK;
+}
+
+int32_t relabel_apply(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, const RelabelPlan& u) {
+    const int64_t n = s->n_nodes;
+    if (n == 0) return ESC_OK;
+    const uint32_t n_gp = c->gi.n_gp;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->rm_valid = false;
+    // the nodes' pods leave the occupancy words of their current entries
+    std::vector<uint32_t> opos, onode;
+    if (c->placed) {
+        for (int64_t i = 0; i < n; ++i) {
+            const uint32_t j = (uint32_t)ids[i];
+            for (uint32_t p = c->h_run_off[j]; p < c->h_run_off[j] + c->h_run_len[j]; ++p) {
+                opos.push_back(p);
+                onode.push_back(j);
+            }
+        }
+        if (int32_t rc = occ_delta(c, opos, onode, -1)) return rc;
+    }
+    // K5: memberships leave their regions while the creation times are the old ones
+    const bool k5 = c->age_built && !c->h_pcap.empty();
+    Patches R;
+    if (k5) {
+        if (c->n_gpad > 0)
+            if (int32_t rc = ensure_gn(c)) return rc;
+        for (int64_t i = 0; i < n; ++i)
+            for (uint32_t m : u.old_m[i]) {
+                if (!u.moved[i] && std::find(u.new_m[i].begin(), u.new_m[i].end(), m) != u.new_m[i].end()) continue;
+                const uint32_t g = m & NODE_GROUP_MASK;
+                if (!owns_group(c, g)) { --c->h_plen[g]; continue; }
+                if (!region_remove(c, g, (uint32_t)ids[i], R)) return fail_hip(hipErrorUnknown, "relabel: region mirror");
+            }
+    }
+    // host mirrors, extra labels, pair-major entries, node -> entries map
+    Patches P;
+    std::vector<uint32_t> oq, nq, keep;
+    std::vector<uint8_t> pair_touched(n_gp, 0);
+    std::vector<std::pair<int64_t, std::vector<uint32_t>>> regrow;   // nodes whose entry list grew
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t j = ids[i];
+        const uint32_t f = s->flags[i], nx = nf_xlbl(f), onx = nf_xlbl(c->h_nflags[j]);
+        group_pairs(n_gp, s->label0[i], nx, s->xl_pair + u.xo[i], nq);
+        keep.clear();
+        std::vector<uint32_t> dead;                                       // retired entries in j's slots
+        for (uint32_t k = c->ne_off[j]; k < c->ne_off[j + 1]; ++k) {
+            const uint32_t e = c->ne_pos[k];
+            if (c->h_e_node[e] != (uint32_t)j) { dead.push_back(e); continue; }   // retired earlier
+            const uint32_t q = entry_pair(c, e);
+            if (q != NONE && std::binary_search(nq.begin(), nq.end(), q)) { keep.push_back(e); continue; }
+            c->h_e_node[e] = NONE;                                        // retired: absent, no node
+            P.add(NT_EFLAGS, e, ESC_NF_ABSENT);
+            P.add(NT_ENODE, e, NONE);
+            dead.push_back(e);
+            if (q != NONE) { --c->pair_live[q]; pair_touched[q] = 1; }
+        }
+        for (uint32_t q : nq) {
+            bool have = false;
+            for (uint32_t e : keep) have |= entry_pair(c, e) == q;
+            if (have) continue;
+            const uint32_t e = c->pair_next[q]++;                         // a spare entry of the pair
+            c->h_e_node[e] = (uint32_t)j;
+            P.add(NT_ENODE, e, (uint32_t)j);                               // flags / cpu / mem: patch_nodes
+            keep.push_back(e);
+            ++c->pair_live[q];
+            pair_touched[q] = 1;
+        }
+        const uint32_t slots = c->ne_off[j + 1] - c->ne_off[j];
+        if (keep.size() <= slots) {
+            // in place; the spare slots repeat a retired entry (there is one whenever a slot is
+            // spare: patch_nodes skips it, its occupancy word is never read)
+            for (uint32_t k = 0; k < slots; ++k)
+                c->ne_pos[c->ne_off[j] + k] = k < keep.size() ? keep[k] : dead[0];
+        } else {
+            regrow.emplace_back(j, keep);
+        }
+        // extra labels: in place, or appended when the node has more of them now
+        if (nx > onx) {
+            c->h_xl_off[j] = (uint32_t)c->xl_used;
+            c->h_xl.resize((size_t)c->xl_used + nx);
+            c->xl_used += nx;
+        }
+        for (uint32_t k = 0; k < nx; ++k) {
+            c->h_xl[c->h_xl_off[j] + k] = s->xl_pair[u.xo[i] + k];
+            P.add(NT_XL, c->h_xl_off[j] + k, s->xl_pair[u.xo[i] + k]);
+        }
+        c->h_label0[j] = s->label0[i];
+        c->h_nflags[j] = (f & ~ESC_NF_TRACKED) | (c->h_nflags[j] & ESC_NF_TRACKED);
+        c->h_ncpu[j] = s->cpu[i];
+        c->h_nmem[j] = s->mem[i];
+        c->h_created[j - c->node_lo] = s->created_ns[i];
+        P.add(NT_LABEL0, j, s->label0[i]);
+        P.add(NT_XLOFF, j, c->h_xl_off[j]);
+        P.add(NT_CREATED, j, (uint64_t)s->created_ns[i]);
+        if (u.moved[i] && c->age_built &&
+            (s->created_ns[i] < c->ts_min || s->created_ns[i] > c->ts_max ||
+             (uint64_t)(s->created_ns[i] - c->ts_min) % c->sort_div != 0))
+            c->age_n = -1;                          // outside the index's key range: the next build is fresh
+    }
+    if (!regrow.empty()) {                          // rebuild the node -> entries map
+        std::sort(regrow.begin(), regrow.end());
+        std::vector<uint32_t> off(c->ne_off.size()), pos;
+        pos.reserve(c->ne_pos.size() + 16);
+        size_t r = 0;
+        for (size_t j = 0; j + 1 < c->ne_off.size(); ++j) {
+            off[j] = (uint32_t)pos.size();
+            if (r < regrow.size() && regrow[r].first == (int64_t)j) {
+                pos.insert(pos.end(), regrow[r].second.begin(), regrow[r].second.end());
+                ++r;
+            } else {
+                pos.insert(pos.end(), c->ne_pos.begin() + c->ne_off[j], c->ne_pos.begin() + c->ne_off[j + 1]);
+            }
+        }
+        off.back() = (uint32_t)pos.size();
+        c->ne_off.swap(off);
+        c->ne_pos.swap(pos);
+    }
+    c->ne_dev_nodes = -1;                           // the device copy is re-sent before its next use
+    // allNodes[0] of the groups whose pair gained or lost a node
+    for (int32_t g = 0; g < c->gi.G; ++g)
+        if (pair_touched[c->gi.gpair[g]]) pair_first(c, c->gi.gpair[g], c->h_gnode[g]);
+    HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
+    if (int32_t rc = apply_patches(c, P, {node_targets(c)})) return rc;
+    // K5: memberships join their regions at their (new) place
+    if (k5) {
+        std::unordered_map<uint32_t, std::vector<uint32_t>> add_by_g;
+        for (int64_t i = 0; i < n; ++i)
+            for (uint32_t m : u.new_m[i]) {
+                if (!u.moved[i] && std::find(u.old_m[i].begin(), u.old_m[i].end(), m) != u.old_m[i].end()) continue;
+                const uint32_t g = m & NODE_GROUP_MASK;
+                if (owns_group(c, g)) add_by_g[g].push_back((uint32_t)ids[i]);
+                else ++c->h_plen[g];
+            }
+        regions_insert(c, add_by_g, R);
+        if (int32_t rc = apply_patches(c, R, {region_targets(c)})) return rc;
+    }
+    // node table flags / allocatable, the entries' copies (the new ones included), allNodes[0]'s
+    // allocatable, the K5 flag copies
+    std::vector<int64_t> touched(ids, ids + n);
+    if (int32_t rc = patch_nodes(c, touched)) return rc;
+    // the nodes' pods join the occupancy words of their entries now
+    if (c->placed) return occ_delta(c, opos, onode, +1);
+    return ESC_OK;
+}
+
+}  // namespace
+
+int32_t esc_nodes_relabel(esc_ctx* c, const int64_t* ids, const esc_node_soa* s) {
+    if (c && c->multi) return esc::multi_nodes_relabel(c, ids, s);
+    RelabelPlan u;
+    const int32_t rc = relabel_plan(c, ids, s, u);
+    return rc ? rc : relabel_apply(c, ids, s, u);
+}
+
+}  // extern "C"
+
+namespace esc {
+int32_t nodes_relabel_check(esc_ctx* c, const int64_t* ids, const esc_node_soa* s) {
+    RelabelPlan u;
+    return relabel_plan(c, ids, s, u);
+}
+}  // namespace esc
+
+extern "C" {
 
 // Dry-mode taintTracker bookkeeping (§8f rank 4).  The reference keeps per group a slice
 // of node names: taintOldestN appends in dry mode (scale_down.go:197-200), untaintNewestN
@@ -3549,6 +3860,8 @@ int32_t esc_removal_nodes(esc_ctx* c, int32_t g, int64_t* idx, int64_t cap, int6
     std::vector<uint32_t> v(n);
     hipSetDevice(c->device);
     HIP_TRY(hipMemcpy(v.data(), c->d_rm_list + c->h_rm_off[g], n * 4, hipMemcpyDeviceToHost));
+    // K7 lists them in entry order: snapshot order, except behind a relabelled node's entry
+    std::sort(v.begin(), v.end());
     for (int64_t k = 0; k < n; ++k) idx[k] = v[k];
     return ESC_OK;
 }
@@ -3676,6 +3989,13 @@ int32_t esc_pods_requests_total(esc_ctx* c, const esc_pod_obj* pods, int64_t n, 
     if (!c || n < 0 || (n > 0 && !pods) || !mem_b || !cpu_m) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     return list_pods_requests_total(c->lred, c->device, c->stream, pods, n, mem_b, cpu_m);
+}
+
+int32_t esc_hbm_probe(esc_ctx* c, int64_t bytes, int32_t reps, double* read_gbps) {
+    if (c && c->multi) return esc_hbm_probe(esc::multi_sub(c, 0), bytes, reps, read_gbps);
+    if (!c || !read_gbps) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    return hbm_probe(c->device, c->stream, bytes, reps, read_gbps);
 }
 
 int32_t esc_nodes_capacity_total(esc_ctx* c, const esc_node_obj* nodes, int64_t n, int64_t* mem_b, int64_t* cpu_m) {

@@ -140,3 +140,31 @@ def node_bytes(nodes: dict, n_gp: int, rank: int = 0, world: int = 1) -> int:
     b = owner_ranges(nodes, n_gp, world)
     mine = (p_pair >= b[rank]) & (p_pair < b[rank + 1])
     return int(8 * int(mine.sum()) + 24 * int(p_len[mine].sum()))
+
+
+def baseline_md_pod_bytes(pods: dict) -> int:
+    """BASELINE.md §2's logical bytes of the pods (see ``baseline_md_bytes``)."""
+    f = np.asarray(pods["flags"], np.uint64)
+    ctr = 1 + (((f >> 8) & 0xFF) + ((f >> 16) & 0xFF) + ((f >> 4) & 1)).astype(np.int64)
+    pairs = (np.asarray(pods["pair0"], np.uint32) != NONE).astype(np.int64) + ((f >> 24) & 0x3F).astype(np.int64)
+    return int((12 + 17 * ctr + 4 * pairs).sum())
+
+
+def baseline_md_node_bytes(nodes: dict) -> int:
+    """BASELINE.md §2's logical bytes of the nodes (see ``baseline_md_bytes``)."""
+    nf = np.asarray(nodes["flags"], np.uint64)
+    labels = (np.asarray(nodes["label0"], np.uint32) != NONE).astype(np.int64) + ((nf >> 8) & 0xFF).astype(np.int64)
+    return int((24 + 4 * labels).sum())
+
+
+def baseline_md_bytes(pods: dict, nodes: dict, n_memb: int = 0) -> dict:
+    """The logical bytes of BASELINE.md §2's metric definition over the generated arrays —
+    the reference-shaped, uncompressed SoA the north star's "% of HBM" is quoted on:
+    per pod 4 (flags) + 4 (ctr_off) + 17 per container (cpu 8, mem 8, kind 1; regular, init
+    and the overhead pseudo-container) + 4 (pair_off) + 4 per selector pair; per node 4
+    (flags) + 8 + 8 (allocatable) + 4 (label_off) + 4 per carried label pair; 12 B per
+    ordered membership (8-B key + 4-B permutation).  The resident format streams fewer bytes
+    (``pod_bytes``: packed tiles), so this figure, divided by the decision time, can exceed
+    the HBM peak; the physical roofline is ``pod_bytes`` over K1's launch time."""
+    pb, nb = baseline_md_pod_bytes(pods), baseline_md_node_bytes(nodes)
+    return {"pods": pb, "nodes": nb, "orderings": 12 * int(n_memb), "total": pb + nb + 12 * int(n_memb)}

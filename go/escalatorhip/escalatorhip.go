@@ -610,6 +610,26 @@ func (x *Context) NodesAdd(nodes []*v1.Node) ([]int64, error) {
 	return ids[:len(nodes)], err
 }
 
+// NodesRelabel applies node Update events that change labels or the creation time (any
+// field): ids[i] takes nodes[i]'s record in place, moving between node groups as
+// NewNodeLabelFilterFunc (node_group.go:278-287) would see it on the next List.  ErrReload
+// when the spare room is short.
+func (x *Context) NodesRelabel(ids []int64, nodes []*v1.Node) error {
+	if len(ids) != len(nodes) {
+		return fmt.Errorf("escalatorhip: %d ids for %d nodes", len(ids), len(nodes))
+	}
+	if len(nodes) == 0 {
+		return nil
+	}
+	return x.pack(nil, nodes, nil, false, func(_ *C.esc_pod_soa, ns *C.esc_node_soa) error {
+		rc := C.esc_nodes_relabel(x.c, (*C.int64_t)(unsafe.Pointer(ptr(ids))), ns)
+		if rc == C.ESC_E_LIMIT {
+			return ErrReload
+		}
+		return rcErr("esc_nodes_relabel", rc)
+	})
+}
+
 // NodesDelete applies node Delete events by snapshot index.
 func (x *Context) NodesDelete(ids []int64) error {
 	return rcErr("esc_nodes_delete", C.esc_nodes_delete(x.c, (*C.int64_t)(unsafe.Pointer(ptr(ids))), C.int64_t(len(ids))))

@@ -432,6 +432,11 @@ int32_t esc_k1_calibrate(esc_ctx* ctx, int32_t rounds);
  * per decision, *full = entries of a whole-row flush (workgroups x pod-slot columns); equal
  * when the compact flush is off.  Multi-device: summed over the devices. */
 int32_t esc_k1_flush_entries(const esc_ctx* ctx, int64_t* entries, int64_t* full);
+/* The device's practical HBM read rate in K1's access shape (a contiguous share per
+ * 512-thread workgroup, 16-B nontemporal loads, 8 in flight per lane) over a fresh buffer
+ * of `bytes` (> the 256 MB Infinity Cache, so HBM-served): best of `reps` launches, GB/s.
+ * The ceiling a roofline fraction of this box is read against (MI355X boards differ). */
+int32_t esc_hbm_probe(esc_ctx* ctx, int64_t bytes, int32_t reps, double* read_gbps);
 
 /* ------------------------------------------- incremental snapshot (§8f rank 1)
  * Informer-style events patch the resident snapshot in place instead of a reload
@@ -443,9 +448,9 @@ int32_t esc_k1_flush_entries(const esc_ctx* ctx, int64_t* entries, int64_t* full
  * class is full) stays in its own C-section slot when that has room, else takes a spare
  * C slot (room for 4 extra regular and 2 init containers, an overhead and 6 extra pairs;
  * unused records stay neutral).  A batch that does not fit in place returns ESC_E_LIMIT
- * with nothing applied, and the caller reloads.  Node events may
- * change Spec.Unschedulable, the escalator taint and allocatable; label or creation-time
- * changes need esc_load_nodes (tracker changes: esc_tracker_update).  Every call
+ * with nothing applied, and the caller reloads.  esc_nodes_update may change
+ * Spec.Unschedulable, the escalator taint and allocatable; label or creation-time changes
+ * go through esc_nodes_relabel (tracker changes: esc_tracker_update).  Every call
  * completes before returning.                                                       */
 int32_t esc_set_spare(esc_ctx* ctx, double fraction);       /* spare room: per K pod class (esc_load_pods),
                                                                 node slots / entries / K5 regions (esc_load_nodes) */
@@ -469,6 +474,17 @@ int32_t esc_nodes_update(esc_ctx* ctx, const int64_t* ids, int64_t n, const uint
  * accept or refuse the same batch. */
 int32_t esc_nodes_add(esc_ctx* ctx, const esc_node_soa* nodes, int64_t* ids_out);
 int32_t esc_nodes_delete(esc_ctx* ctx, const int64_t* ids, int64_t n);
+/* Node informer Update events that change any field of a node — its labels and creation
+ * time included — in place (the reference re-reads the labels on every List:
+ * NewNodeLabelFilterFunc pkg/controller/node_group.go:278-287 via FilteredNodesLister.List
+ * pkg/k8s/node_listers.go:33-48, fed by pkg/k8s/cache.go:37-56).  `nodes` holds the new
+ * packed records of the n = nodes->n_nodes nodes ids[0..n) (as esc_nodes_add's input:
+ * n_trk = 0; a caller's ESC_NF_TRACKED bit is ignored, the tracker is the context's).  The
+ * nodes keep their snapshot indices; they leave the groups whose pair they no longer carry
+ * and join those whose pair they now carry (spare pair-major entries and K5 region slots,
+ * esc_set_spare), allNodes[0] follows, a placement's occupancy follows.  All or nothing:
+ * ESC_E_LIMIT when the spare room is short (reload), ESC_E_INVAL for a bad or absent id. */
+int32_t esc_nodes_relabel(esc_ctx* ctx, const int64_t* ids, const esc_node_soa* nodes);
 
 /* ------------------------------------------- dry-mode taintTracker (§8f rank 4)
  * nodeGroup.taintTracker (controller.go:35) as interned (node, group) pairs on the

@@ -9,7 +9,9 @@ the common "status changed" event), (b) batches of deletes followed by re-insert
 same records (slot recycling), (c) node taint / allocatable updates, and (d) one full
 decision after the events; the decision is checked bit-exact against the C oracle on the
 unchanged snapshot content.  Then (e) node deletions and additions (the same records
-re-added as new nodes).  Prints one JSON line."""
+re-added as new nodes), after (f) node relabels (two sets of nodes trade records: labels,
+creation times, flags, allocatable), checked against the C oracle over the permuted
+snapshot.  Prints one JSON line."""
 import argparse
 import json
 import os
@@ -94,6 +96,37 @@ def main():
 
     nb = max(1, args.node_batch)
     live, src = np.arange(N), np.arange(N)            # snapshot index, record it holds
+    # node informer Updates that change labels and creation times (esc_nodes_relabel): two
+    # disjoint sets of nodes trade their records (labels, creation, flags, allocatable), so
+    # every node of the batch moves groups and age; then one decision and three groups'
+    # orderings against the C oracle over the permuted snapshot
+    res["node_relabel_s"] = []
+    for r in range(args.rounds + 1):                  # round 0 warms the host mirrors
+        pick = rng.choice(N, size=2 * (nb // 2), replace=False)
+        a, b = pick[: nb // 2], pick[nb // 2:]
+        ids = np.concatenate([a, b])
+        rec = node_subset(np.concatenate([src[b], src[a]]))
+        t0 = time.perf_counter()
+        ctx.nodes_relabel(ids, rec)
+        if r:
+            res["node_relabel_s"].append(time.perf_counter() - t0)
+        src[a], src[b] = src[b].copy(), src[a].copy()
+    ctx.run()
+    tot, dec = ctx.results()
+    xl_parts = [nodes["xl_pair"][xo[i]:xo[i + 1]] for i in src]
+    perm = {"flags": (nodes["flags"][src] & ~np.uint32(4)) | (nodes["flags"] & np.uint32(4)),
+            "label0": nodes["label0"][src], "cpu": nodes["cpu"][src], "mem": nodes["mem"][src],
+            "created_ns": nodes["created_ns"][src], "xl_pair": np.concatenate(xl_parts).astype(np.uint32),
+            "trk_node": nodes["trk_node"], "trk_group": nodes["trk_group"]}
+    ptot = soa.totals(pods, perm, s.groups)
+    pdf, pdi = soa.decide(s.groups, s.states, ptot)
+    ok_rl = all(np.array_equal(tot[n], ptot[:, k]) for k, n in enumerate(soa.TOT_FIELDS[:12]))
+    ok_rl &= np.array_equal(dec["delta"], pdi[:, 0]) and np.array_equal(dec["cpu_pct"].view(np.uint64),
+                                                                         pdf[:, 0].view(np.uint64))
+    ctx.sort_nodes()
+    for g in (0, G // 2, G - 1):
+        for w in (0, 1):
+            ok_rl &= np.array_equal(ctx.group_order(g, w), soa.order(perm, s.groups, g, w))
     res["node_delete_s"], res["node_add_s"] = [], []
     for r in range(args.rounds + 1):                  # round 0 warms the host mirrors
         pick = np.sort(rng.choice(len(live), size=nb, replace=False))
@@ -123,6 +156,9 @@ def main():
            "node_batch": nb,
            "node_deletes_per_s": nb / float(np.median(res["node_delete_s"])),
            "node_adds_per_s": nb / float(np.median(res["node_add_s"])),
+           "node_relabels_per_s": 2 * (nb // 2) / float(np.median(res["node_relabel_s"])),
+           "parity_after_relabels": ("bit-exact vs C oracle over the permuted snapshot (10000 groups; orderings of "
+                                     "groups 0, %d, %d)" % (G // 2, G - 1)) if ok_rl else "MISMATCH",
            "decision_after_node_events_s": decide_after_s,
            "raw_s": res,
            "parity_after_events": "bit-exact vs C oracle (10000 groups)" if ok else "MISMATCH"}

@@ -480,6 +480,129 @@ def test_node_add_delete_vs_literal(esc, seed):
         assert before == {(g, w): list(ctx.group_order(g, w)) for g in range(G) for w in (0, 1)}
 
 
+def _relabel(rng, nd, groups, move_time):
+    """A node Update with new labels (group moves, extra labels, labels no group uses), maybe
+    a new creation time, taint / cordon and allocatable."""
+    x = make_nodes(rng, 1, groups, big_frac=0.0)[0]
+    x["name"] = nd["name"]
+    for k in ("taint_value", "annotations"):
+        if k in nd:
+            x[k] = nd[k]
+    if not move_time:
+        x["created_ns"] = nd["created_ns"]
+    elif rng.random() < 0.3:
+        x["created_ns"] = nd["created_ns"] + rng.choice([-1, 1]) * rng.randrange(1, 5) * 1_000
+    return x
+
+
+def _check_nodes_vs_literal(ctx, groups, states, pods, live, trackers, tag):
+    idx = sorted(live)
+    lst = [live[j] for j in idx]
+    tot, dec = ctx.decide_all(states)
+    ctx.sort_nodes()
+    for g in range(len(groups)):
+        L = O.scale_node_group(groups[g], states[g], pods, lst, tracker=trackers.get(g, []))
+        t, d = tot[g], dec[g]
+        first = idx[L["first_node"]] if L["first_node"] >= 0 else -1
+        assert (t["n_pods"], t["n_nodes"], t["n_untainted"], t["n_tainted"], t["n_cordoned"], t["first_node"]) == \
+            (L["n_pods"], L["n_nodes"], L["n_untainted"], L["n_tainted"], L["n_cordoned"], first), (tag, g)
+        if L["pod_cpu_m"] is not None:
+            assert (t["node_cpu_m"], t["node_mem_b"]) == (L["node_cpu_m"], L["node_mem_b"]), (tag, g)
+        assert esc_branch(d) == L["branch"], (tag, g)
+        assert int(d["delta"]) == L["delta"] and int(d["n_to_taint"]) == L["n_to_taint"], (tag, g)
+        assert _bits(d["cpu_pct"]) == _bits(L["cpu_pct"]) and _bits(d["mem_pct"]) == _bits(L["mem_pct"]), (tag, g)
+        assert (int(d["cached_cpu_m"]), int(d["cached_mem_b"])) == (L["cached_cpu_m"], L["cached_mem_b"]), (tag, g)
+        unt, tn = L["untainted"], L["tainted"]
+        assert list(ctx.group_order(g, 0)) == \
+            [idx[unt[i]] for i in O.oldest_first([lst[k]["created_ns"] for k in unt])], (tag, g)
+        assert list(ctx.group_order(g, 1)) == \
+            [idx[tn[i]] for i in O.newest_first([lst[k]["created_ns"] for k in tn])], (tag, g)
+
+
+def esc_branch(d):
+    from escalator_amd._lib import BRANCHES
+    return BRANCHES[d["branch"]]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_node_relabel_vs_literal(esc, seed):
+    """Node Update events that change labels and creation times in place (esc_nodes_relabel,
+    VERDICT r3 item 5): nodes move between groups, gain / lose extra labels and group
+    memberships, change age, taint, cordon and allocatable, between node additions and
+    deletions; no reload.  Totals, allNodes[0], decisions and both orderings equal the literal
+    oracle on the updated nodes after every round, and a fresh age-index build agrees."""
+    rng = random.Random(9900 + seed)
+    G = rng.choice([3, 8, 20])
+    groups = make_groups(rng, G, with_default=rng.random() < 0.6)
+    pods = make_pods(rng, 300, groups, big_frac=0.0)
+    nodes = make_nodes(rng, rng.choice([40, 120]), groups, big_frac=0.0)
+    trackers = make_trackers(rng, groups, nodes)
+    states = make_states(rng, G)
+    ctx = esc.Context(groups)
+    ctx.set_spare(2.0)
+    P, N = ctx.pack(pods, nodes, trackers)
+    ctx.load(P, N)
+    if seed % 2:
+        ctx.set_order_in_step(True)
+    live = dict(enumerate(nodes))
+    hw = len(nodes)
+    _check_nodes_vs_literal(ctx, groups, states, pods, live, trackers, "load")
+    for rnd in range(5):
+        ids = rng.sample(sorted(live), k=min(len(live), rng.randrange(1, 16)))
+        new = [_relabel(rng, live[j], groups, move_time=seed >= 2) for j in ids]
+        _, packed = ctx.pack([], new)
+        ctx.nodes_relabel(ids, packed)
+        for j, x in zip(ids, new):
+            live[j] = x
+        _check_nodes_vs_literal(ctx, groups, states, pods, live, trackers, (rnd, "relabel"))
+        dels = rng.sample(sorted(live), k=min(len(live), rng.randrange(0, 4)))
+        if dels:
+            ctx.nodes_delete(dels)
+            for j in dels:
+                del live[j]
+        add = make_nodes(rng, rng.randrange(0, 4), groups, big_frac=0.0)
+        for k, x in enumerate(add):
+            x["name"] = "r%d-add%d" % (rnd, k)
+        if add:
+            _, packed = ctx.pack([], add)
+            got = ctx.nodes_add(packed)
+            assert list(got) == list(range(hw, hw + len(add)))
+            for j, x in zip(got, add):
+                live[int(j)] = x
+            hw += len(add)
+        _check_nodes_vs_literal(ctx, groups, states, pods, live, trackers, (rnd, "add/delete"))
+    before = {(g, w): list(ctx.group_order(g, w)) for g in range(G) for w in (0, 1)}
+    ctx.build_age_index()
+    ctx.sort_nodes()
+    assert before == {(g, w): list(ctx.group_order(g, w)) for g in range(G) for w in (0, 1)}
+
+
+def test_node_relabel_limit_all_or_nothing(esc):
+    """A relabel batch whose new memberships do not fit the spare room is refused whole
+    (ESC_E_LIMIT); a bad id is ESC_E_INVAL; smaller batches then apply."""
+    groups = [{"name": "a", "label_key": "k", "label_value": "a", "max_nodes": 1000},
+              {"name": "b", "label_key": "k", "label_value": "b", "max_nodes": 1000}]
+    nodes = [{"name": "n%d" % i, "labels": {"k": "a"}, "cpu": 1000, "mem": 1000, "created_ns": i} for i in range(40)]
+    nodes += [{"name": "m%d" % i, "labels": {"k": "b"}, "cpu": 10, "mem": 10, "created_ns": 100 + i} for i in range(4)]
+    ctx = esc.Context(groups)
+    ctx.set_spare(0.01)
+    ctx.load(*ctx.pack([], nodes))
+    moved = [dict(nodes[i], labels={"k": "b"}) for i in range(40)]
+    _, packed = ctx.pack([], moved)
+    with pytest.raises(esc._lib.EscError) as e:
+        ctx.nodes_relabel(list(range(40)), packed)
+    assert e.value.code == esc._lib.ESC_E_LIMIT
+    tot, _ = ctx.decide_all()
+    assert list(tot["n_nodes"]) == [40, 4] and list(tot["node_cpu_m"]) == [40000, 40]
+    with pytest.raises(esc._lib.EscError):
+        ctx.nodes_relabel([99], ctx.pack([], moved[:1])[1])
+    _, packed = ctx.pack([], moved[:3])
+    ctx.nodes_relabel([0, 1, 2], packed)
+    tot, _ = ctx.decide_all()
+    assert list(tot["n_nodes"]) == [37, 7] and list(tot["first_node"]) == [3, 0]
+    assert list(tot["node_cpu_m"]) == [37000, 3040]
+
+
 def test_node_add_limit_all_or_nothing(esc):
     """A batch that does not fit the spare room is refused whole (ESC_E_LIMIT)."""
     groups = [{"name": "a", "label_key": "k", "label_value": "v", "max_nodes": 1000}]
@@ -1017,6 +1140,43 @@ def test_reaping_follows_c_pod_upserts(esc, seed):
             live[i] = q
         P, _ = ctx.pack([live[i] for i in range(len(pods))], [])     # which ids are C pods now
         _check_reaping(ctx, groups, [live[i] for i in sorted(live)], nodes, trackers, now_ns, soft, hard)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_reaping_across_node_relabels(esc, seed):
+    """TryRemoveTaintedNodes after node relabels (esc_nodes_relabel): a relabelled node's
+    pods leave the occupancy of the group pairs it no longer carries and count for the ones
+    it now carries, with no placement reload (the taint facts are refreshed, not the
+    binding); deletions equal the literal oracle, in snapshot order."""
+    from escalator_amd.objects import placement
+    rng = random.Random(9950 + seed)
+    G = rng.choice([4, 8])
+    groups, pods, nodes, now_ns = make_reaping_cluster(rng, G, 800, 60)
+    trackers = make_trackers(rng, groups, nodes)
+    ctx = esc.Context(groups)
+    ctx.set_spare(1.0)
+    P, N = ctx.pack(pods, nodes, trackers)
+    ctx.load(P, N)
+    pn, ts, nd = placement(pods, nodes)
+    ctx.load_placement(pn, ts, nd)
+    soft = np.full(G, 60 * 10**9, np.int64)
+    hard = np.full(G, 4000 * 10**9, np.int64)
+    for rnd in range(4):
+        ids = rng.sample(range(len(nodes)), 12)
+        new = []
+        for j in ids:
+            x = _relabel(rng, nodes[j], groups, move_time=rnd % 2 == 1)
+            x["taint_value"] = nodes[j].get("taint_value")
+            if rng.random() < 0.5 and "atlassian.com/escalator" not in x["taints"]:
+                x["taints"] = x["taints"] + ["atlassian.com/escalator"]
+            new.append(x)
+        _, packed = ctx.pack([], new)
+        ctx.nodes_relabel(ids, packed)
+        for j, x in zip(ids, new):
+            nodes[j] = x
+        _, ts, nd = placement(pods, nodes)
+        ctx.load_placement(None, ts, nd)                   # the node facts (taint times) only
+        _check_reaping(ctx, groups, pods, nodes, trackers, now_ns, soft, hard)
 
 
 @pytest.mark.parametrize("seed", range(4))

@@ -151,6 +151,12 @@ def test_multi_device_events_vs_literal(esc, seed):
         gone = rng.sample(sorted(alive), 3)
         ctx.nodes_delete(gone)
         alive -= set(gone)
+        rl = rng.sample(sorted(alive), 6)                 # relabels: group moves on every device
+        for j in rl:
+            x = make_nodes(rng, 1, groups, big_frac=0.0)[0]
+            nodes[j] = dict(x, name=nodes[j]["name"], created_ns=nodes[j]["created_ns"])
+        _, Nr = ctx.pack([], [nodes[j] for j in rl])
+        ctx.nodes_relabel(rl, Nr)
         idx = sorted(alive)                               # snapshot indices of the live nodes
         cur_nodes = [nodes[j] for j in idx]
         cur = [live[i] for i in sorted(live)]
