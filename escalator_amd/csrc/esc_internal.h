@@ -3,7 +3,10 @@
 #pragma once
 
 #include <stdint.h>
+#include <memory>
 #include <string>
+#include <type_traits>
+#include <utility>
 #include <unordered_map>
 #include <vector>
 
@@ -49,14 +52,32 @@ struct GroupIndex {
     bool is_key(const char* k) const { return keys.count(std::string(k ? k : "")) != 0; }
 };
 
+// std::vector whose resize() leaves new elements default-initialised (no zero fill): the
+// host snapshot's arrays are written in full by their producers (the packer's parallel
+// merge, the generator), so a 100 M-pod resize costs no single-threaded memset.
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind { using other = DefaultInitAlloc<U>; };
+    DefaultInitAlloc() = default;
+    template <class U>
+    DefaultInitAlloc(const DefaultInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) { ::new ((void*)p) U; }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+template <class T>
+using hvec = std::vector<T, DefaultInitAlloc<T>>;
+
 // Host-side packed snapshot (owned vectors) produced by the packer or the generator.
 struct HostSnapshot {
-    std::vector<uint32_t> flags, cpu0, pair0;
-    std::vector<int64_t> mem0, xc_cpu, xc_mem;
-    std::vector<uint32_t> xp;
-    std::vector<uint32_t> nflags, label0, xl;
-    std::vector<int64_t> ncpu, nmem, created;
-    std::vector<int32_t> trk_node, trk_group;
+    hvec<uint32_t> flags, cpu0, pair0;
+    hvec<int64_t> mem0, xc_cpu, xc_mem;
+    hvec<uint32_t> xp;
+    hvec<uint32_t> nflags, label0, xl;
+    hvec<int64_t> ncpu, nmem, created;
+    hvec<int32_t> trk_node, trk_group;
 
     void view(esc_pod_soa* p, esc_node_soa* n) const;
 };

@@ -13,9 +13,11 @@
 //   - container requests become the (inline + extra records) encoding that
 //     ComputePodResourceRequest (scheduler/types.go:72-89) is evaluated on by K1.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <set>
+#include <thread>
 
 #include "esc_internal.h"
 
@@ -121,11 +123,14 @@ void sort_unique(std::vector<uint32_t>& v) {
     v.erase(std::unique(v.begin(), v.end()), v.end());
 }
 
-int32_t pack_pod(esc_packer* pk, const esc_pod_obj& o) {
-    HostSnapshot& s = pk->s;
+// One pod into `s` (HostSnapshot or a parallel part: the same member names); `in(k, v, id)`
+// interns a pair.  `pairs` is scratch.
+template <class Out, class Intern>
+int32_t pack_pod(const GroupIndex* gi, bool list_mode, const esc_pod_obj& o, Out& s, Intern&& in,
+                 std::vector<uint32_t>& pairs) {
     uint32_t f = 0;
-    std::vector<uint32_t> pairs;
-    if (!pk->list_mode) {
+    pairs.clear();
+    if (!list_mode) {
         for (int32_t i = 0; i < o.n_owner_kinds; ++i)                        // util.go:12-16
             if (o.owner_kinds[i] && std::strcmp(o.owner_kinds[i], "DaemonSet") == 0) { f |= ESC_PF_DAEMONSET; break; }
         if (o.has_config_source && o.config_source && std::strcmp(o.config_source, "file") == 0)
@@ -139,19 +144,19 @@ int32_t pack_pod(esc_packer* pk, const esc_pod_obj& o) {
         // a pod once however many routes match.  K1 resolves pair -> groups.
         for (int32_t i = 0; i < o.n_node_selector; ++i) {
             const esc_kv& kv = o.node_selector[i];
-            if (!pk->gi->is_key(kv.key)) continue;
+            if (!gi->is_key(kv.key)) continue;
             uint32_t id;
-            if (!intern(pk, kv.key, kv.value, id)) return ESC_E_LIMIT;
+            if (!in(kv.key, kv.value, id)) return ESC_E_LIMIT;
             pairs.push_back(id);
         }
         if (o.has_affinity && o.has_node_affinity && o.has_required) {     // unwrapNodeSelectorTerms :208
             for (int32_t e = 0; e < o.n_exprs; ++e) {
                 const esc_selector_expr& x = o.exprs[e];
                 if (!x.op || std::strcmp(x.op, "In") != 0) continue;         // only In (:241)
-                if (!pk->gi->is_key(x.key)) continue;
+                if (!gi->is_key(x.key)) continue;
                 for (int32_t v = 0; v < x.n_values; ++v) {
                     uint32_t id;
-                    if (!intern(pk, x.key, x.values[v], id)) return ESC_E_LIMIT;
+                    if (!in(x.key, x.values[v], id)) return ESC_E_LIMIT;
                     pairs.push_back(id);
                 }
             }
@@ -202,18 +207,19 @@ int32_t pack_pod(esc_packer* pk, const esc_pod_obj& o) {
     return ESC_OK;
 }
 
-int32_t pack_node(esc_packer* pk, const esc_node_obj& o) {
-    HostSnapshot& s = pk->s;
+template <class Out, class Intern>
+int32_t pack_node(const GroupIndex* gi, bool list_mode, const esc_node_obj& o, Out& s,
+                  std::vector<std::string>& names, Intern&& in, std::vector<uint32_t>& pairs) {
     uint32_t f = 0;
-    std::vector<uint32_t> pairs;
-    if (!pk->list_mode) {
+    pairs.clear();
+    if (!list_mode) {
         if (o.unschedulable) f |= ESC_NF_UNSCHED;                            // controller.go:141
         for (int32_t i = 0; i < o.n_taints; ++i)                             // taint.go:81-85
             if (o.taint_keys[i] && std::strcmp(o.taint_keys[i], "atlassian.com/escalator") == 0) { f |= ESC_NF_TAINTED; break; }
         for (int32_t i = 0; i < o.n_labels; ++i) {                           // node_group.go:280
-            if (!pk->gi->is_key(o.labels[i].key)) continue;                  // Labels[K] for group keys
+            if (!gi->is_key(o.labels[i].key)) continue;                      // Labels[K] for group keys
             uint32_t id;
-            if (!intern(pk, o.labels[i].key, o.labels[i].value, id)) return ESC_E_LIMIT;
+            if (!in(o.labels[i].key, o.labels[i].value, id)) return ESC_E_LIMIT;
             pairs.push_back(id);
         }
         sort_unique(pairs);
@@ -228,7 +234,200 @@ int32_t pack_node(esc_packer* pk, const esc_node_obj& o) {
     s.ncpu.push_back(req_or(o.allocatable.has_cpu, o.allocatable.cpu_m, 0));   // util.go:47 absent -> 0
     s.nmem.push_back(req_or(o.allocatable.has_mem, o.allocatable.mem_b, 0));
     s.created.push_back(o.created_unix_ns);
-    pk->node_names.emplace_back(o.name ? o.name : "");
+    names.emplace_back(o.name ? o.name : "");
+    return ESC_OK;
+}
+
+// ---- the parallel packer (esc_packer_add_pods / _add_nodes over large slices)
+// Objects are independent, so T threads each pack a contiguous chunk into a part of their
+// own; the parts are then copied into the snapshot in chunk order.  The one shared piece of
+// state is the interner of values no group selects (ids >= n_gp, numbered by first
+// appearance): a part interns a value the packer does not know yet under a provisional id
+// (PROV | its index in the part's new_keys), and the merge numbers the parts' new values in
+// chunk order — exactly the sequential numbering — and rewrites the (rare) objects that used
+// one, re-sorting their pair lists.  The output is identical to the sequential packer's.
+constexpr uint32_t PROV = 0x80000000u;       // > every final id (< ESC_PAIR_LIMIT)
+int64_t par_min() {                          // objects per call below which one thread packs
+    const char* v = std::getenv("ESC_PACK_PAR_MIN");    // (tests lower it)
+    return v ? std::max<int64_t>(1, std::atoll(v)) : (int64_t)1 << 16;
+}
+
+int host_threads() {
+    int n = 0;
+    for (const char* e : {"ESC_HOST_THREADS", "OMP_NUM_THREADS"})
+        if (const char* v = std::getenv(e)) { n = std::atoi(v); if (n > 0) break; }
+    if (n <= 0) n = std::min<int>(16, std::max(1u, std::thread::hardware_concurrency()));
+    return std::max(1, std::min(n, 64));
+}
+
+struct Fix {                                  // an object whose pairs hold provisional ids
+    int64_t item, xoff;                       // part-local index, its first extra pair
+};
+
+struct Part {
+    // pods (HostSnapshot names)
+    hvec<uint32_t> flags, cpu0, pair0, xp;
+    hvec<int64_t> mem0, xc_cpu, xc_mem;
+    // nodes
+    hvec<uint32_t> nflags, label0, xl;
+    hvec<int64_t> ncpu, nmem, created;
+    std::vector<std::string> names;
+    // the part's interner of values the packer did not know
+    std::vector<std::string> new_keys;
+    std::unordered_map<std::string, uint32_t> local;
+    std::vector<Fix> fix;
+    int32_t rc = ESC_OK;
+};
+
+template <class F>
+void run_parts(int64_t n, int T, F f) {
+    std::vector<std::thread> th;
+    th.reserve(T);
+    for (int t = 0; t < T; ++t) th.emplace_back([&, t] { f(t, n * t / T, n * (t + 1) / T); });
+    for (auto& x : th) x.join();
+}
+
+// the provisional-id interner of part P (the packer's known values are read-only meanwhile)
+struct PartIntern {
+    const esc_packer* pk;
+    Part& P;
+    bool used = false;
+    bool operator()(const char* k, const char* v, uint32_t& id) {
+        id = pk->gi->pair_id(k, v);
+        if (id != NONE) return true;
+        std::string key = GroupIndex::pair_key(k, v);
+        auto it = pk->other_pairs.find(key);
+        if (it != pk->other_pairs.end()) { id = it->second; return true; }
+        auto jt = P.local.find(key);
+        if (jt == P.local.end()) {
+            jt = P.local.emplace(key, PROV | (uint32_t)P.new_keys.size()).first;
+            P.new_keys.push_back(std::move(key));
+        }
+        id = jt->second;
+        used = true;
+        return true;
+    }
+};
+
+// Number the parts' new values in chunk order; remap[t][i] = final id of part t's value i.
+int32_t merge_keys(esc_packer* pk, std::vector<Part>& parts, std::vector<std::vector<uint32_t>>& remap) {
+    remap.assign(parts.size(), {});
+    for (size_t t = 0; t < parts.size(); ++t)
+        for (const std::string& key : parts[t].new_keys) {
+            auto it = pk->other_pairs.find(key);
+            uint32_t id;
+            if (it != pk->other_pairs.end()) {
+                id = it->second;
+            } else {
+                const uint64_t nid = (uint64_t)pk->gi->n_gp + pk->other_pairs.size();
+                if (nid >= ESC_PAIR_LIMIT) return ESC_E_LIMIT;
+                id = (uint32_t)nid;
+                pk->other_pairs.emplace(key, id);
+            }
+            remap[t].push_back(id);
+        }
+    return ESC_OK;
+}
+
+// The pair list (head + extras) of a fixed object with final ids, ascending again.
+void refix(uint32_t& head, uint32_t* extra, uint32_t n_extra, const std::vector<uint32_t>& remap,
+           std::vector<uint32_t>& tmp) {
+    tmp.clear();
+    if (head != NONE) tmp.push_back(head);
+    tmp.insert(tmp.end(), extra, extra + n_extra);
+    for (uint32_t& q : tmp)
+        if (q != NONE && (q & PROV)) q = remap[q & ~PROV];
+    std::sort(tmp.begin(), tmp.end());
+    if (head != NONE) head = tmp[0];
+    for (uint32_t k = 0; k < n_extra; ++k) extra[k] = tmp[k + 1];
+}
+
+template <class T, class A>
+void append_at(hvec<T>& dst, size_t at, const std::vector<T, A>& src) {
+    if (!src.empty()) std::memcpy(dst.data() + at, src.data(), src.size() * sizeof(T));
+}
+
+int32_t add_pods_parallel(esc_packer* pk, const esc_pod_obj* pods, int64_t n, int T) {
+    std::vector<Part> parts(T);
+    run_parts(n, T, [&](int t, int64_t lo, int64_t hi) {
+        Part& P = parts[t];
+        P.flags.reserve(hi - lo); P.cpu0.reserve(hi - lo); P.mem0.reserve(hi - lo); P.pair0.reserve(hi - lo);
+        PartIntern in{pk, P};
+        std::vector<uint32_t> scratch;
+        for (int64_t i = lo; i < hi; ++i) {
+            in.used = false;
+            const int64_t xo = (int64_t)P.xp.size();
+            const int32_t rc = pack_pod(pk->gi, pk->list_mode, pods[i], P, in, scratch);
+            if (rc != ESC_OK) { P.rc = rc; return; }
+            if (in.used) P.fix.push_back({i - lo, xo});
+        }
+    });
+    for (const Part& P : parts)
+        if (P.rc != ESC_OK) return P.rc;
+    std::vector<std::vector<uint32_t>> remap;
+    if (int32_t rc = merge_keys(pk, parts, remap)) return rc;
+    HostSnapshot& s = pk->s;
+    std::vector<size_t> b0(T + 1), bx(T + 1), bp(T + 1);
+    b0[0] = s.flags.size(); bx[0] = s.xc_cpu.size(); bp[0] = s.xp.size();
+    for (int t = 0; t < T; ++t) {
+        b0[t + 1] = b0[t] + parts[t].flags.size();
+        bx[t + 1] = bx[t] + parts[t].xc_cpu.size();
+        bp[t + 1] = bp[t] + parts[t].xp.size();
+    }
+    s.flags.resize(b0[T]); s.cpu0.resize(b0[T]); s.mem0.resize(b0[T]); s.pair0.resize(b0[T]);
+    s.xc_cpu.resize(bx[T]); s.xc_mem.resize(bx[T]); s.xp.resize(bp[T]);
+    run_parts(T, T, [&](int t, int64_t, int64_t) {
+        Part& P = parts[t];
+        std::vector<uint32_t> tmp;
+        for (const Fix& x : P.fix)
+            refix(P.pair0[x.item], P.xp.data() + x.xoff, pf_xpair(P.flags[x.item]), remap[t], tmp);
+        append_at(s.flags, b0[t], P.flags); append_at(s.cpu0, b0[t], P.cpu0);
+        append_at(s.mem0, b0[t], P.mem0); append_at(s.pair0, b0[t], P.pair0);
+        append_at(s.xc_cpu, bx[t], P.xc_cpu); append_at(s.xc_mem, bx[t], P.xc_mem);
+        append_at(s.xp, bp[t], P.xp);
+        P = Part();                                   // free the part early
+    });
+    return ESC_OK;
+}
+
+int32_t add_nodes_parallel(esc_packer* pk, const esc_node_obj* nodes, int64_t n, int T) {
+    std::vector<Part> parts(T);
+    run_parts(n, T, [&](int t, int64_t lo, int64_t hi) {
+        Part& P = parts[t];
+        PartIntern in{pk, P};
+        std::vector<uint32_t> scratch;
+        for (int64_t i = lo; i < hi; ++i) {
+            in.used = false;
+            const int64_t xo = (int64_t)P.xl.size();
+            const int32_t rc = pack_node(pk->gi, pk->list_mode, nodes[i], P, P.names, in, scratch);
+            if (rc != ESC_OK) { P.rc = rc; return; }
+            if (in.used) P.fix.push_back({i - lo, xo});
+        }
+    });
+    for (const Part& P : parts)
+        if (P.rc != ESC_OK) return P.rc;
+    std::vector<std::vector<uint32_t>> remap;
+    if (int32_t rc = merge_keys(pk, parts, remap)) return rc;
+    HostSnapshot& s = pk->s;
+    std::vector<size_t> b0(T + 1), bl(T + 1);
+    b0[0] = s.nflags.size(); bl[0] = s.xl.size();
+    for (int t = 0; t < T; ++t) {
+        b0[t + 1] = b0[t] + parts[t].nflags.size();
+        bl[t + 1] = bl[t] + parts[t].xl.size();
+    }
+    s.nflags.resize(b0[T]); s.label0.resize(b0[T]); s.ncpu.resize(b0[T]); s.nmem.resize(b0[T]);
+    s.created.resize(b0[T]); s.xl.resize(bl[T]);
+    run_parts(T, T, [&](int t, int64_t, int64_t) {
+        Part& P = parts[t];
+        std::vector<uint32_t> tmp;
+        for (const Fix& x : P.fix)
+            refix(P.label0[x.item], P.xl.data() + x.xoff, nf_xlbl(P.nflags[x.item]), remap[t], tmp);
+        append_at(s.nflags, b0[t], P.nflags); append_at(s.label0, b0[t], P.label0);
+        append_at(s.ncpu, b0[t], P.ncpu); append_at(s.nmem, b0[t], P.nmem);
+        append_at(s.created, b0[t], P.created); append_at(s.xl, bl[t], P.xl);
+    });
+    for (Part& P : parts)                             // names in order (one thread: strings)
+        for (std::string& nm : P.names) pk->node_names.emplace_back(std::move(nm));
     return ESC_OK;
 }
 
@@ -260,8 +459,12 @@ int32_t esc_packer_set_list_mode(esc_packer* pk, int32_t list_mode) {
 int32_t esc_packer_add_pods(esc_packer* pk, const esc_pod_obj* pods, int64_t n) {
     if (!pk || (n > 0 && !pods) || n < 0) return ESC_E_INVAL;
     if (pk->finished) return ESC_E_STATE;
+    const int T = host_threads();
+    if (n >= par_min() && T > 1) return add_pods_parallel(pk, pods, n, T);
+    auto in = [pk](const char* k, const char* v, uint32_t& id) { return intern(pk, k, v, id); };
+    std::vector<uint32_t> scratch;
     for (int64_t i = 0; i < n; ++i) {
-        int32_t rc = pack_pod(pk, pods[i]);
+        int32_t rc = pack_pod(pk->gi, pk->list_mode, pods[i], pk->s, in, scratch);
         if (rc != ESC_OK) return rc;
     }
     return ESC_OK;
@@ -270,8 +473,12 @@ int32_t esc_packer_add_pods(esc_packer* pk, const esc_pod_obj* pods, int64_t n) 
 int32_t esc_packer_add_nodes(esc_packer* pk, const esc_node_obj* nodes, int64_t n) {
     if (!pk || (n > 0 && !nodes) || n < 0) return ESC_E_INVAL;
     if (pk->finished) return ESC_E_STATE;
+    const int T = host_threads();
+    if (n >= par_min() && T > 1) return add_nodes_parallel(pk, nodes, n, T);
+    auto in = [pk](const char* k, const char* v, uint32_t& id) { return intern(pk, k, v, id); };
+    std::vector<uint32_t> scratch;
     for (int64_t i = 0; i < n; ++i) {
-        int32_t rc = pack_node(pk, nodes[i]);
+        int32_t rc = pack_node(pk->gi, pk->list_mode, nodes[i], pk->s, pk->node_names, in, scratch);
         if (rc != ESC_OK) return rc;
     }
     return ESC_OK;

@@ -192,3 +192,45 @@ def test_packer_over_generator_objects_equals_generator():
         pods = s.pods()
         assert np.array_equal(Pk["pair0"] < 0x7FFFFFFF, pods["pair0"] < 0x7FFFFFFF)
         assert np.array_equal(soa.totals(Pk, Nk, s.groups), soa.totals(pods, nodes, s.groups)), cfg
+
+
+_PACKER_CHILD = r"""
+import json, os, random, sys
+sys.path[:0] = [sys.argv[1], os.path.join(sys.argv[1], "tests")]
+from randobj import make_groups, make_nodes, make_pods, make_trackers
+from escalator_amd.context import Context
+rng = random.Random(int(sys.argv[2]))
+groups = make_groups(rng, 12, with_default=True)
+pods = make_pods(rng, 3000, groups)
+nodes = make_nodes(rng, 900, groups)
+trackers = make_trackers(rng, groups, nodes)
+P, N = Context(groups, device=-1).pack(pods, nodes, trackers)
+print(json.dumps({k: v.tolist() for k, v in list(P.items()) + [("n_" + k, v) for k, v in N.items()]}))
+"""
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_parallel_packer_equals_sequential(seed):
+    """The packer's multi-threaded path (parts packed per thread, provisional ids for values
+    no group selects, renumbered in chunk order at the merge) gives the sequential packer's
+    arrays exactly — pair ids included — on objects full of such values."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+    def run(threads, par_min):
+        env = dict(os.environ, ESC_HOST_THREADS=str(threads), ESC_PACK_PAR_MIN=str(par_min))
+        r = subprocess.run([sys.executable, "-c", _PACKER_CHILD, root, str(seed)], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return json.loads(r.stdout)
+
+    seq = run(1, 1 << 30)
+    for threads in (2, 7):
+        par = run(threads, 16)
+        assert par.keys() == seq.keys()
+        for k in seq:
+            assert par[k] == seq[k], (threads, k)
+    assert any(q >= 12 for q in seq["xp_pair"] + seq["pair0"] if q != 0xFFFFFFFF)   # values no group selects
