@@ -267,8 +267,8 @@ struct esc_ctx {
     esc::esc_multi_state* multi = nullptr;
     // incremental snapshot (§8f rank 1): where each loaded pod lives, free K slots
     double spare_frac = 0.0;                                  // esc_set_spare
-    std::vector<int32_t> pod_cls;                             // by pod id: K class index, -1 C, -2 absent
-    std::vector<int64_t> pod_pos;                             // K: position in its class; C: base-array index
+    hvec<int32_t> pod_cls;                                    // by pod id: K class index, -1 C, -2 absent
+    hvec<int64_t> pod_pos;                                    // K: position in its class; C: base-array index
     std::vector<std::vector<int64_t>> cls_free;               // per K class: free positions
     std::vector<PodClass> h_cls;
     std::vector<int> h_cls_of;                                // signature id -> class index (-1: none)
@@ -328,10 +328,33 @@ int ctx_device(const esc_ctx* c) { return c->device; }
 namespace {
 
 // A kb_write_pod / kb_write_free put into the host copy of the K blocks.
-void put_kb(std::vector<uint32_t>& kb, int width, int64_t at, uint64_t v) {
-    if (width == 8) reinterpret_cast<int64_t*>(kb.data())[at] = (int64_t)v;
+void put_kb(uint32_t* kb, int width, int64_t at, uint64_t v) {
+    if (width == 8) reinterpret_cast<int64_t*>(kb)[at] = (int64_t)v;
     else if (width == 4) kb[at] = (uint32_t)v;
-    else reinterpret_cast<uint16_t*>(kb.data())[at] = (uint16_t)v;
+    else reinterpret_cast<uint16_t*>(kb)[at] = (uint16_t)v;
+}
+
+// Host threads for the load-time layout passes: ESC_HOST_THREADS, else OMP_NUM_THREADS (the
+// GPU box sets 16, its CPU share per GPU), else min(16, hardware threads).
+int host_threads() {
+    int n = 0;
+    for (const char* e : {"ESC_HOST_THREADS", "OMP_NUM_THREADS"})
+        if (const char* v = std::getenv(e)) { n = std::atoi(v); if (n > 0) break; }
+    if (n <= 0) n = std::min<int>(16, std::max(1u, std::thread::hardware_concurrency()));
+    return std::max(1, std::min(n, 64));
+}
+
+// f(t, lo, hi) over T contiguous chunks of [0, n), one host thread each (in order for T = 1)
+template <class F>
+void par_chunks(int64_t n, int T, F&& f) {
+    if (T <= 1 || n < 4096) {
+        f(0, (int64_t)0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T);
+    for (int t = 0; t < T; ++t) th.emplace_back([&, t] { f(t, n * t / T, n * (t + 1) / T); });
+    for (auto& x : th) x.join();
 }
 
 // Spare C slots (esc_load_pods with esc_set_spare): room per slot, slots per 64-pod tile.
@@ -1306,53 +1329,73 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     if (n > 0 && (!p->flags || !p->cpu0 || !p->mem0 || !p->pair0)) return ESC_E_INVAL;
     if ((p->n_xc > 0 && (!p->xc_cpu || !p->xc_mem)) || (p->n_xp > 0 && !p->xp_pair)) return ESC_E_INVAL;
     if (p->n_xc >= (int64_t)0xFFFFFFFF || p->n_xp >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
-    // Validate the pair lists (ascending, unique, < ESC_PAIR_LIMIT: a pod matches each
-    // group at most once) and the record counts; count the pods with extra records.
-    uint64_t sc = 0, sp = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        const uint32_t f = p->flags[i];
-        const uint32_t nx = pf_xpair(f), nc = pf_xctr(f);
-        uint32_t last = p->pair0[i];
-        if (last == NONE ? nx != 0 : last >= ESC_PAIR_LIMIT) return ESC_E_INVAL;
-        if (sp + nx > (uint64_t)p->n_xp) return ESC_E_INVAL;
-        for (uint32_t k = 0; k < nx; ++k) {
-            const uint32_t q = p->xp_pair[sp + k];
-            if (q >= ESC_PAIR_LIMIT || q <= last) return ESC_E_INVAL;
-            last = q;
-        }
-        sc += nc;
-        sp += nx;
-    }
-    if ((int64_t)sc != p->n_xc || (int64_t)sp != p->n_xp) return ESC_E_INVAL;
-    // Layout.  Pods with at most 3 extra container records and at most 3
-    // extra pairs go to homogeneous K classes, one per record signature (extra regular /
-    // init containers, overhead, extra pairs), in 256-pod tiles whose records sit in
-    // per-tile rows; the rest go to 64-pod C tiles with per-tile record offsets.  Sums are
-    // order-independent, so the placement changes no result.  Padding pods carry
-    // ESC_PF_DAEMONSET, padding records are 0 and padding pairs NONE.
-    // class id = record signature | packed << 7 (the pod's values fit the packed block,
-    // esc_kernels.h kp_fits; the packed class is listed first so that K1 streams it first)
-    std::vector<int16_t> pid(n);
-    std::vector<int64_t> cnt(POD_CLASS_IDS, 0);
-    uint64_t sc_c = 0, sp_c = 0;
-    int64_t n_c = 0;
-    {
-        uint64_t rc = 0;
-        for (int64_t i = 0; i < n; ++i) {
+    // The host layout runs in T chunks of the pods, one host thread each: per
+    // chunk counts, then exact prefixes over the chunks, so every pod lands where the
+    // one-pass sequential layout put it.
+    const int T = n >= (1 << 16) ? host_threads() : 1;
+    const int64_t TT = (n >= (1 << 16) && T > 1) ? T : 1;
+    // (1) records and extra pairs of each chunk: its pods' offsets into xc / xp
+    std::vector<uint64_t> ch_c(TT + 1, 0), ch_p(TT + 1, 0);
+    par_chunks(n, (int)TT, [&](int t, int64_t lo, int64_t hi) {
+        uint64_t a = 0, b = 0;
+        for (int64_t i = lo; i < hi; ++i) { a += pf_xctr(p->flags[i]); b += pf_xpair(p->flags[i]); }
+        ch_c[t + 1] = a;
+        ch_p[t + 1] = b;
+    });
+    for (int64_t t = 0; t < TT; ++t) { ch_c[t + 1] += ch_c[t]; ch_p[t + 1] += ch_p[t]; }
+    if ((int64_t)ch_c[TT] != p->n_xc || (int64_t)ch_p[TT] != p->n_xp) return ESC_E_INVAL;
+    // (2) validate the pair lists (ascending, unique, < ESC_PAIR_LIMIT: a pod matches each
+    // group at most once); the class of every pod: pods with at most 3 extra
+    // container records and at most 3 extra pairs go to homogeneous K classes, one per record
+    // signature, in 256-pod tiles whose records sit in per-tile rows; the rest go to 64-pod C
+    // tiles with per-tile record offsets.  Sums are order-independent, so the placement
+    // changes no result.  Padding pods carry ESC_PF_DAEMONSET, padding records are 0 and
+    // padding pairs NONE.  class id = record signature | packed << 7 (the pod's values fit the
+    // packed block, esc_kernels.h kp_fits; the packed class is listed first so that K1
+    // streams it first)
+    hvec<int16_t> pid(n);
+    std::vector<std::vector<int64_t>> ch_cnt(TT, std::vector<int64_t>(POD_CLASS_IDS, 0));
+    std::vector<int64_t> ch_nc(TT + 1, 0);
+    std::vector<uint64_t> ch_sc(TT + 1, 0), ch_sp(TT + 1, 0);
+    std::vector<int32_t> ch_rc(TT, ESC_OK);
+    par_chunks(n, (int)TT, [&](int t, int64_t lo, int64_t hi) {
+        uint64_t rc = ch_c[t], sp = ch_p[t];
+        auto& cn = ch_cnt[t];
+        for (int64_t i = lo; i < hi; ++i) {
             const uint32_t f = p->flags[i];
+            const uint32_t nx = pf_xpair(f), nc = pf_xctr(f);
+            uint32_t last = p->pair0[i];
+            if (last == NONE ? nx != 0 : last >= ESC_PAIR_LIMIT) { ch_rc[t] = ESC_E_INVAL; return; }
+            for (uint32_t k = 0; k < nx; ++k) {
+                const uint32_t q = p->xp_pair[sp + k];
+                if (q >= ESC_PAIR_LIMIT || q <= last) { ch_rc[t] = ESC_E_INVAL; return; }
+                last = q;
+            }
             const int id = pod_class_id(f, p->cpu0[i], p->mem0[i], p->pair0[i], p->xc_cpu ? p->xc_cpu + rc : nullptr,
                                         p->xc_mem ? p->xc_mem + rc : nullptr, c->gi.n_gp);
             pid[i] = (int16_t)id;
-            rc += pf_xctr(f);
             if (id >= 0) {
-                ++cnt[id];
+                ++cn[id];
             } else {
-                ++n_c;
-                sc_c += pf_xctr(f);
-                sp_c += pf_xpair(f);
+                ++ch_nc[t + 1];
+                ch_sc[t + 1] += nc;
+                ch_sp[t + 1] += nx;
             }
+            rc += nc;
+            sp += nx;
         }
+    });
+    for (int32_t r : ch_rc)
+        if (r) return r;
+    std::vector<int64_t> cnt(POD_CLASS_IDS, 0);
+    for (int64_t t = 0; t < TT; ++t) {
+        for (int id = 0; id < POD_CLASS_IDS; ++id) cnt[id] += ch_cnt[t][id];
+        ch_nc[t + 1] += ch_nc[t];
+        ch_sc[t + 1] += ch_sc[t];
+        ch_sp[t + 1] += ch_sp[t];
     }
+    const int64_t n_c = ch_nc[TT];
+    const uint64_t sc_c = ch_sc[TT], sp_c = ch_sp[TT];
     std::vector<PodClass> cls;
     std::vector<int> cls_of(POD_CLASS_IDS, -1);
     int64_t kt = 0, kbw = 0, kw = 0;
@@ -1398,53 +1441,75 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     std::vector<uint32_t> hf(npad, ESC_PF_DAEMONSET), hc(npad, 0), hp(npad, NONE);
     std::vector<int64_t> hm(npad, 0), hxc(nxc_dev, 0), hxm(nxc_dev, 0);
     std::vector<uint32_t> hxp(nxp_dev, NONE);
-    // K blocks: padding pods are daemonset-flagged with no pairs, padding records 0
-    std::vector<uint32_t> hkb((size_t)kbw, 0);
-    for (const PodClass& k : cls)
-        for (int64_t t = k.t0; t < k.t1; ++t) {
-            const int64_t blk = kb_block(k, t);
-            for (int64_t sl = 0; sl < TILE; ++sl)
-                kb_write_free(k, blk, sl, [&](int width, int64_t at, uint64_t v) { put_kb(hkb, width, at, v); });
-            if (!k.packed) std::fill(hkb.begin() + blk + KB_PAIR0, hkb.begin() + blk + KB_PAIR0 + TILE, NONE);
-            const int64_t x0 = kb_xp_row0(k, blk);         // no pairs (u32 or u16 NONE)
-            std::fill(hkb.begin() + x0, hkb.begin() + x0 + kb_xp_words(k), NONE);
-        }
+    // (3) K blocks, every tile first as padding (daemonset-flagged pods with no pairs,
+    // records 0), tiles split over the threads
+    hvec<uint32_t> hkb((size_t)std::max<int64_t>(kbw, 1));
+    {
+        std::vector<std::pair<int, int64_t>> tl;          // (class, first tile) of each class
+        for (int ci = 0; ci < (int)cls.size(); ++ci) tl.emplace_back(ci, cls[ci].t0);
+        par_chunks(k_tiles, (int)TT, [&](int, int64_t lo, int64_t hi) {
+            int ci = 0;
+            for (int64_t t = lo; t < hi; ++t) {
+                while (cls[ci].t1 <= t) ++ci;
+                const PodClass& k = cls[ci];
+                const int64_t blk = kb_block(k, t);
+                std::memset(hkb.data() + blk, 0, (size_t)k.wt * KB_UNIT * 4);
+                for (int64_t sl = 0; sl < TILE; ++sl)
+                    kb_write_free(k, blk, sl, [&](int width, int64_t at, uint64_t v) { put_kb(hkb.data(), width, at, v); });
+                if (!k.packed) std::fill(hkb.begin() + blk + KB_PAIR0, hkb.begin() + blk + KB_PAIR0 + TILE, NONE);
+                const int64_t x0 = kb_xp_row0(k, blk);     // no pairs (u32 or u16 NONE)
+                std::fill(hkb.begin() + x0, hkb.begin() + x0 + kb_xp_words(k), NONE);
+            }
+        });
+    }
     std::vector<uint32_t> xc_base(c_tiles + 1, 0), xp_base(c_tiles + 1, 0);
-    std::vector<int32_t> pod_cls(n);
-    std::vector<int64_t> pod_pos(n);
-    // positions inside each class: counting sort by bucket = pair0 / pod_sort (NONE and
-    // pairs no group selects last); input order inside a bucket
+    hvec<int32_t> pod_cls(n);
+    hvec<int64_t> pod_pos(n);
+    // (4) positions inside each class: counting sort by bucket = pair0 / pod_sort (NONE and
+    // pairs no group selects last); input order inside a bucket, so chunk t's pods of a
+    // (class, bucket) follow every earlier chunk's
     const uint32_t sw = c->pod_sort, n_gp = c->gi.n_gp;
     const int64_t nbk = sw ? (int64_t)(n_gp / sw) + 2 : 1;
     auto bucket = [&](uint32_t q0) -> int64_t { return sw ? (q0 < n_gp ? (int64_t)(q0 / sw) : nbk - 1) : 0; };
-    std::vector<std::vector<int64_t>> next(POD_CLASS_IDS);
+    std::vector<int> dense(POD_CLASS_IDS, -1);
+    int n_dense = 0;
     for (int id = 0; id < POD_CLASS_IDS; ++id)
-        if (cnt[id]) next[id].assign(nbk, 0);
-    if (sw) {
-        for (int64_t i = 0; i < n; ++i)
-            if (pid[i] >= 0) ++next[pid[i]][bucket(p->pair0[i])];
-        for (auto& v : next) {
-            int64_t acc = 0;
-            for (int64_t& x : v) { const int64_t t = x; x = acc; acc += t; }
-        }
+        if (cnt[id]) dense[id] = n_dense++;
+    const int64_t nb_all = (int64_t)n_dense * nbk;
+    std::vector<std::vector<int64_t>> ch_next(TT, std::vector<int64_t>(nb_all, 0));
+    par_chunks(n, (int)TT, [&](int t, int64_t lo, int64_t hi) {
+        auto& v = ch_next[t];
+        for (int64_t i = lo; i < hi; ++i)
+            if (pid[i] >= 0) ++v[dense[pid[i]] * nbk + bucket(p->pair0[i])];
+    });
+    for (int64_t a = 0; a < n_dense; ++a) {              // class-local starts, bucket-major, chunk order
+        int64_t acc = 0;
+        for (int64_t bk = 0; bk < nbk; ++bk)
+            for (int64_t t = 0; t < TT; ++t) {
+                int64_t& x = ch_next[t][a * nbk + bk];
+                const int64_t v = x;
+                x = acc;
+                acc += v;
+            }
     }
-    {
-        int64_t ic = 0;
-        uint64_t rc = 0, rp = 0;                          // the pod's records in the input
-        uint64_t oc = 0, op = 0;                          // C record cursors
-        for (int64_t i = 0; i < n; ++i) {
+    par_chunks(n, (int)TT, [&](int t, int64_t lo, int64_t hi) {
+        auto& next = ch_next[t];
+        int64_t ic = ch_nc[t];
+        uint64_t rc = ch_c[t], rp = ch_p[t];               // the pod's records in the input
+        uint64_t oc = ch_sc[t], op = ch_sp[t];             // C record cursors
+        for (int64_t i = lo; i < hi; ++i) {
             const uint32_t f = p->flags[i];
             const uint32_t nx = pf_xpair(f), nc = pf_xctr(f);
             const int id = pid[i];
             if (id >= 0) {
                 const PodClass& k = cls[cls_of[id]];
-                const int64_t q = next[id][bucket(p->pair0[i])]++, sl = q % TILE;
+                const int64_t q = next[dense[id] * nbk + bucket(p->pair0[i])]++, sl = q % TILE;
                 pod_cls[i] = cls_of[id];
                 pod_pos[i] = q;
                 const int64_t blk = kb_block(k, k.t0 + q / TILE);
                 kb_write_pod(k, blk, sl, f, p->cpu0[i], p->mem0[i], p->pair0[i], nc ? p->xc_cpu + rc : nullptr,
                              nc ? p->xc_mem + rc : nullptr, nx ? p->xp_pair + rp : nullptr,
-                             [&](int width, int64_t at, uint64_t v) { put_kb(hkb, width, at, v); });
+                             [&](int width, int64_t at, uint64_t v) { put_kb(hkb.data(), width, at, v); });
             } else {
                 if (ic % CTILE == 0) { xc_base[ic / CTILE] = (uint32_t)oc; xp_base[ic / CTILE] = (uint32_t)op; }
                 const int64_t d = ic++;                   // C-array index (slot c0 + d)
@@ -1459,6 +1524,9 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
             rc += nc;
             rp += nx;
         }
+    });
+    {
+        uint64_t oc = sc_c, op = sp_c;
         for (int64_t t = c_real; t < c_tiles; ++t) {         // spare C tiles: free slots with room
             xc_base[t] = (uint32_t)oc;
             xp_base[t] = (uint32_t)op;

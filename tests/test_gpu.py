@@ -539,7 +539,7 @@ def test_node_relabel_vs_literal(esc, seed):
     trackers = make_trackers(rng, groups, nodes)
     states = make_states(rng, G)
     ctx = esc.Context(groups)
-    ctx.set_spare(2.0)
+    ctx.set_spare(4.0)
     P, N = ctx.pack(pods, nodes, trackers)
     ctx.load(P, N)
     if seed % 2:
@@ -547,13 +547,27 @@ def test_node_relabel_vs_literal(esc, seed):
     live = dict(enumerate(nodes))
     hw = len(nodes)
     _check_nodes_vs_literal(ctx, groups, states, pods, live, trackers, "load")
+    in_place = 0
     for rnd in range(5):
-        ids = rng.sample(sorted(live), k=min(len(live), rng.randrange(1, 16)))
+        ids = rng.sample(sorted(live), k=min(len(live), rng.randrange(1, 10)))
         new = [_relabel(rng, live[j], groups, move_time=seed >= 2) for j in ids]
         _, packed = ctx.pack([], new)
-        ctx.nodes_relabel(ids, packed)
-        for j, x in zip(ids, new):
-            live[j] = x
+        before = ctx.decide_all(states)[0].tobytes()
+        try:
+            ctx.nodes_relabel(ids, packed)
+            in_place += 1
+        except esc._lib.EscError as e:                   # a small group's spare room is short
+            assert e.code == esc._lib.ESC_E_LIMIT
+            assert ctx.decide_all(states)[0].tobytes() == before          # nothing applied
+            for j, x in zip(ids, new):
+                live[j] = x
+            lst = [live[j] for j in sorted(live)]
+            ctx.load(*ctx.pack(pods, lst, trackers))
+            live = dict(enumerate(lst))
+            hw = len(lst)
+        else:
+            for j, x in zip(ids, new):
+                live[j] = x
         _check_nodes_vs_literal(ctx, groups, states, pods, live, trackers, (rnd, "relabel"))
         dels = rng.sample(sorted(live), k=min(len(live), rng.randrange(0, 4)))
         if dels:
@@ -565,12 +579,21 @@ def test_node_relabel_vs_literal(esc, seed):
             x["name"] = "r%d-add%d" % (rnd, k)
         if add:
             _, packed = ctx.pack([], add)
-            got = ctx.nodes_add(packed)
-            assert list(got) == list(range(hw, hw + len(add)))
-            for j, x in zip(got, add):
-                live[int(j)] = x
-            hw += len(add)
+            try:
+                got = ctx.nodes_add(packed)
+            except esc._lib.EscError as e:               # spare room short: reload
+                assert e.code == esc._lib.ESC_E_LIMIT
+                lst = [live[j] for j in sorted(live)] + add
+                ctx.load(*ctx.pack(pods, lst, trackers))
+                live = dict(enumerate(lst))
+                hw = len(lst)
+            else:
+                assert list(got) == list(range(hw, hw + len(add)))
+                for j, x in zip(got, add):
+                    live[int(j)] = x
+                hw += len(add)
         _check_nodes_vs_literal(ctx, groups, states, pods, live, trackers, (rnd, "add/delete"))
+    assert in_place >= 2, in_place
     before = {(g, w): list(ctx.group_order(g, w)) for g in range(G) for w in (0, 1)}
     ctx.build_age_index()
     ctx.sort_nodes()
@@ -1154,7 +1177,7 @@ def test_reaping_across_node_relabels(esc, seed):
     groups, pods, nodes, now_ns = make_reaping_cluster(rng, G, 800, 60)
     trackers = make_trackers(rng, groups, nodes)
     ctx = esc.Context(groups)
-    ctx.set_spare(1.0)
+    ctx.set_spare(4.0)
     P, N = ctx.pack(pods, nodes, trackers)
     ctx.load(P, N)
     pn, ts, nd = placement(pods, nodes)
@@ -1162,7 +1185,7 @@ def test_reaping_across_node_relabels(esc, seed):
     soft = np.full(G, 60 * 10**9, np.int64)
     hard = np.full(G, 4000 * 10**9, np.int64)
     for rnd in range(4):
-        ids = rng.sample(range(len(nodes)), 12)
+        ids = rng.sample(range(len(nodes)), 6)
         new = []
         for j in ids:
             x = _relabel(rng, nodes[j], groups, move_time=rnd % 2 == 1)

@@ -108,7 +108,7 @@ def test_multi_device_events_vs_literal(esc, seed):
     nodes = make_nodes(rng, 80, groups, big_frac=0.0)
     states = make_states(rng, G)
     ctx = esc.Context(groups, devices=[0, 0, 0])
-    ctx.set_spare(0.5)
+    ctx.set_spare(2.0)
     P, N = ctx.pack(pods, nodes)
     ctx.load(P, N)
     live = dict(enumerate(pods))
