@@ -3,6 +3,8 @@
 #pragma once
 
 #include <stdint.h>
+#include <algorithm>
+#include <cstring>
 #include <memory>
 #include <string>
 #include <type_traits>
@@ -13,6 +15,91 @@
 #include "esc_common.h"
 
 namespace esc {
+
+// Interning table for (key, value) label pairs (and bare keys): open addressing over a
+// 64-bit hash of the bytes "key\0value", the strings kept in one arena.  A lookup hashes the
+// caller's C strings in place — no std::string is built per lookup, which dominated the
+// packer (several lookups per pod at 1-2 M objects/s on one thread with std::unordered_map).
+class PairTable {
+public:
+    // FNV-1a over the key bytes and a separator (not a byte of either string): the state a
+    // key's values continue from, so a key is hashed once for all of its values
+    static uint64_t key_state(const char* k, size_t& kl) {
+        uint64_t h = 0xcbf29ce484222325ull;
+        const char* p = k ? k : "";
+        for (; *p; ++p) h = (h ^ (uint8_t)*p) * 0x100000001b3ull;
+        kl = (size_t)(p - (k ? k : ""));
+        return (h ^ 0xFFu) * 0x100000001b3ull;
+    }
+    static uint64_t finish(uint64_t h) {
+        h ^= h >> 33;
+        h *= 0xff51afd7ed558ccdull;
+        h ^= h >> 33;
+        return h;
+    }
+    static uint64_t value_hash(uint64_t ks, const char* v, size_t& vl) {
+        const char* q = v ? v : "";
+        for (; *q; ++q) ks = (ks ^ (uint8_t)*q) * 0x100000001b3ull;
+        vl = (size_t)(q - (v ? v : ""));
+        return finish(ks);
+    }
+    static uint64_t hash(const char* k, const char* v, size_t& kl, size_t& vl) {
+        return value_hash(key_state(k, kl), v, vl);
+    }
+    // id of (k, v), or NONE
+    uint32_t find(const char* k, const char* v) const {
+        size_t kl, vl;
+        const uint64_t h = hash(k, v, kl, vl);
+        return find_h(h, k ? k : "", kl, v ? v : "", vl);
+    }
+    uint32_t find_h(uint64_t h, const char* k, size_t kl, const char* v, size_t vl) const {
+        if (slots_.empty()) return NONE;
+        for (size_t i = h & mask_;; i = (i + 1) & mask_) {
+            const Slot& s = slots_[i];
+            if (s.id == NONE) return NONE;
+            if (s.h == h && s.kl == kl && s.vl == vl && std::memcmp(arena_.data() + s.off, k, kl) == 0 &&
+                std::memcmp(arena_.data() + s.off + kl, v, vl) == 0)
+                return s.id;
+        }
+    }
+    // inserts (k, v) -> id (the caller checked it is absent)
+    void insert_h(uint64_t h, const char* k, size_t kl, const char* v, size_t vl, uint32_t id) {
+        if ((n_ + 1) * 2 > slots_.size()) grow();
+        const size_t off = arena_.size();
+        arena_.append(k, kl);
+        arena_.append(v, vl);
+        place(Slot{h, off, (uint32_t)kl, (uint32_t)vl, id});
+        ++n_;
+    }
+    void insert(const char* k, const char* v, uint32_t id) {
+        size_t kl, vl;
+        const uint64_t h = hash(k, v, kl, vl);
+        insert_h(h, k ? k : "", kl, v ? v : "", vl, id);
+    }
+    size_t size() const { return n_; }
+
+private:
+    struct Slot {
+        uint64_t h = 0;
+        size_t off = 0;
+        uint32_t kl = 0, vl = 0, id = NONE;
+    };
+    void place(const Slot& x) {
+        for (size_t i = x.h & mask_;; i = (i + 1) & mask_)
+            if (slots_[i].id == NONE) { slots_[i] = x; return; }
+    }
+    void grow() {
+        std::vector<Slot> old;
+        old.swap(slots_);
+        slots_.assign(std::max<size_t>(64, old.size() * 2), Slot{});
+        mask_ = slots_.size() - 1;
+        for (const Slot& x : old)
+            if (x.id != NONE) place(x);
+    }
+    std::vector<Slot> slots_;
+    std::string arena_;
+    size_t mask_ = 0, n_ = 0;
+};
 
 // Owned copy of one NodeGroupOptions' hot-path fields.
 struct GroupSpecCopy {
@@ -44,12 +131,14 @@ struct GroupIndex {
         s.append(v ? v : "");
         return s;
     }
+    PairTable fast_pairs, fast_keys;                       // the same sets, for the packer's lookups
     void build(const esc_group_spec* specs, int32_t n);
-    uint32_t pair_id(const char* k, const char* v) const {
-        auto it = pair_ids.find(pair_key(k, v));
-        return it == pair_ids.end() ? NONE : it->second;
+    uint32_t pair_id(const char* k, const char* v) const { return fast_pairs.find(k, v); }
+    bool is_key(const char* k) const { return fast_keys.find(k, "") != NONE; }
+    // is_key given the key's hash state (PairTable::key_state)
+    bool is_key_s(uint64_t ks, const char* k, size_t kl) const {
+        return fast_keys.find_h(PairTable::finish(ks), k, kl, "", 0) != NONE;
     }
-    bool is_key(const char* k) const { return keys.count(std::string(k ? k : "")) != 0; }
 };
 
 // std::vector whose resize() leaves new elements default-initialised (no zero fill): the

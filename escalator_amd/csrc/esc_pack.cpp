@@ -60,6 +60,13 @@ void GroupIndex::build(const esc_group_spec* specs, int32_t n) {
         node_groups[id].push_back((uint32_t)g | (groups[g].spec.dry_mode ? NODE_DRY_BIT : 0u));
     }
     n_gp = (uint32_t)pair_ids.size();
+    fast_pairs = PairTable();
+    fast_keys = PairTable();
+    for (int32_t g = 0; g < n; ++g) {
+        if (fast_pairs.find(groups[g].key.c_str(), groups[g].value.c_str()) == NONE)
+            fast_pairs.insert(groups[g].key.c_str(), groups[g].value.c_str(), gpair[g]);
+        if (fast_keys.find(groups[g].key.c_str(), "") == NONE) fast_keys.insert(groups[g].key.c_str(), "", 1);
+    }
     code_list.clear();
     auto encode = [&](const std::vector<uint32_t>& gs) -> uint32_t {
         if (gs.empty()) return NONE;
@@ -95,7 +102,7 @@ struct esc_packer {
     HostSnapshot s;
     std::vector<std::string> node_names;
     std::vector<std::vector<std::string>> trackers;
-    std::unordered_map<std::string, uint32_t> other_pairs;   // group-key values no group selects
+    PairTable other_pairs;                                   // group-key values no group selects
 };
 
 namespace {
@@ -105,16 +112,18 @@ inline int64_t req_or(int32_t has, int64_t v, int64_t absent) { return has ? v :
 // Pair id of (key, value) for a key some group uses: the group pair's id, or a
 // packer-local id >= n_gp for a value no group selects (the numbering rule of
 // include/escalator_hip.h).  Returns false when the id space is exhausted.
-bool intern(esc_packer* pk, const char* k, const char* v, uint32_t& id) {
-    id = pk->gi->pair_id(k, v);
+bool intern(esc_packer* pk, const char* k, size_t kl, uint64_t ks, const char* v, uint32_t& id) {
+    size_t vl;
+    const uint64_t h = PairTable::value_hash(ks, v, vl);
+    v = v ? v : "";
+    id = pk->gi->fast_pairs.find_h(h, k, kl, v, vl);
     if (id != NONE) return true;
-    const std::string key = GroupIndex::pair_key(k, v);
-    auto it = pk->other_pairs.find(key);
-    if (it != pk->other_pairs.end()) { id = it->second; return true; }
+    id = pk->other_pairs.find_h(h, k, kl, v, vl);
+    if (id != NONE) return true;
     const uint64_t nid = (uint64_t)pk->gi->n_gp + pk->other_pairs.size();
     if (nid >= ESC_PAIR_LIMIT) return false;
     id = (uint32_t)nid;
-    pk->other_pairs.emplace(key, id);
+    pk->other_pairs.insert_h(h, k, kl, v, vl, id);
     return true;
 }
 
@@ -123,8 +132,8 @@ void sort_unique(std::vector<uint32_t>& v) {
     v.erase(std::unique(v.begin(), v.end()), v.end());
 }
 
-// One pod into `s` (HostSnapshot or a parallel part: the same member names); `in(k, v, id)`
-// interns a pair.  `pairs` is scratch.
+// One pod into `s` (HostSnapshot or a parallel part: the same member names); `in(k, kl,
+// key_state, v, id)` interns a pair.  `pairs` is scratch.
 template <class Out, class Intern>
 int32_t pack_pod(const GroupIndex* gi, bool list_mode, const esc_pod_obj& o, Out& s, Intern&& in,
                  std::vector<uint32_t>& pairs) {
@@ -144,19 +153,25 @@ int32_t pack_pod(const GroupIndex* gi, bool list_mode, const esc_pod_obj& o, Out
         // a pod once however many routes match.  K1 resolves pair -> groups.
         for (int32_t i = 0; i < o.n_node_selector; ++i) {
             const esc_kv& kv = o.node_selector[i];
-            if (!gi->is_key(kv.key)) continue;
+            size_t kl;
+            const uint64_t ks = PairTable::key_state(kv.key, kl);
+            const char* k = kv.key ? kv.key : "";
+            if (!gi->is_key_s(ks, k, kl)) continue;
             uint32_t id;
-            if (!in(kv.key, kv.value, id)) return ESC_E_LIMIT;
+            if (!in(k, kl, ks, kv.value, id)) return ESC_E_LIMIT;
             pairs.push_back(id);
         }
         if (o.has_affinity && o.has_node_affinity && o.has_required) {     // unwrapNodeSelectorTerms :208
             for (int32_t e = 0; e < o.n_exprs; ++e) {
                 const esc_selector_expr& x = o.exprs[e];
                 if (!x.op || std::strcmp(x.op, "In") != 0) continue;         // only In (:241)
-                if (!gi->is_key(x.key)) continue;
+                size_t kl;
+                const uint64_t ks = PairTable::key_state(x.key, kl);
+                const char* k = x.key ? x.key : "";
+                if (!gi->is_key_s(ks, k, kl)) continue;
                 for (int32_t v = 0; v < x.n_values; ++v) {
                     uint32_t id;
-                    if (!in(x.key, x.values[v], id)) return ESC_E_LIMIT;
+                    if (!in(k, kl, ks, x.values[v], id)) return ESC_E_LIMIT;
                     pairs.push_back(id);
                 }
             }
@@ -217,9 +232,12 @@ int32_t pack_node(const GroupIndex* gi, bool list_mode, const esc_node_obj& o, O
         for (int32_t i = 0; i < o.n_taints; ++i)                             // taint.go:81-85
             if (o.taint_keys[i] && std::strcmp(o.taint_keys[i], "atlassian.com/escalator") == 0) { f |= ESC_NF_TAINTED; break; }
         for (int32_t i = 0; i < o.n_labels; ++i) {                           // node_group.go:280
-            if (!gi->is_key(o.labels[i].key)) continue;                      // Labels[K] for group keys
+            size_t kl;
+            const uint64_t ks = PairTable::key_state(o.labels[i].key, kl);
+            const char* k = o.labels[i].key ? o.labels[i].key : "";
+            if (!gi->is_key_s(ks, k, kl)) continue;                          // Labels[K] for group keys
             uint32_t id;
-            if (!in(o.labels[i].key, o.labels[i].value, id)) return ESC_E_LIMIT;
+            if (!in(k, kl, ks, o.labels[i].value, id)) return ESC_E_LIMIT;
             pairs.push_back(id);
         }
         sort_unique(pairs);
@@ -272,9 +290,9 @@ struct Part {
     hvec<uint32_t> nflags, label0, xl;
     hvec<int64_t> ncpu, nmem, created;
     std::vector<std::string> names;
-    // the part's interner of values the packer did not know
-    std::vector<std::string> new_keys;
-    std::unordered_map<std::string, uint32_t> local;
+    // the part's interner of values the packer did not know: (key, value) of each, in order
+    std::vector<std::pair<std::string, std::string>> new_keys;
+    PairTable local;
     std::vector<Fix> fix;
     int32_t rc = ESC_OK;
 };
@@ -292,18 +310,20 @@ struct PartIntern {
     const esc_packer* pk;
     Part& P;
     bool used = false;
-    bool operator()(const char* k, const char* v, uint32_t& id) {
-        id = pk->gi->pair_id(k, v);
+    bool operator()(const char* k, size_t kl, uint64_t ks, const char* v, uint32_t& id) {
+        size_t vl;
+        const uint64_t h = PairTable::value_hash(ks, v, vl);
+        v = v ? v : "";
+        id = pk->gi->fast_pairs.find_h(h, k, kl, v, vl);
         if (id != NONE) return true;
-        std::string key = GroupIndex::pair_key(k, v);
-        auto it = pk->other_pairs.find(key);
-        if (it != pk->other_pairs.end()) { id = it->second; return true; }
-        auto jt = P.local.find(key);
-        if (jt == P.local.end()) {
-            jt = P.local.emplace(key, PROV | (uint32_t)P.new_keys.size()).first;
-            P.new_keys.push_back(std::move(key));
+        id = pk->other_pairs.find_h(h, k, kl, v, vl);
+        if (id != NONE) return true;
+        id = P.local.find_h(h, k, kl, v, vl);
+        if (id == NONE) {
+            id = PROV | (uint32_t)P.new_keys.size();
+            P.local.insert_h(h, k, kl, v, vl, id);
+            P.new_keys.emplace_back(std::string(k, kl), std::string(v, vl));
         }
-        id = jt->second;
         used = true;
         return true;
     }
@@ -313,16 +333,13 @@ struct PartIntern {
 int32_t merge_keys(esc_packer* pk, std::vector<Part>& parts, std::vector<std::vector<uint32_t>>& remap) {
     remap.assign(parts.size(), {});
     for (size_t t = 0; t < parts.size(); ++t)
-        for (const std::string& key : parts[t].new_keys) {
-            auto it = pk->other_pairs.find(key);
-            uint32_t id;
-            if (it != pk->other_pairs.end()) {
-                id = it->second;
-            } else {
+        for (const auto& kv : parts[t].new_keys) {
+            uint32_t id = pk->other_pairs.find(kv.first.c_str(), kv.second.c_str());
+            if (id == NONE) {
                 const uint64_t nid = (uint64_t)pk->gi->n_gp + pk->other_pairs.size();
                 if (nid >= ESC_PAIR_LIMIT) return ESC_E_LIMIT;
                 id = (uint32_t)nid;
-                pk->other_pairs.emplace(key, id);
+                pk->other_pairs.insert(kv.first.c_str(), kv.second.c_str(), id);
             }
             remap[t].push_back(id);
         }
@@ -461,7 +478,9 @@ int32_t esc_packer_add_pods(esc_packer* pk, const esc_pod_obj* pods, int64_t n) 
     if (pk->finished) return ESC_E_STATE;
     const int T = host_threads();
     if (n >= par_min() && T > 1) return add_pods_parallel(pk, pods, n, T);
-    auto in = [pk](const char* k, const char* v, uint32_t& id) { return intern(pk, k, v, id); };
+    auto in = [pk](const char* k, size_t kl, uint64_t ks, const char* v, uint32_t& id) {
+        return intern(pk, k, kl, ks, v, id);
+    };
     std::vector<uint32_t> scratch;
     for (int64_t i = 0; i < n; ++i) {
         int32_t rc = pack_pod(pk->gi, pk->list_mode, pods[i], pk->s, in, scratch);
@@ -475,7 +494,9 @@ int32_t esc_packer_add_nodes(esc_packer* pk, const esc_node_obj* nodes, int64_t 
     if (pk->finished) return ESC_E_STATE;
     const int T = host_threads();
     if (n >= par_min() && T > 1) return add_nodes_parallel(pk, nodes, n, T);
-    auto in = [pk](const char* k, const char* v, uint32_t& id) { return intern(pk, k, v, id); };
+    auto in = [pk](const char* k, size_t kl, uint64_t ks, const char* v, uint32_t& id) {
+        return intern(pk, k, kl, ks, v, id);
+    };
     std::vector<uint32_t> scratch;
     for (int64_t i = 0; i < n; ++i) {
         int32_t rc = pack_node(pk->gi, pk->list_mode, nodes[i], pk->s, pk->node_names, in, scratch);

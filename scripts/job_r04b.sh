@@ -20,4 +20,7 @@ cat $OUT/smoke.log | tail -1
 echo "[job] $(date) events"
 timeout -k 10 600 python -u scripts/bench_events.py > $OUT/events.json 2> $OUT/events.err || { tail -30 $OUT/events.err; exit 1; }
 python -c "import json; d=json.load(open('$OUT/events.json')); d.pop('raw_s'); print(json.dumps(d))"
+echo "[job] $(date) reload"
+timeout -k 10 600 python -u scripts/bench_reload.py > $OUT/reload.json 2> $OUT/reload.err || { tail -30 $OUT/reload.err; exit 1; }
+python -c "import json; d=json.load(open('$OUT/reload.json')); d.pop('raw_s'); print(json.dumps(d))"
 echo "[job] $(date) done"
