@@ -404,6 +404,13 @@ func (x *Context) Load(pods []*v1.Pod, podOffset int64, nodes []*v1.Node, tracke
 	})
 }
 
+// SetSpare reserves room for informer events in the next Load (esc_set_spare): spare slots
+// per pod class, node table slots, pair-major entries and K5 region slots, as a fraction of
+// what the snapshot holds.  Events that do not fit return ErrReload.
+func (x *Context) SetSpare(fraction float64) error {
+	return rcErr("esc_set_spare", C.esc_set_spare(x.c, C.double(fraction)))
+}
+
 // Calibrate balances the pod pass's per-workgroup shares to this GPU's measured streaming
 // rates (esc_k1_calibrate: `rounds` untimed decisions with the current state; results are
 // unchanged).  Call it once after Load and the first RunOnce's state.
