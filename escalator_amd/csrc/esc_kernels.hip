@@ -1315,7 +1315,6 @@ __device__ __forceinline__ bool node_has_pair(const NodeDev& N, int64_t i, uint3
     return false;
 }
 
-constexpr int K2_WAVES = 4;
 
 
 }  // namespace
@@ -1341,8 +1340,9 @@ __device__ __forceinline__ void node_piece_block(const NodeDev& N, const GroupDe
         const uint32_t q = G.gpair[g];
         const int64_t plo = imax64((int64_t)N.pp_off[q], N.pc_lo), phi = imin64((int64_t)N.pp_off[q + 1], N.pc_hi);
         if (phi <= plo) return;
-        const uint32_t lo_node = N.e_node[N.piece_off[plo]], hi_node = N.e_node[N.piece_off[phi] - 1];
-        if ((uint32_t)j < lo_node || (uint32_t)j > hi_node || !node_has_pair(N, j, q)) return;
+        // membership from the node's own labels: the pair's entries are not node-sorted once
+        // relabels / adds have appended to them, and a removed first member leaves a spare
+        if ((N.flags[j] & ESC_NF_ABSENT) || !node_has_pair(N, j, q)) return;
         const int64_t c = N.cpu[j], m = N.mem[j];
         int64_t* r = trk_acc + (int64_t)g * TA_K;
         g_add(r + TA_CNT, 1);
@@ -1414,15 +1414,22 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 // buffer (D.nx) and k_decide runs after the SUM.
 constexpr int NG_WAVES = 4;
 
-__global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeDev N,
-                                                               const int64_t* __restrict__ node_rows,
-                                                               int64_t* __restrict__ trk_acc,
-                                                               int64_t* __restrict__ nwords, NGDecide D) {
+namespace {
+// k_node_groups' work for up to 64 groups, group gid (NONE: no group) on lane l of every
+// wave: the node words from the group pair's piece rows (the waves split the pieces), then
+// the decision or the exchange words.  With `seq` the groups are g_first + l and their
+// compact decisions go out as one contiguous run; else group by group (a fold column's).
+__device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDev& N,
+                                                 const int64_t* __restrict__ node_rows,
+                                                 int64_t* __restrict__ trk_acc, int64_t* __restrict__ nwords,
+                                                 const NGDecide& D, uint32_t gid, bool seq, int32_t g_first,
+                                                 uint32_t n_out) {
     __shared__ uint64_t red[NG_WAVES][6][64];
     __shared__ DecCompact sdec[64];
+    __shared__ uint32_t sid[64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int32_t g = blockIdx.x * 64 + lane;
-    const bool ok = g < G.G;
+    const int32_t g = (int32_t)gid;
+    const bool ok = gid != NONE && g < G.G;
     constexpr int NA = 15;   // 0-2 counts; node sums (lo, carry, hi): 3-5 unt cpu, 6-8 unt mem, 9-11 all cpu, 12-14 all mem
     uint64_t a[NA];
 #pragma unroll
@@ -1446,7 +1453,7 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
 #pragma unroll
     for (int r0 = 0; r0 < NA; r0 += (r0 == 0 ? 3 : 6)) {
         const int nk = r0 == 0 ? 3 : 6;
-        if (r0) __syncthreads();
+        __syncthreads();
 #pragma unroll
         for (int k = 0; k < 6; ++k)
             if (k < nk) red[wid][k][lane] = a[r0 + k];
@@ -1507,14 +1514,36 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
         finalize(G, N.gnode[g], g, D.pwords + (int64_t)g * PW_K, v, d, G.metrics);
         store_full(D.dec + g, d);
         sdec[lane] = compact_of(d);
+        sid[lane] = (uint32_t)g;
     }
     }
-    if (D.dec) {                                         // contiguous 16-B pieces (PCIe writes)
+    if (D.dec) {                                         // 16-B pieces to pinned host memory (PCIe writes)
         __syncthreads();
-        const int32_t g0 = blockIdx.x * 64;
-        const uint32_t n = G.G - g0 < 64 ? (uint32_t)(G.G - g0) : 64u;
-        store_compact(D.cdec, sdec, n, true, (uint32_t)g0, nullptr, threadIdx.x, NG_WAVES * 64);
+        store_compact(D.cdec, sdec, n_out, seq, (uint32_t)g_first, sid, threadIdx.x, NG_WAVES * 64);
     }
+}
+}  // namespace
+
+// K2b + K4 (k_node_groups, last kernel of the step): every group's node words from its
+// pair's K2 piece rows — NewNodeLabelFilterFunc (node_group.go:278) + filterNodes
+// (controller.go:120-154) + CalculateNodesCapacityTotal(untainted) (util.go:41-51): wet
+// groups take the filterNodes classes, dry groups (controller.go:126-138) every member as
+// untainted (cordoned ones included) except the tracked members (K2's tracker sums, read
+// and reset here).  64 groups per block, the 4 waves split each group's pieces.  A rank
+// reduces only the pieces of the pairs it owns, so a group's words are exact on its owner
+// and zero elsewhere.  With a decision target (D.dec: one rank, no exchange) the block then
+// decides its groups (K4 on this rank's fold) and writes the compact records to the
+// decision buffer as one contiguous run; otherwise it writes the words to the exchange
+// buffer (D.nx) and k_decide runs after the SUM.  (The default step fuses this work into
+// k_step_tail: TailDecide.)
+__global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeDev N,
+                                                               const int64_t* __restrict__ node_rows,
+                                                               int64_t* __restrict__ trk_acc,
+                                                               int64_t* __restrict__ nwords, NGDecide D) {
+    const int32_t g0 = blockIdx.x * 64;
+    const int32_t g = g0 + (int32_t)(threadIdx.x & 63);
+    const uint32_t n = G.G - g0 < 64 ? (uint32_t)(G.G - g0) : 64u;
+    node_groups_part(G, N, node_rows, trk_acc, nwords, D, g < G.G ? (uint32_t)g : NONE, true, g0, n);
 }
 
 // K4 alone (esc_decide after an exchange): the pod and node words are the exchanged sums
@@ -2422,23 +2451,70 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdCh
 // Before, K2 and K5 ran on a side stream beside K1: K1 holds every CU's LDS and its loads
 // starve K2's latency-bound waves, so the side chain ended after K1 and the cross-stream
 // join cost ~10 us more (profiles/r02_v9 timeline): ~45 us after K1 at any pod count.
+namespace {
+// One producer of fold column `col` is done (TailDecide): the block that brings the
+// column's count to zero decides the column's groups.  Every thread's stores are made
+// visible device-wide first (the fence writes the XCD's L2 back), and the decider's fence
+// invalidates its own before it reads the others' words.
+__device__ __forceinline__ void column_done(const GroupDev& G, const NodeDev& N, const FoldPlan& F,
+                                            const TailDecide& T, uint32_t col) {
+    __shared__ uint32_t s_last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t left = atomicSub(T.cnt + col, 1u);
+        s_last = left == 1u;
+        if (left == 1u) T.cnt[col] = T.cnt0[col];      // every producer has counted: ready for the next step
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
+    for (uint32_t base = ga; base < gb; base += 64) {
+        const uint32_t l = threadIdx.x & 63, n = gb - base < 64 ? gb - base : 64u;
+        const uint32_t gid = l < n ? F.col_groups[base + l] : NONE;
+        node_groups_part(G, N, T.node_rows, T.trk_acc, T.nwords, T.nd, gid, false, 0, n);
+    }
+}
+}  // namespace
+
 __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPlan F, int64_t* __restrict__ wide_pod,
                                                    int64_t* __restrict__ pwords, int64_t nb_pieces, int64_t n_piece_blk,
                                                    int64_t* __restrict__ rows, int64_t* __restrict__ trk_acc,
                                                    const OrdChunk* __restrict__ chunks, const uint32_t* __restrict__ grp_off,
                                                    const uint32_t* __restrict__ g_node, const uint32_t* __restrict__ g_grp,
                                                    const uint32_t* __restrict__ g_flags, uint32_t* __restrict__ vals,
-                                                   int64_t* __restrict__ seg) {
+                                                   int64_t* __restrict__ seg, TailDecide T) {
     static_assert(FD_WAVES * 64 == 256 && K2_WAVES * 64 == 256 && ORD_BLOCK == 256, "one block size for every role");
     const int64_t b = blockIdx.x;
     // F.ablate (ESC_K3_ABLATE, timing-only, wrong results): 8 / 16 / 32 skip the fold /
     // node-piece / ordering role, 64 the dry-mode tracker blocks, 128 K2's row stores
     if (b < F.n_col) {
         if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)b);
+        if (T.on) column_done(G, N, F, T, (uint32_t)b);
     } else if (b < F.n_col + n_piece_blk) {
         // 64: skip the tracker blocks (timing only)
-        if (!(F.ablate & 16) && !((F.ablate & 64) && b - F.n_col >= nb_pieces))
-            node_piece_block(N, G, nb_pieces, (F.ablate & 128) ? nullptr : rows, trk_acc, b - F.n_col);
+        const int64_t pb = b - F.n_col;
+        if (!(F.ablate & 16) && !((F.ablate & 64) && pb >= nb_pieces))
+            node_piece_block(N, G, nb_pieces, (F.ablate & 128) ? nullptr : rows, trk_acc, pb);
+        if (T.on) {
+            if (pb < nb_pieces) {                            // a K2 span block: the columns it feeds
+                for (uint32_t k = T.dep_off[pb]; k < T.dep_off[pb + 1]; ++k) column_done(G, N, F, T, T.dep_col[k]);
+            } else {                                         // a tracker block: the last one feeds the dry columns
+                __shared__ uint32_t s_lt;
+                __threadfence();
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    const uint32_t nt = (uint32_t)(n_piece_blk - nb_pieces);
+                    const uint32_t done = atomicAdd(T.trk_done, 1u) + 1u;
+                    s_lt = done == nt;
+                    if (done == nt) *T.trk_done = 0u;
+                }
+                __syncthreads();
+                if (s_lt)
+                    for (uint32_t k = 0; k < T.n_dry_col; ++k) column_done(G, N, F, T, T.dry_col[k]);
+            }
+        }
     } else if (!(F.ablate & 32)) {
         ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, g_node, g_grp, g_flags, vals, seg,
                                                        b - F.n_col - n_piece_blk);
@@ -2867,16 +2943,21 @@ hipError_t launch_peer_sum32(const uint32_t* const* src, int n_src, uint32_t* ds
     return peer_sum<uint32_t>(src, n_src, dst, n, st);
 }
 
+int64_t tail_span_blocks(const NodeDev& n) { return (n.n_spans + K2_WAVES - 1) / K2_WAVES; }
+int64_t tail_trk_blocks(const NodeDev& n) { return (n.n_trk + K2_WAVES * 64 - 1) / (K2_WAVES * 64); }
+
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
                             const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
-                            const uint32_t* g_flags, uint32_t* vals, int64_t* seg, hipStream_t st) {
-    const int64_t nb = spans ? (n.n_spans + K2_WAVES - 1) / K2_WAVES : 0;      // else K1 made the rows
-    const int64_t nt = (n.n_trk + K2_WAVES * 64 - 1) / (K2_WAVES * 64);
+                            const uint32_t* g_flags, uint32_t* vals, int64_t* seg, const TailDecide& td,
+                            hipStream_t st) {
+    const int64_t nb = spans ? tail_span_blocks(n) : 0;      // else K1 made the rows
+    const int64_t nt = tail_trk_blocks(n);
     const int64_t grid = f.n_col + nb + nt + std::max<int64_t>(n_small, 0);
     if (grid <= 0) return hipSuccess;
+    if (td.on && !spans) return hipErrorInvalidValue;       // the column counts assume the span blocks
     hipLaunchKernelGGL(k_step_tail, dim3((unsigned)grid), dim3(256), 0, st, g, n, f, wide_pod, pwords, nb, nb + nt, rows,
-                       trk_acc, chunks, grp_off, g_node, g_grp, g_flags, vals, seg);
+                       trk_acc, chunks, grp_off, g_node, g_grp, g_flags, vals, seg, td);
     return hipGetLastError();
 }
 
