@@ -279,14 +279,15 @@ def bench_order(args):
         return
     if world != args.gpus:
         raise SystemExit("bench: n_gpus %d != --gpus %d" % (world, args.gpus))
-    # algorithmic bytes per membership: read node, group, flags (12 B), write the node (4 B;
-    # an upper bound — cordoned nodes feed neither order).  The two-pass default moves 14 B
-    # (classify: flags 4 read, a class byte written; split: the class byte and the node
-    # read, the node written — the group is implied by the region, PMC in
-    # profiles/r03_k5/pmc_config5.json); the fused single pass (ESC_ORDER_FUSED=1) 16 B.
+    # algorithmic bytes per membership (the roofline's): a membership record of node, group
+    # and flags read (12 B) and the node written (4 B; an upper bound —
+    # cordoned nodes feed neither order).  The resident layout moves less: one 4-B region
+    # word (node | flags << 28; the group is implied by the region) read by each of the two
+    # passes and the node written, 12 B (round 3: 14 B, a class byte written and re-read);
+    # the fused single pass (ESC_ORDER_FUSED=1) reads the word and the group word once, 12 B.
     fused = os.environ.get("ESC_ORDER_FUSED", "0") not in ("", "0")
     order_bytes = n_memb * 16
-    moved_bytes = n_memb * (16 if fused else 14)
+    moved_bytes = n_memb * 12
     # the index build: node table read twice (count: flags, label 8 B; list: flags, label,
     # created 16 B), each membership written once (12 B: 8-B key, 4-B node | flags value),
     # LSD passes of <= 8 bits over the (group << R | creation offset) keys (hist: 8 B read;
@@ -312,6 +313,7 @@ def bench_order(args):
                      "bytes_moved_per_decision": moved_bytes,
                      "achieved": order_bytes / (order_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                      "frac": order_bytes / (order_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
+                     "frac_moved": moved_bytes / (order_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
                      "bytes_per_decision": order_bytes},
         "age_index_build": {"ms": index_ms, "nodes_per_s": N / (index_ms * 1e-3), "key_bits": R,
                             "lsd_passes": idx_passes, "GBps_moved": index_bytes / (index_ms * 1e-3) / 1e9},

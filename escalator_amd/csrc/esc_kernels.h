@@ -483,9 +483,8 @@ int64_t tail_span_blocks(const NodeDev& n);
 int64_t tail_trk_blocks(const NodeDev& n);
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
-                            const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
-                            const uint32_t* g_flags, uint32_t* vals, int64_t* seg, const TailDecide& td,
-                            hipStream_t st);
+                            const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                            uint32_t* vals, int64_t* seg, const TailDecide& td, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
 // §8f rank 2: a loaded pod as seen by NodePodsRemaining, listed per node (runs in
 // node order).  p[0..2]: the pod's extra pairs (NONE-padded); a C pod with more than 3
@@ -552,19 +551,27 @@ constexpr int ORD_CHUNK = ESC_ORD_CHUNK;   // memberships per K5 chunk (three-pa
 // region of the group-order arrays: its memberships oldest first, then padding (the round-up
 // to whole 16-B quads and the spare slots node additions take).
 constexpr uint32_t MEMB_PAD = 0x80000000u;
+// A group region's membership word (g_memb, 4 B): node | the low four flag bits of the node
+// as the per-decision split reads them (UNSCHED, TAINTED, TRACKED resolved for the group,
+// ABSENT) << MEMB_FLAG_SHIFT — the age index's sort value, kept as is.  One 4-B word per
+// membership is all the split reads besides the chunk (round 3 read node, flags and a class
+// byte: 9 B).  Nodes < 2^28.  Padding: node 0, ABSENT.
+constexpr uint32_t MEMB_FLAG_SHIFT = 28, MEMB_NODE_MASK = (1u << MEMB_FLAG_SHIFT) - 1;
+constexpr uint32_t MEMB_PAD_WORD = ESC_NF_ABSENT << MEMB_FLAG_SHIFT;
+inline uint32_t memb_word(uint32_t node, uint32_t flags) { return node | ((flags & 0xFu) << MEMB_FLAG_SHIFT); }
 // Small groups (region <= ORD_CHUNK) are packed whole into chunks ordered in one pass:
 // chunks [0, n_small) of groups with regions <= ORD_PCHUNK, packed up to ORD_PCHUNK
 // memberships (more, shorter blocks), then chunks of up to ORD_CHUNK.
 constexpr int ORD_PCHUNK = 1024;
 hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, int64_t n_small,
-                               const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
-                               const uint32_t* g_flags, uint32_t* vals, int64_t* seg, hipStream_t st);
+                               const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                               uint32_t* vals, int64_t* seg, hipStream_t st);
 // Fills the padding of every group's region (after its `len` memberships) with g | MEMB_PAD.
 hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_grp,
-                             uint32_t* g_node, uint32_t* g_flags, hipStream_t st);
+                             uint32_t* g_memb, hipStream_t st);
 hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
-                              const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
-                              const uint32_t* g_flags, unsigned long long* ticket, unsigned long long* status,
+                              const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                              unsigned long long* ticket, unsigned long long* status,
                               uint32_t* vals, int64_t* seg, uint32_t* err, int64_t max_chunk, int ablate,
                               hipStream_t st);
 // The age index (load time): memberships counted per block of nodes (scan: cnt = block
@@ -579,7 +586,7 @@ struct RegionSink {
     const uint32_t* pstart;    // region start of group g
     const uint32_t* plen;      // memberships of group g
     const uint8_t* dry;
-    uint32_t *g_node, *g_grp, *g_flags;
+    uint32_t *g_memb, *g_grp;  // region words (MEMB_FLAG_SHIFT), group words
     uint32_t* err;             // set when a membership falls outside its group's count
     int32_t G;
     int R;                     // creation-offset bits (key = group << R | offset)
@@ -588,8 +595,8 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const
                            int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, uint64_t* keys[2], uint32_t* vals[2],
                            uint32_t* hist, uint32_t* tot, const RegionSink& S, hipStream_t st);
 hipError_t launch_order(const NodeDev& n, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
-                        const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp, const uint32_t* g_flags,
-                        int64_t n_e, int32_t G, uint32_t* cls4, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,
+                        const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                        int64_t n_e, int32_t G, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,
                         int64_t* seg, hipStream_t st);
 
 }  // namespace esc

@@ -772,7 +772,11 @@ __device__ __forceinline__ void node_span(const NodeDev& N, int64_t* __restrict_
         unsigned long long x = 0;
 #pragma unroll
         for (int k = 0; k < NR_K; ++k) x = lane == k ? v[k] : x;
-        if (rows && lane < NR_K) rows[(int64_t)lane * N.n_pieces + p] = (int64_t)x;
+        // write-through (sc1) stores: the fused tail's decider on another XCD reads them
+        // after the span's column counts (TailDecide), with no release fence
+        if (rows && lane < NR_K)
+            __hip_atomic_store(rows + (int64_t)lane * N.n_pieces + p, (int64_t)x, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         acc = PieceAcc();
         ++p;
         ps = pe;
@@ -1689,9 +1693,13 @@ __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, i
             const __int128 pcpu = (__int128)tot[0][sl] + ((__int128)wtot[WP_CPU_HI][sl] << 32) + (__int128)wtot[WP_CPU_LO][sl];
             const __int128 pmem = (__int128)(((unsigned __int128)tot[3][sl] << 64) | tot[2][sl]) +
                                   ((__int128)wtot[WP_MEM_HI][sl] << 32) + (__int128)wtot[WP_MEM_LO][sl];
-            split_store(pw, PW_CPU_LO, pcpu);
-            split_store(pw, PW_MEM_LO, pmem);
-            pw[PW_N] = (int64_t)tot[1][sl] + wtot[WP_CNT][sl];
+            // write-through (sc1) stores, as K2's rows (TailDecide: read by another block)
+            auto st = [&](int k, int64_t v) { __hip_atomic_store(pw + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+            st(PW_CPU_LO, (int64_t)((unsigned __int128)pcpu & 0xFFFFFFFFull));
+            st(PW_CPU_LO + 1, (int64_t)(pcpu >> 32));
+            st(PW_MEM_LO, (int64_t)((unsigned __int128)pmem & 0xFFFFFFFFull));
+            st(PW_MEM_LO + 1, (int64_t)(pmem >> 32));
+            st(PW_N, (int64_t)tot[1][sl] + wtot[WP_CNT][sl]);
         }
     }
 }
@@ -1824,10 +1832,8 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scan_tot(uint32_t* __restrict
 // ballot matching per wave and per-(round, wave) digit counts; the chunk is reordered by
 // digit in LDS and written out in per-digit runs (stored straight from the ranking, a
 // wave's 64 keys went to ~64 different buckets: 8-B scattered stores, 1.6x write traffic).
-// A membership's sort value: node | its flags' low four bits (UNSCHED, TAINTED, TRACKED
-// resolved for the group, ABSENT: all the per-decision split reads) << 28.  4 B instead of
-// node | flags << 32: every LSD pass moves 8 B less per membership.
-constexpr uint32_t MEMB_FLAG_SHIFT = 28, MEMB_NODE_MASK = (1u << MEMB_FLAG_SHIFT) - 1;
+// A membership's sort value is its region word (esc_kernels.h MEMB_FLAG_SHIFT): 4 B instead
+// of node | flags << 32, so every LSD pass moves 8 B less per membership.
 // Sorted membership at position p (key = group << R | offset, value as above)
 // into its group's region: pstart[g] + p - seg[g].  The sorted starts seg are the host's
 // (live entries per pair); a position outside the group's [0, len) means the device listed a
@@ -1837,9 +1843,8 @@ __device__ __forceinline__ void region_put(const RegionSink& S, uint32_t p, uint
     const int64_t r = (int64_t)p - S.seg[g];
     if (g >= (uint32_t)S.G || r < 0 || r >= (int64_t)S.plen[g]) { *S.err = 1u; return; }
     const int64_t d = (int64_t)S.pstart[g] + r;
-    S.g_node[d] = v & MEMB_NODE_MASK;
+    S.g_memb[d] = v;
     S.g_grp[d] = g | (S.dry[g] ? NODE_DRY_BIT : 0u);
-    S.g_flags[d] = v >> MEMB_FLAG_SHIFT;
 }
 
 // FINAL (the age index's last pass): a key's sorted position goes straight into its group's
@@ -2150,9 +2155,10 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
 // ---- per decision: inside every group's run, a stable 3-way split by filterNodes class
 // (controller.go:125-150; dry groups: tracker only).  Chunks never cross a group, so a
 // chunk's untainted / tainted nodes go to two contiguous output streams; two passes:
-//   A  classify (12 B read, 1 B written) + per-chunk class counts,
-//   C  per chunk: its bases from the group's chunk counts, DPP wave ranks, LDS staging
-//      -> vals (5 B read, <= 4 B written, coalesced), the group's segment bounds.
+//   A  classify (the 4-B region words) -> per-chunk class counts,
+//   C  per chunk: its bases from the group's chunk counts, the words again (classes
+//      recomputed: cheaper than writing and re-reading a class byte), DPP wave ranks, LDS
+//      staging -> vals (<= 4 B written, coalesced), the group's segment bounds.
 constexpr int ORD_BLOCK = 256, ORD_WAVES = ORD_BLOCK / 64;
 
 // Membership flags: a dry group's membership has the tracker bit resolved for its group
@@ -2164,14 +2170,13 @@ __device__ __forceinline__ uint32_t ord_class(const NodeDev&, uint32_t, uint32_t
     return (f & ESC_NF_TAINTED) ? 1u : 0u;
 }
 
-// A: classes of the chunk's memberships (one u32 of 4 class bytes per quad) and the
-// chunk's count per class.  A split chunk holds one group's memberships, so the class is a
-// function of the flags alone (4 B per membership): the group's dry mode comes with the
+// A: the chunk's count per class.  A split chunk holds one group's memberships, so the
+// class is a function of the region word's flags alone: the group's dry mode comes with the
 // chunk (OrdChunk::pad & ORD_CHUNK_DRY) and region padding is flagged ESC_NF_ABSENT
-// (k_region_pad) like a deleted node.  Quads: one 16-B load of flags per lane.
+// (k_region_pad) like a deleted node.  Quads: one 16-B load per lane.
 __global__ __launch_bounds__(ORD_BLOCK) void k_ord_count(NodeDev N, const OrdChunk* __restrict__ chunks,
-                                                         const uint32_t* __restrict__ g_flags,
-                                                         uint32_t* __restrict__ cls4, uint32_t* __restrict__ ccnt) {
+                                                         const uint32_t* __restrict__ g_memb,
+                                                         uint32_t* __restrict__ ccnt) {
     __shared__ uint32_t red[ORD_WAVES][3];
     const OrdChunk ch = chunks[blockIdx.x];
     const uint32_t gword = (ch.pad & ORD_CHUNK_DRY) ? NODE_DRY_BIT : 0u;   // ord_class's group word
@@ -2183,22 +2188,19 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_count(NodeDev N, const OrdChu
 #pragma unroll
         for (int h = 0; h < H; ++h) {
             const uint32_t b = b0 + h * STEP < ch.end ? b0 + h * STEP : b0;
-            fl[h] = ld4(g_flags + b);
+            fl[h] = ld4(g_memb + b);
         }
 #pragma unroll
         for (int h = 0; h < H; ++h) {
             const uint32_t b = b0 + h * STEP;
             if (b >= ch.end) break;
-            uint32_t packed = 0;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const uint32_t k = b + j < ch.end ? ord_class(N, 0u, gword, lane4(fl[h], j)) : 3u;
-                packed |= k << (8 * j);
+                const uint32_t k = b + j < ch.end ? ord_class(N, 0u, gword, lane4(fl[h], j) >> MEMB_FLAG_SHIFT) : 3u;
                 c[0] += k == 0;
                 c[1] += k == 1;
                 c[2] += k == 2;
             }
-            cls4[b >> 2] = packed;
         }
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2223,9 +2225,8 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_count(NodeDev N, const OrdChu
 // The chunk's output bases come from the class counts of its group's chunks (pass A):
 // wave 0 sums them (a group has few chunks), and the group's first chunk writes the
 // group's segment bounds (groups without memberships keep the bounds set at load).
-__global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __restrict__ chunks,
-                                                           const uint32_t* __restrict__ cls4,
-                                                           const uint32_t* __restrict__ g_node,
+__global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(NodeDev N, const OrdChunk* __restrict__ chunks,
+                                                           const uint32_t* __restrict__ g_memb,
                                                            const uint32_t* __restrict__ gch_off,
                                                            const uint32_t* __restrict__ grp_off,
                                                            const uint32_t* __restrict__ ccnt,
@@ -2258,14 +2259,21 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __res
             }
         }
     }
+    const uint32_t gword = (ch.pad & ORD_CHUNK_DRY) ? NODE_DRY_BIT : 0u;   // ord_class's group word
     uint32_t packed[STEPS];
     uint4 nd[STEPS];
 #pragma unroll
     for (int st = 0; st < STEPS; ++st) {
         const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
-        const bool ok = b < ch.end;
-        packed[st] = ok ? cls4[b >> 2] : 0x03030303u;
-        nd[st] = ld4(g_node + (ok ? b : ch.start));
+        nd[st] = ld4(g_memb + (b < ch.end ? b : ch.start));
+    }
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {                 // one class byte per membership
+        const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
+        packed[st] = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            packed[st] |= (b + j < ch.end ? ord_class(N, 0u, gword, lane4(nd[st], j) >> MEMB_FLAG_SHIFT) : 3u) << (8 * j);
     }
     uint32_t ex[STEPS];
 #pragma unroll
@@ -2298,8 +2306,8 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(const OrdChunk* __res
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = (packed[st] >> (8 * j)) & 0xFF;
-            if (k == 0) stage[r0++] = lane4(nd[st], j);
-            else if (k == 1) stage[r1++] = lane4(nd[st], j);
+            if (k == 0) stage[r0++] = lane4(nd[st], j) & MEMB_NODE_MASK;
+            else if (k == 1) stage[r1++] = lane4(nd[st], j) & MEMB_NODE_MASK;
         }
     }
     __syncthreads();
@@ -2329,9 +2337,8 @@ __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long lon
 template <int STEPS>
 __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChunk* __restrict__ chunks,
                                                  const uint32_t* __restrict__ grp_off,
-                                                 const uint32_t* __restrict__ g_node,
+                                                 const uint32_t* __restrict__ g_memb,
                                                  const uint32_t* __restrict__ g_grp,
-                                                 const uint32_t* __restrict__ g_flags,
                                                  uint32_t* __restrict__ vals, int64_t* __restrict__ seg, int64_t blk) {
     constexpr int CAP = STEPS * 4 * ORD_BLOCK;           // memberships per chunk
     constexpr int NQ = CAP / 4;
@@ -2343,7 +2350,7 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
     __shared__ uint32_t stage[CAP];
     const OrdChunk ch = chunks[blk];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint4 nd[STEPS], gr[STEPS], fl[STEPS];
+    uint4 nd[STEPS], gr[STEPS];                          // region words, group words
     uint32_t grp[STEPS];
     bool ok[STEPS];
 #pragma unroll
@@ -2351,9 +2358,8 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
         const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
         ok[st] = b < ch.end;
         const uint32_t bb = ok[st] ? b : ch.start;
-        nd[st] = ld4(g_node + bb);
+        nd[st] = ld4(g_memb + bb);
         gr[st] = ld4(g_grp + bb);
-        fl[st] = ld4(g_flags + bb);
     }
     uint32_t cls[STEPS];
     unsigned long long ex[STEPS];
@@ -2364,7 +2370,7 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
         cls[st] = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t k = ok[st] ? ord_class(N, lane4(nd[st], j), lane4(gr[st], j), lane4(fl[st], j)) : 3u;
+            const uint32_t k = ok[st] ? ord_class(N, 0u, lane4(gr[st], j), lane4(nd[st], j) >> MEMB_FLAG_SHIFT) : 3u;
             cls[st] |= k << (8 * j);
             v += k == 0 ? 1ull : (k == 1 ? (1ull << C1) : (k == 2 ? (1ull << C2) : 0ull));
         }
@@ -2424,8 +2430,8 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = (cls[st] >> (8 * j)) & 0xFF;
-            if (k == 0) stage[s0 + r0++] = lane4(nd[st], j);
-            else if (k == 1) stage[s0 + t0 + r1++] = lane4(nd[st], j);
+            if (k == 0) stage[s0 + r0++] = lane4(nd[st], j) & MEMB_NODE_MASK;
+            else if (k == 1) stage[s0 + t0 + r1++] = lane4(nd[st], j) & MEMB_NODE_MASK;
         }
     }
     __syncthreads();
@@ -2437,11 +2443,10 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
 template <int STEPS>
 __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdChunk* __restrict__ chunks,
                                                           const uint32_t* __restrict__ grp_off,
-                                                          const uint32_t* __restrict__ g_node,
+                                                          const uint32_t* __restrict__ g_memb,
                                                           const uint32_t* __restrict__ g_grp,
-                                                          const uint32_t* __restrict__ g_flags,
                                                           uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
-    ord_packed_block<STEPS>(N, chunks, grp_off, g_node, g_grp, g_flags, vals, seg, blockIdx.x);
+    ord_packed_block<STEPS>(N, chunks, grp_off, g_memb, g_grp, vals, seg, blockIdx.x);
 }
 
 // The step's tail in ONE launch (horizontal fusion; every role is 256 threads and none
@@ -2452,86 +2457,115 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdCh
 // starve K2's latency-bound waves, so the side chain ended after K1 and the cross-stream
 // join cost ~10 us more (profiles/r02_v9 timeline): ~45 us after K1 at any pod count.
 namespace {
-// One producer of fold column `col` is done (TailDecide): the block that brings the
-// column's count to zero decides the column's groups.  Every thread's stores are made
-// visible device-wide first (the fence writes the XCD's L2 back), and the decider's fence
-// invalidates its own before it reads the others' words.
-__device__ __forceinline__ void column_done(const GroupDev& G, const NodeDev& N, const FoldPlan& F,
-                                            const TailDecide& T, uint32_t col) {
-    __shared__ uint32_t s_last;
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t left = atomicSub(T.cnt + col, 1u);
-        s_last = left == 1u;
-        if (left == 1u) T.cnt[col] = T.cnt0[col];      // every producer has counted: ready for the next step
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
-    for (uint32_t base = ga; base < gb; base += 64) {
-        const uint32_t l = threadIdx.x & 63, n = gb - base < 64 ? gb - base : 64u;
-        const uint32_t gid = l < n ? F.col_groups[base + l] : NONE;
-        node_groups_part(G, N, T.node_rows, T.trk_acc, T.nwords, T.nd, gid, false, 0, n);
+// Producers of fold columns are done (TailDecide): this block decrements the count of each
+// column in cols[0, n) (one thread per column), and decides every column it brought to
+// zero (k_node_groups' work for the column's groups) after restoring its count for the
+// next step.  Hand-off (cdna_hip_programming.md Guideline 16, R1): the producers' words
+// (K2 rows, pod words) are write-through (sc1) stores, so a producer needs no release
+// fence, only every wave's store drain before the barrier and the count; the decider takes
+// ONE agent-scope acquire before it reads them.  (__threadfence() per producer block —
+// an L2 write-back each — made the step 0.6 ms.)  Dry-mode tracker sums are atomics.
+__device__ __forceinline__ void columns_done(const GroupDev& G, const NodeDev& N, const FoldPlan& F,
+                                             const TailDecide& T, const uint32_t* cols, uint32_t n) {
+    __shared__ uint32_t s_ready[256];
+    __shared__ uint32_t s_n;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's sc1 stores / atomics are done
+    for (uint32_t c0 = 0; c0 < n; c0 += 256) {       // 256 columns per round, one per thread
+        __syncthreads();                             // every wave drained; the previous round's readers are done
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+        if (c0 + threadIdx.x < n) {
+            const uint32_t col = cols[c0 + threadIdx.x];
+            if (__hip_atomic_fetch_add(T.cnt + col, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
+                // every producer has counted: ready for the next step (the launch boundary orders it)
+                __hip_atomic_store(T.cnt + col, T.cnt0[col], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_ready[atomicAdd(&s_n, 1u)] = col;
+            }
+        }
+        __syncthreads();
+        const uint32_t nr = s_n;
+        if (nr == 0) continue;
+        if (threadIdx.x == 0) {                      // ONE acquire for the workgroup (L1 is per CU)
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        for (uint32_t r = 0; r < nr; ++r) {
+            const uint32_t col = s_ready[r];
+            const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
+            for (uint32_t base = ga; base < gb; base += 64) {
+                const uint32_t l = threadIdx.x & 63, m = gb - base < 64 ? gb - base : 64u;
+                const uint32_t gid = l < m ? F.col_groups[base + l] : NONE;
+                node_groups_part(G, N, T.node_rows, T.trk_acc, T.nwords, T.nd, gid, false, 0, m);
+            }
+        }
     }
 }
 }  // namespace
 
+// The step's tail in ONE launch (horizontal fusion; every role is 256 threads): the K2
+// node-piece blocks, the dry-mode tracker blocks, the K5 packed small-group orderings and
+// the K3 fold columns, in that block order.  With TailDecide the node groups + K4 run in
+// the same launch: a column's groups are decided by whichever of its producers (its fold
+// block, the K2 blocks of its groups' pieces, the last tracker block when it has a dry
+// group) finishes last.  The fold blocks come last in the grid so that they are usually
+// that block and the decisions spread over the columns' own blocks.  (Before, K2 and K5
+// ran on a side stream beside K1: K1 holds every CU's LDS and its loads starve K2's
+// latency-bound waves, so the side chain ended after K1 and the cross-stream join cost
+// ~10 us more (profiles/r02_v9 timeline): ~45 us after K1 at any pod count.)
 __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPlan F, int64_t* __restrict__ wide_pod,
                                                    int64_t* __restrict__ pwords, int64_t nb_pieces, int64_t n_piece_blk,
                                                    int64_t* __restrict__ rows, int64_t* __restrict__ trk_acc,
-                                                   const OrdChunk* __restrict__ chunks, const uint32_t* __restrict__ grp_off,
-                                                   const uint32_t* __restrict__ g_node, const uint32_t* __restrict__ g_grp,
-                                                   const uint32_t* __restrict__ g_flags, uint32_t* __restrict__ vals,
-                                                   int64_t* __restrict__ seg, TailDecide T) {
+                                                   const OrdChunk* __restrict__ chunks, int64_t n_small,
+                                                   const uint32_t* __restrict__ grp_off,
+                                                   const uint32_t* __restrict__ g_memb, const uint32_t* __restrict__ g_grp,
+                                                   uint32_t* __restrict__ vals, int64_t* __restrict__ seg, TailDecide T) {
     static_assert(FD_WAVES * 64 == 256 && K2_WAVES * 64 == 256 && ORD_BLOCK == 256, "one block size for every role");
     const int64_t b = blockIdx.x;
     // F.ablate (ESC_K3_ABLATE, timing-only, wrong results): 8 / 16 / 32 skip the fold /
     // node-piece / ordering role, 64 the dry-mode tracker blocks, 128 K2's row stores
-    if (b < F.n_col) {
-        if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)b);
-        if (T.on) column_done(G, N, F, T, (uint32_t)b);
-    } else if (b < F.n_col + n_piece_blk) {
-        // 64: skip the tracker blocks (timing only)
-        const int64_t pb = b - F.n_col;
+    if (b < n_piece_blk) {
+        const int64_t pb = b;
         if (!(F.ablate & 16) && !((F.ablate & 64) && pb >= nb_pieces))
             node_piece_block(N, G, nb_pieces, (F.ablate & 128) ? nullptr : rows, trk_acc, pb);
         if (T.on) {
             if (pb < nb_pieces) {                            // a K2 span block: the columns it feeds
-                for (uint32_t k = T.dep_off[pb]; k < T.dep_off[pb + 1]; ++k) column_done(G, N, F, T, T.dep_col[k]);
+                columns_done(G, N, F, T, T.dep_col + T.dep_off[pb], T.dep_off[pb + 1] - T.dep_off[pb]);
             } else {                                         // a tracker block: the last one feeds the dry columns
                 __shared__ uint32_t s_lt;
-                __threadfence();
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's tracker atomics are done
                 __syncthreads();
                 if (threadIdx.x == 0) {
                     const uint32_t nt = (uint32_t)(n_piece_blk - nb_pieces);
-                    const uint32_t done = atomicAdd(T.trk_done, 1u) + 1u;
+                    const uint32_t done = __hip_atomic_fetch_add(T.trk_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
                     s_lt = done == nt;
-                    if (done == nt) *T.trk_done = 0u;
+                    if (done == nt) __hip_atomic_store(T.trk_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 __syncthreads();
-                if (s_lt)
-                    for (uint32_t k = 0; k < T.n_dry_col; ++k) column_done(G, N, F, T, T.dry_col[k]);
+                if (s_lt) columns_done(G, N, F, T, T.dry_col, T.n_dry_col);
             }
         }
-    } else if (!(F.ablate & 32)) {
-        ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, g_node, g_grp, g_flags, vals, seg,
-                                                       b - F.n_col - n_piece_blk);
+    } else if (b < n_piece_blk + n_small) {
+        if (!(F.ablate & 32))
+            ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, g_memb, g_grp, vals, seg,
+                                                           b - n_piece_blk);
+    } else {
+        const uint32_t col = (uint32_t)(b - n_piece_blk - n_small);
+        if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)col);
+        if (T.on) columns_done(G, N, F, T, &col, 1);
     }
 }
 
-// Region padding: g | MEMB_PAD after each group's memberships (node 0, flags 0).
+// Region padding: g | MEMB_PAD after each group's memberships (node 0, flagged absent:
+// class 3 from the region word alone, k_ord_count).
 __global__ __launch_bounds__(256) void k_region_pad(const uint32_t* __restrict__ pstart,
                                                     const uint32_t* __restrict__ plen, int32_t G,
-                                                    uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_node,
-                                                    uint32_t* __restrict__ g_flags) {
+                                                    uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_memb) {
     const int32_t g = blockIdx.x;
     if (g >= G) return;
     for (uint32_t i = pstart[g] + plen[g] + threadIdx.x; i < pstart[g + 1]; i += blockDim.x) {
         g_grp[i] = (uint32_t)g | MEMB_PAD;
-        g_node[i] = 0;
-        g_flags[i] = ESC_NF_ABSENT;                     // class 3 from the flags alone (k_ord_count)
+        g_memb[i] = MEMB_PAD_WORD;
     }
 }
 
@@ -2560,9 +2594,8 @@ template <int FB>
 __global__ __launch_bounds__(FB) void k_ord_fused(NodeDev N, const OrdChunk* __restrict__ chunks,
                                                          int64_t n_chunks, const uint32_t* __restrict__ gch_off,
                                                          const uint32_t* __restrict__ grp_off,
-                                                         const uint32_t* __restrict__ g_node,
+                                                         const uint32_t* __restrict__ g_memb,
                                                          const uint32_t* __restrict__ g_grp,
-                                                         const uint32_t* __restrict__ g_flags,
                                                          unsigned long long* __restrict__ ticket,
                                                          unsigned long long* __restrict__ status,
                                                          uint32_t* __restrict__ vals, int64_t* __restrict__ seg,
@@ -2579,14 +2612,13 @@ __global__ __launch_bounds__(FB) void k_ord_fused(NodeDev N, const OrdChunk* __r
     const uint32_t epoch = (uint32_t)(tk / (unsigned long long)n_chunks);
     const OrdChunk ch = chunks[q];
     // classify: all four quads' loads in flight
-    uint4 nd[ROUNDS], gr[ROUNDS], fl[ROUNDS];
+    uint4 nd[ROUNDS], gr[ROUNDS];
 #pragma unroll
     for (int r = 0; r < ROUNDS; ++r) {
         const uint32_t b = ch.start + r * 4 * FB + 4 * threadIdx.x;
         const uint32_t bb = b < ch.end ? b : ch.start;
-        nd[r] = ld4(g_node + bb);
+        nd[r] = ld4(g_memb + bb);
         gr[r] = ld4(g_grp + bb);
-        fl[r] = ld4(g_flags + bb);
     }
     uint32_t cls = 0;                                     // 2 bits per membership
     uint32_t v[ROUNDS];                                   // class 0 | class 1 << 16, per round
@@ -2596,7 +2628,7 @@ __global__ __launch_bounds__(FB) void k_ord_fused(NodeDev N, const OrdChunk* __r
         v[r] = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t k = b + j < ch.end ? ord_class(N, lane4(nd[r], j), lane4(gr[r], j), lane4(fl[r], j)) : 3u;
+            const uint32_t k = b + j < ch.end ? ord_class(N, 0u, lane4(gr[r], j), lane4(nd[r], j) >> MEMB_FLAG_SHIFT) : 3u;
             cls |= k << (2 * (4 * r + j));
             v[r] += k == 0 ? 1u : (k == 1 ? 0x10000u : 0u);
         }
@@ -2684,8 +2716,8 @@ __global__ __launch_bounds__(FB) void k_ord_fused(NodeDev N, const OrdChunk* __r
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = (cls >> (2 * (4 * r + j))) & 3u;
-            if (k == 0) vals[base0 + r0++] = lane4(nd[r], j);
-            else if (k == 1) vals[last1 - r1++] = lane4(nd[r], j);
+            if (k == 0) vals[base0 + r0++] = lane4(nd[r], j) & MEMB_NODE_MASK;
+            else if (k == 1) vals[last1 - r1++] = lane4(nd[r], j) & MEMB_NODE_MASK;
         }
     }
 }
@@ -2948,16 +2980,15 @@ int64_t tail_trk_blocks(const NodeDev& n) { return (n.n_trk + K2_WAVES * 64 - 1)
 
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
-                            const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
-                            const uint32_t* g_flags, uint32_t* vals, int64_t* seg, const TailDecide& td,
-                            hipStream_t st) {
+                            const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                            uint32_t* vals, int64_t* seg, const TailDecide& td, hipStream_t st) {
     const int64_t nb = spans ? tail_span_blocks(n) : 0;      // else K1 made the rows
     const int64_t nt = tail_trk_blocks(n);
     const int64_t grid = f.n_col + nb + nt + std::max<int64_t>(n_small, 0);
     if (grid <= 0) return hipSuccess;
     if (td.on && !spans) return hipErrorInvalidValue;       // the column counts assume the span blocks
     hipLaunchKernelGGL(k_step_tail, dim3((unsigned)grid), dim3(256), 0, st, g, n, f, wide_pod, pwords, nb, nb + nt, rows,
-                       trk_acc, chunks, grp_off, g_node, g_grp, g_flags, vals, seg, td);
+                       trk_acc, chunks, std::max<int64_t>(n_small, 0), grp_off, g_memb, g_grp, vals, seg, td);
     return hipGetLastError();
 }
 
@@ -3093,53 +3124,52 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const
 }
 
 hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
-                              const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
-                              const uint32_t* g_flags, unsigned long long* ticket, unsigned long long* status,
+                              const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                              unsigned long long* ticket, unsigned long long* status,
                               uint32_t* vals, int64_t* seg, uint32_t* err, int64_t max_chunk, int ablate,
                               hipStream_t st) {
     if (n_chunks <= 0) return hipSuccess;
     if (max_chunk > 16 * 512)                             // 1024 threads: up to 16384 per chunk
         hipLaunchKernelGGL(k_ord_fused<1024>, dim3((unsigned)n_chunks), dim3(1024), 0, st, nd, chunks, n_chunks,
-                           gch_off, grp_off, g_node, g_grp, g_flags, ticket, status, vals, seg, err, ablate);
+                           gch_off, grp_off, g_memb, g_grp, ticket, status, vals, seg, err, ablate);
     else if (max_chunk > 16 * 256)
         hipLaunchKernelGGL(k_ord_fused<512>, dim3((unsigned)n_chunks), dim3(512), 0, st, nd, chunks, n_chunks,
-                           gch_off, grp_off, g_node, g_grp, g_flags, ticket, status, vals, seg, err, ablate);
+                           gch_off, grp_off, g_memb, g_grp, ticket, status, vals, seg, err, ablate);
     else
         hipLaunchKernelGGL(k_ord_fused<256>, dim3((unsigned)n_chunks), dim3(256), 0, st, nd, chunks, n_chunks,
-                           gch_off, grp_off, g_node, g_grp, g_flags, ticket, status, vals, seg, err, ablate);
+                           gch_off, grp_off, g_memb, g_grp, ticket, status, vals, seg, err, ablate);
     return hipGetLastError();
 }
 
 hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, int64_t n_small,
-                               const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp,
-                               const uint32_t* g_flags, uint32_t* vals, int64_t* seg, hipStream_t st) {
+                               const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                               uint32_t* vals, int64_t* seg, hipStream_t st) {
     if (n_chunks <= 0) return hipSuccess;
     // chunks [0, n_small) hold <= ORD_PCHUNK memberships, the rest <= ORD_CHUNK
     if (n_small > 0)
         hipLaunchKernelGGL(k_ord_packed<ORD_PCHUNK / (4 * ORD_BLOCK)>, dim3((unsigned)n_small), dim3(ORD_BLOCK), 0, st,
-                           nd, chunks, grp_off, g_node, g_grp, g_flags, vals, seg);
+                           nd, chunks, grp_off, g_memb, g_grp, vals, seg);
     if (n_chunks > n_small)
         hipLaunchKernelGGL(k_ord_packed<ORD_CHUNK / (4 * ORD_BLOCK)>, dim3((unsigned)(n_chunks - n_small)),
-                           dim3(ORD_BLOCK), 0, st, nd, chunks + n_small, grp_off, g_node, g_grp, g_flags, vals, seg);
+                           dim3(ORD_BLOCK), 0, st, nd, chunks + n_small, grp_off, g_memb, g_grp, vals, seg);
     return hipGetLastError();
 }
 
 hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_grp,
-                             uint32_t* g_node, uint32_t* g_flags, hipStream_t st) {
+                             uint32_t* g_memb, hipStream_t st) {
     if (G <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_region_pad, dim3((unsigned)G), dim3(256), 0, st, pstart, plen, G, g_grp, g_node, g_flags);
+    hipLaunchKernelGGL(k_region_pad, dim3((unsigned)G), dim3(256), 0, st, pstart, plen, G, g_grp, g_memb);
     return hipGetLastError();
 }
 
 hipError_t launch_order(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
-                        const uint32_t* grp_off, const uint32_t* g_node, const uint32_t* g_grp, const uint32_t* g_flags,
-                        int64_t n_e, int32_t G, uint32_t* cls4, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,
+                        const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                        int64_t n_e, int32_t G, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,
                         int64_t* seg, hipStream_t st) {
     if (n_chunks > 0)
-        hipLaunchKernelGGL(k_ord_count, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, g_flags, cls4,
-                           ccnt);
+        hipLaunchKernelGGL(k_ord_count, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, g_memb, ccnt);
     if (n_chunks > 0)
-        hipLaunchKernelGGL(k_ord_scatter, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, chunks, cls4, g_node, gch_off,
+        hipLaunchKernelGGL(k_ord_scatter, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, g_memb, gch_off,
                            grp_off, ccnt, vals, seg);
     return hipGetLastError();
 }

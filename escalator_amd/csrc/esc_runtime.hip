@@ -232,9 +232,9 @@ struct esc_ctx {
     int64_t n_memb = 0;
     int order_src = 0, memb_blocks = 0;
     // group order of the memberships (per-decision 3-way split by class inside each group)
-    uint32_t *d_g_node = nullptr, *d_g_grp = nullptr, *d_g_flags = nullptr;
+    uint32_t *d_g_memb = nullptr, *d_g_grp = nullptr;   // K5 regions: membership words, group words
     uint32_t *d_grp_off = nullptr, *d_gch_off = nullptr, *d_ccnt = nullptr, *d_cbase = nullptr;
-    uint32_t *d_pstart = nullptr, *d_cls4 = nullptr, *d_plen = nullptr;
+    uint32_t *d_pstart = nullptr, *d_plen = nullptr;
     uint32_t* d_ord = nullptr;                                // K5 output, in the group regions
     OrdChunk* d_pchunks = nullptr;                            // packed chunks of small groups
     int64_t n_pchunks = 0, n_psmall = 0;                      // all / those <= ORD_PCHUNK (first)
@@ -262,7 +262,7 @@ struct esc_ctx {
     std::vector<uint32_t> pair_next, pair_end;                // group pair -> next spare entry, range end
     std::vector<uint32_t> pair_lo;                            // group pair -> its first entry
     uint32_t nodes_piece_lo(uint32_t q) const { return pair_lo[q]; }
-    std::vector<uint32_t> h_gn;                               // group regions' nodes (lazy mirror of d_g_node)
+    std::vector<uint32_t> h_gn;                               // group regions' nodes (lazy mirror of d_g_memb)
     // per-function drop-ins: the list reducer (esc_list.hip); esc_order_by_creation runs
     // on a one-group list context
     esc_ctx* list_ctx = nullptr;
@@ -467,12 +467,12 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out);
 // K5 per-decision ordering (classify + stable split of every group's age-ordered
 // memberships) on stream st; the two-pass kernels (the fused one needs its ticket reset).
 hipError_t enqueue_order(esc_ctx* c, hipStream_t st) {
-    const hipError_t e = launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node,
-                                      c->d_g_grp, c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase,
+    const hipError_t e = launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb,
+                                      c->d_g_grp, c->n_memb, c->gi.G, c->d_ccnt, c->d_cbase,
                                       c->d_ord, c->d_seg, st);
     if (e != hipSuccess) return e;
-    return launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_node, c->d_g_grp,
-                               c->d_g_flags, c->d_ord, c->d_seg, st);
+    return launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_memb, c->d_g_grp,
+                               c->d_ord, c->d_seg, st);
 }
 
 // Replays (capturing on first use) the per-replica graph of enqueue_step(r, decide, decide)
@@ -595,10 +595,10 @@ void release_sort(esc_ctx* c) {
     for (int i = 0; i < 2; ++i) { dfree(c->d_mkeys[i]); dfree(c->d_mvals[i]); }
     c->mcap = 0;
     c->age_built = false;
-    dfree(c->d_g_node); dfree(c->d_g_grp); dfree(c->d_g_flags);
+    dfree(c->d_g_memb); dfree(c->d_g_grp);
     dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks);
     dfree(c->d_oticket); dfree(c->d_ostat); dfree(c->d_oerr);
-    dfree(c->d_pstart); dfree(c->d_cls4); dfree(c->d_plen); dfree(c->d_ord); dfree(c->d_pchunks);
+    dfree(c->d_pstart); dfree(c->d_plen); dfree(c->d_ord); dfree(c->d_pchunks);
     c->n_pchunks = 0;
     c->n_chunks = 0;
     c->n_gpad = 0;
@@ -752,9 +752,8 @@ int32_t build_age_index(esc_ctx* c) {
     }
     const int64_t npad = pstart[g.G];
     if (fresh || npad != c->n_gpad) {
-        dfree(c->d_g_node); dfree(c->d_g_grp); dfree(c->d_g_flags); dfree(c->d_cls4); dfree(c->d_ord);
-        HIP_TRY(dalloc(&c->d_g_node, npad)); HIP_TRY(dalloc(&c->d_g_grp, npad)); HIP_TRY(dalloc(&c->d_g_flags, npad));
-        HIP_TRY(dalloc(&c->d_cls4, (npad + 3) / 4)); HIP_TRY(dalloc(&c->d_ord, npad));
+        dfree(c->d_g_memb); dfree(c->d_g_grp); dfree(c->d_ord);
+        HIP_TRY(dalloc(&c->d_g_memb, npad)); HIP_TRY(dalloc(&c->d_g_grp, npad)); HIP_TRY(dalloc(&c->d_ord, npad));
     }
     c->n_gpad = npad;
     // no clearing: the sort's last pass fills every group's [start, start + len), k_region_pad the
@@ -792,11 +791,11 @@ int32_t build_age_index(esc_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->d_seg, starts.data(), starts.size() * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(c->d_ierr, 0, 4, st));
     const int gbits = bit_width((uint64_t)std::max<int32_t>(g.G - 1, 1));
-    RegionSink sink{c->d_seg, c->d_pstart, c->d_plen, c->d_dry, c->d_g_node, c->d_g_grp, c->d_g_flags, c->d_ierr,
+    RegionSink sink{c->d_seg, c->d_pstart, c->d_plen, c->d_dry, c->d_g_memb, c->d_g_grp, c->d_ierr,
                     g.G, c->sort_R};
     HIP_TRY(launch_age_sort(n, g, c->memb_blocks, c->d_cnt, c->n_memb, c->mcap, c->ts_min, c->sort_div, c->sort_R,
                             gbits, c->d_mkeys, c->d_mvals, c->d_hist, c->d_tot, sink, st));
-    HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_grp, c->d_g_node, c->d_g_flags, st));
+    HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_grp, c->d_g_memb, st));
     if (check) {
         uint32_t err = 0;
         HIP_TRY(hipMemcpyAsync(&err, c->d_ierr, 4, hipMemcpyDeviceToHost, st));
@@ -1182,15 +1181,14 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
                         c->d_td_trk_done, c->nodes.rows, c->d_trk_acc, c->d_nwords, nd};
     }
     HIP_TRY(launch_step_tail(g, n, f, true, c->d_wide_pod, c->d_pwords, c->nodes.rows, c->d_trk_acc, c->d_pchunks,
-                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_node, c->d_g_grp, c->d_g_flags, c->d_ord,
-                             c->d_seg, td, st));
+                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, td, st));
     if (int32_t rc = mark()) return rc;
     if (ord) {                                       // split groups, mid-size packed chunks
-        HIP_TRY(launch_order(n, c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node, c->d_g_grp,
-                             c->d_g_flags, c->n_memb, c->gi.G, c->d_cls4, c->d_ccnt, c->d_cbase, c->d_ord, c->d_seg,
+        HIP_TRY(launch_order(n, c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb, c->d_g_grp,
+                             c->n_memb, c->gi.G, c->d_ccnt, c->d_cbase, c->d_ord, c->d_seg,
                              st));
         HIP_TRY(launch_order_packed(n, c->d_pchunks + c->n_psmall, c->n_pchunks - c->n_psmall, 0, c->d_grp_off,
-                                    c->d_g_node, c->d_g_grp, c->d_g_flags, c->d_ord, c->d_seg, st));
+                                    c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, st));
     }
     if (int32_t rc = mark()) return rc;
     if (!td.on) HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, nd, st));
@@ -2691,7 +2689,8 @@ int32_t ensure_gn(esc_ctx* c) {
     if ((int64_t)c->h_gn.size() == c->n_gpad) return ESC_OK;
     c->h_gn.resize(c->n_gpad);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->n_gpad) HIP_TRY(hipMemcpy(c->h_gn.data(), c->d_g_node, c->n_gpad * 4, hipMemcpyDeviceToHost));
+    if (c->n_gpad) HIP_TRY(hipMemcpy(c->h_gn.data(), c->d_g_memb, c->n_gpad * 4, hipMemcpyDeviceToHost));
+    for (uint32_t& x : c->h_gn) x &= MEMB_NODE_MASK;             // the node ids (the flags live on the device)
     return ESC_OK;
 }
 
@@ -2742,11 +2741,11 @@ int32_t patch_regions(esc_ctx* c, const std::vector<int64_t>& ids) {
             if (!owns_group(c, m & NODE_GROUP_MASK)) continue;          // another rank's K5 region
             const int64_t pos = region_pos(c, m & NODE_GROUP_MASK, (uint32_t)j);
             if (pos < 0) return ESC_E_HIP;                            // mirror out of step: never expected
-            P.add(0, pos, gone ? ESC_NF_ABSENT : memb_flags(c, j, m));
+            P.add(0, pos, memb_word((uint32_t)j, gone ? ESC_NF_ABSENT : memb_flags(c, j, m)));
         }
     }
     PatchTargets t{};
-    t.u32[0] = c->d_g_flags;
+    t.u32[0] = c->d_g_memb;
     return apply_patches(c, P, {t});
 }
 
@@ -2767,10 +2766,10 @@ void pair_first(const esc_ctx* c, uint32_t q, GroupNode& x) {
     }
 }
 
-// Patch targets of the K5 regions: node id, group code, flags copy.
+// Patch targets of the K5 regions: membership word (node | flags), group word.
 PatchTargets region_targets(esc_ctx* c) {
     PatchTargets t{};
-    t.u32[0] = c->d_g_node; t.u32[1] = c->d_g_grp; t.u32[2] = c->d_g_flags;
+    t.u32[0] = c->d_g_memb; t.u32[1] = c->d_g_grp;
     return t;
 }
 
@@ -2797,9 +2796,9 @@ void regions_insert(esc_ctx* c, std::unordered_map<uint32_t, std::vector<uint32_
         const uint32_t mbit = (uint32_t)g | (c->params[g].dry ? NODE_DRY_BIT : 0u);
         for (size_t k = 0; k < merged.size(); ++k) {
             const int64_t pos = (int64_t)a + from + (int64_t)k;
-            R.add(0, pos, merged[k]);
+            R.add(0, pos, memb_word(merged[k], (c->h_nflags[merged[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT
+                                                                                       : memb_flags(c, merged[k], mbit)));
             R.add(1, pos, mbit);
-            R.add(2, pos, (c->h_nflags[merged[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT : memb_flags(c, merged[k], mbit));
         }
     }
 }
@@ -2816,14 +2815,12 @@ bool region_remove(esc_ctx* c, uint32_t g, uint32_t j, Patches& R) {
     const uint32_t mbit = (uint32_t)g | (c->params[g].dry ? NODE_DRY_BIT : 0u);
     for (int64_t k = pos; k < last; ++k) {
         gn[k] = gn[k + 1];
-        R.add(0, k, gn[k]);
+        R.add(0, k, memb_word(gn[k], (c->h_nflags[gn[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT : memb_flags(c, gn[k], mbit)));
         R.add(1, k, mbit);
-        R.add(2, k, (c->h_nflags[gn[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT : memb_flags(c, gn[k], mbit));
     }
     gn[last] = 0;
-    R.add(0, last, 0);
+    R.add(0, last, MEMB_PAD_WORD);
     R.add(1, last, (uint32_t)g | MEMB_PAD);
-    R.add(2, last, ESC_NF_ABSENT);
     c->h_plen[g] = len - 1;
     return true;
 }
@@ -4020,11 +4017,11 @@ int32_t esc_sort_nodes(esc_ctx* c) {
     hipSetDevice(c->device);
     c->fused_ran = c->order_fused && c->fused_fits;
     if (c->fused_ran) {
-        HIP_TRY(launch_order_fused(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_node,
-                                   c->d_g_grp, c->d_g_flags, c->d_oticket, c->d_ostat, c->d_ord, c->d_seg,
+        HIP_TRY(launch_order_fused(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb,
+                                   c->d_g_grp, c->d_oticket, c->d_ostat, c->d_ord, c->d_seg,
                                    c->d_oerr, c->max_chunk, c->order_ablate, c->stream));
-        HIP_TRY(launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_node, c->d_g_grp,
-                                    c->d_g_flags, c->d_ord, c->d_seg, c->stream));
+        HIP_TRY(launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_memb, c->d_g_grp,
+                                    c->d_ord, c->d_seg, c->stream));
     } else {
         HIP_TRY(enqueue_order(c, c->stream));
     }
