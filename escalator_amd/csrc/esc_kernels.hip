@@ -960,11 +960,14 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     typedef __attribute__((address_space(4))) const int64_t ci64;
     if (P.seg && !DYN && !WS && !(ABLATE & 2)) {
         const ci64* sg = (const ci64*)P.seg + (int64_t)blockIdx.x * (2 * K1_SEGS);
+        uint64_t n_runs = 0, run_w = 0;                  // diagnostics (trace[6], trace[7])
 #pragma unroll 1
         for (int k = 0; k < K1_SEGS; ++k) {
             const int64_t t0c = sg[2 * k], b = sg[2 * k + 1];
             if (b == 0) break;
             const PodClass C = load_class(P.cls, (int)(t0c >> 48));
+            ++n_runs;
+            run_w += (uint64_t)(b - (t0c & ((1ll << 48) - 1))) * C.wt;
             const int64_t a = (t0c & ((1ll << 48) - 1)) + wid;
             if (a >= b) continue;
             switch (C.kind) {
@@ -976,6 +979,7 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
             }
         }
         chunk = n_chunks;                                // skip the weight-range walk
+        if (trace && threadIdx.x == 0) { trace[6] = n_runs; trace[7] = run_w; }
     }
     for (int taken = 1; !(ABLATE & 2) && chunk < n_chunks; ++taken) {
         // equal shares of work weight (bytes), not of tiles: a tile of a class with three
@@ -2457,6 +2461,7 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdCh
 // starve K2's latency-bound waves, so the side chain ended after K1 and the cross-stream
 // join cost ~10 us more (profiles/r02_v9 timeline): ~45 us after K1 at any pod count.
 namespace {
+constexpr uint32_t TAIL_SPIN_MAX = 1u << 22;     // fold_done's poll bound (~0.1 s of s_sleep 1)
 // Producers of fold columns are done (TailDecide): this block decrements the count of each
 // column in cols[0, n) (one thread per column), and decides every column it brought to
 // zero (k_node_groups' work for the column's groups) after restoring its count for the
@@ -2465,6 +2470,26 @@ namespace {
 // fence, only every wave's store drain before the barrier and the count; the decider takes
 // ONE agent-scope acquire before it reads them.  (__threadfence() per producer block —
 // an L2 write-back each — made the step 0.6 ms.)  Dry-mode tracker sums are atomics.
+// Decide the columns cols[0, nr) (LDS) whose producers are all done: ONE agent-scope
+// acquire for the workgroup (L1 is per CU), then k_node_groups' work per column.
+__device__ __forceinline__ void decide_columns(const GroupDev& G, const NodeDev& N, const FoldPlan& F,
+                                               const TailDecide& T, const uint32_t* cols, uint32_t nr) {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (uint32_t r = 0; r < nr; ++r) {
+        const uint32_t col = cols[r];
+        const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
+        for (uint32_t base = ga; base < gb; base += 64) {
+            const uint32_t l = threadIdx.x & 63, m = gb - base < 64 ? gb - base : 64u;
+            const uint32_t gid = l < m ? F.col_groups[base + l] : NONE;
+            node_groups_part(G, N, T.node_rows, T.trk_acc, T.nwords, T.nd, gid, false, 0, m);
+        }
+    }
+}
+
 __device__ __forceinline__ void columns_done(const GroupDev& G, const NodeDev& N, const FoldPlan& F,
                                              const TailDecide& T, const uint32_t* cols, uint32_t n) {
     __shared__ uint32_t s_ready[256];
@@ -2485,31 +2510,51 @@ __device__ __forceinline__ void columns_done(const GroupDev& G, const NodeDev& N
         __syncthreads();
         const uint32_t nr = s_n;
         if (nr == 0) continue;
-        if (threadIdx.x == 0) {                      // ONE acquire for the workgroup (L1 is per CU)
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        for (uint32_t r = 0; r < nr; ++r) {
-            const uint32_t col = s_ready[r];
-            const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
-            for (uint32_t base = ga; base < gb; base += 64) {
-                const uint32_t l = threadIdx.x & 63, m = gb - base < 64 ? gb - base : 64u;
-                const uint32_t gid = l < m ? F.col_groups[base + l] : NONE;
-                node_groups_part(G, N, T.node_rows, T.trk_acc, T.nwords, T.nd, gid, false, 0, m);
-            }
-        }
+        decide_columns(G, N, F, T, s_ready, nr);
     }
+}
+
+// The fold block of column `col` (the last role in the grid, so every producer of its
+// column was dispatched before it on its XCD and none of them waits): once its own pod
+// words are out it waits for the column's other producers — thread 0 polls the count,
+// relaxed, until only the fold's own unit is left — then decides the column.  So the
+// decisions run in the columns' own blocks, in parallel, instead of in whichever producer
+// happens to end last (at a rank's shard the folds end first and the last tracker block
+// decided every dry column in turn: 0.36 ms).  The poll is bounded: past it the fold counts
+// itself as an ordinary producer and the last one of them decides (columns_done), so the
+// result never depends on the bound.
+__device__ __forceinline__ void fold_done(const GroupDev& G, const NodeDev& N, const FoldPlan& F,
+                                          const TailDecide& T, uint32_t col) {
+    __shared__ uint32_t s_col[1];
+    __shared__ uint32_t s_go;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t spins = 0, go = 0;
+        for (;;) {
+            if (__hip_atomic_load(T.cnt + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) { go = 1; break; }
+            if (++spins > TAIL_SPIN_MAX) {           // count the fold in; the last producer decides
+                go = __hip_atomic_fetch_add(T.cnt + col, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (go) __hip_atomic_store(T.cnt + col, T.cnt0[col], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_col[0] = col;
+        s_go = go;
+    }
+    __syncthreads();
+    if (s_go) decide_columns(G, N, F, T, s_col, 1);
 }
 }  // namespace
 
 // The step's tail in ONE launch (horizontal fusion; every role is 256 threads): the K2
 // node-piece blocks, the dry-mode tracker blocks, the K5 packed small-group orderings and
 // the K3 fold columns, in that block order.  With TailDecide the node groups + K4 run in
-// the same launch: a column's groups are decided by whichever of its producers (its fold
-// block, the K2 blocks of its groups' pieces, the last tracker block when it has a dry
-// group) finishes last.  The fold blocks come last in the grid so that they are usually
-// that block and the decisions spread over the columns' own blocks.  (Before, K2 and K5
+// the same launch: a column's fold block waits (bounded) for the column's other producers —
+// the K2 blocks of its groups' pieces, the last tracker block when it has a dry group — and
+// decides the column's groups (fold_done); the fold blocks come last in the grid, so the
+// producers they wait for never wait themselves.  (Before, K2 and K5
 // ran on a side stream beside K1: K1 holds every CU's LDS and its loads starve K2's
 // latency-bound waves, so the side chain ended after K1 and the cross-stream join cost
 // ~10 us more (profiles/r02_v9 timeline): ~45 us after K1 at any pod count.)
@@ -2552,7 +2597,7 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
     } else {
         const uint32_t col = (uint32_t)(b - n_piece_blk - n_small);
         if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)col);
-        if (T.on) columns_done(G, N, F, T, &col, 1);
+        if (T.on) fold_done(G, N, F, T, col);
     }
 }
 

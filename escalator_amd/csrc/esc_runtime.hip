@@ -169,8 +169,9 @@ struct esc_ctx {
     uint64_t* d_pod_part = nullptr;
     uint32_t *d_col_off = nullptr, *d_col_groups = nullptr;   // K3: groups by pod slot column
     int k3_ablate = 0;                                        // ESC_K3_ABLATE (timing-only knob)
-    // node groups + decide fused into the tail (TailDecide; ESC_TAIL_FUSED=0: k_node_groups)
-    bool tail_fused = true, td_ready = false;
+    // node groups + decide fused into the tail (TailDecide; ESC_TAIL_FUSED=1).  Measured
+    // slower than the separate k_node_groups launch, so off by default.
+    bool tail_fused = false, td_ready = false;
     uint32_t *d_td_cnt = nullptr, *d_td_cnt0 = nullptr, *d_td_dep_off = nullptr, *d_td_dep_col = nullptr;
     uint32_t *d_td_dry_col = nullptr, *d_td_trk_done = nullptr;
     uint32_t td_n_dry = 0;

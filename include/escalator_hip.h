@@ -421,7 +421,8 @@ int32_t esc_force_wide(esc_ctx* ctx, int32_t enable);   /* testing: always take 
 int32_t esc_set_timing(esc_ctx* ctx, int32_t enable);
 int32_t esc_stage_times(esc_ctx* ctx, double* ms_out, int32_t n);
 /* K1 records per workgroup 8 words (s_memrealtime ticks at 100 MHz at start / after the K
- * tiles / after the C tiles / after the flush, HW_ID, XCC_ID, 0, 0) of the last decision;
+ * tiles / after the C tiles / after the flush, HW_ID, XCC_ID, class runs of its work plan,
+ * K weight of those runs in 16-B lane loads) of the last decision;
  * this copies them out (after esc_sync).  *n_out = workgroups; ESC_E_STATE before a run. */
 int32_t esc_k1_trace(esc_ctx* ctx, uint64_t* out, int64_t cap_words, int64_t* n_out);
 /* Calibrates K1's work split on this device: `rounds` decisions, each moving

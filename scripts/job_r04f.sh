@@ -4,7 +4,7 @@
 # shares: do class-run restarts cost the shard's K phase?).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-r04f}
+TAG=${TAG:-r04g}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
@@ -26,4 +26,7 @@ done
 echo "[job] $(date) config 5"
 timeout -k 10 300 python -u bench.py --config 5 --steps 20 --warmup 3 > $OUT/bench5.json 2> $OUT/bench5.err || { tail -30 $OUT/bench5.err; exit 1; }
 python -c "import json; d=json.load(open('$OUT/bench5.json')); print('config5', round(d['ms_per_step']*1e3,2), d['roofline'], d['age_index_build']['ms'], d['parity'])"
+echo "[job] $(date) k1 trace at 12.5M pods (calibrated)"
+PODS=12500000 CALIBRATE=10 timeout -k 10 300 python -u scripts/k1_trace.py > $OUT/k1_trace_p12.json 2> $OUT/k1_trace.err || { tail -30 $OUT/k1_trace.err; exit 1; }
+python -c "import json; d=json.load(open('$OUT/k1_trace_p12.json'))['variants']['0']; print({k: d[k] for k in ('kernel_us','k_phase_us_mean','k_phase_us_max','end_spread_us','k_phase_fit_us','runs_hist','k_phase_mean_by_runs')})"
 echo "[job] $(date) done"

@@ -63,6 +63,20 @@ for v in variants:
                         "end_mean_us": float((tr[xcc == x, 3] - t0).mean()) * 0.01,
                         "k_phase_mean_us": float((tr[xcc == x, 1] - tr[xcc == x, 0]).mean()) * 0.01}
                for x in sorted(set(xcc))}
+    # the cost of a class run: per-workgroup K phase ~ a + b * K weight + c * runs (least
+    # squares over every workgroup of every decision); c is what a run's restart costs
+    X, y = [], []
+    for r in runs:
+        ok = r[:, 6] > 0
+        X.append(np.stack([np.ones(ok.sum()), r[ok, 7].astype(np.float64), r[ok, 6].astype(np.float64)], 1))
+        y.append((r[ok, 1] - r[ok, 0]).astype(np.float64) * 0.01)
+    if X and sum(len(v) for v in y) > 3:
+        X, y = np.concatenate(X), np.concatenate(y)
+        coef, *_ = np.linalg.lstsq(X, y, rcond=None)
+        agg["k_phase_fit_us"] = {"intercept": float(coef[0]), "per_kweight_ns": float(coef[1] * 1e3),
+                                 "per_run": float(coef[2])}
+        agg["runs_hist"] = {int(k): int(v) for k, v in zip(*np.unique(runs[-1][:, 6], return_counts=True))}
+        agg["k_phase_mean_by_runs"] = {int(k): float(y[X[:, 2] == k].mean()) for k in np.unique(X[:, 2])}
     order = np.argsort(tr[:, 3])
     agg["slowest_blocks"] = [int(b) for b in order[-8:]]
     agg["per_xcc_last_run"] = per_xcc
