@@ -455,28 +455,8 @@ struct FoldPlan {
 hipError_t launch_touch(const PodDev& p, const GroupDev& g, int nblk, int tw, uint32_t* bits, hipStream_t st);
 struct OrdChunk;
 // The step's tail in one launch (esc_kernels.hip k_step_tail): the K3 fold into the pod
-// words, K2's dry-mode tracker entries (+ its piece rows when `spans`: no K1 ran) and,
+// words, K2's dry-mode tracker entries (+ its piece rows when `spans`) and,
 // with n_small > 0, the K5 ordering of the packed small-group chunks [0, n_small).
-// The node groups + decide fused into the tail ("one tail"): every fold column
-// waits for its own fold and for the node-side blocks its groups' words come from (K2 span
-// blocks; the dry-mode tracker blocks when a dry group is in it).  Each producer, when done,
-// decrements the counters of the columns it feeds; the block that brings a column's counter
-// to zero decides the column's groups (k_node_groups' work for those groups) and resets the
-// counter for the next step.  No block waits on another.
-struct TailDecide {
-    int on;                            // 0: k_node_groups runs after the tail instead
-    uint32_t* cnt;                     // [n_col] producers each column still waits for
-    const uint32_t* cnt0;              // [n_col] the full count (the decider restores it)
-    const uint32_t* dep_off;           // [span blocks + 1] the columns a K2 span block feeds (CSR)
-    const uint32_t* dep_col;
-    const uint32_t* dry_col;           // columns with a dry group: fed by the LAST tracker block
-    uint32_t n_dry_col;
-    uint32_t* trk_done;                // tracker blocks done this step (the last one resets it)
-    const int64_t* node_rows;
-    int64_t* trk_acc;
-    int64_t* nwords;
-    NGDecide nd;
-};
 // the tail's K2 span blocks (K2_WAVES spans each) and dry-mode tracker blocks for this node view
 constexpr int K2_WAVES = 4;
 int64_t tail_span_blocks(const NodeDev& n);
@@ -484,7 +464,7 @@ int64_t tail_trk_blocks(const NodeDev& n);
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
                             const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
-                            uint32_t* vals, int64_t* seg, const TailDecide& td, hipStream_t st);
+                            uint32_t* vals, int64_t* seg, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
 // §8f rank 2: a loaded pod as seen by NodePodsRemaining, listed per node (runs in
 // node order).  p[0..2]: the pod's extra pairs (NONE-padded); a C pod with more than 3

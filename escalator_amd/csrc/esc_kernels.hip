@@ -772,11 +772,7 @@ __device__ __forceinline__ void node_span(const NodeDev& N, int64_t* __restrict_
         unsigned long long x = 0;
 #pragma unroll
         for (int k = 0; k < NR_K; ++k) x = lane == k ? v[k] : x;
-        // write-through (sc1) stores: the fused tail's decider on another XCD reads them
-        // after the span's column counts (TailDecide), with no release fence
-        if (rows && lane < NR_K)
-            __hip_atomic_store(rows + (int64_t)lane * N.n_pieces + p, (int64_t)x, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        if (rows && lane < NR_K) rows[(int64_t)lane * N.n_pieces + p] = (int64_t)x;
         acc = PieceAcc();
         ++p;
         ps = pe;
@@ -806,6 +802,43 @@ __device__ __forceinline__ void node_span(const NodeDev& N, int64_t* __restrict_
     }
     while (p < p1) flush();                          // the span's last piece(s)
 }
+
+// Does node i carry label pair q (label0 or one of its ascending extra pairs)?
+__device__ __forceinline__ bool node_has_pair(const NodeDev& N, int64_t i, uint32_t q) {
+    const uint32_t l0 = N.label0[i];
+    if (l0 == q) return true;
+    if (l0 == NONE || l0 > q) return false;
+    const uint32_t nx = nf_xlbl(N.flags[i]), o = N.xl_off[i];
+    for (uint32_t k = 0; k < nx; ++k) {
+        const uint32_t x = N.xl[o + k];
+        if (x >= q) return x == q;
+    }
+    return false;
+}
+
+// Dry-mode tracker entry k (controller.go:128-133): a (node, dry group) entry whose node is
+// a live member of the group, in this rank's share of the group's pieces, adds the node to
+// the group's tracked sums (trk_acc, global atomics: a few thousand entries), which the node
+// groups read and reset.  Membership comes from the node's own labels: a pair's entries are
+// not node-sorted once relabels / adds have appended to them.
+__device__ __forceinline__ void tracker_entry(const NodeDev& N, const GroupDev& G, int64_t* __restrict__ trk_acc,
+                                              int64_t k) {
+    if (k >= N.n_trk) return;
+    const int32_t j = N.trk_node[k], g = N.trk_group[k];
+    if (!G.dry[g]) return;                           // wet groups ignore the tracker
+    const uint32_t q = G.gpair[g];
+    const int64_t plo = imax64((int64_t)N.pp_off[q], N.pc_lo), phi = imin64((int64_t)N.pp_off[q + 1], N.pc_hi);
+    if (phi <= plo) return;
+    if ((N.flags[j] & ESC_NF_ABSENT) || !node_has_pair(N, j, q)) return;
+    const int64_t c = N.cpu[j], m = N.mem[j];
+    int64_t* r = trk_acc + (int64_t)g * TA_K;
+    g_add(r + TA_CNT, 1);
+    g_add(r + TA_CPU_LO, (int64_t)((uint64_t)c & 0xFFFFFFFFull));
+    g_add(r + TA_CPU_HI, c >> 32);
+    g_add(r + TA_MEM_LO, (int64_t)((uint64_t)m & 0xFFFFFFFFull));
+    g_add(r + TA_MEM_HI, m >> 32);
+}
+
 }  // namespace
 
 // =====================================================================  K1 (fast)
@@ -1310,18 +1343,6 @@ __device__ __forceinline__ void node_groups(const NodeDev& N, const GroupDev& G,
     }
 }
 
-// Does node i carry label pair q (label0 or one of its ascending extra pairs)?
-__device__ __forceinline__ bool node_has_pair(const NodeDev& N, int64_t i, uint32_t q) {
-    const uint32_t l0 = N.label0[i];
-    if (l0 == q) return true;
-    if (l0 == NONE || l0 > q) return false;
-    const uint32_t nx = nf_xlbl(N.flags[i]), o = N.xl_off[i];
-    for (uint32_t k = 0; k < nx; ++k) {
-        const uint32_t x = N.xl[o + k];
-        if (x >= q) return x == q;
-    }
-    return false;
-}
 
 
 
@@ -1341,23 +1362,7 @@ __device__ __forceinline__ void node_piece_block(const NodeDev& N, const GroupDe
                                                  int64_t* __restrict__ rows, int64_t* __restrict__ trk_acc, int64_t blk) {
     const int lane = threadIdx.x & 63;
     if (blk >= nb_pieces) {
-        const int64_t k = (blk - nb_pieces) * (K2_WAVES * 64) + threadIdx.x;
-        if (k >= N.n_trk) return;
-        const int32_t j = N.trk_node[k], g = N.trk_group[k];
-        if (!G.dry[g]) return;                       // wet groups ignore the tracker
-        const uint32_t q = G.gpair[g];
-        const int64_t plo = imax64((int64_t)N.pp_off[q], N.pc_lo), phi = imin64((int64_t)N.pp_off[q + 1], N.pc_hi);
-        if (phi <= plo) return;
-        // membership from the node's own labels: the pair's entries are not node-sorted once
-        // relabels / adds have appended to them, and a removed first member leaves a spare
-        if ((N.flags[j] & ESC_NF_ABSENT) || !node_has_pair(N, j, q)) return;
-        const int64_t c = N.cpu[j], m = N.mem[j];
-        int64_t* r = trk_acc + (int64_t)g * TA_K;
-        g_add(r + TA_CNT, 1);
-        g_add(r + TA_CPU_LO, (int64_t)((uint64_t)c & 0xFFFFFFFFull));
-        g_add(r + TA_CPU_HI, c >> 32);
-        g_add(r + TA_MEM_LO, (int64_t)((uint64_t)m & 0xFFFFFFFFull));
-        g_add(r + TA_MEM_HI, m >> 32);
+        tracker_entry(N, G, trk_acc, (blk - nb_pieces) * (K2_WAVES * 64) + threadIdx.x);
         return;
     }
     // one wave per span of whole pieces (~NODE_SPAN entries): the span's entries stream
@@ -1426,7 +1431,7 @@ namespace {
 // k_node_groups' work for up to 64 groups, group gid (NONE: no group) on lane l of every
 // wave: the node words from the group pair's piece rows (the waves split the pieces), then
 // the decision or the exchange words.  With `seq` the groups are g_first + l and their
-// compact decisions go out as one contiguous run; else group by group (a fold column's).
+// compact decisions go out as one contiguous run; else group by group.
 __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDev& N,
                                                  const int64_t* __restrict__ node_rows,
                                                  int64_t* __restrict__ trk_acc, int64_t* __restrict__ nwords,
@@ -1542,8 +1547,8 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
 // and zero elsewhere.  With a decision target (D.dec: one rank, no exchange) the block then
 // decides its groups (K4 on this rank's fold) and writes the compact records to the
 // decision buffer as one contiguous run; otherwise it writes the words to the exchange
-// buffer (D.nx) and k_decide runs after the SUM.  (The default step fuses this work into
-// k_step_tail: TailDecide.)
+// buffer (D.nx) and k_decide runs after the SUM.  (Running this work inside k_step_tail's
+// fold blocks measured slower)
 __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeDev N,
                                                                const int64_t* __restrict__ node_rows,
                                                                int64_t* __restrict__ trk_acc,
@@ -1697,13 +1702,9 @@ __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, i
             const __int128 pcpu = (__int128)tot[0][sl] + ((__int128)wtot[WP_CPU_HI][sl] << 32) + (__int128)wtot[WP_CPU_LO][sl];
             const __int128 pmem = (__int128)(((unsigned __int128)tot[3][sl] << 64) | tot[2][sl]) +
                                   ((__int128)wtot[WP_MEM_HI][sl] << 32) + (__int128)wtot[WP_MEM_LO][sl];
-            // write-through (sc1) stores, as K2's rows (TailDecide: read by another block)
-            auto st = [&](int k, int64_t v) { __hip_atomic_store(pw + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-            st(PW_CPU_LO, (int64_t)((unsigned __int128)pcpu & 0xFFFFFFFFull));
-            st(PW_CPU_LO + 1, (int64_t)(pcpu >> 32));
-            st(PW_MEM_LO, (int64_t)((unsigned __int128)pmem & 0xFFFFFFFFull));
-            st(PW_MEM_LO + 1, (int64_t)(pmem >> 32));
-            st(PW_N, (int64_t)tot[1][sl] + wtot[WP_CNT][sl]);
+            split_store(pw, PW_CPU_LO, pcpu);
+            split_store(pw, PW_MEM_LO, pmem);
+            pw[PW_N] = (int64_t)tot[1][sl] + wtot[WP_CNT][sl];
         }
     }
 }
@@ -1853,7 +1854,10 @@ __device__ __forceinline__ void region_put(const RegionSink& S, uint32_t p, uint
 
 // FINAL (the age index's last pass): a key's sorted position goes straight into its group's
 // padded region (RegionSink) instead of the key / value arrays.
-constexpr int RS_U = 2;
+#ifndef ESC_RS_U
+#define ESC_RS_U 2         // keys per thread per scatter chunk (timing builds may override)
+#endif
+constexpr int RS_U = ESC_RS_U;
 template <class KT, class VT, int BITS, bool FINAL>
 __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict__ kin, const VT* __restrict__ vin,
                                                            KT* __restrict__ kout, VT* __restrict__ vout,
@@ -2460,101 +2464,11 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdCh
 // Before, K2 and K5 ran on a side stream beside K1: K1 holds every CU's LDS and its loads
 // starve K2's latency-bound waves, so the side chain ended after K1 and the cross-stream
 // join cost ~10 us more (profiles/r02_v9 timeline): ~45 us after K1 at any pod count.
-namespace {
-constexpr uint32_t TAIL_SPIN_MAX = 1u << 22;     // fold_done's poll bound (~0.1 s of s_sleep 1)
-// Producers of fold columns are done (TailDecide): this block decrements the count of each
-// column in cols[0, n) (one thread per column), and decides every column it brought to
-// zero (k_node_groups' work for the column's groups) after restoring its count for the
-// next step.  Hand-off (cdna_hip_programming.md Guideline 16, R1): the producers' words
-// (K2 rows, pod words) are write-through (sc1) stores, so a producer needs no release
-// fence, only every wave's store drain before the barrier and the count; the decider takes
-// ONE agent-scope acquire before it reads them.  (__threadfence() per producer block —
-// an L2 write-back each — made the step 0.6 ms.)  Dry-mode tracker sums are atomics.
-// Decide the columns cols[0, nr) (LDS) whose producers are all done: ONE agent-scope
-// acquire for the workgroup (L1 is per CU), then k_node_groups' work per column.
-__device__ __forceinline__ void decide_columns(const GroupDev& G, const NodeDev& N, const FoldPlan& F,
-                                               const TailDecide& T, const uint32_t* cols, uint32_t nr) {
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    for (uint32_t r = 0; r < nr; ++r) {
-        const uint32_t col = cols[r];
-        const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
-        for (uint32_t base = ga; base < gb; base += 64) {
-            const uint32_t l = threadIdx.x & 63, m = gb - base < 64 ? gb - base : 64u;
-            const uint32_t gid = l < m ? F.col_groups[base + l] : NONE;
-            node_groups_part(G, N, T.node_rows, T.trk_acc, T.nwords, T.nd, gid, false, 0, m);
-        }
-    }
-}
 
-__device__ __forceinline__ void columns_done(const GroupDev& G, const NodeDev& N, const FoldPlan& F,
-                                             const TailDecide& T, const uint32_t* cols, uint32_t n) {
-    __shared__ uint32_t s_ready[256];
-    __shared__ uint32_t s_n;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // this wave's sc1 stores / atomics are done
-    for (uint32_t c0 = 0; c0 < n; c0 += 256) {       // 256 columns per round, one per thread
-        __syncthreads();                             // every wave drained; the previous round's readers are done
-        if (threadIdx.x == 0) s_n = 0;
-        __syncthreads();
-        if (c0 + threadIdx.x < n) {
-            const uint32_t col = cols[c0 + threadIdx.x];
-            if (__hip_atomic_fetch_add(T.cnt + col, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
-                // every producer has counted: ready for the next step (the launch boundary orders it)
-                __hip_atomic_store(T.cnt + col, T.cnt0[col], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_ready[atomicAdd(&s_n, 1u)] = col;
-            }
-        }
-        __syncthreads();
-        const uint32_t nr = s_n;
-        if (nr == 0) continue;
-        decide_columns(G, N, F, T, s_ready, nr);
-    }
-}
-
-// The fold block of column `col` (the last role in the grid, so every producer of its
-// column was dispatched before it on its XCD and none of them waits): once its own pod
-// words are out it waits for the column's other producers — thread 0 polls the count,
-// relaxed, until only the fold's own unit is left — then decides the column.  So the
-// decisions run in the columns' own blocks, in parallel, instead of in whichever producer
-// happens to end last (at a rank's shard the folds end first and the last tracker block
-// decided every dry column in turn: 0.36 ms).  The poll is bounded: past it the fold counts
-// itself as an ordinary producer and the last one of them decides (columns_done), so the
-// result never depends on the bound.
-__device__ __forceinline__ void fold_done(const GroupDev& G, const NodeDev& N, const FoldPlan& F,
-                                          const TailDecide& T, uint32_t col) {
-    __shared__ uint32_t s_col[1];
-    __shared__ uint32_t s_go;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t spins = 0, go = 0;
-        for (;;) {
-            if (__hip_atomic_load(T.cnt + col, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u) { go = 1; break; }
-            if (++spins > TAIL_SPIN_MAX) {           // count the fold in; the last producer decides
-                go = __hip_atomic_fetch_add(T.cnt + col, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (go) __hip_atomic_store(T.cnt + col, T.cnt0[col], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_col[0] = col;
-        s_go = go;
-    }
-    __syncthreads();
-    if (s_go) decide_columns(G, N, F, T, s_col, 1);
-}
-}  // namespace
 
 // The step's tail in ONE launch (horizontal fusion; every role is 256 threads): the K2
 // node-piece blocks, the dry-mode tracker blocks, the K5 packed small-group orderings and
-// the K3 fold columns, in that block order.  With TailDecide the node groups + K4 run in
-// the same launch: a column's fold block waits (bounded) for the column's other producers —
-// the K2 blocks of its groups' pieces, the last tracker block when it has a dry group — and
-// decides the column's groups (fold_done); the fold blocks come last in the grid, so the
-// producers they wait for never wait themselves.  (Before, K2 and K5
+// the K3 fold columns, in that block order.  (Before, K2 and K5
 // ran on a side stream beside K1: K1 holds every CU's LDS and its loads starve K2's
 // latency-bound waves, so the side chain ended after K1 and the cross-stream join cost
 // ~10 us more (profiles/r02_v9 timeline): ~45 us after K1 at any pod count.)
@@ -2564,7 +2478,7 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
                                                    const OrdChunk* __restrict__ chunks, int64_t n_small,
                                                    const uint32_t* __restrict__ grp_off,
                                                    const uint32_t* __restrict__ g_memb, const uint32_t* __restrict__ g_grp,
-                                                   uint32_t* __restrict__ vals, int64_t* __restrict__ seg, TailDecide T) {
+                                                   uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
     static_assert(FD_WAVES * 64 == 256 && K2_WAVES * 64 == 256 && ORD_BLOCK == 256, "one block size for every role");
     const int64_t b = blockIdx.x;
     // F.ablate (ESC_K3_ABLATE, timing-only, wrong results): 8 / 16 / 32 skip the fold /
@@ -2573,23 +2487,6 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
         const int64_t pb = b;
         if (!(F.ablate & 16) && !((F.ablate & 64) && pb >= nb_pieces))
             node_piece_block(N, G, nb_pieces, (F.ablate & 128) ? nullptr : rows, trk_acc, pb);
-        if (T.on) {
-            if (pb < nb_pieces) {                            // a K2 span block: the columns it feeds
-                columns_done(G, N, F, T, T.dep_col + T.dep_off[pb], T.dep_off[pb + 1] - T.dep_off[pb]);
-            } else {                                         // a tracker block: the last one feeds the dry columns
-                __shared__ uint32_t s_lt;
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's tracker atomics are done
-                __syncthreads();
-                if (threadIdx.x == 0) {
-                    const uint32_t nt = (uint32_t)(n_piece_blk - nb_pieces);
-                    const uint32_t done = __hip_atomic_fetch_add(T.trk_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
-                    s_lt = done == nt;
-                    if (done == nt) __hip_atomic_store(T.trk_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                __syncthreads();
-                if (s_lt) columns_done(G, N, F, T, T.dry_col, T.n_dry_col);
-            }
-        }
     } else if (b < n_piece_blk + n_small) {
         if (!(F.ablate & 32))
             ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, g_memb, g_grp, vals, seg,
@@ -2597,7 +2494,6 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
     } else {
         const uint32_t col = (uint32_t)(b - n_piece_blk - n_small);
         if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)col);
-        if (T.on) fold_done(G, N, F, T, col);
     }
 }
 
@@ -3026,14 +2922,13 @@ int64_t tail_trk_blocks(const NodeDev& n) { return (n.n_trk + K2_WAVES * 64 - 1)
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
                             const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
-                            uint32_t* vals, int64_t* seg, const TailDecide& td, hipStream_t st) {
+                            uint32_t* vals, int64_t* seg, hipStream_t st) {
     const int64_t nb = spans ? tail_span_blocks(n) : 0;      // else K1 made the rows
     const int64_t nt = tail_trk_blocks(n);
     const int64_t grid = f.n_col + nb + nt + std::max<int64_t>(n_small, 0);
     if (grid <= 0) return hipSuccess;
-    if (td.on && !spans) return hipErrorInvalidValue;       // the column counts assume the span blocks
     hipLaunchKernelGGL(k_step_tail, dim3((unsigned)grid), dim3(256), 0, st, g, n, f, wide_pod, pwords, nb, nb + nt, rows,
-                       trk_acc, chunks, std::max<int64_t>(n_small, 0), grp_off, g_memb, g_grp, vals, seg, td);
+                       trk_acc, chunks, std::max<int64_t>(n_small, 0), grp_off, g_memb, g_grp, vals, seg);
     return hipGetLastError();
 }
 

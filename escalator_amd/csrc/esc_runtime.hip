@@ -169,12 +169,6 @@ struct esc_ctx {
     uint64_t* d_pod_part = nullptr;
     uint32_t *d_col_off = nullptr, *d_col_groups = nullptr;   // K3: groups by pod slot column
     int k3_ablate = 0;                                        // ESC_K3_ABLATE (timing-only knob)
-    // node groups + decide fused into the tail (TailDecide; ESC_TAIL_FUSED=1).  Measured
-    // slower than the separate k_node_groups launch, so off by default.
-    bool tail_fused = false, td_ready = false;
-    uint32_t *d_td_cnt = nullptr, *d_td_cnt0 = nullptr, *d_td_dep_off = nullptr, *d_td_dep_col = nullptr;
-    uint32_t *d_td_dry_col = nullptr, *d_td_trk_done = nullptr;
-    uint32_t td_n_dry = 0;
     int64_t* d_wide_pod = nullptr;
     uint32_t* d_k1_ticket = nullptr;                          // K1 dynamic shares (next chunk, done)
     int64_t* d_k1seg = nullptr;                               // K1 work plan [nblk][K1_SEGS][2]
@@ -500,78 +494,12 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
     return ESC_OK;
 }
 
-void release_tail_deps(esc_ctx* c) {
-    dfree(c->d_td_cnt); dfree(c->d_td_cnt0); dfree(c->d_td_dep_off); dfree(c->d_td_dep_col); dfree(c->d_td_dry_col);
-    dfree(c->d_td_trk_done);
-    c->td_n_dry = 0;
-    c->td_ready = false;
-}
-
-// The fused tail's producer counts (TailDecide) for the current node view: fold column c
-// waits for its own fold block, for every K2 span block whose pieces meet one of its groups'
-// piece ranges (this rank's share), and — when the step has tracker blocks and a dry group
-// sits in c — for the last tracker block.  Rebuilt when the nodes or the tracker list change.
-int32_t build_tail_deps(esc_ctx* c) {
-    release_tail_deps(c);
-    if (!c->tail_fused) return ESC_OK;
-    const NodeDev n = node_dev(c);
-    const int64_t n_col = slot_stride(c) / FC_COL, nb = tail_span_blocks(n);
-    const bool trk = tail_trk_blocks(n) > 0;
-    std::vector<uint32_t> span_off((size_t)c->n_spans + 1, 0), col_off((size_t)n_col + 1), col_groups(c->gi.G);
-    if (c->n_spans) HIP_TRY(hipMemcpy(span_off.data(), c->nodes.span_off, span_off.size() * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(col_off.data(), c->d_col_off, col_off.size() * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(col_groups.data(), c->d_col_groups, col_groups.size() * 4, hipMemcpyDeviceToHost));
-    // block b's pieces: [span_off[b * K2_WAVES], span_off[min((b + 1) * K2_WAVES, n_spans)])
-    std::vector<int64_t> blk_lo((size_t)nb), blk_hi((size_t)nb);
-    for (int64_t b = 0; b < nb; ++b) {
-        blk_lo[b] = span_off[b * K2_WAVES];
-        blk_hi[b] = span_off[std::min<int64_t>((b + 1) * K2_WAVES, c->n_spans)];
-    }
-    std::vector<uint32_t> cnt0((size_t)n_col, 1), dry;
-    std::vector<std::vector<uint32_t>> feeds((size_t)nb);
-    std::vector<int64_t> last((size_t)nb, -1);
-    for (int64_t col = 0; col < n_col; ++col) {
-        bool has_dry = false;
-        for (uint32_t k = col_off[col]; k < col_off[col + 1]; ++k) {
-            const uint32_t g = col_groups[k];
-            has_dry |= c->params[g].dry != 0;
-            const GroupNode& x = c->h_gnode[g];
-            if (x.phi <= x.plo || nb == 0) continue;
-            // the first block whose pieces end past plo, up to the last starting before phi
-            int64_t b = std::upper_bound(blk_hi.begin(), blk_hi.end(), x.plo) - blk_hi.begin();
-            for (; b < nb && blk_lo[b] < x.phi; ++b)
-                if (last[b] != col) { last[b] = col; feeds[b].push_back((uint32_t)col); ++cnt0[col]; }
-        }
-        if (has_dry && trk) { dry.push_back((uint32_t)col); ++cnt0[col]; }
-    }
-    std::vector<uint32_t> dep_off((size_t)nb + 1, 0), dep_col;
-    for (int64_t b = 0; b < nb; ++b) {
-        dep_col.insert(dep_col.end(), feeds[b].begin(), feeds[b].end());
-        dep_off[b + 1] = (uint32_t)dep_col.size();
-    }
-    HIP_TRY(dalloc(&c->d_td_cnt, std::max<size_t>(cnt0.size(), 1))); HIP_TRY(dalloc(&c->d_td_cnt0, std::max<size_t>(cnt0.size(), 1)));
-    HIP_TRY(dalloc(&c->d_td_dep_off, dep_off.size())); HIP_TRY(dalloc(&c->d_td_dep_col, std::max<size_t>(dep_col.size(), 1)));
-    HIP_TRY(dalloc(&c->d_td_dry_col, std::max<size_t>(dry.size(), 1))); HIP_TRY(dalloc(&c->d_td_trk_done, 1));
-    if (n_col) {
-        HIP_TRY(hipMemcpy(c->d_td_cnt, cnt0.data(), cnt0.size() * 4, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(c->d_td_cnt0, cnt0.data(), cnt0.size() * 4, hipMemcpyHostToDevice));
-    }
-    HIP_TRY(hipMemcpy(c->d_td_dep_off, dep_off.data(), dep_off.size() * 4, hipMemcpyHostToDevice));
-    if (!dep_col.empty()) HIP_TRY(hipMemcpy(c->d_td_dep_col, dep_col.data(), dep_col.size() * 4, hipMemcpyHostToDevice));
-    if (!dry.empty()) HIP_TRY(hipMemcpy(c->d_td_dry_col, dry.data(), dry.size() * 4, hipMemcpyHostToDevice));
-    HIP_TRY(hipMemset(c->d_td_trk_done, 0, 4));
-    c->td_n_dry = (uint32_t)dry.size();
-    c->td_ready = true;
-    return ESC_OK;
-}
-
 void release_work(esc_ctx* c) {
     dfree(c->d_k1seg); dfree(c->d_pod_part); dfree(c->d_wide_pod); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
     dfree(c->d_k1_trace);
     dfree(c->d_touch); dfree(c->d_wg_cols); dfree(c->d_wg_off); dfree(c->d_col_rows);
     c->touch_on = false;
     dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_cdec); dfree(c->d_metrics);
-    release_tail_deps(c);
     c->d_pwords = nullptr;
     if (c->h_cdec) hipHostFree(c->h_cdec);
     c->h_cdec = nullptr;
@@ -1119,8 +1047,7 @@ int32_t ensure_work(esc_ctx* c) {
     HIP_TRY(dalloc(&c->d_wg_off, (size_t)nblk + 1));
     HIP_TRY(dalloc(&c->d_col_rows, (size_t)n_col + 1));
     c->work_ready = true;
-    if (int32_t rc = touch_refresh(c, plan)) return rc;
-    return build_tail_deps(c);
+    return touch_refresh(c, plan);
 }
 
 // Enqueue one step for replica r on the context's stream, three launches in order:
@@ -1130,6 +1057,7 @@ int32_t ensure_work(esc_ctx* c) {
 //        in the step,
 //   D   k_node_groups: the node words, then K4 + the decisions when `decide` (one rank;
 //        after an exchange esc_decide launches K4 alone).
+// (Fusing D into the tail, and K2 into K1, measured slower: DESIGN.md §8e.)
 // The ordering's remaining kernels (split groups, mid-size packed chunks) follow the tail.
 // Everything is on one stream: K1 fills every CU's LDS, so nothing overlaps it usefully,
 // and a cross-stream join cost ~10 us per step.  With timing on each
@@ -1172,17 +1100,8 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     f.col_rows = nblk && c->touch_on ? c->d_col_rows : nullptr;
     f.ablate = c->k3_ablate;
     const bool ord = c->order_in_step;
-    // D reads and resets the tracker sums the tail accumulated (once per step); a sharded
-    // step (no decide) computes the node words only and esc_decide runs K4 after the exchange
-    NGDecide nd{nullptr, nullptr, nullptr, node_xwords(c)};
-    if (decide) nd = NGDecide{c->d_pwords, c->d_dec, cdec, nullptr};
-    TailDecide td{};
-    if (c->td_ready) {
-        td = TailDecide{1, c->d_td_cnt, c->d_td_cnt0, c->d_td_dep_off, c->d_td_dep_col, c->d_td_dry_col, c->td_n_dry,
-                        c->d_td_trk_done, c->nodes.rows, c->d_trk_acc, c->d_nwords, nd};
-    }
     HIP_TRY(launch_step_tail(g, n, f, true, c->d_wide_pod, c->d_pwords, c->nodes.rows, c->d_trk_acc, c->d_pchunks,
-                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, td, st));
+                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, st));
     if (int32_t rc = mark()) return rc;
     if (ord) {                                       // split groups, mid-size packed chunks
         HIP_TRY(launch_order(n, c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb, c->d_g_grp,
@@ -1192,7 +1111,11 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
                                     c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, st));
     }
     if (int32_t rc = mark()) return rc;
-    if (!td.on) HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, nd, st));
+    // D reads and resets the tracker sums the tail accumulated (once per step); a sharded
+    // step (no decide) computes the node words only and esc_decide runs K4 after the exchange
+    NGDecide nd{nullptr, nullptr, nullptr, node_xwords(c)};
+    if (decide) nd = NGDecide{c->d_pwords, c->d_dec, cdec, nullptr};
+    HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, nd, st));
     if (int32_t rc = mark()) return rc;
     if (copy_out && !c->zero_copy) {
         HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)g.G * sizeof(DecCompact), hipMemcpyDeviceToHost, st));
@@ -1268,7 +1191,7 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     }
     if (const char* v = std::getenv("ESC_ORDER_ABLATE")) c->order_ablate = std::atoi(v);
     if (const char* v = std::getenv("ESC_K3_ABLATE")) c->k3_ablate = std::atoi(v);
-    if (const char* v = std::getenv("ESC_TAIL_FUSED")) c->tail_fused = std::atoi(v) != 0;
+
     if (const char* v = std::getenv("ESC_ORDER_CHUNK")) {      // 4096 / 8192 / 16384 (measurement knob)
         const int64_t k = std::atoll(v);
         if (k == 4096 || k == 8192 || k == 16384) c->ord_chunk = k;
@@ -2890,7 +2813,7 @@ int32_t write_tracker(esc_ctx* c, std::vector<uint64_t>& next) {
     c->h_trk.swap(next);
     c->n_trk = nt;
     drop_graphs(c);
-    return c->work_ready ? build_tail_deps(c) : ESC_OK;      // the dry columns wait for tracker blocks or not
+    return ESC_OK;
 }
 
 }  // namespace

@@ -305,26 +305,6 @@ def test_k1_calibrated_shares_vs_c_oracle(esc, cfg, P, N, G):
         check_against_c_oracle(*ctx.results(), otot, odf, odi)
 
 
-@pytest.mark.parametrize("graph", [False, True])
-def test_tail_fused_vs_c_oracle(esc, graph, monkeypatch):
-    """ESC_TAIL_FUSED=1: the node groups + decide inside k_step_tail (fold blocks wait for
-    their column's K2 / tracker producers, then decide): repeated decisions (the column counts
-    restore themselves), with and without a graph, config 4's dry-mode groups and trackers."""
-    monkeypatch.setenv("ESC_TAIL_FUSED", "1")
-    s = esc.Synth(2_000_000, 20_000, 10_000, config=4, seed=0xE5CA1A7E00000004)
-    otot = soa.totals(s.pods(), s.nodes(), s.groups)
-    odf, odi = soa.decide(s.groups, s.states, otot)
-    ctx = esc.Context(s)
-    ctx.load_synth(s, replicas=2)
-    ctx.use_graph(graph)
-    ctx.set_state(s.states)
-    ctx.set_order_in_step(True)
-    for _ in range(5):
-        ctx.run()
-        tot, dec = ctx.results()
-        check_against_c_oracle(tot, dec, otot, odf, odi)
-
-
 @pytest.mark.parametrize("variant", ["5"])
 def test_k1_variants_vs_c_oracle(esc, variant, monkeypatch):
     """The exact K1 variant (ESC_K1_VARIANT 5: dynamic shares from the ticket counter —
@@ -1375,16 +1355,13 @@ def test_reaping_sharded_host_exchange(esc, graphless):
 
 
 # ------------------------------------------------ dry-mode taintTracker (§8f rank 4)
-@pytest.mark.parametrize("seed,fused", [(0, "0"), (1, "0"), (2, "0"), (3, "0"), (0, "1"), (1, "1")])
-def test_tracker_updates_vs_literal(esc, seed, fused, monkeypatch):
+@pytest.mark.parametrize("seed", range(4))
+def test_tracker_updates_vs_literal(esc, seed):
     """Dry-mode bookkeeping in place (esc_tracker_update): each round every dry group
     "untaints" its newest tracked members and "taints" its oldest untracked ones, as
     untaintNewestN / taintOldestN do in dry mode (scale_up.go:146-158,
     scale_down.go:197-200); decisions, both orderings and the tracker lists then equal the
-    literal oracle over the updated name slices.  Wet groups' trackers are ignored.
-    fused=1: the node groups + decide inside the tail (ESC_TAIL_FUSED; its column counts are
-    rebuilt when the tracker list changes)."""
-    monkeypatch.setenv("ESC_TAIL_FUSED", fused)
+    literal oracle over the updated name slices.  Wet groups' trackers are ignored."""
     rng = random.Random(9700 + seed)
     G = rng.choice([3, 8])
     groups = make_groups(rng, G, with_default=True)
