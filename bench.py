@@ -569,7 +569,11 @@ def main():
         k1.append(st[0])
         stages.append(st)
     ctx.set_timing(False)
-    k1_ms = float(np.mean(k1))
+    k1_stage_ms = float(np.mean(k1))
+    # the roofline's K1 time: back-to-back K1 launches between two HIP events on the
+    # context's stream (esc_k1_time) -- the stage events above add their own gap to a short
+    # kernel (0.83x rocprof's duration at a rank's shard with them)
+    k1_ms = ctx.k1_time(50)
     # stages of enqueue_step in timing mode: K1, the fused tail (fold + node pieces + packed
     # small-group orderings), the remaining ordering kernels, node groups (+ decide), [copy]
     stage_names = (["k_pod_reduce", "k_step_tail", "k_order_split", "k_node_groups"] +
@@ -658,6 +662,8 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src if traffic else None,
                      "algorithmic_bytes_per_launch": algo, "launch_ms": k1_ms,
+                     "launch_ms_how": "esc_k1_time: 50 back-to-back K1 launches between two HIP events",
+                     "launch_ms_stage_events": k1_stage_ms,
                      "box_read_ceiling_GBps": probe,
                      "frac_of_box_ceiling": achieved / probe if probe else None},
         "frac_baseline_md": frac_md,

@@ -184,6 +184,7 @@ _SIGS = {
     "esc_stage_times": (i32, [VP, P(dbl), i32]),
     "esc_k1_trace": (i32, [VP, P(C.c_uint64), i64, P(i64)]),
     "esc_k1_calibrate": (i32, [VP, i32]),
+    "esc_k1_time": (i32, [VP, i32, P(C.c_double)]),
     "esc_k1_flush_entries": (i32, [VP, P(i64), P(i64)]),
     "esc_sort_nodes": (i32, [VP]),
     "esc_set_order_in_step": (i32, [VP, i32]),

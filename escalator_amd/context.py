@@ -351,6 +351,12 @@ class Context:
         L.check(self.lib.esc_hbm_probe(self.handle, int(nbytes), int(reps), C.byref(v)), "esc_hbm_probe")
         return v.value
 
+    def k1_time(self, reps=20):
+        """K1's mean device time in ms over `reps` back-to-back launches (esc_k1_time)."""
+        ms = C.c_double(0)
+        L.check(self.lib.esc_k1_time(self.handle, int(reps), C.byref(ms)), "esc_k1_time")
+        return ms.value
+
     def k1_trace(self):
         """Per-workgroup K1 timestamps of the last decision (diagnostics):
         uint64 [nblk, 8] = start, K tiles done, C tiles done, flushed (100 MHz ticks), HW_ID, XCC_ID."""

@@ -1562,11 +1562,14 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
 // K4 alone (esc_decide after an exchange): the pod and node words are the exchanged sums
 // (the node words exact from their owner rank); the final node words are kept for
 // esc_results.
-__global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ pwords,
-                                                const int64_t* __restrict__ nx, int64_t* __restrict__ nwords,
-                                                esc_group_decision* __restrict__ dec, DecCompact* __restrict__ cdec) {
-    __shared__ DecCompact sc[256];
-    const int32_t g0 = blockIdx.x * 256, g = g0 + (int32_t)threadIdx.x;
+// One wave per 64 groups (a latency chain per group: 40 blocks of 256 threads left most CUs
+// idle, 8.5 us for 10 k groups).
+constexpr int KD_BLOCK = 64;
+__global__ __launch_bounds__(KD_BLOCK) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ pwords,
+                                                     const int64_t* __restrict__ nx, int64_t* __restrict__ nwords,
+                                                     esc_group_decision* __restrict__ dec, DecCompact* __restrict__ cdec) {
+    __shared__ DecCompact sc[KD_BLOCK];
+    const int32_t g0 = blockIdx.x * KD_BLOCK, g = g0 + (int32_t)threadIdx.x;
     if (g < G.G) {
         const int64_t* x = nx + (int64_t)g * NX_K;
         const uint64_t cnt = (uint64_t)x[NX_CNT], cf = (uint64_t)x[NX_CORD];
@@ -1581,8 +1584,8 @@ __global__ __launch_bounds__(256) void k_decide(GroupDev G, NodeDev N, const int
         sc[threadIdx.x] = compact_of(d);
     }
     __syncthreads();
-    const uint32_t n = G.G - g0 < 256 ? (uint32_t)(G.G - g0) : 256u;
-    store_compact(cdec, sc, n, true, (uint32_t)g0, nullptr, threadIdx.x, 256);
+    const uint32_t n = G.G - g0 < KD_BLOCK ? (uint32_t)(G.G - g0) : (uint32_t)KD_BLOCK;
+    store_compact(cdec, sc, n, true, (uint32_t)g0, nullptr, threadIdx.x, KD_BLOCK);
 }
 
 // K3 fold (fold_col, a role of k_step_tail): the K1 workgroups' slot partials folded and
@@ -2876,7 +2879,8 @@ hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t
 
 hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords, const int64_t* nx,
                          int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st) {
-    hipLaunchKernelGGL(k_decide, dim3((g.G + 255) / 256), dim3(256), 0, st, g, n, pwords, nx, nwords, dec, cdec);
+    hipLaunchKernelGGL(k_decide, dim3((g.G + KD_BLOCK - 1) / KD_BLOCK), dim3(KD_BLOCK), 0, st, g, n, pwords, nx, nwords,
+                       dec, cdec);
     return hipGetLastError();
 }
 

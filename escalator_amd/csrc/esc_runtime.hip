@@ -2073,6 +2073,35 @@ int32_t esc_k1_trace(esc_ctx* c, uint64_t* out, int64_t cap, int64_t* n_out) {
     return ESC_OK;
 }
 
+int32_t esc_k1_time(esc_ctx* c, int32_t reps, double* ms_per_launch) {
+    if (c && c->multi) return esc_k1_time(esc::multi_sub(c, 0), reps, ms_per_launch);
+    if (!ms_per_launch || reps < 1) return ESC_E_INVAL;
+    int32_t rc = check_ready(c);
+    if (rc) return rc;
+    if (c->force_wide || !c->nblk) return ESC_E_STATE;
+    hipSetDevice(c->device);
+    hipStream_t st = c->stream;
+    const PodDev p = pod_dev(c, c->cur);
+    const GroupDev g = group_dev(c);
+    const int32_t S = (int32_t)pod_slots(c);
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipEventRecord(c->ev[0], st));
+    for (int32_t k = 0; k < reps; ++k)
+        for (int32_t g0 = 0; g0 < S; g0 += POD_WINDOW_MAX) {
+            const K1Diag diag{c->d_k1_trace};
+            HIP_TRY(launch_pod_reduce(p, g, g0, std::min(POD_WINDOW_MAX, S - g0), c->nblk, c->k1_variant, c->d_pod_part,
+                                      c->d_wide_pod, c->d_k1_ticket, c->k1_cap, diag, st));
+        }
+    HIP_TRY(hipEventRecord(c->ev[1], st));
+    // the exact-path accumulators K1 added to without a fold: back to zero for the next step
+    HIP_TRY(hipMemsetAsync(c->d_wide_pod, 0, (size_t)pod_slots(c) * WP_K * sizeof(int64_t), st));
+    HIP_TRY(hipStreamSynchronize(st));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    *ms_per_launch = (double)ms / reps;
+    return ESC_OK;
+}
+
 int32_t esc_reduce(esc_ctx* c) {
     if (c && c->multi) return ESC_E_STATE;             // the exchange is internal: esc_step
     int32_t rc = check_ready(c);

@@ -3,7 +3,7 @@
 # then rocprofv3 --kernel-trace --stats of the SAME command, then separate --pmc passes
 # (FETCH_SIZE, WRITE_SIZE; nothing else combined with --pmc), at full size (config 4, N=1)
 # and at rank 0's shard of N=8 (--shard-of 8); scripts/prof_summary.py keeps the timed
-# launches (the last steps + 10 of every decision kernel) into gpurun_out/$TAG/profiles/.
+# launches (K1: the 50 back-to-back launches bench.py times last) into gpurun_out/$TAG/profiles/.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-r04_prof}
@@ -31,7 +31,7 @@ prof_set() {   # name, bench args...
     local wr=$(find $OUT/write_$name -name "run_counter_collection.csv" | head -1)
     cp $st $PROF/kernel_stats_$name.csv
     cp $OUT/bench_$name.json $PROF/bench_$name.json
-    python3 scripts/prof_summary.py --trace $tr --fetch $fe --write $wr --last 30 --bench $OUT/bench_$name.json \
+    python3 scripts/prof_summary.py --trace $tr --fetch $fe --write $wr --last 50 --bench $OUT/bench_$name.json \
         --out $PROF/summary_$name.json
 }
 prof_set full --steps 20 --warmup 5 || exit 1

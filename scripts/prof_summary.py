@@ -5,10 +5,11 @@
         --last 30 --bench bench.json --out summary.json
 
 A bench.py run launches K1 (k_pod_reduce) outside its timed region too: the share
-calibration (esc_k1_calibrate, 16 rounds of decisions) and the warm-up steps.  The timed
-region and the per-stage timing steps are the LAST `--last` launches of every decision
-kernel (steps + min(steps, 10) for bench.py's defaults), so this keeps exactly those, by
-Dispatch_Id, for:
+calibration (esc_k1_calibrate, 16 rounds of decisions) and the warm-up steps.  bench.py's
+roofline times K1 LAST, as 50 back-to-back launches between two HIP events (esc_k1_time),
+so `--last 50` keeps exactly those K1 launches (by Dispatch_Id); for the other decision
+kernels the last `--last` launches are the timed steps and the per-stage timing steps.
+Kept launches feed:
   - the kernel trace (--trace, run_kernel_trace.csv of `rocprofv3 --kernel-trace`): mean and
     median duration per launch;
   - the PMC passes (--fetch / --write, run_counter_collection.csv of separate `--pmc
