@@ -91,7 +91,9 @@ def cpu_baseline(cfg, G, full=None, seconds=12.0):
       the whole snapshot ``full`` on every host core this process may use — the honest
       "best CPU" comparator of BASELINE.md §4 (decision math excluded: O(G));
     - reference-shaped: one full rescan per group, single thread like the reference's
-      RunOnce (controller.go:416), on a bounded sample, extrapolated to all groups."""
+      RunOnce (controller.go:416): over the whole snapshot for a spread of groups,
+      extrapolated to all groups (round 3 used a 2 M-pod sample and extrapolated twice;
+      that remains the fallback when the rank holds no full snapshot)."""
     import numpy as np
     from escalator_amd.context import Synth
     from oracle import soa
@@ -103,37 +105,58 @@ def cpu_baseline(cfg, G, full=None, seconds=12.0):
         n_rec = len(pods["flags"]) + len(nodes["flags"])
         soa.totals(pods, nodes, full.groups, threads=threads)          # warm the pages
         ts, t0 = [], time.perf_counter()
-        while len(ts) < 10 or time.perf_counter() - t0 < 3.0:
+        while len(ts) < 30 or time.perf_counter() - t0 < 6.0:
             t1 = time.perf_counter()
             soa.totals(pods, nodes, full.groups, threads=threads)
             ts.append(time.perf_counter() - t1)
         dt = float(np.median(ts))
+        q1, q3 = np.percentile(ts, [25, 75])
         out["value"] = n_rec / dt
         out["spread"] = [n_rec / max(ts), n_rec / min(ts)]
+        out["iqr"] = [float(n_rec / q3), float(n_rec / q1)]
         out["sample"] = ("B-opt: oracle/esc_oracle.c orc_totals_par (single pass over the SoA snapshot, per-thread "
                          "group accumulators, OpenMP) over the full %d-record snapshot on %d threads, median of %d "
-                         "passes, %.3f s per decision" % (n_rec, threads, len(ts), dt))
-    P_s, N_s = 2_000_000, 20_000
-    s = Synth(P_s, N_s, G, config=cfg["cfg"], seed=0xE5CA1A7E00000000 + cfg["cfg"], threads=16)
-    pods, nodes = s.pods(), s.nodes()
+                         "passes (iqr: their middle half), %.3f s per decision" % (n_rec, threads, len(ts), dt))
+    if full is not None:
+        # the whole snapshot, rescanned once per group for a spread of groups (every
+        # (G / k)-th), k sized to ~`seconds`: only the group count is extrapolated — the
+        # scan's per-record cost depends on the records streamed from DRAM, which a small
+        # pod sample (cache-resident on this host) would understate
+        pods, nodes, groups = full.pods(), full.nodes(), full.groups
+        P_s, N_s = len(pods["flags"]), len(nodes["flags"])
+        t0 = time.perf_counter()
+        soa.totals(pods, nodes, groups, reference_shaped=True, g_range=(G // 2, G // 2 + 1))
+        t1 = time.perf_counter() - t0
+        k = int(max(1, min(G, seconds / max(t1, 1e-6))))
+        picks = sorted(set(int(i * G // k) for i in range(k)))
+        t0 = time.perf_counter()
+        for g in picks:
+            soa.totals(pods, nodes, groups, reference_shaped=True, g_range=(g, g + 1))
+        t_scan = time.perf_counter() - t0
+        how = "the full %d-pod / %d-node snapshot, %d of %d groups (every %d-th) timed (%.1f s), extrapolated " \
+              "linearly to all groups" % (P_s, N_s, len(picks), G, max(1, G // k), t_scan)
+    else:
+        P_s, N_s = 2_000_000, 20_000
+        s = Synth(P_s, N_s, G, config=cfg["cfg"], seed=0xE5CA1A7E00000000 + cfg["cfg"], threads=16)
+        pods, nodes, groups = s.pods(), s.nodes(), s.groups
+        t0 = time.perf_counter()
+        soa.totals(pods, nodes, groups, reference_shaped=True, g_range=(1, 2))
+        t1 = time.perf_counter() - t0
+        picks = list(range(1, 1 + int(max(1, min(G - 1, seconds / max(t1, 1e-6))))))
+        t0 = time.perf_counter()
+        soa.totals(pods, nodes, groups, reference_shaped=True, g_range=(picks[0], picks[-1] + 1))
+        t_scan = time.perf_counter() - t0
+        how = "a %d-pod / %d-node sample of the same config, %d of %d groups timed (%.1f s), extrapolated linearly " \
+              "to the snapshot and to all groups" % (P_s, N_s, len(picks), G, t_scan)
+    per_group = t_scan / len(picks)
     t0 = time.perf_counter()
-    soa.totals(pods, nodes, s.groups, reference_shaped=True, g_range=(1, 2))
-    t1 = time.perf_counter() - t0
-    g_s = int(max(1, min(G - 1, seconds / max(t1, 1e-6))))
-    t0 = time.perf_counter()
-    soa.totals(pods, nodes, s.groups, reference_shaped=True, g_range=(1, 1 + g_s))
-    t_scan = time.perf_counter() - t0
-    per_group = t_scan / g_s
-    t0 = time.perf_counter()
-    soa.totals(pods, nodes, s.groups)
+    soa.totals(pods, nodes, groups)
     t_single = time.perf_counter() - t0
-    np.asarray(0)
     ref = {
         "value": (P_s + N_s) / (per_group * G),
         "cores": 1,
         "sample": ("oracle/esc_oracle.c orc_ref_scan (reference-shaped: every group rescans all pods and nodes, "
-                   "controller.go:416 + pod_listers.go:33) over a %d-pod / %d-node sample of the same config, "
-                   "%d of %d groups timed (%.1f s), extrapolated linearly to all groups" % (P_s, N_s, g_s, G, t_scan)),
+                   "controller.go:416 + pod_listers.go:33) over " + how),
         "single_pass_1thread_records_per_s": (P_s + N_s) / t_single,
     }
     out["reference_shaped"] = ref

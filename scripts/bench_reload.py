@@ -4,7 +4,8 @@ snapshot, what a host does when an event batch does not fit the spare room (ESC_
     python scripts/bench_reload.py [--pods 100000000] [--reps 2]
 
 Times, on the GPU box's host threads (ESC_HOST_THREADS / OMP_NUM_THREADS, 16 per GPU):
-  pack  — esc_packer_create + esc_packer_add_pods / _add_nodes + esc_packer_view over the
+  pack  — esc_packer_create + esc_packer_add_pods / _add_nodes + the dry-mode trackers
+          (esc_packer_set_tracker, node names per dry group) + esc_packer_view over the
           snapshot's object structs (esc_synth_objects: what the cgo shim fills from
           *v1.Pod / *v1.Node; the objects themselves are built before the clock starts);
   load  — esc_load_pods + esc_load_nodes of the packer's arrays into a fresh context (one
@@ -39,6 +40,13 @@ def main():
     po, npods, no, nnodes = s.objects()
     gen_s = time.perf_counter() - t0
     lib = L.load()
+    # the dry-mode taintTrackers (controller.go:128-133): node names per dry group, as the
+    # controller holds them; set on the packer with the objects
+    nd = s.nodes()
+    trk = {}
+    for j, g in zip(nd["trk_node"].tolist(), nd["trk_group"].tolist()):
+        trk.setdefault(g, []).append(b"node-%d" % j)
+    trk_c = {g: (C.c_char_p * len(v))(*v) for g, v in trk.items()}
     res = {"pack_s": [], "load_s": []}
     tot = dec = None
     for _ in range(args.reps):
@@ -48,6 +56,8 @@ def main():
         L.check(lib.esc_packer_create(ctx.handle, C.byref(pk)), "esc_packer_create")
         L.check(lib.esc_packer_add_pods(pk, po, npods), "esc_packer_add_pods")
         L.check(lib.esc_packer_add_nodes(pk, no, nnodes), "esc_packer_add_nodes")
+        for g, arr in trk_c.items():
+            L.check(lib.esc_packer_set_tracker(pk, g, arr, len(arr)), "esc_packer_set_tracker")
         ps, ns = L.PodSoA(), L.NodeSoA()
         L.check(lib.esc_packer_view(pk, C.byref(ps), C.byref(ns)), "esc_packer_view")
         t1 = time.perf_counter()
