@@ -17,6 +17,7 @@
 #include <cstring>
 #include <new>
 #include <set>
+#include <string_view>
 #include <thread>
 
 #include "esc_internal.h"
@@ -517,19 +518,19 @@ int32_t esc_packer_set_tracker(esc_packer* pk, int32_t group, const char* const*
 int32_t esc_packer_view(esc_packer* pk, esc_pod_soa* pods, esc_node_soa* nodes) {
     if (!pk) return ESC_E_INVAL;
     if (!pk->finished) {
-        // Resolve taintTracker names (controller.go:128-133) to (node, group) entries.
-        std::unordered_map<std::string, std::vector<int64_t>> by_name;
-        bool any = false;
-        for (auto& t : pk->trackers) any |= !t.empty();
-        if (any) {
-            for (size_t i = 0; i < pk->node_names.size(); ++i) by_name[pk->node_names[i]].push_back((int64_t)i);
+        // Resolve taintTracker names (controller.go:128-133) to (node, group) entries: the
+        // (few) tracked names in a table, then one pass over the node names (a table of
+        // every node name cost ~0.5 s at 1 M nodes in the reload path)
+        std::unordered_map<std::string_view, std::vector<int32_t>> groups_of;
+        for (int32_t g = 0; g < (int32_t)pk->trackers.size(); ++g)
+            for (auto& nm : pk->trackers[g]) groups_of[std::string_view(nm)].push_back(g);
+        if (!groups_of.empty()) {
             std::vector<std::pair<int32_t, int32_t>> ent;
-            for (int32_t g = 0; g < (int32_t)pk->trackers.size(); ++g)
-                for (auto& nm : pk->trackers[g]) {
-                    auto it = by_name.find(nm);
-                    if (it == by_name.end()) continue;
-                    for (int64_t idx : it->second) ent.emplace_back((int32_t)idx, g);
-                }
+            for (size_t i = 0; i < pk->node_names.size(); ++i) {
+                auto it = groups_of.find(std::string_view(pk->node_names[i]));
+                if (it == groups_of.end()) continue;
+                for (int32_t g : it->second) ent.emplace_back((int32_t)i, g);
+            }
             std::sort(ent.begin(), ent.end());
             ent.erase(std::unique(ent.begin(), ent.end()), ent.end());
             for (auto& e : ent) {
