@@ -340,6 +340,7 @@ struct NodeDev {
     // K2 work: span w = this rank's group-pair pieces [span_off[w], span_off[w + 1]), about
     // NODE_SPAN entries each (several small pieces, or one large), one wave per span
     const uint32_t* span_off;  // [n_spans + 1]
+    const uint32_t* span_e;    // [n_spans + 1] the spans' entry bounds (piece_off[span_off[w]])
     int64_t n_pieces, pc_lo, pc_hi, n_spans;
     // the group pairs this rank owns: their pieces [pc_lo, pc_hi) are its K2
     // work, their groups' memberships its K5 age index; [0, n_gp) with one rank

@@ -739,36 +739,73 @@ namespace {
 // Adds one entry to the piece accumulators: its wet class (filterNodes,
 // controller.go:141-150: Spec.Unschedulable first, then the escalator taint) and the
 // every-member sums used by dry-mode groups.
+// A row's sums are exact as (LO, HI) with LO + HI * 2^32 = the int64 total (K2b joins them in
+// 128 bits).  An entry whose cpu and memory are both in [0, 2^54) adds its whole value to LO
+// (add_small: <= 1024 entries per piece keep LO below 2^64); otherwise its low 32 bits go to
+// LO and its high part, signed, to HI (add_split), and the piece's HI words are reduced
+// only when some wave-load of it took that path (`split`, wave-uniform) — allocatable
+// values are always small in practice, so a flush reduces 5 words instead of 9.
 struct PieceAcc {
     unsigned long long ucl = 0, uch = 0, uml = 0, umh = 0, acl = 0, ach = 0, aml = 0, amh = 0, cnt = 0;
-    __device__ __forceinline__ void add(uint32_t f, int64_t c, int64_t m) {
+    bool split = false;
+    __device__ __forceinline__ void count(uint32_t f, bool& unt) {
+        const int cls = (f & ESC_NF_UNSCHED) ? 2 : ((f & ESC_NF_TAINTED) ? 1 : 0);
+        unt = cls == 0;
+        cnt += 1ull << (NR_CNT_BITS * cls);
+    }
+    __device__ __forceinline__ void add_small(uint32_t f, int64_t c, int64_t m) {
         if (f & ESC_NF_ABSENT) return;               // spare entry or deleted node
+        bool unt;
+        count(f, unt);
+        acl += (uint64_t)c; aml += (uint64_t)m;
+        if (unt) { ucl += (uint64_t)c; uml += (uint64_t)m; }
+    }
+    __device__ __forceinline__ void add_split(uint32_t f, int64_t c, int64_t m) {
+        if (f & ESC_NF_ABSENT) return;
         const unsigned long long cl = (uint64_t)c & 0xFFFFFFFFull, ml = (uint64_t)m & 0xFFFFFFFFull;
         const unsigned long long chh = (unsigned long long)(c >> 32), mhh = (unsigned long long)(m >> 32);
+        bool unt;
+        count(f, unt);
         acl += cl; ach += chh; aml += ml; amh += mhh;
-        const int cls = (f & ESC_NF_UNSCHED) ? 2 : ((f & ESC_NF_TAINTED) ? 1 : 0);
-        if (cls == 0) { ucl += cl; uch += chh; uml += ml; umh += mhh; }
-        cnt += 1ull << (NR_CNT_BITS * cls);
+        if (unt) { ucl += cl; uch += chh; uml += ml; umh += mhh; }
     }
 };
 
-// K2 span w (one wave; see node_piece_block).
+// K2 span w (one wave; see node_piece_block).  The span's entry range comes from a scalar
+// array (span_e), so the first round of entry loads is issued with the piece-bounds load
+// instead of after it (one dependent round trip fewer).
 __device__ __forceinline__ void node_span(const NodeDev& N, int64_t* __restrict__ rows, int64_t w, int lane) {
     if (w >= N.n_spans) return;
     typedef __attribute__((address_space(4))) const uint32_t cu32n;
     const uint32_t p0 = ((const cu32n*)N.span_off)[w], p1 = ((const cu32n*)N.span_off)[w + 1];
+    const uint32_t e0 = ((const cu32n*)N.span_e)[w], z = ((const cu32n*)N.span_e)[w + 1];
     // the span's <= 64 piece bounds, one per lane (a span has <= 63 pieces), read with
     // readlane: no dependent load per piece
     const uint32_t np = p1 - p0;
     const uint32_t bound = N.piece_off[p0 + (lane < (int)np ? (uint32_t)lane : np)];
+    constexpr int U = 8;                             // a NODE_SPAN span's loads in one round
+    uint32_t f[U];
+    int64_t c[U], m[U];
+    auto load = [&](uint32_t base) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = base + u * 64 + lane, ii = i < z ? i : z - 1;
+            f[u] = ldnt(N.e_flags + ii);
+            c[u] = ldnt(N.e_cpu + ii);
+            m[u] = ldnt(N.e_mem + ii);
+        }
+    };
+    if (e0 < z) load(e0);
     auto off = [&](uint32_t k) -> uint32_t { return (uint32_t)__builtin_amdgcn_readlane((int)bound, (int)k); };
-    const uint32_t z = off(np);
-    uint32_t p = p0, ps = off(0), pe = off(1);
+    uint32_t p = p0, ps = e0, pe = off(1);
     PieceAcc acc;
     auto flush = [&]() {                             // piece p's row, then the next piece
-        const unsigned long long v[NR_K] = {wave_total64(acc.ucl), wave_total64(acc.uch), wave_total64(acc.uml),
-                                            wave_total64(acc.umh), wave_total64(acc.acl), wave_total64(acc.ach),
-                                            wave_total64(acc.aml), wave_total64(acc.amh), wave_total64(acc.cnt)};
+        const bool sp = acc.split;                   // wave-uniform: HI words only if used
+        const unsigned long long v[NR_K] = {wave_total64(acc.ucl), sp ? wave_total64(acc.uch) : 0ull,
+                                            wave_total64(acc.uml), sp ? wave_total64(acc.umh) : 0ull,
+                                            wave_total64(acc.acl), sp ? wave_total64(acc.ach) : 0ull,
+                                            wave_total64(acc.aml), sp ? wave_total64(acc.amh) : 0ull,
+                                            wave_total64(acc.cnt)};
         unsigned long long x = 0;
 #pragma unroll
         for (int k = 0; k < NR_K; ++k) x = lane == k ? v[k] : x;
@@ -778,23 +815,21 @@ __device__ __forceinline__ void node_span(const NodeDev& N, int64_t* __restrict_
         ps = pe;
         if (p < p1) pe = off(p + 1 - p0);
     };
-    constexpr int U = 8;                             // a NODE_SPAN span's loads in one round
-    for (uint32_t base = ps; base < z; base += 64 * U) {
-        uint32_t f[U];
-        int64_t c[U], m[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t i = base + u * 64 + lane, ii = i < z ? i : z - 1;
-            f[u] = ldnt(N.e_flags + ii);
-            c[u] = ldnt(N.e_cpu + ii);
-            m[u] = ldnt(N.e_mem + ii);
-        }
+    for (uint32_t base = e0; base < z; base += 64 * U) {
+        if (base != e0) load(base);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t lo = base + u * 64, i = lo + lane;
             if (lo >= z) break;
+            constexpr uint64_t SMALL = 1ull << 54;
+            const bool small = __ballot((uint64_t)c[u] >= SMALL || (uint64_t)m[u] >= SMALL) == 0;   // wave-uniform
             for (;;) {                                   // wave-uniform: p, ps, pe
-                if (i >= ps && i < pe && i < z) acc.add(f[u], c[u], m[u]);
+                if (small) {
+                    if (i >= ps && i < pe && i < z) acc.add_small(f[u], c[u], m[u]);
+                } else {
+                    acc.split = true;
+                    if (i >= ps && i < pe && i < z) acc.add_split(f[u], c[u], m[u]);
+                }
                 if (p >= p1 || pe > lo + 63) break;      // piece p goes on in the next load
                 flush();
             }
@@ -1620,6 +1655,18 @@ __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, i
     const int64_t s0 = (int64_t)col * FC_COL;
     const uint32_t ga = F.col_off[col], gb = F.col_off[col + 1];
     const uint32_t me = threadIdx.x;
+    // loads that do not depend on the fold, issued before it so their latency overlaps the
+    // fold's: the slots' wide rows (threads < FC_COL) and the first round of the column's
+    // groups with their pod slots
+    int64_t p[WP_K] = {0, 0, 0, 0, 0};
+    const bool has_wide = me < FC_COL && s0 + me <= (int64_t)G.n_gp;
+    int64_t* wp = wide_pod + (s0 + me) * WP_K;
+    if (has_wide)
+#pragma unroll
+        for (int k = 0; k < WP_K; ++k) p[k] = ld_agent(wp + k);
+    const bool g_ok0 = ga + me < gb;
+    const int32_t g_0 = g_ok0 ? (int32_t)F.col_groups[ga + me] : 0;
+    const uint32_t sl_0 = g_ok0 ? G.gslot[g_0] : 0;
     // ---- fold: every K1 row of the column; wave w's load u covers rows
     //      (w + FD_WAVES * u) * FD_RPL + sub
     uint64_t cp[2] = {0, 0}, cn[2] = {0, 0}, ml[2] = {0, 0}, mc[2] = {0, 0};
@@ -1660,17 +1707,11 @@ __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, i
     }
     red[wid][0][lane] = cp[0]; red[wid][1][lane] = cp[1]; red[wid][2][lane] = cn[0]; red[wid][3][lane] = cn[1];
     red[wid][4][lane] = ml[0]; red[wid][5][lane] = ml[1]; red[wid][6][lane] = mc[0]; red[wid][7][lane] = mc[1];
-    // the slots' wide rows (threads < FC_COL), read and reset (every reader is in this block)
-    int64_t p[WP_K] = {0, 0, 0, 0, 0};
-    if (me < FC_COL && s0 + me <= (int64_t)G.n_gp) {
-        int64_t* wp = wide_pod + (s0 + me) * WP_K;
+    // the slots' wide rows (loaded above) are reset (every reader is in this block)
+    if (has_wide && (p[0] | p[1] | p[2] | p[3] | p[4]) != 0)
 #pragma unroll
-        for (int k = 0; k < WP_K; ++k) p[k] = ld_agent(wp + k);
-        if ((p[0] | p[1] | p[2] | p[3] | p[4]) != 0)
-#pragma unroll
-            for (int k = 0; k < WP_K; ++k)
-                __hip_atomic_store(wp + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+        for (int k = 0; k < WP_K; ++k)
+            __hip_atomic_store(wp + k, (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (wid < 2 && lane < FD_HL) {                       // wave 0: slots 2l, 2l+1 words 0/1; wave 1: mem words
         const int j = lane;
@@ -1698,9 +1739,10 @@ __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, i
     // ---- the column's groups' pod words, one thread each (a column holds ~FC_COL groups)
     for (uint32_t base = ga; base < gb; base += FD_WAVES * 64) {
         const bool ok = base + me < gb;
-        const int32_t g = ok ? (int32_t)F.col_groups[base + me] : 0;
+        const bool first = base == ga;
+        const int32_t g = first ? g_0 : (ok ? (int32_t)F.col_groups[base + me] : 0);
         if (ok) {
-            const int sl = (int)((int64_t)G.gslot[g] - s0);
+            const int sl = (int)((int64_t)(first ? sl_0 : G.gslot[g]) - s0);
             int64_t* pw = pwords + (int64_t)g * PW_K;
             const __int128 pcpu = (__int128)tot[0][sl] + ((__int128)wtot[WP_CPU_HI][sl] << 32) + (__int128)wtot[WP_CPU_LO][sl];
             const __int128 pmem = (__int128)(((unsigned __int128)tot[3][sl] << 64) | tot[2][sl]) +

@@ -75,13 +75,14 @@ struct NodeBuf {
     // pair-major entries, pieces, tracker by group, K2 rows
     uint32_t *e_flags = nullptr, *e_node = nullptr, *piece_off = nullptr, *piece_pair = nullptr, *pp_off = nullptr;
     uint32_t* span_off = nullptr;                // K2 waves' piece ranges
+    uint32_t* span_e = nullptr;                  // and their entry ranges
     int64_t *e_cpu = nullptr, *e_mem = nullptr, *rows = nullptr;
     GroupNode* gnode = nullptr;
     void release() {
         dfree(gnode);
         dfree(flags); dfree(label0); dfree(xl); dfree(xl_off); dfree(trk_start); dfree(cpu); dfree(mem);
         dfree(created); dfree(trk_node); dfree(trk_group);
-        dfree(e_flags); dfree(e_node); dfree(piece_off); dfree(piece_pair); dfree(pp_off); dfree(span_off);
+        dfree(e_flags); dfree(e_node); dfree(piece_off); dfree(piece_pair); dfree(pp_off); dfree(span_off); dfree(span_e);
         dfree(e_cpu); dfree(e_mem); dfree(rows);
     }
 };
@@ -432,7 +433,7 @@ NodeDev node_dev(const esc_ctx* c) {
     n.e_flags = c->nodes.e_flags; n.e_cpu = c->nodes.e_cpu; n.e_mem = c->nodes.e_mem; n.e_node = c->nodes.e_node;
     n.piece_off = c->nodes.piece_off; n.piece_pair = c->nodes.piece_pair; n.pp_off = c->nodes.pp_off;
     n.n_pieces = c->n_pieces; n.pc_lo = c->pc_lo; n.pc_hi = c->pc_hi;
-    n.span_off = c->nodes.span_off; n.n_spans = c->n_spans;
+    n.span_off = c->nodes.span_off; n.span_e = c->nodes.span_e; n.n_spans = c->n_spans;
     n.q_lo = c->q_lo; n.q_hi = c->q_hi;
     return n;
 }
@@ -1819,6 +1820,12 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     HIP_TRY(hipMemcpy(b.pp_off, pp_off.data(), pp_off.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(dalloc(&b.span_off, span_off.size()));
     HIP_TRY(hipMemcpy(b.span_off, span_off.data(), span_off.size() * 4, hipMemcpyHostToDevice));
+    {
+        std::vector<uint32_t> span_e(span_off.size());
+        for (size_t w = 0; w < span_off.size(); ++w) span_e[w] = piece_off[span_off[w]];
+        HIP_TRY(dalloc(&b.span_e, span_e.size()));
+        HIP_TRY(hipMemcpy(b.span_e, span_e.data(), span_e.size() * 4, hipMemcpyHostToDevice));
+    }
     HIP_TRY(dalloc(&b.rows, (size_t)std::max<int64_t>(n_pieces, 1) * NR_K));
     {   // per-group facts fixed by this snapshot: this rank's pieces of the group's pair and
         // allNodes[0] (controller.go:207-211) = the pair's first entry (lowest node index)

@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round 4: K2 spans with scalar entry bounds + the small-value path, fold prefetch —
+# parity (new value-range test first, then the suite), shard-of-8 and full steps, and the
+# K2-alone / fold-alone tail ablations at config 4.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${TAG:-r04o}
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+export TMPDIR=/tmp
+echo "[job] $(date) pytest"
+timeout -k 10 300 python -u -m pytest tests/test_gpu.py -m gpu -k "value_ranges or node_index_split or big_tiles" -x -v \
+    --timeout 200 --timeout-method thread > $OUT/pytest_new.log 2>&1 || { tail -60 $OUT/pytest_new.log; exit 1; }
+tail -1 $OUT/pytest_new.log
+timeout -k 10 1000 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeout-method thread \
+    > $OUT/pytest_gpu.log 2>&1 || { tail -60 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+show() { python3 -c "import json; d=json.load(open('$1')); print('$2', round(d['ms_per_step']*1e3,1), round(d['roofline']['launch_ms']*1e3,2), {k: round(v*1e3,1) for k, v in d['stage_ms'].items()}, d.get('parity'))"; }
+timeout -k 10 240 python3 bench.py --shard-of 8 --steps 200 --warmup 20 --no-cpu-baseline --no-host > $OUT/shard8.json 2> $OUT/shard8.err || { tail $OUT/shard8.err; exit 1; }
+show $OUT/shard8.json shard8
+timeout -k 10 240 python3 bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-host > $OUT/full.json 2> $OUT/full.err || { tail $OUT/full.err; exit 1; }
+show $OUT/full.json full
+for A in 0 16 40 48 56; do
+  ESC_K3_ABLATE=$A timeout -k 10 240 python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-host --no-parity \
+      > $OUT/tailabl_a$A.json 2> $OUT/tailabl.err || { tail $OUT/tailabl.err; exit 1; }
+  show $OUT/tailabl_a$A.json "ablate $A"
+done
+echo "[job] $(date) done"

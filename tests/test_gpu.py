@@ -729,6 +729,44 @@ def test_big_tiles_and_window_edges(esc):
         assert (tot["pod_cpu_m"][g], tot["pod_mem_b"][g], tot["n_pods"][g]) == (L["pod_cpu_m"], L["pod_mem_b"], L["n_pods"])
 
 
+def test_node_sums_value_ranges(esc):
+    """K2's two accumulation paths: allocatable in [0, 2^54) summed whole (one word per
+    sum), anything else (negative, >= 2^54) split in lo32 / hi parts — in the same piece and
+    the same wave-load as small ones, up to 2^54 - 1 x 1 024 members (the small path's
+    bound), and past int64 (the node-overflow flag) — against the C oracle and the literal
+    one's totals."""
+    rng = random.Random(54)
+    groups = [{"name": "g%d" % i, "label_key": "k", "label_value": "v%d" % i, "max_nodes": 100000}
+              for i in range(7)]
+    nodes, j = [], 0
+
+    def add(g, cpu, mem, n):
+        nonlocal j
+        for _ in range(n):
+            nodes.append({"name": "n%d" % j, "labels": {"k": "v%d" % g}, "cpu": cpu() if callable(cpu) else cpu,
+                          "mem": mem() if callable(mem) else mem, "created_ns": j,
+                          "unschedulable": rng.random() < 0.1})
+            j += 1
+
+    add(0, (1 << 54) - 1, (1 << 54) - 1, 1024)                  # the small path at its bound: LO near 2^64, int64 overflow
+    add(6, 1 << 53, (1 << 53) - 1, 1023)                        # large, whole, still inside int64
+    add(1, lambda: rng.choice([5, 1 << 54, -3]), lambda: rng.choice([7, 1 << 60, -(1 << 40)]), 700)  # mixed
+    add(2, 1 << 62, 1 << 62, 5)                                 # past int64: flagged
+    add(3, lambda: rng.randrange(0, 1 << 20), lambda: rng.randrange(0, 1 << 40), 2000)   # typical
+    add(4, -1, -(1 << 63), 3)                                   # negative extremes
+    add(5, lambda: rng.randrange(-(1 << 63), 1 << 63), lambda: rng.randrange(-(1 << 63), 1 << 63), 300)
+    ctx = esc.Context(groups)
+    P, N = ctx.pack([], nodes)
+    ctx.load(P, N)
+    tot, dec = ctx.decide_all()
+    otot = soa.totals(P, N, groups)
+    odf, odi = soa.decide(groups, None, otot)
+    check_against_c_oracle(tot, dec, otot, odf, odi)
+    assert tot["flags"][0] != 0 and tot["flags"][2] != 0 and tot["flags"][3] == 0 and tot["flags"][6] == 0
+    unt6 = [x for x in nodes if x["labels"]["k"] == "v6" and not x["unschedulable"]]
+    assert (tot["node_cpu_m"][6], tot["node_mem_b"][6]) == (sum(x["cpu"] for x in unt6), sum(x["mem"] for x in unt6))
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 5])
 def test_node_index_split_within_pairs(esc, world):
     """Pairs with many pieces (10k members each), a dry group with tracked members, the
