@@ -357,7 +357,7 @@ enum NodeRow : int {
     NR_K
 };
 constexpr int NODE_PIECE = 1024;
-constexpr int NODE_SPAN = 512;         // entries per K2 wave (whole pieces, <= 63 of them)
+constexpr int NODE_SPAN = 256;         // entries per K2 wave (whole pieces, <= 63 of them)
 constexpr int NR_CNT_BITS = 21;
 constexpr uint64_t NR_CNT_MASK = (uint64_t(1) << NR_CNT_BITS) - 1;
 

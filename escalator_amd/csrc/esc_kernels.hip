@@ -783,7 +783,7 @@ __device__ __forceinline__ void node_span(const NodeDev& N, int64_t* __restrict_
     // readlane: no dependent load per piece
     const uint32_t np = p1 - p0;
     const uint32_t bound = N.piece_off[p0 + (lane < (int)np ? (uint32_t)lane : np)];
-    constexpr int U = 8;                             // a NODE_SPAN span's loads in one round
+    constexpr int U = NODE_SPAN / 64;                // a NODE_SPAN span's loads in one round
     uint32_t f[U];
     int64_t c[U], m[U];
     auto load = [&](uint32_t base) {
@@ -1636,7 +1636,7 @@ __global__ __launch_bounds__(KD_BLOCK) void k_decide(GroupDev G, NodeDev N, cons
 //  - allNodes[0] (controller.go:208): the pair's first entry (GroupNode, set at load).
 namespace {
 constexpr int FD_WAVES = 4;
-constexpr int FD_U = 16;                 // wave-loads per wave in flight (each array)
+constexpr int FD_U = 4;                  // wave-loads per wave in flight (each array)
 constexpr int FD_HL = FC_COL / 2;        // lanes per row (2 slots per 16-B lane load)
 constexpr int FD_RPL = 64 / FD_HL;       // K1 rows per wave-load
 static_assert(FD_RPL * FD_HL == 64 && FD_WAVES >= 2, "fold lane map");
