@@ -896,9 +896,9 @@ __device__ __forceinline__ bool join_split(int64_t lo_sum, int64_t hi_sum, int64
     return t >= (__int128)INT64_MIN && t <= (__int128)INT64_MAX;
 }
 
-__device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn, int32_t g,
-                                         const int64_t* __restrict__ pw, const int64_t* __restrict__ nw,
-                                         esc_group_decision& dec, esc_group_metrics* __restrict__ met) {
+__device__ __forceinline__ void finalize_p(const GroupParams& prm, const GroupNode& gn, int32_t g,
+                                           const int64_t* __restrict__ pw, const int64_t* __restrict__ nw,
+                                           esc_group_decision& dec, esc_group_metrics* __restrict__ met) {
     Totals t;
     int64_t flags = nw[NW_FLAGS];
     if (!join_split(pw[PW_CPU_LO], pw[PW_CPU_HI], t.pod_cpu)) flags |= ESC_TF_POD_OVERFLOW;
@@ -914,12 +914,18 @@ __device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn,
     t.first_cpu = gn.first_cpu;
     t.first_mem = gn.first_mem;
     t.flags = flags;
-    decide_one(G.params[g], t, dec);
+    decide_one(prm, t, dec);
     if (met) {
         esc_group_metrics m;
         metrics_one(t, dec, m);
         met[g] = m;
     }
+}
+
+__device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn, int32_t g,
+                                         const int64_t* __restrict__ pw, const int64_t* __restrict__ nw,
+                                         esc_group_decision& dec, esc_group_metrics* __restrict__ met) {
+    finalize_p(G.params[g], gn, g, pw, nw, dec, met);
 }
 
 __device__ __forceinline__ DecCompact compact_of(const esc_group_decision& d) {
@@ -1483,7 +1489,19 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
 #pragma unroll
     for (int k = 0; k < NA; ++k) a[k] = 0;
     int64_t plo = 0, phi = 0;
-    if (ok) { plo = N.gnode[g].plo; phi = N.gnode[g].phi; }
+    GroupNode gn{};
+    GroupParams prm{};
+    int64_t pwv[PW_K] = {};
+    if (ok) {
+        gn = N.gnode[g];
+        plo = gn.plo;
+        phi = gn.phi;
+        if (D.dec && wid == 0) {                     // K4's inputs (wave 0 decides), loaded beside the piece rows
+            prm = G.params[g];
+#pragma unroll
+            for (int k = 0; k < PW_K; ++k) pwv[k] = D.pwords[(int64_t)g * PW_K + k];
+        }
+    }
     const int64_t np = N.n_pieces;
 #pragma unroll 2
     for (int64_t pc = plo + wid; pc < phi; pc += NG_WAVES) {
@@ -1559,7 +1577,7 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
     }
     if (D.dec) {
         esc_group_decision d;
-        finalize(G, N.gnode[g], g, D.pwords + (int64_t)g * PW_K, v, d, G.metrics);
+        finalize_p(prm, gn, g, pwv, v, d, G.metrics);
         store_full(D.dec + g, d);
         sdec[lane] = compact_of(d);
         sid[lane] = (uint32_t)g;
