@@ -215,6 +215,7 @@ struct esc_ctx {
     // timing
     bool timing = false;
     hipEvent_t ev[MAX_STAGES] = {};
+    hipEvent_t k1t_ev[2] = {};                                // esc_k1_time's own pair (stage events stay readable)
     double stage_ms[MAX_STAGES] = {};
     int n_stage_ev = 0;
     bool pending = false;
@@ -1222,6 +1223,8 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     c->own_stream = true;
     for (int i = 0; i < MAX_STAGES; ++i)
         if (hipEventCreate(&c->ev[i]) != hipSuccess) return fail(ESC_E_HIP);
+    for (int i = 0; i < 2; ++i)
+        if (hipEventCreate(&c->k1t_ev[i]) != hipSuccess) return fail(ESC_E_HIP);
 
     if (const char* v = std::getenv("ESC_NO_ZEROCOPY")) c->zero_copy = std::atoi(v) == 0;
     const size_t G = (size_t)n_groups;
@@ -1281,6 +1284,8 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         dfree(c->d_col_off); dfree(c->d_col_groups);
         for (int i = 0; i < MAX_STAGES; ++i)
             if (c->ev[i]) hipEventDestroy(c->ev[i]);
+        for (int i = 0; i < 2; ++i)
+            if (c->k1t_ev[i]) hipEventDestroy(c->k1t_ev[i]);
         if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     }
     delete c;
@@ -2092,19 +2097,19 @@ int32_t esc_k1_time(esc_ctx* c, int32_t reps, double* ms_per_launch) {
     const GroupDev g = group_dev(c);
     const int32_t S = (int32_t)pod_slots(c);
     HIP_TRY(hipStreamSynchronize(st));
-    HIP_TRY(hipEventRecord(c->ev[0], st));
+    HIP_TRY(hipEventRecord(c->k1t_ev[0], st));
     for (int32_t k = 0; k < reps; ++k)
         for (int32_t g0 = 0; g0 < S; g0 += POD_WINDOW_MAX) {
             const K1Diag diag{c->d_k1_trace};
             HIP_TRY(launch_pod_reduce(p, g, g0, std::min(POD_WINDOW_MAX, S - g0), c->nblk, c->k1_variant, c->d_pod_part,
                                       c->d_wide_pod, c->d_k1_ticket, c->k1_cap, diag, st));
         }
-    HIP_TRY(hipEventRecord(c->ev[1], st));
+    HIP_TRY(hipEventRecord(c->k1t_ev[1], st));
     // the exact-path accumulators K1 added to without a fold: back to zero for the next step
     HIP_TRY(hipMemsetAsync(c->d_wide_pod, 0, (size_t)pod_slots(c) * WP_K * sizeof(int64_t), st));
     HIP_TRY(hipStreamSynchronize(st));
     float ms = 0.f;
-    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    HIP_TRY(hipEventElapsedTime(&ms, c->k1t_ev[0], c->k1t_ev[1]));
     *ms_per_launch = (double)ms / reps;
     return ESC_OK;
 }
