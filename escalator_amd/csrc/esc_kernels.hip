@@ -2530,8 +2530,10 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdCh
 
 
 // The step's tail in ONE launch (horizontal fusion; every role is 256 threads): the K2
-// node-piece blocks, the dry-mode tracker blocks, the K5 packed small-group orderings and
-// the K3 fold columns, in that block order.  (Before, K2 and K5
+// node-piece blocks, the dry-mode tracker blocks, the K3 fold columns and the K5 packed
+// small-group orderings, in that block order — the longest chains first (at config 4
+// the grid is ~2.5 k blocks for ~1.3 k resident slots, and the short ordering blocks fill
+// the second round).  (Before, K2 and K5
 // ran on a side stream beside K1: K1 holds every CU's LDS and its loads starve K2's
 // latency-bound waves, so the side chain ended after K1 and the cross-stream join cost
 // ~10 us more (profiles/r02_v9 timeline): ~45 us after K1 at any pod count.)
@@ -2550,13 +2552,12 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
         const int64_t pb = b;
         if (!(F.ablate & 16) && !((F.ablate & 64) && pb >= nb_pieces))
             node_piece_block(N, G, nb_pieces, (F.ablate & 128) ? nullptr : rows, trk_acc, pb);
-    } else if (b < n_piece_blk + n_small) {
-        if (!(F.ablate & 32))
-            ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, g_memb, g_grp, vals, seg,
-                                                           b - n_piece_blk);
-    } else {
-        const uint32_t col = (uint32_t)(b - n_piece_blk - n_small);
+    } else if (b < n_piece_blk + F.n_col) {
+        const uint32_t col = (uint32_t)(b - n_piece_blk);
         if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)col);
+    } else if (!(F.ablate & 32)) {
+        ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, g_memb, g_grp, vals, seg,
+                                                       b - n_piece_blk - F.n_col);
     }
 }
 
