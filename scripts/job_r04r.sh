@@ -3,7 +3,7 @@
 # entries) — parity suite, then the steps and the role ablations at config 4.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-TAG=${TAG:-r04v}
+TAG=${TAG:-r04w}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
