@@ -1920,6 +1920,9 @@ __device__ __forceinline__ void region_put(const RegionSink& S, uint32_t p, uint
 #ifndef ESC_RS_U
 #define ESC_RS_U 2         // keys per thread per scatter chunk (timing builds may override)
 #endif
+#ifndef ESC_RS_CARRY
+#define ESC_RS_CARRY 0     // whole-line digit runs (below): off until measured on the GPU
+#endif
 constexpr int RS_U = ESC_RS_U;
 template <class KT, class VT, int BITS, bool FINAL>
 __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict__ kin, const VT* __restrict__ vin,
@@ -1934,8 +1937,21 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
     __shared__ uint32_t ws[SORT_WAVES];
     __shared__ KT sk[CH];
     __shared__ VT sv[CH];
+    // Whole lines per digit run (non-FINAL passes): a chunk writes each digit's keys only up
+    // to the last 16-key boundary of its run (16 keys = one 128-B line of 8-B keys, half a
+    // line of 4-B values) and carries the rest in LDS to the front of that digit's run in
+    // the next chunk, where it continues; the block's last chunk flushes everything.  A
+    // chunk's per-digit runs average ~16 keys, so writing each run whole left partial lines
+    // at both ends (1.4x the bytes written).  (32-key alignment would double
+    // the carry's LDS and halve the blocks per CU.)
+    constexpr bool CARRY = !FINAL && ESC_RS_CARRY;
+    constexpr int CW = 16, CD = CARRY ? NB : 1;
+    __shared__ KT ck[CD][CW];
+    __shared__ VT cv[CD][CW];
+    __shared__ uint32_t c_n[CD], c_s[CD], c_e[CD];        // carry count, carry start, write end
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, t = threadIdx.x;
     if (t < NB) run[t] = tot[t] + hist[(int64_t)t * gridDim.x + blockIdx.x];
+    if (CARRY && t < NB) c_n[t] = 0;
     for (int e = t; e < S * NB; e += SORT_BLOCK) (&wh[0][0])[e] = 0;
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
@@ -1983,6 +1999,10 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
             uint32_t p = x - dtot;
             for (int k = 0; k < wid; ++k) p += ws[k];
             lst[t] = p;
+            if constexpr (CARRY) {                      // this chunk writes [begin, E) of digit t
+                const uint32_t begin = c_n[t] ? c_s[t] : run[t], endp = run[t] + dtot;
+                c_e[t] = b + CH >= hi ? endp : imax64((int64_t)begin, (int64_t)(endp & ~(uint32_t)(CW - 1)));
+            }
         }
         __syncthreads();
 #pragma unroll
@@ -1992,7 +2012,41 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
                 sk[s] = key[u];
                 sv[s] = val[u];
             }
+        // the previous carry: written when below this chunk's write end, else kept (it moves
+        // to the front of the new carry, after every thread has read the old one)
+        constexpr int CN = CARRY ? (CD * CW + SORT_BLOCK - 1) / SORT_BLOCK : 1;
+        KT okk[CN];
+        VT ovv[CN];
+        uint32_t opos[CN], odig[CN];
+        bool keep[CN];
+        if constexpr (CARRY) {
+#pragma unroll
+            for (int q = 0; q < CN; ++q) {
+                const int idx = t + q * SORT_BLOCK, dg = idx / CW, j = idx % CW;
+                keep[q] = false;
+                if (dg < CD && j < (int)c_n[dg]) {
+                    okk[q] = ck[dg][j];
+                    ovv[q] = cv[dg][j];
+                    opos[q] = c_s[dg] + (uint32_t)j;
+                    odig[q] = (uint32_t)dg;
+                    if (opos[q] < c_e[dg]) {
+                        kout[opos[q]] = okk[q];
+                        vout[opos[q]] = ovv[q];
+                    } else {
+                        keep[q] = true;
+                    }
+                }
+            }
+        }
         __syncthreads();
+        if constexpr (CARRY) {
+#pragma unroll
+            for (int q = 0; q < CN; ++q)
+                if (keep[q]) {
+                    ck[odig[q]][opos[q] - c_e[odig[q]]] = okk[q];
+                    cv[odig[q]][opos[q] - c_e[odig[q]]] = ovv[q];
+                }
+        }
         // the next chunk's keys in flight during the write-out
 #pragma unroll
         for (int u = 0; u < RS_U; ++u) {
@@ -2006,12 +2060,21 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
             const uint32_t dd = (uint32_t)(kk >> shift) & (NB - 1);
             const uint32_t g = run[dd] + (uint32_t)e - lst[dd];
             if constexpr (FINAL) region_put(sink, g, kk, sv[e]);
-            else {
+            else if (!CARRY || g < c_e[dd]) {
                 kout[g] = kk;
                 vout[g] = sv[e];
+            } else {                                     // the run's partial last line: carried
+                ck[dd][g - c_e[dd]] = kk;
+                cv[dd][g - c_e[dd]] = sv[e];
             }
         }
         for (int e = t; e < S * NB; e += SORT_BLOCK) (&wh[0][0])[e] = 0;
+        if constexpr (CARRY) {
+            if (t < NB) {                                // the new carry: [E, run + count)
+                c_n[t] = run[t] + dtot - c_e[t];
+                c_s[t] = c_e[t];
+            }
+        }
         __syncthreads();
     }
 }
