@@ -1921,7 +1921,7 @@ __device__ __forceinline__ void region_put(const RegionSink& S, uint32_t p, uint
 #define ESC_RS_U 2         // keys per thread per scatter chunk (timing builds may override)
 #endif
 #ifndef ESC_RS_CARRY
-#define ESC_RS_CARRY 0     // whole-line digit runs (below): off until measured on the GPU
+#define ESC_RS_CARRY 1     // whole-line digit runs (below); 0 = the plain scatter, for timing builds
 #endif
 constexpr int RS_U = ESC_RS_U;
 template <class KT, class VT, int BITS, bool FINAL>
