@@ -1,14 +1,14 @@
 #!/bin/bash
 # Round 4: age-index scatter with whole-line digit runs (a build with -DESC_RS_CARRY=1 in
-# escalator_amd/exp/) against the default: K5 parity, config-5 index build, scatter writes.
+# escalator_amd/exp/; LIBS names other builds there) against the default: K5 parity, config-5 index build, scatter writes.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${TAG:-r04x}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-for L in default carry; do
-  if [ $L = carry ]; then export ESC_LIB_PATH=$PWD/escalator_amd/exp/libescalator_carry.so; else unset ESC_LIB_PATH; fi
+for L in ${LIBS:-default carry}; do
+  if [ $L != default ]; then export ESC_LIB_PATH=$PWD/escalator_amd/exp/libescalator_$L.so; else unset ESC_LIB_PATH; fi
   timeout -k 10 300 python -u -m pytest tests/test_gpu.py tests/test_gpu_multi.py -m gpu -k "sort or order or age or synthetic or node_index or relabel or nodes_add" \
       -x -v --timeout 200 --timeout-method thread > $OUT/pytest_k5_$L.log 2>&1 || { tail -60 $OUT/pytest_k5_$L.log; exit 1; }
   echo "$L: $(tail -1 $OUT/pytest_k5_$L.log)"
