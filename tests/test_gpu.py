@@ -350,6 +350,22 @@ def test_synthetic_sort_vs_c_oracle(esc, fused, monkeypatch):
     assert ctx.group_order(g, 1).tolist() == sorted((j for j in members if j in trk), key=lambda j: (-int(t[j]), j))
 
 
+@pytest.mark.parametrize("N", [1, 15, 17, 2_047, 2_049, 8_191, 8_193, 40_000, 1_100_000])
+def test_age_index_sizes_vs_c_oracle(esc, N):
+    """The age index's LSD scatter at memberships around its line (16 keys), chunk (2048)
+    and block (8192) sizes and at several chunks per block: each chunk writes whole lines of
+    a digit's run and carries the partial last line to the next (esc_kernels.hip
+    k_rs_scatter, ESC_RS_CARRY); every group's orderings against the C oracle."""
+    s = esc.Synth(max(1, N // 4), N, 7, config=5, seed=0xE5CA1A7E00000100 + N)
+    nodes = s.nodes()
+    ctx = esc.Context(s)
+    ctx.load_synth(s)
+    ctx.sort_nodes()
+    for g in range(len(s.groups)):
+        for which in (0, 1):
+            assert np.array_equal(ctx.group_order(g, which), soa.order(nodes, s.groups, g, which)), (N, g, which)
+
+
 @pytest.mark.parametrize("graph,N", [(False, 200_000), (True, 200_000), (True, 30_000), (True, 700_000)])
 def test_order_in_step_vs_c_oracle(esc, graph, N):
     """esc_set_order_in_step: the K5 ordering inside every decision (side stream beside K1,
