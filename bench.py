@@ -165,6 +165,82 @@ def cpu_baseline(cfg, G, full=None, seconds=12.0):
     return out
 
 
+PARITY_EXIT = 3                 # exit status of a run whose results differ from the oracle's
+
+
+def report(out: dict, parity_ok: bool) -> int:
+    """Print the bench line; a parity mismatch still prints it (the numbers are evidence)
+    but makes the run fail: a wrong decision must never pass as a measurement."""
+    print(json.dumps(out), flush=True)
+    if not parity_ok:
+        log("bench: PARITY MISMATCH against the C oracle: %s" % out.get("parity"))
+        return PARITY_EXIT
+    return 0
+
+
+def stage_layout(world: int, shard_world: int, multi, backend: str) -> list[str]:
+    """Names of the timing-mode stages enqueue_step / esc_exchange / esc_decide record."""
+    names = ["k_pod_reduce", "k_step_tail", "k_order_split", "k_node_groups"]
+    if os.environ.get("ESC_NO_ZEROCOPY", "0") not in ("", "0"):
+        names.append("d2h")
+    if multi or (world == 1 and shard_world == 1):
+        return names                              # K4 inside k_node_groups (device 0's events)
+    if world > 1:
+        names.append("exchange" if backend == "nccl" else "exchange_host_staged")
+    return names + ["k_decide"]
+
+
+def check_parity(args, ctx, s, multi, rank, world, backend, dist, P, N, G, n_gpus):
+    """Every group's totals and decision against the C oracle over the whole snapshot (at
+    N > 1 the owners' records gathered to every rank, and a second, unsharded generation of
+    the config on rank 0), and every group's two orderings on the rank that orders it, against
+    the oracle's over the node table every rank holds.  Returns (text, ok) on every rank."""
+    import numpy as np
+    import torch
+    from oracle import soa
+    if multi or world == 1:
+        tot, dec = ctx.results()
+    else:
+        from escalator_amd.dist import gather_results
+        tot, dec = gather_results(ctx)              # collective: every rank
+    ord_ok, n_ord = True, 0
+    if not args.no_order:
+        want = soa.order_all(s.nodes(), s.groups)
+        for g in range(G):
+            if multi or world == 1 or ctx.group_owner(g) == rank:
+                n_ord += 1
+                for w in (0, 1):
+                    ord_ok &= bool(np.array_equal(ctx.group_order(g, w), want[(g, w)]))
+    tot_ok = True
+    if rank == 0:
+        from escalator_amd import Synth
+        full = s if world == 1 else Synth(P, N, G, config=args.config, seed=0xE5CA1A7E00000000 + args.config,
+                                          threads=16)
+        otot = soa.totals(full.pods(), full.nodes(), full.groups, threads=16)
+        odf, odi = soa.decide(full.groups, full.states, otot)
+        tot_ok = all(np.array_equal(tot[n], otot[:, k]) for k, n in enumerate(soa.TOT_FIELDS[:12]))
+        tot_ok &= np.array_equal(dec["cpu_pct"].view(np.uint64), odf[:, 0].view(np.uint64))
+        tot_ok &= np.array_equal(dec["mem_pct"].view(np.uint64), odf[:, 1].view(np.uint64))
+        for k, n in enumerate(["delta", "n_to_taint", "cached_cpu_m", "cached_mem_b", "status", "branch",
+                               "taint_status"]):
+            tot_ok &= np.array_equal(dec[n].astype(np.int64), odi[:, k])
+    if dist is not None:                            # the verdict of every rank's checks
+        v = torch.tensor([int(ord_ok and tot_ok), n_ord], dtype=torch.int64,
+                         device="cuda" if backend == "nccl" else "cpu")
+        ok_t = v[:1].clone()
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        dist.all_reduce(v[1:], op=dist.ReduceOp.SUM)
+        ok, n_ord = bool(ok_t.item()), int(v[1].item())
+    else:
+        ok = bool(ord_ok and tot_ok)
+    text = ("bit-exact vs C oracle: all %d groups' totals and decisions%s%s" % (
+            G, "" if args.no_order else ", all %d groups' two orderings" % n_ord,
+            "" if n_gpus == 1 else " (the owners' records over %d ranks gathered; oracle over the unsharded "
+                                   "snapshot)" % n_gpus)
+            if ok else "MISMATCH vs C oracle")
+    return text, ok
+
+
 def _free_port() -> int:
     import socket
     s = socket.socket()
@@ -271,17 +347,40 @@ def bench_order(args):
             el = float(e.item())
         return el / k * 1e3
 
-    order_ms = timed(ctx.sort_nodes, args.steps)
+    def cold(fn, k):
+        """Per-decision device time with the Infinity Cache flushed before each one: the
+        ordering's working set (~130 MB of region words and orders) fits the 256 MB MALL, so
+        back-to-back decisions would be MALL-served.  A 1 GiB write on the context's stream
+        evicts it, then HIP events bracket the ordering kernels alone; mean over k."""
+        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        scrub = torch.empty(1 << 28, dtype=torch.int32, device="cuda")
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k)]
+        for a, b in ev:
+            scrub.fill_(1)
+            a.record()
+            fn()
+            b.record()
+        torch.cuda.synchronize()
+        ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        del scrub
+        ctx.set_stream(None)
+        if dist is not None:                      # max over ranks
+            e = torch.tensor([ms], dtype=torch.float64, device="cuda" if backend == "nccl" else "cpu")
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            ms = float(e.item())
+        return ms
+
+    warm_ms = timed(ctx.sort_nodes, args.steps)
+    order_ms = cold(ctx.sort_nodes, args.steps)
     index_ms = timed(ctx.build_age_index, max(3, args.steps // 4))
     ctx.sort_nodes()
     n_memb, R = ctx.order_info()
     nodes = s.nodes()
-    check = (0, 37, 99)
     if world == 1:
+        want = soa.order_all(nodes, s.groups)
         counts = [len(ctx.group_order(g, w)) for g in range(G) for w in (0, 1)]
-        parity = all(np.array_equal(ctx.group_order(g, w), soa.order(nodes, s.groups, g, w)) for g in check
-                     for w in (0, 1))
-        how = "bit-exact vs C oracle on groups 0, 37, 99 (both orders)"
+        parity = all(np.array_equal(ctx.group_order(g, w), want[(g, w)]) for g in range(G) for w in (0, 1))
+        how = "bit-exact vs C oracle: all %d groups, both orders" % G
         sel_ms = None
     else:
         dev = torch.device("cuda", local) if backend == "nccl" else None
@@ -293,23 +392,21 @@ def bench_order(args):
         merged = {w: gather_orders(ctx, w, n_sel, nodes["created_ns"], device=dev) for w in (0, 1)}
         sel_ms = (time.perf_counter() - t0) * 1e3
         counts = [len(merged[w][g]) for g in range(G) for w in (0, 1)]
-        parity = all(np.array_equal(merged[w][g], soa.order(nodes, s.groups, g, w, cap=n_sel)) for g in check
+        parity = all(np.array_equal(merged[w][g], soa.order(nodes, s.groups, g, w, cap=n_sel)) for g in range(G)
                      for w in (0, 1))
         how = ("merged first %d per group (all_gather of the ranks' prefixes) bit-exact vs the C oracle's "
-               "whole-snapshot order on groups 0, 37, 99 (both orders)" % n_sel)
+               "whole-snapshot order: all %d groups, both orders" % (n_sel, G))
     if rank != 0:
         dist.destroy_process_group()
-        return
+        return 0 if parity else PARITY_EXIT
     if world != args.gpus:
         raise SystemExit("bench: n_gpus %d != --gpus %d" % (world, args.gpus))
-    # algorithmic bytes per membership (the roofline's): a membership record of node, group
-    # and flags read (12 B) and the node written (4 B; an upper bound —
-    # cordoned nodes feed neither order).  The resident layout moves less: one 4-B region
-    # word (node | flags << 28; the group is implied by the region) read by each of the two
-    # passes and the node written, 12 B (round 3: 14 B, a class byte written and re-read);
-    # the fused single pass (ESC_ORDER_FUSED=1) reads the word and the group word once, 12 B.
-    fused = os.environ.get("ESC_ORDER_FUSED", "0") not in ("", "0")
-    order_bytes = n_memb * 16
+    # algorithmic bytes per membership (the roofline's): the 8-B key and the
+    # 4-B node index written, 12 B.  The resident layout moves the same 12 B: one 4-B region
+    # word (node | flags << 28: the key's order is the region's, the group implied by the
+    # region) read by each of the two passes, and the node written (cordoned nodes feed
+    # neither order, so 12 B is an upper bound).
+    order_bytes = n_memb * 12
     moved_bytes = n_memb * 12
     # the index build: node table read twice (count: flags, label 8 B; list: flags, label,
     # created 16 B), each membership written once (12 B: 8-B key, 4-B node | flags value),
@@ -331,22 +428,26 @@ def bench_order(args):
         "data": "synthetic (esc_synth.cpp config 5: 10M nodes, 100 groups, unique ns creation times)",
         "config": {"workload": "config5: 10M nodes oldest-first / newest-first orderings, 100 node groups",
                    "nodes": N, "node_groups": G, "memberships": n_memb, "parallelism": "shard%d" % world},
-        "roofline": {"bound": "hbm", "kernel": ("k_ord_fused (per-decision ordering, one pass)" if fused else
-                                                "per-decision ordering (k_ord_count + k_ord_scatter)"),
+        "roofline": {"bound": "hbm", "kernel": "per-decision ordering (k_ord_count + k_ord_scatter)",
                      "bytes_moved_per_decision": moved_bytes,
                      "achieved": order_bytes / (order_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                      "frac": order_bytes / (order_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
                      "frac_moved": moved_bytes / (order_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
-                     "bytes_per_decision": order_bytes},
+                     "bytes_per_decision": order_bytes,
+                     "bytes_note": "SURVEY.md §8(d): 8-B key + 4-B index per membership; the kernels move 12 B",
+                     "timing": "cold: the Infinity Cache flushed (1 GiB write) before every decision, HIP events "
+                               "around the ordering kernels alone",
+                     "warm_ms": warm_ms, "frac_warm": order_bytes / (warm_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
+                     "warm_note": "back-to-back decisions; the ~130 MB working set may be served from the MALL"},
         "age_index_build": {"ms": index_ms, "nodes_per_s": N / (index_ms * 1e-3), "key_bits": R,
                             "lsd_passes": idx_passes, "GBps_moved": index_bytes / (index_ms * 1e-3) / 1e9},
         "selection_merge_ms": sel_ms,
         "segments_nonempty": int(sum(1 for c in counts if c)),
-        "parity": how if parity else "MISMATCH",
+        "parity": how if parity else "MISMATCH vs C oracle",
     }
-    print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return report(out, parity)
 
 
 def host_side(esc, ctx_dev):
@@ -597,11 +698,14 @@ def main():
     # context's stream (esc_k1_time) -- the stage events above add their own gap to a short
     # kernel (0.83x rocprof's duration at a rank's shard with them)
     k1_ms = ctx.k1_time(50)
-    # stages of enqueue_step in timing mode: K1, the fused tail (fold + node pieces + packed
-    # small-group orderings), the remaining ordering kernels, node groups (+ decide), [copy]
-    stage_names = (["k_pod_reduce", "k_step_tail", "k_order_split", "k_node_groups"] +
-                   (["d2h"] if os.environ.get("ESC_NO_ZEROCOPY", "0") not in ("", "0") else []))
+    # stages in timing mode: K1, the fused tail (fold + node pieces + packed small-group
+    # orderings), the remaining ordering kernels, node groups (+ K4 at one rank), then at
+    # world > 1 the exchange (ncclReduceScatter of the pod words, esc_exchange) and K4 over
+    # the rank's own groups (esc_decide); [9] = the whole step
+    stage_names = stage_layout(world, shard_world, multi, backend)
     stage_mean = np.mean(np.array(stages), axis=0)
+    stage_ms = {k: float(v) for k, v in zip(stage_names, stage_mean) if v > 0}
+    stage_ms["step_events"] = float(stage_mean[9])
 
     # BASELINE.md §2 logical bytes: this rank's pods (every pod for a multi-device context),
     # its ordered memberships (the groups it owns) -- summed over the ranks -- and the node
@@ -613,38 +717,14 @@ def main():
         dist.all_reduce(tmd)
         md = tmd.cpu().numpy()
 
-    parity = None
+    parity, parity_ok = None, True
     if not args.no_parity:
-        # rank 0 checks its decision (after the exchange) against the C oracle over the
-        # whole snapshot: at N > 1 that is a second, unsharded generation of the config
-        if rank == 0:
-            from oracle import soa
-            tot, dec = ctx.results()
-            full = s if world == 1 else esc.Synth(P, N, G, config=args.config, seed=0xE5CA1A7E00000000 + args.config,
-                                                 threads=16)
-            otot = soa.totals(full.pods(), full.nodes(), full.groups, threads=16)
-            odf, odi = soa.decide(full.groups, full.states, otot)
-            ok = all(np.array_equal(tot[n], otot[:, k]) for k, n in enumerate(soa.TOT_FIELDS[:12]))
-            ok &= np.array_equal(dec["cpu_pct"].view(np.uint64), odf[:, 0].view(np.uint64))
-            ok &= np.array_equal(dec["mem_pct"].view(np.uint64), odf[:, 1].view(np.uint64))
-            ok &= np.array_equal(dec["delta"], odi[:, 0])
-            checked = []
-            if not args.no_order:                 # three groups this rank can answer, both orders
-                mine = [g for g in range(G) if multi or ctx.group_owner(g) == rank]
-                for g in sorted(set([mine[0], mine[len(mine) // 2], mine[-1]])) if mine else []:
-                    checked.append(g)
-                    for w in (0, 1):
-                        ok &= np.array_equal(ctx.group_order(g, w), soa.order(full.nodes(), full.groups, g, w))
-            parity = ("bit-exact vs C oracle, all %d groups%s%s" % (
-                      G, "" if args.no_order else " (orderings: groups %s, both orders)" % checked,
-                      "" if n_gpus == 1 else " (rank 0 after the exchange over %d ranks, oracle over the unsharded "
-                                             "snapshot)" % n_gpus)
-                      if ok else "MISMATCH vs C oracle")
+        parity, parity_ok = check_parity(args, ctx, s, multi, rank, world, backend, dist, P, N, G, n_gpus)
 
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
-        return
+        return 0 if parity_ok else PARITY_EXIT
 
     # K1's algorithmic bytes per launch on device 0 (its share of the pods)
     algo = pod_b // (len(multi) if multi else 1)
@@ -699,11 +779,13 @@ def main():
         "node_bytes_per_decision": node_b,
         "exchange": exchange,
         "rccl_ranks": rccl_ranks,
-        # stages timed in order on one stream (timing mode); "d2h" only when the decisions
-        # are copied rather than written to pinned host memory by K3 (zero-copy)
-        "stage_ms": {k: float(v) for k, v in zip(stage_names, stage_mean) if v > 0} if world == 1 else None,
+        # stages timed in order on the context's stream (timing mode, rank 0 / device 0)
+        "stage_ms": stage_ms,
+        "exchange_ms": stage_ms.get("exchange"),
         "stage_note": ("HIP events between the step's launches, timing mode (each event pair adds a few us); "
-                       "k_order_split launches nothing when every group is packed into the tail (config 4)"),
+                       "k_order_split launches nothing when every group is packed into the tail (config 4); "
+                       "exchange = the in-place ncclReduceScatter of the owner-major pod words (DESIGN.md §7), "
+                       "k_decide = K4 over the rank's own groups"),
         "ordering": None if args.no_order else {
             "kernels": "groups of <= 1024 memberships packed as blocks of k_step_tail (one pass); larger groups by k_ord_count + k_ord_scatter after it; all on the context's one stream (esc_set_order_in_step)",
             "memberships": n_memb, "algorithmic_bytes": n_memb * 16},
@@ -721,9 +803,9 @@ def main():
         out["cpu_baseline"] = cpu_baseline(cfg, G, full=s)
     if n_gpus != args.gpus or (rccl_ranks is not None and rccl_ranks != args.gpus):
         raise SystemExit("bench: n_gpus %d / rccl_ranks %s != --gpus %d" % (n_gpus, rccl_ranks, args.gpus))
-    print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    return report(out, parity_ok)
 
 
 if __name__ == "__main__":

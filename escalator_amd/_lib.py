@@ -22,6 +22,8 @@ ESC_NONE = 0xFFFFFFFF
 
 ESC_ST_OK, ESC_ST_ERR_MIN_NODES, ESC_ST_ERR_MAX_NODES, ESC_ST_ERR_DIV_ZERO = 0, 1, 2, 3
 ESC_ST_ERR_NEG_DELTA, ESC_ST_ERR_OVERFLOW, ESC_ST_ERR_TAINT_MIN = 4, 5, 6
+ESC_ST_NOT_OWNED = 7                # world > 1: decided on the group's owner rank
+ESC_TF_NOT_OWNED = 4
 BRANCHES = ["empty", "gate", "below_min", "pct_err", "locked", "fast_down", "slow_down", "scale_up", "none"]
 
 PF_DAEMONSET, PF_STATIC, PF_HAS_SEL, PF_AFF_BLOCK, PF_HAS_OVH = 1, 2, 4, 8, 16
@@ -126,6 +128,7 @@ _SIGS = {
     "esc_ctx_counts": (i32, [VP, P(i64), P(i64)]),
     "esc_group_owner": (i32, [VP, i32, P(i32)]),
     "esc_node_owner_ranges": (i32, [VP, P(NodeSoA), i32, P(u32)]),
+    "esc_exchange_rows": (i32, [VP, P(NodeSoA), i32, P(u32), P(i32)]),
     "esc_comm_size": (i32, [VP, P(i32)]),
     "esc_ctx_destroy": (i32, [VP]),
     "esc_ctx_set_stream": (i32, [VP, VP]),
@@ -146,6 +149,7 @@ _SIGS = {
     "esc_set_state": (i32, [VP, P(GroupState)]),
     "esc_reduce": (i32, [VP]),
     "esc_exchange_buffers": (i32, [VP, P(VP), P(i64), P(VP), P(i64)]),
+    "esc_exchange_slice": (i32, [VP, P(i64), P(i64)]),
     "esc_bind_exchange_buffers": (i32, [VP, VP, VP]),
     "esc_exchange_download": (i32, [VP, P(i64), P(i64)]),
     "esc_exchange_upload": (i32, [VP, P(i64), P(i64)]),

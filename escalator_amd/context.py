@@ -221,6 +221,23 @@ class Context:
         L.check(self.lib.esc_comm_size(self.handle, C.byref(r)), "esc_comm_size")
         return r.value
 
+    def exchange_rows(self, nodes: dict, world: int) -> tuple[np.ndarray, int]:
+        """Host only: every group's owner-major row of the exchanged pod words and the rows
+        per owner (esc_exchange_rows)."""
+        ns, keep = node_soa(nodes)
+        rows = np.zeros(self.G, np.uint32)
+        cap = C.c_int32()
+        L.check(self.lib.esc_exchange_rows(self.handle, C.byref(ns), world, rows.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                           C.byref(cap)), "esc_exchange_rows")
+        del keep
+        return rows, cap.value
+
+    def exchange_slice(self) -> tuple[int, int]:
+        """(word offset, word count) of this rank's own rows in the exchange buffer."""
+        a, b = C.c_int64(), C.c_int64()
+        L.check(self.lib.esc_exchange_slice(self.handle, C.byref(a), C.byref(b)), "esc_exchange_slice")
+        return a.value, b.value
+
     def owner_ranges(self, nodes: dict, world: int) -> np.ndarray:
         """The owner split of the node side for `world` ranks (host only): rank r owns group
         pairs [q[r], q[r + 1])."""
@@ -330,8 +347,10 @@ class Context:
         L.check(self.lib.esc_set_timing(self.handle, int(on)))
 
     def stage_times(self) -> list[float]:
-        a = (C.c_double * 8)()
-        L.check(self.lib.esc_stage_times(self.handle, a, 8))
+        """ms per stage of the last decision (timing mode): K1, tail, orderings, node groups
+        (+ K4 at world 1), [exchange, K4 at world > 1]; [9] the whole step."""
+        a = (C.c_double * 10)()
+        L.check(self.lib.esc_stage_times(self.handle, a, 10))
         return list(a)
 
     def k1_calibrate(self, rounds: int = 4):

@@ -33,19 +33,15 @@ constexpr int64_t PODS_PER_BLOCK_MAX  = int64_t(1) << 20;  // keeps cpu|count<<4
 constexpr int CNT_SHIFT = 40;
 constexpr uint64_t CPU_MASK = (uint64_t(1) << CNT_SHIFT) - 1;
 
-// Per-group pod words, all-reduced with SUM across ranks together with the node words
-// below.  Every sum travels split as
+// Per-group pod words, reduce-scattered with SUM across ranks to each group's owner
+// (DESIGN.md §7).  Every sum travels split as
 // lo = v & 0xffffffff, hi = v >> 32 (arithmetic) so the cross-rank SUM cannot wrap and
 // the exact total is recoverable (Quantity.Add's overflow check).
 enum PodWord : int { PW_CPU_LO = 0, PW_CPU_HI, PW_MEM_LO, PW_MEM_HI, PW_N, PW_K };
 // Per-group node words (final, exact): untainted capacity sums and the filterNodes counts;
-// NW_FLAGS carries ESC_TF_NODE_OVERFLOW.
+// NW_FLAGS carries ESC_TF_NODE_OVERFLOW.  One rank owns each group's node side (its pair's
+// entries) and computes these words exactly; they are never exchanged.
 enum NodeWord : int { NW_CPU = 0, NW_MEM, NW_N_UNT, NW_N_TAINT, NW_N_CORD, NW_FLAGS, NW_K };
-// The node words as exchanged: one rank owns each group's node side (its
-// pair's entries), so its words are exact on the owner and zero on every other rank, and
-// the cross-rank SUM that carries the pod words delivers them unchanged.  Counts are below
-// 2^31 (node slots), so two share a word without carries.
-enum NodeXWord : int { NX_CPU = 0, NX_MEM, NX_CNT /* unt | taint << 32 */, NX_CORD /* cord | flags << 32 */, NX_K };
 
 // Device-side per-group parameters (from esc_group_spec + esc_group_state).
 struct GroupParams {

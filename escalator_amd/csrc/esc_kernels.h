@@ -368,6 +368,7 @@ struct GroupDev {
     const uint32_t* node_code; // [n_gp] pair id -> group code (K5)
     const uint32_t* code_list; // CODE_MULTI lists: [count, g...]
     const uint32_t* gslot;     // [G] the group's pod slot: its pair, or n_gp for the default group
+    const uint32_t* xs;        // [G] the group's row of the exchanged pod words (owner-major)
     esc_group_metrics* metrics; // [G] gauges written by K4, or null (esc_set_metrics)
     int64_t sp;                // K1 partial row stride: pod slots rounded up to FC_COL
     uint32_t n_gp;             // pod slots: pair ids [0, n_gp) + the default filter's slot n_gp
@@ -381,18 +382,14 @@ enum WidePod : int { WP_CPU_LO = 0, WP_CPU_HI, WP_MEM_LO, WP_MEM_HI, WP_CNT, WP_
 // Per dry-mode group: the tracked members' count and split sums (K2 adds, K3 resets).
 enum TrkAcc : int { TA_CNT = 0, TA_CPU_LO, TA_CPU_HI, TA_MEM_LO, TA_MEM_HI, TA_K };
 
-// variant (ESC_K1_VARIANT, measurement knob): 0 = 512 threads (default: 8 waves per CU with
-// up to 256 VGPRs, 3-4 K tiles in flight per wave, one static share per workgroup), 1 = two
-// C tiles in flight, 2 = 1024 threads (16 waves, 128 VGPRs, 1-3 tiles in flight), 5 = 512
-// threads with dynamic shares (below; parity-exact but slower: profiles/r01_v10), 9.. =
-// timing-only ablations (wrong results, scripts/k1_variants.py).
-// Dynamic shares (variant 5): the K tiles' weight is cut into nblk * K1_CHUNKS chunks; a workgroup
-// takes at most `cap` of them (K1_CHUNKS..K1_CHUNK_CAP, the packed LDS partials' exactness
-// bound, see ensure_work).  ticket: two u32 (next chunk, workgroups done), zero between launches —
-// the last workgroup to finish resets them.
+// variant: 0 = the product K1 (512 threads: 8 waves per CU with up to 256 VGPRs, 3-4 K
+// tiles in flight per wave, one static share per workgroup); 3, 4, 9-14 = timing-only
+// ablations (wrong results), present in the measurement library only (ESC_K1_VARIANT,
+// scripts/k1_variants.py).
+// K1_CHUNKS: the unit of a static share's size bound (ensure_work); the K1 template's
+// dynamic-share form (a ticket of nblk * K1_CHUNKS chunks) is instantiated only by the
+// measurement library's ablations.
 constexpr int K1_CHUNKS = 4;
-constexpr int K1_CHUNK_CAP = 8;
-bool k1_dynamic(int variant);
 struct DecCompact;
 // K1 diagnostics.  trace: per workgroup 8 words (esc_k1_trace; the share calibration reads words
 // 0-1): s_memrealtime (100 MHz) at start, after the K tiles, after the C tiles, after the
@@ -400,13 +397,19 @@ struct DecCompact;
 struct K1Diag {
     uint64_t* trace;
 };
-// k_node_groups' decision (one rank without an exchange): null dec = the node words only,
-// written as exchange words (NX_K per group) to nx for the SUM and k_decide.
+// k_node_groups' decision (one rank without an exchange): null dec = the node words only
+// (nwords), which k_decide reads after the exchange.
 struct NGDecide {
     const int64_t* pwords;
     esc_group_decision* dec;
     DecCompact* cdec;
-    int64_t* nx;
+};
+// The groups a launch of k_node_groups / k_decide covers: ids[i] for i < n, or, with null
+// ids, the contiguous run first + i (a rank's owned groups).
+struct GroupList {
+    const uint32_t* ids;
+    int32_t n;
+    int32_t first;
 };
 hipError_t launch_pod_reduce(const PodDev& p, const GroupDev& g, int32_t g0, int32_t gw, int nblk, int variant,
                              uint64_t* part, int64_t* wide, uint32_t* ticket, int cap, const K1Diag& diag,
@@ -428,16 +431,17 @@ static_assert(sizeof(DecCompact) == 32, "compact decision is 2 x 16 B");
 
 // K2b + K4 (k_node_groups): every group's final node words from K2's piece rows, then
 // (nd.dec != null) the decisions.  K4 alone (k_decide): after an exchange.
-// k_decide reads the exchanged pod words (pwords, G x PW_K) and node words (nx, G x NX_K)
-// and writes the final node words (nwords, G x NW_K, for esc_results) besides the decisions.
-hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords, const int64_t* nx,
-                         int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st);
+// k_decide reads the owned groups' exchanged pod words (pwords: row i for the list's group
+// i, the owner's slice after the reduce-scatter) and their node words (nwords, G x NW_K,
+// written by k_node_groups on the owner).
+hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const GroupList& list, const int64_t* pwords,
+                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st);
 // Peer exchange of a multi-device context (esc_ctx_create_multi): dst[i] = sum of src[k][i]
 // over the n_src buffers (peer-mapped device memory), int64 or uint32 words.
 hipError_t launch_peer_sum64(const int64_t* const* src, int n_src, int64_t* dst, int64_t n, hipStream_t st);
 hipError_t launch_peer_sum32(const uint32_t* const* src, int n_src, uint32_t* dst, int64_t n, hipStream_t st);
-hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t* node_rows, int64_t* trk_acc,
-                              int64_t* nwords, const NGDecide& nd, hipStream_t st);
+hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const GroupList& list, const int64_t* node_rows,
+                              int64_t* trk_acc, int64_t* nwords, const NGDecide& nd, hipStream_t st);
 // K3 fold (a role of k_step_tail): the K1 partials of FC_COL pod slots per block.
 constexpr int FC_COL = 32;             // pod slots per K3 column (a 256-B piece of each K1 row)
 struct FoldPlan {
@@ -550,11 +554,6 @@ hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_
 // Fills the padding of every group's region (after its `len` memberships) with g | MEMB_PAD.
 hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_grp,
                              uint32_t* g_memb, hipStream_t st);
-hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
-                              const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
-                              unsigned long long* ticket, unsigned long long* status,
-                              uint32_t* vals, int64_t* seg, uint32_t* err, int64_t max_chunk, int ablate,
-                              hipStream_t st);
 // The age index (load time): memberships counted per block of nodes (scan: cnt = block
 // bases, *total), listed with (group << R | creation offset) keys and (node | flags << 32)
 // values, LSD-sorted (result in keys[*src] / vals[*src]), group starts; then written into

@@ -28,6 +28,13 @@
 
 #include "esc_kernels.h"
 
+// Written for gfx950 only: K1's 10 240-slot LDS window (160 KB) and the age-index scatter's
+// carried lines (~109 KB per 1024-thread block at 8-bit digits) need CDNA4's 160 KB of LDS
+// per CU; a gfx942 (64 KB) build would fail to launch, so it is refused here.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "esc_kernels.hip targets gfx950 (160 KB LDS per CU); build with ARCH=gfx950"
+#endif
+
 #ifndef MK_ABL
 #define MK_ABL 0                                     // k_memb_keys ablations (timing only)
 #endif
@@ -1183,9 +1190,11 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
 
 // ============================================================ K1 launchers by part
 // The K1 template is instantiated once per (variant, 16 record shapes): the production
-// variant in part 0 (with every other kernel), the exact alternatives (1, 2, 5, 6) in
-// part 1 and the timing-only ablations in part 2, each its own translation unit so the
-// build compiles them in parallel (Makefile; part 2 only with ABLATIONS=1).
+// variant in part 0 (with every other kernel) and the timing-only ablations in part 2, its
+// own translation unit, linked only into the measurement library (Makefile ABLATIONS=1,
+// libescalator_hip_measure.so).  The exact alternatives measured slower (1: two C tiles in
+// flight, 2: 1024 threads, 5: dynamic shares, 6: per-wave shares) were
+// removed from the product.
 #define ESC_K1(T, A, DC) ESC_K1D(T, A, DC, 0)
 #define ESC_K1D(T, A, DC, D) ESC_K1W(T, A, DC, D, 0)
 #define ESC_K1W(T, A, DC, D, W)                                                                       \
@@ -1193,36 +1202,17 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
                        wide, ticket, cap, diag)
 #define ESC_K1_ARGS const PodDev &p, const GroupDev &g, int32_t g0, int32_t gw, int nblk, int variant, uint64_t *part, \
                     int64_t *wide, uint32_t *ticket, int cap, const K1Diag &diag, hipStream_t st
-hipError_t launch_pod_reduce_alt(ESC_K1_ARGS);
 hipError_t launch_pod_reduce_ablation(ESC_K1_ARGS) __attribute__((weak));
 
 #if ESC_PART == 0
-bool k1_dynamic(int variant) { return variant == 5; }
-
-
-
 hipError_t launch_pod_reduce(ESC_K1_ARGS) {
     const size_t lds = (size_t)(gw + FC_COL - 1) / FC_COL * FC_COL * 2 * sizeof(uint64_t);
     switch (variant) {
         case 0: ESC_K1(512, 0, 3); break;
-        case 5:
-            return launch_pod_reduce_alt(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, diag, st);
-        default:                                  // timing-only ablations (ABLATIONS=1 build)
+        default:                                  // timing-only ablations (measurement library only)
             if (!launch_pod_reduce_ablation) return hipErrorInvalidValue;
             return launch_pod_reduce_ablation(p, g, g0, gw, nblk, variant, part, wide, ticket, cap, diag,
                                               st);
-    }
-    return hipGetLastError();
-}
-#elif ESC_PART == 1
-hipError_t launch_pod_reduce_alt(ESC_K1_ARGS) {
-    const size_t lds = (size_t)(gw + FC_COL - 1) / FC_COL * FC_COL * 2 * sizeof(uint64_t);
-    switch (variant) {
-        // dynamic shares (measured slower).  (Variants 1: two C tiles in
-        // flight, 2: 1024 threads, 6: per-wave shares were measured and dropped in round 3:
-        // each doubled the build once the packed pipelines joined the plain ones.)
-        case 5: ESC_K1D(512, 0, 3, 1); break;
-        default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
@@ -1498,8 +1488,9 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
         phi = gn.phi;
         if (D.dec && wid == 0) {                     // K4's inputs (wave 0 decides), loaded beside the piece rows
             prm = G.params[g];
+            const int64_t* pw = D.pwords + (int64_t)(G.xs ? G.xs[g] : (uint32_t)g) * PW_K;
 #pragma unroll
-            for (int k = 0; k < PW_K; ++k) pwv[k] = D.pwords[(int64_t)g * PW_K + k];
+            for (int k = 0; k < PW_K; ++k) pwv[k] = pw[k];
         }
     }
     const int64_t np = N.n_pieces;
@@ -1564,13 +1555,7 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
                           n_ok ? 0 : ESC_TF_NODE_OVERFLOW};
     static_assert(NW_CPU == 0 && NW_MEM == 1 && NW_N_UNT == 2 && NW_N_TAINT == 3 && NW_N_CORD == 4 && NW_FLAGS == 5,
                   "node word order");
-    if (!D.dec) {                                    // exchange words: zero unless this rank owns the pair
-        int64_t* x = D.nx + (int64_t)g * NX_K;
-        x[NX_CPU] = v[0];
-        x[NX_MEM] = v[1];
-        x[NX_CNT] = (int64_t)((uint64_t)n_unt | ((uint64_t)n_taint << 32));
-        x[NX_CORD] = (int64_t)((uint64_t)n_cord | ((uint64_t)v[5] << 32));
-    } else {
+    {
         int64_t* nw = nwords + (int64_t)g * NW_K;
 #pragma unroll
         for (int k = 0; k < 6; ++k) nw[k] = v[k];
@@ -1599,46 +1584,49 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
 // reduces only the pieces of the pairs it owns, so a group's words are exact on its owner
 // and zero elsewhere.  With a decision target (D.dec: one rank, no exchange) the block then
 // decides its groups (K4 on this rank's fold) and writes the compact records to the
-// decision buffer as one contiguous run; otherwise it writes the words to the exchange
-// buffer (D.nx) and k_decide runs after the SUM.  (Running this work inside k_step_tail's
-// fold blocks measured slower)
-__global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeDev N,
+// decision buffer as one contiguous run; otherwise it writes only the node words and
+// k_decide runs after the exchange.  With several ranks a launch covers the rank's OWN
+// groups (the list): the others' node words are their owners' to compute.
+// (Running this work inside k_step_tail's fold blocks measured slower)
+__global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeDev N, GroupList L,
                                                                const int64_t* __restrict__ node_rows,
                                                                int64_t* __restrict__ trk_acc,
                                                                int64_t* __restrict__ nwords, NGDecide D) {
-    const int32_t g0 = blockIdx.x * 64;
-    const int32_t g = g0 + (int32_t)(threadIdx.x & 63);
-    const uint32_t n = G.G - g0 < 64 ? (uint32_t)(G.G - g0) : 64u;
-    node_groups_part(G, N, node_rows, trk_acc, nwords, D, g < G.G ? (uint32_t)g : NONE, true, g0, n);
+    const int32_t i0 = blockIdx.x * 64;
+    const int32_t i = i0 + (int32_t)(threadIdx.x & 63);
+    const uint32_t n = L.n - i0 < 64 ? (uint32_t)(L.n - i0) : 64u;
+    const uint32_t g = i >= L.n ? NONE : L.ids ? L.ids[i] : (uint32_t)(L.first + i);
+    node_groups_part(G, N, node_rows, trk_acc, nwords, D, g, !L.ids, L.first + i0, n);
 }
 
-// K4 alone (esc_decide after an exchange): the pod and node words are the exchanged sums
-// (the node words exact from their owner rank); the final node words are kept for
-// esc_results.
+// K4 alone (esc_decide after an exchange), for the rank's OWN groups only:
+// their pod words are the owner's slice of the reduce-scatter (row i for list group i),
+// their node words the owner's own (k_node_groups).  Only the owned decisions cross PCIe.
 // One wave per 64 groups (a latency chain per group: 40 blocks of 256 threads left most CUs
 // idle, 8.5 us for 10 k groups).
 constexpr int KD_BLOCK = 64;
-__global__ __launch_bounds__(KD_BLOCK) void k_decide(GroupDev G, NodeDev N, const int64_t* __restrict__ pwords,
-                                                     const int64_t* __restrict__ nx, int64_t* __restrict__ nwords,
+__global__ __launch_bounds__(KD_BLOCK) void k_decide(GroupDev G, NodeDev N, GroupList L,
+                                                     const int64_t* __restrict__ pwords,
+                                                     const int64_t* __restrict__ nwords,
                                                      esc_group_decision* __restrict__ dec, DecCompact* __restrict__ cdec) {
     __shared__ DecCompact sc[KD_BLOCK];
-    const int32_t g0 = blockIdx.x * KD_BLOCK, g = g0 + (int32_t)threadIdx.x;
-    if (g < G.G) {
-        const int64_t* x = nx + (int64_t)g * NX_K;
-        const uint64_t cnt = (uint64_t)x[NX_CNT], cf = (uint64_t)x[NX_CORD];
-        const int64_t v[NW_K] = {x[NX_CPU], x[NX_MEM], (int64_t)(cnt & 0xFFFFFFFFull), (int64_t)(cnt >> 32),
-                                 (int64_t)(cf & 0xFFFFFFFFull), (int64_t)(cf >> 32)};
-        int64_t* nw = nwords + (int64_t)g * NW_K;
+    __shared__ uint32_t sid[KD_BLOCK];
+    const int32_t i0 = blockIdx.x * KD_BLOCK, i = i0 + (int32_t)threadIdx.x;
+    if (i < L.n) {
+        const int32_t g = L.ids ? (int32_t)L.ids[i] : L.first + i;
+        int64_t v[NW_K];
+        const int64_t* nw = nwords + (int64_t)g * NW_K;
 #pragma unroll
-        for (int k = 0; k < NW_K; ++k) nw[k] = v[k];
+        for (int k = 0; k < NW_K; ++k) v[k] = nw[k];
         esc_group_decision d;
-        finalize(G, N.gnode[g], g, pwords + (int64_t)g * PW_K, v, d, G.metrics);
+        finalize(G, N.gnode[g], g, pwords + (int64_t)i * PW_K, v, d, G.metrics);
         store_full(dec + g, d);
         sc[threadIdx.x] = compact_of(d);
+        sid[threadIdx.x] = (uint32_t)g;
     }
     __syncthreads();
-    const uint32_t n = G.G - g0 < KD_BLOCK ? (uint32_t)(G.G - g0) : (uint32_t)KD_BLOCK;
-    store_compact(cdec, sc, n, true, (uint32_t)g0, nullptr, threadIdx.x, KD_BLOCK);
+    const uint32_t n = L.n - i0 < KD_BLOCK ? (uint32_t)(L.n - i0) : (uint32_t)KD_BLOCK;
+    store_compact(cdec, sc, n, !L.ids, (uint32_t)(L.first + i0), sid, threadIdx.x, KD_BLOCK);
 }
 
 // K3 fold (fold_col, a role of k_step_tail): the K1 workgroups' slot partials folded and
@@ -1761,7 +1749,7 @@ __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, i
         const int32_t g = first ? g_0 : (ok ? (int32_t)F.col_groups[base + me] : 0);
         if (ok) {
             const int sl = (int)((int64_t)(first ? sl_0 : G.gslot[g]) - s0);
-            int64_t* pw = pwords + (int64_t)g * PW_K;
+            int64_t* pw = pwords + (int64_t)(G.xs ? G.xs[g] : (uint32_t)g) * PW_K;
             const __int128 pcpu = (__int128)tot[0][sl] + ((__int128)wtot[WP_CPU_HI][sl] << 32) + (__int128)wtot[WP_CPU_LO][sl];
             const __int128 pmem = (__int128)(((unsigned __int128)tot[3][sl] << 64) | tot[2][sl]) +
                                   ((__int128)wtot[WP_MEM_HI][sl] << 32) + (__int128)wtot[WP_MEM_LO][sl];
@@ -2637,159 +2625,6 @@ __global__ __launch_bounds__(256) void k_region_pad(const uint32_t* __restrict__
     }
 }
 
-// Fused single pass (default): the per-decision order in one launch.  A chunk's block
-// classifies its <= 4096 memberships (12 B each), ranks classes 0 / 1 inside the chunk,
-// takes its exclusive per-class prefix within the group by decoupled look-back over the
-// group's earlier chunks, and writes untainted nodes forward from the group's start
-// (oldest first) and tainted nodes backward from the group's end (so that segment read
-// forward is newest first, untaintNewestN's order).  Cordoned nodes feed neither order
-// and are not written.  16 B per membership instead of the three-pass 22 B.
-// Chunks are taken in ticket order (one global counter), so a chunk's predecessors have
-// started before it spins on them; each status word carries the decision epoch
-// (ticket / n_chunks), so nothing needs resetting between decisions.  A look-back that
-// waits beyond a bound stops and raises *err (a lost predecessor would be a bug; the
-// bound keeps the grid finite whatever happens).
-namespace {
-constexpr uint64_t OST_AGG = 1, OST_INC = 2;
-constexpr int OST_CBITS = 27;
-constexpr uint64_t OST_CMASK = (1ull << OST_CBITS) - 1;
-__device__ __forceinline__ uint64_t ost_pack(uint32_t epoch, uint64_t flag, uint64_t n0, uint64_t n1) {
-    return ((uint64_t)(epoch & 0xFF) << 56) | (flag << 54) | ((n0 & OST_CMASK) << OST_CBITS) | (n1 & OST_CMASK);
-}
-}  // namespace
-
-template <int FB>
-__global__ __launch_bounds__(FB) void k_ord_fused(NodeDev N, const OrdChunk* __restrict__ chunks,
-                                                         int64_t n_chunks, const uint32_t* __restrict__ gch_off,
-                                                         const uint32_t* __restrict__ grp_off,
-                                                         const uint32_t* __restrict__ g_memb,
-                                                         const uint32_t* __restrict__ g_grp,
-                                                         unsigned long long* __restrict__ ticket,
-                                                         unsigned long long* __restrict__ status,
-                                                         uint32_t* __restrict__ vals, int64_t* __restrict__ seg,
-                                                         uint32_t* __restrict__ err, int ablate) {
-    constexpr int ROUNDS = 4, FW = FB / 64;              // 4 quads per thread: 16 * FB memberships
-    __shared__ unsigned long long s_tk;
-    __shared__ uint32_t wt[ROUNDS][FW];
-    __shared__ uint32_t s_pre[2];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_tk = (ablate & 4) ? (unsigned long long)blockIdx.x : atomicAdd(ticket, 1ull);
-    __syncthreads();
-    const unsigned long long tk = s_tk;
-    const int64_t q = (int64_t)(tk % (unsigned long long)n_chunks);
-    const uint32_t epoch = (uint32_t)(tk / (unsigned long long)n_chunks);
-    const OrdChunk ch = chunks[q];
-    // classify: all four quads' loads in flight
-    uint4 nd[ROUNDS], gr[ROUNDS];
-#pragma unroll
-    for (int r = 0; r < ROUNDS; ++r) {
-        const uint32_t b = ch.start + r * 4 * FB + 4 * threadIdx.x;
-        const uint32_t bb = b < ch.end ? b : ch.start;
-        nd[r] = ld4(g_memb + bb);
-        gr[r] = ld4(g_grp + bb);
-    }
-    uint32_t cls = 0;                                     // 2 bits per membership
-    uint32_t v[ROUNDS];                                   // class 0 | class 1 << 16, per round
-#pragma unroll
-    for (int r = 0; r < ROUNDS; ++r) {
-        const uint32_t b = ch.start + r * 4 * FB + 4 * threadIdx.x;
-        v[r] = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t k = b + j < ch.end ? ord_class(N, 0u, lane4(gr[r], j), lane4(nd[r], j) >> MEMB_FLAG_SHIFT) : 3u;
-            cls |= k << (2 * (4 * r + j));
-            v[r] += k == 0 ? 1u : (k == 1 ? 0x10000u : 0u);
-        }
-        const uint32_t inc = wave_incl_scan32(v[r]);
-        if (lane == 63) wt[r][wid] = inc;
-        v[r] = inc - v[r];                                // exclusive, within the wave
-    }
-    __syncthreads();
-    // block prefix in membership order (round, wave, lane) and the chunk's aggregate
-    uint32_t agg = 0;
-    uint32_t pre[ROUNDS];
-#pragma unroll
-    for (int r = 0; r < ROUNDS; ++r)
-#pragma unroll
-        for (int w = 0; w < FW; ++w) {
-            if (w == wid) pre[r] = agg;
-            agg += wt[r][w];
-        }
-    const uint32_t g = ch.group;
-    const uint32_t q0 = gch_off[g];
-    const uint64_t a0 = agg & 0xFFFF, a1 = agg >> 16;
-    if (threadIdx.x < 64) {                               // wave 0: publish, then look back
-        uint64_t p0 = 0, p1 = 0;
-        if ((uint32_t)q == q0 || (ablate & 1)) {        // ablate bit 0 (timing only): no look-back
-            if (lane == 0)
-                __hip_atomic_store(status + q, ost_pack(epoch, OST_INC, a0, a1), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            if (lane == 0)
-                __hip_atomic_store(status + q, ost_pack(epoch, OST_AGG, a0, a1), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            // a window of 64 predecessors per round (lane l: chunk hi - l); the nearest
-            // inclusive word ends the walk once every chunk before it in the window is ready
-            int64_t hi = q - 1;
-            uint32_t spins = 0;
-            for (;;) {
-                const int64_t j = hi - lane;
-                const bool valid = j >= (int64_t)q0;
-                const uint64_t w = valid ? __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-                const uint32_t f = (uint32_t)((w >> 54) & 3);
-                const bool ready = valid && (uint32_t)(w >> 56) == (epoch & 0xFF) && f != 0;
-                const unsigned long long m_inc = __ballot(ready && f == OST_INC);
-                const unsigned long long m_wait = __ballot(valid && !ready);
-                const unsigned long long need = m_inc ? (m_inc & (~m_inc + 1)) * 2 - 1 : ~0ull;   // lanes up to the nearest INC
-                if (m_wait & need) {
-                    if (++spins > (1u << 22)) {
-                        if (lane == 0) atomicOr(err, 1u);
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    continue;
-                }
-                const bool take = valid && ((need >> lane) & 1ull);
-                p0 += wave_sum64(take ? (w >> OST_CBITS) & OST_CMASK : 0);
-                p1 += wave_sum64(take ? w & OST_CMASK : 0);
-                if (m_inc || hi - 64 < (int64_t)q0) break;
-                hi -= 64;
-            }
-            if (lane == 0)
-                __hip_atomic_store(status + q, ost_pack(epoch, OST_INC, p0 + a0, p1 + a1), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (lane == 0) {
-            s_pre[0] = (uint32_t)p0;
-            s_pre[1] = (uint32_t)p1;
-            if ((uint32_t)q + 1 == gch_off[g + 1]) {      // the group's last chunk: segment bounds
-                const int64_t s0 = grp_off[g], s3 = grp_off[g + 1];
-                seg[4 * (int64_t)g + 0] = s0;
-                seg[4 * (int64_t)g + 1] = s0 + (int64_t)(p0 + a0);
-                seg[4 * (int64_t)g + 2] = s3 - (int64_t)(p1 + a1);
-                seg[4 * (int64_t)g + 3] = s3;
-            }
-        }
-    }
-    __syncthreads();
-    if (ablate & 2) {                                    // timing only: no scatter
-        if (cls == 0x12345678u) vals[0] = 0;
-        return;
-    }
-    const uint32_t base0 = grp_off[g] + s_pre[0], last1 = grp_off[g + 1] - 1 - s_pre[1];
-#pragma unroll
-    for (int r = 0; r < ROUNDS; ++r) {
-        const uint32_t x = pre[r] + v[r];
-        uint32_t r0 = x & 0xFFFF, r1 = x >> 16;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t k = (cls >> (2 * (4 * r + j))) & 3u;
-            if (k == 0) vals[base0 + r0++] = lane4(nd[r], j) & MEMB_NODE_MASK;
-            else if (k == 1) vals[last1 - r1++] = lane4(nd[r], j) & MEMB_NODE_MASK;
-        }
-    }
-}
-
 // Start of each (group, class) segment in the partitioned keys: seg[s] = first key >= s.
 
 // ===================================================================== snapshot patches
@@ -2994,17 +2829,19 @@ hipError_t launch_pod_bigtiles(const PodDev& p, const GroupDev& g, const uint32_
     return hipGetLastError();
 }
 
-hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const int64_t* node_rows, int64_t* trk_acc,
-                              int64_t* nwords, const NGDecide& nd, hipStream_t st) {
-    hipLaunchKernelGGL(k_node_groups, dim3((g.G + 63) / 64), dim3(NG_WAVES * 64), 0, st, g, n, node_rows, trk_acc,
-                       nwords, nd);
+hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const GroupList& list, const int64_t* node_rows,
+                              int64_t* trk_acc, int64_t* nwords, const NGDecide& nd, hipStream_t st) {
+    if (list.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_node_groups, dim3((list.n + 63) / 64), dim3(NG_WAVES * 64), 0, st, g, n, list, node_rows,
+                       trk_acc, nwords, nd);
     return hipGetLastError();
 }
 
-hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const int64_t* pwords, const int64_t* nx,
-                         int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st) {
-    hipLaunchKernelGGL(k_decide, dim3((g.G + KD_BLOCK - 1) / KD_BLOCK), dim3(KD_BLOCK), 0, st, g, n, pwords, nx, nwords,
-                       dec, cdec);
+hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const GroupList& list, const int64_t* pwords,
+                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st) {
+    if (list.n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_decide, dim3((list.n + KD_BLOCK - 1) / KD_BLOCK), dim3(KD_BLOCK), 0, st, g, n, list, pwords,
+                       nwords, dec, cdec);
     return hipGetLastError();
 }
 
@@ -3188,24 +3025,6 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const
         const hipError_t e = rs_sort<uint64_t, uint32_t>(keys, vals, n_memb, R + gbits, hist, tot, &src, S, st);
         if (e != hipSuccess) return e;
     }
-    return hipGetLastError();
-}
-
-hipError_t launch_order_fused(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
-                              const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
-                              unsigned long long* ticket, unsigned long long* status,
-                              uint32_t* vals, int64_t* seg, uint32_t* err, int64_t max_chunk, int ablate,
-                              hipStream_t st) {
-    if (n_chunks <= 0) return hipSuccess;
-    if (max_chunk > 16 * 512)                             // 1024 threads: up to 16384 per chunk
-        hipLaunchKernelGGL(k_ord_fused<1024>, dim3((unsigned)n_chunks), dim3(1024), 0, st, nd, chunks, n_chunks,
-                           gch_off, grp_off, g_memb, g_grp, ticket, status, vals, seg, err, ablate);
-    else if (max_chunk > 16 * 256)
-        hipLaunchKernelGGL(k_ord_fused<512>, dim3((unsigned)n_chunks), dim3(512), 0, st, nd, chunks, n_chunks,
-                           gch_off, grp_off, g_memb, g_grp, ticket, status, vals, seg, err, ablate);
-    else
-        hipLaunchKernelGGL(k_ord_fused<256>, dim3((unsigned)n_chunks), dim3(256), 0, st, nd, chunks, n_chunks,
-                           gch_off, grp_off, g_memb, g_grp, ticket, status, vals, seg, err, ablate);
     return hipGetLastError();
 }
 

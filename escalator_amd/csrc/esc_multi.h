@@ -19,6 +19,7 @@ struct RcclApi {
     decltype(&ncclCommInitRank) init_rank = nullptr;
     decltype(&ncclCommInitAll) init_all = nullptr;
     decltype(&ncclAllReduce) all_reduce = nullptr;
+    decltype(&ncclReduceScatter) reduce_scatter = nullptr;
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclCommCount) count = nullptr;
@@ -51,6 +52,7 @@ int32_t multi_set_state(esc_ctx* c, const esc_group_state* st);
 int32_t multi_step(esc_ctx* c);
 int32_t multi_sync(esc_ctx* c);
 int32_t multi_results(esc_ctx* c, esc_group_totals* t, esc_group_decision* d);
+int32_t multi_metrics_results(esc_ctx* c, esc_group_metrics* out);
 int32_t multi_each(esc_ctx* c, int32_t (*fn)(esc_ctx*, int32_t), int32_t arg);   // a setter on every device
 esc_ctx* multi_sub(const esc_ctx* c, int i);                                     // device i's context
 int32_t multi_k1_calibrate(esc_ctx* c, int32_t rounds);

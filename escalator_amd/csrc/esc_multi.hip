@@ -7,15 +7,18 @@
 // context per GPU (rank i of n: pods [lo_i, hi_i) of the loaded snapshot, the whole node
 // table with the node side of the group pairs it owns) and a communicator set from
 // ncclCommInitAll.  A decision enqueues every device's shard step, the in-place
-// ncclAllReduce(int64, SUM) of the exchange words inside ncclGroupStart / ncclGroupEnd,
-// and every device's K4, all from the calling thread.  The layer is a client of the
+// ncclReduceScatter(int64, SUM) of the exchange words inside ncclGroupStart / ncclGroupEnd
+// (every device receives the sums of the groups it owns), and every device's
+// K4 over its own groups, all from the calling thread; esc_results merges the owners'
+// records.  The layer is a client of the
 // per-device ABI (esc_reduce / esc_exchange_buffers / esc_decide ...): it adds the fan-out,
 // the routing of pod ids to shards and the exchange.
 //
 // Exchange modes: RCCL when the devices are distinct (the default); a peer exchange —
-// every device sums the others' words over peer-mapped memory with one kernel, ordered by
-// HIP events — when ESC_EXCHANGE=peer is set or a device is listed twice (several shards
-// on one GPU: how the fan-out, routing and exchange are exercised on a one-GPU machine).
+// every device sums its own slice of everyone's words over peer-mapped memory with one
+// kernel, ordered by HIP events — when ESC_EXCHANGE=peer is set or a device is listed twice
+// (several shards on one GPU: how the fan-out, routing and exchange are exercised on a
+// one-GPU machine).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -83,12 +86,13 @@ int owner_of_pod(const esc_ctx* c, int64_t id) {
     return (int)(std::upper_bound(lo.begin(), lo.end(), id) - lo.begin()) - 1;
 }
 
-// Sums every device's `words[i]` into each device's own buffer over peer-mapped memory:
-// the sums wait for every device's producer (ev_done), the write-backs for every sum
-// (ev_read), so no buffer is rewritten while a peer still reads it.
+// Sums every device's `words[j][off[i], off[i] + n)` into device i's own buffer over
+// peer-mapped memory (off: the slice device i needs — its owned rows — or 0): the sums wait
+// for every device's producer (ev_done), the write-backs for every sum (ev_read), so no
+// buffer is rewritten while a peer still reads it.
 template <class T>
-int32_t peer_exchange(esc_ctx* c, const std::vector<T*>& words, int64_t n, std::vector<T*>& tmp, int64_t& tmp_n,
-                      bool all_devices) {
+int32_t peer_exchange(esc_ctx* c, const std::vector<T*>& words, const std::vector<int64_t>& off, int64_t n,
+                      std::vector<T*>& tmp, int64_t& tmp_n, bool all_devices) {
     esc_multi_state& m = M(c);
     const int k = nsub(c);
     if (tmp_n < n) {
@@ -101,7 +105,7 @@ int32_t peer_exchange(esc_ctx* c, const std::vector<T*>& words, int64_t n, std::
         }
         tmp_n = n;
     }
-    std::vector<const T*> src(words.begin(), words.end());
+    std::vector<const T*> src(k);
     for (int i = 0; i < k; ++i) {
         hipSetDevice(m.devices[i]);
         if (hipEventRecord(m.ev_done[i], ctx_stream(m.subs[i])) != hipSuccess) return ESC_E_HIP;
@@ -112,6 +116,7 @@ int32_t peer_exchange(esc_ctx* c, const std::vector<T*>& words, int64_t n, std::
         hipStream_t st = ctx_stream(m.subs[i]);
         for (int j = 0; j < k; ++j)
             if (j != i && hipStreamWaitEvent(st, m.ev_done[j], 0) != hipSuccess) return ESC_E_HIP;
+        for (int j = 0; j < k; ++j) src[j] = words[j] + off[i];
         hipError_t e;
         if constexpr (sizeof(T) == 8) e = launch_peer_sum64(reinterpret_cast<const int64_t* const*>(src.data()), k,
                                                              reinterpret_cast<int64_t*>(tmp[i]), n, st);
@@ -126,34 +131,36 @@ int32_t peer_exchange(esc_ctx* c, const std::vector<T*>& words, int64_t n, std::
         for (int j = 0; j < n_dst; ++j)
             if (j != i && hipStreamWaitEvent(st, m.ev_read[j], 0) != hipSuccess) return ESC_E_HIP;
         if (i < n_dst && n > 0 &&
-            hipMemcpyAsync(words[i], tmp[i], (size_t)n * sizeof(T), hipMemcpyDeviceToDevice, st) != hipSuccess)
+            hipMemcpyAsync(words[i] + off[i], tmp[i], (size_t)n * sizeof(T), hipMemcpyDeviceToDevice, st) != hipSuccess)
             return ESC_E_HIP;
     }
     return ESC_OK;
 }
 
-// SUM of every device's exchange words (pods' and node words, esc_exchange_buffers).
+// Every device's slice of the SUM of the devices' pod words (esc_exchange_buffers, owner-
+// major rows): a reduce-scatter, each device receiving the rows of the groups it owns.
 int32_t exchange_words(esc_ctx* c) {
     esc_multi_state& m = M(c);
     const int k = nsub(c);
     std::vector<int64_t*> buf(k);
+    std::vector<int64_t> off(k);
     int64_t n = 0;
     for (int i = 0; i < k; ++i) {
         void* b = nullptr;
         int64_t cnt = 0;
         if (int32_t rc = esc_exchange_buffers(m.subs[i], &b, &cnt, nullptr, nullptr)) return rc;
+        if (int32_t rc = esc_exchange_slice(m.subs[i], &off[i], &n)) return rc;
         buf[i] = reinterpret_cast<int64_t*>(b);
-        n = cnt;
     }
-    if (m.comms.empty()) return peer_exchange<int64_t>(c, buf, n, m.psum, m.psum_n, true);
+    if (m.comms.empty()) return peer_exchange<int64_t>(c, buf, off, n, m.psum, m.psum_n, true);
     const RcclApi& r = rccl();
     ncclResult_t e = r.group_start();
     for (int i = 0; i < k && e == ncclSuccess; ++i) {
         hipSetDevice(m.devices[i]);
-        e = r.all_reduce(buf[i], buf[i], (size_t)n, ncclInt64, ncclSum, m.comms[i], ctx_stream(m.subs[i]));
+        e = r.reduce_scatter(buf[i], buf[i] + off[i], (size_t)n, ncclInt64, ncclSum, m.comms[i], ctx_stream(m.subs[i]));
     }
     const ncclResult_t e2 = r.group_end();
-    if (e != ncclSuccess) return fail_comm("ncclAllReduce", r.error_string(e));
+    if (e != ncclSuccess) return fail_comm("ncclReduceScatter", r.error_string(e));
     if (e2 != ncclSuccess) return fail_comm("ncclGroupEnd", r.error_string(e2));
     return ESC_OK;
 }
@@ -286,9 +293,41 @@ int32_t multi_sync(esc_ctx* c) {
     return seq(c, [&](int i) { return esc_sync(M(c).subs[i]); });
 }
 
+// Every group's records from the device that owns it (each device decided its own groups).
 int32_t multi_results(esc_ctx* c, esc_group_totals* t, esc_group_decision* d) {
     if (int32_t rc = multi_sync(c)) return rc;
-    return esc_results(M(c).subs[0], t, d);                  // every device decided alike
+    const int k = nsub(c);
+    if (k == 1) return esc_results(M(c).subs[0], t, d);
+    const int32_t G = esc_ctx_num_groups(M(c).subs[0]);
+    std::vector<esc_group_totals> tt((size_t)G);
+    std::vector<esc_group_decision> dd((size_t)G);
+    for (int i = 0; i < k; ++i) {
+        if (int32_t rc = esc_results(M(c).subs[i], t ? tt.data() : nullptr, d ? dd.data() : nullptr)) return rc;
+        for (int32_t g = 0; g < G; ++g) {
+            int32_t owner = 0;
+            if (int32_t rc = esc_group_owner(M(c).subs[i], g, &owner)) return rc;
+            if (owner != i) continue;
+            if (t) t[g] = tt[(size_t)g];
+            if (d) d[g] = dd[(size_t)g];
+        }
+    }
+    return ESC_OK;
+}
+
+int32_t multi_metrics_results(esc_ctx* c, esc_group_metrics* out) {
+    const int k = nsub(c);
+    if (k == 1) return esc_metrics_results(M(c).subs[0], out);
+    const int32_t G = esc_ctx_num_groups(M(c).subs[0]);
+    std::vector<esc_group_metrics> mm((size_t)G);
+    for (int i = 0; i < k; ++i) {
+        if (int32_t rc = esc_metrics_results(M(c).subs[i], mm.data())) return rc;
+        for (int32_t g = 0; g < G; ++g) {
+            int32_t owner = 0;
+            if (int32_t rc = esc_group_owner(M(c).subs[i], g, &owner)) return rc;
+            if (owner == i) out[g] = mm[(size_t)g];
+        }
+    }
+    return ESC_OK;
 }
 
 int32_t multi_k1_calibrate(esc_ctx* c, int32_t rounds) {
@@ -449,7 +488,9 @@ int32_t multi_try_remove(esc_ctx* c, int64_t now_ns, const int64_t* soft, const 
         buf[i] = reinterpret_cast<uint32_t*>(b);
     }
     if (m.comms.empty()) {
-        if (int32_t rc = peer_exchange<uint32_t>(c, buf, n, m.psum32, m.psum32_n, false)) return rc;
+        if (int32_t rc = peer_exchange<uint32_t>(c, buf, std::vector<int64_t>((size_t)k, 0), n, m.psum32, m.psum32_n,
+                                                 false))
+            return rc;
     } else {
         const RcclApi& r = rccl();
         ncclResult_t e = r.group_start();

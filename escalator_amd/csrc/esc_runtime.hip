@@ -25,6 +25,10 @@
 #include "esc_kernels.h"
 #include "esc_multi.h"
 
+#ifndef ESC_MEASURE
+#define ESC_MEASURE 0   // 1: the measurement library (Makefile ABLATIONS=1) reads its knobs
+#endif
+
 using namespace esc;
 
 namespace {
@@ -32,7 +36,7 @@ namespace {
 constexpr int LDS_BYTES = 160 * 1024;
 constexpr int POD_WINDOW_MAX = LDS_BYTES / 16;      // groups whose pod partials fit in LDS
 static_assert(POD_WINDOW_MAX % 2 == 0 && FC_COL % 2 == 0, "K1's 16-B partial-row stores need even window starts");
-constexpr int MAX_STAGES = 8;
+constexpr int MAX_STAGES = 10;
 
 #define HIP_TRY(x)                                              \
     do {                                                        \
@@ -114,13 +118,14 @@ const RcclApi& rccl() {
         sym(a.init_rank, "ncclCommInitRank");
         sym(a.init_all, "ncclCommInitAll");
         sym(a.all_reduce, "ncclAllReduce");
+        sym(a.reduce_scatter, "ncclReduceScatter");
         sym(a.group_start, "ncclGroupStart");
         sym(a.group_end, "ncclGroupEnd");
         sym(a.count, "ncclCommCount");
         sym(a.destroy, "ncclCommDestroy");
         sym(a.error_string, "ncclGetErrorString");
-        a.ok = a.get_unique_id && a.init_rank && a.init_all && a.all_reduce && a.group_start && a.group_end && a.count &&
-               a.destroy && a.error_string;
+        a.ok = a.get_unique_id && a.init_rank && a.init_all && a.all_reduce && a.reduce_scatter && a.group_start &&
+               a.group_end && a.count && a.destroy && a.error_string;
         return a;
     }();
     return api;
@@ -189,9 +194,16 @@ struct esc_ctx {
     int k1_cap = 0;                                           // K1 chunks per workgroup at most (0: static)
     uint64_t* d_k1_trace = nullptr;                           // K1 per-workgroup timestamps (esc_k1_trace)
     int64_t* d_trk_acc = nullptr;                             // [G][TA_K] dry-mode tracked sums
-    int64_t* d_pwords = nullptr;                              // active exchange buffer [G][PW_K] + [G][NX_K]
+    int64_t* d_pwords = nullptr;                              // active exchange buffer [world * own_cap][PW_K]
     int64_t* own_pwords = nullptr;                            // the context-owned one
-    int64_t* d_nwords = nullptr;                              // [G][NW_K] rank-local node words
+    int64_t* d_nwords = nullptr;                              // [G][NW_K] node words (exact for owned groups)
+    // Owner-major exchange rows: group g's pod words at row h_xs[g] = owner *
+    // own_cap + its index among the owner's groups, so one ncclReduceScatter hands every
+    // owner the exact sums of its own groups; h_own = this rank's groups (ascending).
+    int32_t own_cap = 0, own_first = 0;
+    bool own_seq = true;                                      // h_own is own_first + i
+    std::vector<uint32_t> h_own, h_xs;
+    uint32_t *d_own = nullptr, *d_xs = nullptr;
     esc_group_decision* d_dec = nullptr;                     // full records (device)
     DecCompact* d_cdec = nullptr;                             // compact records (device; no zero-copy)
     DecCompact* h_cdec = nullptr;                             // compact records (pinned host)
@@ -203,6 +215,11 @@ struct esc_ctx {
     int64_t* bound_pwords = nullptr;                          // caller-bound exchange buffer
     void* comm = nullptr;                                     // RCCL communicator (esc_comm_init)
     bool work_ready = false;
+    // An informer-event batch that failed after its first write (a HIP error mid-apply)
+    // leaves host mirrors and device arrays half-updated: decisions and reaping are refused
+    // (ESC_E_STATE) until the snapshot is reloaded (STALE_PODS: esc_load_pods, STALE_NODES:
+    // esc_load_nodes).  ADVICE r4.
+    uint32_t stale = 0;
     bool force_wide = false;
     int k1_variant = 0;                                       // ESC_K1_VARIANT (measurement knob)
     // K pods of a class are laid out in order of pair0 / pod_sort (0: input order), so that a
@@ -240,14 +257,7 @@ struct esc_ctx {
     std::vector<uint32_t> h_gch_off;                          // group -> its split chunks (big groups)
     int64_t n_gpad = 0;                                       // padded group-order length
     OrdChunk* d_chunks = nullptr;
-    int64_t n_chunks = 0, max_chunk = 0;
-    bool order_fused = false;                                 // single-pass K5 (ESC_ORDER_FUSED=1), DESIGN.md §4
-    bool fused_fits = true;                                   // every group's run < 2^27 (look-back words)
-    bool fused_ran = false;                                   // layout of the last esc_sort_nodes
-    int order_ablate = 0;                                     // ESC_ORDER_ABLATE (timing-only knob)
-    int64_t ord_chunk = ORD_CHUNK;                            // memberships per K5 chunk (ESC_ORDER_CHUNK)
-    unsigned long long *d_oticket = nullptr, *d_ostat = nullptr;   // fused: chunk tickets, look-back words
-    uint32_t* d_oerr = nullptr;
+    int64_t n_chunks = 0;
     uint64_t sort_div = 1;
     int sort_R = 1;
     bool sorted = false;
@@ -383,10 +393,13 @@ int pod_class_id(uint32_t f, uint32_t cpu0, int64_t mem0, uint32_t pair0, const 
 // rounded up to whole K3 columns.
 int64_t slot_stride(const esc_ctx* c) { return ((int64_t)c->gi.n_gp + 1 + FC_COL - 1) / FC_COL * FC_COL; }
 
-// The exchange buffer (SUM across ranks): the pods' words [G][PW_K], then the node words
-// [G][NX_K].
-constexpr int XW_K = PW_K + NX_K;
-int64_t* node_xwords(const esc_ctx* c) { return c->d_pwords + (int64_t)c->gi.G * PW_K; }
+// The exchange buffer (SUM across ranks, reduce-scattered to the owners): the pods' words
+// in owner-major rows, [world][own_cap][PW_K].
+int64_t xw_count(const esc_ctx* c) { return (int64_t)c->world * c->own_cap * PW_K; }
+int64_t* own_xwords(const esc_ctx* c) { return c->d_pwords + (int64_t)c->rank * c->own_cap * PW_K; }
+GroupList own_list(const esc_ctx* c) {
+    return GroupList{c->own_seq ? nullptr : c->d_own, (int32_t)c->h_own.size(), c->own_first};
+}
 
 GroupDev group_dev(const esc_ctx* c) {
     GroupDev g;
@@ -396,6 +409,7 @@ GroupDev group_dev(const esc_ctx* c) {
     g.node_code = c->d_node_code;
     g.code_list = c->d_code_list;
     g.gslot = c->d_gslot;
+    g.xs = c->world > 1 ? c->d_xs : nullptr;
     g.metrics = c->want_metrics ? c->d_metrics : nullptr;
     g.n_gp = c->gi.n_gp;
     g.sp = slot_stride(c);
@@ -462,7 +476,7 @@ void drop_graphs(esc_ctx* c) {
 int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out);
 
 // K5 per-decision ordering (classify + stable split of every group's age-ordered
-// memberships) on stream st; the two-pass kernels (the fused one needs its ticket reset).
+// memberships) on stream st: the two-pass kernels and the packed small / mid-size groups.
 hipError_t enqueue_order(esc_ctx* c, hipStream_t st) {
     const hipError_t e = launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb,
                                       c->d_g_grp, c->n_memb, c->gi.G, c->d_ccnt, c->d_cbase,
@@ -502,6 +516,7 @@ void release_work(esc_ctx* c) {
     dfree(c->d_touch); dfree(c->d_wg_cols); dfree(c->d_wg_off); dfree(c->d_col_rows);
     c->touch_on = false;
     dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_cdec); dfree(c->d_metrics);
+    dfree(c->d_own); dfree(c->d_xs);
     c->d_pwords = nullptr;
     if (c->h_cdec) hipHostFree(c->h_cdec);
     c->h_cdec = nullptr;
@@ -528,7 +543,6 @@ void release_sort(esc_ctx* c) {
     c->age_built = false;
     dfree(c->d_g_memb); dfree(c->d_g_grp);
     dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks);
-    dfree(c->d_oticket); dfree(c->d_ostat); dfree(c->d_oerr);
     dfree(c->d_pstart); dfree(c->d_plen); dfree(c->d_ord); dfree(c->d_pchunks);
     c->n_pchunks = 0;
     c->n_chunks = 0;
@@ -630,8 +644,8 @@ int32_t build_age_index(esc_ctx* c) {
         if ((int64_t)pstart[q] + reg >= (int64_t)0xFFFFFFFF) return ESC_E_LIMIT;
         pstart[q + 1] = pstart[q] + (uint32_t)reg;
     }
-    // chunks: a group whose region exceeds ORD_CHUNK is split (two-pass or fused kernels,
-    // chunk prefix across the group); smaller groups are packed whole, several per chunk,
+    // chunks: a group whose region exceeds ORD_CHUNK is split (two-pass kernels, chunk
+    // prefix across the group); smaller groups are packed whole, several per chunk,
     // and ordered in one pass (k_ord_packed)
     std::vector<OrdChunk> chunks, pchunks, pbig;
     uint32_t pk_lo = 0, pk_hi = 0, qk_lo = 0, qk_hi = 0;
@@ -651,8 +665,8 @@ int32_t build_age_index(esc_ctx* c) {
             flush_small();
             flush_mid();
             pk_lo = pk_hi = qk_lo = qk_hi = pstart[q + 1];
-            for (int64_t a = 0; a < reg; a += c->ord_chunk)
-                chunks.push_back({pstart[q] + (uint32_t)a, pstart[q] + (uint32_t)std::min<int64_t>(reg, a + c->ord_chunk),
+            for (int64_t a = 0; a < reg; a += ORD_CHUNK)
+                chunks.push_back({pstart[q] + (uint32_t)a, pstart[q] + (uint32_t)std::min<int64_t>(reg, a + ORD_CHUNK),
                                   (uint32_t)q, c->params[q].dry ? ORD_CHUNK_DRY : 0u});
             continue;
         }
@@ -674,13 +688,6 @@ int32_t build_age_index(esc_ctx* c) {
     c->n_psmall = (int64_t)pchunks.size();
     pchunks.insert(pchunks.end(), pbig.begin(), pbig.end());
     gch_off[g.G] = (uint32_t)chunks.size();
-    c->fused_fits = true;
-    c->max_chunk = 0;
-    for (int32_t q = 0; q < g.G; ++q) {
-        if (pstart[q + 1] - pstart[q] >= (1u << 27)) c->fused_fits = false;
-        if (gch_off[q + 1] > gch_off[q])
-            c->max_chunk = std::max<int64_t>(c->max_chunk, std::min<int64_t>(pstart[q + 1] - pstart[q], c->ord_chunk));
-    }
     const int64_t npad = pstart[g.G];
     if (fresh || npad != c->n_gpad) {
         dfree(c->d_g_memb); dfree(c->d_g_grp); dfree(c->d_ord);
@@ -698,16 +705,7 @@ int32_t build_age_index(esc_ctx* c) {
         HIP_TRY(dalloc(&c->d_chunks, std::max<size_t>(chunks.size(), 1)));
         HIP_TRY(dalloc(&c->d_pchunks, std::max<size_t>(pchunks.size(), 1)));
         HIP_TRY(dalloc(&c->d_pstart, pstart.size())); HIP_TRY(dalloc(&c->d_plen, plen.size()));
-        dfree(c->d_oticket); dfree(c->d_ostat); dfree(c->d_oerr);
-        HIP_TRY(dalloc(&c->d_oticket, 1)); HIP_TRY(dalloc(&c->d_ostat, std::max<size_t>(chunks.size(), 1)));
-        HIP_TRY(dalloc(&c->d_oerr, 1));
     }
-    // fused ordering: tickets restart at 0 (a decision consumes exactly n_chunks), status
-    // words at epoch 0 / not ready; groups without memberships get their (empty) segment
-    // bounds here, the others from their last chunk every decision
-    HIP_TRY(hipMemsetAsync(c->d_oticket, 0, 8, st));
-    HIP_TRY(hipMemsetAsync(c->d_ostat, 0, std::max<size_t>(chunks.size(), 1) * 8, st));
-    HIP_TRY(hipMemsetAsync(c->d_oerr, 0, 4, st));
 
     c->n_chunks = (int64_t)chunks.size();
     c->n_pchunks = (int64_t)pchunks.size();
@@ -980,6 +978,26 @@ bool touch_mark_c(esc_ctx* c, int64_t d, uint32_t f, uint32_t pair0, const uint3
     return grew;
 }
 
+// The rank owning group g's node side: the one whose pair range holds the group's pair
+// (q_bounds from esc_load_nodes).
+int32_t group_owner_rank(const esc_ctx* c, int32_t g) {
+    if (c->world <= 1 || c->q_bounds.size() < 2) return 0;
+    const uint32_t q = c->gi.gpair[(size_t)g];
+    return (int32_t)(std::upper_bound(c->q_bounds.begin(), c->q_bounds.end() - 1, q) - c->q_bounds.begin()) - 1;
+}
+
+constexpr uint32_t STALE_PODS = 1, STALE_NODES = 2;
+
+// The apply phase of an event batch (its checks passed): on failure the context is marked
+// stale (esc_ctx::stale) until the matching reload.
+template <class F>
+int32_t guarded(esc_ctx* c, uint32_t bit, F&& apply) {
+    const uint32_t was = c->stale;
+    const int32_t rc = apply();
+    c->stale = rc == ESC_OK ? was : (was | bit);
+    return rc;
+}
+
 // Grid geometry for the current snapshot.
 int32_t ensure_work(esc_ctx* c) {
     if (c->work_ready) return ESC_OK;
@@ -1001,13 +1019,10 @@ int32_t ensure_work(esc_ctx* c) {
         return cap * ((c->k_weight + nch - 1) / nch / K_TILE_WEIGHT_MIN + c->n_cls + 1) * TILE +
                ((c->c_tiles + b - 1) / b) * CTILE;
     };
-    // the static share (cap K1_CHUNKS) sets the grid; dynamic shares then take the largest
-    // cap up to K1_CHUNK_CAP that keeps the bound (K1_CHUNKS = one static share: always)
+    // the static share (cap K1_CHUNKS: one share) sets the grid
     cap = K1_CHUNKS;
     while (block_pods(nblk) > PODS_PER_BLOCK_MAX) nblk *= 2;
-    cap = K1_CHUNK_CAP;
-    while (cap > K1_CHUNKS && block_pods(nblk) > PODS_PER_BLOCK_MAX) --cap;
-    c->k1_cap = k1_dynamic(c->k1_variant) ? (int)cap : 0;
+    c->k1_cap = 0;
     nblk = std::min<int64_t>(nblk, std::max(c->k_tiles, c->c_tiles));
     std::vector<int64_t> plan;
     for (;;) {            // the plan's own per-workgroup pod counts must keep the LDS words exact
@@ -1032,8 +1047,28 @@ int32_t ensure_work(esc_ctx* c) {
     HIP_TRY(hipMemset(c->d_wide_pod, 0, (size_t)S * WP_K * sizeof(int64_t)));
     HIP_TRY(dalloc(&c->d_trk_acc, (size_t)G * TA_K));
     HIP_TRY(hipMemset(c->d_trk_acc, 0, (size_t)G * TA_K * sizeof(int64_t)));
-    HIP_TRY(dalloc(&c->own_pwords, (size_t)G * XW_K));
+    {   // owner-major exchange rows: every rank derives the same split
+        std::vector<std::vector<uint32_t>> lists((size_t)c->world);
+        for (int32_t g = 0; g < G; ++g) lists[(size_t)group_owner_rank(c, g)].push_back((uint32_t)g);
+        size_t cap = 1;
+        for (const auto& l : lists) cap = std::max(cap, l.size());
+        c->own_cap = (int32_t)cap;
+        c->h_xs.assign((size_t)G, 0);
+        for (int32_t r = 0; r < c->world; ++r)
+            for (size_t i = 0; i < lists[(size_t)r].size(); ++i) c->h_xs[lists[(size_t)r][i]] = (uint32_t)(r * cap + i);
+        c->h_own = lists[(size_t)c->rank];
+        c->own_first = c->h_own.empty() ? 0 : (int32_t)c->h_own[0];
+        c->own_seq = true;
+        for (size_t i = 0; i < c->h_own.size(); ++i) c->own_seq &= c->h_own[i] == (uint32_t)c->own_first + i;
+        HIP_TRY(dalloc(&c->d_xs, (size_t)G));
+        HIP_TRY(dalloc(&c->d_own, std::max<size_t>(c->h_own.size(), 1)));
+        HIP_TRY(hipMemcpy(c->d_xs, c->h_xs.data(), (size_t)G * 4, hipMemcpyHostToDevice));
+        if (!c->h_own.empty()) HIP_TRY(hipMemcpy(c->d_own, c->h_own.data(), c->h_own.size() * 4, hipMemcpyHostToDevice));
+    }
+    HIP_TRY(dalloc(&c->own_pwords, (size_t)xw_count(c)));
+    HIP_TRY(hipMemset(c->own_pwords, 0, (size_t)xw_count(c) * 8));
     HIP_TRY(dalloc(&c->d_nwords, (size_t)G * NW_K));
+    HIP_TRY(hipMemset(c->d_nwords, 0, (size_t)G * NW_K * 8));
     c->d_pwords = c->bound_pwords ? c->bound_pwords : c->own_pwords;
     HIP_TRY(dalloc(&c->d_dec, (size_t)G));
     HIP_TRY(dalloc(&c->d_metrics, (size_t)G));
@@ -1065,6 +1100,15 @@ int32_t ensure_work(esc_ctx* c) {
 // and a cross-stream join cost ~10 us per step.  With timing on each
 // stage has its own events.  Decisions go straight to pinned host memory (zero-copy)
 // unless disabled, in which case a copy follows.
+// Timing mode: one more stage boundary on the context's stream (esc_exchange and esc_decide
+// append theirs to enqueue_step's, so a sharded step reads K1 / tail / orderings / node
+// groups / exchange / decide).
+int32_t stage_mark(esc_ctx* c) {
+    if (!c->timing || c->n_stage_ev >= MAX_STAGES - 1) return ESC_OK;
+    HIP_TRY(hipEventRecord(c->ev[c->n_stage_ev++], c->stream));
+    return ESC_OK;
+}
+
 int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     const GroupDev g = group_dev(c);
     const NodeDev n = node_dev(c);
@@ -1113,11 +1157,12 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
                                     c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, st));
     }
     if (int32_t rc = mark()) return rc;
-    // D reads and resets the tracker sums the tail accumulated (once per step); a sharded
-    // step (no decide) computes the node words only and esc_decide runs K4 after the exchange
-    NGDecide nd{nullptr, nullptr, nullptr, node_xwords(c)};
-    if (decide) nd = NGDecide{c->d_pwords, c->d_dec, cdec, nullptr};
-    HIP_TRY(launch_node_groups(g, n, c->nodes.rows, c->d_trk_acc, c->d_nwords, nd, st));
+    // D reads and resets the tracker sums the tail accumulated (once per step), for this
+    // rank's own groups; a sharded step (no decide) computes their node words only and
+    // esc_decide runs K4 on them after the exchange
+    NGDecide nd{nullptr, nullptr, nullptr};
+    if (decide) nd = NGDecide{c->d_pwords, c->d_dec, cdec};
+    HIP_TRY(launch_node_groups(g, n, own_list(c), c->nodes.rows, c->d_trk_acc, c->d_nwords, nd, st));
     if (int32_t rc = mark()) return rc;
     if (copy_out && !c->zero_copy) {
         HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)g.G * sizeof(DecCompact), hipMemcpyDeviceToHost, st));
@@ -1130,7 +1175,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
 int32_t check_ready(esc_ctx* c) {
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
-    if (!c->pods_loaded || !c->nodes_loaded) return ESC_E_STATE;
+    if (!c->pods_loaded || !c->nodes_loaded || c->stale) return ESC_E_STATE;
     hipSetDevice(c->device);          // a multi-device host drives several contexts from one thread
     return ensure_work(c);
 }
@@ -1165,6 +1210,7 @@ const char* esc_status_string(int32_t status) {
         case ESC_ST_ERR_NEG_DELTA: return "negative scale up delta";
         case ESC_ST_ERR_OVERFLOW: return "int64 overflow (Quantity inf.Dec regime, not emulated)";
         case ESC_ST_ERR_TAINT_MIN: return "the number of nodes is less than specified minimum. Taking no action";
+        case ESC_ST_NOT_OWNED: return "decided on the group's owner rank";
         default: return "unknown status";
     }
 }
@@ -1184,21 +1230,14 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     if (!c) return ESC_E_NOMEM;
     c->rank = rank;
     c->world = world;
+#if ESC_MEASURE
+    // measurement knobs: read by the measurement library only (Makefile ABLATIONS=1,
+    // libescalator_hip_measure.so); the product library's results depend on its inputs alone
     if (const char* v = std::getenv("ESC_K1_VARIANT")) c->k1_variant = std::atoi(v);
     if (const char* v = std::getenv("ESC_POD_SORT")) c->pod_sort = (uint32_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("ESC_K1_FULL_FLUSH")) c->full_flush = std::atoi(v) != 0;
-    if (const char* v = std::getenv("ESC_ORDER_FUSED")) {
-        c->order_fused = std::atoi(v) != 0;
-        if (c->order_fused) c->ord_chunk = 8192;               // its best chunk on config 5
-    }
-    if (const char* v = std::getenv("ESC_ORDER_ABLATE")) c->order_ablate = std::atoi(v);
     if (const char* v = std::getenv("ESC_K3_ABLATE")) c->k3_ablate = std::atoi(v);
-
-    if (const char* v = std::getenv("ESC_ORDER_CHUNK")) {      // 4096 / 8192 / 16384 (measurement knob)
-        const int64_t k = std::atoll(v);
-        if (k == 4096 || k == 8192 || k == 16384) c->ord_chunk = k;
-    }
-    if (!c->order_fused) c->ord_chunk = ORD_CHUNK;             // k_ord_scatter stages one ORD_CHUNK in LDS
+#endif
     c->gi.build(groups, n_groups);
     c->params.resize(n_groups);
     for (int32_t g = 0; g < n_groups; ++g) params_from(c->params[g], groups[g], nullptr);
@@ -1226,7 +1265,9 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     for (int i = 0; i < 2; ++i)
         if (hipEventCreate(&c->k1t_ev[i]) != hipSuccess) return fail(ESC_E_HIP);
 
+#if ESC_MEASURE
     if (const char* v = std::getenv("ESC_NO_ZEROCOPY")) c->zero_copy = std::atoi(v) == 0;
+#endif
     const size_t G = (size_t)n_groups;
     if (dalloc(&c->d_dry, G) || dalloc(&c->d_params, G)) return fail(ESC_E_NOMEM);
     const GroupIndex& gi = c->gi;
@@ -1568,10 +1609,6 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
         HIP_TRY(dalloc(&b.pair0, npad)); HIP_TRY(dalloc(&b.xc_cpu, nxc_dev)); HIP_TRY(dalloc(&b.xc_mem, nxc_dev));
         HIP_TRY(dalloc(&b.xp, nxp_dev)); HIP_TRY(dalloc(&b.xc_base, c_tiles + 1)); HIP_TRY(dalloc(&b.xp_base, c_tiles + 1));
         HIP_TRY(dalloc(&b.big, big.size())); HIP_TRY(dalloc(&b.cls, n_cls));
-        if (std::getenv("ESC_DEBUG_PTRS"))
-            fprintf(stderr, "[esc] replica %d flags %p cpu0 %p pair0 %p mem0 %p xc_cpu %p xc_mem %p xp %p\n", r,
-                    (void*)b.flags, (void*)b.cpu0, (void*)b.pair0, (void*)b.mem0, (void*)b.xc_cpu, (void*)b.xc_mem,
-                    (void*)b.xp);
         const hipMemcpyKind kind = r == 0 ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
         const PodBuf& a = c->pods[0];
         auto src = [&](const void* host, const void* dev) { return r == 0 ? host : dev; };
@@ -1633,6 +1670,7 @@ int32_t esc_load_pods(esc_ctx* c, const esc_pod_soa* p, int64_t global_offset) {
     c->pod_offset = global_offset;
     c->cur = 0;
     c->pods_loaded = true;
+    c->stale &= ~STALE_PODS;                          // a failed pod event's half-writes are gone
     return ESC_OK;
 }
 
@@ -1906,6 +1944,7 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     c->ts_max = tmax;
     c->h_created.assign(s->created_ns + lo, s->created_ns + hi);
     c->nodes_loaded = true;
+    c->stale &= ~STALE_NODES;
     return build_age_index(c);
 }
 
@@ -1945,7 +1984,7 @@ int32_t esc_set_metrics(esc_ctx* c, int32_t enable) {
 }
 
 int32_t esc_metrics_results(esc_ctx* c, esc_group_metrics* out) {
-    if (c && c->multi) return esc_metrics_results(esc::multi_sub(c, 0), out);
+    if (c && c->multi) return esc::multi_metrics_results(c, out);
     if (!c || !out) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->work_ready || !c->want_metrics) return ESC_E_STATE;
@@ -2098,12 +2137,16 @@ int32_t esc_k1_time(esc_ctx* c, int32_t reps, double* ms_per_launch) {
     const int32_t S = (int32_t)pod_slots(c);
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipEventRecord(c->k1t_ev[0], st));
-    for (int32_t k = 0; k < reps; ++k)
+    // every K1 launch of a step (its LDS windows and the big C tiles, so the pod bytes the
+    // roofline divides are all timed); no trace, so esc_k1_trace keeps the last decision's
+    for (int32_t k = 0; k < reps; ++k) {
         for (int32_t g0 = 0; g0 < S; g0 += POD_WINDOW_MAX) {
-            const K1Diag diag{c->d_k1_trace};
+            const K1Diag diag{nullptr};
             HIP_TRY(launch_pod_reduce(p, g, g0, std::min(POD_WINDOW_MAX, S - g0), c->nblk, c->k1_variant, c->d_pod_part,
                                       c->d_wide_pod, c->d_k1_ticket, c->k1_cap, diag, st));
         }
+        HIP_TRY(launch_pod_bigtiles(p, g, c->pods[c->cur].big, c->n_big, c->d_wide_pod, st));
+    }
     HIP_TRY(hipEventRecord(c->k1t_ev[1], st));
     // the exact-path accumulators K1 added to without a fold: back to zero for the next step
     HIP_TRY(hipMemsetAsync(c->d_wide_pod, 0, (size_t)pod_slots(c) * WP_K * sizeof(int64_t), st));
@@ -2122,7 +2165,6 @@ int32_t esc_reduce(esc_ctx* c) {
     const int r = c->cur;
     c->cur = (c->cur + 1) % (int)c->pods.size();
     c->pending = true;
-    c->fused_ran = false;
     if (c->order_in_step) { c->order_src = 0; c->sorted = true; }
     if (!c->use_graph || c->timing) return enqueue_step(c, r, false, false);
     return replay_step(c, c->rgraphs, r, false);
@@ -2133,11 +2175,38 @@ int32_t esc_exchange_buffers(esc_ctx* c, void** sum_buf, int64_t* sum_count, voi
     int32_t rc = check_ready(c);
     if (rc) return rc;
     if (sum_buf) *sum_buf = c->d_pwords;
-    if (sum_count) *sum_count = (int64_t)c->gi.G * XW_K;
+    if (sum_count) *sum_count = xw_count(c);
     // allNodes[0] is resolved from the whole node table every rank holds, so the
     // first-member words need no MIN exchange in this build
     if (min_buf) *min_buf = nullptr;
     if (min_count) *min_count = 0;
+    return ESC_OK;
+}
+
+int32_t esc_exchange_slice(const esc_ctx* c, int64_t* offset, int64_t* count) {
+    if (c && c->multi) return ESC_E_STATE;
+    if (!c || !offset || !count) return ESC_E_INVAL;
+    if (!c->work_ready) return ESC_E_STATE;
+    *offset = (int64_t)c->rank * c->own_cap * PW_K;
+    *count = (int64_t)c->own_cap * PW_K;
+    return ESC_OK;
+}
+
+int32_t esc_exchange_rows(const esc_ctx* c, const esc_node_soa* s, int32_t world, uint32_t* rows, int32_t* own_rows) {
+    if (!c || !s || !rows || !own_rows || world < 1) return ESC_E_INVAL;
+    const int32_t G = c->gi.G;
+    std::vector<uint32_t> qb((size_t)world + 1);
+    if (int32_t rc = esc_node_owner_ranges(c, s, world, qb.data())) return rc;
+    std::vector<int32_t> n((size_t)world, 0), owner((size_t)G);
+    for (int32_t g = 0; g < G; ++g) {
+        const uint32_t q = c->gi.gpair[(size_t)g];
+        owner[(size_t)g] = world == 1 ? 0 : (int32_t)(std::upper_bound(qb.begin(), qb.end() - 1, q) - qb.begin()) - 1;
+        ++n[(size_t)owner[(size_t)g]];
+    }
+    const int32_t cap = std::max(1, *std::max_element(n.begin(), n.end()));
+    std::fill(n.begin(), n.end(), 0);
+    for (int32_t g = 0; g < G; ++g) rows[g] = (uint32_t)(owner[(size_t)g] * cap + n[(size_t)owner[(size_t)g]]++);
+    *own_rows = cap;
     return ESC_OK;
 }
 
@@ -2160,7 +2229,7 @@ int32_t esc_exchange_download(esc_ctx* c, int64_t* sum_out, int64_t* min_out) {
     (void)min_out;                                   // min_count is 0: nothing to MIN-exchange
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(sum_out, c->d_pwords, (size_t)c->gi.G * XW_K * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(sum_out, c->d_pwords, (size_t)xw_count(c) * 8, hipMemcpyDeviceToHost));
     return ESC_OK;
 }
 
@@ -2172,7 +2241,7 @@ int32_t esc_exchange_upload(esc_ctx* c, const int64_t* sum_in, const int64_t* mi
     (void)min_in;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(c->d_pwords, sum_in, (size_t)c->gi.G * XW_K * 8, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->d_pwords, sum_in, (size_t)xw_count(c) * 8, hipMemcpyHostToDevice));
     return ESC_OK;
 }
 
@@ -2181,12 +2250,13 @@ int32_t esc_decide(esc_ctx* c) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
     hipSetDevice(c->device);
-    // K4 over the exchanged pod and node words
-    HIP_TRY(launch_decide(group_dev(c), node_dev(c), c->d_pwords, node_xwords(c), c->d_nwords, c->d_dec,
+    // K4 over this rank's own groups: its slice of the exchanged pod words, its node words
+    HIP_TRY(launch_decide(group_dev(c), node_dev(c), own_list(c), own_xwords(c), c->d_nwords, c->d_dec,
                           c->zero_copy ? c->h_cdec_dev : c->d_cdec, c->stream));
     if (!c->zero_copy)
         HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)c->gi.G * sizeof(DecCompact), hipMemcpyDeviceToHost,
                                c->stream));
+    if (int32_t rc = stage_mark(c)) return rc;
     c->pending = true;
     return ESC_OK;
 }
@@ -2202,7 +2272,6 @@ int32_t esc_run(esc_ctx* c) {
     c->cur = (c->cur + 1) % nrep;
     c->pending = true;
     (void)nrep;
-    c->fused_ran = false;
     if (c->order_in_step) { c->order_src = 0; c->sorted = true; }
     if (!c->use_graph || c->timing) return enqueue_step(c, r, true, true);
     return replay_step(c, c->graphs, r, true);
@@ -2250,11 +2319,13 @@ int32_t esc_exchange(esc_ctx* c) {
     if (rc) return rc;
     if (!c->comm) return ESC_E_STATE;
     hipSetDevice(c->device);
-    // int64 SUM is exact in any order: the pod words are split lo32 / hi, the node words are
-    // non-zero on their owner rank only
-    const ncclResult_t r = rccl().all_reduce(c->d_pwords, c->d_pwords, (size_t)c->gi.G * XW_K, ncclInt64, ncclSum,
-                                             reinterpret_cast<ncclComm_t>(c->comm), c->stream);
-    if (r != ncclSuccess) return fail_comm("ncclAllReduce", rccl().error_string(r));
+    // int64 SUM is exact in any order (the pod words are split lo32 / hi): one in-place
+    // reduce-scatter leaves every owner the sums of its own groups' rows; the
+    // node words never travel (each owner computed its own)
+    const ncclResult_t r = rccl().reduce_scatter(c->d_pwords, own_xwords(c), (size_t)c->own_cap * PW_K, ncclInt64,
+                                                 ncclSum, reinterpret_cast<ncclComm_t>(c->comm), c->stream);
+    if (r != ncclSuccess) return fail_comm("ncclReduceScatter", rccl().error_string(r));
+    if (int32_t rc = stage_mark(c)) return rc;
     c->pending = true;
     return ESC_OK;
 }
@@ -2296,12 +2367,20 @@ int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* de
     int32_t rc = esc_sync(c);
     if (rc) return rc;
     const int32_t G = c->gi.G;
+    // With several ranks a rank decides its own groups only: the others'
+    // records come back zeroed, flagged ESC_TF_NOT_OWNED / ESC_ST_NOT_OWNED.
+    auto mine = [&](int32_t g) { return c->world == 1 || group_owner_rank(c, g) == c->rank; };
     if (decisions) {
         // the compact records -> esc_group_decision (cached capacity: allNodes[0]'s allocatable
         // when the group has nodes, else the state's, controller.go:207-211)
         for (int32_t g = 0; g < G; ++g) {
             const DecCompact& x = c->h_cdec[g];
             esc_group_decision& d = decisions[g];
+            if (!mine(g)) {
+                std::memset(&d, 0, sizeof d);
+                d.status = ESC_ST_NOT_OWNED;
+                continue;
+            }
             if (x.wide) {                                // delta / n_to_taint beyond int32
                 HIP_TRY(hipMemcpy(&d, c->d_dec + g, sizeof d, hipMemcpyDeviceToHost));
                 continue;
@@ -2320,11 +2399,17 @@ int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* de
         }
     }
     if (totals) {
-        std::vector<int64_t> w((size_t)G * PW_K), nw((size_t)G * NW_K);
+        std::vector<int64_t> w((size_t)xw_count(c)), nw((size_t)G * NW_K);
         HIP_TRY(hipMemcpy(w.data(), c->d_pwords, w.size() * 8, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(nw.data(), c->d_nwords, nw.size() * 8, hipMemcpyDeviceToHost));
         for (int32_t g = 0; g < G; ++g) {
-            const int64_t* x = &w[(size_t)g * PW_K];
+            if (!mine(g)) {
+                std::memset(&totals[g], 0, sizeof totals[g]);
+                totals[g].first_node = -1;
+                totals[g].flags = ESC_TF_NOT_OWNED;
+                continue;
+            }
+            const int64_t* x = &w[(size_t)(c->world > 1 ? c->h_xs[(size_t)g] : (uint32_t)g) * PW_K];
             const int64_t* y = &nw[(size_t)g * NW_K];
             esc_group_totals& t = totals[g];
             auto join = [&](int k, int64_t& out) {
@@ -2984,9 +3069,6 @@ int32_t upsert_plan(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p, Upsert
                 cslot[i] = c->c_free[k];
             }
         if (cslot[i] < 0) {                                // no room in place: reload
-            if (std::getenv("ESC_DEBUG_UPSERT"))
-                fprintf(stderr, "[esc] upsert %lld: no C room for flags %08x (class %d, free C slots %zu)\n",
-                        (long long)id, f, sid, c->c_free.size());
             return ESC_E_LIMIT;
         }
     }
@@ -3105,7 +3187,7 @@ int32_t esc_pods_upsert(esc_ctx* c, const int64_t* ids, const esc_pod_soa* p) {
     if (c && c->multi) return multi_pods_upsert(c, ids, p);
     UpsertPlan u;
     const int32_t rc = upsert_plan(c, ids, p, u);
-    return rc ? rc : upsert_apply(c, ids, p, u);
+    return rc ? rc : guarded(c, STALE_PODS, [&] { return upsert_apply(c, ids, p, u); });
 }
 
 int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
@@ -3115,6 +3197,7 @@ int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
     if (!c->pods_loaded) return ESC_E_STATE;
     for (int64_t i = 0; i < n; ++i)
         if (ids[i] < 0 || ids[i] >= (int64_t)c->pod_cls.size()) return ESC_E_INVAL;
+    return guarded(c, STALE_PODS, [&]() -> int32_t {
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     Patches P;
@@ -3136,6 +3219,7 @@ int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
     int32_t rc = apply_patches(c, P, pod_targets(c));
     if (rc || !c->placed) return rc;
     return sync_placement(c, touched, runs);
+    });
 }
 
 // Spec.NodeName of pods (the informer's pod Update once the scheduler binds a pod, or a
@@ -3145,6 +3229,7 @@ int32_t esc_pods_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
 int32_t esc_pods_bind(esc_ctx* c, const int64_t* ids, const uint32_t* pod_node, int64_t n) {
     if (c && c->multi) return multi_pods_bind(c, ids, pod_node, n);
     if (int32_t rc = bind_check(c, ids, pod_node, n)) return rc;
+    return guarded(c, STALE_PODS, [&]() -> int32_t {
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     if ((int64_t)c->h_pod_node.size() < (int64_t)c->pod_cls.size()) {
@@ -3162,6 +3247,7 @@ int32_t esc_pods_bind(esc_ctx* c, const int64_t* ids, const uint32_t* pod_node, 
     if (int32_t rc = sync_placement(c, touched, runs)) return rc;
     bound_of(c, ids, n, bpos, bnode);                // and join their new ones'
     return occ_delta(c, bpos, bnode, +1);
+    });
 }
 
 int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32_t* flags, const int64_t* cpu,
@@ -3431,6 +3517,17 @@ uint32_t entry_pair(const esc_ctx* c, uint32_t e) {
     return e < c->pair_end[q] ? q : NONE;
 }
 
+// Node j's own retired entry of pair q (an entry it left earlier and nobody took since),
+// or NONE: a relabel that brings j back to q reuses it instead of a spare entry, so label
+// churn (A -> B -> A ...) does not use up the pair's spare room.
+uint32_t retired_entry(const esc_ctx* c, int64_t j, uint32_t q) {
+    for (uint32_t k = c->ne_off[j]; k < c->ne_off[j + 1]; ++k) {
+        const uint32_t e = c->ne_pos[k];
+        if (c->h_e_node[e] == NONE && entry_pair(c, e) == q) return e;
+    }
+    return NONE;
+}
+
 int32_t relabel_plan(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, RelabelPlan& u) {
     if (!c || !s || s->n_nodes < 0 || (s->n_nodes > 0 && (!ids || !s->flags || !s->label0 || !s->cpu || !s->mem ||
                                                           !s->created_ns)))
@@ -3470,7 +3567,7 @@ int32_t relabel_plan(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, Rela
         group_pairs(n_gp, c->h_label0[j], nf_xlbl(c->h_nflags[j]), c->h_xl.data() + c->h_xl_off[j], oq);
         group_pairs(n_gp, s->label0[i], nx, s->xl_pair + sx, nq);
         for (uint32_t q : nq)
-            if (!std::binary_search(oq.begin(), oq.end(), q)) ++need_e[q];
+            if (!std::binary_search(oq.begin(), oq.end(), q) && retired_entry(c, j, q) == NONE) ++need_e[q];
         // K5 regions: memberships left / joined (all of them when the creation time moved)
         node_membs(c, j, u.old_m[i]);
         node_membs_from(c, s->label0[i], nx, s->xl_pair + sx, u.new_m[i]);
@@ -3530,7 +3627,8 @@ int32_t relabel_apply(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, con
     Patches P;
     std::vector<uint32_t> oq, nq, keep;
     std::vector<uint8_t> pair_touched(n_gp, 0);
-    std::vector<std::pair<int64_t, std::vector<uint32_t>>> regrow;   // nodes whose entry list grew
+    std::vector<std::pair<int64_t, std::vector<uint32_t>>> regrow;   // nodes whose entry list changed size
+    std::vector<uint32_t> reused;                                       // retired entries taken back
     for (int64_t i = 0; i < n; ++i) {
         const int64_t j = ids[i];
         const uint32_t f = s->flags[i], nx = nf_xlbl(f), onx = nf_xlbl(c->h_nflags[j]);
@@ -3552,7 +3650,15 @@ int32_t relabel_apply(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, con
             bool have = false;
             for (uint32_t e : keep) have |= entry_pair(c, e) == q;
             if (have) continue;
-            const uint32_t e = c->pair_next[q]++;                         // a spare entry of the pair
+            uint32_t e = NONE;                                            // j's own retired entry of q
+            for (uint32_t d : dead)
+                if (c->h_e_node[d] == NONE && entry_pair(c, d) == q) { e = d; break; }
+            if (e != NONE) {
+                dead.erase(std::remove(dead.begin(), dead.end(), e), dead.end());
+                reused.push_back(e);
+            } else {
+                e = c->pair_next[q]++;                                    // a spare entry of the pair
+            }
             c->h_e_node[e] = (uint32_t)j;
             P.add(NT_ENODE, e, (uint32_t)j);                               // flags / cpu / mem: patch_nodes
             keep.push_back(e);
@@ -3560,7 +3666,9 @@ int32_t relabel_apply(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, con
             pair_touched[q] = 1;
         }
         const uint32_t slots = c->ne_off[j + 1] - c->ne_off[j];
-        if (keep.size() <= slots) {
+        if (keep.size() < slots && dead.empty()) {
+            regrow.emplace_back(j, keep);           // no retired entry left to fill the spare slots
+        } else if (keep.size() <= slots) {
             // in place; the spare slots repeat a retired entry (there is one whenever a slot is
             // spare: patch_nodes skips it, its occupancy word is never read)
             for (uint32_t k = 0; k < slots; ++k)
@@ -3610,6 +3718,15 @@ int32_t relabel_apply(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, con
         c->ne_pos.swap(pos);
     }
     c->ne_dev_nodes = -1;                           // the device copy is re-sent before its next use
+    // a reused entry's occupancy words restart at zero (a retired entry repeated in a node's
+    // spare map slots may have collected counts nobody read); the +1 below re-adds its pods
+    if (c->placed)
+        for (uint32_t e : reused)
+            for (uint32_t* w : {c->d_occ, c->d_occ_local})
+                if (w) {
+                    HIP_TRY(hipMemsetAsync(w + e, 0, 4, c->stream));
+                    HIP_TRY(hipMemsetAsync(w + c->n_entries + e, 0, 4, c->stream));
+                }
     // allNodes[0] of the groups whose pair gained or lost a node
     for (int32_t g = 0; g < c->gi.G; ++g)
         if (pair_touched[c->gi.gpair[g]]) pair_first(c, c->gi.gpair[g], c->h_gnode[g]);
@@ -3643,7 +3760,7 @@ int32_t esc_nodes_relabel(esc_ctx* c, const int64_t* ids, const esc_node_soa* s)
     if (c && c->multi) return esc::multi_nodes_relabel(c, ids, s);
     RelabelPlan u;
     const int32_t rc = relabel_plan(c, ids, s, u);
-    return rc ? rc : relabel_apply(c, ids, s, u);
+    return rc ? rc : guarded(c, STALE_NODES, [&] { return relabel_apply(c, ids, s, u); });
 }
 
 }  // extern "C"
@@ -3863,7 +3980,7 @@ int32_t esc_reap_occupancy(esc_ctx* c) {
     if (c && c->multi) return ESC_E_STATE;              // esc_try_remove exchanges internally
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
-    if (!c->placed || !c->node_removal) return ESC_E_STATE;
+    if (!c->placed || !c->node_removal || c->stale) return ESC_E_STATE;
     hipSetDevice(c->device);
     // the words are current (events maintain them); with several ranks this rank's words
     // go into the exchange buffer the SUM works on
@@ -3909,7 +4026,7 @@ int32_t esc_reap_finish(esc_ctx* c, int64_t now_ns, const int64_t* soft_ns, cons
     if (c && c->multi) return ESC_E_STATE;
     if (!c || !soft_ns || !hard_ns || !out) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
-    if (!c->placed || !c->node_removal) return ESC_E_STATE;
+    if (!c->placed || !c->node_removal || c->stale) return ESC_E_STATE;
     const int32_t G = c->gi.G;
     hipSetDevice(c->device);
     // the grace periods are node-group options: uploaded when they change
@@ -3980,16 +4097,7 @@ int32_t esc_sort_nodes(esc_ctx* c) {
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->nodes_loaded) return ESC_E_STATE;
     hipSetDevice(c->device);
-    c->fused_ran = c->order_fused && c->fused_fits;
-    if (c->fused_ran) {
-        HIP_TRY(launch_order_fused(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb,
-                                   c->d_g_grp, c->d_oticket, c->d_ostat, c->d_ord, c->d_seg,
-                                   c->d_oerr, c->max_chunk, c->order_ablate, c->stream));
-        HIP_TRY(launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_memb, c->d_g_grp,
-                                    c->d_ord, c->d_seg, c->stream));
-    } else {
-        HIP_TRY(enqueue_order(c, c->stream));
-    }
+    HIP_TRY(enqueue_order(c, c->stream));
     c->order_src = 0;
     c->sorted = true;
     return ESC_OK;
@@ -4021,16 +4129,8 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
     if (!c->sorted) return ESC_E_STATE;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->fused_ran) {
-        uint32_t err = 0;
-        HIP_TRY(hipMemcpy(&err, c->d_oerr, 4, hipMemcpyDeviceToHost));
-        if (err) return ESC_E_HIP;                      // a look-back gave up: order not valid
-    }
-    // three-pass layout: class segments [b0, b1), [b1, b2) in age order; fused: untainted
-    // [s0, s1) in age order, tainted [s2, s3) newest first
-    // packed (small) groups always take the three-pass layout
-    const bool fused_g = c->fused_ran && c->h_gch_off[group + 1] > c->h_gch_off[group];
-    const int64_t so = fused_g ? 2 * (int64_t)which : (int64_t)which;
+    // class segments [b0, b1) (untainted), [b1, b2) (tainted), both in age order
+    const int64_t so = which;
     int64_t seg[2];
     HIP_TRY(hipMemcpy(seg, c->d_seg + 4 * (int64_t)group + so, 16, hipMemcpyDeviceToHost));
     const int64_t cnt = seg[1] - seg[0];
@@ -4053,12 +4153,8 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
     std::vector<uint32_t> v;
     for (;;) {
         v.resize(take);
-        if (fused_g) {
-            HIP_TRY(hipMemcpy(v.data(), vals + seg[0], take * 4, hipMemcpyDeviceToHost));
-        } else {
-            HIP_TRY(hipMemcpy(v.data(), vals + seg[1] - take, take * 4, hipMemcpyDeviceToHost));
-            std::reverse(v.begin(), v.end());
-        }
+        HIP_TRY(hipMemcpy(v.data(), vals + seg[1] - take, take * 4, hipMemcpyDeviceToHost));
+        std::reverse(v.begin(), v.end());
         if (take == cnt || ts(v[take - 1]) != ts(v[m - 1])) break;
         take = std::min(cnt, take * 2);
     }

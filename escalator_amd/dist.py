@@ -1,17 +1,20 @@
 """One process per GPU: sharded pods, the node side split by pair ownership, and one SUM
-exchange of the per-group words.
+reduce-scatter of the pods' per-group words to each group's owner.
 
 The reference has no parallelism (groups run sequentially,
 controller.go:416).  Here every rank holds a contiguous shard of the pod SoA and the whole
-node table; it reduces and orders the node side of the group pairs it owns (a contiguous
-pair range balanced by node entries, the same split on every rank).  The
-per-group words — the pods' sums split lo32 / hi, and the node words, exact on the owner
-and zero elsewhere — are all-reduced with SUM: by the library's own RCCL communicator
-(esc_comm_init / esc_exchange: ncclAllReduce over xGMI on the context's stream), or
-host-staged over ``gloo``.  int64 addition is associative, so any reduction order gives
-bit-identical totals; every rank then runs K4 on the same words.  (One process driving
-every GPU is ``Context(..., devices=[...])``: the same sharding with the exchange inside
-the library.)
+node table; it reduces, orders and DECIDES the groups whose node pairs it owns (a
+contiguous pair range balanced by node entries, the same split on every rank, DESIGN.md
+§7).  The pods' per-group words (sums split lo32 / hi, so a cross-rank SUM cannot wrap)
+sit in owner-major rows and are reduce-scattered with SUM — by the library's own RCCL
+communicator (esc_comm_init / esc_exchange: ncclReduceScatter over xGMI on the context's
+stream), or host-staged over ``gloo`` — so every owner receives the exact sums of its own
+groups and nothing else; the node words never travel.  int64 addition is associative, so
+any reduction order gives bit-identical totals.  A rank's esc_results holds its own groups
+(the others flagged ESC_TF_NOT_OWNED); ``gather_results`` collects every group's records
+where one host needs them all.  (One process driving every GPU is
+``Context(..., devices=[...])``: the same sharding with the exchange inside the library and
+the owners' records merged into one result.)
 """
 from __future__ import annotations
 
@@ -38,9 +41,10 @@ class Exchange:
 
     device_collective: the library's own RCCL communicator (esc_comm_init; rank 0's
     unique id travels over the torch.distributed group), one in-place
-    ncclAllReduce(int64, SUM) of the pods' and node words on the context's stream between
-    the shard step and K4 (esc_step) — the path a Go host drives through the C ABI alone.
-    Otherwise host-staged over the group (gloo): download, all_reduce, upload."""
+    ncclReduceScatter(int64, SUM) of the owner-major pod words on the context's stream
+    between the shard step and K4 (esc_step) — the path a Go host drives through the C ABI
+    alone.  Otherwise host-staged over the group (gloo): download, reduce_scatter into this
+    rank's slice, upload."""
 
     def __init__(self, ctx, device_collective: bool):
         import torch
@@ -62,10 +66,44 @@ class Exchange:
             return
         self.ctx.reduce()
         s, _ = self.ctx.exchange_download()
-        ts = self.torch.from_numpy(s)
-        self.dist.all_reduce(ts, op=self.dist.ReduceOp.SUM)
-        self.ctx.exchange_upload(ts.numpy(), np.zeros(0, np.int64))
+        off, n = self.ctx.exchange_slice()
+        mine = self.torch.zeros(n, dtype=self.torch.int64)
+        self.dist.reduce_scatter_tensor(mine, self.torch.from_numpy(s), op=self.dist.ReduceOp.SUM)
+        s[off:off + n] = mine.numpy()
+        self.ctx.exchange_upload(s, np.zeros(0, np.int64))
         self.ctx.decide()
+
+
+def merge_owned(parts):
+    """Every group's (totals, decision) from the ranks' esc_results: each group's records
+    from the rank that owns it (the others carry ESC_TF_NOT_OWNED in their totals' flags)."""
+    from ._lib import ESC_TF_NOT_OWNED
+    tot, dec = parts[0][0].copy(), parts[0][1].copy()
+    for t, d in parts[1:]:
+        m = (t["flags"] & ESC_TF_NOT_OWNED) == 0
+        tot[m] = t[m]
+        dec[m] = d[m]
+    assert not ((tot["flags"] & ESC_TF_NOT_OWNED) != 0).any(), "a group without an owner"
+    return tot, dec
+
+
+def merge_owned_metrics(parts, owners):
+    """Every group's gauges (esc_metrics_results) from the rank that owns it."""
+    out = parts[0].copy()
+    for r, m in enumerate(parts):
+        sel = np.asarray(owners) == r
+        out[sel] = m[sel]
+    return out
+
+
+def gather_results(ctx):
+    """All ranks: every group's totals and decision (the owners' records all-gathered over
+    the process group: G x 168 B per rank, outside any timed step)."""
+    import torch.distributed as dist
+    mine = ctx.results()
+    got = [None] * dist.get_world_size()
+    dist.all_gather_object(got, mine)
+    return merge_owned(got)
 
 
 def try_remove(ctx, now_ns: int, soft_ns, hard_ns, device_collective: bool):

@@ -125,6 +125,26 @@ def owner_ranges(nodes: dict, n_gp: int, world: int) -> list[int]:
     return bounds + [n_gp]
 
 
+def exchange_rows(gpair, bounds: list[int]) -> tuple[np.ndarray, int]:
+    """Owner-major rows of the exchanged pod words: the owner of group g is
+    the rank whose pair range [bounds[r], bounds[r + 1]) holds gpair[g]; its row is
+    owner * cap + its index among the owner's groups (ascending), cap the largest owner's
+    group count.  A reduce-scatter of cap * 5 words per rank then hands every owner exactly
+    its own groups' sums."""
+    gpair = np.asarray(gpair, np.int64)
+    world = len(bounds) - 1
+    owner = np.searchsorted(np.asarray(bounds[:-1], np.int64), gpair, side="right") - 1 if world > 1 \
+        else np.zeros(len(gpair), np.int64)
+    counts = np.bincount(owner, minlength=world)
+    cap = max(1, int(counts.max()) if len(counts) else 1)
+    rows = np.zeros(len(gpair), np.uint32)
+    seen = np.zeros(world, np.int64)
+    for g, r in enumerate(owner):
+        rows[g] = r * cap + seen[r]
+        seen[r] += 1
+    return rows, cap
+
+
 def node_bytes(nodes: dict, n_gp: int, rank: int = 0, world: int = 1) -> int:
     q = node_entries(nodes)
     E = len(q)

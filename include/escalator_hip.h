@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ESC_ABI_VERSION 4
+#define ESC_ABI_VERSION 5
 
 /* ---------------------------------------------------------------- return codes */
 #define ESC_OK          0
@@ -58,6 +58,8 @@ extern "C" {
 #define ESC_ST_ERR_OVERFLOW   5  /* a sum left int64: the reference switches Quantity to inf.Dec
                                     (apimachinery v0.22.5, not vendored) — reported, not emulated     */
 #define ESC_ST_ERR_TAINT_MIN  6  /* pkg/controller/scale_down.go:150-154 (formatted; see esc_taint_error) */
+#define ESC_ST_NOT_OWNED      7  /* world > 1: this group is decided on its owner rank (esc_group_owner);
+                                    the record here is zero. Not a reference status.            */
 
 /* ------------------------------------------------------------- decision branch
  * Which arm of scaleNodeGroup (pkg/controller/controller.go:192-397) produced delta. */
@@ -117,6 +119,7 @@ typedef struct esc_group_totals {
 
 #define ESC_TF_POD_OVERFLOW   1  /* a pod sum left int64 (Quantity would switch to inf.Dec) */
 #define ESC_TF_NODE_OVERFLOW  2  /* a node capacity sum left int64                          */
+#define ESC_TF_NOT_OWNED      4  /* world > 1: totals held by the group's owner rank (zero here) */
 
 /* Per-group scale decision. */
 typedef struct esc_group_decision {
@@ -295,8 +298,9 @@ int32_t     esc_taint_error(int64_t n_untainted, int32_t min_nodes, char* buf, i
  * drives each GPU: rank r holds a contiguous shard of the pods and the whole node table,
  * of which it reduces and orders the node side of the group pairs it owns (a contiguous
  * pair range balanced by node entries, the same split on every rank: esc_group_owner,
- * DESIGN.md §7).  The per-group words are summed across ranks inside the library
- * (esc_comm_init + esc_step) or by the caller's collective on esc_exchange_buffers.
+ * DESIGN.md §7).  The pods' per-group words are reduce-scattered across ranks to each
+ * group's owner inside the library (esc_comm_init + esc_step) or by the caller's collective
+ * on esc_exchange_buffers; each rank then decides its OWN groups only.
  * device < 0 creates a host-only context (packer, scalar math, esc_node_owner_ranges). */
 typedef struct esc_ctx esc_ctx;
 
@@ -305,8 +309,9 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
 /* One context driving n_dev devices from one thread: rank i of n_dev on
  * devices[i], one communicator set from ncclCommInitAll, and every call below fanned out
  * internally — esc_load_pods splits the pods into n_dev contiguous shards, esc_step /
- * esc_run enqueue every device's shard step, the ncclAllReduce of the exchange words inside
- * ncclGroupStart / ncclGroupEnd and every device's decision; pod events are routed to the
+ * esc_run enqueue every device's shard step, the ncclReduceScatter of the exchange words
+ * inside ncclGroupStart / ncclGroupEnd and every device's decision of the groups it owns
+ * (esc_results merges them: every group, as at one device); pod events are routed to the
  * shard holding the id, node events reach every device; esc_group_order answers from the
  * owner device.  The per-device calls esc_reduce, esc_exchange*, esc_decide, esc_comm_init,
  * esc_reap_* and esc_ctx_set_stream return ESC_E_STATE on it.  A device listed twice (or
@@ -367,15 +372,18 @@ int32_t esc_node_owner_ranges(const esc_ctx* ctx, const esc_node_soa* nodes, int
 
 /* ------------------------------------------------------------ scale decision
  * esc_reduce     : async. Per-shard group totals (K1 pods + K2 nodes + combine).
- * esc_exchange_buffers: device buffers to all-reduce between esc_reduce and esc_decide:
+ * esc_exchange_buffers: device buffers to exchange between esc_reduce and esc_decide:
  *                  sum_buf  int64[sum_count]  with op SUM: the pods' per-group words
- *                  (G x 5: cpu and memory split lo32 / hi, count), then the node words
- *                  (G x 4, exact on the group's owner rank and zero elsewhere),
+ *                  (5 per group: cpu and memory split lo32 / hi, count) in OWNER-MAJOR
+ *                  rows, world x own_count / 5 rows; rank r needs only the SUM of its own
+ *                  slice [r * own_count, (r + 1) * own_count) (esc_exchange_slice): a
+ *                  reduce-scatter with recvcount own_count, or an all-reduce (a superset).
+ *                  The node words never travel: each group's owner computes them whole.
  *                  min_buf  int64[min_count]  with op MIN (min_count 0 = nothing to
  *                  exchange: every rank holds the whole node table and resolves
  *                  allNodes[0] from it, so min_buf is NULL).
- * esc_decide     : async. K4 decide on the (exchanged) totals; results land in the
- *                  context's host buffers after esc_sync.
+ * esc_decide     : async. K4 decide on the (exchanged) totals of the rank's own groups;
+ *                  results land in the context's host buffers after esc_sync.
  * esc_run        : esc_reduce + esc_decide for world == 1, optionally graph-captured.
  * esc_sync       : waits for the queued work (records outside the fast path's packing
  *                  range are summed exactly in-kernel).               */
@@ -383,6 +391,14 @@ int32_t esc_set_state(esc_ctx* ctx, const esc_group_state* state);   /* NULL = z
 int32_t esc_reduce(esc_ctx* ctx);
 int32_t esc_exchange_buffers(esc_ctx* ctx, void** sum_buf, int64_t* sum_count,
                              void** min_buf, int64_t* min_count);
+/* This rank's slice of sum_buf (word offset, word count): the rows of the groups it owns,
+ * whose SUM across ranks esc_decide reads.  At world 1: (0, sum_count). */
+int32_t esc_exchange_slice(const esc_ctx* ctx, int64_t* offset, int64_t* count);
+/* The owner-major row of every group (host only, like esc_node_owner_ranges): rows[g] =
+ * owner * own_rows + its index among the owner's groups (ascending); *own_rows = the largest
+ * owner's group count. */
+int32_t esc_exchange_rows(const esc_ctx* ctx, const esc_node_soa* nodes, int32_t world, uint32_t* rows,
+                          int32_t* own_rows);
 /* Use caller-allocated device buffers (e.g. torch tensors handed to RCCL) as the
  * exchange buffers; sizes as reported by esc_exchange_buffers.  NULL restores the
  * context's own buffers (min_buf may be NULL when min_count is 0). */
@@ -399,8 +415,9 @@ int32_t esc_sync(esc_ctx* ctx);
  * per GPU: rank 0 calls esc_comm_unique_id and ships the ESC_COMM_ID_BYTES bytes to the
  * other ranks over any host channel; every rank then calls esc_comm_init (collective,
  * blocking until all ranks joined; rank / world must equal the context's).  esc_exchange
- * enqueues ncclAllReduce(int64, SUM) of the pod words (esc_exchange_buffers) in place on
- * the context's stream; esc_step = esc_reduce + esc_exchange + esc_decide (esc_run when
+ * enqueues ncclReduceScatter(int64, SUM) of the pod words (esc_exchange_buffers) in place
+ * on the context's stream, every rank receiving its own slice (esc_exchange_slice);
+ * esc_step = esc_reduce + esc_exchange + esc_decide (esc_run when
  * world == 1 and no communicator was set up).  The library resolves librccl at run time
  * (the copy already loaded in the process, else librccl.so.1).                         */
 #define ESC_COMM_ID_BYTES 128
@@ -410,6 +427,9 @@ int32_t esc_exchange(esc_ctx* ctx);
 int32_t esc_step(esc_ctx* ctx);
 /* Ranks of the context's communicator (ncclCommCount; a multi-device context: its devices). */
 int32_t esc_comm_size(const esc_ctx* ctx, int32_t* ranks);
+/* Every group's totals and decision.  world > 1 (one process per GPU): the rank's own
+ * groups; the others' records are zero, flagged ESC_TF_NOT_OWNED / ESC_ST_NOT_OWNED (their
+ * owner's esc_results holds them).  A multi-device context returns every group. */
 int32_t esc_results(esc_ctx* ctx, esc_group_totals* totals, esc_group_decision* decisions);
 /* Metric gauges (§8f): computed by K4 beside the decisions when enabled (off by default;
  * they stay in device memory until esc_metrics_results copies them out, after esc_sync). */
@@ -417,7 +437,10 @@ int32_t esc_set_metrics(esc_ctx* ctx, int32_t enable);
 int32_t esc_metrics_results(esc_ctx* ctx, esc_group_metrics* out);
 int32_t esc_use_graph(esc_ctx* ctx, int32_t enable);
 int32_t esc_force_wide(esc_ctx* ctx, int32_t enable);   /* testing: always take the wide path */
-/* Last kernel's device time in ms per stage (timing mode), see DESIGN.md §6. */
+/* Device time in ms per stage of the last decision (timing mode), see DESIGN.md §6:
+ * [0] K1, [1] the fused tail, [2] the remaining orderings, [3] node groups (+ K4 at world
+ * 1), then at world > 1 [4] the exchange (esc_exchange) and [5] K4 (esc_decide);
+ * ms_out[9] = the whole step (first to last event). */
 int32_t esc_set_timing(esc_ctx* ctx, int32_t enable);
 int32_t esc_stage_times(esc_ctx* ctx, double* ms_out, int32_t n);
 /* K1 records per workgroup 8 words (s_memrealtime ticks at 100 MHz at start / after the K

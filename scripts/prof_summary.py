@@ -28,8 +28,13 @@ import json
 import os
 import statistics
 
-KERNELS = ("k_pod_reduce", "k_step_tail", "k_node_groups", "k_decide", "k_ord_count", "k_ord_scatter", "k_ord_packed")
 PEAK_GBS = 8000.0
+ORDER_KERNELS = ("k_ord_count", "k_ord_scatter", "k_ord_packed")
+
+
+def ours(k):
+    """The library's kernels (every one is named k_*)."""
+    return k.startswith("k_")
 
 
 def short(name):
@@ -46,7 +51,7 @@ def trace_summary(path, n):
     per = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         k = short(r["Kernel_Name"])
-        if k in KERNELS:
+        if ours(k):
             per[k].append((int(r["Dispatch_Id"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     out = {}
     for k, rows in per.items():
@@ -62,7 +67,7 @@ def counter_summary(path, counter, n):
         if r["Counter_Name"] != counter:
             continue
         k = short(r["Kernel_Name"])
-        if k in KERNELS:
+        if ours(k):
             per[k].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     return {k: (len(rows), last_dispatches(rows, n)) for k, rows in per.items()}
 
@@ -89,8 +94,23 @@ def main():
     for e in res["kernels"].values():
         if "hbm_read_bytes" in e and "hbm_write_bytes" in e:
             e["hbm_bytes"] = e["hbm_read_bytes"] + e["hbm_write_bytes"]
-    if a.bench:
-        b = json.load(open(a.bench))
+    b = json.load(open(a.bench)) if a.bench else None
+    if b and b["metric"].startswith("config5"):
+        # config 5: the per-decision ordering kernels of the cold (cache-flushed) decisions
+        # bench.py times last (--last = its steps + the final sort); algorithmic bytes =
+        # SURVEY.md §8(d)'s 12 B per membership
+        ks = [k for k in ORDER_KERNELS if k in res["kernels"]]
+        t_ns = sum(res["kernels"][k]["mean_ns"] for k in ks)
+        algo = b["roofline"]["bytes_per_decision"]
+        hb = [res["kernels"][k].get("hbm_bytes") for k in ks]
+        res["order"] = {"kernels": ks, "algorithmic_bytes_per_decision": algo, "rocprof_ns_per_decision": t_ns,
+                        "rocprof_frac": algo / (t_ns * 1e-9) / 1e9 / PEAK_GBS if t_ns else None,
+                        "bench_ms": b["ms_per_step"], "bench_frac": b["roofline"]["frac"],
+                        "traffic_bytes": sum(hb) if all(x is not None for x in hb) and hb else None}
+        if res["order"]["traffic_bytes"]:
+            res["order"]["traffic_over_algorithmic"] = res["order"]["traffic_bytes"] / algo
+        b = None
+    if b:
         rf = b["roofline"]
         k1 = res["kernels"].get("k_pod_reduce", {})
         algo = rf["algorithmic_bytes_per_launch"]
@@ -107,7 +127,7 @@ def main():
         }
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1, sort_keys=True)
-    print(json.dumps(res.get("k1", {})))
+    print(json.dumps(res.get("k1", res.get("order", {}))))
     for k, e in sorted(res["kernels"].items()):
         print(k, {x: (round(y, 1) if isinstance(y, float) else y) for x, y in e.items()})
 

@@ -14,7 +14,30 @@ def test_library_exports_every_header_symbol():
     assert len(fns) >= 40
     assert [f for f in fns if not hasattr(lib, f)] == []
     assert sorted(set(fns) - set(L._SIGS)) == []
-    assert lib.esc_abi_version() == 4
+    assert lib.esc_abi_version() == 5
+
+
+def test_product_library_reads_no_result_changing_knob():
+    """The product library's results depend on its inputs alone: the
+    only environment variables it names are this allow-list, none of which changes a result
+    — host thread counts (ESC_HOST_THREADS, ESC_PACK_PAR_MIN: the packer's and the load's
+    parallel passes give identical arrays, test_parallel_packer_equals_sequential), an extra
+    self-check of the age index (ESC_CHECK_INDEX) and the multi-device exchange transport
+    (ESC_EXCHANGE=peer: the same integer SUM).  The measurement knobs (ESC_K1_VARIANT,
+    ESC_K3_ABLATE, ESC_K1_FULL_FLUSH, ESC_POD_SORT, ESC_NO_ZEROCOPY) live in the separate
+    measurement library only (Makefile ABLATIONS=1)."""
+    import re
+    from escalator_amd import _lib as L
+    with open(L.LIB_PATH, "rb") as f:
+        data = f.read()
+    # NUL-terminated literals (what getenv takes), not pieces of mangled names or debug info
+    names = set(m.decode() for m in re.findall(rb"(?<![A-Za-z0-9_])(ESC_[A-Z0-9_]{3,})\x00", data))
+    assert names <= {"ESC_HOST_THREADS", "ESC_PACK_PAR_MIN", "ESC_CHECK_INDEX", "ESC_EXCHANGE"}, names
+    for knob in ("ESC_K1_VARIANT", "ESC_K3_ABLATE", "ESC_ORDER_ABLATE", "ESC_ORDER_FUSED", "ESC_K1_FULL_FLUSH",
+                 "ESC_POD_SORT", "ESC_NO_ZEROCOPY", "ESC_ORDER_CHUNK"):
+        assert knob.encode() not in data, knob
+    # the measurement-only K1 ablations are not linked into the product library
+    assert b"launch_pod_reduce_ablation" not in data or not hasattr(L.load(), "launch_pod_reduce_ablation")
 
 
 def test_status_strings_verbatim():
@@ -24,6 +47,7 @@ def test_status_strings_verbatim():
     assert lib.esc_status_string(2) == b"node count larger than the maximum"
     assert lib.esc_status_string(3) == b"cannot divide by zero in percent calculation"
     assert lib.esc_status_string(4) == b"negative scale up delta"
+    assert lib.esc_status_string(7) == b"decided on the group's owner rank"       # world > 1, not a reference status
     buf = C.create_string_buffer(200)
     lib.esc_taint_error(2, 3, buf, 200)
     assert buf.value == b"the number of nodes(2) is less than specified minimum of 3. Taking no action"

@@ -44,3 +44,26 @@ def test_rank_count_mismatch_fails():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--launch-check"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_parity_mismatch_fails_the_run(capsys):
+    """A bench line whose results differ from the oracle is still printed, but the run exits
+    non-zero (bench.report is what main() and bench_order() return to sys.exit)."""
+    out = {"metric": "m", "value": 1.0, "parity": "MISMATCH vs C oracle"}
+    assert bench.report(out, False) == bench.PARITY_EXIT != 0
+    line = capsys.readouterr().out.strip()
+    assert json.loads(line)["parity"] == "MISMATCH vs C oracle"
+    assert bench.report(dict(out, parity="bit-exact"), True) == 0
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert "return report(out, parity_ok)" in src and "return report(out, parity)" in src
+    assert "sys.exit(main())" in src
+
+
+def test_stage_layout_names_every_event():
+    """The timing-mode stages the bench line reports at each shape."""
+    base = ["k_pod_reduce", "k_step_tail", "k_order_split", "k_node_groups"]
+    assert bench.stage_layout(1, 1, None, "nccl") == base
+    assert bench.stage_layout(1, 8, None, "nccl") == base + ["k_decide"]            # --shard-of 8
+    assert bench.stage_layout(8, 8, None, "nccl") == base + ["exchange", "k_decide"]
+    assert bench.stage_layout(2, 2, None, "gloo") == base + ["exchange_host_staged", "k_decide"]
+    assert bench.stage_layout(1, 1, [0, 1], "multi") == base

@@ -1,10 +1,12 @@
 """CPU, world_size 2 / 3 over gloo: the N-GPU exchange — sharded pods, the node side split
-by pair ownership, one SUM of the per-group words — reproduces the whole-snapshot totals.
+by pair ownership, one SUM reduce-scatter of the pods' per-group words to the groups'
+owners — reproduces the whole-snapshot totals.
 
 No GPU here, so each rank's words are restated from the C oracle in the library's layout
-(the pods' words split lo32 / hi; the node words exact on the group's owner
-rank, escalator_amd.layout.owner_ranges, and zero elsewhere); the GPU suite checks the
-library's own words against the same layout (tests/test_gpu_multi.py)."""
+(the pods' words split lo32 / hi in owner-major rows,
+escalator_amd.layout.exchange_rows; the node words computed whole on the group's owner,
+escalator_amd.layout.owner_ranges, and never exchanged); the GPU suite checks the library's
+own words against the same layout (tests/test_gpu_multi.py, tests/test_gpu_dist.py)."""
 import os
 import socket
 
@@ -22,49 +24,28 @@ def _free_port():
     return p
 
 
-def exchange_words(tot_shard: np.ndarray, tot_all: np.ndarray, groups, nodes, rank: int, world: int) -> np.ndarray:
-    """One rank's exchange words (esc_exchange_buffers layout): [G][5] pods (cpu lo, cpu hi,
-    mem lo, mem hi, count) from its pod shard, then [G][4] nodes (cpu, mem, unt | taint << 32,
-    cord | flags << 32) for the groups whose pairs it owns."""
+def exchange_words(tot_shard: np.ndarray, groups, nodes, world: int) -> tuple[np.ndarray, np.ndarray, int]:
+    """One rank's exchange words (esc_exchange_buffers layout): [world * cap][5] pod words
+    (cpu lo, cpu hi, mem lo, mem hi, count) from its pod shard, group g in row rows[g]."""
     from escalator_amd import layout
     from oracle import soa
     t = soa.group_tables(groups)
-    G = len(groups)
-    pw = np.zeros((G, 5), np.int64)
+    b = layout.owner_ranges(nodes, len(t["pair_ids"]), world)
+    rows, cap = layout.exchange_rows(t["gpair"], b)
+    pw = np.zeros((world * cap, 5), np.int64)
     for k, col in ((0, 0), (2, 1)):
         v = tot_shard[:, col].astype(object)
-        pw[:, k] = [int(x) & 0xFFFFFFFF for x in v]
-        pw[:, k + 1] = [int(x) >> 32 for x in v]
-    pw[:, 4] = tot_shard[:, 2]
-    b = layout.owner_ranges(nodes, len(t["pair_ids"]), world)
-    own = (np.asarray(t["gpair"]) >= b[rank]) & (np.asarray(t["gpair"]) < b[rank + 1])
-    F = soa.TOT_FIELDS
-    nx = np.zeros((G, 4), np.int64)
-    nx[:, 0] = tot_all[:, F.index("node_cpu_m")]
-    nx[:, 1] = tot_all[:, F.index("node_mem_b")]
-    nx[:, 2] = tot_all[:, F.index("n_untainted")] | (tot_all[:, F.index("n_tainted")] << 32)
-    nx[:, 3] = tot_all[:, F.index("n_cordoned")]
-    nx[~own] = 0
-    return np.concatenate([pw.ravel(), nx.ravel()])
-
-
-def decode_words(W: np.ndarray, G: int) -> np.ndarray:
-    """The exchanged words back to (pod cpu, pod mem, pods, node cpu, node mem, unt, taint, cord)."""
-    pw = W[:G * 5].reshape(G, 5).astype(object)
-    nx = W[G * 5:].reshape(G, 4)
-    out = np.zeros((G, 8), np.int64)
-    out[:, 0] = [int(a) + (int(b) << 32) for a, b in zip(pw[:, 0], pw[:, 1])]
-    out[:, 1] = [int(a) + (int(b) << 32) for a, b in zip(pw[:, 2], pw[:, 3])]
-    out[:, 2] = W[:G * 5].reshape(G, 5)[:, 4]
-    out[:, 3], out[:, 4] = nx[:, 0], nx[:, 1]
-    out[:, 5], out[:, 6], out[:, 7] = nx[:, 2] & 0xFFFFFFFF, nx[:, 2] >> 32, nx[:, 3] & 0xFFFFFFFF
-    return out
+        pw[rows, k] = [int(x) & 0xFFFFFFFF for x in v]
+        pw[rows, k + 1] = [int(x) >> 32 for x in v]
+    pw[rows, 4] = tot_shard[:, 2]
+    return pw.ravel(), rows, cap
 
 
 def _worker(rank, world, port, out):
+    import torch
     import torch.distributed as dist
+    from escalator_amd import layout
     from escalator_amd.context import Synth
-    from escalator_amd.dist import exchange_host
     from oracle import soa
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -72,10 +53,27 @@ def _worker(rank, world, port, out):
     lo, hi = shard_range(P, rank, world)
     s = Synth(P, N, G, config=4, seed=5, p_lo=lo, p_hi=hi)
     t = soa.totals(s.pods(), s.nodes(), s.groups)        # this rank's pods, every node
-    w = exchange_words(t, t, s.groups, s.nodes(), rank, world)
-    S, _ = exchange_host(w, np.zeros(0, np.int64))
+    w, rows, cap = exchange_words(t, s.groups, s.nodes(), world)
+    mine = torch.zeros(cap * 5, dtype=torch.int64)
+    dist.reduce_scatter_tensor(mine, torch.from_numpy(w))    # what esc_exchange does over RCCL
+    sl = mine.numpy().reshape(cap, 5)
+    tg = soa.group_tables(s.groups)
+    b = layout.owner_ranges(s.nodes(), len(tg["pair_ids"]), world)
+    own = [g for g in range(G) if b[rank] <= tg["gpair"][g] < b[rank + 1]]
+    F = soa.TOT_FIELDS
+    res = {}
+    for i, g in enumerate(own):                          # the owner's groups: pod SUMs + its node words
+        assert rows[g] == rank * cap + i
+        res[g] = [int(sl[i, 0]) + (int(sl[i, 1]) << 32), int(sl[i, 2]) + (int(sl[i, 3]) << 32), int(sl[i, 4])] + \
+                 [int(t[g, F.index(k)]) for k in ("node_cpu_m", "node_mem_b", "n_untainted", "n_tainted", "n_cordoned")]
+    got = [None] * world
+    dist.all_gather_object(got, res)
     if rank == 0:
-        out.put(S)
+        merged = {}
+        for r in got:
+            assert not set(r) & set(merged), "a group decided on two ranks"
+            merged.update(r)
+        out.put(np.array([merged[g] for g in range(G)], np.int64))
     dist.destroy_process_group()
 
 
@@ -99,7 +97,7 @@ def test_two_and_three_rank_exchange_equals_whole():
         for p in procs:
             p.join(timeout=60)
             assert p.exitcode == 0
-        assert np.array_equal(decode_words(S, 64), want), world
+        assert np.array_equal(S, want), world
 
 
 def test_owner_split_library_equals_restatement():
@@ -116,6 +114,14 @@ def test_owner_split_library_equals_restatement():
             b = [int(x) for x in ctx.owner_ranges(s.nodes(), world)]
             assert b == layout.owner_ranges(s.nodes(), n_gp, world), (cfg, world)
             assert b[0] == 0 and b[-1] == n_gp and b == sorted(b)
+            # owner-major exchange rows: the library's == the restatement's, a permutation
+            # into world x cap rows whose block r holds exactly rank r's groups
+            rows, cap = ctx.exchange_rows(s.nodes(), world)
+            want, wcap = layout.exchange_rows(soa.group_tables(s.groups)["gpair"], b)
+            assert cap == wcap and np.array_equal(rows, want), (cfg, world)
+            assert len(set(rows.tolist())) == G and int(rows.max()) < world * cap
+            gp = soa.group_tables(s.groups)["gpair"]
+            assert all(b[r // cap] <= gp[g] < b[r // cap + 1] for g, r in enumerate(rows.tolist()))
         # ranks' node bytes add up to the whole index's
         assert sum(layout.node_bytes(s.nodes(), n_gp, r, 8) for r in range(8)) == layout.node_bytes(s.nodes(), n_gp)
 

@@ -305,31 +305,9 @@ def test_k1_calibrated_shares_vs_c_oracle(esc, cfg, P, N, G):
         check_against_c_oracle(*ctx.results(), otot, odf, odi)
 
 
-@pytest.mark.parametrize("variant", ["5"])
-def test_k1_variants_vs_c_oracle(esc, variant, monkeypatch):
-    """The exact K1 variant (ESC_K1_VARIANT 5: dynamic shares from the ticket counter —
-    repeated launches check its reset)."""
-    monkeypatch.setenv("ESC_K1_VARIANT", variant)
-    s = esc.Synth(2_000_000, 20_000, 10_000, config=4, seed=0xE5CA1A7E00000004)
-    pods, nodes = s.pods(), s.nodes()
-    otot = soa.totals(pods, nodes, s.groups)
-    odf, odi = soa.decide(s.groups, s.states, otot)
-    ctx = esc.Context(s)
-    ctx.load_synth(s, replicas=2)
-    ctx.use_graph(True)
-    ctx.set_state(s.states)
-    for _ in range(4):
-        ctx.run()
-        tot, dec = ctx.results()
-        check_against_c_oracle(tot, dec, otot, odf, odi)
-
-
-@pytest.mark.parametrize("fused", ["0", "1"])
-def test_synthetic_sort_vs_c_oracle(esc, fused, monkeypatch):
-    """Both K5 per-decision paths (three passes; ESC_ORDER_FUSED=1: one pass with
-    decoupled look-back across a group's chunks, several chunks per group here), repeated
-    decisions (look-back epochs) and a dry-mode tracker change in between."""
-    monkeypatch.setenv("ESC_ORDER_FUSED", fused)
+def test_synthetic_sort_vs_c_oracle(esc):
+    """The K5 per-decision ordering (two passes over the groups' split chunks, several
+    chunks per group here), repeated decisions and a dry-mode tracker change in between."""
     s = esc.Synth(10_000, 400_000, 100, config=5, seed=0xE5CA1A7E00000005)
     nodes = s.nodes()
     ctx = esc.Context(s)
@@ -642,6 +620,36 @@ def test_node_relabel_limit_all_or_nothing(esc):
     assert list(tot["node_cpu_m"]) == [37000, 3040]
 
 
+def test_node_relabel_churn_reuses_entries(esc):
+    """Label churn (nodes moving a -> b -> a ... every round) takes each node's own retired
+    entry back instead of a spare one, so 30 rounds fit a spare room of a few
+    entries; the totals, allNodes[0] and both orderings stay equal to the literal oracle."""
+    groups = [{"name": "a", "label_key": "k", "label_value": "a", "max_nodes": 1000},
+              {"name": "b", "label_key": "k", "label_value": "b", "max_nodes": 1000}]
+    nodes = [{"name": "n%d" % i, "labels": {"k": "a"}, "cpu": 1000 + i, "mem": 1000, "created_ns": i}
+             for i in range(40)]
+    nodes += [{"name": "m%d" % i, "labels": {"k": "b"}, "cpu": 10, "mem": 10, "created_ns": 100 + i} for i in range(4)]
+    ctx = esc.Context(groups)
+    ctx.set_spare(0.01)
+    ctx.load(*ctx.pack([], nodes))
+    live = dict(enumerate(nodes))
+    movers = [0, 5, 17]
+    for rnd in range(30):
+        to = "b" if rnd % 2 == 0 else "a"
+        new = [dict(live[j], labels={"k": to}) for j in movers]
+        ctx.nodes_relabel(movers, ctx.pack([], new)[1])          # never ESC_E_LIMIT
+        for j, x in zip(movers, new):
+            live[j] = x
+        tot, _ = ctx.decide_all()
+        na = sum(1 for x in live.values() if x["labels"]["k"] == "a")
+        assert list(tot["n_nodes"]) == [na, 44 - na], rnd
+        assert int(tot["node_cpu_m"][0]) == sum(x["cpu"] for x in live.values() if x["labels"]["k"] == "a")
+        assert int(tot["first_node"][0]) == min(j for j, x in live.items() if x["labels"]["k"] == "a")
+        for g, name in enumerate("ab"):
+            mem = sorted((x["created_ns"], j) for j, x in live.items() if x["labels"]["k"] == name)
+            assert list(ctx.group_order(g, 0)) == [j for _, j in mem], (rnd, g)
+
+
 def test_node_add_limit_all_or_nothing(esc):
     """A batch that does not fit the spare room is refused whole (ESC_E_LIMIT)."""
     groups = [{"name": "a", "label_key": "k", "label_value": "v", "max_nodes": 1000}]
@@ -671,8 +679,9 @@ def _members_oldest(nodes, groups, g):
 @pytest.mark.parametrize("graph", [False, True])
 def test_sharded_two_contexts_host_exchange(esc, graph):
     """Three ranks' shards on one device, exchanged through the host: == whole snapshot
-    (graph: each shard's K1/K2/K3 step replayed from its captured graph, twice)."""
-    from escalator_amd.dist import shard_range
+    (graph: each shard's K1/K2/K3 step replayed from its captured graph, twice); each rank
+    decides the groups it owns and the owners' records make up every group."""
+    from escalator_amd.dist import merge_owned, merge_owned_metrics, shard_range
     P, N, G = 300_000, 30_000, 1000
     full = esc.Synth(P, N, G, config=4, seed=11)
     otot = soa.totals(full.pods(), full.nodes(), full.groups)
@@ -693,13 +702,18 @@ def test_sharded_two_contexts_host_exchange(esc, graph):
         ctxs.append((c, s))
     W = np.sum(words, axis=0)
     F = np.min(firsts, axis=0)
+    parts, mets = [], []
     for c, _ in ctxs:
         c.set_metrics(True)
         c.exchange_upload(W, F)
         c.decide()
-        tot, dec = c.results()
-        check_against_c_oracle(tot, dec, otot, odf, odi)
-        check_metrics(c.metrics(), soa.metrics(otot, odf, odi))
+        parts.append(c.results())                # each rank: its own groups
+        mets.append(c.metrics())
+    tot, dec = merge_owned(parts)
+    check_against_c_oracle(tot, dec, otot, odf, odi)
+    owners = [ctxs[0][0].group_owner(g) for g in range(G)]
+    assert set(owners) == {0, 1, 2}
+    check_metrics(merge_owned_metrics(mets, owners), soa.metrics(otot, odf, odi))
 
 
 def test_determinism_repeat(esc):
@@ -813,11 +827,14 @@ def test_node_index_split_within_pairs(esc, world):
         words.append(w)
         ctxs.append((c, s))
     W = np.sum(words, axis=0)
+    parts = []
     for c, _ in ctxs:
         c.exchange_upload(W, np.zeros(0, np.int64))
         c.decide()
-        tot, dec = c.results()
-        check_against_c_oracle(tot, dec, otot, odf, odi)
+        parts.append(c.results())
+    from escalator_amd.dist import merge_owned
+    tot, dec = merge_owned(parts)
+    check_against_c_oracle(tot, dec, otot, odf, odi)
 
 
 # ------------------------------------------------- incremental snapshot (§8f)
@@ -1591,12 +1608,13 @@ def test_config3_full_size_vs_c_oracle(esc):
 
 def test_config4_full_size_vs_c_oracle(esc):
     """BASELINE config #4 at its stated size on one GPU: 100M pods / 1M nodes / 10k groups;
-    every group's totals and decision, and three groups' orderings, equal the C oracle
-    (the check bench.py makes, here in the GPU suite)."""
+    every group's totals and decision, and every group's two orderings (taintOldestN,
+    untaintNewestN), equal the C oracle (the check bench.py makes, here in the GPU suite)."""
     s = esc.Synth(100_000_000, 1_000_000, 10_000, config=4, seed=0xE5CA1A7E00000004, threads=16)
     pods, nodes = s.pods(), s.nodes()
     otot = soa.totals(pods, nodes, s.groups, threads=16)
     odf, odi = soa.decide(s.groups, s.states, otot)
+    want = soa.order_all(nodes, s.groups)
     ctx = esc.Context(s)
     ctx.load_synth(s)
     ctx.set_state(s.states)
@@ -1605,9 +1623,13 @@ def test_config4_full_size_vs_c_oracle(esc):
         ctx.run()
         tot, dec = ctx.results()
         check_against_c_oracle(tot, dec, otot, odf, odi)
-    for g in (0, 5_000, 9_999):
+    n = 0
+    for g in range(10_000):
         for w in (0, 1):
-            assert np.array_equal(ctx.group_order(g, w), soa.order(nodes, s.groups, g, w)), (g, w)
+            got = ctx.group_order(g, w)
+            assert np.array_equal(got, want[(g, w)]), (g, w, len(got), len(want[(g, w)]))
+            n += len(got)
+    assert n > 900_000
 
 
 def test_config5_full_size_orderings_vs_c_oracle(esc):
@@ -1657,7 +1679,8 @@ def test_rccl_step_world1_vs_c_oracle(esc, graph):
         tot, dec = ctx.results()
         check_against_c_oracle(tot, dec, otot, odf, odi)
     (sb, sc), (mb, mc) = ctx.exchange_buffers()
-    assert sc == (5 + 4) * 10_000 and mc == 0 and mb is None
+    assert sc == 5 * 10_000 and mc == 0 and mb is None        # the pod words only
+    assert ctx.exchange_slice() == (0, 5 * 10_000)
     assert ctx.comm_size() == 1
 
 

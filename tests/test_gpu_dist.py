@@ -60,7 +60,7 @@ def _decision_worker(rank, world, port, out):
     import torch.distributed as dist
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import escalator_amd as esc
-    from escalator_amd.dist import Exchange, gather_orders, shard_range
+    from escalator_amd.dist import Exchange, gather_orders, gather_results, shard_range
     lo, hi = shard_range(P, rank, world)
     s = esc.Synth(P, N, G, config=4, seed=SEED, p_lo=lo, p_hi=hi)
     ctx = esc.Context(s, device=0, rank=rank, world=world)
@@ -70,16 +70,17 @@ def _decision_worker(rank, world, port, out):
     ctx.set_order_in_step(True)
     ctx.k1_calibrate(2)
     ex = Exchange(ctx, device_collective=False)
-    res = []
+    res, own = [], []
     for _ in range(3):                      # replicas rotate: every step a fresh exchange
         ex.step()
-        tot, dec = ctx.results()
-        res.append((tot, dec))
+        own.append(ctx.results())           # this rank's own groups
+        res.append(gather_results(ctx))     # every group, from the owners
     owners = [ctx.group_owner(g) for g in range(G)]
     merged = {w: gather_orders(ctx, w, N_SEL, s.nodes()["created_ns"]) for w in (0, 1)}
-    words, _ = ctx.exchange_download()      # the SUM the last decide ran on
-    out.put((rank, dict(res=res, metrics=ctx.metrics(), owners=owners, merged=merged, words=words,
-                        pod_bytes=ctx.stream_bytes()[0])))
+    words, _ = ctx.exchange_download()      # this rank's slice holds the SUM the last decide ran on
+    off, n = ctx.exchange_slice()
+    out.put((rank, dict(res=res, own=own, metrics=ctx.metrics(), owners=owners, merged=merged,
+                        slice=words[off:off + n], pod_bytes=ctx.stream_bytes()[0])))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -92,18 +93,27 @@ def test_two_process_exchange_vs_c_oracle():
     full = esc.Synth(P, N, G, config=4, seed=SEED)
     otot = soa.totals(full.pods(), full.nodes(), full.groups)
     odf, odi = soa.decide(full.groups, full.states, otot)
+    from escalator_amd.dist import merge_owned_metrics
     got = _run_ranks(_decision_worker, 2)
     n_gp = len(soa.group_tables(full.groups)["pair_ids"])
+    owners = got[0]["owners"]
+    assert owners == got[1]["owners"] and owners == sorted(owners) and set(owners) == {0, 1}
+    mine = {r: np.array(owners) == r for r in (0, 1)}
     for r in (0, 1):
         g = got[r]
         for tot, dec in g["res"]:
             check_against_c_oracle(tot, dec, otot, odf, odi)
-        check_metrics(g["metrics"], soa.metrics(otot, odf, odi))
+        for tot, dec in g["own"]:           # a rank decides only its own groups
+            assert np.array_equal((tot["flags"] & 4) == 0, mine[r])
+            assert (dec["status"][~mine[r]] == 7).all()
         lo, hi = shard_range(P, r, 2)
         assert g["pod_bytes"] == layout.pod_bytes(full.pods(), n_gp, lo, hi)
-    assert np.array_equal(got[0]["words"], got[1]["words"])
-    owners = got[0]["owners"]
-    assert owners == got[1]["owners"] and owners == sorted(owners) and set(owners) == {0, 1}
+        # the owner's slice: the SUM of its groups' pod words, nothing else exchanged
+        sl = g["slice"].reshape(-1, 5)[:int(mine[r].sum())]
+        F = soa.TOT_FIELDS
+        assert np.array_equal(sl[:, 0] + (sl[:, 1] << 32), otot[mine[r], F.index("pod_cpu_m")])
+        assert np.array_equal(sl[:, 4], otot[mine[r], F.index("n_pods")])
+    check_metrics(merge_owned_metrics([got[0]["metrics"], got[1]["metrics"]], owners), soa.metrics(otot, odf, odi))
     for w in (0, 1):
         for g in range(G):
             want = soa.order(full.nodes(), full.groups, g, w, cap=N_SEL)

@@ -61,14 +61,15 @@ def test_multi_device_context_vs_c_oracle(esc, devices):
 
 def test_multi_device_shards_equal_per_process_ranks(esc):
     """The multi-device context's shards are the per-process ranks: the same pod shards,
-    owner split and exchange words (summed through the host for the per-process contexts)."""
-    from escalator_amd.dist import shard_range
+    owner split and exchange words (summed through the host for the per-process contexts,
+    whose owners then decide their own groups)."""
+    from escalator_amd.dist import merge_owned, shard_range
     P, N, G = 120_000, 20_000, 300
     full = esc.Synth(P, N, G, config=4, seed=21)
     otot = soa.totals(full.pods(), full.nodes(), full.groups)
     odf, odi = soa.decide(full.groups, full.states, otot)
     world = 3
-    words = []
+    words, ctxs = [], []
     for r in range(world):
         lo, hi = shard_range(P, r, world)
         s = esc.Synth(P, N, G, config=4, seed=21, p_lo=lo, p_hi=hi)
@@ -78,6 +79,7 @@ def test_multi_device_shards_equal_per_process_ranks(esc):
         c.reduce()
         w, _ = c.exchange_download()
         words.append(w)
+        ctxs.append((c, s))
     m = esc.Context(full, devices=[0] * world)
     m.load_synth(full)
     m.set_state(full.states)
@@ -85,14 +87,24 @@ def test_multi_device_shards_equal_per_process_ranks(esc):
     tot, dec = m.results()
     check_against_c_oracle(tot, dec, otot, odf, odi)
     W = np.sum(words, axis=0)
-    # the SUM's node words: exact on the owner, zero elsewhere -> the node totals
-    nx = W[G * 5:].reshape(G, 4)
-    assert np.array_equal(nx[:, 0], otot[:, soa.TOT_FIELDS.index("node_cpu_m")])
-    assert np.array_equal(nx[:, 2] & 0xFFFFFFFF, otot[:, soa.TOT_FIELDS.index("n_untainted")])
-    assert np.array_equal(nx[:, 2] >> 32, otot[:, soa.TOT_FIELDS.index("n_tainted")])
-    for r in range(world):                             # non-owners contribute zero node words
+    # the SUM's owner-major pod rows -> every group's pod totals (only the pod words travel)
+    rows, cap = ctxs[0][0].exchange_rows(full.nodes(), world)
+    assert len(W) == world * cap * 5
+    pw = W.reshape(world * cap, 5)[rows.astype(np.int64)]
+    assert np.array_equal(pw[:, 0] + (pw[:, 1] << 32), otot[:, soa.TOT_FIELDS.index("pod_cpu_m")])
+    assert np.array_equal(pw[:, 4], otot[:, soa.TOT_FIELDS.index("n_pods")])
+    parts = []
+    for r, (c, _) in enumerate(ctxs):
+        off, n = c.exchange_slice()
+        assert (off, n) == (r * cap * 5, cap * 5)
+        c.exchange_upload(W, np.zeros(0, np.int64))
+        c.decide()
+        t, d = c.results()
         mine = np.array([m.group_owner(g) == r for g in range(G)])
-        assert not words[r][G * 5:].reshape(G, 4)[~mine].any()
+        assert np.array_equal((t["flags"] & 4) == 0, mine), r           # ESC_TF_NOT_OWNED elsewhere
+        assert (d["status"][~mine] == 7).all()                          # ESC_ST_NOT_OWNED
+        parts.append((t, d))
+    check_against_c_oracle(*merge_owned(parts), otot, odf, odi)
 
 
 @pytest.mark.parametrize("seed", range(3))
