@@ -645,6 +645,7 @@ def test_node_relabel_churn_reuses_entries(esc):
         assert list(tot["n_nodes"]) == [na, 44 - na], rnd
         assert int(tot["node_cpu_m"][0]) == sum(x["cpu"] for x in live.values() if x["labels"]["k"] == "a")
         assert int(tot["first_node"][0]) == min(j for j, x in live.items() if x["labels"]["k"] == "a")
+        ctx.sort_nodes()
         for g, name in enumerate("ab"):
             mem = sorted((x["created_ns"], j) for j, x in live.items() if x["labels"]["k"] == name)
             assert list(ctx.group_order(g, 0)) == [j for _, j in mem], (rnd, g)
