@@ -567,13 +567,19 @@ struct RegionSink {
     const uint32_t* plen;      // memberships of group g
     const uint8_t* dry;
     uint32_t *g_memb, *g_grp;  // region words (MEMB_FLAG_SHIFT), group words
-    uint32_t* err;             // set when a membership falls outside its group's count
+    uint32_t* err;             // bit 0: a membership fell outside its group's count; bit 1: a
+                               // coarse-key run too long for k_age_fix (rebuild exact)
     int32_t G;
-    int R;                     // creation-offset bits (key = group << R | offset)
+    int R;                     // the group's shift in the key (key = group << R | time bits)
+    int fix;                   // coarse keys with dropped time bits: the final pass also writes
+                               // the sorted keys and k_age_fix orders equal-key runs exactly
 };
+// coarse_shift < 0: exact 64-bit keys (group << R | offset); >= 0: 32-bit coarse keys
+// (group << (32 - gbits) | offset >> coarse_shift) + the run fix-up (S.R = 32 - gbits).
 hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const uint32_t* base, int64_t n_memb,
-                           int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, uint64_t* keys[2], uint32_t* vals[2],
-                           uint32_t* hist, uint32_t* tot, const RegionSink& S, hipStream_t st);
+                           int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, int coarse_shift,
+                           uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t* tot, const RegionSink& S,
+                           hipStream_t st);
 hipError_t launch_order(const NodeDev& n, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
                         const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
                         int64_t n_e, int32_t G, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,

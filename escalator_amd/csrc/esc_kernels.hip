@@ -35,9 +35,6 @@
 #error "esc_kernels.hip targets gfx950 (160 KB LDS per CU); build with ARCH=gfx950"
 #endif
 
-#ifndef MK_ABL
-#define MK_ABL 0                                     // k_memb_keys ablations (timing only)
-#endif
 #ifndef ESC_PART
 #define ESC_PART 0
 #endif
@@ -2047,7 +2044,10 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
             const KT kk = sk[e];
             const uint32_t dd = (uint32_t)(kk >> shift) & (NB - 1);
             const uint32_t g = run[dd] + (uint32_t)e - lst[dd];
-            if constexpr (FINAL) region_put(sink, g, kk, sv[e]);
+            if constexpr (FINAL) {
+                region_put(sink, g, kk, sv[e]);
+                if (sink.fix) kout[g] = kk;                      // coarse keys: k_age_fix reads them
+            }
             else if (!CARRY || g < c_e[dd]) {
                 kout[g] = kk;
                 vout[g] = sv[e];
@@ -2065,6 +2065,48 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
         }
         __syncthreads();
     }
+}
+
+// Coarse keys (launch_age_sort): the LSD sort orders the memberships by (group, creation
+// offset >> shift), equal coarse keys in snapshot order.  Each run of equal coarse keys
+// (k_rs_scatter's final pass also left the sorted keys in its key output) is put in exact order here:
+// its region words re-sorted by (creation time, node) — the exact sort's order, as a group
+// holds a node once and snapshot order is node order.  Runs are rare (config 5: a few per
+// thousand memberships) and short; one longer than AF_RUN sets bit 2 of *S.err and the
+// host rebuilds the index with the exact 64-bit keys.
+constexpr int AF_RUN = 8;
+__global__ __launch_bounds__(256) void k_age_fix(const uint32_t* __restrict__ keys, int64_t n, RegionSink S,
+                                                 const int64_t* __restrict__ created, int64_t ts_min) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t k = keys[i];
+    if ((i > 0 && keys[i - 1] == k) || i + 1 >= n || keys[i + 1] != k) return;     // not a run's first
+    int len = 2;
+    while (len <= AF_RUN && i + len < n && keys[i + len] == k) ++len;
+    if (len > AF_RUN) { atomicOr(S.err, 2u); return; }
+    const uint32_t g = k >> S.R;
+    if (g >= (uint32_t)S.G) { atomicOr(S.err, 1u); return; }
+    const int64_t d0 = (int64_t)S.pstart[g] + (i - S.seg[g]);
+    uint32_t w[AF_RUN];
+    int64_t t[AF_RUN];
+#pragma unroll
+    for (int j = 0; j < AF_RUN; ++j) {
+        w[j] = j < len ? S.g_memb[d0 + j] : 0xFFFFFFFFu;
+        t[j] = j < len ? created[w[j] & MEMB_NODE_MASK] - ts_min : INT64_MAX;
+    }
+#pragma unroll
+    for (int a = 0; a < AF_RUN; ++a)                   // odd-even transposition: static indices only
+#pragma unroll
+        for (int j = a & 1; j + 1 < AF_RUN; j += 2) {
+            const bool sw = t[j] > t[j + 1] ||
+                            (t[j] == t[j + 1] && (w[j] & MEMB_NODE_MASK) > (w[j + 1] & MEMB_NODE_MASK));
+            const uint32_t wa = sw ? w[j + 1] : w[j], wb = sw ? w[j] : w[j + 1];
+            const int64_t ta = sw ? t[j + 1] : t[j], tb = sw ? t[j] : t[j + 1];
+            w[j] = wa; w[j + 1] = wb; t[j] = ta; t[j + 1] = tb;
+        }
+#pragma unroll
+    for (int j = 0; j < AF_RUN; ++j)
+        if (j < len) S.g_memb[d0 + j] = w[j];
 }
 
 // ---- the age index (load time): memberships listed in snapshot order (streaming over
@@ -2186,18 +2228,19 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_scan_small(uint32_t* __restrict_
 }
 
 // Lists the memberships in snapshot order (a block's nodes in order, a node's groups in
-// label order): key = group << R | creation offset (R bits), value = node | membership
-// flags << 32 — a dry group's membership carries "tracked by this group" in the tracker
-// bit (controller.go:126-138), so the per-decision split needs no lookup.
-template <int ABL>                                   // ABL != 0: timing ablations (MK_ABL builds)
+// label order): key = group << R | (creation offset >> KS), value = node | membership
+// flags << MEMB_FLAG_SHIFT — a dry group's membership carries "tracked by this group" in
+// the tracker bit (controller.go:126-138), so the per-decision split needs no lookup.  KT =
+// uint64_t with KS = 0 (the exact key), or uint32_t (the coarse key, launch_age_sort).
+template <class KT>
 __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G, int64_t n, const uint32_t* __restrict__ base,
-                                                          int64_t cap, int64_t ts_min, uint64_t div, int R,
-                                                          uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                                          int64_t cap, int64_t ts_min, uint64_t div, int R, int KS,
+                                                          KT* __restrict__ keys, uint32_t* __restrict__ vals) {
     // A round's memberships are staged in LDS and written out as two contiguous streams:
     // stored straight from the walk, a wave's 8-B stores land ~4 entries apart per lane and
     // the listing took 5x its store-free time (measured, r03_mk).
     __shared__ uint32_t wsum[MEMB_WAVES];
-    __shared__ uint64_t sk[MEMB_CAP];
+    __shared__ KT sk[MEMB_CAP];
     __shared__ uint32_t sv[MEMB_CAP];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     uint32_t carry = base[blockIdx.x];
@@ -2224,13 +2267,8 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
             tg[u] = v ? N.trk_group[tk[u]] : -1;
         }
         uint32_t c = 0;
-        if constexpr (ABL == 2) {
 #pragma unroll
-            for (int u = 0; u < MEMB_U; ++u) c += (f[u] & ESC_NF_ABSENT) ? 0u : 1u;
-        } else {
-#pragma unroll
-            for (int u = 0; u < MEMB_U; ++u) node_groups_c0(N, G, f[u], N.lo + r0 + u, c0[u], [&](uint32_t) { ++c; });
-        }
+        for (int u = 0; u < MEMB_U; ++u) node_groups_c0(N, G, f[u], N.lo + r0 + u, c0[u], [&](uint32_t) { ++c; });
         const uint32_t x = wave_incl_scan32(c);
         if (lane == 63) wsum[wid] = x;
         __syncthreads();
@@ -2246,25 +2284,22 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
         for (int u = 0; u < MEMB_U; ++u) {
             const int64_t i = N.lo + r0 + u;
             const uint64_t off = (uint64_t)(cr[u] - ts_min);
-            const uint64_t ak = ABL == 3 ? off : div_pow10(off, div);
+            const KT ak = (KT)(div_pow10(off, div) >> KS);
             const uint32_t fu = f[u];
             node_groups_c0(N, G, fu, i, c0[u], [&](uint32_t mb) {
                 bool tr = false;
-                if (ABL != 5 && mdry(mb) && (fu & ESC_NF_TRACKED))
+                if (mdry(mb) && (fu & ESC_NF_TRACKED))
                     tr = (tn[u] == (int32_t)i && tg[u] == (int32_t)mg(mb)) || tracked(N, (int32_t)i, (int32_t)mg(mb));
                 const uint32_t mf = mdry(mb) ? ((fu & ~ESC_NF_TRACKED) | (tr ? ESC_NF_TRACKED : 0u)) : fu;
-                const uint64_t kw = ((uint64_t)mg(mb) << R) | ak;
+                const KT kw = ((KT)mg(mb) << R) | ak;
                 const uint32_t vw = (uint32_t)i | ((mf & 0xFu) << MEMB_FLAG_SHIFT);
-                if constexpr (ABL == 2 || ABL == 4) asm volatile("" :: "v"(kw), "v"(vw));
-                else {
-                    if (stage) { sk[pos] = kw; sv[pos] = vw; }
-                    else if (carry + pos < cap) { keys[carry + pos] = kw; vals[carry + pos] = vw; }
-                }
+                if (stage) { sk[pos] = kw; sv[pos] = vw; }
+                else if (carry + pos < cap) { keys[carry + pos] = kw; vals[carry + pos] = vw; }
                 ++pos;
             });
         }
         __syncthreads();
-        if (stage && ABL != 1 && ABL != 2 && ABL != 4)
+        if (stage)
             for (uint32_t e = threadIdx.x; e < total && carry + e < cap; e += MEMB_BLOCK) {
                 keys[carry + e] = sk[e];
                 vals[carry + e] = sv[e];
@@ -3002,28 +3037,34 @@ hipError_t launch_memb_count(const NodeDev& nd, const GroupDev& g, int nblk, uin
 }
 
 hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const uint32_t* base, int64_t n_memb,
-                           int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, uint64_t* keys[2], uint32_t* vals[2],
-                           uint32_t* hist, uint32_t* tot, const RegionSink& S, hipStream_t st) {
+                           int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, int coarse_shift,
+                           uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t* tot, const RegionSink& S,
+                           hipStream_t st) {
     const int64_t n = nd.hi - nd.lo;
-#if MK_ABL
-    // timing ablations: LDS staging without the write-out (1), no stores and no group walk
-    // in the count (2), no division (3), no stores (4), no tracker lookups (5); those that
-    // store are overwritten by the real listing that follows
-    if (n > 0) {
-        hipLaunchKernelGGL(k_memb_keys<1>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0], vals[0]);
-        hipLaunchKernelGGL(k_memb_keys<2>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0], vals[0]);
-        hipLaunchKernelGGL(k_memb_keys<3>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0], vals[0]);
-        hipLaunchKernelGGL(k_memb_keys<4>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0], vals[0]);
-        hipLaunchKernelGGL(k_memb_keys<5>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0], vals[0]);
+    if (coarse_shift < 0) {                          // exact 64-bit keys: group << R | offset
+        if (n > 0)
+            hipLaunchKernelGGL(k_memb_keys<uint64_t>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min,
+                               div, R, 0, keys[0], vals[0]);
+        if (n_memb > 0) {
+            int src = 0;
+            const hipError_t e = rs_sort<uint64_t, uint32_t>(keys, vals, n_memb, R + gbits, hist, tot, &src, S, st);
+            if (e != hipSuccess) return e;
+        }
+        return hipGetLastError();
     }
-#endif
+    // coarse 32-bit keys: group << (32 - gbits) | (offset >> coarse_shift), then k_age_fix
+    // orders each run of equal coarse keys by the exact creation time
+    uint32_t* k32[2] = {reinterpret_cast<uint32_t*>(keys[0]), reinterpret_cast<uint32_t*>(keys[1])};
     if (n > 0)
-        hipLaunchKernelGGL(k_memb_keys<0>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div, R, keys[0],
-                           vals[0]);
+        hipLaunchKernelGGL(k_memb_keys<uint32_t>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div,
+                           32 - gbits, coarse_shift, k32[0], vals[0]);
     if (n_memb > 0) {
         int src = 0;
-        const hipError_t e = rs_sort<uint64_t, uint32_t>(keys, vals, n_memb, R + gbits, hist, tot, &src, S, st);
+        const hipError_t e = rs_sort<uint32_t, uint32_t>(k32, vals, n_memb, 32, hist, tot, &src, S, st);
         if (e != hipSuccess) return e;
+        if (S.fix)                                   // the final pass's key output: k32[src]
+            hipLaunchKernelGGL(k_age_fix, dim3((unsigned)((n_memb + 255) / 256)), dim3(256), 0, st, k32[src], n_memb, S,
+                               nd.created, ts_min);
     }
     return hipGetLastError();
 }

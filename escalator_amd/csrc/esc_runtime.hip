@@ -260,6 +260,7 @@ struct esc_ctx {
     int64_t n_chunks = 0;
     uint64_t sort_div = 1;
     int sort_R = 1;
+    bool age_exact = false;                                   // this snapshot needs the exact 64-bit keys
     bool sorted = false;
     std::vector<int64_t> h_created;                           // [lo, hi) creation times (tie order)
     // node informer events (§8f rank 1): capacity and host mirrors for in-place add / delete
@@ -567,6 +568,7 @@ int32_t build_age_index(esc_ctx* c) {
     const bool fresh = !c->age_built;
     if (fresh) {
         c->age_n = nl;
+        c->age_exact = false;
         c->h_gn.clear();
         if (nl) {                                    // creation-time range of the node range
             c->ts_min = *std::min_element(c->h_created.begin(), c->h_created.end());
@@ -716,20 +718,31 @@ int32_t build_age_index(esc_ctx* c) {
     if (!chunks.empty()) HIP_TRY(hipMemcpy(c->d_chunks, chunks.data(), chunks.size() * sizeof(OrdChunk), hipMemcpyHostToDevice));
     if (!pchunks.empty())
         HIP_TRY(hipMemcpy(c->d_pchunks, pchunks.data(), pchunks.size() * sizeof(OrdChunk), hipMemcpyHostToDevice));
-    // the listing and the sort; its last pass writes the regions at the host's sorted starts
-    HIP_TRY(hipMemcpyAsync(c->d_seg, starts.data(), starts.size() * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemsetAsync(c->d_ierr, 0, 4, st));
+    // the listing and the sort; its last pass writes the regions at the host's sorted starts.
+    // Keys: 32-bit coarse keys — the group in the top gbits, the creation offset's top
+    // (32 - gbits) bits — when the groups leave at least 16 bits of time: four 8-bit LSD
+    // passes over 8-B (key, value) pairs instead of six over 12-B ones; if offset bits were
+    // dropped, k_age_fix orders the runs of equal coarse keys by the exact time, and a run
+    // too long for it sends the build back to the exact 64-bit keys.
     const int gbits = bit_width((uint64_t)std::max<int32_t>(g.G - 1, 1));
-    RegionSink sink{c->d_seg, c->d_pstart, c->d_plen, c->d_dry, c->d_g_memb, c->d_g_grp, c->d_ierr,
-                    g.G, c->sort_R};
-    HIP_TRY(launch_age_sort(n, g, c->memb_blocks, c->d_cnt, c->n_memb, c->mcap, c->ts_min, c->sort_div, c->sort_R,
-                            gbits, c->d_mkeys, c->d_mvals, c->d_hist, c->d_tot, sink, st));
-    HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_grp, c->d_g_memb, st));
-    if (check) {
+    for (int attempt = 0;; ++attempt) {
+        const bool coarse = !c->age_exact && gbits <= 16;
+        const int cshift = coarse ? std::max(0, c->sort_R - (32 - gbits)) : -1;
+        HIP_TRY(hipMemcpyAsync(c->d_seg, starts.data(), starts.size() * 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemsetAsync(c->d_ierr, 0, 4, st));
+        RegionSink sink{c->d_seg, c->d_pstart, c->d_plen, c->d_dry, c->d_g_memb, c->d_g_grp, c->d_ierr,
+                        g.G, coarse ? 32 - gbits : c->sort_R, cshift > 0 ? 1 : 0};
+        HIP_TRY(launch_age_sort(n, g, c->memb_blocks, c->d_cnt, c->n_memb, c->mcap, c->ts_min, c->sort_div, c->sort_R,
+                                gbits, cshift, c->d_mkeys, c->d_mvals, c->d_hist, c->d_tot, sink, st));
+        HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_grp, c->d_g_memb, st));
+        if (!check && cshift <= 0) break;
         uint32_t err = 0;
         HIP_TRY(hipMemcpyAsync(&err, c->d_ierr, 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        if (err) return fail_hip(hipErrorUnknown, "age index: membership count");
+        if (err & 1u) return fail_hip(hipErrorUnknown, "age index: membership count");
+        if (!(err & 2u)) break;
+        if (attempt) return fail_hip(hipErrorUnknown, "age index: exact rebuild");
+        c->age_exact = true;                        // a long run of equal coarse keys: exact keys
     }
     {   // after the sort's last pass, which reads d_seg as the groups' unpadded starts
         std::vector<int64_t> seg0((size_t)4 * g.G + 1);
@@ -3665,16 +3678,19 @@ int32_t relabel_apply(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, con
             ++c->pair_live[q];
             pair_touched[q] = 1;
         }
+        // the node's map: its live entries, then its retired ones (each once; patch_nodes
+        // skips them, and a later relabel back to their pair takes them again)
+        std::sort(dead.begin(), dead.end());
+        dead.erase(std::unique(dead.begin(), dead.end()), dead.end());
+        std::vector<uint32_t> list(keep);
+        list.insert(list.end(), dead.begin(), dead.end());
         const uint32_t slots = c->ne_off[j + 1] - c->ne_off[j];
-        if (keep.size() < slots && dead.empty()) {
-            regrow.emplace_back(j, keep);           // no retired entry left to fill the spare slots
-        } else if (keep.size() <= slots) {
-            // in place; the spare slots repeat a retired entry (there is one whenever a slot is
-            // spare: patch_nodes skips it, its occupancy word is never read)
+        if (list.size() <= slots && !list.empty() && (list.size() == slots || !dead.empty())) {
+            // in place; spare slots repeat a retired entry
             for (uint32_t k = 0; k < slots; ++k)
-                c->ne_pos[c->ne_off[j] + k] = k < keep.size() ? keep[k] : dead[0];
+                c->ne_pos[c->ne_off[j] + k] = k < list.size() ? list[k] : dead[0];
         } else {
-            regrow.emplace_back(j, keep);
+            regrow.emplace_back(j, list);
         }
         // extra labels: in place, or appended when the node has more of them now
         if (nx > onx) {
