@@ -352,15 +352,18 @@ def bench_order(args):
         ordering's working set (~130 MB of region words and orders) fits the 256 MB MALL, so
         back-to-back decisions would be MALL-served.  A 1 GiB write on the context's stream
         evicts it, then HIP events bracket the ordering kernels alone; mean over k."""
-        ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+        ctx.sync()
+        stream = torch.cuda.Stream()                  # a real stream (the default one's handle is 0)
+        ctx.set_stream(stream.cuda_stream)
         scrub = torch.empty(1 << 28, dtype=torch.int32, device="cuda")
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(k)]
-        for a, b in ev:
-            scrub.fill_(1)
-            a.record()
-            fn()
-            b.record()
-        torch.cuda.synchronize()
+        with torch.cuda.stream(stream):
+            for a, b in ev:
+                scrub.fill_(1)
+                a.record(stream)
+                fn()
+                b.record(stream)
+        stream.synchronize()
         ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
         del scrub
         ctx.set_stream(None)
@@ -412,8 +415,17 @@ def bench_order(args):
     # created 16 B), each membership written once (12 B: 8-B key, 4-B node | flags value),
     # LSD passes of <= 8 bits over the (group << R | creation offset) keys (hist: 8 B read;
     # scatter: 12 B read + 12 B written), the last pass writing the regions instead (12 B)
-    idx_passes = -(-(R + max(1, (G - 1).bit_length())) // 8)
-    index_bytes = N * 24 + n_memb * (12 + idx_passes * 32)
+    gbits = max(1, (G - 1).bit_length())
+    coarse = gbits <= 16                          # build_age_index: 32-bit coarse keys
+    if coarse:
+        # 8-B (key, value) pairs, four 8-bit passes (hist 4 B read; scatter 8 B read + 8 B
+        # written; the last pass 8 B read + 8 B region words + 4 B sorted keys), the run
+        # fix-up reading the keys once
+        idx_passes = 4
+        index_bytes = N * 24 + n_memb * (8 + 3 * 20 + (4 + 20) + 4)
+    else:
+        idx_passes = -(-(R + gbits) // 8)
+        index_bytes = N * 24 + n_memb * (12 + idx_passes * 32)
     out = {
         "metric": "config5 node orderings: memberships ordered/sec per decision (taint/untaint selection)",
         "value": n_memb / (order_ms * 1e-3),
@@ -439,7 +451,9 @@ def bench_order(args):
                                "around the ordering kernels alone",
                      "warm_ms": warm_ms, "frac_warm": order_bytes / (warm_ms * 1e-3) / 1e9 / (HBM_PEAK_GBS * world),
                      "warm_note": "back-to-back decisions; the ~130 MB working set may be served from the MALL"},
-        "age_index_build": {"ms": index_ms, "nodes_per_s": N / (index_ms * 1e-3), "key_bits": R,
+        "age_index_build": {"ms": index_ms, "nodes_per_s": N / (index_ms * 1e-3), "creation_offset_bits": R,
+                            "keys": ("32-bit coarse (group | top time bits) + exact fix-up of equal-key runs"
+                                     if coarse else "64-bit exact (group << R | offset)"),
                             "lsd_passes": idx_passes, "GBps_moved": index_bytes / (index_ms * 1e-3) / 1e9},
         "selection_merge_ms": sel_ms,
         "segments_nonempty": int(sum(1 for c in counts if c)),

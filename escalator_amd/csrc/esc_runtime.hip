@@ -2043,10 +2043,12 @@ int32_t esc_stage_times(esc_ctx* c, double* ms, int32_t n) {
 // workgroup's K phase took 1.14x the mean (odd XCDs ~5 % slower than even ones, plus a
 // within-XCD spread), and the per-workgroup durations correlate 0.9-0.98 between
 // decisions and 0.96-0.99 between processes (profiles/r02_v8/k1_trace_stability_*.json).
-// Each round runs three decisions, averages every workgroup's K-phase time (trace words 0-1) and
-// scales each share by sqrt(mean time / its time) (a damped step: a share that moves also
-// changes which tiles — classes of other costs — the workgroup streams); the plan with
-// the lowest slowest-workgroup time seen is kept.  The grid and the per-workgroup pod bound
+// Each round runs three decisions and averages every workgroup's start offset, K phase and
+// tail (trace words 0, 1, 3), then moves each share half-way to the one that would end every
+// workgroup at the same time under its measured streaming rate (round 5: balancing END
+// times, so the XCDs' dispatch stagger and the flush are paid for too — balancing the K
+// phases alone left the slowest workgroup ~2.5 us after the mean at a rank's shard); the
+// plan with the lowest slowest-workgroup end seen is kept.  The grid and the per-workgroup pod bound
 // do not change, and sums are order-independent, so every result is unchanged; the graphs
 // read the plan from device memory, so they stay valid.
 int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
@@ -2070,28 +2072,46 @@ int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
     };
     constexpr int REPS = 3;                              // decisions averaged per round (noise ~1-4 %)
     for (int32_t r = 0; r <= rounds; ++r) {
-        std::vector<double> t(nblk, 0.0);
+        // per workgroup: its start offset from the grid's first start (the XCDs are dispatched
+        // ~1.4 us apart, the same XCD order every launch), its K phase, and what follows it
+        // (C tiles, the compact flush), averaged over REPS decisions
+        std::vector<double> st(nblk, 0.0), kp(nblk, 0.0), tl(nblk, 0.0);
         for (int k = 0; k < REPS; ++k) {
             rc = c->world == 1 ? esc_run(c) : esc_reduce(c);
             if (!rc) rc = esc_sync(c);
             if (rc) return rc;
             HIP_TRY(hipMemcpy(tr.data(), c->d_k1_trace, tr.size() * 8, hipMemcpyDeviceToHost));
+            uint64_t t0 = tr[0];
+            for (int64_t b = 0; b < nblk; ++b) t0 = std::min<uint64_t>(t0, tr[b * 8 + 0]);
             for (int64_t b = 0; b < nblk; ++b) {
                 const double d = (double)(int64_t)(tr[b * 8 + 1] - tr[b * 8 + 0]);
                 if (!(d > 0)) return ESC_OK;            // no K phase measured: keep the plan
-                t[b] += d / REPS;
+                st[b] += (double)(int64_t)(tr[b * 8 + 0] - t0) / REPS;
+                kp[b] += d / REPS;
+                tl[b] += std::max(0.0, (double)(int64_t)(tr[b * 8 + 3] - tr[b * 8 + 1])) / REPS;
             }
         }
-        double mean = 0, mx = 0;
+        // the grid ends with its last workgroup: balance END times (start + K phase + tail),
+        // not K phases — a workgroup of a late XCD or with a long flush gets less weight
+        double mx = 0, rsum = 0, rfix = 0;
         for (int64_t b = 0; b < nblk; ++b) {
-            mean += t[b] / (double)nblk;
-            mx = std::max(mx, t[b]);
+            mx = std::max(mx, st[b] + kp[b] + tl[b]);
+            const double rate = share[b] / kp[b];        // share per tick while streaming
+            rsum += rate;
+            rfix += rate * (st[b] + tl[b]);
         }
         if (best.empty() || mx < best_max) { best = share; best_max = mx; }
         if (r == rounds) break;
+        // shares that would end every workgroup at the same time T under the measured rates
+        // (sum = 1), half-way from the current ones (the rates move with the tiles a share
+        // takes)
+        const double T = (1.0 + rfix) / rsum;
         std::vector<double> next(nblk);
         double sum = 0;
-        for (int64_t b = 0; b < nblk; ++b) sum += (next[b] = share[b] * std::sqrt(mean / t[b]));
+        for (int64_t b = 0; b < nblk; ++b) {
+            const double want = std::max(0.25 * share[b], share[b] / kp[b] * (T - st[b] - tl[b]));
+            sum += (next[b] = 0.5 * share[b] + 0.5 * want);
+        }
         for (double& x : next) x /= sum;
         if (upload(next) != ESC_OK) break;               // outside the exactness bound: stop here
         share = next;

@@ -75,10 +75,10 @@ prof() {       # name
     timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$name -o run \
         -- python3 bench.py $a > $OUT/trace_$name.log 2>&1 || { tail -20 $OUT/trace_$name.log; return 1; }
     echo "[gpu] $(date +%T) prof $name: pmc FETCH_SIZE"
-    timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "(^| )k_" --output-format csv -d $OUT/fetch_$name -o run \
+    timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "(^|[ :])k_" --output-format csv -d $OUT/fetch_$name -o run \
         -- python3 bench.py $a --no-cpu-baseline --no-host > $OUT/fetch_$name.log 2>&1 || { tail -20 $OUT/fetch_$name.log; return 1; }
     echo "[gpu] $(date +%T) prof $name: pmc WRITE_SIZE"
-    timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "(^| )k_" --output-format csv -d $OUT/write_$name -o run \
+    timeout -s KILL 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "(^|[ :])k_" --output-format csv -d $OUT/write_$name -o run \
         -- python3 bench.py $a --no-cpu-baseline --no-host > $OUT/write_$name.log 2>&1 || { tail -20 $OUT/write_$name.log; return 1; }
     local tr st fe wr
     tr=$(find $OUT/trace_$name -name "run_kernel_trace.csv" | head -1)
@@ -99,7 +99,7 @@ for src, dst, cols in ((tr, "kernel_trace.csv", ["Kernel_Name", "Dispatch_Id", "
         w = csv.writer(g)
         w.writerow(cols)
         for r in csv.DictReader(f):
-            if r["Kernel_Name"].replace("void ", "").startswith("k_"):
+            if r["Kernel_Name"].replace("void ", "").replace("esc::", "").startswith("k_"):
                 w.writerow([r[c] for c in cols])
 PY
     python3 scripts/prof_summary.py --trace $PROF/raw_$name/kernel_trace.csv --fetch $PROF/raw_$name/pmc_fetch.csv \
@@ -112,7 +112,7 @@ pmcsq() {      # name: one SQ counter pass (<= 8 SQ counters)
     a=$(args_of $name) || return 1
     echo "[gpu] $(date +%T) pmc SQ $name"
     timeout -s KILL 400 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU \
-        SQ_INSTS_LDS SQ_INSTS_VMEM_RD --kernel-include-regex "(^| )k_" --output-format csv -d $OUT/sq_$name -o run \
+        SQ_INSTS_LDS SQ_INSTS_VMEM_RD --kernel-include-regex "(^|[ :])k_" --output-format csv -d $OUT/sq_$name -o run \
         -- python3 bench.py $a --no-cpu-baseline --no-host > $OUT/sq_$name.log 2>&1 || { tail -20 $OUT/sq_$name.log; return 1; }
     find $OUT/sq_$name -name "run_counter_collection.csv" -exec cp {} $PROF/pmc_sq_$name.csv \;
 }
