@@ -185,9 +185,10 @@ def stage_layout(world: int, shard_world: int, multi, backend: str) -> list[str]
         names.append("d2h")
     if multi or (world == 1 and shard_world == 1):
         return names                              # K4 inside k_node_groups (device 0's events)
+    names = names[:3] + names[4:]                 # node groups run with K4, after the exchange
     if world > 1:
         names.append("exchange" if backend == "nccl" else "exchange_host_staged")
-    return names + ["k_decide"]
+    return names + ["k_node_groups+decide"]
 
 
 def check_parity(args, ctx, s, multi, rank, world, backend, dist, P, N, G, n_gpus):
@@ -799,7 +800,7 @@ def main():
         "stage_note": ("HIP events between the step's launches, timing mode (each event pair adds a few us); "
                        "k_order_split launches nothing when every group is packed into the tail (config 4); "
                        "exchange = the in-place ncclReduceScatter of the owner-major pod words (DESIGN.md §7), "
-                       "k_decide = K4 over the rank's own groups"),
+                       "k_node_groups+decide = the rank's own groups' node words and K4, after the exchange"),
         "ordering": None if args.no_order else {
             "kernels": "groups of <= 1024 memberships packed as blocks of k_step_tail (one pass); larger groups by k_ord_count + k_ord_scatter after it; all on the context's one stream (esc_set_order_in_step)",
             "memberships": n_memb, "algorithmic_bytes": n_memb * 16},

@@ -397,14 +397,14 @@ struct DecCompact;
 struct K1Diag {
     uint64_t* trace;
 };
-// k_node_groups' decision (one rank without an exchange): null dec = the node words only
-// (nwords), which k_decide reads after the exchange.
+// k_node_groups' decision target: null dec = the node words only (a reduce that was never
+// decided, esc_reduce).
 struct NGDecide {
     const int64_t* pwords;
     esc_group_decision* dec;
     DecCompact* cdec;
 };
-// The groups a launch of k_node_groups / k_decide covers: ids[i] for i < n, or, with null
+// The groups a launch of k_node_groups covers: ids[i] for i < n, or, with null
 // ids, the contiguous run first + i (a rank's owned groups).
 struct GroupList {
     const uint32_t* ids;
@@ -429,13 +429,8 @@ struct DecCompact {
 };
 static_assert(sizeof(DecCompact) == 32, "compact decision is 2 x 16 B");
 
-// K2b + K4 (k_node_groups): every group's final node words from K2's piece rows, then
-// (nd.dec != null) the decisions.  K4 alone (k_decide): after an exchange.
-// k_decide reads the owned groups' exchanged pod words (pwords: row i for the list's group
-// i, the owner's slice after the reduce-scatter) and their node words (nwords, G x NW_K,
-// written by k_node_groups on the owner).
-hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const GroupList& list, const int64_t* pwords,
-                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st);
+// K2b + K4 (k_node_groups): the listed groups' final node words from K2's piece rows, then
+// (nd.dec != null) their decisions (K4) from the pod words at rows xs[g] (or g).
 // Peer exchange of a multi-device context (esc_ctx_create_multi): dst[i] = sum of src[k][i]
 // over the n_src buffers (peer-mapped device memory), int64 or uint32 words.
 hipError_t launch_peer_sum64(const int64_t* const* src, int n_src, int64_t* dst, int64_t n, hipStream_t st);

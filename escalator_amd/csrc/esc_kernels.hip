@@ -1448,11 +1448,10 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 // groups take the filterNodes classes, dry groups (controller.go:126-138) every member as
 // untainted (cordoned ones included) except the tracked members (K2's tracker sums, read
 // and reset here).  64 groups per block, the 4 waves split each group's pieces.  A rank
-// reduces only the pieces of the pairs it owns, so a group's words are exact on its owner
-// and zero elsewhere.  With a decision target (D.dec: one rank, no exchange) the block then
-// decides its groups (K4 on this rank's fold) and writes the compact records to the
-// decision buffer as one contiguous run; otherwise it writes the words to the exchange
-// buffer (D.nx) and k_decide runs after the SUM.
+// reduces only the pieces of the pairs it owns and runs this over its own groups only.
+// With a decision target (D.dec) the block then decides its groups (K4: at one rank on its
+// fold, at several after the exchange) and writes the compact records to the decision
+// buffer.
 constexpr int NG_WAVES = 4;
 
 namespace {
@@ -1580,10 +1579,10 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
 // and reset here).  64 groups per block, the 4 waves split each group's pieces.  A rank
 // reduces only the pieces of the pairs it owns, so a group's words are exact on its owner
 // and zero elsewhere.  With a decision target (D.dec: one rank, no exchange) the block then
-// decides its groups (K4 on this rank's fold) and writes the compact records to the
-// decision buffer as one contiguous run; otherwise it writes only the node words and
-// k_decide runs after the exchange.  With several ranks a launch covers the rank's OWN
-// groups (the list): the others' node words are their owners' to compute.
+// decides its groups (K4) and writes the compact records to the decision buffer as one
+// contiguous run; otherwise it writes only the node words.  With several ranks it runs
+// after the exchange (esc_decide), over the rank's OWN groups (the list),
+// their pod words at rows xs[g] of the reduce-scattered buffer.
 // (Running this work inside k_step_tail's fold blocks measured slower)
 __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeDev N, GroupList L,
                                                                const int64_t* __restrict__ node_rows,
@@ -1594,36 +1593,6 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
     const uint32_t n = L.n - i0 < 64 ? (uint32_t)(L.n - i0) : 64u;
     const uint32_t g = i >= L.n ? NONE : L.ids ? L.ids[i] : (uint32_t)(L.first + i);
     node_groups_part(G, N, node_rows, trk_acc, nwords, D, g, !L.ids, L.first + i0, n);
-}
-
-// K4 alone (esc_decide after an exchange), for the rank's OWN groups only:
-// their pod words are the owner's slice of the reduce-scatter (row i for list group i),
-// their node words the owner's own (k_node_groups).  Only the owned decisions cross PCIe.
-// One wave per 64 groups (a latency chain per group: 40 blocks of 256 threads left most CUs
-// idle, 8.5 us for 10 k groups).
-constexpr int KD_BLOCK = 64;
-__global__ __launch_bounds__(KD_BLOCK) void k_decide(GroupDev G, NodeDev N, GroupList L,
-                                                     const int64_t* __restrict__ pwords,
-                                                     const int64_t* __restrict__ nwords,
-                                                     esc_group_decision* __restrict__ dec, DecCompact* __restrict__ cdec) {
-    __shared__ DecCompact sc[KD_BLOCK];
-    __shared__ uint32_t sid[KD_BLOCK];
-    const int32_t i0 = blockIdx.x * KD_BLOCK, i = i0 + (int32_t)threadIdx.x;
-    if (i < L.n) {
-        const int32_t g = L.ids ? (int32_t)L.ids[i] : L.first + i;
-        int64_t v[NW_K];
-        const int64_t* nw = nwords + (int64_t)g * NW_K;
-#pragma unroll
-        for (int k = 0; k < NW_K; ++k) v[k] = nw[k];
-        esc_group_decision d;
-        finalize(G, N.gnode[g], g, pwords + (int64_t)i * PW_K, v, d, G.metrics);
-        store_full(dec + g, d);
-        sc[threadIdx.x] = compact_of(d);
-        sid[threadIdx.x] = (uint32_t)g;
-    }
-    __syncthreads();
-    const uint32_t n = L.n - i0 < KD_BLOCK ? (uint32_t)(L.n - i0) : (uint32_t)KD_BLOCK;
-    store_compact(cdec, sc, n, !L.ids, (uint32_t)(L.first + i0), sid, threadIdx.x, KD_BLOCK);
 }
 
 // K3 fold (fold_col, a role of k_step_tail): the K1 workgroups' slot partials folded and
@@ -2869,14 +2838,6 @@ hipError_t launch_node_groups(const GroupDev& g, const NodeDev& n, const GroupLi
     if (list.n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_node_groups, dim3((list.n + 63) / 64), dim3(NG_WAVES * 64), 0, st, g, n, list, node_rows,
                        trk_acc, nwords, nd);
-    return hipGetLastError();
-}
-
-hipError_t launch_decide(const GroupDev& g, const NodeDev& n, const GroupList& list, const int64_t* pwords,
-                         const int64_t* nwords, esc_group_decision* dec, DecCompact* cdec, hipStream_t st) {
-    if (list.n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_decide, dim3((list.n + KD_BLOCK - 1) / KD_BLOCK), dim3(KD_BLOCK), 0, st, g, n, list, pwords,
-                       nwords, dec, cdec);
     return hipGetLastError();
 }
 

@@ -220,6 +220,9 @@ struct esc_ctx {
     // (ESC_E_STATE) until the snapshot is reloaded (STALE_PODS: esc_load_pods, STALE_NODES:
     // esc_load_nodes).  ADVICE r4.
     uint32_t stale = 0;
+    // world > 1: a shard step's node groups run with K4 after the exchange (esc_decide); a
+    // reduce not followed by a decide leaves them pending (the tail's tracker sums unread)
+    bool ng_pending = false;
     bool force_wide = false;
     int k1_variant = 0;                                       // ESC_K1_VARIANT (measurement knob)
     // K pods of a class are laid out in order of pair0 / pod_sort (0: input order), so that a
@@ -1171,12 +1174,14 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     }
     if (int32_t rc = mark()) return rc;
     // D reads and resets the tracker sums the tail accumulated (once per step), for this
-    // rank's own groups; a sharded step (no decide) computes their node words only and
-    // esc_decide runs K4 on them after the exchange
-    NGDecide nd{nullptr, nullptr, nullptr};
-    if (decide) nd = NGDecide{c->d_pwords, c->d_dec, cdec};
-    HIP_TRY(launch_node_groups(g, n, own_list(c), c->nodes.rows, c->d_trk_acc, c->d_nwords, nd, st));
-    if (int32_t rc = mark()) return rc;
+    // rank's own groups, and decides them (K4).  A sharded step (no decide) stops before D:
+    // the node groups do not depend on the exchange, so they run with K4 after it in ONE
+    // launch (esc_decide) — one kernel boundary less on the rank's critical path.
+    if (decide) {
+        HIP_TRY(launch_node_groups(g, n, own_list(c), c->nodes.rows, c->d_trk_acc, c->d_nwords,
+                                   NGDecide{c->d_pwords, c->d_dec, cdec}, st));
+        if (int32_t rc = mark()) return rc;
+    }
     if (copy_out && !c->zero_copy) {
         HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)g.G * sizeof(DecCompact), hipMemcpyDeviceToHost, st));
         if (int32_t rc = mark()) return rc;
@@ -2195,6 +2200,12 @@ int32_t esc_reduce(esc_ctx* c) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
     hipSetDevice(c->device);
+    if (c->ng_pending) {                               // the previous reduce was not decided:
+        // its node groups consume its tracker sums now (no decisions), so no step's sums mix
+        HIP_TRY(launch_node_groups(group_dev(c), node_dev(c), own_list(c), c->nodes.rows, c->d_trk_acc, c->d_nwords,
+                                   NGDecide{nullptr, nullptr, nullptr}, c->stream));
+    }
+    c->ng_pending = true;
     const int r = c->cur;
     c->cur = (c->cur + 1) % (int)c->pods.size();
     c->pending = true;
@@ -2283,9 +2294,12 @@ int32_t esc_decide(esc_ctx* c) {
     int32_t rc = check_ready(c);
     if (rc) return rc;
     hipSetDevice(c->device);
-    // K4 over this rank's own groups: its slice of the exchanged pod words, its node words
-    HIP_TRY(launch_decide(group_dev(c), node_dev(c), own_list(c), own_xwords(c), c->d_nwords, c->d_dec,
-                          c->zero_copy ? c->h_cdec_dev : c->d_cdec, c->stream));
+    // node groups + K4 over this rank's own groups: their node words from K2's piece rows
+    // (the tracker sums of the step), their exchanged pod words (the rank's slice, rows xs[g])
+    if (!c->ng_pending) return ESC_E_STATE;            // nothing reduced since the last decide
+    HIP_TRY(launch_node_groups(group_dev(c), node_dev(c), own_list(c), c->nodes.rows, c->d_trk_acc, c->d_nwords,
+                               NGDecide{c->d_pwords, c->d_dec, c->zero_copy ? c->h_cdec_dev : c->d_cdec}, c->stream));
+    c->ng_pending = false;
     if (!c->zero_copy)
         HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)c->gi.G * sizeof(DecCompact), hipMemcpyDeviceToHost,
                                c->stream));

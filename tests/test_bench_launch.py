@@ -61,9 +61,9 @@ def test_parity_mismatch_fails_the_run(capsys):
 
 def test_stage_layout_names_every_event():
     """The timing-mode stages the bench line reports at each shape."""
-    base = ["k_pod_reduce", "k_step_tail", "k_order_split", "k_node_groups"]
-    assert bench.stage_layout(1, 1, None, "nccl") == base
-    assert bench.stage_layout(1, 8, None, "nccl") == base + ["k_decide"]            # --shard-of 8
-    assert bench.stage_layout(8, 8, None, "nccl") == base + ["exchange", "k_decide"]
-    assert bench.stage_layout(2, 2, None, "gloo") == base + ["exchange_host_staged", "k_decide"]
-    assert bench.stage_layout(1, 1, [0, 1], "multi") == base
+    base = ["k_pod_reduce", "k_step_tail", "k_order_split"]
+    assert bench.stage_layout(1, 1, None, "nccl") == base + ["k_node_groups"]
+    assert bench.stage_layout(1, 8, None, "nccl") == base + ["k_node_groups+decide"]            # --shard-of 8
+    assert bench.stage_layout(8, 8, None, "nccl") == base + ["exchange", "k_node_groups+decide"]
+    assert bench.stage_layout(2, 2, None, "gloo") == base + ["exchange_host_staged", "k_node_groups+decide"]
+    assert bench.stage_layout(1, 1, [0, 1], "multi") == base + ["k_node_groups"]
