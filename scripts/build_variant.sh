@@ -16,4 +16,4 @@ if [ -n "$REBUILD_RT" ]; then            # flags that change the runtime's view 
     RT=$B/esc_runtime.o
 fi
 $HIPCC --offload-arch=gfx950 -shared -fPIC -o ../libescalator_hip_$NAME.so $B/esc_kernels.o $RT \
-    $O/esc_multi.o $O/esc_kernels_p1.o $O/esc_pack.o $O/esc_synth.o -pthread
+    $O/esc_multi.o $O/esc_list.o $O/esc_pack.o $O/esc_synth.o -pthread

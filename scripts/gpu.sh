@@ -11,6 +11,9 @@
 #                    to $OUT/profiles/summary_NAME.json.  NAME: full (config 4), shard8, config5
 #   pmcsq:NAME       SQ counter pass (one --pmc run) of the same command
 #   py:SCRIPT        python3 scripts/SCRIPT (e.g. k1_trace.py), output to $OUT
+#   variants:A,B,..  A/B timing of library builds (scripts/build_variant.sh NAME ...:
+#                    escalator_amd/libescalator_hip_NAME.so; "base" = the product library):
+#                    rank 0 of 8 and config 4, each in turn, twice
 # usage: TAG=r05a scripts/gpu.sh suite bench prof:shard8
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -117,6 +120,27 @@ pmcsq() {      # name: one SQ counter pass (<= 8 SQ counters)
     find $OUT/sq_$name -name "run_counter_collection.csv" -exec cp {} $PROF/pmc_sq_$name.csv \;
 }
 
+variants() {   # comma-separated names
+    local v lib
+    for rep in 1 2; do
+        for v in ${1//,/ }; do
+            lib=$PWD/escalator_amd/libescalator_hip_$v.so
+            [ "$v" = base ] && lib=$PWD/escalator_amd/libescalator_hip.so
+            echo "[gpu] $(date +%T) variant $v (rep $rep)"
+            ESC_LIB_PATH=$lib timeout -k 10 300 python3 -u bench.py --shard-of 8 --steps 50 --warmup 10 --no-cpu-baseline \
+                > $OUT/var_${v}_shard8_$rep.json 2> $OUT/var_${v}_shard8_$rep.err || { tail $OUT/var_${v}_shard8_$rep.err; return 1; }
+            ESC_LIB_PATH=$lib timeout -k 10 400 python3 -u bench.py --steps $STEPS --warmup 5 --no-cpu-baseline --no-host \
+                --no-parity > $OUT/var_${v}_full_$rep.json 2> $OUT/var_${v}_full_$rep.err || { tail $OUT/var_${v}_full_$rep.err; return 1; }
+            python3 -c "
+import json
+for n in ('shard8', 'full'):
+    d = json.load(open('$OUT/var_${v}_%s_$rep.json' % n))
+    print('  $v', n, 'step %.4f ms' % d['ms_per_step'], 'K1 %.4f ms' % d['roofline']['launch_ms'],
+          {k: round(x * 1e3, 1) for k, x in (d.get('stage_ms') or {}).items()})"
+        done
+    done
+}
+
 for stage in "$@"; do
     case $stage in
         suite) suite || exit 1 ;;
@@ -124,6 +148,7 @@ for stage in "$@"; do
         rehearse2) rehearse2 || exit 1 ;;
         prof:*) prof ${stage#prof:} || exit 1 ;;
         pmcsq:*) pmcsq ${stage#pmcsq:} || exit 1 ;;
+        variants:*) variants ${stage#variants:} || exit 1 ;;
         py:*) timeout -k 10 600 python3 -u scripts/${stage#py:} > $OUT/${stage#py:}.out 2>&1 || { tail -20 $OUT/${stage#py:}.out; exit 1; } ;;
         *) echo "unknown stage $stage"; exit 2 ;;
     esac

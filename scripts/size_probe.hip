@@ -88,7 +88,7 @@ int main() {
     printf("{\"cus\": %d, \"empty_ms\": %.4f, \"sizes\": [", cus,
            med([&](int) { hipLaunchKernelGGL(k_empty, dim3(cus), dim3(512), 0, 0, out); }));
     bool first = true;
-    for (int64_t mb : {32ll, 64ll, 128ll, 300ll, 600ll, 1200ll, 2400ll}) {
+    for (int64_t mb : {32ll, 64ll, 124ll, 248ll, 500ll, 1000ll, 2400ll}) {
         const int64_t bytes = mb << 20, n16 = bytes / 16, nbuf = std::max<int64_t>(1, total / bytes);
         auto at = [&](int r) { return base + (r % nbuf) * n16; };
         const float r4 = med([&](int r) { hipLaunchKernelGGL((k_read<4, false>), dim3(cus), dim3(512), 0, 0, at(r), n16, part, out); });
