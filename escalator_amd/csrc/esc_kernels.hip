@@ -1860,6 +1860,16 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scan_tot(uint32_t* __restrict
 // into its group's region: pstart[g] + p - seg[g].  The sorted starts seg are the host's
 // (live entries per pair); a position outside the group's [0, len) means the device listed a
 // different count, and is flagged in *err instead of written.
+// (value-less sorts carry the value in a packed element's low 32 bits, the key above it)
+struct NoVal {};
+template <class KT, class VT>
+struct RsElem {
+    static constexpr bool HASV = true;
+};
+template <class KT>
+struct RsElem<KT, NoVal> {
+    static constexpr bool HASV = false;
+};
 __device__ __forceinline__ void region_put(const RegionSink& S, uint32_t p, uint64_t key, uint32_t v) {
     const uint32_t g = (uint32_t)(key >> S.R);
     const int64_t r = (int64_t)p - S.seg[g];
@@ -1884,13 +1894,14 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
                                                            int64_t n, int shift, const uint32_t* __restrict__ hist,
                                                            const uint32_t* __restrict__ tot, RegionSink sink) {
     constexpr int NB = 1 << BITS, S = RS_U * SORT_WAVES, CH = RS_U * SORT_BLOCK;
+    constexpr bool HASV = RsElem<KT, VT>::HASV;          // else: packed (key << 32 | value) elements
     static_assert(NB <= SORT_BLOCK, "one thread per digit");
     __shared__ uint32_t run[NB];                         // output position of the digit's next key
     __shared__ uint32_t lst[NB];                         // the digit's first slot in the chunk
     __shared__ uint32_t wh[S][NB];                       // (round, wave) digit counts -> offsets
     __shared__ uint32_t ws[SORT_WAVES];
     __shared__ KT sk[CH];
-    __shared__ VT sv[CH];
+    __shared__ VT sv[HASV ? CH : 1];
     // Whole lines per digit run (non-FINAL passes): a chunk writes each digit's keys only up
     // to the last 16-key boundary of its run (16 keys = one 128-B line of 8-B keys, half a
     // line of 4-B values) and carries the rest in LDS to the front of that digit's run in
@@ -1901,7 +1912,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
     constexpr bool CARRY = !FINAL && ESC_RS_CARRY;
     constexpr int CW = 16, CD = CARRY ? NB : 1;
     __shared__ KT ck[CD][CW];
-    __shared__ VT cv[CD][CW];
+    __shared__ VT cv[HASV ? CD : 1][CW];
     __shared__ uint32_t c_n[CD], c_s[CD], c_e[CD];        // carry count, carry start, write end
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, t = threadIdx.x;
     if (t < NB) run[t] = tot[t] + hist[(int64_t)t * gridDim.x + blockIdx.x];
@@ -1917,7 +1928,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
     for (int u = 0; u < RS_U; ++u) {
         const int64_t i = lo + u * SORT_BLOCK + t;
         key[u] = i < hi ? kin[i] : (KT)0;
-        val[u] = i < hi ? vin[i] : (VT)0;
+        if constexpr (HASV) val[u] = i < hi ? vin[i] : (VT)0;
     }
     __syncthreads();
     for (int64_t b = lo; b < hi; b += CH) {
@@ -1964,7 +1975,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
             if (ok[u]) {
                 const uint32_t s = lst[d[u]] + wh[u * SORT_WAVES + wid][d[u]] + r[u];
                 sk[s] = key[u];
-                sv[s] = val[u];
+                if constexpr (HASV) sv[s] = val[u];
             }
         // the previous carry: written when below this chunk's write end, else kept (it moves
         // to the front of the new carry, after every thread has read the old one)
@@ -1980,12 +1991,12 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
                 keep[q] = false;
                 if (dg < CD && j < (int)c_n[dg]) {
                     okk[q] = ck[dg][j];
-                    ovv[q] = cv[dg][j];
+                    if constexpr (HASV) ovv[q] = cv[dg][j];
                     opos[q] = c_s[dg] + (uint32_t)j;
                     odig[q] = (uint32_t)dg;
                     if (opos[q] < c_e[dg]) {
                         kout[opos[q]] = okk[q];
-                        vout[opos[q]] = ovv[q];
+                        if constexpr (HASV) vout[opos[q]] = ovv[q];
                     } else {
                         keep[q] = true;
                     }
@@ -1998,7 +2009,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
             for (int q = 0; q < CN; ++q)
                 if (keep[q]) {
                     ck[odig[q]][opos[q] - c_e[odig[q]]] = okk[q];
-                    cv[odig[q]][opos[q] - c_e[odig[q]]] = ovv[q];
+                    if constexpr (HASV) cv[odig[q]][opos[q] - c_e[odig[q]]] = ovv[q];
                 }
         }
         // the next chunk's keys in flight during the write-out
@@ -2006,7 +2017,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
         for (int u = 0; u < RS_U; ++u) {
             const int64_t i = b + CH + u * SORT_BLOCK + t;
             key[u] = i < hi ? kin[i] : (KT)0;
-            val[u] = i < hi ? vin[i] : (VT)0;
+            if constexpr (HASV) val[u] = i < hi ? vin[i] : (VT)0;
         }
         const int cn = (int)imin64(CH, hi - b);
         for (int e = t; e < cn; e += SORT_BLOCK) {
@@ -2014,15 +2025,20 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
             const uint32_t dd = (uint32_t)(kk >> shift) & (NB - 1);
             const uint32_t g = run[dd] + (uint32_t)e - lst[dd];
             if constexpr (FINAL) {
-                region_put(sink, g, kk, sv[e]);
-                if (sink.fix) kout[g] = kk;                      // coarse keys: k_age_fix reads them
+                if constexpr (HASV) {
+                    region_put(sink, g, kk, sv[e]);
+                    if (sink.fix) kout[g] = kk;                  // coarse keys: k_age_fix reads them
+                } else {                                         // packed: key << 32 | value
+                    region_put(sink, g, (uint64_t)kk >> 32, (uint32_t)kk);
+                    if (sink.fix) reinterpret_cast<uint32_t*>(kout)[g] = (uint32_t)((uint64_t)kk >> 32);
+                }
             }
             else if (!CARRY || g < c_e[dd]) {
                 kout[g] = kk;
-                vout[g] = sv[e];
+                if constexpr (HASV) vout[g] = sv[e];
             } else {                                     // the run's partial last line: carried
                 ck[dd][g - c_e[dd]] = kk;
-                cv[dd][g - c_e[dd]] = sv[e];
+                if constexpr (HASV) cv[dd][g - c_e[dd]] = sv[e];
             }
         }
         for (int e = t; e < S * NB; e += SORT_BLOCK) (&wh[0][0])[e] = 0;
@@ -2201,10 +2217,12 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_scan_small(uint32_t* __restrict_
 // flags << MEMB_FLAG_SHIFT — a dry group's membership carries "tracked by this group" in
 // the tracker bit (controller.go:126-138), so the per-decision split needs no lookup.  KT =
 // uint64_t with KS = 0 (the exact key), or uint32_t (the coarse key, launch_age_sort).
-template <class KT>
+template <class KT, bool PACK = false>
 __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G, int64_t n, const uint32_t* __restrict__ base,
                                                           int64_t cap, int64_t ts_min, uint64_t div, int R, int KS,
                                                           KT* __restrict__ keys, uint32_t* __restrict__ vals) {
+    // PACK: one 8-B element per membership, the 32-bit coarse key above the value (keys is
+    // uint64_t*, vals unused)
     // A round's memberships are staged in LDS and written out as two contiguous streams:
     // stored straight from the walk, a wave's 8-B stores land ~4 entries apart per lane and
     // the listing took 5x its store-free time (measured, r03_mk).
@@ -2260,10 +2278,11 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
                 if (mdry(mb) && (fu & ESC_NF_TRACKED))
                     tr = (tn[u] == (int32_t)i && tg[u] == (int32_t)mg(mb)) || tracked(N, (int32_t)i, (int32_t)mg(mb));
                 const uint32_t mf = mdry(mb) ? ((fu & ~ESC_NF_TRACKED) | (tr ? ESC_NF_TRACKED : 0u)) : fu;
-                const KT kw = ((KT)mg(mb) << R) | ak;
                 const uint32_t vw = (uint32_t)i | ((mf & 0xFu) << MEMB_FLAG_SHIFT);
-                if (stage) { sk[pos] = kw; sv[pos] = vw; }
-                else if (carry + pos < cap) { keys[carry + pos] = kw; vals[carry + pos] = vw; }
+                const KT kw = PACK ? (KT)(((uint64_t)(((uint32_t)mg(mb) << R) | (uint32_t)ak) << 32) | vw)
+                                   : (((KT)mg(mb) << R) | ak);
+                if (stage) { sk[pos] = kw; if (!PACK) sv[pos] = vw; }
+                else if (carry + pos < cap) { keys[carry + pos] = kw; if (!PACK) vals[carry + pos] = vw; }
                 ++pos;
             });
         }
@@ -2271,7 +2290,7 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
         if (stage)
             for (uint32_t e = threadIdx.x; e < total && carry + e < cap; e += MEMB_BLOCK) {
                 keys[carry + e] = sk[e];
-                vals[carry + e] = sv[e];
+                if (!PACK) vals[carry + e] = sv[e];
             }
         carry += total;
         __syncthreads();
@@ -2952,13 +2971,14 @@ hipError_t rs_pass(const KT* kin, const VT* vin, KT* kout, VT* vout, int64_t n, 
 // narrower digits cost the scatter fewer LDS histogram words per element at equal traffic.
 template <class KT, class VT>
 hipError_t rs_sort(KT* keys[2], VT* vals[2], int64_t n, int bits, uint32_t* hist, uint32_t* tot, int* src,
-                   const RegionSink& S, hipStream_t st) {
+                   const RegionSink& S, hipStream_t st, int lo_bit = 0) {
     *src = 0;
     // digits of at most 8 bits (9-bit digits were measured: the scatter's per-chunk digit
-    // bookkeeping grows with the bins, 5 passes of 8-9 bits took longer than 6 of 6-7)
+    // bookkeeping grows with the bins, 5 passes of 8-9 bits took longer than 6 of 6-7);
+    // the key is bits [lo_bit, lo_bit + bits) of the element
     const int passes = (bits + 7) / 8;
-    for (int p = 0, shift = 0; p < passes; ++p) {
-        const int w = (bits - shift + (passes - p) - 1) / (passes - p);
+    for (int p = 0, shift = lo_bit; p < passes; ++p) {
+        const int w = (lo_bit + bits - shift + (passes - p) - 1) / (passes - p);
         hipError_t e;
         KT *ki = keys[*src], *ko = keys[*src ^ 1];
         VT *vi = vals[*src], *vo = vals[*src ^ 1];
@@ -3013,19 +3033,21 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const
         }
         return hipGetLastError();
     }
-    // coarse 32-bit keys: group << (32 - gbits) | (offset >> coarse_shift), then k_age_fix
-    // orders each run of equal coarse keys by the exact creation time
-    uint32_t* k32[2] = {reinterpret_cast<uint32_t*>(keys[0]), reinterpret_cast<uint32_t*>(keys[1])};
+    // coarse 32-bit keys: group << (32 - gbits) | (offset >> coarse_shift), packed with the
+    // value into ONE 8-B element (key << 32 | value: one stream, whole 128-B lines per carried
+    // digit run), sorted on the element's top 32 bits; then k_age_fix orders each run of
+    // equal coarse keys by the exact creation time
     if (n > 0)
-        hipLaunchKernelGGL(k_memb_keys<uint32_t>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min, div,
-                           32 - gbits, coarse_shift, k32[0], vals[0]);
+        hipLaunchKernelGGL((k_memb_keys<uint64_t, true>), dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min,
+                           div, 32 - gbits, coarse_shift, keys[0], nullptr);
     if (n_memb > 0) {
         int src = 0;
-        const hipError_t e = rs_sort<uint32_t, uint32_t>(k32, vals, n_memb, 32, hist, tot, &src, S, st);
+        NoVal* nv[2] = {nullptr, nullptr};
+        const hipError_t e = rs_sort<uint64_t, NoVal>(keys, nv, n_memb, 32, hist, tot, &src, S, st, 32);
         if (e != hipSuccess) return e;
-        if (S.fix)                                   // the final pass's key output: k32[src]
-            hipLaunchKernelGGL(k_age_fix, dim3((unsigned)((n_memb + 255) / 256)), dim3(256), 0, st, k32[src], n_memb, S,
-                               nd.created, ts_min);
+        if (S.fix)                                   // the final pass's coarse keys (u32) in keys[src]
+            hipLaunchKernelGGL(k_age_fix, dim3((unsigned)((n_memb + 255) / 256)), dim3(256), 0, st,
+                               reinterpret_cast<const uint32_t*>(keys[src]), n_memb, S, nd.created, ts_min);
     }
     return hipGetLastError();
 }
