@@ -546,15 +546,15 @@ constexpr int ORD_PCHUNK = 1024;
 hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, int64_t n_small,
                                const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
                                uint32_t* vals, int64_t* seg, hipStream_t st);
-// Fills the padding of every group's region (after its `len` memberships) with g | MEMB_PAD.
+// Fills the padding of every group's region (after its `len` memberships) with g | MEMB_PAD
+// and sets the ordering's segment starts (seg[4g + k] = pstart[g], seg[4G] = pstart[G]).
 hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_grp,
-                             uint32_t* g_memb, hipStream_t st);
-// The age index (load time): memberships counted per block of nodes (scan: cnt = block
-// bases, *total), listed with (group << R | creation offset) keys and (node | flags << 32)
-// values, LSD-sorted (result in keys[*src] / vals[*src]), group starts; then written into
-// the groups' padded regions.
-hipError_t launch_memb_count(const NodeDev& n, const GroupDev& g, int nblk, uint32_t* cnt, uint32_t* total,
-                             hipStream_t st);
+                             uint32_t* g_memb, int64_t* seg, hipStream_t st);
+// The age index (load time): memberships listed in one pass (per-tile counts, decoupled
+// look-back: status = memb_status_words(n) u64 words, zeroed by the launcher) with
+// (group << R | creation offset) keys and (node | flags) values, LSD-sorted, then written
+// into the groups' padded regions; *total = the listed count.
+size_t memb_status_words(int64_t n);
 // The age index's destination: every group's padded region (k_rs_scatter<FINAL>).
 struct RegionSink {
     const int64_t* seg;        // sorted start of group g's memberships (host-computed)
@@ -571,7 +571,7 @@ struct RegionSink {
 };
 // coarse_shift < 0: exact 64-bit keys (group << R | offset); >= 0: 32-bit coarse keys
 // (group << (32 - gbits) | offset >> coarse_shift) + the run fix-up (S.R = 32 - gbits).
-hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const uint32_t* base, int64_t n_memb,
+hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, uint64_t* status, uint32_t* total, int64_t n_memb,
                            int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, int coarse_shift,
                            uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t* tot, const RegionSink& S,
                            hipStream_t st);

@@ -1762,14 +1762,12 @@ __device__ __forceinline__ uint64_t div_pow10(uint64_t x, uint64_t d) {
 template <class KT, int BITS>
 __global__ __launch_bounds__(SORT_BLOCK) void k_rs_hist(const KT* __restrict__ keys, int64_t n, int shift,
                                                         uint32_t* __restrict__ hist) {
-    // per wave: lanes with equal digits are matched with BITS ballots and the first of
-    // them adds the group's size to the wave's own counters (no atomics, no conflicts)
+    // per wave: one LDS atomic add per key into the wave's own counters
     constexpr int NB = 1 << BITS;
     __shared__ uint32_t wh[SORT_WAVES][NB];
     for (int i = threadIdx.x; i < SORT_WAVES * NB; i += SORT_BLOCK) (&wh[0][0])[i] = 0;
     __syncthreads();
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int wid = threadIdx.x >> 6;
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
     constexpr int U = 8;                                 // keys in flight per thread
@@ -1784,13 +1782,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_hist(const KT* __restrict__ k
         for (int u = 0; u < U; ++u) {
             const bool ok = b + (int64_t)u * SORT_BLOCK + threadIdx.x < hi;
             const uint32_t d = (uint32_t)(k[u] >> shift) & (NB - 1);
-            unsigned long long m = __ballot(ok);
-#pragma unroll
-            for (int bit = 0; bit < BITS; ++bit) {
-                const unsigned long long bb = __ballot((d >> bit) & 1);
-                m &= ((d >> bit) & 1) ? bb : ~bb;
-            }
-            if (ok && (m & lt) == 0) wh[wid][d] += (uint32_t)__popcll(m);
+            if (ok) atomicAdd(&wh[wid][d], 1u);
         }
     }
     __syncthreads();
@@ -1953,8 +1945,11 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
         uint32_t c = 0;
         if (t < NB) {
             run[t] += dtot;
-#pragma unroll 8
-            for (int s = 0; s < S; ++s) { const uint32_t v = wh[s][t]; wh[s][t] = c; c += v; }
+            uint32_t v[S];                               // every segment's count in flight at once
+#pragma unroll
+            for (int s = 0; s < S; ++s) v[s] = wh[s][t];
+#pragma unroll
+            for (int s = 0; s < S; ++s) { wh[s][t] = c; c += v[s]; }
             dtot = c;
         }
         const uint32_t x = wave_incl_scan32(c);          // digits in thread order (0 past NB)
@@ -2118,12 +2113,6 @@ constexpr int MEMB_U = 4;                            // consecutive nodes per th
 constexpr int MEMB_BLOCK = 512, MEMB_WAVES = MEMB_BLOCK / 64;
 // LDS staging of one round's memberships (1.5 per node; a round with more stores directly)
 constexpr int MEMB_CAP = MEMB_BLOCK * MEMB_U * 3 / 2;
-// A block's share of the node range: whole groups of MEMB_U nodes, so a thread's nodes start
-// on a 16-B boundary (the node arrays start at node 0: N.lo == 0, one rank holds the table).
-__device__ __forceinline__ int64_t memb_share(int64_t n) {
-    const int64_t per = (n + gridDim.x - 1) / gridDim.x;
-    return (per + MEMB_U - 1) / MEMB_U * MEMB_U;
-}
 // Flags, label0 (and creation times) of nodes [r0, r0 + MEMB_U) with 16-B loads when all are
 // below hi (absent / NONE past it).
 __device__ __forceinline__ void memb_load(const NodeDev& N, int64_t r0, int64_t hi, uint32_t (&f)[MEMB_U],
@@ -2162,78 +2151,40 @@ __device__ __forceinline__ void memb_codes(const NodeDev& N, const GroupDev& G, 
     }
 }
 
-// Each thread takes MEMB_U consecutive nodes per round, their flags and labels loaded
-// before any is looked at (the listing is latency-bound: one node per thread per round
-// left a chain of dependent loads per 1024 nodes).
-__global__ __launch_bounds__(MEMB_BLOCK) void k_memb_count(NodeDev N, GroupDev G, int64_t n, uint32_t* __restrict__ cnt) {
-    __shared__ uint32_t tot;
-    if (threadIdx.x == 0) tot = 0;
-    __syncthreads();
-    const int64_t per = memb_share(n);
-    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
-    uint32_t c = 0;
-    for (int64_t b = lo; b < hi; b += (int64_t)MEMB_BLOCK * MEMB_U) {
-        uint32_t f[MEMB_U], l0[MEMB_U];
-        memb_load(N, b + (int64_t)threadIdx.x * MEMB_U, hi, f, l0, nullptr);
-        uint32_t c0[MEMB_U];
-        memb_codes(N, G, f, l0, c0);
-#pragma unroll
-        for (int u = 0; u < MEMB_U; ++u)
-            node_groups_c0(N, G, f[u], N.lo + b + (int64_t)threadIdx.x * MEMB_U + u, c0[u], [&](uint32_t) { ++c; });
-    }
-    atomicAdd(&tot, c);
-    __syncthreads();
-    if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
-}
-
-// Exclusive scan of n u32 in place by one workgroup; total to *total.
-__global__ __launch_bounds__(SORT_BLOCK) void k_scan_small(uint32_t* __restrict__ a, int n, uint32_t* __restrict__ total) {
-    __shared__ uint32_t carry;
-    __shared__ uint32_t wsum[SORT_WAVES];
-    if (threadIdx.x == 0) carry = 0;
-    __syncthreads();
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int base = 0; base < n; base += SORT_BLOCK) {
-        const int i = base + threadIdx.x;
-        const uint32_t v = i < n ? a[i] : 0;
-        uint32_t s = v;
-        for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(s, d, 64); if (lane >= d) s += y; }
-        if (lane == 63) wsum[wid] = s;
-        __syncthreads();
-        uint32_t wpre = 0;
-        for (int k = 0; k < wid; ++k) wpre += wsum[k];
-        uint32_t blk = 0;
-        for (int k = 0; k < SORT_WAVES; ++k) blk += wsum[k];
-        if (i < n) a[i] = carry + wpre + s - v;
-        __syncthreads();
-        if (threadIdx.x == 0) carry += blk;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0 && total) *total = carry;
-}
-
-// Lists the memberships in snapshot order (a block's nodes in order, a node's groups in
+// Lists the memberships in snapshot order (a tile's nodes in order, a node's groups in
 // label order): key = group << R | (creation offset >> KS), value = node | membership
 // flags << MEMB_FLAG_SHIFT — a dry group's membership carries "tracked by this group" in
 // the tracker bit (controller.go:126-138), so the per-decision split needs no lookup.  KT =
-// uint64_t with KS = 0 (the exact key), or uint32_t (the coarse key, launch_age_sort).
+// uint64_t with KS = 0 (the exact key); PACK: one 8-B element per membership, the 32-bit
+// coarse key above the value (vals unused).
+// Single pass (round 5; a counting pass + scan before it read the node table twice): one
+// workgroup per tile of MEMB_BLOCK * MEMB_U nodes, tiles taken in order from a ticket, so
+// every tile a workgroup waits on belongs to a workgroup already running; a tile publishes
+// its membership count (LB_AGG) before it looks back, then its inclusive prefix (LB_INC)
+// once one wave has summed its predecessors' words back to the nearest inclusive one.
+constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
 template <class KT, bool PACK = false>
-__global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G, int64_t n, const uint32_t* __restrict__ base,
-                                                          int64_t cap, int64_t ts_min, uint64_t div, int R, int KS,
-                                                          KT* __restrict__ keys, uint32_t* __restrict__ vals) {
-    // PACK: one 8-B element per membership, the 32-bit coarse key above the value (keys is
-    // uint64_t*, vals unused)
-    // A round's memberships are staged in LDS and written out as two contiguous streams:
+__global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G, int64_t n, uint64_t* __restrict__ status,
+                                                          uint32_t* __restrict__ total_out, uint32_t* __restrict__ err,
+                                                          int64_t cap, int64_t ts_min,
+                                                          uint64_t div, int R, int KS, KT* __restrict__ keys,
+                                                          uint32_t* __restrict__ vals) {
+    // A tile's memberships are staged in LDS and written out as two contiguous streams:
     // stored straight from the walk, a wave's 8-B stores land ~4 entries apart per lane and
     // the listing took 5x its store-free time (measured, r03_mk).
     __shared__ uint32_t wsum[MEMB_WAVES];
     __shared__ KT sk[MEMB_CAP];
-    __shared__ uint32_t sv[MEMB_CAP];
+    __shared__ uint32_t sv[PACK ? 1 : MEMB_CAP];
+    __shared__ uint32_t s_tile, s_base;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t carry = base[blockIdx.x];
-    const int64_t per = memb_share(n);
-    const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
-    for (int64_t b = lo; b < hi; b += (int64_t)MEMB_BLOCK * MEMB_U) {
+    const int64_t n_tiles = (n + MEMB_BLOCK * MEMB_U - 1) / (MEMB_BLOCK * MEMB_U);
+    uint32_t* ticket = reinterpret_cast<uint32_t*>(status + n_tiles);
+    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int64_t tile = s_tile;
+    if (tile >= n_tiles) return;                         // (the grid is exactly n_tiles)
+    {
+        const int64_t b = tile * (MEMB_BLOCK * MEMB_U), hi = imin64(n, b + MEMB_BLOCK * MEMB_U);
         // MEMB_U consecutive nodes per thread (snapshot order = thread order), loads first
         const int64_t r0 = b + (int64_t)threadIdx.x * MEMB_U;
         uint32_t f[MEMB_U], l0[MEMB_U];
@@ -2267,6 +2218,48 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
             total += s;
         }
         const bool stage = total <= (uint32_t)MEMB_CAP;   // block-uniform
+        if (threadIdx.x == 0)
+            __hip_atomic_store(status + tile, (tile ? LB_AGG : LB_INC) | total, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        // look back (wave 0; lane l reads tile look - l) -> s_base, this tile's first position
+        auto look_back = [&]() {
+            uint32_t excl = 0;
+            uint32_t spins = 0;                          // a bound on waiting (never reached when the
+            for (int64_t look = tile - 1; look >= 0;) {  // status words were zeroed): err bit 0
+                if (++spins > (1u << 22)) {
+                    if (lane == 0) atomicOr(err, 1u);
+                    break;
+                }
+                const int64_t j = look - lane;
+                // relaxed: a word carries its own value and nothing else is read through it (an
+                // acquire invalidates the CU's vector L1 under the other workgroups' loads)
+                const uint64_t w = j >= 0 ? __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                          : LB_INC;      // before tile 0: an inclusive 0
+                const unsigned long long inc = __ballot((w >> 62) == 2), wait = __ballot((w >> 62) == 0);
+                const int fi = inc ? __builtin_ctzll(inc) : 63;   // nearest inclusive word
+                const unsigned long long need = ~0ull >> (63 - fi);      // lanes 0..fi
+                if (wait & need) {                       // a predecessor has not counted yet
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += wave_total32(lane <= fi ? (uint32_t)w : 0u);
+                if (inc) break;
+                look -= 64;
+            }
+            if (lane == 0) {
+                if (tile) __hip_atomic_store(status + tile, LB_INC | (uint64_t)(uint32_t)(excl + total), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+                s_base = excl;
+                if (tile == n_tiles - 1) total_out[0] = excl + total;
+            }
+        };
+        // staged tiles look back after their walk (the predecessors' counts are published by
+        // then); a tile too large for the staging stores directly and needs its base first
+        if (!stage) {
+            if (wid == 0) look_back();
+            __syncthreads();
+        }
+        const uint32_t carry = stage ? 0u : s_base;
 #pragma unroll
         for (int u = 0; u < MEMB_U; ++u) {
             const int64_t i = N.lo + r0 + u;
@@ -2286,14 +2279,15 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
                 ++pos;
             });
         }
-        __syncthreads();
-        if (stage)
-            for (uint32_t e = threadIdx.x; e < total && carry + e < cap; e += MEMB_BLOCK) {
-                keys[carry + e] = sk[e];
-                if (!PACK) vals[carry + e] = sv[e];
+        if (stage) {
+            if (wid == 0) look_back();
+            __syncthreads();
+            const uint32_t base = s_base;
+            for (uint32_t e = threadIdx.x; e < total && base + e < cap; e += MEMB_BLOCK) {
+                keys[base + e] = sk[e];
+                if (!PACK) vals[base + e] = sv[e];
             }
-        carry += total;
-        __syncthreads();
+        }
     }
 }
 
@@ -2639,9 +2633,14 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
 // class 3 from the region word alone, k_ord_count).
 __global__ __launch_bounds__(256) void k_region_pad(const uint32_t* __restrict__ pstart,
                                                     const uint32_t* __restrict__ plen, int32_t G,
-                                                    uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_memb) {
+                                                    uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_memb,
+                                                    int64_t* __restrict__ seg) {
     const int32_t g = blockIdx.x;
     if (g >= G) return;
+    // the ordering's segment starts (the sort's last pass read seg as the unpadded starts):
+    // all four of the group's at its region start
+    if (threadIdx.x < 4) seg[4 * (int64_t)g + threadIdx.x] = pstart[g];
+    if (g == 0 && threadIdx.x == 4) seg[4 * (int64_t)G] = pstart[G];
     for (uint32_t i = pstart[g] + plen[g] + threadIdx.x; i < pstart[g + 1]; i += blockDim.x) {
         g_grp[i] = (uint32_t)g | MEMB_PAD;
         g_memb[i] = MEMB_PAD_WORD;
@@ -3009,22 +3008,19 @@ hipError_t rs_sort(KT* keys[2], VT* vals[2], int64_t n, int bits, uint32_t* hist
 
 size_t sort_hist_words(int64_t n) { return (size_t)256 * rs_blocks(n); }
 
-hipError_t launch_memb_count(const NodeDev& nd, const GroupDev& g, int nblk, uint32_t* cnt, uint32_t* total,
-                             hipStream_t st) {
-    const int64_t n = nd.hi - nd.lo;
-    hipLaunchKernelGGL(k_memb_count, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, cnt);
-    hipLaunchKernelGGL(k_scan_small, dim3(1), dim3(SORT_BLOCK), 0, st, cnt, nblk, total);
-    return hipGetLastError();
-}
+size_t memb_status_words(int64_t n) { return (size_t)((n + MEMB_BLOCK * MEMB_U - 1) / (MEMB_BLOCK * MEMB_U)) + 1; }
 
-hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const uint32_t* base, int64_t n_memb,
+hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, uint64_t* status, uint32_t* total, int64_t n_memb,
                            int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, int coarse_shift,
                            uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t* tot, const RegionSink& S,
                            hipStream_t st) {
     const int64_t n = nd.hi - nd.lo;
+    const size_t nst = memb_status_words(n);
+    const dim3 tiles((unsigned)(nst - 1));
+    if (n > 0 && hipMemsetAsync(status, 0, nst * 8, st) != hipSuccess) return hipGetLastError();
     if (coarse_shift < 0) {                          // exact 64-bit keys: group << R | offset
         if (n > 0)
-            hipLaunchKernelGGL(k_memb_keys<uint64_t>, dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min,
+            hipLaunchKernelGGL(k_memb_keys<uint64_t>, tiles, dim3(MEMB_BLOCK), 0, st, nd, g, n, status, total, S.err, cap, ts_min,
                                div, R, 0, keys[0], vals[0]);
         if (n_memb > 0) {
             int src = 0;
@@ -3038,8 +3034,8 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, int nblk, const
     // digit run), sorted on the element's top 32 bits; then k_age_fix orders each run of
     // equal coarse keys by the exact creation time
     if (n > 0)
-        hipLaunchKernelGGL((k_memb_keys<uint64_t, true>), dim3(nblk), dim3(MEMB_BLOCK), 0, st, nd, g, n, base, cap, ts_min,
-                           div, 32 - gbits, coarse_shift, keys[0], nullptr);
+        hipLaunchKernelGGL((k_memb_keys<uint64_t, true>), tiles, dim3(MEMB_BLOCK), 0, st, nd, g, n, status, total, S.err, cap,
+                           ts_min, div, 32 - gbits, coarse_shift, keys[0], nullptr);
     if (n_memb > 0) {
         int src = 0;
         NoVal* nv[2] = {nullptr, nullptr};
@@ -3067,9 +3063,9 @@ hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_
 }
 
 hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_grp,
-                             uint32_t* g_memb, hipStream_t st) {
+                             uint32_t* g_memb, int64_t* seg, hipStream_t st) {
     if (G <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_region_pad, dim3((unsigned)G), dim3(256), 0, st, pstart, plen, G, g_grp, g_memb);
+    hipLaunchKernelGGL(k_region_pad, dim3((unsigned)G), dim3(256), 0, st, pstart, plen, G, g_grp, g_memb, seg);
     return hipGetLastError();
 }
 
