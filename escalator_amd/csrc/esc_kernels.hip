@@ -1740,8 +1740,14 @@ __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, i
 // every membership and stable-partition by (group, class): LSD radix passes over the
 // segment id alone.  A segment then lists its nodes oldest first; newest first is the
 // segment read backwards (esc_group_order restores index order inside equal timestamps).
+#ifndef ESC_SORT_BLOCK
+#define ESC_SORT_BLOCK 1024   // sort workgroup size (timing builds may override)
+#endif
+#ifndef ESC_RS_MAXBLK
+#define ESC_RS_MAXBLK 512     // the most workgroups per sort pass
+#endif
 namespace {
-constexpr int SORT_BLOCK = 1024;
+constexpr int SORT_BLOCK = ESC_SORT_BLOCK;
 constexpr int SORT_WAVES = SORT_BLOCK / 64;
 }
 
@@ -1874,14 +1880,19 @@ __device__ __forceinline__ void region_put(const RegionSink& S, uint32_t p, uint
 // FINAL (the age index's last pass): a key's sorted position goes straight into its group's
 // padded region (RegionSink) instead of the key / value arrays.
 #ifndef ESC_RS_U
-#define ESC_RS_U 2         // keys per thread per scatter chunk (timing builds may override)
+#define ESC_RS_U 3         // keys per thread per scatter chunk (r05w: 3 beat 2 and 4 by 4%)
 #endif
 #ifndef ESC_RS_CARRY
 #define ESC_RS_CARRY 1     // whole-line digit runs (below); 0 = the plain scatter, for timing builds
 #endif
 constexpr int RS_U = ESC_RS_U;
+#ifdef ESC_RS_WPE
+#define RS_SCATTER_BOUNDS __launch_bounds__(SORT_BLOCK, ESC_RS_WPE)
+#else
+#define RS_SCATTER_BOUNDS __launch_bounds__(SORT_BLOCK)
+#endif
 template <class KT, class VT, int BITS, bool FINAL>
-__global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict__ kin, const VT* __restrict__ vin,
+__global__ RS_SCATTER_BOUNDS void k_rs_scatter(const KT* __restrict__ kin, const VT* __restrict__ vin,
                                                            KT* __restrict__ kout, VT* __restrict__ vout,
                                                            int64_t n, int shift, const uint32_t* __restrict__ hist,
                                                            const uint32_t* __restrict__ tot, RegionSink sink) {
@@ -1890,7 +1901,10 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
     static_assert(NB <= SORT_BLOCK, "one thread per digit");
     __shared__ uint32_t run[NB];                         // output position of the digit's next key
     __shared__ uint32_t lst[NB];                         // the digit's first slot in the chunk
-    __shared__ uint32_t wh[S][NB];                       // (round, wave) digit counts -> offsets
+    // (round, wave) digit counts -> offsets (< CH: 16 bits; the LDS then holds two workgroups
+    // per CU instead of one)
+    __shared__ uint16_t wh[S][NB];
+    static_assert(CH <= 65535, "16-bit chunk offsets");
     __shared__ uint32_t ws[SORT_WAVES];
     __shared__ KT sk[CH];
     __shared__ VT sv[HASV ? CH : 1];
@@ -1909,7 +1923,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, t = threadIdx.x;
     if (t < NB) run[t] = tot[t] + hist[(int64_t)t * gridDim.x + blockIdx.x];
     if (CARRY && t < NB) c_n[t] = 0;
-    for (int e = t; e < S * NB; e += SORT_BLOCK) (&wh[0][0])[e] = 0;
+    for (int e = t; e < S * NB / 2; e += SORT_BLOCK) reinterpret_cast<uint32_t*>(&wh[0][0])[e] = 0;
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
     const int64_t lo = (int64_t)blockIdx.x * per, hi = imin64(n, lo + per);
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -1937,7 +1951,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
                 m &= ((d[u] >> bit) & 1) ? bb : ~bb;
             }
             r[u] = __popcll(m & lt);
-            if (ok[u] && r[u] == 0) wh[u * SORT_WAVES + wid][d[u]] = __popcll(m);
+            if (ok[u] && r[u] == 0) wh[u * SORT_WAVES + wid][d[u]] = (uint16_t)__popcll(m);
         }
         __syncthreads();
         // per digit: offsets of the (round, wave) segments, the digit's count; the previous
@@ -1949,7 +1963,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
 #pragma unroll
             for (int s = 0; s < S; ++s) v[s] = wh[s][t];
 #pragma unroll
-            for (int s = 0; s < S; ++s) { wh[s][t] = c; c += v[s]; }
+            for (int s = 0; s < S; ++s) { wh[s][t] = (uint16_t)c; c += v[s]; }
             dtot = c;
         }
         const uint32_t x = wave_incl_scan32(c);          // digits in thread order (0 past NB)
@@ -2036,7 +2050,7 @@ __global__ __launch_bounds__(SORT_BLOCK) void k_rs_scatter(const KT* __restrict_
                 if constexpr (HASV) cv[dd][g - c_e[dd]] = sv[e];
             }
         }
-        for (int e = t; e < S * NB; e += SORT_BLOCK) (&wh[0][0])[e] = 0;
+        for (int e = t; e < S * NB / 2; e += SORT_BLOCK) reinterpret_cast<uint32_t*>(&wh[0][0])[e] = 0;
         if constexpr (CARRY) {
             if (t < NB) {                                // the new carry: [E, run + count)
                 c_n[t] = run[t] + dtot - c_e[t];
@@ -2950,7 +2964,9 @@ hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, h
 
 
 namespace {
-int rs_blocks(int64_t n) { return (int)std::max<int64_t>(1, std::min<int64_t>(512, (n + 8191) / 8192)); }
+int rs_blocks(int64_t n) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>(ESC_RS_MAXBLK, (n + 8 * SORT_BLOCK - 1) / (8 * SORT_BLOCK)));
+}
 
 template <class KT, class VT, int BITS, bool FINAL = false>
 hipError_t rs_pass(const KT* kin, const VT* vin, KT* kout, VT* vout, int64_t n, int shift, uint32_t* hist,

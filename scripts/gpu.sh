@@ -14,6 +14,7 @@
 #   variants:A,B,..  A/B timing of library builds (scripts/build_variant.sh NAME ...:
 #                    escalator_amd/libescalator_hip_NAME.so; "base" = the product library):
 #                    rank 0 of 8 and config 4, each in turn, twice
+#   variants5:A,B,.. the same for config 5 (age-index build and ordering times)
 # usage: TAG=r05a scripts/gpu.sh suite bench prof:shard8
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -141,6 +142,23 @@ for n in ('shard8', 'full'):
     done
 }
 
+variants5() {  # config 5 (age-index build, orderings) per library build
+    local v lib
+    for rep in 1 2; do
+        for v in ${1//,/ }; do
+            lib=$PWD/escalator_amd/libescalator_hip_$v.so
+            [ "$v" = base ] && lib=$PWD/escalator_amd/libescalator_hip.so
+            echo "[gpu] $(date +%T) variant $v config 5 (rep $rep)"
+            ESC_LIB_PATH=$lib timeout -k 10 400 python3 -u bench.py --config 5 --steps $STEPS --warmup 3 --no-cpu-baseline \
+                > $OUT/var5_${v}_$rep.json 2> $OUT/var5_${v}_$rep.err || { tail $OUT/var5_${v}_$rep.err; return 1; }
+            python3 -c "
+import json
+d = json.load(open('$OUT/var5_${v}_$rep.json'))
+print('  $v', 'index %.4f ms' % d['age_index_build']['ms'], 'order %.4f ms' % d['ms_per_step'])"
+        done
+    done
+}
+
 for stage in "$@"; do
     case $stage in
         suite) suite || exit 1 ;;
@@ -149,6 +167,7 @@ for stage in "$@"; do
         prof:*) prof ${stage#prof:} || exit 1 ;;
         pmcsq:*) pmcsq ${stage#pmcsq:} || exit 1 ;;
         variants:*) variants ${stage#variants:} || exit 1 ;;
+        variants5:*) variants5 ${stage#variants5:} || exit 1 ;;
         py:*) timeout -k 10 600 python3 -u scripts/${stage#py:} > $OUT/${stage#py:}.out 2>&1 || { tail -20 $OUT/${stage#py:}.out; exit 1; } ;;
         *) echo "unknown stage $stage"; exit 2 ;;
     esac
