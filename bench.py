@@ -465,7 +465,7 @@ def bench_order(args):
     return report(out, parity)
 
 
-def host_side(esc, ctx_dev):
+def host_side(esc, ctx_dev, device: int):
     """BASELINE.md §2's host-side figures: the K0 packer over object structs (esc_synth_objects:
     what the cgo shim fills from *v1.Pod / *v1.Node) of BASELINE config #2, in objects/s on
     one host thread; and the per-call drop-in esc_pods_requests_total (pkg/k8s/util.go:27:
@@ -476,6 +476,7 @@ def host_side(esc, ctx_dev):
     import numpy as np
     from escalator_amd import _lib as L
     from oracle import soa
+    from escalator_amd.context import TOTALS_DTYPE
     s = esc.Synth(1_000_000, 10_000, 100, config=2, seed=0xE5CA1A7E00000002, threads=16)
     po, n, no, nn = s.objects()
     host = esc.Context(s.groups, device=-1)
@@ -521,6 +522,29 @@ def host_side(esc, ctx_dev):
     want = fn()[0]
     L.check(lib.esc_pods_requests_total(ctx_dev.handle, p1, n1, C.byref(mem), C.byref(cpu)))
     assert int(want[2]) == n1, "config #1 filter restatement"
+    # the controller wiring's answer: config #1 resident on the device, one
+    # batched decision (RunOnce: esc_set_state + esc_step + esc_sync + esc_results), then the
+    # group's CalculatePodsRequestsTotal read from esc_results' totals
+    r1 = esc.Context(c1, device=device)
+    r1.load_synth(c1)
+    r1.set_state(c1.states)
+    r1.step()
+    r1.sync()
+    tot = np.zeros(1, TOTALS_DTYPE)
+    tptr = tot.ctypes.data_as(C.POINTER(L.GroupTotals))
+    runs, answers = [], []
+    for _ in range(200):
+        t0 = time.perf_counter()
+        L.check(lib.esc_set_state(r1.handle, r1._state))
+        L.check(lib.esc_step(r1.handle))
+        L.check(lib.esc_sync(r1.handle))
+        L.check(lib.esc_results(r1.handle, tptr, None))
+        runs.append(time.perf_counter() - t0)
+    for _ in range(200):
+        t0 = time.perf_counter()
+        L.check(lib.esc_results(r1.handle, tptr, None))
+        answers.append(time.perf_counter() - t0)
+    resident_ok = bool(int(tot["pod_cpu_m"][0]) == int(want[0]) and int(tot["pod_mem_b"][0]) == int(want[1]))
     return {"packer_objects_per_s": (n + nn) / t_pack,
             "packer_sample": "esc_packer_add_pods + _add_nodes + _view over config #2's %d pod and %d node "
                              "objects (esc_synth_objects), one host thread, median of 3: %.3f s" % (n, nn, t_pack),
@@ -529,6 +553,15 @@ def host_side(esc, ctx_dev):
             "dropin_nodes_capacity_total_ms": float(np.median(ncalls)) * 1e3,
             "dropin_oracle_1thread_ms": t_orc * 1e3,
             "dropin_parity": bool(cpu.value == want[0] and mem.value == want[1]),
+            "resident_pods_requests_total_ms": float(np.median(answers)) * 1e3,
+            "resident_run_once_ms": float(np.median(runs)) * 1e3,
+            "resident_parity": resident_ok,
+            "resident_sample": "config #1 resident (1000 pods, 50 nodes, 1 group): the controller wiring answers "
+                               "CalculatePodsRequestsTotal from the batched decision's totals (Decision."
+                               "PodsRequestsTotal in the Go shim); resident_pods_requests_total_ms = one "
+                               "esc_results(totals) after the decision (the pod and node words to pinned memory, "
+                               "one wait), resident_run_once_ms = the whole RunOnce (esc_set_state + esc_step + "
+                               "esc_sync + esc_results), medians of 200",
             "dropin_sample": "config #1 (1000 pods, 50 nodes, 1 group): esc_pods_requests_total over the group's "
                              "%d filtered pod objects (what scaleNodeGroup passes, controller.go:262) / "
                              "esc_nodes_capacity_total over the 50 nodes per call (records into reused "
@@ -796,7 +829,7 @@ def main():
         "rccl_ranks": rccl_ranks,
         # stages timed in order on the context's stream (timing mode, rank 0 / device 0)
         "stage_ms": stage_ms,
-        "exchange_ms": stage_ms.get("exchange"),
+        "exchange_ms": (stage_ms.get("exchange", stage_ms.get("exchange_host_staged")) if stage_ms else None),
         "stage_note": ("HIP events between the step's launches, timing mode (each event pair adds a few us); "
                        "k_order_split launches nothing when every group is packed into the tail (config 4); "
                        "exchange = the in-place ncclReduceScatter of the owner-major pod words (DESIGN.md §7), "
@@ -813,7 +846,7 @@ def main():
                                 "note": "esc_load_ms: esc_load_pods + esc_load_nodes (host layout, the H2D copies of "
                                         "every replica, the age index), once per snapshot; h2d_ms: the SoA's "
                                         "pageable host -> HBM copy alone, what a non-resident decision would add"}
-        out["host_side"] = host_side(esc, ctx)
+        out["host_side"] = host_side(esc, ctx, local)
     if world == 1 and shard_world == 1 and not multi and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(cfg, G, full=s)
     if n_gpus != args.gpus or (rccl_ranks is not None and rccl_ranks != args.gpus):

@@ -370,6 +370,8 @@ struct GroupDev {
     const uint32_t* gslot;     // [G] the group's pod slot: its pair, or n_gp for the default group
     const uint32_t* xs;        // [G] the group's row of the exchanged pod words (owner-major)
     esc_group_metrics* metrics; // [G] gauges written by K4, or null (esc_set_metrics)
+    esc_group_totals* htot;    // [G] totals written by K4 with the decision (pinned host memory,
+                               // small contexts: esc_results then copies nothing), or null
     int64_t sp;                // K1 partial row stride: pod slots rounded up to FC_COL
     uint32_t n_gp;             // pod slots: pair ids [0, n_gp) + the default filter's slot n_gp
     int32_t G;

@@ -902,7 +902,8 @@ __device__ __forceinline__ bool join_split(int64_t lo_sum, int64_t hi_sum, int64
 
 __device__ __forceinline__ void finalize_p(const GroupParams& prm, const GroupNode& gn, int32_t g,
                                            const int64_t* __restrict__ pw, const int64_t* __restrict__ nw,
-                                           esc_group_decision& dec, esc_group_metrics* __restrict__ met) {
+                                           esc_group_decision& dec, esc_group_metrics* __restrict__ met,
+                                           esc_group_totals* __restrict__ htot) {
     Totals t;
     int64_t flags = nw[NW_FLAGS];
     if (!join_split(pw[PW_CPU_LO], pw[PW_CPU_HI], t.pod_cpu)) flags |= ESC_TF_POD_OVERFLOW;
@@ -924,12 +925,22 @@ __device__ __forceinline__ void finalize_p(const GroupParams& prm, const GroupNo
         metrics_one(t, dec, m);
         met[g] = m;
     }
+    if (htot) {                                          // esc_results' record, zero-copy
+        static_assert(sizeof(esc_group_totals) == 13 * 8, "totals record is 13 words");
+        const bool has = t.first != INT64_MAX;
+        const int64_t w[13] = {t.pod_cpu, t.pod_mem, t.n_pods, t.node_cpu, t.node_mem, t.n_nodes, t.n_unt,
+                               t.n_taint, t.n_cord, has ? t.first : -1, has ? t.first_cpu : 0,
+                               has ? t.first_mem : 0, t.flags};
+        int64_t* o = reinterpret_cast<int64_t*>(htot + g);
+#pragma unroll
+        for (int k = 0; k < 13; ++k) o[k] = w[k];
+    }
 }
 
 __device__ __forceinline__ void finalize(const GroupDev& G, const GroupNode& gn, int32_t g,
                                          const int64_t* __restrict__ pw, const int64_t* __restrict__ nw,
                                          esc_group_decision& dec, esc_group_metrics* __restrict__ met) {
-    finalize_p(G.params[g], gn, g, pw, nw, dec, met);
+    finalize_p(G.params[g], gn, g, pw, nw, dec, met, G.htot);
 }
 
 __device__ __forceinline__ DecCompact compact_of(const esc_group_decision& d) {
@@ -1558,7 +1569,7 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
     }
     if (D.dec) {
         esc_group_decision d;
-        finalize_p(prm, gn, g, pwv, v, d, G.metrics);
+        finalize_p(prm, gn, g, pwv, v, d, G.metrics, G.htot);
         store_full(D.dec + g, d);
         sdec[lane] = compact_of(d);
         sid[lane] = (uint32_t)g;

@@ -37,6 +37,7 @@ constexpr int LDS_BYTES = 160 * 1024;
 constexpr int POD_WINDOW_MAX = LDS_BYTES / 16;      // groups whose pod partials fit in LDS
 static_assert(POD_WINDOW_MAX % 2 == 0 && FC_COL % 2 == 0, "K1's 16-B partial-row stores need even window starts");
 constexpr int MAX_STAGES = 10;
+constexpr int32_t HTOT_MAX_GROUPS = 1024;   // K4 writes the totals records to host memory (<= 104 KB)
 
 #define HIP_TRY(x)                                              \
     do {                                                        \
@@ -196,7 +197,8 @@ struct esc_ctx {
     int64_t* d_trk_acc = nullptr;                             // [G][TA_K] dry-mode tracked sums
     int64_t* d_pwords = nullptr;                              // active exchange buffer [world * own_cap][PW_K]
     int64_t* own_pwords = nullptr;                            // the context-owned one
-    int64_t* d_nwords = nullptr;                              // [G][NW_K] node words (exact for owned groups)
+    int64_t* d_nwords = nullptr;                              // [G][NW_K] node words (exact for owned groups),
+                                                              // right after own_pwords (one allocation)
     // Owner-major exchange rows: group g's pod words at row h_xs[g] = owner *
     // own_cap + its index among the owner's groups, so one ncclReduceScatter hands every
     // owner the exact sums of its own groups; h_own = this rank's groups (ascending).
@@ -331,6 +333,14 @@ struct esc_ctx {
     RmRec* h_rm = nullptr;                                    // K7 results (pinned copy)
     uint8_t* h_istage = nullptr;                              // age-index build uploads (pinned)
     size_t istage_cap = 0;
+    int64_t* h_words = nullptr;                               // esc_results' pod + node words (pinned)
+    size_t words_cap = 0;
+    // Small contexts (G <= HTOT_MAX_GROUPS): K4 writes every decided group's totals record
+    // straight to pinned host memory with its decision (<= 104 KB over PCIe), so esc_results
+    // copies nothing; tot_dec = the last enqueued step decided (the records are current).
+    esc_group_totals* h_tot = nullptr;
+    esc_group_totals* h_tot_dev = nullptr;
+    bool tot_dec = false;
     std::vector<int64_t> h_soft, h_hard;                      // grace periods last uploaded
     bool rm_valid = false;                                    // esc_try_remove results current
     int64_t rm_nodes = -1;                                    // node count the reaping buffers are sized for
@@ -418,6 +428,7 @@ GroupDev group_dev(const esc_ctx* c) {
     g.gslot = c->d_gslot;
     g.xs = c->world > 1 ? c->d_xs : nullptr;
     g.metrics = c->want_metrics ? c->d_metrics : nullptr;
+    g.htot = c->h_tot_dev;
     g.n_gp = c->gi.n_gp;
     g.sp = slot_stride(c);
     g.G = c->gi.G;
@@ -522,12 +533,15 @@ void release_work(esc_ctx* c) {
     dfree(c->d_k1_trace);
     dfree(c->d_touch); dfree(c->d_wg_cols); dfree(c->d_wg_off); dfree(c->d_col_rows);
     c->touch_on = false;
-    dfree(c->own_pwords); dfree(c->d_nwords); dfree(c->d_dec); dfree(c->d_cdec); dfree(c->d_metrics);
+    dfree(c->own_pwords); c->d_nwords = nullptr; dfree(c->d_dec); dfree(c->d_cdec); dfree(c->d_metrics);
     dfree(c->d_own); dfree(c->d_xs);
     c->d_pwords = nullptr;
     if (c->h_cdec) hipHostFree(c->h_cdec);
     c->h_cdec = nullptr;
     c->h_cdec_dev = nullptr;
+    if (c->h_tot) hipHostFree(c->h_tot);
+    c->h_tot = c->h_tot_dev = nullptr;
+    c->tot_dec = false;
     c->work_ready = false;
     drop_graphs(c);
 }
@@ -1093,10 +1107,12 @@ int32_t ensure_work(esc_ctx* c) {
         HIP_TRY(hipMemcpy(c->d_xs, c->h_xs.data(), (size_t)G * 4, hipMemcpyHostToDevice));
         if (!c->h_own.empty()) HIP_TRY(hipMemcpy(c->d_own, c->h_own.data(), c->h_own.size() * 4, hipMemcpyHostToDevice));
     }
-    HIP_TRY(dalloc(&c->own_pwords, (size_t)xw_count(c)));
-    HIP_TRY(hipMemset(c->own_pwords, 0, (size_t)xw_count(c) * 8));
-    HIP_TRY(dalloc(&c->d_nwords, (size_t)G * NW_K));
-    HIP_TRY(hipMemset(c->d_nwords, 0, (size_t)G * NW_K * 8));
+    // the pod words, then (at a 256-B boundary) the node words: esc_results reads both with
+    // one copy when they are adjacent
+    const size_t pw_span = ((size_t)xw_count(c) + 31) & ~(size_t)31;
+    HIP_TRY(dalloc(&c->own_pwords, pw_span + (size_t)G * NW_K));
+    HIP_TRY(hipMemset(c->own_pwords, 0, (pw_span + (size_t)G * NW_K) * 8));
+    c->d_nwords = c->own_pwords + pw_span;
     c->d_pwords = c->bound_pwords ? c->bound_pwords : c->own_pwords;
     HIP_TRY(dalloc(&c->d_dec, (size_t)G));
     HIP_TRY(dalloc(&c->d_metrics, (size_t)G));
@@ -1104,6 +1120,10 @@ int32_t ensure_work(esc_ctx* c) {
     HIP_TRY(dalloc(&c->d_cdec, (size_t)G));
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_cdec), (size_t)G * sizeof(DecCompact)));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_cdec_dev), c->h_cdec, 0));
+    if (G <= HTOT_MAX_GROUPS) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_tot), (size_t)G * sizeof(esc_group_totals)));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_tot_dev), c->h_tot, 0));
+    }
     // compact flush: every workgroup may touch every column at most once, so the lists and
     // the entries fit the full-row buffers' sizes
     c->touch_tw = (int)((n_col + 31) / 32);
@@ -1147,6 +1167,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
         return ESC_OK;
     };
     DecCompact* cdec = c->zero_copy ? c->h_cdec_dev : c->d_cdec;
+    c->tot_dec = decide;                                 // K4's host totals records (small contexts)
     if (int32_t rc = mark()) return rc;
     int nblk = 0;
     if (c->force_wide) {
@@ -1359,6 +1380,8 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
             if (c->k1t_ev[i]) hipEventDestroy(c->k1t_ev[i]);
         if (c->h_istage) hipHostFree(c->h_istage);
         c->h_istage = nullptr;
+        if (c->h_words) hipHostFree(c->h_words);
+        c->h_words = nullptr;
         if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     }
     delete c;
@@ -2314,6 +2337,7 @@ int32_t esc_decide(esc_ctx* c) {
     HIP_TRY(launch_node_groups(group_dev(c), node_dev(c), own_list(c), c->nodes.rows, c->d_trk_acc, c->d_nwords,
                                NGDecide{c->d_pwords, c->d_dec, c->zero_copy ? c->h_cdec_dev : c->d_cdec}, c->stream));
     c->ng_pending = false;
+    c->tot_dec = true;
     if (!c->zero_copy)
         HIP_TRY(hipMemcpyAsync(c->h_cdec, c->d_cdec, (size_t)c->gi.G * sizeof(DecCompact), hipMemcpyDeviceToHost,
                                c->stream));
@@ -2459,10 +2483,38 @@ int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* de
             d.reserved = 0;
         }
     }
-    if (totals) {
-        std::vector<int64_t> w((size_t)xw_count(c)), nw((size_t)G * NW_K);
-        HIP_TRY(hipMemcpy(w.data(), c->d_pwords, w.size() * 8, hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(nw.data(), c->d_nwords, nw.size() * 8, hipMemcpyDeviceToHost));
+    if (totals && c->h_tot && c->tot_dec) {
+        // small contexts: K4 wrote every decided group's record to pinned memory (the answer
+        // a controller's CalculatePodsRequestsTotal takes from the batched decision)
+        for (int32_t g = 0; g < G; ++g) {
+            if (mine(g)) {
+                totals[g] = c->h_tot[g];
+                continue;
+            }
+            std::memset(&totals[g], 0, sizeof totals[g]);
+            totals[g].first_node = -1;
+            totals[g].flags = ESC_TF_NOT_OWNED;
+        }
+    } else if (totals) {
+        // both word arrays into one pinned buffer, one queued copy (two when the pod words are
+        // a bound buffer) and one wait
+        const size_t nwp = (size_t)(c->d_nwords - c->own_pwords), nwn = (size_t)G * NW_K;   // nwp >= xw_count
+        if (nwp + nwn > c->words_cap) {
+            if (c->h_words) hipHostFree(c->h_words);
+            c->h_words = nullptr;
+            c->words_cap = 0;
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_words), (nwp + nwn) * 8));
+            c->words_cap = nwp + nwn;
+        }
+        if (c->d_pwords == c->own_pwords) {              // adjacent (the context's own pod words)
+            HIP_TRY(hipMemcpyAsync(c->h_words, c->d_pwords, (nwp + nwn) * 8, hipMemcpyDeviceToHost, c->stream));
+        } else {
+            HIP_TRY(hipMemcpyAsync(c->h_words, c->d_pwords, (size_t)xw_count(c) * 8, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipMemcpyAsync(c->h_words + nwp, c->d_nwords, nwn * 8, hipMemcpyDeviceToHost, c->stream));
+        }
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        const int64_t* w = c->h_words;
+        const int64_t* nw = c->h_words + nwp;
         for (int32_t g = 0; g < G; ++g) {
             if (!mine(g)) {
                 std::memset(&totals[g], 0, sizeof totals[g]);
@@ -2470,8 +2522,8 @@ int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* de
                 totals[g].flags = ESC_TF_NOT_OWNED;
                 continue;
             }
-            const int64_t* x = &w[(size_t)(c->world > 1 ? c->h_xs[(size_t)g] : (uint32_t)g) * PW_K];
-            const int64_t* y = &nw[(size_t)g * NW_K];
+            const int64_t* x = w + (size_t)(c->world > 1 ? c->h_xs[(size_t)g] : (uint32_t)g) * PW_K;
+            const int64_t* y = nw + (size_t)g * NW_K;
             esc_group_totals& t = totals[g];
             auto join = [&](int k, int64_t& out) {
                 const __int128 v = ((__int128)x[k + 1] << 32) + (__int128)x[k];

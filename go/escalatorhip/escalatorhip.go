@@ -276,6 +276,23 @@ type Decision struct {
 	TaintErr                   error // scaleDownTaint's formatted error
 }
 
+// PodsRequestsTotal is the group's CalculatePodsRequestsTotal(pods) (pkg/k8s/util.go:27-38,
+// called at controller.go:262) answered from the batched decision: (mem, cpu) built with the
+// constructors util.go:34-36 uses, no call into the library.  The controller wiring uses it
+// (INTEGRATION.md §1); the per-call Context.CalculatePodsRequestsTotal stays for slices that
+// are not a group's.
+func (d *Decision) PodsRequestsTotal() (resource.Quantity, resource.Quantity) {
+	return *resource.NewQuantity(d.PodMemBytes, resource.BinarySI),
+		*resource.NewMilliQuantity(d.PodCPUMilli, resource.DecimalSI)
+}
+
+// NodesCapacityTotal is CalculateNodesCapacityTotal(untaintedNodes) (pkg/k8s/util.go:41-52,
+// called at controller.go:268) from the batched decision, as PodsRequestsTotal.
+func (d *Decision) NodesCapacityTotal() (resource.Quantity, resource.Quantity) {
+	return *resource.NewQuantity(d.NodeMemBytes, resource.BinarySI),
+		*resource.NewMilliQuantity(d.NodeCPUMilli, resource.DecimalSI)
+}
+
 // Context is one process's handle on one GPU (one esc_ctx, driven from one goroutine —
 // the reference's RunOnce is single-threaded, controller.go:416).
 type Context struct {

@@ -510,8 +510,12 @@ int32_t esc_nodes_delete(esc_ctx* ctx, const int64_t* ids, int64_t n);
  * n_trk = 0; a caller's ESC_NF_TRACKED bit is ignored, the tracker is the context's).  The
  * nodes keep their snapshot indices; they leave the groups whose pair they no longer carry
  * and join those whose pair they now carry (spare pair-major entries and K5 region slots,
- * esc_set_spare), allNodes[0] follows, a placement's occupancy follows.  All or nothing:
- * ESC_E_LIMIT when the spare room is short (reload), ESC_E_INVAL for a bad or absent id. */
+ * esc_set_spare), allNodes[0] follows, a placement's occupancy follows.  A node that
+ * returns to a pair it carried before reuses its own retired entry of that pair, so label
+ * churn (A -> B -> A ...) takes spare room once per (node, pair), not per flip.  All or
+ * nothing: ESC_E_LIMIT when the spare room is short (reload), ESC_E_INVAL for a bad or
+ * absent id; a device failure after the first change marks the node side stale (decisions
+ * and reaping return ESC_E_STATE until esc_load_nodes). */
 int32_t esc_nodes_relabel(esc_ctx* ctx, const int64_t* ids, const esc_node_soa* nodes);
 
 /* ------------------------------------------- dry-mode taintTracker (§8f rank 4)
