@@ -682,7 +682,7 @@ def main():
     exchange = None
     if multi:
         step = ctx.step
-        exchange = "rccl (esc_ctx_create_multi: ncclCommInitAll, one ncclAllReduce per device in a group call)" \
+        exchange = "rccl (esc_ctx_create_multi: ncclCommInitAll, one in-place ncclReduceScatter per device in a group call)" \
             if len(set(multi)) == len(multi) and os.environ.get("ESC_EXCHANGE") != "peer" else \
             "peer (esc_ctx_create_multi: every device sums the others' words over peer-mapped memory)"
     elif world == 1 and shard_world > 1:
@@ -694,7 +694,7 @@ def main():
     else:
         ex = Exchange(ctx, device_collective=backend == "nccl")
         step = ex.step
-        exchange = ("rccl (esc_comm_init + esc_step: ncclAllReduce on the context's stream)" if backend == "nccl"
+        exchange = ("rccl (esc_comm_init + esc_step: in-place ncclReduceScatter on the context's stream)" if backend == "nccl"
                     else "host-staged over torch.distributed %s" % backend)
     ctx.use_graph(args.graph)
     rccl_ranks = ctx.comm_size() if (multi or (world > 1 and backend == "nccl")) else None

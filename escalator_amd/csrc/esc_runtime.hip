@@ -2323,7 +2323,7 @@ int32_t esc_exchange_upload(esc_ctx* c, const int64_t* sum_in, const int64_t* mi
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipMemcpy(c->d_pwords, sum_in, (size_t)xw_count(c) * 8, hipMemcpyHostToDevice));
-    return ESC_OK;
+    return stage_mark(c);                               // timing mode: the host-staged exchange's end
 }
 
 int32_t esc_decide(esc_ctx* c) {

@@ -77,7 +77,7 @@ prof() {       # name
     timeout -k 10 500 python3 -u bench.py $a > $OUT/pbench_$name.json 2> $OUT/pbench_$name.err || { tail -20 $OUT/pbench_$name.err; return 1; }
     echo "[gpu] $(date +%T) prof $name: kernel trace"
     timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace_$name -o run \
-        -- python3 bench.py $a > $OUT/trace_$name.log 2>&1 || { tail -20 $OUT/trace_$name.log; return 1; }
+        -- python3 bench.py $a --no-cpu-baseline --no-host > $OUT/trace_$name.log 2>&1 || { tail -20 $OUT/trace_$name.log; return 1; }
     echo "[gpu] $(date +%T) prof $name: pmc FETCH_SIZE"
     timeout -s KILL 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "(^|[ :])k_" --output-format csv -d $OUT/fetch_$name -o run \
         -- python3 bench.py $a --no-cpu-baseline --no-host > $OUT/fetch_$name.log 2>&1 || { tail -20 $OUT/fetch_$name.log; return 1; }
