@@ -577,9 +577,15 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, uint64_t* statu
                            int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, int coarse_shift,
                            uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t* tot, const RegionSink& S,
                            hipStream_t st);
+// The split groups' ordering in one pass (k_ord_split): ostat = 2 * n_chunks + 1 u64 words,
+// zeroed when the chunk table is made: two arrays of status words used by alternate
+// decisions (par = 0, 1: a decision clears its chunks' words of the other), then a sticky
+// error word.
+// Output layout of every group (split and packed): untainted forward from the region start,
+// tainted newest first backward from the region end; seg[4g..4g+3] = start, start +
+// untainted, end - tainted, end.
 hipError_t launch_order(const NodeDev& n, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
-                        const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
-                        int64_t n_e, int32_t G, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,
+                        const uint32_t* grp_off, const uint32_t* g_memb, uint64_t* ostat, int par, uint32_t* vals,
                         int64_t* seg, hipStream_t st);
 
 }  // namespace esc

@@ -2183,10 +2183,13 @@ __device__ __forceinline__ void memb_codes(const NodeDev& N, const GroupDev& G, 
 // uint64_t with KS = 0 (the exact key); PACK: one 8-B element per membership, the 32-bit
 // coarse key above the value (vals unused).
 // Single pass (round 5; a counting pass + scan before it read the node table twice): one
-// workgroup per tile of MEMB_BLOCK * MEMB_U nodes, tiles taken in order from a ticket, so
-// every tile a workgroup waits on belongs to a workgroup already running; a tile publishes
-// its membership count (LB_AGG) before it looks back, then its inclusive prefix (LB_INC)
-// once one wave has summed its predecessors' words back to the nearest inclusive one.
+// workgroup per tile of MEMB_BLOCK * MEMB_U nodes (tile = blockIdx.x); a tile publishes its
+// membership count (LB_AGG) before it looks back, then its inclusive prefix (LB_INC) once
+// one wave has summed its predecessors' words back to the nearest inclusive one.  No
+// ticket: one shared ticket word serialises its grabs (≈ 88 per µs, the guide's dequeue
+// price: 56 µs for config 5's 4 900 tiles).  HIP does not promise dispatch order, so the
+// wait is bounded: a tile that waited ~4 M probes gives up and sets error bit 0 (the build
+// then fails loudly) instead of hanging on a predecessor that was never dispatched.
 constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
 template <class KT, bool PACK = false>
 __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G, int64_t n, uint64_t* __restrict__ status,
@@ -2200,13 +2203,10 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
     __shared__ uint32_t wsum[MEMB_WAVES];
     __shared__ KT sk[MEMB_CAP];
     __shared__ uint32_t sv[PACK ? 1 : MEMB_CAP];
-    __shared__ uint32_t s_tile, s_base;
+    __shared__ uint32_t s_base;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t n_tiles = (n + MEMB_BLOCK * MEMB_U - 1) / (MEMB_BLOCK * MEMB_U);
-    uint32_t* ticket = reinterpret_cast<uint32_t*>(status + n_tiles);
-    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int64_t tile = s_tile;
+    const int64_t tile = blockIdx.x;
     if (tile >= n_tiles) return;                         // (the grid is exactly n_tiles)
     {
         const int64_t b = tile * (MEMB_BLOCK * MEMB_U), hi = imin64(n, b + MEMB_BLOCK * MEMB_U);
@@ -2334,95 +2334,47 @@ __device__ __forceinline__ uint32_t ord_class(const NodeDev&, uint32_t, uint32_t
     return (f & ESC_NF_TAINTED) ? 1u : 0u;
 }
 
-// A: the chunk's count per class.  A split chunk holds one group's memberships, so the
-// class is a function of the region word's flags alone: the group's dry mode comes with the
-// chunk (OrdChunk::pad & ORD_CHUNK_DRY) and region padding is flagged ESC_NF_ABSENT
-// (k_region_pad) like a deleted node.  Quads: one 16-B load per lane.
-__global__ __launch_bounds__(ORD_BLOCK) void k_ord_count(NodeDev N, const OrdChunk* __restrict__ chunks,
+// Split groups (region > ORD_CHUNK memberships), ONE pass (round 5; it replaced a counting
+// pass and a scatter pass that read every region word twice).  A split chunk holds one
+// group's memberships, so the class is a function of the region word's flags alone: the
+// group's dry mode comes with the chunk (OrdChunk::pad & ORD_CHUNK_DRY) and region padding
+// is flagged ESC_NF_ABSENT (k_region_pad) like a deleted node.  Every chunk loads its
+// region words (4 steps of 1 024, 4 per lane), classifies them, ranks them by packed DPP
+// wave scans and publishes its two class counts; its group's earlier chunks' counts come
+// from a decoupled look-back (one wave, 64 status words per probe, relaxed agent-scope
+// atomics), so the bases need no second pass over the words.  Output layout (DESIGN.md §4
+// K5): untainted forward from the region start, tainted BACKWARD from the region end — a
+// chunk knows how many tainted nodes precede it in its group but not how many untainted
+// nodes the whole group has — so the tainted segment is stored newest first.  Cordoned
+// nodes (class 2) feed neither order and are not written.  The group's last chunk writes
+// the segment bounds [start, start + untainted) and [end - tainted, end).
+// Status words: flag << 62 | n1 << 28 | n0 (class counts < 2^28: nodes < 2^28) for chunk
+// v = blockIdx.x in one of two arrays, ostat[par * n + v]; a decision uses array `par` and
+// zeroes its chunk's word of the other, which the next decision (parity flipped by the
+// host, a graph captured per parity) finds clear — no clearing launch (a memset before
+// every decision cost ~6 µs of the 30).  ostat[2n]: error word (a bounded look-back that
+// gave up: HIP does not promise dispatch order, so a chunk never waits unboundedly on one
+// that was not dispatched).  A ticket for in-order chunk ids would serialise ~2 800 grabs
+// on one word (≈ 32 µs: measured 49 µs per decision against 30 µs for the two-pass form).
+constexpr uint64_t OS_AGG = 1ull << 62, OS_INC = 2ull << 62;
+constexpr uint32_t OS_M = (1u << 28) - 1;
+__global__ __launch_bounds__(ORD_BLOCK) void k_ord_split(NodeDev N, const OrdChunk* __restrict__ chunks, int64_t n_chunks,
                                                          const uint32_t* __restrict__ g_memb,
-                                                         uint32_t* __restrict__ ccnt) {
-    __shared__ uint32_t red[ORD_WAVES][3];
-    const OrdChunk ch = chunks[blockIdx.x];
-    const uint32_t gword = (ch.pad & ORD_CHUNK_DRY) ? NODE_DRY_BIT : 0u;   // ord_class's group word
-    uint32_t c[3] = {0, 0, 0};
-    constexpr uint32_t STEP = 4 * ORD_BLOCK;
-    constexpr int H = ORD_CHUNK / STEP;                  // the whole chunk's quads in flight
-    for (uint32_t b0 = ch.start + 4 * threadIdx.x; b0 < ch.end; b0 += H * STEP) {
-        uint4 fl[H];
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-            const uint32_t b = b0 + h * STEP < ch.end ? b0 + h * STEP : b0;
-            fl[h] = ld4(g_memb + b);
-        }
-#pragma unroll
-        for (int h = 0; h < H; ++h) {
-            const uint32_t b = b0 + h * STEP;
-            if (b >= ch.end) break;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t k = b + j < ch.end ? ord_class(N, 0u, gword, lane4(fl[h], j) >> MEMB_FLAG_SHIFT) : 3u;
-                c[0] += k == 0;
-                c[1] += k == 1;
-                c[2] += k == 2;
-            }
-        }
-    }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < 3; ++k)
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) c[k] += __shfl_xor(c[k], o, 64);
-    if (lane == 0) for (int k = 0; k < 3; ++k) red[wid][k] = c[k];
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        uint32_t t = 0;
-        for (int w = 0; w < ORD_WAVES; ++w) t += red[w][threadIdx.x];
-        ccnt[(int64_t)blockIdx.x * 3 + threadIdx.x] = t;
-    }
-}
-
-// C: every chunk's untainted and tainted nodes into their class segments, stable.  All of
-// the chunk's class bytes and node ids are loaded up front (4 steps of 1024 memberships,
-// 4 per lane); per-class ranks come from packed DPP wave scans; the nodes are staged in
-// LDS in output order (class 0 then class 1) and written out with consecutive lanes on
-// consecutive addresses.  Cordoned nodes (class 2) feed neither order and are not written.
-// The chunk's output bases come from the class counts of its group's chunks (pass A):
-// wave 0 sums them (a group has few chunks), and the group's first chunk writes the
-// group's segment bounds (groups without memberships keep the bounds set at load).
-__global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(NodeDev N, const OrdChunk* __restrict__ chunks,
-                                                           const uint32_t* __restrict__ g_memb,
-                                                           const uint32_t* __restrict__ gch_off,
-                                                           const uint32_t* __restrict__ grp_off,
-                                                           const uint32_t* __restrict__ ccnt,
-                                                           uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
+                                                         const uint32_t* __restrict__ gch_off,
+                                                         const uint32_t* __restrict__ grp_off,
+                                                         uint64_t* __restrict__ ostat_all, int par,
+                                                         uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
+    uint64_t* __restrict__ ostat = ostat_all + (par ? n_chunks : 0);
+    uint64_t* __restrict__ onext = ostat_all + (par ? 0 : n_chunks);
+    uint64_t* __restrict__ oerr = ostat_all + 2 * n_chunks;
     constexpr int STEPS = ORD_CHUNK / (4 * ORD_BLOCK);
     __shared__ uint32_t wt[STEPS][ORD_WAVES];
     __shared__ uint32_t stage[ORD_CHUNK];
     __shared__ uint32_t s_base[2];
-    const OrdChunk ch = chunks[blockIdx.x];
+    const uint32_t v = blockIdx.x;
+    const OrdChunk ch = chunks[v];
+    if (threadIdx.x == 0) onext[v] = 0;                  // the next decision's word (last used two ago)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (wid == 0) {
-        const uint32_t g = ch.group, q0 = gch_off[g], q1 = gch_off[g + 1], me = blockIdx.x;
-        uint32_t t0 = 0, t1 = 0, t2 = 0, p0 = 0, p1 = 0;
-        for (uint32_t q = q0 + lane; q < q1; q += 64) {
-            const uint32_t c0 = ccnt[(int64_t)q * 3], c1 = ccnt[(int64_t)q * 3 + 1], c2 = ccnt[(int64_t)q * 3 + 2];
-            t0 += c0; t1 += c1; t2 += c2;
-            if (q < me) { p0 += c0; p1 += c1; }
-        }
-        t0 = (uint32_t)wave_sum64(t0); t1 = (uint32_t)wave_sum64(t1); t2 = (uint32_t)wave_sum64(t2);
-        p0 = (uint32_t)wave_sum64(p0); p1 = (uint32_t)wave_sum64(p1);
-        const uint32_t s0 = grp_off[g];
-        if (lane == 0) {
-            s_base[0] = s0 + p0;
-            s_base[1] = s0 + t0 + p1;
-            if (me == q0) {
-                seg[4 * (int64_t)g + 0] = s0;
-                seg[4 * (int64_t)g + 1] = (int64_t)s0 + t0;
-                seg[4 * (int64_t)g + 2] = (int64_t)s0 + t0 + t1;
-                seg[4 * (int64_t)g + 3] = (int64_t)s0 + t0 + t1 + t2;
-            }
-        }
-    }
     const uint32_t gword = (ch.pad & ORD_CHUNK_DRY) ? NODE_DRY_BIT : 0u;   // ord_class's group word
     uint32_t packed[STEPS];
     uint4 nd[STEPS];
@@ -2442,15 +2394,15 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(NodeDev N, const OrdC
     uint32_t ex[STEPS];
 #pragma unroll
     for (int st = 0; st < STEPS; ++st) {
-        uint32_t v = 0;                                  // class 0 | class 1 << 16
+        uint32_t x = 0;                                  // class 0 | class 1 << 16
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = (packed[st] >> (8 * j)) & 0xFF;
-            v += k == 0 ? 1u : (k == 1 ? 0x10000u : 0u);
+            x += k == 0 ? 1u : (k == 1 ? 0x10000u : 0u);
         }
-        const uint32_t inc = wave_incl_scan32(v);
+        const uint32_t inc = wave_incl_scan32(x);
         if (lane == 63) wt[st][wid] = inc;
-        ex[st] = inc - v;
+        ex[st] = inc - x;
     }
     __syncthreads();
     uint32_t tot = 0;                                    // chunk totals (packed)
@@ -2463,15 +2415,60 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(NodeDev N, const OrdC
             tot += wt[st][w];
         }
     const uint32_t n0 = tot & 0xFFFF, n1 = tot >> 16;
+    const uint32_t g = ch.group, q0 = gch_off[g];
+    if (threadIdx.x == 0)                                // the count first, then the look-back
+        __hip_atomic_store(ostat + v, (v == q0 ? OS_INC : OS_AGG) | ((uint64_t)n1 << 28) | n0, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    // stage in chunk order: class 0 ascending at [0, n0), class 1 descending at [n0, n0 + n1)
 #pragma unroll
     for (int st = 0; st < STEPS; ++st) {
         const uint32_t x = pre[st] + ex[st];
-        uint32_t r0 = x & 0xFFFF, r1 = n0 + (x >> 16);
+        uint32_t r0 = x & 0xFFFF, r1 = n0 + n1 - 1 - (x >> 16);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = (packed[st] >> (8 * j)) & 0xFF;
             if (k == 0) stage[r0++] = lane4(nd[st], j) & MEMB_NODE_MASK;
-            else if (k == 1) stage[r1++] = lane4(nd[st], j) & MEMB_NODE_MASK;
+            else if (k == 1) stage[r1--] = lane4(nd[st], j) & MEMB_NODE_MASK;
+        }
+    }
+    if (wid == 0) {                                      // look back over the group's earlier chunks
+        uint32_t e0 = 0, e1 = 0, spins = 0;
+        for (int64_t look = (int64_t)v - 1; look >= (int64_t)q0;) {
+            if (++spins > (1u << 22)) {                  // never reached: every earlier chunk runs
+                if (lane == 0) __hip_atomic_fetch_or(oerr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            const int64_t jj = look - lane;
+            const uint64_t w = jj >= (int64_t)q0 ? __hip_atomic_load(ostat + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                 : OS_INC;   // before the group: an inclusive 0
+            const bool ready = (w >> 62) != 0;
+            const unsigned long long inc = __ballot(ready && (w >> 62) == 2), wait = __ballot(!ready);
+            const int fi = inc ? __builtin_ctzll(inc) : 63;
+            const unsigned long long need = ~0ull >> (63 - fi);
+            if (wait & need) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            const bool mine = lane <= fi;
+            e0 += wave_total32(mine ? (uint32_t)(w & OS_M) : 0u);
+            e1 += wave_total32(mine ? (uint32_t)((w >> 28) & OS_M) : 0u);
+            if (inc) break;
+            look -= 64;
+        }
+        if (lane == 0) {
+            const uint32_t t0 = e0 + n0, t1 = e1 + n1;
+            if (v != q0)
+                __hip_atomic_store(ostat + v, OS_INC | ((uint64_t)t1 << 28) | t0, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t s0 = grp_off[g], e = grp_off[g + 1];
+            s_base[0] = s0 + e0;                         // class 0 output start
+            s_base[1] = e - e1 - n1;                     // class 1 output start (stored descending)
+            if (v + 1 == gch_off[g + 1]) {               // the group's last chunk: its bounds
+                seg[4 * (int64_t)g + 0] = s0;
+                seg[4 * (int64_t)g + 1] = (int64_t)s0 + t0;
+                seg[4 * (int64_t)g + 2] = (int64_t)e - t1;
+                seg[4 * (int64_t)g + 3] = e;
+            }
         }
     }
     __syncthreads();
@@ -2484,9 +2481,10 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_scatter(NodeDev N, const OrdC
 // quads): one pass, no cross-chunk prefix.  Classes are counted by one packed 64-bit block
 // scan (class 0 | class 1 << 21 | class 2 << 42) in membership order; a group's base is the
 // scan value at its region's first quad (hp, indexed by quad), its class totals come from
-// its region's last quad (tt), and the output segment of group g is [grp_off[g], ...):
-// class 0 then class 1, i.e. the chunk's own slots — so the nodes are staged in LDS and the
-// chunk written back coalesced.  The last quad of each group writes its segment bounds.
+// its region's last quad, and the output of group g lies in its own region: class 0 forward
+// from its start, class 1 backward from its end (the split groups' layout, k_ord_split) —
+// the chunk's own slots, so the nodes are staged in LDS and the chunk written back
+// coalesced.  The last quad of each group writes its segment bounds.
 // Inclusive 64-bit scan over the wave with DPP (see wave_total64).
 __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long v) {
     v += dpp64<0x111, 0xF>(v);
@@ -2510,7 +2508,6 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
     constexpr unsigned long long M = (1ull << C1) - 1;
     __shared__ unsigned long long wt[STEPS][ORD_WAVES];
     __shared__ unsigned long long hp[NQ];                // scan value at each group's first quad
-    __shared__ unsigned long long tt[NQ];                // each group's totals, at its first quad
     __shared__ uint32_t stage[CAP];
     const OrdChunk ch = chunks[blk];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -2575,27 +2572,26 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
                 inc += k == 0 ? 1ull : (k == 1 ? (1ull << C1) : (k == 2 ? (1ull << C2) : 0ull));
             }
             const unsigned long long t = inc - hp[hq[st]];
-            tt[hq[st]] = t;
-            const int64_t s0 = grp_off[g], t0 = (int64_t)(t & M), t1 = (int64_t)((t >> C1) & M), t2 = (int64_t)(t >> C2);
-            seg[4 * (int64_t)g + 0] = s0;
-            seg[4 * (int64_t)g + 1] = s0 + t0;
-            seg[4 * (int64_t)g + 2] = s0 + t0 + t1;
-            seg[4 * (int64_t)g + 3] = s0 + t0 + t1 + t2;
+            const int64_t s0 = grp_off[g], t0 = (int64_t)(t & M), t1 = (int64_t)((t >> C1) & M);
+            seg[4 * (int64_t)g + 0] = s0;                // untainted forward from the start,
+            seg[4 * (int64_t)g + 1] = s0 + t0;           // tainted newest first at the end
+            seg[4 * (int64_t)g + 2] = (int64_t)end - t1;
+            seg[4 * (int64_t)g + 3] = end;
         }
     }
     __syncthreads();
 #pragma unroll
     for (int st = 0; st < STEPS; ++st) {
         if (!ok[st]) continue;
-        const unsigned long long base = hp[hq[st]], t = tt[hq[st]];
+        const unsigned long long base = hp[hq[st]];
         const uint32_t s0 = (hq[st] << 2);               // the group's first slot, chunk-relative
-        const uint32_t t0 = (uint32_t)(t & M);
+        const uint32_t e1 = grp_off[mg(grp[st]) + 1] - ch.start - 1;   // its last slot
         uint32_t r0 = (uint32_t)((ex[st] - base) & M), r1 = (uint32_t)(((ex[st] - base) >> C1) & M);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t k = (cls[st] >> (8 * j)) & 0xFF;
             if (k == 0) stage[s0 + r0++] = lane4(nd[st], j) & MEMB_NODE_MASK;
-            else if (k == 1) stage[s0 + t0 + r1++] = lane4(nd[st], j) & MEMB_NODE_MASK;
+            else if (k == 1) stage[e1 - r1++] = lane4(nd[st], j) & MEMB_NODE_MASK;   // newest first at the end
         }
     }
     __syncthreads();
@@ -2655,7 +2651,7 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
 }
 
 // Region padding: g | MEMB_PAD after each group's memberships (node 0, flagged absent:
-// class 3 from the region word alone, k_ord_count).
+// class 3 from the region word alone, k_ord_split).
 __global__ __launch_bounds__(256) void k_region_pad(const uint32_t* __restrict__ pstart,
                                                     const uint32_t* __restrict__ plen, int32_t G,
                                                     uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_memb,
@@ -3097,14 +3093,11 @@ hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32
 }
 
 hipError_t launch_order(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
-                        const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
-                        int64_t n_e, int32_t G, uint32_t* ccnt, uint32_t* cbase, uint32_t* vals,
+                        const uint32_t* grp_off, const uint32_t* g_memb, uint64_t* ostat, int par, uint32_t* vals,
                         int64_t* seg, hipStream_t st) {
-    if (n_chunks > 0)
-        hipLaunchKernelGGL(k_ord_count, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, g_memb, ccnt);
-    if (n_chunks > 0)
-        hipLaunchKernelGGL(k_ord_scatter, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, g_memb, gch_off,
-                           grp_off, ccnt, vals, seg);
+    if (n_chunks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_ord_split, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, n_chunks, g_memb,
+                       gch_off, grp_off, ostat, par, vals, seg);
     return hipGetLastError();
 }
 

@@ -253,7 +253,9 @@ struct esc_ctx {
     int order_src = 0;
     // group order of the memberships (per-decision 3-way split by class inside each group)
     uint32_t *d_g_memb = nullptr, *d_g_grp = nullptr;   // K5 regions: membership words, group words
-    uint32_t *d_grp_off = nullptr, *d_gch_off = nullptr, *d_ccnt = nullptr, *d_cbase = nullptr;
+    uint32_t *d_grp_off = nullptr, *d_gch_off = nullptr;
+    uint64_t* d_ostat = nullptr;                              // k_ord_split status words (x2), error word
+    int ord_parity = 0;                                       // which status array the next ordering uses
     uint32_t *d_pstart = nullptr, *d_plen = nullptr;
     uint32_t* d_ord = nullptr;                                // K5 output, in the group regions
     OrdChunk* d_pchunks = nullptr;                            // packed chunks of small groups
@@ -497,8 +499,8 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out);
 // memberships) on stream st: the two-pass kernels and the packed small / mid-size groups.
 hipError_t enqueue_order(esc_ctx* c, hipStream_t st) {
     const hipError_t e = launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb,
-                                      c->d_g_grp, c->n_memb, c->gi.G, c->d_ccnt, c->d_cbase,
-                                      c->d_ord, c->d_seg, st);
+                                      c->d_ostat, c->ord_parity, c->d_ord, c->d_seg, st);
+    c->ord_parity ^= 1;
     if (e != hipSuccess) return e;
     return launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_memb, c->d_g_grp,
                                c->d_ord, c->d_seg, st);
@@ -506,25 +508,31 @@ hipError_t enqueue_order(esc_ctx* c, hipStream_t st) {
 
 // Replays (capturing on first use) the per-replica graph of enqueue_step(r, decide, decide)
 // on the context's stream: one launch instead of the step's kernels, events and waits.
+// With the ordering in the step there is one graph per (replica, ordering parity): the
+// split ordering alternates two status arrays (k_ord_split), and a graph holds its launch's.
 int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool decide) {
     const int nrep = (int)c->pods.size();
-    if ((int)gs.size() != nrep) {
+    if ((int)gs.size() != 2 * nrep) {
         for (auto& g : gs)
             if (g) hipGraphExecDestroy(g);
-        gs.assign(nrep, nullptr);
+        gs.assign(2 * (size_t)nrep, nullptr);
     }
-    if (!gs[r]) {
+    const bool ord = c->order_in_step;
+    const int k = 2 * r + (ord ? c->ord_parity : 0);
+    if (!gs[k]) {
         hipGraph_t graph = nullptr;
         HIP_TRY(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-        const int32_t rc = enqueue_step(c, r, decide, decide);
+        const int32_t rc = enqueue_step(c, r, decide, decide);          // flips the parity (ord)
         hipError_t e = hipStreamEndCapture(c->stream, &graph);
         if (rc) { if (graph) hipGraphDestroy(graph); return rc; }
         if (e != hipSuccess) return fail_hip(e, "hipStreamEndCapture");
-        e = hipGraphInstantiate(&gs[r], graph, nullptr, nullptr, 0);
+        e = hipGraphInstantiate(&gs[k], graph, nullptr, nullptr, 0);
         hipGraphDestroy(graph);
         if (e != hipSuccess) return fail_hip(e, "hipGraphInstantiate");
+    } else if (ord) {
+        c->ord_parity ^= 1;
     }
-    HIP_TRY(hipGraphLaunch(gs[r], c->stream));
+    HIP_TRY(hipGraphLaunch(gs[k], c->stream));
     return ESC_OK;
 }
 
@@ -563,7 +571,7 @@ void release_sort(esc_ctx* c) {
     c->mcap = 0;
     c->age_built = false;
     dfree(c->d_g_memb); dfree(c->d_g_grp);
-    dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks);
+    dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ostat); dfree(c->d_chunks);
     dfree(c->d_pstart); dfree(c->d_plen); dfree(c->d_ord); dfree(c->d_pchunks);
     c->n_pchunks = 0;
     c->n_chunks = 0;
@@ -709,11 +717,13 @@ int32_t build_age_index(esc_ctx* c) {
     // no clearing: the sort's last pass fills every group's [start, start + len), k_region_pad the
     // rest of its region
     if (fresh || (int64_t)chunks.size() != c->n_chunks || (int64_t)pchunks.size() != c->n_pchunks) {
-        dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ccnt); dfree(c->d_cbase); dfree(c->d_chunks);
+        dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ostat); dfree(c->d_chunks);
         dfree(c->d_pstart); dfree(c->d_plen); dfree(c->d_pchunks);
         HIP_TRY(dalloc(&c->d_grp_off, pstart.size())); HIP_TRY(dalloc(&c->d_gch_off, gch_off.size()));
-        HIP_TRY(dalloc(&c->d_ccnt, std::max<size_t>(chunks.size(), 1) * 3));
-        HIP_TRY(dalloc(&c->d_cbase, std::max<size_t>(chunks.size(), 1) * 3));
+        HIP_TRY(dalloc(&c->d_ostat, 2 * chunks.size() + 1));
+        HIP_TRY(hipMemsetAsync(c->d_ostat, 0, (2 * chunks.size() + 1) * 8, st));
+        c->ord_parity = 0;
+        drop_graphs(c);                                 // captured steps hold the old tables
         HIP_TRY(dalloc(&c->d_chunks, std::max<size_t>(chunks.size(), 1)));
         HIP_TRY(dalloc(&c->d_pchunks, std::max<size_t>(pchunks.size(), 1)));
         HIP_TRY(dalloc(&c->d_pstart, pstart.size())); HIP_TRY(dalloc(&c->d_plen, plen.size()));
@@ -765,15 +775,13 @@ int32_t build_age_index(esc_ctx* c) {
         HIP_TRY(launch_age_sort(n, g, c->d_lstat, c->d_total, c->n_memb, c->mcap, c->ts_min, c->sort_div, c->sort_R,
                                 gbits, cshift, c->d_mkeys, c->d_mvals, c->d_hist, c->d_tot, sink, st));
         HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_grp, c->d_g_memb, c->d_seg, st));
-        const bool need_err = check || cshift > 0;
-        if (need_err) {                             // the error word and the listed total
-            h_err[0] = 0;
-            h_err[1] = 0;
-            HIP_TRY(hipMemcpyAsync(c->h_istage, c->d_ierr, 4, hipMemcpyDeviceToHost, st));
-            if (check) HIP_TRY(hipMemcpyAsync(c->h_istage + 4, c->d_total, 4, hipMemcpyDeviceToHost, st));
-        }
+        // the error word (the listing's bounded look-back, region counts, the run fix-up) and
+        // the listed total, read at the build's one wait
+        h_err[0] = 0;
+        h_err[1] = 0;
+        HIP_TRY(hipMemcpyAsync(c->h_istage, c->d_ierr, 4, hipMemcpyDeviceToHost, st));
+        if (check) HIP_TRY(hipMemcpyAsync(c->h_istage + 4, c->d_total, 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        if (!need_err) break;
         const uint32_t err = h_err[0];
         if (check && nl && h_err[1] != total) return fail_hip(hipErrorUnknown, "age index: membership total");
         if (err & 1u) return fail_hip(hipErrorUnknown, "age index: membership count");
@@ -1199,9 +1207,9 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
                              ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, st));
     if (int32_t rc = mark()) return rc;
     if (ord) {                                       // split groups, mid-size packed chunks
-        HIP_TRY(launch_order(n, c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb, c->d_g_grp,
-                             c->n_memb, c->gi.G, c->d_ccnt, c->d_cbase, c->d_ord, c->d_seg,
-                             st));
+        HIP_TRY(launch_order(n, c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb, c->d_ostat,
+                             c->ord_parity, c->d_ord, c->d_seg, st));
+        c->ord_parity ^= 1;
         HIP_TRY(launch_order_packed(n, c->d_pchunks + c->n_psmall, c->n_pchunks - c->n_psmall, 0, c->d_grp_off,
                                     c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, st));
     }
@@ -4245,8 +4253,13 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
     if (!c->sorted) return ESC_E_STATE;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    // class segments [b0, b1) (untainted), [b1, b2) (tainted), both in age order
-    const int64_t so = which;
+    if (c->d_ostat && c->n_chunks) {                  // a split-group ordering that gave up waiting
+        uint64_t e = 0;
+        HIP_TRY(hipMemcpy(&e, c->d_ostat + 2 * c->n_chunks, 8, hipMemcpyDeviceToHost));
+        if (e) return fail_hip(hipErrorUnknown, "ordering: look-back bound");
+    }
+    // class segments [s0, s1) (untainted, oldest first) and [s2, s3) (tainted, newest first)
+    const int64_t so = 2 * which;
     int64_t seg[2];
     HIP_TRY(hipMemcpy(seg, c->d_seg + 4 * (int64_t)group + so, 16, hipMemcpyDeviceToHost));
     const int64_t cnt = seg[1] - seg[0];
@@ -4260,17 +4273,17 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
         for (int64_t i = 0; i < m; ++i) idx_out[i] = v[i];
         return ESC_OK;
     }
-    // untaintNewestN: the segment backwards; equal creation times keep ascending snapshot
-    // index (the age index breaks ties that way), so read on until the tie run that
-    // straddles position m ends, then sort each run of equal times by index.
+    // untaintNewestN: the segment is stored newest first; equal creation times keep
+    // ascending snapshot index (the age index breaks ties that way, so the stored run is
+    // descending), so read on until the tie run that straddles position m ends, then sort
+    // each run of equal times by index.
     const int64_t lo_ts = c->node_lo;
     auto ts = [&](uint32_t i) { return c->h_created[(int64_t)i - lo_ts]; };
     int64_t take = std::min(cnt, m + 64);
     std::vector<uint32_t> v;
     for (;;) {
         v.resize(take);
-        HIP_TRY(hipMemcpy(v.data(), vals + seg[1] - take, take * 4, hipMemcpyDeviceToHost));
-        std::reverse(v.begin(), v.end());
+        HIP_TRY(hipMemcpy(v.data(), vals + seg[0], take * 4, hipMemcpyDeviceToHost));
         if (take == cnt || ts(v[take - 1]) != ts(v[m - 1])) break;
         take = std::min(cnt, take * 2);
     }

@@ -29,7 +29,7 @@ import os
 import statistics
 
 PEAK_GBS = 8000.0
-ORDER_KERNELS = ("k_ord_count", "k_ord_scatter", "k_ord_packed")
+ORDER_KERNELS = ("k_ord_split", "k_ord_packed")
 
 
 def ours(k):
@@ -97,8 +97,8 @@ def main():
     b = json.load(open(a.bench)) if a.bench else None
     if b and b["metric"].startswith("config5"):
         # config 5: the per-decision ordering kernels of the cold (cache-flushed) decisions
-        # bench.py times last (--last = its steps + the final sort); algorithmic bytes =
-        # SURVEY.md §8(d)'s 12 B per membership
+        # bench.py times last (--last = its steps + the final sort); bytes = the bench line's
+        # roofline bytes per decision (8 B moved per membership; its bytes_8d: §8(d)'s 12 B)
         ks = [k for k in ORDER_KERNELS if k in res["kernels"]]
         t_ns = sum(res["kernels"][k]["mean_ns"] for k in ks)
         algo = b["roofline"]["bytes_per_decision"]

@@ -344,6 +344,34 @@ def test_age_index_sizes_vs_c_oracle(esc, N):
             assert np.array_equal(ctx.group_order(g, which), soa.order(nodes, s.groups, g, which)), (N, g, which)
 
 
+@pytest.mark.parametrize("run", [2, 8, 9, 64])
+def test_age_index_coarse_key_runs_vs_c_oracle(esc, run):
+    """The age index's 32-bit coarse keys: with the creation range widened
+    past the bits a key keeps, `run` members of one group share ONE timestamp and `run` more
+    lie within one coarse-key bucket (times descending with the index).  Runs of <= 8 equal
+    coarse keys are ordered exactly by k_age_fix; a longer run sends the build back to the
+    exact 64-bit keys.  Every group's two orders against the C oracle, before and after a
+    rebuild."""
+    s = esc.Synth(2_000, 20_000, 7, config=5, seed=0xE5CA1A7E00000200 + run)
+    pods = s.pods()
+    nodes = {k: np.array(v, copy=True) for k, v in s.nodes().items()}
+    t = nodes["created_ns"]
+    t[0] = int(t.min()) - (1 << 37) - 1              # range > 2^37 ns, divisor 1: bits dropped
+    m = [j for j in _members_oldest(nodes, s.groups, 1) if j != 0]
+    assert len(m) >= 2 * run
+    mid = int(np.median(t))
+    t[m[:run]] = mid + 7                              # exact ties: equal keys at any width
+    t[m[run:2 * run]] = mid + (1 << 30) + np.arange(run)[::-1]   # one bucket, times falling
+    ctx = esc.Context(s)
+    ctx.load(pods, nodes)
+    for _ in range(2):
+        ctx.sort_nodes()
+        for g in range(len(s.groups)):
+            for which in (0, 1):
+                assert np.array_equal(ctx.group_order(g, which), soa.order(nodes, s.groups, g, which)), (run, g, which)
+        ctx.build_age_index()
+
+
 @pytest.mark.parametrize("graph,N", [(False, 200_000), (True, 200_000), (True, 30_000), (True, 700_000)])
 def test_order_in_step_vs_c_oracle(esc, graph, N):
     """esc_set_order_in_step: the K5 ordering inside every decision (side stream beside K1,
