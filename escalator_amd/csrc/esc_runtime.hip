@@ -256,6 +256,7 @@ struct esc_ctx {
     uint32_t *d_grp_off = nullptr, *d_gch_off = nullptr;
     uint64_t* d_ostat = nullptr;                              // k_ord_split status words (x2), error word
     int ord_parity = 0;                                       // which status array the next ordering uses
+    bool ord_err_read = false;                                // the error word was read since the last ordering
     uint32_t *d_pstart = nullptr, *d_plen = nullptr;
     uint32_t* d_ord = nullptr;                                // K5 output, in the group regions
     OrdChunk* d_pchunks = nullptr;                            // packed chunks of small groups
@@ -501,6 +502,7 @@ hipError_t enqueue_order(esc_ctx* c, hipStream_t st) {
     const hipError_t e = launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb,
                                       c->d_ostat, c->ord_parity, c->d_ord, c->d_seg, st);
     c->ord_parity ^= 1;
+    c->ord_err_read = false;
     if (e != hipSuccess) return e;
     return launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_memb, c->d_g_grp,
                                c->d_ord, c->d_seg, st);
@@ -531,6 +533,7 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
         if (e != hipSuccess) return fail_hip(e, "hipGraphInstantiate");
     } else if (ord) {
         c->ord_parity ^= 1;
+        c->ord_err_read = false;
     }
     HIP_TRY(hipGraphLaunch(gs[k], c->stream));
     return ESC_OK;
@@ -1210,6 +1213,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
         HIP_TRY(launch_order(n, c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb, c->d_ostat,
                              c->ord_parity, c->d_ord, c->d_seg, st));
         c->ord_parity ^= 1;
+        c->ord_err_read = false;
         HIP_TRY(launch_order_packed(n, c->d_pchunks + c->n_psmall, c->n_pchunks - c->n_psmall, 0, c->d_grp_off,
                                     c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, st));
     }
@@ -2120,7 +2124,13 @@ int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
         c->k1_share = sh;
         return touch_refresh(c, plan);
     };
-    constexpr int REPS = 3;                              // decisions averaged per round (noise ~1-4 %)
+#ifndef ESC_CAL_REPS
+#define ESC_CAL_REPS 3       // (timing builds may override)
+#endif
+#ifndef ESC_CAL_STEP
+#define ESC_CAL_STEP 0.5
+#endif
+    constexpr int REPS = ESC_CAL_REPS;                   // decisions averaged per round (noise ~1-4 %)
     for (int32_t r = 0; r <= rounds; ++r) {
         // per workgroup: its start offset from the grid's first start (the XCDs are dispatched
         // ~1.4 us apart, the same XCD order every launch), its K phase, and what follows it
@@ -2145,7 +2155,7 @@ int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
         // not K phases — a workgroup of a late XCD or with a long flush gets less weight
         double mx = 0, rsum = 0, rfix = 0;
         for (int64_t b = 0; b < nblk; ++b) {
-            mx = std::max(mx, st[b] + kp[b] + tl[b]);
+            mx = std::max(mx, st[b] + kp[b] + tl[b]);    // (the REPS-mean end of the latest workgroup)
             const double rate = share[b] / kp[b];        // share per tick while streaming
             rsum += rate;
             rfix += rate * (st[b] + tl[b]);
@@ -2160,7 +2170,7 @@ int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
         double sum = 0;
         for (int64_t b = 0; b < nblk; ++b) {
             const double want = std::max(0.25 * share[b], share[b] / kp[b] * (T - st[b] - tl[b]));
-            sum += (next[b] = 0.5 * share[b] + 0.5 * want);
+            sum += (next[b] = (1.0 - ESC_CAL_STEP) * share[b] + ESC_CAL_STEP * want);
         }
         for (double& x : next) x /= sum;
         if (upload(next) != ESC_OK) break;               // outside the exactness bound: stop here
@@ -4253,10 +4263,11 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
     if (!c->sorted) return ESC_E_STATE;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->d_ostat && c->n_chunks) {                  // a split-group ordering that gave up waiting
+    if (c->d_ostat && c->n_chunks && !c->ord_err_read) {   // once per ordering: a split chunk that gave up
         uint64_t e = 0;
         HIP_TRY(hipMemcpy(&e, c->d_ostat + 2 * c->n_chunks, 8, hipMemcpyDeviceToHost));
         if (e) return fail_hip(hipErrorUnknown, "ordering: look-back bound");
+        c->ord_err_read = true;
     }
     // class segments [s0, s1) (untainted, oldest first) and [s2, s3) (tainted, newest first)
     const int64_t so = 2 * which;

@@ -2,7 +2,7 @@
 per workgroup its XCD, K weight, class runs, start / K-phase / end times over several
 decisions, before and after the share calibration (esc_k1_calibrate).
 
-    SHARD_OF=8 python scripts/k1_shard_diag.py > out.json
+    SHARD_OF=8 [CAL_MORE=32,32] python scripts/k1_shard_diag.py > out.json
 """
 import json
 import os
@@ -50,6 +50,10 @@ def summarize(rs):
 out = {"shard_of": W, "pods": hi - lo, "uncalibrated": summarize(runs())}
 c.k1_calibrate(16)
 out["calibrated"] = summarize(runs())
+# CAL_MORE=32,32: further esc_k1_calibrate calls (continuing from the current shares)
+for i, r in enumerate(x for x in os.environ.get("CAL_MORE", "").split(",") if x):
+    c.k1_calibrate(int(r))
+    out["calibrated_more_%d" % i] = summarize(runs())
 c.set_timing(True)
 st = []
 for _ in range(10):
