@@ -2125,10 +2125,10 @@ int32_t esc_k1_calibrate(esc_ctx* c, int32_t rounds) {
         return touch_refresh(c, plan);
     };
 #ifndef ESC_CAL_REPS
-#define ESC_CAL_REPS 3       // (timing builds may override)
+#define ESC_CAL_REPS 8       // (timing builds may override; r05cal2: 8 decisions per round, 0.7 steps)
 #endif
 #ifndef ESC_CAL_STEP
-#define ESC_CAL_STEP 0.5
+#define ESC_CAL_STEP 0.7
 #endif
     constexpr int REPS = ESC_CAL_REPS;                   // decisions averaged per round (noise ~1-4 %)
     for (int32_t r = 0; r <= rounds; ++r) {
