@@ -6,6 +6,8 @@
 #                    config 5 (orderings + age index)
 #   rehearse2        N = 2 on one device: two gloo ranks (bench.py --gpus 2, ESC_BENCH_BACKEND=gloo,
 #                    ESC_BENCH_DEVICE=0), and one process driving two shards (peer exchange)
+#   rehearse2c5      config 5 (10 M nodes) at N = 2 on one device: two gloo ranks, each ordering its
+#                    half of the nodes, the merged selections checked against the oracle
 #   prof:NAME        rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE and --pmc
 #                    WRITE_SIZE passes of the same bench command, reduced by scripts/prof_summary.py
 #                    to $OUT/profiles/summary_NAME.json.  NAME: full (config 4), shard8, config5
@@ -68,6 +70,13 @@ rehearse2() {
     ESC_BENCH_DEVICES=0,0 timeout -k 10 600 python3 -u bench.py --gpus 2 --single-process --steps 10 --warmup 3 \
         --no-cpu-baseline > $OUT/bench_n2_multi.json 2> $OUT/bench_n2_multi.err || { tail -30 $OUT/bench_n2_multi.err; return 1; }
     cut -c1-900 $OUT/bench_n2_multi.json
+}
+
+rehearse2c5() {
+    echo "[gpu] $(date +%T) N = 2 rehearsal of config 5: two gloo ranks on device 0"
+    ESC_BENCH_BACKEND=gloo ESC_BENCH_DEVICE=0 timeout -k 10 600 python3 -u bench.py --config 5 --gpus 2 --steps 10 \
+        --warmup 3 > $OUT/bench5_n2_gloo.json 2> $OUT/bench5_n2_gloo.err || { tail -30 $OUT/bench5_n2_gloo.err; return 1; }
+    cut -c1-900 $OUT/bench5_n2_gloo.json
 }
 
 prof() {       # name
@@ -164,6 +173,7 @@ for stage in "$@"; do
         suite) suite || exit 1 ;;
         bench) bench || exit 1 ;;
         rehearse2) rehearse2 || exit 1 ;;
+        rehearse2c5) rehearse2c5 || exit 1 ;;
         prof:*) prof ${stage#prof:} || exit 1 ;;
         pmcsq:*) pmcsq ${stage#pmcsq:} || exit 1 ;;
         variants:*) variants ${stage#variants:} || exit 1 ;;
