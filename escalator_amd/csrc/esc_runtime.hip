@@ -570,6 +570,7 @@ void release_placement(esc_ctx* c) {
 }
 
 void release_sort(esc_ctx* c) {
+    drop_graphs(c);                                     // captured steps hold the index's buffers
     for (int i = 0; i < 2; ++i) { dfree(c->d_mkeys[i]); dfree(c->d_mvals[i]); }
     c->mcap = 0;
     c->age_built = false;
@@ -713,6 +714,7 @@ int32_t build_age_index(esc_ctx* c) {
     gch_off[g.G] = (uint32_t)chunks.size();
     const int64_t npad = pstart[g.G];
     if (fresh || npad != c->n_gpad) {
+        drop_graphs(c);                                 // captured steps hold the old regions
         dfree(c->d_g_memb); dfree(c->d_g_grp); dfree(c->d_ord);
         HIP_TRY(dalloc(&c->d_g_memb, npad)); HIP_TRY(dalloc(&c->d_g_grp, npad)); HIP_TRY(dalloc(&c->d_ord, npad));
     }

@@ -408,6 +408,15 @@ def test_order_in_step_vs_c_oracle(esc, graph, N):
     for g in range(0, 100, 3):
         for which in (0, 1):
             assert np.array_equal(ctx.group_order(g, which), full[(g, which)]), (g, which)
+    # an explicit index rebuild, then decisions through the (re)captured step: the ordering's
+    # status arrays alternate by decision parity, so run an odd and an even number
+    ctx.build_age_index()
+    for k in range(3):
+        ctx.run()
+        ctx.results()
+        for g in range(k, 100, 7):
+            for which in (0, 1):
+                assert np.array_equal(ctx.group_order(g, which), full[(g, which)]), (k, g, which)
 
 
 @pytest.mark.parametrize("seed", range(6))
