@@ -2134,7 +2134,11 @@ __device__ __forceinline__ void node_groups_c0(const NodeDev& N, const GroupDev&
         }
     }
 }
-constexpr int MEMB_U = 4;                            // consecutive nodes per thread per round
+#ifndef ESC_MEMB_U
+#define ESC_MEMB_U 4         // consecutive nodes per thread per tile (a multiple of 4; timing builds may override)
+#endif
+constexpr int MEMB_U = ESC_MEMB_U;
+static_assert(MEMB_U % 4 == 0, "16-B loads of 4 nodes");
 constexpr int MEMB_BLOCK = 512, MEMB_WAVES = MEMB_BLOCK / 64;
 // LDS staging of one round's memberships (1.5 per node; a round with more stores directly)
 constexpr int MEMB_CAP = MEMB_BLOCK * MEMB_U * 3 / 2;
@@ -2144,13 +2148,17 @@ __device__ __forceinline__ void memb_load(const NodeDev& N, int64_t r0, int64_t 
                                           uint32_t (&l0)[MEMB_U], int64_t* cr) {
     const int64_t i0 = N.lo + r0;
     if (r0 + MEMB_U <= hi && (i0 & 3) == 0) {
-        const uint4 a = *reinterpret_cast<const uint4*>(N.flags + i0), b = *reinterpret_cast<const uint4*>(N.label0 + i0);
-        f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
-        l0[0] = b.x; l0[1] = b.y; l0[2] = b.z; l0[3] = b.w;
-        if (cr) {
-            const longlong2 c0 = *reinterpret_cast<const longlong2*>(N.created + i0);
-            const longlong2 c1 = *reinterpret_cast<const longlong2*>(N.created + i0 + 2);
-            cr[0] = c0.x; cr[1] = c0.y; cr[2] = c1.x; cr[3] = c1.y;
+#pragma unroll
+        for (int q = 0; q < MEMB_U; q += 4) {
+            const uint4 a = *reinterpret_cast<const uint4*>(N.flags + i0 + q);
+            const uint4 b = *reinterpret_cast<const uint4*>(N.label0 + i0 + q);
+            f[q] = a.x; f[q + 1] = a.y; f[q + 2] = a.z; f[q + 3] = a.w;
+            l0[q] = b.x; l0[q + 1] = b.y; l0[q + 2] = b.z; l0[q + 3] = b.w;
+            if (cr) {
+                const longlong2 c0 = *reinterpret_cast<const longlong2*>(N.created + i0 + q);
+                const longlong2 c1 = *reinterpret_cast<const longlong2*>(N.created + i0 + q + 2);
+                cr[q] = c0.x; cr[q + 1] = c0.y; cr[q + 2] = c1.x; cr[q + 3] = c1.y;
+            }
         }
         return;
     }
