@@ -581,20 +581,23 @@ int32_t esc_removal_nodes(esc_ctx* ctx, int32_t group, int64_t* idx_out, int64_t
  * Writes up to `cap` snapshot node indices; *n_out = number of members in that list.
  * Ties (equal timestamps) are broken by snapshot index (Go's sort.Sort is unstable,
  * so its tie order is not reproducible).                             */
-/* esc_load_nodes builds the AGE INDEX once per snapshot: the node range sorted by
- * creation time (LSD radix sort) and the group memberships listed in that order.
+/* esc_load_nodes builds the AGE INDEX once per snapshot: the group memberships listed in
+ * one pass and sorted by (group, creation time) (LSD radix sort of coarse keys + an exact
+ * fix-up of equal-key runs; exact 64-bit keys when a run is too long).
  * esc_sort_nodes (async, per decision) classifies every membership (filterNodes,
- * controller.go:120-154) and stable-partitions by (group, class); a group's untainted
- * segment is then oldest-first and its tainted one, read backwards, newest-first.
+ * controller.go:120-154) and stable-partitions by (group, class) in one pass: a group's
+ * untainted segment is stored oldest-first from its region's start, its tainted segment
+ * newest-first from its region's end (esc_group_order reads both forward).
  * esc_build_age_index rebuilds the index (snapshot ingestion; exposed for measurement).
  * The index carries node indices in 28 bits: a node table of 2^28 slots or more returns
  * ESC_E_LIMIT.  Its group starts come from the host's live entry counts; the device's own
- * counts are checked against them on a fresh build (every build with ESC_CHECK_INDEX=1),
- * a mismatch returning ESC_E_HIP.                                                       */
+ * total is checked against them on a fresh build (every build with ESC_CHECK_INDEX=1),
+ * a mismatch (or a listing or ordering chunk that gave up its bounded wait) returning
+ * ESC_E_HIP.                                                                              */
 int32_t esc_sort_nodes(esc_ctx* ctx);
 /* Include the per-decision ordering in every decision (esc_run / esc_reduce / esc_step):
  * the packed small groups are ordered by blocks of the step's fused tail launch (after K1,
- * beside the fold and K2), the larger groups by the split kernels right after it, all on
+ * beside the fold and K2), the larger groups by the split kernel right after it, all on
  * the context's one stream (and in its graph when esc_use_graph); esc_group_order is then
  * valid after each decision without a separate esc_sort_nodes (one
  * decision = membership, sums, percentages, deltas and oldest-first ordering). */
