@@ -1818,46 +1818,25 @@ __global__ __launch_bounds__(256) void k_rs_scan_rows(uint32_t* __restrict__ his
     if (d >= nb) return;
     uint32_t* row = hist + (int64_t)d * nblk;
     uint32_t carry = 0;
-    for (int b0 = 0; b0 < nblk; b0 += 64) {
-        const int b = b0 + lane;
-        const uint32_t v = b < nblk ? row[b] : 0;
-        uint32_t x = v;
+    constexpr int RW = 8;                                // the row's loads in flight (rows <= 512 go in one round)
+    for (int b0 = 0; b0 < nblk; b0 += 64 * RW) {
+        uint32_t v[RW];
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
+        for (int r = 0; r < RW; ++r) {
+            const int b = b0 + r * 64 + lane;
+            v[r] = b < nblk ? row[b] : 0u;
         }
-        if (b < nblk) row[b] = carry + x - v;
-        carry += __shfl(x, 63, 64);
+#pragma unroll
+        for (int r = 0; r < RW; ++r) {
+            const int b = b0 + r * 64 + lane;
+            const uint32_t x = wave_incl_scan32(v[r]);   // DPP, no LDS round trips
+            if (b < nblk) row[b] = carry + x - v[r];
+            carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+        }
     }
     if (lane == 0) tot[d] = carry;
 }
 
-// Exclusive scan of the digit totals in place (one workgroup, nb <= 4096).
-__global__ __launch_bounds__(SORT_BLOCK) void k_rs_scan_tot(uint32_t* __restrict__ tot, int nb) {
-    __shared__ uint32_t wsum[SORT_WAVES];
-    __shared__ uint32_t carry;
-    if (threadIdx.x == 0) carry = 0;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int b0 = 0; b0 < nb; b0 += SORT_BLOCK) {
-        __syncthreads();
-        const int i = b0 + threadIdx.x;
-        const uint32_t v = i < nb ? tot[i] : 0;
-        uint32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) wsum[wid] = x;
-        __syncthreads();
-        uint32_t pre = carry;
-        for (int k = 0; k < wid; ++k) pre += wsum[k];
-        if (i < nb) tot[i] = pre + x - v;
-        __syncthreads();
-        if (threadIdx.x == 0) for (int k = 0; k < SORT_WAVES; ++k) carry += wsum[k];
-    }
-}
 
 // Stable scatter of one pass, a chunk of RS_U * SORT_BLOCK keys at a time: ranks from
 // ballot matching per wave and per-(round, wave) digit counts; the chunk is reordered by
@@ -1932,7 +1911,17 @@ __global__ RS_SCATTER_BOUNDS void k_rs_scatter(const KT* __restrict__ kin, const
     __shared__ VT cv[HASV ? CD : 1][CW];
     __shared__ uint32_t c_n[CD], c_s[CD], c_e[CD];        // carry count, carry start, write end
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, t = threadIdx.x;
-    if (t < NB) run[t] = tot[t] + hist[(int64_t)t * gridDim.x + blockIdx.x];
+    {   // the digits' start: the exclusive scan of the digit totals (round 5: every block scans
+        // the NB totals itself instead of a one-workgroup launch per pass), + this block's
+        // prefix of its digit row (k_rs_scan_rows)
+        const uint32_t dv = t < NB ? tot[t] : 0u;
+        const uint32_t xi = wave_incl_scan32(dv);
+        if (lane == 63) ws[wid] = xi;
+        __syncthreads();
+        uint32_t base = xi - dv;
+        for (int k = 0; k < wid; ++k) base += ws[k];
+        if (t < NB) run[t] = base + hist[(int64_t)t * gridDim.x + blockIdx.x];
+    }
     if (CARRY && t < NB) c_n[t] = 0;
     for (int e = t; e < S * NB / 2; e += SORT_BLOCK) reinterpret_cast<uint32_t*>(&wh[0][0])[e] = 0;
     const int64_t per = (n + gridDim.x - 1) / gridDim.x;
@@ -2989,7 +2978,6 @@ hipError_t rs_pass(const KT* kin, const VT* vin, KT* kout, VT* vout, int64_t n, 
     const int nblk = rs_blocks(n), nb = 1 << BITS;
     hipLaunchKernelGGL((k_rs_hist<KT, BITS>), dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, n, shift, hist);
     hipLaunchKernelGGL(k_rs_scan_rows, dim3((nb + 3) / 4), dim3(256), 0, st, hist, nblk, nb, tot);
-    hipLaunchKernelGGL(k_rs_scan_tot, dim3(1), dim3(SORT_BLOCK), 0, st, tot, nb);
     hipLaunchKernelGGL((k_rs_scatter<KT, VT, BITS, FINAL>), dim3(nblk), dim3(SORT_BLOCK), 0, st, kin, vin, kout, vout, n,
                        shift, hist, tot, S);
     return hipGetLastError();
