@@ -2069,12 +2069,10 @@ __global__ RS_SCATTER_BOUNDS void k_rs_scatter(const KT* __restrict__ kin, const
 // thousand memberships) and short; one longer than AF_RUN sets bit 2 of *S.err and the
 // host rebuilds the index with the exact 64-bit keys.
 constexpr int AF_RUN = 8;
-__global__ __launch_bounds__(256) void k_age_fix(const uint32_t* __restrict__ keys, int64_t n, RegionSink S,
-                                                 const int64_t* __restrict__ created, int64_t ts_min) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t k = keys[i];
-    if ((i > 0 && keys[i - 1] == k) || i + 1 >= n || keys[i + 1] != k) return;     // not a run's first
+// One run of equal coarse keys starting at sorted position i (len >= 2 members), put in
+// exact (creation time, node) order in its group's region.
+__device__ __forceinline__ void age_fix_run(const uint32_t* __restrict__ keys, int64_t n, const RegionSink& S,
+                                            const int64_t* __restrict__ created, int64_t ts_min, int64_t i, uint32_t k) {
     int len = 2;
     while (len <= AF_RUN && i + len < n && keys[i + len] == k) ++len;
     if (len > AF_RUN) { atomicOr(S.err, 2u); return; }
@@ -2101,6 +2099,32 @@ __global__ __launch_bounds__(256) void k_age_fix(const uint32_t* __restrict__ ke
 #pragma unroll
     for (int j = 0; j < AF_RUN; ++j)
         if (j < len) S.g_memb[d0 + j] = w[j];
+}
+
+// Grid-stride over quads of the sorted coarse keys (one 16-B load + the neighbours at the
+// quad's ends): a position starts a run when its key equals the next one and not the
+// previous one.  Runs are rare (config 5: a handful per 10^4 memberships), so the pass is
+// a streaming read of the keys; one thread per key (43 k blocks) took 39 µs for it.
+__global__ __launch_bounds__(256) void k_age_fix(const uint32_t* __restrict__ keys, int64_t n, RegionSink S,
+                                                 const int64_t* __restrict__ created, int64_t ts_min) {
+    const int64_t nq = (n + 3) / 4;
+    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
+        const int64_t i0 = 4 * q;
+        uint32_t k[6];                                   // keys[i0 - 1 .. i0 + 4]; absent ends never match
+        if (i0 + 4 <= n) {
+            const uint4 v = *reinterpret_cast<const uint4*>(keys + i0);
+            k[1] = v.x; k[2] = v.y; k[3] = v.z; k[4] = v.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) k[1 + j] = i0 + j < n ? keys[i0 + j] : ~keys[n - 1];
+        }
+        k[0] = i0 > 0 ? keys[i0 - 1] : ~k[1];
+        k[5] = i0 + 4 < n ? keys[i0 + 4] : ~k[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (i0 + j + 1 < n && k[1 + j] == k[2 + j] && k[j] != k[1 + j])
+                age_fix_run(keys, n, S, created, ts_min, i0 + j, k[1 + j]);
+    }
 }
 
 // ---- the age index (load time): memberships listed in snapshot order (streaming over
@@ -3061,7 +3085,7 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, uint64_t* statu
         const hipError_t e = rs_sort<uint64_t, NoVal>(keys, nv, n_memb, 32, hist, tot, &src, S, st, 32);
         if (e != hipSuccess) return e;
         if (S.fix)                                   // the final pass's coarse keys (u32) in keys[src]
-            hipLaunchKernelGGL(k_age_fix, dim3((unsigned)((n_memb + 255) / 256)), dim3(256), 0, st,
+            hipLaunchKernelGGL(k_age_fix, dim3((unsigned)std::min<int64_t>(4096, (n_memb + 1023) / 1024)), dim3(256), 0, st,
                                reinterpret_cast<const uint32_t*>(keys[src]), n_memb, S, nd.created, ts_min);
     }
     return hipGetLastError();
