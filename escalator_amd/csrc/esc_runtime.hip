@@ -2227,20 +2227,26 @@ int32_t esc_k1_time(esc_ctx* c, int32_t reps, double* ms_per_launch) {
     if (c->force_wide || !c->nblk) return ESC_E_STATE;
     hipSetDevice(c->device);
     hipStream_t st = c->stream;
-    const PodDev p = pod_dev(c, c->cur);
     const GroupDev g = group_dev(c);
     const int32_t S = (int32_t)pod_slots(c);
+    const int nrep = (int)c->pods.size();
     HIP_TRY(hipStreamSynchronize(st));
     HIP_TRY(hipEventRecord(c->k1t_ev[0], st));
     // every K1 launch of a step (its LDS windows and the big C tiles, so the pod bytes the
-    // roofline divides are all timed); no trace, so esc_k1_trace keeps the last decision's
+    // roofline divides are all timed); no trace, so esc_k1_trace keeps the last decision's.
+    // The launches rotate over the replicas as the decisions do: a shard small enough for
+    // the 256 MB Infinity Cache, launched on one replica back to back, is read from the
+    // cache, not HBM (round 5, a rank of 8's 124 MB: 29.7-30.0 us on one replica, 30.7-31.1
+    // rotating)
     for (int32_t k = 0; k < reps; ++k) {
+        const int r = (c->cur + k) % nrep;
+        const PodDev p = pod_dev(c, r);
         for (int32_t g0 = 0; g0 < S; g0 += POD_WINDOW_MAX) {
             const K1Diag diag{nullptr};
             HIP_TRY(launch_pod_reduce(p, g, g0, std::min(POD_WINDOW_MAX, S - g0), c->nblk, c->k1_variant, c->d_pod_part,
                                       c->d_wide_pod, c->d_k1_ticket, c->k1_cap, diag, st));
         }
-        HIP_TRY(launch_pod_bigtiles(p, g, c->pods[c->cur].big, c->n_big, c->d_wide_pod, st));
+        HIP_TRY(launch_pod_bigtiles(p, g, c->pods[r].big, c->n_big, c->d_wide_pod, st));
     }
     HIP_TRY(hipEventRecord(c->k1t_ev[1], st));
     // the exact-path accumulators K1 added to without a fold: back to zero for the next step

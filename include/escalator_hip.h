@@ -449,8 +449,10 @@ int32_t esc_stage_times(esc_ctx* ctx, double* ms_out, int32_t n);
  * this copies them out (after esc_sync).  *n_out = workgroups; ESC_E_STATE before a run. */
 int32_t esc_k1_trace(esc_ctx* ctx, uint64_t* out, int64_t cap_words, int64_t* n_out);
 /* K1's device time (measurement): `reps` back-to-back K1 launches over the
- * current snapshot between two HIP events on the context's stream; *ms_per_launch = elapsed
- * / reps.  Synchronous; leaves every decision result as it was. */
+ * current snapshot, rotating over its replicas as decisions do (esc_set_replicas: a replica
+ * small enough for the Infinity Cache is not re-read from it), between two HIP events on
+ * the context's stream; *ms_per_launch = elapsed / reps.  Synchronous; leaves every
+ * decision result as it was. */
 int32_t esc_k1_time(esc_ctx* ctx, int32_t reps, double* ms_per_launch);
 /* Calibrates K1's work split on this device: `rounds` decisions, each moving
  * every workgroup's share of the pod bytes toward its measured streaming rate.  Results are
