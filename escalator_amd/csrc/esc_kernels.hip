@@ -1463,7 +1463,10 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 // With a decision target (D.dec) the block then decides its groups (K4: at one rank on its
 // fold, at several after the exchange) and writes the compact records to the decision
 // buffer.
-constexpr int NG_WAVES = 4;
+#ifndef ESC_NG_WAVES
+#define ESC_NG_WAVES 4       // waves splitting a group's node pieces in k_node_groups (timing builds may override)
+#endif
+constexpr int NG_WAVES = ESC_NG_WAVES;
 
 namespace {
 // k_node_groups' work for up to 64 groups, group gid (NONE: no group) on lane l of every
