@@ -183,12 +183,83 @@ def stage_layout(world: int, shard_world: int, multi, backend: str) -> list[str]
     names = ["k_pod_reduce", "k_step_tail", "k_order_split", "k_node_groups"]
     if os.environ.get("ESC_NO_ZEROCOPY", "0") not in ("", "0"):
         names.append("d2h")
-    if multi or (world == 1 and shard_world == 1):
-        return names                              # K4 inside k_node_groups (device 0's events)
+    if world == 1 and shard_world == 1 and not multi:
+        return names                              # K4 inside k_node_groups
     names = names[:3] + names[4:]                 # node groups run with K4, after the exchange
-    if world > 1:
+    if multi:                                     # device 0's events; the exchange marks its end
+        names.append("exchange")
+    elif world > 1:
         names.append("exchange" if backend == "nccl" else "exchange_host_staged")
     return names + ["k_node_groups+decide"]
+
+
+def rccl_ranks_field(comm_size, multi, world: int, backend: str):
+    """The bench line's `rccl_ranks`: ncclCommCount of the live communicators (esc_comm_size),
+    None where no RCCL communicator exists — one rank, a gloo run, or a multi-device context on
+    its peer exchange (esc_comm_size reports 0 there)."""
+    if not (multi or (world > 1 and backend == "nccl")):
+        return None
+    return comm_size() or None
+
+
+SEL_SLACK, SEL_CAP = 4, 256     # selections delivered with each decision (esc_set_selections)
+
+
+def selections_ok(sel, dec, want, owned, slack=SEL_SLACK, cap=SEL_CAP):
+    """Every owned group's delivered selection (esc_selections) is the prefix of the oracle's
+    order its decision walks: delta < 0 (taint clamp passed) the untainted oldest first,
+    n_to_taint + slack of them; delta > 0 the tainted newest first, delta + slack; at most cap
+    (then flagged cut).  Returns (ok, groups with a list, nodes delivered)."""
+    import numpy as np
+    which, off, idx = sel
+    ok, n_lists = True, 0
+    for g in range(len(which)):
+        if not owned[g]:
+            continue
+        delta, ts = int(dec["delta"][g]), int(dec["taint_status"][g])
+        w, need = (1, delta) if delta > 0 else ((0, int(dec["n_to_taint"][g])) if delta < 0 and ts == 0 else (-1, 0))
+        got = idx[off[g]:off[g + 1]]
+        if w < 0:
+            ok &= bool(which[g] == -1 and len(got) == 0)
+            continue
+        order = want[(g, w)]
+        c = min(max(need, 0) + slack, len(order))
+        ok &= bool(which[g] & 3 == w and bool(which[g] & 4) == (c > cap) and np.array_equal(got, order[:min(c, cap)]))
+        n_lists += 1
+    return ok, n_lists, len(idx)
+
+
+def resident_run_once(ctx, select: bool, reps: int = 30) -> dict:
+    """The Go shim's RunOnce on the resident snapshot (go/escalatorhip: esc_set_state +
+    esc_step + esc_sync + esc_results of every group + esc_selections, sizes then nodes): the
+    wall time a controller scan waits for before it walks the selections, median of `reps`."""
+    import ctypes as C
+    import numpy as np
+    from escalator_amd import _lib as L
+    from escalator_amd.context import DECISION_DTYPE, TOTALS_DTYPE
+    lib, h, G = ctx.lib, ctx.handle, ctx.G
+    tot, dec = np.zeros(G, TOTALS_DTYPE), np.zeros(G, DECISION_DTYPE)
+    which, off = np.zeros(G, np.int32), np.zeros(G + 1, np.int64)
+    idx = np.zeros(G * (SEL_CAP + 1), np.int64)
+    tp, dp = tot.ctypes.data_as(C.POINTER(L.GroupTotals)), dec.ctypes.data_as(C.POINTER(L.GroupDecision))
+    wp, op, ip = (which.ctypes.data_as(C.POINTER(C.c_int32)), off.ctypes.data_as(C.POINTER(C.c_int64)),
+                  idx.ctypes.data_as(C.POINTER(C.c_int64)))
+    n = C.c_int64()
+    ms = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        L.check(lib.esc_set_state(h, ctx._state))
+        L.check(lib.esc_step(h))
+        L.check(lib.esc_sync(h))
+        L.check(lib.esc_results(h, tp, dp))
+        if select:
+            L.check(lib.esc_selections(h, wp, op, None, 0, C.byref(n)))
+            L.check(lib.esc_selections(h, wp, op, ip, len(idx), C.byref(n)))
+        ms.append((time.perf_counter() - t0) * 1e3)
+    return {"ms": float(np.median(ms)), "p90_ms": float(np.percentile(ms, 90)), "selections": select,
+            "groups_walking": int((which >= 0).sum()) if select else None, "nodes_delivered": int(n.value),
+            "how": "esc_set_state + esc_step + esc_sync + esc_results (every group) + esc_selections (sizes, "
+                   "then nodes) on the resident snapshot, the Go shim's RunOnce; median of %d" % reps}
 
 
 def check_parity(args, ctx, s, multi, rank, world, backend, dist, P, N, G, n_gpus):
@@ -204,14 +275,18 @@ def check_parity(args, ctx, s, multi, rank, world, backend, dist, P, N, G, n_gpu
     else:
         from escalator_amd.dist import gather_results
         tot, dec = gather_results(ctx)              # collective: every rank
-    ord_ok, n_ord = True, 0
+    ord_ok, n_ord, n_sel = True, 0, 0
     if not args.no_order:
         want = soa.order_all(s.nodes(), s.groups)
+        owned = [bool(multi or world == 1 or ctx.group_owner(g) == rank) for g in range(G)]
         for g in range(G):
-            if multi or world == 1 or ctx.group_owner(g) == rank:
+            if owned[g]:
                 n_ord += 1
                 for w in (0, 1):
                     ord_ok &= bool(np.array_equal(ctx.group_order(g, w), want[(g, w)]))
+        if not args.no_select:                      # the walks' prefixes delivered with the decision
+            sok, n_sel, _ = selections_ok(ctx.selections(), dec, want, owned)
+            ord_ok &= sok
     tot_ok = True
     if rank == 0:
         from escalator_amd import Synth
@@ -226,16 +301,18 @@ def check_parity(args, ctx, s, multi, rank, world, backend, dist, P, N, G, n_gpu
                                "taint_status"]):
             tot_ok &= np.array_equal(dec[n].astype(np.int64), odi[:, k])
     if dist is not None:                            # the verdict of every rank's checks
-        v = torch.tensor([int(ord_ok and tot_ok), n_ord], dtype=torch.int64,
+        v = torch.tensor([int(ord_ok and tot_ok), n_ord, n_sel], dtype=torch.int64,
                          device="cuda" if backend == "nccl" else "cpu")
         ok_t = v[:1].clone()
         dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
         dist.all_reduce(v[1:], op=dist.ReduceOp.SUM)
-        ok, n_ord = bool(ok_t.item()), int(v[1].item())
+        ok, n_ord, n_sel = bool(ok_t.item()), int(v[1].item()), int(v[2].item())
     else:
         ok = bool(ord_ok and tot_ok)
-    text = ("bit-exact vs C oracle: all %d groups' totals and decisions%s%s" % (
+    text = ("bit-exact vs C oracle: all %d groups' totals and decisions%s%s%s" % (
             G, "" if args.no_order else ", all %d groups' two orderings" % n_ord,
+            "" if args.no_order or args.no_select else ", the %d taint / untaint selections delivered with the "
+                                                       "decision" % n_sel,
             "" if n_gpus == 1 else " (the owners' records over %d ranks gathered; oracle over the unsharded "
                                    "snapshot)" % n_gpus)
             if ok else "MISMATCH vs C oracle")
@@ -617,6 +694,8 @@ def main():
                          "the Go host's drop-in shape; ESC_BENCH_DEVICES=0,0 rehearses it on one GPU)")
     ap.add_argument("--no-order", action="store_true",
                     help="leave the K5 ordering out of the decision (ablation; BASELINE.md §2 includes it)")
+    ap.add_argument("--no-select", action="store_true",
+                    help="do not deliver the taint / untaint selections with the decision (ablation)")
     ap.add_argument("--launch-check", action="store_true",
                     help="print this rank's RANK / WORLD_SIZE and exit before any GPU call (tests the launch)")
     args = ap.parse_args()
@@ -674,6 +753,9 @@ def main():
     load_ms = (time.perf_counter() - t_load) * 1e3
     ctx.set_state(s.states)
     ctx.set_order_in_step(not args.no_order)          # oldest-first ordering is part of a decision
+    args.no_select = args.no_select or args.no_order
+    if not args.no_select:                            # and the walks' first nodes go out with it
+        ctx.set_selections(SEL_SLACK, SEL_CAP)
     n_memb = ctx.order_info()[0]
     if multi:
         pod_b, node_b = ctx.stream_bytes()            # every device's shard
@@ -700,7 +782,7 @@ def main():
         exchange = ("rccl (esc_comm_init + esc_step: in-place ncclReduceScatter on the context's stream)" if backend == "nccl"
                     else "host-staged over torch.distributed %s" % backend)
     ctx.use_graph(args.graph)
-    rccl_ranks = ctx.comm_size() if (multi or (world > 1 and backend == "nccl")) else None
+    rccl_ranks = rccl_ranks_field(ctx.comm_size, multi, world, backend)
     ctx.k1_calibrate(16)                          # K1 shares to this device's rates (untimed, once per load)
     fe, ff = ctx.k1_flush_entries()
     k1_partials = {"entries": fe, "whole_row_entries": ff, "bytes": fe * 512,
@@ -772,6 +854,8 @@ def main():
     if not args.no_parity:
         parity, parity_ok = check_parity(args, ctx, s, multi, rank, world, backend, dist, P, N, G, n_gpus)
 
+    run_once = resident_run_once(ctx, not args.no_select) if world == 1 and shard_world == 1 and not multi else None
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -840,6 +924,11 @@ def main():
         "ordering": None if args.no_order else {
             "kernels": "groups of <= 1024 memberships packed as blocks of k_step_tail (one pass); mid-size groups by k_ord_packed, larger ones by k_ord_split (one pass, look-back over the group's chunks) after it; all on the context's one stream (esc_set_order_in_step)",
             "memberships": n_memb, "algorithmic_bytes": n_memb * 16},
+        "selections": None if args.no_select else {
+            "slack": SEL_SLACK, "group_cap": SEL_CAP,
+            "note": "every decided group's taint / untaint walk prefix (n_to_taint or delta + slack nodes of its "
+                    "order) written by K4 to pinned host memory inside the step (esc_set_selections)"},
+        "run_once": run_once,
         "parity": parity,
     }
     if not args.no_host and n_gpus == 1 and shard_world == 1:

@@ -17,7 +17,9 @@ HEADER = os.path.join(os.path.dirname(HERE), "include", "escalator_hip.h")
 
 ESC_OK = 0
 ESC_E_INVAL, ESC_E_HIP, ESC_E_NOMEM, ESC_E_LIMIT, ESC_E_STATE, ESC_E_NODEV, ESC_E_COMM = -1, -2, -3, -4, -5, -6, -7
+ESC_E_ORDER = -8                    # a K5 ordering's bounded look-back gave up (that ordering only)
 ESC_COMM_ID_BYTES = 128
+ESC_SEL_NONE, ESC_SEL_TAINT, ESC_SEL_UNTAINT, ESC_SEL_CUT = -1, 0, 1, 4
 ESC_NONE = 0xFFFFFFFF
 
 ESC_ST_OK, ESC_ST_ERR_MIN_NODES, ESC_ST_ERR_MAX_NODES, ESC_ST_ERR_DIV_ZERO = 0, 1, 2, 3
@@ -195,6 +197,8 @@ _SIGS = {
     "esc_build_age_index": (i32, [VP]),
     "esc_order_info": (i32, [VP, P(i64), P(i32)]),
     "esc_group_order": (i32, [VP, i32, i32, P(i64), i64, P(i64)]),
+    "esc_set_selections": (i32, [VP, i32, i32]),
+    "esc_selections": (i32, [VP, P(i32), P(i64), P(i64), i64, P(i64)]),
     "esc_pods_requests_total": (i32, [VP, P(PodObj), i64, P(i64), P(i64)]),
     "esc_nodes_capacity_total": (i32, [VP, P(NodeObj), i64, P(i64), P(i64)]),
     "esc_order_by_creation": (i32, [VP, P(i64), i64, i32, i64, P(i64)]),

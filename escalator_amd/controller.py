@@ -123,16 +123,23 @@ class Controller:
     MaxSize - TargetSize (calculateNodesToAdd, scale_up.go:48-56) in wet and dry mode, and a
     clamp <= 0 is scaleUpCloudProviderNodeGroup's error without a lock (scale_up.go:66-74);
     TryRemoveTaintedNodes (scale_down.go:51-136) runs before tainting and in the no-change
-    branch (controller.go:369-383) on the GPU's reaping pass.  The ``actuator`` provides
+    branch (controller.go:369-383) on the GPU's reaping pass.  The walks read the selections
+    the decision delivers (esc_selections: each group's first n + ``selection_slack`` nodes of
+    its order, written to pinned memory inside the step) and continue on esc_group_order only
+    when failed writes use up the slack (``walk_fallback`` in the group's result).  The ``actuator`` provides
     ``taint(g, node) -> bool``, ``untaint(g, node) -> bool``, ``target_size(g)``,
     ``max_size(g)``, ``increase_size(g, n)`` and ``delete_nodes(g, nodes)`` (raising on an
     API error); without one a ``SimulatedCloud`` stands in (every write succeeds)."""
 
-    def __init__(self, groups: list[dict], device: int = 0, dry_mode: bool = False, clock=None, actuator=None):
+    def __init__(self, groups: list[dict], device: int = 0, dry_mode: bool = False, clock=None, actuator=None,
+                 selection_slack: int = 4):
         import time
         from .context import Context
         self.groups = [dict(g, dry_mode=bool(g.get("dry_mode")) or dry_mode) for g in groups]
         self.ctx = Context(self.groups, device=device)
+        self.ctx.set_order_in_step(True)                   # the orderings and the walks' prefixes
+        self.ctx.set_selections(selection_slack)           # come with every decision
+        self._sel = None
         self.state = [{"locked": False, "requested_nodes": 0, "cached_cpu_m": 0, "cached_mem_b": 0}
                       for _ in groups]
         self.lock_time = [None] * len(groups)          # scaleLock.lockTime (None: never locked)
@@ -156,18 +163,31 @@ class Controller:
                 self.state[g]["locked"] = False
                 self.state[g]["requested_nodes"] = 0
 
-    def _scale_up(self, g: int, n: int, tainted: list[int], names: list[str], out: dict):
+    def _walk(self, g: int, which: int, n_avail: int, out: dict):
+        """The order a taint / untaint walk goes down (0: untainted oldest first, 1: tainted
+        newest first): the selection the decision delivered, then — only if the walk needs
+        more (failed writes used up the slack, or the list was cut) — esc_group_order beyond it."""
+        got = []
+        if self._sel is not None:
+            w, off, idx = self._sel
+            if int(w[g]) >= 0 and int(w[g]) & 3 == which:
+                got = [int(j) for j in idx[off[g]:off[g + 1]]]
+        yield from got
+        if len(got) >= n_avail:                             # the list is the whole order
+            return
+        out["walk_fallback"] = True
+        yield from (int(j) for j in self.ctx.group_order(g, which)[len(got):])
+
+    def _scale_up(self, g: int, n: int, n_tainted: int, names: list[str], out: dict):
         """ScaleUp (scale_up.go:14-46): untaintNewestN over the tainted nodes, the rest
         from the cloud node group (clamped to its MaxSize), then the lock.  Returns
         (nodes brought up, error-or-None)."""
         dry = self.groups[g]["dry_mode"]
         picked = []
-        if tainted:                                        # scaleUpUntaint :98-116
-            order = self.ctx.group_order(g, 1)            # newest first (sort.go:27-39)
-            for j in order:                                # untaintNewestN :127-160
+        if n_tainted:                                      # scaleUpUntaint :98-116
+            for j in self._walk(g, 1, n_tainted, out):     # newest first (sort.go:27-39), untaintNewestN :127-160
                 if len(picked) >= n:
                     break
-                j = int(j)
                 if dry:                                    # delete the tracked name, if any
                     trk = self.taint_tracker[g]
                     if names[j] in trk:
@@ -197,15 +217,14 @@ class Controller:
         out["added"] = add
         return len(picked) + add, None
 
-    def _scale_down_taint(self, g: int, n: int, names: list[str], out: dict):
+    def _scale_down_taint(self, g: int, n: int, n_untainted: int, names: list[str], out: dict):
         """scaleDownTaint -> taintOldestN (scale_down.go:138-205) with the clamped n: the
         untainted nodes oldest first until n taints succeeded."""
         dry = self.groups[g]["dry_mode"]
         picked = []
-        for j in self.ctx.group_order(g, 0):
+        for j in self._walk(g, 0, n_untainted, out):
             if len(picked) >= max(n, 0):
                 break
-            j = int(j)
             if dry:
                 self.taint_tracker[g].append(names[j])
                 picked.append(j)
@@ -241,8 +260,14 @@ class Controller:
         trackers = {g: list(t) for g, t in self.taint_tracker.items() if t}
         P, N = self.ctx.pack(pods, nodes, trackers)
         self.ctx.load(P, N)
-        tot, dec = self.ctx.decide_all(self.state)
-        self.ctx.sort_nodes()
+        tot, dec = self.ctx.decide_all(self.state)       # the ordering is in the step
+        try:
+            self._sel = self.ctx.selections()
+        except L.EscError as e:
+            if e.code != L.ESC_E_ORDER:
+                raise
+            self._sel = None                               # that ordering gave up: order afresh,
+            self.ctx.sort_nodes()                          # the walks read esc_group_order
         # CreateNodeNameToInfoMap (controller.go:259) + the reaping pass for every group
         self.ctx.load_placement(*placement(pods, nodes))
         soft = [int(grp.get("soft_delete_grace_ns", 0)) for grp in self.groups]
@@ -261,21 +286,22 @@ class Controller:
                  "branch": branch, "cpu_pct": float(d["cpu_pct"]),
                  "mem_pct": float(d["mem_pct"]), "n_to_taint": int(d["n_to_taint"]),
                  "totals": {k: int(tot[g][k]) for k in tot.dtype.names},
-                 "tainted_now": [], "untainted_now": [], "added": 0, "removed": [], "pods_evicted": 0}
-            tainted = self.ctx.group_order(g, 1) if int(tot["n_tainted"][g]) else []
+                 "tainted_now": [], "untainted_now": [], "added": 0, "removed": [], "pods_evicted": 0,
+                 "walk_fallback": False}
+            n_tainted, n_untainted = int(tot["n_tainted"][g]), int(tot["n_untainted"][g])
             if branch == "below_min":                                     # controller.go:281-295
-                r["delta"], r["err"] = self._scale_up(g, r["delta"], list(tainted), names, r)
+                r["delta"], r["err"] = self._scale_up(g, r["delta"], n_tainted, names, r)
             elif r["err"] is None and branch in ("fast_down", "slow_down", "scale_up", "none"):
                 # the action switch is on nodesDelta's sign, whichever branch computed it
                 # (controller.go:367-383; a scale-up from zero can compute 0)
                 if r["delta"] < 0:
                     self._reap(g, r)                                      # ScaleDown: reap first
                     if int(d["taint_status"]) == 0:
-                        self._scale_down_taint(g, r["n_to_taint"], names, r)   # controller.go:368-371
+                        self._scale_down_taint(g, r["n_to_taint"], n_untainted, names, r)   # controller.go:368-371
                     else:
                         r["action_err"] = "taint clamp"                   # scale_down.go:150-154
                 elif r["delta"] > 0:
-                    _, r["action_err"] = self._scale_up(g, r["delta"], list(tainted), names, r)   # :372-375
+                    _, r["action_err"] = self._scale_up(g, r["delta"], n_tainted, names, r)   # :372-375
                 else:
                     self._reap(g, r)                                      # default: controller.go:377-383
             out.append(r)

@@ -399,12 +399,36 @@ struct DecCompact;
 struct K1Diag {
     uint64_t* trace;
 };
+// Selections delivered with the decision (esc_set_selections; controller.go:367-383): K4
+// also writes, for every group it decides with delta < 0 (and the taint clamp passed) the
+// first min(n_to_taint + slack, group_cap) untainted nodes oldest first (taintOldestN's walk,
+// scale_down.go:171-205), with delta > 0 the first min(delta + slack, group_cap) tainted
+// nodes newest first (untaintNewestN, scale_up.go:118-163; equal creation times by ascending
+// index, the ordering's tie rule), copied from the ordering of the same decision into the
+// pinned buffer `out` — a block's groups as one contiguous run of [header, nodes...] words
+// (one device-scope add per block reserves it) — and the run's offset into the compact
+// record's `sel` field.  Header: count | which << 28 (1 taint, 2 untaint) | SEL_CUT (more
+// wanted than group_cap: the nodes are the walk's first ones) | SEL_TIE (a run of equal
+// creation times longer than SEL_TIE_MAX: the nodes are not used; in both cases the host
+// continues with esc_group_order).  `total` is zeroed by k_step_tail's first block every step.
+struct SelOut {
+    const uint32_t* ord;       // K5 output: every group's segments
+    const int64_t* seg;        // [4G] segment bounds (K5)
+    uint32_t* out;             // device view of the pinned selection buffer; null: no selections
+    uint32_t* total;           // words reserved this decision
+    int64_t cap_words;         // out's size (a block whose run does not fit gets SEL_OVERFLOW)
+    int32_t slack, group_cap;
+};
+constexpr uint32_t SEL_NONE = 0xFFFFFFFFu, SEL_OVERFLOW = 0xFFFFFFFEu;   // DecCompact::sel without a run
+constexpr uint32_t SEL_COUNT_MASK = (1u << 28) - 1, SEL_CUT = 1u << 30, SEL_TIE = 1u << 31;
+constexpr int SEL_TIE_MAX = 64;
 // k_node_groups' decision target: null dec = the node words only (a reduce that was never
 // decided, esc_reduce).
 struct NGDecide {
     const int64_t* pwords;
     esc_group_decision* dec;
     DecCompact* cdec;
+    SelOut sel;
 };
 // The groups a launch of k_node_groups covers: ids[i] for i < n, or, with null
 // ids, the contiguous run first + i (a rank's owned groups).
@@ -427,7 +451,7 @@ struct DecCompact {
     double cpu_pct, mem_pct;
     int32_t delta, n_to_taint;
     uint8_t status, branch, taint_status, wide;
-    uint32_t pad;
+    uint32_t sel;              // word offset of the group's selection run (SelOut), or SEL_NONE / SEL_OVERFLOW
 };
 static_assert(sizeof(DecCompact) == 32, "compact decision is 2 x 16 B");
 
@@ -466,7 +490,7 @@ int64_t tail_trk_blocks(const NodeDev& n);
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
                             const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
-                            uint32_t* vals, int64_t* seg, hipStream_t st);
+                            uint32_t* vals, int64_t* seg, uint32_t* sel_total, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
 // §8f rank 2: a loaded pod as seen by NodePodsRemaining, listed per node (runs in
 // node order).  p[0..2]: the pod's extra pairs (NONE-padded); a C pod with more than 3
@@ -570,6 +594,7 @@ struct RegionSink {
     int R;                     // the group's shift in the key (key = group << R | time bits)
     int fix;                   // coarse keys with dropped time bits: the final pass also writes
                                // the sorted keys and k_age_fix orders equal-key runs exactly
+    uint32_t spins;            // the listing's look-back bound (LOOKBACK_SPINS; err bit 0 on a give-up)
 };
 // coarse_shift < 0: exact 64-bit keys (group << R | offset); >= 0: 32-bit coarse keys
 // (group << (32 - gbits) | offset >> coarse_shift) + the run fix-up (S.R = 32 - gbits).
@@ -577,15 +602,25 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, uint64_t* statu
                            int64_t cap, int64_t ts_min, uint64_t div, int R, int gbits, int coarse_shift,
                            uint64_t* keys[2], uint32_t* vals[2], uint32_t* hist, uint32_t* tot, const RegionSink& S,
                            hipStream_t st);
+// The bounded waits of the decoupled look-backs (k_ord_split, k_memb_keys): HIP does not
+// promise dispatch order, so a chunk never waits unboundedly on one that was not dispatched.
+// A chunk that waited `spins` probes gives up: it publishes a FAILED status word (never an
+// inclusive prefix it could not compute; its successors fail in turn instead of waiting),
+// writes none of its output and sets *err (k_ord_split: a pinned host word the runtime reads
+// after its stream wait and reports as ESC_E_ORDER, then clears).
+constexpr uint32_t LOOKBACK_SPINS = 1u << 22;
+struct OrdFail {
+    uint32_t* err;             // device view of a pinned host word: set to 1 by a give-up
+    uint32_t spins;            // LOOKBACK_SPINS (smaller in measurement builds' tests)
+};
 // The split groups' ordering in one pass (k_ord_split): ostat = 2 * n_chunks + 1 u64 words,
 // zeroed when the chunk table is made: two arrays of status words used by alternate
-// decisions (par = 0, 1: a decision clears its chunks' words of the other), then a sticky
-// error word.
+// decisions (par = 0, 1: a decision clears its chunks' words of the other).
 // Output layout of every group (split and packed): untainted forward from the region start,
 // tainted newest first backward from the region end; seg[4g..4g+3] = start, start +
 // untainted, end - tainted, end.
 hipError_t launch_order(const NodeDev& n, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
                         const uint32_t* grp_off, const uint32_t* g_memb, uint64_t* ostat, int par, uint32_t* vals,
-                        int64_t* seg, hipStream_t st);
+                        int64_t* seg, const OrdFail& fail, hipStream_t st);
 
 }  // namespace esc

@@ -954,7 +954,7 @@ __device__ __forceinline__ DecCompact compact_of(const esc_group_decision& d) {
     c.branch = (uint8_t)d.branch;
     c.taint_status = (uint8_t)d.taint_status;
     c.wide = fits ? 0 : 1;
-    c.pad = 0;
+    c.sel = SEL_NONE;
     return c;
 }
 
@@ -1469,6 +1469,28 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 constexpr int NG_WAVES = ESC_NG_WAVES;
 
 namespace {
+// Entry q of a group's selection (SelOut): the untainted segment is stored oldest first
+// (ties by ascending index, the age index's order), the tainted one newest first with equal
+// creation times by DESCENDING index (it is written backward), so a tainted entry is taken
+// from the mirror position inside its run of equal creation times — the runs are found by
+// comparing neighbours (bounded by SEL_TIE_MAX each way; a longer run sets *cut and the host
+// falls back to esc_group_order, which reads until the run ends).
+__device__ __forceinline__ uint32_t sel_entry(const NodeDev& N, const uint32_t* __restrict__ sg, int64_t len,
+                                              uint32_t q, bool newest, bool& cut) {
+    if (!newest) return sg[q];
+    const int64_t t = N.created[sg[q]];
+    int64_t a = q, b = (int64_t)q + 1;
+    for (int k = 0; a > 0 && N.created[sg[a - 1]] == t; ++k) {
+        if (k == SEL_TIE_MAX) { cut = true; break; }
+        --a;
+    }
+    for (int k = 0; b < len && N.created[sg[b]] == t; ++k) {
+        if (k == SEL_TIE_MAX) { cut = true; break; }
+        ++b;
+    }
+    return sg[a + b - 1 - (int64_t)q];
+}
+
 // k_node_groups' work for up to 64 groups, group gid (NONE: no group) on lane l of every
 // wave: the node words from the group pair's piece rows (the waves split the pieces), then
 // the decision or the exchange words.  With `seq` the groups are g_first + l and their
@@ -1481,6 +1503,11 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
     __shared__ uint64_t red[NG_WAVES][6][64];
     __shared__ DecCompact sdec[64];
     __shared__ uint32_t sid[64];
+    // selections: per lane's group its run's first word in the block's run (exclusive scan,
+    // [64] = the block's words), which (0 none, 1 taint, 2 untaint), count, segment, cut
+    __shared__ uint32_t s_ex[65], s_w[64], s_c[64], s_cut[64];
+    __shared__ int64_t s_s[64], s_len[64];
+    __shared__ uint32_t s_base;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int32_t g = (int32_t)gid;
     const bool ok = gid != NONE && g < G.G;
@@ -1492,6 +1519,8 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
     GroupNode gn{};
     GroupParams prm{};
     int64_t pwv[PW_K] = {};
+    uint32_t sel_w = 0, sel_c = 0, sel_cut = 0;          // this lane's group's selection (wave 0)
+    int64_t sel_s = 0, sel_len = 0;
     if (ok) {
         gn = N.gnode[g];
         plo = gn.plo;
@@ -1576,7 +1605,59 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
         store_full(D.dec + g, d);
         sdec[lane] = compact_of(d);
         sid[lane] = (uint32_t)g;
+        if (D.sel.out) {                                 // which selection the decision asks for
+            int64_t need = 0;
+            if (d.delta > 0) { sel_w = 2; need = d.delta; }                       // ScaleUp: untaintNewestN
+            else if (d.delta < 0 && d.taint_status == ESC_ST_OK) { sel_w = 1; need = d.n_to_taint; }   // taintOldestN
+            if (sel_w) {
+                const int64_t* sg = D.sel.seg + 4 * (int64_t)g + (sel_w == 1 ? 0 : 2);
+                sel_s = sg[0];
+                sel_len = sg[1] - sg[0];
+                const int64_t want = (need > 0 ? need : 0) + D.sel.slack;
+                const int64_t c = want < sel_len ? want : sel_len;
+                sel_c = (uint32_t)(c < D.sel.group_cap ? c : D.sel.group_cap);
+                sel_cut = c > D.sel.group_cap ? SEL_CUT : 0u;
+            }
+        }
     }
+    }
+    if (D.dec && D.sel.out) {
+        // one device-scope add per block reserves the block's run; lane l's group takes
+        // [base + ex, base + ex + 1 + count): its header, then its nodes
+        if (wid == 0) {
+            const uint32_t words = sel_w ? sel_c + 1 : 0u;
+            const uint32_t inc = wave_incl_scan32(words);
+            const uint32_t tot = __builtin_amdgcn_readlane(inc, 63);
+            uint32_t base = 0;
+            if (lane == 63 && tot) base = atomicAdd(D.sel.total, tot);
+            base = __builtin_amdgcn_readlane(base, 63);
+            const bool fits = (int64_t)base + tot <= D.sel.cap_words;
+            s_ex[lane] = inc - words;
+            if (lane == 63) { s_ex[64] = fits ? tot : 0u; s_base = base; }
+            s_w[lane] = fits ? sel_w : 0u;
+            s_c[lane] = sel_c;
+            s_s[lane] = sel_s;
+            s_len[lane] = sel_len;
+            s_cut[lane] = sel_cut;
+            if (ok) sdec[lane].sel = !sel_w ? SEL_NONE : (fits ? base + inc - words : SEL_OVERFLOW);
+        }
+        __syncthreads();
+        const uint32_t total = s_ex[64], base = s_base;
+        for (uint32_t f = threadIdx.x; f < total; f += NG_WAVES * 64) {
+            uint32_t l = 0;                              // the run holding word f: last l with s_ex[l] <= f
+#pragma unroll
+            for (uint32_t st = 32; st; st >>= 1)
+                if (s_ex[l + st] <= f) l += st;
+            const uint32_t q = f - s_ex[l];
+            if (q == 0) continue;                        // the header, once the cuts are known
+            bool cut = false;
+            const uint32_t v = sel_entry(N, D.sel.ord + s_s[l], s_len[l], q - 1, s_w[l] == 2, cut);
+            if (cut) s_cut[l] |= SEL_TIE;
+            D.sel.out[base + f] = v;
+        }
+        __syncthreads();
+        if (wid == 0 && s_w[lane])
+            D.sel.out[base + s_ex[lane]] = s_c[lane] | s_w[lane] << 28 | s_cut[lane];
     }
     if (D.dec) {                                         // 16-B pieces to pinned host memory (PCIe writes)
         __syncthreads();
@@ -2212,13 +2293,15 @@ __device__ __forceinline__ void memb_codes(const NodeDev& N, const GroupDev& G, 
 // one wave has summed its predecessors' words back to the nearest inclusive one.  No
 // ticket: one shared ticket word serialises its grabs (≈ 88 per µs, the guide's dequeue
 // price: 56 µs for config 5's 4 900 tiles).  HIP does not promise dispatch order, so the
-// wait is bounded: a tile that waited ~4 M probes gives up and sets error bit 0 (the build
-// then fails loudly) instead of hanging on a predecessor that was never dispatched.
-constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62;
+// wait is bounded: a tile that waited `spins` probes gives up, publishes LB_ERR (its
+// successors give up at once instead of waiting, and none publishes an inclusive prefix it
+// could not compute), writes nothing and sets error bit 0 (the build then fails loudly)
+// instead of hanging on a predecessor that was never dispatched.
+constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_ERR = 3ull << 62;
 template <class KT, bool PACK = false>
 __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G, int64_t n, uint64_t* __restrict__ status,
                                                           uint32_t* __restrict__ total_out, uint32_t* __restrict__ err,
-                                                          int64_t cap, int64_t ts_min,
+                                                          uint32_t spin_limit, int64_t cap, int64_t ts_min,
                                                           uint64_t div, int R, int KS, KT* __restrict__ keys,
                                                           uint32_t* __restrict__ vals) {
     // A tile's memberships are staged in LDS and written out as two contiguous streams:
@@ -2227,7 +2310,7 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
     __shared__ uint32_t wsum[MEMB_WAVES];
     __shared__ KT sk[MEMB_CAP];
     __shared__ uint32_t sv[PACK ? 1 : MEMB_CAP];
-    __shared__ uint32_t s_base;
+    __shared__ uint32_t s_base, s_fail;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int64_t n_tiles = (n + MEMB_BLOCK * MEMB_U - 1) / (MEMB_BLOCK * MEMB_U);
     const int64_t tile = blockIdx.x;
@@ -2274,9 +2357,10 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
         auto look_back = [&]() {
             uint32_t excl = 0;
             uint32_t spins = 0;                          // a bound on waiting (never reached when the
-            for (int64_t look = tile - 1; look >= 0;) {  // status words were zeroed): err bit 0
-                if (++spins > (1u << 22)) {
-                    if (lane == 0) atomicOr(err, 1u);
+            bool failed = false;                         // status words were zeroed): err bit 0
+            for (int64_t look = tile - 1; look >= 0;) {
+                if (++spins > spin_limit) {
+                    failed = true;
                     break;
                 }
                 const int64_t j = look - lane;
@@ -2284,22 +2368,29 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
                 // acquire invalidates the CU's vector L1 under the other workgroups' loads)
                 const uint64_t w = j >= 0 ? __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                           : LB_INC;      // before tile 0: an inclusive 0
-                const unsigned long long inc = __ballot((w >> 62) == 2), wait = __ballot((w >> 62) == 0);
-                const int fi = inc ? __builtin_ctzll(inc) : 63;   // nearest inclusive word
+                // the nearest inclusive or failed word ends the look-back
+                const unsigned long long inc = __ballot((w >> 62) >= 2), wait = __ballot((w >> 62) == 0);
+                const int fi = inc ? __builtin_ctzll(inc) : 63;
                 const unsigned long long need = ~0ull >> (63 - fi);      // lanes 0..fi
                 if (wait & need) {                       // a predecessor has not counted yet
                     __builtin_amdgcn_s_sleep(1);
                     continue;
+                }
+                if (inc && (__builtin_amdgcn_readlane((uint32_t)(w >> 32), fi) >> 30) == 3) {   // it gave up
+                    failed = true;
+                    break;
                 }
                 excl += wave_total32(lane <= fi ? (uint32_t)w : 0u);
                 if (inc) break;
                 look -= 64;
             }
             if (lane == 0) {
-                if (tile) __hip_atomic_store(status + tile, LB_INC | (uint64_t)(uint32_t)(excl + total), __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT);
+                if (failed) atomicOr(err, 1u);
+                if (tile) __hip_atomic_store(status + tile, failed ? LB_ERR : (LB_INC | (uint64_t)(uint32_t)(excl + total)),
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 s_base = excl;
-                if (tile == n_tiles - 1) total_out[0] = excl + total;
+                s_fail = failed ? 1u : 0u;
+                if (tile == n_tiles - 1 && !failed) total_out[0] = excl + total;
             }
         };
         // staged tiles look back after their walk (the predecessors' counts are published by
@@ -2307,6 +2398,7 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
         if (!stage) {
             if (wid == 0) look_back();
             __syncthreads();
+            if (s_fail) return;                          // no base: write nothing (err is set)
         }
         const uint32_t carry = stage ? 0u : s_base;
 #pragma unroll
@@ -2331,6 +2423,7 @@ __global__ __launch_bounds__(MEMB_BLOCK) void k_memb_keys(NodeDev N, GroupDev G,
         if (stage) {
             if (wid == 0) look_back();
             __syncthreads();
+            if (s_fail) return;
             const uint32_t base = s_base;
             for (uint32_t e = threadIdx.x; e < total && base + e < cap; e += MEMB_BLOCK) {
                 keys[base + e] = sk[e];
@@ -2376,25 +2469,27 @@ __device__ __forceinline__ uint32_t ord_class(const NodeDev&, uint32_t, uint32_t
 // v = blockIdx.x in one of two arrays, ostat[par * n + v]; a decision uses array `par` and
 // zeroes its chunk's word of the other, which the next decision (parity flipped by the
 // host, a graph captured per parity) finds clear — no clearing launch (a memset before
-// every decision cost ~6 µs of the 30).  ostat[2n]: error word (a bounded look-back that
-// gave up: HIP does not promise dispatch order, so a chunk never waits unboundedly on one
-// that was not dispatched).  A ticket for in-order chunk ids would serialise ~2 800 grabs
-// on one word (≈ 32 µs: measured 49 µs per decision against 30 µs for the two-pass form).
-constexpr uint64_t OS_AGG = 1ull << 62, OS_INC = 2ull << 62;
+// every decision cost ~6 µs of the 30).  The wait is bounded (OrdFail, esc_kernels.h): a
+// chunk that gives up publishes OS_ERR — never an inclusive prefix it could not compute —
+// so its group's later chunks give up at once, writes no output and sets the host-visible
+// error word the runtime reports (ESC_E_ORDER) and clears.  A ticket for in-order chunk ids
+// would serialise ~2 800 grabs on one word (≈ 32 µs: measured 49 µs per decision against
+// 30 µs for the two-pass form).
+constexpr uint64_t OS_AGG = 1ull << 62, OS_INC = 2ull << 62, OS_ERR = 3ull << 62;
 constexpr uint32_t OS_M = (1u << 28) - 1;
 __global__ __launch_bounds__(ORD_BLOCK) void k_ord_split(NodeDev N, const OrdChunk* __restrict__ chunks, int64_t n_chunks,
                                                          const uint32_t* __restrict__ g_memb,
                                                          const uint32_t* __restrict__ gch_off,
                                                          const uint32_t* __restrict__ grp_off,
                                                          uint64_t* __restrict__ ostat_all, int par,
-                                                         uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
+                                                         uint32_t* __restrict__ vals, int64_t* __restrict__ seg,
+                                                         OrdFail fail) {
     uint64_t* __restrict__ ostat = ostat_all + (par ? n_chunks : 0);
     uint64_t* __restrict__ onext = ostat_all + (par ? 0 : n_chunks);
-    uint64_t* __restrict__ oerr = ostat_all + 2 * n_chunks;
     constexpr int STEPS = ORD_CHUNK / (4 * ORD_BLOCK);
     __shared__ uint32_t wt[STEPS][ORD_WAVES];
     __shared__ uint32_t stage[ORD_CHUNK];
-    __shared__ uint32_t s_base[2];
+    __shared__ uint32_t s_base[2], s_fail;
     const uint32_t v = blockIdx.x;
     const OrdChunk ch = chunks[v];
     if (threadIdx.x == 0) onext[v] = 0;                  // the next decision's word (last used two ago)
@@ -2457,21 +2552,27 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_split(NodeDev N, const OrdChu
     }
     if (wid == 0) {                                      // look back over the group's earlier chunks
         uint32_t e0 = 0, e1 = 0, spins = 0;
+        bool failed = false;
         for (int64_t look = (int64_t)v - 1; look >= (int64_t)q0;) {
-            if (++spins > (1u << 22)) {                  // never reached: every earlier chunk runs
-                if (lane == 0) __hip_atomic_fetch_or(oerr, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (++spins > fail.spins) {                  // never reached: every earlier chunk runs
+                failed = true;
                 break;
             }
             const int64_t jj = look - lane;
             const uint64_t w = jj >= (int64_t)q0 ? __hip_atomic_load(ostat + jj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
                                                  : OS_INC;   // before the group: an inclusive 0
             const bool ready = (w >> 62) != 0;
-            const unsigned long long inc = __ballot(ready && (w >> 62) == 2), wait = __ballot(!ready);
+            // the nearest inclusive (or failed) word ends the look-back
+            const unsigned long long inc = __ballot((w >> 62) >= 2), wait = __ballot(!ready);
             const int fi = inc ? __builtin_ctzll(inc) : 63;
             const unsigned long long need = ~0ull >> (63 - fi);
             if (wait & need) {
                 __builtin_amdgcn_s_sleep(1);
                 continue;
+            }
+            if (inc && (__builtin_amdgcn_readlane((uint32_t)(w >> 32), fi) >> 30) == 3) {   // it gave up
+                failed = true;
+                break;
             }
             const bool mine = lane <= fi;
             e0 += wave_total32(mine ? (uint32_t)(w & OS_M) : 0u);
@@ -2481,21 +2582,28 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_split(NodeDev N, const OrdChu
         }
         if (lane == 0) {
             const uint32_t t0 = e0 + n0, t1 = e1 + n1;
-            if (v != q0)
-                __hip_atomic_store(ostat + v, OS_INC | ((uint64_t)t1 << 28) | t0, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t s0 = grp_off[g], e = grp_off[g + 1];
-            s_base[0] = s0 + e0;                         // class 0 output start
-            s_base[1] = e - e1 - n1;                     // class 1 output start (stored descending)
-            if (v + 1 == gch_off[g + 1]) {               // the group's last chunk: its bounds
-                seg[4 * (int64_t)g + 0] = s0;
-                seg[4 * (int64_t)g + 1] = (int64_t)s0 + t0;
-                seg[4 * (int64_t)g + 2] = (int64_t)e - t1;
-                seg[4 * (int64_t)g + 3] = e;
+            s_fail = failed ? 1u : 0u;
+            if (failed) {
+                __hip_atomic_store(ostat + v, OS_ERR, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(fail.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            } else {
+                if (v != q0)
+                    __hip_atomic_store(ostat + v, OS_INC | ((uint64_t)t1 << 28) | t0, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t s0 = grp_off[g], e = grp_off[g + 1];
+                s_base[0] = s0 + e0;                     // class 0 output start
+                s_base[1] = e - e1 - n1;                 // class 1 output start (stored descending)
+                if (v + 1 == gch_off[g + 1]) {           // the group's last chunk: its bounds
+                    seg[4 * (int64_t)g + 0] = s0;
+                    seg[4 * (int64_t)g + 1] = (int64_t)s0 + t0;
+                    seg[4 * (int64_t)g + 2] = (int64_t)e - t1;
+                    seg[4 * (int64_t)g + 3] = e;
+                }
             }
         }
     }
     __syncthreads();
+    if (s_fail) return;                                  // no bases: nothing written
     const uint32_t b0 = s_base[0], b1 = s_base[1];
     for (uint32_t i = threadIdx.x; i < n0 + n1; i += ORD_BLOCK)
         __builtin_nontemporal_store(stage[i], vals + (i < n0 ? b0 + i : b1 + (i - n0)));   // read by the host only
@@ -2656,9 +2764,11 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
                                                    const OrdChunk* __restrict__ chunks, int64_t n_small,
                                                    const uint32_t* __restrict__ grp_off,
                                                    const uint32_t* __restrict__ g_memb, const uint32_t* __restrict__ g_grp,
-                                                   uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
+                                                   uint32_t* __restrict__ vals, int64_t* __restrict__ seg,
+                                                   uint32_t* __restrict__ sel_total) {
     static_assert(FD_WAVES * 64 == 256 && K2_WAVES * 64 == 256 && ORD_BLOCK == 256, "one block size for every role");
     const int64_t b = blockIdx.x;
+    if (b == 0 && threadIdx.x == 0 && sel_total) *sel_total = 0;   // this step's selection runs (k_node_groups)
     // F.ablate (ESC_K3_ABLATE, timing-only, wrong results): 8 / 16 / 32 skip the fold /
     // node-piece / ordering role, 64 the dry-mode tracker blocks, 128 K2's row stores
     if (b < n_piece_blk) {
@@ -2946,13 +3056,13 @@ int64_t tail_trk_blocks(const NodeDev& n) { return (n.n_trk + K2_WAVES * 64 - 1)
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
                             const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
-                            uint32_t* vals, int64_t* seg, hipStream_t st) {
+                            uint32_t* vals, int64_t* seg, uint32_t* sel_total, hipStream_t st) {
     const int64_t nb = spans ? tail_span_blocks(n) : 0;      // else K1 made the rows
     const int64_t nt = tail_trk_blocks(n);
     const int64_t grid = f.n_col + nb + nt + std::max<int64_t>(n_small, 0);
     if (grid <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_step_tail, dim3((unsigned)grid), dim3(256), 0, st, g, n, f, wide_pod, pwords, nb, nb + nt, rows,
-                       trk_acc, chunks, std::max<int64_t>(n_small, 0), grp_off, g_memb, g_grp, vals, seg);
+                       trk_acc, chunks, std::max<int64_t>(n_small, 0), grp_off, g_memb, g_grp, vals, seg, sel_total);
     return hipGetLastError();
 }
 
@@ -3066,7 +3176,7 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, uint64_t* statu
     if (n > 0 && hipMemsetAsync(status, 0, nst * 8, st) != hipSuccess) return hipGetLastError();
     if (coarse_shift < 0) {                          // exact 64-bit keys: group << R | offset
         if (n > 0)
-            hipLaunchKernelGGL(k_memb_keys<uint64_t>, tiles, dim3(MEMB_BLOCK), 0, st, nd, g, n, status, total, S.err, cap, ts_min,
+            hipLaunchKernelGGL(k_memb_keys<uint64_t>, tiles, dim3(MEMB_BLOCK), 0, st, nd, g, n, status, total, S.err, S.spins, cap, ts_min,
                                div, R, 0, keys[0], vals[0]);
         if (n_memb > 0) {
             int src = 0;
@@ -3080,7 +3190,7 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, uint64_t* statu
     // digit run), sorted on the element's top 32 bits; then k_age_fix orders each run of
     // equal coarse keys by the exact creation time
     if (n > 0)
-        hipLaunchKernelGGL((k_memb_keys<uint64_t, true>), tiles, dim3(MEMB_BLOCK), 0, st, nd, g, n, status, total, S.err, cap,
+        hipLaunchKernelGGL((k_memb_keys<uint64_t, true>), tiles, dim3(MEMB_BLOCK), 0, st, nd, g, n, status, total, S.err, S.spins, cap,
                            ts_min, div, 32 - gbits, coarse_shift, keys[0], nullptr);
     if (n_memb > 0) {
         int src = 0;
@@ -3117,10 +3227,10 @@ hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32
 
 hipError_t launch_order(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, const uint32_t* gch_off,
                         const uint32_t* grp_off, const uint32_t* g_memb, uint64_t* ostat, int par, uint32_t* vals,
-                        int64_t* seg, hipStream_t st) {
+                        int64_t* seg, const OrdFail& fail, hipStream_t st) {
     if (n_chunks <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_ord_split, dim3((unsigned)n_chunks), dim3(ORD_BLOCK), 0, st, nd, chunks, n_chunks, g_memb,
-                       gch_off, grp_off, ostat, par, vals, seg);
+                       gch_off, grp_off, ostat, par, vals, seg, fail);
     return hipGetLastError();
 }
 

@@ -35,6 +35,8 @@ esc_multi_state* ctx_multi(const esc_ctx* c);
 void ctx_set_multi(esc_ctx* c, esc_multi_state* m);
 hipStream_t ctx_stream(const esc_ctx* c);
 int ctx_device(const esc_ctx* c);
+// timing mode: one more stage boundary on the context's stream (the exchange's end)
+int32_t ctx_stage_mark(esc_ctx* c);
 int32_t fail_comm(const char* what, const char* why);
 int32_t fail_hip(hipError_t e, const char* what);
 // check phases of esc_pods_upsert / esc_pods_bind (nothing applied)

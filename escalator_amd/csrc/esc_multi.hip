@@ -152,7 +152,16 @@ int32_t exchange_words(esc_ctx* c) {
         if (int32_t rc = esc_exchange_slice(m.subs[i], &off[i], &n)) return rc;
         buf[i] = reinterpret_cast<int64_t*>(b);
     }
-    if (m.comms.empty()) return peer_exchange<int64_t>(c, buf, off, n, m.psum, m.psum_n, true);
+    // timing mode: every device's exchange ends a stage of its own (bench.py exchange_ms)
+    auto marks = [&]() -> int32_t {
+        for (int i = 0; i < k; ++i)
+            if (int32_t rc = ctx_stage_mark(m.subs[i])) return rc;
+        return ESC_OK;
+    };
+    if (m.comms.empty()) {
+        if (int32_t rc = peer_exchange<int64_t>(c, buf, off, n, m.psum, m.psum_n, true)) return rc;
+        return marks();
+    }
     const RcclApi& r = rccl();
     ncclResult_t e = r.group_start();
     for (int i = 0; i < k && e == ncclSuccess; ++i) {
@@ -162,7 +171,7 @@ int32_t exchange_words(esc_ctx* c) {
     const ncclResult_t e2 = r.group_end();
     if (e != ncclSuccess) return fail_comm("ncclReduceScatter", r.error_string(e));
     if (e2 != ncclSuccess) return fail_comm("ncclGroupEnd", r.error_string(e2));
-    return ESC_OK;
+    return marks();
 }
 
 // Pods of the batch that go to device i, as a packed SoA of their own.
@@ -210,7 +219,7 @@ esc_ctx* multi_sub(const esc_ctx* c, int i) {
 
 int32_t multi_size(const esc_ctx* c) {
     const esc_multi_state& m = M(c);
-    if (m.comms.empty()) return (int32_t)m.subs.size();
+    if (m.comms.empty()) return 0;                      // the peer exchange: no communicator
     int n = 0;
     return rccl().count(m.comms[0], &n) == ncclSuccess ? n : -1;
 }
@@ -289,13 +298,18 @@ int32_t multi_step(esc_ctx* c) {
     return seq(c, [&](int i) { return esc_decide(M(c).subs[i]); });
 }
 
+// Every device is waited for even when one reports (ESC_E_ORDER leaves the others' work
+// queued otherwise); the first error is returned.
 int32_t multi_sync(esc_ctx* c) {
-    return seq(c, [&](int i) { return esc_sync(M(c).subs[i]); });
+    int32_t first = ESC_OK;
+    for (int i = 0; i < nsub(c); ++i)
+        if (int32_t rc = esc_sync(M(c).subs[i]); rc && !first) first = rc;
+    return first;
 }
 
 // Every group's records from the device that owns it (each device decided its own groups).
 int32_t multi_results(esc_ctx* c, esc_group_totals* t, esc_group_decision* d) {
-    if (int32_t rc = multi_sync(c)) return rc;
+    if (int32_t rc = multi_sync(c); rc && rc != ESC_E_ORDER) return rc;   // orderings apart, the records are valid
     const int k = nsub(c);
     if (k == 1) return esc_results(M(c).subs[0], t, d);
     const int32_t G = esc_ctx_num_groups(M(c).subs[0]);

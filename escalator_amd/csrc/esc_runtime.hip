@@ -212,9 +212,16 @@ struct esc_ctx {
     DecCompact* h_cdec_dev = nullptr;                         // device view of h_cdec (zero-copy)
     bool zero_copy = true;                                    // K3/K4 write compact decisions to h_cdec
     bool order_in_step = false;                               // K5 ordering inside every decision
+    // selections delivered with the decision (esc_set_selections, SelOut): K4 writes every
+    // decided group's taint / untaint nodes into h_sel (pinned, zero-copy) as [header, nodes]
+    // runs, their offsets into the compact records
+    int32_t sel_slack = -1, sel_group_cap = 0;
+    uint32_t *h_sel = nullptr, *h_sel_dev = nullptr, *d_sel_total = nullptr;
+    int64_t sel_words = 0;
     bool want_metrics = false;                                // K4 also writes the gauges
     esc_group_metrics* d_metrics = nullptr;
     int64_t* bound_pwords = nullptr;                          // caller-bound exchange buffer
+    int64_t bound_words = 0;                                  // its size: xw_count when bound
     void* comm = nullptr;                                     // RCCL communicator (esc_comm_init)
     bool work_ready = false;
     // An informer-event batch that failed after its first write (a HIP error mid-apply)
@@ -254,9 +261,17 @@ struct esc_ctx {
     // group order of the memberships (per-decision 3-way split by class inside each group)
     uint32_t *d_g_memb = nullptr, *d_g_grp = nullptr;   // K5 regions: membership words, group words
     uint32_t *d_grp_off = nullptr, *d_gch_off = nullptr;
-    uint64_t* d_ostat = nullptr;                              // k_ord_split status words (x2), error word
+    uint64_t* d_ostat = nullptr;                              // k_ord_split status words (x2)
     int ord_parity = 0;                                       // which status array the next ordering uses
-    bool ord_err_read = false;                                // the error word was read since the last ordering
+    // A look-back that gave up (k_ord_split, OrdFail) sets the pinned word h_oerr; the host
+    // reads it after its stream waits: esc_sync reports it once as ESC_E_ORDER and clears it,
+    // and esc_group_order refuses (ESC_E_ORDER) until the next ordering is enqueued.
+    uint32_t *h_oerr = nullptr, *h_oerr_dev = nullptr;
+    bool ord_failed = false;
+    // fault injection, measurement library only (esc_debug_*: tests/test_gpu_faults.py): the
+    // next n ordering / listing launches give up their look-back at once, the next n event
+    // patch applications fail after their host-side writes
+    int lb_fail_order = 0, lb_fail_list = 0, fail_patches = 0;
     uint32_t *d_pstart = nullptr, *d_plen = nullptr;
     uint32_t* d_ord = nullptr;                                // K5 output, in the group regions
     OrdChunk* d_pchunks = nullptr;                            // packed chunks of small groups
@@ -496,13 +511,56 @@ void drop_graphs(esc_ctx* c) {
 
 int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out);
 
+// The look-back bound of the next K5 launch (ordering or listing): LOOKBACK_SPINS, except
+// for launches a measurement-library test set to give up at once (esc_debug_lookback_fail,
+// tests/test_gpu_faults.py).
+uint32_t lb_spins(int& fail_next) {
+    if (fail_next > 0) {
+        --fail_next;
+        return 0;
+    }
+    return LOOKBACK_SPINS;
+}
+OrdFail ord_fail(esc_ctx* c) { return OrdFail{c->h_oerr_dev, lb_spins(c->lb_fail_order)}; }
+
+// K4's selection target for a deciding launch (null out: off, or no ordering in the step to
+// select from)
+SelOut sel_out(const esc_ctx* c) {
+    SelOut s{};
+    if (c->sel_slack < 0 || !c->h_sel || !c->order_in_step || !c->d_ord || !c->d_seg) return s;
+    s.ord = c->d_ord;
+    s.seg = c->d_seg;
+    s.out = c->h_sel_dev;
+    s.total = c->d_sel_total;
+    s.cap_words = c->sel_words;
+    s.slack = c->sel_slack;
+    s.group_cap = c->sel_group_cap;
+    return s;
+}
+
+void release_selections(esc_ctx* c) {
+    if (c->h_sel) hipHostFree(c->h_sel);
+    c->h_sel = c->h_sel_dev = nullptr;
+    dfree(c->d_sel_total);
+    c->sel_words = 0;
+}
+
+// After a wait on the context's stream: a split ordering that gave up since the last check
+// latches ord_failed (clearing the host word for the next one); true when it was new.
+bool order_gave_up(esc_ctx* c) {
+    if (!c->h_oerr || !*reinterpret_cast<volatile uint32_t*>(c->h_oerr)) return false;
+    *reinterpret_cast<volatile uint32_t*>(c->h_oerr) = 0;
+    c->ord_failed = true;
+    return true;
+}
+
 // K5 per-decision ordering (classify + stable split of every group's age-ordered
 // memberships) on stream st: the two-pass kernels and the packed small / mid-size groups.
 hipError_t enqueue_order(esc_ctx* c, hipStream_t st) {
     const hipError_t e = launch_order(node_dev(c), c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb,
-                                      c->d_ostat, c->ord_parity, c->d_ord, c->d_seg, st);
+                                      c->d_ostat, c->ord_parity, c->d_ord, c->d_seg, ord_fail(c), st);
     c->ord_parity ^= 1;
-    c->ord_err_read = false;
+    c->ord_failed = false;
     if (e != hipSuccess) return e;
     return launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_memb, c->d_g_grp,
                                c->d_ord, c->d_seg, st);
@@ -533,7 +591,7 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
         if (e != hipSuccess) return fail_hip(e, "hipGraphInstantiate");
     } else if (ord) {
         c->ord_parity ^= 1;
-        c->ord_err_read = false;
+        c->ord_failed = false;
     }
     HIP_TRY(hipGraphLaunch(gs[k], c->stream));
     return ESC_OK;
@@ -727,6 +785,7 @@ int32_t build_age_index(esc_ctx* c) {
         HIP_TRY(dalloc(&c->d_grp_off, pstart.size())); HIP_TRY(dalloc(&c->d_gch_off, gch_off.size()));
         HIP_TRY(dalloc(&c->d_ostat, 2 * chunks.size() + 1));
         HIP_TRY(hipMemsetAsync(c->d_ostat, 0, (2 * chunks.size() + 1) * 8, st));
+        c->ord_failed = false;
         c->ord_parity = 0;
         drop_graphs(c);                                 // captured steps hold the old tables
         HIP_TRY(dalloc(&c->d_chunks, std::max<size_t>(chunks.size(), 1)));
@@ -776,7 +835,7 @@ int32_t build_age_index(esc_ctx* c) {
         HIP_TRY(hipMemcpyAsync(c->d_seg, c->h_istage + ups[0].at, ups[0].bytes, hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemsetAsync(c->d_ierr, 0, 4, st));
         RegionSink sink{c->d_seg, c->d_pstart, c->d_plen, c->d_dry, c->d_g_memb, c->d_g_grp, c->d_ierr,
-                        g.G, coarse ? 32 - gbits : c->sort_R, cshift > 0 ? 1 : 0};
+                        g.G, coarse ? 32 - gbits : c->sort_R, cshift > 0 ? 1 : 0, lb_spins(c->lb_fail_list)};
         HIP_TRY(launch_age_sort(n, g, c->d_lstat, c->d_total, c->n_memb, c->mcap, c->ts_min, c->sort_div, c->sort_R,
                                 gbits, cshift, c->d_mkeys, c->d_mvals, c->d_hist, c->d_tot, sink, st));
         HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_grp, c->d_g_memb, c->d_seg, st));
@@ -1209,13 +1268,14 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     f.ablate = c->k3_ablate;
     const bool ord = c->order_in_step;
     HIP_TRY(launch_step_tail(g, n, f, true, c->d_wide_pod, c->d_pwords, c->nodes.rows, c->d_trk_acc, c->d_pchunks,
-                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, st));
+                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg,
+                             c->d_sel_total, st));
     if (int32_t rc = mark()) return rc;
     if (ord) {                                       // split groups, mid-size packed chunks
         HIP_TRY(launch_order(n, c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb, c->d_ostat,
-                             c->ord_parity, c->d_ord, c->d_seg, st));
+                             c->ord_parity, c->d_ord, c->d_seg, ord_fail(c), st));
         c->ord_parity ^= 1;
-        c->ord_err_read = false;
+        c->ord_failed = false;
         HIP_TRY(launch_order_packed(n, c->d_pchunks + c->n_psmall, c->n_pchunks - c->n_psmall, 0, c->d_grp_off,
                                     c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, st));
     }
@@ -1226,7 +1286,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     // launch (esc_decide) — one kernel boundary less on the rank's critical path.
     if (decide) {
         HIP_TRY(launch_node_groups(g, n, own_list(c), c->nodes.rows, c->d_trk_acc, c->d_nwords,
-                                   NGDecide{c->d_pwords, c->d_dec, cdec}, st));
+                                   NGDecide{c->d_pwords, c->d_dec, cdec, sel_out(c)}, st));
         if (int32_t rc = mark()) return rc;
     }
     if (copy_out && !c->zero_copy) {
@@ -1237,15 +1297,26 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     return ESC_OK;
 }
 
-int32_t check_ready(esc_ctx* c) {
+// fit = false: the exchange-buffer queries, which must still report the new size when a
+// bound buffer no longer fits.
+int32_t check_ready(esc_ctx* c, bool fit = true) {
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->pods_loaded || !c->nodes_loaded || c->stale) return ESC_E_STATE;
     hipSetDevice(c->device);          // a multi-device host drives several contexts from one thread
-    return ensure_work(c);
+    if (int32_t rc = ensure_work(c)) return rc;
+    // a node reload can change the owner split and so the exchange words (own_cap): a
+    // caller-bound buffer sized before it may be too small, so nothing runs on it until the
+    // caller binds one of the new size
+    if (fit && c->bound_pwords && xw_count(c) > c->bound_words) return ESC_E_STATE;
+    return ESC_OK;
 }
 
 }  // namespace
+
+namespace esc {
+int32_t ctx_stage_mark(esc_ctx* c) { return stage_mark(c); }
+}  // namespace esc
 
 // ======================================================================= C ABI
 extern "C" {
@@ -1262,6 +1333,7 @@ const char* esc_strerror(int32_t code) {
         case ESC_E_STATE: return "call order violated";
         case ESC_E_NODEV: return "no gfx950 device available";
         case ESC_E_COMM: return g_last_error[0] ? g_last_error : "RCCL unavailable or a collective failed";
+        case ESC_E_ORDER: return "an ordering's bounded look-back gave up (that ordering is invalid; the next one runs afresh)";
         default: return "unknown error";
     }
 }
@@ -1333,6 +1405,9 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
 #if ESC_MEASURE
     if (const char* v = std::getenv("ESC_NO_ZEROCOPY")) c->zero_copy = std::atoi(v) == 0;
 #endif
+    if (hipHostMalloc(reinterpret_cast<void**>(&c->h_oerr), sizeof(uint32_t)) != hipSuccess) return fail(ESC_E_NOMEM);
+    *c->h_oerr = 0;
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_oerr_dev), c->h_oerr, 0) != hipSuccess) return fail(ESC_E_HIP);
     const size_t G = (size_t)n_groups;
     if (dalloc(&c->d_dry, G) || dalloc(&c->d_params, G)) return fail(ESC_E_NOMEM);
     const GroupIndex& gi = c->gi;
@@ -1396,6 +1471,9 @@ int32_t esc_ctx_destroy(esc_ctx* c) {
         c->h_istage = nullptr;
         if (c->h_words) hipHostFree(c->h_words);
         c->h_words = nullptr;
+        if (c->h_oerr) hipHostFree(c->h_oerr);
+        c->h_oerr = c->h_oerr_dev = nullptr;
+        release_selections(c);
         if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
     }
     delete c;
@@ -2269,6 +2347,8 @@ int32_t esc_reduce(esc_ctx* c) {
                                    NGDecide{nullptr, nullptr, nullptr}, c->stream));
     }
     c->ng_pending = true;
+    c->tot_dec = false;              // the host totals records are the last decide's (a replayed
+                                     // graph does not run enqueue_step, which also says so: ADVICE r5)
     const int r = c->cur;
     c->cur = (c->cur + 1) % (int)c->pods.size();
     c->pending = true;
@@ -2279,7 +2359,7 @@ int32_t esc_reduce(esc_ctx* c) {
 
 int32_t esc_exchange_buffers(esc_ctx* c, void** sum_buf, int64_t* sum_count, void** min_buf, int64_t* min_count) {
     if (c && c->multi) return ESC_E_STATE;
-    int32_t rc = check_ready(c);
+    int32_t rc = check_ready(c, false);
     if (rc) return rc;
     if (sum_buf) *sum_buf = c->d_pwords;
     if (sum_count) *sum_count = xw_count(c);
@@ -2322,6 +2402,13 @@ int32_t esc_bind_exchange_buffers(esc_ctx* c, void* sum_buf, void* min_buf) {
     if (!c || (!sum_buf && min_buf)) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
     if (min_buf) return ESC_E_INVAL;                  // min_count is 0: nothing to MIN-exchange
+    if (sum_buf) {
+        // the buffer holds sum_count words as esc_exchange_buffers reports them now: record
+        // that, so a reload that grows them is refused instead of overrunning it
+        c->bound_pwords = nullptr;
+        if (int32_t rc = check_ready(c, false)) return rc;
+        c->bound_words = xw_count(c);
+    }
     c->bound_pwords = reinterpret_cast<int64_t*>(sum_buf);
     if (c->work_ready) c->d_pwords = c->bound_pwords ? c->bound_pwords : c->own_pwords;
     drop_graphs(c);
@@ -2361,7 +2448,8 @@ int32_t esc_decide(esc_ctx* c) {
     // (the tracker sums of the step), their exchanged pod words (the rank's slice, rows xs[g])
     if (!c->ng_pending) return ESC_E_STATE;            // nothing reduced since the last decide
     HIP_TRY(launch_node_groups(group_dev(c), node_dev(c), own_list(c), c->nodes.rows, c->d_trk_acc, c->d_nwords,
-                               NGDecide{c->d_pwords, c->d_dec, c->zero_copy ? c->h_cdec_dev : c->d_cdec}, c->stream));
+                               NGDecide{c->d_pwords, c->d_dec, c->zero_copy ? c->h_cdec_dev : c->d_cdec, sel_out(c)},
+                               c->stream));
     c->ng_pending = false;
     c->tot_dec = true;
     if (!c->zero_copy)
@@ -2383,6 +2471,7 @@ int32_t esc_run(esc_ctx* c) {
     c->cur = (c->cur + 1) % nrep;
     c->pending = true;
     (void)nrep;
+    c->tot_dec = true;
     if (c->order_in_step) { c->order_src = 0; c->sorted = true; }
     if (!c->use_graph || c->timing) return enqueue_step(c, r, true, true);
     return replay_step(c, c->graphs, r, true);
@@ -2394,6 +2483,111 @@ int32_t esc_set_order_in_step(esc_ctx* c, int32_t enable) {
     c->order_in_step = enable != 0;
     drop_graphs(c);
     return ESC_OK;
+}
+
+#if ESC_MEASURE
+// Fault injection (measurement library only; not in the header): the next n_order ordering
+// and n_list listing launches give up their look-back at once; the next n apply phases of
+// informer events fail after their host-side writes.
+int32_t esc_debug_lookback_fail(esc_ctx* c, int32_t n_order, int32_t n_list) {
+    if (!c || c->multi) return ESC_E_INVAL;
+    c->lb_fail_order = std::max(0, n_order);
+    c->lb_fail_list = std::max(0, n_list);
+    drop_graphs(c);                                     // captured launches hold their bound
+    return ESC_OK;
+}
+int32_t esc_debug_fail_patches(esc_ctx* c, int32_t n) {
+    if (!c || c->multi) return ESC_E_INVAL;
+    c->fail_patches = std::max(0, n);
+    return ESC_OK;
+}
+#endif
+
+int32_t esc_set_selections(esc_ctx* c, int32_t slack, int32_t group_cap) {
+    if (c && c->multi) {
+        for (int i = 0; esc::multi_sub(c, i); ++i)
+            if (int32_t rc = esc_set_selections(esc::multi_sub(c, i), slack, group_cap)) return rc;
+        return ESC_OK;
+    }
+    if (!c) return ESC_E_INVAL;
+    if (!c->has_device) return ESC_E_NODEV;
+    if (group_cap <= 0) group_cap = 256;
+    if ((uint32_t)group_cap > SEL_COUNT_MASK) return ESC_E_LIMIT;
+    hipSetDevice(c->device);
+    HIP_TRY(hipStreamSynchronize(c->stream));          // queued decisions may still write the buffer
+    drop_graphs(c);                                     // captured steps hold the old target
+    release_selections(c);
+    c->sel_slack = slack < 0 ? -1 : slack;
+    c->sel_group_cap = group_cap;
+    if (slack < 0) return ESC_OK;
+    // every group's run at its largest (header + group_cap nodes): no decision overflows it
+    c->sel_words = (int64_t)c->gi.G * (group_cap + 1);
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_sel), (size_t)c->sel_words * 4));
+    HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_sel_dev), c->h_sel, 0));
+    HIP_TRY(dalloc(&c->d_sel_total, 1));
+    HIP_TRY(hipMemset(c->d_sel_total, 0, 4));
+    for (int32_t g = 0; c->h_cdec && g < c->gi.G; ++g) c->h_cdec[g].sel = SEL_NONE;
+    return ESC_OK;
+}
+
+namespace {
+// Group g's selection in the last decision (after a wait): which (ESC_SEL_*), its nodes.
+int32_t group_selection(const esc_ctx* c, int32_t g, int32_t* which, const uint32_t** nodes, int64_t* n) {
+    *which = ESC_SEL_NONE;
+    *nodes = nullptr;
+    *n = 0;
+    if (c->multi) {
+        int32_t owner = 0;
+        if (int32_t rc = esc_group_owner(c, g, &owner)) return rc;
+        return group_selection(esc::multi_sub(c, owner), g, which, nodes, n);
+    }
+    if (c->world > 1 && group_owner_rank(c, g) != c->rank) return ESC_OK;   // decided on its owner
+    const uint32_t at = c->h_cdec[g].sel;
+    if (at == SEL_NONE) return ESC_OK;
+    if (at == SEL_OVERFLOW || (int64_t)at >= c->sel_words) {   // not delivered: the walk reads esc_group_order
+        *which = ESC_SEL_CUT;
+        return ESC_OK;
+    }
+    const uint32_t h = c->h_sel[at];
+    const uint32_t w = (h >> 28) & 3u;
+    if (w == 0) return ESC_OK;
+    *which = (int32_t)w - 1;
+    if (h & SEL_TIE) {                                  // a long tie run: no nodes delivered
+        *which |= ESC_SEL_CUT;
+        return ESC_OK;
+    }
+    if (h & SEL_CUT) *which |= ESC_SEL_CUT;
+    *nodes = c->h_sel + at + 1;
+    *n = h & SEL_COUNT_MASK;
+    return ESC_OK;
+}
+}  // namespace
+
+int32_t esc_selections(esc_ctx* c, int32_t* which, int64_t* offsets, int64_t* idx, int64_t cap, int64_t* n_total) {
+    if (!c || !which || !offsets || !n_total || cap < 0 || (cap > 0 && !idx)) return ESC_E_INVAL;
+    esc_ctx* c0 = c->multi ? esc::multi_sub(c, 0) : c;
+    if (!c0 || !c0->has_device) return ESC_E_NODEV;
+    if (c0->sel_slack < 0 || !c0->h_cdec) return ESC_E_STATE;
+    if (int32_t rc = esc_sync(c); rc != ESC_OK && rc != ESC_E_ORDER) return rc;
+    // the ordering the selections come from gave up: they are invalid, as its orderings
+    bool failed = false;
+    for (int i = 0; c->multi ? esc::multi_sub(c, i) != nullptr : i < 1; ++i)
+        failed |= (c->multi ? esc::multi_sub(c, i) : c)->ord_failed;
+    if (failed) return ESC_E_ORDER;
+    const int32_t G = c0->gi.G;
+    int64_t total = 0;
+    offsets[0] = 0;
+    for (int32_t g = 0; g < G; ++g) {
+        const uint32_t* nodes = nullptr;
+        int64_t n = 0;
+        if (int32_t rc = group_selection(c, g, &which[g], &nodes, &n)) return rc;
+        if (idx && total + n <= cap)
+            for (int64_t k = 0; k < n; ++k) idx[total + k] = nodes[k];
+        total += n;
+        offsets[g + 1] = total;
+    }
+    *n_total = total;
+    return idx && total > cap ? ESC_E_LIMIT : ESC_OK;
 }
 
 // ------------------------------------------------- RCCL exchange (§8e) inside the library
@@ -2467,7 +2661,9 @@ int32_t esc_sync(esc_ctx* c) {
         c->stage_ms[MAX_STAGES - 1] = ms;
     }
     c->pending = false;
-    return ESC_OK;
+    // an ordering whose look-back gave up: reported once (its orderings stay refused by
+    // esc_group_order until the next ordering), the next decision orders afresh
+    return order_gave_up(c) ? ESC_E_ORDER : ESC_OK;
 }
 
 int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* decisions) {
@@ -2476,7 +2672,7 @@ int32_t esc_results(esc_ctx* c, esc_group_totals* totals, esc_group_decision* de
     if (!c->has_device) return ESC_E_NODEV;
     if (!c->work_ready) return ESC_E_STATE;
     int32_t rc = esc_sync(c);
-    if (rc) return rc;
+    if (rc && rc != ESC_E_ORDER) return rc;           // a failed ordering leaves totals and decisions valid
     const int32_t G = c->gi.G;
     // With several ranks a rank decides its own groups only: the others'
     // records come back zeroed, flagged ESC_TF_NOT_OWNED / ESC_ST_NOT_OWNED.
@@ -2609,6 +2805,12 @@ int32_t apply_patches(esc_ctx* c, Patches& P, const std::vector<PatchTargets>& t
     if (hipMemcpy(dw, w.data(), w.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
         hipMemcpy(dv, v.data(), v.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
         rc = ESC_E_HIP;
+#if ESC_MEASURE
+    if (!rc && c->fail_patches > 0) {                  // injected (esc_debug_fail_patches)
+        --c->fail_patches;
+        rc = fail_hip(hipErrorUnknown, "injected patch failure");
+    }
+#endif
     for (const PatchTargets& t : targets)
         if (!rc && launch_patch(t, dw, dv, (int64_t)w.size(), c->stream) != hipSuccess) rc = ESC_E_HIP;
     if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = ESC_E_HIP;
@@ -3403,14 +3605,18 @@ int32_t esc_nodes_update(esc_ctx* c, const int64_t* ids, int64_t n, const uint32
     }
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    std::vector<int64_t> touched(ids, ids + n);
-    for (int64_t i = 0; i < n; ++i) {
-        const int64_t j = ids[i];
-        c->h_nflags[j] = (flags[i] & ~ESC_NF_TRACKED) | (c->h_nflags[j] & ESC_NF_TRACKED);
-        c->h_ncpu[j] = cpu[i];
-        c->h_nmem[j] = mem[i];
-    }
-    return patch_nodes(c, touched);
+    // the host mirrors change first: a device write that fails after them leaves the
+    // context stale until esc_load_nodes
+    return guarded(c, STALE_NODES, [&]() -> int32_t {
+        std::vector<int64_t> touched(ids, ids + n);
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t j = ids[i];
+            c->h_nflags[j] = (flags[i] & ~ESC_NF_TRACKED) | (c->h_nflags[j] & ESC_NF_TRACKED);
+            c->h_ncpu[j] = cpu[i];
+            c->h_nmem[j] = mem[i];
+        }
+        return patch_nodes(c, touched);
+    });
 }
 
 // Node informer events that add or delete nodes (pkg/k8s/cache.go:37-56 feeds the
@@ -3492,83 +3698,86 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
                 return ESC_E_LIMIT;
             }
     }
-    // commit: node table, extra labels, pair-major entries, allNodes[0]
-    c->h_xl.insert(c->h_xl.end(), s->xl_pair, s->xl_pair + s->n_xl);
-    Patches P;
-    bool first_changed = false;
-    std::vector<uint32_t> pairs;
-    for (int64_t i = 0; i < n; ++i) {
-        const int64_t j = j0 + i;
-        const uint32_t f = s->flags[i];
-        P.add(NT_FLAGS, j, f);
-        P.add(NT_LABEL0, j, s->label0[i]);
-        P.add(NT_XLOFF, j, c->h_xl_off[j]);
-        P.add(NT_CPU, j, (uint64_t)s->cpu[i]);
-        P.add(NT_MEM, j, (uint64_t)s->mem[i]);
-        P.add(NT_CREATED, j, (uint64_t)s->created_ns[i]);
-        for (uint32_t k = 0; k < nf_xlbl(f); ++k) P.add(NT_XL, c->h_xl_off[j] + k, s->xl_pair[xo[i] + k]);
-        pairs.clear();
-        if (s->label0[i] < n_gp) pairs.push_back(s->label0[i]);
-        for (uint32_t k = 0; k < nf_xlbl(f); ++k)
-            if (s->xl_pair[xo[i] + k] < n_gp) pairs.push_back(s->xl_pair[xo[i] + k]);
-        for (uint32_t q : pairs) {
-            const uint32_t e = c->pair_next[q]++;
-            ++c->pair_live[q];
-            P.add(NT_EFLAGS, e, f);
-            P.add(NT_ENODE, e, (uint32_t)j);
-            P.add(NT_ECPU, e, (uint64_t)s->cpu[i]);
-            P.add(NT_EMEM, e, (uint64_t)s->mem[i]);
-            c->h_e_node[e] = (uint32_t)j;
-            c->ne_pos.push_back(e);
-            const uint32_t code = c->gi.node_code[q];
-            auto first_of = [&](uint32_t g) {
-                GroupNode& x = c->h_gnode[g];
-                if (x.first == INT64_MAX) {           // the group's first member (controller.go:208)
-                    x.first = j;
-                    x.first_cpu = s->cpu[i];
-                    x.first_mem = s->mem[i];
-                    first_changed = true;
-                }
-            };
-            if (code < CODE_MULTI) first_of(code & NODE_GROUP_MASK);
-            else if (code != NONE) {
-                const uint32_t* l = c->gi.code_list.data() + (code & ~CODE_MULTI);
-                for (uint32_t k = 1; k <= l[0]; ++k) first_of(l[k] & NODE_GROUP_MASK);
-            }
-        }
-        c->ne_off.push_back((uint32_t)c->ne_pos.size());
-        ids_out[i] = j;
-    }
-    c->xl_used += s->n_xl;
-    c->n_nodes += n;
-    c->rm_valid = false;            // the placement stays: every table slot has a run and facts
-    int32_t rc = apply_patches(c, P, {node_targets(c)});
-    if (rc) return rc;
-    if (first_changed)
-        HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
-    for (int64_t i = 0; i < n; ++i) c->h_created.push_back(s->created_ns[i]);
-    c->node_hi = c->n_nodes;
-    if (k5) {
-        // K5: insert each new membership at its place by (creation time, index) in its
-        // group's region (the groups this rank owns; the others only count it); every group
-        // touched is rewritten from its first insertion on
-        std::unordered_map<uint32_t, std::vector<uint32_t>> add_by_g;
+    // commit: node table, extra labels, pair-major entries, allNodes[0] (a failure from here
+    // on leaves the context stale until esc_load_nodes)
+    return guarded(c, STALE_NODES, [&]() -> int32_t {
+        c->h_xl.insert(c->h_xl.end(), s->xl_pair, s->xl_pair + s->n_xl);
+        Patches P;
+        bool first_changed = false;
+        std::vector<uint32_t> pairs;
         for (int64_t i = 0; i < n; ++i) {
-            node_membs(c, j0 + i, mb);
-            for (uint32_t m : mb) {
-                const uint32_t g = m & NODE_GROUP_MASK;
-                if (owns_group(c, g)) add_by_g[g].push_back((uint32_t)(j0 + i));
-                else ++c->h_plen[g];
+            const int64_t j = j0 + i;
+            const uint32_t f = s->flags[i];
+            P.add(NT_FLAGS, j, f);
+            P.add(NT_LABEL0, j, s->label0[i]);
+            P.add(NT_XLOFF, j, c->h_xl_off[j]);
+            P.add(NT_CPU, j, (uint64_t)s->cpu[i]);
+            P.add(NT_MEM, j, (uint64_t)s->mem[i]);
+            P.add(NT_CREATED, j, (uint64_t)s->created_ns[i]);
+            for (uint32_t k = 0; k < nf_xlbl(f); ++k) P.add(NT_XL, c->h_xl_off[j] + k, s->xl_pair[xo[i] + k]);
+            pairs.clear();
+            if (s->label0[i] < n_gp) pairs.push_back(s->label0[i]);
+            for (uint32_t k = 0; k < nf_xlbl(f); ++k)
+                if (s->xl_pair[xo[i] + k] < n_gp) pairs.push_back(s->xl_pair[xo[i] + k]);
+            for (uint32_t q : pairs) {
+                const uint32_t e = c->pair_next[q]++;
+                ++c->pair_live[q];
+                P.add(NT_EFLAGS, e, f);
+                P.add(NT_ENODE, e, (uint32_t)j);
+                P.add(NT_ECPU, e, (uint64_t)s->cpu[i]);
+                P.add(NT_EMEM, e, (uint64_t)s->mem[i]);
+                c->h_e_node[e] = (uint32_t)j;
+                c->ne_pos.push_back(e);
+                const uint32_t code = c->gi.node_code[q];
+                auto first_of = [&](uint32_t g) {
+                    GroupNode& x = c->h_gnode[g];
+                    if (x.first == INT64_MAX) {           // the group's first member (controller.go:208)
+                        x.first = j;
+                        x.first_cpu = s->cpu[i];
+                        x.first_mem = s->mem[i];
+                        first_changed = true;
+                    }
+                };
+                if (code < CODE_MULTI) first_of(code & NODE_GROUP_MASK);
+                else if (code != NONE) {
+                    const uint32_t* l = c->gi.code_list.data() + (code & ~CODE_MULTI);
+                    for (uint32_t k = 1; k <= l[0]; ++k) first_of(l[k] & NODE_GROUP_MASK);
+                }
             }
+            c->ne_off.push_back((uint32_t)c->ne_pos.size());
+            ids_out[i] = j;
         }
-        Patches R;                                   // one scatter for every touched region
-        regions_insert(c, add_by_g, R);
-        PatchTargets t = region_targets(c);
-        rc = apply_patches(c, R, {t});
+        c->xl_used += s->n_xl;
+        c->n_nodes += n;
+        c->rm_valid = false;            // the placement stays: every table slot has a run and facts
+        int32_t rc = apply_patches(c, P, {node_targets(c)});
         if (rc) return rc;
-    }
-    c->sorted = false;
-    return ESC_OK;
+        if (first_changed)
+            HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
+        for (int64_t i = 0; i < n; ++i) c->h_created.push_back(s->created_ns[i]);
+        c->node_hi = c->n_nodes;
+        if (k5) {
+            // K5: insert each new membership at its place by (creation time, index) in its
+            // group's region (the groups this rank owns; the others only count it); every group
+            // touched is rewritten from its first insertion on
+            std::unordered_map<uint32_t, std::vector<uint32_t>> add_by_g;
+            for (int64_t i = 0; i < n; ++i) {
+                node_membs(c, j0 + i, mb);
+                for (uint32_t m : mb) {
+                    const uint32_t g = m & NODE_GROUP_MASK;
+                    if (owns_group(c, g)) add_by_g[g].push_back((uint32_t)(j0 + i));
+                    else ++c->h_plen[g];
+                }
+            }
+            Patches R;                                   // one scatter for every touched region
+            regions_insert(c, add_by_g, R);
+            PatchTargets t = region_targets(c);
+            rc = apply_patches(c, R, {t});
+            if (rc) return rc;
+        }
+        c->sorted = false;
+        return ESC_OK;
+    });
 }
 
 int32_t esc_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
@@ -3584,35 +3793,38 @@ int32_t esc_nodes_delete(esc_ctx* c, const int64_t* ids, int64_t n) {
     if (n == 0) return ESC_OK;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    // tracker entries of the deleted nodes go (a re-added name is re-tracked by the host)
-    std::vector<uint64_t> next;
-    next.reserve(c->h_trk.size());
-    for (uint64_t k : c->h_trk)
-        if (!std::binary_search(del.begin(), del.end(), (int64_t)(k >> 32))) next.push_back(k);
-    if (next.size() != c->h_trk.size()) {
-        int32_t rc = write_tracker(c, next);
-        if (rc) return rc;
-    }
-    for (int64_t j : del) {
-        auto drop = [&](uint32_t q) { if (q < c->gi.n_gp) --c->pair_live[q]; };   // live entries (owner split)
-        drop(c->h_label0[j]);
-        for (uint32_t k = 0; k < nf_xlbl(c->h_nflags[j]); ++k) drop(c->h_xl[c->h_xl_off[j] + k]);
-        c->h_nflags[j] = (c->h_nflags[j] & ~ESC_NF_TRACKED) | ESC_NF_ABSENT;
-    }
-    // allNodes[0] of the groups whose first member went: the next live entry of the pair
-    bool first_changed = false;
-    for (int32_t g = 0; g < c->gi.G; ++g) {
-        GroupNode& x = c->h_gnode[g];
-        if (x.first == INT64_MAX || !(c->h_nflags[x.first] & ESC_NF_ABSENT)) continue;
-        pair_first(c, c->gi.gpair[g], x);
-        first_changed = true;
-    }
-    if (first_changed)
-        HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
-    // the placement stays: a deleted node's entries are absent (K6 / K7 skip them) and its
-    // pods' PodRefs stay in its run until they are rebound or deleted
-    c->rm_valid = false;
-    return patch_nodes(c, del);
+    // from the first write on, a failure leaves the context stale until esc_load_nodes
+    return guarded(c, STALE_NODES, [&]() -> int32_t {
+        // tracker entries of the deleted nodes go (a re-added name is re-tracked by the host)
+        std::vector<uint64_t> next;
+        next.reserve(c->h_trk.size());
+        for (uint64_t k : c->h_trk)
+            if (!std::binary_search(del.begin(), del.end(), (int64_t)(k >> 32))) next.push_back(k);
+        if (next.size() != c->h_trk.size()) {
+            int32_t rc = write_tracker(c, next);
+            if (rc) return rc;
+        }
+        for (int64_t j : del) {
+            auto drop = [&](uint32_t q) { if (q < c->gi.n_gp) --c->pair_live[q]; };   // live entries (owner split)
+            drop(c->h_label0[j]);
+            for (uint32_t k = 0; k < nf_xlbl(c->h_nflags[j]); ++k) drop(c->h_xl[c->h_xl_off[j] + k]);
+            c->h_nflags[j] = (c->h_nflags[j] & ~ESC_NF_TRACKED) | ESC_NF_ABSENT;
+        }
+        // allNodes[0] of the groups whose first member went: the next live entry of the pair
+        bool first_changed = false;
+        for (int32_t g = 0; g < c->gi.G; ++g) {
+            GroupNode& x = c->h_gnode[g];
+            if (x.first == INT64_MAX || !(c->h_nflags[x.first] & ESC_NF_ABSENT)) continue;
+            pair_first(c, c->gi.gpair[g], x);
+            first_changed = true;
+        }
+        if (first_changed)
+            HIP_TRY(hipMemcpy(c->nodes.gnode, c->h_gnode.data(), c->h_gnode.size() * sizeof(GroupNode), hipMemcpyHostToDevice));
+        // the placement stays: a deleted node's entries are absent (K6 / K7 skip them) and its
+        // pods' PodRefs stay in its run until they are rebound or deleted
+        c->rm_valid = false;
+        return patch_nodes(c, del);
+    });
 }
 
 // Node informer Update events that change a node's LABELS or CREATION TIME (besides its
@@ -3957,28 +4169,32 @@ int32_t esc_tracker_update(esc_ctx* c, int32_t group, const int64_t* add, int64_
     std::merge(kept.begin(), kept.end(), ak.begin(), ak.end(), next.begin());
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    int32_t rc = write_tracker(c, next);
-    if (rc) return rc;
-    // ESC_NF_TRACKED = tracked by some group (controller.go:128 is per group; the kernels
-    // confirm the group through the list)
-    std::vector<int64_t> flip;
-    std::sort(touched.begin(), touched.end());
-    touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
-    for (int64_t j : touched) {
-        const uint64_t lo = (uint64_t)(uint32_t)j << 32;
-        const auto it = std::lower_bound(c->h_trk.begin(), c->h_trk.end(), lo);
-        const bool on = it != c->h_trk.end() && (*it >> 32) == (uint64_t)(uint32_t)j;
-        const uint32_t f = on ? (c->h_nflags[j] | ESC_NF_TRACKED) : (c->h_nflags[j] & ~ESC_NF_TRACKED);
-        if (f != c->h_nflags[j]) { c->h_nflags[j] = f; flip.push_back(j); }
-    }
-    c->sorted = false;
-    c->rm_valid = false;
-    if (!flip.empty()) return patch_nodes(c, touched);     // node table + entries + K5 copies
-    // the K5 copies carry each dry membership's tracker bit: patch the touched nodes'
-    rc = patch_regions(c, touched);
-    if (rc) return rc;
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return ESC_OK;
+    // the tracker list, then the flags: a failure after the first write leaves the context
+    // stale until esc_load_nodes
+    return guarded(c, STALE_NODES, [&]() -> int32_t {
+        int32_t rc = write_tracker(c, next);
+        if (rc) return rc;
+        // ESC_NF_TRACKED = tracked by some group (controller.go:128 is per group; the kernels
+        // confirm the group through the list)
+        std::vector<int64_t> flip;
+        std::sort(touched.begin(), touched.end());
+        touched.erase(std::unique(touched.begin(), touched.end()), touched.end());
+        for (int64_t j : touched) {
+            const uint64_t lo = (uint64_t)(uint32_t)j << 32;
+            const auto it = std::lower_bound(c->h_trk.begin(), c->h_trk.end(), lo);
+            const bool on = it != c->h_trk.end() && (*it >> 32) == (uint64_t)(uint32_t)j;
+            const uint32_t f = on ? (c->h_nflags[j] | ESC_NF_TRACKED) : (c->h_nflags[j] & ~ESC_NF_TRACKED);
+            if (f != c->h_nflags[j]) { c->h_nflags[j] = f; flip.push_back(j); }
+        }
+        c->sorted = false;
+        c->rm_valid = false;
+        if (!flip.empty()) return patch_nodes(c, touched);     // node table + entries + K5 copies
+        // the K5 copies carry each dry membership's tracker bit: patch the touched nodes'
+        rc = patch_regions(c, touched);
+        if (rc) return rc;
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        return ESC_OK;
+    });
 }
 
 int32_t esc_tracker_list(const esc_ctx* c, int32_t group, int64_t* idx_out, int64_t cap, int64_t* n_out) {
@@ -4271,12 +4487,9 @@ int32_t esc_group_order(esc_ctx* c, int32_t group, int32_t which, int64_t* idx_o
     if (!c->sorted) return ESC_E_STATE;
     hipSetDevice(c->device);
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (c->d_ostat && c->n_chunks && !c->ord_err_read) {   // once per ordering: a split chunk that gave up
-        uint64_t e = 0;
-        HIP_TRY(hipMemcpy(&e, c->d_ostat + 2 * c->n_chunks, 8, hipMemcpyDeviceToHost));
-        if (e) return fail_hip(hipErrorUnknown, "ordering: look-back bound");
-        c->ord_err_read = true;
-    }
+    order_gave_up(c);
+    if (c->ord_failed) return ESC_E_ORDER;          // this ordering's look-back gave up
+
     // class segments [s0, s1) (untainted, oldest first) and [s2, s3) (tainted, newest first)
     const int64_t so = 2 * which;
     int64_t seg[2];

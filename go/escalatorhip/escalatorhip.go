@@ -274,7 +274,22 @@ type Decision struct {
 	Branch                     int32 // ESC_BR_*
 	Err                        error // the reference's error, text verbatim
 	TaintErr                   error // scaleDownTaint's formatted error
+	// With SetSelections: the first nodes of the walk the decision asks for, delivered with
+	// it — SelTaint: untainted oldest first (taintOldestN, scale_down.go:171-205), SelUntaint:
+	// tainted newest first (untaintNewestN, scale_up.go:118-163), NToTaint / Delta + slack of
+	// them.  The walk skips a node whose API write fails; when it runs past Selection (or
+	// SelectionCut is set) it continues with Context.Order.
+	SelectionKind int32 // SelNone, SelTaint, SelUntaint
+	Selection     []int64
+	SelectionCut  bool
 }
+
+// Selection kinds (ESC_SEL_*).
+const (
+	SelNone    = int32(C.ESC_SEL_NONE)
+	SelTaint   = int32(C.ESC_SEL_TAINT)
+	SelUntaint = int32(C.ESC_SEL_UNTAINT)
+)
 
 // PodsRequestsTotal is the group's CalculatePodsRequestsTotal(pods) (pkg/k8s/util.go:27-38,
 // called at controller.go:262) answered from the batched decision: (mem, cpu) built with the
@@ -300,6 +315,22 @@ type Context struct {
 	groups []GroupSpec
 	cspecs unsafe.Pointer // C copy of the group specs, alive as long as the context
 	names  arena
+	sel    bool // SetSelections on: RunOnce returns the walks' first nodes
+}
+
+// SetSelections puts the orderings into every decision and has RunOnce return each group's
+// walk prefix (NToTaint or Delta, plus slack for failed API writes; at most groupCap nodes,
+// 0 = 256) in its Decision, so the controller's taint / untaint loop needs no per-group
+// Order call (controller.go:367-383).  slack < 0 turns them off.
+func (x *Context) SetSelections(slack, groupCap int) error {
+	if rc := C.esc_set_order_in_step(x.c, 1); rc != C.ESC_OK {
+		return rcErr("esc_set_order_in_step", rc)
+	}
+	if rc := C.esc_set_selections(x.c, C.int32_t(slack), C.int32_t(groupCap)); rc != C.ESC_OK {
+		return rcErr("esc_set_selections", rc)
+	}
+	x.sel = slack >= 0
+	return nil
 }
 
 // NewContext creates the context for groups (fixed for its lifetime, client.go:55-64).
@@ -312,8 +343,8 @@ func NewContext(groups []GroupSpec, device, rank, world int) (*Context, error) {
 
 // NewContextMulti creates ONE context driving every listed GPU from this process
 // (esc_ctx_create_multi): the pods are sharded over the devices, each owns the node side
-// of a range of groups, and RunOnce's exchange is an ncclAllReduce per device inside one
-// RCCL group call — the reference stays one process with one informer set
+// of a range of groups, and RunOnce's exchange is an in-place ncclReduceScatter per device
+// (each receiving its own groups' rows) inside one RCCL group call — the reference stays one process with one informer set
 // (cmd/main.go:187, controller.go:416-445).
 func NewContextMulti(groups []GroupSpec, devices []int) (*Context, error) {
 	if len(devices) == 0 {
@@ -438,7 +469,8 @@ func (x *Context) Calibrate(rounds int) error {
 // RunOnce evaluates scaleNodeGroup's decision for every group at once (controller.go:192-351):
 // listers + filters + sums + filterNodes + cached capacity + gates + percentages + delta +
 // the scale-down clamp.  With a communicator (CommInit) the per-group pod sums are
-// all-reduced over RCCL inside esc_step.
+// reduce-scattered over RCCL inside esc_step, every rank receiving (and deciding) the
+// groups it owns.
 func (x *Context) RunOnce(states []GroupState) ([]Decision, error) {
 	G := len(x.groups)
 	if len(states) != G {
@@ -459,13 +491,39 @@ func (x *Context) RunOnce(states []GroupState) ([]Decision, error) {
 	if rc := C.esc_step(x.c); rc != C.ESC_OK {
 		return nil, rcErr("esc_step", rc)
 	}
-	if rc := C.esc_sync(x.c); rc != C.ESC_OK {
+	// ESC_E_ORDER: the step's ordering gave up a bounded wait; the totals and decisions
+	// stand, and the walks order afresh through Order (esc_sort_nodes + esc_group_order)
+	orderFailed := false
+	if rc := C.esc_sync(x.c); rc == C.ESC_E_ORDER {
+		orderFailed = true
+	} else if rc != C.ESC_OK {
 		return nil, rcErr("esc_sync", rc)
 	}
 	tot := make([]C.esc_group_totals, G)
 	dec := make([]C.esc_group_decision, G)
 	if rc := C.esc_results(x.c, ptr(tot), ptr(dec)); rc != C.ESC_OK {
 		return nil, rcErr("esc_results", rc)
+	}
+	which := make([]C.int32_t, G)
+	off := make([]C.int64_t, G+1)
+	var sel []C.int64_t
+	if x.sel && !orderFailed {
+		var n C.int64_t
+		rc := C.esc_selections(x.c, ptr(which), ptr(off), nil, 0, &n)
+		if rc == C.ESC_OK {
+			sel = make([]C.int64_t, n+1)
+			rc = C.esc_selections(x.c, ptr(which), ptr(off), ptr(sel), n, &n)
+		}
+		if rc == C.ESC_E_ORDER {
+			orderFailed = true
+		} else if rc != C.ESC_OK {
+			return nil, rcErr("esc_selections", rc)
+		}
+	}
+	if orderFailed {
+		if err := x.SortNodes(); err != nil {
+			return nil, err
+		}
 	}
 	out := make([]Decision, G)
 	for g := range out {
@@ -479,6 +537,19 @@ func (x *Context) RunOnce(states []GroupState) ([]Decision, error) {
 			Delta: int64(d.delta), NToTaint: int64(d.n_to_taint),
 			CachedCPUMilli: int64(d.cached_cpu_m), CachedMemBytes: int64(d.cached_mem_b),
 			Branch: int32(d.branch), Err: statusErr(d.status),
+			SelectionKind: SelNone,
+		}
+		if x.sel {
+			if orderFailed {
+				out[g].SelectionCut = true // no list: the walk reads Order
+			} else if w := int32(which[g]); w != SelNone {
+				out[g].SelectionKind = w & 3
+				out[g].SelectionCut = w&int32(C.ESC_SEL_CUT) != 0
+				out[g].Selection = make([]int64, off[g+1]-off[g])
+				for i := range out[g].Selection {
+					out[g].Selection[i] = int64(sel[int(off[g])+i])
+				}
+			}
 		}
 		if d.taint_status == C.ESC_ST_ERR_TAINT_MIN { // scale_down.go:150-154
 			buf := make([]byte, 160)
@@ -505,6 +576,12 @@ func (x *Context) Order(g int, oldest bool, n int) ([]int64, error) {
 	idx := make([]int64, n+1)
 	var got C.int64_t
 	rc := C.esc_group_order(x.c, C.int32_t(g), which, (*C.int64_t)(unsafe.Pointer(ptr(idx))), C.int64_t(n), &got)
+	if rc == C.ESC_E_ORDER { // that ordering gave up its bounded wait: order afresh, once
+		if err := x.SortNodes(); err != nil {
+			return nil, err
+		}
+		rc = C.esc_group_order(x.c, C.int32_t(g), which, (*C.int64_t)(unsafe.Pointer(ptr(idx))), C.int64_t(n), &got)
+	}
 	if rc != C.ESC_OK {
 		return nil, rcErr("esc_group_order", rc)
 	}
@@ -571,7 +648,7 @@ func CommUniqueID() ([]byte, error) {
 }
 
 // CommInit joins the RCCL communicator (collective: blocks until every rank joined).
-// RunOnce then all-reduces the per-group pod words over xGMI inside esc_step.
+// RunOnce then reduce-scatters the owner-major pod words over xGMI inside esc_step.
 func (x *Context) CommInit(id []byte, rank, world int) error {
 	cid := C.CBytes(id)
 	defer C.free(cid)

@@ -13,8 +13,9 @@
  *                       esc_packer_set_tracker (dry-mode groups), esc_packer_view,
  *                       esc_load_pods, esc_load_nodes, esc_packer_destroy
  *   (*Context).Calibrate esc_k1_calibrate (once, after the first state)
- *   (*Context).RunOnce  esc_set_state, esc_step, esc_sync, esc_results,
- *                       esc_sort_nodes, esc_group_order (taintOldestN / untaintNewestN)
+ *   (*Context).SetSelections esc_set_order_in_step, esc_set_selections (slack 1)
+ *   (*Context).RunOnce  esc_set_state, esc_step, esc_sync, esc_results, esc_selections
+ *   (*Context).Order    esc_sort_nodes, esc_group_order (taintOldestN / untaintNewestN)
  *   CalculatePodsRequestsTotal / CalculateNodesCapacityTotal
  *                       esc_pods_requests_total, esc_nodes_capacity_total
  *   calcPercentUsage / calcScaleUpDelta
@@ -302,6 +303,10 @@ int main(int argc, char** argv) {
     device_call("esc_load_nodes", esc_load_nodes(ctx, &ns, 0, ns.n_nodes));
     esc_packer_destroy(pk);      /* inputs are never retained: the snapshot lives in HBM */
 
+    /* (*Context).SetSelections(1, 0): the walks' first nodes come with every decision */
+    device_call("esc_set_order_in_step", esc_set_order_in_step(ctx, 1));
+    device_call("esc_set_selections", esc_set_selections(ctx, 1, 0));
+
     /* (*Context).RunOnce */
     device_call("esc_set_state", esc_set_state(ctx, states));
     device_call("esc_k1_calibrate", esc_k1_calibrate(ctx, 2));     /* (*Context).Calibrate */
@@ -324,6 +329,19 @@ int main(int argc, char** argv) {
                g, bits(d->cpu_pct), bits(d->mem_pct), d->delta, d->n_to_taint, d->cached_cpu_m, d->cached_mem_b,
                d->status, d->branch, d->taint_status);
         printf("status %d %s|%s\n", g, d->status ? esc_status_string(d->status) : "", msg);
+    }
+    {   /* RunOnce's esc_selections: sizes, then the nodes */
+        int32_t* which = cal((size_t)G, sizeof(int32_t));
+        int64_t* off = cal((size_t)G + 1, sizeof(int64_t));
+        int64_t total = 0;
+        device_call("esc_selections", esc_selections(ctx, which, off, NULL, 0, &total));
+        int64_t* sel = cal((size_t)(total ? total : 1), sizeof(int64_t));
+        device_call("esc_selections", esc_selections(ctx, which, off, sel, total, &total));
+        for (int g = 0; g < G; g++) {
+            printf("select %d %d %" PRId64, g, which[g], off[g + 1] - off[g]);
+            for (int64_t i = off[g]; i < off[g + 1]; i++) printf(" %" PRId64, sel[i]);
+            printf("\n");
+        }
     }
     device_call("esc_sort_nodes", esc_sort_nodes(ctx));
     int64_t* idx = cal((size_t)(N ? N : 1), sizeof(int64_t));

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ESC_ABI_VERSION 5
+#define ESC_ABI_VERSION 6
 
 /* ---------------------------------------------------------------- return codes */
 #define ESC_OK          0
@@ -47,6 +47,9 @@ extern "C" {
 #define ESC_E_STATE    -5   /* call order violated (e.g. decide before load)          */
 #define ESC_E_NODEV    -6   /* library loaded without a usable gfx950 device          */
 #define ESC_E_COMM     -7   /* RCCL not loadable, or an RCCL call failed               */
+#define ESC_E_ORDER    -8   /* a K5 ordering's bounded look-back gave up: that ordering is
+                               invalid (esc_sync reports it once, esc_group_order refuses it);
+                               totals, decisions and the next ordering are unaffected      */
 
 /* ------------------------------------------------------- per-group status codes
  * esc_status_string(code) returns the reference's error text verbatim.            */
@@ -400,8 +403,12 @@ int32_t esc_exchange_slice(const esc_ctx* ctx, int64_t* offset, int64_t* count);
 int32_t esc_exchange_rows(const esc_ctx* ctx, const esc_node_soa* nodes, int32_t world, uint32_t* rows,
                           int32_t* own_rows);
 /* Use caller-allocated device buffers (e.g. torch tensors handed to RCCL) as the
- * exchange buffers; sizes as reported by esc_exchange_buffers.  NULL restores the
- * context's own buffers (min_buf may be NULL when min_count is 0). */
+ * exchange buffers; sizes as reported by esc_exchange_buffers at the time of the bind
+ * (a snapshot must be loaded).  NULL restores the context's own buffers (min_buf may be
+ * NULL when min_count is 0).  sum_count follows the owner split, which every
+ * esc_load_nodes recomputes: when a reload grows it past the bound buffer's size, every
+ * call that would write the buffer returns ESC_E_STATE until a buffer of the new
+ * sum_count (esc_exchange_buffers still reports it) is bound. */
 int32_t esc_bind_exchange_buffers(esc_ctx* ctx, void* sum_buf, void* min_buf);
 /* Host-staged exchange for hosts without a device collective (synchronous); the min
  * arrays are ignored (may be NULL) when min_count is 0. */
@@ -425,7 +432,9 @@ int32_t esc_comm_unique_id(void* id_out);
 int32_t esc_comm_init(esc_ctx* ctx, const void* id, int32_t rank, int32_t world);
 int32_t esc_exchange(esc_ctx* ctx);
 int32_t esc_step(esc_ctx* ctx);
-/* Ranks of the context's communicator (ncclCommCount; a multi-device context: its devices). */
+/* Ranks of the context's RCCL communicator (ncclCommCount; a multi-device context: of its
+ * ncclCommInitAll communicators).  0 for a multi-device context on the peer exchange (no
+ * communicator exists); ESC_E_STATE for a per-device context before esc_comm_init. */
 int32_t esc_comm_size(const esc_ctx* ctx, int32_t* ranks);
 /* Every group's totals and decision.  world > 1 (one process per GPU): the rank's own
  * groups; the others' records are zero, flagged ESC_TF_NOT_OWNED / ESC_ST_NOT_OWNED (their
@@ -594,9 +603,11 @@ int32_t esc_removal_nodes(esc_ctx* ctx, int32_t group, int64_t* idx_out, int64_t
  * The index carries node indices in 28 bits: a node table of 2^28 slots or more returns
  * ESC_E_LIMIT.  Its group starts come from the host's live entry counts; the device's own
  * total is checked against them on a fresh build (every build with ESC_CHECK_INDEX=1),
- * a mismatch (or a listing or ordering chunk that gave up its bounded wait) returning
- * ESC_E_HIP.                                                                              */
+ * a mismatch (or a listing chunk that gave up its bounded wait) returning ESC_E_HIP.       */
 int32_t esc_sort_nodes(esc_ctx* ctx);
+/* (esc_sort_nodes' look-backs are bounded waits: a chunk that gives up leaves that ordering
+ * invalid and is reported as ESC_E_ORDER — once by esc_sync, and by esc_group_order and
+ * esc_selections until the next ordering; the next ordering runs afresh.) */
 /* Include the per-decision ordering in every decision (esc_run / esc_reduce / esc_step):
  * the packed small groups are ordered by blocks of the step's fused tail launch (after K1,
  * beside the fold and K2), the larger groups by the split kernel right after it, all on
@@ -610,6 +621,34 @@ int32_t esc_build_age_index(esc_ctx* ctx);
 int32_t esc_order_info(const esc_ctx* ctx, int64_t* n_memberships, int32_t* key_bits);
 int32_t esc_group_order(esc_ctx* ctx, int32_t group, int32_t which,
                         int64_t* idx_out, int64_t cap, int64_t* n_out);
+
+/* Selections delivered WITH the decision (controller.go:367-383: ScaleDown -> taintOldestN,
+ * scale_down.go:171-205; ScaleUp -> untaintNewestN, scale_up.go:118-163), so a host walks
+ * them without one esc_group_order round trip per group.  esc_set_selections(slack >= 0)
+ * turns them on (the ordering must be in the step: esc_set_order_in_step), slack < 0 off;
+ * group_cap <= 0 means 256.  Every decision then writes, for every group it decides:
+ *   delta < 0 with taint_status ESC_ST_OK: the first min(n_to_taint + slack, untainted)
+ *     untainted nodes, oldest first (ESC_SEL_TAINT);
+ *   delta > 0 (scale-up and below-minimum branches): the first min(delta + slack, tainted)
+ *     tainted nodes, newest first (ESC_SEL_UNTAINT);
+ * at most group_cap nodes, ties by ascending snapshot index (as esc_group_order).  `slack`
+ * covers the API writes that fail: the reference's walk skips a node whose taint / untaint
+ * fails and goes on down the order.  The nodes go to pinned host memory inside the step
+ * (zero-copy), so esc_selections copies nothing from the device. */
+int32_t esc_set_selections(esc_ctx* ctx, int32_t slack, int32_t group_cap);
+#define ESC_SEL_NONE    -1   /* the decision asks for no walk                          */
+#define ESC_SEL_TAINT    0   /* untainted nodes, oldest first (taintOldestN)           */
+#define ESC_SEL_UNTAINT  1   /* tainted nodes, newest first (untaintNewestN)            */
+#define ESC_SEL_CUT      4   /* or'ed: the walk may need more than the list holds (group_cap,
+                                or a tie run too long to resolve in-kernel: then the list is
+                                empty): continue with esc_group_order                   */
+/* After a decision: which[g] (ESC_SEL_*) and offsets[g] .. offsets[g + 1] (G + 1 entries)
+ * of group g's nodes in idx (snapshot indices); idx == NULL (cap 0) fills which, offsets and
+ * *n_total only (the size idx needs; ESC_E_LIMIT when cap is short).  world > 1: the rank's
+ * own groups (the others ESC_SEL_NONE); a multi-device context: every group.  ESC_E_STATE
+ * when selections are off; ESC_E_ORDER when the decision's ordering gave up (then use
+ * esc_sort_nodes + esc_group_order). */
+int32_t esc_selections(esc_ctx* ctx, int32_t* which, int64_t* offsets, int64_t* idx, int64_t cap, int64_t* n_total);
 
 /* ----------------------------------------------- per-function drop-ins (GPU)
  * Same argument meaning as the Go functions; these pack the given slice in list mode

@@ -100,7 +100,9 @@ prof() {       # name
     wr=$(find $OUT/write_$name -name "run_counter_collection.csv" | head -1)
     mkdir -p $PROF/raw_$name
     cp $st $PROF/kernel_stats_$name.csv
-    cp $OUT/pbench_$name.json $PROF/bench_$name.json
+    # the profile's own bench line under its own name (the bench stage writes bench_*.json
+    # in $OUT: a later stage can never overwrite what the summary was computed from)
+    cp $OUT/pbench_$name.json $PROF/pbench_$name.json
     # the raw CSVs, cut to our kernels' columns, so the summary can be recomputed from the tree
     python3 - "$tr" "$fe" "$wr" "$PROF/raw_$name" <<'PY'
 import csv, sys
@@ -116,7 +118,7 @@ for src, dst, cols in ((tr, "kernel_trace.csv", ["Kernel_Name", "Dispatch_Id", "
                 w.writerow([r[c] for c in cols])
 PY
     python3 scripts/prof_summary.py --trace $PROF/raw_$name/kernel_trace.csv --fetch $PROF/raw_$name/pmc_fetch.csv \
-        --write $PROF/raw_$name/pmc_write.csv --last $(last_of $name) --bench $PROF/bench_$name.json \
+        --write $PROF/raw_$name/pmc_write.csv --last $(last_of $name) --bench $PROF/pbench_$name.json \
         --out $PROF/summary_$name.json
 }
 

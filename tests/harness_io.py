@@ -125,6 +125,8 @@ def run(path: str, timeout: int = 120, shards: int = 0) -> dict:
             res["status"][int(w[1])] = line.split(" ", 2)[2]
         elif w[0] == "order":
             res["order"][(int(w[1]), int(w[2]))] = [int(x) for x in w[4:4 + int(w[3])]]
+        elif w[0] == "select":
+            res.setdefault("select", {})[int(w[1])] = (int(w[2]), [int(x) for x in w[4:4 + int(w[3])]])
         elif w[0] == "nodev":
             res["nodev"] = w[1]
         elif w[0] in ("list_pods", "list_nodes"):

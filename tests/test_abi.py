@@ -14,7 +14,7 @@ def test_library_exports_every_header_symbol():
     assert len(fns) >= 40
     assert [f for f in fns if not hasattr(lib, f)] == []
     assert sorted(set(fns) - set(L._SIGS)) == []
-    assert lib.esc_abi_version() == 5
+    assert lib.esc_abi_version() == 6
 
 
 def test_product_library_reads_no_result_changing_knob():

@@ -66,4 +66,16 @@ def test_stage_layout_names_every_event():
     assert bench.stage_layout(1, 8, None, "nccl") == base + ["k_node_groups+decide"]            # --shard-of 8
     assert bench.stage_layout(8, 8, None, "nccl") == base + ["exchange", "k_node_groups+decide"]
     assert bench.stage_layout(2, 2, None, "gloo") == base + ["exchange_host_staged", "k_node_groups+decide"]
-    assert bench.stage_layout(1, 1, [0, 1], "multi") == base + ["k_node_groups"]
+    assert bench.stage_layout(1, 1, [0, 1], "multi") == base + ["exchange", "k_node_groups+decide"]
+
+
+def test_rccl_ranks_field_is_truthful():
+    """`rccl_ranks` is ncclCommCount of a live communicator, never a device count: None for a
+    multi-device context on its peer exchange (esc_comm_size 0), for gloo and for one rank."""
+    def never():
+        raise AssertionError("no communicator to ask")
+    assert bench.rccl_ranks_field(lambda: 0, [0, 0], 1, "multi") is None          # peer exchange
+    assert bench.rccl_ranks_field(lambda: 2, [0, 1], 1, "multi") == 2             # ncclCommInitAll
+    assert bench.rccl_ranks_field(lambda: 8, None, 8, "nccl") == 8
+    assert bench.rccl_ranks_field(never, None, 2, "gloo") is None
+    assert bench.rccl_ranks_field(never, None, 1, "nccl") is None

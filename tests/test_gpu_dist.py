@@ -4,7 +4,7 @@ OWN exchange words.
 Each rank is its own process with its own context (esc_ctx_create(rank, world)): it loads
 its contiguous pod shard and the whole node table, runs its shard step (K1, the fused tail,
 its owned node pairs), hands its words to escalator_amd.dist.Exchange (esc_exchange_download
--> torch.distributed all_reduce SUM -> esc_exchange_upload) and runs K4 — the
+-> torch.distributed reduce_scatter_tensor SUM into its own slice -> esc_exchange_upload) and runs K4 — the
 one-process-per-GPU shape bench.py --gpus N runs, with the collective host-staged because
 RCCL cannot put two ranks on one device.  Rank 0's and rank 1's totals, decisions and
 gauges, and the ranks' merged orderings (dist.gather_orders), are compared with the C

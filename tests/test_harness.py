@@ -72,8 +72,18 @@ def test_harness_shim_sequence_vs_literal(harness, tmp_path, seed, shards):
         assert err == (L["err"] or ""), g
         assert terr == (L["taint_err"] or ""), g
         unt, tn = L["untainted"], L["tainted"]
-        assert r["order"][(g, 0)] == [unt[i] for i in O.oldest_first([nodes[i]["created_ns"] for i in unt])]
-        assert r["order"][(g, 1)] == [tn[i] for i in O.newest_first([nodes[i]["created_ns"] for i in tn])]
+        oldest = [unt[i] for i in O.oldest_first([nodes[i]["created_ns"] for i in unt])]
+        newest = [tn[i] for i in O.newest_first([nodes[i]["created_ns"] for i in tn])]
+        assert r["order"][(g, 0)] == oldest
+        assert r["order"][(g, 1)] == newest
+        # RunOnce's selections (slack 1): the walk's first nodes, delivered with the decision
+        which, sel = r["select"][g]
+        if L["delta"] > 0:
+            assert which == 1 and sel == newest[:L["delta"] + 1], (g, which, sel)
+        elif L["delta"] < 0 and not L["taint_err"]:
+            assert which == 0 and sel == oldest[:L["n_to_taint"] + 1], (g, which, sel)
+        else:
+            assert which == -1 and sel == [], (g, which, sel)
     try:
         mem, cpu = O.calculate_pods_requests_total(pods)
         assert r["list_pods"] == (mem, cpu)
