@@ -911,6 +911,13 @@ def main():
                                             "(> 1 possible: the resident format is packed, see roofline for the physical "
                                             "bytes)"),
         "k1_partials": k1_partials,
+        # this rank's (device 0's) algorithmic bytes per step: K1's pod blocks, K2's node
+        # entries, 12 B per ordered membership (the region and group words read, the node
+        # written) -- what scripts/prof_summary.py sets the step's PMC traffic against
+        "step_bytes": {"pods": int(algo), "nodes": int(node_b // (len(multi) if multi else 1)),
+                       "orderings": 0 if args.no_order else int(12 * n_memb // (len(multi) if multi else 1)),
+                       "total": int(algo + node_b // (len(multi) if multi else 1) +
+                                    (0 if args.no_order else 12 * n_memb // (len(multi) if multi else 1)))},
         "node_bytes_per_decision": node_b,
         "exchange": exchange,
         "rccl_ranks": rccl_ranks,

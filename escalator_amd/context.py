@@ -106,24 +106,6 @@ class Synth:
     def nodes(self) -> dict:
         return _view(self.node_c, _NODE_FIELDS)
 
-    def set_selections(self, slack: int = 0, group_cap: int = 0):
-        """Deliver every decided group's taint / untaint nodes with the decision
-        (esc_set_selections; slack < 0 turns them off).  Needs the ordering in the step."""
-        L.check(self.lib.esc_set_selections(self.handle, int(slack), int(group_cap)), "esc_set_selections")
-
-    def selections(self):
-        """The last decision's selections: (which[G] (ESC_SEL_*), offsets[G + 1], nodes) —
-        group g's snapshot indices are nodes[offsets[g]:offsets[g + 1]] (esc_selections)."""
-        which = np.zeros(self.G, np.int32)
-        off = np.zeros(self.G + 1, np.int64)
-        n = C.c_int64()
-        wp, op = which.ctypes.data_as(C.POINTER(C.c_int32)), off.ctypes.data_as(C.POINTER(C.c_int64))
-        L.check(self.lib.esc_selections(self.handle, wp, op, None, 0, C.byref(n)), "esc_selections")
-        idx = np.zeros(max(n.value, 1), np.int64)
-        L.check(self.lib.esc_selections(self.handle, wp, op, idx.ctypes.data_as(C.POINTER(C.c_int64)), len(idx),
-                                        C.byref(n)), "esc_selections")
-        return which, off, idx[:n.value]
-
     def close(self):
         if self.handle:
             self.lib.esc_synth_destroy(self.handle)
@@ -578,6 +560,24 @@ class Context:
         L.check(self.lib.esc_group_order(self.handle, group, which, out.ctypes.data_as(C.POINTER(C.c_int64)), m,
                                          C.byref(n)), "esc_group_order")
         return out[:m]
+
+    def set_selections(self, slack: int = 0, group_cap: int = 0):
+        """Deliver every decided group's taint / untaint nodes with the decision
+        (esc_set_selections; slack < 0 turns them off).  Needs the ordering in the step."""
+        L.check(self.lib.esc_set_selections(self.handle, int(slack), int(group_cap)), "esc_set_selections")
+
+    def selections(self):
+        """The last decision's selections: (which[G] (ESC_SEL_*), offsets[G + 1], nodes) —
+        group g's snapshot indices are nodes[offsets[g]:offsets[g + 1]] (esc_selections)."""
+        which = np.zeros(self.G, np.int32)
+        off = np.zeros(self.G + 1, np.int64)
+        n = C.c_int64()
+        wp, op = which.ctypes.data_as(C.POINTER(C.c_int32)), off.ctypes.data_as(C.POINTER(C.c_int64))
+        L.check(self.lib.esc_selections(self.handle, wp, op, None, 0, C.byref(n)), "esc_selections")
+        idx = np.zeros(max(n.value, 1), np.int64)
+        L.check(self.lib.esc_selections(self.handle, wp, op, idx.ctypes.data_as(C.POINTER(C.c_int64)), len(idx),
+                                        C.byref(n)), "esc_selections")
+        return which, off, idx[:n.value]
 
     def close(self):
         if self.handle:

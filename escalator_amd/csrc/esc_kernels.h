@@ -333,6 +333,10 @@ struct NodeDev {
     const uint32_t* e_flags;
     const int64_t*  e_cpu;
     const int64_t*  e_mem;
+    // the same entries as one 16-B record each (flags, cpu as u32, mem lo, mem hi) when every
+    // node's allocatable cpu is in [0, 2^32) (checked at load and by every node event; null
+    // otherwise): K2 streams one load per entry instead of three, 16 B instead of 20
+    const uint4*    e_pk;
     const uint32_t* e_node;    // snapshot index of the entry's node
     const uint32_t* piece_off; // [n_pieces + 1] entry offsets
     const uint32_t* piece_pair;// [n_pieces]
@@ -357,7 +361,10 @@ enum NodeRow : int {
     NR_K
 };
 constexpr int NODE_PIECE = 1024;
-constexpr int NODE_SPAN = 256;         // entries per K2 wave (whole pieces, <= 63 of them)
+#ifndef ESC_NODE_SPAN
+#define ESC_NODE_SPAN 256                  // (timing builds may override; the runtime builds the spans too)
+#endif
+constexpr int NODE_SPAN = ESC_NODE_SPAN;   // entries per K2 wave (whole pieces, <= 63 of them)
 constexpr int NR_CNT_BITS = 21;
 constexpr uint64_t NR_CNT_MASK = (uint64_t(1) << NR_CNT_BITS) - 1;
 
@@ -489,7 +496,7 @@ int64_t tail_span_blocks(const NodeDev& n);
 int64_t tail_trk_blocks(const NodeDev& n);
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
-                            const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                            const uint32_t* grp_off, const uint32_t* g_memb,
                             uint32_t* vals, int64_t* seg, uint32_t* sel_total, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
 // §8f rank 2: a loaded pod as seen by NodePodsRemaining, listed per node (runs in
@@ -546,17 +553,19 @@ hipError_t launch_patch(const PatchTargets& t, const uint64_t* where, const uint
 // (group, class) partition.
 size_t sort_hist_words(int64_t n);   // digit-histogram words one LSD pass over n keys needs
 struct OrdChunk {               // K5 per-decision chunk: memberships [start, end) of one group
-    uint32_t start, end, group, pad;
-};
+    uint32_t start, end, group, pad;   // a packed chunk: its first group, and pad = how many
+};                                     // groups [group, group + pad) it covers (<= ORD_GCAP)
 constexpr uint32_t ORD_CHUNK_DRY = 2u;   // OrdChunk::pad bit of a split chunk: its group is in dry mode
+constexpr uint32_t ORD_GCAP = 512;       // groups a packed chunk covers at most (empty ones included)
 #ifndef ESC_ORD_CHUNK
 #define ESC_ORD_CHUNK 4096         // (timing builds may override)
 #endif
 constexpr int ORD_CHUNK = ESC_ORD_CHUNK;   // memberships per K5 chunk (three-pass default)
-// Group-order padding slot of group g: g | MEMB_PAD (class 3, skipped).  Every group owns a
-// region of the group-order arrays: its memberships oldest first, then padding (the round-up
-// to whole 16-B quads and the spare slots node additions take).
-constexpr uint32_t MEMB_PAD = 0x80000000u;
+// Every group owns a region of the group-order arrays: its memberships oldest first, then
+// padding (the round-up to whole 16-B quads and the spare slots node additions take,
+// DESIGN.md §4) — MEMB_PAD_WORD, class 3 from the word alone.  The packed orderings find a
+// quad's group from the chunk's region starts (round 6: no group word per slot).
+constexpr uint32_t MEMB_PAD = 0x80000000u;   // (a group word's padding bit: ord_class)
 // A group region's membership word (g_memb, 4 B): node | the low four flag bits of the node
 // as the per-decision split reads them (UNSCHED, TAINTED, TRACKED resolved for the group,
 // ABSENT) << MEMB_FLAG_SHIFT — the age index's sort value, kept as is.  One 4-B word per
@@ -570,12 +579,12 @@ inline uint32_t memb_word(uint32_t node, uint32_t flags) { return node | ((flags
 // memberships (more, shorter blocks), then chunks of up to ORD_CHUNK.
 constexpr int ORD_PCHUNK = 1024;
 hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, int64_t n_small,
-                               const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                               const uint32_t* grp_off, const uint8_t* dry, const uint32_t* g_memb,
                                uint32_t* vals, int64_t* seg, hipStream_t st);
-// Fills the padding of every group's region (after its `len` memberships) with g | MEMB_PAD
+// Fills the padding of every group's region (after its `len` memberships) with MEMB_PAD_WORD
 // and sets the ordering's segment starts (seg[4g + k] = pstart[g], seg[4G] = pstart[G]).
-hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_grp,
-                             uint32_t* g_memb, int64_t* seg, hipStream_t st);
+hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_memb, int64_t* seg,
+                             hipStream_t st);
 // The age index (load time): memberships listed in one pass (per-tile counts, decoupled
 // look-back: status = memb_status_words(n) u64 words, zeroed by the launcher) with
 // (group << R | creation offset) keys and (node | flags) values, LSD-sorted, then written
@@ -586,8 +595,7 @@ struct RegionSink {
     const int64_t* seg;        // sorted start of group g's memberships (host-computed)
     const uint32_t* pstart;    // region start of group g
     const uint32_t* plen;      // memberships of group g
-    const uint8_t* dry;
-    uint32_t *g_memb, *g_grp;  // region words (MEMB_FLAG_SHIFT), group words
+    uint32_t* g_memb;          // region words (MEMB_FLAG_SHIFT)
     uint32_t* err;             // bit 0: a membership fell outside its group's count; bit 1: a
                                // coarse-key run too long for k_age_fix (rebuild exact)
     int32_t G;

@@ -791,6 +791,19 @@ __device__ __forceinline__ void node_span(const NodeDev& N, int64_t* __restrict_
     uint32_t f[U];
     int64_t c[U], m[U];
     auto load = [&](uint32_t base) {
+#ifndef ESC_K2_ARRAYS                                // (timing builds: the three arrays only)
+        if (N.e_pk) {                                // packed entries: one 16-B load each
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t i = base + u * 64 + lane, ii = i < z ? i : z - 1;
+                const uint4 v = ld4(reinterpret_cast<const uint32_t*>(N.e_pk + ii));
+                f[u] = v.x;
+                c[u] = (int64_t)v.y;
+                m[u] = (int64_t)((uint64_t)v.z | (uint64_t)v.w << 32);
+            }
+            return;
+        }
+#endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint32_t i = base + u * 64 + lane, ii = i < z ? i : z - 1;
@@ -1944,11 +1957,10 @@ struct RsElem<KT, NoVal> {
 };
 __device__ __forceinline__ void region_put(const RegionSink& S, uint32_t p, uint64_t key, uint32_t v) {
     const uint32_t g = (uint32_t)(key >> S.R);
+    if (g >= (uint32_t)S.G) { *S.err = 1u; return; }   // (keys of a listing that gave up)
     const int64_t r = (int64_t)p - S.seg[g];
-    if (g >= (uint32_t)S.G || r < 0 || r >= (int64_t)S.plen[g]) { *S.err = 1u; return; }
-    const int64_t d = (int64_t)S.pstart[g] + r;
-    S.g_memb[d] = v;
-    S.g_grp[d] = g | (S.dry[g] ? NODE_DRY_BIT : 0u);
+    if (r < 0 || r >= (int64_t)S.plen[g]) { *S.err = 1u; return; }
+    S.g_memb[(int64_t)S.pstart[g] + r] = v;
 }
 
 // FINAL (the age index's last pass): a key's sorted position goes straight into its group's
@@ -2156,20 +2168,27 @@ constexpr int AF_RUN = 8;
 // One run of equal coarse keys starting at sorted position i (len >= 2 members), put in
 // exact (creation time, node) order in its group's region.
 __device__ __forceinline__ void age_fix_run(const uint32_t* __restrict__ keys, int64_t n, const RegionSink& S,
-                                            const int64_t* __restrict__ created, int64_t ts_min, int64_t i, uint32_t k) {
+                                            const int64_t* __restrict__ created, int64_t n_nodes, int64_t ts_min,
+                                            int64_t i, uint32_t k) {
     int len = 2;
     while (len <= AF_RUN && i + len < n && keys[i + len] == k) ++len;
     if (len > AF_RUN) { atomicOr(S.err, 2u); return; }
     const uint32_t g = k >> S.R;
     if (g >= (uint32_t)S.G) { atomicOr(S.err, 1u); return; }
-    const int64_t d0 = (int64_t)S.pstart[g] + (i - S.seg[g]);
+    // the run lies inside its group's sorted range, and its words name table nodes — always,
+    // unless the keys are not the listing's (bit 0: the build fails; nothing is touched)
+    const int64_t r = i - S.seg[g];
+    if (r < 0 || r + len > (int64_t)S.plen[g]) { atomicOr(S.err, 1u); return; }
+    const int64_t d0 = (int64_t)S.pstart[g] + r;
     uint32_t w[AF_RUN];
     int64_t t[AF_RUN];
 #pragma unroll
-    for (int j = 0; j < AF_RUN; ++j) {
-        w[j] = j < len ? S.g_memb[d0 + j] : 0xFFFFFFFFu;
-        t[j] = j < len ? created[w[j] & MEMB_NODE_MASK] - ts_min : INT64_MAX;
-    }
+    for (int j = 0; j < AF_RUN; ++j) w[j] = j < len ? S.g_memb[d0 + j] : 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < AF_RUN; ++j)
+        if (j < len && (int64_t)(w[j] & MEMB_NODE_MASK) >= n_nodes) { atomicOr(S.err, 1u); return; }
+#pragma unroll
+    for (int j = 0; j < AF_RUN; ++j) t[j] = j < len ? created[w[j] & MEMB_NODE_MASK] - ts_min : INT64_MAX;
 #pragma unroll
     for (int a = 0; a < AF_RUN; ++a)                   // odd-even transposition: static indices only
 #pragma unroll
@@ -2190,7 +2209,8 @@ __device__ __forceinline__ void age_fix_run(const uint32_t* __restrict__ keys, i
 // previous one.  Runs are rare (config 5: a handful per 10^4 memberships), so the pass is
 // a streaming read of the keys; one thread per key (43 k blocks) took 39 µs for it.
 __global__ __launch_bounds__(256) void k_age_fix(const uint32_t* __restrict__ keys, int64_t n, RegionSink S,
-                                                 const int64_t* __restrict__ created, int64_t ts_min) {
+                                                 const int64_t* __restrict__ created, int64_t n_nodes, int64_t ts_min) {
+    if (*S.err & 1u) return;                             // the listing gave up: its keys are not memberships
     const int64_t nq = (n + 3) / 4;
     for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
         const int64_t i0 = 4 * q;
@@ -2207,7 +2227,7 @@ __global__ __launch_bounds__(256) void k_age_fix(const uint32_t* __restrict__ ke
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             if (i0 + j + 1 < n && k[1 + j] == k[2 + j] && k[j] != k[1 + j])
-                age_fix_run(keys, n, S, created, ts_min, i0 + j, k[1 + j]);
+                age_fix_run(keys, n, S, created, n_nodes, ts_min, i0 + j, k[1 + j]);
     }
 }
 
@@ -2610,13 +2630,17 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_split(NodeDev N, const OrdChu
 }
 
 // Small groups packed whole into one chunk (<= ORD_CHUNK memberships, regions start on
-// quads): one pass, no cross-chunk prefix.  Classes are counted by one packed 64-bit block
-// scan (class 0 | class 1 << 21 | class 2 << 42) in membership order; a group's base is the
-// scan value at its region's first quad (hp, indexed by quad), its class totals come from
-// its region's last quad, and the output of group g lies in its own region: class 0 forward
-// from its start, class 1 backward from its end (the split groups' layout, k_ord_split) —
-// the chunk's own slots, so the nodes are staged in LDS and the chunk written back
-// coalesced.  The last quad of each group writes its segment bounds.
+// quads): one pass, no cross-chunk prefix.  The chunk covers groups [ch.group, ch.group +
+// ch.pad) (empty ones included); their region starts and dry flags are read once into LDS
+// and every quad finds its group there by binary search (round 6: a group word per
+// membership, 4 B read per membership and a dependent region-start load per quad, went).
+// Classes are counted by one packed 64-bit block scan (class 0 | class 1 << 21 | class 2 <<
+// 42) in membership order; a group's base is the scan value at its region's first quad (hp,
+// indexed by quad), its class totals come from its region's last quad, and the output of
+// group g lies in its own region: class 0 forward from its start, class 1 backward from its
+// end (the split groups' layout, k_ord_split) — the chunk's own slots, so the nodes are
+// staged in LDS and the chunk written back coalesced.  The last quad of each group writes its
+// segment bounds.
 // Inclusive 64-bit scan over the wave with DPP (see wave_total64).
 __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long v) {
     v += dpp64<0x111, 0xF>(v);
@@ -2631,8 +2655,8 @@ __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long lon
 template <int STEPS>
 __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChunk* __restrict__ chunks,
                                                  const uint32_t* __restrict__ grp_off,
+                                                 const uint8_t* __restrict__ dry,
                                                  const uint32_t* __restrict__ g_memb,
-                                                 const uint32_t* __restrict__ g_grp,
                                                  uint32_t* __restrict__ vals, int64_t* __restrict__ seg, int64_t blk) {
     constexpr int CAP = STEPS * 4 * ORD_BLOCK;           // memberships per chunk
     constexpr int NQ = CAP / 4;
@@ -2641,29 +2665,47 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
     __shared__ unsigned long long wt[STEPS][ORD_WAVES];
     __shared__ unsigned long long hp[NQ];                // scan value at each group's first quad
     __shared__ uint32_t stage[CAP];
+    __shared__ uint32_t s_go[ORD_GCAP + 1];              // the chunk's groups' region starts (+ the end)
+    __shared__ uint8_t s_dry[ORD_GCAP];
     const OrdChunk ch = chunks[blk];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint4 nd[STEPS], gr[STEPS];                          // region words, group words
-    uint32_t grp[STEPS];
+    const uint32_t g0 = ch.group, ng = ch.pad;           // ng <= ORD_GCAP (the host's chunking)
+    uint4 nd[STEPS];                                     // region words
     bool ok[STEPS];
 #pragma unroll
     for (int st = 0; st < STEPS; ++st) {
         const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
         ok[st] = b < ch.end;
-        const uint32_t bb = ok[st] ? b : ch.start;
-        nd[st] = ld4(g_memb + bb);
-        gr[st] = ld4(g_grp + bb);
+        nd[st] = ld4(g_memb + (ok[st] ? b : ch.start));
+    }
+    for (uint32_t t = threadIdx.x; t <= ng; t += ORD_BLOCK) {
+        s_go[t] = grp_off[g0 + t];
+        if (t < ng) s_dry[t] = dry[g0 + t];
+    }
+    __syncthreads();
+    // a quad lies in one group's region: the last table group starting at or before it (an
+    // empty group shares its start with the next one, which is then the last)
+    uint32_t gt[STEPS], grp[STEPS];
+#pragma unroll
+    for (int st = 0; st < STEPS; ++st) {
+        const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
+        uint32_t lo = 0, hi = ng - 1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (s_go[mid] <= b) lo = mid; else hi = mid - 1;
+        }
+        gt[st] = lo;
+        grp[st] = (g0 + lo) | (s_dry[lo] ? NODE_DRY_BIT : 0u);
     }
     uint32_t cls[STEPS];
     unsigned long long ex[STEPS];
 #pragma unroll
     for (int st = 0; st < STEPS; ++st) {
-        grp[st] = gr[st].x;                              // a quad lies in one group's region
         unsigned long long v = 0;
         cls[st] = 0;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const uint32_t k = ok[st] ? ord_class(N, 0u, lane4(gr[st], j), lane4(nd[st], j) >> MEMB_FLAG_SHIFT) : 3u;
+            const uint32_t k = ok[st] ? ord_class(N, 0u, grp[st], lane4(nd[st], j) >> MEMB_FLAG_SHIFT) : 3u;
             cls[st] |= k << (8 * j);
             v += k == 0 ? 1ull : (k == 1 ? (1ull << C1) : (k == 2 ? (1ull << C2) : 0ull));
         }
@@ -2685,7 +2727,7 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
     for (int st = 0; st < STEPS; ++st) {
         ex[st] += pre[st];                               // exclusive scan value of this quad
         const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
-        if (ok[st] && b == grp_off[mg(grp[st])]) hp[(b - ch.start) >> 2] = ex[st];
+        if (ok[st] && b == s_go[gt[st]]) hp[(b - ch.start) >> 2] = ex[st];
     }
     __syncthreads();
     uint32_t hq[STEPS];
@@ -2694,8 +2736,8 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
         const uint32_t b = ch.start + st * 4 * ORD_BLOCK + 4 * threadIdx.x;
         if (!ok[st]) continue;
         const uint32_t g = mg(grp[st]);
-        hq[st] = (grp_off[g] - ch.start) >> 2;
-        const uint32_t end = grp_off[g + 1];
+        hq[st] = (s_go[gt[st]] - ch.start) >> 2;
+        const uint32_t end = s_go[gt[st] + 1];
         if (b + 4 == end) {                              // the group's last quad: totals + bounds
             unsigned long long inc = ex[st];
 #pragma unroll
@@ -2704,7 +2746,7 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
                 inc += k == 0 ? 1ull : (k == 1 ? (1ull << C1) : (k == 2 ? (1ull << C2) : 0ull));
             }
             const unsigned long long t = inc - hp[hq[st]];
-            const int64_t s0 = grp_off[g], t0 = (int64_t)(t & M), t1 = (int64_t)((t >> C1) & M);
+            const int64_t s0 = s_go[gt[st]], t0 = (int64_t)(t & M), t1 = (int64_t)((t >> C1) & M);
             seg[4 * (int64_t)g + 0] = s0;                // untainted forward from the start,
             seg[4 * (int64_t)g + 1] = s0 + t0;           // tainted newest first at the end
             seg[4 * (int64_t)g + 2] = (int64_t)end - t1;
@@ -2717,7 +2759,7 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
         if (!ok[st]) continue;
         const unsigned long long base = hp[hq[st]];
         const uint32_t s0 = (hq[st] << 2);               // the group's first slot, chunk-relative
-        const uint32_t e1 = grp_off[mg(grp[st]) + 1] - ch.start - 1;   // its last slot
+        const uint32_t e1 = s_go[gt[st] + 1] - ch.start - 1;           // its last slot
         uint32_t r0 = (uint32_t)((ex[st] - base) & M), r1 = (uint32_t)(((ex[st] - base) >> C1) & M);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -2735,10 +2777,10 @@ __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChun
 template <int STEPS>
 __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdChunk* __restrict__ chunks,
                                                           const uint32_t* __restrict__ grp_off,
+                                                          const uint8_t* __restrict__ dry,
                                                           const uint32_t* __restrict__ g_memb,
-                                                          const uint32_t* __restrict__ g_grp,
                                                           uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
-    ord_packed_block<STEPS>(N, chunks, grp_off, g_memb, g_grp, vals, seg, blockIdx.x);
+    ord_packed_block<STEPS>(N, chunks, grp_off, dry, g_memb, vals, seg, blockIdx.x);
 }
 
 // The step's tail in ONE launch (horizontal fusion; every role is 256 threads and none
@@ -2763,7 +2805,7 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
                                                    int64_t* __restrict__ rows, int64_t* __restrict__ trk_acc,
                                                    const OrdChunk* __restrict__ chunks, int64_t n_small,
                                                    const uint32_t* __restrict__ grp_off,
-                                                   const uint32_t* __restrict__ g_memb, const uint32_t* __restrict__ g_grp,
+                                                   const uint32_t* __restrict__ g_memb,
                                                    uint32_t* __restrict__ vals, int64_t* __restrict__ seg,
                                                    uint32_t* __restrict__ sel_total) {
     static_assert(FD_WAVES * 64 == 256 && K2_WAVES * 64 == 256 && ORD_BLOCK == 256, "one block size for every role");
@@ -2779,27 +2821,23 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
         const uint32_t col = (uint32_t)(b - n_piece_blk);
         if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)col);
     } else if (!(F.ablate & 32)) {
-        ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, g_memb, g_grp, vals, seg,
+        ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, G.dry, g_memb, vals, seg,
                                                        b - n_piece_blk - F.n_col);
     }
 }
 
-// Region padding: g | MEMB_PAD after each group's memberships (node 0, flagged absent:
-// class 3 from the region word alone, k_ord_split).
+// Region padding: MEMB_PAD_WORD after each group's memberships (node 0, flagged absent:
+// class 3 from the region word alone, k_ord_split and the packed orderings).
 __global__ __launch_bounds__(256) void k_region_pad(const uint32_t* __restrict__ pstart,
                                                     const uint32_t* __restrict__ plen, int32_t G,
-                                                    uint32_t* __restrict__ g_grp, uint32_t* __restrict__ g_memb,
-                                                    int64_t* __restrict__ seg) {
+                                                    uint32_t* __restrict__ g_memb, int64_t* __restrict__ seg) {
     const int32_t g = blockIdx.x;
     if (g >= G) return;
     // the ordering's segment starts (the sort's last pass read seg as the unpadded starts):
     // all four of the group's at its region start
     if (threadIdx.x < 4) seg[4 * (int64_t)g + threadIdx.x] = pstart[g];
     if (g == 0 && threadIdx.x == 4) seg[4 * (int64_t)G] = pstart[G];
-    for (uint32_t i = pstart[g] + plen[g] + threadIdx.x; i < pstart[g + 1]; i += blockDim.x) {
-        g_grp[i] = (uint32_t)g | MEMB_PAD;
-        g_memb[i] = MEMB_PAD_WORD;
-    }
+    for (uint32_t i = pstart[g] + plen[g] + threadIdx.x; i < pstart[g + 1]; i += blockDim.x) g_memb[i] = MEMB_PAD_WORD;
 }
 
 // Start of each (group, class) segment in the partitioned keys: seg[s] = first key >= s.
@@ -3055,14 +3093,14 @@ int64_t tail_trk_blocks(const NodeDev& n) { return (n.n_trk + K2_WAVES * 64 - 1)
 
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
-                            const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                            const uint32_t* grp_off, const uint32_t* g_memb,
                             uint32_t* vals, int64_t* seg, uint32_t* sel_total, hipStream_t st) {
     const int64_t nb = spans ? tail_span_blocks(n) : 0;      // else K1 made the rows
     const int64_t nt = tail_trk_blocks(n);
     const int64_t grid = f.n_col + nb + nt + std::max<int64_t>(n_small, 0);
     if (grid <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_step_tail, dim3((unsigned)grid), dim3(256), 0, st, g, n, f, wide_pod, pwords, nb, nb + nt, rows,
-                       trk_acc, chunks, std::max<int64_t>(n_small, 0), grp_off, g_memb, g_grp, vals, seg, sel_total);
+                       trk_acc, chunks, std::max<int64_t>(n_small, 0), grp_off, g_memb, vals, seg, sel_total);
     return hipGetLastError();
 }
 
@@ -3199,29 +3237,29 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, uint64_t* statu
         if (e != hipSuccess) return e;
         if (S.fix)                                   // the final pass's coarse keys (u32) in keys[src]
             hipLaunchKernelGGL(k_age_fix, dim3((unsigned)std::min<int64_t>(4096, (n_memb + 1023) / 1024)), dim3(256), 0, st,
-                               reinterpret_cast<const uint32_t*>(keys[src]), n_memb, S, nd.created, ts_min);
+                               reinterpret_cast<const uint32_t*>(keys[src]), n_memb, S, nd.created, nd.hi, ts_min);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_t n_chunks, int64_t n_small,
-                               const uint32_t* grp_off, const uint32_t* g_memb, const uint32_t* g_grp,
+                               const uint32_t* grp_off, const uint8_t* dry, const uint32_t* g_memb,
                                uint32_t* vals, int64_t* seg, hipStream_t st) {
     if (n_chunks <= 0) return hipSuccess;
     // chunks [0, n_small) hold <= ORD_PCHUNK memberships, the rest <= ORD_CHUNK
     if (n_small > 0)
         hipLaunchKernelGGL(k_ord_packed<ORD_PCHUNK / (4 * ORD_BLOCK)>, dim3((unsigned)n_small), dim3(ORD_BLOCK), 0, st,
-                           nd, chunks, grp_off, g_memb, g_grp, vals, seg);
+                           nd, chunks, grp_off, dry, g_memb, vals, seg);
     if (n_chunks > n_small)
         hipLaunchKernelGGL(k_ord_packed<ORD_CHUNK / (4 * ORD_BLOCK)>, dim3((unsigned)(n_chunks - n_small)),
-                           dim3(ORD_BLOCK), 0, st, nd, chunks + n_small, grp_off, g_memb, g_grp, vals, seg);
+                           dim3(ORD_BLOCK), 0, st, nd, chunks + n_small, grp_off, dry, g_memb, vals, seg);
     return hipGetLastError();
 }
 
-hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_grp,
-                             uint32_t* g_memb, int64_t* seg, hipStream_t st) {
+hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_memb, int64_t* seg,
+                             hipStream_t st) {
     if (G <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_region_pad, dim3((unsigned)G), dim3(256), 0, st, pstart, plen, G, g_grp, g_memb, seg);
+    hipLaunchKernelGGL(k_region_pad, dim3((unsigned)G), dim3(256), 0, st, pstart, plen, G, g_memb, seg);
     return hipGetLastError();
 }
 

@@ -82,13 +82,14 @@ struct NodeBuf {
     uint32_t* span_off = nullptr;                // K2 waves' piece ranges
     uint32_t* span_e = nullptr;                  // and their entry ranges
     int64_t *e_cpu = nullptr, *e_mem = nullptr, *rows = nullptr;
+    uint4* e_pk = nullptr;                       // the entries packed 16 B each (NodeDev::e_pk)
     GroupNode* gnode = nullptr;
     void release() {
         dfree(gnode);
         dfree(flags); dfree(label0); dfree(xl); dfree(xl_off); dfree(trk_start); dfree(cpu); dfree(mem);
         dfree(created); dfree(trk_node); dfree(trk_group);
         dfree(e_flags); dfree(e_node); dfree(piece_off); dfree(piece_pair); dfree(pp_off); dfree(span_off); dfree(span_e);
-        dfree(e_cpu); dfree(e_mem); dfree(rows);
+        dfree(e_cpu); dfree(e_mem); dfree(rows); dfree(e_pk);
     }
 };
 
@@ -168,6 +169,9 @@ struct esc_ctx {
     int64_t n_entries = 0, n_pieces = 0, pc_lo = 0, pc_hi = 0, node_bytes = 0, n_spans = 0;
     int64_t ts_min = 0, ts_max = 0;
     bool nodes_loaded = false;
+    // every node's allocatable cpu is in [0, 2^32): K2 reads the packed 16-B entries (node
+    // events that break it switch K2 back to the three entry arrays, dropping the graphs)
+    bool e_pk_ok = false;
     uint32_t q_lo = 0, q_hi = 0;                              // the group pairs this rank owns (§7)
     std::vector<uint32_t> q_bounds;                           // every rank's first owned pair, + n_gp
     std::vector<int64_t> pair_live;                           // group pair -> live node entries
@@ -253,13 +257,14 @@ struct esc_ctx {
     uint32_t* d_mvals[2] = {nullptr, nullptr};               //              (node | flags << 28)
     int64_t mcap = 0;                                         // their capacity (memberships)
     bool age_built = false;
+    bool age_ok = false;                                      // the last build succeeded (its regions are valid)
     uint32_t *d_hist = nullptr, *d_tot = nullptr, *d_total = nullptr, *d_ierr = nullptr;
     uint64_t* d_lstat = nullptr;                              // single-pass listing status words
     int64_t* d_seg = nullptr;
     int64_t n_memb = 0;
     int order_src = 0;
     // group order of the memberships (per-decision 3-way split by class inside each group)
-    uint32_t *d_g_memb = nullptr, *d_g_grp = nullptr;   // K5 regions: membership words, group words
+    uint32_t* d_g_memb = nullptr;                             // K5 regions: membership words
     uint32_t *d_grp_off = nullptr, *d_gch_off = nullptr;
     uint64_t* d_ostat = nullptr;                              // k_ord_split status words (x2)
     int ord_parity = 0;                                       // which status array the next ordering uses
@@ -424,6 +429,9 @@ int pod_class_id(uint32_t f, uint32_t cpu0, int64_t mem0, uint32_t pair0, const 
     return sig | (n_gp < KP8_PAIR_NONE && kp8_fits(cpu0, mem0) ? 2 : 1) * POD_SIG_IDS;
 }
 
+// A node's allocatable cpu fits K2's packed entry (NodeDev::e_pk).
+bool entry_cpu_packs(int64_t cpu) { return cpu >= 0 && cpu <= (int64_t)0xFFFFFFFF; }
+
 // K1 partial row stride: the pod slots (one per group pair + the default filter's)
 // rounded up to whole K3 columns.
 int64_t slot_stride(const esc_ctx* c) { return ((int64_t)c->gi.n_gp + 1 + FC_COL - 1) / FC_COL * FC_COL; }
@@ -482,6 +490,7 @@ NodeDev node_dev(const esc_ctx* c) {
     n.n_trk = c->n_trk;
     n.lo = c->node_lo; n.hi = c->node_hi;
     n.e_flags = c->nodes.e_flags; n.e_cpu = c->nodes.e_cpu; n.e_mem = c->nodes.e_mem; n.e_node = c->nodes.e_node;
+    n.e_pk = c->e_pk_ok ? c->nodes.e_pk : nullptr;
     n.piece_off = c->nodes.piece_off; n.piece_pair = c->nodes.piece_pair; n.pp_off = c->nodes.pp_off;
     n.n_pieces = c->n_pieces; n.pc_lo = c->pc_lo; n.pc_hi = c->pc_hi;
     n.span_off = c->nodes.span_off; n.span_e = c->nodes.span_e; n.n_spans = c->n_spans;
@@ -562,7 +571,7 @@ hipError_t enqueue_order(esc_ctx* c, hipStream_t st) {
     c->ord_parity ^= 1;
     c->ord_failed = false;
     if (e != hipSuccess) return e;
-    return launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_g_memb, c->d_g_grp,
+    return launch_order_packed(node_dev(c), c->d_pchunks, c->n_pchunks, c->n_psmall, c->d_grp_off, c->d_dry, c->d_g_memb,
                                c->d_ord, c->d_seg, st);
 }
 
@@ -632,7 +641,7 @@ void release_sort(esc_ctx* c) {
     for (int i = 0; i < 2; ++i) { dfree(c->d_mkeys[i]); dfree(c->d_mvals[i]); }
     c->mcap = 0;
     c->age_built = false;
-    dfree(c->d_g_memb); dfree(c->d_g_grp);
+    dfree(c->d_g_memb);
     dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ostat); dfree(c->d_chunks);
     dfree(c->d_pstart); dfree(c->d_plen); dfree(c->d_ord); dfree(c->d_pchunks);
     c->n_pchunks = 0;
@@ -656,6 +665,9 @@ int32_t build_age_index(esc_ctx* c) {
     const int64_t nl = c->node_hi - c->node_lo;
     if (c->age_built && c->age_n != nl) release_sort(c);   // the range grew (esc_nodes_add)
     const bool fresh = !c->age_built;
+    // until this build succeeds the regions are not an ordering's input: orderings, steps with
+    // the ordering inside and region patches are refused (ESC_E_STATE) or skipped
+    c->age_ok = false;
     if (fresh) {
         c->age_n = nl;
         c->age_exact = false;
@@ -730,13 +742,15 @@ int32_t build_age_index(esc_ctx* c) {
     // prefix across the group); smaller groups are packed whole, several per chunk,
     // and ordered in one pass (k_ord_packed)
     std::vector<OrdChunk> chunks, pchunks, pbig;
-    uint32_t pk_lo = 0, pk_hi = 0, qk_lo = 0, qk_hi = 0;
+    // a packed chunk covers the groups [g0, g1] (the empty ones between included: the kernel
+    // finds a quad's group in that table, <= ORD_GCAP of them)
+    uint32_t pk_lo = 0, pk_hi = 0, qk_lo = 0, qk_hi = 0, pk_g0 = 0, pk_g1 = 0, qk_g0 = 0, qk_g1 = 0;
     auto flush_small = [&]() {
-        if (pk_hi > pk_lo) pchunks.push_back({pk_lo, pk_hi, NONE, 1u});
+        if (pk_hi > pk_lo) pchunks.push_back({pk_lo, pk_hi, pk_g0, pk_g1 - pk_g0 + 1});
         pk_lo = pk_hi;
     };
     auto flush_mid = [&]() {
-        if (qk_hi > qk_lo) pbig.push_back({qk_lo, qk_hi, NONE, 1u});
+        if (qk_hi > qk_lo) pbig.push_back({qk_lo, qk_hi, qk_g0, qk_g1 - qk_g0 + 1});
         qk_lo = qk_hi;
     };
     for (int32_t q = 0; q < g.G; ++q) {
@@ -754,15 +768,23 @@ int32_t build_age_index(esc_ctx* c) {
         }
         if (reg > (uint32_t)ORD_PCHUNK) {          // mid-size: packed up to ORD_CHUNK
             flush_small();
-            if (qk_hi - qk_lo + reg > (uint32_t)ORD_CHUNK || qk_hi != pstart[q]) flush_mid();
-            if (qk_hi == qk_lo) qk_lo = qk_hi = pstart[q];
+            if (qk_hi - qk_lo + reg > (uint32_t)ORD_CHUNK || qk_hi != pstart[q] ||
+                (qk_hi > qk_lo && (uint32_t)q - qk_g0 + 1 > ORD_GCAP))
+                flush_mid();
+            if (qk_hi == qk_lo) { qk_lo = qk_hi = pstart[q]; qk_g0 = (uint32_t)q; }
             qk_hi = pstart[q + 1];
+            qk_g1 = (uint32_t)q;
             pk_lo = pk_hi = pstart[q + 1];
             continue;
         }
-        if (pk_hi - pk_lo + reg > (uint32_t)ORD_PCHUNK || pk_hi != pstart[q]) flush_small();
-        if (pk_hi == pk_lo) pk_lo = pk_hi = pstart[q];
+        flush_mid();                               // a pending mid-size chunk ends here (it was
+                                                   // dropped before round 6: test_packed_chunk_mix)
+        if (pk_hi - pk_lo + reg > (uint32_t)ORD_PCHUNK || pk_hi != pstart[q] ||
+            (pk_hi > pk_lo && (uint32_t)q - pk_g0 + 1 > ORD_GCAP))
+            flush_small();
+        if (pk_hi == pk_lo) { pk_lo = pk_hi = pstart[q]; pk_g0 = (uint32_t)q; }
         pk_hi = pstart[q + 1];
+        pk_g1 = (uint32_t)q;
         qk_lo = qk_hi = pstart[q + 1];
     }
     flush_small();
@@ -773,8 +795,8 @@ int32_t build_age_index(esc_ctx* c) {
     const int64_t npad = pstart[g.G];
     if (fresh || npad != c->n_gpad) {
         drop_graphs(c);                                 // captured steps hold the old regions
-        dfree(c->d_g_memb); dfree(c->d_g_grp); dfree(c->d_ord);
-        HIP_TRY(dalloc(&c->d_g_memb, npad)); HIP_TRY(dalloc(&c->d_g_grp, npad)); HIP_TRY(dalloc(&c->d_ord, npad));
+        dfree(c->d_g_memb); dfree(c->d_ord);
+        HIP_TRY(dalloc(&c->d_g_memb, npad)); HIP_TRY(dalloc(&c->d_ord, npad));
     }
     c->n_gpad = npad;
     // no clearing: the sort's last pass fills every group's [start, start + len), k_region_pad the
@@ -834,11 +856,11 @@ int32_t build_age_index(esc_ctx* c) {
         const int cshift = coarse ? std::max(0, c->sort_R - (32 - gbits)) : -1;
         HIP_TRY(hipMemcpyAsync(c->d_seg, c->h_istage + ups[0].at, ups[0].bytes, hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemsetAsync(c->d_ierr, 0, 4, st));
-        RegionSink sink{c->d_seg, c->d_pstart, c->d_plen, c->d_dry, c->d_g_memb, c->d_g_grp, c->d_ierr,
+        RegionSink sink{c->d_seg, c->d_pstart, c->d_plen, c->d_g_memb, c->d_ierr,
                         g.G, coarse ? 32 - gbits : c->sort_R, cshift > 0 ? 1 : 0, lb_spins(c->lb_fail_list)};
         HIP_TRY(launch_age_sort(n, g, c->d_lstat, c->d_total, c->n_memb, c->mcap, c->ts_min, c->sort_div, c->sort_R,
                                 gbits, cshift, c->d_mkeys, c->d_mvals, c->d_hist, c->d_tot, sink, st));
-        HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_grp, c->d_g_memb, c->d_seg, st));
+        HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_memb, c->d_seg, st));
         // the error word (the listing's bounded look-back, region counts, the run fix-up) and
         // the listed total, read at the build's one wait
         h_err[0] = 0;
@@ -858,6 +880,7 @@ int32_t build_age_index(esc_ctx* c) {
     c->h_pcap.swap(pcap);
     c->h_gch_off.swap(gch_off);
     c->sorted = false;
+    c->age_ok = true;
     return ESC_OK;
 }
 
@@ -1268,7 +1291,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     f.ablate = c->k3_ablate;
     const bool ord = c->order_in_step;
     HIP_TRY(launch_step_tail(g, n, f, true, c->d_wide_pod, c->d_pwords, c->nodes.rows, c->d_trk_acc, c->d_pchunks,
-                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg,
+                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_ord, c->d_seg,
                              c->d_sel_total, st));
     if (int32_t rc = mark()) return rc;
     if (ord) {                                       // split groups, mid-size packed chunks
@@ -1277,7 +1300,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
         c->ord_parity ^= 1;
         c->ord_failed = false;
         HIP_TRY(launch_order_packed(n, c->d_pchunks + c->n_psmall, c->n_pchunks - c->n_psmall, 0, c->d_grp_off,
-                                    c->d_g_memb, c->d_g_grp, c->d_ord, c->d_seg, st));
+                                    c->d_dry, c->d_g_memb, c->d_ord, c->d_seg, st));
     }
     if (int32_t rc = mark()) return rc;
     // D reads and resets the tracker sums the tail accumulated (once per step), for this
@@ -1309,6 +1332,7 @@ int32_t check_ready(esc_ctx* c, bool fit = true) {
     // caller-bound buffer sized before it may be too small, so nothing runs on it until the
     // caller binds one of the new size
     if (fit && c->bound_pwords && xw_count(c) > c->bound_words) return ESC_E_STATE;
+    if (c->order_in_step && !c->age_ok) return ESC_E_STATE;   // the age index build failed: rebuild
     return ESC_OK;
 }
 
@@ -1935,10 +1959,15 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     uint32_t q_lo = 0, q_hi = n_gp;
     owned_pairs(pair_cnt, c->world, c->rank, q_lo, q_hi);
     const int64_t pc_lo = pp_off[q_lo], pc_hi = pp_off[q_hi];
-    int64_t node_bytes = 0;                          // algorithmic bytes K2 streams per decision
+    bool pk_ok = true;                               // K2's packed entries (NodeDev::e_pk)
+    for (int64_t i = 0; i < n && pk_ok; ++i) pk_ok = entry_cpu_packs(s->cpu[i]);
+    // algorithmic bytes K2 streams per decision: per piece its pair and offset, per entry 16 B
+    // packed (flags, cpu, memory in one record) or 20 B (the three arrays)
+    const int64_t per_entry = pk_ok ? 16 : 20;
+    int64_t node_bytes = 0;
     for (int64_t p = pc_lo; p < pc_hi; ++p) {
         node_bytes += 8;                             // piece_pair + piece_off
-        if (piece_pair[p] < n_gp) node_bytes += 24 * (int64_t)(piece_off[p + 1] - piece_off[p]);
+        if (piece_pair[p] < n_gp) node_bytes += per_entry * (int64_t)(piece_off[p + 1] - piece_off[p]);
     }
     // K2 spans: consecutive whole pieces of the group pairs (a prefix: pieces are pair-sorted
     // and ids >= n_gp come last), <= NODE_SPAN entries (or one larger piece) and <= 63
@@ -2003,6 +2032,15 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     HIP_TRY(hipMemcpy(b.e_node, e_node.data(), e_node.size() * 4, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(b.e_cpu, e_cpu.data(), e_cpu.size() * 8, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(b.e_mem, e_mem.data(), e_mem.size() * 8, hipMemcpyHostToDevice));
+    {   // the packed copy K2 reads (kept current by entry_patch even when not in use)
+        std::vector<uint4> pk(e_flags.size());
+        for (size_t k = 0; k < pk.size(); ++k)
+            pk[k] = make_uint4(e_flags[k], (uint32_t)e_cpu[k], (uint32_t)(uint64_t)e_mem[k],
+                               (uint32_t)((uint64_t)e_mem[k] >> 32));
+        HIP_TRY(dalloc(&b.e_pk, pk.size()));
+        HIP_TRY(hipMemcpy(b.e_pk, pk.data(), pk.size() * sizeof(uint4), hipMemcpyHostToDevice));
+    }
+    c->e_pk_ok = pk_ok;
     HIP_TRY(dalloc(&b.piece_off, piece_off.size())); HIP_TRY(dalloc(&b.piece_pair, std::max<size_t>(piece_pair.size(), 1)));
     HIP_TRY(dalloc(&b.pp_off, pp_off.size()));
     HIP_TRY(hipMemcpy(b.piece_off, piece_off.data(), piece_off.size() * 4, hipMemcpyHostToDevice));
@@ -3099,7 +3137,22 @@ int64_t region_pos(const esc_ctx* c, uint32_t g, uint32_t j) {
 }
 
 enum : uint32_t { NT_FLAGS = 0, NT_EFLAGS = 1, NT_LABEL0 = 2, NT_XLOFF = 3, NT_ENODE = 4, NT_XL = 5, NT_CPU = 6,
-                  NT_MEM = 7, NT_ECPU = 8, NT_EMEM = 9, NT_CREATED = 10 };
+                  NT_MEM = 7, NT_ECPU = 8, NT_EMEM = 9, NT_CREATED = 10, NT_EPK = 11 };
+
+// Pair-major entry e's flags, cpu and memory: the three arrays and the packed record (as two
+// 8-B words: flags | cpu << 32, memory).  A cpu the record cannot hold switches K2 to the
+// arrays for the rest of the snapshot (the captured steps hold the packed pointer).
+void entry_patch(esc_ctx* c, Patches& P, uint32_t e, uint32_t f, int64_t cpu, int64_t mem) {
+    P.add(NT_EFLAGS, e, f);
+    P.add(NT_ECPU, e, (uint64_t)cpu);
+    P.add(NT_EMEM, e, (uint64_t)mem);
+    P.add(NT_EPK, 2 * (int64_t)e, (uint64_t)f | (uint64_t)(uint32_t)cpu << 32);
+    P.add(NT_EPK, 2 * (int64_t)e + 1, (uint64_t)mem);
+    if (c->e_pk_ok && !entry_cpu_packs(cpu) && !(f & ESC_NF_ABSENT)) {
+        c->e_pk_ok = false;
+        drop_graphs(c);
+    }
+}
 
 PatchTargets node_targets(esc_ctx* c) {
     PatchTargets t{};
@@ -3107,6 +3160,7 @@ PatchTargets node_targets(esc_ctx* c) {
     t.u32[NT_XLOFF] = c->nodes.xl_off; t.u32[NT_ENODE] = c->nodes.e_node; t.u32[NT_XL] = c->nodes.xl;
     t.i64[NT_CPU - 6] = c->nodes.cpu; t.i64[NT_MEM - 6] = c->nodes.mem;
     t.i64[NT_ECPU - 6] = c->nodes.e_cpu; t.i64[NT_EMEM - 6] = c->nodes.e_mem;
+    t.i64[NT_EPK - 6] = reinterpret_cast<int64_t*>(c->nodes.e_pk);
     t.i64[NT_CREATED - 6] = c->nodes.created;
     return t;
 }
@@ -3157,10 +3211,10 @@ void pair_first(const esc_ctx* c, uint32_t q, GroupNode& x) {
     }
 }
 
-// Patch targets of the K5 regions: membership word (node | flags), group word.
+// Patch targets of the K5 regions: membership word (node | flags).
 PatchTargets region_targets(esc_ctx* c) {
     PatchTargets t{};
-    t.u32[0] = c->d_g_memb; t.u32[1] = c->d_g_grp;
+    t.u32[0] = c->d_g_memb;
     return t;
 }
 
@@ -3189,14 +3243,13 @@ void regions_insert(esc_ctx* c, std::unordered_map<uint32_t, std::vector<uint32_
             const int64_t pos = (int64_t)a + from + (int64_t)k;
             R.add(0, pos, memb_word(merged[k], (c->h_nflags[merged[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT
                                                                                        : memb_flags(c, merged[k], mbit)));
-            R.add(1, pos, mbit);
         }
     }
 }
 
 // Node events, K5 regions: take node j's membership out of group g's region (owned by this
 // rank; found by the node's CURRENT creation time): the region's tail moves up one slot and
-// its last slot becomes padding (g | MEMB_PAD, absent), as k_region_pad writes it.
+// its last slot becomes padding (MEMB_PAD_WORD, absent), as k_region_pad writes it.
 bool region_remove(esc_ctx* c, uint32_t g, uint32_t j, Patches& R) {
     const int64_t pos = region_pos(c, g, j);
     if (pos < 0) return false;
@@ -3207,11 +3260,9 @@ bool region_remove(esc_ctx* c, uint32_t g, uint32_t j, Patches& R) {
     for (int64_t k = pos; k < last; ++k) {
         gn[k] = gn[k + 1];
         R.add(0, k, memb_word(gn[k], (c->h_nflags[gn[k]] & ESC_NF_ABSENT) ? ESC_NF_ABSENT : memb_flags(c, gn[k], mbit)));
-        R.add(1, k, mbit);
     }
     gn[last] = 0;
     R.add(0, last, MEMB_PAD_WORD);
-    R.add(1, last, (uint32_t)g | MEMB_PAD);
     c->h_plen[g] = len - 1;
     return true;
 }
@@ -3231,9 +3282,7 @@ int32_t patch_nodes(esc_ctx* c, const std::vector<int64_t>& ids) {
         P.add(NT_MEM, j, mem);
         for (uint32_t e = c->ne_off[j]; e < c->ne_off[j + 1]; ++e) {
             if (c->h_e_node[c->ne_pos[e]] != (uint32_t)j) continue;   // an entry a relabel retired
-            P.add(NT_EFLAGS, c->ne_pos[e], f);
-            P.add(NT_ECPU, c->ne_pos[e], cpu);
-            P.add(NT_EMEM, c->ne_pos[e], mem);
+            entry_patch(c, P, c->ne_pos[e], f, (int64_t)cpu, (int64_t)mem);
         }
     }
     for (GroupNode& g : c->h_gnode)                  // allNodes[0]'s allocatable (controller.go:208)
@@ -3672,7 +3721,7 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
     // K5 regions: every rank checks the capacity of every group the batch touches (the host
     // knows them all), so that all ranks accept or refuse alike; it inserts into the regions
     // of the groups it owns
-    const bool k5 = c->age_built && !c->h_pcap.empty();
+    const bool k5 = c->age_built && c->age_ok && !c->h_pcap.empty();
     if (k5 && c->n_gpad > 0) {
         int32_t rc = ensure_gn(c);
         if (rc) return rc;
@@ -3722,10 +3771,8 @@ int32_t esc_nodes_add(esc_ctx* c, const esc_node_soa* s, int64_t* ids_out) {
             for (uint32_t q : pairs) {
                 const uint32_t e = c->pair_next[q]++;
                 ++c->pair_live[q];
-                P.add(NT_EFLAGS, e, f);
+                entry_patch(c, P, e, f, s->cpu[i], s->mem[i]);
                 P.add(NT_ENODE, e, (uint32_t)j);
-                P.add(NT_ECPU, e, (uint64_t)s->cpu[i]);
-                P.add(NT_EMEM, e, (uint64_t)s->mem[i]);
                 c->h_e_node[e] = (uint32_t)j;
                 c->ne_pos.push_back(e);
                 const uint32_t code = c->gi.node_code[q];
@@ -3935,7 +3982,7 @@ int32_t relabel_plan(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, Rela
     if (c->xl_used + (int64_t)xl_grow > c->xl_cap) return ESC_E_LIMIT;
     for (const auto& kv : need_e)
         if ((int64_t)c->pair_next[kv.first] + kv.second > (int64_t)c->pair_end[kv.first]) return ESC_E_LIMIT;
-    if (c->age_built && !c->h_pcap.empty())
+    if (c->age_built && c->age_ok && !c->h_pcap.empty())
         for (const auto& kv : need_r)
             if ((int64_t)c->h_plen[kv.first] + kv.second > (int64_t)c->h_pcap[kv.first]) return ESC_E_LIMIT;
     return ESC_OK;
@@ -3961,7 +4008,7 @@ int32_t relabel_apply(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, con
         if (int32_t rc = occ_delta(c, opos, onode, -1)) return rc;
     }
     // K5: memberships leave their regions while the creation times are the old ones
-    const bool k5 = c->age_built && !c->h_pcap.empty();
+    const bool k5 = c->age_built && c->age_ok && !c->h_pcap.empty();
     Patches R;
     if (k5) {
         if (c->n_gpad > 0)
@@ -3992,7 +4039,7 @@ int32_t relabel_apply(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, con
             const uint32_t q = entry_pair(c, e);
             if (q != NONE && std::binary_search(nq.begin(), nq.end(), q)) { keep.push_back(e); continue; }
             c->h_e_node[e] = NONE;                                        // retired: absent, no node
-            P.add(NT_EFLAGS, e, ESC_NF_ABSENT);
+            entry_patch(c, P, e, ESC_NF_ABSENT, 0, 0);
             P.add(NT_ENODE, e, NONE);
             dead.push_back(e);
             if (q != NONE) { --c->pair_live[q]; pair_touched[q] = 1; }
@@ -4048,7 +4095,7 @@ int32_t relabel_apply(esc_ctx* c, const int64_t* ids, const esc_node_soa* s, con
         P.add(NT_LABEL0, j, s->label0[i]);
         P.add(NT_XLOFF, j, c->h_xl_off[j]);
         P.add(NT_CREATED, j, (uint64_t)s->created_ns[i]);
-        if (u.moved[i] && c->age_built &&
+        if (u.moved[i] && c->age_built && c->age_ok &&
             (s->created_ns[i] < c->ts_min || s->created_ns[i] > c->ts_max ||
              (uint64_t)(s->created_ns[i] - c->ts_min) % c->sort_div != 0))
             c->age_n = -1;                          // outside the index's key range: the next build is fresh
@@ -4453,7 +4500,7 @@ int32_t esc_sort_nodes(esc_ctx* c) {
     if (c && c->multi) return esc::multi_each(c, [](esc_ctx* x, int32_t) { return esc_sort_nodes(x); }, 0);
     if (!c) return ESC_E_INVAL;
     if (!c->has_device) return ESC_E_NODEV;
-    if (!c->nodes_loaded) return ESC_E_STATE;
+    if (!c->nodes_loaded || !c->age_ok) return ESC_E_STATE;
     hipSetDevice(c->device);
     HIP_TRY(enqueue_order(c, c->stream));
     c->order_src = 0;

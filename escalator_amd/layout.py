@@ -8,8 +8,9 @@ pairs; all other pods sit in homogeneous 256-pod K tiles that need no offsets). 
 whose values fit the packed block (``packed_mask``) takes 12 B (pair0 | flags 4, cpu0 | mem0
 8) and 8 B per record; one that also fits the packed small block (``small_mask``) 8 B
 (cpu0 | mem0 | pair0 | flags in one u64), 8 B per record and 2 B per extra pair.
-K2 reads the node index once per decision: 24 B per (label pair, node) entry of a pair
-some group selects (flags 4 + cpu 8 + mem 8 + node 4) and 8 B per piece (offset + pair).
+K2 reads the node index once per decision: per (label pair, node) entry of a pair some group
+selects 16 B when every node's allocatable cpu is in [0, 2^32) (one packed record: flags 4 +
+cpu 4 + mem 8), else 20 B (flags 4 + cpu 8 + mem 8), and 8 B per piece (offset + pair).
 With several ranks each reads the pieces of the group pairs it owns (``owner_ranges``:
 contiguous pair ranges balanced by entry count).
 """
@@ -159,7 +160,11 @@ def node_bytes(nodes: dict, n_gp: int, rank: int = 0, world: int = 1) -> int:
     p_pair = q[p_start]
     b = owner_ranges(nodes, n_gp, world)
     mine = (p_pair >= b[rank]) & (p_pair < b[rank + 1])
-    return int(8 * int(mine.sum()) + 24 * int(p_len[mine].sum()))
+    # K2 reads 16 B per entry when every node's cpu fits the packed record (flags, cpu as u32,
+    # memory), else the three arrays' 20 B (esc_runtime.hip esc_load_nodes)
+    cpu = np.asarray(nodes["cpu"], np.int64)
+    per_entry = 16 if bool(((cpu >= 0) & (cpu <= 0xFFFFFFFF)).all()) else 20
+    return int(8 * int(mine.sum()) + per_entry * int(p_len[mine].sum()))
 
 
 def baseline_md_pod_bytes(pods: dict) -> int:

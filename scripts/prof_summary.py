@@ -30,6 +30,7 @@ import statistics
 
 PEAK_GBS = 8000.0
 ORDER_KERNELS = ("k_ord_split", "k_ord_packed")
+STEP_KERNELS = ("k_pod_reduce", "k_pod_bigtiles", "k_step_tail", "k_ord_split", "k_ord_packed", "k_node_groups")
 
 
 def ours(k):
@@ -110,6 +111,17 @@ def main():
         if res["order"]["traffic_bytes"]:
             res["order"]["traffic_over_algorithmic"] = res["order"]["traffic_bytes"] / algo
         b = None
+    if b and b.get("step_bytes"):
+        # the whole decision step: every kernel one step launches, its PMC bytes against the
+        # bench line's algorithmic bytes of the step (K1 pods + K2 node entries + orderings)
+        ks = [k for k in STEP_KERNELS if k in res["kernels"]]
+        hb = [res["kernels"][k].get("hbm_bytes") for k in ks]
+        algo = b["step_bytes"]["total"]
+        res["step"] = {"kernels": ks, "rocprof_ns": sum(res["kernels"][k]["mean_ns"] for k in ks),
+                       "algorithmic_bytes": algo, "bench_ms_per_step": b["ms_per_step"],
+                       "traffic_bytes": sum(hb) if hb and all(x is not None for x in hb) else None}
+        if res["step"]["traffic_bytes"]:
+            res["step"]["traffic_over_algorithmic"] = res["step"]["traffic_bytes"] / algo
     if b:
         rf = b["roofline"]
         k1 = res["kernels"].get("k_pod_reduce", {})

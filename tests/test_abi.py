@@ -59,6 +59,10 @@ def test_no_device_is_reported_not_faked():
     ctx = Context([{"name": "a", "label_key": "k", "label_value": "v"}], device=-1)
     assert ctx.lib.esc_run(ctx.handle) == L.ESC_E_NODEV
     assert ctx.lib.esc_sort_nodes(ctx.handle) == L.ESC_E_NODEV
+    assert ctx.lib.esc_set_selections(ctx.handle, 0, 0) == L.ESC_E_NODEV
+    import pytest
+    with pytest.raises(L.EscError):
+        ctx.set_selections(2, 0)
 
 
 def test_group_interning_matches_oracle_tables():

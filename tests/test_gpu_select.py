@@ -230,3 +230,62 @@ def test_controller_walks_selections_and_falls_back(esc):
         assert act.calls == oldest[:oldest.index(good[-1]) + 1], (slack, bad)
         assert r["tainted_now"] == good
         assert r["walk_fallback"] == (len(bad) > slack), (slack, bad, r["walk_fallback"])
+
+
+def _relabel(nodes, groups, sizes, seed=0):
+    """The node table with its nodes reassigned so that group g's label pair holds sizes[g]
+    nodes (no extra labels, no trackers; the rest unlabelled), in a shuffled order."""
+    t = soa.group_tables(groups)
+    n = len(nodes["flags"])
+    assert sum(sizes) <= n
+    lab = np.full(n, 0xFFFFFFFF, np.uint32)
+    at = 0
+    for g, k in enumerate(sizes):
+        lab[at:at + k] = t["gpair"][g]
+        at += k
+    np.random.default_rng(seed).shuffle(lab)
+    out = {k: v.copy() for k, v in nodes.items()}
+    out["label0"] = lab
+    out["flags"] = out["flags"] & ~np.uint32(0xFF00 | 4)          # no extra labels, not tracked
+    out["xl_pair"] = np.zeros(0, np.uint32)
+    out["trk_node"] = np.zeros(0, np.int32)
+    out["trk_group"] = np.zeros(0, np.int32)
+    return out
+
+
+@pytest.mark.parametrize("shape", ["mixed", "sparse"])
+def test_packed_chunk_mix(esc, shape):
+    """Region sizes around the chunk limits: small (<= 1024), mid-size (<= 4096, packed up to
+    4096) and split groups interleaved — a mid-size chunk followed by a small group was
+    dropped (never ordered) before round 6 — and ('sparse') 20 000 groups of which every 50th
+    has members, so that packed chunks span more groups than ORD_GCAP.  Every group's two
+    orderings and selections against the oracle."""
+    rng = np.random.default_rng(5)
+    if shape == "mixed":
+        G = 200
+        pick = rng.integers(0, 5, G)
+        sizes = [int(x) for x in np.choose(pick, [rng.integers(0, 60, G), rng.integers(60, 1000, G),
+                                                  rng.integers(1025, 4097, G), rng.integers(4097, 9000, G),
+                                                  np.zeros(G, np.int64)])]
+    else:
+        G = 20_000
+        sizes = [5 if g % 50 == 0 else 0 for g in range(G)]
+    s = esc.Synth(50_000, sum(sizes) + 100, G, config=4, seed=77)
+    pods = s.pods()
+    nodes = _relabel(s.nodes(), s.groups, sizes)
+    want = soa.order_all(nodes, s.groups)
+    otot = soa.totals(pods, nodes, s.groups)
+    odf, odi = soa.decide(s.groups, s.states, otot)
+    ctx = esc.Context(s)
+    ctx.load(pods, nodes)
+    ctx.set_state(s.states)
+    ctx.set_order_in_step(True)
+    ctx.set_selections(1, 64)
+    for _ in range(2):
+        ctx.run()
+        tot, dec = ctx.results()
+        assert np.array_equal(dec["delta"], odi[:, 0])
+        for g in range(G):
+            for w in (0, 1):
+                assert np.array_equal(ctx.group_order(g, w), want[(g, w)]), (g, w, sizes[g])
+        check_selections(ctx, dec, want, nodes["created_ns"], 1, 64)
