@@ -2,6 +2,7 @@
 
 Bit-exact everywhere: int64 sums and counts, float64 percentages compared as bits,
 deltas, statuses and node orderings."""
+import ctypes as C
 import random
 import struct
 
@@ -1740,3 +1741,39 @@ def test_decision_beyond_int32_round_trips(esc):
         assert int(dec["delta"][g]) == L["delta"] and esc._lib.BRANCHES[dec["branch"][g]] == L["branch"], (g, L)
         assert (int(dec["cached_cpu_m"][g]), int(dec["cached_mem_b"][g])) == (L["cached_cpu_m"], L["cached_mem_b"])
     assert int(dec["delta"][0]) > (1 << 31)
+
+
+def test_bound_exchange_buffer_refused_after_growing_reload(esc):
+    """the exchange words follow the owner split, which every esc_load_nodes
+    recomputes.  A caller-bound buffer sized for the old split must not be overrun after a
+    reload that grows it: esc_reduce returns ESC_E_STATE until a buffer of the new size is
+    bound (esc_exchange_buffers still reports it), and then the step runs."""
+    import torch
+    from escalator_amd._lib import ESC_E_STATE
+    from escalator_amd.context import node_soa
+    s = esc.Synth(200_000, 20_000, 200, config=4, seed=3)
+    ctx = esc.Context(s, rank=0, world=2)
+    ctx.load_synth(s)
+    ctx.set_state(s.states)
+    (_, sc), _ = ctx.exchange_buffers()
+    buf = torch.zeros(sc, dtype=torch.int64, device="cuda")
+    ctx.bind_exchange(buf.data_ptr(), None)
+    ctx.reduce()
+    ctx.sync()
+    # every node into the first group's pair: rank 0 owns that one heavy pair, rank 1 the
+    # rest, so the largest owner's group count (the rows per rank) grows
+    nodes = {k: v.copy() for k, v in s.nodes().items()}
+    nodes["label0"][:] = soa.group_tables(s.groups)["gpair"][0]
+    nodes["flags"] &= ~np.uint32(0xFF00)
+    nodes["xl_pair"] = np.zeros(0, np.uint32)
+    ns, keep = node_soa(nodes)
+    assert ctx.lib.esc_load_nodes(ctx.handle, C.byref(ns), 0, len(nodes["flags"])) == 0
+    (_, sc2), _ = ctx.exchange_buffers()
+    assert sc2 > sc
+    assert ctx.lib.esc_reduce(ctx.handle) == ESC_E_STATE
+    buf2 = torch.zeros(sc2, dtype=torch.int64, device="cuda")
+    ctx.bind_exchange(buf2.data_ptr(), None)
+    ctx.reduce()
+    ctx.sync()
+    ctx.bind_exchange(None, None)
+    del keep
