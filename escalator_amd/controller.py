@@ -184,10 +184,10 @@ class Controller:
         (nodes brought up, error-or-None)."""
         dry = self.groups[g]["dry_mode"]
         picked = []
-        if n_tainted:                                      # scaleUpUntaint :98-116
+        if n_tainted and n > 0:                            # scaleUpUntaint :98-116
+            # the count is checked after each pick, so the walk never asks for a node past
+            # the last one it needs (that would read on beyond the delivered selection)
             for j in self._walk(g, 1, n_tainted, out):     # newest first (sort.go:27-39), untaintNewestN :127-160
-                if len(picked) >= n:
-                    break
                 if dry:                                    # delete the tracked name, if any
                     trk = self.taint_tracker[g]
                     if names[j] in trk:
@@ -195,6 +195,8 @@ class Controller:
                         picked.append(j)
                 elif self.actuator.untaint(g, j):          # a failed write moves on
                     picked.append(j)
+                if len(picked) >= n:
+                    break
         out["untainted_now"] = picked
         rest = n - len(picked)
         out["added"] = 0
@@ -222,14 +224,14 @@ class Controller:
         untainted nodes oldest first until n taints succeeded."""
         dry = self.groups[g]["dry_mode"]
         picked = []
-        for j in self._walk(g, 0, n_untainted, out):
-            if len(picked) >= max(n, 0):
-                break
+        for j in (self._walk(g, 0, n_untainted, out) if n > 0 else ()):
             if dry:
                 self.taint_tracker[g].append(names[j])
                 picked.append(j)
             elif self.actuator.taint(g, j):
                 picked.append(j)
+            if len(picked) >= n:
+                break
         out["tainted_now"] = picked
 
     def _reap(self, g: int, out: dict):

@@ -1533,7 +1533,7 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
     GroupParams prm{};
     int64_t pwv[PW_K] = {};
     uint32_t sel_w = 0, sel_c = 0, sel_cut = 0;          // this lane's group's selection (wave 0)
-    int64_t sel_s = 0, sel_len = 0;
+    int64_t sel_s = 0, sel_len = 0, segv[4] = {};
     if (ok) {
         gn = N.gnode[g];
         plo = gn.plo;
@@ -1543,6 +1543,11 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
             const int64_t* pw = D.pwords + (int64_t)(G.xs ? G.xs[g] : (uint32_t)g) * PW_K;
 #pragma unroll
             for (int k = 0; k < PW_K; ++k) pwv[k] = pw[k];
+            if (D.sel.out) {                         // both orders' segment bounds, with them
+                const int64_t* sg = D.sel.seg + 4 * (int64_t)g;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) segv[k] = sg[k];
+            }
         }
     }
     const int64_t np = N.n_pieces;
@@ -1623,9 +1628,8 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
             if (d.delta > 0) { sel_w = 2; need = d.delta; }                       // ScaleUp: untaintNewestN
             else if (d.delta < 0 && d.taint_status == ESC_ST_OK) { sel_w = 1; need = d.n_to_taint; }   // taintOldestN
             if (sel_w) {
-                const int64_t* sg = D.sel.seg + 4 * (int64_t)g + (sel_w == 1 ? 0 : 2);
-                sel_s = sg[0];
-                sel_len = sg[1] - sg[0];
+                sel_s = sel_w == 1 ? segv[0] : segv[2];
+                sel_len = sel_w == 1 ? segv[1] - segv[0] : segv[3] - segv[2];
                 const int64_t want = (need > 0 ? need : 0) + D.sel.slack;
                 const int64_t c = want < sel_len ? want : sel_len;
                 sel_c = (uint32_t)(c < D.sel.group_cap ? c : D.sel.group_cap);

@@ -114,7 +114,7 @@ def test_selections_long_tie_runs_fall_back(esc):
     """Every node of a group created in the same second: the kernel resolves runs of equal
     times up to SEL_TIE_MAX each way; a longer run comes back as a cut with no nodes, and
     esc_group_order (which reads on until the run ends) gives the walk."""
-    s, pods, nodes = _snapshot(esc, 500_000, 40_000, 100, coarse=10**15)
+    s, pods, nodes = _snapshot(esc, 500_000, 40_000, 20, coarse=10**15)   # ~2 000 nodes a group
     want = soa.order_all(nodes, s.groups)
     otot = soa.totals(pods, nodes, s.groups)
     odf, odi = soa.decide(s.groups, s.states, otot)
@@ -130,8 +130,10 @@ def test_selections_long_tie_runs_fall_back(esc):
     for g in np.nonzero((which >= 0) & ((which & SEL_CUT) != 0))[0][:5]:
         w = int(which[g]) & 3
         assert np.array_equal(ctx.group_order(int(g), w), want[(int(g), w)]), g
-    assert seen[SEL_TAINT] > 0
-    assert seen[3] > 0 or seen[SEL_UNTAINT] == 0, seen
+    long_up = [g for g in range(len(odi)) if odi[g, 0] > 0
+               and _long_tie(nodes["created_ns"], want[(g, SEL_UNTAINT)], min(odi[g, 0] + 4, 64))]
+    assert seen[SEL_TAINT] > 0 and len(long_up) > 0, (seen, long_up)
+    assert seen[3] == len(long_up), (seen, long_up)
 
 
 def test_selections_config4_full_size(esc):
