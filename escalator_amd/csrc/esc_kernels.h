@@ -421,6 +421,8 @@ struct K1Diag {
 struct SelOut {
     const uint32_t* ord;       // K5 output: every group's segments
     const int64_t* seg;        // [4G] segment bounds (K5)
+    const uint32_t* tie;       // [G] RegionSink::tie: only these groups' untaint lists need the
+                               // tie rule (the others copy their segment's prefix as it stands)
     uint32_t* out;             // device view of the pinned selection buffer; null: no selections
     uint32_t* total;           // words reserved this decision
     int64_t cap_words;         // out's size (a block whose run does not fit gets SEL_OVERFLOW)
@@ -600,9 +602,13 @@ struct RegionSink {
                                // coarse-key run too long for k_age_fix (rebuild exact)
     int32_t G;
     int R;                     // the group's shift in the key (key = group << R | time bits)
-    int fix;                   // coarse keys with dropped time bits: the final pass also writes
-                               // the sorted keys and k_age_fix orders equal-key runs exactly
+    int fix;                   // coarse keys: the final pass also writes the sorted keys and
+                               // k_age_fix reads them — 1 (time bits were dropped): it orders each
+                               // run of equal keys exactly and flags the groups with equal times;
+                               // 2 (the keys are exact): it only flags the groups of equal-key runs
     uint32_t spins;            // the listing's look-back bound (LOOKBACK_SPINS; err bit 0 on a give-up)
+    uint32_t* tie;             // [G] nonzero: two of the group's members share a creation time (the
+                               // selections resolve such ties, SelOut); zeroed by the host first
 };
 // coarse_shift < 0: exact 64-bit keys (group << R | offset); >= 0: 32-bit coarse keys
 // (group << (32 - gbits) | offset >> coarse_shift) + the run fix-up (S.R = 32 - gbits).

@@ -259,6 +259,7 @@ struct esc_ctx {
     bool age_built = false;
     bool age_ok = false;                                      // the last build succeeded (its regions are valid)
     uint32_t *d_hist = nullptr, *d_tot = nullptr, *d_total = nullptr, *d_ierr = nullptr;
+    uint32_t* d_g_tie = nullptr;                              // [G] equal creation times in the group (RegionSink::tie)
     uint64_t* d_lstat = nullptr;                              // single-pass listing status words
     int64_t* d_seg = nullptr;
     int64_t n_memb = 0;
@@ -536,9 +537,10 @@ OrdFail ord_fail(esc_ctx* c) { return OrdFail{c->h_oerr_dev, lb_spins(c->lb_fail
 // select from)
 SelOut sel_out(const esc_ctx* c) {
     SelOut s{};
-    if (c->sel_slack < 0 || !c->h_sel || !c->order_in_step || !c->d_ord || !c->d_seg) return s;
+    if (c->sel_slack < 0 || !c->h_sel || !c->order_in_step || !c->d_ord || !c->d_seg || !c->d_g_tie) return s;
     s.ord = c->d_ord;
     s.seg = c->d_seg;
+    s.tie = c->d_g_tie;
     s.out = c->h_sel_dev;
     s.total = c->d_sel_total;
     s.cap_words = c->sel_words;
@@ -648,6 +650,7 @@ void release_sort(esc_ctx* c) {
     c->n_chunks = 0;
     c->n_gpad = 0;
     dfree(c->d_hist); dfree(c->d_tot); dfree(c->d_lstat); dfree(c->d_total); dfree(c->d_ierr); dfree(c->d_seg);
+    dfree(c->d_g_tie);
     c->n_memb = 0;
     c->sorted = false;
 }
@@ -690,6 +693,7 @@ int32_t build_age_index(esc_ctx* c) {
         HIP_TRY(dalloc(&c->d_total, 1));
         HIP_TRY(dalloc(&c->d_ierr, 1));
         HIP_TRY(dalloc(&c->d_seg, (size_t)4 * g.G + 1));
+        HIP_TRY(dalloc(&c->d_g_tie, std::max<int32_t>(g.G, 1)));
         HIP_TRY(dalloc(&c->d_lstat, memb_status_words(nl)));
         c->age_built = true;
     }
@@ -856,8 +860,12 @@ int32_t build_age_index(esc_ctx* c) {
         const int cshift = coarse ? std::max(0, c->sort_R - (32 - gbits)) : -1;
         HIP_TRY(hipMemcpyAsync(c->d_seg, c->h_istage + ups[0].at, ups[0].bytes, hipMemcpyHostToDevice, st));
         HIP_TRY(hipMemsetAsync(c->d_ierr, 0, 4, st));
+        // the groups with equal creation times: found by k_age_fix on coarse keys (exact keys:
+        // every group is taken to have them, the selections' tie rule is then always applied)
+        HIP_TRY(hipMemsetAsync(c->d_g_tie, coarse ? 0 : 1, (size_t)std::max<int32_t>(g.G, 1) * 4, st));
         RegionSink sink{c->d_seg, c->d_pstart, c->d_plen, c->d_g_memb, c->d_ierr,
-                        g.G, coarse ? 32 - gbits : c->sort_R, cshift > 0 ? 1 : 0, lb_spins(c->lb_fail_list)};
+                        g.G, coarse ? 32 - gbits : c->sort_R, coarse ? (cshift > 0 ? 1 : 2) : 0, lb_spins(c->lb_fail_list),
+                        c->d_g_tie};
         HIP_TRY(launch_age_sort(n, g, c->d_lstat, c->d_total, c->n_memb, c->mcap, c->ts_min, c->sort_div, c->sort_R,
                                 gbits, cshift, c->d_mkeys, c->d_mvals, c->d_hist, c->d_tot, sink, st));
         HIP_TRY(launch_region_pad(c->d_pstart, c->d_plen, g.G, c->d_g_memb, c->d_seg, st));
@@ -3211,10 +3219,11 @@ void pair_first(const esc_ctx* c, uint32_t q, GroupNode& x) {
     }
 }
 
-// Patch targets of the K5 regions: membership word (node | flags).
+// Patch targets of the K5 regions: membership word (node | flags), the groups' tie flags.
 PatchTargets region_targets(esc_ctx* c) {
     PatchTargets t{};
     t.u32[0] = c->d_g_memb;
+    t.u32[1] = c->d_g_tie;
     return t;
 }
 
@@ -3238,6 +3247,14 @@ void regions_insert(esc_ctx* c, std::unordered_map<uint32_t, std::vector<uint32_
         std::merge(run + from, run + len, nw.begin(), nw.end(), merged.begin(), less);
         std::copy(merged.begin(), merged.end(), run + from);
         c->h_plen[g] = len + (uint32_t)nw.size();
+        // equal creation times side by side from the insertion on: the group's selections take
+        // the tie rule from now on (RegionSink::tie; a removal never clears the flag)
+        bool tie = false;
+        for (size_t k = 0; k < merged.size() && !tie; ++k) {
+            const int64_t prev = k ? (int64_t)merged[k - 1] : (from ? (int64_t)run[from - 1] : -1);
+            tie = prev >= 0 && created_of(c, (uint32_t)prev) == created_of(c, merged[k]);
+        }
+        if (tie) R.add(1, g, 1);
         const uint32_t mbit = (uint32_t)g | (c->params[g].dry ? NODE_DRY_BIT : 0u);
         for (size_t k = 0; k < merged.size(); ++k) {
             const int64_t pos = (int64_t)a + from + (int64_t)k;

@@ -291,3 +291,57 @@ def test_packed_chunk_mix(esc, shape):
             for w in (0, 1):
                 assert np.array_equal(ctx.group_order(g, w), want[(g, w)]), (g, w, sizes[g])
         check_selections(ctx, dec, want, nodes["created_ns"], 1, 64)
+
+
+def test_selections_ties_from_node_adds(esc):
+    """The tie rule is applied per group, only where equal creation times exist
+    (RegionSink::tie): a group loaded with unique times copies its tainted segment as is;
+    node additions with the creation times of its newest tainted nodes flag it, and its
+    untaint list (newest first, equal times by ascending index) still equals the literal
+    order; a second group, never given a tie, keeps copying."""
+    from builders import build_test_node, build_test_pods
+    from oracle import oracle as O
+    grp = {"label_key": "k", "min_nodes": 0, "max_nodes": 10_000, "scale_up_pct": 70, "taint_lower_pct": 10,
+           "taint_upper_pct": 20, "fast_removal_rate": 4, "slow_removal_rate": 2}
+    groups = [dict(grp, name="a", label_value="a"), dict(grp, name="b", label_value="b")]
+    nodes = []
+    for v in ("a", "b"):
+        for i in range(300):                               # unique times; 200 tainted, 100 not
+            nodes.append(build_test_node({"Name": "%s%d" % (v, i), "LabelKey": "k", "LabelValue": v,
+                                          "CPU": 1000, "Mem": 1 << 30, "Tainted": i % 3 != 0,
+                                          "Creation": 10**12 + 7919 * ((i * 37) % 300) + (v == "b")}))
+    pods = []
+    for v in ("a", "b"):                                   # far over the untainted capacity: ScaleUp
+        pods += build_test_pods(400, {"CPU": [900], "Mem": [1 << 20], "NodeSelectorKey": "k",
+                                      "NodeSelectorValue": v})
+    ctx = esc.Context(groups)
+    ctx.set_spare(1.0)
+    P, N = ctx.pack(pods, nodes)
+    ctx.load(P, N)
+    states = [{"locked": False, "requested_nodes": 0, "cached_cpu_m": 0, "cached_mem_b": 0}] * 2
+    ctx.set_state(states)
+    ctx.set_order_in_step(True)
+    ctx.set_selections(2, 64)
+
+    def check(lst, tied):
+        ctx.run()
+        tot, dec = ctx.results()
+        which, off, idx = ctx.selections()
+        for g, v in enumerate(("a", "b")):
+            assert int(dec["delta"][g]) > 0 and which[g] & 3 == SEL_UNTAINT, (g, dec["delta"][g], which[g])
+            tn = [j for j, nd in enumerate(lst) if nd["labels"].get("k") == v and nd["taints"]]
+            want = [tn[i] for i in O.newest_first([lst[j]["created_ns"] for j in tn])]
+            assert list(ctx.group_order(g, 1)) == want
+            c = min(int(dec["delta"][g]) + 2, len(want))
+            assert list(idx[off[g]:off[g + 1]]) == want[:min(c, 64)], (g, list(idx[off[g]:off[g] + 6]), want[:6])
+            head = [lst[j]["created_ns"] for j in want[:c]]
+            assert (len(set(head)) < len(head)) == (tied and v == "a"), g   # the case at hand
+
+    check(nodes, False)
+    newest = [j for j in O.newest_first([nd["created_ns"] for nd in nodes[:300]]) if nodes[j]["taints"]][:5]
+    add = [build_test_node({"Name": "x%d" % k, "LabelKey": "k", "LabelValue": "a", "CPU": 1000, "Mem": 1 << 30,
+                            "Tainted": True, "Creation": nodes[j]["created_ns"]}) for k, j in enumerate(newest[::-1])]
+    _, packed = ctx.pack([], add)
+    ids = ctx.nodes_add(packed)
+    assert list(ids) == list(range(600, 605))
+    check(nodes + add, True)
