@@ -413,18 +413,17 @@ struct K1Diag {
 // nodes newest first (untaintNewestN, scale_up.go:118-163; equal creation times by ascending
 // index, the ordering's tie rule), copied from the ordering of the same decision into the
 // pinned buffer `out` — a block's groups as one contiguous run of [header, nodes...] words
-// (one device-scope add per block reserves it) — and the run's offset into the compact
-// record's `sel` field.  Header: count | which << 28 (1 taint, 2 untaint) | SEL_CUT (more
-// wanted than group_cap: the nodes are the walk's first ones) | SEL_TIE (a run of equal
-// creation times longer than SEL_TIE_MAX: the nodes are not used; in both cases the host
-// continues with esc_group_order).  `total` is zeroed by k_step_tail's first block every step.
+// at the block's own slot (blockIdx.x * 64 * (group_cap + 1): no reservation across blocks)
+// — and the run's offset into the compact record's `sel` field.  Header: count | which << 28
+// (1 taint, 2 untaint) | SEL_CUT (more wanted than group_cap: the nodes are the walk's first
+// ones) | SEL_TIE (a run of equal creation times longer than SEL_TIE_MAX: the nodes are not
+// used; in both cases the host continues with esc_group_order).
 struct SelOut {
     const uint32_t* ord;       // K5 output: every group's segments
     const int64_t* seg;        // [4G] segment bounds (K5)
     const uint32_t* tie;       // [G] RegionSink::tie: only these groups' untaint lists need the
                                // tie rule (the others copy their segment's prefix as it stands)
     uint32_t* out;             // device view of the pinned selection buffer; null: no selections
-    uint32_t* total;           // words reserved this decision
     int64_t cap_words;         // out's size (a block whose run does not fit gets SEL_OVERFLOW)
     int32_t slack, group_cap;
 };
@@ -499,7 +498,7 @@ int64_t tail_trk_blocks(const NodeDev& n);
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
                             const uint32_t* grp_off, const uint32_t* g_memb,
-                            uint32_t* vals, int64_t* seg, uint32_t* sel_total, hipStream_t st);
+                            uint32_t* vals, int64_t* seg, hipStream_t st);
 hipError_t launch_wide_pods(const PodDev& p, const GroupDev& g, int64_t* wide, hipStream_t st);
 // §8f rank 2: a loaded pod as seen by NodePodsRemaining, listed per node (runs in
 // node order).  p[0..2]: the pod's extra pairs (NONE-padded); a C pod with more than 3
@@ -588,7 +587,7 @@ hipError_t launch_order_packed(const NodeDev& nd, const OrdChunk* chunks, int64_
 hipError_t launch_region_pad(const uint32_t* pstart, const uint32_t* plen, int32_t G, uint32_t* g_memb, int64_t* seg,
                              hipStream_t st);
 // The age index (load time): memberships listed in one pass (per-tile counts, decoupled
-// look-back: status = memb_status_words(n) u64 words, zeroed by the launcher) with
+// look-back: status = memb_status_words(n) u64 words, zeroed by the caller) with
 // (group << R | creation offset) keys and (node | flags) values, LSD-sorted, then written
 // into the groups' padded regions; *total = the listed count.
 size_t memb_status_words(int64_t n);

@@ -1481,6 +1481,7 @@ __device__ __forceinline__ int64_t ld_agent(const int64_t* p) {
 #endif
 constexpr int NG_WAVES = ESC_NG_WAVES;
 
+
 namespace {
 // Entry q of a group's selection (SelOut): the untainted segment is stored oldest first
 // (ties by ascending index, the age index's order), the tainted one newest first with equal
@@ -1523,7 +1524,7 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
     // [64] = the block's words), which (0 none, 1 taint, 2 untaint), count, segment, cut
     __shared__ uint32_t s_ex[65], s_w[64], s_c[64], s_cut[64];
     __shared__ int64_t s_s[64], s_len[64];
-    __shared__ uint32_t s_base;
+
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int32_t g = (int32_t)gid;
     const bool ok = gid != NONE && g < G.G;
@@ -1643,18 +1644,17 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
     }
     }
     if (D.dec && D.sel.out) {
-        // one device-scope add per block reserves the block's run; lane l's group takes
+        // the block's run starts at its own slot, blockIdx.x * 64 * (group_cap + 1) words (room
+        // for 64 groups at their largest: no reservation across blocks); lane l's group takes
         // [base + ex, base + ex + 1 + count): its header, then its nodes
+        const uint32_t base = blockIdx.x * 64u * (uint32_t)(D.sel.group_cap + 1);
         if (wid == 0) {
             const uint32_t words = sel_w ? sel_c + 1 : 0u;
             const uint32_t inc = wave_incl_scan32(words);
             const uint32_t tot = __builtin_amdgcn_readlane(inc, 63);
-            uint32_t base = 0;
-            if (lane == 63 && tot) base = atomicAdd(D.sel.total, tot);
-            base = __builtin_amdgcn_readlane(base, 63);
             const bool fits = (int64_t)base + tot <= D.sel.cap_words;
             s_ex[lane] = inc - words;
-            if (lane == 63) { s_ex[64] = fits ? tot : 0u; s_base = base; }
+            if (lane == 63) s_ex[64] = fits ? tot : 0u;
             s_w[lane] = fits ? sel_w : 0u;
             s_c[lane] = sel_c;
             s_s[lane] = sel_s;
@@ -1663,7 +1663,7 @@ __device__ __forceinline__ void node_groups_part(const GroupDev& G, const NodeDe
             if (ok) sdec[lane].sel = !sel_w ? SEL_NONE : (fits ? base + inc - words : SEL_OVERFLOW);
         }
         __syncthreads();
-        const uint32_t total = s_ex[64], base = s_base;
+        const uint32_t total = s_ex[64];
         // SEL_U words per thread per round, their segment loads issued together (one memory
         // latency for the block's whole run in the common case); a group flagged with equal
         // creation times takes sel_entry's tie rule after
@@ -2203,8 +2203,18 @@ __device__ __forceinline__ void age_fix_run(const uint32_t* __restrict__ keys, i
     const uint32_t g = k >> S.R;
     if (g >= (uint32_t)S.G) { atomicOr(S.err, 1u); return; }
     if (S.fix == 2) { S.tie[g] = 1u; return; }         // exact keys: equal keys are equal times
-    int len = 2;
-    while (len <= AF_RUN && i + len < n && keys[i + len] == k) ++len;
+    int len = 2;                                       // the run's length: its next keys loaded together
+    {
+        uint32_t nk[AF_RUN - 1];
+#pragma unroll
+        for (int j = 0; j < AF_RUN - 1; ++j) nk[j] = i + 2 + j < n ? keys[i + 2 + j] : ~k;
+        bool on = true;
+#pragma unroll
+        for (int j = 0; j < AF_RUN - 1; ++j) {
+            on = on && nk[j] == k;
+            len += on ? 1 : 0;
+        }
+    }
     if (len > AF_RUN) { atomicOr(S.err, 2u); return; }
     // the run lies inside its group's sorted range, and its words name table nodes — always,
     // unless the keys are not the listing's (bit 0: the build fails; nothing is touched)
@@ -2239,30 +2249,59 @@ __device__ __forceinline__ void age_fix_run(const uint32_t* __restrict__ keys, i
     if (tie) S.tie[g] = 1u;
 }
 
-// Grid-stride over quads of the sorted coarse keys (one 16-B load + the neighbours at the
-// quad's ends): a position starts a run when its key equals the next one and not the
-// previous one.  Runs are rare (config 5: a handful per 10^4 memberships), so the pass is
-// a streaming read of the keys; one thread per key (43 k blocks) took 39 µs for it.
+// Two phases per block over its contiguous share of quads of the sorted coarse keys (one
+// 16-B load + the neighbours at the quad's ends; a position starts a run when its key equals
+// the next one and not the previous one): the run starts found are listed in LDS, then every
+// listed run is fixed by its own thread, all of the block's runs in flight together.  Runs
+// are rare (config 5: a few per 10^3 memberships) but each is a chain of dependent loads
+// (region starts, region words, creation times): fixed where found, a grid-stride
+// iteration that met one waited out its chain before its next quads (37 µs, round 6).
+// (one call site: every inlined copy of age_fix_run is ~30 compare-exchanges and 16 loads)
+constexpr int AF_QPT = 4;                                // quads per thread per round
+constexpr int AF_CAP = 256 * AF_QPT * 2;                 // a round's run starts at most (one per two keys)
 __global__ __launch_bounds__(256) void k_age_fix(const uint32_t* __restrict__ keys, int64_t n, RegionSink S,
                                                  const int64_t* __restrict__ created, int64_t n_nodes, int64_t ts_min) {
+    __shared__ uint32_t s_n;
+    __shared__ uint32_t s_i[AF_CAP];                     // run start - 4 * q0
+    __shared__ uint32_t s_k[AF_CAP];
     if (*S.err & 1u) return;                             // the listing gave up: its keys are not memberships
     const int64_t nq = (n + 3) / 4;
-    for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < nq; q += (int64_t)gridDim.x * 256) {
-        const int64_t i0 = 4 * q;
-        uint32_t k[6];                                   // keys[i0 - 1 .. i0 + 4]; absent ends never match
-        if (i0 + 4 <= n) {
-            const uint4 v = *reinterpret_cast<const uint4*>(keys + i0);
-            k[1] = v.x; k[2] = v.y; k[3] = v.z; k[4] = v.w;
-        } else {
+    const int64_t per = (nq + gridDim.x - 1) / gridDim.x;
+    const int64_t qa = (int64_t)blockIdx.x * per, qb = imin64(nq, qa + per);
+    for (int64_t q0 = qa; q0 < qb; q0 += 256 * AF_QPT) {
+        if (threadIdx.x == 0) s_n = 0;
+        __syncthreads();
+        uint32_t k[AF_QPT][6];                           // keys[i0 - 1 .. i0 + 4]; absent ends never match
 #pragma unroll
-            for (int j = 0; j < 4; ++j) k[1 + j] = i0 + j < n ? keys[i0 + j] : ~keys[n - 1];
+        for (int u = 0; u < AF_QPT; ++u) {
+            const int64_t q = q0 + u * 256 + threadIdx.x, i0 = 4 * q;
+            if (q >= qb) { k[u][1] = 0; k[u][2] = 1; k[u][3] = 2; k[u][4] = 3; k[u][0] = k[u][5] = 4; continue; }
+            if (i0 + 4 <= n) {
+                const uint4 v = *reinterpret_cast<const uint4*>(keys + i0);
+                k[u][1] = v.x; k[u][2] = v.y; k[u][3] = v.z; k[u][4] = v.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) k[u][1 + j] = i0 + j < n ? keys[i0 + j] : ~keys[n - 1];
+            }
+            k[u][0] = i0 > 0 ? keys[i0 - 1] : ~k[u][1];
+            k[u][5] = i0 + 4 < n ? keys[i0 + 4] : ~k[u][4];
         }
-        k[0] = i0 > 0 ? keys[i0 - 1] : ~k[1];
-        k[5] = i0 + 4 < n ? keys[i0 + 4] : ~k[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (i0 + j + 1 < n && k[1 + j] == k[2 + j] && k[j] != k[1 + j])
-                age_fix_run(keys, n, S, created, n_nodes, ts_min, i0 + j, k[1 + j]);
+        for (int u = 0; u < AF_QPT; ++u) {
+            const int64_t i0 = 4 * (q0 + u * 256 + threadIdx.x);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (i0 + j + 1 < n && k[u][1 + j] == k[u][2 + j] && k[u][j] != k[u][1 + j]) {
+                    const uint32_t s = atomicAdd(&s_n, 1u);      // < AF_CAP: runs start >= 2 keys apart
+                    s_i[s] = (uint32_t)(i0 + j - 4 * q0);
+                    s_k[s] = k[u][1 + j];
+                }
+        }
+        __syncthreads();
+        const uint32_t m = s_n;
+        for (uint32_t r = threadIdx.x; r < m; r += 256)
+            age_fix_run(keys, n, S, created, n_nodes, ts_min, 4 * q0 + s_i[r], s_k[r]);
+        __syncthreads();
     }
 }
 
@@ -2841,11 +2880,9 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
                                                    const OrdChunk* __restrict__ chunks, int64_t n_small,
                                                    const uint32_t* __restrict__ grp_off,
                                                    const uint32_t* __restrict__ g_memb,
-                                                   uint32_t* __restrict__ vals, int64_t* __restrict__ seg,
-                                                   uint32_t* __restrict__ sel_total) {
+                                                   uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
     static_assert(FD_WAVES * 64 == 256 && K2_WAVES * 64 == 256 && ORD_BLOCK == 256, "one block size for every role");
     const int64_t b = blockIdx.x;
-    if (b == 0 && threadIdx.x == 0 && sel_total) *sel_total = 0;   // this step's selection runs (k_node_groups)
     // F.ablate (ESC_K3_ABLATE, timing-only, wrong results): 8 / 16 / 32 skip the fold /
     // node-piece / ordering role, 64 the dry-mode tracker blocks, 128 K2's row stores
     if (b < n_piece_blk) {
@@ -3129,13 +3166,13 @@ int64_t tail_trk_blocks(const NodeDev& n) { return (n.n_trk + K2_WAVES * 64 - 1)
 hipError_t launch_step_tail(const GroupDev& g, const NodeDev& n, const FoldPlan& f, bool spans, int64_t* wide_pod,
                             int64_t* pwords, int64_t* rows, int64_t* trk_acc, const OrdChunk* chunks, int64_t n_small,
                             const uint32_t* grp_off, const uint32_t* g_memb,
-                            uint32_t* vals, int64_t* seg, uint32_t* sel_total, hipStream_t st) {
+                            uint32_t* vals, int64_t* seg, hipStream_t st) {
     const int64_t nb = spans ? tail_span_blocks(n) : 0;      // else K1 made the rows
     const int64_t nt = tail_trk_blocks(n);
     const int64_t grid = f.n_col + nb + nt + std::max<int64_t>(n_small, 0);
     if (grid <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_step_tail, dim3((unsigned)grid), dim3(256), 0, st, g, n, f, wide_pod, pwords, nb, nb + nt, rows,
-                       trk_acc, chunks, std::max<int64_t>(n_small, 0), grp_off, g_memb, vals, seg, sel_total);
+                       trk_acc, chunks, std::max<int64_t>(n_small, 0), grp_off, g_memb, vals, seg);
     return hipGetLastError();
 }
 
@@ -3246,7 +3283,7 @@ hipError_t launch_age_sort(const NodeDev& nd, const GroupDev& g, uint64_t* statu
     const int64_t n = nd.hi - nd.lo;
     const size_t nst = memb_status_words(n);
     const dim3 tiles((unsigned)(nst - 1));
-    if (n > 0 && hipMemsetAsync(status, 0, nst * 8, st) != hipSuccess) return hipGetLastError();
+    // (status: zeroed by the caller, with the index's other tables in one upload)
     if (coarse_shift < 0) {                          // exact 64-bit keys: group << R | offset
         if (n > 0)
             hipLaunchKernelGGL(k_memb_keys<uint64_t>, tiles, dim3(MEMB_BLOCK), 0, st, nd, g, n, status, total, S.err, S.spins, cap, ts_min,

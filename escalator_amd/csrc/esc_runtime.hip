@@ -220,7 +220,7 @@ struct esc_ctx {
     // decided group's taint / untaint nodes into h_sel (pinned, zero-copy) as [header, nodes]
     // runs, their offsets into the compact records
     int32_t sel_slack = -1, sel_group_cap = 0;
-    uint32_t *h_sel = nullptr, *h_sel_dev = nullptr, *d_sel_total = nullptr;
+    uint32_t *h_sel = nullptr, *h_sel_dev = nullptr;
     int64_t sel_words = 0;
     bool want_metrics = false;                                // K4 also writes the gauges
     esc_group_metrics* d_metrics = nullptr;
@@ -258,7 +258,13 @@ struct esc_ctx {
     int64_t mcap = 0;                                         // their capacity (memberships)
     bool age_built = false;
     bool age_ok = false;                                      // the last build succeeded (its regions are valid)
-    uint32_t *d_hist = nullptr, *d_tot = nullptr, *d_total = nullptr, *d_ierr = nullptr;
+    uint32_t *d_hist = nullptr, *d_tot = nullptr;
+    // The index's small tables live in ONE allocation, filled by ONE upload per build
+    // (build_age_index): sorted starts d_seg, region starts / lengths, chunk tables, the
+    // listing's status words, the error word and listed total, the groups' tie flags.
+    uint8_t* d_itab = nullptr;
+    size_t itab_cap = 0;
+    uint32_t *d_total = nullptr, *d_ierr = nullptr;           // (views into d_itab)
     uint32_t* d_g_tie = nullptr;                              // [G] equal creation times in the group (RegionSink::tie)
     uint64_t* d_lstat = nullptr;                              // single-pass listing status words
     int64_t* d_seg = nullptr;
@@ -542,7 +548,6 @@ SelOut sel_out(const esc_ctx* c) {
     s.seg = c->d_seg;
     s.tie = c->d_g_tie;
     s.out = c->h_sel_dev;
-    s.total = c->d_sel_total;
     s.cap_words = c->sel_words;
     s.slack = c->sel_slack;
     s.group_cap = c->sel_group_cap;
@@ -552,7 +557,6 @@ SelOut sel_out(const esc_ctx* c) {
 void release_selections(esc_ctx* c) {
     if (c->h_sel) hipHostFree(c->h_sel);
     c->h_sel = c->h_sel_dev = nullptr;
-    dfree(c->d_sel_total);
     c->sel_words = 0;
 }
 
@@ -644,13 +648,15 @@ void release_sort(esc_ctx* c) {
     c->mcap = 0;
     c->age_built = false;
     dfree(c->d_g_memb);
-    dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ostat); dfree(c->d_chunks);
-    dfree(c->d_pstart); dfree(c->d_plen); dfree(c->d_ord); dfree(c->d_pchunks);
+    dfree(c->d_ostat); dfree(c->d_ord);
     c->n_pchunks = 0;
     c->n_chunks = 0;
     c->n_gpad = 0;
-    dfree(c->d_hist); dfree(c->d_tot); dfree(c->d_lstat); dfree(c->d_total); dfree(c->d_ierr); dfree(c->d_seg);
-    dfree(c->d_g_tie);
+    dfree(c->d_hist); dfree(c->d_tot);
+    dfree(c->d_itab);
+    c->itab_cap = 0;
+    c->d_seg = nullptr; c->d_grp_off = c->d_gch_off = c->d_pstart = c->d_plen = nullptr;
+    c->d_chunks = c->d_pchunks = nullptr; c->d_lstat = nullptr; c->d_total = c->d_ierr = c->d_g_tie = nullptr;
     c->n_memb = 0;
     c->sorted = false;
 }
@@ -690,11 +696,6 @@ int32_t build_age_index(esc_ctx* c) {
         if (c->sort_R + bit_width((uint64_t)std::max<int32_t>(g.G - 1, 1)) > 64) return ESC_E_LIMIT;
         if (c->node_hi >= ((int64_t)1 << 28)) return ESC_E_LIMIT;   // node | flags << 28 sort values
         HIP_TRY(dalloc(&c->d_tot, 256));
-        HIP_TRY(dalloc(&c->d_total, 1));
-        HIP_TRY(dalloc(&c->d_ierr, 1));
-        HIP_TRY(dalloc(&c->d_seg, (size_t)4 * g.G + 1));
-        HIP_TRY(dalloc(&c->d_g_tie, std::max<int32_t>(g.G, 1)));
-        HIP_TRY(dalloc(&c->d_lstat, memb_status_words(nl)));
         c->age_built = true;
     }
     // Every group's membership count is the live entry count of its pair (the host's), so
@@ -805,35 +806,51 @@ int32_t build_age_index(esc_ctx* c) {
     c->n_gpad = npad;
     // no clearing: the sort's last pass fills every group's [start, start + len), k_region_pad the
     // rest of its region
-    if (fresh || (int64_t)chunks.size() != c->n_chunks || (int64_t)pchunks.size() != c->n_pchunks) {
-        dfree(c->d_grp_off); dfree(c->d_gch_off); dfree(c->d_ostat); dfree(c->d_chunks);
-        dfree(c->d_pstart); dfree(c->d_plen); dfree(c->d_pchunks);
-        HIP_TRY(dalloc(&c->d_grp_off, pstart.size())); HIP_TRY(dalloc(&c->d_gch_off, gch_off.size()));
+    if (fresh || (int64_t)chunks.size() != c->n_chunks) {
+        dfree(c->d_ostat);
         HIP_TRY(dalloc(&c->d_ostat, 2 * chunks.size() + 1));
         HIP_TRY(hipMemsetAsync(c->d_ostat, 0, (2 * chunks.size() + 1) * 8, st));
         c->ord_failed = false;
         c->ord_parity = 0;
-        drop_graphs(c);                                 // captured steps hold the old tables
-        HIP_TRY(dalloc(&c->d_chunks, std::max<size_t>(chunks.size(), 1)));
-        HIP_TRY(dalloc(&c->d_pchunks, std::max<size_t>(pchunks.size(), 1)));
-        HIP_TRY(dalloc(&c->d_pstart, pstart.size())); HIP_TRY(dalloc(&c->d_plen, plen.size()));
+        drop_graphs(c);                                 // captured steps hold the old status words
     }
-
     c->n_chunks = (int64_t)chunks.size();
     c->n_pchunks = (int64_t)pchunks.size();
-    // Every host-made array goes through one pinned staging area, so the uploads queue on the
-    // stream behind each other with no synchronisation between them; the build waits once, at
-    // its end (round 5: eight pageable copies, each a wait, were ~0.1 ms of the build).
-    struct Up { void* dst; const void* src; size_t bytes; size_t at; };
-    Up ups[] = {{c->d_seg, starts.data(), starts.size() * 8, 0},
-                {c->d_grp_off, pstart.data(), pstart.size() * 4, 0},
-                {c->d_gch_off, gch_off.data(), gch_off.size() * 4, 0},
-                {c->d_pstart, pstart.data(), pstart.size() * 4, 0},
-                {c->d_plen, plen.data(), plen.size() * 4, 0},
-                {c->d_chunks, chunks.data(), chunks.size() * sizeof(OrdChunk), 0},
-                {c->d_pchunks, pchunks.data(), pchunks.size() * sizeof(OrdChunk), 0}};
-    size_t stage = 256;                                     // [0, 4): the error word read back
-    for (Up& u : ups) { u.at = stage; stage += (u.bytes + 255) & ~(size_t)255; }
+    // The host-made tables, the listing's status words (zero), the error word and listed total
+    // (zero) and the tie flags (coarse keys: zero, k_age_fix sets them; exact keys: every group)
+    // are laid out in the pinned staging area exactly as in d_itab and go up as ONE copy per
+    // attempt (round 5: seven queued copies and three fills, ~10 stream operations of a few µs
+    // each); the build waits once, at its end, for the error word and total read back.
+    const int gbits = bit_width((uint64_t)std::max<int32_t>(g.G - 1, 1));
+    const size_t Gw = (size_t)std::max<int32_t>(g.G, 1);
+    struct Part { void** view; const void* src; size_t src_bytes; size_t bytes; size_t at; };   // src: copied, else zero
+    void* v_seg = nullptr; void* v_grp = nullptr; void* v_gch = nullptr; void* v_ps = nullptr; void* v_pl = nullptr;
+    void* v_ch = nullptr; void* v_pch = nullptr; void* v_st = nullptr; void* v_err = nullptr; void* v_tie = nullptr;
+    // d_seg: the G + 1 sorted starts the sort's last pass reads, room for the 4G + 1 segment
+    // bounds k_region_pad and the orderings write over them
+    Part parts[] = {{&v_seg, starts.data(), starts.size() * 8, (4 * (size_t)g.G + 1) * 8, 0},
+                    {&v_grp, pstart.data(), pstart.size() * 4, pstart.size() * 4, 0},
+                    {&v_gch, gch_off.data(), gch_off.size() * 4, gch_off.size() * 4, 0},
+                    {&v_ps, pstart.data(), pstart.size() * 4, pstart.size() * 4, 0},
+                    {&v_pl, plen.data(), plen.size() * 4, plen.size() * 4, 0},
+                    {&v_ch, chunks.data(), chunks.size() * sizeof(OrdChunk), std::max<size_t>(chunks.size(), 1) * sizeof(OrdChunk), 0},
+                    {&v_pch, pchunks.data(), pchunks.size() * sizeof(OrdChunk),
+                     std::max<size_t>(pchunks.size(), 1) * sizeof(OrdChunk), 0},
+                    {&v_st, nullptr, 0, memb_status_words(nl) * 8, 0},
+                    {&v_err, nullptr, 0, 8, 0},                          // error word, listed total
+                    {&v_tie, nullptr, 0, Gw * 4, 0}};
+    size_t bytes = 0;
+    for (Part& q : parts) { q.at = bytes; bytes += (q.bytes + 255) & ~(size_t)255; }
+    const size_t rb_at = bytes;                              // the read-back words (error, total)
+    const size_t stage = bytes + 256;
+    if (bytes > c->itab_cap) {
+        drop_graphs(c);                                      // captured steps hold the old tables
+        HIP_TRY(hipStreamSynchronize(st));
+        dfree(c->d_itab);
+        c->itab_cap = 0;
+        HIP_TRY(hipMalloc(reinterpret_cast<void**>(&c->d_itab), bytes));
+        c->itab_cap = bytes;
+    }
     if (stage > c->istage_cap) {
         HIP_TRY(hipStreamSynchronize(st));                  // the previous build's copies are done
         if (c->h_istage) hipHostFree(c->h_istage);
@@ -842,27 +859,46 @@ int32_t build_age_index(esc_ctx* c) {
         HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_istage), stage));
         c->istage_cap = stage;
     }
-    for (Up& u : ups) {
-        if (!u.bytes) continue;
-        std::memcpy(c->h_istage + u.at, u.src, u.bytes);
-        if (u.dst != c->d_seg) HIP_TRY(hipMemcpyAsync(u.dst, c->h_istage + u.at, u.bytes, hipMemcpyHostToDevice, st));
-    }
-    volatile uint32_t* h_err = reinterpret_cast<volatile uint32_t*>(c->h_istage);
+    for (Part& q : parts) *q.view = c->d_itab + q.at;
+    int64_t* const new_seg = static_cast<int64_t*>(v_seg);
+    if (new_seg != c->d_seg || static_cast<OrdChunk*>(v_pch) != c->d_pchunks || static_cast<OrdChunk*>(v_ch) != c->d_chunks ||
+        static_cast<uint32_t*>(v_tie) != c->d_g_tie)
+        drop_graphs(c);                                      // the layout moved: captured steps hold the old views
+    c->d_seg = new_seg;
+    c->d_grp_off = static_cast<uint32_t*>(v_grp);
+    c->d_gch_off = static_cast<uint32_t*>(v_gch);
+    c->d_pstart = static_cast<uint32_t*>(v_ps);
+    c->d_plen = static_cast<uint32_t*>(v_pl);
+    c->d_chunks = static_cast<OrdChunk*>(v_ch);
+    c->d_pchunks = static_cast<OrdChunk*>(v_pch);
+    c->d_lstat = static_cast<uint64_t*>(v_st);
+    c->d_ierr = static_cast<uint32_t*>(v_err);
+    c->d_total = c->d_ierr + 1;
+    c->d_g_tie = static_cast<uint32_t*>(v_tie);
+    auto stage_tables = [&](bool coarse) {
+        for (Part& q : parts) {
+            uint8_t* h = c->h_istage + q.at;
+            if (q.view == &v_tie && !coarse) {
+                for (size_t k = 0; k < Gw; ++k) reinterpret_cast<uint32_t*>(h)[k] = 1u;
+                continue;
+            }
+            if (q.src_bytes) std::memcpy(h, q.src, q.src_bytes);
+            if (q.bytes > q.src_bytes) std::memset(h + q.src_bytes, 0, q.bytes - q.src_bytes);
+        }
+    };
+    volatile uint32_t* h_err = reinterpret_cast<volatile uint32_t*>(c->h_istage + rb_at);
     // the listing and the sort; its last pass writes the regions at the host's sorted starts.
     // Keys: 32-bit coarse keys — the group in the top gbits, the creation offset's top
     // (32 - gbits) bits — when the groups leave at least 16 bits of time: four 8-bit LSD
     // passes over 8-B (key, value) pairs instead of six over 12-B ones; if offset bits were
     // dropped, k_age_fix orders the runs of equal coarse keys by the exact time, and a run
     // too long for it sends the build back to the exact 64-bit keys.
-    const int gbits = bit_width((uint64_t)std::max<int32_t>(g.G - 1, 1));
     for (int attempt = 0;; ++attempt) {
         const bool coarse = !c->age_exact && gbits <= 16;
         const int cshift = coarse ? std::max(0, c->sort_R - (32 - gbits)) : -1;
-        HIP_TRY(hipMemcpyAsync(c->d_seg, c->h_istage + ups[0].at, ups[0].bytes, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemsetAsync(c->d_ierr, 0, 4, st));
-        // the groups with equal creation times: found by k_age_fix on coarse keys (exact keys:
-        // every group is taken to have them, the selections' tie rule is then always applied)
-        HIP_TRY(hipMemsetAsync(c->d_g_tie, coarse ? 0 : 1, (size_t)std::max<int32_t>(g.G, 1) * 4, st));
+        if (attempt) HIP_TRY(hipStreamSynchronize(st));      // (the staging is rewritten)
+        stage_tables(coarse);
+        HIP_TRY(hipMemcpyAsync(c->d_itab, c->h_istage, bytes, hipMemcpyHostToDevice, st));
         RegionSink sink{c->d_seg, c->d_pstart, c->d_plen, c->d_g_memb, c->d_ierr,
                         g.G, coarse ? 32 - gbits : c->sort_R, coarse ? (cshift > 0 ? 1 : 2) : 0, lb_spins(c->lb_fail_list),
                         c->d_g_tie};
@@ -873,8 +909,7 @@ int32_t build_age_index(esc_ctx* c) {
         // the listed total, read at the build's one wait
         h_err[0] = 0;
         h_err[1] = 0;
-        HIP_TRY(hipMemcpyAsync(c->h_istage, c->d_ierr, 4, hipMemcpyDeviceToHost, st));
-        if (check) HIP_TRY(hipMemcpyAsync(c->h_istage + 4, c->d_total, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(c->h_istage + rb_at, c->d_ierr, 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         const uint32_t err = h_err[0];
         if (check && nl && h_err[1] != total) return fail_hip(hipErrorUnknown, "age index: membership total");
@@ -1299,8 +1334,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     f.ablate = c->k3_ablate;
     const bool ord = c->order_in_step;
     HIP_TRY(launch_step_tail(g, n, f, true, c->d_wide_pod, c->d_pwords, c->nodes.rows, c->d_trk_acc, c->d_pchunks,
-                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_ord, c->d_seg,
-                             c->d_sel_total, st));
+                             ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_ord, c->d_seg, st));
     if (int32_t rc = mark()) return rc;
     if (ord) {                                       // split groups, mid-size packed chunks
         HIP_TRY(launch_order(n, c->d_chunks, c->n_chunks, c->d_gch_off, c->d_grp_off, c->d_g_memb, c->d_ostat,
@@ -2563,15 +2597,16 @@ int32_t esc_set_selections(esc_ctx* c, int32_t slack, int32_t group_cap) {
     HIP_TRY(hipStreamSynchronize(c->stream));          // queued decisions may still write the buffer
     drop_graphs(c);                                     // captured steps hold the old target
     release_selections(c);
+    // every block of 64 groups has a slot for its groups' runs at their largest (header +
+    // group_cap nodes; k_node_groups): no decision overflows it
+    const int64_t words = (((int64_t)c->gi.G + 63) / 64) * 64 * ((int64_t)group_cap + 1);
+    if (slack >= 0 && words > (int64_t)0xFFFFFFFE) return ESC_E_LIMIT;   // 32-bit run offsets
     c->sel_slack = slack < 0 ? -1 : slack;
     c->sel_group_cap = group_cap;
     if (slack < 0) return ESC_OK;
-    // every group's run at its largest (header + group_cap nodes): no decision overflows it
-    c->sel_words = (int64_t)c->gi.G * (group_cap + 1);
+    c->sel_words = words;
     HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_sel), (size_t)c->sel_words * 4));
     HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_sel_dev), c->h_sel, 0));
-    HIP_TRY(dalloc(&c->d_sel_total, 1));
-    HIP_TRY(hipMemset(c->d_sel_total, 0, 4));
     for (int32_t g = 0; c->h_cdec && g < c->gi.G; ++g) c->h_cdec[g].sel = SEL_NONE;
     return ESC_OK;
 }

@@ -4,6 +4,9 @@
 #   suite            pytest -m gpu (-x), then __graft_entry__.smoke()
 #   bench            the default bench line (config 4, N = 1), rank 0 of N = 8 (--shard-of 8),
 #                    config 5 (orderings + age index)
+#   ablate:NAME:A,.. the tail without some of its roles (measurement library, ESC_K3_ABLATE=A;
+#                    timing only: wrong results) for profile NAME's bench command
+#   nosel            config 4 and rank 0 of 8 without selections (--no-select)
 #   rehearse2        N = 2 on one device: two gloo ranks (bench.py --gpus 2, ESC_BENCH_BACKEND=gloo,
 #                    ESC_BENCH_DEVICE=0), and one process driving two shards (peer exchange)
 #   rehearse2c5      config 5 (10 M nodes) at N = 2 on one device: two gloo ranks, each ordering its
@@ -11,6 +14,7 @@
 #   prof:NAME        rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE and --pmc
 #                    WRITE_SIZE passes of the same bench command, reduced by scripts/prof_summary.py
 #                    to $OUT/profiles/summary_NAME.json.  NAME: full (config 4), shard8, config5
+#   rt:NAME          rocprofv3 --kernel-trace --memory-copy-trace of the bench command (6 steps)
 #   pmcsq:NAME       SQ counter pass (one --pmc run) of the same command
 #   py:SCRIPT        python3 scripts/SCRIPT (e.g. k1_trace.py), output to $OUT
 #   variants:A,B,..  A/B timing of library builds (scripts/build_variant.sh NAME ...:
@@ -59,6 +63,34 @@ bench() {
     echo "[gpu] $(date +%T) bench config 5"
     timeout -k 10 400 python3 -u bench.py --config 5 --steps $STEPS --warmup 3 > $OUT/bench5.json 2> $OUT/bench5.err || { tail $OUT/bench5.err; return 1; }
     cat $OUT/bench5.json
+}
+
+nosel() {      # the bench without selections (esc_set_selections off): their cost in the step
+    echo "[gpu] $(date +%T) bench without selections: config 4, rank 0 of 8"
+    timeout -k 10 400 python3 -u bench.py --steps $STEPS --warmup 5 --no-cpu-baseline --no-host --no-select \
+        > $OUT/bench_nosel.json 2> $OUT/bench_nosel.err || { tail $OUT/bench_nosel.err; return 1; }
+    timeout -k 10 300 python3 -u bench.py --shard-of 8 --steps 50 --warmup 10 --no-cpu-baseline --no-host --no-select \
+        > $OUT/bench_shard8_nosel.json 2> $OUT/bench_shard8_nosel.err || { tail $OUT/bench_shard8_nosel.err; return 1; }
+    python3 -c "
+import json
+for n in ('bench_nosel', 'bench_shard8_nosel'):
+    d = json.load(open('$OUT/%s.json' % n))
+    print(' ', n, 'step %.4f ms' % d['ms_per_step'], {k: round(x * 1e3, 1) for k, x in (d.get('stage_ms') or {}).items()})"
+}
+
+ablate() {     # NAME:A,B,..  the tail's roles dropped (measurement library, ESC_K3_ABLATE; wrong results)
+    local name=${1%%:*} list=${1#*:} a args
+    args=$(args_of $name) || return 1
+    for a in ${list//,/ }; do
+        echo "[gpu] $(date +%T) ablate $name $a"
+        ESC_LIB_PATH=$PWD/escalator_amd/libescalator_hip_measure.so ESC_K3_ABLATE=$a timeout -k 10 300 python3 -u bench.py \
+            $args --no-cpu-baseline --no-host --no-parity > $OUT/abl_${name}_$a.json 2> $OUT/abl_${name}_$a.err \
+            || { tail $OUT/abl_${name}_$a.err; return 1; }
+        python3 -c "
+import json
+d = json.load(open('$OUT/abl_${name}_$a.json'))
+print('  $name a=$a step %.4f ms' % d['ms_per_step'], {k: round(x * 1e3, 1) for k, x in (d.get('stage_ms') or {}).items()})"
+    done
 }
 
 rehearse2() {
@@ -122,6 +154,14 @@ PY
         --out $PROF/summary_$name.json
 }
 
+rt() {         # name: rocprofv3 --runtime-trace (HIP API + kernels + copies; no counters) of the bench command
+    local name=$1 a
+    a=$(args_of $name) || return 1
+    echo "[gpu] $(date +%T) runtime trace $name"
+    timeout -k 10 400 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/rt_$name -o run \
+        -- python3 bench.py $a --no-cpu-baseline --no-host > $OUT/rt_$name.log 2>&1 || { tail -20 $OUT/rt_$name.log; return 1; }
+}
+
 pmcsq() {      # name: one SQ counter pass (<= 8 SQ counters)
     local name=$1 a
     a=$(args_of $name) || return 1
@@ -175,9 +215,12 @@ for stage in "$@"; do
         suite) suite || exit 1 ;;
         bench) bench || exit 1 ;;
         rehearse2) rehearse2 || exit 1 ;;
+        nosel) nosel || exit 1 ;;
+        ablate:*) ablate ${stage#ablate:} || exit 1 ;;
         rehearse2c5) rehearse2c5 || exit 1 ;;
         prof:*) prof ${stage#prof:} || exit 1 ;;
         pmcsq:*) pmcsq ${stage#pmcsq:} || exit 1 ;;
+        rt:*) STEPS=6 rt ${stage#rt:} || exit 1 ;;
         variants:*) variants ${stage#variants:} || exit 1 ;;
         variants5:*) variants5 ${stage#variants5:} || exit 1 ;;
         py:*) timeout -k 10 600 python3 -u scripts/${stage#py:} > $OUT/${stage#py:}.out 2>&1 || { tail -20 $OUT/${stage#py:}.out; exit 1; } ;;
