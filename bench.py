@@ -28,9 +28,9 @@ CONFIGS = {
             name="config4: 100M pods / 1M nodes / 10k node groups (BASELINE.json configs[3]), sharded over N GPUs"),
 }
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
-# rocprofv3 kernel-trace + PMC passes of this same command (scripts/job_r04c.sh), reduced to
+# rocprofv3 kernel-trace + PMC passes of this same command (scripts/gpu.sh prof:NAME), reduced to
 # the timed launches by scripts/prof_summary.py: HBM bytes per K1 launch, by workload
-PROF_DIR = os.path.join(ROOT, "profiles", "r05_prof")
+PROF_DIR = os.path.join(ROOT, "profiles", "r06_prof")
 PMC_SUMMARY = {(4, 1): os.path.join(PROF_DIR, "summary_full.json"),       # (config, shard-of)
                (4, 8): os.path.join(PROF_DIR, "summary_shard8.json")}
 
