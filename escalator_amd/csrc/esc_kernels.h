@@ -437,6 +437,7 @@ struct NGDecide {
     esc_group_decision* dec;
     DecCompact* cdec;
     SelOut sel;
+    uint64_t* trace = nullptr;         // measurement library: per block {start, end} (esc_debug_tail_trace)
 };
 // The groups a launch of k_node_groups covers: ids[i] for i < n, or, with null
 // ids, the contiguous run first + i (a rank's owned groups).
@@ -482,6 +483,7 @@ struct FoldPlan {
     const uint32_t* col_groups;        // group ids ordered by pod slot, then id
     const uint32_t* col_rows;          // compact flush: [n_col + 1] partial entries of each column (null: nblk rows)
     int ablate;                        // ESC_K3_ABLATE (timing-only knob)
+    uint64_t* trace = nullptr;         // measurement library: per block {start, end, role} (esc_debug_tail_trace)
 };
 // The pod-slot columns each K1 workgroup's share touches (compact flush): bitmap words of
 // tw u32 per workgroup, from the same work plan as K1 (daemonset pods skipped: they add

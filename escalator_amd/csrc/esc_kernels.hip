@@ -1729,7 +1729,19 @@ __global__ __launch_bounds__(NG_WAVES * 64) void k_node_groups(GroupDev G, NodeD
     const int32_t i = i0 + (int32_t)(threadIdx.x & 63);
     const uint32_t n = L.n - i0 < 64 ? (uint32_t)(L.n - i0) : 64u;
     const uint32_t g = i >= L.n ? NONE : L.ids ? L.ids[i] : (uint32_t)(L.first + i);
+#if ESC_MEASURE
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     node_groups_part(G, N, node_rows, trk_acc, nwords, D, g, !L.ids, L.first + i0, n);
+#if ESC_MEASURE
+    if (D.trace) {                                       // {start, end}
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            D.trace[2 * blockIdx.x] = t_start;
+            D.trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+#endif
 }
 
 // K3 fold (fold_col, a role of k_step_tail): the K1 workgroups' slot partials folded and
@@ -1752,13 +1764,20 @@ static_assert(FD_RPL * FD_HL == 64 && FD_WAVES >= 2, "fold lane map");
 }  // namespace
 
 namespace {
+// The fold's LDS (a member of k_step_tail's role union: the roles' LDS overlaid, so the
+// tail's blocks are not limited by the sum of every role's arrays)
+struct FoldLds {
+    uint64_t red[FD_WAVES][8][64];                       // 16 KB
+    uint64_t tot[4][FC_COL];                             // per slot: cpu, count, mem lo, mem carry
+    int64_t wtot[WP_K][FC_COL];                          // per slot: its wide row
+};
 __device__ __forceinline__ void fold_col(const GroupDev& G, const FoldPlan& F, int64_t* __restrict__ wide_pod,
-                                         int64_t* __restrict__ pwords, int col) {
+                                         int64_t* __restrict__ pwords, int col, FoldLds& S) {
     // F.ablate (timing-only, wrong results): 1 no group phase, 4 no fold loads
     const int ablate = F.ablate;
-    __shared__ uint64_t red[FD_WAVES][8][64];            // 16 KB
-    __shared__ uint64_t tot[4][FC_COL];                 // per slot: cpu, count, mem lo, mem carry
-    __shared__ int64_t wtot[WP_K][FC_COL];              // per slot: its wide row
+    auto& red = S.red;
+    auto& tot = S.tot;
+    auto& wtot = S.wtot;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int sub = lane / FD_HL, hl = lane % FD_HL;
     const int64_t s0 = (int64_t)col * FC_COL;
@@ -2726,21 +2745,30 @@ __device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long lon
     return v;
 }
 
+// A packed ordering block's LDS (in k_step_tail, a member of the role union)
+template <int STEPS>
+struct OrdLds {
+    static constexpr int CAP = STEPS * 4 * ORD_BLOCK;    // memberships per chunk
+    unsigned long long wt[STEPS][ORD_WAVES];
+    unsigned long long hp[CAP / 4];                      // scan value at each group's first quad
+    uint32_t stage[CAP];
+    uint32_t s_go[ORD_GCAP + 1];                         // the chunk's groups' region starts (+ the end)
+    uint8_t s_dry[ORD_GCAP];
+};
 template <int STEPS>
 __device__ __forceinline__ void ord_packed_block(const NodeDev& N, const OrdChunk* __restrict__ chunks,
                                                  const uint32_t* __restrict__ grp_off,
                                                  const uint8_t* __restrict__ dry,
                                                  const uint32_t* __restrict__ g_memb,
-                                                 uint32_t* __restrict__ vals, int64_t* __restrict__ seg, int64_t blk) {
-    constexpr int CAP = STEPS * 4 * ORD_BLOCK;           // memberships per chunk
-    constexpr int NQ = CAP / 4;
+                                                 uint32_t* __restrict__ vals, int64_t* __restrict__ seg, int64_t blk,
+                                                 OrdLds<STEPS>& S) {
     constexpr int C1 = 21, C2 = 42;
     constexpr unsigned long long M = (1ull << C1) - 1;
-    __shared__ unsigned long long wt[STEPS][ORD_WAVES];
-    __shared__ unsigned long long hp[NQ];                // scan value at each group's first quad
-    __shared__ uint32_t stage[CAP];
-    __shared__ uint32_t s_go[ORD_GCAP + 1];              // the chunk's groups' region starts (+ the end)
-    __shared__ uint8_t s_dry[ORD_GCAP];
+    auto& wt = S.wt;
+    auto& hp = S.hp;
+    auto& stage = S.stage;
+    auto& s_go = S.s_go;
+    auto& s_dry = S.s_dry;
     const OrdChunk ch = chunks[blk];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t g0 = ch.group, ng = ch.pad;           // ng <= ORD_GCAP (the host's chunking)
@@ -2854,7 +2882,8 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdCh
                                                           const uint8_t* __restrict__ dry,
                                                           const uint32_t* __restrict__ g_memb,
                                                           uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
-    ord_packed_block<STEPS>(N, chunks, grp_off, dry, g_memb, vals, seg, blockIdx.x);
+    __shared__ OrdLds<STEPS> lds;
+    ord_packed_block<STEPS>(N, chunks, grp_off, dry, g_memb, vals, seg, blockIdx.x, lds);
 }
 
 // The step's tail in ONE launch (horizontal fusion; every role is 256 threads and none
@@ -2874,7 +2903,19 @@ __global__ __launch_bounds__(ORD_BLOCK) void k_ord_packed(NodeDev N, const OrdCh
 // ran on a side stream beside K1: K1 holds every CU's LDS and its loads starve K2's
 // latency-bound waves, so the side chain ended after K1 and the cross-stream join cost
 // ~10 us more (profiles/r02_v9 timeline): ~45 us after K1 at any pod count.)
-__global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPlan F, int64_t* __restrict__ wide_pod,
+// k_step_tail's blocks per CU the compiler must allow: 6 caps its VGPRs at 80 (84 unbounded:
+// 5 blocks; 12 B spilled); with the roles' LDS overlaid (18.7 KB) 6 blocks fit.  r06o: the
+// config-4 tail 20.8-21.5 -> 19.6-19.7 us (stage events); 8 (64 VGPRs) spilled 76 B and
+// took 30 us.  0 = no bound (timing builds)
+#ifndef ESC_TAIL_MINB
+#define ESC_TAIL_MINB 6
+#endif
+#if ESC_TAIL_MINB > 0
+#define TAIL_BOUNDS __launch_bounds__(256, ESC_TAIL_MINB)
+#else
+#define TAIL_BOUNDS __launch_bounds__(256)
+#endif
+__global__ TAIL_BOUNDS void k_step_tail(GroupDev G, NodeDev N, FoldPlan F, int64_t* __restrict__ wide_pod,
                                                    int64_t* __restrict__ pwords, int64_t nb_pieces, int64_t n_piece_blk,
                                                    int64_t* __restrict__ rows, int64_t* __restrict__ trk_acc,
                                                    const OrdChunk* __restrict__ chunks, int64_t n_small,
@@ -2882,7 +2923,23 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
                                                    const uint32_t* __restrict__ g_memb,
                                                    uint32_t* __restrict__ vals, int64_t* __restrict__ seg) {
     static_assert(FD_WAVES * 64 == 256 && K2_WAVES * 64 == 256 && ORD_BLOCK == 256, "one block size for every role");
+    // the roles' LDS overlaid: a block takes one role, so its LDS is the largest role's (the
+    // arrays of all roles side by side were 27.4 KB, which with 84 VGPRs held 5 blocks per CU)
+#ifndef ESC_TAIL_NOUNION
+    __shared__ union {
+        FoldLds fold;
+        OrdLds<ORD_PCHUNK / (4 * ORD_BLOCK)> ord;
+    } lds;
+#else                                                    // (timing builds: the roles' arrays side by side)
+    __shared__ struct {
+        FoldLds fold;
+        OrdLds<ORD_PCHUNK / (4 * ORD_BLOCK)> ord;
+    } lds;
+#endif
     const int64_t b = blockIdx.x;
+#if ESC_MEASURE
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     // F.ablate (ESC_K3_ABLATE, timing-only, wrong results): 8 / 16 / 32 skip the fold /
     // node-piece / ordering role, 64 the dry-mode tracker blocks, 128 K2's row stores
     if (b < n_piece_blk) {
@@ -2891,11 +2948,21 @@ __global__ __launch_bounds__(256) void k_step_tail(GroupDev G, NodeDev N, FoldPl
             node_piece_block(N, G, nb_pieces, (F.ablate & 128) ? nullptr : rows, trk_acc, pb);
     } else if (b < n_piece_blk + F.n_col) {
         const uint32_t col = (uint32_t)(b - n_piece_blk);
-        if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)col);
+        if (!(F.ablate & 8)) fold_col(G, F, wide_pod, pwords, (int)col, lds.fold);
     } else if (!(F.ablate & 32)) {
         ord_packed_block<ORD_PCHUNK / (4 * ORD_BLOCK)>(N, chunks, grp_off, G.dry, g_memb, vals, seg,
-                                                       b - n_piece_blk - F.n_col);
+                                                       b - n_piece_blk - F.n_col, lds.ord);
     }
+#if ESC_MEASURE
+    if (F.trace) {                                       // {start, end, role: 0 pieces, 1 tracker, 2 fold, 3 ordering}
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            F.trace[3 * b] = t_start;
+            F.trace[3 * b + 1] = __builtin_amdgcn_s_memrealtime();
+            F.trace[3 * b + 2] = b < nb_pieces ? 0 : b < n_piece_blk ? 1 : b < n_piece_blk + F.n_col ? 2 : 3;
+        }
+    }
+#endif
 }
 
 // Region padding: MEMB_PAD_WORD after each group's memberships (node 0, flagged absent:

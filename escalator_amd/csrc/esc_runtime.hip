@@ -180,6 +180,9 @@ struct esc_ctx {
     uint64_t* d_pod_part = nullptr;
     uint32_t *d_col_off = nullptr, *d_col_groups = nullptr;   // K3: groups by pod slot column
     int k3_ablate = 0;                                        // ESC_K3_ABLATE (timing-only knob)
+    bool tail_trace = false;                                  // ESC_TAIL_TRACE (measurement library)
+    uint64_t* d_ttrace = nullptr;                             // tail + node-groups block timestamps
+    int64_t ttrace_cap = 0, ttrace_tail = 0, ttrace_ng = 0;   // words; blocks of the last traced step
     int64_t* d_wide_pod = nullptr;
     uint32_t* d_k1_ticket = nullptr;                          // K1 dynamic shares (next chunk, done)
     int64_t* d_k1seg = nullptr;                               // K1 work plan [nblk][K1_SEGS][2]
@@ -615,6 +618,8 @@ int32_t replay_step(esc_ctx* c, std::vector<hipGraphExec_t>& gs, int r, bool dec
 void release_work(esc_ctx* c) {
     dfree(c->d_k1seg); dfree(c->d_pod_part); dfree(c->d_wide_pod); dfree(c->d_k1_ticket); dfree(c->d_trk_acc);
     dfree(c->d_k1_trace);
+    dfree(c->d_ttrace);
+    c->ttrace_cap = 0;
     dfree(c->d_touch); dfree(c->d_wg_cols); dfree(c->d_wg_off); dfree(c->d_col_rows);
     c->touch_on = false;
     dfree(c->own_pwords); c->d_nwords = nullptr; dfree(c->d_dec); dfree(c->d_cdec); dfree(c->d_metrics);
@@ -1333,6 +1338,23 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     f.col_rows = nblk && c->touch_on ? c->d_col_rows : nullptr;
     f.ablate = c->k3_ablate;
     const bool ord = c->order_in_step;
+    uint64_t* ng_trace = nullptr;
+#if ESC_MEASURE
+    if (c->tail_trace) {                             // block timestamps of the tail and node groups
+        const int64_t nt = f.n_col + tail_span_blocks(n) + tail_trk_blocks(n) + (ord ? c->n_psmall : 0);
+        const int64_t nn = (own_list(c).n + 63) / 64;
+        if (3 * nt + 2 * nn > c->ttrace_cap) {
+            dfree(c->d_ttrace);
+            c->ttrace_cap = 0;
+            HIP_TRY(dalloc(&c->d_ttrace, (size_t)(3 * nt + 2 * nn)));
+            c->ttrace_cap = 3 * nt + 2 * nn;
+        }
+        c->ttrace_tail = nt;
+        c->ttrace_ng = decide ? nn : 0;
+        f.trace = c->d_ttrace;
+        ng_trace = c->d_ttrace + 3 * nt;
+    }
+#endif
     HIP_TRY(launch_step_tail(g, n, f, true, c->d_wide_pod, c->d_pwords, c->nodes.rows, c->d_trk_acc, c->d_pchunks,
                              ord ? c->n_psmall : 0, c->d_grp_off, c->d_g_memb, c->d_ord, c->d_seg, st));
     if (int32_t rc = mark()) return rc;
@@ -1351,7 +1373,7 @@ int32_t enqueue_step(esc_ctx* c, int r, bool decide, bool copy_out) {
     // launch (esc_decide) — one kernel boundary less on the rank's critical path.
     if (decide) {
         HIP_TRY(launch_node_groups(g, n, own_list(c), c->nodes.rows, c->d_trk_acc, c->d_nwords,
-                                   NGDecide{c->d_pwords, c->d_dec, cdec, sel_out(c)}, st));
+                                   NGDecide{c->d_pwords, c->d_dec, cdec, sel_out(c), ng_trace}, st));
         if (int32_t rc = mark()) return rc;
     }
     if (copy_out && !c->zero_copy) {
@@ -1440,6 +1462,7 @@ int32_t esc_ctx_create(const esc_group_spec* groups, int32_t n_groups, int32_t d
     if (const char* v = std::getenv("ESC_POD_SORT")) c->pod_sort = (uint32_t)std::max(0, std::atoi(v));
     if (const char* v = std::getenv("ESC_K1_FULL_FLUSH")) c->full_flush = std::atoi(v) != 0;
     if (const char* v = std::getenv("ESC_K3_ABLATE")) c->k3_ablate = std::atoi(v);
+    if (const char* v = std::getenv("ESC_TAIL_TRACE")) c->tail_trace = std::atoi(v) != 0;
 #endif
     c->gi.build(groups, n_groups);
     c->params.resize(n_groups);
@@ -2527,8 +2550,18 @@ int32_t esc_decide(esc_ctx* c) {
     // node groups + K4 over this rank's own groups: their node words from K2's piece rows
     // (the tracker sums of the step), their exchanged pod words (the rank's slice, rows xs[g])
     if (!c->ng_pending) return ESC_E_STATE;            // nothing reduced since the last decide
+    uint64_t* ng_trace = nullptr;
+#if ESC_MEASURE
+    if (c->tail_trace && c->d_ttrace) {                // after the reduce's tail blocks (esc_debug_tail_trace)
+        const int64_t nn = (own_list(c).n + 63) / 64;
+        if (3 * c->ttrace_tail + 2 * nn <= c->ttrace_cap) {
+            ng_trace = c->d_ttrace + 3 * c->ttrace_tail;
+            c->ttrace_ng = nn;
+        }
+    }
+#endif
     HIP_TRY(launch_node_groups(group_dev(c), node_dev(c), own_list(c), c->nodes.rows, c->d_trk_acc, c->d_nwords,
-                               NGDecide{c->d_pwords, c->d_dec, c->zero_copy ? c->h_cdec_dev : c->d_cdec, sel_out(c)},
+                               NGDecide{c->d_pwords, c->d_dec, c->zero_copy ? c->h_cdec_dev : c->d_cdec, sel_out(c), ng_trace},
                                c->stream));
     c->ng_pending = false;
     c->tot_dec = true;
@@ -2574,6 +2607,20 @@ int32_t esc_debug_lookback_fail(esc_ctx* c, int32_t n_order, int32_t n_list) {
     c->lb_fail_order = std::max(0, n_order);
     c->lb_fail_list = std::max(0, n_list);
     drop_graphs(c);                                     // captured launches hold their bound
+    return ESC_OK;
+}
+// [n_tail, n_ng, the tail's {start, end, role} per block, the node groups' {start, end}]
+// of the last step traced (ESC_TAIL_TRACE=1; s_memrealtime ticks, 100 MHz).
+int32_t esc_debug_tail_trace(esc_ctx* c, uint64_t* out, int64_t cap, int64_t* n_out) {
+    if (!c || c->multi || !out || !n_out) return ESC_E_INVAL;
+    if (!c->d_ttrace) return ESC_E_STATE;
+    const int64_t w = 3 * c->ttrace_tail + 2 * c->ttrace_ng;
+    *n_out = w + 2;
+    if (cap < w + 2) return ESC_E_LIMIT;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    out[0] = (uint64_t)c->ttrace_tail;
+    out[1] = (uint64_t)c->ttrace_ng;
+    HIP_TRY(hipMemcpy(out + 2, c->d_ttrace, (size_t)w * 8, hipMemcpyDeviceToHost));
     return ESC_OK;
 }
 int32_t esc_debug_fail_patches(esc_ctx* c, int32_t n) {
