@@ -302,7 +302,8 @@ struct PodDev {
 //    at load (e_flags / e_cpu / e_mem / e_node).  NewNodeLabelFilterFunc
 //    (node_group.go:278) is "(K_g, V_g) in the node's label pairs", so a group's members
 //    are exactly the entries of its pair, in snapshot order.  K2 reduces the entries per
-//    piece (a run of <= NODE_PIECE entries of one pair); this rank reduces the pieces
+//    piece (a run of entries of one pair that crosses no multiple of PIECE_ALIGN entries:
+//    K2's spans of whole pieces come out full); this rank reduces the pieces
 //    [pc_lo, pc_hi) of the pairs [q_lo, q_hi) it owns.  K3 joins each group to its pair's
 //    pieces.
 // Per-group node facts that are fixed for a loaded snapshot (esc_load_nodes): this rank's
@@ -341,8 +342,8 @@ struct NodeDev {
     const uint32_t* piece_off; // [n_pieces + 1] entry offsets
     const uint32_t* piece_pair;// [n_pieces]
     const uint32_t* pp_off;    // [n_gp + 1]: pieces of group pair q are [pp_off[q], pp_off[q+1])
-    // K2 work: span w = this rank's group-pair pieces [span_off[w], span_off[w + 1]), about
-    // NODE_SPAN entries each (several small pieces, or one large), one wave per span
+    // K2 work: span w = this rank's group-pair pieces [span_off[w], span_off[w + 1]), at
+    // most NODE_SPAN entries of whole pieces, one wave per span
     const uint32_t* span_off;  // [n_spans + 1]
     const uint32_t* span_e;    // [n_spans + 1] the spans' entry bounds (piece_off[span_off[w]])
     int64_t n_pieces, pc_lo, pc_hi, n_spans;
@@ -361,6 +362,8 @@ enum NodeRow : int {
     NR_K
 };
 constexpr int NODE_PIECE = 1024;
+constexpr int PIECE_ALIGN = 256;           // no piece crosses a multiple of it (esc_load_nodes)
+static_assert(NODE_PIECE % PIECE_ALIGN == 0, "the alignment bounds every piece");
 #ifndef ESC_NODE_SPAN
 #define ESC_NODE_SPAN 256                  // (timing builds may override; the runtime builds the spans too)
 #endif

@@ -1950,8 +1950,13 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     }
     // Pair-major entries: one per (label pair, node) of the whole table, sorted by
     // (pair, node) — the group-independent index K2 streams.  Pieces are
-    // runs of <= NODE_PIECE entries of one pair; this rank reduces the pieces that start
-    // in its 1/world share of the entries.
+    // runs of entries of one pair that never cross a multiple of PIECE_ALIGN (256) entries,
+    // so K2's spans (whole pieces, <= NODE_SPAN entries) come out full: cut only
+    // at pairs, spans averaged 72 % of NODE_SPAN at config 4 (a pair's run seldom fits
+    // beside the previous one), 1 460 tail blocks of mostly-masked loads instead of ~1 060
+    // (round 6); a pair cut in two is summed from both rows by k_node_groups, as any
+    // multi-piece pair.  This rank reduces the pieces that start in its 1/world share of
+    // the entries.
     std::vector<uint64_t> ent;
     ent.reserve((size_t)n + (size_t)s->n_xl);
     const uint32_t n_gp0 = c->gi.n_gp;
@@ -1984,7 +1989,7 @@ int32_t esc_load_nodes(esc_ctx* c, const esc_node_soa* s, int64_t lo, int64_t hi
     std::vector<uint32_t> piece_off, piece_pair;
     for (int64_t k = 0; k < E; ++k) {
         const uint32_t q = (uint32_t)(ent[k] >> 32), i = (uint32_t)ent[k];
-        if (k == 0 || q != piece_pair.back() || k - (int64_t)piece_off.back() == NODE_PIECE) {
+        if (k == 0 || q != piece_pair.back() || k % PIECE_ALIGN == 0) {
             piece_off.push_back((uint32_t)k);
             piece_pair.push_back(q);
         }

@@ -17,6 +17,7 @@ contiguous pair ranges balanced by entry count).
 import numpy as np
 
 NODE_PIECE = 1024
+PIECE_ALIGN = 256          # esc_kernels.h: no piece crosses a multiple of it (K2's spans come out full)
 NONE = 0xFFFFFFFF
 
 
@@ -151,11 +152,11 @@ def node_bytes(nodes: dict, n_gp: int, rank: int = 0, world: int = 1) -> int:
     E = len(q)
     if E == 0:
         return 0
-    # pieces: runs of <= NODE_PIECE entries of one pair
+    # pieces: runs of one pair's entries cut at every multiple of PIECE_ALIGN entries too
+    # (K2's spans come out full, esc_runtime.hip esc_load_nodes), so <= NODE_PIECE long
+    assert NODE_PIECE % PIECE_ALIGN == 0
     starts = np.flatnonzero(np.r_[True, q[1:] != q[:-1]])
-    counts = np.diff(np.r_[starts, E])
-    n_pc = (counts + NODE_PIECE - 1) // NODE_PIECE
-    p_start = np.repeat(starts, n_pc) + NODE_PIECE * (np.arange(n_pc.sum()) - np.repeat(np.cumsum(n_pc) - n_pc, n_pc))
+    p_start = np.union1d(starts, np.arange(0, E, PIECE_ALIGN))
     p_len = np.diff(np.r_[p_start, E])
     p_pair = q[p_start]
     b = owner_ranges(nodes, n_gp, world)
