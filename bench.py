@@ -231,8 +231,9 @@ def selections_ok(sel, dec, want, owned, slack=SEL_SLACK, cap=SEL_CAP):
 
 def resident_run_once(ctx, select: bool, reps: int = 30) -> dict:
     """The Go shim's RunOnce on the resident snapshot (go/escalatorhip: esc_set_state +
-    esc_step + esc_sync + esc_results of every group + esc_selections, sizes then nodes): the
-    wall time a controller scan waits for before it walks the selections, median of `reps`."""
+    esc_step + esc_sync + esc_results of every group + ONE esc_selections into the context's
+    persistent buffer, allocated once at its largest here): the wall time a controller scan
+    waits for before it walks the selections, median of `reps`."""
     import ctypes as C
     import numpy as np
     from escalator_amd import _lib as L
@@ -253,13 +254,12 @@ def resident_run_once(ctx, select: bool, reps: int = 30) -> dict:
         L.check(lib.esc_sync(h))
         L.check(lib.esc_results(h, tp, dp))
         if select:
-            L.check(lib.esc_selections(h, wp, op, None, 0, C.byref(n)))
             L.check(lib.esc_selections(h, wp, op, ip, len(idx), C.byref(n)))
         ms.append((time.perf_counter() - t0) * 1e3)
     return {"ms": float(np.median(ms)), "p90_ms": float(np.percentile(ms, 90)), "selections": select,
             "groups_walking": int((which >= 0).sum()) if select else None, "nodes_delivered": int(n.value),
-            "how": "esc_set_state + esc_step + esc_sync + esc_results (every group) + esc_selections (sizes, "
-                   "then nodes) on the resident snapshot, the Go shim's RunOnce; median of %d" % reps}
+            "how": "esc_set_state + esc_step + esc_sync + esc_results (every group) + one esc_selections into "
+                   "a persistent buffer, on the resident snapshot: the Go shim's RunOnce; median of %d" % reps}
 
 
 def check_parity(args, ctx, s, multi, rank, world, backend, dist, P, N, G, n_gpus):

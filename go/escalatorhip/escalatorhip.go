@@ -316,6 +316,7 @@ type Context struct {
 	cspecs unsafe.Pointer // C copy of the group specs, alive as long as the context
 	names  arena
 	sel    bool // SetSelections on: RunOnce returns the walks' first nodes
+	selBuf []C.int64_t // RunOnce's selection buffer (grows once to the decisions' size)
 }
 
 // SetSelections puts the orderings into every decision and has RunOnce return each group's
@@ -508,11 +509,19 @@ func (x *Context) RunOnce(states []GroupState) ([]Decision, error) {
 	off := make([]C.int64_t, G+1)
 	var sel []C.int64_t
 	if x.sel && !orderFailed {
+		// one call into the context's persistent buffer; a second only when it was short
+		// (ESC_E_LIMIT reports the size: the buffer grows once and keeps that size)
 		var n C.int64_t
-		rc := C.esc_selections(x.c, ptr(which), ptr(off), nil, 0, &n)
+		if len(x.selBuf) == 0 {
+			x.selBuf = make([]C.int64_t, 4*G+1)
+		}
+		rc := C.esc_selections(x.c, ptr(which), ptr(off), ptr(x.selBuf), C.int64_t(len(x.selBuf)), &n)
+		if rc == C.ESC_E_LIMIT {
+			x.selBuf = make([]C.int64_t, 2*n+1)
+			rc = C.esc_selections(x.c, ptr(which), ptr(off), ptr(x.selBuf), C.int64_t(len(x.selBuf)), &n)
+		}
 		if rc == C.ESC_OK {
-			sel = make([]C.int64_t, n+1)
-			rc = C.esc_selections(x.c, ptr(which), ptr(off), ptr(sel), n, &n)
+			sel = x.selBuf[:n]
 		}
 		if rc == C.ESC_E_ORDER {
 			orderFailed = true

@@ -330,13 +330,20 @@ int main(int argc, char** argv) {
                d->status, d->branch, d->taint_status);
         printf("status %d %s|%s\n", g, d->status ? esc_status_string(d->status) : "", msg);
     }
-    {   /* RunOnce's esc_selections: sizes, then the nodes */
+    {   /* RunOnce's esc_selections: one call into the context's persistent buffer, a second
+           only when it was short (ESC_E_LIMIT: the sizes are known, the buffer grows) */
         int32_t* which = cal((size_t)G, sizeof(int32_t));
         int64_t* off = cal((size_t)G + 1, sizeof(int64_t));
-        int64_t total = 0;
-        device_call("esc_selections", esc_selections(ctx, which, off, NULL, 0, &total));
-        int64_t* sel = cal((size_t)(total ? total : 1), sizeof(int64_t));
-        device_call("esc_selections", esc_selections(ctx, which, off, sel, total, &total));
+        int64_t total = 0, cap = 4;                      /* small on purpose: the grow path runs */
+        int64_t* sel = cal((size_t)cap, sizeof(int64_t));
+        int32_t rc = esc_selections(ctx, which, off, sel, cap, &total);
+        if (rc == ESC_E_LIMIT) {
+            free(sel);
+            cap = total;
+            sel = cal((size_t)(cap ? cap : 1), sizeof(int64_t));
+            rc = esc_selections(ctx, which, off, sel, cap, &total);
+        }
+        device_call("esc_selections", rc);
         for (int g = 0; g < G; g++) {
             printf("select %d %d %" PRId64, g, which[g], off[g + 1] - off[g]);
             for (int64_t i = off[g]; i < off[g + 1]; i++) printf(" %" PRId64, sel[i]);
