@@ -345,3 +345,20 @@ def test_selections_ties_from_node_adds(esc):
     ids = ctx.nodes_add(packed)
     assert list(ids) == list(range(600, 605))
     check(nodes + add, True)
+    # group b: a relabel (esc_nodes_relabel) moves one of its tainted nodes' creation time
+    # onto its newest tainted node's: b now has equal times in its walk prefix too
+    lst = nodes + add
+    nb = [j for j in O.newest_first([nd["created_ns"] for nd in nodes[300:]]) if nodes[300 + j]["taints"]]
+    newest_b, mover = 300 + nb[0], 300 + nb[10]
+    moved = dict(lst[mover], created_ns=lst[newest_b]["created_ns"])
+    ctx.nodes_relabel([mover], ctx.pack([], [moved])[1])
+    lst = lst[:mover] + [moved] + lst[mover + 1:]
+    ctx.run()
+    tot, dec = ctx.results()
+    which, off, idx = ctx.selections()
+    for g, v in enumerate(("a", "b")):
+        tn = [j for j, nd in enumerate(lst) if nd["labels"].get("k") == v and nd["taints"]]
+        want = [tn[i] for i in O.newest_first([lst[j]["created_ns"] for j in tn])]
+        c = min(int(dec["delta"][g]) + 2, len(want), 64)
+        assert which[g] & 3 == SEL_UNTAINT and list(idx[off[g]:off[g + 1]]) == want[:c], (g, want[:4])
+    assert {newest_b, mover} <= set(idx[off[1]:off[1] + 3].tolist())
