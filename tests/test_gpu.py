@@ -1645,6 +1645,45 @@ def test_config3_full_size_vs_c_oracle(esc):
     assert (dec["branch"] == 7).sum() >= 50, "config 3 is tuned so that most groups scale up"
 
 
+def test_config2_full_size_vs_c_oracle(esc):
+    """BASELINE config #2 (configs[1]) at its stated size: 1M pods / 10k nodes / 100 groups;
+    every group's totals and decision, its two orderings and its delivered selection (the
+    walk's first need + slack nodes) against the C oracle, through the graph and eagerly."""
+    s = esc.Synth(1_000_000, 10_000, 100, config=2, seed=0xE5CA1A7E00000002, threads=16)
+    pods, nodes = s.pods(), s.nodes()
+    otot = soa.totals(pods, nodes, s.groups)
+    odf, odi = soa.decide(s.groups, s.states, otot)
+    want = soa.order_all(nodes, s.groups)
+    ctx = esc.Context(s)
+    ctx.load_synth(s, replicas=2)
+    ctx.set_state(s.states)
+    ctx.set_order_in_step(True)
+    ctx.set_selections(3, 64)
+    for graph in (True, False):
+        ctx.use_graph(graph)
+        for _ in range(2):
+            ctx.run()
+            tot, dec = ctx.results()
+            check_against_c_oracle(tot, dec, otot, odf, odi)
+            which, off, idx = ctx.selections()
+            for g in range(len(s.groups)):
+                for w in (0, 1):
+                    assert np.array_equal(ctx.group_order(g, w), want[(g, w)]), (g, w)
+                delta, ntt = int(dec["delta"][g]), int(dec["n_to_taint"][g])
+                if delta > 0:
+                    k, need = 1, delta
+                elif delta < 0 and int(dec["taint_status"][g]) == 0:
+                    k, need = 0, ntt
+                else:
+                    assert which[g] == -1, g
+                    continue
+                c = min(max(need, 0) + 3, len(want[(g, k)]), 64)
+                assert which[g] & 3 == k, g
+                if which[g] & 4 and off[g + 1] == off[g] and c:   # a tie run too long for the kernel
+                    continue
+                assert np.array_equal(idx[off[g]:off[g + 1]], want[(g, k)][:c]), g
+
+
 def test_config4_full_size_vs_c_oracle(esc):
     """BASELINE config #4 at its stated size on one GPU: 100M pods / 1M nodes / 10k groups;
     every group's totals and decision, and every group's two orderings (taintOldestN,
