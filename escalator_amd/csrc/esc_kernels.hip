@@ -1009,6 +1009,17 @@ __device__ __forceinline__ void decide_store(const GroupDev& G, const GroupNode&
     case 16: case 17: case 18: case 19: case 20: case 21: case 22: case 23:                    \
     case 24: case 25: case 26: case 27: case 28: case 29: case 30: ESC_KRUN(1, 3, 3)   /* = case 31 */
 #define ESC_KRUN_ALL ESC_KRUN_SHAPES(2) ESC_KRUN_PK1 ESC_KRUN_PLAIN
+// LDS copies of the slot partials per K1 workgroup: K1_REPS when the window's slots are few
+// (lane l adds to copy l % K1_REPS, so lanes of one wave that hit the same slot mostly hit
+// different addresses — and, the copies 2 words apart mod the bank count, different banks;
+// the copies are summed before the flush), else one.  With ~100 groups (configs 2 and 3) a
+// wave's 64 ds_add_u64 met on the same few slots: K1 took 94 us for 99 MB at config 3,
+// 25 us with the adds replaced by a sink (r06ab); one copy per wave changed nothing.
+constexpr uint32_t K1_REPS = 8, K1_REP_LDS = 64 * 1024;
+__host__ __device__ constexpr uint32_t k1_copy_words(uint32_t gw) { return (gw + FC_COL - 1) / FC_COL * FC_COL * 2 + 2; }
+__host__ __device__ constexpr uint32_t k1_reps(uint32_t gw) {
+    return (uint64_t)k1_copy_words(gw) * 8 * K1_REPS <= K1_REP_LDS ? K1_REPS : 1u;
+}
 template <int THREADS, int ABLATE = 0, int DC = 3, int DYN = 0, int WS = 0>
 __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, int32_t g0, uint32_t gw,
                                                         uint64_t* __restrict__ part,
@@ -1026,10 +1037,12 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
     // cpu|count words [0, gwp), mem words [gwp, 2 gwp): whole FC_COL columns per half, so the
     // compact flush reads a column's 16 B per lane unconditionally (ds_read_b128, no conflicts)
     const uint32_t gwp = (gw + FC_COL - 1) / FC_COL * FC_COL;
-    for (uint32_t i = threadIdx.x; i < 2 * gwp; i += THREADS) lds[i] = 0;
+    const uint32_t reps = k1_reps(gw), cw = k1_copy_words(gw);   // copies when the slots are few
+    for (uint32_t i = threadIdx.x; i < (reps > 1 ? reps * cw : 2 * gwp); i += THREADS) lds[i] = 0;
     const uint32_t plim = (int64_t)G.n_gp <= (int64_t)g0 ? 0u : (uint32_t)imin64((int64_t)gw, (int64_t)G.n_gp - g0);
     const uint32_t dslot = (G.default_group != NONE && G.n_gp - (uint32_t)g0 < gw) ? G.n_gp - (uint32_t)g0 : NONE;
-    const PodSink<ABLATE> K{PodLds{lds, lds + gwp, g0, gw, plim, dslot}, PodWide{wide}};
+    uint64_t* const mine = lds + (reps > 1 ? (threadIdx.x & (reps - 1)) * cw : 0u);
+    const PodSink<ABLATE> K{PodLds{mine, mine + gwp, g0, gw, plim, dslot}, PodWide{wide}};
     // compact flush: this workgroup's entry range and the descriptors of its first 32 rounds,
     // fetched now so the flush does not wait on them (see the flush)
     // (entries of workgroup b: wg_cols[b * n_col + i], i < wg_off[b]; fixed-stride, so the two
@@ -1149,6 +1162,14 @@ __global__ __launch_bounds__(THREADS) void k_pod_reduce(PodDev P, GroupDev G, in
         }
     }
     __syncthreads();
+    if (reps > 1) {                                          // the waves' copies into copy 0
+        for (uint32_t i = threadIdx.x; i < 2 * gwp; i += THREADS) {
+            uint64_t s = lds[i];
+            for (uint32_t r = 1; r < reps; ++r) s += lds[r * cw + i];
+            lds[i] = s;
+        }
+        __syncthreads();
+    }
     if (trace && threadIdx.x == 0) trace[2] = __builtin_amdgcn_s_memrealtime();
     const int64_t S = G.sp;                                  // row stride (K3 reads whole columns)
     uint64_t* out = part + (int64_t)blockIdx.x * 2 * S + g0;
@@ -1227,7 +1248,8 @@ hipError_t launch_pod_reduce_ablation(ESC_K1_ARGS) __attribute__((weak));
 
 #if ESC_PART == 0
 hipError_t launch_pod_reduce(ESC_K1_ARGS) {
-    const size_t lds = (size_t)(gw + FC_COL - 1) / FC_COL * FC_COL * 2 * sizeof(uint64_t);
+    const size_t lds = k1_reps((uint32_t)gw) > 1 ? (size_t)k1_reps((uint32_t)gw) * k1_copy_words((uint32_t)gw) * 8
+                                                 : (size_t)(gw + FC_COL - 1) / FC_COL * FC_COL * 2 * sizeof(uint64_t);
     switch (variant) {
         case 0: ESC_K1(512, 0, 3); break;
         default:                                  // timing-only ablations (measurement library only)
@@ -1239,7 +1261,8 @@ hipError_t launch_pod_reduce(ESC_K1_ARGS) {
 }
 #elif ESC_PART == 2
 hipError_t launch_pod_reduce_ablation(ESC_K1_ARGS) {
-    const size_t lds = (size_t)(gw + FC_COL - 1) / FC_COL * FC_COL * 2 * sizeof(uint64_t);
+    const size_t lds = k1_reps((uint32_t)gw) > 1 ? (size_t)k1_reps((uint32_t)gw) * k1_copy_words((uint32_t)gw) * 8
+                                                 : (size_t)(gw + FC_COL - 1) / FC_COL * FC_COL * 2 * sizeof(uint64_t);
     switch (variant) {
         case 14: ESC_K1W(512, 4 | 32, 3, 0, 1); break;   // per-wave shares, K tiles, loads only
         case 3: ESC_K1(512, 64, 3); break;       // <= 2 K tiles in flight per wave
